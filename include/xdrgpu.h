@@ -1,0 +1,273 @@
+/*
+ * xdrgpu.h — C ABI of the MI355X-native batched XDR (RFC 4506) marshal engine.
+ *
+ * This is the drop-in boundary for xdrpp's encode/decode hot path.  Every
+ * entry point below replaces one reference interface; the reference
+ * file:line it stands in for is cited next to it (paths relative to the
+ * xdrpp source tree):
+ *
+ *   xdrg_plan_create      <- the compile-time field walk xdr_traits<T>::save/load
+ *                            performs (xdrc/gen_hh.cc:212-250 structs,
+ *                            :575-675 unions; xdrpp/types.h:676-730)
+ *   xdrg_encode           <- xdr_to_opaque(r0, ..., rN-1)   xdrpp/marshal.h:264-272
+ *                            (xdr_generic_put, xdrpp/marshal.h:84-137)
+ *   xdrg_decode           <- xdr_from_opaque(bytes, r...)    xdrpp/marshal.h:299-306
+ *                            (xdr_generic_get, xdrpp/marshal.h:142-211)
+ *   xdrg_serial_sizes     <- xdr_argpack_size / xdr_size     xdrpp/marshal.h:223-234,
+ *                                                            xdrpp/types.h:240-244
+ *   xdrg_swap32/xdrg_swap64 <- swap32 / swap64               xdrpp/endian.h:56-68
+ *   xdrg_error_message    <- the what() strings of the exception types
+ *                            xdrpp/types.h:57-99, marshal.h:104-108,152-170,
+ *                            :131-136,:207-210, marshal.cc:43-57
+ *
+ * Conventions
+ *  - All data pointers passed to encode/decode are DEVICE pointers
+ *    (hipMalloc / torch CUDA tensors).  No allocation happens inside the
+ *    encode/decode calls; scratch comes from a caller-provided workspace.
+ *  - Calls are stream-ordered and asynchronous.  Errors found by the
+ *    kernels are recorded in a device-resident xdrg_status that the caller
+ *    reads back with xdrg_status_read (which synchronises the stream).
+ *  - No C++ exceptions cross this boundary.  Return values are
+ *    XDRG_OK or a negative XDRG_E* API error; data errors are positive
+ *    XDRG_ERR_* codes reported through xdrg_status.
+ *  - "Native" records are the in-memory representation the kernels read
+ *    (encode) or write (decode): for fixed-size schemas this is exactly the
+ *    C++ struct produced by xdrc; variable-length bytes fields are staged as
+ *    an xdrg_bytes_ref into a byte heap (std::vector / std::string storage is
+ *    not device addressable).  See DESIGN.md "Data layout in HBM".
+ */
+#ifndef XDRGPU_H_INCLUDED
+#define XDRGPU_H_INCLUDED 1
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define XDRG_ABI_VERSION 1
+
+/* ---------------------------------------------------------------------- */
+/* Plan ops: a flat, wire-ordered walk of xdr_traits<T>::save.             */
+/* ---------------------------------------------------------------------- */
+
+enum xdrg_op_kind {
+  XDRG_OP_U32 = 1,       /* int / unsigned / float: 4-byte native, 4-byte wire   (types.h:286-332) */
+  XDRG_OP_U64 = 2,       /* hyper / unsigned hyper / double                     (types.h:286-332) */
+  XDRG_OP_BOOL = 3,      /* 1-byte native bool, wire u32 0/1; any nonzero decodes true (types.h:335-349) */
+  XDRG_OP_ENUM = 4,      /* int32 native; arg0/arg1 = enum value list in table (gen_hh.cc:271-305) */
+  XDRG_OP_OPAQUE = 5,    /* opaque[arg0]: fixed bytes, wire pad4(arg0)          (types.h:455-470) */
+  XDRG_OP_VAROPAQUE = 6, /* opaque<arg0>: native xdrg_bytes_ref                 (types.h:515-524) */
+  XDRG_OP_STRING = 7,    /* string<arg0>: native xdrg_bytes_ref                 (types.h:530-587) */
+  XDRG_OP_UNION = 8,     /* discriminant int32 at noff, then the selected arm   (gen_hh.cc:639-673) */
+  XDRG_OP_JUMP = 9,      /* pc = arg0 (end of a union arm)                      */
+  XDRG_OP_END = 10       /* end of record                                       */
+};
+
+enum xdrg_op_flags {
+  XDRG_F_VALIDATE = 1,   /* ENUM / UNION: opt-in xdr_validate_enum (types.h:157-173) */
+  XDRG_F_DEFAULT = 2     /* UNION: has a default arm; arg4 = its pc             */
+};
+
+/*
+ * One plan op (32 bytes).  `depth` is the number of class/container levels
+ * (xdr_generic_put/get operator() for is_class||is_container,
+ * marshal.h:129-136 and :198-205) enclosing the op, the top-level record
+ * counting as 1; a union op counts its own level.  The kernels raise the
+ * stack-overflow error when depth > stack_limit, which is what
+ * marshaling_stack_limit (marshal.h:21,34) does in the reference.
+ *
+ *   kind       arg0              arg1          arg2             arg3     arg4
+ *   U32/U64/BOOL  -              -             -                -        -
+ *   ENUM       table idx         count         -                -        -
+ *   OPAQUE     length            -             -                -        -
+ *   VAROPAQUE  max length        -             -                -        -
+ *   STRING     max length        -             -                -        -
+ *   UNION      enum table idx    enum count    case table idx   ncases   default pc
+ *   JUMP       target pc         -             -                -        -
+ *
+ * The case table is a run of (int32 value, uint32 target pc) pairs in the
+ * shared uint32 table.  `name` is an opaque caller id (for messages).
+ */
+typedef struct xdrg_op {
+  uint8_t kind;
+  uint8_t flags;
+  uint16_t depth;
+  uint32_t noff; /* byte offset of the field in the native record */
+  uint32_t arg0;
+  uint32_t arg1;
+  uint32_t arg2;
+  uint32_t arg3;
+  uint32_t arg4;
+  uint32_t name;
+} xdrg_op;
+
+/* Staged representation of a variable-length opaque<>/string<> field. */
+typedef struct xdrg_bytes_ref {
+  uint64_t off; /* byte offset into the heap buffer */
+  uint32_t len; /* number of payload bytes          */
+  uint32_t rsv; /* must be zero                      */
+} xdrg_bytes_ref;
+
+typedef struct xdrg_plan xdrg_plan;
+
+enum xdrg_path {
+  XDRG_PATH_FIXED_REG = 1, /* fixed size, identity layout: register permute kernel */
+  XDRG_PATH_FIXED_LDS = 2, /* fixed size, general layout: LDS-staged gather kernel */
+  XDRG_PATH_VAR = 3        /* variable length / unions: size pass + scan + interpreter */
+};
+
+typedef struct xdrg_plan_info {
+  uint32_t path;          /* enum xdrg_path */
+  uint32_t native_stride; /* bytes per native record */
+  uint32_t fixed_size;    /* wire bytes per record if fixed, else 0 */
+  uint32_t max_depth;     /* deepest op depth */
+  uint32_t nops;
+  uint32_t has_checks;    /* decode validates something (pads, enums) */
+} xdrg_plan_info;
+
+/* ---------------------------------------------------------------------- */
+/* Status / errors                                                         */
+/* ---------------------------------------------------------------------- */
+
+/* API errors (return values). */
+#define XDRG_OK 0
+#define XDRG_EINVAL (-1)
+#define XDRG_EALIGN (-2)
+#define XDRG_EUNSUPPORTED (-3)
+#define XDRG_EHIP (-4)
+#define XDRG_ENOMEM (-5)
+#define XDRG_ESPACE (-6) /* workspace or output buffer too small */
+
+/* Data errors (reported through xdrg_status); each maps to one reference
+ * exception class and what() string, see xdrg_error_message. */
+enum xdrg_err {
+  XDRG_ERR_NONE = 0,
+  XDRG_ERR_OVERFLOW_GET = 1,    /* xdr_overflow        marshal.h:166-170 */
+  XDRG_ERR_OVERFLOW_PUT = 2,    /* xdr_overflow        marshal.h:104-108 */
+  XDRG_ERR_XVECTOR_BOUND = 3,   /* xdr_overflow        types.h:486-489   */
+  XDRG_ERR_XSTRING_BOUND = 4,   /* xdr_overflow        types.h:539-542   */
+  XDRG_ERR_NONZERO_PAD = 5,     /* xdr_should_be_zero  marshal.cc:52-55  */
+  XDRG_ERR_BAD_DISCRIMINANT = 6,/* xdr_bad_discriminant gen_hh.cc:479-481,645,658 */
+  XDRG_ERR_INVALID_ENUM = 7,    /* xdr_invariant_failed types.h:168-170  */
+  XDRG_ERR_STACK_PUT = 8,       /* xdr_stack_overflow  marshal.h:131-132 */
+  XDRG_ERR_STACK_GET = 9,       /* xdr_stack_overflow  marshal.h:200-201 */
+  XDRG_ERR_SIZE_NOT_MULT4 = 10, /* xdr_bad_message_size marshal.h:157-159 */
+  XDRG_ERR_TRAILING = 11        /* xdr_bad_message_size marshal.h:207-210 */
+};
+
+/* Exception class a data error maps to (for host-side rethrow). */
+enum xdrg_exc {
+  XDRG_EXC_NONE = 0,
+  XDRG_EXC_OVERFLOW = 1,          /* xdr::xdr_overflow */
+  XDRG_EXC_STACK_OVERFLOW = 2,    /* xdr::xdr_stack_overflow */
+  XDRG_EXC_BAD_MESSAGE_SIZE = 3,  /* xdr::xdr_bad_message_size */
+  XDRG_EXC_BAD_DISCRIMINANT = 4,  /* xdr::xdr_bad_discriminant */
+  XDRG_EXC_SHOULD_BE_ZERO = 5,    /* xdr::xdr_should_be_zero */
+  XDRG_EXC_INVARIANT_FAILED = 6   /* xdr::xdr_invariant_failed */
+};
+
+/*
+ * Device-resident status block.  first_error packs the lowest failing
+ * (record, op) pair: (record << 24) | (op << 8) | code; all-ones = no error.
+ * The lowest record wins because the reference stops at the first failing
+ * record of the concatenated stream; within a record the lowest op index
+ * wins because the reference walks fields in wire order.
+ */
+typedef struct xdrg_status {
+  uint64_t first_error;
+  uint64_t total_bytes; /* var encode: total wire bytes produced */
+} xdrg_status;
+
+typedef struct xdrg_error {
+  int32_t code;     /* enum xdrg_err */
+  int32_t exc;      /* enum xdrg_exc */
+  uint64_t record;  /* index of the failing record */
+  uint32_t op;      /* plan op index within the record (0xffffffff: record level) */
+  uint32_t rsv;
+  uint64_t total_bytes;
+} xdrg_error;
+
+/* ---------------------------------------------------------------------- */
+/* Entry points                                                            */
+/* ---------------------------------------------------------------------- */
+
+int xdrg_abi_version(void);
+
+/* Build an immutable, device-resident plan.  `table` holds enum value lists
+ * and union case tables referenced by the ops.  native_stride is the byte
+ * distance between consecutive native records. */
+int xdrg_plan_create(const xdrg_op *ops, uint32_t nops, const uint32_t *table,
+                     uint32_t ntable, uint32_t native_stride, xdrg_plan **out);
+void xdrg_plan_destroy(xdrg_plan *plan);
+int xdrg_plan_get_info(const xdrg_plan *plan, xdrg_plan_info *info);
+
+/* Workspace bytes encode/decode/serial_sizes need for n records. */
+size_t xdrg_workspace_size(const xdrg_plan *plan, uint64_t n);
+
+/* Zero a status block (first_error = all ones) on `stream`. */
+int xdrg_status_init(xdrg_status *d_status, void *stream);
+/* Synchronise `stream`, then read and decode the status block. */
+int xdrg_status_read(const xdrg_status *d_status, void *stream, xdrg_error *out);
+
+/*
+ * Encode n native records to the concatenated XDR stream, i.e. the bytes of
+ * xdr_to_opaque(r0, ..., rn-1).
+ *   d_native    n records, native_stride apart
+ *   d_heap      byte heap the xdrg_bytes_ref fields point into (var plans)
+ *   heap_len    heap size in bytes (reads are clamped to it)
+ *   d_xdr       output; xdr_capacity bytes available
+ *   d_offsets   var plans: out, n+1 uint64 record offsets (record i occupies
+ *               [off[i], off[i+1]); off[n] = total).  May be NULL for fixed.
+ *   stack_limit marshaling_stack_limit in effect (0xffffffff = default)
+ * For a fixed plan the output is exactly n * fixed_size bytes.
+ */
+int xdrg_encode(const xdrg_plan *plan, const void *d_native, uint64_t n,
+                const uint8_t *d_heap, uint64_t heap_len, void *d_xdr,
+                uint64_t xdr_capacity, uint64_t *d_offsets,
+                uint32_t stack_limit, void *d_workspace, size_t workspace_bytes,
+                xdrg_status *d_status, void *stream);
+
+/*
+ * Decode n records from an XDR stream of xdr_len bytes.
+ * Fixed plans: the stream is n * fixed_size bytes (the records' offsets are
+ *   implied); a shorter stream fails the record it runs out in
+ *   (xdr_overflow), a longer one fails with "did not consume whole message",
+ *   exactly as xdr_from_opaque(bytes, r0, ..., rn-1) would.
+ * Var plans: d_offsets (n+1 entries, from the encoder or from RPC record
+ *   framing) is required; record i is decoded from [off[i], off[i+1]) with
+ *   the semantics of xdr_from_opaque on that slice.  Var-length payloads are
+ *   written to d_heap_out (at least xdr_len bytes): record i's payloads go
+ *   to the heap range [off[i], off[i+1]), each field 4-byte aligned.
+ */
+int xdrg_decode(const xdrg_plan *plan, const void *d_xdr, uint64_t xdr_len,
+                const uint64_t *d_offsets, uint64_t n, void *d_native,
+                uint8_t *d_heap_out, uint64_t heap_capacity,
+                uint32_t stack_limit, void *d_workspace, size_t workspace_bytes,
+                xdrg_status *d_status, void *stream);
+
+/* Size pass alone: d_sizes[i] = xdr_size(record i) (uint32). */
+int xdrg_serial_sizes(const xdrg_plan *plan, const void *d_native, uint64_t n,
+                      uint32_t *d_sizes, uint32_t stack_limit,
+                      xdrg_status *d_status, void *stream);
+
+/* Bulk big-endian swaps (endian.h swap32/swap64) over device arrays. */
+int xdrg_swap32(const uint32_t *d_in, uint32_t *d_out, uint64_t n, void *stream);
+int xdrg_swap64(const uint64_t *d_in, uint64_t *d_out, uint64_t n, void *stream);
+
+/* what() string and exception class of a data error.  For
+ * XDRG_ERR_BAD_DISCRIMINANT the reference message names the union
+ * ("bad value of <tag> in <union>"); the C++/Python layers format it from
+ * the op's name id, this returns the generic prefix. */
+const char *xdrg_error_message(int code);
+int xdrg_error_exception(int code);
+
+/* Last HIP error string recorded by this thread (for XDRG_EHIP). */
+const char *xdrg_last_hip_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* XDRGPU_H_INCLUDED */

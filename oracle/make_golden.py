@@ -1,0 +1,73 @@
+"""Regenerate tests/golden/ from the REAL reference marshaler.
+
+ORACLE / TEST INFRASTRUCTURE ONLY.  Needs oracle/_ref/ref_golden (built by
+`make -C oracle` from /root/reference sources in place).  Writes
+
+  tests/golden/<schema>_<n>.{native,heap,xdr,offsets}   small fixtures
+  tests/golden/kat.json                                  known answers + error cases
+  tests/golden/manifest.json                             sizes + sha256 of
+                                                         full-size reference outputs
+
+Full-size outputs (1M records) are hashed, not committed.
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+GOLD = os.path.join(ROOT, "tests", "golden")
+BIN = os.path.join(HERE, "_ref", "ref_golden")
+
+SMALL = {"numerics": 1000, "rec128": 1024, "recvar": 1024, "rpc": 1024}
+FULL = {"rec128": 1 << 20, "recvar": 1 << 20, "rpc": 1 << 20, "numerics": 1 << 16,
+        "rec128_mgpu": 1 << 24}
+MID = {"recvar": 1 << 16, "rpc": 1 << 16}
+EXTS = ("native", "heap", "xdr", "offsets")
+
+
+def sha(path: str) -> str:
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for b in iter(lambda: f.read(1 << 24), b""):
+            h.update(b)
+    return h.hexdigest()
+
+
+def main() -> int:
+    if not os.path.exists(BIN):
+        print("build oracle/_ref/ref_golden first (make -C oracle)", file=sys.stderr)
+        return 2
+    os.makedirs(GOLD, exist_ok=True)
+    manifest = {"generator": "oracle/ref_golden.cc (reference xdrpp/marshal.cc compiled in place)",
+                "small": {}, "hashes": {}}
+    for schema, n in SMALL.items():
+        pre = os.path.join(GOLD, f"{schema}_{n}")
+        subprocess.check_call([BIN, "gen", schema, str(n), pre])
+        manifest["small"][schema] = {"n": n, "files": {e: f"{schema}_{n}.{e}" for e in EXTS},
+                                     "xdr_bytes": os.path.getsize(pre + ".xdr")}
+    subprocess.check_call([BIN, "kat", os.path.join(GOLD, "kat.json")])
+    with tempfile.TemporaryDirectory() as td:
+        for table in (FULL, MID):
+            for schema, n in table.items():
+                pre = os.path.join(td, f"{schema}_{n}")
+                subprocess.check_call([BIN, "gen", schema, str(n), pre])
+                manifest["hashes"][f"{schema}_{n}"] = {
+                    "n": n, **{e: sha(pre + "." + e) for e in EXTS},
+                    "xdr_bytes": os.path.getsize(pre + ".xdr")}
+                for e in EXTS:
+                    os.remove(pre + "." + e)
+    with open(os.path.join(GOLD, "manifest.json"), "w") as f:
+        json.dump(manifest, f, indent=1, sort_keys=True)
+    print("wrote", GOLD)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,524 @@
+// ORACLE / TEST INFRASTRUCTURE ONLY — never shipped, never measured as
+// the product.
+//
+// Drives the REAL reference marshaler (xdrpp/marshal.{h,cc}, compiled from
+// /root/reference in place by oracle/Makefile) over the four benchmark
+// workloads and writes golden fixtures, plus a CPU timing mode used as the
+// "reference" CPU baseline.
+//
+//   ref_golden gen   <schema> <n> <outprefix>
+//       writes <outprefix>.native (staged native records), .heap (var
+//       payload heap), .xdr (concatenated xdr_put output) and .offsets
+//       (n+1 little-endian u64 record offsets).  The XDR bytes are produced
+//       by one xdr_put archive over the whole buffer (= xdr_to_opaque of the
+//       argument pack, xdrpp/marshal.h:264-272); each record is also
+//       checked against its own xdr_to_opaque and round-tripped through
+//       xdr_from_opaque (marshal.h:299-306).
+//   ref_golden kat   <outfile.json>
+//       known-answer vectors and error cases (exception class + what()).
+//   ref_golden bench <schema> <n> <threads> <reps>
+//       times xdr_put / xdr_get streams over contiguous slices, one
+//       std::thread per slice, and per-record xdr_to_opaque; prints JSON.
+#include "ref_schemas.hh"
+#include "workload_gen.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <functional>
+#include <sstream>
+#include <string>
+#include <thread>
+#include <vector>
+
+using std::size_t;
+using std::string;
+using std::vector;
+
+static void die(const string &m) {
+  fprintf(stderr, "ref_golden: %s\n", m.c_str());
+  exit(2);
+}
+template <typename T> static T bits_as(uint64_t v) {
+  T t;
+  memcpy(&t, &v, sizeof(T));
+  return t;
+}
+static void write_file(const string &path, const void *p, size_t n) {
+  FILE *f = fopen(path.c_str(), "wb");
+  if (!f) die("cannot open " + path);
+  if (n && fwrite(p, 1, n, f) != n) die("short write " + path);
+  fclose(f);
+}
+
+// ------------------------------------------------------------ generators
+static void gen_numerics(size_t n, uint64_t seed, vector<testns::numerics> &v) {
+  v.resize(n);
+  for (size_t r = 0; r < n; ++r) {
+    testns::numerics &x = v[r];
+    memset(&x, 0, sizeof x);  // padding bytes are zero in the fixture
+    uint64_t d[8];
+    for (int k = 0; k < 8; ++k) d[k] = wg_draw(seed, r * 8 + k);
+    x.b = d[0] & 1;
+    x.i1 = (int32_t)(uint32_t)d[1];
+    x.i2 = (uint32_t)d[2];
+    x.i3 = (int64_t)d[3];
+    x.i4 = d[4];
+    x.f1 = bits_as<float>((uint32_t)d[5]);
+    x.f2 = bits_as<double>(d[6]);
+    x.e1 = testns::other_color(d[7] % 3);
+    if (r == 0) {  // tests/marshal.cc:482-490
+      x.b = false;
+      x.i1 = 0x7eeeeeee;
+      x.i2 = 0xffffffff;
+      x.i3 = UINT64_C(0x7ddddddddddddddd);
+      x.i4 = UINT64_C(0xfccccccccccccccc);
+      x.f1 = 3.141592654;
+      x.f2 = 2.71828182846;
+      x.e1 = testns::REDDER;
+    }
+  }
+}
+
+static void gen_rec128(size_t n, uint64_t seed, uint64_t first, vector<rec128> &v) {
+  v.resize(n);
+  for (size_t r = 0; r < n; ++r) {
+    uint64_t g = first + r, d[20];
+    for (int k = 0; k < 20; ++k) d[k] = wg_draw(seed, g * 20 + k);
+    rec128 &x = v[r];
+    int32_t *a = &x.a0;
+    for (int k = 0; k < 8; ++k) a[k] = (int32_t)(uint32_t)d[k];
+    uint64_t *u = &x.u0;
+    for (int k = 0; k < 6; ++k) u[k] = d[8 + k];
+    double *dd = &x.d0;
+    for (int k = 0; k < 6; ++k) dd[k] = bits_as<double>(d[14 + k]);
+  }
+}
+
+static void gen_recvar(size_t n, uint64_t seed, vector<recvar> &v) {
+  v.resize(n);
+  const uint64_t ps = seed ^ WG_PAYLOAD_XOR;
+  for (size_t r = 0; r < n; ++r) {
+    uint64_t d[5];
+    for (int k = 0; k < 5; ++k) d[k] = wg_draw(seed, r * 5 + k);
+    recvar &x = v[r];
+    x.id = d[0];
+    x.kind = (int32_t)(uint32_t)d[1];
+    uint32_t bl = d[2] % 257, nl = d[3] % 65;
+    x.score = bits_as<double>(d[4]);
+    x.blob.resize(bl);
+    for (uint32_t j = 0; j < bl; ++j) x.blob[j] = wg_byte(ps, r * 40 + j / 8, j);
+    string s(nl, '\0');
+    for (uint32_t j = 0; j < nl; ++j)
+      s[j] = char(0x61 + wg_byte(ps, r * 40 + 32 + j / 8, j) % 26);
+    x.name = s;
+  }
+}
+
+static void fill_auth(rpcx::opaque_auth &a, int32_t flavor, uint32_t len, uint64_t ps,
+                      uint64_t word0) {
+  a.flavor = flavor;
+  a.body.resize(len);
+  for (uint32_t j = 0; j < len; ++j) a.body[j] = wg_byte(ps, word0 + j / 8, j);
+}
+
+static void gen_rpc(size_t n, uint64_t seed, vector<rpcx::rpc_msg> &v) {
+  v.resize(n);
+  const uint64_t ps = seed ^ WG_PAYLOAD_XOR;
+  for (size_t r = 0; r < n; ++r) {
+    uint64_t d[16];
+    for (int k = 0; k < 16; ++k) d[k] = wg_draw(seed, r * 16 + k);
+    rpcx::rpc_msg &m = v[r];
+    m = rpcx::rpc_msg{};
+    m.xid = (uint32_t)d[0];
+    unsigned sel = d[1] % 10;
+    if (sel <= WG_RPC_CALL_MAX) {
+      m.body.mtype = rpcx::CALL;
+      rpcx::call_body &c = m.body.cbody;
+      c.rpcvers = 2;
+      c.prog = (uint32_t)d[2];
+      c.vers = (uint32_t)d[3];
+      c.proc = (uint32_t)d[4];
+      fill_auth(c.cred, int32_t(d[5] % 2), d[6] % 401, ps, r * 128);
+      fill_auth(c.verf, int32_t(d[7] % 2), d[8] % 401, ps, r * 128 + 64);
+    } else {
+      m.body.mtype = rpcx::REPLY;
+      rpcx::reply_body &b = m.body.rbody;
+      if (sel <= WG_RPC_PROG_UNAVAIL) {
+        b.stat = rpcx::MSG_ACCEPTED;
+        fill_auth(b.areply.verf, int32_t(d[5] % 2), d[6] % 41, ps, r * 128 + 64);
+        rpcx::reply_data_u &rd = b.areply.reply_data;
+        if (sel == WG_RPC_SUCCESS) rd.stat = rpcx::SUCCESS;
+        else if (sel == WG_RPC_PROG_MISMATCH) {
+          rd.stat = rpcx::PROG_MISMATCH;
+          rd.mismatch_info_.low = (uint32_t)d[9];
+          rd.mismatch_info_.high = (uint32_t)d[10];
+        } else rd.stat = rpcx::PROG_UNAVAIL;
+      } else {
+        b.stat = rpcx::MSG_DENIED;
+        if (sel == WG_RPC_RPC_MISMATCH) {
+          b.rreply.stat = rpcx::RPC_MISMATCH;
+          b.rreply.mismatch_info_.low = (uint32_t)d[9];
+          b.rreply.mismatch_info_.high = (uint32_t)d[10];
+        } else {
+          b.rreply.stat = rpcx::AUTH_ERROR;
+          b.rreply.rj_why = int32_t(d[11] % 15);
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------- staging
+// Heap packing for encode inputs: payloads in record order, field order,
+// no alignment (exercises unaligned heap reads on the device).
+struct heap_t {
+  vector<uint8_t> b;
+  xdrg_bytes_ref put(const uint8_t *p, size_t n) {
+    xdrg_bytes_ref r{b.size(), uint32_t(n), 0};
+    b.insert(b.end(), p, p + n);
+    return r;
+  }
+};
+
+static void stage(const vector<testns::numerics> &v, vector<uint8_t> &nat, heap_t &) {
+  nat.resize(v.size() * sizeof(testns::numerics));
+  memcpy(nat.data(), v.data(), nat.size());
+}
+static void stage(const vector<rec128> &v, vector<uint8_t> &nat, heap_t &) {
+  nat.resize(v.size() * sizeof(rec128));
+  memcpy(nat.data(), v.data(), nat.size());
+}
+static void stage(const vector<recvar> &v, vector<uint8_t> &nat, heap_t &h) {
+  nat.assign(v.size() * sizeof(st_recvar), 0);
+  st_recvar *s = reinterpret_cast<st_recvar *>(nat.data());
+  for (size_t r = 0; r < v.size(); ++r) {
+    s[r].id = v[r].id;
+    s[r].kind = v[r].kind;
+    s[r].blob = h.put(v[r].blob.data(), v[r].blob.size());
+    s[r].name = h.put(reinterpret_cast<const uint8_t *>(v[r].name.data()), v[r].name.size());
+    s[r].score = v[r].score;
+  }
+}
+static void stage_auth(const rpcx::opaque_auth &a, st_opaque_auth &s, heap_t &h) {
+  s.flavor = a.flavor;
+  s.body = h.put(a.body.data(), a.body.size());
+}
+static void stage(const vector<rpcx::rpc_msg> &v, vector<uint8_t> &nat, heap_t &h) {
+  nat.assign(v.size() * sizeof(st_rpc_msg), 0);
+  st_rpc_msg *s = reinterpret_cast<st_rpc_msg *>(nat.data());
+  for (size_t r = 0; r < v.size(); ++r) {
+    const rpcx::rpc_msg &m = v[r];
+    s[r].xid = m.xid;
+    s[r].body.mtype = m.body.mtype;
+    if (m.body.mtype == rpcx::CALL) {
+      st_call_body &c = s[r].body.u.cbody;
+      c.rpcvers = m.body.cbody.rpcvers;
+      c.prog = m.body.cbody.prog;
+      c.vers = m.body.cbody.vers;
+      c.proc = m.body.cbody.proc;
+      stage_auth(m.body.cbody.cred, c.cred, h);
+      stage_auth(m.body.cbody.verf, c.verf, h);
+    } else {
+      st_reply_body &b = s[r].body.u.rbody;
+      b.stat = m.body.rbody.stat;
+      if (b.stat == rpcx::MSG_ACCEPTED) {
+        const rpcx::accepted_reply &a = m.body.rbody.areply;
+        stage_auth(a.verf, b.u.areply.verf, h);
+        b.u.areply.reply_data.stat = a.reply_data.stat;
+        if (a.reply_data.stat == rpcx::PROG_MISMATCH) {
+          b.u.areply.reply_data.u.mismatch_info.low = a.reply_data.mismatch_info_.low;
+          b.u.areply.reply_data.u.mismatch_info.high = a.reply_data.mismatch_info_.high;
+        }
+      } else {
+        const rpcx::rejected_reply &j = m.body.rbody.rreply;
+        b.u.rreply.stat = j.stat;
+        if (j.stat == rpcx::RPC_MISMATCH) {
+          b.u.rreply.u.mismatch_info.low = j.mismatch_info_.low;
+          b.u.rreply.u.mismatch_info.high = j.mismatch_info_.high;
+        } else
+          b.u.rreply.u.rj_why = j.rj_why;
+      }
+    }
+  }
+}
+
+// Equality for round-trip checks (byte-level for fixed structs).
+static bool same(const testns::numerics &a, const testns::numerics &b) {
+  return a.b == b.b && a.i1 == b.i1 && a.i2 == b.i2 && a.i3 == b.i3 && a.i4 == b.i4 &&
+         !memcmp(&a.f1, &b.f1, 4) && !memcmp(&a.f2, &b.f2, 8) && a.e1 == b.e1;
+}
+static bool same(const rec128 &a, const rec128 &b) { return !memcmp(&a, &b, sizeof a); }
+static bool same(const recvar &a, const recvar &b) {
+  return a.id == b.id && a.kind == b.kind && a.blob == b.blob && a.name == b.name &&
+         !memcmp(&a.score, &b.score, 8);
+}
+static bool same(const rpcx::rpc_msg &a, const rpcx::rpc_msg &b) {
+  return xdr::xdr_to_opaque(a) == xdr::xdr_to_opaque(b);
+}
+
+template <typename T>
+static void emit(const vector<T> &v, const string &prefix) {
+  vector<uint8_t> nat;
+  heap_t heap;
+  stage(v, nat, heap);
+  vector<uint64_t> off(v.size() + 1, 0);
+  for (size_t r = 0; r < v.size(); ++r) off[r + 1] = off[r] + xdr::xdr_size(v[r]);
+  vector<uint8_t> out(off.back());
+  {
+    // One archive over the whole stream: xdr_to_opaque(r0, ..., rn-1).
+    xdr::xdr_put p(out.data(), out.data() + out.size());
+    for (const T &x : v) archive(p, x);
+    if (p.p_ != p.e_) die("size mismatch");
+  }
+  // Spot-check per-record xdr_to_opaque and the round trip (all records
+  // for small n, a stride sample for large n).
+  size_t step = v.size() <= 65536 ? 1 : v.size() / 4096;
+  for (size_t r = 0; r < v.size(); r += step) {
+    auto one = xdr::xdr_to_opaque(v[r]);
+    if (one.size() != off[r + 1] - off[r] || memcmp(one.data(), out.data() + off[r], one.size()))
+      die("per-record encode differs at " + std::to_string(r));
+    T back{};
+    xdr::xdr_from_opaque(one, back);
+    if (!same(back, v[r])) die("round trip differs at " + std::to_string(r));
+  }
+  write_file(prefix + ".native", nat.data(), nat.size());
+  write_file(prefix + ".heap", heap.b.data(), heap.b.size());
+  write_file(prefix + ".xdr", out.data(), out.size());
+  write_file(prefix + ".offsets", off.data(), off.size() * 8);
+}
+
+// ------------------------------------------------------------- KAT / errors
+static string hex(const uint8_t *p, size_t n) {
+  static const char *d = "0123456789abcdef";
+  string s;
+  for (size_t i = 0; i < n; ++i) { s += d[p[i] >> 4]; s += d[p[i] & 15]; }
+  return s;
+}
+static vector<uint8_t> unhex(const string &s) {
+  vector<uint8_t> v;
+  for (size_t i = 0; i + 1 < s.size(); i += 2) v.push_back(uint8_t(std::stoul(s.substr(i, 2), nullptr, 16)));
+  return v;
+}
+template <typename T> static string enc(const T &t) {
+  auto v = xdr::xdr_to_opaque(t);
+  return hex(v.data(), v.size());
+}
+static string json_str(const string &s) {
+  string o = "\"";
+  for (char c : s) { if (c == '"' || c == '\\') o += '\\'; o += c; }
+  return o + "\"";
+}
+
+// Decode `h` (hex) as T with the reference; report exception class + what().
+template <typename T>
+static string try_decode(const string &h, std::function<void(xdr::opaque_vec<> &)> mut = nullptr) {
+  auto v = unhex(h);
+  xdr::opaque_vec<> m(v.begin(), v.end());
+  if (mut) mut(m);
+  T t{};
+  string cls = "none", what;
+  try {
+    xdr::xdr_from_opaque(m, t);
+  } catch (const xdr::xdr_overflow &e) { cls = "xdr_overflow"; what = e.what(); }
+  catch (const xdr::xdr_stack_overflow &e) { cls = "xdr_stack_overflow"; what = e.what(); }
+  catch (const xdr::xdr_bad_message_size &e) { cls = "xdr_bad_message_size"; what = e.what(); }
+  catch (const xdr::xdr_bad_discriminant &e) { cls = "xdr_bad_discriminant"; what = e.what(); }
+  catch (const xdr::xdr_should_be_zero &e) { cls = "xdr_should_be_zero"; what = e.what(); }
+  catch (const xdr::xdr_invariant_failed &e) { cls = "xdr_invariant_failed"; what = e.what(); }
+  std::ostringstream o;
+  o << "{\"input\": \"" << hex(m.data(), m.size()) << "\", \"exception\": \"" << cls
+    << "\", \"what\": " << json_str(what) << "}";
+  return o.str();
+}
+
+static void kat(const string &path) {
+  std::ostringstream o;
+  o << "{\n";
+  // numerics with the tests/marshal.cc:482-490 values
+  vector<testns::numerics> nv;
+  gen_numerics(1, WG_SEED_NUMERICS, nv);
+  o << "  \"numerics_marshal_cc\": \"" << enc(nv[0]) << "\",\n";
+  // rec128 record 0 of the benchmark stream
+  vector<rec128> rv;
+  gen_rec128(1, WG_SEED_REC128, 0, rv);
+  o << "  \"rec128_0\": \"" << enc(rv[0]) << "\",\n";
+  // scalar known answers
+  o << "  \"int64_m2\": \"" << enc(int64_t(-2)) << "\",\n";
+  o << "  \"float_m0\": \"" << enc(-0.0f) << "\",\n";
+  o << "  \"bool_true\": \"" << enc(true) << "\",\n";
+  // recvar with lengths 0..7 for every residue mod 4
+  for (int bl = 0; bl < 8; ++bl) {
+    recvar x{};
+    x.id = 0x0102030405060708ULL;
+    x.kind = -2;
+    x.score = 1.5;
+    for (int j = 0; j < bl; ++j) x.blob.push_back(uint8_t(j + 1));
+    x.name = string(size_t((bl * 3) % 7), 'h');
+    o << "  \"recvar_len" << bl << "\": \"" << enc(x) << "\",\n";
+  }
+  // rpc: one of each arm
+  vector<rpcx::rpc_msg> pv;
+  gen_rpc(64, WG_SEED_RPC, pv);
+  o << "  \"rpc_first64\": [";
+  for (size_t i = 0; i < pv.size(); ++i) o << (i ? ", " : "") << "\"" << enc(pv[i]) << "\"";
+  o << "],\n";
+
+  // ---- error cases: exception class + what() from the reference decoder
+  o << "  \"errors\": {\n";
+  string good_nv = enc(nv[0]);
+  vector<recvar> vv;
+  gen_recvar(4, WG_SEED_RECVAR, vv);
+  recvar odd{};
+  odd.blob = {1, 2, 3};  // 3 bytes -> one pad byte
+  odd.name = "hello";
+  string good_rv = enc(odd);
+  o << "    \"numerics_ok\": " << try_decode<testns::numerics>(good_nv) << ",\n";
+  o << "    \"numerics_short\": " << try_decode<testns::numerics>(good_nv.substr(0, 80)) << ",\n";
+  o << "    \"numerics_trailing\": " << try_decode<testns::numerics>(good_nv + "00000000") << ",\n";
+  o << "    \"numerics_not_mult4\": " << try_decode<testns::numerics>(good_nv + "00") << ",\n";
+  o << "    \"numerics_bool2\": "
+    << try_decode<testns::numerics>(good_nv, [](xdr::opaque_vec<> &m) { m[3] = 2; }) << ",\n";
+  o << "    \"numerics_enum99_novalidate\": "
+    << try_decode<testns::numerics>(good_nv, [](xdr::opaque_vec<> &m) { m[43] = 99; }) << ",\n";
+  o << "    \"numerics_enum99_validate\": "
+    << try_decode<testns_v::numerics>(good_nv, [](xdr::opaque_vec<> &m) { m[43] = 99; }) << ",\n";
+  o << "    \"recvar_ok\": " << try_decode<recvar>(good_rv) << ",\n";
+  // blob is 01020300: make the pad byte nonzero
+  o << "    \"recvar_nonzero_pad\": "
+    << try_decode<recvar>(good_rv, [](xdr::opaque_vec<> &m) { m[19] = 0x7f; }) << ",\n";
+  o << "    \"recvar_blob_over_bound\": "
+    << try_decode<recvar>(good_rv, [](xdr::opaque_vec<> &m) {
+         // claim 260 bytes (> 256) and supply them
+         xdr::opaque_vec<> n(m.begin(), m.begin() + 12);  // id kind
+         uint32_t L = 260;
+         n.push_back(uint8_t(L >> 24)); n.push_back(uint8_t(L >> 16));
+         n.push_back(uint8_t(L >> 8)); n.push_back(uint8_t(L));
+         for (uint32_t j = 0; j < L; ++j) n.push_back(1);
+         for (int j = 0; j < 12; ++j) n.push_back(0);
+         m = n;
+       }) << ",\n";
+  o << "    \"recvar_name_over_bound\": "
+    << try_decode<recvar>(good_rv, [](xdr::opaque_vec<> &m) {
+         xdr::opaque_vec<> n(m.begin(), m.begin() + 20);  // id kind blob(3)
+         uint32_t L = 68;
+         n.push_back(0); n.push_back(0); n.push_back(0); n.push_back(uint8_t(L));
+         for (uint32_t j = 0; j < L; ++j) n.push_back('x');
+         for (int j = 0; j < 8; ++j) n.push_back(0);
+         m = n;
+       }) << ",\n";
+  o << "    \"recvar_len_past_end\": "
+    << try_decode<recvar>(good_rv, [](xdr::opaque_vec<> &m) { m[15] = 200; }) << ",\n";
+  string good_rpc = enc(pv[0]);
+  o << "    \"rpc_ok\": " << try_decode<rpcx::rpc_msg>(good_rpc) << ",\n";
+  o << "    \"rpc_bad_mtype\": "
+    << try_decode<rpcx::rpc_msg>(good_rpc, [](xdr::opaque_vec<> &m) { m[7] = 7; }) << ",\n";
+  {
+    // a MSG_DENIED reply with a bad reject_stat
+    rpcx::rpc_msg d{};
+    d.xid = 9;
+    d.body.mtype = rpcx::REPLY;
+    d.body.rbody.stat = rpcx::MSG_DENIED;
+    d.body.rbody.rreply.stat = rpcx::AUTH_ERROR;
+    d.body.rbody.rreply.rj_why = 3;
+    string h = enc(d);
+    o << "    \"rpc_denied_ok\": " << try_decode<rpcx::rpc_msg>(h) << ",\n";
+    o << "    \"rpc_bad_reject_stat\": "
+      << try_decode<rpcx::rpc_msg>(h, [](xdr::opaque_vec<> &m) { m[15] = 5; }) << ",\n";
+    o << "    \"rpc_bad_reply_stat\": "
+      << try_decode<rpcx::rpc_msg>(h, [](xdr::opaque_vec<> &m) { m[11] = 2; }) << "\n";
+  }
+  o << "  }\n}\n";
+  std::ofstream f(path);
+  f << o.str();
+}
+
+// ------------------------------------------------------------- bench mode
+template <typename T>
+static void bench_one(const char *name, const vector<T> &v, int threads, int reps) {
+  vector<uint64_t> off(v.size() + 1, 0);
+  for (size_t r = 0; r < v.size(); ++r) off[r + 1] = off[r] + xdr::xdr_size(v[r]);
+  vector<uint8_t> out(off.back());
+  vector<T> back(v.size());
+  auto run = [&](auto &&body) {
+    vector<std::thread> th;
+    size_t n = v.size();
+    auto t0 = std::chrono::steady_clock::now();
+    for (int t = 0; t < threads; ++t)
+      th.emplace_back([&, t] { body(n * t / threads, n * (t + 1) / threads); });
+    for (auto &x : th) x.join();
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  };
+  auto encode = [&](size_t a, size_t b) {
+    xdr::xdr_put p(out.data() + off[a], out.data() + off[b]);
+    for (size_t r = a; r < b; ++r) archive(p, v[r]);
+  };
+  auto decode = [&](size_t a, size_t b) {
+    xdr::xdr_get g(out.data() + off[a], out.data() + off[b]);
+    for (size_t r = a; r < b; ++r) archive(g, back[r]);
+    g.done();
+  };
+  auto per_record = [&](size_t a, size_t b) {
+    for (size_t r = a; r < b; ++r) {
+      auto m = xdr::xdr_to_opaque(v[r]);
+      memcpy(out.data() + off[r], m.data(), m.size());
+    }
+  };
+  run(encode);  // pre-fault
+  run(decode);
+  vector<double> te, td, tp;
+  for (int i = 0; i < reps; ++i) {
+    te.push_back(run(encode));
+    td.push_back(run(decode));
+    tp.push_back(run(per_record));
+  }
+  std::sort(te.begin(), te.end());
+  std::sort(td.begin(), td.end());
+  std::sort(tp.begin(), tp.end());
+  double gib = double(off.back()) / (1024.0 * 1024 * 1024);
+  printf("{\"schema\": \"%s\", \"records\": %zu, \"xdr_bytes\": %llu, \"threads\": %d, "
+         "\"reps\": %d, \"encode_s_best\": %.6f, \"encode_s_median\": %.6f, "
+         "\"decode_s_best\": %.6f, \"decode_s_median\": %.6f, \"to_opaque_s_best\": %.6f, "
+         "\"encode_gib_s\": %.4f, \"decode_gib_s\": %.4f, \"to_opaque_gib_s\": %.4f, "
+         "\"encode_decode_gib_s\": %.4f}\n",
+         name, v.size(), (unsigned long long)off.back(), threads, reps, te[0], te[reps / 2],
+         td[0], td[reps / 2], tp[0], gib / te[0], gib / td[0], gib / tp[0],
+         2 * gib / (te[0] + td[0]));
+}
+
+int main(int argc, char **argv) {
+  if (argc < 2) die("usage: gen|kat|bench ...");
+  string mode = argv[1];
+  if (mode == "kat") {
+    if (argc != 3) die("kat <out.json>");
+    kat(argv[2]);
+    return 0;
+  }
+  if (argc < 4) die("missing args");
+  string schema = argv[2];
+  size_t n = std::stoull(argv[3]);
+  if (mode == "gen") {
+    if (argc != 5) die("gen <schema> <n> <prefix>");
+    string pre = argv[4];
+    if (schema == "numerics") { vector<testns::numerics> v; gen_numerics(n, WG_SEED_NUMERICS, v); emit(v, pre); }
+    else if (schema == "rec128") { vector<rec128> v; gen_rec128(n, WG_SEED_REC128, 0, v); emit(v, pre); }
+    else if (schema == "rec128_mgpu") { vector<rec128> v; gen_rec128(n, WG_SEED_REC128_MGPU, 0, v); emit(v, pre); }
+    else if (schema == "recvar") { vector<recvar> v; gen_recvar(n, WG_SEED_RECVAR, v); emit(v, pre); }
+    else if (schema == "rpc") { vector<rpcx::rpc_msg> v; gen_rpc(n, WG_SEED_RPC, v); emit(v, pre); }
+    else die("unknown schema " + schema);
+    return 0;
+  }
+  if (mode == "bench") {
+    if (argc != 6) die("bench <schema> <n> <threads> <reps>");
+    int threads = atoi(argv[4]), reps = atoi(argv[5]);
+    if (schema == "rec128") { vector<rec128> v; gen_rec128(n, WG_SEED_REC128, 0, v); bench_one("rec128", v, threads, reps); }
+    else if (schema == "numerics") { vector<testns::numerics> v; gen_numerics(n, WG_SEED_NUMERICS, v); bench_one("numerics", v, threads, reps); }
+    else if (schema == "recvar") { vector<recvar> v; gen_recvar(n, WG_SEED_RECVAR, v); bench_one("recvar", v, threads, reps); }
+    else if (schema == "rpc") { vector<rpcx::rpc_msg> v; gen_rpc(n, WG_SEED_RPC, v); bench_one("rpc", v, threads, reps); }
+    else die("unknown schema " + schema);
+    return 0;
+  }
+  die("unknown mode " + mode);
+}

@@ -1,0 +1,310 @@
+/*
+ * ORACLE / TEST INFRASTRUCTURE ONLY.  Imported by tests/, by
+ * __graft_entry__.smoke() as the checker, and by bench.py's cpu_baseline leg
+ * (as the "port" CPU baseline when the reference build is absent).  Never
+ * part of the product path.
+ *
+ * A scalar CPU restatement of xdrpp's marshal hot path, driven by the same
+ * flat plan (xdrg_op[]) the GPU kernels execute.  Every step follows the
+ * reference archive one field at a time:
+ *
+ *   check(n) before every read/write     xdrpp/marshal.h:104-108 (put),
+ *                                        :166-170 (get)
+ *   put32/put64 = swap32 per word, high  xdrpp/marshal.h:65-80,
+ *   word first for 64-bit                xdrpp/endian.h:56-68
+ *   bytes: length word if variable,      xdrpp/marshal.h:118-127 (put),
+ *   memcpy, zero pad to 4 / verify pad   :185-196 (get), marshal.cc:43-72
+ *   bool decodes nonzero as true         xdrpp/types.h:335-349
+ *   opt-in enum validation               xdrpp/types.h:157-173
+ *   union: discriminant, then arm;       xdrc/gen_hh.cc:639-673, :472-487
+ *   unknown -> bad discriminant
+ *   stack budget per class level         xdrpp/marshal.h:129-136, :198-205
+ *   misaligned end / trailing bytes      xdrpp/marshal.h:152-162, :207-210
+ *
+ * Parity of this restatement is pinned by tests/test_oracle.py against the
+ * golden fixtures that oracle/ref_golden (the real reference, compiled from
+ * /root/reference) produced.
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/xdrgpu.h"
+
+static inline uint32_t bswap32(uint32_t v) {
+  return v << 24 | (v & 0xff00) << 8 | (v >> 8 & 0xff00) | v >> 24;
+}
+static inline uint32_t rd32(const uint8_t *p) { uint32_t v; memcpy(&v, p, 4); return v; }
+static inline uint64_t rd64(const uint8_t *p) { uint64_t v; memcpy(&v, p, 8); return v; }
+static inline void wr32(uint8_t *p, uint32_t v) { memcpy(p, &v, 4); }
+static inline void wr64(uint8_t *p, uint64_t v) { memcpy(p, &v, 8); }
+static inline uint64_t pad4(uint64_t n) { return (n + 3) & ~(uint64_t)3; }
+
+typedef struct {
+  const xdrg_op *ops;
+  uint32_t nops;
+  const uint32_t *table;
+  uint32_t stride;
+} plan_t;
+
+/* Find the target pc of a union discriminant, or -1. */
+static int64_t union_target(const plan_t *P, const xdrg_op *op, uint32_t disc) {
+  const uint32_t *ct = P->table + op->arg2;
+  for (uint32_t i = 0; i < op->arg3; ++i)
+    if (ct[2 * i] == disc) return ct[2 * i + 1];
+  if (op->flags & XDRG_F_DEFAULT) return op->arg4;
+  return -1;
+}
+static int enum_ok(const plan_t *P, const xdrg_op *op, uint32_t v) {
+  if (!(op->flags & XDRG_F_VALIDATE)) return 1;
+  const uint32_t *t = P->table + op->arg0;
+  for (uint32_t i = 0; i < op->arg1; ++i)
+    if (t[i] == v) return 1;
+  return 0;
+}
+
+/* xdr_size of one record (xdr_traits<T>::serial_size).  Returns 0 and sets
+ * *err/*eop on a bad discriminant. */
+static uint64_t rec_size(const plan_t *P, const uint8_t *nat, uint32_t *err, uint32_t *eop) {
+  uint64_t s = 0;
+  uint32_t pc = 0;
+  for (;;) {
+    const xdrg_op *op = &P->ops[pc];
+    switch (op->kind) {
+    case XDRG_OP_U32: case XDRG_OP_BOOL: case XDRG_OP_ENUM: s += 4; ++pc; break;
+    case XDRG_OP_U64: s += 8; ++pc; break;
+    case XDRG_OP_OPAQUE: s += pad4(op->arg0); ++pc; break;
+    case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
+      xdrg_bytes_ref r;
+      memcpy(&r, nat + op->noff, sizeof r);
+      s += 4 + pad4(r.len);
+      ++pc;
+      break;
+    }
+    case XDRG_OP_UNION: {
+      int64_t t = union_target(P, op, rd32(nat + op->noff));
+      if (t < 0) { *err = XDRG_ERR_BAD_DISCRIMINANT; *eop = pc; return 0; }
+      s += 4;
+      pc = (uint32_t)t;
+      break;
+    }
+    case XDRG_OP_JUMP: pc = op->arg0; break;
+    default: return s;
+    }
+  }
+}
+
+/* ---------------------------------------------------------------- encode */
+/* One xdr_generic_put over [out, out+cap) for n records.  Returns 0 or the
+ * error code; *erec/*eop receive the failing record and op. */
+int xdro_encode(const xdrg_op *ops, uint32_t nops, const uint32_t *table, uint32_t stride,
+                const uint8_t *native, uint64_t n, const uint8_t *heap, uint64_t heap_len,
+                uint8_t *out, uint64_t cap, uint64_t *offsets, uint32_t stack_limit,
+                uint64_t *erec, uint32_t *eop, uint64_t *total) {
+  plan_t P = {ops, nops, table, stride};
+  uint64_t pos = 0;
+  (void)heap_len;
+  for (uint64_t r = 0; r < n; ++r) {
+    const uint8_t *nat = native + r * stride;
+    uint32_t err = 0, op_i = 0;
+    if (offsets) offsets[r] = pos;
+    /* xdr_to_opaque sizes the argument pack first (marshal.h:264-268):
+     * a bad discriminant throws before any byte is written. */
+    rec_size(&P, nat, &err, &op_i);
+    if (err) { *erec = r; *eop = op_i; return (int)err; }
+    uint32_t pc = 0;
+    for (;;) {
+      const xdrg_op *op = &ops[pc];
+      if (op->kind == XDRG_OP_END) break;
+      if (op->kind != XDRG_OP_JUMP && op->depth > stack_limit) {
+        *erec = r; *eop = pc; return XDRG_ERR_STACK_PUT;
+      }
+      uint64_t need = 0;
+      switch (op->kind) {
+      case XDRG_OP_U32: case XDRG_OP_ENUM: case XDRG_OP_BOOL: case XDRG_OP_UNION: need = 4; break;
+      case XDRG_OP_U64: need = 8; break;
+      case XDRG_OP_OPAQUE: need = op->arg0; break;
+      case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
+        xdrg_bytes_ref ref; memcpy(&ref, nat + op->noff, sizeof ref);
+        need = 4 + (uint64_t)ref.len;
+        break;
+      }
+      default: break;
+      }
+      /* check(n): marshal.h:104-108 */
+      if (need > cap - pos) { *erec = r; *eop = pc; return XDRG_ERR_OVERFLOW_PUT; }
+      switch (op->kind) {
+      case XDRG_OP_U32: case XDRG_OP_ENUM:
+        wr32(out + pos, bswap32(rd32(nat + op->noff))); pos += 4; ++pc; break;
+      case XDRG_OP_BOOL:
+        wr32(out + pos, bswap32(nat[op->noff] != 0)); pos += 4; ++pc; break;
+      case XDRG_OP_U64: {
+        uint64_t v = rd64(nat + op->noff);
+        wr32(out + pos, bswap32((uint32_t)(v >> 32)));
+        wr32(out + pos + 4, bswap32((uint32_t)v));
+        pos += 8; ++pc; break;
+      }
+      case XDRG_OP_OPAQUE: {
+        uint32_t len = op->arg0;
+        if (len) {
+          memcpy(out + pos, nat + op->noff, len);
+          for (uint64_t k = len; k & 3; ++k) out[pos + k] = 0;
+          pos += pad4(len);
+        }
+        ++pc; break;
+      }
+      case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
+        xdrg_bytes_ref ref; memcpy(&ref, nat + op->noff, sizeof ref);
+        wr32(out + pos, bswap32(ref.len)); pos += 4;
+        if (ref.len) {
+          memcpy(out + pos, heap + ref.off, ref.len);
+          for (uint64_t k = ref.len; k & 3; ++k) out[pos + k] = 0;
+          pos += pad4(ref.len);
+        }
+        ++pc; break;
+      }
+      case XDRG_OP_UNION: {
+        uint32_t d = rd32(nat + op->noff);
+        wr32(out + pos, bswap32(d)); pos += 4;
+        pc = (uint32_t)union_target(&P, op, d);
+        break;
+      }
+      case XDRG_OP_JUMP: pc = op->arg0; break;
+      default: ++pc; break;
+      }
+    }
+  }
+  if (offsets) offsets[n] = pos;
+  *total = pos;
+  return 0;
+}
+
+/* Per-record xdr_size (no writes). */
+int xdro_sizes(const xdrg_op *ops, uint32_t nops, const uint32_t *table, uint32_t stride,
+               const uint8_t *native, uint64_t n, uint32_t *sizes, uint64_t *erec, uint32_t *eop) {
+  plan_t P = {ops, nops, table, stride};
+  for (uint64_t r = 0; r < n; ++r) {
+    uint32_t err = 0, op_i = 0;
+    uint64_t s = rec_size(&P, native + r * stride, &err, &op_i);
+    if (err) { *erec = r; *eop = op_i; return (int)err; }
+    sizes[r] = (uint32_t)s;
+  }
+  return 0;
+}
+
+/* ---------------------------------------------------------------- decode */
+/* Decode one record from [p, e); returns 0 or an error code (op in *eop).
+ * *pp is advanced.  Native record is zero-filled first. */
+static int dec_record(const plan_t *P, const uint8_t **pp, const uint8_t *e, uint8_t *nat,
+                      uint8_t *heap_out, uint64_t *hcur, uint32_t stack_limit, uint32_t *eop) {
+  const uint8_t *p = *pp;
+  uint32_t pc = 0;
+  memset(nat, 0, P->stride);
+#define CHECK(nb) do { if ((uint64_t)(nb) > (uint64_t)(e - p)) { *eop = pc; *pp = p; return XDRG_ERR_OVERFLOW_GET; } } while (0)
+  for (;;) {
+    const xdrg_op *op = &P->ops[pc];
+    if (op->kind == XDRG_OP_END) break;
+    if (op->kind != XDRG_OP_JUMP && op->depth > stack_limit) {
+      *eop = pc; *pp = p; return XDRG_ERR_STACK_GET;
+    }
+    switch (op->kind) {
+    case XDRG_OP_U32:
+      CHECK(4); wr32(nat + op->noff, bswap32(rd32(p))); p += 4; ++pc; break;
+    case XDRG_OP_ENUM: {
+      CHECK(4);
+      uint32_t v = bswap32(rd32(p));
+      wr32(nat + op->noff, v); p += 4;
+      if (!enum_ok(P, op, v)) { *eop = pc; *pp = p; return XDRG_ERR_INVALID_ENUM; }
+      ++pc; break;
+    }
+    case XDRG_OP_BOOL:
+      CHECK(4); nat[op->noff] = rd32(p) != 0; p += 4; ++pc; break;
+    case XDRG_OP_U64: {
+      CHECK(8);
+      uint64_t hi = bswap32(rd32(p)), lo = bswap32(rd32(p + 4));
+      wr64(nat + op->noff, hi << 32 | lo); p += 8; ++pc; break;
+    }
+    case XDRG_OP_OPAQUE: {
+      uint32_t len = op->arg0;
+      CHECK(len);
+      if (len) {
+        memcpy(nat + op->noff, p, len);
+        p += len;
+        for (uint64_t k = len; k & 3; ++k)
+          if (*p++ != 0) { *eop = pc; *pp = p; return XDRG_ERR_NONZERO_PAD; }
+      }
+      ++pc; break;
+    }
+    case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
+      CHECK(4);
+      uint32_t len = bswap32(rd32(p)); p += 4;
+      CHECK(len);
+      if (len > op->arg0) {
+        *eop = pc; *pp = p;
+        return op->kind == XDRG_OP_STRING ? XDRG_ERR_XSTRING_BOUND : XDRG_ERR_XVECTOR_BOUND;
+      }
+      xdrg_bytes_ref ref = {*hcur, len, 0};
+      if (len) {
+        memcpy(heap_out + *hcur, p, pad4(len)); /* payload + (verified zero) pad */
+        p += len;
+        for (uint64_t k = len; k & 3; ++k)
+          if (*p++ != 0) { *eop = pc; *pp = p; return XDRG_ERR_NONZERO_PAD; }
+        *hcur += pad4(len);
+      }
+      memcpy(nat + op->noff, &ref, sizeof ref);
+      ++pc; break;
+    }
+    case XDRG_OP_UNION: {
+      CHECK(4);
+      uint32_t d = bswap32(rd32(p)); p += 4;
+      if (!enum_ok(P, op, d)) { *eop = pc; *pp = p; return XDRG_ERR_INVALID_ENUM; }
+      int64_t t = union_target(P, op, d);
+      if (t < 0) { *eop = pc; *pp = p; return XDRG_ERR_BAD_DISCRIMINANT; }
+      wr32(nat + op->noff, d);
+      pc = (uint32_t)t;
+      break;
+    }
+    case XDRG_OP_JUMP: pc = op->arg0; break;
+    default: ++pc; break;
+    }
+  }
+#undef CHECK
+  *pp = p;
+  return 0;
+}
+
+/*
+ * Fixed or indexed batch decode (see xdrg_decode in include/xdrgpu.h for the
+ * contract).  offsets == NULL: one xdr_generic_get over [xdr, xdr+len) for n
+ * records, then done().  offsets != NULL: record r is xdr_from_opaque of the
+ * slice [off[r], off[r+1]); heap output for record r starts at off[r].
+ */
+int xdro_decode(const xdrg_op *ops, uint32_t nops, const uint32_t *table, uint32_t stride,
+                const uint8_t *xdr, uint64_t len, const uint64_t *offsets, uint64_t n,
+                uint8_t *native, uint8_t *heap_out, uint32_t stack_limit, uint64_t *erec,
+                uint32_t *eop) {
+  plan_t P = {ops, nops, table, stride};
+  if (!offsets) {
+    if (len & 3) { *erec = 0; *eop = 0xffffffffu; return XDRG_ERR_SIZE_NOT_MULT4; }
+    const uint8_t *p = xdr, *e = xdr + len;
+    uint64_t hcur = 0;
+    for (uint64_t r = 0; r < n; ++r) {
+      int rc = dec_record(&P, &p, e, native + r * stride, heap_out, &hcur, stack_limit, eop);
+      if (rc) { *erec = r; return rc; }
+    }
+    if (p != e) { *erec = n; *eop = 0xffffffffu; return XDRG_ERR_TRAILING; }
+    return 0;
+  }
+  for (uint64_t r = 0; r < n; ++r) {
+    uint64_t a = offsets[r], b = offsets[r + 1];
+    if (b < a || b > len) { *erec = r; *eop = 0; return XDRG_ERR_OVERFLOW_GET; }
+    if ((b - a) & 3) { *erec = r; *eop = 0xffffffffu; return XDRG_ERR_SIZE_NOT_MULT4; }
+    const uint8_t *p = xdr + a, *e = xdr + b;
+    uint64_t hcur = a;
+    int rc = dec_record(&P, &p, e, native + r * stride, heap_out, &hcur, stack_limit, eop);
+    if (rc) { *erec = r; return rc; }
+    if (p != e) { *erec = r; *eop = 0xffffffffu; return XDRG_ERR_TRAILING; }
+  }
+  if (offsets[n] != len) { *erec = n; *eop = 0xffffffffu; return XDRG_ERR_TRAILING; }
+  return 0;
+}

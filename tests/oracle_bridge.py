@@ -1,0 +1,90 @@
+"""ctypes bridge to the C restatement oracle (oracle/_build/liboracle.so).
+
+TEST INFRASTRUCTURE: used only by tests/, __graft_entry__.smoke() (as the
+checker) and bench.py's cpu_baseline leg.  Builds the oracle with gcc on
+first use if it is missing (gcc exists on the GPU box too).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+LIB = os.path.join(ORACLE_DIR, "_build", "liboracle.so")
+REF_BIN = os.path.join(ORACLE_DIR, "_ref", "ref_golden")
+
+_lib = None
+
+
+def build() -> None:
+    src = os.path.join(ORACLE_DIR, "xdr_oracle.c")
+    os.makedirs(os.path.dirname(LIB), exist_ok=True)
+    subprocess.check_call(["gcc", "-O2", "-fPIC", "-shared", "-std=c11", "-o", LIB, src])
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        src = os.path.join(ORACLE_DIR, "xdr_oracle.c")
+        if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(src):
+            build()
+        L = C.CDLL(LIB)
+        vp, u64, u32 = C.c_void_p, C.c_uint64, C.c_uint32
+        L.xdro_encode.argtypes = [vp, u32, vp, u32, vp, u64, vp, u64, vp, u64, vp, u32,
+                                  C.POINTER(u64), C.POINTER(u32), C.POINTER(u64)]
+        L.xdro_decode.argtypes = [vp, u32, vp, u32, vp, u64, vp, u64, vp, vp, u32,
+                                  C.POINTER(u64), C.POINTER(u32)]
+        L.xdro_sizes.argtypes = [vp, u32, vp, u32, vp, u64, vp, C.POINTER(u64), C.POINTER(u32)]
+        _lib = L
+    return _lib
+
+
+def _p(a: np.ndarray | None):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+class OracleError(Exception):
+    def __init__(self, code: int, record: int, op: int):
+        super().__init__(f"oracle error code={code} record={record} op={op}")
+        self.code, self.record, self.op = code, record, op
+
+
+def encode(plan, native: np.ndarray, n: int, heap: np.ndarray | None = None,
+           stack_limit: int = 0xFFFFFFFF, cap: int | None = None):
+    """Returns (xdr bytes, offsets[n+1]) or raises OracleError."""
+    if heap is None or heap.size == 0:
+        heap = np.zeros(1, dtype=np.uint8)
+    sizes = np.zeros(max(n, 1), dtype=np.uint32)
+    er, eo = C.c_uint64(0), C.c_uint32(0)
+    if cap is None:
+        rc = lib().xdro_sizes(_p(plan.ops), len(plan.ops), _p(plan.table), plan.stride,
+                              _p(native), n, _p(sizes), C.byref(er), C.byref(eo))
+        cap = int(sizes[:n].astype(np.uint64).sum()) if rc == 0 else 1 << 20
+    out = np.zeros(max(cap, 4), dtype=np.uint8)
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    tot = C.c_uint64(0)
+    rc = lib().xdro_encode(_p(plan.ops), len(plan.ops), _p(plan.table), plan.stride,
+                           _p(native), n, _p(heap), heap.size, _p(out), cap, _p(offs),
+                           stack_limit, C.byref(er), C.byref(eo), C.byref(tot))
+    if rc:
+        raise OracleError(rc, er.value, eo.value)
+    return out[:tot.value], offs
+
+
+def decode(plan, xdr: np.ndarray, n: int, offsets: np.ndarray | None = None,
+           stack_limit: int = 0xFFFFFFFF):
+    """Returns (native, heap) or raises OracleError."""
+    native = np.zeros(max(n, 1) * plan.stride, dtype=np.uint8)
+    heap = np.zeros(max(xdr.size, 4), dtype=np.uint8)
+    er, eo = C.c_uint64(0), C.c_uint32(0)
+    x = xdr if xdr.size else np.zeros(4, dtype=np.uint8)
+    rc = lib().xdro_decode(_p(plan.ops), len(plan.ops), _p(plan.table), plan.stride,
+                           _p(x), xdr.size, _p(offsets), n, _p(native), _p(heap),
+                           stack_limit, C.byref(er), C.byref(eo))
+    if rc:
+        raise OracleError(rc, er.value, eo.value)
+    return native[:n * plan.stride], heap[:xdr.size]

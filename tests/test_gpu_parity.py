@@ -1,0 +1,326 @@
+"""GPU parity: libxdrgpu.so (through the C ABI) against the reference.
+
+Every comparison is against bytes the REAL reference produced
+(tests/golden, made by oracle/ref_golden from xdrpp/marshal.cc) or against
+the C restatement oracle where the reference has no fixture (fuzzed error
+streams).  XDR is integer work: everything is bit-exact.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+from conftest import SMALL_N, golden
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from xdrpp_amd import _abi as A  # noqa: E402
+from xdrpp_amd import marshal as M  # noqa: E402
+from xdrpp_amd import schemas as S  # noqa: E402
+from xdrpp_amd import workloads as W  # noqa: E402
+import oracle_bridge as O  # noqa: E402
+
+SCHEMAS = ["numerics", "rec128", "recvar", "rpc"]
+_plans = {}
+
+
+def plan(name):
+    if name not in _plans:
+        t = S.numerics_validated if name == "numerics_v" else S.ALL[name]
+        _plans[name] = M.Plan(t)
+    return _plans[name]
+
+
+def to_dev(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def sha(t):
+    return hashlib.sha256(t.cpu().numpy().tobytes()).hexdigest()
+
+
+# ----------------------------------------------------------------- golden
+@pytest.mark.parametrize("name", SCHEMAS)
+def test_golden_encode(dev, name):
+    n = SMALL_N[name]
+    p = plan(name)
+    mar = M.Marshaler(p, dev)
+    nat = golden(name, n, "native")
+    heap = golden(name, n, "heap")
+    res = mar.encode(to_dev(nat, dev), n, to_dev(heap, dev) if heap.size else None)
+    want = golden(name, n, "xdr")
+    assert np.array_equal(res.xdr.cpu().numpy(), want)
+    if not p.is_fixed:
+        offs = golden(name, n, "offsets", np.uint64)
+        assert np.array_equal(res.offsets.cpu().numpy().view(np.uint64), offs)
+
+
+@pytest.mark.parametrize("name", SCHEMAS)
+def test_golden_decode(dev, name):
+    n = SMALL_N[name]
+    p = plan(name)
+    mar = M.Marshaler(p, dev)
+    x = golden(name, n, "xdr")
+    offs = golden(name, n, "offsets", np.uint64)
+    t_off = None if p.is_fixed else to_dev(offs.view(np.int64), dev)
+    nat, heap = mar.decode(to_dev(x, dev), n, t_off)
+    if p.is_fixed:
+        assert np.array_equal(nat.cpu().numpy(), golden(name, n, "native"))
+    else:
+        o_nat, o_heap = O.decode(p.cp, x, n, offs)
+        assert np.array_equal(nat.cpu().numpy(), o_nat)
+        assert np.array_equal(heap.cpu().numpy(), o_heap)
+        # decode -> encode reproduces the reference bytes exactly
+        res = mar.encode(nat, n, heap)
+        assert np.array_equal(res.xdr.cpu().numpy(), x)
+
+
+# ------------------------------------------------------------- full size
+@pytest.mark.parametrize("name,n", [("rec128", 1 << 20), ("numerics", 1 << 16),
+                                    ("recvar", 1 << 16), ("rpc", 1 << 16),
+                                    ("recvar", 1 << 20), ("rpc", 1 << 20)])
+def test_full_size_hash(dev, manifest, name, n):
+    h = manifest["hashes"][f"{name}_{n}"]
+    p = plan(name)
+    mar = M.Marshaler(p, dev)
+    nat, heap = W.GENERATORS[name](n)
+    assert hashlib.sha256(nat.tobytes()).hexdigest() == h["native"]
+    t_nat = to_dev(nat, dev)
+    t_heap = to_dev(heap, dev) if heap.size else None
+    res = mar.encode(t_nat, n, t_heap)
+    assert res.xdr.numel() == h["xdr_bytes"]
+    assert sha(res.xdr) == h["xdr"]
+    back, bheap = mar.decode(res.xdr, n, res.offsets)
+    if p.is_fixed:
+        assert torch.equal(back, t_nat)
+    else:
+        assert sha(res.offsets) == h["offsets"]
+        res2 = mar.encode(back, n, bheap)
+        assert torch.equal(res2.xdr, res.xdr)  # round trip is the identity on the wire
+
+
+# -------------------------------------------------------------- KAT
+def test_known_answers(dev, kat):
+    mar = M.Marshaler(plan("numerics"), dev)
+    nat, _ = W.numerics(1)
+    assert mar.encode(to_dev(nat, dev), 1).xdr.cpu().numpy().tobytes().hex() == kat["numerics_marshal_cc"]
+    mar = M.Marshaler(plan("rec128"), dev)
+    nat, _ = W.rec128(1)
+    assert mar.encode(to_dev(nat, dev), 1).xdr.cpu().numpy().tobytes().hex() == kat["rec128_0"]
+    mar = M.Marshaler(plan("rpc"), dev)
+    nat, heap = W.rpc(64)
+    res = mar.encode(to_dev(nat, dev), 64, to_dev(heap, dev))
+    offs = res.offsets.cpu().numpy()
+    x = res.xdr.cpu().numpy()
+    for i, want in enumerate(kat["rpc_first64"]):
+        assert x[offs[i]:offs[i + 1]].tobytes().hex() == want
+
+
+def _recvar_record(bl):
+    """recvar with lengths as in ref_golden kat(): blob 1..bl, name 'h'*((3bl)%7)."""
+    t = S.recvar
+    buf = np.zeros(t.size, dtype=np.uint8)
+    heap = bytes(range(1, bl + 1)) + b"h" * ((bl * 3) % 7)
+
+    def put(off, v, dt):
+        buf[off:off + np.dtype(dt).itemsize] = np.array([v], dtype=dt).view(np.uint8)
+    put(t.offsets["id"], 0x0102030405060708, "<u8")
+    put(t.offsets["kind"], -2, "<i4")
+    put(t.offsets["blob"], 0, "<u8")
+    put(t.offsets["blob"] + 8, bl, "<u4")
+    put(t.offsets["name"], bl, "<u8")
+    put(t.offsets["name"] + 8, (bl * 3) % 7, "<u4")
+    put(t.offsets["score"], 1.5, "<f8")
+    return buf, np.frombuffer(heap, dtype=np.uint8).copy()
+
+
+@pytest.mark.parametrize("bl", range(8))
+def test_recvar_residues(dev, kat, bl):
+    mar = M.Marshaler(plan("recvar"), dev)
+    nat, heap = _recvar_record(bl)
+    res = mar.encode(to_dev(nat, dev), 1, to_dev(heap, dev) if heap.size else None)
+    assert res.xdr.cpu().numpy().tobytes().hex() == kat[f"recvar_len{bl}"]
+
+
+# ------------------------------------------------------------ error cases
+EXC_NAME = {"xdr_overflow": M.XdrOverflow, "xdr_stack_overflow": M.XdrStackOverflow,
+            "xdr_bad_message_size": M.XdrBadMessageSize,
+            "xdr_bad_discriminant": M.XdrBadDiscriminant,
+            "xdr_should_be_zero": M.XdrShouldBeZero,
+            "xdr_invariant_failed": M.XdrInvariantFailed}
+
+
+@pytest.mark.parametrize("case", [
+    "numerics_ok", "numerics_short", "numerics_trailing", "numerics_not_mult4",
+    "numerics_bool2", "numerics_enum99_novalidate", "numerics_enum99_validate",
+    "recvar_ok", "recvar_nonzero_pad", "recvar_blob_over_bound", "recvar_name_over_bound",
+    "recvar_len_past_end", "rpc_ok", "rpc_bad_mtype", "rpc_denied_ok", "rpc_bad_reject_stat",
+    "rpc_bad_reply_stat"])
+def test_reference_error_cases(dev, kat, case):
+    """Decode the reference's error inputs; exception class and what() must
+    equal what the reference threw (tests/golden/kat.json)."""
+    c = kat["errors"][case]
+    schema = case.split("_")[0]
+    pname = "numerics_v" if case == "numerics_enum99_validate" else schema
+    p = plan(pname)
+    mar = M.Marshaler(p, dev)
+    x = np.frombuffer(bytes.fromhex(c["input"]), dtype=np.uint8).copy()
+    offs = None
+    if not p.is_fixed:
+        offs = to_dev(np.array([0, x.size], dtype=np.int64), dev)
+    t_x = to_dev(x, dev) if x.size else torch.empty(0, dtype=torch.uint8, device=dev)
+    if c["exception"] == "none":
+        nat, _ = mar.decode(t_x, 1, offs)
+        if case == "numerics_bool2":
+            assert nat.cpu().numpy()[0] == 1  # any nonzero decodes as true
+        return
+    with pytest.raises(EXC_NAME[c["exception"]]) as ei:
+        mar.decode(t_x, 1, offs)
+    assert str(ei.value) == c["what"]
+    # trailing bytes after the last record are reported past it (record n)
+    assert ei.value.record == (1 if case == "numerics_trailing" else 0)
+
+
+# --------------------------------------------- batch errors vs the oracle
+def _oracle_err(fn):
+    try:
+        fn()
+    except O.OracleError as e:
+        return (e.code, e.record, e.op)
+    return None
+
+
+def _gpu_err(fn):
+    try:
+        fn()
+    except M.XdrRuntimeError as e:
+        return (e.code, e.record, 0xFFFFFFFF if e.op is None else e.op)
+    return None
+
+
+@pytest.mark.parametrize("name", ["numerics_v", "recvar", "rpc"])
+@pytest.mark.parametrize("seed", range(6))
+def test_fuzzed_stream_errors_match_oracle(dev, name, seed):
+    """Flip random bytes of a valid batch stream; the first failing record,
+    its op and the error code must match the C restatement, and every
+    record before it must decode identically."""
+    base = "numerics" if name == "numerics_v" else name
+    n = SMALL_N[base]
+    p = plan(name)
+    mar = M.Marshaler(p, dev)
+    x = golden(base, n, "xdr").copy()
+    offs = golden(base, n, "offsets", np.uint64)
+    rng = np.random.default_rng(seed)
+    for _ in range(3):
+        i = int(rng.integers(0, x.size))
+        x[i] = np.uint8(rng.integers(0, 256))
+    o_off = None if p.is_fixed else offs
+    want = _oracle_err(lambda: O.decode(p.cp, x, n, o_off))
+    t_off = None if p.is_fixed else to_dev(offs.view(np.int64), dev)
+    got = _gpu_err(lambda: mar.decode(to_dev(x, dev), n, t_off))
+    assert got == want
+
+
+@pytest.mark.parametrize("n", [0, 1, 3, 255, 257, 1023])
+@pytest.mark.parametrize("name", SCHEMAS)
+def test_ragged_batch_sizes(dev, name, n):
+    p = plan(name)
+    mar = M.Marshaler(p, dev)
+    nat, heap = W.GENERATORS[name](max(n, 1))
+    nat = nat[:n * p.stride]
+    want, offs = O.encode(p.cp, nat, n, heap)
+    t_nat = to_dev(nat, dev) if n else torch.empty(0, dtype=torch.uint8, device=dev)
+    res = mar.encode(t_nat, n, to_dev(heap, dev) if heap.size else None)
+    assert np.array_equal(res.xdr.cpu().numpy(), want)
+    back, bheap = mar.decode(res.xdr, n, res.offsets)
+    o_nat, o_heap = O.decode(p.cp, want, n, None if p.is_fixed else offs)
+    assert np.array_equal(back.cpu().numpy(), o_nat)
+
+
+@pytest.mark.parametrize("name", ["numerics", "rec128"])
+def test_unaligned_buffers(dev, name):
+    """4-byte-aligned (not 16) device buffers take the scalar-load variant."""
+    n = 333
+    p = plan(name)
+    mar = M.Marshaler(p, dev)
+    nat, _ = W.GENERATORS[name](n)
+    big = torch.zeros(nat.size + 16, dtype=torch.uint8, device=dev)
+    big[4:4 + nat.size] = to_dev(nat, dev)
+    src = big[4:4 + nat.size]
+    out = torch.zeros(n * p.fixed_size + 16, dtype=torch.uint8, device=dev)[4:4 + n * p.fixed_size]
+    s = torch.cuda.current_stream().cuda_stream
+    mar.status.init(s)
+    mar.launch_encode(src, n, out)
+    mar.check()
+    want, _ = O.encode(p.cp, nat, n)
+    assert np.array_equal(out.cpu().numpy(), want)
+
+
+def test_fixed_capacity_and_length_errors(dev):
+    p = plan("numerics")
+    mar = M.Marshaler(p, dev)
+    n = 100
+    nat, _ = W.numerics(n)
+    t_nat = to_dev(nat, dev)
+    cap = 44 * 37 + 16  # record 37 runs out at op 3 (i3 needs bytes 12..20)
+    with pytest.raises(M.XdrOverflow) as ei:
+        mar.encode(t_nat, n, capacity=cap)
+    assert str(ei.value) == "insufficient buffer space in xdr_generic_put"
+    assert (ei.value.record, ei.value.op) == (37, 3)
+    assert _oracle_err(lambda: O.encode(p.cp, nat, n, cap=cap)) == (A.ERR_OVERFLOW_PUT, 37, 3)
+    x = golden("numerics", 1000, "xdr")[:44 * 100]
+    for L, exc, rec in ((44 * 50 + 8, M.XdrOverflow, 50), (44 * 100 + 4, M.XdrBadMessageSize, 100),
+                        (44 * 100 - 2, M.XdrBadMessageSize, 0)):
+        xx = np.zeros(L, dtype=np.uint8)
+        xx[:min(L, x.size)] = x[:min(L, x.size)]
+        with pytest.raises(exc) as ei:
+            mar.decode(to_dev(xx, dev), n)
+        assert ei.value.record == rec
+        want = _oracle_err(lambda: O.decode(p.cp, xx, n))
+        assert (ei.value.code, ei.value.record) == want[:2]
+
+
+@pytest.mark.parametrize("name,limit", [("numerics", 0), ("numerics", 1), ("rpc", 3),
+                                        ("rpc", 4), ("rpc", 5), ("recvar", 0)])
+def test_stack_limit(dev, name, limit):
+    """marshaling_stack_limit (marshal.h:21,34,131-136,198-205)."""
+    n = 64
+    p = plan(name)
+    mar = M.Marshaler(p, dev)
+    nat, heap = W.GENERATORS[name](n)
+    t_heap = to_dev(heap, dev) if heap.size else None
+    want = _oracle_err(lambda: O.encode(p.cp, nat, n, heap, stack_limit=limit))
+    got = _gpu_err(lambda: mar.encode(to_dev(nat, dev), n, t_heap, stack_limit=limit))
+    assert got == want
+    x, offs = O.encode(p.cp, nat, n, heap)
+    o_off = None if p.is_fixed else offs
+    t_off = None if p.is_fixed else to_dev(offs.view(np.int64), dev)
+    want = _oracle_err(lambda: O.decode(p.cp, x, n, o_off, stack_limit=limit))
+    got = _gpu_err(lambda: mar.decode(to_dev(x, dev), n, t_off, stack_limit=limit))
+    assert got == want
+
+
+def test_bad_discriminant_encode(dev):
+    p = plan("rpc")
+    mar = M.Marshaler(p, dev)
+    n = 200
+    nat, heap = W.rpc(n)
+    nat = nat.reshape(n, p.stride).copy()
+    mt = S.rpc_msg.offset_of("body")
+    nat[150, mt:mt + 4] = np.array([7], dtype="<u4").view(np.uint8)
+    nat[170, mt:mt + 4] = np.array([9], dtype="<u4").view(np.uint8)
+    nat = nat.reshape(-1)
+    with pytest.raises(M.XdrBadDiscriminant) as ei:
+        mar.encode(to_dev(nat, dev), n, to_dev(heap, dev))
+    assert str(ei.value) == "bad value of mtype in _body_t"
+    assert ei.value.record == 150
+    assert _oracle_err(lambda: O.encode(p.cp, nat, n, heap))[:2] == (A.ERR_BAD_DISCRIMINANT, 150)
+
+
+def test_swaps(dev):
+    x = np.random.default_rng(1).integers(0, 2**63, 100003, dtype=np.int64)
+    t = to_dev(x, dev)
+    assert np.array_equal(M.swap64(t).cpu().numpy(), x.byteswap())
+    x32 = x.view(np.int32)
+    assert np.array_equal(M.swap32(to_dev(x32, dev)).cpu().numpy(), x32.byteswap())

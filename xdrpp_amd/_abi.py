@@ -1,0 +1,152 @@
+"""ctypes binding of the C ABI declared in include/xdrgpu.h.
+
+The shared library is built in-tree (xdrpp_amd/libxdrgpu.so, see
+xdrpp_amd/build.py).  There is no fallback: if the library is missing the
+import of anything that needs it raises, so a GPU run can never silently
+take a CPU path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libxdrgpu.so")
+
+# enum xdrg_op_kind
+OP_U32, OP_U64, OP_BOOL, OP_ENUM, OP_OPAQUE, OP_VAROPAQUE, OP_STRING, OP_UNION, OP_JUMP, OP_END = range(1, 11)
+F_VALIDATE = 1
+F_DEFAULT = 2
+
+PATH_FIXED_REG, PATH_FIXED_LDS, PATH_VAR = 1, 2, 3
+
+OK = 0
+API_ERRORS = {-1: "EINVAL", -2: "EALIGN", -3: "EUNSUPPORTED", -4: "EHIP", -5: "ENOMEM", -6: "ESPACE"}
+
+# enum xdrg_err
+ERR_NONE = 0
+ERR_OVERFLOW_GET = 1
+ERR_OVERFLOW_PUT = 2
+ERR_XVECTOR_BOUND = 3
+ERR_XSTRING_BOUND = 4
+ERR_NONZERO_PAD = 5
+ERR_BAD_DISCRIMINANT = 6
+ERR_INVALID_ENUM = 7
+ERR_STACK_PUT = 8
+ERR_STACK_GET = 9
+ERR_SIZE_NOT_MULT4 = 10
+ERR_TRAILING = 11
+
+XDR_MAX_LEN = 0xFFFFFFFC  # xdrpp/types.h:360
+DEFAULT_STACK_LIMIT = 0xFFFFFFFF  # xdrpp/marshal.cc:6
+
+
+class XdrgOp(C.Structure):
+    _fields_ = [
+        ("kind", C.c_uint8),
+        ("flags", C.c_uint8),
+        ("depth", C.c_uint16),
+        ("noff", C.c_uint32),
+        ("arg0", C.c_uint32),
+        ("arg1", C.c_uint32),
+        ("arg2", C.c_uint32),
+        ("arg3", C.c_uint32),
+        ("arg4", C.c_uint32),
+        ("name", C.c_uint32),
+    ]
+
+
+assert C.sizeof(XdrgOp) == 32
+
+
+class XdrgPlanInfo(C.Structure):
+    _fields_ = [
+        ("path", C.c_uint32),
+        ("native_stride", C.c_uint32),
+        ("fixed_size", C.c_uint32),
+        ("max_depth", C.c_uint32),
+        ("nops", C.c_uint32),
+        ("has_checks", C.c_uint32),
+    ]
+
+
+class XdrgStatus(C.Structure):
+    _fields_ = [("first_error", C.c_uint64), ("total_bytes", C.c_uint64)]
+
+
+class XdrgError(C.Structure):
+    _fields_ = [
+        ("code", C.c_int32),
+        ("exc", C.c_int32),
+        ("record", C.c_uint64),
+        ("op", C.c_uint32),
+        ("rsv", C.c_uint32),
+        ("total_bytes", C.c_uint64),
+    ]
+
+
+# Every symbol include/xdrgpu.h declares (checked by tests/test_abi.py).
+EXPORTED = (
+    "xdrg_abi_version", "xdrg_plan_create", "xdrg_plan_destroy", "xdrg_plan_get_info",
+    "xdrg_workspace_size", "xdrg_status_init", "xdrg_status_read", "xdrg_encode",
+    "xdrg_decode", "xdrg_serial_sizes", "xdrg_swap32", "xdrg_swap64",
+    "xdrg_error_message", "xdrg_error_exception", "xdrg_last_hip_error",
+)
+
+_lib = None
+
+
+class AbiError(RuntimeError):
+    """An API-level failure (bad arguments, HIP error) of the C ABI."""
+
+
+def lib() -> C.CDLL:
+    """Load libxdrgpu.so (once).  Raises if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+            " (there is no CPU fallback)")
+    L = C.CDLL(LIB_PATH)
+    vp, u64, u32, sz = C.c_void_p, C.c_uint64, C.c_uint32, C.c_size_t
+    L.xdrg_abi_version.restype = C.c_int
+    L.xdrg_plan_create.argtypes = [C.POINTER(XdrgOp), u32, C.POINTER(C.c_uint32), u32, u32, C.POINTER(vp)]
+    L.xdrg_plan_create.restype = C.c_int
+    L.xdrg_plan_destroy.argtypes = [vp]
+    L.xdrg_plan_destroy.restype = None
+    L.xdrg_plan_get_info.argtypes = [vp, C.POINTER(XdrgPlanInfo)]
+    L.xdrg_plan_get_info.restype = C.c_int
+    L.xdrg_workspace_size.argtypes = [vp, u64]
+    L.xdrg_workspace_size.restype = sz
+    L.xdrg_status_init.argtypes = [vp, vp]
+    L.xdrg_status_init.restype = C.c_int
+    L.xdrg_status_read.argtypes = [vp, vp, C.POINTER(XdrgError)]
+    L.xdrg_status_read.restype = C.c_int
+    L.xdrg_encode.argtypes = [vp, vp, u64, vp, u64, vp, u64, vp, u32, vp, sz, vp, vp]
+    L.xdrg_encode.restype = C.c_int
+    L.xdrg_decode.argtypes = [vp, vp, u64, vp, u64, vp, vp, u64, u32, vp, sz, vp, vp]
+    L.xdrg_decode.restype = C.c_int
+    L.xdrg_serial_sizes.argtypes = [vp, vp, u64, vp, u32, vp, vp]
+    L.xdrg_serial_sizes.restype = C.c_int
+    L.xdrg_swap32.argtypes = [vp, vp, u64, vp]
+    L.xdrg_swap32.restype = C.c_int
+    L.xdrg_swap64.argtypes = [vp, vp, u64, vp]
+    L.xdrg_swap64.restype = C.c_int
+    L.xdrg_error_message.argtypes = [C.c_int]
+    L.xdrg_error_message.restype = C.c_char_p
+    L.xdrg_error_exception.argtypes = [C.c_int]
+    L.xdrg_error_exception.restype = C.c_int
+    L.xdrg_last_hip_error.restype = C.c_char_p
+    if L.xdrg_abi_version() != 1:
+        raise ImportError("libxdrgpu.so ABI version mismatch")
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str) -> None:
+    if rc != OK:
+        msg = API_ERRORS.get(rc, str(rc))
+        if rc == -4:
+            msg += ": " + lib().xdrg_last_hip_error().decode()
+        raise AbiError(f"{what} failed: {msg}")

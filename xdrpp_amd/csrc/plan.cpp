@@ -1,0 +1,264 @@
+// Host-side plan compiler.
+//
+// A plan is the flat, wire-ordered field walk that xdr_traits<T>::save
+// performs (xdrc/gen_hh.cc:233-243 for structs, :649-660 for unions).  For
+// fixed-size plans (no opaque<>/string<>/unions: xdr_traits<T>::
+// has_fixed_size, xdrpp/types.h:689-700) the walk is turned into two
+// per-word byte-permutation programs:
+//   encode: wire word j  <- bytes of the native record (swap32 per 32-bit
+//           half, high half first for 64-bit values: xdrpp/marshal.h:65-80)
+//   decode: native word k <- bytes of the wire record (the inverse), with
+//           padding bytes of the native struct set to zero.
+// Variable plans are executed by the device interpreter directly.
+#include "plan.h"
+
+#include <algorithm>
+#include <cstring>
+
+namespace xdrg {
+namespace {
+
+constexpr int kNone = -1;
+constexpr int kBoolBase = -1000000;  // marks "bool of word w": kBoolBase - w
+
+uint32_t pad4(uint32_t n) { return (n + 3u) & ~3u; }
+
+bool is_fixed_kind(uint8_t k) {
+  return k == XDRG_OP_U32 || k == XDRG_OP_U64 || k == XDRG_OP_BOOL || k == XDRG_OP_ENUM ||
+         k == XDRG_OP_OPAQUE;
+}
+
+uint32_t native_size(const xdrg_op &op) {
+  switch (op.kind) {
+  case XDRG_OP_U32: case XDRG_OP_ENUM: case XDRG_OP_UNION: return 4;
+  case XDRG_OP_U64: return 8;
+  case XDRG_OP_BOOL: return 1;
+  case XDRG_OP_OPAQUE: return op.arg0;
+  case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: return sizeof(xdrg_bytes_ref);
+  default: return 0;
+  }
+}
+
+// Build a byte-permutation program: out word w takes bytes from the input
+// record per `src[4w + i]` (input byte index, kNone for zero, or a bool
+// marker).  `prefer_pair` asks for window base (w & ~1) when possible.
+void build_prog(const std::vector<int> &src, uint32_t in_words, uint32_t out_words,
+                fixed_prog &pg) {
+  pg.in_words = in_words;
+  pg.out_words = out_words;
+  pg.idx.assign(out_words, {0, 0});
+  pg.terms.clear();
+  pg.reg.assign(out_words, reg_word{0x0C0C0C0Cu, T_PERM, 0, 0, 0, 0});
+  bool reg_ok = true;
+  for (uint32_t w = 0; w < out_words; ++w) {
+    pg.idx[w].start = uint16_t(pg.terms.size());
+    int bytes[4];
+    for (int i = 0; i < 4; ++i) bytes[i] = src[4 * w + i];
+    // bool terms
+    for (int i = 0; i < 4; ++i) {
+      if (bytes[i] <= kBoolBase) {
+        // marker payload: (src word << 3) | (whole-word test << 2) | src byte
+        int sw = kBoolBase - bytes[i];
+        term t;
+        t.kind = T_BOOL;
+        t.src = uint16_t(sw >> 3);
+        t.sel = uint32_t(sw & 3) | (uint32_t((sw >> 2) & 1) << 16) | (uint32_t(i) << 8);
+        pg.terms.push_back(t);
+        bytes[i] = kNone;
+        pg.has_bool = true;
+      }
+    }
+    // perm terms: greedily cover the remaining source bytes with 8-byte
+    // windows; prefer the aligned pair containing word w.
+    bool done[4] = {false, false, false, false};
+    for (;;) {
+      int m = -1;
+      for (int i = 0; i < 4; ++i)
+        if (!done[i] && bytes[i] >= 0 && (m < 0 || bytes[i] < m)) m = bytes[i];
+      if (m < 0) break;
+      uint32_t base = uint32_t(m) / 4;
+      uint32_t pair = w & ~1u;
+      bool fits_pair = true;
+      for (int i = 0; i < 4; ++i)
+        if (!done[i] && bytes[i] >= 0 &&
+            !(uint32_t(bytes[i]) >= 4 * pair && uint32_t(bytes[i]) < 4 * pair + 8))
+          fits_pair = false;
+      if (fits_pair && pair + 1 < in_words) base = pair;
+      if (base + 1 >= in_words && base > 0) --base;  // window stays inside the record
+      uint32_t sel = 0;
+      for (int i = 0; i < 4; ++i) {
+        uint32_t s = 0x0C;
+        if (!done[i] && bytes[i] >= 0 && uint32_t(bytes[i]) >= 4 * base &&
+            uint32_t(bytes[i]) < 4 * base + 8) {
+          s = uint32_t(bytes[i]) - 4 * base;
+          done[i] = true;
+        }
+        sel |= s << (8 * i);
+      }
+      pg.terms.push_back(term{T_PERM, uint16_t(base), sel});
+    }
+    pg.idx[w].count = uint16_t(pg.terms.size() - pg.idx[w].start);
+    // register-path eligibility: at most one term; PERM within the pair,
+    // BOOL reading the same word index.
+    const uint32_t c = pg.idx[w].count;
+    if (c == 1) {
+      const term &t = pg.terms[pg.idx[w].start];
+      if (t.kind == T_PERM) {
+        if (t.src != (w & ~1u)) reg_ok = false;
+        pg.reg[w].sel = t.sel;
+        pg.reg[w].kind = T_PERM;
+      } else {
+        if (t.src != w) reg_ok = false;
+        pg.reg[w].sel = t.sel;
+        pg.reg[w].kind = T_BOOL;
+      }
+    } else if (c > 1) {
+      reg_ok = false;
+    }
+  }
+  pg.reg_ok = reg_ok;
+}
+
+}  // namespace
+
+int compile_plan(xdrg_plan &p) {
+  const uint32_t n = uint32_t(p.ops.size());
+  if (n == 0 || p.stride == 0) return XDRG_EINVAL;
+  bool fixed = true, saw_end = false;
+  p.max_depth = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const xdrg_op &op = p.ops[i];
+    if (op.kind < XDRG_OP_U32 || op.kind > XDRG_OP_END) return XDRG_EINVAL;
+    if (op.kind == XDRG_OP_END) { saw_end = true; continue; }
+    if (op.kind == XDRG_OP_JUMP) {
+      if (op.arg0 >= n || op.arg0 <= i) return XDRG_EINVAL;  // forward jumps only
+      fixed = false;
+      continue;
+    }
+    if (!is_fixed_kind(op.kind)) fixed = false;
+    p.max_depth = std::max<uint32_t>(p.max_depth, op.depth);
+    if (uint64_t(op.noff) + native_size(op) > p.stride) return XDRG_EINVAL;
+    if ((op.kind == XDRG_OP_ENUM || op.kind == XDRG_OP_UNION) && (op.flags & XDRG_F_VALIDATE) &&
+        uint64_t(op.arg0) + op.arg1 > p.table.size())
+      return XDRG_EINVAL;
+    if (op.kind == XDRG_OP_UNION) {
+      if (uint64_t(op.arg2) + 2ull * op.arg3 > p.table.size()) return XDRG_EINVAL;
+      for (uint32_t c = 0; c < op.arg3; ++c) {
+        uint32_t t = p.table[op.arg2 + 2 * c + 1];
+        if (t >= n || t <= i) return XDRG_EINVAL;
+      }
+      if ((op.flags & XDRG_F_DEFAULT) && (op.arg4 >= n || op.arg4 <= i)) return XDRG_EINVAL;
+    }
+    if ((op.kind == XDRG_OP_U32 || op.kind == XDRG_OP_ENUM || op.kind == XDRG_OP_UNION) &&
+        (op.noff & 3))
+      return XDRG_EINVAL;  // natural alignment (C ABI of the xdrc structs)
+    if (op.kind == XDRG_OP_U64 && (op.noff & 3)) return XDRG_EINVAL;
+    if ((op.kind == XDRG_OP_VAROPAQUE || op.kind == XDRG_OP_STRING) && (op.noff & 7))
+      return XDRG_EINVAL;
+  }
+  if (!saw_end || p.ops.back().kind != XDRG_OP_END) return XDRG_EINVAL;
+
+  p.has_checks = false;
+  p.checks.clear();
+  if (!fixed) {
+    p.fixed_size = 0;
+    p.path = XDRG_PATH_VAR;
+    for (const xdrg_op &op : p.ops)
+      if (op.kind == XDRG_OP_VAROPAQUE || op.kind == XDRG_OP_STRING || op.kind == XDRG_OP_UNION ||
+          op.kind == XDRG_OP_OPAQUE || (op.kind == XDRG_OP_ENUM && (op.flags & XDRG_F_VALIDATE)))
+        p.has_checks = true;
+    return XDRG_OK;
+  }
+
+  // ---- fixed plan: byte maps
+  uint32_t W = 0;
+  p.op_wire_off.assign(n, 0);
+  for (uint32_t i = 0; i + 1 < n; ++i) {
+    const xdrg_op &op = p.ops[i];
+    p.op_wire_off[i] = W;
+    W += op.kind == XDRG_OP_U64 ? 8 : op.kind == XDRG_OP_OPAQUE ? pad4(op.arg0) : 4;
+  }
+  p.op_wire_off[n - 1] = W;
+  p.fixed_size = W;
+  if (p.stride % 4) return XDRG_EUNSUPPORTED;  // word-granular native records
+  if (W == 0) return XDRG_EUNSUPPORTED;
+  const uint32_t S = p.stride;
+
+  std::vector<int> enc_src(W, kNone), dec_src(S, kNone);
+  for (uint32_t i = 0; i + 1 < n; ++i) {
+    const xdrg_op &op = p.ops[i];
+    const uint32_t wo = p.op_wire_off[i], no = op.noff;
+    switch (op.kind) {
+    case XDRG_OP_U32: case XDRG_OP_ENUM:
+      for (int k = 0; k < 4; ++k) {  // wire byte k = native byte 3-k (swap32)
+        enc_src[wo + k] = int(no + 3 - k);
+        dec_src[no + 3 - k] = int(wo + k);
+      }
+      break;
+    case XDRG_OP_U64:
+      for (int k = 0; k < 8; ++k) {  // full 64-bit byte reversal
+        enc_src[wo + k] = int(no + 7 - k);
+        dec_src[no + 7 - k] = int(wo + k);
+      }
+      break;
+    case XDRG_OP_BOOL:
+      // wire word = 0/1 in its last (least significant) byte
+      enc_src[wo + 3] = kBoolBase - int(no);               // src byte index = no
+      dec_src[no] = kBoolBase - int(wo);                    // src word*4
+      p.has_bool = true;
+      break;
+    case XDRG_OP_OPAQUE:
+      for (uint32_t k = 0; k < op.arg0; ++k) {
+        enc_src[wo + k] = int(no + k);
+        dec_src[no + k] = int(wo + k);
+      }
+      break;
+    default: break;
+    }
+  }
+  // Bool markers: encode tests one native byte (the C++ bool), decode tests
+  // the whole wire word ("any nonzero is true", types.h:341).  build_prog
+  // expects the payload (word << 3) | (whole << 2) | byte.
+  for (uint32_t b = 0; b < W; ++b)
+    if (enc_src[b] <= kBoolBase) {
+      int nb = kBoolBase - enc_src[b];
+      enc_src[b] = kBoolBase - ((nb / 4) << 3 | (nb & 3));
+    }
+  for (uint32_t b = 0; b < S; ++b)
+    if (dec_src[b] <= kBoolBase) {
+      int wb = kBoolBase - dec_src[b];
+      dec_src[b] = kBoolBase - ((wb / 4) << 3 | 4);
+    }
+  build_prog(enc_src, S / 4, W / 4, p.enc);
+  build_prog(dec_src, W / 4, S / 4, p.dec);
+
+  // decode checks
+  for (uint32_t i = 0; i + 1 < n; ++i) {
+    const xdrg_op &op = p.ops[i];
+    if (op.kind == XDRG_OP_OPAQUE && (op.arg0 & 3)) {
+      uint32_t last = (p.op_wire_off[i] + op.arg0) / 4;  // word holding the pad
+      uint32_t keep = op.arg0 & 3;
+      uint32_t mask = ~((1u << (8 * keep)) - 1u);
+      p.checks.push_back(check{C_PAD, uint16_t(last), i, mask, 0});
+    }
+    if (op.kind == XDRG_OP_ENUM && (op.flags & XDRG_F_VALIDATE))
+      p.checks.push_back(check{C_ENUM, uint16_t(p.op_wire_off[i] / 4), i, op.arg0, op.arg1});
+  }
+  p.has_checks = !p.checks.empty();
+
+  const bool identity = (S == W) && (W % 16 == 0) && p.enc.reg_ok && p.dec.reg_ok;
+  if (identity) {
+    for (const check &c : p.checks) {
+      reg_word &rw = p.dec.reg[c.word];  // identity layout: native word == wire word
+      if (rw.ck_kind) return XDRG_EUNSUPPORTED;
+      rw.ck_kind = c.kind;
+      rw.ck_op = c.op;
+      rw.ck_a = c.a;
+      rw.ck_b = c.b;
+    }
+  }
+  p.path = identity ? XDRG_PATH_FIXED_REG : XDRG_PATH_FIXED_LDS;
+  return XDRG_OK;
+}
+
+}  // namespace xdrg

@@ -1,0 +1,91 @@
+// Internal plan representation shared by the host plan compiler
+// (plan.cpp) and the kernels/launchers (xdrgpu.hip).
+#pragma once
+#include <cstdint>
+#include <vector>
+
+#include "../../include/xdrgpu.h"
+
+namespace xdrg {
+
+// One output word of a fixed-size program.  An output word is the OR of
+// one or more terms; each term reads an 8-byte window of the input record
+// (two consecutive 4-byte words starting at word `src`) and picks bytes
+// with a v_perm_b32 selector (byte values 0-7 pick window bytes, 0x0C
+// yields zero).  BOOL terms implement xdr_traits<bool> (types.h:335-349):
+//   encode: wire = (native byte `sel` of word `src` != 0) as big-endian 1
+//   decode: native byte `sel` = (wire word `src` != 0)
+enum term_kind : uint16_t { T_PERM = 1, T_BOOL = 2 };
+struct term {
+  uint16_t kind;
+  uint16_t src;  // input word index within the record
+  uint32_t sel;  // v_perm selector (PERM) or byte position (BOOL)
+};
+// Index of the terms producing output word j: terms[start, start+count).
+struct term_idx {
+  uint16_t start;
+  uint16_t count;
+};
+// Decode-time validation of one wire word (fixed plans).
+enum check_kind : uint16_t { C_PAD = 1, C_ENUM = 2 };
+struct check {
+  uint16_t kind;
+  uint16_t word;  // wire word index within the record
+  uint32_t op;    // plan op index (error ordering)
+  uint32_t a;     // PAD: register-order mask of bytes that must be zero; ENUM: table idx
+  uint32_t b;     // ENUM: count
+};
+
+// Register-path program for one 16-byte chunk position: output word i of
+// the chunk takes window pair (i & 2) of the same input chunk.
+// Decode-side checks ride along (ck_kind 0 = none) so a lane holds its
+// chunk's whole program in registers.
+struct reg_word {
+  uint32_t sel;
+  uint32_t kind;     // T_PERM or T_BOOL (BOOL: sel = byte position)
+  uint32_t ck_kind;  // 0, C_PAD or C_ENUM (decode only)
+  uint32_t ck_op;
+  uint32_t ck_a;
+  uint32_t ck_b;
+};
+
+struct fixed_prog {
+  uint32_t in_words;   // words per input record
+  uint32_t out_words;  // words per output record
+  std::vector<term_idx> idx;  // [out_words]
+  std::vector<term> terms;
+  bool reg_ok = false;         // eligible for the register path
+  std::vector<reg_word> reg;   // [out_words] when reg_ok
+  bool has_bool = false;
+};
+
+}  // namespace xdrg
+
+struct xdrg_plan {
+  std::vector<xdrg_op> ops;
+  std::vector<uint32_t> table;
+  uint32_t stride = 0;
+  uint32_t fixed_size = 0;  // 0 => variable
+  uint32_t path = 0;
+  uint32_t max_depth = 0;
+  bool has_checks = false;
+  bool has_bool = false;
+  // fixed plans
+  std::vector<uint32_t> op_wire_off;  // wire byte offset of each op (fixed)
+  xdrg::fixed_prog enc, dec;
+  std::vector<xdrg::check> checks;
+  // device copies (one allocation)
+  void *d_mem = nullptr;
+  const xdrg_op *d_ops = nullptr;
+  const uint32_t *d_table = nullptr;
+  const xdrg::term_idx *d_enc_idx = nullptr, *d_dec_idx = nullptr;
+  const xdrg::term *d_enc_terms = nullptr, *d_dec_terms = nullptr;
+  const xdrg::reg_word *d_enc_reg = nullptr, *d_dec_reg = nullptr;
+  const xdrg::check *d_checks = nullptr;
+};
+
+namespace xdrg {
+// Validates ops and builds all host-side programs.  Returns XDRG_OK or an
+// API error.  Does not touch the device.
+int compile_plan(xdrg_plan &p);
+}  // namespace xdrg

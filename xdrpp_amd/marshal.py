@@ -1,0 +1,259 @@
+"""Batched xdr_to_opaque / xdr_from_opaque on MI355X through the C ABI.
+
+Host-side mirror of the reference entry points (xdrpp/marshal.h:252-306):
+
+    xdr_to_opaque(r0, ..., rn-1)      -> to_opaque_batch(plan, native, heap)
+    xdr_from_opaque(bytes, r0, ...)   -> from_opaque_batch(plan, xdr, n, offsets)
+
+with the reference's exception classes and what() strings
+(xdrpp/types.h:57-99).  Buffers are torch CUDA(HIP) tensors; torch is only
+plumbing for device memory and streams — every byte is produced by the HIP
+kernels in libxdrgpu.so.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import torch
+
+from . import _abi as A
+from .xdr_types import CompiledPlan, XdrType, compile_plan
+
+
+# ---------------------------------------------------------------- exceptions
+class XdrRuntimeError(RuntimeError):
+    """xdr::xdr_runtime_error (types.h:59-61).  ``record``: index of the
+    failing record in the batch; ``op``: plan op index (None: record level)."""
+
+    def __init__(self, what: str, record: int | None = None, op: int | None = None,
+                 code: int = 0):
+        super().__init__(what)
+        self.what, self.record, self.op, self.code = what, record, op, code
+
+
+class XdrOverflow(XdrRuntimeError):  # types.h:64-66
+    pass
+
+
+class XdrStackOverflow(XdrRuntimeError):  # types.h:69-71
+    pass
+
+
+class XdrBadMessageSize(XdrRuntimeError):  # types.h:74-76
+    pass
+
+
+class XdrBadDiscriminant(XdrRuntimeError):  # types.h:79-81
+    pass
+
+
+class XdrShouldBeZero(XdrRuntimeError):  # types.h:84-86
+    pass
+
+
+class XdrInvariantFailed(XdrRuntimeError):  # types.h:89-91
+    pass
+
+
+_EXC = {1: XdrOverflow, 2: XdrStackOverflow, 3: XdrBadMessageSize, 4: XdrBadDiscriminant,
+        5: XdrShouldBeZero, 6: XdrInvariantFailed}
+
+
+# ---------------------------------------------------------------------- plan
+class Plan:
+    """A compiled, device-resident plan for one XDR type (xdrg_plan_create)."""
+
+    def __init__(self, t: XdrType | CompiledPlan):
+        self.cp = t if isinstance(t, CompiledPlan) else compile_plan(t)
+        L = A.lib()
+        ops = self.cp.ops
+        table = self.cp.table if self.cp.table.size else None
+        h = C.c_void_p()
+        A.check(L.xdrg_plan_create(
+            ops.ctypes.data_as(C.POINTER(A.XdrgOp)), len(ops),
+            None if table is None else table.ctypes.data_as(C.POINTER(C.c_uint32)),
+            0 if table is None else table.size, self.cp.stride, C.byref(h)), "xdrg_plan_create")
+        self.handle = h
+        info = A.XdrgPlanInfo()
+        A.check(L.xdrg_plan_get_info(h, C.byref(info)), "xdrg_plan_get_info")
+        self.path = info.path
+        self.fixed_size = info.fixed_size or None
+        self.stride = info.native_stride
+        self.max_depth = info.max_depth
+        self.has_checks = bool(info.has_checks)
+
+    @property
+    def is_fixed(self) -> bool:
+        return self.path != A.PATH_VAR
+
+    def workspace_bytes(self, n: int) -> int:
+        return int(A.lib().xdrg_workspace_size(self.handle, n))
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            A.lib().xdrg_plan_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+# -------------------------------------------------------------------- status
+class Status:
+    """Device-resident xdrg_status (16 bytes)."""
+
+    def __init__(self, device: torch.device):
+        self.buf = torch.empty(2, dtype=torch.int64, device=device)
+
+    @property
+    def ptr(self) -> int:
+        return self.buf.data_ptr()
+
+    def init(self, stream: int) -> None:
+        A.check(A.lib().xdrg_status_init(self.ptr, stream), "xdrg_status_init")
+
+    def read(self, stream: int) -> A.XdrgError:
+        e = A.XdrgError()
+        A.check(A.lib().xdrg_status_read(self.ptr, stream, C.byref(e)), "xdrg_status_read")
+        return e
+
+
+def error_from(plan: Plan, e: A.XdrgError) -> XdrRuntimeError | None:
+    if e.code == 0:
+        return None
+    what = A.lib().xdrg_error_message(e.code).decode()
+    op = None if e.op == 0xFFFFFFFF else int(e.op)
+    if e.code == A.ERR_BAD_DISCRIMINANT and op is not None:
+        what = plan.cp.bad_discriminant_message(op)
+    cls = _EXC.get(A.lib().xdrg_error_exception(e.code), XdrRuntimeError)
+    return cls(what, int(e.record), op, int(e.code))
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None or t.numel() == 0 else t.data_ptr()
+
+
+@dataclass
+class EncodeResult:
+    xdr: torch.Tensor            # uint8, exactly the encoded bytes
+    offsets: torch.Tensor | None  # uint64-as-int64 [n+1] record offsets (var plans)
+
+
+class Marshaler:
+    """Reusable encode/decode launcher for one plan: owns the status block
+    and the var-plan workspace so repeated calls allocate nothing."""
+
+    def __init__(self, plan: Plan, device: torch.device | str = "cuda"):
+        self.plan = plan
+        self.device = torch.device(device)
+        self.status = Status(self.device)
+        self._ws = torch.empty(0, dtype=torch.uint8, device=self.device)
+
+    def _workspace(self, n: int) -> torch.Tensor:
+        need = self.plan.workspace_bytes(n)
+        if self._ws.numel() < need:
+            self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+        return self._ws
+
+    # ---- raw launches (no sync, no status handling) -----------------------
+    def launch_encode(self, native, n, out, heap=None, offsets=None, stack_limit=A.DEFAULT_STACK_LIMIT,
+                      stream=None):
+        ws = self._workspace(n) if not self.plan.is_fixed else None
+        A.check(A.lib().xdrg_encode(
+            self.plan.handle, _ptr(native), n, _ptr(heap), 0 if heap is None else heap.numel(),
+            _ptr(out), out.numel(), _ptr(offsets), stack_limit, _ptr(ws),
+            0 if ws is None else ws.numel(), self.status.ptr,
+            _stream() if stream is None else stream), "xdrg_encode")
+
+    def launch_decode(self, xdr, n, native_out, offsets=None, heap_out=None,
+                      stack_limit=A.DEFAULT_STACK_LIMIT, stream=None):
+        A.check(A.lib().xdrg_decode(
+            self.plan.handle, _ptr(xdr), xdr.numel(), _ptr(offsets), n, _ptr(native_out),
+            _ptr(heap_out), 0 if heap_out is None else heap_out.numel(), stack_limit, None, 0,
+            self.status.ptr, _stream() if stream is None else stream), "xdrg_decode")
+
+    def check(self, stream=None) -> A.XdrgError:
+        e = self.status.read(_stream() if stream is None else stream)
+        err = error_from(self.plan, e)
+        if err is not None:
+            raise err
+        return e
+
+    # ---- reference-shaped API --------------------------------------------
+    def serial_sizes(self, native, n, stack_limit=A.DEFAULT_STACK_LIMIT) -> torch.Tensor:
+        """xdr_size of every record (xdrpp/types.h:240-244)."""
+        sizes = torch.empty(max(n, 1), dtype=torch.int32, device=self.device)
+        s = _stream()
+        self.status.init(s)
+        A.check(A.lib().xdrg_serial_sizes(self.plan.handle, _ptr(native), n, _ptr(sizes),
+                                          stack_limit, self.status.ptr, s), "xdrg_serial_sizes")
+        self.check(s)
+        return sizes[:n]
+
+    def encode(self, native: torch.Tensor, n: int, heap: torch.Tensor | None = None,
+               stack_limit: int = A.DEFAULT_STACK_LIMIT, capacity: int | None = None) -> EncodeResult:
+        """= xdr_to_opaque(r0, ..., rn-1) (marshal.h:264-272)."""
+        s = _stream()
+        if self.plan.is_fixed:
+            cap = n * self.plan.fixed_size if capacity is None else capacity
+            out = torch.empty(max(cap, 4), dtype=torch.uint8, device=self.device)[:cap]
+            self.status.init(s)
+            self.launch_encode(native, n, out, stack_limit=stack_limit, stream=s)
+            self.check(s)
+            return EncodeResult(out, None)
+        if capacity is None:
+            capacity = int(self.serial_sizes(native, n, stack_limit).to(torch.int64).sum().item())
+        out = torch.empty(max(capacity, 4), dtype=torch.uint8, device=self.device)
+        offsets = torch.empty(n + 1, dtype=torch.int64, device=self.device)
+        self.status.init(s)
+        self.launch_encode(native, n, out, heap=heap, offsets=offsets, stack_limit=stack_limit,
+                           stream=s)
+        e = self.check(s)
+        return EncodeResult(out[:e.total_bytes], offsets)
+
+    def decode(self, xdr: torch.Tensor, n: int, offsets: torch.Tensor | None = None,
+               stack_limit: int = A.DEFAULT_STACK_LIMIT):
+        """= xdr_from_opaque(bytes, r0, ..., rn-1) (marshal.h:299-306).
+        Returns (native uint8 tensor [n*stride], heap uint8 tensor or None)."""
+        s = _stream()
+        native = torch.zeros(max(n, 1) * self.plan.stride, dtype=torch.uint8, device=self.device)
+        heap = None
+        if not self.plan.is_fixed:
+            heap = torch.zeros(max(xdr.numel(), 4), dtype=torch.uint8, device=self.device)
+        self.status.init(s)
+        self.launch_decode(xdr, n, native, offsets=offsets, heap_out=heap,
+                           stack_limit=stack_limit, stream=s)
+        self.check(s)
+        return native[:n * self.plan.stride], (None if heap is None else heap[:xdr.numel()])
+
+
+def to_opaque_batch(plan: Plan, native: torch.Tensor, n: int, heap: torch.Tensor | None = None,
+                    **kw) -> EncodeResult:
+    return Marshaler(plan, native.device).encode(native, n, heap, **kw)
+
+
+def from_opaque_batch(plan: Plan, xdr: torch.Tensor, n: int, offsets: torch.Tensor | None = None,
+                      **kw):
+    return Marshaler(plan, xdr.device).decode(xdr, n, offsets, **kw)
+
+
+def swap32(x: torch.Tensor) -> torch.Tensor:
+    """Device swap32 over an int32 tensor (xdrpp/endian.h:56-60)."""
+    out = torch.empty_like(x)
+    A.check(A.lib().xdrg_swap32(_ptr(x), _ptr(out), x.numel(), _stream()), "xdrg_swap32")
+    return out
+
+
+def swap64(x: torch.Tensor) -> torch.Tensor:
+    """Device swap64 over an int64 tensor (xdrpp/endian.h:62-68)."""
+    out = torch.empty_like(x)
+    A.check(A.lib().xdrg_swap64(_ptr(x), _ptr(out), x.numel(), _stream()), "xdrg_swap64")
+    return out

@@ -1,0 +1,208 @@
+"""Deterministic synthetic record batches for the benchmark configs
+(SURVEY.md §8(d)).  numpy restatement of oracle/workload_gen.h +
+oracle/ref_golden.cc's generators; tests pin the two together through the
+committed fixtures (byte-equal small batches, sha256 of full-size ones).
+
+    draw(seed, i) = splitmix64 finaliser of seed + (i + 1) * GAMMA
+
+Every generator returns (native, heap): ``native`` is n * stride bytes in
+the staged layout of the schema (xdrpp_amd.schemas), ``heap`` the payload
+bytes the xdrg_bytes_ref fields point into (empty for fixed schemas).
+Payload heaps are packed in record order with no alignment, so device
+encodes exercise unaligned heap reads.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import schemas as S
+
+GAMMA = np.uint64(0x9E3779B97F4A7C15)
+SEED_NUMERICS = 0x5EED0001
+SEED_REC128 = 0x5EED0002
+SEED_RECVAR = 0x5EED0003
+SEED_RPC = 0x5EED0004
+SEED_REC128_MGPU = 0x5EED0005
+PAYLOAD_XOR = 0xB10BB10BB10BB10B
+
+_M1 = np.uint64(0xBF58476D1CE4E5B9)
+_M2 = np.uint64(0x94D049BB133111EB)
+
+
+def draw(seed: int, idx: np.ndarray) -> np.ndarray:
+    """splitmix64 outputs #idx of the stream seeded with ``seed``."""
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + (idx.astype(np.uint64) + np.uint64(1)) * GAMMA
+        z = (z ^ (z >> np.uint64(30))) * _M1
+        z = (z ^ (z >> np.uint64(27))) * _M2
+        return z ^ (z >> np.uint64(31))
+
+
+def _draws(seed: int, n: int, per: int, first: int = 0) -> np.ndarray:
+    idx = (np.arange(first, first + n, dtype=np.uint64)[:, None] * np.uint64(per)
+           + np.arange(per, dtype=np.uint64)[None, :])
+    return draw(seed, idx)
+
+
+def _put(buf: np.ndarray, off: int, values: np.ndarray, dt: str) -> None:
+    v = np.ascontiguousarray(values.astype(dt))
+    k = v.dtype.itemsize
+    buf[:, off:off + k] = v.view(np.uint8).reshape(-1, k)
+
+
+def numerics(n: int, seed: int = SEED_NUMERICS) -> tuple[np.ndarray, np.ndarray]:
+    t = S.numerics
+    d = _draws(seed, n, 8)
+    buf = np.zeros((n, t.size), dtype=np.uint8)
+    o = t.offsets
+    _put(buf, o["b"], d[:, 0] & np.uint64(1), "u1")
+    for f, k, dt in (("i1", 1, "<u4"), ("i2", 2, "<u4"), ("i3", 3, "<u8"), ("i4", 4, "<u8"),
+                     ("f1", 5, "<u4"), ("f2", 6, "<u8")):
+        _put(buf, o[f], d[:, k] & np.uint64(0xFFFFFFFF) if dt == "<u4" else d[:, k], dt)
+    _put(buf, o["e1"], d[:, 7] % np.uint64(3), "<u4")
+    if n:
+        # record 0 = tests/marshal.cc:482-490
+        r0 = np.zeros((1, t.size), dtype=np.uint8)
+        _put(r0, o["b"], np.array([0]), "u1")
+        _put(r0, o["i1"], np.array([0x7eeeeeee]), "<u4")
+        _put(r0, o["i2"], np.array([0xffffffff]), "<u4")
+        _put(r0, o["i3"], np.array([0x7ddddddddddddddd], dtype=np.uint64), "<u8")
+        _put(r0, o["i4"], np.array([0xfccccccccccccccc], dtype=np.uint64), "<u8")
+        _put(r0, o["f1"], np.array([3.141592654], dtype="<f4").view("<u4"), "<u4")
+        _put(r0, o["f2"], np.array([2.71828182846], dtype="<f8").view("<u8"), "<u8")
+        _put(r0, o["e1"], np.array([1]), "<u4")
+        buf[0] = r0[0]
+    return buf.reshape(-1), np.zeros(0, dtype=np.uint8)
+
+
+def rec128(n: int, seed: int = SEED_REC128, first: int = 0) -> tuple[np.ndarray, np.ndarray]:
+    """rec128 has the identity layout: field k of the C++ struct is words
+    [4k..] / [8k..], so the record is just the draws laid out in order."""
+    d = _draws(seed, n, 20, first)
+    buf = np.empty((n, 128), dtype=np.uint8)
+    buf[:, 0:32] = (d[:, 0:8] & np.uint64(0xFFFFFFFF)).astype("<u4").view(np.uint8).reshape(n, 32)
+    buf[:, 32:128] = d[:, 8:20].astype("<u8").view(np.uint8).reshape(n, 96)
+    return buf.reshape(-1), np.zeros(0, dtype=np.uint8)
+
+
+def _payload_bytes(seed: int, n: int, words_per_rec: int, first_word: int, nwords: int,
+                   rec0: int = 0) -> np.ndarray:
+    """(n, 8*nwords) payload bytes: byte j of a field = byte (j % 8) of
+    draw(seed ^ PAYLOAD_XOR, r * words_per_rec + first_word + j // 8)."""
+    ps = seed ^ PAYLOAD_XOR
+    idx = (np.arange(rec0, rec0 + n, dtype=np.uint64)[:, None] * np.uint64(words_per_rec)
+           + np.uint64(first_word) + np.arange(nwords, dtype=np.uint64)[None, :])
+    return draw(ps, idx).astype("<u8").view(np.uint8).reshape(n, 8 * nwords)
+
+
+def _pack_heap(fields: list[tuple[np.ndarray, np.ndarray]]) -> tuple[np.ndarray, list[np.ndarray]]:
+    """Pack per-record payload fields into one heap in record order, field
+    order.  fields = [(bytes (n, maxlen), lengths (n,)), ...].  Returns the
+    heap and, per field, the heap offset of each record's payload."""
+    n = fields[0][1].shape[0]
+    lens = np.stack([f[1].astype(np.int64) for f in fields], axis=1)  # (n, F)
+    flat = lens.reshape(-1)
+    starts = np.zeros(flat.shape[0], dtype=np.int64)
+    if flat.shape[0] > 1:
+        np.cumsum(flat[:-1], out=starts[1:])
+    starts = starts.reshape(n, len(fields))
+    cols = np.concatenate([f[0] for f in fields], axis=1)
+    mask = np.concatenate([np.arange(f[0].shape[1])[None, :] < f[1][:, None] for f in fields],
+                          axis=1)
+    return cols[mask], [starts[:, k] for k in range(len(fields))]
+
+
+def _put_ref(buf, off, hoff, lens):
+    _put(buf, off, hoff, "<u8")
+    _put(buf, off + 8, lens, "<u4")
+
+
+def recvar(n: int, seed: int = SEED_RECVAR) -> tuple[np.ndarray, np.ndarray]:
+    t = S.recvar
+    o = t.offsets
+    d = _draws(seed, n, 5)
+    blen = (d[:, 2] % np.uint64(257)).astype(np.int64)
+    nlen = (d[:, 3] % np.uint64(65)).astype(np.int64)
+    pb = _payload_bytes(seed, n, 40, 0, 40)
+    blob = pb[:, :256]
+    name = (np.uint8(0x61) + pb[:, 256:320] % np.uint8(26)).astype(np.uint8)
+    heap, (hb, hn) = _pack_heap([(blob, blen), (name, nlen)])
+    buf = np.zeros((n, t.size), dtype=np.uint8)
+    _put(buf, o["id"], d[:, 0], "<u8")
+    _put(buf, o["kind"], d[:, 1] & np.uint64(0xFFFFFFFF), "<u4")
+    _put_ref(buf, o["blob"], hb, blen)
+    _put_ref(buf, o["name"], hn, nlen)
+    _put(buf, o["score"], d[:, 4], "<u8")
+    return buf.reshape(-1), heap
+
+
+def rpc(n: int, seed: int = SEED_RPC) -> tuple[np.ndarray, np.ndarray]:
+    """rpc_msg records: sel = draw1 % 10; 0-4 CALL, 5 SUCCESS, 6 PROG_MISMATCH,
+    7 PROG_UNAVAIL (default void arm), 8 RPC_MISMATCH, 9 AUTH_ERROR."""
+    t = S.rpc_msg
+    off = t.offset_of
+    d = _draws(seed, n, 16)
+    sel = (d[:, 1] % np.uint64(10)).astype(np.int64)
+    call = sel <= 4
+    acc = (sel >= 5) & (sel <= 7)
+    den = sel >= 8
+    lo32 = lambda x: x & np.uint64(0xFFFFFFFF)  # noqa: E731
+    cred_len = np.where(call, (d[:, 6] % np.uint64(401)).astype(np.int64), 0)
+    verf_len = np.where(call, (d[:, 8] % np.uint64(401)).astype(np.int64),
+                        np.where(acc, (d[:, 6] % np.uint64(41)).astype(np.int64), 0))
+    cred_b = _payload_bytes(seed, n, 128, 0, 50)
+    verf_b = _payload_bytes(seed, n, 128, 64, 50)
+    heap, (hc, hv) = _pack_heap([(cred_b, cred_len), (verf_b, verf_len)])
+
+    buf = np.zeros((n, t.size), dtype=np.uint8)
+    _put(buf, off("xid"), lo32(d[:, 0]), "<u4")
+    _put(buf, off("body"), np.where(call, 0, 1).astype(np.uint64), "<u4")
+
+    def put_rows(mask, o, vals, dt):
+        if mask.any():
+            sub = buf[mask]
+            _put(sub, o, vals[mask], dt)
+            buf[mask] = sub
+
+    cb = "body.cbody"
+    put_rows(call, off(cb + ".rpcvers"), np.full(n, 2, dtype=np.uint64), "<u4")
+    put_rows(call, off(cb + ".prog"), lo32(d[:, 2]), "<u4")
+    put_rows(call, off(cb + ".vers"), lo32(d[:, 3]), "<u4")
+    put_rows(call, off(cb + ".proc"), lo32(d[:, 4]), "<u4")
+    put_rows(call, off(cb + ".cred.flavor"), d[:, 5] % np.uint64(2), "<u4")
+    put_rows(call, off(cb + ".cred.body"), hc.astype(np.uint64), "<u8")
+    put_rows(call, off(cb + ".cred.body") + 8, cred_len.astype(np.uint64), "<u4")
+    put_rows(call, off(cb + ".verf.flavor"), d[:, 7] % np.uint64(2), "<u4")
+    put_rows(call, off(cb + ".verf.body"), hv.astype(np.uint64), "<u8")
+    put_rows(call, off(cb + ".verf.body") + 8, verf_len.astype(np.uint64), "<u4")
+
+    rb = "body.rbody"
+    rep = ~call
+    put_rows(rep, off(rb), np.where(den, 1, 0).astype(np.uint64), "<u4")
+    ar = rb + ".areply"
+    put_rows(acc, off(ar + ".verf.flavor"), d[:, 5] % np.uint64(2), "<u4")
+    put_rows(acc, off(ar + ".verf.body"), hv.astype(np.uint64), "<u8")
+    put_rows(acc, off(ar + ".verf.body") + 8, verf_len.astype(np.uint64), "<u4")
+    astat = np.select([sel == 5, sel == 6, sel == 7], [0, 2, 1], 0).astype(np.uint64)
+    put_rows(acc, off(ar + ".reply_data"), astat, "<u4")
+    pm = sel == 6
+    put_rows(pm, off(ar + ".reply_data.mismatch_info.low"), lo32(d[:, 9]), "<u4")
+    put_rows(pm, off(ar + ".reply_data.mismatch_info.high"), lo32(d[:, 10]), "<u4")
+    rr = rb + ".rreply"
+    put_rows(den, off(rr), np.where(sel == 9, 1, 0).astype(np.uint64), "<u4")
+    rm = sel == 8
+    put_rows(rm, off(rr + ".mismatch_info.low"), lo32(d[:, 9]), "<u4")
+    put_rows(rm, off(rr + ".mismatch_info.high"), lo32(d[:, 10]), "<u4")
+    ae = sel == 9
+    put_rows(ae, off(rr + ".rj_why"), d[:, 11] % np.uint64(15), "<u4")
+    return buf.reshape(-1), heap
+
+
+GENERATORS = {"numerics": numerics, "rec128": rec128, "recvar": recvar, "rpc": rpc}
+
+
+def generate(schema: str, n: int, chunk: int = 1 << 16) -> tuple[np.ndarray, np.ndarray]:
+    """Generate in chunks (bounded temporaries); heap offsets are rebased."""
+    if schema in ("numerics", "rec128") or n <= chunk:
+        return GENERATORS[schema](n)
+    raise NotImplementedError("chunked generation of var schemas: use generate_var")
