@@ -42,10 +42,15 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--n", type=int, default=1 << 20, help="records per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-host-inclusive", action="store_true")
+    ap.add_argument("--host-inclusive", action="store_true",
+                    help="also measure pinned host->device->host rates (PCIe-bound, reported apart)")
+    ap.add_argument("--cold", action="store_true",
+                    help="also time each kernel alone after evicting the caches")
     ap.add_argument("--gather", action="store_true",
                     help="also time an RCCL gather of encoded shards to rank 0 (reported apart)")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--schema", default="rec128", choices=["rec128", "numerics", "recvar", "rpc"],
+                    help="rec128 is the headline; the others measure BASELINE.json configs 1, 3, 4")
     return ap.parse_args()
 
 
@@ -67,20 +72,20 @@ def barrier(dist):
         dist.barrier()
 
 
-def cpu_baseline(n_records: int, threads: int) -> dict | None:
+def cpu_baseline(schema: str, n_records: int, threads: int) -> dict | None:
     """The reference's CPU marshaler on this host: oracle/_ref/ref_golden
     (xdrpp/marshal.cc compiled from the reference sources) when present,
     else the C restatement in oracle/ (single thread)."""
     ref = os.path.join(ROOT, "oracle", "_ref", "ref_golden")
     if os.path.exists(ref) and os.access(ref, os.X_OK):
         reps = 10
-        out = subprocess.run([ref, "bench", "rec128", str(n_records), str(threads), str(reps)],
+        out = subprocess.run([ref, "bench", schema, str(n_records), str(threads), str(reps)],
                              capture_output=True, text=True, timeout=600)
         if out.returncode == 0:
             r = json.loads(out.stdout.strip().splitlines()[-1])
             return {"value": round(r["encode_decode_gib_s"], 4), "unit": "GiB/s", "cores": threads,
                     "kind": "reference",
-                    "sample": f"rec128 x {n_records} (the full batch), xdr_put/xdr_get streams over "
+                    "sample": f"{schema} x {n_records} (the full batch), xdr_put/xdr_get streams over "
                               f"{threads} contiguous slices, best of {reps}; per-record "
                               f"xdr_to_opaque {r['to_opaque_gib_s']:.3f} GiB/s",
                     "encode_gib_s": round(r["encode_gib_s"], 4),
@@ -88,16 +93,16 @@ def cpu_baseline(n_records: int, threads: int) -> dict | None:
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_bridge as O
 
-    plan = __import__("xdrpp_amd.xdr_types", fromlist=["compile_plan"]).compile_plan(S.rec128)
+    plan = __import__("xdrpp_amd.xdr_types", fromlist=["compile_plan"]).compile_plan(S.ALL[schema])
     ns = min(n_records, 1 << 18)
-    nat, _ = W.rec128(ns)
+    nat, heap = W.GENERATORS[schema](ns)
     t0 = time.perf_counter()
-    x, _ = O.encode(plan, nat, ns)
+    x, offs = O.encode(plan, nat, ns, heap)
     t1 = time.perf_counter()
-    O.decode(plan, x, ns)
+    O.decode(plan, x, ns, None if plan.fixed_size else offs)
     t2 = time.perf_counter()
     return {"value": round(2 * x.size / GIB / (t2 - t0), 4), "unit": "GiB/s", "cores": 1,
-            "kind": "port", "sample": f"rec128 x {ns}, oracle/xdr_oracle.c, 1 thread",
+            "kind": "port", "sample": f"{schema} x {ns}, oracle/xdr_oracle.c, 1 thread",
             "encode_gib_s": round(x.size / GIB / (t1 - t0), 4),
             "decode_gib_s": round(x.size / GIB / (t2 - t1), 4)}
 
@@ -149,20 +154,67 @@ def host_inclusive(mar, plan, nat_dev, n, W_, reps=5, nstreams=2, chunk_records=
             "chunk_records": chunk_records, "streams": nstreams}
 
 
+def cold_cache(mar, nat, xdr, back, n, alg_bytes, reps=5):
+    """Each kernel timed alone after a 1 GiB streaming READ that evicts the
+    256 MiB Infinity Cache and the L2s without leaving dirty lines whose
+    write-back would land inside the timed kernel."""
+    scratch = torch.ones(1 << 27, dtype=torch.int64, device=nat.device)  # 1 GiB
+    stream = torch.cuda.current_stream()
+    s = stream.cuda_stream
+    enc, dec = [], []
+    for r in range(reps):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        sink = scratch.sum()
+        ev[0].record(stream)
+        mar.launch_encode(nat, n, xdr, stream=s)
+        ev[1].record(stream)
+        sink = sink + scratch.sum()
+        ev[2].record(stream)
+        mar.launch_decode(xdr, n, back, stream=s)
+        ev[3].record(stream)
+        torch.cuda.synchronize()
+        enc.append(ev[0].elapsed_time(ev[1]))
+        dec.append(ev[2].elapsed_time(ev[3]))
+    del scratch
+    e, d = float(np.median(enc)), float(np.median(dec))
+    xb = n * 128
+    return {"encode_ms": round(e, 4), "decode_ms": round(d, 4),
+            "encode_decode_gib_s": round(2 * xb / GIB / ((e + d) * 1e-3), 2),
+            "achieved_GBps": round(alg_bytes / ((e + d) / 2 * 1e-3) / 1e9, 1),
+            "protocol": "1 GiB read sweep before each kernel, HIP events around the kernel, "
+                        f"median of {reps}"}
+
+
+def setup(schema, n, dev, rank, world):
+    """Plan, resident inputs and preallocated outputs for one rank."""
+    plan = M.Plan(S.ALL[schema])
+    mar = M.Marshaler(plan, dev)
+    if schema == "rec128":
+        seed = W.SEED_REC128 if world == 1 else W.SEED_REC128_MGPU
+        nat_np, heap_np = W.rec128(n, seed=seed, first=rank * n)
+    else:
+        nat_np, heap_np = W.GENERATORS[schema](n)
+    nat = torch.from_numpy(nat_np).to(dev)
+    heap = torch.from_numpy(heap_np).to(dev) if heap_np.size else None
+    back = torch.empty(n * plan.stride, dtype=torch.uint8, device=dev)
+    if plan.is_fixed:
+        xdr = torch.empty(n * plan.fixed_size, dtype=torch.uint8, device=dev)
+        return plan, mar, nat, heap, xdr, back, None, None
+    total = int(mar.serial_sizes(nat, n).to(torch.int64).sum().item())
+    xdr = torch.empty(total, dtype=torch.uint8, device=dev)
+    offsets = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    heap_out = torch.empty(total, dtype=torch.uint8, device=dev)
+    return plan, mar, nat, heap, xdr, back, offsets, heap_out
+
+
 def main():
     args = parse()
     dist, world, rank, local = dist_init(args)
     dev = torch.device("cuda", local)
     n = args.n
-    plan = M.Plan(S.rec128)
-    W_ = plan.fixed_size
+    plan, mar, nat, heap, xdr, back, offsets, heap_out = setup(args.schema, n, dev, rank, world)
     S_ = plan.stride
-    mar = M.Marshaler(plan, dev)
-    seed = W.SEED_REC128 if world == 1 else W.SEED_REC128_MGPU
-    nat_np, _ = W.rec128(n, seed=seed, first=rank * n)
-    nat = torch.from_numpy(nat_np).to(dev)
-    xdr = torch.empty(n * W_, dtype=torch.uint8, device=dev)
-    back = torch.empty(n * S_, dtype=torch.uint8, device=dev)
+    X = xdr.numel()
     stream = torch.cuda.current_stream()
     s = stream.cuda_stream
     mar.status.init(s)
@@ -170,10 +222,10 @@ def main():
     def step(ev=None):
         if ev is not None:
             ev[0].record(stream)
-        mar.launch_encode(nat, n, xdr, stream=s)
+        mar.launch_encode(nat, n, xdr, heap=heap, offsets=offsets, stream=s)
         if ev is not None:
             ev[1].record(stream)
-        mar.launch_decode(xdr, n, back, stream=s)
+        mar.launch_decode(xdr, n, back, offsets=offsets, heap_out=heap_out, stream=s)
         if ev is not None:
             ev[2].record(stream)
 
@@ -199,14 +251,25 @@ def main():
     enc_ms = [e[0].elapsed_time(e[1]) for e in evs]
     dec_ms = [e[1].elapsed_time(e[2]) for e in evs]
 
-    # correctness of what was timed: decode(encode(x)) == x everywhere, and
-    # on rank 0 of the 1-GPU config the stream hashes to the reference's.
-    ok_rt = bool(torch.equal(back, nat))
+    # correctness of what was timed: decode(encode(x)) == x (fixed) or
+    # encode(decode(encode(x))) == encode(x) (var); on the 1-GPU headline
+    # config the stream also hashes to the reference's output.
+    if plan.is_fixed:
+        ok_rt = bool(torch.equal(back, nat))
+    else:
+        x2 = torch.empty_like(xdr)
+        o2 = torch.empty_like(offsets)
+        mar.status.init(s)
+        mar.launch_encode(back, n, x2, heap=heap_out, offsets=o2, stream=s)
+        mar.check(s)
+        ok_rt = bool(torch.equal(x2, xdr))
     bit_exact = None
     man = os.path.join(ROOT, "tests", "golden", "manifest.json")
-    if world == 1 and n == (1 << 20) and os.path.exists(man):
-        want = json.load(open(man))["hashes"]["rec128_1048576"]["xdr"]
-        bit_exact = hashlib.sha256(xdr.cpu().numpy().tobytes()).hexdigest() == want
+    key = f"{args.schema}_{n}"
+    if world == 1 and os.path.exists(man):
+        hashes = json.load(open(man))["hashes"]
+        if key in hashes:
+            bit_exact = hashlib.sha256(xdr.cpu().numpy().tobytes()).hexdigest() == hashes[key]["xdr"]
 
     gather_ms = None
     if args.gather and dist is not None:
@@ -223,25 +286,44 @@ def main():
             dist.destroy_process_group()
         return
 
-    xdr_bytes_step = 2 * n * W_ * world
+    xdr_bytes_step = 2 * X * world
     value = xdr_bytes_step / GIB / (elapsed / args.steps)
-    # dominant kernel: k_fixed_reg (encode and decode are the same kernel
-    # with the encode / decode permutation programs)
-    alg_bytes = n * (S_ + W_)  # read one side + write the other, per launch
-    med = float(np.median(enc_ms + dec_ms))
-    avg = float(np.mean(enc_ms + dec_ms))
+    if plan.is_fixed:
+        # dominant kernel: k_fixed_reg / k_fixed_lds (encode and decode are
+        # the same kernel with the encode / decode permutation programs)
+        kern = "k_fixed_reg" if plan.path == A.PATH_FIXED_REG else "k_fixed_lds"
+        alg_bytes = n * S_ + X  # read one side + write the other, per launch
+        launches = enc_ms + dec_ms
+    else:
+        # dominant phase: encode (size pass + scan + k_var_encode) vs decode
+        H = 0 if heap is None else heap.numel()
+        enc_alg = n * S_ + H + X + 8 * (n + 1)
+        dec_alg = X + 8 * (n + 1) + n * S_ + X
+        if np.mean(enc_ms) >= np.mean(dec_ms):
+            kern, alg_bytes, launches = "k_var_size+k_scan_blocks+k_var_encode", enc_alg, enc_ms
+        else:
+            kern, alg_bytes, launches = "k_var_decode", dec_alg, dec_ms
+    med = float(np.median(launches))
+    avg = float(np.mean(launches))
     achieved = alg_bytes / (avg * 1e-3) / 1e9
     traffic = None
     tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tf):
         try:
             tj = json.load(open(tf))
-            if tj.get("records") == n and tj.get("kernel", "").startswith("k_fixed_reg"):
+            if tj.get("records") == n and tj.get("schema", "rec128") == args.schema \
+                    and tj.get("kernel") == kern:
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
+    wl = {"rec128": "rec128: 1M fixed-width 128-byte XDR records per GPU",
+          "numerics": "numerics (tests/xdrtest.x) fixed 44-byte records, 56-byte native",
+          "recvar": "recvar: opaque<256> + string<64> variable-length records",
+          "rpc": "rpc_msg (xdrpp/rpc_msg.x) nested discriminated unions"}[args.schema]
     line = {
-        "metric": "XDR encode+decode GiB/s (device-resident, 1M×128B records) + %HBM roofline",
+        "metric": ("XDR encode+decode GiB/s (device-resident, 1M×128B records) + %HBM roofline"
+                   if args.schema == "rec128" else
+                   f"XDR encode+decode GiB/s (device-resident, {args.schema}) + %HBM roofline"),
         "value": round(value, 2),
         "unit": "GiB/s",
         "n_gpus": world,
@@ -252,31 +334,33 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u32",
-        "data": "synthetic (splitmix64 seed 0x5EED0002 / 0x5EED0005, FP fields as raw bit patterns)",
-        "config": {"workload": "rec128: 1M fixed-width 128-byte XDR records per GPU, "
-                               "encode (xdr_to_opaque) + decode (xdr_from_opaque), device-resident",
-                   "records_per_gpu": n, "record_bytes": W_, "native_stride": S_,
-                   "parallelism": f"dp{world}"},
+        "data": "synthetic (splitmix64 seeds 0x5EED000x per SURVEY.md §8(d); FP fields as raw bit patterns)",
+        "config": {"workload": wl + ", encode (xdr_to_opaque) + decode (xdr_from_opaque), device-resident",
+                   "schema": args.schema, "records_per_gpu": n, "xdr_bytes_per_gpu": X,
+                   "native_stride": S_, "parallelism": f"dp{world}"},
         "encode_ms": round(float(np.mean(enc_ms)), 4),
         "decode_ms": round(float(np.mean(dec_ms)), 4),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "kernel": "k_fixed_reg", "median_launch_ms": round(med, 4),
+                     "traffic": traffic, "kernel": kern, "median_launch_ms": round(med, 4),
                      "alg_bytes_per_launch": alg_bytes},
         "round_trip_ok": ok_rt,
         "bit_exact_vs_reference": bit_exact,
     }
     if gather_ms is not None:
         line["gather_ms"] = round(gather_ms, 3)
-    if world == 1 and not args.no_host_inclusive:
+    if world == 1 and args.cold and plan.is_fixed:
+        line["cold_cache"] = cold_cache(mar, nat, xdr, back, n, alg_bytes)
+        mar.check(s)
+    if world == 1 and args.host_inclusive and plan.is_fixed:
         try:
-            line["host_inclusive"] = host_inclusive(mar, plan, nat, n, W_)
+            line["host_inclusive"] = host_inclusive(mar, plan, nat, n, plan.fixed_size)
         except Exception as e:  # reported, never fatal
             line["host_inclusive"] = {"error": str(e)[:200]}
     if world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         try:
-            line["cpu_baseline"] = cpu_baseline(n, threads)
+            line["cpu_baseline"] = cpu_baseline(args.schema, n, threads)
         except Exception as e:
             line["cpu_baseline"] = {"error": str(e)[:200]}
     print(json.dumps(line), flush=True)

@@ -46,193 +46,12 @@ int hip_fail(hipError_t e, const char *what) {
     if (e_ != hipSuccess) return hip_fail(e_, #x);  \
   } while (0)
 
-constexpr uint32_t kOpRecordLevel = 0xffff;  // op field for record-level errors
+}  // namespace
 
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+#include "kernels.h"
+using namespace xdrg::dev;
 
-// ------------------------------------------------------------------ device
-__device__ __forceinline__ uint32_t bswap32(uint32_t v) { return __builtin_bswap32(v); }
-
-// D = bytes of {hi:lo} picked by sel (v_perm_b32): 0-3 from lo, 4-7 from hi,
-// 0x0C -> 0x00.
-__device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
-  return __builtin_amdgcn_perm(hi, lo, sel);
-}
-
-// xdr_traits<bool> (xdrpp/types.h:335-349).  sel: src byte | dst byte << 8 |
-// whole-word test << 16.
-__device__ __forceinline__ uint32_t bool_term(uint32_t v, uint32_t sel) {
-  const bool nz = (sel & 0x10000u) ? (v != 0u) : (((v >> (8u * (sel & 3u))) & 0xffu) != 0u);
-  return nz ? (1u << (8u * ((sel >> 8) & 3u))) : 0u;
-}
-
-__device__ __forceinline__ void report(unsigned long long *err, uint64_t rec, uint32_t op,
-                                       uint32_t code) {
-  const unsigned long long key =
-      (static_cast<unsigned long long>(rec) << 24) |
-      (static_cast<unsigned long long>(op & 0xffffu) << 8) | code;
-  atomicMin(err, key);
-}
-
-__device__ __forceinline__ bool enum_ok(const uint32_t *__restrict__ table, uint32_t idx,
-                                        uint32_t cnt, uint32_t v) {
-  for (uint32_t i = 0; i < cnt; ++i)
-    if (table[idx + i] == v) return true;
-  return false;
-}
-
-// Decode-time word checks: padding of fixed opaque (marshal.cc:52-55) and
-// opt-in enum validation (types.h:157-173).  Returns an xdrg_err or 0.
-__device__ __forceinline__ uint32_t check_word(uint32_t w, uint32_t kind, uint32_t a, uint32_t b,
-                                               const uint32_t *__restrict__ table) {
-  if (kind == C_PAD) return (w & a) ? XDRG_ERR_NONZERO_PAD : 0u;
-  if (kind == C_ENUM) return enum_ok(table, a, b, bswap32(w)) ? 0u : XDRG_ERR_INVALID_ENUM;
-  return 0u;
-}
-
-__global__ void k_report(unsigned long long *err, uint64_t rec, uint32_t op, uint32_t code) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) report(err, rec, op, code);
-}
-
-// ---------------------------------------------------------- fixed: registers
-// One lane = one 16-byte chunk per step.  The grid stride is a multiple of
-// the chunks-per-record, so a lane's chunk position (and its program) never
-// changes: selectors live in registers for the whole launch.
-template <bool BOOLS, bool CHECKS, int U>
-__global__ __launch_bounds__(256) void k_fixed_reg(const u32x4 *__restrict__ in,
-                                                   u32x4 *__restrict__ out, uint64_t nchunks,
-                                                   uint32_t cpr, const reg_word *__restrict__ prog,
-                                                   const uint32_t *__restrict__ table,
-                                                   unsigned long long *err) {
-  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
-  const uint64_t c0 = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  const uint32_t q = static_cast<uint32_t>(c0 % cpr);
-  const reg_word *pw = prog + 4u * q;
-  const uint32_t s0 = pw[0].sel, s1 = pw[1].sel, s2 = pw[2].sel, s3 = pw[3].sel;
-  uint32_t k0 = T_PERM, k1 = T_PERM, k2 = T_PERM, k3 = T_PERM;
-  if (BOOLS) { k0 = pw[0].kind; k1 = pw[1].kind; k2 = pw[2].kind; k3 = pw[3].kind; }
-  uint32_t ck[4] = {0, 0, 0, 0}, cop[4] = {0, 0, 0, 0}, ca[4] = {0, 0, 0, 0}, cb[4] = {0, 0, 0, 0};
-  if (CHECKS) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      ck[i] = pw[i].ck_kind; cop[i] = pw[i].ck_op; ca[i] = pw[i].ck_a; cb[i] = pw[i].ck_b;
-    }
-  }
-  for (uint64_t c = c0; c < nchunks; c += U * stride) {
-    u32x4 v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint64_t cc = c + u * stride;
-      if (cc < nchunks) v[u] = __builtin_nontemporal_load(in + cc);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint64_t cc = c + u * stride;
-      if (cc < nchunks) {
-        const u32x4 w = v[u];
-        u32x4 o;
-        o.x = perm(w.y, w.x, s0);
-        o.y = perm(w.y, w.x, s1);
-        o.z = perm(w.w, w.z, s2);
-        o.w = perm(w.w, w.z, s3);
-        if (BOOLS) {
-          if (k0 == T_BOOL) o.x = bool_term(w.x, s0);
-          if (k1 == T_BOOL) o.y = bool_term(w.y, s1);
-          if (k2 == T_BOOL) o.z = bool_term(w.z, s2);
-          if (k3 == T_BOOL) o.w = bool_term(w.w, s3);
-        }
-        if (CHECKS) {
-          const uint32_t wv[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (ck[i]) {
-              const uint32_t e = check_word(wv[i], ck[i], ca[i], cb[i], table);
-              if (e) report(err, cc / cpr, cop[i], e);
-            }
-        }
-        __builtin_nontemporal_store(o, out + cc);
-      }
-    }
-  }
-}
-
-// -------------------------------------------------------------- fixed: LDS
-// A workgroup processes tiles of T records: coalesced load of T input
-// records into LDS, optional validation of the staged wire words, then each
-// lane builds 4 consecutive output words from the term program and stores
-// them as one 16-byte write.
-template <bool CHECKS, bool VEC>
-__global__ __launch_bounds__(256) void k_fixed_lds(
-    const uint32_t *__restrict__ in, uint32_t *__restrict__ out, uint64_t n, uint32_t in_words,
-    uint32_t out_words, uint32_t T, const term_idx *__restrict__ g_idx,
-    const term *__restrict__ g_terms, uint32_t nterms, const check *__restrict__ g_checks,
-    uint32_t nchecks, const uint32_t *__restrict__ table, unsigned long long *err) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  uint32_t *tile = smem;                         // T*in_words (+4 pad)
-  const uint32_t tile_words = T * in_words + 4;  // multiple of 4 (T % 4 == 0)
-  term_idx *sidx = reinterpret_cast<term_idx *>(smem + tile_words);
-  term *sterms = reinterpret_cast<term *>(smem + tile_words + ((out_words + 3u) & ~3u));
-  const uint32_t tid = threadIdx.x;
-  for (uint32_t i = tid; i < out_words; i += blockDim.x) sidx[i] = g_idx[i];
-  for (uint32_t i = tid; i < nterms; i += blockDim.x) sterms[i] = g_terms[i];
-  if (tid < 4) tile[T * in_words + tid] = 0u;
-
-  for (uint64_t t = blockIdx.x; t * T < n; t += gridDim.x) {
-    const uint64_t r0 = t * T;
-    const uint32_t nt = static_cast<uint32_t>(min<uint64_t>(T, n - r0));
-    const uint32_t nin = nt * in_words;
-    const uint32_t *src = in + r0 * in_words;
-    __syncthreads();  // previous tile fully consumed (and table copies visible)
-    if (VEC) {
-      const uint32_t nv = nin >> 2;
-      const u32x4 *s4 = reinterpret_cast<const u32x4 *>(src);
-      u32x4 *t4 = reinterpret_cast<u32x4 *>(tile);
-      for (uint32_t i = tid; i < nv; i += blockDim.x) t4[i] = __builtin_nontemporal_load(s4 + i);
-      for (uint32_t i = (nv << 2) + tid; i < nin; i += blockDim.x) tile[i] = src[i];
-    } else {
-      for (uint32_t i = tid; i < nin; i += blockDim.x) tile[i] = src[i];
-    }
-    __syncthreads();
-    if (CHECKS) {
-      for (uint32_t i = tid; i < nt * nchecks; i += blockDim.x) {
-        const uint32_t r = i / nchecks, k = i - r * nchecks;
-        const check ck = g_checks[k];
-        const uint32_t e = check_word(tile[r * in_words + ck.word], ck.kind, ck.a, ck.b, table);
-        if (e) report(err, r0 + r, ck.op, e);
-      }
-    }
-    const uint32_t nout = nt * out_words;
-    uint32_t *dst = out + r0 * out_words;
-    for (uint32_t o4 = tid * 4u; o4 < nout; o4 += blockDim.x * 4u) {
-      uint32_t r = o4 / out_words;
-      uint32_t j = o4 - r * out_words;
-      uint32_t vals[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        uint32_t v = 0u;
-        const term_idx ix = sidx[j];
-        const uint32_t base = r * in_words;
-        for (uint32_t q = 0; q < ix.count; ++q) {
-          const term tm = sterms[ix.start + q];
-          if (tm.kind == T_PERM)
-            v |= perm(tile[base + tm.src + 1u], tile[base + tm.src], tm.sel);
-          else
-            v |= bool_term(tile[base + tm.src], tm.sel);
-        }
-        vals[i] = v;
-        if (++j == out_words) { j = 0; ++r; }
-      }
-      if (VEC && o4 + 4u <= nout) {
-        __builtin_nontemporal_store(u32x4{vals[0], vals[1], vals[2], vals[3]},
-                                    reinterpret_cast<u32x4 *>(dst + o4));
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (o4 + i < nout) dst[o4 + i] = vals[i];
-      }
-    }
-  }
-}
+namespace {
 
 // ------------------------------------------------------------ var: helpers
 __device__ __forceinline__ uint32_t ld32(const uint8_t *p) {
@@ -587,6 +406,8 @@ __global__ void k_swap64(const uint64_t *__restrict__ in, uint64_t *__restrict__
 }
 
 // ------------------------------------------------------------------ host
+constexpr uint64_t kMallBytes = 256ull << 20;  // MI355X Infinity Cache
+
 uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 bool aligned(const void *p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) % a) == 0; }
 uint32_t gcd32(uint32_t a, uint32_t b) { while (b) { uint32_t t = a % b; a = b; b = t; } return a; }
@@ -621,32 +442,37 @@ int run_fixed(const xdrg_plan &p, bool decode, const void *in, void *out, uint64
   const fixed_prog &pg = decode ? p.dec : p.enc;
   const bool checks = decode && p.has_checks;
   if (p.path == XDRG_PATH_FIXED_REG && aligned(in, 16) && aligned(out, 16)) {
+    // Launch shapes from tools/tune/tune_fixed.py (rec128):
+    //  * working set (input + output) that fits the 256 MiB Infinity Cache
+    //    (1M records = 256 MiB): plain 16-byte loads/stores, one chunk in
+    //    flight per lane, 1024 workgroups -> 6.9 TB/s back to back;
+    //  * larger batches stream from HBM: non-temporal loads/stores, two
+    //    chunks in flight per lane, 512 workgroups -> 5.76 TB/s at 16M
+    //    records (a plain 16-byte copy of the same bytes: 5.67 TB/s).
     const uint32_t W = p.fixed_size;
     const uint32_t cpr = W / 16;
     const uint64_t nchunks = nrec * cpr;
-    constexpr int U = 4;
-    uint64_t blocks = (nchunks + 256ull * U - 1) / (256ull * U);
-    blocks = std::min<uint64_t>(blocks, 8192);
+    const bool streaming = nchunks * 32ull > kMallBytes * 3 / 2;  // in+out bytes > 384 MiB
+    uint64_t blocks = (nchunks + 255) / 256;
+    blocks = std::min<uint64_t>(blocks, streaming ? 512 : 1024);
     const uint32_t g0 = cpr / gcd32(cpr, 256);
     blocks = align_up(std::max<uint64_t>(blocks, 1), g0);
     const reg_word *prog = decode ? p.d_dec_reg : p.d_enc_reg;
     const bool bools = pg.has_bool;
-    if (!bools && !checks)
-      k_fixed_reg<false, false, U><<<blocks, 256, 0, s>>>(
-          static_cast<const u32x4 *>(in), static_cast<u32x4 *>(out), nchunks, cpr, prog,
-          p.d_table, err);
-    else if (bools && !checks)
-      k_fixed_reg<true, false, U><<<blocks, 256, 0, s>>>(
-          static_cast<const u32x4 *>(in), static_cast<u32x4 *>(out), nchunks, cpr, prog,
-          p.d_table, err);
-    else if (!bools && checks)
-      k_fixed_reg<false, true, U><<<blocks, 256, 0, s>>>(
-          static_cast<const u32x4 *>(in), static_cast<u32x4 *>(out), nchunks, cpr, prog,
-          p.d_table, err);
-    else
-      k_fixed_reg<true, true, U><<<blocks, 256, 0, s>>>(
-          static_cast<const u32x4 *>(in), static_cast<u32x4 *>(out), nchunks, cpr, prog,
-          p.d_table, err);
+    const u32x4 *i4 = static_cast<const u32x4 *>(in);
+    u32x4 *o4 = static_cast<u32x4 *>(out);
+#define LAUNCH_REG(B, C)                                                                         \
+  do {                                                                                           \
+    if (streaming)                                                                               \
+      k_fixed_reg<B, C, 2, true><<<blocks, 256, 0, s>>>(i4, o4, nchunks, cpr, prog, p.d_table, err); \
+    else                                                                                         \
+      k_fixed_reg<B, C, 1, false><<<blocks, 256, 0, s>>>(i4, o4, nchunks, cpr, prog, p.d_table, err); \
+  } while (0)
+    if (!bools && !checks) LAUNCH_REG(false, false);
+    else if (bools && !checks) LAUNCH_REG(true, false);
+    else if (!bools && checks) LAUNCH_REG(false, true);
+    else LAUNCH_REG(true, true);
+#undef LAUNCH_REG
     HIPCHK(hipGetLastError());
     return XDRG_OK;
   }
