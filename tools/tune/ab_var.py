@@ -1,0 +1,77 @@
+"""A/B the var-path kernel families (group-copy vs record-image) in one
+process, interleaved (cdna_hip_programming.md §5.4 rule 24)."""
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+from xdrpp_amd import _abi as A, marshal as M, schemas as S, workloads as W  # noqa: E402
+
+L = A.lib()
+L.xdrg__select_var_kernel.argtypes = [C.c_int]
+L.xdrg__set_image_bytes.argtypes = [C.c_int]
+# (kernel family, LDS image bytes): 0 = LDS image, 1 = record image, 2 = group copy
+VARIANTS = [(1, 16384), (3, 16384)]
+
+
+def select(v):
+    L.xdrg__select_var_kernel(v[0])
+    L.xdrg__set_image_bytes(v[1])
+dev = torch.device("cuda:0")
+out = {}
+for schema in sys.argv[1:] or ["recvar", "rpc"]:
+    n = 1 << 20
+    plan = M.Plan(S.ALL[schema])
+    mar = M.Marshaler(plan, dev)
+    nat_np, heap_np = W.GENERATORS[schema](n)
+    nat = torch.from_numpy(nat_np).to(dev)
+    heap = torch.from_numpy(heap_np).to(dev)
+    total = int(mar.serial_sizes(nat, n).to(torch.int64).sum().item())
+    xdr = torch.empty(total, dtype=torch.uint8, device=dev)
+    offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    back = torch.empty_like(nat)
+    hout = torch.empty(total, dtype=torch.uint8, device=dev)
+    ref = None
+    s = torch.cuda.current_stream().cuda_stream
+    times = {v: ([], []) for v in VARIANTS}
+    for v in VARIANTS:  # correctness + warmup
+        select(v)
+        mar.status.init(s)
+        mar.launch_encode(nat, n, xdr, heap=heap, offsets=offs)
+        mar.launch_decode(xdr, n, back, offsets=offs, heap_out=hout)
+        mar.check()
+        x = xdr.clone()
+        ref = x if ref is None else ref
+        assert torch.equal(x, ref), f"{schema}: variant {v} encode differs"
+        x2 = torch.empty_like(xdr)
+        mar.launch_encode(back, n, x2, heap=hout, offsets=offs)
+        mar.check()
+        assert torch.equal(x2, ref), f"{schema}: variant {v} decode->encode differs"
+    for rnd in range(5):
+        for v in VARIANTS:
+            select(v)
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            ev[0].record()
+            for _ in range(5):
+                mar.launch_encode(nat, n, xdr, heap=heap, offsets=offs)
+            ev[1].record()
+            for _ in range(5):
+                mar.launch_decode(xdr, n, back, offsets=offs, heap_out=hout)
+            ev[2].record()
+            torch.cuda.synchronize()
+            times[v][0].append(ev[0].elapsed_time(ev[1]) / 5)
+            times[v][1].append(ev[1].elapsed_time(ev[2]) / 5)
+    select(VARIANTS[-1])
+    mar.check()
+    for v in VARIANTS:
+        name = f"k{v[0]}_{v[1] // 1024}K"
+        e, d = float(np.median(times[v][0])), float(np.median(times[v][1]))
+        out[f"{schema}_{name}"] = {"encode_ms": round(e, 4), "decode_ms": round(d, 4),
+                                   "gib_s": round(2 * total / 2**30 / ((e + d) * 1e-3), 1)}
+        print(schema, name, out[f"{schema}_{name}"])
+json.dump(out, open(os.path.join(ROOT, "gpurun_out", "ab_var.json"), "w"), indent=1)

@@ -163,6 +163,55 @@ int compile_plan(xdrg_plan &p) {
   if (!fixed) {
     p.fixed_size = 0;
     p.path = XDRG_PATH_VAR;
+    // Longest count of var-length fields along any control path (jumps are
+    // forward-only, so one reverse sweep over the DAG suffices).
+    // Same sweep for the scalar (non-payload) wire words of a record.
+    std::vector<uint32_t> slots(n, 0), words(n, 0);
+    std::vector<uint64_t> pieces(n, 0), bytes(n, 0);
+    for (uint32_t i = n; i-- > 0;) {
+      const xdrg_op &op = p.ops[i];
+      uint32_t best = 0, bw = 0;
+      uint64_t bp = 0, bb = 0;
+      switch (op.kind) {
+      case XDRG_OP_END: break;
+      case XDRG_OP_JUMP:
+        best = slots[op.arg0]; bw = words[op.arg0]; bp = pieces[op.arg0]; bb = bytes[op.arg0];
+        break;
+      case XDRG_OP_UNION:
+        for (uint32_t c = 0; c < op.arg3; ++c) {
+          const uint32_t t = p.table[op.arg2 + 2 * c + 1];
+          best = std::max(best, slots[t]);
+          bw = std::max(bw, words[t]);
+          bp = std::max(bp, pieces[t]);
+          bb = std::max(bb, bytes[t]);
+        }
+        if (op.flags & XDRG_F_DEFAULT) {
+          best = std::max(best, slots[op.arg4]);
+          bw = std::max(bw, words[op.arg4]);
+          bp = std::max(bp, pieces[op.arg4]);
+          bb = std::max(bb, bytes[op.arg4]);
+        }
+        bw += 1;
+        bb += 4;
+        break;
+      default: {
+        const bool var = op.kind == XDRG_OP_VAROPAQUE || op.kind == XDRG_OP_STRING;
+        best = slots[i + 1] + (var ? 1u : 0u);
+        const uint32_t w = op.kind == XDRG_OP_U64 ? 2u : op.kind == XDRG_OP_OPAQUE ? (op.arg0 + 3u) / 4u : 1u;
+        bw = words[i + 1] + w;
+        bp = pieces[i + 1] + (var ? (uint64_t(op.arg0) + 255u) / 256u : 0u);
+        bb = bytes[i + 1] + 4ull * w + (var ? (uint64_t(op.arg0) + 3u) & ~3ull : 0u);
+      }
+      }
+      slots[i] = best;
+      words[i] = bw;
+      pieces[i] = bp;
+      bytes[i] = bb;
+    }
+    p.max_var_slots = slots[0];
+    p.max_scalar_words = words[0];
+    p.max_pieces = uint32_t(std::min<uint64_t>(pieces[0], 0xffffffffu));
+    p.max_record_bytes = bytes[0];
     for (const xdrg_op &op : p.ops)
       if (op.kind == XDRG_OP_VAROPAQUE || op.kind == XDRG_OP_STRING || op.kind == XDRG_OP_UNION ||
           op.kind == XDRG_OP_OPAQUE || (op.kind == XDRG_OP_ENUM && (op.flags & XDRG_F_VALIDATE)))

@@ -68,6 +68,10 @@ struct xdrg_plan {
   uint32_t fixed_size = 0;  // 0 => variable
   uint32_t path = 0;
   uint32_t max_depth = 0;
+  uint32_t max_var_slots = 0;  // var plans: most opaque<>/string<> fields on one path
+  uint32_t max_scalar_words = 0;  // var plans: most non-payload wire words on one path
+  uint32_t max_pieces = 0;  // var plans: most 256-byte payload pieces on one path (by bounds)
+  uint64_t max_record_bytes = 0;  // var plans: largest wire record the bounds allow
   bool has_checks = false;
   bool has_bool = false;
   // fixed plans

@@ -102,45 +102,68 @@ constexpr uint32_t kSizeErr = 0x80000000u;
 // xdr_traits<T>::serial_size per record and bad discriminants
 // (gen_hh.cc:639-648).  The stack budget is a put-side check
 // (marshal.h:129-136) and is applied by k_var_encode.
+// All var kernels walk the plan with a wave-uniform schedule: jumps are
+// forward-only, so the plan is a DAG in pc order and one sweep
+// upc = 0..nops-1 visits every op a lane can reach.  At each upc the op is
+// read through the scalar cache and dispatched with scalar branches; only
+// the lanes whose own pc equals upc do the field work (and jump forward).
+constexpr uint32_t kPcDone = 0xffffffffu;
+
+// Diagnostic phase stamps (in-kernel s_memtime, one row of 8 per wave);
+// only when the stamp buffer is set (tools/tune), never in timed runs.
+#define XDRG_STAMP(i)                                                              \
+  do {                                                                             \
+    if (stamps) {                                                                  \
+      __builtin_amdgcn_sched_barrier(0);                                           \
+      unsigned long long t_;                                                       \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");  \
+      __builtin_amdgcn_sched_barrier(0);                                           \
+      stv[i] = t_;                                                                 \
+    }                                                                              \
+  } while (0)
+#define XDRG_STAMP_FLUSH(wave_id)                                                  \
+  do {                                                                             \
+    if (stamps && (threadIdx.x & 63) == 0)                                         \
+      for (int q_ = 0; q_ < 8; ++q_) stamps[(wave_id) * 8 + q_] = stv[q_];         \
+  } while (0)
+
 __global__ __launch_bounds__(256) void k_var_size(const uint8_t *__restrict__ native, uint64_t n,
                                                   uint32_t stride, const xdrg_op *__restrict__ ops,
                                                   uint32_t nops, const uint32_t *__restrict__ table,
                                                   uint32_t *__restrict__ sizes,
                                                   unsigned long long *__restrict__ block_sums,
                                                   unsigned long long *err) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  xdrg_op *sops = reinterpret_cast<xdrg_op *>(smem);
   __shared__ unsigned long long wsum[4];
-  load_ops(sops, ops, nops);
   const uint64_t r = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const uint8_t *nat = native + r * stride;
+  uint64_t s = 0;
+  uint32_t pc = r < n ? 0u : kPcDone, bad_op = kPcDone;
+  for (uint32_t upc = 0; upc < nops; ++upc) {
+    if (!__any(pc == upc)) continue;
+    const xdrg_op op = ops[upc];
+    if (pc != upc) continue;
+    switch (op.kind) {
+    case XDRG_OP_END: pc = kPcDone; break;
+    case XDRG_OP_JUMP: pc = op.arg0; break;
+    case XDRG_OP_U64: s += 8; ++pc; break;
+    case XDRG_OP_OPAQUE: s += (op.arg0 + 3u) & ~3u; ++pc; break;
+    case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING:
+      s += 4u + ((static_cast<uint64_t>(ld32(nat + op.noff + 8)) + 3u) & ~3ull);
+      ++pc;
+      break;
+    case XDRG_OP_UNION: {
+      const int t = union_target(op, table, ld32(nat + op.noff));
+      s += 4;
+      if (t < 0) { bad_op = upc; pc = kPcDone; }
+      else pc = static_cast<uint32_t>(t);
+      break;
+    }
+    default: s += 4; ++pc; break;
+    }
+  }
   uint32_t size = 0;
   if (r < n) {
-    const uint8_t *nat = native + r * stride;
-    uint64_t s = 0;
-    uint32_t pc = 0, bad_op = 0xffffffffu;
-    for (;;) {
-      const xdrg_op &op = sops[pc];
-      if (op.kind == XDRG_OP_END) break;
-      if (op.kind == XDRG_OP_JUMP) { pc = op.arg0; continue; }
-      switch (op.kind) {
-      case XDRG_OP_U64: s += 8; ++pc; break;
-      case XDRG_OP_OPAQUE: s += (op.arg0 + 3u) & ~3u; ++pc; break;
-      case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING:
-        s += 4u + ((static_cast<uint64_t>(ld32(nat + op.noff + 8)) + 3u) & ~3ull);
-        ++pc;
-        break;
-      case XDRG_OP_UNION: {
-        const int t = union_target(op, table, ld32(nat + op.noff));
-        s += 4;
-        if (t < 0) { bad_op = pc; goto done; }
-        pc = static_cast<uint32_t>(t);
-        break;
-      }
-      default: s += 4; ++pc; break;
-      }
-    }
-  done:
-    if (bad_op != 0xffffffffu) {
+    if (bad_op != kPcDone) {
       report(err, r, bad_op, XDRG_ERR_BAD_DISCRIMINANT);
       size = kSizeErr;
     } else if (s >= kSizeErr) {
@@ -393,6 +416,1411 @@ overflow:
   report(err, r, pc, XDRG_ERR_OVERFLOW_GET);
 }
 
+// ------------------------------------------- var: record-image kernels
+// Encode, record-image form.  The lane walk (one lane per record) writes
+// nothing to global memory: it leaves each record's scalar wire words in
+// LDS and keeps the record's size and payload table in its own registers.
+// The wave then emits whole records: pass p of record j stores words
+// [64p, 64p+64) of the record, one per lane, fully contiguous, with
+// kEmitBatch records' loads in flight per lane.  Record j's table reaches
+// every lane through v_readlane (j is wave-uniform), so the emission loop
+// has no LDS round trips except the scalar words themselves, and no
+// partially written line is ever left for the L2 to evict.
+struct enc_lds {
+  uint32_t ops_bytes, tile_bytes, sw_words, per_wave, total;
+};
+__host__ __device__ inline enc_lds enc_lds_layout(uint32_t nops, uint32_t stride, uint32_t MSW) {
+  enc_lds L;
+  (void)nops;
+  L.ops_bytes = 0;  // ops are read through the scalar cache
+  L.tile_bytes = (64u * stride + 15u) & ~15u;
+  L.sw_words = MSW ? MSW : 1u;
+  L.per_wave = L.tile_bytes + ((64u * L.sw_words * 4u + 15u) & ~15u);  // tile | sw u32[64*MSW]
+  L.total = L.ops_bytes + 4u * L.per_wave;
+  return L;
+}
+
+constexpr int kEmitBatch = 8;
+
+__device__ __forceinline__ uint32_t rl32(uint32_t v, uint32_t lane) {
+  return __builtin_amdgcn_readlane(v, lane);
+}
+__device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t lane) {
+  return static_cast<uint64_t>(rl32(static_cast<uint32_t>(v), lane)) |
+         (static_cast<uint64_t>(rl32(static_cast<uint32_t>(v >> 32), lane)) << 32);
+}
+
+template <int KMAX>
+__global__ __launch_bounds__(256) void k_var_encode_c(
+    const uint8_t *__restrict__ native, uint64_t n, uint32_t stride, const uint8_t *__restrict__ heap,
+    uint64_t heap_len, uint8_t *__restrict__ xdr, uint64_t cap, uint64_t *__restrict__ offsets,
+    const uint32_t *__restrict__ sizes, const unsigned long long *__restrict__ block_base,
+    const xdrg_op *__restrict__ ops, uint32_t nops, const uint32_t *__restrict__ table,
+    uint32_t stack_limit, uint32_t MSW, unsigned long long *err, unsigned long long *stamps) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
+  __shared__ unsigned long long wsum[4];
+  unsigned long long stv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  XDRG_STAMP(0);
+  const enc_lds L = enc_lds_layout(nops, stride, MSW);
+  const uint32_t msw = L.sw_words;
+  xdrg_op *sops = reinterpret_cast<xdrg_op *>(sm);
+  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint8_t *wb = sm + L.ops_bytes + wid * L.per_wave;
+  uint8_t *tile = wb;
+  uint32_t *sw = reinterpret_cast<uint32_t *>(wb + L.tile_bytes);
+  (void)sops;
+
+  const uint64_t r = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const uint32_t sz = r < n ? sizes[r] : 0u;
+  unsigned long long v = (sz & kSizeErr) ? 0ull : sz;
+  unsigned long long incl = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long x = __shfl_up(incl, o, 64);
+    if (lane >= static_cast<uint32_t>(o)) incl += x;
+  }
+  if (lane == 63) wsum[wid] = incl;
+  XDRG_STAMP(1);
+
+  const uint64_t wr0 = static_cast<uint64_t>(blockIdx.x) * blockDim.x + wid * 64u;
+  const uint32_t wn = wr0 < n ? static_cast<uint32_t>(min<uint64_t>(64, n - wr0)) : 0u;
+  const uint32_t nbytes = wn * stride;
+  const uint8_t *nsrc = native + wr0 * stride;
+  for (uint32_t i = lane; i < nbytes / 16u; i += 64u)
+    reinterpret_cast<u32x4 *>(tile)[i] = reinterpret_cast<const u32x4 *>(nsrc)[i];
+  for (uint32_t i = (nbytes / 16u) * 4u + lane; i < nbytes / 4u; i += 64u)
+    reinterpret_cast<uint32_t *>(tile)[i] = reinterpret_cast<const uint32_t *>(nsrc)[i];
+  __syncthreads();
+  XDRG_STAMP(2);
+
+  unsigned long long wbase = 0;
+  for (uint32_t w = 0; w < wid; ++w) wbase += wsum[w];
+  const uint64_t off = block_base[blockIdx.x] + wbase + incl - v;
+
+  // per-record table, in this lane's registers
+  uint32_t rsize = 0;
+  uint32_t pst[KMAX], pln[KMAX];
+  uint64_t psr[KMAX];
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) { pst[k] = 0xffffffffu; pln[k] = 0; psr[k] = 0; }
+  if (r < n) offsets[r] = off;
+  {
+    const uint8_t *nat = tile + lane * stride;
+    uint32_t *mysw = sw + lane * msw;
+    uint32_t nsw = 0, wpos = 0, nslot = 0;  // wpos: record word index
+    uint64_t pos = off;
+    uint32_t pc = (r < n && !(sz & kSizeErr)) ? 0u : kPcDone;
+    bool ok = pc == 0u;
+    for (uint32_t upc = 0; upc < nops; ++upc) {
+      if (!__any(pc == upc)) continue;
+      const xdrg_op op = ops[upc];
+      if (pc != upc) continue;
+      if (op.kind == XDRG_OP_END) { pc = kPcDone; continue; }
+      if (op.kind == XDRG_OP_JUMP) { pc = op.arg0; continue; }
+      if (op.depth > stack_limit) { report(err, r, upc, XDRG_ERR_STACK_PUT); ok = false; pc = kPcDone; continue; }
+      const uint32_t *nw = reinterpret_cast<const uint32_t *>(nat + op.noff);
+      uint32_t blen = 0;
+      uint64_t need = 4;
+      if (op.kind == XDRG_OP_U64) need = 8;
+      else if (op.kind == XDRG_OP_OPAQUE) need = op.arg0;
+      else if (op.kind == XDRG_OP_VAROPAQUE || op.kind == XDRG_OP_STRING) {
+        blen = nw[2];
+        need = 4ull + blen;
+      }
+      if (need > cap - min(pos, cap)) { report(err, r, upc, XDRG_ERR_OVERFLOW_PUT); ok = false; pc = kPcDone; continue; }
+      switch (op.kind) {
+      case XDRG_OP_U32: case XDRG_OP_ENUM:
+        mysw[nsw++] = bswap32(nw[0]); pos += 4; ++wpos; ++pc; break;
+      case XDRG_OP_BOOL:
+        mysw[nsw++] = nat[op.noff] ? 0x01000000u : 0u; pos += 4; ++wpos; ++pc; break;
+      case XDRG_OP_U64:
+        mysw[nsw++] = bswap32(nw[1]);
+        mysw[nsw++] = bswap32(nw[0]);
+        pos += 8; wpos += 2; ++pc; break;
+      case XDRG_OP_OPAQUE: {
+        const uint32_t BL = op.arg0, nwd = (BL + 3u) >> 2;
+        for (uint32_t k = 0; k < nwd; ++k) {
+          uint32_t w = 0;
+          for (uint32_t bb = 0; bb < 4u && 4u * k + bb < BL; ++bb)
+            w |= static_cast<uint32_t>(nat[op.noff + 4u * k + bb]) << (8u * bb);
+          mysw[nsw++] = w;
+        }
+        pos += 4ull * nwd; wpos += nwd; ++pc; break;
+      }
+      case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
+        mysw[nsw++] = bswap32(blen);
+        ++wpos;
+        const uint32_t nwd = (blen + 3u) >> 2;
+        if (blen) {
+          const uint64_t hsrc = *reinterpret_cast<const uint64_t *>(nw);
+#pragma unroll
+          for (int k = 0; k < KMAX; ++k)
+            if (static_cast<uint32_t>(k) == nslot) { pst[k] = wpos; pln[k] = blen; psr[k] = hsrc; }
+          ++nslot;
+        }
+        wpos += nwd;
+        pos += 4ull + 4ull * nwd; ++pc; break;
+      }
+      case XDRG_OP_UNION: {
+        const uint32_t d = nw[0];
+        mysw[nsw++] = bswap32(d);
+        pos += 4; ++wpos;
+        pc = static_cast<uint32_t>(union_target(op, table, d));  // validated by k_var_size
+        break;
+      }
+      default: ++pc; break;
+      }
+    }
+    if (ok) rsize = wpos;  // a failing record emits nothing (never past `cap`)
+  }
+  __syncthreads();
+  XDRG_STAMP(3);
+
+  // ---- emission: whole records, kEmitBatch records per step
+  for (uint32_t j0 = 0; j0 < wn; j0 += kEmitBatch) {
+    uint32_t rs[kEmitBatch];
+    uint32_t passes = 0;
+#pragma unroll
+    for (int u = 0; u < kEmitBatch; ++u) {
+      rs[u] = (j0 + u < wn) ? rl32(rsize, j0 + u) : 0u;
+      passes = max(passes, (rs[u] + 63u) >> 6);
+    }
+    for (uint32_t pss = 0; pss < passes; ++pss) {
+      const uint32_t w = pss * 64u + lane;
+      uint32_t val[kEmitBatch];
+#pragma unroll
+      for (int u = 0; u < kEmitBatch; ++u) {
+        const uint32_t j = j0 + u;
+        val[u] = 0u;
+        if (w < rs[u]) {
+          // which payload (if any) holds word w of record j; scalar index otherwise
+          uint32_t skip = 0;
+          int slot = -1;
+          uint32_t st = 0, bl = 0;
+          uint64_t src = 0;
+#pragma unroll
+          for (int k = 0; k < KMAX; ++k) {
+            const uint32_t stk = rl32(pst[k], j), blk = rl32(pln[k], j);
+            const uint32_t nwk = (blk + 3u) >> 2;
+            if (slot < 0 && stk != 0xffffffffu) {
+              if (w >= stk + nwk) skip += nwk;
+              else if (w >= stk) { slot = k; st = stk; bl = blk; src = rl64(psr[k], j); }
+            }
+          }
+          if (slot < 0) {
+            val[u] = sw[j * msw + (w - skip)];
+          } else {
+            const uint32_t kw = w - st;
+            const uint64_t hs = src + 4ull * kw;
+            const uint64_t a = hs & ~3ull;
+            const uint32_t sh = static_cast<uint32_t>(hs & 3u);
+            uint32_t x;
+            if (a + 8 <= heap_len) {
+              const uint32_t lo = ld32(heap + a);
+              x = sh ? __builtin_amdgcn_alignbyte(ld32(heap + a + 4), lo, sh) : lo;
+            } else {
+              x = unaligned_word(heap, heap_len, hs);
+            }
+            if (4u * kw + 4u > bl) x &= keep_mask(bl - 4u * kw);
+            val[u] = x;
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kEmitBatch; ++u) {
+        const uint32_t j = j0 + u;
+        if (w < rs[u]) st32(xdr + rl64(off, j) + 4ull * w, val[u]);
+      }
+    }
+  }
+  XDRG_STAMP(4);
+  XDRG_STAMP(5);
+  XDRG_STAMP_FLUSH(wr0 / 64u);
+}
+
+// Decode, record-image form.  Lane-per-record parse of the wire (scalar
+// fields into an LDS native tile, payload table in registers), then the
+// wave writes each record's heap region [off[j], ...) -- its payloads packed
+// back to back, 4-byte aligned -- as one contiguous stream, checking every
+// payload's pad bytes (get_bytes, marshal.cc:43-57), and finally copies the
+// native tile out with 16-byte stores.
+template <int KMAX>
+__global__ __launch_bounds__(256) void k_var_decode_c(
+    const uint8_t *__restrict__ xdr, uint64_t len, const uint64_t *__restrict__ offsets, uint64_t n,
+    uint8_t *__restrict__ native, uint32_t stride, uint8_t *__restrict__ heap,
+    const xdrg_op *__restrict__ ops, uint32_t nops, const uint32_t *__restrict__ table,
+    uint32_t stack_limit, unsigned long long *err) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
+  const uint32_t ops_bytes = 0;  // ops are read through the scalar cache
+  const uint32_t tile_bytes = (64u * stride + 15u) & ~15u;
+  xdrg_op *sops = reinterpret_cast<xdrg_op *>(sm);
+  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint8_t *tile = sm + ops_bytes + wid * tile_bytes;
+  const uint64_t wr0 = static_cast<uint64_t>(blockIdx.x) * blockDim.x + wid * 64u;
+  const uint32_t wn = wr0 < n ? static_cast<uint32_t>(min<uint64_t>(64, n - wr0)) : 0u;
+  const uint32_t nbytes = wn * stride;
+  for (uint32_t i = lane; i < (nbytes + 15u) / 16u; i += 64u)
+    reinterpret_cast<u32x4 *>(tile)[i] = u32x4{0u, 0u, 0u, 0u};
+  (void)sops;
+  __syncthreads();  // tile zeroed before any lane writes a field
+
+  const uint64_t r = wr0 + lane;
+  uint32_t hwords = 0;  // heap words of this record (all payloads, padded)
+  uint32_t pst[KMAX], pln[KMAX], pop[KMAX];
+  uint64_t psr[KMAX];
+  uint64_t a = 0;
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) { pst[k] = 0xffffffffu; pln[k] = 0; pop[k] = 0; psr[k] = 0; }
+  {
+    uint8_t *nat = tile + lane * stride;
+    uint64_t b = 0;
+    uint32_t pc = kPcDone;
+    if (r < n) {
+      a = offsets[r];
+      b = offsets[r + 1];
+      if (r == n - 1 && b != len) report(err, n, kOpRecordLevel, XDRG_ERR_TRAILING);
+      if (b < a || b > len) report(err, r, 0, XDRG_ERR_OVERFLOW_GET);
+      else if ((b - a) & 3u) report(err, r, kOpRecordLevel, XDRG_ERR_SIZE_NOT_MULT4);
+      else pc = 0;
+    }
+    uint64_t p = a;
+    uint32_t nslot = 0;
+    bool ok = pc == 0u;
+    for (uint32_t upc = 0; upc < nops; ++upc) {
+      if (!__any(pc == upc)) continue;
+      const xdrg_op op = ops[upc];
+      if (pc != upc) continue;
+      if (op.kind == XDRG_OP_END) { pc = kPcDone; continue; }
+      if (op.kind == XDRG_OP_JUMP) { pc = op.arg0; continue; }
+      if (op.depth > stack_limit) { report(err, r, upc, XDRG_ERR_STACK_GET); ok = false; pc = kPcDone; continue; }
+      const uint64_t rem = b - p;
+      uint32_t *nw = reinterpret_cast<uint32_t *>(nat + op.noff);
+      const uint32_t need = op.kind == XDRG_OP_U64 ? 8u : op.kind == XDRG_OP_OPAQUE ? op.arg0 : 4u;
+      if (rem < need) { report(err, r, upc, XDRG_ERR_OVERFLOW_GET); ok = false; pc = kPcDone; continue; }
+      switch (op.kind) {
+      case XDRG_OP_U32:
+        nw[0] = bswap32(ld32(xdr + p)); p += 4; ++pc; break;
+      case XDRG_OP_ENUM: {
+        const uint32_t v = bswap32(ld32(xdr + p));
+        nw[0] = v; p += 4; ++pc;
+        if ((op.flags & XDRG_F_VALIDATE) && !enum_ok(table, op.arg0, op.arg1, v)) {
+          report(err, r, upc, XDRG_ERR_INVALID_ENUM); ok = false; pc = kPcDone;
+        }
+        break;
+      }
+      case XDRG_OP_BOOL:
+        nat[op.noff] = ld32(xdr + p) != 0u; p += 4; ++pc; break;
+      case XDRG_OP_U64:
+        nw[1] = bswap32(ld32(xdr + p));
+        nw[0] = bswap32(ld32(xdr + p + 4));
+        p += 8; ++pc; break;
+      case XDRG_OP_OPAQUE: {
+        const uint32_t BL = op.arg0;
+        for (uint32_t k = 0; k < BL; ++k) nat[op.noff + k] = xdr[p + k];
+        ++pc;
+        if ((BL & 3u) && (ld32(xdr + p + (BL & ~3u)) & ~keep_mask(BL & 3u))) {
+          report(err, r, upc, XDRG_ERR_NONZERO_PAD); ok = false; pc = kPcDone;
+        }
+        p += (BL + 3u) & ~3u;
+        break;
+      }
+      case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
+        const uint32_t BL = bswap32(ld32(xdr + p));
+        p += 4;
+        if (BL > b - p) { report(err, r, upc, XDRG_ERR_OVERFLOW_GET); ok = false; pc = kPcDone; break; }
+        if (BL > op.arg0) {
+          report(err, r, upc,
+                 op.kind == XDRG_OP_STRING ? XDRG_ERR_XSTRING_BOUND : XDRG_ERR_XVECTOR_BOUND);
+          ok = false;
+          pc = kPcDone;
+          break;
+        }
+        const uint32_t nwd = (BL + 3u) >> 2;
+        if (BL) {
+#pragma unroll
+          for (int k = 0; k < KMAX; ++k)
+            if (static_cast<uint32_t>(k) == nslot) { pst[k] = hwords; pln[k] = BL; psr[k] = p; pop[k] = upc; }
+          ++nslot;
+        }
+        *reinterpret_cast<uint64_t *>(nat + op.noff) = a + 4ull * hwords;
+        nw[2] = BL;
+        hwords += nwd;
+        p += 4ull * nwd; ++pc;
+        break;
+      }
+      case XDRG_OP_UNION: {
+        const uint32_t d = bswap32(ld32(xdr + p));
+        p += 4;
+        if ((op.flags & XDRG_F_VALIDATE) && !enum_ok(table, op.arg0, op.arg1, d)) {
+          report(err, r, upc, XDRG_ERR_INVALID_ENUM); ok = false; pc = kPcDone; break;
+        }
+        const int t = union_target(op, table, d);
+        if (t < 0) { report(err, r, upc, XDRG_ERR_BAD_DISCRIMINANT); ok = false; pc = kPcDone; break; }
+        nw[0] = d;
+        pc = static_cast<uint32_t>(t);
+        break;
+      }
+      default: ++pc; break;
+      }
+    }
+    if (ok && p != b) report(err, r, kOpRecordLevel, XDRG_ERR_TRAILING);
+  }
+
+  // ---- heap regions: record j's payloads, contiguous from offsets[j]
+  for (uint32_t j0 = 0; j0 < wn; j0 += kEmitBatch) {
+    uint32_t hw[kEmitBatch];
+    uint32_t passes = 0;
+#pragma unroll
+    for (int u = 0; u < kEmitBatch; ++u) {
+      hw[u] = (j0 + u < wn) ? rl32(hwords, j0 + u) : 0u;
+      passes = max(passes, (hw[u] + 63u) >> 6);
+    }
+    for (uint32_t pss = 0; pss < passes; ++pss) {
+      const uint32_t h = pss * 64u + lane;
+      uint32_t val[kEmitBatch];
+      bool bad[kEmitBatch];
+      uint32_t bop[kEmitBatch];
+#pragma unroll
+      for (int u = 0; u < kEmitBatch; ++u) {
+        const uint32_t j = j0 + u;
+        val[u] = 0u;
+        bad[u] = false;
+        bop[u] = 0u;
+        if (h < hw[u]) {
+#pragma unroll
+          for (int k = 0; k < KMAX; ++k) {
+            const uint32_t stk = rl32(pst[k], j), blk = rl32(pln[k], j);
+            const uint32_t nwk = (blk + 3u) >> 2;
+            if (stk != 0xffffffffu && h >= stk && h < stk + nwk) {
+              const uint32_t kw = h - stk;
+              const uint32_t x = ld32(xdr + rl64(psr[k], j) + 4ull * kw);
+              val[u] = x;
+              if (4u * kw + 4u > blk && (x & ~keep_mask(blk - 4u * kw))) {
+                bad[u] = true;
+                bop[u] = rl32(pop[k], j);
+              }
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kEmitBatch; ++u) {
+        const uint32_t j = j0 + u;
+        if (h < hw[u]) {
+          if (bad[u]) report(err, wr0 + j, bop[u], XDRG_ERR_NONZERO_PAD);
+          st32(heap + rl64(a, j) + 4ull * h, val[u]);
+        }
+      }
+    }
+  }
+  __syncthreads();  // every lane's native fields are in the tile
+  uint8_t *ndst = native + wr0 * stride;
+  for (uint32_t i = lane; i < nbytes / 16u; i += 64u)
+    reinterpret_cast<u32x4 *>(ndst)[i] = reinterpret_cast<const u32x4 *>(tile)[i];
+  for (uint32_t i = (nbytes / 16u) * 4u + lane; i < nbytes / 4u; i += 64u)
+    reinterpret_cast<uint32_t *>(ndst)[i] = reinterpret_cast<const uint32_t *>(tile)[i];
+}
+
+// ---------------------------------------------- var: group-copy kernels
+// Payloads move as <=256-byte pieces; a 16-lane group copies one piece per
+// step with 16-byte loads/stores (gfx950 handles unaligned 16-byte global
+// accesses: tools/probe/unaligned.hip), four groups per wave and
+// kGroupBatch steps in flight.  The lane-per-record walk writes only the
+// scalar words; the pieces of a wave go out right behind them, so the
+// lines they share complete in L2.
+constexpr int kGroupBatch = 4;
+
+constexpr uint32_t kPieceBytes = 256u;
+constexpr uint32_t kLastPiece = 0x80000000u;
+
+struct piece_arrays {
+  uint64_t *src, *dst;
+  uint32_t *len, *tag;
+};
+__host__ __device__ inline uint32_t piece_wave_bytes(uint32_t PM) { return 64u * (PM ? PM : 1u) * 24u; }
+__device__ __forceinline__ piece_arrays piece_carve(uint8_t *base, uint32_t PM) {
+  const uint32_t cap = 64u * (PM ? PM : 1u);
+  piece_arrays pa;
+  pa.src = reinterpret_cast<uint64_t *>(base);
+  pa.dst = pa.src + cap;
+  pa.len = reinterpret_cast<uint32_t *>(pa.dst + cap);
+  pa.tag = pa.len + cap;
+  return pa;
+}
+
+// Split each lane's payload slots into pieces, compacted in record order.
+// Returns the wave's piece count.  tag = last-piece bit | lane << 16 | op.
+template <int KMAX>
+__device__ __forceinline__ uint32_t wave_pieces(const piece_arrays &pa, uint32_t lane,
+                                                const uint64_t (&psr)[KMAX],
+                                                const uint64_t (&pds)[KMAX],
+                                                const uint32_t (&pln)[KMAX],
+                                                const uint32_t (&pop)[KMAX]) {
+  uint32_t np = 0;
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) np += (pln[k] + kPieceBytes - 1u) / kPieceBytes;
+  uint32_t incl = np;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t x = __shfl_up(incl, o, 64);
+    if (lane >= static_cast<uint32_t>(o)) incl += x;
+  }
+  uint32_t e = incl - np;
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+    const uint32_t L = pln[k];
+    for (uint32_t q = 0; q * kPieceBytes < L; ++q, ++e) {
+      pa.src[e] = psr[k] + q * kPieceBytes;
+      pa.dst[e] = pds[k] + q * kPieceBytes;
+      pa.len[e] = min(kPieceBytes, L - q * kPieceBytes);
+      pa.tag[e] = ((q + 1u) * kPieceBytes >= L ? kLastPiece : 0u) | (lane << 16) | (pop[k] & 0xffffu);
+    }
+  }
+  return __shfl(incl, 63, 64);
+}
+
+__device__ __forceinline__ u32x4 ld16u(const uint8_t *p) { return *reinterpret_cast<const u32x4 *>(p); }
+__device__ __forceinline__ void st16u(uint8_t *p, u32x4 v) { *reinterpret_cast<u32x4 *>(p) = v; }
+__device__ __forceinline__ uint32_t keep_bytes(int32_t k) {  // mask of the low k bytes, k clamped
+  return k <= 0 ? 0u : k >= 4 ? 0xffffffffu : ((1u << (8 * k)) - 1u);
+}
+// Store bytes [0, nb) of v (nb a multiple of 4, 4..16) at p.
+__device__ __forceinline__ void st_words(uint8_t *p, const u32x4 &v, uint32_t nb) {
+  if (nb >= 16u) { st16u(p, v); return; }
+  st32(p, v.x);
+  if (nb > 4u) st32(p + 4, v.y);
+  if (nb > 8u) st32(p + 8, v.z);
+}
+
+// Encode with group copy.  The lane walk stages the record's scalar wire
+// words in LDS (never global) and appends pieces in record order: scalar
+// runs (source: LDS) interleaved with payload pieces (source: heap).  The
+// groups then write each record's bytes within a step or two, so every
+// output line is completed while it is still in L2.
+struct epiece {  // 16 bytes
+  uint64_t src;    // heap byte offset, or LDS byte offset for scalar runs
+  uint32_t dst;    // byte offset from the wave's first record
+  uint32_t meta;   // len (9 bits) | from-LDS (bit 9)
+};
+constexpr uint32_t kFromLds = 1u << 9;
+
+__host__ __device__ inline uint32_t enc_g_wave_bytes(uint32_t stride, uint32_t MSW, uint32_t PM,
+                                                     uint32_t SL) {
+  const uint32_t tile = (64u * stride + 15u) & ~15u;
+  const uint32_t sw = (64u * (MSW ? MSW : 1u) * 4u + 15u) & ~15u;
+  const uint32_t np = 64u * ((PM ? PM : 1u) + (SL ? SL : 1u) + 1u);  // payload + scalar pieces
+  return tile + sw + np * 16u;
+}
+
+template <int KMAX>
+__global__ __launch_bounds__(256) void k_var_encode_g(
+    const uint8_t *__restrict__ native, uint64_t n, uint32_t stride, const uint8_t *__restrict__ heap,
+    uint64_t heap_len, uint8_t *__restrict__ xdr, uint64_t cap, uint64_t *__restrict__ offsets,
+    const uint32_t *__restrict__ sizes, const unsigned long long *__restrict__ block_base,
+    const xdrg_op *__restrict__ ops, uint32_t nops, const uint32_t *__restrict__ table,
+    uint32_t stack_limit, uint32_t PM, uint32_t MSW, uint32_t SL, unsigned long long *err) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
+  __shared__ unsigned long long wsum[4];
+  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint32_t tile_bytes = (64u * stride + 15u) & ~15u;
+  const uint32_t msw = MSW ? MSW : 1u;
+  uint8_t *tile = sm + wid * enc_g_wave_bytes(stride, MSW, PM, SL);
+  uint32_t *sw = reinterpret_cast<uint32_t *>(tile + tile_bytes);
+  epiece *pcs = reinterpret_cast<epiece *>(tile + tile_bytes + ((64u * msw * 4u + 15u) & ~15u));
+
+  const uint64_t r = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const uint32_t sz = r < n ? sizes[r] : 0u;
+  unsigned long long v = (sz & kSizeErr) ? 0ull : sz;
+  unsigned long long incl = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long x = __shfl_up(incl, o, 64);
+    if (lane >= static_cast<uint32_t>(o)) incl += x;
+  }
+  if (lane == 63) wsum[wid] = incl;
+  const uint64_t wr0 = static_cast<uint64_t>(blockIdx.x) * blockDim.x + wid * 64u;
+  const uint32_t wn = wr0 < n ? static_cast<uint32_t>(min<uint64_t>(64, n - wr0)) : 0u;
+  const uint32_t nbytes = wn * stride;
+  const uint8_t *nsrc = native + wr0 * stride;
+  for (uint32_t i = lane; i < nbytes / 16u; i += 64u)
+    reinterpret_cast<u32x4 *>(tile)[i] = reinterpret_cast<const u32x4 *>(nsrc)[i];
+  for (uint32_t i = (nbytes / 16u) * 4u + lane; i < nbytes / 4u; i += 64u)
+    reinterpret_cast<uint32_t *>(tile)[i] = reinterpret_cast<const uint32_t *>(nsrc)[i];
+  __syncthreads();
+  unsigned long long wbase = 0;
+  for (uint32_t w = 0; w < wid; ++w) wbase += wsum[w];
+  const uint64_t off = block_base[blockIdx.x] + wbase + incl - v;
+  const uint64_t wave_out = __shfl(off, 0, 64);  // first record of the wave
+
+  // ---- walk: scalar words -> LDS, payload slots -> registers
+  uint64_t psr[KMAX];
+  uint32_t pat[KMAX], pln[KMAX];  // pat: word index in the record where the payload starts
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) { psr[k] = 0; pat[k] = 0; pln[k] = 0; }
+  uint32_t nsw = 0, wpos = 0, nslot = 0;
+  bool ok = false;
+  if (r < n) offsets[r] = off;
+  {
+    const uint8_t *nat = tile + lane * stride;
+    uint32_t *mysw = sw + lane * msw;
+    uint64_t pos = off;
+    uint32_t pc = (r < n && !(sz & kSizeErr)) ? 0u : kPcDone;
+    ok = pc == 0u;
+    for (uint32_t upc = 0; upc < nops; ++upc) {
+      if (!__any(pc == upc)) continue;
+      const xdrg_op op = ops[upc];
+      if (pc != upc) continue;
+      if (op.kind == XDRG_OP_END) { pc = kPcDone; continue; }
+      if (op.kind == XDRG_OP_JUMP) { pc = op.arg0; continue; }
+      if (op.depth > stack_limit) { report(err, r, upc, XDRG_ERR_STACK_PUT); ok = false; pc = kPcDone; continue; }
+      const uint32_t *nw = reinterpret_cast<const uint32_t *>(nat + op.noff);
+      uint32_t blen = 0;
+      uint64_t need = 4;
+      if (op.kind == XDRG_OP_U64) need = 8;
+      else if (op.kind == XDRG_OP_OPAQUE) need = op.arg0;
+      else if (op.kind == XDRG_OP_VAROPAQUE || op.kind == XDRG_OP_STRING) {
+        blen = nw[2];
+        need = 4ull + blen;
+      }
+      if (need > cap - min(pos, cap)) { report(err, r, upc, XDRG_ERR_OVERFLOW_PUT); ok = false; pc = kPcDone; continue; }
+      switch (op.kind) {
+      case XDRG_OP_U32: case XDRG_OP_ENUM:
+        mysw[nsw++] = bswap32(nw[0]); pos += 4; ++wpos; ++pc; break;
+      case XDRG_OP_BOOL:
+        mysw[nsw++] = nat[op.noff] ? 0x01000000u : 0u; pos += 4; ++wpos; ++pc; break;
+      case XDRG_OP_U64:
+        mysw[nsw++] = bswap32(nw[1]);
+        mysw[nsw++] = bswap32(nw[0]);
+        pos += 8; wpos += 2; ++pc; break;
+      case XDRG_OP_OPAQUE: {
+        const uint32_t BL = op.arg0, nwd = (BL + 3u) >> 2;
+        for (uint32_t k = 0; k < nwd; ++k) {
+          uint32_t w = 0;
+          for (uint32_t bb = 0; bb < 4u && 4u * k + bb < BL; ++bb)
+            w |= static_cast<uint32_t>(nat[op.noff + 4u * k + bb]) << (8u * bb);
+          mysw[nsw++] = w;
+        }
+        pos += 4ull * nwd; wpos += nwd; ++pc; break;
+      }
+      case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
+        mysw[nsw++] = bswap32(blen);
+        ++wpos;
+        if (blen) {
+          const uint64_t hsrc = *reinterpret_cast<const uint64_t *>(nw);
+#pragma unroll
+          for (int k = 0; k < KMAX; ++k)
+            if (static_cast<uint32_t>(k) == nslot) { psr[k] = hsrc; pat[k] = wpos; pln[k] = blen; }
+          ++nslot;
+        }
+        wpos += (blen + 3u) >> 2;
+        pos += 4ull + ((static_cast<uint64_t>(blen) + 3u) & ~3ull); ++pc; break;
+      }
+      case XDRG_OP_UNION: {
+        const uint32_t d = nw[0];
+        mysw[nsw++] = bswap32(d);
+        pos += 4; ++wpos;
+        pc = static_cast<uint32_t>(union_target(op, table, d));  // validated by k_var_size
+        break;
+      }
+      default: ++pc; break;
+      }
+    }
+  }
+  // ---- pieces in record order: scalar run 0, payload 0, run 1, payload 1,
+  // ..., tail run.  Runs and payloads are cut into <=256-byte pieces.
+  uint32_t np = 0;
+  if (ok) {
+    uint32_t wcur = 0;
+#pragma unroll
+    for (int k = 0; k <= KMAX; ++k) {
+      if (static_cast<uint32_t>(k) > nslot) break;
+      const bool have = static_cast<uint32_t>(k) < nslot;
+      const uint32_t run_end = have ? pat[k < KMAX ? k : 0] : wpos;
+      np += (run_end - wcur + 63u) / 64u;
+      wcur = run_end;
+      if (!have) break;
+      np += (pln[k < KMAX ? k : 0] + kPieceBytes - 1u) / kPieceBytes;
+      wcur += (pln[k < KMAX ? k : 0] + 3u) >> 2;
+    }
+  }
+  uint32_t pincl = np;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t x = __shfl_up(pincl, o, 64);
+    if (lane >= static_cast<uint32_t>(o)) pincl += x;
+  }
+  if (ok) {
+    uint32_t e = pincl - np;
+    const uint32_t rel = static_cast<uint32_t>(off - wave_out);
+    const uint32_t swbase = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(sw + lane * msw) -
+                                                  reinterpret_cast<uintptr_t>(sm));
+    uint32_t wcur = 0, scur = 0;
+#pragma unroll
+    for (int k = 0; k <= KMAX; ++k) {
+      if (static_cast<uint32_t>(k) > nslot) break;
+      const bool have = static_cast<uint32_t>(k) < nslot;
+      const int kk = k < KMAX ? k : 0;
+      const uint32_t run_end = have ? pat[kk] : wpos;
+      for (uint32_t q = wcur; q < run_end; q += 64u, ++e) {
+        pcs[e].src = swbase + 4u * (scur + (q - wcur));
+        pcs[e].dst = rel + 4u * q;
+        pcs[e].meta = (4u * min(64u, run_end - q)) | kFromLds;
+      }
+      scur += run_end - wcur;
+      wcur = run_end;
+      if (!have) break;
+      for (uint32_t q = 0; q * kPieceBytes < pln[kk]; ++q, ++e) {
+        pcs[e].src = psr[kk] + q * kPieceBytes;
+        pcs[e].dst = rel + 4u * wcur + q * kPieceBytes;
+        pcs[e].meta = min(kPieceBytes, pln[kk] - q * kPieceBytes);
+      }
+      wcur += (pln[kk] + 3u) >> 2;
+    }
+  }
+  const uint32_t M = __shfl(pincl, 63, 64);
+  __syncthreads();
+  // ---- copy: group g = lane >> 4 copies piece e0 + 4u + g, lane t = 16 B
+  const uint32_t g = lane >> 4, t16 = (lane & 15u) * 16u;
+  uint8_t *wout = xdr + wave_out;
+  for (uint32_t e0 = 0; e0 < M; e0 += 4u * kGroupBatch) {
+    u32x4 val[kGroupBatch];
+    uint32_t dst[kGroupBatch], nbo[kGroupBatch];
+#pragma unroll
+    for (int u = 0; u < kGroupBatch; ++u) {
+      const uint32_t pe = e0 + 4u * u + g;
+      val[u] = u32x4{0u, 0u, 0u, 0u};
+      nbo[u] = 0u;
+      dst[u] = 0u;
+      if (pe < M) {
+        const epiece pc = pcs[pe];
+        const uint32_t Lr = pc.meta & 0x1ffu;
+        if (t16 < Lr) {
+          dst[u] = pc.dst + t16;
+          nbo[u] = min(16u, ((Lr + 3u) & ~3u) - t16);
+          if (pc.meta & kFromLds) {
+            const uint32_t *ls = reinterpret_cast<const uint32_t *>(sm + pc.src + t16);
+            val[u].x = ls[0];
+            if (nbo[u] > 4u) val[u].y = ls[1];
+            if (nbo[u] > 8u) val[u].z = ls[2];
+            if (nbo[u] > 12u) val[u].w = ls[3];
+          } else {
+            const uint64_t hs = pc.src + t16;
+            u32x4 x;
+            if (hs + 16u <= heap_len) {
+              x = ld16u(heap + hs);
+            } else {
+              x = u32x4{unaligned_word(heap, heap_len, hs), unaligned_word(heap, heap_len, hs + 4),
+                        unaligned_word(heap, heap_len, hs + 8), unaligned_word(heap, heap_len, hs + 12)};
+            }
+            const int32_t rem = static_cast<int32_t>(Lr - t16);
+            if (rem < 16) {  // zero the pad bytes after the payload (put_bytes)
+              x.x &= keep_bytes(rem);
+              x.y &= keep_bytes(rem - 4);
+              x.z &= keep_bytes(rem - 8);
+              x.w &= keep_bytes(rem - 12);
+            }
+            val[u] = x;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kGroupBatch; ++u)
+      if (nbo[u]) st_words(wout + dst[u], val[u], nbo[u]);
+  }
+}
+
+template <int KMAX, int GB = kGroupBatch>
+__global__ __launch_bounds__(256) void k_var_decode_g(
+    const uint8_t *__restrict__ xdr, uint64_t len, const uint64_t *__restrict__ offsets, uint64_t n,
+    uint8_t *__restrict__ native, uint32_t stride, uint8_t *__restrict__ heap,
+    const xdrg_op *__restrict__ ops, uint32_t nops, const uint32_t *__restrict__ table,
+    uint32_t stack_limit, uint32_t PM, unsigned long long *err, unsigned long long *stamps) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
+  unsigned long long stv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  XDRG_STAMP(0);
+  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint32_t tile_bytes = (64u * stride + 15u) & ~15u;
+  const uint32_t per_wave = tile_bytes + piece_wave_bytes(PM);
+  uint8_t *tile = sm + wid * per_wave;
+  const piece_arrays pa = piece_carve(tile + tile_bytes, PM);
+  const uint64_t wr0 = static_cast<uint64_t>(blockIdx.x) * blockDim.x + wid * 64u;
+  const uint32_t wn = wr0 < n ? static_cast<uint32_t>(min<uint64_t>(64, n - wr0)) : 0u;
+  const uint32_t nbytes = wn * stride;
+  for (uint32_t i = lane; i < (nbytes + 15u) / 16u; i += 64u)
+    reinterpret_cast<u32x4 *>(tile)[i] = u32x4{0u, 0u, 0u, 0u};
+  __syncthreads();  // tile zeroed before any lane writes a field
+  XDRG_STAMP(1);
+
+  const uint64_t r = wr0 + lane;
+  uint64_t psr[KMAX], pds[KMAX];
+  uint32_t pln[KMAX], pop[KMAX];
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) { psr[k] = 0; pds[k] = 0; pln[k] = 0; pop[k] = 0; }
+  {
+    uint8_t *nat = tile + lane * stride;
+    uint64_t a = 0, b = 0;
+    uint32_t pc = kPcDone;
+    if (r < n) {
+      a = offsets[r];
+      b = offsets[r + 1];
+      if (r == n - 1 && b != len) report(err, n, kOpRecordLevel, XDRG_ERR_TRAILING);
+      if (b < a || b > len) report(err, r, 0, XDRG_ERR_OVERFLOW_GET);
+      else if ((b - a) & 3u) report(err, r, kOpRecordLevel, XDRG_ERR_SIZE_NOT_MULT4);
+      else pc = 0;
+    }
+    uint64_t p = a, hcur = a;
+    uint32_t nslot = 0;
+    bool ok = pc == 0u;
+    for (uint32_t upc = 0; upc < nops; ++upc) {
+      if (!__any(pc == upc)) continue;
+      const xdrg_op op = ops[upc];
+      if (pc != upc) continue;
+      if (op.kind == XDRG_OP_END) { pc = kPcDone; continue; }
+      if (op.kind == XDRG_OP_JUMP) { pc = op.arg0; continue; }
+      if (op.depth > stack_limit) { report(err, r, upc, XDRG_ERR_STACK_GET); ok = false; pc = kPcDone; continue; }
+      const uint64_t rem = b - p;
+      uint32_t *nw = reinterpret_cast<uint32_t *>(nat + op.noff);
+      const uint32_t need = op.kind == XDRG_OP_U64 ? 8u : op.kind == XDRG_OP_OPAQUE ? op.arg0 : 4u;
+      if (rem < need) { report(err, r, upc, XDRG_ERR_OVERFLOW_GET); ok = false; pc = kPcDone; continue; }
+      switch (op.kind) {
+      case XDRG_OP_U32:
+        nw[0] = bswap32(ld32(xdr + p)); p += 4; ++pc; break;
+      case XDRG_OP_ENUM: {
+        const uint32_t v = bswap32(ld32(xdr + p));
+        nw[0] = v; p += 4; ++pc;
+        if ((op.flags & XDRG_F_VALIDATE) && !enum_ok(table, op.arg0, op.arg1, v)) {
+          report(err, r, upc, XDRG_ERR_INVALID_ENUM); ok = false; pc = kPcDone;
+        }
+        break;
+      }
+      case XDRG_OP_BOOL:
+        nat[op.noff] = ld32(xdr + p) != 0u; p += 4; ++pc; break;
+      case XDRG_OP_U64:
+        nw[1] = bswap32(ld32(xdr + p));
+        nw[0] = bswap32(ld32(xdr + p + 4));
+        p += 8; ++pc; break;
+      case XDRG_OP_OPAQUE: {
+        const uint32_t BL = op.arg0;
+        for (uint32_t k = 0; k < BL; ++k) nat[op.noff + k] = xdr[p + k];
+        ++pc;
+        if ((BL & 3u) && (ld32(xdr + p + (BL & ~3u)) & ~keep_mask(BL & 3u))) {
+          report(err, r, upc, XDRG_ERR_NONZERO_PAD); ok = false; pc = kPcDone;
+        }
+        p += (BL + 3u) & ~3u;
+        break;
+      }
+      case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
+        const uint32_t BL = bswap32(ld32(xdr + p));
+        p += 4;
+        if (BL > b - p) { report(err, r, upc, XDRG_ERR_OVERFLOW_GET); ok = false; pc = kPcDone; break; }
+        if (BL > op.arg0) {
+          report(err, r, upc,
+                 op.kind == XDRG_OP_STRING ? XDRG_ERR_XSTRING_BOUND : XDRG_ERR_XVECTOR_BOUND);
+          ok = false;
+          pc = kPcDone;
+          break;
+        }
+        const uint64_t padded = (static_cast<uint64_t>(BL) + 3u) & ~3ull;
+        if (BL) {
+#pragma unroll
+          for (int k = 0; k < KMAX; ++k)
+            if (static_cast<uint32_t>(k) == nslot) { psr[k] = p; pds[k] = hcur; pln[k] = BL; pop[k] = upc; }
+          ++nslot;
+        }
+        *reinterpret_cast<uint64_t *>(nat + op.noff) = hcur;
+        nw[2] = BL;
+        hcur += padded;
+        p += padded; ++pc;
+        break;
+      }
+      case XDRG_OP_UNION: {
+        const uint32_t d = bswap32(ld32(xdr + p));
+        p += 4;
+        if ((op.flags & XDRG_F_VALIDATE) && !enum_ok(table, op.arg0, op.arg1, d)) {
+          report(err, r, upc, XDRG_ERR_INVALID_ENUM); ok = false; pc = kPcDone; break;
+        }
+        const int t = union_target(op, table, d);
+        if (t < 0) { report(err, r, upc, XDRG_ERR_BAD_DISCRIMINANT); ok = false; pc = kPcDone; break; }
+        nw[0] = d;
+        pc = static_cast<uint32_t>(t);
+        break;
+      }
+      default: ++pc; break;
+      }
+    }
+    if (ok && p != b) report(err, r, kOpRecordLevel, XDRG_ERR_TRAILING);
+  }
+  XDRG_STAMP(2);
+  const uint32_t M = wave_pieces<KMAX>(pa, lane, psr, pds, pln, pop);
+  __syncthreads();
+  XDRG_STAMP(3);
+  // ---- pieces: wire -> heap (both 4-byte aligned); pad check on last words
+  const uint32_t g = lane >> 4, t16 = (lane & 15u) * 16u;
+  for (uint32_t e0 = 0; e0 < M; e0 += 4u * GB) {
+    u32x4 val[GB];
+#pragma unroll
+    for (int u = 0; u < GB; ++u) {
+      const uint32_t e = e0 + 4u * u + g;
+      val[u] = u32x4{0u, 0u, 0u, 0u};
+      if (e < M) {
+        const uint32_t L = pa.len[e];
+        if (t16 < L) {
+          const uint64_t s0 = pa.src[e] + t16;
+          const uint32_t nb = min(16u, ((L + 3u) & ~3u) - t16);
+          if (nb == 16u) val[u] = ld16u(xdr + s0);
+          else {
+            val[u].x = ld32(xdr + s0);
+            if (nb > 4u) val[u].y = ld32(xdr + s0 + 4);
+            if (nb > 8u) val[u].z = ld32(xdr + s0 + 8);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < GB; ++u) {
+      const uint32_t e = e0 + 4u * u + g;
+      if (e < M) {
+        const uint32_t L = pa.len[e];
+        if (t16 < L) {
+          const u32x4 x = val[u];
+          const int32_t rem = static_cast<int32_t>(L - t16);
+          if (rem < 16 && (pa.tag[e] & kLastPiece)) {
+            const uint32_t bad = (x.x & ~keep_bytes(rem)) | (x.y & ~keep_bytes(rem - 4) & (rem > 4 ? ~0u : 0u)) |
+                                 (x.z & ~keep_bytes(rem - 8) & (rem > 8 ? ~0u : 0u)) |
+                                 (x.w & ~keep_bytes(rem - 12) & (rem > 12 ? ~0u : 0u));
+            if (bad) report(err, wr0 + ((pa.tag[e] >> 16) & 0x7fffu), pa.tag[e] & 0xffffu, XDRG_ERR_NONZERO_PAD);
+          }
+          st_words(heap + pa.dst[e] + t16, x, min(16u, ((L + 3u) & ~3u) - t16));
+        }
+      }
+    }
+  }
+  XDRG_STAMP(4);
+  __syncthreads();  // every lane's native fields are in the tile
+  uint8_t *ndst = native + wr0 * stride;
+  for (uint32_t i = lane; i < nbytes / 16u; i += 64u)
+    reinterpret_cast<u32x4 *>(ndst)[i] = reinterpret_cast<const u32x4 *>(tile)[i];
+  for (uint32_t i = (nbytes / 16u) * 4u + lane; i < nbytes / 4u; i += 64u)
+    reinterpret_cast<uint32_t *>(ndst)[i] = reinterpret_cast<const uint32_t *>(tile)[i];
+  XDRG_STAMP(5);
+  XDRG_STAMP_FLUSH(wr0 / 64u);
+}
+
+// -------------------------------------------- var: LDS-image kernels
+// One workgroup = one wave = 64 consecutive records, so each wave owns
+// its LDS.  Encode assembles the wave's whole output stretch in an LDS
+// image (scalar words written by their record's lane, payload pieces by
+// 16-lane groups with 16-byte heap loads), then stores it with aligned
+// 16-byte writes.  The image is phase-shifted so that image byte j sits at
+// LDS (j + (global & 15)): global and LDS 16-byte chunks coincide.  Decode
+// loads the wave's input stretch into an LDS window the same way, parses
+// every record from LDS, and copies payload pieces out to the heap.
+// Stretches larger than the image / window are processed in rounds.
+template <int K>
+__device__ __forceinline__ uint32_t pick(const uint32_t (&a)[K], uint32_t k) {
+  uint32_t v = a[0];
+#pragma unroll
+  for (int i = 1; i < K; ++i) v = (k == static_cast<uint32_t>(i)) ? a[i] : v;
+  return v;
+}
+
+struct lpiece {  // 16 bytes
+  uint64_t src;   // encode: heap byte offset; decode: xdr byte offset
+  uint32_t dst;   // byte offset from the wave's stretch start
+  uint32_t meta;  // len (9 bits) | last piece (bit 31) | lane << 16 | op (decode: in tag)
+};
+
+__host__ __device__ inline uint32_t encL_lds(uint32_t MSW, uint32_t PM, uint32_t C) {
+  return ((64u * (MSW ? MSW : 1u) * 4u + 15u) & ~15u) + 64u * (PM ? PM : 1u) * 16u + C + 16u;
+}
+
+template <int KMAX>
+__global__ __launch_bounds__(64) void k_var_encode_L(
+    const uint8_t *__restrict__ native, uint64_t n, uint32_t stride, const uint8_t *__restrict__ heap,
+    uint64_t heap_len, uint8_t *__restrict__ xdr, uint64_t cap, uint64_t *__restrict__ offsets,
+    const uint32_t *__restrict__ sizes, const unsigned long long *__restrict__ block_base,
+    const xdrg_op *__restrict__ ops, uint32_t nops, const uint32_t *__restrict__ table,
+    uint32_t stack_limit, uint32_t MSW, uint32_t PM, uint32_t C, unsigned long long *err) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
+  const uint32_t lane = threadIdx.x;
+  const uint32_t msw = MSW ? MSW : 1u;
+  uint32_t *sw = reinterpret_cast<uint32_t *>(sm);
+  lpiece *pcs = reinterpret_cast<lpiece *>(sm + ((64u * msw * 4u + 15u) & ~15u));
+  uint8_t *img = reinterpret_cast<uint8_t *>(pcs + 64u * (PM ? PM : 1u));
+
+  const uint64_t r = static_cast<uint64_t>(blockIdx.x) * 64u + lane;
+  const uint32_t sz = r < n ? sizes[r] : 0u;
+  const unsigned long long v = (sz & kSizeErr) ? 0ull : sz;
+  unsigned long long incl = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long x = __shfl_up(incl, o, 64);
+    if (lane >= static_cast<uint32_t>(o)) incl += x;
+  }
+  const uint64_t off = block_base[blockIdx.x] + incl - v;
+  const uint64_t wave_out = rl64(off, 0);
+  const uint64_t region = static_cast<uint64_t>(__shfl(incl, 63, 64));
+  if (r < n) offsets[r] = off;
+
+  // ---- walk: native fields straight from global (lanes read adjacent records)
+  uint64_t psr[KMAX];
+  uint32_t pat[KMAX], pln[KMAX];
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) { psr[k] = 0; pat[k] = 0xffffffffu; pln[k] = 0; }
+  uint32_t nsw = 0, nslot = 0;
+  bool ok;
+  {
+    const uint8_t *nat = native + r * stride;
+    uint32_t *mysw = sw + lane * msw;
+    uint32_t wpos = 0;
+    uint64_t pos = off;
+    uint32_t pc = (r < n && !(sz & kSizeErr)) ? 0u : kPcDone;
+    ok = pc == 0u;
+    for (uint32_t upc = 0; upc < nops; ++upc) {
+      if (!__any(pc == upc)) continue;
+      const xdrg_op op = ops[upc];
+      if (pc != upc) continue;
+      if (op.kind == XDRG_OP_END) { pc = kPcDone; continue; }
+      if (op.kind == XDRG_OP_JUMP) { pc = op.arg0; continue; }
+      if (op.depth > stack_limit) { report(err, r, upc, XDRG_ERR_STACK_PUT); ok = false; pc = kPcDone; continue; }
+      const uint32_t *nw = reinterpret_cast<const uint32_t *>(nat + op.noff);
+      uint32_t blen = 0;
+      uint64_t need = 4;
+      if (op.kind == XDRG_OP_U64) need = 8;
+      else if (op.kind == XDRG_OP_OPAQUE) need = op.arg0;
+      else if (op.kind == XDRG_OP_VAROPAQUE || op.kind == XDRG_OP_STRING) {
+        blen = nw[2];
+        need = 4ull + blen;
+      }
+      if (need > cap - min(pos, cap)) { report(err, r, upc, XDRG_ERR_OVERFLOW_PUT); ok = false; pc = kPcDone; continue; }
+      switch (op.kind) {
+      case XDRG_OP_U32: case XDRG_OP_ENUM:
+        mysw[nsw++] = bswap32(nw[0]); pos += 4; ++wpos; ++pc; break;
+      case XDRG_OP_BOOL:
+        mysw[nsw++] = nat[op.noff] ? 0x01000000u : 0u; pos += 4; ++wpos; ++pc; break;
+      case XDRG_OP_U64: {
+        const uint32_t lo = nw[0], hi = nw[1];
+        mysw[nsw++] = bswap32(hi);
+        mysw[nsw++] = bswap32(lo);
+        pos += 8; wpos += 2; ++pc; break;
+      }
+      case XDRG_OP_OPAQUE: {
+        const uint32_t BL = op.arg0, nwd = (BL + 3u) >> 2;
+        for (uint32_t k = 0; k < nwd; ++k) {
+          uint32_t w = 0;
+          for (uint32_t bb = 0; bb < 4u && 4u * k + bb < BL; ++bb)
+            w |= static_cast<uint32_t>(nat[op.noff + 4u * k + bb]) << (8u * bb);
+          mysw[nsw++] = w;
+        }
+        pos += 4ull * nwd; wpos += nwd; ++pc; break;
+      }
+      case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
+        mysw[nsw++] = bswap32(blen);
+        ++wpos;
+        if (blen) {
+          const uint64_t hsrc = *reinterpret_cast<const uint64_t *>(nw);
+#pragma unroll
+          for (int k = 0; k < KMAX; ++k)
+            if (static_cast<uint32_t>(k) == nslot) { psr[k] = hsrc; pat[k] = wpos; pln[k] = blen; }
+          ++nslot;
+        }
+        wpos += (blen + 3u) >> 2;
+        pos += 4ull + ((static_cast<uint64_t>(blen) + 3u) & ~3ull); ++pc; break;
+      }
+      case XDRG_OP_UNION: {
+        const uint32_t d = nw[0];
+        mysw[nsw++] = bswap32(d);
+        pos += 4; ++wpos;
+        pc = static_cast<uint32_t>(union_target(op, table, d));  // validated by k_var_size
+        break;
+      }
+      default: ++pc; break;
+      }
+    }
+  }
+  if (!ok) nslot = 0, nsw = 0;  // a failing record contributes no bytes (its range is unspecified)
+
+  // ---- payload pieces (<=256 B), compacted in record order
+  const uint32_t rel = static_cast<uint32_t>(off - wave_out);
+  uint32_t np = 0;
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k)
+    if (static_cast<uint32_t>(k) < nslot) np += (pln[k] + kPieceBytes - 1u) / kPieceBytes;
+  uint32_t pincl = np;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t x = __shfl_up(pincl, o, 64);
+    if (lane >= static_cast<uint32_t>(o)) pincl += x;
+  }
+  {
+    uint32_t e = pincl - np;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      if (static_cast<uint32_t>(k) >= nslot) break;
+      for (uint32_t q = 0; q * kPieceBytes < pln[k]; ++q, ++e) {
+        pcs[e].src = psr[k] + q * kPieceBytes;
+        pcs[e].dst = rel + 4u * pat[k] + q * kPieceBytes;
+        pcs[e].meta = min(kPieceBytes, pln[k] - q * kPieceBytes);
+      }
+    }
+  }
+  const uint32_t M = __shfl(pincl, 63, 64);
+  __syncthreads();
+
+  const uint32_t g = lane >> 4, t16 = (lane & 15u) * 16u;
+  for (uint64_t base = 0; base < region; base += C) {
+    const uint32_t sh = static_cast<uint32_t>((wave_out + base) & 15u);
+    const uint32_t lim = static_cast<uint32_t>(min<uint64_t>(C, region - base));
+    uint8_t *im = img + sh;  // image byte j <-> global byte wave_out + base + j
+    // scalar words of this lane's record
+    {
+      uint32_t w = 0, k = 0;
+      uint32_t next = nslot ? pat[0] : 0xffffffffu;
+      for (uint32_t i = 0; i < nsw; ++i) {
+        while (w == next) {
+          w += (pick(pln, k) + 3u) >> 2;
+          ++k;
+          next = k < nslot ? pick(pat, k) : 0xffffffffu;
+        }
+        const int64_t at = static_cast<int64_t>(rel) + 4ll * w - static_cast<int64_t>(base);
+        if (at >= 0 && at < lim) *reinterpret_cast<uint32_t *>(im + at) = sw[lane * msw + i];
+        ++w;
+      }
+    }
+    // payload pieces
+    for (uint32_t e0 = 0; e0 < M; e0 += 4u * kGroupBatch) {
+      u32x4 val[kGroupBatch];
+      int64_t at[kGroupBatch];
+      uint32_t nbo[kGroupBatch];
+#pragma unroll
+      for (int u = 0; u < kGroupBatch; ++u) {
+        const uint32_t pe = e0 + 4u * u + g;
+        nbo[u] = 0u;
+        at[u] = 0;
+        val[u] = u32x4{0u, 0u, 0u, 0u};
+        if (pe < M) {
+          const lpiece pc = pcs[pe];
+          const uint32_t L = pc.meta & 0x1ffu;
+          at[u] = static_cast<int64_t>(pc.dst) + t16 - static_cast<int64_t>(base);
+          if (t16 < L && at[u] + 16 > 0 && at[u] < lim) {
+            nbo[u] = min(16u, ((L + 3u) & ~3u) - t16);
+            const uint64_t hs = pc.src + t16;
+            u32x4 x;
+            if (hs + 16u <= heap_len) {
+              x = ld16u(heap + hs);
+            } else {
+              x = u32x4{unaligned_word(heap, heap_len, hs), unaligned_word(heap, heap_len, hs + 4),
+                        unaligned_word(heap, heap_len, hs + 8), unaligned_word(heap, heap_len, hs + 12)};
+            }
+            const int32_t rem = static_cast<int32_t>(L - t16);
+            if (rem < 16) {  // zero pad bytes after the payload (put_bytes)
+              x.x &= keep_bytes(rem);
+              x.y &= keep_bytes(rem - 4);
+              x.z &= keep_bytes(rem - 8);
+              x.w &= keep_bytes(rem - 12);
+            }
+            val[u] = x;
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kGroupBatch; ++u) {
+        if (!nbo[u]) continue;
+        const uint32_t xs[4] = {val[u].x, val[u].y, val[u].z, val[u].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int64_t a = at[u] + 4 * q;
+          if (static_cast<uint32_t>(4 * q) < nbo[u] && a >= 0 && a < lim)
+            *reinterpret_cast<uint32_t *>(im + a) = xs[q];
+        }
+      }
+    }
+    __syncthreads();
+    // image -> global: aligned 16-byte chunks, partial words at the edges
+    const uint64_t gs = wave_out + base;
+    const uint64_t ge = min<uint64_t>(gs + lim, cap);
+    if (ge > gs) {
+      const uint64_t c0 = gs & ~15ull;
+      const uint32_t nch = static_cast<uint32_t>((ge - c0 + 15u) >> 4);
+      for (uint32_t c = lane; c < nch; c += 64u) {
+        const uint64_t ca = c0 + 16ull * c;
+        const uint8_t *lsrc = img + 16u * c;  // img + sh <-> gs, and gs - sh = c0
+        if (ca >= gs && ca + 16u <= ge) {
+          *reinterpret_cast<u32x4 *>(xdr + ca) = *reinterpret_cast<const u32x4 *>(lsrc);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint64_t wa = ca + 4u * q;
+            if (wa >= gs && wa + 4u <= ge) st32(xdr + wa, *reinterpret_cast<const uint32_t *>(lsrc + 4 * q));
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+__host__ __device__ inline uint32_t decL_lds(uint32_t stride, uint32_t PM, uint32_t C) {
+  return ((64u * stride + 15u) & ~15u) + 64u * (PM ? PM : 1u) * 16u + C + 16u;
+}
+
+// Parse one record (words read through `rd`), fields into the LDS native
+// tile, payload slots into registers.  Returns false on a reported error.
+template <int KMAX, typename RD>
+__device__ __forceinline__ void decode_walk(bool active, uint64_t r, uint64_t a, uint64_t b,
+                                            uint8_t *nat, const xdrg_op *__restrict__ ops,
+                                            uint32_t nops, const uint32_t *__restrict__ table,
+                                            uint32_t stack_limit, unsigned long long *err,
+                                            const RD &rd, uint64_t (&psr)[KMAX],
+                                            uint32_t (&pat)[KMAX], uint32_t (&pln)[KMAX],
+                                            uint32_t (&pop)[KMAX], uint32_t &nslot) {
+  uint64_t p = a, hcur = a;
+  uint32_t pc = active ? 0u : kPcDone;
+  bool ok = active;
+  for (uint32_t upc = 0; upc < nops; ++upc) {
+    if (!__any(pc == upc)) continue;
+    const xdrg_op op = ops[upc];
+    if (pc != upc) continue;
+    if (op.kind == XDRG_OP_END) { pc = kPcDone; continue; }
+    if (op.kind == XDRG_OP_JUMP) { pc = op.arg0; continue; }
+    if (op.depth > stack_limit) { report(err, r, upc, XDRG_ERR_STACK_GET); ok = false; pc = kPcDone; continue; }
+    const uint64_t rem = b - p;
+    uint32_t *nw = reinterpret_cast<uint32_t *>(nat + op.noff);
+    const uint32_t need = op.kind == XDRG_OP_U64 ? 8u : op.kind == XDRG_OP_OPAQUE ? op.arg0 : 4u;
+    if (rem < need) { report(err, r, upc, XDRG_ERR_OVERFLOW_GET); ok = false; pc = kPcDone; continue; }
+    switch (op.kind) {
+    case XDRG_OP_U32:
+      nw[0] = bswap32(rd(p)); p += 4; ++pc; break;
+    case XDRG_OP_ENUM: {
+      const uint32_t v = bswap32(rd(p));
+      nw[0] = v; p += 4; ++pc;
+      if ((op.flags & XDRG_F_VALIDATE) && !enum_ok(table, op.arg0, op.arg1, v)) {
+        report(err, r, upc, XDRG_ERR_INVALID_ENUM); ok = false; pc = kPcDone;
+      }
+      break;
+    }
+    case XDRG_OP_BOOL:
+      nat[op.noff] = rd(p) != 0u; p += 4; ++pc; break;
+    case XDRG_OP_U64: {
+      const uint32_t hi = rd(p), lo = rd(p + 4);
+      nw[1] = bswap32(hi);
+      nw[0] = bswap32(lo);
+      p += 8; ++pc; break;
+    }
+    case XDRG_OP_OPAQUE: {
+      const uint32_t BL = op.arg0;
+      for (uint32_t k = 0; k < BL; k += 4) {
+        const uint32_t w = rd(p + k);
+        for (uint32_t bb = 0; bb < 4u && k + bb < BL; ++bb) nat[op.noff + k + bb] = uint8_t(w >> (8 * bb));
+      }
+      ++pc;
+      if ((BL & 3u) && (rd(p + (BL & ~3u)) & ~keep_mask(BL & 3u))) {
+        report(err, r, upc, XDRG_ERR_NONZERO_PAD); ok = false; pc = kPcDone;
+      }
+      p += (BL + 3u) & ~3u;
+      break;
+    }
+    case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
+      const uint32_t BL = bswap32(rd(p));
+      p += 4;
+      if (BL > b - p) { report(err, r, upc, XDRG_ERR_OVERFLOW_GET); ok = false; pc = kPcDone; break; }
+      if (BL > op.arg0) {
+        report(err, r, upc, op.kind == XDRG_OP_STRING ? XDRG_ERR_XSTRING_BOUND : XDRG_ERR_XVECTOR_BOUND);
+        ok = false;
+        pc = kPcDone;
+        break;
+      }
+      const uint64_t padded = (static_cast<uint64_t>(BL) + 3u) & ~3ull;
+      if (BL) {
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k)
+          if (static_cast<uint32_t>(k) == nslot) { psr[k] = p; pat[k] = static_cast<uint32_t>(hcur - a); pln[k] = BL; pop[k] = upc; }
+        ++nslot;
+      }
+      *reinterpret_cast<uint64_t *>(nat + op.noff) = hcur;
+      nw[2] = BL;
+      hcur += padded;
+      p += padded; ++pc;
+      break;
+    }
+    case XDRG_OP_UNION: {
+      const uint32_t d = bswap32(rd(p));
+      p += 4;
+      if ((op.flags & XDRG_F_VALIDATE) && !enum_ok(table, op.arg0, op.arg1, d)) {
+        report(err, r, upc, XDRG_ERR_INVALID_ENUM); ok = false; pc = kPcDone; break;
+      }
+      const int t = union_target(op, table, d);
+      if (t < 0) { report(err, r, upc, XDRG_ERR_BAD_DISCRIMINANT); ok = false; pc = kPcDone; break; }
+      nw[0] = d;
+      pc = static_cast<uint32_t>(t);
+      break;
+    }
+    default: ++pc; break;
+    }
+  }
+  if (ok && p != b) report(err, r, kOpRecordLevel, XDRG_ERR_TRAILING);
+}
+
+template <int KMAX>
+__global__ __launch_bounds__(64) void k_var_decode_L(
+    const uint8_t *__restrict__ xdr, uint64_t len, const uint64_t *__restrict__ offsets, uint64_t n,
+    uint8_t *__restrict__ native, uint32_t stride, uint8_t *__restrict__ heap,
+    const xdrg_op *__restrict__ ops, uint32_t nops, const uint32_t *__restrict__ table,
+    uint32_t stack_limit, uint32_t PM, uint32_t C, unsigned long long *err) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
+  const uint32_t lane = threadIdx.x;
+  const uint32_t tile_bytes = (64u * stride + 15u) & ~15u;
+  uint8_t *tile = sm;
+  lpiece *pcs = reinterpret_cast<lpiece *>(sm + tile_bytes);
+  uint8_t *win = reinterpret_cast<uint8_t *>(pcs + 64u * (PM ? PM : 1u));
+  const uint64_t wr0 = static_cast<uint64_t>(blockIdx.x) * 64u;
+  const uint32_t wn = static_cast<uint32_t>(min<uint64_t>(64, n - wr0));
+  const uint32_t nbytes = wn * stride;
+  for (uint32_t i = lane; i < (nbytes + 15u) / 16u; i += 64u)
+    reinterpret_cast<u32x4 *>(tile)[i] = u32x4{0u, 0u, 0u, 0u};
+
+  const uint64_t r = wr0 + lane;
+  uint64_t a = 0, b = 0;
+  bool todo = false;
+  if (r < n) {
+    a = offsets[r];
+    b = offsets[r + 1];
+    if (r == n - 1 && b != len) report(err, n, kOpRecordLevel, XDRG_ERR_TRAILING);
+    if (b < a || b > len) report(err, r, 0, XDRG_ERR_OVERFLOW_GET);
+    else if ((b - a) & 3u) report(err, r, kOpRecordLevel, XDRG_ERR_SIZE_NOT_MULT4);
+    else todo = true;
+  }
+  __syncthreads();  // tile zeroed
+
+  const uint32_t g = lane >> 4, t16 = (lane & 15u) * 16u;
+  for (;;) {
+    const unsigned long long pend = __ballot(todo);
+    if (!pend) break;
+    const uint32_t first = static_cast<uint32_t>(__builtin_ctzll(pend));
+    const uint64_t wbase = rl64(a, first);
+    // window end: the last pending record that still fits after wbase
+    const bool fits = todo && b - wbase <= C;
+    const unsigned long long fit = __ballot(fits);
+    uint64_t wend = 0;
+    if (fit) {
+      const uint32_t last = 63u - static_cast<uint32_t>(__builtin_clzll(fit));
+      wend = rl64(b, last);
+    }
+    const bool from_lds = fit != 0ull;
+    const uint32_t sh = static_cast<uint32_t>(wbase & 15u);
+    if (from_lds) {
+      // load [wbase, wend) into the window (16-byte chunks aligned to global)
+      const uint64_t c0 = wbase & ~15ull;
+      const uint32_t nch = static_cast<uint32_t>((wend - c0 + 15u) >> 4);
+      for (uint32_t c = lane; c < nch; c += 64u) {
+        const uint64_t ca = c0 + 16ull * c;
+        uint8_t *ldst = win + 16u * c;  // win + sh <-> wbase, and wbase - sh = c0
+        if (ca >= wbase && ca + 16u <= wend) {
+          *reinterpret_cast<u32x4 *>(ldst) = *reinterpret_cast<const u32x4 *>(xdr + ca);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint64_t wa = ca + 4u * q;
+            if (wa >= wbase && wa + 4u <= wend) *reinterpret_cast<uint32_t *>(ldst + 4 * q) = ld32(xdr + wa);
+          }
+        }
+      }
+      __syncthreads();
+    }
+    // this round's records: those inside the window, else the first one alone
+    const bool mine = from_lds ? fits : (todo && lane == first);
+    uint64_t psr[KMAX];
+    uint32_t pat[KMAX], pln[KMAX], pop[KMAX];
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) { psr[k] = 0; pat[k] = 0; pln[k] = 0; pop[k] = 0; }
+    uint32_t nslot = 0;
+    uint8_t *nat = tile + lane * stride;
+    if (from_lds) {
+      const uint8_t *wl = win + sh;
+      auto rd = [wl, wbase](uint64_t q) -> uint32_t {
+        return *reinterpret_cast<const uint32_t *>(wl + (q - wbase));
+      };
+      decode_walk<KMAX>(mine, r, a, b, nat, ops, nops, table, stack_limit, err, rd, psr, pat, pln, pop, nslot);
+    } else {
+      auto rd = [xdr](uint64_t q) -> uint32_t { return ld32(xdr + q); };
+      decode_walk<KMAX>(mine, r, a, b, nat, ops, nops, table, stack_limit, err, rd, psr, pat, pln, pop, nslot);
+    }
+    // pieces of this round (heap dst relative to wbase; src absolute xdr offset)
+    uint32_t np = 0;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k)
+      if (static_cast<uint32_t>(k) < nslot) np += (pln[k] + kPieceBytes - 1u) / kPieceBytes;
+    uint32_t pincl = np;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t x = __shfl_up(pincl, o, 64);
+      if (lane >= static_cast<uint32_t>(o)) pincl += x;
+    }
+    {
+      uint32_t e = pincl - np;
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) {
+        if (static_cast<uint32_t>(k) >= nslot) break;
+        for (uint32_t q = 0; q * kPieceBytes < pln[k]; ++q, ++e) {
+          pcs[e].src = psr[k] + q * kPieceBytes;
+          pcs[e].dst = static_cast<uint32_t>(a - wbase) + pat[k] + q * kPieceBytes;
+          pcs[e].meta = min(kPieceBytes, pln[k] - q * kPieceBytes) |
+                        ((q + 1u) * kPieceBytes >= pln[k] ? kLastPiece : 0u) | (lane << 16);
+          pcs[e].src |= static_cast<uint64_t>(pop[k] & 0xffffu) << 48;  // op, for pad errors
+        }
+      }
+    }
+    const uint32_t M = __shfl(pincl, 63, 64);
+    __syncthreads();
+    for (uint32_t e0 = 0; e0 < M; e0 += 4u * kGroupBatch) {
+      u32x4 val[kGroupBatch];
+      uint32_t nbo[kGroupBatch];
+      uint64_t dst[kGroupBatch];
+#pragma unroll
+      for (int u = 0; u < kGroupBatch; ++u) {
+        const uint32_t pe = e0 + 4u * u + g;
+        nbo[u] = 0u;
+        dst[u] = 0u;
+        val[u] = u32x4{0u, 0u, 0u, 0u};
+        if (pe < M) {
+          const lpiece pc = pcs[pe];
+          const uint32_t L = pc.meta & 0x1ffu;
+          if (t16 < L) {
+            nbo[u] = min(16u, ((L + 3u) & ~3u) - t16);
+            dst[u] = wbase + pc.dst + t16;
+            const uint64_t s0 = (pc.src & 0xffffffffffffull) + t16;
+            if (from_lds) {
+              const uint32_t *ls = reinterpret_cast<const uint32_t *>(win + sh + (s0 - wbase));
+              val[u].x = ls[0];
+              if (nbo[u] > 4u) val[u].y = ls[1];
+              if (nbo[u] > 8u) val[u].z = ls[2];
+              if (nbo[u] > 12u) val[u].w = ls[3];
+            } else if (nbo[u] == 16u) {
+              val[u] = ld16u(xdr + s0);
+            } else {
+              val[u].x = ld32(xdr + s0);
+              if (nbo[u] > 4u) val[u].y = ld32(xdr + s0 + 4);
+              if (nbo[u] > 8u) val[u].z = ld32(xdr + s0 + 8);
+            }
+            const int32_t rem = static_cast<int32_t>(L - t16);
+            if (rem < 16 && (pc.meta & kLastPiece)) {  // get_bytes pad check
+              const u32x4 x = val[u];
+              if ((x.x & ~keep_bytes(rem)) | (x.y & ~keep_bytes(rem - 4)) | (x.z & ~keep_bytes(rem - 8)) |
+                  (x.w & ~keep_bytes(rem - 12)))
+                report(err, wr0 + ((pc.meta >> 16) & 63u), static_cast<uint32_t>(pc.src >> 48),
+                       XDRG_ERR_NONZERO_PAD);
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kGroupBatch; ++u)
+        if (nbo[u]) st_words(heap + dst[u], val[u], nbo[u]);
+    }
+    if (mine) todo = false;
+    __syncthreads();  // window and pieces free for the next round
+  }
+  uint8_t *ndst = native + wr0 * stride;
+  for (uint32_t i = lane; i < nbytes / 16u; i += 64u)
+    reinterpret_cast<u32x4 *>(ndst)[i] = reinterpret_cast<const u32x4 *>(tile)[i];
+  for (uint32_t i = (nbytes / 16u) * 4u + lane; i < nbytes / 4u; i += 64u)
+    reinterpret_cast<uint32_t *>(ndst)[i] = reinterpret_cast<const uint32_t *>(tile)[i];
+}
+
 // ------------------------------------------------------------------ swaps
 __global__ void k_swap32(const uint32_t *__restrict__ in, uint32_t *__restrict__ out, uint64_t n) {
   for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
@@ -407,6 +1835,11 @@ __global__ void k_swap64(const uint64_t *__restrict__ in, uint64_t *__restrict__
 
 // ------------------------------------------------------------------ host
 constexpr uint64_t kMallBytes = 256ull << 20;  // MI355X Infinity Cache
+constexpr uint32_t kVarLdsBudget = 64u << 10;  // wave-cooperative var kernels
+int g_var_kernel = 3;  // A/B (tools/tune): 0 LDS image, 1 record image, 2/3/4 group decode batch 4/8/16
+uint32_t g_img_bytes = 16u << 10;  // LDS image / window per wave (tuning)
+unsigned long long *g_stamps = nullptr;      // diagnostic phase stamps, decode (tuning)
+unsigned long long *g_stamps_enc = nullptr;  // diagnostic phase stamps, encode (tuning)
 
 uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 bool aligned(const void *p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) % a) == 0; }
@@ -507,7 +1940,7 @@ int run_fixed(const xdrg_plan &p, bool decode, const void *in, void *out, uint64
 }
 
 size_t var_ws_layout(uint64_t n, size_t *sizes_off, size_t *bsum_off) {
-  const uint64_t nb = (n + 255) / 256;
+  const uint64_t nb = (n + 63) / 64;  // block sums at the finest block size (64)
   *sizes_off = 0;
   *bsum_off = align_up(n * 4, 256);
   return *bsum_off + align_up(nb * 8, 256);
@@ -525,6 +1958,20 @@ extern "C" {
 int xdrg_abi_version(void) { return XDRG_ABI_VERSION; }
 
 const char *xdrg_last_hip_error(void) { return g_hip_err; }
+
+// Internal A/B hook for tools/tune (not part of include/xdrgpu.h).
+int xdrg__select_var_kernel(int which) {
+  const int old = g_var_kernel;
+  g_var_kernel = which;
+  return old;
+}
+void xdrg__set_stamps(void *buf) { g_stamps = static_cast<unsigned long long *>(buf); }
+void xdrg__set_stamps_enc(void *buf) { g_stamps_enc = static_cast<unsigned long long *>(buf); }
+int xdrg__set_image_bytes(int bytes) {
+  const int old = static_cast<int>(g_img_bytes);
+  g_img_bytes = static_cast<uint32_t>(bytes) & ~15u;
+  return old;
+}
 
 int xdrg_plan_create(const xdrg_op *ops, uint32_t nops, const uint32_t *table, uint32_t ntable,
                      uint32_t native_stride, xdrg_plan **out) {
@@ -654,19 +2101,65 @@ int xdrg_encode(const xdrg_plan *p, const void *d_native, uint64_t n, const uint
   if (!d_ws || ws_bytes < need) return XDRG_ESPACE;
   uint32_t *sizes = reinterpret_cast<uint32_t *>(static_cast<char *>(d_ws) + so);
   unsigned long long *bsum = reinterpret_cast<unsigned long long *>(static_cast<char *>(d_ws) + bo);
-  const uint64_t nb = (n + 255) / 256;
+  // LDS-image path: 64-record workgroups (sizes scanned per 64 records)
+  const uint32_t Cimg = static_cast<uint32_t>(std::min<uint64_t>(
+      g_img_bytes, (64ull * std::max<uint64_t>(p->max_record_bytes, 16) + 15u) & ~15ull));
+  const uint32_t lL = encL_lds(p->max_scalar_words, p->max_pieces, Cimg);
+  const bool use_L = g_var_kernel == 0 && lL <= kVarLdsBudget && p->max_var_slots <= 4 &&
+                     p->max_pieces <= 16 && p->max_scalar_words <= 256;
+  const uint32_t vb = use_L ? 64u : 256u;
+  const uint64_t nb = (n + vb - 1) / vb;
   if (nb > 0xffffffffull) return XDRG_EUNSUPPORTED;
   const size_t lds_ops = p->ops.size() * sizeof(xdrg_op);
-  k_var_size<<<nb, 256, lds_ops, s>>>(static_cast<const uint8_t *>(d_native), n, p->stride,
-                                       p->d_ops, uint32_t(p->ops.size()), p->d_table, sizes,
-                                       bsum, err);
+  k_var_size<<<nb, vb, lds_ops, s>>>(static_cast<const uint8_t *>(d_native), n, p->stride,
+                                      p->d_ops, uint32_t(p->ops.size()), p->d_table, sizes,
+                                      bsum, err);
   HIPCHK(hipGetLastError());
   k_scan_blocks<<<1, 1024, 0, s>>>(bsum, uint32_t(nb), d_status, d_offsets, n);
   HIPCHK(hipGetLastError());
-  k_var_encode<<<nb, 256, lds_ops, s>>>(static_cast<const uint8_t *>(d_native), n, p->stride,
-                                         d_heap, heap_len, static_cast<uint8_t *>(d_xdr), cap,
-                                         d_offsets, sizes, bsum, p->d_ops,
-                                         uint32_t(p->ops.size()), p->d_table, stack_limit, err);
+  if (use_L) {
+#define LAUNCH_ENC_L(K)                                                                         \
+  k_var_encode_L<K><<<nb, 64, lL, s>>>(static_cast<const uint8_t *>(d_native), n, p->stride,   \
+                                       d_heap, heap_len, static_cast<uint8_t *>(d_xdr), cap,  \
+                                       d_offsets, sizes, bsum, p->d_ops,                      \
+                                       uint32_t(p->ops.size()), p->d_table, stack_limit,      \
+                                       p->max_scalar_words, p->max_pieces, Cimg, err)
+    if (p->max_var_slots <= 1) LAUNCH_ENC_L(1);
+    else if (p->max_var_slots <= 2) LAUNCH_ENC_L(2);
+    else LAUNCH_ENC_L(4);
+#undef LAUNCH_ENC_L
+    HIPCHK(hipGetLastError());
+    return XDRG_OK;
+  }
+  const uint32_t gl = 4u * enc_g_wave_bytes(p->stride, p->max_scalar_words, p->max_pieces,
+                                             p->max_var_slots);
+  const bool gfits = gl <= kVarLdsBudget && aligned(d_native, 16) && p->max_pieces <= 16;
+#define LAUNCH_ENC_G(K)                                                                         \
+  k_var_encode_g<K><<<nb, 256, gl, s>>>(                                                       \
+      static_cast<const uint8_t *>(d_native), n, p->stride, d_heap, heap_len,                 \
+      static_cast<uint8_t *>(d_xdr), cap, d_offsets, sizes, bsum, p->d_ops,                   \
+      uint32_t(p->ops.size()), p->d_table, stack_limit, p->max_pieces, p->max_scalar_words,   \
+      p->max_var_slots, err)
+  const enc_lds EL = enc_lds_layout(uint32_t(p->ops.size()), p->stride, p->max_scalar_words);
+  const bool fits = EL.total <= kVarLdsBudget && aligned(d_native, 16);
+  if (g_var_kernel == 2 && gfits && p->max_var_slots <= 2) LAUNCH_ENC_G(2);
+  else if (g_var_kernel == 2 && gfits && p->max_var_slots <= 4) LAUNCH_ENC_G(4);
+  else
+#define LAUNCH_ENC_C(K)                                                                         \
+  k_var_encode_c<K><<<nb, 256, EL.total, s>>>(                                                 \
+      static_cast<const uint8_t *>(d_native), n, p->stride, d_heap, heap_len,                 \
+      static_cast<uint8_t *>(d_xdr), cap, d_offsets, sizes, bsum, p->d_ops,                   \
+      uint32_t(p->ops.size()), p->d_table, stack_limit, p->max_scalar_words, err, g_stamps_enc)
+  if (fits && p->max_var_slots <= 1) LAUNCH_ENC_C(1);
+  else if (fits && p->max_var_slots <= 2) LAUNCH_ENC_C(2);
+  else if (fits && p->max_var_slots <= 4) LAUNCH_ENC_C(4);
+  else
+    k_var_encode<<<nb, 256, lds_ops, s>>>(static_cast<const uint8_t *>(d_native), n, p->stride,
+                                          d_heap, heap_len, static_cast<uint8_t *>(d_xdr), cap,
+                                          d_offsets, sizes, bsum, p->d_ops,
+                                          uint32_t(p->ops.size()), p->d_table, stack_limit, err);
+#undef LAUNCH_ENC_C
+#undef LAUNCH_ENC_G
   HIPCHK(hipGetLastError());
   return XDRG_OK;
 }
@@ -709,12 +2202,63 @@ int xdrg_decode(const xdrg_plan *p, const void *d_xdr, uint64_t len, const uint6
   if (heap_cap < len || (len && !d_heap_out)) return XDRG_ESPACE;
   if (!aligned(d_xdr, 4) || !aligned(d_native, 8) || (d_heap_out && !aligned(d_heap_out, 4)))
     return XDRG_EALIGN;
+  const uint32_t Cwin = static_cast<uint32_t>(std::min<uint64_t>(
+      g_img_bytes, (64ull * std::max<uint64_t>(p->max_record_bytes, 16) + 15u) & ~15ull));
+  const uint32_t dL = decL_lds(p->stride, p->max_pieces, Cwin);
+  if (g_var_kernel == 0 && dL <= kVarLdsBudget && p->max_var_slots <= 4 && p->max_pieces <= 16 &&
+      aligned(d_native, 16)) {
+    const uint64_t nb64 = (n + 63) / 64;
+#define LAUNCH_DEC_L(K)                                                                        \
+  k_var_decode_L<K><<<nb64, 64, dL, s>>>(static_cast<const uint8_t *>(d_xdr), len, d_offsets, n, \
+                                         static_cast<uint8_t *>(d_native), p->stride, d_heap_out, \
+                                         p->d_ops, uint32_t(p->ops.size()), p->d_table,         \
+                                         stack_limit, p->max_pieces, Cwin, err)
+    if (p->max_var_slots <= 1) LAUNCH_DEC_L(1);
+    else if (p->max_var_slots <= 2) LAUNCH_DEC_L(2);
+    else LAUNCH_DEC_L(4);
+#undef LAUNCH_DEC_L
+    HIPCHK(hipGetLastError());
+    return XDRG_OK;
+  }
   const uint64_t nb = (n + 255) / 256;
   const size_t lds_ops = p->ops.size() * sizeof(xdrg_op);
-  k_var_decode<<<nb, 256, lds_ops, s>>>(static_cast<const uint8_t *>(d_xdr), len, d_offsets, n,
-                                         static_cast<uint8_t *>(d_native), p->stride, d_heap_out,
-                                         p->d_ops, uint32_t(p->ops.size()), p->d_table,
-                                         stack_limit, err);
+  const size_t dl = 4u * ((64u * p->stride + 15u) & ~15u);
+  const bool fits = dl <= kVarLdsBudget && aligned(d_native, 16);
+  const uint32_t gl = 4u * (((64u * p->stride + 15u) & ~15u) + piece_wave_bytes(p->max_pieces));
+  const bool gfits = gl <= kVarLdsBudget && aligned(d_native, 16) && p->max_pieces <= 16;
+#define LAUNCH_DEC_G2(K, B)                                                                    \
+  k_var_decode_g<K, B><<<nb, 256, gl, s>>>(static_cast<const uint8_t *>(d_xdr), len, d_offsets, n, \
+                                        static_cast<uint8_t *>(d_native), p->stride, d_heap_out, \
+                                        p->d_ops, uint32_t(p->ops.size()), p->d_table,         \
+                                        stack_limit, p->max_pieces, err, g_stamps)
+#define LAUNCH_DEC_G(K)                                                                        \
+  k_var_decode_g<K><<<nb, 256, gl, s>>>(static_cast<const uint8_t *>(d_xdr), len, d_offsets, n, \
+                                        static_cast<uint8_t *>(d_native), p->stride, d_heap_out, \
+                                        p->d_ops, uint32_t(p->ops.size()), p->d_table,         \
+                                        stack_limit, p->max_pieces, err, g_stamps)
+  if (g_var_kernel == 2 && gfits && p->max_var_slots <= 2) LAUNCH_DEC_G(2);
+  else if (g_var_kernel == 2 && gfits && p->max_var_slots <= 4) LAUNCH_DEC_G(4);
+  else if (g_var_kernel == 3 && gfits && p->max_var_slots <= 2) LAUNCH_DEC_G2(2, 8);
+  else if (g_var_kernel == 3 && gfits && p->max_var_slots <= 4) LAUNCH_DEC_G2(4, 8);
+  else if (g_var_kernel == 4 && gfits && p->max_var_slots <= 2) LAUNCH_DEC_G2(2, 16);
+  else if (g_var_kernel == 4 && gfits && p->max_var_slots <= 4) LAUNCH_DEC_G2(4, 16);
+  else
+#define LAUNCH_DEC_C(K)                                                                        \
+  k_var_decode_c<K><<<nb, 256, dl, s>>>(static_cast<const uint8_t *>(d_xdr), len, d_offsets, n, \
+                                        static_cast<uint8_t *>(d_native), p->stride, d_heap_out, \
+                                        p->d_ops, uint32_t(p->ops.size()), p->d_table,         \
+                                        stack_limit, err)
+  if (fits && p->max_var_slots <= 1) LAUNCH_DEC_C(1);
+  else if (fits && p->max_var_slots <= 2) LAUNCH_DEC_C(2);
+  else if (fits && p->max_var_slots <= 4) LAUNCH_DEC_C(4);
+  else
+    k_var_decode<<<nb, 256, lds_ops, s>>>(static_cast<const uint8_t *>(d_xdr), len, d_offsets, n,
+                                          static_cast<uint8_t *>(d_native), p->stride, d_heap_out,
+                                          p->d_ops, uint32_t(p->ops.size()), p->d_table,
+                                          stack_limit, err);
+#undef LAUNCH_DEC_C
+#undef LAUNCH_DEC_G
+#undef LAUNCH_DEC_G2
   HIPCHK(hipGetLastError());
   return XDRG_OK;
 }
