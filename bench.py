@@ -29,6 +29,7 @@ sys.path.insert(0, ROOT)
 from xdrpp_amd import _abi as A  # noqa: E402
 from xdrpp_amd import marshal as M  # noqa: E402
 from xdrpp_amd import schemas as S  # noqa: E402
+from xdrpp_amd import shard as SH  # noqa: E402
 from xdrpp_amd import workloads as W  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
@@ -189,11 +190,7 @@ def setup(schema, n, dev, rank, world):
     """Plan, resident inputs and preallocated outputs for one rank."""
     plan = M.Plan(S.ALL[schema])
     mar = M.Marshaler(plan, dev)
-    if schema == "rec128":
-        seed = W.SEED_REC128 if world == 1 else W.SEED_REC128_MGPU
-        nat_np, heap_np = W.rec128(n, seed=seed, first=rank * n)
-    else:
-        nat_np, heap_np = W.GENERATORS[schema](n)
+    nat_np, heap_np = SH.shard_inputs(schema, n, rank, world)
     nat = torch.from_numpy(nat_np).to(dev)
     heap = torch.from_numpy(heap_np).to(dev) if heap_np.size else None
     back = torch.empty(n * plan.stride, dtype=torch.uint8, device=dev)
@@ -273,20 +270,26 @@ def main():
 
     gather_ms = None
     if args.gather and dist is not None:
-        gl = [torch.empty_like(xdr) for _ in range(world)] if rank == 0 else None
         torch.cuda.synchronize()
         barrier(dist)
         g0 = time.perf_counter()
-        dist.gather(xdr, gl, dst=0)
+        SH.gather_streams(dist, xdr, offsets, rank, world)
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - g0) * 1e3
+
+    # whole-job bytes: shards of var-length schemas differ in size
+    X_all = X * world
+    if dist is not None:
+        t = torch.tensor([X], dtype=torch.int64, device=dev)
+        dist.all_reduce(t)
+        X_all = int(t.item())
 
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
         return
 
-    xdr_bytes_step = 2 * X * world
+    xdr_bytes_step = 2 * X_all
     value = xdr_bytes_step / GIB / (elapsed / args.steps)
     if plan.is_fixed:
         # dominant kernel: k_fixed_reg / k_fixed_lds (encode and decode are

@@ -195,9 +195,12 @@ typedef struct xdrg_error {
 
 int xdrg_abi_version(void);
 
-/* Build an immutable, device-resident plan.  `table` holds enum value lists
+/* Validate and compile an immutable plan.  `table` holds enum value lists
  * and union case tables referenced by the ops.  native_stride is the byte
- * distance between consecutive native records. */
+ * distance between consecutive native records.  Host-only: the plan's
+ * device tables are uploaded (synchronously, to the current device) by its
+ * first encode/decode/serial_sizes call, so run one launch before capturing
+ * a plan's launches into a hipGraph. */
 int xdrg_plan_create(const xdrg_op *ops, uint32_t nops, const uint32_t *table,
                      uint32_t ntable, uint32_t native_stride, xdrg_plan **out);
 void xdrg_plan_destroy(xdrg_plan *plan);

@@ -14,6 +14,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libxdrgpu.s
 
 # enum xdrg_op_kind
 OP_U32, OP_U64, OP_BOOL, OP_ENUM, OP_OPAQUE, OP_VAROPAQUE, OP_STRING, OP_UNION, OP_JUMP, OP_END = range(1, 11)
+ABI_VERSION = 1  # XDRG_ABI_VERSION, include/xdrgpu.h
 F_VALIDATE = 1
 F_DEFAULT = 2
 
@@ -138,7 +139,7 @@ def lib() -> C.CDLL:
     L.xdrg_error_exception.argtypes = [C.c_int]
     L.xdrg_error_exception.restype = C.c_int
     L.xdrg_last_hip_error.restype = C.c_char_p
-    if L.xdrg_abi_version() != 1:
+    if L.xdrg_abi_version() != ABI_VERSION:
         raise ImportError("libxdrgpu.so ABI version mismatch")
     _lib = L
     return L

@@ -1,7 +1,9 @@
 // Internal plan representation shared by the host plan compiler
 // (plan.cpp) and the kernels/launchers (xdrgpu.hip).
 #pragma once
+#include <atomic>
 #include <cstdint>
+#include <mutex>
 #include <vector>
 
 #include "../../include/xdrgpu.h"
@@ -78,7 +80,10 @@ struct xdrg_plan {
   std::vector<uint32_t> op_wire_off;  // wire byte offset of each op (fixed)
   xdrg::fixed_prog enc, dec;
   std::vector<xdrg::check> checks;
-  // device copies (one allocation)
+  // device copies (one allocation), made by the plan's first launch so that
+  // plan creation and validation never touch the device
+  std::mutex upload_mu;
+  std::atomic<bool> uploaded{false};
   void *d_mem = nullptr;
   const xdrg_op *d_ops = nullptr;
   const uint32_t *d_table = nullptr;

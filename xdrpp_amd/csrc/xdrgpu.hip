@@ -1985,7 +1985,16 @@ int xdrg_plan_create(const xdrg_op *ops, uint32_t nops, const uint32_t *table, u
   int rc = xdrg::compile_plan(*p);
   if (rc != XDRG_OK) { delete p; return rc; }
   if (p->stride % 4) { delete p; return XDRG_EUNSUPPORTED; }
-  // One device allocation holding every table.
+  *out = p;
+  return XDRG_OK;
+}
+
+// First launch of a plan: one device allocation holding every table.
+static int plan_upload(const xdrg_plan *cp) {
+  if (cp->uploaded.load(std::memory_order_acquire)) return XDRG_OK;
+  xdrg_plan *p = const_cast<xdrg_plan *>(cp);
+  std::lock_guard<std::mutex> g(p->upload_mu);
+  if (p->uploaded.load(std::memory_order_relaxed)) return XDRG_OK;
   struct part { const void *src; size_t bytes; size_t off; };
   part parts[10] = {
       {p->ops.data(), p->ops.size() * sizeof(xdrg_op), 0},
@@ -2000,14 +2009,16 @@ int xdrg_plan_create(const xdrg_op *ops, uint32_t nops, const uint32_t *table, u
       {nullptr, 16, 0}};
   size_t total = 0;
   for (part &q : parts) { q.off = total; total += align_up(q.bytes, 256); }
-  hipError_t e = hipMalloc(&p->d_mem, total);
-  if (e != hipSuccess) { delete p; return hip_fail(e, "hipMalloc(plan)"); }
-  char *base = static_cast<char *>(p->d_mem);
+  void *mem = nullptr;
+  hipError_t e = hipMalloc(&mem, total);
+  if (e != hipSuccess) return hip_fail(e, "hipMalloc(plan)");
+  char *base = static_cast<char *>(mem);
   for (part &q : parts)
     if (q.src && q.bytes) {
       e = hipMemcpy(base + q.off, q.src, q.bytes, hipMemcpyHostToDevice);
-      if (e != hipSuccess) { (void)hipFree(p->d_mem); delete p; return hip_fail(e, "hipMemcpy(plan)"); }
+      if (e != hipSuccess) { (void)hipFree(mem); return hip_fail(e, "hipMemcpy(plan)"); }
     }
+  p->d_mem = mem;
   p->d_ops = reinterpret_cast<const xdrg_op *>(base + parts[0].off);
   p->d_table = reinterpret_cast<const uint32_t *>(base + parts[1].off);
   p->d_enc_idx = reinterpret_cast<const term_idx *>(base + parts[2].off);
@@ -2017,7 +2028,7 @@ int xdrg_plan_create(const xdrg_op *ops, uint32_t nops, const uint32_t *table, u
   p->d_enc_reg = reinterpret_cast<const reg_word *>(base + parts[6].off);
   p->d_dec_reg = reinterpret_cast<const reg_word *>(base + parts[7].off);
   p->d_checks = reinterpret_cast<const check *>(base + parts[8].off);
-  *out = p;
+  p->uploaded.store(true, std::memory_order_release);
   return XDRG_OK;
 }
 
@@ -2072,6 +2083,7 @@ int xdrg_encode(const xdrg_plan *p, const void *d_native, uint64_t n, const uint
                 uint32_t stack_limit, void *d_ws, size_t ws_bytes, xdrg_status *d_status,
                 void *stream) {
   if (!p || !d_status || (n && (!d_native || !d_xdr))) return XDRG_EINVAL;
+  if (int rc = plan_upload(p)) return rc;
   hipStream_t s = static_cast<hipStream_t>(stream);
   unsigned long long *err = err_ptr(d_status);
   if (p->path != XDRG_PATH_VAR) {
@@ -2171,6 +2183,7 @@ int xdrg_decode(const xdrg_plan *p, const void *d_xdr, uint64_t len, const uint6
   (void)d_ws;
   (void)ws_bytes;
   if (!p || !d_status || (n && (!d_native || (len && !d_xdr)))) return XDRG_EINVAL;
+  if (int rc = plan_upload(p)) return rc;
   hipStream_t s = static_cast<hipStream_t>(stream);
   unsigned long long *err = err_ptr(d_status);
   if (p->path != XDRG_PATH_VAR) {
@@ -2267,6 +2280,7 @@ int xdrg_serial_sizes(const xdrg_plan *p, const void *d_native, uint64_t n, uint
                       uint32_t stack_limit, xdrg_status *d_status, void *stream) {
   if (!p || !d_status || (n && (!d_native || !d_sizes))) return XDRG_EINVAL;
   if (n == 0) return XDRG_OK;
+  if (int rc = plan_upload(p)) return rc;
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (p->path != XDRG_PATH_VAR) {
     // fixed_size for every record (xdr_struct_base_fs, types.h:691-700)

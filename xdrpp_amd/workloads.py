@@ -50,9 +50,9 @@ def _put(buf: np.ndarray, off: int, values: np.ndarray, dt: str) -> None:
     buf[:, off:off + k] = v.view(np.uint8).reshape(-1, k)
 
 
-def numerics(n: int, seed: int = SEED_NUMERICS) -> tuple[np.ndarray, np.ndarray]:
+def numerics(n: int, seed: int = SEED_NUMERICS, first: int = 0) -> tuple[np.ndarray, np.ndarray]:
     t = S.numerics
-    d = _draws(seed, n, 8)
+    d = _draws(seed, n, 8, first)
     buf = np.zeros((n, t.size), dtype=np.uint8)
     o = t.offsets
     _put(buf, o["b"], d[:, 0] & np.uint64(1), "u1")
@@ -60,7 +60,7 @@ def numerics(n: int, seed: int = SEED_NUMERICS) -> tuple[np.ndarray, np.ndarray]
                      ("f1", 5, "<u4"), ("f2", 6, "<u8")):
         _put(buf, o[f], d[:, k] & np.uint64(0xFFFFFFFF) if dt == "<u4" else d[:, k], dt)
     _put(buf, o["e1"], d[:, 7] % np.uint64(3), "<u4")
-    if n:
+    if n and first == 0:
         # record 0 = tests/marshal.cc:482-490
         r0 = np.zeros((1, t.size), dtype=np.uint8)
         _put(r0, o["b"], np.array([0]), "u1")
@@ -117,13 +117,14 @@ def _put_ref(buf, off, hoff, lens):
     _put(buf, off + 8, lens, "<u4")
 
 
-def recvar(n: int, seed: int = SEED_RECVAR) -> tuple[np.ndarray, np.ndarray]:
+def recvar(n: int, seed: int = SEED_RECVAR, first: int = 0) -> tuple[np.ndarray, np.ndarray]:
+    """Records [first, first + n); heap offsets are relative to this batch's heap."""
     t = S.recvar
     o = t.offsets
-    d = _draws(seed, n, 5)
+    d = _draws(seed, n, 5, first)
     blen = (d[:, 2] % np.uint64(257)).astype(np.int64)
     nlen = (d[:, 3] % np.uint64(65)).astype(np.int64)
-    pb = _payload_bytes(seed, n, 40, 0, 40)
+    pb = _payload_bytes(seed, n, 40, 0, 40, first)
     blob = pb[:, :256]
     name = (np.uint8(0x61) + pb[:, 256:320] % np.uint8(26)).astype(np.uint8)
     heap, (hb, hn) = _pack_heap([(blob, blen), (name, nlen)])
@@ -136,12 +137,13 @@ def recvar(n: int, seed: int = SEED_RECVAR) -> tuple[np.ndarray, np.ndarray]:
     return buf.reshape(-1), heap
 
 
-def rpc(n: int, seed: int = SEED_RPC) -> tuple[np.ndarray, np.ndarray]:
-    """rpc_msg records: sel = draw1 % 10; 0-4 CALL, 5 SUCCESS, 6 PROG_MISMATCH,
-    7 PROG_UNAVAIL (default void arm), 8 RPC_MISMATCH, 9 AUTH_ERROR."""
+def rpc(n: int, seed: int = SEED_RPC, first: int = 0) -> tuple[np.ndarray, np.ndarray]:
+    """rpc_msg records [first, first + n): sel = draw1 % 10; 0-4 CALL,
+    5 SUCCESS, 6 PROG_MISMATCH, 7 PROG_UNAVAIL (default void arm),
+    8 RPC_MISMATCH, 9 AUTH_ERROR."""
     t = S.rpc_msg
     off = t.offset_of
-    d = _draws(seed, n, 16)
+    d = _draws(seed, n, 16, first)
     sel = (d[:, 1] % np.uint64(10)).astype(np.int64)
     call = sel <= 4
     acc = (sel >= 5) & (sel <= 7)
@@ -150,8 +152,8 @@ def rpc(n: int, seed: int = SEED_RPC) -> tuple[np.ndarray, np.ndarray]:
     cred_len = np.where(call, (d[:, 6] % np.uint64(401)).astype(np.int64), 0)
     verf_len = np.where(call, (d[:, 8] % np.uint64(401)).astype(np.int64),
                         np.where(acc, (d[:, 6] % np.uint64(41)).astype(np.int64), 0))
-    cred_b = _payload_bytes(seed, n, 128, 0, 50)
-    verf_b = _payload_bytes(seed, n, 128, 64, 50)
+    cred_b = _payload_bytes(seed, n, 128, 0, 50, first)
+    verf_b = _payload_bytes(seed, n, 128, 64, 50, first)
     heap, (hc, hv) = _pack_heap([(cred_b, cred_len), (verf_b, verf_len)])
 
     buf = np.zeros((n, t.size), dtype=np.uint8)

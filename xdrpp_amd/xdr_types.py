@@ -313,6 +313,11 @@ class CompiledPlan:
         self.stride = _align_up(root.size, root.align)
         self.fixed_size = root.fixed_wire
 
+    @property
+    def is_var(self) -> bool:
+        """Variable-length wire records (opaque<>/string<>/unions)."""
+        return self.fixed_size is None
+
     def bad_discriminant_message(self, op: int) -> str:
         return self.messages.get(op, "bad value of discriminant")
 
