@@ -178,7 +178,7 @@ def cold_cache(mar, nat, xdr, back, n, alg_bytes, reps=5):
         dec.append(ev[2].elapsed_time(ev[3]))
     del scratch
     e, d = float(np.median(enc)), float(np.median(dec))
-    xb = n * 128
+    xb = xdr.numel()  # XDR bytes of the batch
     return {"encode_ms": round(e, 4), "decode_ms": round(d, 4),
             "encode_decode_gib_s": round(2 * xb / GIB / ((e + d) * 1e-3), 2),
             "achieved_GBps": round(alg_bytes / ((e + d) / 2 * 1e-3) / 1e9, 1),

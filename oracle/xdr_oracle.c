@@ -96,7 +96,7 @@ static uint64_t rec_size(const plan_t *P, const uint8_t *nat, uint32_t *err, uin
 
 /* ---------------------------------------------------------------- encode */
 /* One xdr_generic_put over [out, out+cap) for n records.  Returns 0 or the
- * error code; *erec/*eop receive the failing record and op. */
+ * error code; *erec and *eop receive the failing record and op. */
 int xdro_encode(const xdrg_op *ops, uint32_t nops, const uint32_t *table, uint32_t stride,
                 const uint8_t *native, uint64_t n, const uint8_t *heap, uint64_t heap_len,
                 uint8_t *out, uint64_t cap, uint64_t *offsets, uint32_t stack_limit,
