@@ -1,0 +1,742 @@
+// -*- C++ -*-
+// xdrpp_gpu.hh — header-only C++ layer of the MI355X batched XDR engine.
+//
+// Host code that uses xdrpp's xdrc-generated xdr_traits<T> keeps doing so;
+// this header turns xdr_traits<T> into a device plan and calls libxdrgpu.so
+// through the C ABI (xdrgpu.h).  Requires the xdrpp headers (<xdrpp/types.h>,
+// <xdrpp/marshal.h>) and the HIP runtime headers.
+//
+//   xdr::gpu::to_opaque_batch(recs, n)        == xdr::xdr_to_opaque(r0, ..., rn-1)
+//                                                (xdrpp/marshal.h:264-272)
+//   xdr::gpu::from_opaque_batch(bytes, out, n) == xdr::xdr_from_opaque(bytes, r0, ..., rn-1)
+//                                                (xdrpp/marshal.h:299-306)
+//
+// with the reference's exception classes and what() strings
+// (xdrpp/types.h:57-99) and its marshaling_stack_limit (marshal.h:21,34).
+//
+// How the plan is obtained (plan_for<T>()): a recorder Archive walks
+// xdr_traits<T>::save on a prototype object, field by field, exactly as
+// xdr_generic_put does (marshal.h:110-136).  Unions are recorded arm by arm
+// by driving xdr_traits<U>::load with each candidate discriminant
+// (xdrc/gen_hh.cc:661-673): the candidates come from the discriminant's
+// enum_values() (gen_hh.cc:271-305), or from U::_xdr_case_values()
+// (gen_hh.cc:410-432), or from a union_cases<U> specialization.  The
+// "bad value of <tag> in <union>" string is taken from the reference's own
+// exception by loading one invalid discriminant.
+//
+// Staged layout.  A device record holds every field at natural alignment;
+// opaque<>/string<> fields become xdrg_bytes_ref into a byte heap.  For
+// fixed-size, trivially copyable types whose C++ layout already IS that
+// layout (e.g. structs of ints/hypers/doubles) records are passed as-is;
+// other types are staged/unstaged on the host by plan-following archives.
+#ifndef XDRPP_GPU_HH_INCLUDED
+#define XDRPP_GPU_HH_INCLUDED 1
+
+#include <xdrpp/marshal.h>
+#include <xdrpp/types.h>
+
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <type_traits>
+#include <utility>
+#include <vector>
+
+#include "xdrgpu.h"
+
+namespace xdr {
+namespace gpu {
+
+//! Customization point: the case values of union U and whether it has a
+//! default arm.  The primary template uses what xdrc generates.
+template <typename U, typename = void> struct union_cases {
+  static std::vector<std::int64_t> values();
+  static constexpr bool has_default = U::_xdr_has_default_case;
+};
+
+//! API-level failure of the C ABI (bad arguments, HIP error).
+struct api_error : std::runtime_error {
+  int code;
+  api_error(int c, const std::string &what) : std::runtime_error(what), code(c) {}
+};
+
+namespace detail {
+
+inline std::uint32_t align_up(std::uint32_t x, std::uint32_t a) { return (x + a - 1) / a * a; }
+
+// ---------------------------------------------------------------- type tests
+template <typename T> struct bytes_kind {
+  static constexpr int kind = 0;
+  static constexpr std::uint32_t n = 0;
+};
+template <std::uint32_t N> struct bytes_kind<opaque_array<N>> {
+  static constexpr int kind = XDRG_OP_OPAQUE;
+  static constexpr std::uint32_t n = N;
+};
+template <std::uint32_t N> struct bytes_kind<xvector<std::uint8_t, N>> {
+  static constexpr int kind = XDRG_OP_VAROPAQUE;
+  static constexpr std::uint32_t n = N;
+};
+template <std::uint32_t N> struct bytes_kind<xstring<N>> {
+  static constexpr int kind = XDRG_OP_STRING;
+  static constexpr std::uint32_t n = N;
+};
+template <typename T> struct xarray_info : std::false_type {};
+template <typename E, std::uint32_t N> struct xarray_info<xarray<E, N>> : std::true_type {
+  using elem = E;
+  static constexpr std::uint32_t n = N;
+};
+
+// enum validation opt-in: the same test validate_enum<T> makes
+// (xdrpp/types.h:157-173).
+template <typename E> struct enum_validated {
+  template <typename U> static std::false_type test(...);
+  template <typename U> static decltype(xdr_validate_enum(U{}), std::true_type{}) test(int);
+  static constexpr bool value = decltype(test<E>(0))::value;
+};
+
+template <typename U, typename = void> struct has_case_values : std::false_type {};
+template <typename U>
+struct has_case_values<U, std::void_t<decltype(U::_xdr_case_values())>> : std::true_type {};
+
+template <typename T> using plain = std::remove_cv_t<std::remove_reference_t<T>>;
+
+// ---------------------------------------------------------------- sub-plans
+// Ops of one type placed at offset 0, pcs relative to the sub-plan start,
+// depths relative to the level the type is placed at.
+struct subplan {
+  std::vector<xdrg_op> ops;
+  std::vector<std::uint32_t> table;
+  std::vector<std::pair<std::uint32_t, std::string>> msgs;  // op -> bad-discriminant what()
+  std::uint32_t size = 0, align = 1;
+  bool identity = true;  // staged layout == C++ layout of the type
+  bool fixed = true;     // fixed wire size (xdr_traits<T>::has_fixed_size)
+
+  bool same_ops(const subplan &o) const {
+    if (ops.size() != o.ops.size() || table != o.table) return false;
+    for (std::size_t i = 0; i < ops.size(); ++i)
+      if (std::memcmp(&ops[i], &o.ops[i], sizeof(xdrg_op)) != 0) return false;
+    return true;
+  }
+};
+
+inline xdrg_op mkop(int kind, std::uint32_t noff, std::uint16_t depth, std::uint32_t a0 = 0,
+                    std::uint32_t a1 = 0, std::uint8_t flags = 0) {
+  xdrg_op o{};
+  o.kind = static_cast<std::uint8_t>(kind);
+  o.flags = flags;
+  o.depth = depth;
+  o.noff = noff;
+  o.arg0 = a0;
+  o.arg1 = a1;
+  return o;
+}
+
+// Append `src` to `dst` at byte offset `base`, `dadd` levels deeper.
+inline void append(subplan &dst, const subplan &src, std::uint32_t base, std::uint16_t dadd) {
+  const std::uint32_t pc0 = static_cast<std::uint32_t>(dst.ops.size());
+  const std::uint32_t t0 = static_cast<std::uint32_t>(dst.table.size());
+  dst.table.insert(dst.table.end(), src.table.begin(), src.table.end());
+  for (xdrg_op o : src.ops) {
+    if (o.kind != XDRG_OP_JUMP) o.noff += base;
+    o.depth = static_cast<std::uint16_t>(o.depth + dadd);
+    if (o.kind == XDRG_OP_JUMP) o.arg0 += pc0;
+    if ((o.kind == XDRG_OP_ENUM || o.kind == XDRG_OP_UNION) && (o.flags & XDRG_F_VALIDATE))
+      o.arg0 += t0;
+    if (o.kind == XDRG_OP_UNION) {
+      o.arg2 += t0;
+      for (std::uint32_t c = 0; c < o.arg3; ++c) dst.table[o.arg2 + 2 * c + 1] += pc0;
+      if (o.flags & XDRG_F_DEFAULT) o.arg4 += pc0;
+    }
+    dst.ops.push_back(o);
+  }
+  for (const auto &m : src.msgs) dst.msgs.emplace_back(m.first + pc0, m.second);
+}
+
+template <typename T> subplan record_type();
+
+// Walks xdr_traits<S>::save on a prototype: each archived field is placed
+// at its natural alignment (the C++ rule xdrc structs follow).
+struct struct_recorder {
+  subplan *sp;
+  const char *proto;
+  std::uint32_t off = 0;
+  template <typename F> void operator()(const F &f) {
+    const subplan fp = record_type<plain<F>>();
+    off = align_up(off, fp.align);
+    const std::uintptr_t cxx = reinterpret_cast<const char *>(&f) - proto;
+    if (cxx != off || !fp.identity) sp->identity = false;
+    append(*sp, fp, off, 1);  // class level (marshal.h:129-136)
+    off += fp.size;
+    sp->align = std::max(sp->align, fp.align);
+    sp->fixed = sp->fixed && fp.fixed;
+  }
+};
+
+// Drives xdr_traits<U>::load: the first archived value is the discriminant
+// (fed `disc`), the next (if any) is the selected arm.
+struct union_feeder {
+  std::int64_t disc;
+  int seen = 0;
+  bool disc_validated = false;
+  std::vector<std::int32_t> disc_values;  // when validated
+  subplan arm;
+  bool have_arm = false;
+  template <typename F> void operator()(F &f) {
+    using P = plain<F>;
+    if (seen++ == 0) {
+      if constexpr (std::is_integral_v<P> || std::is_enum_v<P>) {
+        f = static_cast<P>(disc);
+        if constexpr (xdr_traits<P>::is_enum && !std::is_same_v<P, bool>) {
+          if constexpr (enum_validated<P>::value) {
+            disc_validated = true;
+            for (std::int32_t v : xdr_traits<P>::enum_values()) disc_values.push_back(v);
+          }
+        }
+      } else {
+        throw std::logic_error("xdr::gpu: union discriminant is not a 32-bit integer");
+      }
+      return;
+    }
+    if (have_arm) throw std::logic_error("xdr::gpu: union load archived two arms");
+    arm = record_type<P>();
+    have_arm = true;
+  }
+};
+
+}  // namespace detail
+
+template <typename U, typename E>
+std::vector<std::int64_t> union_cases<U, E>::values() {
+  std::vector<std::int64_t> v;
+  if constexpr (detail::has_case_values<U>::value)
+    for (auto c : U::_xdr_case_values()) v.push_back(static_cast<std::int64_t>(c));
+  return v;
+}
+
+namespace detail {
+
+template <typename U> subplan record_union() {
+  // candidate discriminants: union_cases<U>, else the discriminant enum's tags
+  std::vector<std::int64_t> cand = union_cases<U>::values();
+  const bool has_default = union_cases<U>::has_default;
+  if constexpr (has_case_values<U>::value) {
+    if (cand.empty()) {  // xdrc lists no cases for unions with a default arm
+      using D = plain<decltype(std::declval<U>()._xdr_discriminant())>;
+      if constexpr (xdr_traits<D>::is_enum)
+        for (auto v : xdr_traits<D>::enum_values()) cand.push_back(v);
+    }
+  }
+  if (cand.empty() && !has_default)
+    throw std::logic_error("xdr::gpu: cannot enumerate the cases of a union (specialize xdr::gpu::union_cases)");
+  std::int64_t probe = 0;
+  for (auto v : cand) probe = std::max(probe, v + 1);
+
+  struct arm_rec { bool is_void; subplan sp; };
+  std::vector<std::pair<std::int64_t, arm_rec>> cases;
+  bool validated = false;
+  std::vector<std::int32_t> vvals;
+  std::string message;
+  auto run = [&](std::int64_t v, arm_rec &out) -> bool {
+    U u{};
+    union_feeder f{v};
+    try {
+      xdr_traits<U>::load(f, u);
+    } catch (const xdr_bad_discriminant &e) {
+      message = e.what();
+      return false;
+    }
+    validated = f.disc_validated;
+    vvals = f.disc_values;
+    out.is_void = !f.have_arm;
+    if (f.have_arm) out.sp = std::move(f.arm);
+    return true;
+  };
+  arm_rec dflt{};
+  bool have_dflt = false;
+  if (has_default) have_dflt = run(probe, dflt);
+  for (auto v : cand) {
+    arm_rec a{};
+    if (!run(v, a)) continue;
+    if (have_dflt && a.is_void == dflt.is_void && (a.is_void || a.sp.same_ops(dflt.sp))) continue;
+    cases.emplace_back(v, std::move(a));
+  }
+  if (!has_default) {
+    arm_rec junk{};
+    run(probe, junk);  // the reference's own "bad value of <tag> in <union>"
+  }
+
+  subplan sp;
+  sp.fixed = false;
+  sp.identity = false;
+  std::uint32_t aal = 4, asz = 0;
+  auto grow = [&](const arm_rec &a) {
+    if (!a.is_void) { aal = std::max(aal, a.sp.align); asz = std::max(asz, a.sp.size); }
+  };
+  for (auto &c : cases) grow(c.second);
+  if (have_dflt) grow(dflt);
+  const std::uint32_t arms_off = align_up(4, aal);
+  sp.align = aal;
+  sp.size = align_up(arms_off + asz, aal);
+
+  std::uint8_t flags = 0;
+  std::uint32_t a0 = 0, a1 = 0;
+  if (validated) {
+    flags |= XDRG_F_VALIDATE;
+    a0 = static_cast<std::uint32_t>(sp.table.size());
+    std::vector<std::int32_t> s(vvals);
+    std::sort(s.begin(), s.end());
+    s.erase(std::unique(s.begin(), s.end()), s.end());
+    for (auto v : s) sp.table.push_back(static_cast<std::uint32_t>(v));
+    a1 = static_cast<std::uint32_t>(s.size());
+  }
+  sp.ops.push_back(mkop(XDRG_OP_UNION, 0, 1, a0, a1, flags));
+  if (!message.empty() && !has_default) sp.msgs.emplace_back(0, message);
+
+  // arms, each once; identical arms share code
+  std::vector<std::pair<std::int64_t, std::int64_t>> targets;  // (value, pc or -1 = end)
+  std::vector<std::uint32_t> jumps;
+  std::vector<std::pair<const subplan *, std::uint32_t>> placed;
+  auto place = [&](const arm_rec &a) -> std::int64_t {
+    if (a.is_void) return -1;
+    for (auto &p : placed)
+      if (p.first->same_ops(a.sp)) return p.second;
+    const std::uint32_t pc = static_cast<std::uint32_t>(sp.ops.size());
+    append(sp, a.sp, arms_off, 1);
+    jumps.push_back(static_cast<std::uint32_t>(sp.ops.size()));
+    sp.ops.push_back(mkop(XDRG_OP_JUMP, 0, 1));
+    placed.emplace_back(&a.sp, pc);
+    return pc;
+  };
+  for (auto &c : cases) targets.emplace_back(c.first, place(c.second));
+  std::int64_t dpc = 0;
+  if (have_dflt) dpc = place(dflt);
+  const std::uint32_t end = static_cast<std::uint32_t>(sp.ops.size());
+  for (auto j : jumps) sp.ops[j].arg0 = end;
+  xdrg_op &u = sp.ops[0];
+  u.arg2 = static_cast<std::uint32_t>(sp.table.size());
+  u.arg3 = static_cast<std::uint32_t>(targets.size());
+  for (auto &t : targets) {
+    sp.table.push_back(static_cast<std::uint32_t>(t.first));
+    sp.table.push_back(t.second < 0 ? end : static_cast<std::uint32_t>(t.second));
+  }
+  if (have_dflt) {
+    u.flags |= XDRG_F_DEFAULT;
+    u.arg4 = dpc < 0 ? end : static_cast<std::uint32_t>(dpc);
+  }
+  return sp;
+}
+
+template <typename T> subplan record_type() {
+  using TR = xdr_traits<T>;
+  subplan sp;
+  if constexpr (std::is_same_v<T, bool>) {
+    sp.ops.push_back(mkop(XDRG_OP_BOOL, 0, 0));
+    sp.size = sp.align = 1;
+  } else if constexpr (bytes_kind<T>::kind != 0) {
+    constexpr int k = bytes_kind<T>::kind;
+    sp.ops.push_back(mkop(k, 0, 0, bytes_kind<T>::n));
+    if constexpr (k == XDRG_OP_OPAQUE) {
+      sp.size = bytes_kind<T>::n;
+      sp.align = 1;
+    } else {
+      sp.size = sizeof(xdrg_bytes_ref);
+      sp.align = alignof(xdrg_bytes_ref);
+      sp.identity = false;
+      sp.fixed = false;
+    }
+  } else if constexpr (TR::is_enum) {
+    static_assert(sizeof(T) == 4, "XDR enums are 32-bit");
+    if constexpr (enum_validated<T>::value) {
+      std::vector<std::int32_t> s(TR::enum_values().begin(), TR::enum_values().end());
+      std::sort(s.begin(), s.end());
+      s.erase(std::unique(s.begin(), s.end()), s.end());
+      for (auto v : s) sp.table.push_back(static_cast<std::uint32_t>(v));
+      sp.ops.push_back(mkop(XDRG_OP_ENUM, 0, 0, 0, static_cast<std::uint32_t>(s.size()),
+                            XDRG_F_VALIDATE));
+    } else {
+      sp.ops.push_back(mkop(XDRG_OP_ENUM, 0, 0));
+    }
+    sp.size = sp.align = 4;
+  } else if constexpr (TR::is_numeric) {
+    using UT = typename TR::uint_type;
+    sp.ops.push_back(mkop(sizeof(UT) == 8 ? XDRG_OP_U64 : XDRG_OP_U32, 0, 0));
+    sp.size = sizeof(T);
+    sp.align = alignof(T);
+  } else if constexpr (xarray_info<T>::value) {
+    using E = typename xarray_info<T>::elem;
+    const subplan e = record_type<E>();
+    const std::uint32_t step = align_up(e.size, e.align);
+    for (std::uint32_t i = 0; i < xarray_info<T>::n; ++i) append(sp, e, i * step, 1);  // container level
+    sp.size = step * xarray_info<T>::n;
+    sp.align = e.align;
+    sp.identity = e.identity && sizeof(E) == step && sizeof(T) == sp.size;
+    sp.fixed = e.fixed;
+  } else if constexpr (TR::is_union) {
+    sp = record_union<T>();
+  } else if constexpr (TR::is_struct || TR::is_class) {
+    static const T proto{};
+    struct_recorder r{&sp, reinterpret_cast<const char *>(&proto)};
+    TR::save(r, proto);
+    sp.size = align_up(std::max<std::uint32_t>(r.off, 1), sp.align);
+    if (sizeof(T) != sp.size || !std::is_trivially_copyable_v<T>) sp.identity = false;
+  } else {
+    static_assert(!sizeof(T *), "xdr::gpu: xvector<T>/pointer<T> of non-bytes T is not supported yet");
+  }
+  return sp;
+}
+
+// ------------------------------------------------- plan-following archives
+// Stage: xdr_traits<T>::save writes the staged record + heap.
+// Unstage: xdr_traits<T>::load reads them back.  Both follow the plan's
+// pc in step with the archive calls (wire order), so every field lands at
+// the op's staged offset; union discriminants pick the arm's pc.
+struct cursor {
+  const xdrg_op *ops;
+  const std::uint32_t *table;
+  std::uint32_t pc = 0;
+  const xdrg_op &next() {
+    while (ops[pc].kind == XDRG_OP_JUMP) pc = ops[pc].arg0;
+    return ops[pc];
+  }
+  void branch(const xdrg_op &u, std::int32_t d) {
+    for (std::uint32_t c = 0; c < u.arg3; ++c)
+      if (static_cast<std::int32_t>(table[u.arg2 + 2 * c]) == d) { pc = table[u.arg2 + 2 * c + 1]; return; }
+    if (u.flags & XDRG_F_DEFAULT) { pc = u.arg4; return; }
+    throw xdr_bad_discriminant("bad value of discriminant");  // save() threw already
+  }
+};
+
+struct stager : cursor {
+  std::uint8_t *rec;
+  std::vector<std::uint8_t> *heap;
+  template <typename F> void operator()(const F &f) {
+    using P = plain<F>;
+    using TR = xdr_traits<P>;
+    if constexpr (std::is_same_v<P, bool>) {
+      rec[next().noff] = f ? 1 : 0;
+      ++pc;
+    } else if constexpr (bytes_kind<P>::kind == XDRG_OP_OPAQUE) {
+      std::memcpy(rec + next().noff, f.data(), f.size());
+      ++pc;
+    } else if constexpr (bytes_kind<P>::kind != 0) {
+      xdrg_bytes_ref r{heap->size(), static_cast<std::uint32_t>(f.size()), 0};
+      heap->insert(heap->end(), reinterpret_cast<const std::uint8_t *>(f.data()),
+                   reinterpret_cast<const std::uint8_t *>(f.data()) + f.size());
+      std::memcpy(rec + next().noff, &r, sizeof r);
+      ++pc;
+    } else if constexpr (TR::is_enum || TR::is_numeric) {
+      const xdrg_op &o = next();
+      if (o.kind == XDRG_OP_UNION) {
+        const std::int32_t d = static_cast<std::int32_t>(f);
+        std::memcpy(rec + o.noff, &d, 4);
+        branch(o, d);
+      } else {
+        std::memcpy(rec + o.noff, &f, sizeof(P));
+        ++pc;
+      }
+    } else if constexpr (xarray_info<P>::value) {
+      for (const auto &e : f) (*this)(e);
+    } else {
+      TR::save(*this, f);
+    }
+  }
+};
+
+struct unstager : cursor {
+  const std::uint8_t *rec;
+  const std::uint8_t *heap;
+  template <typename F> void operator()(F &f) {
+    using P = plain<F>;
+    using TR = xdr_traits<P>;
+    if constexpr (std::is_same_v<P, bool>) {
+      f = rec[next().noff] != 0;
+      ++pc;
+    } else if constexpr (bytes_kind<P>::kind == XDRG_OP_OPAQUE) {
+      std::memcpy(f.data(), rec + next().noff, f.size());
+      ++pc;
+    } else if constexpr (bytes_kind<P>::kind != 0) {
+      xdrg_bytes_ref r;
+      std::memcpy(&r, rec + next().noff, sizeof r);
+      const char *p = reinterpret_cast<const char *>(heap + r.off);
+      f.assign(p, p + r.len);
+      ++pc;
+    } else if constexpr (TR::is_enum || TR::is_numeric) {
+      const xdrg_op &o = next();
+      std::memcpy(&f, rec + o.noff, sizeof(P));
+      if (o.kind == XDRG_OP_UNION) branch(o, static_cast<std::int32_t>(f));
+      else ++pc;
+    } else if constexpr (xarray_info<P>::value) {
+      for (auto &e : f) (*this)(e);
+    } else {
+      TR::load(*this, f);
+    }
+  }
+};
+
+inline std::uint32_t be32(const std::uint8_t *p) {
+  return (std::uint32_t(p[0]) << 24) | (std::uint32_t(p[1]) << 16) | (std::uint32_t(p[2]) << 8) | p[3];
+}
+
+inline void hipcheck(hipError_t e, const char *what) {
+  if (e != hipSuccess) throw api_error(XDRG_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+inline void abicheck(int rc, const char *what) {
+  if (rc != XDRG_OK) {
+    const char *h = xdrg_last_hip_error();
+    throw api_error(rc, std::string(what) + " failed (" + std::to_string(rc) + ")" +
+                            (rc == XDRG_EHIP && h ? std::string(": ") + h : std::string()));
+  }
+}
+
+template <typename T> struct dev_buf {
+  T *p = nullptr;
+  explicit dev_buf(std::size_t n) {
+    if (n) hipcheck(hipMalloc(reinterpret_cast<void **>(&p), n * sizeof(T)), "hipMalloc");
+  }
+  ~dev_buf() { if (p) (void)hipFree(p); }
+  dev_buf(const dev_buf &) = delete;
+  dev_buf &operator=(const dev_buf &) = delete;
+};
+
+}  // namespace detail
+
+// ---------------------------------------------------------------- the plan
+//! The device plan of T (built once, thread-safe).
+template <typename T> class batch_plan {
+ public:
+  static const batch_plan &get() {
+    static const batch_plan p;
+    return p;
+  }
+  xdrg_plan *handle() const { return h_.get(); }
+  const std::vector<xdrg_op> &ops() const { return ops_; }
+  const std::vector<std::uint32_t> &table() const { return table_; }
+  std::uint32_t stride() const { return stride_; }
+  //! Records are passed to the device as-is (staged layout == C++ layout).
+  bool identity() const { return identity_; }
+  bool fixed() const { return fixed_; }
+  std::uint32_t fixed_size() const { return fixed_size_; }
+
+  //! Throw the reference's exception for a device status.
+  [[noreturn]] void raise(const xdrg_error &e) const {
+    std::string what = xdrg_error_message(e.code);
+    if (e.code == XDRG_ERR_BAD_DISCRIMINANT)
+      for (const auto &m : msgs_)
+        if (m.first == e.op) what = m.second;
+    switch (xdrg_error_exception(e.code)) {
+    case XDRG_EXC_OVERFLOW: throw xdr_overflow(what);
+    case XDRG_EXC_STACK_OVERFLOW: throw xdr_stack_overflow(what);
+    case XDRG_EXC_BAD_MESSAGE_SIZE: throw xdr_bad_message_size(what);
+    case XDRG_EXC_BAD_DISCRIMINANT: throw xdr_bad_discriminant(what);
+    case XDRG_EXC_SHOULD_BE_ZERO: throw xdr_should_be_zero(what);
+    case XDRG_EXC_INVARIANT_FAILED: throw xdr_invariant_failed(what);
+    default: throw xdr_runtime_error(what);
+    }
+  }
+
+ private:
+  struct deleter { void operator()(xdrg_plan *p) const { xdrg_plan_destroy(p); } };
+  batch_plan() {
+    detail::subplan sp = detail::record_type<T>();
+    detail::subplan top;
+    detail::append(top, sp, 0, 0);
+    top.ops.push_back(detail::mkop(XDRG_OP_END, 0, 0));
+    ops_ = std::move(top.ops);
+    table_ = std::move(top.table);
+    msgs_ = std::move(top.msgs);
+    stride_ = detail::align_up(std::max<std::uint32_t>(sp.size, 1), std::max<std::uint32_t>(sp.align, 4));
+    identity_ = sp.identity && sp.fixed && sizeof(T) == stride_;
+    fixed_ = sp.fixed;
+    xdrg_plan *h = nullptr;
+    detail::abicheck(xdrg_plan_create(ops_.data(), static_cast<std::uint32_t>(ops_.size()),
+                                      table_.empty() ? nullptr : table_.data(),
+                                      static_cast<std::uint32_t>(table_.size()), stride_, &h),
+                     "xdrg_plan_create");
+    h_.reset(h);
+    xdrg_plan_info info{};
+    detail::abicheck(xdrg_plan_get_info(h, &info), "xdrg_plan_get_info");
+    fixed_size_ = info.fixed_size;
+  }
+  std::unique_ptr<xdrg_plan, deleter> h_;
+  std::vector<xdrg_op> ops_;
+  std::vector<std::uint32_t> table_;
+  std::vector<std::pair<std::uint32_t, std::string>> msgs_;
+  std::uint32_t stride_ = 0, fixed_size_ = 0;
+  bool identity_ = false, fixed_ = false;
+};
+
+template <typename T> const batch_plan<T> &plan_for() { return batch_plan<T>::get(); }
+
+// ---------------------------------------------------------------- staging
+//! Host staging of a batch: records in the staged layout + payload heap.
+struct staged_batch {
+  std::vector<std::uint8_t> native;
+  std::vector<std::uint8_t> heap;
+};
+
+template <typename T> staged_batch stage(const T *recs, std::size_t n) {
+  const batch_plan<T> &P = plan_for<T>();
+  staged_batch b;
+  b.native.assign(n * P.stride(), 0);
+  if (P.identity()) {
+    std::memcpy(b.native.data(), recs, n * sizeof(T));
+    return b;
+  }
+  for (std::size_t i = 0; i < n; ++i) {
+    detail::stager s;
+    s.ops = P.ops().data();
+    s.table = P.table().data();
+    s.rec = b.native.data() + i * P.stride();
+    s.heap = &b.heap;
+    s(recs[i]);
+  }
+  return b;
+}
+
+template <typename T>
+void unstage(const std::uint8_t *native, const std::uint8_t *heap, std::size_t n, T *out) {
+  const batch_plan<T> &P = plan_for<T>();
+  if (P.identity()) {
+    std::memcpy(static_cast<void *>(out), native, n * sizeof(T));
+    return;
+  }
+  for (std::size_t i = 0; i < n; ++i) {
+    detail::unstager u;
+    u.ops = P.ops().data();
+    u.table = P.table().data();
+    u.rec = native + i * P.stride();
+    u.heap = heap;
+    u(out[i]);
+  }
+}
+
+//! Record index of a concatenated batch (host walk of lengths and
+//! discriminants only).  Records that would overrun `len` or carry a bad
+//! discriminant end the walk; the remaining offsets are `len`, and the
+//! device decode then reports the reference's error for that record.
+template <typename T>
+std::vector<std::uint64_t> index_records(const std::uint8_t *xdr, std::size_t len, std::size_t n) {
+  const batch_plan<T> &P = plan_for<T>();
+  std::vector<std::uint64_t> off(n + 1, len);
+  std::uint64_t p = 0;
+  const xdrg_op *ops = P.ops().data();
+  const std::uint32_t *tab = P.table().data();
+  for (std::size_t r = 0; r < n; ++r) {
+    off[r] = std::min<std::uint64_t>(p, len);
+    std::uint32_t pc = 0;
+    bool bad = false;
+    while (!bad && ops[pc].kind != XDRG_OP_END) {
+      const xdrg_op &o = ops[pc];
+      switch (o.kind) {
+      case XDRG_OP_JUMP: pc = o.arg0; continue;
+      case XDRG_OP_U64: p += 8; break;
+      case XDRG_OP_OPAQUE: p += detail::align_up(o.arg0, 4); break;
+      case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING:
+        if (p + 4 > len) { bad = true; break; }
+        p += 4 + ((std::uint64_t(detail::be32(xdr + p)) + 3) & ~3ull);
+        break;
+      case XDRG_OP_UNION: {
+        if (p + 4 > len) { bad = true; break; }
+        const std::int32_t d = static_cast<std::int32_t>(detail::be32(xdr + p));
+        p += 4;
+        detail::cursor c{ops, tab, pc};
+        try { c.branch(o, d); } catch (const xdr_bad_discriminant &) { bad = true; break; }
+        pc = c.pc;
+        continue;
+      }
+      default: p += 4; break;
+      }
+      ++pc;
+    }
+    if (bad || p > len) return off;  // off[r] is set; the rest stay at len
+  }
+  off[n] = p;  // p < len: trailing bytes, which decode reports at record n
+  return off;
+}
+
+// ------------------------------------------------------------ batch calls
+//! xdr::xdr_to_opaque(recs[0], ..., recs[n-1]) on the GPU.  Host in, host
+//! out (pinned staging is the caller's business for peak PCIe rates; the
+//! device-resident entry point is xdrg_encode).
+template <typename T>
+opaque_vec<> to_opaque_batch(const T *recs, std::size_t n, hipStream_t s = nullptr) {
+  const batch_plan<T> &P = plan_for<T>();
+  staged_batch b = stage(recs, n);
+  detail::dev_buf<std::uint8_t> d_nat(b.native.size()), d_heap(b.heap.size());
+  detail::dev_buf<xdrg_status> d_st(1);
+  detail::hipcheck(hipMemcpyAsync(d_nat.p, b.native.data(), b.native.size(), hipMemcpyHostToDevice, s), "H2D");
+  if (!b.heap.empty())
+    detail::hipcheck(hipMemcpyAsync(d_heap.p, b.heap.data(), b.heap.size(), hipMemcpyHostToDevice, s), "H2D");
+  detail::abicheck(xdrg_status_init(d_st.p, s), "xdrg_status_init");
+  std::size_t total = std::size_t(P.fixed_size()) * n;
+  const std::size_t ws_bytes = xdrg_workspace_size(P.handle(), n);
+  detail::dev_buf<std::uint8_t> ws(ws_bytes);
+  detail::dev_buf<std::uint64_t> d_off(P.fixed() ? 0 : n + 1);
+  if (!P.fixed()) {  // size pass for the output capacity (xdr_argpack_size)
+    detail::dev_buf<std::uint32_t> d_sz(n);
+    detail::abicheck(xdrg_serial_sizes(P.handle(), d_nat.p, n, d_sz.p, marshaling_stack_limit, d_st.p, s),
+                     "xdrg_serial_sizes");
+    std::vector<std::uint32_t> sz(n);
+    if (n) detail::hipcheck(hipMemcpyAsync(sz.data(), d_sz.p, n * 4, hipMemcpyDeviceToHost, s), "D2H");
+    xdrg_error e{};
+    detail::abicheck(xdrg_status_read(d_st.p, s, &e), "xdrg_status_read");
+    if (e.code) P.raise(e);
+    total = 0;
+    for (auto v : sz) total += v;
+  }
+  detail::dev_buf<std::uint8_t> d_xdr(total);
+  detail::abicheck(xdrg_encode(P.handle(), d_nat.p, n, b.heap.empty() ? nullptr : d_heap.p, b.heap.size(),
+                               d_xdr.p, total, d_off.p, marshaling_stack_limit, ws.p, ws_bytes, d_st.p, s),
+                   "xdrg_encode");
+  opaque_vec<> out;
+  out.resize(total);
+  if (total) detail::hipcheck(hipMemcpyAsync(out.data(), d_xdr.p, total, hipMemcpyDeviceToHost, s), "D2H");
+  xdrg_error e{};
+  detail::abicheck(xdrg_status_read(d_st.p, s, &e), "xdrg_status_read");
+  if (e.code) P.raise(e);
+  return out;
+}
+
+//! xdr::xdr_from_opaque(bytes, out[0], ..., out[n-1]) on the GPU.
+template <typename T>
+void from_opaque_batch(const void *bytes, std::size_t len, T *out, std::size_t n,
+                       hipStream_t s = nullptr) {
+  const batch_plan<T> &P = plan_for<T>();
+  const auto *x = static_cast<const std::uint8_t *>(bytes);
+  detail::dev_buf<std::uint8_t> d_xdr(len);
+  detail::dev_buf<std::uint8_t> d_nat(n * P.stride());
+  detail::dev_buf<xdrg_status> d_st(1);
+  if (len) detail::hipcheck(hipMemcpyAsync(d_xdr.p, x, len, hipMemcpyHostToDevice, s), "H2D");
+  detail::abicheck(xdrg_status_init(d_st.p, s), "xdrg_status_init");
+  std::vector<std::uint64_t> idx;
+  detail::dev_buf<std::uint64_t> d_off(P.fixed() ? 0 : n + 1);
+  detail::dev_buf<std::uint8_t> d_heap(P.fixed() ? 0 : len);
+  if (!P.fixed()) {
+    idx = index_records<T>(x, len, n);
+    detail::hipcheck(hipMemcpyAsync(d_off.p, idx.data(), (n + 1) * 8, hipMemcpyHostToDevice, s), "H2D");
+  }
+  detail::abicheck(xdrg_decode(P.handle(), d_xdr.p, len, d_off.p, n, d_nat.p, d_heap.p,
+                               P.fixed() ? 0 : len, marshaling_stack_limit, nullptr, 0, d_st.p, s),
+                   "xdrg_decode");
+  std::vector<std::uint8_t> nat(n * P.stride()), heap(P.fixed() ? 0 : len);
+  if (!nat.empty())
+    detail::hipcheck(hipMemcpyAsync(nat.data(), d_nat.p, nat.size(), hipMemcpyDeviceToHost, s), "D2H");
+  if (!heap.empty())
+    detail::hipcheck(hipMemcpyAsync(heap.data(), d_heap.p, heap.size(), hipMemcpyDeviceToHost, s), "D2H");
+  xdrg_error e{};
+  detail::abicheck(xdrg_status_read(d_st.p, s, &e), "xdrg_status_read");
+  if (e.code) P.raise(e);
+  unstage(nat.data(), heap.data(), n, out);
+}
+
+}  // namespace gpu
+}  // namespace xdr
+
+#endif  // XDRPP_GPU_HH_INCLUDED

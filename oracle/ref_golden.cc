@@ -19,8 +19,7 @@
 //   ref_golden bench <schema> <n> <threads> <reps>
 //       times xdr_put / xdr_get streams over contiguous slices, one
 //       std::thread per slice, and per-record xdr_to_opaque; prints JSON.
-#include "ref_schemas.hh"
-#include "workload_gen.h"
+#include "ref_objects.hh"
 
 #include <algorithm>
 #include <chrono>
@@ -37,227 +36,7 @@ using std::size_t;
 using std::string;
 using std::vector;
 
-static void die(const string &m) {
-  fprintf(stderr, "ref_golden: %s\n", m.c_str());
-  exit(2);
-}
-template <typename T> static T bits_as(uint64_t v) {
-  T t;
-  memcpy(&t, &v, sizeof(T));
-  return t;
-}
-static void write_file(const string &path, const void *p, size_t n) {
-  FILE *f = fopen(path.c_str(), "wb");
-  if (!f) die("cannot open " + path);
-  if (n && fwrite(p, 1, n, f) != n) die("short write " + path);
-  fclose(f);
-}
-
-// ------------------------------------------------------------ generators
-static void gen_numerics(size_t n, uint64_t seed, vector<testns::numerics> &v) {
-  v.resize(n);
-  for (size_t r = 0; r < n; ++r) {
-    testns::numerics &x = v[r];
-    memset(&x, 0, sizeof x);  // padding bytes are zero in the fixture
-    uint64_t d[8];
-    for (int k = 0; k < 8; ++k) d[k] = wg_draw(seed, r * 8 + k);
-    x.b = d[0] & 1;
-    x.i1 = (int32_t)(uint32_t)d[1];
-    x.i2 = (uint32_t)d[2];
-    x.i3 = (int64_t)d[3];
-    x.i4 = d[4];
-    x.f1 = bits_as<float>((uint32_t)d[5]);
-    x.f2 = bits_as<double>(d[6]);
-    x.e1 = testns::other_color(d[7] % 3);
-    if (r == 0) {  // tests/marshal.cc:482-490
-      x.b = false;
-      x.i1 = 0x7eeeeeee;
-      x.i2 = 0xffffffff;
-      x.i3 = UINT64_C(0x7ddddddddddddddd);
-      x.i4 = UINT64_C(0xfccccccccccccccc);
-      x.f1 = 3.141592654;
-      x.f2 = 2.71828182846;
-      x.e1 = testns::REDDER;
-    }
-  }
-}
-
-static void gen_rec128(size_t n, uint64_t seed, uint64_t first, vector<rec128> &v) {
-  v.resize(n);
-  for (size_t r = 0; r < n; ++r) {
-    uint64_t g = first + r, d[20];
-    for (int k = 0; k < 20; ++k) d[k] = wg_draw(seed, g * 20 + k);
-    rec128 &x = v[r];
-    int32_t *a = &x.a0;
-    for (int k = 0; k < 8; ++k) a[k] = (int32_t)(uint32_t)d[k];
-    uint64_t *u = &x.u0;
-    for (int k = 0; k < 6; ++k) u[k] = d[8 + k];
-    double *dd = &x.d0;
-    for (int k = 0; k < 6; ++k) dd[k] = bits_as<double>(d[14 + k]);
-  }
-}
-
-static void gen_recvar(size_t n, uint64_t seed, vector<recvar> &v) {
-  v.resize(n);
-  const uint64_t ps = seed ^ WG_PAYLOAD_XOR;
-  for (size_t r = 0; r < n; ++r) {
-    uint64_t d[5];
-    for (int k = 0; k < 5; ++k) d[k] = wg_draw(seed, r * 5 + k);
-    recvar &x = v[r];
-    x.id = d[0];
-    x.kind = (int32_t)(uint32_t)d[1];
-    uint32_t bl = d[2] % 257, nl = d[3] % 65;
-    x.score = bits_as<double>(d[4]);
-    x.blob.resize(bl);
-    for (uint32_t j = 0; j < bl; ++j) x.blob[j] = wg_byte(ps, r * 40 + j / 8, j);
-    string s(nl, '\0');
-    for (uint32_t j = 0; j < nl; ++j)
-      s[j] = char(0x61 + wg_byte(ps, r * 40 + 32 + j / 8, j) % 26);
-    x.name = s;
-  }
-}
-
-static void fill_auth(rpcx::opaque_auth &a, int32_t flavor, uint32_t len, uint64_t ps,
-                      uint64_t word0) {
-  a.flavor = flavor;
-  a.body.resize(len);
-  for (uint32_t j = 0; j < len; ++j) a.body[j] = wg_byte(ps, word0 + j / 8, j);
-}
-
-static void gen_rpc(size_t n, uint64_t seed, vector<rpcx::rpc_msg> &v) {
-  v.resize(n);
-  const uint64_t ps = seed ^ WG_PAYLOAD_XOR;
-  for (size_t r = 0; r < n; ++r) {
-    uint64_t d[16];
-    for (int k = 0; k < 16; ++k) d[k] = wg_draw(seed, r * 16 + k);
-    rpcx::rpc_msg &m = v[r];
-    m = rpcx::rpc_msg{};
-    m.xid = (uint32_t)d[0];
-    unsigned sel = d[1] % 10;
-    if (sel <= WG_RPC_CALL_MAX) {
-      m.body.mtype = rpcx::CALL;
-      rpcx::call_body &c = m.body.cbody;
-      c.rpcvers = 2;
-      c.prog = (uint32_t)d[2];
-      c.vers = (uint32_t)d[3];
-      c.proc = (uint32_t)d[4];
-      fill_auth(c.cred, int32_t(d[5] % 2), d[6] % 401, ps, r * 128);
-      fill_auth(c.verf, int32_t(d[7] % 2), d[8] % 401, ps, r * 128 + 64);
-    } else {
-      m.body.mtype = rpcx::REPLY;
-      rpcx::reply_body &b = m.body.rbody;
-      if (sel <= WG_RPC_PROG_UNAVAIL) {
-        b.stat = rpcx::MSG_ACCEPTED;
-        fill_auth(b.areply.verf, int32_t(d[5] % 2), d[6] % 41, ps, r * 128 + 64);
-        rpcx::reply_data_u &rd = b.areply.reply_data;
-        if (sel == WG_RPC_SUCCESS) rd.stat = rpcx::SUCCESS;
-        else if (sel == WG_RPC_PROG_MISMATCH) {
-          rd.stat = rpcx::PROG_MISMATCH;
-          rd.mismatch_info_.low = (uint32_t)d[9];
-          rd.mismatch_info_.high = (uint32_t)d[10];
-        } else rd.stat = rpcx::PROG_UNAVAIL;
-      } else {
-        b.stat = rpcx::MSG_DENIED;
-        if (sel == WG_RPC_RPC_MISMATCH) {
-          b.rreply.stat = rpcx::RPC_MISMATCH;
-          b.rreply.mismatch_info_.low = (uint32_t)d[9];
-          b.rreply.mismatch_info_.high = (uint32_t)d[10];
-        } else {
-          b.rreply.stat = rpcx::AUTH_ERROR;
-          b.rreply.rj_why = int32_t(d[11] % 15);
-        }
-      }
-    }
-  }
-}
-
-// ------------------------------------------------------------- staging
-// Heap packing for encode inputs: payloads in record order, field order,
-// no alignment (exercises unaligned heap reads on the device).
-struct heap_t {
-  vector<uint8_t> b;
-  xdrg_bytes_ref put(const uint8_t *p, size_t n) {
-    xdrg_bytes_ref r{b.size(), uint32_t(n), 0};
-    b.insert(b.end(), p, p + n);
-    return r;
-  }
-};
-
-static void stage(const vector<testns::numerics> &v, vector<uint8_t> &nat, heap_t &) {
-  nat.resize(v.size() * sizeof(testns::numerics));
-  memcpy(nat.data(), v.data(), nat.size());
-}
-static void stage(const vector<rec128> &v, vector<uint8_t> &nat, heap_t &) {
-  nat.resize(v.size() * sizeof(rec128));
-  memcpy(nat.data(), v.data(), nat.size());
-}
-static void stage(const vector<recvar> &v, vector<uint8_t> &nat, heap_t &h) {
-  nat.assign(v.size() * sizeof(st_recvar), 0);
-  st_recvar *s = reinterpret_cast<st_recvar *>(nat.data());
-  for (size_t r = 0; r < v.size(); ++r) {
-    s[r].id = v[r].id;
-    s[r].kind = v[r].kind;
-    s[r].blob = h.put(v[r].blob.data(), v[r].blob.size());
-    s[r].name = h.put(reinterpret_cast<const uint8_t *>(v[r].name.data()), v[r].name.size());
-    s[r].score = v[r].score;
-  }
-}
-static void stage_auth(const rpcx::opaque_auth &a, st_opaque_auth &s, heap_t &h) {
-  s.flavor = a.flavor;
-  s.body = h.put(a.body.data(), a.body.size());
-}
-static void stage(const vector<rpcx::rpc_msg> &v, vector<uint8_t> &nat, heap_t &h) {
-  nat.assign(v.size() * sizeof(st_rpc_msg), 0);
-  st_rpc_msg *s = reinterpret_cast<st_rpc_msg *>(nat.data());
-  for (size_t r = 0; r < v.size(); ++r) {
-    const rpcx::rpc_msg &m = v[r];
-    s[r].xid = m.xid;
-    s[r].body.mtype = m.body.mtype;
-    if (m.body.mtype == rpcx::CALL) {
-      st_call_body &c = s[r].body.u.cbody;
-      c.rpcvers = m.body.cbody.rpcvers;
-      c.prog = m.body.cbody.prog;
-      c.vers = m.body.cbody.vers;
-      c.proc = m.body.cbody.proc;
-      stage_auth(m.body.cbody.cred, c.cred, h);
-      stage_auth(m.body.cbody.verf, c.verf, h);
-    } else {
-      st_reply_body &b = s[r].body.u.rbody;
-      b.stat = m.body.rbody.stat;
-      if (b.stat == rpcx::MSG_ACCEPTED) {
-        const rpcx::accepted_reply &a = m.body.rbody.areply;
-        stage_auth(a.verf, b.u.areply.verf, h);
-        b.u.areply.reply_data.stat = a.reply_data.stat;
-        if (a.reply_data.stat == rpcx::PROG_MISMATCH) {
-          b.u.areply.reply_data.u.mismatch_info.low = a.reply_data.mismatch_info_.low;
-          b.u.areply.reply_data.u.mismatch_info.high = a.reply_data.mismatch_info_.high;
-        }
-      } else {
-        const rpcx::rejected_reply &j = m.body.rbody.rreply;
-        b.u.rreply.stat = j.stat;
-        if (j.stat == rpcx::RPC_MISMATCH) {
-          b.u.rreply.u.mismatch_info.low = j.mismatch_info_.low;
-          b.u.rreply.u.mismatch_info.high = j.mismatch_info_.high;
-        } else
-          b.u.rreply.u.rj_why = j.rj_why;
-      }
-    }
-  }
-}
-
-// Equality for round-trip checks (byte-level for fixed structs).
-static bool same(const testns::numerics &a, const testns::numerics &b) {
-  return a.b == b.b && a.i1 == b.i1 && a.i2 == b.i2 && a.i3 == b.i3 && a.i4 == b.i4 &&
-         !memcmp(&a.f1, &b.f1, 4) && !memcmp(&a.f2, &b.f2, 8) && a.e1 == b.e1;
-}
-static bool same(const rec128 &a, const rec128 &b) { return !memcmp(&a, &b, sizeof a); }
-static bool same(const recvar &a, const recvar &b) {
-  return a.id == b.id && a.kind == b.kind && a.blob == b.blob && a.name == b.name &&
-         !memcmp(&a.score, &b.score, 8);
-}
-static bool same(const rpcx::rpc_msg &a, const rpcx::rpc_msg &b) {
-  return xdr::xdr_to_opaque(a) == xdr::xdr_to_opaque(b);
-}
+using namespace refobj;
 
 template <typename T>
 static void emit(const vector<T> &v, const string &prefix) {

@@ -64,7 +64,7 @@ static int enum_ok(const plan_t *P, const xdrg_op *op, uint32_t v) {
 }
 
 /* xdr_size of one record (xdr_traits<T>::serial_size).  Returns 0 and sets
- * *err/*eop on a bad discriminant. */
+ * *err and *eop on a bad discriminant. */
 static uint64_t rec_size(const plan_t *P, const uint8_t *nat, uint32_t *err, uint32_t *eop) {
   uint64_t s = 0;
   uint32_t pc = 0;

@@ -1,0 +1,238 @@
+// C++ drop-in test: the xdr::gpu layer (include/xdrpp_gpu.hh) over the
+// reference's own xdr_traits<T> and exceptions.
+//
+// TEST INFRASTRUCTURE: built by oracle/Makefile against the reference headers
+// and xdrpp/marshal.cc (in place, into oracle/_ref/dropin_test), because
+// the types it marshals are xdrpp types and the bytes it compares against
+// come from the reference marshaler in the same process.
+//
+//   dropin_test plans <dir>   (CPU)  write the plans recorded from
+//                                    xdr_traits<T> (ops/table/stride) per schema
+//   dropin_test stage         (CPU)  stage() == the reference-side staged layout,
+//                                    unstage(stage(x)) == x, index_records ==
+//                                    the reference's record offsets
+//   dropin_test gpu           (GPU)  to_opaque_batch == xdr_put stream,
+//                                    from_opaque_batch round trip, and the
+//                                    reference's exceptions on bad input
+#include "ref_objects.hh"
+#include "xdrpp_gpu.hh"
+
+#include <cstdio>
+#include <fstream>
+#include <functional>
+
+using namespace refobj;
+
+// The hand-expanded unions of oracle/ref_schemas.hh are plain structs with
+// switch-based traits (no xdrc union helpers): name their cases here.
+namespace xdr {
+namespace gpu {
+template <> struct union_cases<rpcx::body_u> {
+  static std::vector<std::int64_t> values() { return {rpcx::CALL, rpcx::REPLY}; }
+  static constexpr bool has_default = false;
+};
+template <> struct union_cases<rpcx::reply_body> {
+  static std::vector<std::int64_t> values() { return {rpcx::MSG_ACCEPTED, rpcx::MSG_DENIED}; }
+  static constexpr bool has_default = false;
+};
+template <> struct union_cases<rpcx::reply_data_u> {
+  static std::vector<std::int64_t> values() {
+    return {rpcx::SUCCESS, rpcx::PROG_UNAVAIL, rpcx::PROG_MISMATCH};
+  }
+  static constexpr bool has_default = true;
+};
+template <> struct union_cases<rpcx::rejected_reply> {
+  static std::vector<std::int64_t> values() { return {rpcx::RPC_MISMATCH, rpcx::AUTH_ERROR}; }
+  static constexpr bool has_default = false;
+};
+}  // namespace gpu
+}  // namespace xdr
+
+static int failures = 0;
+#define CHECK(c, ...)                                  \
+  do {                                                 \
+    if (!(c)) {                                        \
+      ++failures;                                      \
+      std::fprintf(stderr, "FAIL %s:%d: ", __FILE__, __LINE__); \
+      std::fprintf(stderr, __VA_ARGS__);               \
+      std::fprintf(stderr, "\n");                      \
+    }                                                  \
+  } while (0)
+
+template <typename T> static void write_plan(const std::string &dir, const char *name) {
+  const auto &P = xdr::gpu::plan_for<T>();
+  std::ofstream f(dir + "/" + name + ".plan", std::ios::binary);
+  const std::uint32_t hdr[4] = {static_cast<std::uint32_t>(P.ops().size()),
+                                static_cast<std::uint32_t>(P.table().size()), P.stride(),
+                                P.identity() ? 1u : 0u};
+  f.write(reinterpret_cast<const char *>(hdr), sizeof hdr);
+  f.write(reinterpret_cast<const char *>(P.ops().data()), P.ops().size() * sizeof(xdrg_op));
+  f.write(reinterpret_cast<const char *>(P.table().data()), P.table().size() * 4);
+}
+
+// reference stream: one xdr_put over all records (= xdr_to_opaque of the pack)
+template <typename T>
+static std::vector<std::uint8_t> ref_stream(const std::vector<T> &v, std::vector<std::uint64_t> &off) {
+  std::size_t total = 0;
+  off.assign(v.size() + 1, 0);
+  for (std::size_t i = 0; i < v.size(); ++i) {
+    off[i] = total;
+    total += xdr::xdr_size(v[i]);
+  }
+  off[v.size()] = total;
+  std::vector<std::uint8_t> out(total);
+  xdr::xdr_put p(out.data(), out.data() + total);
+  for (const T &t : v) xdr::archive(p, t);
+  return out;
+}
+
+template <typename T>
+static void check_stage(const char *name, const std::vector<T> &v) {
+  const auto &P = xdr::gpu::plan_for<T>();
+  xdr::gpu::staged_batch b = xdr::gpu::stage(v.data(), v.size());
+  std::vector<std::uint8_t> nat;
+  heap_t h;
+  stage(v, nat, h);  // the reference-side staged layout (oracle/ref_objects.hh)
+  CHECK(nat.size() == b.native.size(), "%s: staged size %zu vs %zu", name, b.native.size(), nat.size());
+  CHECK(nat == b.native, "%s: staged native bytes differ", name);
+  CHECK(h.b == b.heap, "%s: staged heap differs", name);
+  std::vector<T> back(v.size());
+  xdr::gpu::unstage(b.native.data(), b.heap.data(), v.size(), back.data());
+  bool ok = true;
+  for (std::size_t i = 0; i < v.size(); ++i) ok = ok && same(v[i], back[i]);
+  CHECK(ok, "%s: unstage(stage(x)) != x", name);
+  std::vector<std::uint64_t> off;
+  std::vector<std::uint8_t> s = ref_stream(v, off);
+  CHECK(xdr::gpu::index_records<T>(s.data(), s.size(), v.size()) == off, "%s: index_records differs",
+        name);
+  std::printf("stage %s: %zu records, stride %u, identity %d ok\n", name, v.size(), P.stride(),
+              int(P.identity()));
+}
+
+template <typename T>
+static void check_gpu(const char *name, const std::vector<T> &v) {
+  std::vector<std::uint64_t> off;
+  const std::vector<std::uint8_t> want = ref_stream(v, off);
+  xdr::opaque_vec<> got = xdr::gpu::to_opaque_batch(v.data(), v.size());
+  CHECK(got.size() == want.size() && std::equal(got.begin(), got.end(), want.begin()),
+        "%s: to_opaque_batch differs from xdr_put (%zu vs %zu bytes)", name, got.size(), want.size());
+  std::vector<T> back(v.size());
+  xdr::gpu::from_opaque_batch(want.data(), want.size(), back.data(), back.size());
+  bool ok = true;
+  for (std::size_t i = 0; i < v.size(); ++i) ok = ok && same(v[i], back[i]);
+  CHECK(ok, "%s: from_opaque_batch(xdr_put stream) != records", name);
+  // per-record entry point: the batch of one equals xdr_to_opaque(r)
+  xdr::opaque_vec<> one = xdr::gpu::to_opaque_batch(&v[1], 1);
+  CHECK(one == xdr::xdr_to_opaque(v[1]), "%s: batch of one differs from xdr_to_opaque", name);
+  std::printf("gpu %s: %zu records, %zu bytes bit-exact, round trip ok\n", name, v.size(), want.size());
+}
+
+// Run `f`; return the exception's class name and what(), as the reference would.
+static std::pair<std::string, std::string> catch_what(const std::function<void()> &f) {
+  try {
+    f();
+  } catch (const xdr::xdr_overflow &e) {
+    return {"xdr_overflow", e.what()};
+  } catch (const xdr::xdr_stack_overflow &e) {
+    return {"xdr_stack_overflow", e.what()};
+  } catch (const xdr::xdr_bad_message_size &e) {
+    return {"xdr_bad_message_size", e.what()};
+  } catch (const xdr::xdr_bad_discriminant &e) {
+    return {"xdr_bad_discriminant", e.what()};
+  } catch (const xdr::xdr_should_be_zero &e) {
+    return {"xdr_should_be_zero", e.what()};
+  } catch (const xdr::xdr_invariant_failed &e) {
+    return {"xdr_invariant_failed", e.what()};
+  }
+  return {"none", ""};
+}
+
+template <typename T>
+static void check_error(const char *label, const std::vector<std::uint8_t> &bytes, std::size_t n) {
+  std::vector<T> a(n), b(n);
+  auto ref = catch_what([&] {
+    // reference: xdr_from_opaque over the concatenation (one archive)
+    xdr::xdr_get g(bytes.data(), bytes.data() + bytes.size());
+    for (T &t : a) xdr::archive(g, t);
+    g.done();
+  });
+  auto gpu = catch_what([&] { xdr::gpu::from_opaque_batch(bytes.data(), bytes.size(), b.data(), n); });
+  CHECK(ref == gpu, "%s: reference %s(\"%s\") vs gpu %s(\"%s\")", label, ref.first.c_str(),
+        ref.second.c_str(), gpu.first.c_str(), gpu.second.c_str());
+  std::printf("error %s: %s(\"%s\") matches\n", label, ref.first.c_str(), ref.second.c_str());
+}
+
+static void gpu_errors() {
+  std::vector<rpcx::rpc_msg> m;
+  gen_rpc(64, WG_SEED_RPC, m);
+  std::vector<std::uint64_t> off;
+  std::vector<std::uint8_t> s = ref_stream(m, off);
+  {  // unknown mtype in record 5
+    auto x = s;
+    x[off[5] + 7] = 7;
+    check_error<rpcx::rpc_msg>("rpc bad mtype", x, m.size());
+  }
+  {  // trailing bytes
+    auto x = s;
+    x.insert(x.end(), {0, 0, 0, 0});
+    check_error<rpcx::rpc_msg>("rpc trailing", x, m.size());
+  }
+  {  // truncated stream
+    auto x = s;
+    x.resize(x.size() - 8);
+    check_error<rpcx::rpc_msg>("rpc short", x, m.size());
+  }
+  std::vector<recvar> r;
+  gen_recvar(32, WG_SEED_RECVAR, r);
+  std::vector<std::uint8_t> rs = ref_stream(r, off);
+  for (std::size_t i = 0; i < r.size(); ++i) {
+    if (r[i].blob.size() % 4 == 0) continue;
+    auto x = rs;  // nonzero pad byte after record i's blob
+    x[off[i] + 16 + r[i].blob.size()] = 0x5a;
+    check_error<recvar>("recvar nonzero pad", x, r.size());
+    break;
+  }
+  std::vector<rec128> f;
+  gen_rec128(16, WG_SEED_REC128, 0, f);
+  std::vector<std::uint8_t> fs = ref_stream(f, off);
+  fs.pop_back();
+  check_error<rec128>("rec128 size not multiple of 4", fs, f.size());
+  fs.resize(fs.size() - 3 - 64);
+  check_error<rec128>("rec128 short", fs, f.size());
+}
+
+int main(int argc, char **argv) {
+  const std::string mode = argc > 1 ? argv[1] : "stage";
+  std::vector<testns::numerics> nu;
+  std::vector<rec128> rc;
+  std::vector<recvar> rv;
+  std::vector<rpcx::rpc_msg> rp;
+  gen_numerics(1000, WG_SEED_NUMERICS, nu);
+  gen_rec128(1024, WG_SEED_REC128, 0, rc);
+  gen_recvar(1024, WG_SEED_RECVAR, rv);
+  gen_rpc(1024, WG_SEED_RPC, rp);
+  if (mode == "plans") {
+    const std::string dir = argc > 2 ? argv[2] : ".";
+    write_plan<testns::numerics>(dir, "numerics");
+    write_plan<testns_v::numerics>(dir, "numerics_validated");
+    write_plan<rec128>(dir, "rec128");
+    write_plan<recvar>(dir, "recvar");
+    write_plan<rpcx::rpc_msg>(dir, "rpc");
+  } else if (mode == "stage") {
+    check_stage("numerics", nu);
+    check_stage("rec128", rc);
+    check_stage("recvar", rv);
+    check_stage("rpc", rp);
+  } else if (mode == "gpu") {
+    check_gpu("numerics", nu);
+    check_gpu("rec128", rc);
+    check_gpu("recvar", rv);
+    check_gpu("rpc", rp);
+    gpu_errors();
+  } else {
+    std::fprintf(stderr, "usage: dropin_test plans <dir> | stage | gpu\n");
+    return 2;
+  }
+  if (failures) std::fprintf(stderr, "%d failure(s)\n", failures);
+  return failures ? 1 : 0;
+}
