@@ -324,3 +324,70 @@ def test_swaps(dev):
     assert np.array_equal(M.swap64(t).cpu().numpy(), x.byteswap())
     x32 = x.view(np.int32)
     assert np.array_equal(M.swap32(to_dev(x32, dev)).cpu().numpy(), x32.byteswap())
+
+
+# ------------------------------------- every var kernel, forced in turn
+KERNELS = {"per_lane": (1, 1), "record_image": (2, 2), "chunk_image_group": (3, 3)}
+
+
+@pytest.fixture(params=list(KERNELS))
+def forced(request):
+    import ctypes as C
+    L = A.lib()
+    L.xdrg__force_var_kernels.argtypes = [C.c_int, C.c_int]
+    L.xdrg__force_var_kernels(*KERNELS[request.param])
+    yield request.param
+    L.xdrg__force_var_kernels(0, 0)
+
+
+@pytest.mark.parametrize("name", ["recvar", "rpc"])
+@pytest.mark.parametrize("n", [1, 63, 65, 1024])
+def test_var_kernels_golden(dev, forced, name, n):
+    p = plan(name)
+    mar = M.Marshaler(p, dev)
+    N = SMALL_N[name]
+    nat_all = golden(name, N, "native")
+    heap = golden(name, N, "heap")
+    nat = nat_all[:n * p.stride]
+    want, offs = O.encode(p.cp, nat, n, heap)
+    res = mar.encode(to_dev(nat, dev), n, to_dev(heap, dev))
+    assert np.array_equal(res.xdr.cpu().numpy(), want)
+    assert np.array_equal(res.offsets.cpu().numpy().view(np.uint64), offs)
+    back, bheap = mar.decode(res.xdr, n, res.offsets)
+    o_nat, o_heap = O.decode(p.cp, want, n, offs)
+    assert np.array_equal(back.cpu().numpy(), o_nat)
+    assert np.array_equal(bheap.cpu().numpy(), o_heap)
+
+
+@pytest.mark.parametrize("name", ["recvar", "rpc"])
+@pytest.mark.parametrize("seed", range(3))
+def test_var_kernels_fuzzed_errors(dev, forced, name, seed):
+    n = SMALL_N[name]
+    p = plan(name)
+    mar = M.Marshaler(p, dev)
+    x = golden(name, n, "xdr").copy()
+    offs = golden(name, n, "offsets", np.uint64)
+    rng = np.random.default_rng(100 + seed)
+    for _ in range(3):
+        i = int(rng.integers(0, x.size))
+        x[i] = np.uint8(rng.integers(0, 256))
+    want = _oracle_err(lambda: O.decode(p.cp, x, n, offs))
+    got = _gpu_err(lambda: mar.decode(to_dev(x, dev), n, to_dev(offs.view(np.int64), dev)))
+    assert got == want
+
+
+@pytest.mark.parametrize("name", ["recvar", "rpc"])
+def test_var_kernels_capacity_and_stack(dev, forced, name):
+    n = 300
+    p = plan(name)
+    mar = M.Marshaler(p, dev)
+    nat, heap = W.GENERATORS[name](n)
+    full, offs = O.encode(p.cp, nat, n, heap)
+    cap = int(offs[200]) + 10  # record 200 runs out of room
+    want = _oracle_err(lambda: O.encode(p.cp, nat, n, heap, cap=cap))
+    got = _gpu_err(lambda: mar.encode(to_dev(nat, dev), n, to_dev(heap, dev), capacity=cap))
+    assert got == want and want[1] == 200
+    for limit in (0, 1, 3):
+        want = _oracle_err(lambda: O.encode(p.cp, nat, n, heap, stack_limit=limit))
+        got = _gpu_err(lambda: mar.encode(to_dev(nat, dev), n, to_dev(heap, dev), stack_limit=limit))
+        assert got == want

@@ -13,15 +13,18 @@ sys.path.insert(0, ROOT)
 from xdrpp_amd import _abi as A, marshal as M, schemas as S, workloads as W  # noqa: E402
 
 L = A.lib()
-L.xdrg__select_var_kernel.argtypes = [C.c_int]
+L.xdrg__force_var_kernels.argtypes = [C.c_int, C.c_int]
 L.xdrg__set_image_bytes.argtypes = [C.c_int]
-# (kernel family, LDS image bytes): 0 = LDS image, 1 = record image, 2 = group copy
-VARIANTS = [(1, 16384), (3, 16384)]
+# (encode kernel, decode kernel, encode LDS image bytes); kernels as in
+# xdrgpu.hip g_force_enc/g_force_dec: 0 auto, 1 per-lane, 2 record image,
+# 3 chunk-map image (encode) / group copy (decode)
+VARIANTS = [tuple(int(x) for x in v.split(",")) for v in
+            os.environ.get("VARIANTS", "2,3,16384 3,3,4096 3,3,0 3,3,8192").split()]
 
 
 def select(v):
-    L.xdrg__select_var_kernel(v[0])
-    L.xdrg__set_image_bytes(v[1])
+    L.xdrg__force_var_kernels(v[0], v[1])
+    L.xdrg__set_image_bytes(v[2])
 dev = torch.device("cuda:0")
 out = {}
 for schema in sys.argv[1:] or ["recvar", "rpc"]:
@@ -66,10 +69,10 @@ for schema in sys.argv[1:] or ["recvar", "rpc"]:
             torch.cuda.synchronize()
             times[v][0].append(ev[0].elapsed_time(ev[1]) / 5)
             times[v][1].append(ev[1].elapsed_time(ev[2]) / 5)
-    select(VARIANTS[-1])
+    select((0, 0, 4096))
     mar.check()
     for v in VARIANTS:
-        name = f"k{v[0]}_{v[1] // 1024}K"
+        name = f"e{v[0]}d{v[1]}_{v[2] // 1024}K"
         e, d = float(np.median(times[v][0])), float(np.median(times[v][1]))
         out[f"{schema}_{name}"] = {"encode_ms": round(e, 4), "decode_ms": round(d, 4),
                                    "gib_s": round(2 * total / 2**30 / ((e + d) * 1e-3), 1)}

@@ -2,7 +2,7 @@
 (diagnostic build path: s_memtime stamps, cdna_hip_programming.md §7
 In-kernel stamps).  Read the SHARES, not the total (stamps cost time).
 
-    VK=<kernel select> python tools/tune/stamps_var.py recvar rpc
+    VENC=<0-3> VDEC=<0-3> python tools/tune/stamps_var.py recvar rpc
 """
 import ctypes as C
 import os
@@ -16,11 +16,12 @@ sys.path.insert(0, ROOT)
 from xdrpp_amd import _abi as A, marshal as M, schemas as S, workloads as W  # noqa: E402
 
 L = A.lib()
-L.xdrg__select_var_kernel.argtypes = [C.c_int]
+L.xdrg__force_var_kernels.argtypes = [C.c_int, C.c_int]
 L.xdrg__set_stamps.argtypes = [C.c_void_p]
 L.xdrg__set_stamps_enc.argtypes = [C.c_void_p]
 dev = torch.device("cuda:0")
-ENC = ["sizes+scan", "tile load+barrier", "walk", "emit", "-"]
+ENC = (["sizes+scan", "tile load+barrier", "walk", "emit", "-"]
+       if os.environ.get("VENC", "0") == "2" else ["prologue+tile", "walk", "chunk map", "chunk copy", "image out"])
 DEC = ["tile zero+barrier", "walk (parse)", "pieces+barrier", "piece copy", "tile out"]
 
 
@@ -47,7 +48,7 @@ for schema in sys.argv[1:] or ["recvar"]:
     offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
     back = torch.empty_like(nat)
     hout = torch.empty(total, dtype=torch.uint8, device=dev)
-    L.xdrg__select_var_kernel(int(os.environ.get('VK', '3')))
+    L.xdrg__force_var_kernels(int(os.environ.get('VENC', '0')), int(os.environ.get('VDEC', '0')))
     mar.status.init(torch.cuda.current_stream().cuda_stream)
     nwaves = (n + 63) // 64
     se = torch.zeros(nwaves * 8, dtype=torch.int64, device=dev)

@@ -167,15 +167,16 @@ int compile_plan(xdrg_plan &p) {
     // forward-only, so one reverse sweep over the DAG suffices).
     // Same sweep for the scalar (non-payload) wire words of a record.
     std::vector<uint32_t> slots(n, 0), words(n, 0);
-    std::vector<uint64_t> pieces(n, 0), bytes(n, 0);
+    std::vector<uint64_t> pieces(n, 0), bytes(n, 0), chunks(n, 0);
     for (uint32_t i = n; i-- > 0;) {
       const xdrg_op &op = p.ops[i];
       uint32_t best = 0, bw = 0;
-      uint64_t bp = 0, bb = 0;
+      uint64_t bp = 0, bb = 0, bc = 0;
       switch (op.kind) {
       case XDRG_OP_END: break;
       case XDRG_OP_JUMP:
         best = slots[op.arg0]; bw = words[op.arg0]; bp = pieces[op.arg0]; bb = bytes[op.arg0];
+        bc = chunks[op.arg0];
         break;
       case XDRG_OP_UNION:
         for (uint32_t c = 0; c < op.arg3; ++c) {
@@ -184,12 +185,14 @@ int compile_plan(xdrg_plan &p) {
           bw = std::max(bw, words[t]);
           bp = std::max(bp, pieces[t]);
           bb = std::max(bb, bytes[t]);
+          bc = std::max(bc, chunks[t]);
         }
         if (op.flags & XDRG_F_DEFAULT) {
           best = std::max(best, slots[op.arg4]);
           bw = std::max(bw, words[op.arg4]);
           bp = std::max(bp, pieces[op.arg4]);
           bb = std::max(bb, bytes[op.arg4]);
+          bc = std::max(bc, chunks[op.arg4]);
         }
         bw += 1;
         bb += 4;
@@ -201,13 +204,17 @@ int compile_plan(xdrg_plan &p) {
         bw = words[i + 1] + w;
         bp = pieces[i + 1] + (var ? (uint64_t(op.arg0) + 255u) / 256u : 0u);
         bb = bytes[i + 1] + 4ull * w + (var ? (uint64_t(op.arg0) + 3u) & ~3ull : 0u);
+        bc = chunks[i + 1] + (var ? (uint64_t(op.arg0) + 15u) / 16u : 0u);
+        if (var) p.max_slot_len = std::max(p.max_slot_len, op.arg0);
       }
       }
       slots[i] = best;
       words[i] = bw;
       pieces[i] = bp;
       bytes[i] = bb;
+      chunks[i] = bc;
     }
+    p.max_chunks16 = chunks[0];
     p.max_var_slots = slots[0];
     p.max_scalar_words = words[0];
     p.max_pieces = uint32_t(std::min<uint64_t>(pieces[0], 0xffffffffu));

@@ -74,6 +74,8 @@ struct xdrg_plan {
   uint32_t max_scalar_words = 0;  // var plans: most non-payload wire words on one path
   uint32_t max_pieces = 0;  // var plans: most 256-byte payload pieces on one path (by bounds)
   uint64_t max_record_bytes = 0;  // var plans: largest wire record the bounds allow
+  uint64_t max_chunks16 = 0;      // var plans: most 16-byte payload chunks on one path
+  uint32_t max_slot_len = 0;      // var plans: largest opaque<>/string<> bound
   bool has_checks = false;
   bool has_bool = false;
   // fixed plans

@@ -890,242 +890,6 @@ __device__ __forceinline__ void st_words(uint8_t *p, const u32x4 &v, uint32_t nb
   if (nb > 8u) st32(p + 8, v.z);
 }
 
-// Encode with group copy.  The lane walk stages the record's scalar wire
-// words in LDS (never global) and appends pieces in record order: scalar
-// runs (source: LDS) interleaved with payload pieces (source: heap).  The
-// groups then write each record's bytes within a step or two, so every
-// output line is completed while it is still in L2.
-struct epiece {  // 16 bytes
-  uint64_t src;    // heap byte offset, or LDS byte offset for scalar runs
-  uint32_t dst;    // byte offset from the wave's first record
-  uint32_t meta;   // len (9 bits) | from-LDS (bit 9)
-};
-constexpr uint32_t kFromLds = 1u << 9;
-
-__host__ __device__ inline uint32_t enc_g_wave_bytes(uint32_t stride, uint32_t MSW, uint32_t PM,
-                                                     uint32_t SL) {
-  const uint32_t tile = (64u * stride + 15u) & ~15u;
-  const uint32_t sw = (64u * (MSW ? MSW : 1u) * 4u + 15u) & ~15u;
-  const uint32_t np = 64u * ((PM ? PM : 1u) + (SL ? SL : 1u) + 1u);  // payload + scalar pieces
-  return tile + sw + np * 16u;
-}
-
-template <int KMAX>
-__global__ __launch_bounds__(256) void k_var_encode_g(
-    const uint8_t *__restrict__ native, uint64_t n, uint32_t stride, const uint8_t *__restrict__ heap,
-    uint64_t heap_len, uint8_t *__restrict__ xdr, uint64_t cap, uint64_t *__restrict__ offsets,
-    const uint32_t *__restrict__ sizes, const unsigned long long *__restrict__ block_base,
-    const xdrg_op *__restrict__ ops, uint32_t nops, const uint32_t *__restrict__ table,
-    uint32_t stack_limit, uint32_t PM, uint32_t MSW, uint32_t SL, unsigned long long *err) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
-  __shared__ unsigned long long wsum[4];
-  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const uint32_t tile_bytes = (64u * stride + 15u) & ~15u;
-  const uint32_t msw = MSW ? MSW : 1u;
-  uint8_t *tile = sm + wid * enc_g_wave_bytes(stride, MSW, PM, SL);
-  uint32_t *sw = reinterpret_cast<uint32_t *>(tile + tile_bytes);
-  epiece *pcs = reinterpret_cast<epiece *>(tile + tile_bytes + ((64u * msw * 4u + 15u) & ~15u));
-
-  const uint64_t r = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  const uint32_t sz = r < n ? sizes[r] : 0u;
-  unsigned long long v = (sz & kSizeErr) ? 0ull : sz;
-  unsigned long long incl = v;
-  for (int o = 1; o < 64; o <<= 1) {
-    const unsigned long long x = __shfl_up(incl, o, 64);
-    if (lane >= static_cast<uint32_t>(o)) incl += x;
-  }
-  if (lane == 63) wsum[wid] = incl;
-  const uint64_t wr0 = static_cast<uint64_t>(blockIdx.x) * blockDim.x + wid * 64u;
-  const uint32_t wn = wr0 < n ? static_cast<uint32_t>(min<uint64_t>(64, n - wr0)) : 0u;
-  const uint32_t nbytes = wn * stride;
-  const uint8_t *nsrc = native + wr0 * stride;
-  for (uint32_t i = lane; i < nbytes / 16u; i += 64u)
-    reinterpret_cast<u32x4 *>(tile)[i] = reinterpret_cast<const u32x4 *>(nsrc)[i];
-  for (uint32_t i = (nbytes / 16u) * 4u + lane; i < nbytes / 4u; i += 64u)
-    reinterpret_cast<uint32_t *>(tile)[i] = reinterpret_cast<const uint32_t *>(nsrc)[i];
-  __syncthreads();
-  unsigned long long wbase = 0;
-  for (uint32_t w = 0; w < wid; ++w) wbase += wsum[w];
-  const uint64_t off = block_base[blockIdx.x] + wbase + incl - v;
-  const uint64_t wave_out = __shfl(off, 0, 64);  // first record of the wave
-
-  // ---- walk: scalar words -> LDS, payload slots -> registers
-  uint64_t psr[KMAX];
-  uint32_t pat[KMAX], pln[KMAX];  // pat: word index in the record where the payload starts
-#pragma unroll
-  for (int k = 0; k < KMAX; ++k) { psr[k] = 0; pat[k] = 0; pln[k] = 0; }
-  uint32_t nsw = 0, wpos = 0, nslot = 0;
-  bool ok = false;
-  if (r < n) offsets[r] = off;
-  {
-    const uint8_t *nat = tile + lane * stride;
-    uint32_t *mysw = sw + lane * msw;
-    uint64_t pos = off;
-    uint32_t pc = (r < n && !(sz & kSizeErr)) ? 0u : kPcDone;
-    ok = pc == 0u;
-    for (uint32_t upc = 0; upc < nops; ++upc) {
-      if (!__any(pc == upc)) continue;
-      const xdrg_op op = ops[upc];
-      if (pc != upc) continue;
-      if (op.kind == XDRG_OP_END) { pc = kPcDone; continue; }
-      if (op.kind == XDRG_OP_JUMP) { pc = op.arg0; continue; }
-      if (op.depth > stack_limit) { report(err, r, upc, XDRG_ERR_STACK_PUT); ok = false; pc = kPcDone; continue; }
-      const uint32_t *nw = reinterpret_cast<const uint32_t *>(nat + op.noff);
-      uint32_t blen = 0;
-      uint64_t need = 4;
-      if (op.kind == XDRG_OP_U64) need = 8;
-      else if (op.kind == XDRG_OP_OPAQUE) need = op.arg0;
-      else if (op.kind == XDRG_OP_VAROPAQUE || op.kind == XDRG_OP_STRING) {
-        blen = nw[2];
-        need = 4ull + blen;
-      }
-      if (need > cap - min(pos, cap)) { report(err, r, upc, XDRG_ERR_OVERFLOW_PUT); ok = false; pc = kPcDone; continue; }
-      switch (op.kind) {
-      case XDRG_OP_U32: case XDRG_OP_ENUM:
-        mysw[nsw++] = bswap32(nw[0]); pos += 4; ++wpos; ++pc; break;
-      case XDRG_OP_BOOL:
-        mysw[nsw++] = nat[op.noff] ? 0x01000000u : 0u; pos += 4; ++wpos; ++pc; break;
-      case XDRG_OP_U64:
-        mysw[nsw++] = bswap32(nw[1]);
-        mysw[nsw++] = bswap32(nw[0]);
-        pos += 8; wpos += 2; ++pc; break;
-      case XDRG_OP_OPAQUE: {
-        const uint32_t BL = op.arg0, nwd = (BL + 3u) >> 2;
-        for (uint32_t k = 0; k < nwd; ++k) {
-          uint32_t w = 0;
-          for (uint32_t bb = 0; bb < 4u && 4u * k + bb < BL; ++bb)
-            w |= static_cast<uint32_t>(nat[op.noff + 4u * k + bb]) << (8u * bb);
-          mysw[nsw++] = w;
-        }
-        pos += 4ull * nwd; wpos += nwd; ++pc; break;
-      }
-      case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
-        mysw[nsw++] = bswap32(blen);
-        ++wpos;
-        if (blen) {
-          const uint64_t hsrc = *reinterpret_cast<const uint64_t *>(nw);
-#pragma unroll
-          for (int k = 0; k < KMAX; ++k)
-            if (static_cast<uint32_t>(k) == nslot) { psr[k] = hsrc; pat[k] = wpos; pln[k] = blen; }
-          ++nslot;
-        }
-        wpos += (blen + 3u) >> 2;
-        pos += 4ull + ((static_cast<uint64_t>(blen) + 3u) & ~3ull); ++pc; break;
-      }
-      case XDRG_OP_UNION: {
-        const uint32_t d = nw[0];
-        mysw[nsw++] = bswap32(d);
-        pos += 4; ++wpos;
-        pc = static_cast<uint32_t>(union_target(op, table, d));  // validated by k_var_size
-        break;
-      }
-      default: ++pc; break;
-      }
-    }
-  }
-  // ---- pieces in record order: scalar run 0, payload 0, run 1, payload 1,
-  // ..., tail run.  Runs and payloads are cut into <=256-byte pieces.
-  uint32_t np = 0;
-  if (ok) {
-    uint32_t wcur = 0;
-#pragma unroll
-    for (int k = 0; k <= KMAX; ++k) {
-      if (static_cast<uint32_t>(k) > nslot) break;
-      const bool have = static_cast<uint32_t>(k) < nslot;
-      const uint32_t run_end = have ? pat[k < KMAX ? k : 0] : wpos;
-      np += (run_end - wcur + 63u) / 64u;
-      wcur = run_end;
-      if (!have) break;
-      np += (pln[k < KMAX ? k : 0] + kPieceBytes - 1u) / kPieceBytes;
-      wcur += (pln[k < KMAX ? k : 0] + 3u) >> 2;
-    }
-  }
-  uint32_t pincl = np;
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t x = __shfl_up(pincl, o, 64);
-    if (lane >= static_cast<uint32_t>(o)) pincl += x;
-  }
-  if (ok) {
-    uint32_t e = pincl - np;
-    const uint32_t rel = static_cast<uint32_t>(off - wave_out);
-    const uint32_t swbase = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(sw + lane * msw) -
-                                                  reinterpret_cast<uintptr_t>(sm));
-    uint32_t wcur = 0, scur = 0;
-#pragma unroll
-    for (int k = 0; k <= KMAX; ++k) {
-      if (static_cast<uint32_t>(k) > nslot) break;
-      const bool have = static_cast<uint32_t>(k) < nslot;
-      const int kk = k < KMAX ? k : 0;
-      const uint32_t run_end = have ? pat[kk] : wpos;
-      for (uint32_t q = wcur; q < run_end; q += 64u, ++e) {
-        pcs[e].src = swbase + 4u * (scur + (q - wcur));
-        pcs[e].dst = rel + 4u * q;
-        pcs[e].meta = (4u * min(64u, run_end - q)) | kFromLds;
-      }
-      scur += run_end - wcur;
-      wcur = run_end;
-      if (!have) break;
-      for (uint32_t q = 0; q * kPieceBytes < pln[kk]; ++q, ++e) {
-        pcs[e].src = psr[kk] + q * kPieceBytes;
-        pcs[e].dst = rel + 4u * wcur + q * kPieceBytes;
-        pcs[e].meta = min(kPieceBytes, pln[kk] - q * kPieceBytes);
-      }
-      wcur += (pln[kk] + 3u) >> 2;
-    }
-  }
-  const uint32_t M = __shfl(pincl, 63, 64);
-  __syncthreads();
-  // ---- copy: group g = lane >> 4 copies piece e0 + 4u + g, lane t = 16 B
-  const uint32_t g = lane >> 4, t16 = (lane & 15u) * 16u;
-  uint8_t *wout = xdr + wave_out;
-  for (uint32_t e0 = 0; e0 < M; e0 += 4u * kGroupBatch) {
-    u32x4 val[kGroupBatch];
-    uint32_t dst[kGroupBatch], nbo[kGroupBatch];
-#pragma unroll
-    for (int u = 0; u < kGroupBatch; ++u) {
-      const uint32_t pe = e0 + 4u * u + g;
-      val[u] = u32x4{0u, 0u, 0u, 0u};
-      nbo[u] = 0u;
-      dst[u] = 0u;
-      if (pe < M) {
-        const epiece pc = pcs[pe];
-        const uint32_t Lr = pc.meta & 0x1ffu;
-        if (t16 < Lr) {
-          dst[u] = pc.dst + t16;
-          nbo[u] = min(16u, ((Lr + 3u) & ~3u) - t16);
-          if (pc.meta & kFromLds) {
-            const uint32_t *ls = reinterpret_cast<const uint32_t *>(sm + pc.src + t16);
-            val[u].x = ls[0];
-            if (nbo[u] > 4u) val[u].y = ls[1];
-            if (nbo[u] > 8u) val[u].z = ls[2];
-            if (nbo[u] > 12u) val[u].w = ls[3];
-          } else {
-            const uint64_t hs = pc.src + t16;
-            u32x4 x;
-            if (hs + 16u <= heap_len) {
-              x = ld16u(heap + hs);
-            } else {
-              x = u32x4{unaligned_word(heap, heap_len, hs), unaligned_word(heap, heap_len, hs + 4),
-                        unaligned_word(heap, heap_len, hs + 8), unaligned_word(heap, heap_len, hs + 12)};
-            }
-            const int32_t rem = static_cast<int32_t>(Lr - t16);
-            if (rem < 16) {  // zero the pad bytes after the payload (put_bytes)
-              x.x &= keep_bytes(rem);
-              x.y &= keep_bytes(rem - 4);
-              x.z &= keep_bytes(rem - 8);
-              x.w &= keep_bytes(rem - 12);
-            }
-            val[u] = x;
-          }
-        }
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < kGroupBatch; ++u)
-      if (nbo[u]) st_words(wout + dst[u], val[u], nbo[u]);
-  }
-}
-
 template <int KMAX, int GB = kGroupBatch>
 __global__ __launch_bounds__(256) void k_var_decode_g(
     const uint8_t *__restrict__ xdr, uint64_t len, const uint64_t *__restrict__ offsets, uint64_t n,
@@ -1303,49 +1067,67 @@ __global__ __launch_bounds__(256) void k_var_decode_g(
   XDRG_STAMP_FLUSH(wr0 / 64u);
 }
 
-// -------------------------------------------- var: LDS-image kernels
-// One workgroup = one wave = 64 consecutive records, so each wave owns
-// its LDS.  Encode assembles the wave's whole output stretch in an LDS
-// image (scalar words written by their record's lane, payload pieces by
-// 16-lane groups with 16-byte heap loads), then stores it with aligned
-// 16-byte writes.  The image is phase-shifted so that image byte j sits at
-// LDS (j + (global & 15)): global and LDS 16-byte chunks coincide.  Decode
-// loads the wave's input stretch into an LDS window the same way, parses
-// every record from LDS, and copies payload pieces out to the heap.
-// Stretches larger than the image / window are processed in rounds.
-template <int K>
-__device__ __forceinline__ uint32_t pick(const uint32_t (&a)[K], uint32_t k) {
-  uint32_t v = a[0];
-#pragma unroll
-  for (int i = 1; i < K; ++i) v = (k == static_cast<uint32_t>(i)) ? a[i] : v;
-  return v;
+// -------------------------------------------- var: image encode (chunk map)
+// One workgroup = one wave = 64 consecutive records.  The wave's output
+// stretch [wave_out, wave_out + T) is assembled in an LDS image:
+//   * the lane-per-record walk of the plan (native fields from an LDS tile)
+//     writes each scalar wire word straight into the image;
+//   * payloads are cut into 16-byte chunks listed in a flat chunk map
+//     (u16: lane | slot | chunk), so every lane copies one chunk per step
+//     -- consecutive lanes take consecutive chunks of the same payload
+//     (coalesced heap reads) and no lane idles on a short record;
+//   * the image leaves with aligned 16-byte stores (image byte j sits at
+//     LDS j + (wave_out & 15), so LDS and global 16-byte chunks coincide).
+// Bytes past the image capacity C are written straight to global memory,
+// so a stretch of any size is handled in one pass.
+struct enc_i_lds {
+  uint32_t tile, desc, map, img, total;
+};
+__host__ __device__ inline enc_i_lds enc_i_layout(uint32_t stride, uint32_t KMAX, uint32_t MC,
+                                                 uint32_t C) {
+  enc_i_lds L;
+  L.tile = 0;
+  L.desc = (64u * stride + 15u) & ~15u;
+  L.map = L.desc + 64u * KMAX * 16u;
+  L.img = L.map + ((MC * 2u + 15u) & ~15u);
+  L.total = L.img + C + 32u;  // phase shift + the last (partial) chunk read
+  return L;
 }
 
-struct lpiece {  // 16 bytes
-  uint64_t src;   // encode: heap byte offset; decode: xdr byte offset
-  uint32_t dst;   // byte offset from the wave's stretch start
-  uint32_t meta;  // len (9 bits) | last piece (bit 31) | lane << 16 | op (decode: in tag)
+struct echunk_desc {  // 16 bytes: one payload slot of one lane
+  uint64_t src;       // heap byte offset
+  uint32_t dst;       // byte offset in the wave's stretch
+  uint32_t len;       // payload bytes
 };
 
-__host__ __device__ inline uint32_t encL_lds(uint32_t MSW, uint32_t PM, uint32_t C) {
-  return ((64u * (MSW ? MSW : 1u) * 4u + 15u) & ~15u) + 64u * (PM ? PM : 1u) * 16u + C + 16u;
+// Store word `v` at stretch offset `at`: image if it fits, else global.
+__device__ __forceinline__ void img_put(uint8_t *im, uint32_t C, uint8_t *gout, uint32_t at,
+                                        uint32_t v) {
+  if (at < C) *reinterpret_cast<uint32_t *>(im + at) = v;
+  else st32(gout + at, v);
 }
 
-template <int KMAX>
-__global__ __launch_bounds__(64) void k_var_encode_L(
+template <int KMAX, int U>
+__global__ __launch_bounds__(64) void k_var_encode_i(
     const uint8_t *__restrict__ native, uint64_t n, uint32_t stride, const uint8_t *__restrict__ heap,
     uint64_t heap_len, uint8_t *__restrict__ xdr, uint64_t cap, uint64_t *__restrict__ offsets,
     const uint32_t *__restrict__ sizes, const unsigned long long *__restrict__ block_base,
     const xdrg_op *__restrict__ ops, uint32_t nops, const uint32_t *__restrict__ table,
-    uint32_t stack_limit, uint32_t MSW, uint32_t PM, uint32_t C, unsigned long long *err) {
+    uint32_t stack_limit, uint32_t MC, uint32_t C, unsigned long long *err,
+    unsigned long long *stamps) {
   extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
+  unsigned long long stv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  XDRG_STAMP(0);
+  const enc_i_lds L = enc_i_layout(stride, KMAX, MC, C);
+  uint8_t *tile = sm + L.tile;
+  echunk_desc *desc = reinterpret_cast<echunk_desc *>(sm + L.desc);
+  uint16_t *map = reinterpret_cast<uint16_t *>(sm + L.map);
+  uint8_t *img = sm + L.img;
   const uint32_t lane = threadIdx.x;
-  const uint32_t msw = MSW ? MSW : 1u;
-  uint32_t *sw = reinterpret_cast<uint32_t *>(sm);
-  lpiece *pcs = reinterpret_cast<lpiece *>(sm + ((64u * msw * 4u + 15u) & ~15u));
-  uint8_t *img = reinterpret_cast<uint8_t *>(pcs + 64u * (PM ? PM : 1u));
+  const uint64_t wr0 = static_cast<uint64_t>(blockIdx.x) * 64u;
+  const uint64_t r = wr0 + lane;
 
-  const uint64_t r = static_cast<uint64_t>(blockIdx.x) * 64u + lane;
+  // ---- record offsets: wave scan of the sizes on top of the block base
   const uint32_t sz = r < n ? sizes[r] : 0u;
   const unsigned long long v = (sz & kSizeErr) ? 0ull : sz;
   unsigned long long incl = v;
@@ -1355,23 +1137,37 @@ __global__ __launch_bounds__(64) void k_var_encode_L(
   }
   const uint64_t off = block_base[blockIdx.x] + incl - v;
   const uint64_t wave_out = rl64(off, 0);
-  const uint64_t region = static_cast<uint64_t>(__shfl(incl, 63, 64));
+  const uint64_t T = rl64(incl, 63);  // bytes of the wave's stretch
   if (r < n) offsets[r] = off;
-
-  // ---- walk: native fields straight from global (lanes read adjacent records)
-  uint64_t psr[KMAX];
-  uint32_t pat[KMAX], pln[KMAX];
-#pragma unroll
-  for (int k = 0; k < KMAX; ++k) { psr[k] = 0; pat[k] = 0xffffffffu; pln[k] = 0; }
-  uint32_t nsw = 0, nslot = 0;
-  bool ok;
+  const uint32_t nrec = wr0 < n ? static_cast<uint32_t>(min<uint64_t>(64, n - wr0)) : 0u;
   {
-    const uint8_t *nat = native + r * stride;
-    uint32_t *mysw = sw + lane * msw;
-    uint32_t wpos = 0;
+    const uint32_t nbytes = nrec * stride;
+    const uint8_t *nsrc = native + wr0 * stride;
+    for (uint32_t i = lane; i < nbytes / 16u; i += 64u)
+      reinterpret_cast<u32x4 *>(tile)[i] = reinterpret_cast<const u32x4 *>(nsrc)[i];
+    for (uint32_t i = (nbytes / 16u) * 4u + lane; i < nbytes / 4u; i += 64u)
+      reinterpret_cast<uint32_t *>(tile)[i] = reinterpret_cast<const uint32_t *>(nsrc)[i];
+  }
+  __syncthreads();
+  XDRG_STAMP(1);
+
+  const uint32_t sh = static_cast<uint32_t>(wave_out & 15u);
+  uint8_t *im = img + sh;               // image byte j <-> global wave_out + j
+  uint8_t *gout = xdr + wave_out;       // direct path for j >= C
+  const uint32_t rel = static_cast<uint32_t>(off - wave_out);
+
+  // ---- walk: scalar words -> image, payload slots -> registers
+  uint64_t psr[KMAX];
+  uint32_t pds[KMAX], pln[KMAX];
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) { psr[k] = 0; pds[k] = 0; pln[k] = 0; }
+  uint32_t nslot = 0;
+  {
+    const uint8_t *nat = tile + lane * stride;
+    uint32_t at = rel;  // stretch offset of the next wire word
     uint64_t pos = off;
     uint32_t pc = (r < n && !(sz & kSizeErr)) ? 0u : kPcDone;
-    ok = pc == 0u;
+    bool ok = pc == 0u;
     for (uint32_t upc = 0; upc < nops; ++upc) {
       if (!__any(pc == upc)) continue;
       const xdrg_op op = ops[upc];
@@ -1391,153 +1187,138 @@ __global__ __launch_bounds__(64) void k_var_encode_L(
       if (need > cap - min(pos, cap)) { report(err, r, upc, XDRG_ERR_OVERFLOW_PUT); ok = false; pc = kPcDone; continue; }
       switch (op.kind) {
       case XDRG_OP_U32: case XDRG_OP_ENUM:
-        mysw[nsw++] = bswap32(nw[0]); pos += 4; ++wpos; ++pc; break;
+        img_put(im, C, gout, at, bswap32(nw[0])); at += 4; pos += 4; ++pc; break;
       case XDRG_OP_BOOL:
-        mysw[nsw++] = nat[op.noff] ? 0x01000000u : 0u; pos += 4; ++wpos; ++pc; break;
-      case XDRG_OP_U64: {
-        const uint32_t lo = nw[0], hi = nw[1];
-        mysw[nsw++] = bswap32(hi);
-        mysw[nsw++] = bswap32(lo);
-        pos += 8; wpos += 2; ++pc; break;
-      }
+        img_put(im, C, gout, at, nat[op.noff] ? 0x01000000u : 0u); at += 4; pos += 4; ++pc; break;
+      case XDRG_OP_U64:
+        img_put(im, C, gout, at, bswap32(nw[1]));
+        img_put(im, C, gout, at + 4, bswap32(nw[0]));
+        at += 8; pos += 8; ++pc; break;
       case XDRG_OP_OPAQUE: {
         const uint32_t BL = op.arg0, nwd = (BL + 3u) >> 2;
         for (uint32_t k = 0; k < nwd; ++k) {
           uint32_t w = 0;
           for (uint32_t bb = 0; bb < 4u && 4u * k + bb < BL; ++bb)
             w |= static_cast<uint32_t>(nat[op.noff + 4u * k + bb]) << (8u * bb);
-          mysw[nsw++] = w;
+          img_put(im, C, gout, at + 4u * k, w);
         }
-        pos += 4ull * nwd; wpos += nwd; ++pc; break;
+        at += 4u * nwd; pos += 4ull * nwd; ++pc; break;
       }
       case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
-        mysw[nsw++] = bswap32(blen);
-        ++wpos;
+        img_put(im, C, gout, at, bswap32(blen));
+        at += 4;
         if (blen) {
           const uint64_t hsrc = *reinterpret_cast<const uint64_t *>(nw);
 #pragma unroll
           for (int k = 0; k < KMAX; ++k)
-            if (static_cast<uint32_t>(k) == nslot) { psr[k] = hsrc; pat[k] = wpos; pln[k] = blen; }
+            if (static_cast<uint32_t>(k) == nslot) { psr[k] = hsrc; pds[k] = at; pln[k] = blen; }
           ++nslot;
         }
-        wpos += (blen + 3u) >> 2;
+        at += (blen + 3u) & ~3u;
         pos += 4ull + ((static_cast<uint64_t>(blen) + 3u) & ~3ull); ++pc; break;
       }
       case XDRG_OP_UNION: {
         const uint32_t d = nw[0];
-        mysw[nsw++] = bswap32(d);
-        pos += 4; ++wpos;
+        img_put(im, C, gout, at, bswap32(d));
+        at += 4; pos += 4;
         pc = static_cast<uint32_t>(union_target(op, table, d));  // validated by k_var_size
         break;
       }
       default: ++pc; break;
       }
     }
+    if (!ok) nslot = 0;  // a failing record's bytes are unspecified (never past `cap`)
   }
-  if (!ok) nslot = 0, nsw = 0;  // a failing record contributes no bytes (its range is unspecified)
+  XDRG_STAMP(2);
 
-  // ---- payload pieces (<=256 B), compacted in record order
-  const uint32_t rel = static_cast<uint32_t>(off - wave_out);
-  uint32_t np = 0;
+  // ---- chunk map: u16 lane << 10 | slot << 8 | chunk
+  uint32_t nch = 0;
 #pragma unroll
   for (int k = 0; k < KMAX; ++k)
-    if (static_cast<uint32_t>(k) < nslot) np += (pln[k] + kPieceBytes - 1u) / kPieceBytes;
-  uint32_t pincl = np;
+    if (static_cast<uint32_t>(k) < nslot) nch += (pln[k] + 15u) >> 4;
+  uint32_t cincl = nch;
   for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t x = __shfl_up(pincl, o, 64);
-    if (lane >= static_cast<uint32_t>(o)) pincl += x;
+    const uint32_t x = __shfl_up(cincl, o, 64);
+    if (lane >= static_cast<uint32_t>(o)) cincl += x;
   }
+  const uint32_t M = __shfl(cincl, 63, 64);
   {
-    uint32_t e = pincl - np;
+    uint32_t e = cincl - nch;
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
       if (static_cast<uint32_t>(k) >= nslot) break;
-      for (uint32_t q = 0; q * kPieceBytes < pln[k]; ++q, ++e) {
-        pcs[e].src = psr[k] + q * kPieceBytes;
-        pcs[e].dst = rel + 4u * pat[k] + q * kPieceBytes;
-        pcs[e].meta = min(kPieceBytes, pln[k] - q * kPieceBytes);
+      desc[lane * KMAX + k] = echunk_desc{psr[k], pds[k], pln[k]};
+      const uint32_t nq = (pln[k] + 15u) >> 4;
+      const uint32_t tag = (lane << 10) | (static_cast<uint32_t>(k) << 8);
+      for (uint32_t q = 0; q < nq; ++q) map[e + q] = static_cast<uint16_t>(tag | q);
+      e += nq;
+    }
+  }
+  __syncthreads();
+  XDRG_STAMP(3);
+
+  // ---- payload chunks: heap -> image, U chunks in flight per lane
+  for (uint32_t c0 = 0; c0 < M; c0 += 64u * U) {
+    u32x4 val[U];
+    uint32_t at[U], nb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t c = c0 + 64u * u + lane;
+      nb[u] = 0u;
+      at[u] = 0u;
+      val[u] = u32x4{0u, 0u, 0u, 0u};
+      if (c < M) {
+        const uint32_t m = map[c];
+        const echunk_desc d = desc[(m >> 10) * KMAX + ((m >> 8) & 3u)];
+        const uint32_t q16 = (m & 0xffu) << 4;
+        const uint64_t hs = d.src + q16;
+        u32x4 x;
+        if (hs + 16u <= heap_len) {
+          x = ld16u(heap + hs);
+        } else {
+          x = u32x4{unaligned_word(heap, heap_len, hs), unaligned_word(heap, heap_len, hs + 4),
+                    unaligned_word(heap, heap_len, hs + 8), unaligned_word(heap, heap_len, hs + 12)};
+        }
+        const int32_t rem = static_cast<int32_t>(d.len - q16);
+        if (rem < 16) {  // zero the pad bytes after the payload (put_bytes)
+          x.x &= keep_bytes(rem);
+          x.y &= keep_bytes(rem - 4);
+          x.z &= keep_bytes(rem - 8);
+          x.w &= keep_bytes(rem - 12);
+        }
+        val[u] = x;
+        at[u] = d.dst + q16;
+        nb[u] = min(16u, ((d.len + 3u) & ~3u) - q16);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (!nb[u]) continue;
+      if (at[u] + 16u <= C) {
+        uint32_t *w = reinterpret_cast<uint32_t *>(im + at[u]);
+        w[0] = val[u].x;
+        if (nb[u] > 4u) w[1] = val[u].y;
+        if (nb[u] > 8u) w[2] = val[u].z;
+        if (nb[u] > 12u) w[3] = val[u].w;
+      } else {
+        img_put(im, C, gout, at[u], val[u].x);
+        if (nb[u] > 4u) img_put(im, C, gout, at[u] + 4, val[u].y);
+        if (nb[u] > 8u) img_put(im, C, gout, at[u] + 8, val[u].z);
+        if (nb[u] > 12u) img_put(im, C, gout, at[u] + 12, val[u].w);
       }
     }
   }
-  const uint32_t M = __shfl(pincl, 63, 64);
   __syncthreads();
+  XDRG_STAMP(4);
 
-  const uint32_t g = lane >> 4, t16 = (lane & 15u) * 16u;
-  for (uint64_t base = 0; base < region; base += C) {
-    const uint32_t sh = static_cast<uint32_t>((wave_out + base) & 15u);
-    const uint32_t lim = static_cast<uint32_t>(min<uint64_t>(C, region - base));
-    uint8_t *im = img + sh;  // image byte j <-> global byte wave_out + base + j
-    // scalar words of this lane's record
-    {
-      uint32_t w = 0, k = 0;
-      uint32_t next = nslot ? pat[0] : 0xffffffffu;
-      for (uint32_t i = 0; i < nsw; ++i) {
-        while (w == next) {
-          w += (pick(pln, k) + 3u) >> 2;
-          ++k;
-          next = k < nslot ? pick(pat, k) : 0xffffffffu;
-        }
-        const int64_t at = static_cast<int64_t>(rel) + 4ll * w - static_cast<int64_t>(base);
-        if (at >= 0 && at < lim) *reinterpret_cast<uint32_t *>(im + at) = sw[lane * msw + i];
-        ++w;
-      }
-    }
-    // payload pieces
-    for (uint32_t e0 = 0; e0 < M; e0 += 4u * kGroupBatch) {
-      u32x4 val[kGroupBatch];
-      int64_t at[kGroupBatch];
-      uint32_t nbo[kGroupBatch];
-#pragma unroll
-      for (int u = 0; u < kGroupBatch; ++u) {
-        const uint32_t pe = e0 + 4u * u + g;
-        nbo[u] = 0u;
-        at[u] = 0;
-        val[u] = u32x4{0u, 0u, 0u, 0u};
-        if (pe < M) {
-          const lpiece pc = pcs[pe];
-          const uint32_t L = pc.meta & 0x1ffu;
-          at[u] = static_cast<int64_t>(pc.dst) + t16 - static_cast<int64_t>(base);
-          if (t16 < L && at[u] + 16 > 0 && at[u] < lim) {
-            nbo[u] = min(16u, ((L + 3u) & ~3u) - t16);
-            const uint64_t hs = pc.src + t16;
-            u32x4 x;
-            if (hs + 16u <= heap_len) {
-              x = ld16u(heap + hs);
-            } else {
-              x = u32x4{unaligned_word(heap, heap_len, hs), unaligned_word(heap, heap_len, hs + 4),
-                        unaligned_word(heap, heap_len, hs + 8), unaligned_word(heap, heap_len, hs + 12)};
-            }
-            const int32_t rem = static_cast<int32_t>(L - t16);
-            if (rem < 16) {  // zero pad bytes after the payload (put_bytes)
-              x.x &= keep_bytes(rem);
-              x.y &= keep_bytes(rem - 4);
-              x.z &= keep_bytes(rem - 8);
-              x.w &= keep_bytes(rem - 12);
-            }
-            val[u] = x;
-          }
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < kGroupBatch; ++u) {
-        if (!nbo[u]) continue;
-        const uint32_t xs[4] = {val[u].x, val[u].y, val[u].z, val[u].w};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int64_t a = at[u] + 4 * q;
-          if (static_cast<uint32_t>(4 * q) < nbo[u] && a >= 0 && a < lim)
-            *reinterpret_cast<uint32_t *>(im + a) = xs[q];
-        }
-      }
-    }
-    __syncthreads();
-    // image -> global: aligned 16-byte chunks, partial words at the edges
-    const uint64_t gs = wave_out + base;
-    const uint64_t ge = min<uint64_t>(gs + lim, cap);
+  // ---- image -> global: aligned 16-byte chunks, partial words at the edges
+  {
+    const uint64_t gs = wave_out;
+    const uint64_t ge = min<uint64_t>(gs + min<uint64_t>(T, C), cap);
     if (ge > gs) {
       const uint64_t c0 = gs & ~15ull;
-      const uint32_t nch = static_cast<uint32_t>((ge - c0 + 15u) >> 4);
-      for (uint32_t c = lane; c < nch; c += 64u) {
+      const uint32_t nc = static_cast<uint32_t>((ge - c0 + 15u) >> 4);
+      for (uint32_t c = lane; c < nc; c += 64u) {
         const uint64_t ca = c0 + 16ull * c;
         const uint8_t *lsrc = img + 16u * c;  // img + sh <-> gs, and gs - sh = c0
         if (ca >= gs && ca + 16u <= ge) {
@@ -1551,274 +1332,9 @@ __global__ __launch_bounds__(64) void k_var_encode_L(
         }
       }
     }
-    __syncthreads();
   }
-}
-
-__host__ __device__ inline uint32_t decL_lds(uint32_t stride, uint32_t PM, uint32_t C) {
-  return ((64u * stride + 15u) & ~15u) + 64u * (PM ? PM : 1u) * 16u + C + 16u;
-}
-
-// Parse one record (words read through `rd`), fields into the LDS native
-// tile, payload slots into registers.  Returns false on a reported error.
-template <int KMAX, typename RD>
-__device__ __forceinline__ void decode_walk(bool active, uint64_t r, uint64_t a, uint64_t b,
-                                            uint8_t *nat, const xdrg_op *__restrict__ ops,
-                                            uint32_t nops, const uint32_t *__restrict__ table,
-                                            uint32_t stack_limit, unsigned long long *err,
-                                            const RD &rd, uint64_t (&psr)[KMAX],
-                                            uint32_t (&pat)[KMAX], uint32_t (&pln)[KMAX],
-                                            uint32_t (&pop)[KMAX], uint32_t &nslot) {
-  uint64_t p = a, hcur = a;
-  uint32_t pc = active ? 0u : kPcDone;
-  bool ok = active;
-  for (uint32_t upc = 0; upc < nops; ++upc) {
-    if (!__any(pc == upc)) continue;
-    const xdrg_op op = ops[upc];
-    if (pc != upc) continue;
-    if (op.kind == XDRG_OP_END) { pc = kPcDone; continue; }
-    if (op.kind == XDRG_OP_JUMP) { pc = op.arg0; continue; }
-    if (op.depth > stack_limit) { report(err, r, upc, XDRG_ERR_STACK_GET); ok = false; pc = kPcDone; continue; }
-    const uint64_t rem = b - p;
-    uint32_t *nw = reinterpret_cast<uint32_t *>(nat + op.noff);
-    const uint32_t need = op.kind == XDRG_OP_U64 ? 8u : op.kind == XDRG_OP_OPAQUE ? op.arg0 : 4u;
-    if (rem < need) { report(err, r, upc, XDRG_ERR_OVERFLOW_GET); ok = false; pc = kPcDone; continue; }
-    switch (op.kind) {
-    case XDRG_OP_U32:
-      nw[0] = bswap32(rd(p)); p += 4; ++pc; break;
-    case XDRG_OP_ENUM: {
-      const uint32_t v = bswap32(rd(p));
-      nw[0] = v; p += 4; ++pc;
-      if ((op.flags & XDRG_F_VALIDATE) && !enum_ok(table, op.arg0, op.arg1, v)) {
-        report(err, r, upc, XDRG_ERR_INVALID_ENUM); ok = false; pc = kPcDone;
-      }
-      break;
-    }
-    case XDRG_OP_BOOL:
-      nat[op.noff] = rd(p) != 0u; p += 4; ++pc; break;
-    case XDRG_OP_U64: {
-      const uint32_t hi = rd(p), lo = rd(p + 4);
-      nw[1] = bswap32(hi);
-      nw[0] = bswap32(lo);
-      p += 8; ++pc; break;
-    }
-    case XDRG_OP_OPAQUE: {
-      const uint32_t BL = op.arg0;
-      for (uint32_t k = 0; k < BL; k += 4) {
-        const uint32_t w = rd(p + k);
-        for (uint32_t bb = 0; bb < 4u && k + bb < BL; ++bb) nat[op.noff + k + bb] = uint8_t(w >> (8 * bb));
-      }
-      ++pc;
-      if ((BL & 3u) && (rd(p + (BL & ~3u)) & ~keep_mask(BL & 3u))) {
-        report(err, r, upc, XDRG_ERR_NONZERO_PAD); ok = false; pc = kPcDone;
-      }
-      p += (BL + 3u) & ~3u;
-      break;
-    }
-    case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
-      const uint32_t BL = bswap32(rd(p));
-      p += 4;
-      if (BL > b - p) { report(err, r, upc, XDRG_ERR_OVERFLOW_GET); ok = false; pc = kPcDone; break; }
-      if (BL > op.arg0) {
-        report(err, r, upc, op.kind == XDRG_OP_STRING ? XDRG_ERR_XSTRING_BOUND : XDRG_ERR_XVECTOR_BOUND);
-        ok = false;
-        pc = kPcDone;
-        break;
-      }
-      const uint64_t padded = (static_cast<uint64_t>(BL) + 3u) & ~3ull;
-      if (BL) {
-#pragma unroll
-        for (int k = 0; k < KMAX; ++k)
-          if (static_cast<uint32_t>(k) == nslot) { psr[k] = p; pat[k] = static_cast<uint32_t>(hcur - a); pln[k] = BL; pop[k] = upc; }
-        ++nslot;
-      }
-      *reinterpret_cast<uint64_t *>(nat + op.noff) = hcur;
-      nw[2] = BL;
-      hcur += padded;
-      p += padded; ++pc;
-      break;
-    }
-    case XDRG_OP_UNION: {
-      const uint32_t d = bswap32(rd(p));
-      p += 4;
-      if ((op.flags & XDRG_F_VALIDATE) && !enum_ok(table, op.arg0, op.arg1, d)) {
-        report(err, r, upc, XDRG_ERR_INVALID_ENUM); ok = false; pc = kPcDone; break;
-      }
-      const int t = union_target(op, table, d);
-      if (t < 0) { report(err, r, upc, XDRG_ERR_BAD_DISCRIMINANT); ok = false; pc = kPcDone; break; }
-      nw[0] = d;
-      pc = static_cast<uint32_t>(t);
-      break;
-    }
-    default: ++pc; break;
-    }
-  }
-  if (ok && p != b) report(err, r, kOpRecordLevel, XDRG_ERR_TRAILING);
-}
-
-template <int KMAX>
-__global__ __launch_bounds__(64) void k_var_decode_L(
-    const uint8_t *__restrict__ xdr, uint64_t len, const uint64_t *__restrict__ offsets, uint64_t n,
-    uint8_t *__restrict__ native, uint32_t stride, uint8_t *__restrict__ heap,
-    const xdrg_op *__restrict__ ops, uint32_t nops, const uint32_t *__restrict__ table,
-    uint32_t stack_limit, uint32_t PM, uint32_t C, unsigned long long *err) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
-  const uint32_t lane = threadIdx.x;
-  const uint32_t tile_bytes = (64u * stride + 15u) & ~15u;
-  uint8_t *tile = sm;
-  lpiece *pcs = reinterpret_cast<lpiece *>(sm + tile_bytes);
-  uint8_t *win = reinterpret_cast<uint8_t *>(pcs + 64u * (PM ? PM : 1u));
-  const uint64_t wr0 = static_cast<uint64_t>(blockIdx.x) * 64u;
-  const uint32_t wn = static_cast<uint32_t>(min<uint64_t>(64, n - wr0));
-  const uint32_t nbytes = wn * stride;
-  for (uint32_t i = lane; i < (nbytes + 15u) / 16u; i += 64u)
-    reinterpret_cast<u32x4 *>(tile)[i] = u32x4{0u, 0u, 0u, 0u};
-
-  const uint64_t r = wr0 + lane;
-  uint64_t a = 0, b = 0;
-  bool todo = false;
-  if (r < n) {
-    a = offsets[r];
-    b = offsets[r + 1];
-    if (r == n - 1 && b != len) report(err, n, kOpRecordLevel, XDRG_ERR_TRAILING);
-    if (b < a || b > len) report(err, r, 0, XDRG_ERR_OVERFLOW_GET);
-    else if ((b - a) & 3u) report(err, r, kOpRecordLevel, XDRG_ERR_SIZE_NOT_MULT4);
-    else todo = true;
-  }
-  __syncthreads();  // tile zeroed
-
-  const uint32_t g = lane >> 4, t16 = (lane & 15u) * 16u;
-  for (;;) {
-    const unsigned long long pend = __ballot(todo);
-    if (!pend) break;
-    const uint32_t first = static_cast<uint32_t>(__builtin_ctzll(pend));
-    const uint64_t wbase = rl64(a, first);
-    // window end: the last pending record that still fits after wbase
-    const bool fits = todo && b - wbase <= C;
-    const unsigned long long fit = __ballot(fits);
-    uint64_t wend = 0;
-    if (fit) {
-      const uint32_t last = 63u - static_cast<uint32_t>(__builtin_clzll(fit));
-      wend = rl64(b, last);
-    }
-    const bool from_lds = fit != 0ull;
-    const uint32_t sh = static_cast<uint32_t>(wbase & 15u);
-    if (from_lds) {
-      // load [wbase, wend) into the window (16-byte chunks aligned to global)
-      const uint64_t c0 = wbase & ~15ull;
-      const uint32_t nch = static_cast<uint32_t>((wend - c0 + 15u) >> 4);
-      for (uint32_t c = lane; c < nch; c += 64u) {
-        const uint64_t ca = c0 + 16ull * c;
-        uint8_t *ldst = win + 16u * c;  // win + sh <-> wbase, and wbase - sh = c0
-        if (ca >= wbase && ca + 16u <= wend) {
-          *reinterpret_cast<u32x4 *>(ldst) = *reinterpret_cast<const u32x4 *>(xdr + ca);
-        } else {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const uint64_t wa = ca + 4u * q;
-            if (wa >= wbase && wa + 4u <= wend) *reinterpret_cast<uint32_t *>(ldst + 4 * q) = ld32(xdr + wa);
-          }
-        }
-      }
-      __syncthreads();
-    }
-    // this round's records: those inside the window, else the first one alone
-    const bool mine = from_lds ? fits : (todo && lane == first);
-    uint64_t psr[KMAX];
-    uint32_t pat[KMAX], pln[KMAX], pop[KMAX];
-#pragma unroll
-    for (int k = 0; k < KMAX; ++k) { psr[k] = 0; pat[k] = 0; pln[k] = 0; pop[k] = 0; }
-    uint32_t nslot = 0;
-    uint8_t *nat = tile + lane * stride;
-    if (from_lds) {
-      const uint8_t *wl = win + sh;
-      auto rd = [wl, wbase](uint64_t q) -> uint32_t {
-        return *reinterpret_cast<const uint32_t *>(wl + (q - wbase));
-      };
-      decode_walk<KMAX>(mine, r, a, b, nat, ops, nops, table, stack_limit, err, rd, psr, pat, pln, pop, nslot);
-    } else {
-      auto rd = [xdr](uint64_t q) -> uint32_t { return ld32(xdr + q); };
-      decode_walk<KMAX>(mine, r, a, b, nat, ops, nops, table, stack_limit, err, rd, psr, pat, pln, pop, nslot);
-    }
-    // pieces of this round (heap dst relative to wbase; src absolute xdr offset)
-    uint32_t np = 0;
-#pragma unroll
-    for (int k = 0; k < KMAX; ++k)
-      if (static_cast<uint32_t>(k) < nslot) np += (pln[k] + kPieceBytes - 1u) / kPieceBytes;
-    uint32_t pincl = np;
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t x = __shfl_up(pincl, o, 64);
-      if (lane >= static_cast<uint32_t>(o)) pincl += x;
-    }
-    {
-      uint32_t e = pincl - np;
-#pragma unroll
-      for (int k = 0; k < KMAX; ++k) {
-        if (static_cast<uint32_t>(k) >= nslot) break;
-        for (uint32_t q = 0; q * kPieceBytes < pln[k]; ++q, ++e) {
-          pcs[e].src = psr[k] + q * kPieceBytes;
-          pcs[e].dst = static_cast<uint32_t>(a - wbase) + pat[k] + q * kPieceBytes;
-          pcs[e].meta = min(kPieceBytes, pln[k] - q * kPieceBytes) |
-                        ((q + 1u) * kPieceBytes >= pln[k] ? kLastPiece : 0u) | (lane << 16);
-          pcs[e].src |= static_cast<uint64_t>(pop[k] & 0xffffu) << 48;  // op, for pad errors
-        }
-      }
-    }
-    const uint32_t M = __shfl(pincl, 63, 64);
-    __syncthreads();
-    for (uint32_t e0 = 0; e0 < M; e0 += 4u * kGroupBatch) {
-      u32x4 val[kGroupBatch];
-      uint32_t nbo[kGroupBatch];
-      uint64_t dst[kGroupBatch];
-#pragma unroll
-      for (int u = 0; u < kGroupBatch; ++u) {
-        const uint32_t pe = e0 + 4u * u + g;
-        nbo[u] = 0u;
-        dst[u] = 0u;
-        val[u] = u32x4{0u, 0u, 0u, 0u};
-        if (pe < M) {
-          const lpiece pc = pcs[pe];
-          const uint32_t L = pc.meta & 0x1ffu;
-          if (t16 < L) {
-            nbo[u] = min(16u, ((L + 3u) & ~3u) - t16);
-            dst[u] = wbase + pc.dst + t16;
-            const uint64_t s0 = (pc.src & 0xffffffffffffull) + t16;
-            if (from_lds) {
-              const uint32_t *ls = reinterpret_cast<const uint32_t *>(win + sh + (s0 - wbase));
-              val[u].x = ls[0];
-              if (nbo[u] > 4u) val[u].y = ls[1];
-              if (nbo[u] > 8u) val[u].z = ls[2];
-              if (nbo[u] > 12u) val[u].w = ls[3];
-            } else if (nbo[u] == 16u) {
-              val[u] = ld16u(xdr + s0);
-            } else {
-              val[u].x = ld32(xdr + s0);
-              if (nbo[u] > 4u) val[u].y = ld32(xdr + s0 + 4);
-              if (nbo[u] > 8u) val[u].z = ld32(xdr + s0 + 8);
-            }
-            const int32_t rem = static_cast<int32_t>(L - t16);
-            if (rem < 16 && (pc.meta & kLastPiece)) {  // get_bytes pad check
-              const u32x4 x = val[u];
-              if ((x.x & ~keep_bytes(rem)) | (x.y & ~keep_bytes(rem - 4)) | (x.z & ~keep_bytes(rem - 8)) |
-                  (x.w & ~keep_bytes(rem - 12)))
-                report(err, wr0 + ((pc.meta >> 16) & 63u), static_cast<uint32_t>(pc.src >> 48),
-                       XDRG_ERR_NONZERO_PAD);
-            }
-          }
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < kGroupBatch; ++u)
-        if (nbo[u]) st_words(heap + dst[u], val[u], nbo[u]);
-    }
-    if (mine) todo = false;
-    __syncthreads();  // window and pieces free for the next round
-  }
-  uint8_t *ndst = native + wr0 * stride;
-  for (uint32_t i = lane; i < nbytes / 16u; i += 64u)
-    reinterpret_cast<u32x4 *>(ndst)[i] = reinterpret_cast<const u32x4 *>(tile)[i];
-  for (uint32_t i = (nbytes / 16u) * 4u + lane; i < nbytes / 4u; i += 64u)
-    reinterpret_cast<uint32_t *>(ndst)[i] = reinterpret_cast<const uint32_t *>(tile)[i];
+  XDRG_STAMP(5);
+  XDRG_STAMP_FLUSH(blockIdx.x);
 }
 
 // ------------------------------------------------------------------ swaps
@@ -1836,8 +1352,11 @@ __global__ void k_swap64(const uint64_t *__restrict__ in, uint64_t *__restrict__
 // ------------------------------------------------------------------ host
 constexpr uint64_t kMallBytes = 256ull << 20;  // MI355X Infinity Cache
 constexpr uint32_t kVarLdsBudget = 64u << 10;  // wave-cooperative var kernels
-int g_var_kernel = 3;  // A/B (tools/tune): 0 LDS image, 1 record image, 2/3/4 group decode batch 4/8/16
-uint32_t g_img_bytes = 16u << 10;  // LDS image / window per wave (tuning)
+// Var-kernel choice: 0 = automatic (the fastest eligible kernel).  Forcing
+// (tools/tune A/B, tests): encode 1 = per-lane, 2 = record image,
+// 3 = chunk-map image; decode 1 = per-lane, 2 = record image, 3 = group copy.
+int g_force_enc = 0, g_force_dec = 0;
+uint32_t g_img_bytes = 4u << 10;  // encode LDS image per wave (tools/tune/ab_var.py)
 unsigned long long *g_stamps = nullptr;      // diagnostic phase stamps, decode (tuning)
 unsigned long long *g_stamps_enc = nullptr;  // diagnostic phase stamps, encode (tuning)
 
@@ -1959,11 +1478,10 @@ int xdrg_abi_version(void) { return XDRG_ABI_VERSION; }
 
 const char *xdrg_last_hip_error(void) { return g_hip_err; }
 
-// Internal A/B hook for tools/tune (not part of include/xdrgpu.h).
-int xdrg__select_var_kernel(int which) {
-  const int old = g_var_kernel;
-  g_var_kernel = which;
-  return old;
+// Internal A/B hooks for tools/tune and the tests (not part of include/xdrgpu.h).
+void xdrg__force_var_kernels(int enc, int dec) {
+  g_force_enc = enc;
+  g_force_dec = dec;
 }
 void xdrg__set_stamps(void *buf) { g_stamps = static_cast<unsigned long long *>(buf); }
 void xdrg__set_stamps_enc(void *buf) { g_stamps_enc = static_cast<unsigned long long *>(buf); }
@@ -2113,13 +1631,23 @@ int xdrg_encode(const xdrg_plan *p, const void *d_native, uint64_t n, const uint
   if (!d_ws || ws_bytes < need) return XDRG_ESPACE;
   uint32_t *sizes = reinterpret_cast<uint32_t *>(static_cast<char *>(d_ws) + so);
   unsigned long long *bsum = reinterpret_cast<unsigned long long *>(static_cast<char *>(d_ws) + bo);
-  // LDS-image path: 64-record workgroups (sizes scanned per 64 records)
-  const uint32_t Cimg = static_cast<uint32_t>(std::min<uint64_t>(
+  // chunk-map image encode (64-record workgroups); chunk map entries are
+  // u16 (lane 6 | slot 2 | chunk 8 bits)
+  const uint32_t MC = static_cast<uint32_t>(std::min<uint64_t>(64ull * p->max_chunks16, 1u << 20));
+  const uint32_t Ci = static_cast<uint32_t>(std::min<uint64_t>(
       g_img_bytes, (64ull * std::max<uint64_t>(p->max_record_bytes, 16) + 15u) & ~15ull));
-  const uint32_t lL = encL_lds(p->max_scalar_words, p->max_pieces, Cimg);
-  const bool use_L = g_var_kernel == 0 && lL <= kVarLdsBudget && p->max_var_slots <= 4 &&
-                     p->max_pieces <= 16 && p->max_scalar_words <= 256;
-  const uint32_t vb = use_L ? 64u : 256u;
+  const uint32_t KI = p->max_var_slots <= 1 ? 1u : p->max_var_slots <= 2 ? 2u : 4u;
+  const enc_i_lds LI = enc_i_layout(p->stride, KI, MC, Ci);
+  const bool ok_I = p->max_var_slots <= 4 && p->max_slot_len <= 4096u &&
+                    64ull * p->max_record_bytes < (1ull << 31) && LI.total <= kVarLdsBudget &&
+                    aligned(d_native, 16);
+  const enc_lds EL = enc_lds_layout(uint32_t(p->ops.size()), p->stride, p->max_scalar_words);
+  const bool ok_C = EL.total <= kVarLdsBudget && aligned(d_native, 16) && p->max_var_slots <= 4;
+  int kern = g_force_enc;
+  if (kern == 3 && !ok_I) kern = 0;
+  if (kern == 2 && !ok_C) kern = 0;
+  if (kern == 0) kern = ok_I ? 3 : ok_C ? 2 : 1;
+  const uint32_t vb = kern == 3 ? 64u : 256u;
   const uint64_t nb = (n + vb - 1) / vb;
   if (nb > 0xffffffffull) return XDRG_EUNSUPPORTED;
   const size_t lds_ops = p->ops.size() * sizeof(xdrg_op);
@@ -2129,49 +1657,34 @@ int xdrg_encode(const xdrg_plan *p, const void *d_native, uint64_t n, const uint
   HIPCHK(hipGetLastError());
   k_scan_blocks<<<1, 1024, 0, s>>>(bsum, uint32_t(nb), d_status, d_offsets, n);
   HIPCHK(hipGetLastError());
-  if (use_L) {
-#define LAUNCH_ENC_L(K)                                                                         \
-  k_var_encode_L<K><<<nb, 64, lL, s>>>(static_cast<const uint8_t *>(d_native), n, p->stride,   \
-                                       d_heap, heap_len, static_cast<uint8_t *>(d_xdr), cap,  \
-                                       d_offsets, sizes, bsum, p->d_ops,                      \
-                                       uint32_t(p->ops.size()), p->d_table, stack_limit,      \
-                                       p->max_scalar_words, p->max_pieces, Cimg, err)
-    if (p->max_var_slots <= 1) LAUNCH_ENC_L(1);
-    else if (p->max_var_slots <= 2) LAUNCH_ENC_L(2);
-    else LAUNCH_ENC_L(4);
-#undef LAUNCH_ENC_L
-    HIPCHK(hipGetLastError());
-    return XDRG_OK;
-  }
-  const uint32_t gl = 4u * enc_g_wave_bytes(p->stride, p->max_scalar_words, p->max_pieces,
-                                             p->max_var_slots);
-  const bool gfits = gl <= kVarLdsBudget && aligned(d_native, 16) && p->max_pieces <= 16;
-#define LAUNCH_ENC_G(K)                                                                         \
-  k_var_encode_g<K><<<nb, 256, gl, s>>>(                                                       \
-      static_cast<const uint8_t *>(d_native), n, p->stride, d_heap, heap_len,                 \
-      static_cast<uint8_t *>(d_xdr), cap, d_offsets, sizes, bsum, p->d_ops,                   \
-      uint32_t(p->ops.size()), p->d_table, stack_limit, p->max_pieces, p->max_scalar_words,   \
-      p->max_var_slots, err)
-  const enc_lds EL = enc_lds_layout(uint32_t(p->ops.size()), p->stride, p->max_scalar_words);
-  const bool fits = EL.total <= kVarLdsBudget && aligned(d_native, 16);
-  if (g_var_kernel == 2 && gfits && p->max_var_slots <= 2) LAUNCH_ENC_G(2);
-  else if (g_var_kernel == 2 && gfits && p->max_var_slots <= 4) LAUNCH_ENC_G(4);
-  else
-#define LAUNCH_ENC_C(K)                                                                         \
-  k_var_encode_c<K><<<nb, 256, EL.total, s>>>(                                                 \
-      static_cast<const uint8_t *>(d_native), n, p->stride, d_heap, heap_len,                 \
-      static_cast<uint8_t *>(d_xdr), cap, d_offsets, sizes, bsum, p->d_ops,                   \
-      uint32_t(p->ops.size()), p->d_table, stack_limit, p->max_scalar_words, err, g_stamps_enc)
-  if (fits && p->max_var_slots <= 1) LAUNCH_ENC_C(1);
-  else if (fits && p->max_var_slots <= 2) LAUNCH_ENC_C(2);
-  else if (fits && p->max_var_slots <= 4) LAUNCH_ENC_C(4);
-  else
-    k_var_encode<<<nb, 256, lds_ops, s>>>(static_cast<const uint8_t *>(d_native), n, p->stride,
-                                          d_heap, heap_len, static_cast<uint8_t *>(d_xdr), cap,
-                                          d_offsets, sizes, bsum, p->d_ops,
-                                          uint32_t(p->ops.size()), p->d_table, stack_limit, err);
+  const uint8_t *nat8 = static_cast<const uint8_t *>(d_native);
+  uint8_t *xdr8 = static_cast<uint8_t *>(d_xdr);
+  const uint32_t nops = uint32_t(p->ops.size());
+  if (kern == 3) {
+#define LAUNCH_ENC_I(K)                                                                        \
+  k_var_encode_i<K, 16><<<nb, 64, LI.total, s>>>(nat8, n, p->stride, d_heap, heap_len, xdr8,  \
+                                                 cap, d_offsets, sizes, bsum, p->d_ops, nops, \
+                                                 p->d_table, stack_limit, MC, Ci, err,        \
+                                                 g_stamps_enc)
+    if (KI == 1) LAUNCH_ENC_I(1);
+    else if (KI == 2) LAUNCH_ENC_I(2);
+    else LAUNCH_ENC_I(4);
+#undef LAUNCH_ENC_I
+  } else if (kern == 2) {
+#define LAUNCH_ENC_C(K)                                                                        \
+  k_var_encode_c<K><<<nb, 256, EL.total, s>>>(nat8, n, p->stride, d_heap, heap_len, xdr8, cap, \
+                                              d_offsets, sizes, bsum, p->d_ops, nops,          \
+                                              p->d_table, stack_limit, p->max_scalar_words,   \
+                                              err, g_stamps_enc)
+    if (p->max_var_slots <= 1) LAUNCH_ENC_C(1);
+    else if (p->max_var_slots <= 2) LAUNCH_ENC_C(2);
+    else LAUNCH_ENC_C(4);
 #undef LAUNCH_ENC_C
-#undef LAUNCH_ENC_G
+  } else {
+    k_var_encode<<<nb, 256, lds_ops, s>>>(nat8, n, p->stride, d_heap, heap_len, xdr8, cap,
+                                          d_offsets, sizes, bsum, p->d_ops, nops, p->d_table,
+                                          stack_limit, err);
+  }
   HIPCHK(hipGetLastError());
   return XDRG_OK;
 }
@@ -2215,63 +1728,40 @@ int xdrg_decode(const xdrg_plan *p, const void *d_xdr, uint64_t len, const uint6
   if (heap_cap < len || (len && !d_heap_out)) return XDRG_ESPACE;
   if (!aligned(d_xdr, 4) || !aligned(d_native, 8) || (d_heap_out && !aligned(d_heap_out, 4)))
     return XDRG_EALIGN;
-  const uint32_t Cwin = static_cast<uint32_t>(std::min<uint64_t>(
-      g_img_bytes, (64ull * std::max<uint64_t>(p->max_record_bytes, 16) + 15u) & ~15ull));
-  const uint32_t dL = decL_lds(p->stride, p->max_pieces, Cwin);
-  if (g_var_kernel == 0 && dL <= kVarLdsBudget && p->max_var_slots <= 4 && p->max_pieces <= 16 &&
-      aligned(d_native, 16)) {
-    const uint64_t nb64 = (n + 63) / 64;
-#define LAUNCH_DEC_L(K)                                                                        \
-  k_var_decode_L<K><<<nb64, 64, dL, s>>>(static_cast<const uint8_t *>(d_xdr), len, d_offsets, n, \
-                                         static_cast<uint8_t *>(d_native), p->stride, d_heap_out, \
-                                         p->d_ops, uint32_t(p->ops.size()), p->d_table,         \
-                                         stack_limit, p->max_pieces, Cwin, err)
-    if (p->max_var_slots <= 1) LAUNCH_DEC_L(1);
-    else if (p->max_var_slots <= 2) LAUNCH_DEC_L(2);
-    else LAUNCH_DEC_L(4);
-#undef LAUNCH_DEC_L
-    HIPCHK(hipGetLastError());
-    return XDRG_OK;
-  }
   const uint64_t nb = (n + 255) / 256;
   const size_t lds_ops = p->ops.size() * sizeof(xdrg_op);
   const size_t dl = 4u * ((64u * p->stride + 15u) & ~15u);
-  const bool fits = dl <= kVarLdsBudget && aligned(d_native, 16);
+  const bool ok_C = dl <= kVarLdsBudget && aligned(d_native, 16) && p->max_var_slots <= 4;
   const uint32_t gl = 4u * (((64u * p->stride + 15u) & ~15u) + piece_wave_bytes(p->max_pieces));
-  const bool gfits = gl <= kVarLdsBudget && aligned(d_native, 16) && p->max_pieces <= 16;
-#define LAUNCH_DEC_G2(K, B)                                                                    \
-  k_var_decode_g<K, B><<<nb, 256, gl, s>>>(static_cast<const uint8_t *>(d_xdr), len, d_offsets, n, \
-                                        static_cast<uint8_t *>(d_native), p->stride, d_heap_out, \
-                                        p->d_ops, uint32_t(p->ops.size()), p->d_table,         \
-                                        stack_limit, p->max_pieces, err, g_stamps)
+  const bool ok_G = gl <= kVarLdsBudget && aligned(d_native, 16) && p->max_pieces <= 16 &&
+                    p->max_var_slots <= 4;
+  int kern = g_force_dec;
+  if (kern == 3 && !ok_G) kern = 0;
+  if (kern == 2 && !ok_C) kern = 0;
+  if (kern == 0) kern = ok_G ? 3 : ok_C ? 2 : 1;
+  const uint8_t *xdr8 = static_cast<const uint8_t *>(d_xdr);
+  uint8_t *nat8 = static_cast<uint8_t *>(d_native);
+  const uint32_t nops = uint32_t(p->ops.size());
+  if (kern == 3) {
 #define LAUNCH_DEC_G(K)                                                                        \
-  k_var_decode_g<K><<<nb, 256, gl, s>>>(static_cast<const uint8_t *>(d_xdr), len, d_offsets, n, \
-                                        static_cast<uint8_t *>(d_native), p->stride, d_heap_out, \
-                                        p->d_ops, uint32_t(p->ops.size()), p->d_table,         \
-                                        stack_limit, p->max_pieces, err, g_stamps)
-  if (g_var_kernel == 2 && gfits && p->max_var_slots <= 2) LAUNCH_DEC_G(2);
-  else if (g_var_kernel == 2 && gfits && p->max_var_slots <= 4) LAUNCH_DEC_G(4);
-  else if (g_var_kernel == 3 && gfits && p->max_var_slots <= 2) LAUNCH_DEC_G2(2, 8);
-  else if (g_var_kernel == 3 && gfits && p->max_var_slots <= 4) LAUNCH_DEC_G2(4, 8);
-  else if (g_var_kernel == 4 && gfits && p->max_var_slots <= 2) LAUNCH_DEC_G2(2, 16);
-  else if (g_var_kernel == 4 && gfits && p->max_var_slots <= 4) LAUNCH_DEC_G2(4, 16);
-  else
-#define LAUNCH_DEC_C(K)                                                                        \
-  k_var_decode_c<K><<<nb, 256, dl, s>>>(static_cast<const uint8_t *>(d_xdr), len, d_offsets, n, \
-                                        static_cast<uint8_t *>(d_native), p->stride, d_heap_out, \
-                                        p->d_ops, uint32_t(p->ops.size()), p->d_table,         \
-                                        stack_limit, err)
-  if (fits && p->max_var_slots <= 1) LAUNCH_DEC_C(1);
-  else if (fits && p->max_var_slots <= 2) LAUNCH_DEC_C(2);
-  else if (fits && p->max_var_slots <= 4) LAUNCH_DEC_C(4);
-  else
-    k_var_decode<<<nb, 256, lds_ops, s>>>(static_cast<const uint8_t *>(d_xdr), len, d_offsets, n,
-                                          static_cast<uint8_t *>(d_native), p->stride, d_heap_out,
-                                          p->d_ops, uint32_t(p->ops.size()), p->d_table,
-                                          stack_limit, err);
-#undef LAUNCH_DEC_C
+  k_var_decode_g<K, 8><<<nb, 256, gl, s>>>(xdr8, len, d_offsets, n, nat8, p->stride, d_heap_out, \
+                                           p->d_ops, nops, p->d_table, stack_limit,            \
+                                           p->max_pieces, err, g_stamps)
+    if (p->max_var_slots <= 2) LAUNCH_DEC_G(2);
+    else LAUNCH_DEC_G(4);
 #undef LAUNCH_DEC_G
-#undef LAUNCH_DEC_G2
+  } else if (kern == 2) {
+#define LAUNCH_DEC_C(K)                                                                        \
+  k_var_decode_c<K><<<nb, 256, dl, s>>>(xdr8, len, d_offsets, n, nat8, p->stride, d_heap_out, \
+                                        p->d_ops, nops, p->d_table, stack_limit, err)
+    if (p->max_var_slots <= 1) LAUNCH_DEC_C(1);
+    else if (p->max_var_slots <= 2) LAUNCH_DEC_C(2);
+    else LAUNCH_DEC_C(4);
+#undef LAUNCH_DEC_C
+  } else {
+    k_var_decode<<<nb, 256, lds_ops, s>>>(xdr8, len, d_offsets, n, nat8, p->stride, d_heap_out,
+                                          p->d_ops, nops, p->d_table, stack_limit, err);
+  }
   HIPCHK(hipGetLastError());
   return XDRG_OK;
 }
