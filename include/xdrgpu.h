@@ -240,9 +240,12 @@ int xdrg_encode(const xdrg_plan *plan, const void *d_native, uint64_t n,
  *   exactly as xdr_from_opaque(bytes, r0, ..., rn-1) would.
  * Var plans: d_offsets (n+1 entries, from the encoder or from RPC record
  *   framing) is required; record i is decoded from [off[i], off[i+1]) with
- *   the semantics of xdr_from_opaque on that slice.  Var-length payloads are
- *   written to d_heap_out (at least xdr_len bytes): record i's payloads go
- *   to the heap range [off[i], off[i+1]), each field 4-byte aligned.
+ *   the semantics of xdr_from_opaque on that slice.  The decoded heap is
+ *   the stream itself: d_heap_out (at least xdr_len bytes) receives the
+ *   stream bytes verbatim, and every decoded xdrg_bytes_ref holds the stream
+ *   offset of its payload (so payloads are never gathered one by one).
+ *   Passing d_heap_out == d_xdr decodes without copying: the refs then
+ *   point into the input stream, which must outlive the decoded records.
  */
 int xdrg_decode(const xdrg_plan *plan, const void *d_xdr, uint64_t xdr_len,
                 const uint64_t *d_offsets, uint64_t n, void *d_native,

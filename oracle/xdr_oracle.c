@@ -194,9 +194,11 @@ int xdro_sizes(const xdrg_op *ops, uint32_t nops, const uint32_t *table, uint32_
 
 /* ---------------------------------------------------------------- decode */
 /* Decode one record from [p, e); returns 0 or an error code (op in *eop).
- * *pp is advanced.  Native record is zero-filled first. */
+ * *pp is advanced.  Native record is zero-filled first.  A payload's
+ * xdrg_bytes_ref holds its byte offset in the stream (`base`): the decoded
+ * heap is the stream itself (xdro_decode copies it to heap_out). */
 static int dec_record(const plan_t *P, const uint8_t **pp, const uint8_t *e, uint8_t *nat,
-                      uint8_t *heap_out, uint64_t *hcur, uint32_t stack_limit, uint32_t *eop) {
+                      const uint8_t *base, uint32_t stack_limit, uint32_t *eop) {
   const uint8_t *p = *pp;
   uint32_t pc = 0;
   memset(nat, 0, P->stride);
@@ -243,13 +245,11 @@ static int dec_record(const plan_t *P, const uint8_t **pp, const uint8_t *e, uin
         *eop = pc; *pp = p;
         return op->kind == XDRG_OP_STRING ? XDRG_ERR_XSTRING_BOUND : XDRG_ERR_XVECTOR_BOUND;
       }
-      xdrg_bytes_ref ref = {*hcur, len, 0};
+      xdrg_bytes_ref ref = {(uint64_t)(p - base), len, 0};
       if (len) {
-        memcpy(heap_out + *hcur, p, pad4(len)); /* payload + (verified zero) pad */
         p += len;
         for (uint64_t k = len; k & 3; ++k)
           if (*p++ != 0) { *eop = pc; *pp = p; return XDRG_ERR_NONZERO_PAD; }
-        *hcur += pad4(len);
       }
       memcpy(nat + op->noff, &ref, sizeof ref);
       ++pc; break;
@@ -277,19 +277,20 @@ static int dec_record(const plan_t *P, const uint8_t **pp, const uint8_t *e, uin
  * Fixed or indexed batch decode (see xdrg_decode in include/xdrgpu.h for the
  * contract).  offsets == NULL: one xdr_generic_get over [xdr, xdr+len) for n
  * records, then done().  offsets != NULL: record r is xdr_from_opaque of the
- * slice [off[r], off[r+1]); heap output for record r starts at off[r].
+ * slice [off[r], off[r+1]).  heap_out (if given) receives the stream
+ * verbatim; every decoded xdrg_bytes_ref points at its payload in it.
  */
 int xdro_decode(const xdrg_op *ops, uint32_t nops, const uint32_t *table, uint32_t stride,
                 const uint8_t *xdr, uint64_t len, const uint64_t *offsets, uint64_t n,
                 uint8_t *native, uint8_t *heap_out, uint32_t stack_limit, uint64_t *erec,
                 uint32_t *eop) {
   plan_t P = {ops, nops, table, stride};
+  if (heap_out && len) memcpy(heap_out, xdr, len);
   if (!offsets) {
     if (len & 3) { *erec = 0; *eop = 0xffffffffu; return XDRG_ERR_SIZE_NOT_MULT4; }
     const uint8_t *p = xdr, *e = xdr + len;
-    uint64_t hcur = 0;
     for (uint64_t r = 0; r < n; ++r) {
-      int rc = dec_record(&P, &p, e, native + r * stride, heap_out, &hcur, stack_limit, eop);
+      int rc = dec_record(&P, &p, e, native + r * stride, xdr, stack_limit, eop);
       if (rc) { *erec = r; return rc; }
     }
     if (p != e) { *erec = n; *eop = 0xffffffffu; return XDRG_ERR_TRAILING; }
@@ -300,8 +301,7 @@ int xdro_decode(const xdrg_op *ops, uint32_t nops, const uint32_t *table, uint32
     if (b < a || b > len) { *erec = r; *eop = 0; return XDRG_ERR_OVERFLOW_GET; }
     if ((b - a) & 3) { *erec = r; *eop = 0xffffffffu; return XDRG_ERR_SIZE_NOT_MULT4; }
     const uint8_t *p = xdr + a, *e = xdr + b;
-    uint64_t hcur = a;
-    int rc = dec_record(&P, &p, e, native + r * stride, heap_out, &hcur, stack_limit, eop);
+    int rc = dec_record(&P, &p, e, native + r * stride, xdr, stack_limit, eop);
     if (rc) { *erec = r; return rc; }
     if (p != e) { *erec = r; *eop = 0xffffffffu; return XDRG_ERR_TRAILING; }
   }

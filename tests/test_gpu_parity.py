@@ -327,7 +327,7 @@ def test_swaps(dev):
 
 
 # ------------------------------------- every var kernel, forced in turn
-KERNELS = {"per_lane": (1, 1), "record_image": (2, 2), "chunk_image_group": (3, 3)}
+KERNELS = {"per_lane": (1, 1), "record_image_window": (2, 2), "chunk_image_window": (3, 2)}
 
 
 @pytest.fixture(params=list(KERNELS))

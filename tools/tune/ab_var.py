@@ -15,16 +15,18 @@ from xdrpp_amd import _abi as A, marshal as M, schemas as S, workloads as W  # n
 L = A.lib()
 L.xdrg__force_var_kernels.argtypes = [C.c_int, C.c_int]
 L.xdrg__set_image_bytes.argtypes = [C.c_int]
-# (encode kernel, decode kernel, encode LDS image bytes); kernels as in
-# xdrgpu.hip g_force_enc/g_force_dec: 0 auto, 1 per-lane, 2 record image,
-# 3 chunk-map image (encode) / group copy (decode)
+L.xdrg__set_window_bytes.argtypes = [C.c_int]
+# (encode kernel, decode kernel, encode LDS image bytes, decode LDS window
+# bytes); kernels as in xdrgpu.hip g_force_enc/g_force_dec: 0 auto,
+# 1 per-lane, 2 record image, 3 chunk-map image (encode) / 2 window (decode)
 VARIANTS = [tuple(int(x) for x in v.split(",")) for v in
-            os.environ.get("VARIANTS", "2,3,16384 3,3,4096 3,3,0 3,3,8192").split()]
+            os.environ.get("VARIANTS", "2,2,4096,4096 3,2,4096,4096 3,2,2048,4096 3,2,0,4096 3,2,4096,2048").split()]
 
 
 def select(v):
     L.xdrg__force_var_kernels(v[0], v[1])
     L.xdrg__set_image_bytes(v[2])
+    L.xdrg__set_window_bytes(v[3])
 dev = torch.device("cuda:0")
 out = {}
 for schema in sys.argv[1:] or ["recvar", "rpc"]:
@@ -69,10 +71,10 @@ for schema in sys.argv[1:] or ["recvar", "rpc"]:
             torch.cuda.synchronize()
             times[v][0].append(ev[0].elapsed_time(ev[1]) / 5)
             times[v][1].append(ev[1].elapsed_time(ev[2]) / 5)
-    select((0, 0, 4096))
+    select((0, 0, 4096, 16384))
     mar.check()
     for v in VARIANTS:
-        name = f"e{v[0]}d{v[1]}_{v[2] // 1024}K"
+        name = f"e{v[0]}d{v[1]}_i{v[2] // 1024}K_w{v[3] // 1024}K"
         e, d = float(np.median(times[v][0])), float(np.median(times[v][1]))
         out[f"{schema}_{name}"] = {"encode_ms": round(e, 4), "decode_ms": round(d, 4),
                                    "gib_s": round(2 * total / 2**30 / ((e + d) * 1e-3), 1)}

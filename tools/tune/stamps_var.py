@@ -19,10 +19,11 @@ L = A.lib()
 L.xdrg__force_var_kernels.argtypes = [C.c_int, C.c_int]
 L.xdrg__set_stamps.argtypes = [C.c_void_p]
 L.xdrg__set_stamps_enc.argtypes = [C.c_void_p]
+L.xdrg__set_window_bytes.argtypes = [C.c_int]
 dev = torch.device("cuda:0")
 ENC = (["sizes+scan", "tile load+barrier", "walk", "emit", "-"]
-       if os.environ.get("VENC", "0") == "2" else ["prologue+tile", "walk", "chunk map", "chunk copy", "image out"])
-DEC = ["tile zero+barrier", "walk (parse)", "pieces+barrier", "piece copy", "tile out"]
+       if os.environ.get("VENC", "0") == "2" else ["tile+size pass", "look-back", "walk", "chunk map+copy", "image out"])
+DEC = ["window load+copy", "walk (parse)", "tile out", "-", "-"]
 
 
 def report(tag, st, nwaves, names):
@@ -49,6 +50,7 @@ for schema in sys.argv[1:] or ["recvar"]:
     back = torch.empty_like(nat)
     hout = torch.empty(total, dtype=torch.uint8, device=dev)
     L.xdrg__force_var_kernels(int(os.environ.get('VENC', '0')), int(os.environ.get('VDEC', '0')))
+    L.xdrg__set_window_bytes(int(os.environ.get('WIN', '8192')))
     mar.status.init(torch.cuda.current_stream().cuda_stream)
     nwaves = (n + 63) // 64
     se = torch.zeros(nwaves * 8, dtype=torch.int64, device=dev)

@@ -96,6 +96,14 @@ __device__ __forceinline__ void load_ops(xdrg_op *sops, const xdrg_op *__restric
   __syncthreads();
 }
 
+// Unaligned 16-byte global access: correct at any byte alignment on gfx950
+// (tools/probe/unaligned.hip).
+__device__ __forceinline__ u32x4 ld16u(const uint8_t *p) { return *reinterpret_cast<const u32x4 *>(p); }
+__device__ __forceinline__ void st16u(uint8_t *p, u32x4 v) { *reinterpret_cast<u32x4 *>(p) = v; }
+__device__ __forceinline__ uint32_t keep_bytes(int32_t k) {  // mask of the low k bytes, k clamped
+  return k <= 0 ? 0u : k >= 4 ? 0xffffffffu : ((1u << (8 * k)) - 1u);
+}
+
 constexpr uint32_t kSizeErr = 0x80000000u;
 
 // -------------------------------------------------------- var: size pass
@@ -127,15 +135,36 @@ constexpr uint32_t kPcDone = 0xffffffffu;
       for (int q_ = 0; q_ < 8; ++q_) stamps[(wave_id) * 8 + q_] = stv[q_];         \
   } while (0)
 
-__global__ __launch_bounds__(256) void k_var_size(const uint8_t *__restrict__ native, uint64_t n,
-                                                  uint32_t stride, const xdrg_op *__restrict__ ops,
-                                                  uint32_t nops, const uint32_t *__restrict__ table,
-                                                  uint32_t *__restrict__ sizes,
-                                                  unsigned long long *__restrict__ block_sums,
-                                                  unsigned long long *err) {
-  __shared__ unsigned long long wsum[4];
-  const uint64_t r = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  const uint8_t *nat = native + r * stride;
+// One 64-thread workgroup = 64 consecutive records.  The native records are
+// staged in LDS with coalesced 16-byte loads, so the walk reads fields from
+// LDS instead of issuing one dependent global load per op.
+template <bool TILE>
+__global__ __launch_bounds__(64) void k_var_size(const uint8_t *__restrict__ native, uint64_t n,
+                                                 uint32_t stride, const xdrg_op *__restrict__ ops,
+                                                 uint32_t nops, const uint32_t *__restrict__ table,
+                                                 uint32_t *__restrict__ sizes,
+                                                 unsigned long long *__restrict__ block_sums,
+                                                 unsigned long long *err) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t tile[];
+  const uint32_t lane = threadIdx.x;
+  const uint64_t wr0 = static_cast<uint64_t>(blockIdx.x) * 64u;
+  const uint64_t r = wr0 + lane;
+  const uint32_t nrec = static_cast<uint32_t>(min<uint64_t>(64, n - wr0));
+  if (TILE) {
+    const uint32_t nbytes = nrec * stride;
+    const uint8_t *nsrc = native + wr0 * stride;
+    if ((reinterpret_cast<uintptr_t>(nsrc) & 15u) == 0) {
+      for (uint32_t i = lane; i < nbytes / 16u; i += 64u)
+        reinterpret_cast<u32x4 *>(tile)[i] = reinterpret_cast<const u32x4 *>(nsrc)[i];
+      for (uint32_t i = (nbytes / 16u) * 4u + lane; i < nbytes / 4u; i += 64u)
+        reinterpret_cast<uint32_t *>(tile)[i] = reinterpret_cast<const uint32_t *>(nsrc)[i];
+    } else {
+      for (uint32_t i = lane; i < nbytes / 4u; i += 64u)
+        reinterpret_cast<uint32_t *>(tile)[i] = reinterpret_cast<const uint32_t *>(nsrc)[i];
+    }
+  }
+  __syncthreads();
+  const uint8_t *nat = TILE ? tile + lane * stride : native + r * stride;
   uint64_t s = 0;
   uint32_t pc = r < n ? 0u : kPcDone, bad_op = kPcDone;
   for (uint32_t upc = 0; upc < nops; ++upc) {
@@ -148,11 +177,11 @@ __global__ __launch_bounds__(256) void k_var_size(const uint8_t *__restrict__ na
     case XDRG_OP_U64: s += 8; ++pc; break;
     case XDRG_OP_OPAQUE: s += (op.arg0 + 3u) & ~3u; ++pc; break;
     case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING:
-      s += 4u + ((static_cast<uint64_t>(ld32(nat + op.noff + 8)) + 3u) & ~3ull);
+      s += 4u + ((static_cast<uint64_t>(*reinterpret_cast<const uint32_t *>(nat + op.noff + 8)) + 3u) & ~3ull);
       ++pc;
       break;
     case XDRG_OP_UNION: {
-      const int t = union_target(op, table, ld32(nat + op.noff));
+      const int t = union_target(op, table, *reinterpret_cast<const uint32_t *>(nat + op.noff));
       s += 4;
       if (t < 0) { bad_op = upc; pc = kPcDone; }
       else pc = static_cast<uint32_t>(t);
@@ -174,45 +203,54 @@ __global__ __launch_bounds__(256) void k_var_size(const uint8_t *__restrict__ na
     }
     sizes[r] = size;
   }
-  // block sum of the valid sizes
   unsigned long long v = (size & kSizeErr) ? 0ull : size;
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
-  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = v;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned long long t = 0;
-    for (uint32_t w = 0; w < (blockDim.x + 63) / 64; ++w) t += wsum[w];
-    block_sums[blockIdx.x] = t;
-  }
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if (block_sums && lane == 0) block_sums[blockIdx.x] = v;
 }
 
-// Exclusive scan of nb block sums in place; writes the total.
+// Exclusive scan of nb block sums in place; writes the total.  Tiles of
+// 16 x 1024 values: every thread loads its 16 contiguous values with
+// independent loads (one round trip per tile), scans them, and the block
+// scans the thread totals.
 __global__ __launch_bounds__(1024) void k_scan_blocks(unsigned long long *__restrict__ v,
                                                       uint32_t nb, xdrg_status *status,
                                                       uint64_t *__restrict__ offsets, uint64_t n) {
-  __shared__ unsigned long long part[1024];
-  const uint32_t tid = threadIdx.x;
-  const uint32_t per = (nb + 1023u) / 1024u;
-  const uint32_t a = min(nb, tid * per), b = min(nb, a + per);
-  unsigned long long s = 0;
-  for (uint32_t i = a; i < b; ++i) s += v[i];
-  part[tid] = s;
-  __syncthreads();
-  for (uint32_t o = 1; o < 1024; o <<= 1) {
-    unsigned long long x = tid >= o ? part[tid - o] : 0ull;
+  constexpr uint32_t PER = 16;
+  __shared__ unsigned long long wtot[16];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  unsigned long long carry = 0;
+  for (uint64_t t0 = 0; t0 < nb; t0 += 1024ull * PER) {
+    unsigned long long x[PER];
+    const uint64_t b0 = t0 + static_cast<uint64_t>(tid) * PER;
+#pragma unroll
+    for (uint32_t k = 0; k < PER; ++k) x[k] = b0 + k < nb ? v[b0 + k] : 0ull;
+    unsigned long long tsum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < PER; ++k) tsum += x[k];
+    unsigned long long incl = tsum;
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned long long y = __shfl_up(incl, o, 64);
+      if (lane >= static_cast<uint32_t>(o)) incl += y;
+    }
+    if (lane == 63) wtot[wid] = incl;
     __syncthreads();
-    part[tid] += x;
-    __syncthreads();
+    unsigned long long wbase = 0, all = 0;
+    for (uint32_t w = 0; w < 16; ++w) {
+      if (w < wid) wbase += wtot[w];
+      all += wtot[w];
+    }
+    unsigned long long run = carry + wbase + incl - tsum;
+#pragma unroll
+    for (uint32_t k = 0; k < PER; ++k) {
+      if (b0 + k < nb) v[b0 + k] = run;
+      run += x[k];
+    }
+    carry += all;
+    __syncthreads();  // wtot reused by the next tile
   }
-  unsigned long long run = part[tid] - s;  // exclusive prefix of this thread's range
-  for (uint32_t i = a; i < b; ++i) {
-    const unsigned long long x = v[i];
-    v[i] = run;
-    run += x;
-  }
-  if (tid == 1023) {
-    status->total_bytes = part[1023];
-    offsets[n] = part[1023];
+  if (tid == 0) {
+    status->total_bytes = carry;
+    offsets[n] = carry;
   }
 }
 
@@ -239,9 +277,7 @@ __global__ __launch_bounds__(256) void k_var_encode(
   }
   if (lane == 63) wsum[wid] = incl;
   __syncthreads();
-  unsigned long long wbase = 0;
-  for (uint32_t w = 0; w < wid; ++w) wbase += wsum[w];
-  const uint64_t off = block_base[blockIdx.x] + wbase + incl - v;
+  const uint64_t off = block_base[blockIdx.x * 4u + wid] + incl - v;  // 64-record block bases
   if (r >= n) return;
   offsets[r] = off;
   if (sz & kSizeErr) return;  // size pass reported this record
@@ -316,13 +352,13 @@ __global__ __launch_bounds__(256) void k_var_encode(
 
 // ------------------------------------------------------------ var: decode
 // Record r = xdr_from_opaque(stream[off[r], off[r+1]), r): fields walk in
-// plan order with check() before every read; payloads go to the heap at
-// [off[r], ...) 4-byte aligned; the native record is zero-filled first.
+// plan order with check() before every read; the native record is
+// zero-filled first.  The decoded heap is the stream itself (the host
+// copies it to heap_out): a payload's xdrg_bytes_ref holds its stream offset.
 __global__ __launch_bounds__(256) void k_var_decode(
     const uint8_t *__restrict__ xdr, uint64_t len, const uint64_t *__restrict__ offsets, uint64_t n,
-    uint8_t *__restrict__ native, uint32_t stride, uint8_t *__restrict__ heap,
-    const xdrg_op *__restrict__ ops, uint32_t nops, const uint32_t *__restrict__ table,
-    uint32_t stack_limit, unsigned long long *err) {
+    uint8_t *__restrict__ native, uint32_t stride, const xdrg_op *__restrict__ ops, uint32_t nops,
+    const uint32_t *__restrict__ table, uint32_t stack_limit, unsigned long long *err) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   xdrg_op *sops = reinterpret_cast<xdrg_op *>(smem);
   load_ops(sops, ops, nops);
@@ -334,7 +370,7 @@ __global__ __launch_bounds__(256) void k_var_decode(
   if ((b - a) & 3u) { report(err, r, kOpRecordLevel, XDRG_ERR_SIZE_NOT_MULT4); return; }
   uint8_t *nat = native + r * stride;
   for (uint32_t k = 0; k < stride / 4; ++k) st32(nat + 4 * k, 0u);
-  uint64_t p = a, hcur = a;
+  uint64_t p = a;
   uint32_t pc = 0;
   for (;;) {
     const xdrg_op &op = sops[pc];
@@ -384,14 +420,12 @@ __global__ __launch_bounds__(256) void k_var_decode(
         return;
       }
       const uint32_t nw = (L + 3u) >> 2;
-      for (uint32_t k = 0; k < nw; ++k) st32(heap + hcur + 4ull * k, ld32(xdr + p + 4ull * k));
       if (L & 3u) {
         const uint32_t w = ld32(xdr + p + 4ull * (nw - 1));
         if (w & ~keep_mask(L & 3u)) { report(err, r, pc, XDRG_ERR_NONZERO_PAD); return; }
       }
-      *reinterpret_cast<uint64_t *>(nat + op.noff) = hcur;
+      *reinterpret_cast<uint64_t *>(nat + op.noff) = p;  // the payload stays in the stream
       st32(nat + op.noff + 8, L);
-      hcur += 4ull * nw;
       p += 4ull * nw; ++pc; break;
     }
     case XDRG_OP_UNION: {
@@ -492,9 +526,7 @@ __global__ __launch_bounds__(256) void k_var_encode_c(
   __syncthreads();
   XDRG_STAMP(2);
 
-  unsigned long long wbase = 0;
-  for (uint32_t w = 0; w < wid; ++w) wbase += wsum[w];
-  const uint64_t off = block_base[blockIdx.x] + wbase + incl - v;
+  const uint64_t off = block_base[blockIdx.x * 4u + wid] + incl - v;  // 64-record block bases
 
   // per-record table, in this lane's registers
   uint32_t rsize = 0;
@@ -637,436 +669,6 @@ __global__ __launch_bounds__(256) void k_var_encode_c(
   XDRG_STAMP_FLUSH(wr0 / 64u);
 }
 
-// Decode, record-image form.  Lane-per-record parse of the wire (scalar
-// fields into an LDS native tile, payload table in registers), then the
-// wave writes each record's heap region [off[j], ...) -- its payloads packed
-// back to back, 4-byte aligned -- as one contiguous stream, checking every
-// payload's pad bytes (get_bytes, marshal.cc:43-57), and finally copies the
-// native tile out with 16-byte stores.
-template <int KMAX>
-__global__ __launch_bounds__(256) void k_var_decode_c(
-    const uint8_t *__restrict__ xdr, uint64_t len, const uint64_t *__restrict__ offsets, uint64_t n,
-    uint8_t *__restrict__ native, uint32_t stride, uint8_t *__restrict__ heap,
-    const xdrg_op *__restrict__ ops, uint32_t nops, const uint32_t *__restrict__ table,
-    uint32_t stack_limit, unsigned long long *err) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
-  const uint32_t ops_bytes = 0;  // ops are read through the scalar cache
-  const uint32_t tile_bytes = (64u * stride + 15u) & ~15u;
-  xdrg_op *sops = reinterpret_cast<xdrg_op *>(sm);
-  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  uint8_t *tile = sm + ops_bytes + wid * tile_bytes;
-  const uint64_t wr0 = static_cast<uint64_t>(blockIdx.x) * blockDim.x + wid * 64u;
-  const uint32_t wn = wr0 < n ? static_cast<uint32_t>(min<uint64_t>(64, n - wr0)) : 0u;
-  const uint32_t nbytes = wn * stride;
-  for (uint32_t i = lane; i < (nbytes + 15u) / 16u; i += 64u)
-    reinterpret_cast<u32x4 *>(tile)[i] = u32x4{0u, 0u, 0u, 0u};
-  (void)sops;
-  __syncthreads();  // tile zeroed before any lane writes a field
-
-  const uint64_t r = wr0 + lane;
-  uint32_t hwords = 0;  // heap words of this record (all payloads, padded)
-  uint32_t pst[KMAX], pln[KMAX], pop[KMAX];
-  uint64_t psr[KMAX];
-  uint64_t a = 0;
-#pragma unroll
-  for (int k = 0; k < KMAX; ++k) { pst[k] = 0xffffffffu; pln[k] = 0; pop[k] = 0; psr[k] = 0; }
-  {
-    uint8_t *nat = tile + lane * stride;
-    uint64_t b = 0;
-    uint32_t pc = kPcDone;
-    if (r < n) {
-      a = offsets[r];
-      b = offsets[r + 1];
-      if (r == n - 1 && b != len) report(err, n, kOpRecordLevel, XDRG_ERR_TRAILING);
-      if (b < a || b > len) report(err, r, 0, XDRG_ERR_OVERFLOW_GET);
-      else if ((b - a) & 3u) report(err, r, kOpRecordLevel, XDRG_ERR_SIZE_NOT_MULT4);
-      else pc = 0;
-    }
-    uint64_t p = a;
-    uint32_t nslot = 0;
-    bool ok = pc == 0u;
-    for (uint32_t upc = 0; upc < nops; ++upc) {
-      if (!__any(pc == upc)) continue;
-      const xdrg_op op = ops[upc];
-      if (pc != upc) continue;
-      if (op.kind == XDRG_OP_END) { pc = kPcDone; continue; }
-      if (op.kind == XDRG_OP_JUMP) { pc = op.arg0; continue; }
-      if (op.depth > stack_limit) { report(err, r, upc, XDRG_ERR_STACK_GET); ok = false; pc = kPcDone; continue; }
-      const uint64_t rem = b - p;
-      uint32_t *nw = reinterpret_cast<uint32_t *>(nat + op.noff);
-      const uint32_t need = op.kind == XDRG_OP_U64 ? 8u : op.kind == XDRG_OP_OPAQUE ? op.arg0 : 4u;
-      if (rem < need) { report(err, r, upc, XDRG_ERR_OVERFLOW_GET); ok = false; pc = kPcDone; continue; }
-      switch (op.kind) {
-      case XDRG_OP_U32:
-        nw[0] = bswap32(ld32(xdr + p)); p += 4; ++pc; break;
-      case XDRG_OP_ENUM: {
-        const uint32_t v = bswap32(ld32(xdr + p));
-        nw[0] = v; p += 4; ++pc;
-        if ((op.flags & XDRG_F_VALIDATE) && !enum_ok(table, op.arg0, op.arg1, v)) {
-          report(err, r, upc, XDRG_ERR_INVALID_ENUM); ok = false; pc = kPcDone;
-        }
-        break;
-      }
-      case XDRG_OP_BOOL:
-        nat[op.noff] = ld32(xdr + p) != 0u; p += 4; ++pc; break;
-      case XDRG_OP_U64:
-        nw[1] = bswap32(ld32(xdr + p));
-        nw[0] = bswap32(ld32(xdr + p + 4));
-        p += 8; ++pc; break;
-      case XDRG_OP_OPAQUE: {
-        const uint32_t BL = op.arg0;
-        for (uint32_t k = 0; k < BL; ++k) nat[op.noff + k] = xdr[p + k];
-        ++pc;
-        if ((BL & 3u) && (ld32(xdr + p + (BL & ~3u)) & ~keep_mask(BL & 3u))) {
-          report(err, r, upc, XDRG_ERR_NONZERO_PAD); ok = false; pc = kPcDone;
-        }
-        p += (BL + 3u) & ~3u;
-        break;
-      }
-      case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
-        const uint32_t BL = bswap32(ld32(xdr + p));
-        p += 4;
-        if (BL > b - p) { report(err, r, upc, XDRG_ERR_OVERFLOW_GET); ok = false; pc = kPcDone; break; }
-        if (BL > op.arg0) {
-          report(err, r, upc,
-                 op.kind == XDRG_OP_STRING ? XDRG_ERR_XSTRING_BOUND : XDRG_ERR_XVECTOR_BOUND);
-          ok = false;
-          pc = kPcDone;
-          break;
-        }
-        const uint32_t nwd = (BL + 3u) >> 2;
-        if (BL) {
-#pragma unroll
-          for (int k = 0; k < KMAX; ++k)
-            if (static_cast<uint32_t>(k) == nslot) { pst[k] = hwords; pln[k] = BL; psr[k] = p; pop[k] = upc; }
-          ++nslot;
-        }
-        *reinterpret_cast<uint64_t *>(nat + op.noff) = a + 4ull * hwords;
-        nw[2] = BL;
-        hwords += nwd;
-        p += 4ull * nwd; ++pc;
-        break;
-      }
-      case XDRG_OP_UNION: {
-        const uint32_t d = bswap32(ld32(xdr + p));
-        p += 4;
-        if ((op.flags & XDRG_F_VALIDATE) && !enum_ok(table, op.arg0, op.arg1, d)) {
-          report(err, r, upc, XDRG_ERR_INVALID_ENUM); ok = false; pc = kPcDone; break;
-        }
-        const int t = union_target(op, table, d);
-        if (t < 0) { report(err, r, upc, XDRG_ERR_BAD_DISCRIMINANT); ok = false; pc = kPcDone; break; }
-        nw[0] = d;
-        pc = static_cast<uint32_t>(t);
-        break;
-      }
-      default: ++pc; break;
-      }
-    }
-    if (ok && p != b) report(err, r, kOpRecordLevel, XDRG_ERR_TRAILING);
-  }
-
-  // ---- heap regions: record j's payloads, contiguous from offsets[j]
-  for (uint32_t j0 = 0; j0 < wn; j0 += kEmitBatch) {
-    uint32_t hw[kEmitBatch];
-    uint32_t passes = 0;
-#pragma unroll
-    for (int u = 0; u < kEmitBatch; ++u) {
-      hw[u] = (j0 + u < wn) ? rl32(hwords, j0 + u) : 0u;
-      passes = max(passes, (hw[u] + 63u) >> 6);
-    }
-    for (uint32_t pss = 0; pss < passes; ++pss) {
-      const uint32_t h = pss * 64u + lane;
-      uint32_t val[kEmitBatch];
-      bool bad[kEmitBatch];
-      uint32_t bop[kEmitBatch];
-#pragma unroll
-      for (int u = 0; u < kEmitBatch; ++u) {
-        const uint32_t j = j0 + u;
-        val[u] = 0u;
-        bad[u] = false;
-        bop[u] = 0u;
-        if (h < hw[u]) {
-#pragma unroll
-          for (int k = 0; k < KMAX; ++k) {
-            const uint32_t stk = rl32(pst[k], j), blk = rl32(pln[k], j);
-            const uint32_t nwk = (blk + 3u) >> 2;
-            if (stk != 0xffffffffu && h >= stk && h < stk + nwk) {
-              const uint32_t kw = h - stk;
-              const uint32_t x = ld32(xdr + rl64(psr[k], j) + 4ull * kw);
-              val[u] = x;
-              if (4u * kw + 4u > blk && (x & ~keep_mask(blk - 4u * kw))) {
-                bad[u] = true;
-                bop[u] = rl32(pop[k], j);
-              }
-            }
-          }
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < kEmitBatch; ++u) {
-        const uint32_t j = j0 + u;
-        if (h < hw[u]) {
-          if (bad[u]) report(err, wr0 + j, bop[u], XDRG_ERR_NONZERO_PAD);
-          st32(heap + rl64(a, j) + 4ull * h, val[u]);
-        }
-      }
-    }
-  }
-  __syncthreads();  // every lane's native fields are in the tile
-  uint8_t *ndst = native + wr0 * stride;
-  for (uint32_t i = lane; i < nbytes / 16u; i += 64u)
-    reinterpret_cast<u32x4 *>(ndst)[i] = reinterpret_cast<const u32x4 *>(tile)[i];
-  for (uint32_t i = (nbytes / 16u) * 4u + lane; i < nbytes / 4u; i += 64u)
-    reinterpret_cast<uint32_t *>(ndst)[i] = reinterpret_cast<const uint32_t *>(tile)[i];
-}
-
-// ---------------------------------------------- var: group-copy kernels
-// Payloads move as <=256-byte pieces; a 16-lane group copies one piece per
-// step with 16-byte loads/stores (gfx950 handles unaligned 16-byte global
-// accesses: tools/probe/unaligned.hip), four groups per wave and
-// kGroupBatch steps in flight.  The lane-per-record walk writes only the
-// scalar words; the pieces of a wave go out right behind them, so the
-// lines they share complete in L2.
-constexpr int kGroupBatch = 4;
-
-constexpr uint32_t kPieceBytes = 256u;
-constexpr uint32_t kLastPiece = 0x80000000u;
-
-struct piece_arrays {
-  uint64_t *src, *dst;
-  uint32_t *len, *tag;
-};
-__host__ __device__ inline uint32_t piece_wave_bytes(uint32_t PM) { return 64u * (PM ? PM : 1u) * 24u; }
-__device__ __forceinline__ piece_arrays piece_carve(uint8_t *base, uint32_t PM) {
-  const uint32_t cap = 64u * (PM ? PM : 1u);
-  piece_arrays pa;
-  pa.src = reinterpret_cast<uint64_t *>(base);
-  pa.dst = pa.src + cap;
-  pa.len = reinterpret_cast<uint32_t *>(pa.dst + cap);
-  pa.tag = pa.len + cap;
-  return pa;
-}
-
-// Split each lane's payload slots into pieces, compacted in record order.
-// Returns the wave's piece count.  tag = last-piece bit | lane << 16 | op.
-template <int KMAX>
-__device__ __forceinline__ uint32_t wave_pieces(const piece_arrays &pa, uint32_t lane,
-                                                const uint64_t (&psr)[KMAX],
-                                                const uint64_t (&pds)[KMAX],
-                                                const uint32_t (&pln)[KMAX],
-                                                const uint32_t (&pop)[KMAX]) {
-  uint32_t np = 0;
-#pragma unroll
-  for (int k = 0; k < KMAX; ++k) np += (pln[k] + kPieceBytes - 1u) / kPieceBytes;
-  uint32_t incl = np;
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t x = __shfl_up(incl, o, 64);
-    if (lane >= static_cast<uint32_t>(o)) incl += x;
-  }
-  uint32_t e = incl - np;
-#pragma unroll
-  for (int k = 0; k < KMAX; ++k) {
-    const uint32_t L = pln[k];
-    for (uint32_t q = 0; q * kPieceBytes < L; ++q, ++e) {
-      pa.src[e] = psr[k] + q * kPieceBytes;
-      pa.dst[e] = pds[k] + q * kPieceBytes;
-      pa.len[e] = min(kPieceBytes, L - q * kPieceBytes);
-      pa.tag[e] = ((q + 1u) * kPieceBytes >= L ? kLastPiece : 0u) | (lane << 16) | (pop[k] & 0xffffu);
-    }
-  }
-  return __shfl(incl, 63, 64);
-}
-
-__device__ __forceinline__ u32x4 ld16u(const uint8_t *p) { return *reinterpret_cast<const u32x4 *>(p); }
-__device__ __forceinline__ void st16u(uint8_t *p, u32x4 v) { *reinterpret_cast<u32x4 *>(p) = v; }
-__device__ __forceinline__ uint32_t keep_bytes(int32_t k) {  // mask of the low k bytes, k clamped
-  return k <= 0 ? 0u : k >= 4 ? 0xffffffffu : ((1u << (8 * k)) - 1u);
-}
-// Store bytes [0, nb) of v (nb a multiple of 4, 4..16) at p.
-__device__ __forceinline__ void st_words(uint8_t *p, const u32x4 &v, uint32_t nb) {
-  if (nb >= 16u) { st16u(p, v); return; }
-  st32(p, v.x);
-  if (nb > 4u) st32(p + 4, v.y);
-  if (nb > 8u) st32(p + 8, v.z);
-}
-
-template <int KMAX, int GB = kGroupBatch>
-__global__ __launch_bounds__(256) void k_var_decode_g(
-    const uint8_t *__restrict__ xdr, uint64_t len, const uint64_t *__restrict__ offsets, uint64_t n,
-    uint8_t *__restrict__ native, uint32_t stride, uint8_t *__restrict__ heap,
-    const xdrg_op *__restrict__ ops, uint32_t nops, const uint32_t *__restrict__ table,
-    uint32_t stack_limit, uint32_t PM, unsigned long long *err, unsigned long long *stamps) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
-  unsigned long long stv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  XDRG_STAMP(0);
-  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const uint32_t tile_bytes = (64u * stride + 15u) & ~15u;
-  const uint32_t per_wave = tile_bytes + piece_wave_bytes(PM);
-  uint8_t *tile = sm + wid * per_wave;
-  const piece_arrays pa = piece_carve(tile + tile_bytes, PM);
-  const uint64_t wr0 = static_cast<uint64_t>(blockIdx.x) * blockDim.x + wid * 64u;
-  const uint32_t wn = wr0 < n ? static_cast<uint32_t>(min<uint64_t>(64, n - wr0)) : 0u;
-  const uint32_t nbytes = wn * stride;
-  for (uint32_t i = lane; i < (nbytes + 15u) / 16u; i += 64u)
-    reinterpret_cast<u32x4 *>(tile)[i] = u32x4{0u, 0u, 0u, 0u};
-  __syncthreads();  // tile zeroed before any lane writes a field
-  XDRG_STAMP(1);
-
-  const uint64_t r = wr0 + lane;
-  uint64_t psr[KMAX], pds[KMAX];
-  uint32_t pln[KMAX], pop[KMAX];
-#pragma unroll
-  for (int k = 0; k < KMAX; ++k) { psr[k] = 0; pds[k] = 0; pln[k] = 0; pop[k] = 0; }
-  {
-    uint8_t *nat = tile + lane * stride;
-    uint64_t a = 0, b = 0;
-    uint32_t pc = kPcDone;
-    if (r < n) {
-      a = offsets[r];
-      b = offsets[r + 1];
-      if (r == n - 1 && b != len) report(err, n, kOpRecordLevel, XDRG_ERR_TRAILING);
-      if (b < a || b > len) report(err, r, 0, XDRG_ERR_OVERFLOW_GET);
-      else if ((b - a) & 3u) report(err, r, kOpRecordLevel, XDRG_ERR_SIZE_NOT_MULT4);
-      else pc = 0;
-    }
-    uint64_t p = a, hcur = a;
-    uint32_t nslot = 0;
-    bool ok = pc == 0u;
-    for (uint32_t upc = 0; upc < nops; ++upc) {
-      if (!__any(pc == upc)) continue;
-      const xdrg_op op = ops[upc];
-      if (pc != upc) continue;
-      if (op.kind == XDRG_OP_END) { pc = kPcDone; continue; }
-      if (op.kind == XDRG_OP_JUMP) { pc = op.arg0; continue; }
-      if (op.depth > stack_limit) { report(err, r, upc, XDRG_ERR_STACK_GET); ok = false; pc = kPcDone; continue; }
-      const uint64_t rem = b - p;
-      uint32_t *nw = reinterpret_cast<uint32_t *>(nat + op.noff);
-      const uint32_t need = op.kind == XDRG_OP_U64 ? 8u : op.kind == XDRG_OP_OPAQUE ? op.arg0 : 4u;
-      if (rem < need) { report(err, r, upc, XDRG_ERR_OVERFLOW_GET); ok = false; pc = kPcDone; continue; }
-      switch (op.kind) {
-      case XDRG_OP_U32:
-        nw[0] = bswap32(ld32(xdr + p)); p += 4; ++pc; break;
-      case XDRG_OP_ENUM: {
-        const uint32_t v = bswap32(ld32(xdr + p));
-        nw[0] = v; p += 4; ++pc;
-        if ((op.flags & XDRG_F_VALIDATE) && !enum_ok(table, op.arg0, op.arg1, v)) {
-          report(err, r, upc, XDRG_ERR_INVALID_ENUM); ok = false; pc = kPcDone;
-        }
-        break;
-      }
-      case XDRG_OP_BOOL:
-        nat[op.noff] = ld32(xdr + p) != 0u; p += 4; ++pc; break;
-      case XDRG_OP_U64:
-        nw[1] = bswap32(ld32(xdr + p));
-        nw[0] = bswap32(ld32(xdr + p + 4));
-        p += 8; ++pc; break;
-      case XDRG_OP_OPAQUE: {
-        const uint32_t BL = op.arg0;
-        for (uint32_t k = 0; k < BL; ++k) nat[op.noff + k] = xdr[p + k];
-        ++pc;
-        if ((BL & 3u) && (ld32(xdr + p + (BL & ~3u)) & ~keep_mask(BL & 3u))) {
-          report(err, r, upc, XDRG_ERR_NONZERO_PAD); ok = false; pc = kPcDone;
-        }
-        p += (BL + 3u) & ~3u;
-        break;
-      }
-      case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
-        const uint32_t BL = bswap32(ld32(xdr + p));
-        p += 4;
-        if (BL > b - p) { report(err, r, upc, XDRG_ERR_OVERFLOW_GET); ok = false; pc = kPcDone; break; }
-        if (BL > op.arg0) {
-          report(err, r, upc,
-                 op.kind == XDRG_OP_STRING ? XDRG_ERR_XSTRING_BOUND : XDRG_ERR_XVECTOR_BOUND);
-          ok = false;
-          pc = kPcDone;
-          break;
-        }
-        const uint64_t padded = (static_cast<uint64_t>(BL) + 3u) & ~3ull;
-        if (BL) {
-#pragma unroll
-          for (int k = 0; k < KMAX; ++k)
-            if (static_cast<uint32_t>(k) == nslot) { psr[k] = p; pds[k] = hcur; pln[k] = BL; pop[k] = upc; }
-          ++nslot;
-        }
-        *reinterpret_cast<uint64_t *>(nat + op.noff) = hcur;
-        nw[2] = BL;
-        hcur += padded;
-        p += padded; ++pc;
-        break;
-      }
-      case XDRG_OP_UNION: {
-        const uint32_t d = bswap32(ld32(xdr + p));
-        p += 4;
-        if ((op.flags & XDRG_F_VALIDATE) && !enum_ok(table, op.arg0, op.arg1, d)) {
-          report(err, r, upc, XDRG_ERR_INVALID_ENUM); ok = false; pc = kPcDone; break;
-        }
-        const int t = union_target(op, table, d);
-        if (t < 0) { report(err, r, upc, XDRG_ERR_BAD_DISCRIMINANT); ok = false; pc = kPcDone; break; }
-        nw[0] = d;
-        pc = static_cast<uint32_t>(t);
-        break;
-      }
-      default: ++pc; break;
-      }
-    }
-    if (ok && p != b) report(err, r, kOpRecordLevel, XDRG_ERR_TRAILING);
-  }
-  XDRG_STAMP(2);
-  const uint32_t M = wave_pieces<KMAX>(pa, lane, psr, pds, pln, pop);
-  __syncthreads();
-  XDRG_STAMP(3);
-  // ---- pieces: wire -> heap (both 4-byte aligned); pad check on last words
-  const uint32_t g = lane >> 4, t16 = (lane & 15u) * 16u;
-  for (uint32_t e0 = 0; e0 < M; e0 += 4u * GB) {
-    u32x4 val[GB];
-#pragma unroll
-    for (int u = 0; u < GB; ++u) {
-      const uint32_t e = e0 + 4u * u + g;
-      val[u] = u32x4{0u, 0u, 0u, 0u};
-      if (e < M) {
-        const uint32_t L = pa.len[e];
-        if (t16 < L) {
-          const uint64_t s0 = pa.src[e] + t16;
-          const uint32_t nb = min(16u, ((L + 3u) & ~3u) - t16);
-          if (nb == 16u) val[u] = ld16u(xdr + s0);
-          else {
-            val[u].x = ld32(xdr + s0);
-            if (nb > 4u) val[u].y = ld32(xdr + s0 + 4);
-            if (nb > 8u) val[u].z = ld32(xdr + s0 + 8);
-          }
-        }
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < GB; ++u) {
-      const uint32_t e = e0 + 4u * u + g;
-      if (e < M) {
-        const uint32_t L = pa.len[e];
-        if (t16 < L) {
-          const u32x4 x = val[u];
-          const int32_t rem = static_cast<int32_t>(L - t16);
-          if (rem < 16 && (pa.tag[e] & kLastPiece)) {
-            const uint32_t bad = (x.x & ~keep_bytes(rem)) | (x.y & ~keep_bytes(rem - 4) & (rem > 4 ? ~0u : 0u)) |
-                                 (x.z & ~keep_bytes(rem - 8) & (rem > 8 ? ~0u : 0u)) |
-                                 (x.w & ~keep_bytes(rem - 12) & (rem > 12 ? ~0u : 0u));
-            if (bad) report(err, wr0 + ((pa.tag[e] >> 16) & 0x7fffu), pa.tag[e] & 0xffffu, XDRG_ERR_NONZERO_PAD);
-          }
-          st_words(heap + pa.dst[e] + t16, x, min(16u, ((L + 3u) & ~3u) - t16));
-        }
-      }
-    }
-  }
-  XDRG_STAMP(4);
-  __syncthreads();  // every lane's native fields are in the tile
-  uint8_t *ndst = native + wr0 * stride;
-  for (uint32_t i = lane; i < nbytes / 16u; i += 64u)
-    reinterpret_cast<u32x4 *>(ndst)[i] = reinterpret_cast<const u32x4 *>(tile)[i];
-  for (uint32_t i = (nbytes / 16u) * 4u + lane; i < nbytes / 4u; i += 64u)
-    reinterpret_cast<uint32_t *>(ndst)[i] = reinterpret_cast<const uint32_t *>(tile)[i];
-  XDRG_STAMP(5);
-  XDRG_STAMP_FLUSH(wr0 / 64u);
-}
-
 // -------------------------------------------- var: image encode (chunk map)
 // One workgroup = one wave = 64 consecutive records.  The wave's output
 // stretch [wave_out, wave_out + T) is assembled in an LDS image:
@@ -1126,20 +728,21 @@ __global__ __launch_bounds__(64) void k_var_encode_i(
   const uint32_t lane = threadIdx.x;
   const uint64_t wr0 = static_cast<uint64_t>(blockIdx.x) * 64u;
   const uint64_t r = wr0 + lane;
+  const uint32_t nrec = static_cast<uint32_t>(min<uint64_t>(64, n - wr0));
 
   // ---- record offsets: wave scan of the sizes on top of the block base
-  const uint32_t sz = r < n ? sizes[r] : 0u;
-  const unsigned long long v = (sz & kSizeErr) ? 0ull : sz;
+  const uint32_t sz = r < n ? sizes[r] : kSizeErr;
+  const bool szok = !(sz & kSizeErr);
+  const unsigned long long v = szok ? sz : 0ull;
   unsigned long long incl = v;
   for (int o = 1; o < 64; o <<= 1) {
     const unsigned long long x = __shfl_up(incl, o, 64);
     if (lane >= static_cast<uint32_t>(o)) incl += x;
   }
-  const uint64_t off = block_base[blockIdx.x] + incl - v;
-  const uint64_t wave_out = rl64(off, 0);
+  const uint64_t wave_out = block_base[blockIdx.x];
+  const uint64_t off = wave_out + incl - v;
   const uint64_t T = rl64(incl, 63);  // bytes of the wave's stretch
   if (r < n) offsets[r] = off;
-  const uint32_t nrec = wr0 < n ? static_cast<uint32_t>(min<uint64_t>(64, n - wr0)) : 0u;
   {
     const uint32_t nbytes = nrec * stride;
     const uint8_t *nsrc = native + wr0 * stride;
@@ -1150,6 +753,7 @@ __global__ __launch_bounds__(64) void k_var_encode_i(
   }
   __syncthreads();
   XDRG_STAMP(1);
+  XDRG_STAMP(2);
 
   const uint32_t sh = static_cast<uint32_t>(wave_out & 15u);
   uint8_t *im = img + sh;               // image byte j <-> global wave_out + j
@@ -1166,8 +770,8 @@ __global__ __launch_bounds__(64) void k_var_encode_i(
     const uint8_t *nat = tile + lane * stride;
     uint32_t at = rel;  // stretch offset of the next wire word
     uint64_t pos = off;
-    uint32_t pc = (r < n && !(sz & kSizeErr)) ? 0u : kPcDone;
-    bool ok = pc == 0u;
+    uint32_t pc = szok ? 0u : kPcDone;
+    bool ok = szok;
     for (uint32_t upc = 0; upc < nops; ++upc) {
       if (!__any(pc == upc)) continue;
       const xdrg_op op = ops[upc];
@@ -1229,7 +833,7 @@ __global__ __launch_bounds__(64) void k_var_encode_i(
     }
     if (!ok) nslot = 0;  // a failing record's bytes are unspecified (never past `cap`)
   }
-  XDRG_STAMP(2);
+  XDRG_STAMP(3);
 
   // ---- chunk map: u16 lane << 10 | slot << 8 | chunk
   uint32_t nch = 0;
@@ -1255,7 +859,6 @@ __global__ __launch_bounds__(64) void k_var_encode_i(
     }
   }
   __syncthreads();
-  XDRG_STAMP(3);
 
   // ---- payload chunks: heap -> image, U chunks in flight per lane
   for (uint32_t c0 = 0; c0 < M; c0 += 64u * U) {
@@ -1337,6 +940,208 @@ __global__ __launch_bounds__(64) void k_var_encode_i(
   XDRG_STAMP_FLUSH(blockIdx.x);
 }
 
+// -------------------------------------------------- var: window decode
+// One workgroup = one wave = 64 consecutive records.  The decoded heap is
+// the stream itself (xdrg_decode contract), so decode never gathers
+// payloads:
+//   * the wave's input stretch [a0, a_end) is read once with aligned
+//     16-byte loads into an LDS window (window byte j sits at LDS
+//     j + ((xdr + a0) & 15)) and written to heap_out at the same offsets;
+//     bytes past the window capacity C are copied global -> global;
+//   * the lane-per-record walk parses from the window (global for bytes
+//     past C): fields into a zeroed LDS native tile, payloads as
+//     xdrg_bytes_ref {stream offset, len}, with every bound / pad /
+//     discriminant / enum check of xdr_generic_get;
+//   * the tile leaves with 16-byte stores.
+__host__ __device__ inline uint32_t dec_w_lds(uint32_t stride, uint32_t C) {
+  return ((64u * stride + 15u) & ~15u) + C + 32u;
+}
+
+template <bool COPY>
+__global__ __launch_bounds__(64) void k_var_decode_w(
+    const uint8_t *__restrict__ xdr, uint64_t len, const uint64_t *__restrict__ offsets, uint64_t n,
+    uint8_t *__restrict__ native, uint32_t stride, uint8_t *__restrict__ heap,
+    const xdrg_op *__restrict__ ops, uint32_t nops, const uint32_t *__restrict__ table,
+    uint32_t stack_limit, uint32_t C, unsigned long long *err, unsigned long long *stamps) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
+  unsigned long long stv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  XDRG_STAMP(0);
+  const uint32_t lane = threadIdx.x;
+  const uint32_t tile_bytes = (64u * stride + 15u) & ~15u;
+  uint8_t *tile = sm;
+  uint8_t *win = sm + tile_bytes;
+  const uint64_t wr0 = static_cast<uint64_t>(blockIdx.x) * 64u;
+  const uint32_t nrec = static_cast<uint32_t>(min<uint64_t>(64, n - wr0));
+  const uint64_t r = wr0 + lane;
+  uint64_t a = 0, b = 0;
+  if (lane < nrec) {
+    a = offsets[r];
+    b = offsets[r + 1];
+  }
+  // the wave's stretch, clamped to the stream (bad indices are reported by
+  // the per-record checks below; the window just gets smaller)
+  const uint64_t ws = min<uint64_t>(rl64(a, 0), len);
+  const uint64_t we = max<uint64_t>(ws, min<uint64_t>(rl64(b, nrec - 1), len));
+  const uint64_t wc = min<uint64_t>(we - ws, C);  // bytes held in the window
+  const uintptr_t gbase = reinterpret_cast<uintptr_t>(xdr) + ws;
+  const uint32_t sh = static_cast<uint32_t>(gbase & 15u);
+  const uint8_t *wnd = win + sh;  // window byte j <-> stream byte ws + j
+
+  for (uint32_t i = lane; i < tile_bytes / 16u; i += 64u)
+    reinterpret_cast<u32x4 *>(tile)[i] = u32x4{0u, 0u, 0u, 0u};
+  {
+    // Aligned 16-byte chunks covering the stretch [ws, we), 8 loads in
+    // flight per lane.  A chunk never leaves the pages that hold stream
+    // bytes, so edge chunks load whole; only in-range words reach the heap.
+    // Chunks inside [ws, ws + wc) also fill the window.
+    const uint32_t nwin = static_cast<uint32_t>((sh + wc + 15u) >> 4);
+    const uint64_t nall = COPY ? (sh + (we - ws) + 15u) >> 4 : nwin;
+    const uint8_t *g0 = xdr + ws - sh;
+    constexpr int UL = 8;
+    for (uint64_t c0 = 0; c0 < nall; c0 += 64u * UL) {
+      u32x4 v[UL];
+#pragma unroll
+      for (int u = 0; u < UL; ++u) {
+        const uint64_t c = c0 + 64u * u + lane;
+        if (c < nall) v[u] = *reinterpret_cast<const u32x4 *>(g0 + 16u * c);
+      }
+#pragma unroll
+      for (int u = 0; u < UL; ++u) {
+        const uint64_t c = c0 + 64u * u + lane;
+        if (c >= nall) continue;
+        if (c < nwin) reinterpret_cast<u32x4 *>(win)[c] = v[u];
+        if (COPY) {
+          const int64_t o = static_cast<int64_t>(16u * c) - sh;  // stream offset - ws
+          const int64_t lim = static_cast<int64_t>(we - ws);
+          uint8_t *hd = heap + ws + o;
+          if (o >= 0 && o + 16 <= lim) {
+            st16u(hd, v[u]);
+          } else {
+            const uint32_t w4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              if (o + 4 * q >= 0 && o + 4 * q + 4 <= lim) st32(hd + 4 * q, w4[q]);
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  XDRG_STAMP(1);
+
+  // word reader: window for stream bytes in [ws, ws + wc), global otherwise
+  auto rd = [&](uint64_t pos) -> uint32_t {
+    const uint64_t rel = pos - ws;
+    if (pos >= ws && rel + 4 <= wc) {
+      const uint8_t *q = wnd + rel;
+      if (((sh + rel) & 3u) == 0) return *reinterpret_cast<const uint32_t *>(q);
+      return uint32_t(q[0]) | (uint32_t(q[1]) << 8) | (uint32_t(q[2]) << 16) | (uint32_t(q[3]) << 24);
+    }
+    return unaligned_word(xdr, len, pos);
+  };
+
+  {
+    uint8_t *nat = tile + lane * stride;
+    uint32_t pc = kPcDone;
+    if (lane < nrec) {
+      if (r == n - 1 && b != len) report(err, n, kOpRecordLevel, XDRG_ERR_TRAILING);
+      if (b < a || b > len) report(err, r, 0, XDRG_ERR_OVERFLOW_GET);
+      else if ((b - a) & 3u) report(err, r, kOpRecordLevel, XDRG_ERR_SIZE_NOT_MULT4);
+      else pc = 0;
+    }
+    uint64_t p = a;
+    bool ok = pc == 0u;
+    for (uint32_t upc = 0; upc < nops; ++upc) {
+      if (!__any(pc == upc)) continue;
+      const xdrg_op op = ops[upc];
+      if (pc != upc) continue;
+      if (op.kind == XDRG_OP_END) { pc = kPcDone; continue; }
+      if (op.kind == XDRG_OP_JUMP) { pc = op.arg0; continue; }
+      if (op.depth > stack_limit) { report(err, r, upc, XDRG_ERR_STACK_GET); ok = false; pc = kPcDone; continue; }
+      const uint64_t rem = b - p;
+      uint32_t *nw = reinterpret_cast<uint32_t *>(nat + op.noff);
+      const uint32_t need = op.kind == XDRG_OP_U64 ? 8u : op.kind == XDRG_OP_OPAQUE ? op.arg0 : 4u;
+      if (rem < need) { report(err, r, upc, XDRG_ERR_OVERFLOW_GET); ok = false; pc = kPcDone; continue; }
+      switch (op.kind) {
+      case XDRG_OP_U32:
+        nw[0] = bswap32(rd(p)); p += 4; ++pc; break;
+      case XDRG_OP_ENUM: {
+        const uint32_t v = bswap32(rd(p));
+        nw[0] = v; p += 4; ++pc;
+        if ((op.flags & XDRG_F_VALIDATE) && !enum_ok(table, op.arg0, op.arg1, v)) {
+          report(err, r, upc, XDRG_ERR_INVALID_ENUM); ok = false; pc = kPcDone;
+        }
+        break;
+      }
+      case XDRG_OP_BOOL:
+        nat[op.noff] = rd(p) != 0u; p += 4; ++pc; break;
+      case XDRG_OP_U64:
+        nw[1] = bswap32(rd(p));
+        nw[0] = bswap32(rd(p + 4));
+        p += 8; ++pc; break;
+      case XDRG_OP_OPAQUE: {
+        const uint32_t BL = op.arg0;
+        for (uint32_t k = 0; k < BL; k += 4) {
+          const uint32_t w = rd(p + k);
+          for (uint32_t bb = 0; bb < 4u && k + bb < BL; ++bb) nat[op.noff + k + bb] = uint8_t(w >> (8 * bb));
+        }
+        ++pc;
+        if ((BL & 3u) && (rd(p + (BL & ~3u)) & ~keep_mask(BL & 3u))) {
+          report(err, r, upc, XDRG_ERR_NONZERO_PAD); ok = false; pc = kPcDone;
+        }
+        p += (BL + 3u) & ~3u;
+        break;
+      }
+      case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
+        const uint32_t BL = bswap32(rd(p));
+        p += 4;
+        if (BL > b - p) { report(err, r, upc, XDRG_ERR_OVERFLOW_GET); ok = false; pc = kPcDone; break; }
+        if (BL > op.arg0) {
+          report(err, r, upc,
+                 op.kind == XDRG_OP_STRING ? XDRG_ERR_XSTRING_BOUND : XDRG_ERR_XVECTOR_BOUND);
+          ok = false;
+          pc = kPcDone;
+          break;
+        }
+        if ((BL & 3u) && (rd(p + (BL & ~3u)) & ~keep_mask(BL & 3u))) {  // get_bytes pad check
+          report(err, r, upc, XDRG_ERR_NONZERO_PAD); ok = false; pc = kPcDone; break;
+        }
+        *reinterpret_cast<uint64_t *>(nat + op.noff) = p;  // the payload stays in the stream
+        nw[2] = BL;
+        p += (static_cast<uint64_t>(BL) + 3u) & ~3ull; ++pc;
+        break;
+      }
+      case XDRG_OP_UNION: {
+        const uint32_t d = bswap32(rd(p));
+        p += 4;
+        if ((op.flags & XDRG_F_VALIDATE) && !enum_ok(table, op.arg0, op.arg1, d)) {
+          report(err, r, upc, XDRG_ERR_INVALID_ENUM); ok = false; pc = kPcDone; break;
+        }
+        const int t = union_target(op, table, d);
+        if (t < 0) { report(err, r, upc, XDRG_ERR_BAD_DISCRIMINANT); ok = false; pc = kPcDone; break; }
+        nw[0] = d;
+        pc = static_cast<uint32_t>(t);
+        break;
+      }
+      default: ++pc; break;
+      }
+    }
+    if (ok && p != b) report(err, r, kOpRecordLevel, XDRG_ERR_TRAILING);
+  }
+  __syncthreads();
+  XDRG_STAMP(2);
+  uint8_t *ndst = native + wr0 * stride;
+  const uint32_t nbytes = nrec * stride;
+  for (uint32_t i = lane; i < nbytes / 16u; i += 64u)
+    reinterpret_cast<u32x4 *>(ndst)[i] = reinterpret_cast<const u32x4 *>(tile)[i];
+  for (uint32_t i = (nbytes / 16u) * 4u + lane; i < nbytes / 4u; i += 64u)
+    reinterpret_cast<uint32_t *>(ndst)[i] = reinterpret_cast<const uint32_t *>(tile)[i];
+  XDRG_STAMP(3);
+  XDRG_STAMP(4);
+  XDRG_STAMP(5);
+  XDRG_STAMP_FLUSH(blockIdx.x);
+}
+
 // ------------------------------------------------------------------ swaps
 __global__ void k_swap32(const uint32_t *__restrict__ in, uint32_t *__restrict__ out, uint64_t n) {
   for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
@@ -1354,9 +1159,10 @@ constexpr uint64_t kMallBytes = 256ull << 20;  // MI355X Infinity Cache
 constexpr uint32_t kVarLdsBudget = 64u << 10;  // wave-cooperative var kernels
 // Var-kernel choice: 0 = automatic (the fastest eligible kernel).  Forcing
 // (tools/tune A/B, tests): encode 1 = per-lane, 2 = record image,
-// 3 = chunk-map image; decode 1 = per-lane, 2 = record image, 3 = group copy.
+// 3 = chunk-map image; decode 1 = per-lane, 2 = window.
 int g_force_enc = 0, g_force_dec = 0;
-uint32_t g_img_bytes = 4u << 10;  // encode LDS image per wave (tools/tune/ab_var.py)
+uint32_t g_img_bytes = 4u << 10;   // encode LDS image per wave (tools/tune/ab_var.py)
+uint32_t g_win_bytes = 16u << 10;  // decode LDS window per wave (tools/tune/ab_var.py)
 unsigned long long *g_stamps = nullptr;      // diagnostic phase stamps, decode (tuning)
 unsigned long long *g_stamps_enc = nullptr;  // diagnostic phase stamps, encode (tuning)
 
@@ -1462,7 +1268,21 @@ size_t var_ws_layout(uint64_t n, size_t *sizes_off, size_t *bsum_off) {
   const uint64_t nb = (n + 63) / 64;  // block sums at the finest block size (64)
   *sizes_off = 0;
   *bsum_off = align_up(n * 4, 256);
-  return *bsum_off + align_up(nb * 8, 256);
+  return *bsum_off + align_up((nb + 1) * 8, 256);  // block sums / look-back flags + ticket
+}
+
+// Size pass (xdr_size per record + 64-record block sums).
+hipError_t launch_size_pass(const xdrg_plan &p, const uint8_t *nat, uint64_t n, uint32_t *sizes,
+                            unsigned long long *bsum, unsigned long long *err, hipStream_t s) {
+  const uint64_t nb = (n + 63) / 64;
+  const size_t tile = 64ull * p.stride;
+  if (tile <= kVarLdsBudget)
+    k_var_size<true><<<nb, 64, tile, s>>>(nat, n, p.stride, p.d_ops, uint32_t(p.ops.size()),
+                                          p.d_table, sizes, bsum, err);
+  else
+    k_var_size<false><<<nb, 64, 0, s>>>(nat, n, p.stride, p.d_ops, uint32_t(p.ops.size()),
+                                        p.d_table, sizes, bsum, err);
+  return hipGetLastError();
 }
 
 unsigned long long *err_ptr(xdrg_status *st) {
@@ -1485,6 +1305,11 @@ void xdrg__force_var_kernels(int enc, int dec) {
 }
 void xdrg__set_stamps(void *buf) { g_stamps = static_cast<unsigned long long *>(buf); }
 void xdrg__set_stamps_enc(void *buf) { g_stamps_enc = static_cast<unsigned long long *>(buf); }
+int xdrg__set_window_bytes(int bytes) {
+  const int old = static_cast<int>(g_win_bytes);
+  g_win_bytes = static_cast<uint32_t>(bytes) & ~15u;
+  return old;
+}
 int xdrg__set_image_bytes(int bytes) {
   const int old = static_cast<int>(g_img_bytes);
   g_img_bytes = static_cast<uint32_t>(bytes) & ~15u;
@@ -1647,32 +1472,32 @@ int xdrg_encode(const xdrg_plan *p, const void *d_native, uint64_t n, const uint
   if (kern == 3 && !ok_I) kern = 0;
   if (kern == 2 && !ok_C) kern = 0;
   if (kern == 0) kern = ok_I ? 3 : ok_C ? 2 : 1;
-  const uint32_t vb = kern == 3 ? 64u : 256u;
-  const uint64_t nb = (n + vb - 1) / vb;
+  const uint64_t nb = (n + 63) / 64;  // 64-record blocks for the size pass, scan and kernel 3
   if (nb > 0xffffffffull) return XDRG_EUNSUPPORTED;
   const size_t lds_ops = p->ops.size() * sizeof(xdrg_op);
-  k_var_size<<<nb, vb, lds_ops, s>>>(static_cast<const uint8_t *>(d_native), n, p->stride,
-                                      p->d_ops, uint32_t(p->ops.size()), p->d_table, sizes,
-                                      bsum, err);
-  HIPCHK(hipGetLastError());
-  k_scan_blocks<<<1, 1024, 0, s>>>(bsum, uint32_t(nb), d_status, d_offsets, n);
-  HIPCHK(hipGetLastError());
   const uint8_t *nat8 = static_cast<const uint8_t *>(d_native);
   uint8_t *xdr8 = static_cast<uint8_t *>(d_xdr);
   const uint32_t nops = uint32_t(p->ops.size());
+  HIPCHK(launch_size_pass(*p, nat8, n, sizes, bsum, err, s));
+  k_scan_blocks<<<1, 1024, 0, s>>>(bsum, uint32_t(nb), d_status, d_offsets, n);
+  HIPCHK(hipGetLastError());
   if (kern == 3) {
 #define LAUNCH_ENC_I(K)                                                                        \
   k_var_encode_i<K, 16><<<nb, 64, LI.total, s>>>(nat8, n, p->stride, d_heap, heap_len, xdr8,  \
-                                                 cap, d_offsets, sizes, bsum, p->d_ops, nops, \
-                                                 p->d_table, stack_limit, MC, Ci, err,        \
+                                                 cap, d_offsets, sizes, bsum, p->d_ops, nops,  \
+                                                 p->d_table, stack_limit, MC, Ci, err,         \
                                                  g_stamps_enc)
     if (KI == 1) LAUNCH_ENC_I(1);
     else if (KI == 2) LAUNCH_ENC_I(2);
     else LAUNCH_ENC_I(4);
 #undef LAUNCH_ENC_I
-  } else if (kern == 2) {
+    HIPCHK(hipGetLastError());
+    return XDRG_OK;
+  }
+  const uint64_t nb256 = (n + 255) / 256;
+  if (kern == 2) {
 #define LAUNCH_ENC_C(K)                                                                        \
-  k_var_encode_c<K><<<nb, 256, EL.total, s>>>(nat8, n, p->stride, d_heap, heap_len, xdr8, cap, \
+  k_var_encode_c<K><<<nb256, 256, EL.total, s>>>(nat8, n, p->stride, d_heap, heap_len, xdr8, cap, \
                                               d_offsets, sizes, bsum, p->d_ops, nops,          \
                                               p->d_table, stack_limit, p->max_scalar_words,   \
                                               err, g_stamps_enc)
@@ -1681,7 +1506,7 @@ int xdrg_encode(const xdrg_plan *p, const void *d_native, uint64_t n, const uint
     else LAUNCH_ENC_C(4);
 #undef LAUNCH_ENC_C
   } else {
-    k_var_encode<<<nb, 256, lds_ops, s>>>(nat8, n, p->stride, d_heap, heap_len, xdr8, cap,
+    k_var_encode<<<nb256, 256, lds_ops, s>>>(nat8, n, p->stride, d_heap, heap_len, xdr8, cap,
                                           d_offsets, sizes, bsum, p->d_ops, nops, p->d_table,
                                           stack_limit, err);
   }
@@ -1728,39 +1553,32 @@ int xdrg_decode(const xdrg_plan *p, const void *d_xdr, uint64_t len, const uint6
   if (heap_cap < len || (len && !d_heap_out)) return XDRG_ESPACE;
   if (!aligned(d_xdr, 4) || !aligned(d_native, 8) || (d_heap_out && !aligned(d_heap_out, 4)))
     return XDRG_EALIGN;
-  const uint64_t nb = (n + 255) / 256;
-  const size_t lds_ops = p->ops.size() * sizeof(xdrg_op);
-  const size_t dl = 4u * ((64u * p->stride + 15u) & ~15u);
-  const bool ok_C = dl <= kVarLdsBudget && aligned(d_native, 16) && p->max_var_slots <= 4;
-  const uint32_t gl = 4u * (((64u * p->stride + 15u) & ~15u) + piece_wave_bytes(p->max_pieces));
-  const bool ok_G = gl <= kVarLdsBudget && aligned(d_native, 16) && p->max_pieces <= 16 &&
-                    p->max_var_slots <= 4;
-  int kern = g_force_dec;
-  if (kern == 3 && !ok_G) kern = 0;
-  if (kern == 2 && !ok_C) kern = 0;
-  if (kern == 0) kern = ok_G ? 3 : ok_C ? 2 : 1;
   const uint8_t *xdr8 = static_cast<const uint8_t *>(d_xdr);
   uint8_t *nat8 = static_cast<uint8_t *>(d_native);
   const uint32_t nops = uint32_t(p->ops.size());
-  if (kern == 3) {
-#define LAUNCH_DEC_G(K)                                                                        \
-  k_var_decode_g<K, 8><<<nb, 256, gl, s>>>(xdr8, len, d_offsets, n, nat8, p->stride, d_heap_out, \
-                                           p->d_ops, nops, p->d_table, stack_limit,            \
-                                           p->max_pieces, err, g_stamps)
-    if (p->max_var_slots <= 2) LAUNCH_DEC_G(2);
-    else LAUNCH_DEC_G(4);
-#undef LAUNCH_DEC_G
-  } else if (kern == 2) {
-#define LAUNCH_DEC_C(K)                                                                        \
-  k_var_decode_c<K><<<nb, 256, dl, s>>>(xdr8, len, d_offsets, n, nat8, p->stride, d_heap_out, \
-                                        p->d_ops, nops, p->d_table, stack_limit, err)
-    if (p->max_var_slots <= 1) LAUNCH_DEC_C(1);
-    else if (p->max_var_slots <= 2) LAUNCH_DEC_C(2);
-    else LAUNCH_DEC_C(4);
-#undef LAUNCH_DEC_C
+  const bool copy = d_heap_out != d_xdr;  // heap_out == d_xdr: zero-copy (refs into the stream)
+  const uint32_t Cw = static_cast<uint32_t>(std::min<uint64_t>(
+      g_win_bytes, (64ull * std::max<uint64_t>(p->max_record_bytes, 16) + 15u) & ~15ull));
+  const uint32_t lw = dec_w_lds(p->stride, Cw);
+  const bool ok_W = lw <= kVarLdsBudget && aligned(d_native, 16);
+  int kern = g_force_dec;
+  if (kern == 2 && !ok_W) kern = 0;
+  if (kern == 0) kern = ok_W ? 2 : 1;
+  if (kern == 2) {
+    const uint64_t nb = (n + 63) / 64;
+    if (copy)
+      k_var_decode_w<true><<<nb, 64, lw, s>>>(xdr8, len, d_offsets, n, nat8, p->stride, d_heap_out,
+                                              p->d_ops, nops, p->d_table, stack_limit, Cw, err,
+                                              g_stamps);
+    else
+      k_var_decode_w<false><<<nb, 64, lw, s>>>(xdr8, len, d_offsets, n, nat8, p->stride, d_heap_out,
+                                               p->d_ops, nops, p->d_table, stack_limit, Cw, err,
+                                               g_stamps);
   } else {
-    k_var_decode<<<nb, 256, lds_ops, s>>>(xdr8, len, d_offsets, n, nat8, p->stride, d_heap_out,
-                                          p->d_ops, nops, p->d_table, stack_limit, err);
+    if (copy && len) HIPCHK(hipMemcpyAsync(d_heap_out, d_xdr, len, hipMemcpyDeviceToDevice, s));
+    const uint64_t nb = (n + 255) / 256;
+    k_var_decode<<<nb, 256, p->ops.size() * sizeof(xdrg_op), s>>>(
+        xdr8, len, d_offsets, n, nat8, p->stride, p->d_ops, nops, p->d_table, stack_limit, err);
   }
   HIPCHK(hipGetLastError());
   return XDRG_OK;
@@ -1777,14 +1595,8 @@ int xdrg_serial_sizes(const xdrg_plan *p, const void *d_native, uint64_t n, uint
     HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_sizes), int(p->fixed_size), n, s));
     return XDRG_OK;
   }
-  const uint64_t nb = (n + 255) / 256;
-  unsigned long long *bsum = nullptr;
-  HIPCHK(hipMallocAsync(reinterpret_cast<void **>(&bsum), nb * 8, s));
-  k_var_size<<<nb, 256, p->ops.size() * sizeof(xdrg_op), s>>>(
-      static_cast<const uint8_t *>(d_native), n, p->stride, p->d_ops, uint32_t(p->ops.size()),
-      p->d_table, d_sizes, bsum, err_ptr(d_status));
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipFreeAsync(bsum, s));
+  HIPCHK(launch_size_pass(*p, static_cast<const uint8_t *>(d_native), n, d_sizes, nullptr,
+                          err_ptr(d_status), s));
   return XDRG_OK;
 }
 
