@@ -50,8 +50,10 @@ def parse():
     ap.add_argument("--gather", action="store_true",
                     help="also time an RCCL gather of encoded shards to rank 0 (reported apart)")
     ap.add_argument("--cpu-threads", type=int, default=0)
-    ap.add_argument("--schema", default="rec128", choices=["rec128", "numerics", "recvar", "rpc"],
-                    help="rec128 is the headline; the others measure BASELINE.json configs 1, 3, 4")
+    ap.add_argument("--schema", default="rec128",
+                    choices=["rec128", "numerics", "recvar", "rpc", "vecrec"],
+                    help="rec128 is the headline; numerics/recvar/rpc measure BASELINE.json "
+                         "configs 1, 3, 4; vecrec covers xvector<T>/pointer<T>")
     return ap.parse_args()
 
 
@@ -200,7 +202,7 @@ def setup(schema, n, dev, rank, world):
     total = int(mar.serial_sizes(nat, n).to(torch.int64).sum().item())
     xdr = torch.empty(total, dtype=torch.uint8, device=dev)
     offsets = torch.empty(n + 1, dtype=torch.int64, device=dev)
-    heap_out = torch.empty(total, dtype=torch.uint8, device=dev)
+    heap_out = torch.empty(plan.decode_heap_bytes(total), dtype=torch.uint8, device=dev)
     return plan, mar, nat, heap, xdr, back, offsets, heap_out
 
 
@@ -322,7 +324,8 @@ def main():
     wl = {"rec128": "rec128: 1M fixed-width 128-byte XDR records per GPU",
           "numerics": "numerics (tests/xdrtest.x) fixed 44-byte records, 56-byte native",
           "recvar": "recvar: opaque<256> + string<64> variable-length records",
-          "rpc": "rpc_msg (xdrpp/rpc_msg.x) nested discriminated unions"}[args.schema]
+          "rpc": "rpc_msg (xdrpp/rpc_msg.x) nested discriminated unions",
+          "vecrec": "vecrec: int<16>, mismatch_info *, vpair<8> counted/optional containers"}[args.schema]
     line = {
         "metric": ("XDR encode+decode GiB/s (device-resident, 1M×128B records) + %HBM roofline"
                    if args.schema == "rec128" else

@@ -62,12 +62,18 @@ enum xdrg_op_kind {
   XDRG_OP_STRING = 7,    /* string<arg0>: native xdrg_bytes_ref                 (types.h:530-587) */
   XDRG_OP_UNION = 8,     /* discriminant int32 at noff, then the selected arm   (gen_hh.cc:639-673) */
   XDRG_OP_JUMP = 9,      /* pc = arg0 (end of a union arm)                      */
-  XDRG_OP_END = 10       /* end of record                                       */
+  XDRG_OP_END = 10,      /* end of record                                       */
+  XDRG_OP_VECTOR = 11    /* xvector<T,arg0> / pointer<T> (F_POINTER, arg0 = 1):  (types.h:365-414,476-512,591-665)
+                          * native xdrg_bytes_ref {heap offset, count} of an
+                          * element array with stride arg1; wire u32 count then
+                          * the elements.  The element's ops follow inline:
+                          * ops [pc+1, pc+1+arg2); fixed-size elements only. */
 };
 
 enum xdrg_op_flags {
   XDRG_F_VALIDATE = 1,   /* ENUM / UNION: opt-in xdr_validate_enum (types.h:157-173) */
-  XDRG_F_DEFAULT = 2     /* UNION: has a default arm; arg4 = its pc             */
+  XDRG_F_DEFAULT = 2,    /* UNION: has a default arm; arg4 = its pc             */
+  XDRG_F_POINTER = 4     /* VECTOR: xdr::pointer (count 0 or 1)                 */
 };
 
 /*
@@ -154,7 +160,8 @@ enum xdrg_err {
   XDRG_ERR_STACK_PUT = 8,       /* xdr_stack_overflow  marshal.h:131-132 */
   XDRG_ERR_STACK_GET = 9,       /* xdr_stack_overflow  marshal.h:200-201 */
   XDRG_ERR_SIZE_NOT_MULT4 = 10, /* xdr_bad_message_size marshal.h:157-159 */
-  XDRG_ERR_TRAILING = 11        /* xdr_bad_message_size marshal.h:207-210 */
+  XDRG_ERR_TRAILING = 11,       /* xdr_bad_message_size marshal.h:207-210 */
+  XDRG_ERR_POINTER_BOUND = 12   /* xdr_overflow        types.h:605-608   */
 };
 
 /* Exception class a data error maps to (for host-side rethrow). */
@@ -252,6 +259,13 @@ int xdrg_decode(const xdrg_plan *plan, const void *d_xdr, uint64_t xdr_len,
                 uint8_t *d_heap_out, uint64_t heap_capacity,
                 uint32_t stack_limit, void *d_workspace, size_t workspace_bytes,
                 xdrg_status *d_status, void *stream);
+
+/* Heap capacity xdrg_decode needs for a stream of xdr_len bytes: xdr_len,
+ * plus, for plans with xvector<T>/pointer<T> fields, an area for the
+ * decoded element arrays.  Record i's element arrays are placed from byte
+ * align16(xdr_len) + F * off[i] (F = 1 + the largest native/wire size ratio
+ * of an element type, so no extra pass is needed), each 8-byte aligned. */
+uint64_t xdrg_decode_heap_size(const xdrg_plan *plan, uint64_t xdr_len);
 
 /* Size pass alone: d_sizes[i] = xdr_size(record i) (uint32). */
 int xdrg_serial_sizes(const xdrg_plan *plan, const void *d_native, uint64_t n,

@@ -87,6 +87,19 @@ template <std::uint32_t N> struct bytes_kind<xstring<N>> {
   static constexpr int kind = XDRG_OP_STRING;
   static constexpr std::uint32_t n = N;
 };
+// xvector<T,N> (T not a byte) and pointer<T>: counted / optional containers
+template <typename T> struct vector_info : std::false_type {};
+template <typename E, std::uint32_t N> struct vector_info<xvector<E, N>> : std::true_type {
+  using elem = E;
+  static constexpr std::uint32_t max = N;
+  static constexpr bool pointer = false;
+};
+template <std::uint32_t N> struct vector_info<xvector<std::uint8_t, N>> : std::false_type {};
+template <typename E> struct vector_info<pointer<E>> : std::true_type {
+  using elem = E;
+  static constexpr std::uint32_t max = 1;
+  static constexpr bool pointer = true;
+};
 template <typename T> struct xarray_info : std::false_type {};
 template <typename E, std::uint32_t N> struct xarray_info<xarray<E, N>> : std::true_type {
   using elem = E;
@@ -143,8 +156,11 @@ inline void append(subplan &dst, const subplan &src, std::uint32_t base, std::ui
   const std::uint32_t pc0 = static_cast<std::uint32_t>(dst.ops.size());
   const std::uint32_t t0 = static_cast<std::uint32_t>(dst.table.size());
   dst.table.insert(dst.table.end(), src.table.begin(), src.table.end());
+  std::uint32_t body = 0;  // ops left in a VECTOR body (element-relative offsets)
   for (xdrg_op o : src.ops) {
-    if (o.kind != XDRG_OP_JUMP) o.noff += base;
+    if (body) --body;
+    else if (o.kind != XDRG_OP_JUMP) o.noff += base;
+    if (o.kind == XDRG_OP_VECTOR) body = o.arg2;
     o.depth = static_cast<std::uint16_t>(o.depth + dadd);
     if (o.kind == XDRG_OP_JUMP) o.arg0 += pc0;
     if ((o.kind == XDRG_OP_ENUM || o.kind == XDRG_OP_UNION) && (o.flags & XDRG_F_VALIDATE))
@@ -369,6 +385,19 @@ template <typename T> subplan record_type() {
     sp.ops.push_back(mkop(sizeof(UT) == 8 ? XDRG_OP_U64 : XDRG_OP_U32, 0, 0));
     sp.size = sizeof(T);
     sp.align = alignof(T);
+  } else if constexpr (vector_info<T>::value) {
+    using E = typename vector_info<T>::elem;
+    const subplan e = record_type<E>();
+    if (!e.fixed) throw std::logic_error("xdr::gpu: xvector<T>/pointer<T> of variable-size T is not supported");
+    xdrg_op v = mkop(XDRG_OP_VECTOR, 0, 1, vector_info<T>::max, align_up(e.size, e.align),
+                     vector_info<T>::pointer ? XDRG_F_POINTER : 0);
+    v.arg2 = static_cast<std::uint32_t>(e.ops.size());
+    sp.ops.push_back(v);
+    append(sp, e, 0, 1);  // elements inside the container level
+    sp.size = sizeof(xdrg_bytes_ref);
+    sp.align = alignof(xdrg_bytes_ref);
+    sp.identity = false;
+    sp.fixed = false;
   } else if constexpr (xarray_info<T>::value) {
     using E = typename xarray_info<T>::elem;
     const subplan e = record_type<E>();
@@ -441,6 +470,25 @@ struct stager : cursor {
         std::memcpy(rec + o.noff, &f, sizeof(P));
         ++pc;
       }
+    } else if constexpr (vector_info<P>::value) {
+      const xdrg_op &o = next();
+      const std::uint32_t cnt = static_cast<std::uint32_t>(f.size());
+      heap->resize((heap->size() + 7) & ~std::size_t(7), 0);
+      const std::uint64_t off = heap->size();
+      heap->resize(off + std::uint64_t(cnt) * o.arg1, 0);
+      std::uint32_t i = 0;
+      for (const auto &e : f) {  // fixed-size elements: staging them never grows the heap
+        stager s2;
+        s2.ops = ops;
+        s2.table = table;
+        s2.pc = pc + 1;
+        s2.rec = heap->data() + off + std::uint64_t(i++) * o.arg1;
+        s2.heap = heap;
+        s2(e);
+      }
+      const xdrg_bytes_ref r{off, cnt, 0};
+      std::memcpy(rec + o.noff, &r, sizeof r);
+      pc += 1 + o.arg2;
     } else if constexpr (xarray_info<P>::value) {
       for (const auto &e : f) (*this)(e);
     } else {
@@ -472,6 +520,26 @@ struct unstager : cursor {
       std::memcpy(&f, rec + o.noff, sizeof(P));
       if (o.kind == XDRG_OP_UNION) branch(o, static_cast<std::int32_t>(f));
       else ++pc;
+    } else if constexpr (vector_info<P>::value) {
+      const xdrg_op &o = next();
+      xdrg_bytes_ref r;
+      std::memcpy(&r, rec + o.noff, sizeof r);
+      if constexpr (vector_info<P>::pointer) {
+        if (r.len) f.activate(); else f.reset();
+      } else {
+        f.resize(r.len);
+      }
+      std::uint32_t i = 0;
+      for (auto &e : f) {
+        unstager u2;
+        u2.ops = ops;
+        u2.table = table;
+        u2.pc = pc + 1;
+        u2.rec = heap + r.off + std::uint64_t(i++) * o.arg1;
+        u2.heap = heap;
+        u2(e);
+      }
+      pc += 1 + o.arg2;
     } else if constexpr (xarray_info<P>::value) {
       for (auto &e : f) (*this)(e);
     } else {
@@ -642,6 +710,17 @@ std::vector<std::uint64_t> index_records(const std::uint8_t *xdr, std::size_t le
         if (p + 4 > len) { bad = true; break; }
         p += 4 + ((std::uint64_t(detail::be32(xdr + p)) + 3) & ~3ull);
         break;
+      case XDRG_OP_VECTOR: {
+        if (p + 4 > len) { bad = true; break; }
+        std::uint64_t we = 0;
+        for (std::uint32_t k = 1; k <= o.arg2; ++k) {
+          const xdrg_op &e = ops[pc + k];
+          we += e.kind == XDRG_OP_U64 ? 8u : e.kind == XDRG_OP_OPAQUE ? detail::align_up(e.arg0, 4) : 4u;
+        }
+        p += 4 + detail::be32(xdr + p) * we;
+        pc += 1 + o.arg2;
+        continue;
+      }
       case XDRG_OP_UNION: {
         if (p + 4 > len) { bad = true; break; }
         const std::int32_t d = static_cast<std::int32_t>(detail::be32(xdr + p));
@@ -717,15 +796,16 @@ void from_opaque_batch(const void *bytes, std::size_t len, T *out, std::size_t n
   detail::abicheck(xdrg_status_init(d_st.p, s), "xdrg_status_init");
   std::vector<std::uint64_t> idx;
   detail::dev_buf<std::uint64_t> d_off(P.fixed() ? 0 : n + 1);
-  detail::dev_buf<std::uint8_t> d_heap(P.fixed() ? 0 : len);
+  const std::uint64_t hcap = P.fixed() ? 0 : xdrg_decode_heap_size(P.handle(), len);
+  detail::dev_buf<std::uint8_t> d_heap(hcap);
   if (!P.fixed()) {
     idx = index_records<T>(x, len, n);
     detail::hipcheck(hipMemcpyAsync(d_off.p, idx.data(), (n + 1) * 8, hipMemcpyHostToDevice, s), "H2D");
   }
-  detail::abicheck(xdrg_decode(P.handle(), d_xdr.p, len, d_off.p, n, d_nat.p, d_heap.p,
-                               P.fixed() ? 0 : len, marshaling_stack_limit, nullptr, 0, d_st.p, s),
+  detail::abicheck(xdrg_decode(P.handle(), d_xdr.p, len, d_off.p, n, d_nat.p, d_heap.p, hcap,
+                               marshaling_stack_limit, nullptr, 0, d_st.p, s),
                    "xdrg_decode");
-  std::vector<std::uint8_t> nat(n * P.stride()), heap(P.fixed() ? 0 : len);
+  std::vector<std::uint8_t> nat(n * P.stride()), heap(hcap);
   if (!nat.empty())
     detail::hipcheck(hipMemcpyAsync(nat.data(), d_nat.p, nat.size(), hipMemcpyDeviceToHost, s), "D2H");
   if (!heap.empty())

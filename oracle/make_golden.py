@@ -25,10 +25,10 @@ ROOT = os.path.dirname(HERE)
 GOLD = os.path.join(ROOT, "tests", "golden")
 BIN = os.path.join(HERE, "_ref", "ref_golden")
 
-SMALL = {"numerics": 1000, "rec128": 1024, "recvar": 1024, "rpc": 1024}
+SMALL = {"numerics": 1000, "rec128": 1024, "recvar": 1024, "rpc": 1024, "vecrec": 1024}
 FULL = {"rec128": 1 << 20, "recvar": 1 << 20, "rpc": 1 << 20, "numerics": 1 << 16,
         "rec128_mgpu": 1 << 24}
-MID = {"recvar": 1 << 16, "rpc": 1 << 16}
+MID = {"recvar": 1 << 16, "rpc": 1 << 16, "vecrec": 1 << 16}
 EXTS = ("native", "heap", "xdr", "offsets")
 
 

@@ -207,7 +207,30 @@ static void kat(const string &path) {
     o << "    \"rpc_bad_reject_stat\": "
       << try_decode<rpcx::rpc_msg>(h, [](xdr::opaque_vec<> &m) { m[15] = 5; }) << ",\n";
     o << "    \"rpc_bad_reply_stat\": "
-      << try_decode<rpcx::rpc_msg>(h, [](xdr::opaque_vec<> &m) { m[11] = 2; }) << "\n";
+      << try_decode<rpcx::rpc_msg>(h, [](xdr::opaque_vec<> &m) { m[11] = 2; }) << ",\n";
+  }
+  {
+    // vecrec: id, vals<16> = {5, -6}, opt = {7, 8}, pairs<8> = {(9, true)}, flag
+    vecrec x{};
+    x.id = 1;
+    x.vals = {5, -6};
+    x.opt.activate() = rpcx::mismatch_info{7, 8};
+    x.pairs.resize(1);
+    x.pairs[0].h = 9;
+    x.pairs[0].b = true;
+    x.flag = false;
+    const string h = enc(x);
+    // layout: id @0, vals count @4, vals @8..16, opt count @16, opt @20..28,
+    // pairs count @28, pair @32..44, flag @44
+    o << "    \"vecrec_ok\": " << try_decode<vecrec>(h) << ",\n";
+    o << "    \"vecrec_vals_over_bound\": "
+      << try_decode<vecrec>(h, [](xdr::opaque_vec<> &m) { m[7] = 17; }) << ",\n";
+    o << "    \"vecrec_pointer_two\": "
+      << try_decode<vecrec>(h, [](xdr::opaque_vec<> &m) { m[19] = 2; }) << ",\n";
+    o << "    \"vecrec_pairs_past_end\": "
+      << try_decode<vecrec>(h, [](xdr::opaque_vec<> &m) { m[31] = 3; }) << ",\n";
+    o << "    \"vecrec_bool2\": "
+      << try_decode<vecrec>(h, [](xdr::opaque_vec<> &m) { m[43] = 2; }) << "\n";
   }
   o << "  }\n}\n";
   std::ofstream f(path);
@@ -285,6 +308,7 @@ int main(int argc, char **argv) {
     else if (schema == "rec128") { vector<rec128> v; gen_rec128(n, WG_SEED_REC128, 0, v); emit(v, pre); }
     else if (schema == "rec128_mgpu") { vector<rec128> v; gen_rec128(n, WG_SEED_REC128_MGPU, 0, v); emit(v, pre); }
     else if (schema == "recvar") { vector<recvar> v; gen_recvar(n, WG_SEED_RECVAR, v); emit(v, pre); }
+    else if (schema == "vecrec") { vector<vecrec> v; gen_vecrec(n, WG_SEED_VECREC, v); emit(v, pre); }
     else if (schema == "rpc") { vector<rpcx::rpc_msg> v; gen_rpc(n, WG_SEED_RPC, v); emit(v, pre); }
     else die("unknown schema " + schema);
     return 0;
@@ -295,6 +319,7 @@ int main(int argc, char **argv) {
     if (schema == "rec128") { vector<rec128> v; gen_rec128(n, WG_SEED_REC128, 0, v); bench_one("rec128", v, threads, reps); }
     else if (schema == "numerics") { vector<testns::numerics> v; gen_numerics(n, WG_SEED_NUMERICS, v); bench_one("numerics", v, threads, reps); }
     else if (schema == "recvar") { vector<recvar> v; gen_recvar(n, WG_SEED_RECVAR, v); bench_one("recvar", v, threads, reps); }
+    else if (schema == "vecrec") { vector<vecrec> v; gen_vecrec(n, WG_SEED_VECREC, v); bench_one("vecrec", v, threads, reps); }
     else if (schema == "rpc") { vector<rpcx::rpc_msg> v; gen_rpc(n, WG_SEED_RPC, v); bench_one("rpc", v, threads, reps); }
     else die("unknown schema " + schema);
     return 0;

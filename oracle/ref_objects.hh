@@ -100,6 +100,34 @@ template <typename T> [[maybe_unused]] static T bits_as(uint64_t v) {
   }
 }
 
+// vecrec: draws d[0..5] = draw(seed, 6r + k); element values from the
+// payload stream draw(seed ^ XOR, 32r + j)
+[[maybe_unused]] static void gen_vecrec(size_t n, uint64_t seed, vector<vecrec> &v) {
+  v.resize(n);
+  const uint64_t ps = seed ^ WG_PAYLOAD_XOR;
+  for (size_t r = 0; r < n; ++r) {
+    uint64_t d[6];
+    for (int k = 0; k < 6; ++k) d[k] = wg_draw(seed, r * 6 + k);
+    vecrec &x = v[r];
+    x.id = (uint32_t)d[0];
+    const uint32_t nv = d[1] % 17, np = d[3] % 9;
+    x.vals.resize(nv);
+    for (uint32_t j = 0; j < nv; ++j) x.vals[j] = (int32_t)(uint32_t)wg_draw(ps, r * 32 + j);
+    if (d[2] & 1) {
+      const uint64_t w = wg_draw(ps, r * 32 + 16);
+      x.opt.activate() = rpcx::mismatch_info{(uint32_t)w, (uint32_t)(w >> 32)};
+    } else {
+      x.opt.reset();
+    }
+    x.pairs.resize(np);
+    for (uint32_t j = 0; j < np; ++j) {
+      x.pairs[j].h = (int64_t)wg_draw(ps, r * 32 + 17 + j);
+      x.pairs[j].b = (d[5] >> j) & 1;
+    }
+    x.flag = (d[4] >> 8) & 1;
+  }
+}
+
 [[maybe_unused]] static void fill_auth(rpcx::opaque_auth &a, int32_t flavor, uint32_t len, uint64_t ps,
                       uint64_t word0) {
   a.flavor = flavor;
@@ -162,6 +190,14 @@ struct heap_t {
   xdrg_bytes_ref put(const uint8_t *p, size_t n) {
     xdrg_bytes_ref r{b.size(), uint32_t(n), 0};
     b.insert(b.end(), p, p + n);
+    return r;
+  }
+  // element array of a vector / pointer: 8-byte aligned, count elements
+  xdrg_bytes_ref put_elems(const void *p, size_t count, size_t stride) {
+    b.resize((b.size() + 7) & ~size_t(7), 0);
+    xdrg_bytes_ref r{b.size(), uint32_t(count), 0};
+    const uint8_t *q = static_cast<const uint8_t *>(p);
+    b.insert(b.end(), q, q + count * stride);
     return r;
   }
 };
@@ -228,6 +264,27 @@ struct heap_t {
   }
 }
 
+[[maybe_unused]] static void stage(const vector<vecrec> &v, vector<uint8_t> &nat, heap_t &h) {
+  nat.assign(v.size() * sizeof(st_vecrec), 0);
+  st_vecrec *s = reinterpret_cast<st_vecrec *>(nat.data());
+  for (size_t r = 0; r < v.size(); ++r) {
+    const vecrec &x = v[r];
+    s[r].id = x.id;
+    s[r].vals = h.put_elems(x.vals.data(), x.vals.size(), 4);
+    st_mismatch m{};
+    if (x.opt) m = st_mismatch{x.opt->low, x.opt->high};
+    s[r].opt = h.put_elems(&m, x.opt ? 1 : 0, sizeof m);
+    vector<st_vpair> pv(x.pairs.size());
+    for (size_t j = 0; j < pv.size(); ++j) {
+      pv[j] = st_vpair{};
+      pv[j].h = x.pairs[j].h;
+      pv[j].b = x.pairs[j].b;
+    }
+    s[r].pairs = h.put_elems(pv.data(), pv.size(), sizeof(st_vpair));
+    s[r].flag = x.flag;
+  }
+}
+
 // Equality for round-trip checks (byte-level for fixed structs).
 [[maybe_unused]] static bool same(const testns::numerics &a, const testns::numerics &b) {
   return a.b == b.b && a.i1 == b.i1 && a.i2 == b.i2 && a.i3 == b.i3 && a.i4 == b.i4 &&
@@ -237,6 +294,9 @@ struct heap_t {
 [[maybe_unused]] static bool same(const recvar &a, const recvar &b) {
   return a.id == b.id && a.kind == b.kind && a.blob == b.blob && a.name == b.name &&
          !memcmp(&a.score, &b.score, 8);
+}
+[[maybe_unused]] static bool same(const vecrec &a, const vecrec &b) {
+  return xdr::xdr_to_opaque(a) == xdr::xdr_to_opaque(b);
 }
 [[maybe_unused]] static bool same(const rpcx::rpc_msg &a, const rpcx::rpc_msg &b) {
   return xdr::xdr_to_opaque(a) == xdr::xdr_to_opaque(b);

@@ -388,3 +388,48 @@ RPC_UNION_BEGIN(rpcx::body_u)
 };
 RPC_STRUCT2(rpcx::rpc_msg, xid, body)
 }  // namespace xdr
+
+// ------------------------------------------------------------------ vecrec
+// Counted and optional containers of fixed-size elements:
+//   struct vpair { hyper h; bool b; };
+//   struct vecrec { unsigned id; int vals<16>; mismatch_info *opt;
+//                   vpair pairs<8>; bool flag; };
+struct vpair {
+  std::int64_t h;
+  bool b;
+};
+struct vecrec {
+  std::uint32_t id;
+  xdr::xvector<std::int32_t, 16> vals;
+  xdr::pointer<rpcx::mismatch_info> opt;
+  xdr::xvector<vpair, 8> pairs;
+  bool flag;
+};
+namespace xdr {
+template <>
+struct xdr_traits<::vpair> : xdr_struct_base<XF(::vpair, h), XF(::vpair, b)> {
+  template <typename A> static void save(A &ar, const ::vpair &obj) {
+    archive(ar, obj.h, "h"); archive(ar, obj.b, "b");
+  }
+  template <typename A> static void load(A &ar, ::vpair &obj) {
+    archive(ar, obj.h, "h"); archive(ar, obj.b, "b");
+    using xdr::validate; validate(obj);
+  }
+};
+template <>
+struct xdr_traits<::vecrec>
+    : xdr_struct_base<XF(::vecrec, id), XF(::vecrec, vals), XF(::vecrec, opt),
+                      XF(::vecrec, pairs), XF(::vecrec, flag)> {
+#define VECREC_FIELDS(X) X(id) X(vals) X(opt) X(pairs) X(flag)
+#define ARCH(f) archive(ar, obj.f, #f);
+  template <typename Archive> static void save(Archive &ar, const ::vecrec &obj) {
+    VECREC_FIELDS(ARCH)
+  }
+  template <typename Archive> static void load(Archive &ar, ::vecrec &obj) {
+    VECREC_FIELDS(ARCH)
+    using xdr::validate;
+    validate(obj);
+  }
+#undef ARCH
+};
+}  // namespace xdr

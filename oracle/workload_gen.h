@@ -25,6 +25,7 @@
 #define WG_SEED_RECVAR 0x5EED0003ULL
 #define WG_SEED_RPC 0x5EED0004ULL
 #define WG_SEED_REC128_MGPU 0x5EED0005ULL
+#define WG_SEED_VECREC 0x5EED0006ULL
 #define WG_PAYLOAD_XOR 0xB10BB10BB10BB10BULL
 
 static inline uint64_t wg_draw(uint64_t seed, uint64_t i) {
@@ -56,6 +57,18 @@ typedef struct { int32_t stat; union { st_mismatch mismatch_info; int32_t rj_why
 typedef struct { int32_t stat; uint32_t pad_; union { st_accepted_reply areply; st_rejected_reply rreply; } u; } st_reply_body;
 typedef struct { int32_t mtype; uint32_t pad_; union { st_call_body cbody; st_reply_body rbody; } u; } st_body;
 typedef struct { uint32_t xid; uint32_t pad_; st_body body; } st_rpc_msg; /* 80 bytes */
+
+/* vecrec: element arrays live in the heap, each 8-byte aligned */
+typedef struct { int64_t h; uint8_t b; uint8_t pad_[7]; } st_vpair; /* 16 bytes */
+typedef struct {
+  uint32_t id;
+  uint32_t pad_;
+  xdrg_bytes_ref vals;  /* int32[count] */
+  xdrg_bytes_ref opt;   /* st_mismatch[0 or 1] */
+  xdrg_bytes_ref pairs; /* st_vpair[count] */
+  uint8_t flag;
+  uint8_t pad2_[7];
+} st_vecrec; /* 64 bytes */
 
 /* rpc record kinds drawn per record: sel = draw1 % 10 */
 enum { WG_RPC_CALL_MAX = 4, WG_RPC_SUCCESS = 5, WG_RPC_PROG_MISMATCH = 6,

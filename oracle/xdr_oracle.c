@@ -63,6 +63,33 @@ static int enum_ok(const plan_t *P, const xdrg_op *op, uint32_t v) {
   return 0;
 }
 
+/* xvector<T> / pointer<T> (XDRG_OP_VECTOR): the element's ops follow the
+ * op inline, [pc+1, pc+1+arg2); elements are fixed-size. */
+static uint32_t elem_wire(const xdrg_op *e) {
+  return e->kind == XDRG_OP_U64 ? 8u : e->kind == XDRG_OP_OPAQUE ? pad4(e->arg0) : 4u;
+}
+static uint32_t vec_wire(const plan_t *P, uint32_t pc) {
+  uint32_t w = 0;
+  for (uint32_t k = 1; k <= P->ops[pc].arg2; ++k) w += elem_wire(&P->ops[pc + k]);
+  return w;
+}
+/* Decoded element arrays of record r start at align16(len) + F * off[r]
+ * (F = 1 + the largest native/wire size ratio of an element type). */
+static uint32_t heap_factor(const plan_t *P) {
+  uint32_t f = 0;
+  for (uint32_t pc = 0; pc < P->nops; ++pc)
+    if (P->ops[pc].kind == XDRG_OP_VECTOR) {
+      uint32_t we = vec_wire(P, pc), g = (P->ops[pc].arg1 + we - 1) / we + 1;
+      if (g > f) f = g;
+    }
+  return f;
+}
+uint64_t xdro_decode_heap_size(const xdrg_op *ops, uint32_t nops, uint64_t len) {
+  plan_t P = {ops, nops, NULL, 0};
+  uint32_t f = heap_factor(&P);
+  return f ? ((len + 15) & ~15ull) + (uint64_t)f * len : len;
+}
+
 /* xdr_size of one record (xdr_traits<T>::serial_size).  Returns 0 and sets
  * *err and *eop on a bad discriminant. */
 static uint64_t rec_size(const plan_t *P, const uint8_t *nat, uint32_t *err, uint32_t *eop) {
@@ -89,6 +116,13 @@ static uint64_t rec_size(const plan_t *P, const uint8_t *nat, uint32_t *err, uin
       break;
     }
     case XDRG_OP_JUMP: pc = op->arg0; break;
+    case XDRG_OP_VECTOR: {
+      xdrg_bytes_ref r;
+      memcpy(&r, nat + op->noff, sizeof r);
+      s += 4 + (uint64_t)r.len * vec_wire(P, pc);
+      pc += 1 + op->arg2;
+      break;
+    }
     default: return s;
     }
   }
@@ -121,7 +155,8 @@ int xdro_encode(const xdrg_op *ops, uint32_t nops, const uint32_t *table, uint32
       }
       uint64_t need = 0;
       switch (op->kind) {
-      case XDRG_OP_U32: case XDRG_OP_ENUM: case XDRG_OP_BOOL: case XDRG_OP_UNION: need = 4; break;
+      case XDRG_OP_U32: case XDRG_OP_ENUM: case XDRG_OP_BOOL: case XDRG_OP_UNION:
+      case XDRG_OP_VECTOR: need = 4; break;
       case XDRG_OP_U64: need = 8; break;
       case XDRG_OP_OPAQUE: need = op->arg0; break;
       case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
@@ -170,6 +205,38 @@ int xdro_encode(const xdrg_op *ops, uint32_t nops, const uint32_t *table, uint32
         break;
       }
       case XDRG_OP_JUMP: pc = op->arg0; break;
+      case XDRG_OP_VECTOR: {
+        /* container save (types.h:374-379): size32 count, then each element
+         * archived field by field (stack + space checks per field) */
+        xdrg_bytes_ref ref; memcpy(&ref, nat + op->noff, sizeof ref);
+        wr32(out + pos, bswap32(ref.len)); pos += 4;
+        for (uint32_t i = 0; i < ref.len; ++i) {
+          const uint8_t *el = heap + ref.off + (uint64_t)i * op->arg1;
+          for (uint32_t k = 1; k <= op->arg2; ++k) {
+            const xdrg_op *e = &ops[pc + k];
+            if (e->depth > stack_limit) { *erec = r; *eop = pc + k; return XDRG_ERR_STACK_PUT; }
+            uint32_t wb = elem_wire(e);
+            if (wb > cap - pos) { *erec = r; *eop = pc + k; return XDRG_ERR_OVERFLOW_PUT; }
+            switch (e->kind) {
+            case XDRG_OP_BOOL: wr32(out + pos, bswap32(el[e->noff] != 0)); break;
+            case XDRG_OP_U64: {
+              uint64_t v = rd64(el + e->noff);
+              wr32(out + pos, bswap32((uint32_t)(v >> 32)));
+              wr32(out + pos + 4, bswap32((uint32_t)v));
+              break;
+            }
+            case XDRG_OP_OPAQUE:
+              memcpy(out + pos, el + e->noff, e->arg0);
+              for (uint64_t q = e->arg0; q & 3; ++q) out[pos + q] = 0;
+              break;
+            default: wr32(out + pos, bswap32(rd32(el + e->noff))); break;
+            }
+            pos += wb;
+          }
+        }
+        pc += 1 + op->arg2;
+        break;
+      }
       default: ++pc; break;
       }
     }
@@ -198,7 +265,8 @@ int xdro_sizes(const xdrg_op *ops, uint32_t nops, const uint32_t *table, uint32_
  * xdrg_bytes_ref holds its byte offset in the stream (`base`): the decoded
  * heap is the stream itself (xdro_decode copies it to heap_out). */
 static int dec_record(const plan_t *P, const uint8_t **pp, const uint8_t *e, uint8_t *nat,
-                      const uint8_t *base, uint32_t stack_limit, uint32_t *eop) {
+                      const uint8_t *base, uint8_t *heap_out, uint64_t ecur,
+                      uint32_t stack_limit, uint32_t *eop) {
   const uint8_t *p = *pp;
   uint32_t pc = 0;
   memset(nat, 0, P->stride);
@@ -254,6 +322,51 @@ static int dec_record(const plan_t *P, const uint8_t **pp, const uint8_t *e, uin
       memcpy(nat + op->noff, &ref, sizeof ref);
       ++pc; break;
     }
+    case XDRG_OP_VECTOR: {
+      /* container load (types.h:380-392): count, check_size, elements */
+      CHECK(4);
+      uint32_t cnt = bswap32(rd32(p)); p += 4;
+      if (cnt > op->arg0) {
+        *eop = pc; *pp = p;
+        return (op->flags & XDRG_F_POINTER) ? XDRG_ERR_POINTER_BOUND : XDRG_ERR_XVECTOR_BOUND;
+      }
+      ecur = (ecur + 7) & ~7ull;
+      xdrg_bytes_ref ref = {ecur, cnt, 0};
+      memcpy(nat + op->noff, &ref, sizeof ref);
+      for (uint32_t i = 0; i < cnt; ++i) {
+        uint8_t *el = heap_out + ecur + (uint64_t)i * op->arg1;
+        memset(el, 0, op->arg1);
+        for (uint32_t k = 1; k <= op->arg2; ++k) {
+          const xdrg_op *f = &P->ops[pc + k];
+          if (f->depth > stack_limit) { *eop = pc + k; *pp = p; return XDRG_ERR_STACK_GET; }
+          uint32_t need = f->kind == XDRG_OP_U64 ? 8u : f->kind == XDRG_OP_OPAQUE ? f->arg0 : 4u;
+          if ((uint64_t)need > (uint64_t)(e - p)) { *eop = pc + k; *pp = p; return XDRG_ERR_OVERFLOW_GET; }
+          switch (f->kind) {
+          case XDRG_OP_BOOL: el[f->noff] = rd32(p) != 0; break;
+          case XDRG_OP_U64: {
+            uint64_t hi = bswap32(rd32(p)), lo = bswap32(rd32(p + 4));
+            wr64(el + f->noff, hi << 32 | lo);
+            break;
+          }
+          case XDRG_OP_OPAQUE:
+            memcpy(el + f->noff, p, f->arg0);
+            for (uint64_t q = f->arg0; q & 3; ++q)
+              if (p[q] != 0) { *eop = pc + k; *pp = p; return XDRG_ERR_NONZERO_PAD; }
+            break;
+          default: {
+            uint32_t v = bswap32(rd32(p));
+            wr32(el + f->noff, v);
+            if (f->kind == XDRG_OP_ENUM && !enum_ok(P, f, v)) { *eop = pc + k; *pp = p; return XDRG_ERR_INVALID_ENUM; }
+            break;
+          }
+          }
+          p += elem_wire(f);
+        }
+      }
+      ecur += (uint64_t)cnt * op->arg1;
+      pc += 1 + op->arg2;
+      break;
+    }
     case XDRG_OP_UNION: {
       CHECK(4);
       uint32_t d = bswap32(rd32(p)); p += 4;
@@ -286,11 +399,14 @@ int xdro_decode(const xdrg_op *ops, uint32_t nops, const uint32_t *table, uint32
                 uint32_t *eop) {
   plan_t P = {ops, nops, table, stride};
   if (heap_out && len) memcpy(heap_out, xdr, len);
+  const uint32_t F = heap_factor(&P);
+  const uint64_t ebase = F ? ((len + 15) & ~15ull) : 0;
   if (!offsets) {
     if (len & 3) { *erec = 0; *eop = 0xffffffffu; return XDRG_ERR_SIZE_NOT_MULT4; }
     const uint8_t *p = xdr, *e = xdr + len;
     for (uint64_t r = 0; r < n; ++r) {
-      int rc = dec_record(&P, &p, e, native + r * stride, xdr, stack_limit, eop);
+      int rc = dec_record(&P, &p, e, native + r * stride, xdr, heap_out,
+                          ebase + (uint64_t)F * (uint64_t)(p - xdr), stack_limit, eop);
       if (rc) { *erec = r; return rc; }
     }
     if (p != e) { *erec = n; *eop = 0xffffffffu; return XDRG_ERR_TRAILING; }
@@ -301,7 +417,8 @@ int xdro_decode(const xdrg_op *ops, uint32_t nops, const uint32_t *table, uint32
     if (b < a || b > len) { *erec = r; *eop = 0; return XDRG_ERR_OVERFLOW_GET; }
     if ((b - a) & 3) { *erec = r; *eop = 0xffffffffu; return XDRG_ERR_SIZE_NOT_MULT4; }
     const uint8_t *p = xdr + a, *e = xdr + b;
-    int rc = dec_record(&P, &p, e, native + r * stride, xdr, stack_limit, eop);
+    int rc = dec_record(&P, &p, e, native + r * stride, xdr, heap_out, ebase + (uint64_t)F * a,
+                        stack_limit, eop);
     if (rc) { *erec = r; return rc; }
     if (p != e) { *erec = r; *eop = 0xffffffffu; return XDRG_ERR_TRAILING; }
   }

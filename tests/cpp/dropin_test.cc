@@ -192,6 +192,22 @@ static void gpu_errors() {
     check_error<recvar>("recvar nonzero pad", x, r.size());
     break;
   }
+  std::vector<vecrec> vr;
+  gen_vecrec(64, WG_SEED_VECREC, vr);
+  std::vector<std::uint8_t> vs = ref_stream(vr, off);
+  for (std::size_t i = 0; i < vr.size(); ++i) {
+    if (vr[i].opt) {  // pointer count 2 in record i
+      auto x = vs;
+      x[off[i] + 4 + 4 + 4 * vr[i].vals.size() + 3] = 2;
+      check_error<vecrec>("vecrec pointer count 2", x, vr.size());
+      break;
+    }
+  }
+  {  // xvector count past its bound in record 3
+    auto x = vs;
+    x[off[3] + 4 + 3] = 17;
+    check_error<vecrec>("vecrec xvector overflow", x, vr.size());
+  }
   std::vector<rec128> f;
   gen_rec128(16, WG_SEED_REC128, 0, f);
   std::vector<std::uint8_t> fs = ref_stream(f, off);
@@ -207,6 +223,8 @@ int main(int argc, char **argv) {
   std::vector<rec128> rc;
   std::vector<recvar> rv;
   std::vector<rpcx::rpc_msg> rp;
+  std::vector<vecrec> vr;
+  gen_vecrec(1024, WG_SEED_VECREC, vr);
   gen_numerics(1000, WG_SEED_NUMERICS, nu);
   gen_rec128(1024, WG_SEED_REC128, 0, rc);
   gen_recvar(1024, WG_SEED_RECVAR, rv);
@@ -218,16 +236,19 @@ int main(int argc, char **argv) {
     write_plan<rec128>(dir, "rec128");
     write_plan<recvar>(dir, "recvar");
     write_plan<rpcx::rpc_msg>(dir, "rpc");
+    write_plan<vecrec>(dir, "vecrec");
   } else if (mode == "stage") {
     check_stage("numerics", nu);
     check_stage("rec128", rc);
     check_stage("recvar", rv);
     check_stage("rpc", rp);
+    check_stage("vecrec", vr);
   } else if (mode == "gpu") {
     check_gpu("numerics", nu);
     check_gpu("rec128", rc);
     check_gpu("recvar", rv);
     check_gpu("rpc", rp);
+    check_gpu("vecrec", vr);
     gpu_errors();
   } else {
     std::fprintf(stderr, "usage: dropin_test plans <dir> | stage | gpu\n");

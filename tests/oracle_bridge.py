@@ -39,6 +39,8 @@ def lib() -> C.CDLL:
         L.xdro_decode.argtypes = [vp, u32, vp, u32, vp, u64, vp, u64, vp, vp, u32,
                                   C.POINTER(u64), C.POINTER(u32)]
         L.xdro_sizes.argtypes = [vp, u32, vp, u32, vp, u64, vp, C.POINTER(u64), C.POINTER(u32)]
+        L.xdro_decode_heap_size.argtypes = [vp, u32, u64]
+        L.xdro_decode_heap_size.restype = u64
         _lib = L
     return _lib
 
@@ -77,9 +79,11 @@ def encode(plan, native: np.ndarray, n: int, heap: np.ndarray | None = None,
 
 def decode(plan, xdr: np.ndarray, n: int, offsets: np.ndarray | None = None,
            stack_limit: int = 0xFFFFFFFF):
-    """Returns (native, heap) or raises OracleError."""
+    """Returns (native, heap) or raises OracleError.  heap = the stream
+    verbatim, then (plans with xvector/pointer fields) the element area."""
     native = np.zeros(max(n, 1) * plan.stride, dtype=np.uint8)
-    heap = np.zeros(max(xdr.size, 4), dtype=np.uint8)
+    hsize = int(lib().xdro_decode_heap_size(_p(plan.ops), len(plan.ops), xdr.size))
+    heap = np.zeros(max(hsize, 4), dtype=np.uint8)
     er, eo = C.c_uint64(0), C.c_uint32(0)
     x = xdr if xdr.size else np.zeros(4, dtype=np.uint8)
     rc = lib().xdro_decode(_p(plan.ops), len(plan.ops), _p(plan.table), plan.stride,
@@ -87,4 +91,4 @@ def decode(plan, xdr: np.ndarray, n: int, offsets: np.ndarray | None = None,
                            stack_limit, C.byref(er), C.byref(eo))
     if rc:
         raise OracleError(rc, er.value, eo.value)
-    return native[:n * plan.stride], heap[:xdr.size]
+    return native[:n * plan.stride], heap[:hsize]

@@ -52,7 +52,8 @@ def test_cpp_staging_matches_reference_layout():
     assert r.returncode == 0, r.stdout + r.stderr
 
 
-@pytest.mark.parametrize("name", ["numerics", "numerics_validated", "rec128", "recvar", "rpc"])
+@pytest.mark.parametrize("name", ["numerics", "numerics_validated", "rec128", "recvar", "rpc",
+                                  "vecrec"])
 def test_recorded_plan_equals_compiled_plan(tmp_path, name):
     r = run("plans", str(tmp_path))
     assert r.returncode == 0, r.stderr

@@ -21,7 +21,7 @@ from xdrpp_amd import schemas as S  # noqa: E402
 from xdrpp_amd import workloads as W  # noqa: E402
 import oracle_bridge as O  # noqa: E402
 
-SCHEMAS = ["numerics", "rec128", "recvar", "rpc"]
+SCHEMAS = ["numerics", "rec128", "recvar", "rpc", "vecrec"]
 _plans = {}
 
 
@@ -78,7 +78,7 @@ def test_golden_decode(dev, name):
 
 # ------------------------------------------------------------- full size
 @pytest.mark.parametrize("name,n", [("rec128", 1 << 20), ("numerics", 1 << 16),
-                                    ("recvar", 1 << 16), ("rpc", 1 << 16),
+                                    ("recvar", 1 << 16), ("rpc", 1 << 16), ("vecrec", 1 << 16),
                                     ("recvar", 1 << 20), ("rpc", 1 << 20)])
 def test_full_size_hash(dev, manifest, name, n):
     h = manifest["hashes"][f"{name}_{n}"]
@@ -156,7 +156,8 @@ EXC_NAME = {"xdr_overflow": M.XdrOverflow, "xdr_stack_overflow": M.XdrStackOverf
     "numerics_bool2", "numerics_enum99_novalidate", "numerics_enum99_validate",
     "recvar_ok", "recvar_nonzero_pad", "recvar_blob_over_bound", "recvar_name_over_bound",
     "recvar_len_past_end", "rpc_ok", "rpc_bad_mtype", "rpc_denied_ok", "rpc_bad_reject_stat",
-    "rpc_bad_reply_stat"])
+    "rpc_bad_reply_stat", "vecrec_ok", "vecrec_vals_over_bound", "vecrec_pointer_two",
+    "vecrec_pairs_past_end", "vecrec_bool2"])
 def test_reference_error_cases(dev, kat, case):
     """Decode the reference's error inputs; exception class and what() must
     equal what the reference threw (tests/golden/kat.json)."""
@@ -199,7 +200,7 @@ def _gpu_err(fn):
     return None
 
 
-@pytest.mark.parametrize("name", ["numerics_v", "recvar", "rpc"])
+@pytest.mark.parametrize("name", ["numerics_v", "recvar", "rpc", "vecrec"])
 @pytest.mark.parametrize("seed", range(6))
 def test_fuzzed_stream_errors_match_oracle(dev, name, seed):
     """Flip random bytes of a valid batch stream; the first failing record,
@@ -340,7 +341,7 @@ def forced(request):
     L.xdrg__force_var_kernels(0, 0)
 
 
-@pytest.mark.parametrize("name", ["recvar", "rpc"])
+@pytest.mark.parametrize("name", ["recvar", "rpc", "vecrec"])
 @pytest.mark.parametrize("n", [1, 63, 65, 1024])
 def test_var_kernels_golden(dev, forced, name, n):
     p = plan(name)
@@ -359,7 +360,7 @@ def test_var_kernels_golden(dev, forced, name, n):
     assert np.array_equal(bheap.cpu().numpy(), o_heap)
 
 
-@pytest.mark.parametrize("name", ["recvar", "rpc"])
+@pytest.mark.parametrize("name", ["recvar", "rpc", "vecrec"])
 @pytest.mark.parametrize("seed", range(3))
 def test_var_kernels_fuzzed_errors(dev, forced, name, seed):
     n = SMALL_N[name]
@@ -376,7 +377,7 @@ def test_var_kernels_fuzzed_errors(dev, forced, name, seed):
     assert got == want
 
 
-@pytest.mark.parametrize("name", ["recvar", "rpc"])
+@pytest.mark.parametrize("name", ["recvar", "rpc", "vecrec"])
 def test_var_kernels_capacity_and_stack(dev, forced, name):
     n = 300
     p = plan(name)

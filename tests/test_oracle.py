@@ -30,7 +30,7 @@ from xdrpp_amd import schemas as S
 from xdrpp_amd import workloads as W
 from xdrpp_amd.xdr_types import compile_plan
 
-SCHEMAS = ["numerics", "rec128", "recvar", "rpc"]
+SCHEMAS = ["numerics", "rec128", "recvar", "rpc", "vecrec"]
 CP = {k: compile_plan(t) for k, t in S.ALL.items()}
 CP["numerics_v"] = compile_plan(S.numerics_validated)
 
@@ -48,7 +48,8 @@ def test_generator_matches_reference_fixture(name):
     assert np.array_equal(heap, golden(name, n, "heap"))
 
 
-@pytest.mark.parametrize("key", ["numerics_65536", "recvar_65536", "rpc_65536", "rec128_1048576"])
+@pytest.mark.parametrize("key", ["numerics_65536", "recvar_65536", "rpc_65536", "vecrec_65536",
+                                 "rec128_1048576"])
 def test_generator_matches_manifest(manifest, key):
     name, n = key.rsplit("_", 1)
     h = manifest["hashes"][key]
@@ -57,7 +58,7 @@ def test_generator_matches_manifest(manifest, key):
     assert sha(heap) == h["heap"]
 
 
-@pytest.mark.parametrize("name", ["numerics", "rec128", "recvar", "rpc"])
+@pytest.mark.parametrize("name", ["numerics", "rec128", "recvar", "rpc", "vecrec"])
 def test_generator_first_is_a_slice(name):
     """Shard generation (first=k) reproduces records [k, k+n) of the batch."""
     nat, heap = W.GENERATORS[name](96)
@@ -99,7 +100,8 @@ def test_oracle_decode_golden(name):
         assert np.array_equal(offs2, offs)
 
 
-@pytest.mark.parametrize("key", ["numerics_65536", "recvar_65536", "rpc_65536", "rec128_1048576"])
+@pytest.mark.parametrize("key", ["numerics_65536", "recvar_65536", "rpc_65536", "vecrec_65536",
+                                 "rec128_1048576"])
 def test_oracle_full_size_hash(manifest, key):
     name, n = key.rsplit("_", 1)
     n = int(n)
@@ -156,7 +158,8 @@ EXC_NAME = {"xdr_overflow": M.XdrOverflow, "xdr_stack_overflow": M.XdrStackOverf
     "numerics_bool2", "numerics_enum99_novalidate", "numerics_enum99_validate",
     "recvar_ok", "recvar_nonzero_pad", "recvar_blob_over_bound", "recvar_name_over_bound",
     "recvar_len_past_end", "rpc_ok", "rpc_bad_mtype", "rpc_denied_ok", "rpc_bad_reject_stat",
-    "rpc_bad_reply_stat"])
+    "rpc_bad_reply_stat", "vecrec_ok", "vecrec_vals_over_bound", "vecrec_pointer_two",
+    "vecrec_pairs_past_end", "vecrec_bool2"])
 def test_oracle_reference_error_cases(kat, case):
     """The oracle's (code, op) for the reference's error inputs, mapped by
     the product's host error path, gives the exception class and what()

@@ -13,10 +13,11 @@ import os
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libxdrgpu.so")
 
 # enum xdrg_op_kind
-OP_U32, OP_U64, OP_BOOL, OP_ENUM, OP_OPAQUE, OP_VAROPAQUE, OP_STRING, OP_UNION, OP_JUMP, OP_END = range(1, 11)
+OP_U32, OP_U64, OP_BOOL, OP_ENUM, OP_OPAQUE, OP_VAROPAQUE, OP_STRING, OP_UNION, OP_JUMP, OP_END, OP_VECTOR = range(1, 12)
 ABI_VERSION = 1  # XDRG_ABI_VERSION, include/xdrgpu.h
 F_VALIDATE = 1
 F_DEFAULT = 2
+F_POINTER = 4
 
 PATH_FIXED_REG, PATH_FIXED_LDS, PATH_VAR = 1, 2, 3
 
@@ -36,6 +37,7 @@ ERR_STACK_PUT = 8
 ERR_STACK_GET = 9
 ERR_SIZE_NOT_MULT4 = 10
 ERR_TRAILING = 11
+ERR_POINTER_BOUND = 12
 
 XDR_MAX_LEN = 0xFFFFFFFC  # xdrpp/types.h:360
 DEFAULT_STACK_LIMIT = 0xFFFFFFFF  # xdrpp/marshal.cc:6
@@ -91,6 +93,7 @@ EXPORTED = (
     "xdrg_workspace_size", "xdrg_status_init", "xdrg_status_read", "xdrg_encode",
     "xdrg_decode", "xdrg_serial_sizes", "xdrg_swap32", "xdrg_swap64",
     "xdrg_error_message", "xdrg_error_exception", "xdrg_last_hip_error",
+    "xdrg_decode_heap_size",
 )
 
 _lib = None
@@ -134,6 +137,8 @@ def lib() -> C.CDLL:
     L.xdrg_swap32.restype = C.c_int
     L.xdrg_swap64.argtypes = [vp, vp, u64, vp]
     L.xdrg_swap64.restype = C.c_int
+    L.xdrg_decode_heap_size.argtypes = [vp, u64]
+    L.xdrg_decode_heap_size.restype = u64
     L.xdrg_error_message.argtypes = [C.c_int]
     L.xdrg_error_message.restype = C.c_char_p
     L.xdrg_error_exception.argtypes = [C.c_int]

@@ -126,10 +126,41 @@ int compile_plan(xdrg_plan &p) {
   if (n == 0 || p.stride == 0) return XDRG_EINVAL;
   bool fixed = true, saw_end = false;
   p.max_depth = 0;
+  p.has_vector = false;
+  p.heap_factor = 0;
   for (uint32_t i = 0; i < n; ++i) {
-    const xdrg_op &op = p.ops[i];
-    if (op.kind < XDRG_OP_U32 || op.kind > XDRG_OP_END) return XDRG_EINVAL;
+    xdrg_op &op = p.ops[i];
+    if (op.kind < XDRG_OP_U32 || op.kind > XDRG_OP_VECTOR) return XDRG_EINVAL;
     if (op.kind == XDRG_OP_END) { saw_end = true; continue; }
+    if (op.kind == XDRG_OP_VECTOR) {
+      // xvector<T,arg0> / pointer<T>: element ops inline in [i+1, i+1+arg2)
+      const uint32_t b0 = i + 1, b1 = i + 1 + op.arg2;
+      if (op.arg2 == 0 || b1 >= n || op.arg1 == 0) return XDRG_EINVAL;
+      if ((op.flags & XDRG_F_POINTER) && op.arg0 != 1) return XDRG_EINVAL;
+      if ((op.noff & 7) || uint64_t(op.noff) + sizeof(xdrg_bytes_ref) > p.stride) return XDRG_EINVAL;
+      uint32_t we = 0;
+      for (uint32_t k = b0; k < b1; ++k) {
+        const xdrg_op &e = p.ops[k];
+        if (!is_fixed_kind(e.kind)) return XDRG_EUNSUPPORTED;  // fixed-size elements only
+        if (uint64_t(e.noff) + native_size(e) > op.arg1) return XDRG_EINVAL;
+        if ((e.kind == XDRG_OP_U32 || e.kind == XDRG_OP_ENUM || e.kind == XDRG_OP_U64) && (e.noff & 3))
+          return XDRG_EINVAL;
+        if (e.kind == XDRG_OP_ENUM && (e.flags & XDRG_F_VALIDATE) &&
+            uint64_t(e.arg0) + e.arg1 > p.table.size())
+          return XDRG_EINVAL;
+        if (e.depth < op.depth) return XDRG_EINVAL;  // elements sit inside the container level
+        we += e.kind == XDRG_OP_U64 ? 8u : e.kind == XDRG_OP_OPAQUE ? pad4(e.arg0) : 4u;
+        p.max_depth = std::max<uint32_t>(p.max_depth, e.depth);
+      }
+      if (we == 0) return XDRG_EUNSUPPORTED;
+      op.arg3 = we;  // element wire size, used by the kernels
+      p.heap_factor = std::max<uint32_t>(p.heap_factor, (op.arg1 + we - 1) / we + 1u);
+      p.has_vector = true;
+      p.max_depth = std::max<uint32_t>(p.max_depth, op.depth);
+      fixed = false;
+      i = b1 - 1;
+      continue;
+    }
     if (op.kind == XDRG_OP_JUMP) {
       if (op.arg0 >= n || op.arg0 <= i) return XDRG_EINVAL;  // forward jumps only
       fixed = false;
@@ -178,6 +209,13 @@ int compile_plan(xdrg_plan &p) {
         best = slots[op.arg0]; bw = words[op.arg0]; bp = pieces[op.arg0]; bb = bytes[op.arg0];
         bc = chunks[op.arg0];
         break;
+      case XDRG_OP_VECTOR: {
+        const uint32_t nx = i + 1 + op.arg2;
+        best = slots[nx]; bp = pieces[nx]; bc = chunks[nx];
+        bw = words[nx] + 1u;  // the count word; elements are unbounded scalar words
+        bb = bytes[nx] + 4ull + uint64_t(op.arg0) * op.arg3;
+        break;
+      }
       case XDRG_OP_UNION:
         for (uint32_t c = 0; c < op.arg3; ++c) {
           const uint32_t t = p.table[op.arg2 + 2 * c + 1];
@@ -221,6 +259,7 @@ int compile_plan(xdrg_plan &p) {
     p.max_record_bytes = bytes[0];
     for (const xdrg_op &op : p.ops)
       if (op.kind == XDRG_OP_VAROPAQUE || op.kind == XDRG_OP_STRING || op.kind == XDRG_OP_UNION ||
+          op.kind == XDRG_OP_VECTOR ||
           op.kind == XDRG_OP_OPAQUE || (op.kind == XDRG_OP_ENUM && (op.flags & XDRG_F_VALIDATE)))
         p.has_checks = true;
     return XDRG_OK;

@@ -106,6 +106,115 @@ __device__ __forceinline__ uint32_t keep_bytes(int32_t k) {  // mask of the low 
 
 constexpr uint32_t kSizeErr = 0x80000000u;
 
+
+// ------------------------------------------- var: xvector<T> / pointer<T>
+// Elements of a VECTOR op (fixed-size element plans; ops [b0, b0+nb)).
+// Each element field checks the stack budget (the element's class level)
+// and the remaining space before it is archived, as xdr_generic_put/get
+// do field by field (marshal.h:110-136, 186-205).
+__device__ __forceinline__ uint32_t elem_wire_bytes(const xdrg_op &e) {
+  return e.kind == XDRG_OP_U64 ? 8u : e.kind == XDRG_OP_OPAQUE ? (e.arg0 + 3u) & ~3u : 4u;
+}
+
+// Encode: native elements from the heap at eoff (stride `es`); put(at, w)
+// stores wire word w at stretch offset `at`.
+template <typename PUT>
+__device__ bool enc_vector_elems(const xdrg_op *__restrict__ ops, uint32_t b0, uint32_t nb,
+                                 const uint8_t *__restrict__ heap, uint64_t heap_len, uint64_t eoff,
+                                 uint32_t cnt, uint32_t es, uint64_t &pos, uint64_t cap,
+                                 uint32_t &at, uint32_t stack_limit, uint64_t r,
+                                 unsigned long long *err, const PUT &put) {
+  for (uint32_t i = 0; i < cnt; ++i) {
+    const uint64_t eb = eoff + static_cast<uint64_t>(i) * es;
+    for (uint32_t k = 0; k < nb; ++k) {
+      const xdrg_op e = ops[b0 + k];
+      if (e.depth > stack_limit) { report(err, r, b0 + k, XDRG_ERR_STACK_PUT); return false; }
+      const uint32_t wb = elem_wire_bytes(e);
+      if (wb > cap - min(pos, cap)) { report(err, r, b0 + k, XDRG_ERR_OVERFLOW_PUT); return false; }
+      const uint64_t f = eb + e.noff;
+      switch (e.kind) {
+      case XDRG_OP_BOOL:
+        put(at, (unaligned_word(heap, heap_len, f) & 0xffu) ? 0x01000000u : 0u);
+        break;
+      case XDRG_OP_U64:
+        put(at, bswap32(unaligned_word(heap, heap_len, f + 4)));
+        put(at + 4, bswap32(unaligned_word(heap, heap_len, f)));
+        break;
+      case XDRG_OP_OPAQUE:
+        for (uint32_t w = 0; 4u * w < e.arg0; ++w) {
+          uint32_t x = unaligned_word(heap, heap_len, f + 4u * w);
+          if (4u * w + 4u > e.arg0) x &= keep_mask(e.arg0 - 4u * w);
+          put(at + 4u * w, x);
+        }
+        break;
+      default:  // U32, ENUM
+        put(at, bswap32(unaligned_word(heap, heap_len, f)));
+        break;
+      }
+      at += wb;
+      pos += wb;
+    }
+  }
+  return true;
+}
+
+// Decode: wire words through rd(pos); native elements written to `dst`
+// (stride `es`, zero-filled first).  p advances; b = end of the record.
+template <typename RD>
+__device__ bool dec_vector_elems(const xdrg_op *__restrict__ ops, const uint32_t *__restrict__ table,
+                                 uint32_t b0, uint32_t nb, uint32_t cnt, uint32_t es, uint8_t *dst,
+                                 uint64_t &p, uint64_t b, uint32_t stack_limit, uint64_t r,
+                                 unsigned long long *err, const RD &rd) {
+  const bool w4 = (es & 3u) == 0;  // 4-byte stores (dst is 8-aligned)
+  for (uint32_t i = 0; i < cnt; ++i) {
+    uint8_t *el = dst + static_cast<uint64_t>(i) * es;
+    if (w4) for (uint32_t z = 0; z < es; z += 4) st32(el + z, 0u);
+    else for (uint32_t z = 0; z < es; ++z) el[z] = 0;
+    for (uint32_t k = 0; k < nb; ++k) {
+      const xdrg_op e = ops[b0 + k];
+      if (e.depth > stack_limit) { report(err, r, b0 + k, XDRG_ERR_STACK_GET); return false; }
+      const uint32_t need = e.kind == XDRG_OP_U64 ? 8u : e.kind == XDRG_OP_OPAQUE ? e.arg0 : 4u;
+      if (b - p < need) { report(err, r, b0 + k, XDRG_ERR_OVERFLOW_GET); return false; }
+      uint8_t *f = el + e.noff;
+      switch (e.kind) {
+      case XDRG_OP_BOOL:
+        f[0] = rd(p) != 0u;
+        break;
+      case XDRG_OP_U64: {
+        const uint32_t hi = bswap32(rd(p)), lo = bswap32(rd(p + 4));
+        if (w4) { st32(f, lo); st32(f + 4, hi); }
+        else for (int q = 0; q < 4; ++q) { f[q] = uint8_t(lo >> (8 * q)); f[4 + q] = uint8_t(hi >> (8 * q)); }
+        break;
+      }
+      case XDRG_OP_OPAQUE: {
+        const uint32_t BL = e.arg0;
+        for (uint32_t q = 0; q < BL; q += 4) {
+          const uint32_t w = rd(p + q);
+          for (uint32_t bb = 0; bb < 4u && q + bb < BL; ++bb) f[q + bb] = uint8_t(w >> (8 * bb));
+        }
+        if ((BL & 3u) && (rd(p + (BL & ~3u)) & ~keep_mask(BL & 3u))) {
+          report(err, r, b0 + k, XDRG_ERR_NONZERO_PAD);
+          return false;
+        }
+        break;
+      }
+      default: {  // U32, ENUM
+        const uint32_t v = bswap32(rd(p));
+        if (w4) st32(f, v);
+        else for (int q = 0; q < 4; ++q) f[q] = uint8_t(v >> (8 * q));
+        if (e.kind == XDRG_OP_ENUM && (e.flags & XDRG_F_VALIDATE) && !enum_ok(table, e.arg0, e.arg1, v)) {
+          report(err, r, b0 + k, XDRG_ERR_INVALID_ENUM);
+          return false;
+        }
+        break;
+      }
+      }
+      p += elem_wire_bytes(e);
+    }
+  }
+  return true;
+}
+
 // -------------------------------------------------------- var: size pass
 // xdr_traits<T>::serial_size per record and bad discriminants
 // (gen_hh.cc:639-648).  The stack budget is a put-side check
@@ -187,6 +296,10 @@ __global__ __launch_bounds__(64) void k_var_size(const uint8_t *__restrict__ nat
       else pc = static_cast<uint32_t>(t);
       break;
     }
+    case XDRG_OP_VECTOR:  // count word + count fixed-size elements (arg3 = element wire bytes)
+      s += 4ull + static_cast<uint64_t>(*reinterpret_cast<const uint32_t *>(nat + op.noff + 8)) * op.arg3;
+      pc = upc + 1 + op.arg2;
+      break;
     default: s += 4; ++pc; break;
     }
   }
@@ -345,6 +458,19 @@ __global__ __launch_bounds__(256) void k_var_encode(
       pc = static_cast<uint32_t>(union_target(op, table, d));  // validated by k_var_size
       break;
     }
+    case XDRG_OP_VECTOR: {
+      const uint64_t eoff = *reinterpret_cast<const uint64_t *>(nat + op.noff);
+      const uint32_t cnt = ld32(nat + op.noff + 8);
+      o[0] = bswap32(cnt);
+      pos += 4;
+      uint32_t at = static_cast<uint32_t>(pos - off);
+      auto put = [&](uint32_t a, uint32_t w) { st32(xdr + off + a, w); };
+      if (!enc_vector_elems(sops, pc + 1, op.arg2, heap, heap_len, eoff, cnt, op.arg1, pos, cap, at,
+                            stack_limit, r, err, put))
+        return;
+      pc += 1 + op.arg2;
+      break;
+    }
     default: ++pc; break;
     }
   }
@@ -358,7 +484,8 @@ __global__ __launch_bounds__(256) void k_var_encode(
 __global__ __launch_bounds__(256) void k_var_decode(
     const uint8_t *__restrict__ xdr, uint64_t len, const uint64_t *__restrict__ offsets, uint64_t n,
     uint8_t *__restrict__ native, uint32_t stride, const xdrg_op *__restrict__ ops, uint32_t nops,
-    const uint32_t *__restrict__ table, uint32_t stack_limit, unsigned long long *err) {
+    const uint32_t *__restrict__ table, uint32_t stack_limit, uint8_t *__restrict__ heap,
+    uint64_t ebase, uint32_t F, unsigned long long *err) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   xdrg_op *sops = reinterpret_cast<xdrg_op *>(smem);
   load_ops(sops, ops, nops);
@@ -371,6 +498,7 @@ __global__ __launch_bounds__(256) void k_var_decode(
   uint8_t *nat = native + r * stride;
   for (uint32_t k = 0; k < stride / 4; ++k) st32(nat + 4 * k, 0u);
   uint64_t p = a;
+  uint64_t ecur = ebase + static_cast<uint64_t>(F) * a;  // this record's element arrays
   uint32_t pc = 0;
   for (;;) {
     const xdrg_op &op = sops[pc];
@@ -439,6 +567,25 @@ __global__ __launch_bounds__(256) void k_var_decode(
       if (t < 0) { report(err, r, pc, XDRG_ERR_BAD_DISCRIMINANT); return; }
       st32(nat + op.noff, d);
       pc = static_cast<uint32_t>(t);
+      break;
+    }
+    case XDRG_OP_VECTOR: {
+      if (rem < 4) goto overflow;
+      const uint32_t cnt = bswap32(ld32(xdr + p));
+      p += 4;
+      if (cnt > op.arg0) {  // check_size (types.h:486-489, 605-608)
+        report(err, r, pc, (op.flags & XDRG_F_POINTER) ? XDRG_ERR_POINTER_BOUND : XDRG_ERR_XVECTOR_BOUND);
+        return;
+      }
+      ecur = (ecur + 7u) & ~7ull;
+      *reinterpret_cast<uint64_t *>(nat + op.noff) = ecur;
+      st32(nat + op.noff + 8, cnt);
+      auto rd = [&](uint64_t q) { return ld32(xdr + q); };
+      if (!dec_vector_elems(sops, table, pc + 1, op.arg2, cnt, op.arg1, heap + ecur, p, b,
+                            stack_limit, r, err, rd))
+        return;
+      ecur += static_cast<uint64_t>(cnt) * op.arg1;
+      pc += 1 + op.arg2;
       break;
     }
     default: ++pc; break;
@@ -828,6 +975,21 @@ __global__ __launch_bounds__(64) void k_var_encode_i(
         pc = static_cast<uint32_t>(union_target(op, table, d));  // validated by k_var_size
         break;
       }
+      case XDRG_OP_VECTOR: {
+        const uint64_t eoff = *reinterpret_cast<const uint64_t *>(nw);
+        const uint32_t cnt = nw[2];
+        img_put(im, C, gout, at, bswap32(cnt));
+        at += 4; pos += 4;
+        auto put = [&](uint32_t a, uint32_t w) { img_put(im, C, gout, a, w); };
+        if (!enc_vector_elems(ops, upc + 1, op.arg2, heap, heap_len, eoff, cnt, op.arg1, pos, cap,
+                              at, stack_limit, r, err, put)) {
+          ok = false;
+          pc = kPcDone;
+          break;
+        }
+        pc = upc + 1 + op.arg2;
+        break;
+      }
       default: ++pc; break;
       }
     }
@@ -962,7 +1124,8 @@ __global__ __launch_bounds__(64) void k_var_decode_w(
     const uint8_t *__restrict__ xdr, uint64_t len, const uint64_t *__restrict__ offsets, uint64_t n,
     uint8_t *__restrict__ native, uint32_t stride, uint8_t *__restrict__ heap,
     const xdrg_op *__restrict__ ops, uint32_t nops, const uint32_t *__restrict__ table,
-    uint32_t stack_limit, uint32_t C, unsigned long long *err, unsigned long long *stamps) {
+    uint32_t stack_limit, uint32_t C, uint64_t ebase, uint32_t F, unsigned long long *err,
+    unsigned long long *stamps) {
   extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
   unsigned long long stv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   XDRG_STAMP(0);
@@ -1050,6 +1213,7 @@ __global__ __launch_bounds__(64) void k_var_decode_w(
       else pc = 0;
     }
     uint64_t p = a;
+    uint64_t ecur = ebase + static_cast<uint64_t>(F) * a;  // this record's element arrays
     bool ok = pc == 0u;
     for (uint32_t upc = 0; upc < nops; ++upc) {
       if (!__any(pc == upc)) continue;
@@ -1121,6 +1285,24 @@ __global__ __launch_bounds__(64) void k_var_decode_w(
         if (t < 0) { report(err, r, upc, XDRG_ERR_BAD_DISCRIMINANT); ok = false; pc = kPcDone; break; }
         nw[0] = d;
         pc = static_cast<uint32_t>(t);
+        break;
+      }
+      case XDRG_OP_VECTOR: {
+        const uint32_t cnt = bswap32(rd(p));
+        p += 4;
+        if (cnt > op.arg0) {  // check_size (types.h:486-489, 605-608)
+          report(err, r, upc, (op.flags & XDRG_F_POINTER) ? XDRG_ERR_POINTER_BOUND : XDRG_ERR_XVECTOR_BOUND);
+          ok = false; pc = kPcDone; break;
+        }
+        ecur = (ecur + 7u) & ~7ull;
+        *reinterpret_cast<uint64_t *>(nat + op.noff) = ecur;
+        nw[2] = cnt;
+        if (!dec_vector_elems(ops, table, upc + 1, op.arg2, cnt, op.arg1, heap + ecur, p, b,
+                              stack_limit, r, err, rd)) {
+          ok = false; pc = kPcDone; break;
+        }
+        ecur += static_cast<uint64_t>(cnt) * op.arg1;
+        pc = upc + 1 + op.arg2;
         break;
       }
       default: ++pc; break;
@@ -1271,6 +1453,11 @@ size_t var_ws_layout(uint64_t n, size_t *sizes_off, size_t *bsum_off) {
   return *bsum_off + align_up((nb + 1) * 8, 256);  // block sums / look-back flags + ticket
 }
 
+// Heap bytes xdrg_decode needs (include/xdrgpu.h xdrg_decode_heap_size).
+uint64_t decode_heap_bytes(const xdrg_plan &p, uint64_t len) {
+  return p.has_vector ? align_up(len, 16) + static_cast<uint64_t>(p.heap_factor) * len : len;
+}
+
 // Size pass (xdr_size per record + 64-record block sums).
 hipError_t launch_size_pass(const xdrg_plan &p, const uint8_t *nat, uint64_t n, uint32_t *sizes,
                             unsigned long long *bsum, unsigned long long *err, hipStream_t s) {
@@ -1392,6 +1579,10 @@ int xdrg_plan_get_info(const xdrg_plan *p, xdrg_plan_info *info) {
   return XDRG_OK;
 }
 
+uint64_t xdrg_decode_heap_size(const xdrg_plan *p, uint64_t len) {
+  return p ? decode_heap_bytes(*p, len) : 0;
+}
+
 size_t xdrg_workspace_size(const xdrg_plan *p, uint64_t n) {
   if (!p || p->path != XDRG_PATH_VAR) return 0;
   size_t a, b;
@@ -1467,7 +1658,8 @@ int xdrg_encode(const xdrg_plan *p, const void *d_native, uint64_t n, const uint
                     64ull * p->max_record_bytes < (1ull << 31) && LI.total <= kVarLdsBudget &&
                     aligned(d_native, 16);
   const enc_lds EL = enc_lds_layout(uint32_t(p->ops.size()), p->stride, p->max_scalar_words);
-  const bool ok_C = EL.total <= kVarLdsBudget && aligned(d_native, 16) && p->max_var_slots <= 4;
+  const bool ok_C = EL.total <= kVarLdsBudget && aligned(d_native, 16) && p->max_var_slots <= 4 &&
+                    !p->has_vector;  // its per-lane scalar-word array cannot bound element words
   int kern = g_force_enc;
   if (kern == 3 && !ok_I) kern = 0;
   if (kern == 2 && !ok_C) kern = 0;
@@ -1550,7 +1742,8 @@ int xdrg_decode(const xdrg_plan *p, const void *d_xdr, uint64_t len, const uint6
     if (len) return launch_report(err, 0, kOpRecordLevel, XDRG_ERR_TRAILING, s);
     return XDRG_OK;
   }
-  if (heap_cap < len || (len && !d_heap_out)) return XDRG_ESPACE;
+  if (heap_cap < decode_heap_bytes(*p, len) || (len && !d_heap_out)) return XDRG_ESPACE;
+  const uint64_t ebase = p->has_vector ? align_up(len, 16) : 0;  // decoded element arrays
   if (!aligned(d_xdr, 4) || !aligned(d_native, 8) || (d_heap_out && !aligned(d_heap_out, 4)))
     return XDRG_EALIGN;
   const uint8_t *xdr8 = static_cast<const uint8_t *>(d_xdr);
@@ -1568,17 +1761,18 @@ int xdrg_decode(const xdrg_plan *p, const void *d_xdr, uint64_t len, const uint6
     const uint64_t nb = (n + 63) / 64;
     if (copy)
       k_var_decode_w<true><<<nb, 64, lw, s>>>(xdr8, len, d_offsets, n, nat8, p->stride, d_heap_out,
-                                              p->d_ops, nops, p->d_table, stack_limit, Cw, err,
-                                              g_stamps);
+                                              p->d_ops, nops, p->d_table, stack_limit, Cw, ebase,
+                                              p->heap_factor, err, g_stamps);
     else
       k_var_decode_w<false><<<nb, 64, lw, s>>>(xdr8, len, d_offsets, n, nat8, p->stride, d_heap_out,
-                                               p->d_ops, nops, p->d_table, stack_limit, Cw, err,
-                                               g_stamps);
+                                               p->d_ops, nops, p->d_table, stack_limit, Cw, ebase,
+                                               p->heap_factor, err, g_stamps);
   } else {
     if (copy && len) HIPCHK(hipMemcpyAsync(d_heap_out, d_xdr, len, hipMemcpyDeviceToDevice, s));
     const uint64_t nb = (n + 255) / 256;
     k_var_decode<<<nb, 256, p->ops.size() * sizeof(xdrg_op), s>>>(
-        xdr8, len, d_offsets, n, nat8, p->stride, p->d_ops, nops, p->d_table, stack_limit, err);
+        xdr8, len, d_offsets, n, nat8, p->stride, p->d_ops, nops, p->d_table, stack_limit,
+        d_heap_out, ebase, p->heap_factor, err);
   }
   HIPCHK(hipGetLastError());
   return XDRG_OK;
@@ -1632,6 +1826,7 @@ const char *xdrg_error_message(int code) {
   case XDRG_ERR_STACK_GET: return "stack overflow in xdr_generic_get";
   case XDRG_ERR_SIZE_NOT_MULT4: return "xdr_generic_get: message size not multiple of 4";
   case XDRG_ERR_TRAILING: return "unmarshaling did not consume whole message";
+  case XDRG_ERR_POINTER_BOUND: return "xdr::pointer size must be 0 or 1";
   default: return "unknown xdrgpu error";
   }
 }
@@ -1639,7 +1834,7 @@ const char *xdrg_error_message(int code) {
 int xdrg_error_exception(int code) {
   switch (code) {
   case XDRG_ERR_OVERFLOW_GET: case XDRG_ERR_OVERFLOW_PUT: case XDRG_ERR_XVECTOR_BOUND:
-  case XDRG_ERR_XSTRING_BOUND: return XDRG_EXC_OVERFLOW;
+  case XDRG_ERR_XSTRING_BOUND: case XDRG_ERR_POINTER_BOUND: return XDRG_EXC_OVERFLOW;
   case XDRG_ERR_NONZERO_PAD: return XDRG_EXC_SHOULD_BE_ZERO;
   case XDRG_ERR_BAD_DISCRIMINANT: return XDRG_EXC_BAD_DISCRIMINANT;
   case XDRG_ERR_INVALID_ENUM: return XDRG_EXC_INVARIANT_FAILED;

@@ -87,6 +87,11 @@ class Plan:
     def is_fixed(self) -> bool:
         return self.path != A.PATH_VAR
 
+    def decode_heap_bytes(self, xdr_len: int) -> int:
+        """Heap capacity decode needs (xdrg_decode_heap_size): the stream
+        verbatim, plus the element area of xvector/pointer fields."""
+        return int(A.lib().xdrg_decode_heap_size(self.handle, xdr_len))
+
     def workspace_bytes(self, n: int) -> int:
         return int(A.lib().xdrg_workspace_size(self.handle, n))
 
@@ -226,13 +231,15 @@ class Marshaler:
         s = _stream()
         native = torch.zeros(max(n, 1) * self.plan.stride, dtype=torch.uint8, device=self.device)
         heap = None
+        hsize = 0
         if not self.plan.is_fixed:
-            heap = torch.zeros(max(xdr.numel(), 4), dtype=torch.uint8, device=self.device)
+            hsize = self.plan.decode_heap_bytes(xdr.numel())
+            heap = torch.zeros(max(hsize, 4), dtype=torch.uint8, device=self.device)
         self.status.init(s)
         self.launch_decode(xdr, n, native, offsets=offsets, heap_out=heap,
                            stack_limit=stack_limit, stream=s)
         self.check(s)
-        return native[:n * self.plan.stride], (None if heap is None else heap[:xdr.numel()])
+        return native[:n * self.plan.stride], (None if heap is None else heap[:hsize])
 
 
 def to_opaque_batch(plan: Plan, native: torch.Tensor, n: int, heap: torch.Tensor | None = None,

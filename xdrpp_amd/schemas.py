@@ -12,8 +12,8 @@ messages equal the reference's ("bad value of mtype in _body_t", ...).
 """
 from __future__ import annotations
 
-from .xdr_types import (Bool, Double, Enum, Float, Hyper, Int, Opaque, OpaqueArray, String,
-                        Struct, UHyper, UInt, Union, Void)
+from .xdr_types import (Bool, Double, Enum, Float, Hyper, Int, Opaque, OpaqueArray, Pointer, String,
+                        Struct, UHyper, UInt, Union, Void, XVector)
 
 # ------------------------------------------------------------- numerics
 _COLOR_TAGS = {"RED": 0, "REDDER": 1, "REDDEST": 2}
@@ -76,4 +76,14 @@ rpc_body = Union("_body_t", "mtype", msg_type, [
 ])
 rpc_msg = Struct("rpc_msg", [("xid", UInt), ("body", rpc_body)])
 
-ALL = {"numerics": numerics, "rec128": rec128, "recvar": recvar, "rpc": rpc_msg}
+# --------------------------------------------------------------- vecrec
+# Counted and optional containers of fixed-size elements (xvector<T>,
+# pointer<T>; xdrpp/types.h:365-414, 476-512, 591-665):
+#   struct vpair { hyper h; bool b; };
+#   struct vecrec { unsigned id; int vals<16>; mismatch_info *opt;
+#                   vpair pairs<8>; bool flag; };
+vpair = Struct("vpair", [("h", Hyper), ("b", Bool)])
+vecrec = Struct("vecrec", [("id", UInt), ("vals", XVector(Int, 16)), ("opt", Pointer(mismatch_info)),
+                           ("pairs", XVector(vpair, 8)), ("flag", Bool)])
+
+ALL = {"numerics": numerics, "rec128": rec128, "recvar": recvar, "rpc": rpc_msg, "vecrec": vecrec}

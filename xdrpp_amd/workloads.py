@@ -23,6 +23,7 @@ SEED_REC128 = 0x5EED0002
 SEED_RECVAR = 0x5EED0003
 SEED_RPC = 0x5EED0004
 SEED_REC128_MGPU = 0x5EED0005
+SEED_VECREC = 0x5EED0006
 PAYLOAD_XOR = 0xB10BB10BB10BB10B
 
 _M1 = np.uint64(0xBF58476D1CE4E5B9)
@@ -200,7 +201,55 @@ def rpc(n: int, seed: int = SEED_RPC, first: int = 0) -> tuple[np.ndarray, np.nd
     return buf.reshape(-1), heap
 
 
-GENERATORS = {"numerics": numerics, "rec128": rec128, "recvar": recvar, "rpc": rpc}
+def vecrec(n: int, seed: int = SEED_VECREC, first: int = 0) -> tuple[np.ndarray, np.ndarray]:
+    """Records [first, first + n) of oracle/ref_objects.hh gen_vecrec; each
+    element array is staged in the heap 8-byte aligned, in field order."""
+    t = S.vecrec
+    o = t.offsets
+    d = _draws(seed, n, 6, first)
+    ps = seed ^ PAYLOAD_XOR
+    r = np.arange(first, first + n, dtype=np.uint64)
+    nv = (d[:, 1] % np.uint64(17)).astype(np.int64)
+    has = (d[:, 2] & np.uint64(1)).astype(np.int64)
+    npairs = (d[:, 3] % np.uint64(9)).astype(np.int64)
+    flag = ((d[:, 4] >> np.uint64(8)) & np.uint64(1)).astype(np.uint8)
+    vals = draw(ps, r[:, None] * np.uint64(32) + np.arange(16, dtype=np.uint64)[None, :])
+    vals = (vals & np.uint64(0xFFFFFFFF)).astype("<u4")                  # (n, 16)
+    optw = draw(ps, r * np.uint64(32) + np.uint64(16)).astype("<u8")     # low | high << 32
+    ph = draw(ps, r[:, None] * np.uint64(32) + np.uint64(17) + np.arange(8, dtype=np.uint64)[None, :])
+    pb = ((d[:, 5][:, None] >> np.arange(8, dtype=np.uint64)[None, :]) & np.uint64(1)).astype(np.uint8)
+    # element bytes per field, padded to 8 after each array
+    vals_b = vals.view(np.uint8).reshape(n, 64)
+    opt_b = optw.view(np.uint8).reshape(n, 8)
+    pair = np.zeros((n, 8, 16), dtype=np.uint8)
+    pair[:, :, 0:8] = ph.astype("<u8").view(np.uint8).reshape(n, 8, 8)
+    pair[:, :, 8] = pb
+    pair_b = pair.reshape(n, 128)
+    lens = np.stack([4 * nv, 8 * has, 16 * npairs], axis=1)              # bytes per array
+    padded = (lens + 7) & ~7
+    starts = np.zeros(3 * n, dtype=np.int64)
+    flat = padded.reshape(-1)
+    if flat.size > 1:
+        np.cumsum(flat[:-1], out=starts[1:])
+    starts = starts.reshape(n, 3)
+    cols = np.concatenate([vals_b, opt_b, pair_b], axis=1)              # (n, 200)
+    widths = [64, 8, 128]
+    mask = np.concatenate([np.arange(w)[None, :] < padded[:, k][:, None] for k, w in enumerate(widths)],
+                          axis=1)
+    # bytes past an array's length (its 8-byte pad) are zero
+    live = np.concatenate([np.arange(w)[None, :] < lens[:, k][:, None] for k, w in enumerate(widths)],
+                          axis=1)
+    heap = np.where(live, cols, 0).astype(np.uint8)[mask]
+    buf = np.zeros((n, t.size), dtype=np.uint8)
+    _put(buf, o["id"], d[:, 0] & np.uint64(0xFFFFFFFF), "<u4")
+    _put_ref(buf, o["vals"], starts[:, 0], nv)
+    _put_ref(buf, o["opt"], starts[:, 1], has)
+    _put_ref(buf, o["pairs"], starts[:, 2], npairs)
+    _put(buf, o["flag"], flag, "u1")
+    return buf.reshape(-1), heap
+
+
+GENERATORS = {"numerics": numerics, "rec128": rec128, "recvar": recvar, "rpc": rpc, "vecrec": vecrec}
 
 
 def generate(schema: str, n: int, chunk: int = 1 << 16) -> tuple[np.ndarray, np.ndarray]:

@@ -20,6 +20,8 @@ Each descriptor knows
 | Opaque(max)       | opaque_vec<N>    (opaque x<N>)         | types.h:515-524        |
 | String(max)       | xstring<N>       (string x<N>)         | types.h:530-587        |
 | XArray(t, n)      | xarray<T,N>      (T x[N])              | types.h:424-452        |
+| XVector(t, max)   | xvector<T,N>     (T x<N>), T fixed     | types.h:365-414,476-512|
+| Pointer(t)        | pointer<T>       (T *x), T fixed       | types.h:591-665        |
 | Struct            | xdrc struct + xdr_struct_base          | types.h:676-730, gen_hh.cc:212-250 |
 | Union             | xdrc union                             | gen_hh.cc:368-675      |
 """
@@ -31,7 +33,8 @@ from . import _abi as A
 
 __all__ = [
     "XdrType", "Int", "UInt", "Hyper", "UHyper", "Float", "Double", "Bool", "Enum",
-    "OpaqueArray", "Opaque", "String", "XArray", "Struct", "Union", "Void", "CompiledPlan",
+    "OpaqueArray", "Opaque", "String", "XArray", "XVector", "Pointer", "Struct", "Union", "Void",
+    "CompiledPlan",
     "compile_plan", "OP_DTYPE",
 ]
 
@@ -167,6 +170,40 @@ class XArray(XdrType):
         step = _align_up(self.elem.size, self.elem.align)
         for i in range(self.n):
             self.elem.emit(ctx, noff + i * step, depth + 1, f"{path}[{i}]")
+
+
+class XVector(XdrType):
+    """T x<N> for non-byte, fixed-size T (xvector<T,N>): a container level,
+    then a u32 count and the elements.  Staged as xdrg_bytes_ref {heap
+    offset, count} of an element array (stride = T's aligned size).  The
+    element's ops follow the VECTOR op inline (arg2 of them)."""
+
+    size, align = 16, 8
+    fixed_wire = None
+    pointer = False
+
+    def __init__(self, elem: XdrType, max_len: int = A.XDR_MAX_LEN):
+        if elem.fixed_wire is None:
+            raise NotImplementedError("xvector<T>/pointer<T> of variable-size T")
+        self.elem, self.max_len = elem, max_len
+        self.stride = _align_up(elem.size, elem.align)
+
+    def emit(self, ctx, noff, depth, path):
+        d = depth + 1  # container level (marshal.h:129-136)
+        upc = ctx.emit(A.OP_VECTOR, noff, d, path, A.F_POINTER if self.pointer else 0,
+                       self.max_len, self.stride)
+        start = len(ctx.ops)
+        self.elem.emit(ctx, 0, d, f"{path}[]")  # element-relative offsets
+        ctx.ops[upc][6] = len(ctx.ops) - start  # arg2 = number of element ops
+
+
+class Pointer(XVector):
+    """T *x (xdr::pointer<T>): a vector of at most one element."""
+
+    pointer = True
+
+    def __init__(self, elem: XdrType):
+        super().__init__(elem, 1)
 
 
 class Struct(XdrType):
