@@ -1344,7 +1344,7 @@ constexpr uint32_t kVarLdsBudget = 64u << 10;  // wave-cooperative var kernels
 // 3 = chunk-map image; decode 1 = per-lane, 2 = window.
 int g_force_enc = 0, g_force_dec = 0;
 uint32_t g_img_bytes = 4u << 10;   // encode LDS image per wave (tools/tune/ab_var.py)
-uint32_t g_win_bytes = 16u << 10;  // decode LDS window per wave (tools/tune/ab_var.py)
+uint32_t g_win_bytes = 4u << 10;   // decode LDS window per wave (tools/tune/ab_var.py)
 unsigned long long *g_stamps = nullptr;      // diagnostic phase stamps, decode (tuning)
 unsigned long long *g_stamps_enc = nullptr;  // diagnostic phase stamps, encode (tuning)
 

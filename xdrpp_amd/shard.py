@@ -32,7 +32,8 @@ def seed_for(schema: str, world: int) -> int:
     """rec128 on N>1 GPUs uses its own seed."""
     if schema == "rec128":
         return W.SEED_REC128 if world == 1 else W.SEED_REC128_MGPU
-    return {"numerics": W.SEED_NUMERICS, "recvar": W.SEED_RECVAR, "rpc": W.SEED_RPC}[schema]
+    return {"numerics": W.SEED_NUMERICS, "recvar": W.SEED_RECVAR, "rpc": W.SEED_RPC,
+            "vecrec": W.SEED_VECREC}[schema]
 
 
 def shard_inputs(schema: str, n_per_rank: int, rank: int, world: int
