@@ -13,6 +13,12 @@
  *                            (xdr_generic_put, xdrpp/marshal.h:84-137)
  *   xdrg_decode           <- xdr_from_opaque(bytes, r...)    xdrpp/marshal.h:299-306
  *                            (xdr_generic_get, xdrpp/marshal.h:142-211)
+ *   xdrg_encode_msgs      <- xdr_to_msg(r) per record       xdrpp/marshal.h:252-260
+ *                            (record mark: message_t::alloc, xdrpp/marshal.cc:15-31)
+ *   xdrg_decode_msgs      <- xdr_from_msg(m, r) per message  xdrpp/marshal.h:278-284
+ *   xdrg_index_msgs       <- the record-mark framing of read_message /
+ *                            msg_sock::input                 xdrpp/srpc.cc:29-55,
+ *                                                            xdrpp/msgsock.cc:38-119
  *   xdrg_serial_sizes     <- xdr_argpack_size / xdr_size     xdrpp/marshal.h:223-234,
  *                                                            xdrpp/types.h:240-244
  *   xdrg_swap32/xdrg_swap64 <- swap32 / swap64               xdrpp/endian.h:56-68
@@ -46,7 +52,7 @@
 extern "C" {
 #endif
 
-#define XDRG_ABI_VERSION 1
+#define XDRG_ABI_VERSION 2
 
 /* ---------------------------------------------------------------------- */
 /* Plan ops: a flat, wire-ordered walk of xdr_traits<T>::save.             */
@@ -131,6 +137,8 @@ typedef struct xdrg_plan_info {
   uint32_t max_depth;     /* deepest op depth */
   uint32_t nops;
   uint32_t has_checks;    /* decode validates something (pads, enums) */
+  uint64_t max_record_bytes; /* largest wire record the plan's bounds allow
+                              * (fixed: fixed_size); a message's body bound */
 } xdrg_plan_info;
 
 /* ---------------------------------------------------------------------- */
@@ -161,7 +169,14 @@ enum xdrg_err {
   XDRG_ERR_STACK_GET = 9,       /* xdr_stack_overflow  marshal.h:200-201 */
   XDRG_ERR_SIZE_NOT_MULT4 = 10, /* xdr_bad_message_size marshal.h:157-159 */
   XDRG_ERR_TRAILING = 11,       /* xdr_bad_message_size marshal.h:207-210 */
-  XDRG_ERR_POINTER_BOUND = 12   /* xdr_overflow        types.h:605-608   */
+  XDRG_ERR_POINTER_BOUND = 12,  /* xdr_overflow        types.h:605-608   */
+  /* Record-marked message framing (RFC 5531 record marks of message_t). */
+  XDRG_ERR_MSG_EOF = 13,        /* xdr_bad_message_size srpc.cc:36-37,51-52 */
+  XDRG_ERR_MSG_SIZE4 = 14,      /* xdr_bad_message_size srpc.cc:38-39    */
+  XDRG_ERR_MSG_FRAGMENT = 15,   /* xdr_bad_message_size srpc.cc:42-45    */
+  XDRG_ERR_MSG_TOO_LONG = 16,   /* msg_sock maxmsglen_  msgsock.cc:99-111 */
+  XDRG_ERR_MSG_MISMATCH = 17,   /* mark disagrees with the record index  */
+  XDRG_ERR_MSG_COUNT = 18       /* more messages than the index can hold */
 };
 
 /* Exception class a data error maps to (for host-side rethrow). */
@@ -213,7 +228,8 @@ int xdrg_plan_create(const xdrg_op *ops, uint32_t nops, const uint32_t *table,
 void xdrg_plan_destroy(xdrg_plan *plan);
 int xdrg_plan_get_info(const xdrg_plan *plan, xdrg_plan_info *info);
 
-/* Workspace bytes encode/decode/serial_sizes need for n records. */
+/* Workspace bytes encode (var plans), encode_msgs (any plan) and
+ * serial_sizes need for n records. */
 size_t xdrg_workspace_size(const xdrg_plan *plan, uint64_t n);
 
 /* Zero a status block (first_error = all ones) on `stream`. */
@@ -266,6 +282,66 @@ int xdrg_decode(const xdrg_plan *plan, const void *d_xdr, uint64_t xdr_len,
  * align16(xdr_len) + F * off[i] (F = 1 + the largest native/wire size ratio
  * of an element type, so no extra pass is needed), each 8-byte aligned. */
 uint64_t xdrg_decode_heap_size(const xdrg_plan *plan, uint64_t xdr_len);
+
+/* ---------------------------------------------------------------------- */
+/* Record-marked batches: message_t buffers (RFC 5531 record marking)      */
+/* ---------------------------------------------------------------------- */
+/*
+ * A message is a 4-byte record mark BE(size | 0x80000000) followed by
+ * `size` bytes: message_t's raw_data()/raw_size() (xdrpp/message.h:33-64,
+ * mark written by message_t::alloc, xdrpp/marshal.cc:15-31).  A batch is
+ * messages back to back, which is what msg_sock::output writes for a queue
+ * of messages (xdrpp/msgsock.cc:158-188) and what read_message /
+ * msg_sock::input read (xdrpp/srpc.cc:29-55, msgsock.cc:38-119).
+ */
+#define XDRG_MARK_LAST 0x80000000u
+/* Largest max_msg_len xdrg_index_msgs accepts (its segment window). */
+#define XDRG_INDEX_MAX_MSG 16380u
+
+/*
+ * Encode n records as n messages: message i = xdr_to_msg(r_i)
+ * (xdrpp/marshal.h:252-260).  Arguments as xdrg_encode; d_offsets is
+ * required for every plan: d_offsets[i] = byte offset of message i's mark,
+ * d_offsets[n] = total bytes.  The workspace is xdrg_workspace_size bytes.
+ */
+int xdrg_encode_msgs(const xdrg_plan *plan, const void *d_native, uint64_t n,
+                     const uint8_t *d_heap, uint64_t heap_len, void *d_out,
+                     uint64_t out_capacity, uint64_t *d_offsets, uint32_t stack_limit,
+                     void *d_workspace, size_t workspace_bytes, xdrg_status *d_status,
+                     void *stream);
+
+/*
+ * Decode n messages: message i occupies [d_offsets[i], d_offsets[i+1]) of
+ * the stream (mark included) and decodes as xdr_from_msg(m_i, r_i)
+ * (xdrpp/marshal.h:278-284).  The mark must be a last-fragment mark whose
+ * size is the message's byte count (XDRG_ERR_MSG_* otherwise).  Heap
+ * contract as xdrg_decode (refs are stream offsets); for plans without
+ * opaque<>/string<>/xvector fields d_heap_out may be NULL.
+ */
+int xdrg_decode_msgs(const xdrg_plan *plan, const void *d_stream, uint64_t len,
+                     const uint64_t *d_offsets, uint64_t n, void *d_native,
+                     uint8_t *d_heap_out, uint64_t heap_capacity, uint32_t stack_limit,
+                     void *d_workspace, size_t workspace_bytes, xdrg_status *d_status,
+                     void *stream);
+
+/*
+ * Record index of a stream of messages, computed on the device: the
+ * framing of read_message (srpc.cc:29-55) applied message after message,
+ * plus msg_sock's length limit (maxmsglen_, msgsock.cc:99-111).  Writes
+ * d_offsets[k] = byte offset of mark k for every message k, d_offsets[count]
+ * = len, and *d_count (a device u64) = count.  On a framing error at
+ * message k (premature EOF, fragment bit clear, size bits, too long, size
+ * not a multiple of 4) the error is reported at record k through d_status,
+ * *d_count = k and d_offsets[k] = the failing mark's offset.  At most
+ * max_msgs messages are indexed (d_offsets holds max_msgs + 1 entries);
+ * more is XDRG_ERR_MSG_COUNT at record max_msgs.  Entries past count are
+ * unspecified.  max_msg_len <= XDRG_INDEX_MAX_MSG.
+ */
+int xdrg_index_msgs(const void *d_stream, uint64_t len, uint32_t max_msg_len,
+                    uint64_t max_msgs, uint64_t *d_offsets, uint64_t *d_count,
+                    void *d_workspace, size_t workspace_bytes, xdrg_status *d_status,
+                    void *stream);
+size_t xdrg_index_workspace_size(uint64_t len, uint32_t max_msg_len);
 
 /* Size pass alone: d_sizes[i] = xdr_size(record i) (uint32). */
 int xdrg_serial_sizes(const xdrg_plan *plan, const void *d_native, uint64_t n,

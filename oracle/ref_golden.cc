@@ -39,7 +39,7 @@ using std::vector;
 using namespace refobj;
 
 template <typename T>
-static void emit(const vector<T> &v, const string &prefix) {
+static void emit(const vector<T> &v, const string &prefix, bool with_msgs = true) {
   vector<uint8_t> nat;
   heap_t heap;
   stage(v, nat, heap);
@@ -67,6 +67,28 @@ static void emit(const vector<T> &v, const string &prefix) {
   write_file(prefix + ".heap", heap.b.data(), heap.b.size());
   write_file(prefix + ".xdr", out.data(), out.size());
   write_file(prefix + ".offsets", off.data(), off.size() * 8);
+  if (!with_msgs) return;
+  // The same records as messages: xdr_to_msg(r) per record (marshal.h:
+  // 252-260; mark by message_t::alloc, marshal.cc:15-31), raw_data() of
+  // raw_size() bytes each, back to back as msg_sock::output writes them;
+  // each message is also read back with xdr_from_msg.
+  vector<uint8_t> msgs;
+  vector<uint64_t> moff(v.size() + 1, 0);
+  msgs.reserve(out.size() + 4 * v.size());
+  for (size_t r = 0; r < v.size(); ++r) {
+    xdr::msg_ptr m = xdr::xdr_to_msg(v[r]);
+    moff[r] = msgs.size();
+    msgs.insert(msgs.end(), reinterpret_cast<const uint8_t *>(m->raw_data()),
+                reinterpret_cast<const uint8_t *>(m->raw_data()) + m->raw_size());
+    if (r % step == 0) {
+      T back{};
+      xdr::xdr_from_msg(m, back);
+      if (!same(back, v[r])) die("xdr_from_msg round trip differs at " + std::to_string(r));
+    }
+  }
+  moff[v.size()] = msgs.size();
+  write_file(prefix + ".msgs", msgs.data(), msgs.size());
+  write_file(prefix + ".msgoffs", moff.data(), moff.size() * 8);
 }
 
 // ------------------------------------------------------------- KAT / errors
@@ -120,6 +142,11 @@ static void kat(const string &path) {
   vector<testns::numerics> nv;
   gen_numerics(1, WG_SEED_NUMERICS, nv);
   o << "  \"numerics_marshal_cc\": \"" << enc(nv[0]) << "\",\n";
+  {
+    xdr::msg_ptr m = xdr::xdr_to_msg(nv[0]);  // message_t::alloc's mark + the record
+    o << "  \"numerics_msg\": \"" << hex(reinterpret_cast<const uint8_t *>(m->raw_data()), m->raw_size())
+      << "\",\n";
+  }
   // rec128 record 0 of the benchmark stream
   vector<rec128> rv;
   gen_rec128(1, WG_SEED_REC128, 0, rv);
@@ -302,14 +329,15 @@ int main(int argc, char **argv) {
   string schema = argv[2];
   size_t n = std::stoull(argv[3]);
   if (mode == "gen") {
-    if (argc != 5) die("gen <schema> <n> <prefix>");
+    if (argc != 5 && argc != 6) die("gen <schema> <n> <prefix> [nomsgs]");
     string pre = argv[4];
-    if (schema == "numerics") { vector<testns::numerics> v; gen_numerics(n, WG_SEED_NUMERICS, v); emit(v, pre); }
-    else if (schema == "rec128") { vector<rec128> v; gen_rec128(n, WG_SEED_REC128, 0, v); emit(v, pre); }
-    else if (schema == "rec128_mgpu") { vector<rec128> v; gen_rec128(n, WG_SEED_REC128_MGPU, 0, v); emit(v, pre); }
-    else if (schema == "recvar") { vector<recvar> v; gen_recvar(n, WG_SEED_RECVAR, v); emit(v, pre); }
-    else if (schema == "vecrec") { vector<vecrec> v; gen_vecrec(n, WG_SEED_VECREC, v); emit(v, pre); }
-    else if (schema == "rpc") { vector<rpcx::rpc_msg> v; gen_rpc(n, WG_SEED_RPC, v); emit(v, pre); }
+    const bool wm = !(argc == 6 && string(argv[5]) == "nomsgs");
+    if (schema == "numerics") { vector<testns::numerics> v; gen_numerics(n, WG_SEED_NUMERICS, v); emit(v, pre, wm); }
+    else if (schema == "rec128") { vector<rec128> v; gen_rec128(n, WG_SEED_REC128, 0, v); emit(v, pre, wm); }
+    else if (schema == "rec128_mgpu") { vector<rec128> v; gen_rec128(n, WG_SEED_REC128_MGPU, 0, v); emit(v, pre, wm); }
+    else if (schema == "recvar") { vector<recvar> v; gen_recvar(n, WG_SEED_RECVAR, v); emit(v, pre, wm); }
+    else if (schema == "vecrec") { vector<vecrec> v; gen_vecrec(n, WG_SEED_VECREC, v); emit(v, pre, wm); }
+    else if (schema == "rpc") { vector<rpcx::rpc_msg> v; gen_rpc(n, WG_SEED_RPC, v); emit(v, pre, wm); }
     else die("unknown schema " + schema);
     return 0;
   }

@@ -425,3 +425,100 @@ int xdro_decode(const xdrg_op *ops, uint32_t nops, const uint32_t *table, uint32
   if (offsets[n] != len) { *erec = n; *eop = 0xffffffffu; return XDRG_ERR_TRAILING; }
   return 0;
 }
+
+/* ------------------------------------------------------ record-marked messages
+ * message_t framing (RFC 5531 record marking): a 4-byte mark
+ * BE(size | 0x80000000) before each message's bytes.
+ *   xdr_to_msg(r)          marshal.h:252-260, mark by message_t::alloc
+ *                          (marshal.cc:15-31)
+ *   xdr_from_msg(m, r)     marshal.h:278-284 (xdr_get over m->data())
+ *   read_message framing   srpc.cc:29-55; msg_sock's maxmsglen_
+ *                          msgsock.cc:85-111
+ */
+static inline uint32_t mark_code(uint32_t raw, uint64_t body) {
+  if (raw & 3) return XDRG_ERR_MSG_SIZE4;       /* srpc.cc:38-39, pre-swap test */
+  uint32_t v = bswap32(raw);
+  if (!(v & XDRG_MARK_LAST)) return XDRG_ERR_MSG_FRAGMENT; /* srpc.cc:41-45 */
+  if ((v & ~XDRG_MARK_LAST) != body) return XDRG_ERR_MSG_MISMATCH;
+  return 0;
+}
+
+/* n messages, message r = xdr_to_msg(record r). */
+int xdro_encode_msgs(const xdrg_op *ops, uint32_t nops, const uint32_t *table, uint32_t stride,
+                     const uint8_t *native, uint64_t n, const uint8_t *heap, uint64_t heap_len,
+                     uint8_t *out, uint64_t cap, uint64_t *offsets, uint32_t stack_limit,
+                     uint64_t *erec, uint32_t *eop, uint64_t *total) {
+  plan_t P = {ops, nops, table, stride};
+  uint64_t pos = 0;
+  for (uint64_t r = 0; r < n; ++r) {
+    const uint8_t *nat = native + r * stride;
+    uint32_t err = 0, op_i = 0;
+    if (offsets) offsets[r] = pos;
+    uint64_t size = rec_size(&P, nat, &err, &op_i);  /* xdr_argpack_size */
+    if (err) { *erec = r; *eop = op_i; return (int)err; }
+    if (4 > cap - pos) { *erec = r; *eop = 0xffffffffu; return XDRG_ERR_OVERFLOW_PUT; }
+    wr32(out + pos, bswap32((uint32_t)size | XDRG_MARK_LAST));
+    pos += 4;
+    uint64_t er = 0, sub = 0;
+    int rc = xdro_encode(ops, nops, table, stride, nat, 1, heap, heap_len, out + pos, cap - pos,
+                         NULL, stack_limit, &er, eop, &sub);
+    if (rc) { *erec = r; return rc; }
+    pos += sub;
+  }
+  if (offsets) offsets[n] = pos;
+  *total = pos;
+  return 0;
+}
+
+/* n messages indexed by offsets (message r = [off[r], off[r+1]), mark
+ * included), each decoded as xdr_from_msg. */
+int xdro_decode_msgs(const xdrg_op *ops, uint32_t nops, const uint32_t *table, uint32_t stride,
+                     const uint8_t *xdr, uint64_t len, const uint64_t *offsets, uint64_t n,
+                     uint8_t *native, uint8_t *heap_out, uint32_t stack_limit, uint64_t *erec,
+                     uint32_t *eop) {
+  plan_t P = {ops, nops, table, stride};
+  if (heap_out && len) memcpy(heap_out, xdr, len);
+  const uint32_t F = heap_factor(&P);
+  const uint64_t ebase = F ? ((len + 15) & ~15ull) : 0;
+  for (uint64_t r = 0; r < n; ++r) {
+    uint64_t a = offsets[r], b = offsets[r + 1];
+    if (b < a || b > len) { *erec = r; *eop = 0; return XDRG_ERR_OVERFLOW_GET; }
+    uint32_t c = b - a < 4 ? (uint32_t)XDRG_ERR_MSG_EOF : mark_code(rd32(xdr + a), b - a - 4);
+    if (c) { *erec = r; *eop = 0xffffffffu; return (int)c; }
+    if ((b - a) & 3) { *erec = r; *eop = 0xffffffffu; return XDRG_ERR_SIZE_NOT_MULT4; }
+    const uint8_t *p = xdr + a + 4, *e = xdr + b;
+    int rc = dec_record(&P, &p, e, native + r * stride, xdr, heap_out, ebase + (uint64_t)F * a,
+                        stack_limit, eop);
+    if (rc) { *erec = r; return rc; }
+    if (p != e) { *erec = r; *eop = 0xffffffffu; return XDRG_ERR_TRAILING; }
+  }
+  if (offsets[n] != len) { *erec = n; *eop = 0xffffffffu; return XDRG_ERR_TRAILING; }
+  return 0;
+}
+
+/* read_message applied message after message over [s, s+len): offsets[k]
+ * = mark k, offsets[count] = len (or the failing mark on an error, which
+ * is returned with *erec = count).  A size that is not a multiple of 4
+ * stops the index there: xdr_from_msg rejects that message. */
+int xdro_index_msgs(const uint8_t *s, uint64_t len, uint32_t maxlen, uint64_t max_msgs,
+                    uint64_t *offsets, uint64_t *count, uint64_t *erec) {
+  uint64_t pos = 0, k = 0;
+  for (;;) {
+    offsets[k] = pos;
+    *count = k;
+    *erec = k;
+    if (pos == len) return 0;
+    if (k == max_msgs) return XDRG_ERR_MSG_COUNT;
+    if (len - pos < 4) return XDRG_ERR_MSG_EOF;            /* srpc.cc:33-37 */
+    uint32_t raw = rd32(s + pos);
+    if (raw & 3) return XDRG_ERR_MSG_SIZE4;                 /* srpc.cc:38-39 */
+    uint32_t v = bswap32(raw);
+    if (!(v & XDRG_MARK_LAST)) return XDRG_ERR_MSG_FRAGMENT;  /* srpc.cc:41-45 */
+    uint32_t size = v & ~XDRG_MARK_LAST;
+    if (size > maxlen) return XDRG_ERR_MSG_TOO_LONG;        /* msgsock.cc:99-111 */
+    if (len - pos - 4 < size) return XDRG_ERR_MSG_EOF;      /* srpc.cc:48-52 */
+    if (size & 3) return XDRG_ERR_SIZE_NOT_MULT4;           /* marshal.h:152-162 */
+    pos += 4 + (uint64_t)size;
+    ++k;
+  }
+}

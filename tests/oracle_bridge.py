@@ -39,6 +39,9 @@ def lib() -> C.CDLL:
         L.xdro_decode.argtypes = [vp, u32, vp, u32, vp, u64, vp, u64, vp, vp, u32,
                                   C.POINTER(u64), C.POINTER(u32)]
         L.xdro_sizes.argtypes = [vp, u32, vp, u32, vp, u64, vp, C.POINTER(u64), C.POINTER(u32)]
+        L.xdro_encode_msgs.argtypes = L.xdro_encode.argtypes
+        L.xdro_decode_msgs.argtypes = L.xdro_decode.argtypes
+        L.xdro_index_msgs.argtypes = [vp, u64, u32, u64, vp, C.POINTER(u64), C.POINTER(u64)]
         L.xdro_decode_heap_size.argtypes = [vp, u32, u64]
         L.xdro_decode_heap_size.restype = u64
         _lib = L
@@ -92,3 +95,55 @@ def decode(plan, xdr: np.ndarray, n: int, offsets: np.ndarray | None = None,
     if rc:
         raise OracleError(rc, er.value, eo.value)
     return native[:n * plan.stride], heap[:hsize]
+
+
+# ------------------------------------------------- record-marked messages
+def encode_msgs(plan, native: np.ndarray, n: int, heap: np.ndarray | None = None,
+                stack_limit: int = 0xFFFFFFFF, cap: int | None = None):
+    """xdr_to_msg of every record, back to back: (stream, offsets[n+1])."""
+    if heap is None or heap.size == 0:
+        heap = np.zeros(1, dtype=np.uint8)
+    er, eo = C.c_uint64(0), C.c_uint32(0)
+    if cap is None:
+        sizes = np.zeros(max(n, 1), dtype=np.uint32)
+        rc = lib().xdro_sizes(_p(plan.ops), len(plan.ops), _p(plan.table), plan.stride,
+                              _p(native), n, _p(sizes), C.byref(er), C.byref(eo))
+        cap = int(sizes[:n].astype(np.uint64).sum()) + 4 * n if rc == 0 else 1 << 20
+    out = np.zeros(max(cap, 4), dtype=np.uint8)
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    tot = C.c_uint64(0)
+    rc = lib().xdro_encode_msgs(_p(plan.ops), len(plan.ops), _p(plan.table), plan.stride,
+                                _p(native), n, _p(heap), heap.size, _p(out), cap, _p(offs),
+                                stack_limit, C.byref(er), C.byref(eo), C.byref(tot))
+    if rc:
+        raise OracleError(rc, er.value, eo.value)
+    return out[:tot.value], offs
+
+
+def decode_msgs(plan, stream: np.ndarray, n: int, offsets: np.ndarray,
+                stack_limit: int = 0xFFFFFFFF):
+    """xdr_from_msg of every indexed message: (native, heap)."""
+    native = np.zeros(max(n, 1) * plan.stride, dtype=np.uint8)
+    hsize = int(lib().xdro_decode_heap_size(_p(plan.ops), len(plan.ops), stream.size))
+    heap = np.zeros(max(hsize, 4), dtype=np.uint8)
+    er, eo = C.c_uint64(0), C.c_uint32(0)
+    x = stream if stream.size else np.zeros(4, dtype=np.uint8)
+    offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+    rc = lib().xdro_decode_msgs(_p(plan.ops), len(plan.ops), _p(plan.table), plan.stride,
+                                _p(x), stream.size, _p(offs), n, _p(native), _p(heap),
+                                stack_limit, C.byref(er), C.byref(eo))
+    if rc:
+        raise OracleError(rc, er.value, eo.value)
+    return native[:n * plan.stride], heap[:hsize]
+
+
+def index_msgs(stream: np.ndarray, max_msg_len: int, max_msgs: int | None = None):
+    """read_message framing over the stream: (rc, count, offsets[:count+1])."""
+    if max_msgs is None:
+        max_msgs = stream.size // 4
+    offs = np.zeros(max_msgs + 1, dtype=np.uint64)
+    cnt, erec = C.c_uint64(0), C.c_uint64(0)
+    x = stream if stream.size else np.zeros(4, dtype=np.uint8)
+    rc = lib().xdro_index_msgs(_p(x), stream.size, max_msg_len, max_msgs, _p(offs),
+                               C.byref(cnt), C.byref(erec))
+    return rc, int(cnt.value), offs[:cnt.value + 1]

@@ -59,7 +59,8 @@ def test_validated_enum_plan_has_checks():
 
 def test_workspace_size():
     fixed = M.Plan(S.rec128)
-    assert fixed.workspace_bytes(1 << 20) == 0
+    # fixed plans: encode needs none, encode_msgs (interpreter path) does
+    assert fixed.workspace_bytes(1 << 20) >= 4 * (1 << 20)
     var = M.Plan(S.recvar)
     w = [var.workspace_bytes(n) for n in (1, 1000, 1 << 20, 1 << 24)]
     assert all(x > 0 for x in w) and w == sorted(w)

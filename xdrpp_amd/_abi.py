@@ -14,7 +14,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libxdrgpu.s
 
 # enum xdrg_op_kind
 OP_U32, OP_U64, OP_BOOL, OP_ENUM, OP_OPAQUE, OP_VAROPAQUE, OP_STRING, OP_UNION, OP_JUMP, OP_END, OP_VECTOR = range(1, 12)
-ABI_VERSION = 1  # XDRG_ABI_VERSION, include/xdrgpu.h
+ABI_VERSION = 2  # XDRG_ABI_VERSION, include/xdrgpu.h
 F_VALIDATE = 1
 F_DEFAULT = 2
 F_POINTER = 4
@@ -38,6 +38,15 @@ ERR_STACK_GET = 9
 ERR_SIZE_NOT_MULT4 = 10
 ERR_TRAILING = 11
 ERR_POINTER_BOUND = 12
+ERR_MSG_EOF = 13
+ERR_MSG_SIZE4 = 14
+ERR_MSG_FRAGMENT = 15
+ERR_MSG_TOO_LONG = 16
+ERR_MSG_MISMATCH = 17
+ERR_MSG_COUNT = 18
+
+MARK_LAST = 0x80000000  # XDRG_MARK_LAST: last-fragment bit of a record mark
+INDEX_MAX_MSG = 16380   # XDRG_INDEX_MAX_MSG
 
 XDR_MAX_LEN = 0xFFFFFFFC  # xdrpp/types.h:360
 DEFAULT_STACK_LIMIT = 0xFFFFFFFF  # xdrpp/marshal.cc:6
@@ -69,6 +78,7 @@ class XdrgPlanInfo(C.Structure):
         ("max_depth", C.c_uint32),
         ("nops", C.c_uint32),
         ("has_checks", C.c_uint32),
+        ("max_record_bytes", C.c_uint64),
     ]
 
 
@@ -93,7 +103,8 @@ EXPORTED = (
     "xdrg_workspace_size", "xdrg_status_init", "xdrg_status_read", "xdrg_encode",
     "xdrg_decode", "xdrg_serial_sizes", "xdrg_swap32", "xdrg_swap64",
     "xdrg_error_message", "xdrg_error_exception", "xdrg_last_hip_error",
-    "xdrg_decode_heap_size",
+    "xdrg_decode_heap_size", "xdrg_encode_msgs", "xdrg_decode_msgs", "xdrg_index_msgs",
+    "xdrg_index_workspace_size",
 )
 
 _lib = None
@@ -131,6 +142,14 @@ def lib() -> C.CDLL:
     L.xdrg_encode.restype = C.c_int
     L.xdrg_decode.argtypes = [vp, vp, u64, vp, u64, vp, vp, u64, u32, vp, sz, vp, vp]
     L.xdrg_decode.restype = C.c_int
+    L.xdrg_encode_msgs.argtypes = [vp, vp, u64, vp, u64, vp, u64, vp, u32, vp, sz, vp, vp]
+    L.xdrg_encode_msgs.restype = C.c_int
+    L.xdrg_decode_msgs.argtypes = [vp, vp, u64, vp, u64, vp, vp, u64, u32, vp, sz, vp, vp]
+    L.xdrg_decode_msgs.restype = C.c_int
+    L.xdrg_index_msgs.argtypes = [vp, u64, u32, u64, vp, vp, vp, sz, vp, vp]
+    L.xdrg_index_msgs.restype = C.c_int
+    L.xdrg_index_workspace_size.argtypes = [u64, u32]
+    L.xdrg_index_workspace_size.restype = sz
     L.xdrg_serial_sizes.argtypes = [vp, vp, u64, vp, u32, vp, vp]
     L.xdrg_serial_sizes.restype = C.c_int
     L.xdrg_swap32.argtypes = [vp, vp, u64, vp]

@@ -191,12 +191,12 @@ int compile_plan(xdrg_plan &p) {
 
   p.has_checks = false;
   p.checks.clear();
-  if (!fixed) {
-    p.fixed_size = 0;
-    p.path = XDRG_PATH_VAR;
+  {
     // Longest count of var-length fields along any control path (jumps are
     // forward-only, so one reverse sweep over the DAG suffices).
     // Same sweep for the scalar (non-payload) wire words of a record.
+    // Computed for fixed plans too: record-marked batches of any plan run
+    // on the interpreter kernels, which size themselves with these.
     std::vector<uint32_t> slots(n, 0), words(n, 0);
     std::vector<uint64_t> pieces(n, 0), bytes(n, 0), chunks(n, 0);
     for (uint32_t i = n; i-- > 0;) {
@@ -257,6 +257,10 @@ int compile_plan(xdrg_plan &p) {
     p.max_scalar_words = words[0];
     p.max_pieces = uint32_t(std::min<uint64_t>(pieces[0], 0xffffffffu));
     p.max_record_bytes = bytes[0];
+  }
+  if (!fixed) {
+    p.fixed_size = 0;
+    p.path = XDRG_PATH_VAR;
     for (const xdrg_op &op : p.ops)
       if (op.kind == XDRG_OP_VAROPAQUE || op.kind == XDRG_OP_STRING || op.kind == XDRG_OP_UNION ||
           op.kind == XDRG_OP_VECTOR ||

@@ -106,6 +106,25 @@ __device__ __forceinline__ uint32_t keep_bytes(int32_t k) {  // mask of the low 
 
 constexpr uint32_t kSizeErr = 0x80000000u;
 
+// ------------------------------------------- record marks (RFC 5531)
+// message_t keeps a 4-byte mark BE(size | 0x80000000) in front of the
+// message bytes (message_t::alloc, xdrpp/marshal.cc:15-31: always one
+// last-fragment record).
+__device__ __forceinline__ uint32_t mark_word(uint32_t size) { return bswap32(size | XDRG_MARK_LAST); }
+
+// Framing checks of a message whose record index gives it `body` bytes
+// after the mark, in read_message's order (xdrpp/srpc.cc:29-55).  The
+// first test reads the mark before swap32le, so on a little-endian host it
+// looks at the low bits of the mark's first byte (bits 24-25 of the size),
+// which is what the reference does on this platform.  0 = well framed.
+__device__ __forceinline__ uint32_t mark_code(uint32_t raw, uint64_t body) {
+  if (raw & 3u) return XDRG_ERR_MSG_SIZE4;          // srpc.cc:38-39
+  const uint32_t v = bswap32(raw);
+  if (!(v & XDRG_MARK_LAST)) return XDRG_ERR_MSG_FRAGMENT;  // srpc.cc:41-45
+  if ((v & ~XDRG_MARK_LAST) != body) return XDRG_ERR_MSG_MISMATCH;
+  return 0u;
+}
+
 
 // ------------------------------------------- var: xvector<T> / pointer<T>
 // Elements of a VECTOR op (fixed-size element plans; ops [b0, b0+nb)).
@@ -253,7 +272,7 @@ __global__ __launch_bounds__(64) void k_var_size(const uint8_t *__restrict__ nat
                                                  uint32_t nops, const uint32_t *__restrict__ table,
                                                  uint32_t *__restrict__ sizes,
                                                  unsigned long long *__restrict__ block_sums,
-                                                 unsigned long long *err) {
+                                                 uint32_t mark, unsigned long long *err) {
   extern __shared__ __attribute__((aligned(16))) uint8_t tile[];
   const uint32_t lane = threadIdx.x;
   const uint64_t wr0 = static_cast<uint64_t>(blockIdx.x) * 64u;
@@ -274,7 +293,7 @@ __global__ __launch_bounds__(64) void k_var_size(const uint8_t *__restrict__ nat
   }
   __syncthreads();
   const uint8_t *nat = TILE ? tile + lane * stride : native + r * stride;
-  uint64_t s = 0;
+  uint64_t s = mark;  // record-marked batches: the message's 4-byte mark
   uint32_t pc = r < n ? 0u : kPcDone, bad_op = kPcDone;
   for (uint32_t upc = 0; upc < nops; ++upc) {
     if (!__any(pc == upc)) continue;
@@ -373,7 +392,7 @@ __global__ __launch_bounds__(256) void k_var_encode(
     uint64_t heap_len, uint8_t *__restrict__ xdr, uint64_t cap, uint64_t *__restrict__ offsets,
     const uint32_t *__restrict__ sizes, const unsigned long long *__restrict__ block_base,
     const xdrg_op *__restrict__ ops, uint32_t nops, const uint32_t *__restrict__ table,
-    uint32_t stack_limit, unsigned long long *err) {
+    uint32_t stack_limit, uint32_t mark, unsigned long long *err) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   xdrg_op *sops = reinterpret_cast<xdrg_op *>(smem);
   __shared__ unsigned long long wsum[4];
@@ -397,6 +416,11 @@ __global__ __launch_bounds__(256) void k_var_encode(
 
   const uint8_t *nat = native + r * stride;
   uint64_t pos = off;
+  if (mark) {  // the message's record mark (message_t::alloc, marshal.cc:15-31)
+    if (4 > cap - min(pos, cap)) { report(err, r, kOpRecordLevel, XDRG_ERR_OVERFLOW_PUT); return; }
+    st32(xdr + pos, mark_word(sz - 4u));
+    pos += 4;
+  }
   uint32_t pc = 0;
   for (;;) {
     const xdrg_op &op = sops[pc];
@@ -485,7 +509,7 @@ __global__ __launch_bounds__(256) void k_var_decode(
     const uint8_t *__restrict__ xdr, uint64_t len, const uint64_t *__restrict__ offsets, uint64_t n,
     uint8_t *__restrict__ native, uint32_t stride, const xdrg_op *__restrict__ ops, uint32_t nops,
     const uint32_t *__restrict__ table, uint32_t stack_limit, uint8_t *__restrict__ heap,
-    uint64_t ebase, uint32_t F, unsigned long long *err) {
+    uint64_t ebase, uint32_t F, uint32_t mark, unsigned long long *err) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   xdrg_op *sops = reinterpret_cast<xdrg_op *>(smem);
   load_ops(sops, ops, nops);
@@ -494,10 +518,14 @@ __global__ __launch_bounds__(256) void k_var_decode(
   const uint64_t a = offsets[r], b = offsets[r + 1];
   if (r == n - 1 && b != len) report(err, n, kOpRecordLevel, XDRG_ERR_TRAILING);
   if (b < a || b > len) { report(err, r, 0, XDRG_ERR_OVERFLOW_GET); return; }
+  if (mark) {  // xdr_from_msg: the message read_message framed (srpc.cc:29-55)
+    const uint32_t c = b - a < 4 ? XDRG_ERR_MSG_EOF : mark_code(ld32(xdr + a), b - a - 4);
+    if (c) { report(err, r, kOpRecordLevel, c); return; }
+  }
   if ((b - a) & 3u) { report(err, r, kOpRecordLevel, XDRG_ERR_SIZE_NOT_MULT4); return; }
   uint8_t *nat = native + r * stride;
   for (uint32_t k = 0; k < stride / 4; ++k) st32(nat + 4 * k, 0u);
-  uint64_t p = a;
+  uint64_t p = a + mark;
   uint64_t ecur = ebase + static_cast<uint64_t>(F) * a;  // this record's element arrays
   uint32_t pc = 0;
   for (;;) {
@@ -862,7 +890,7 @@ __global__ __launch_bounds__(64) void k_var_encode_i(
     uint64_t heap_len, uint8_t *__restrict__ xdr, uint64_t cap, uint64_t *__restrict__ offsets,
     const uint32_t *__restrict__ sizes, const unsigned long long *__restrict__ block_base,
     const xdrg_op *__restrict__ ops, uint32_t nops, const uint32_t *__restrict__ table,
-    uint32_t stack_limit, uint32_t MC, uint32_t C, unsigned long long *err,
+    uint32_t stack_limit, uint32_t MC, uint32_t C, uint32_t mark, unsigned long long *err,
     unsigned long long *stamps) {
   extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
   unsigned long long stv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -919,6 +947,17 @@ __global__ __launch_bounds__(64) void k_var_encode_i(
     uint64_t pos = off;
     uint32_t pc = szok ? 0u : kPcDone;
     bool ok = szok;
+    if (ok && mark) {  // the message's record mark (message_t::alloc, marshal.cc:15-31)
+      if (4 > cap - min(pos, cap)) {
+        report(err, r, kOpRecordLevel, XDRG_ERR_OVERFLOW_PUT);
+        ok = false;
+        pc = kPcDone;
+      } else {
+        img_put(im, C, gout, at, mark_word(sz - 4u));
+        at += 4;
+        pos += 4;
+      }
+    }
     for (uint32_t upc = 0; upc < nops; ++upc) {
       if (!__any(pc == upc)) continue;
       const xdrg_op op = ops[upc];
@@ -1124,8 +1163,8 @@ __global__ __launch_bounds__(64) void k_var_decode_w(
     const uint8_t *__restrict__ xdr, uint64_t len, const uint64_t *__restrict__ offsets, uint64_t n,
     uint8_t *__restrict__ native, uint32_t stride, uint8_t *__restrict__ heap,
     const xdrg_op *__restrict__ ops, uint32_t nops, const uint32_t *__restrict__ table,
-    uint32_t stack_limit, uint32_t C, uint64_t ebase, uint32_t F, unsigned long long *err,
-    unsigned long long *stamps) {
+    uint32_t stack_limit, uint32_t C, uint64_t ebase, uint32_t F, uint32_t mark,
+    unsigned long long *err, unsigned long long *stamps) {
   extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
   unsigned long long stv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   XDRG_STAMP(0);
@@ -1207,12 +1246,16 @@ __global__ __launch_bounds__(64) void k_var_decode_w(
     uint8_t *nat = tile + lane * stride;
     uint32_t pc = kPcDone;
     if (lane < nrec) {
+      // xdr_from_msg: the message read_message framed (srpc.cc:29-55)
+      const uint32_t mc = !mark || b < a || b > len ? 0u
+                          : b - a < 4 ? XDRG_ERR_MSG_EOF : mark_code(rd(a), b - a - 4);
       if (r == n - 1 && b != len) report(err, n, kOpRecordLevel, XDRG_ERR_TRAILING);
       if (b < a || b > len) report(err, r, 0, XDRG_ERR_OVERFLOW_GET);
+      else if (mc) report(err, r, kOpRecordLevel, mc);
       else if ((b - a) & 3u) report(err, r, kOpRecordLevel, XDRG_ERR_SIZE_NOT_MULT4);
       else pc = 0;
     }
-    uint64_t p = a;
+    uint64_t p = a + mark;
     uint64_t ecur = ebase + static_cast<uint64_t>(F) * a;  // this record's element arrays
     bool ok = pc == 0u;
     for (uint32_t upc = 0; upc < nops; ++upc) {
@@ -1322,6 +1365,201 @@ __global__ __launch_bounds__(64) void k_var_decode_w(
   XDRG_STAMP(4);
   XDRG_STAMP(5);
   XDRG_STAMP_FLUSH(blockIdx.x);
+}
+
+// ------------------------------------------- record marks: the index pass
+// The marks of a message stream form a chain (each names the next one's
+// position), so finding the messages is list ranking.  The stream is cut
+// into segments of kIxSW words; a message is at most max_msg_len bytes,
+// so the chain enters every segment within its first K = max_msg_len/4 + 1
+// words.
+//   k_ix_seg   per segment, pointer jumping in LDS over all its words: the
+//              exit (entry word of the next segment) and the number of
+//              marks passed, or the terminal state (end of stream or a
+//              framing error), for each of the K entries;
+//   k_ix_up    composes F consecutive tables into one (levels until one
+//              node remains);
+//   k_ix_down  from the top: each node's entry and the count of messages
+//              before it, which reach every segment;
+//   k_ix_emit  per segment on the chain, one lane walks it from its entry
+//              through an LDS copy and writes the offsets.
+constexpr uint32_t kIxSW = 4096;  // words per segment (16 KiB)
+constexpr uint32_t kIxLog = 12;   // log2(kIxSW) pointer-jumping rounds
+constexpr uint64_t kIxCnt = (1ull << 40) - 1;  // table / entry word: count bits
+static_assert(XDRG_INDEX_MAX_MSG == 4 * (kIxSW - 1), "index window = one segment");
+
+enum ix_state : uint32_t { IX_RUN = 0, IX_END, IX_EOF, IX_SIZE4, IX_FRAG, IX_LONG, IX_MULT4 };
+
+__device__ __forceinline__ uint32_t ix_error(uint32_t st) {
+  switch (st) {
+  case IX_EOF: return XDRG_ERR_MSG_EOF;
+  case IX_SIZE4: return XDRG_ERR_MSG_SIZE4;
+  case IX_FRAG: return XDRG_ERR_MSG_FRAGMENT;
+  case IX_LONG: return XDRG_ERR_MSG_TOO_LONG;
+  default: return XDRG_ERR_SIZE_NOT_MULT4;  // xdr_from_msg of it would throw this
+  }
+}
+
+// The mark at stream word w (raw = its little-endian word when it lies
+// inside the stream), checked as read_message reads it (srpc.cc:29-55):
+// premature EOF on the mark, the pre-swap size test, the last-fragment
+// bit; then msg_sock's maxmsglen_ (msgsock.cc:99-111) and a body that ends
+// past the stream.  A size that is not a multiple of 4 ends the index at
+// that message: xdr_from_msg rejects it (marshal.h:152-162) and the next
+// mark would not be word aligned.  *nxt = word of the next mark.
+__device__ __forceinline__ uint32_t ix_mark(uint32_t raw, uint64_t w, uint64_t len, uint32_t maxlen,
+                                            uint64_t *nxt) {
+  const uint64_t at = 4 * w;
+  if (at == len) return IX_END;
+  if (at + 4 > len) return IX_EOF;
+  if (raw & 3u) return IX_SIZE4;
+  const uint32_t v = bswap32(raw);
+  if (!(v & XDRG_MARK_LAST)) return IX_FRAG;
+  const uint32_t size = v & ~XDRG_MARK_LAST;
+  if (size > maxlen) return IX_LONG;
+  if (len - at - 4 < size) return IX_EOF;
+  if (size & 3u) return IX_MULT4;
+  *nxt = w + 1 + size / 4;
+  return IX_RUN;
+}
+
+// LDS node: target (13 bits: < kIxSW a word of this segment, kIxSW + e =
+// entry e of the next one) | marks passed << 13 (13 bits) | state << 26.
+// Table word: marks (40 bits) | exit entry << 40 (16 bits) | state << 56.
+__global__ __launch_bounds__(256) void k_ix_seg(const uint8_t *__restrict__ s, uint64_t len,
+                                                uint32_t maxlen, uint32_t K,
+                                                uint64_t *__restrict__ tab) {
+  __shared__ uint32_t node[kIxSW];
+  const uint64_t w0 = static_cast<uint64_t>(blockIdx.x) * kIxSW;
+  for (uint32_t i = threadIdx.x; i < kIxSW; i += 256) {
+    const uint64_t w = w0 + i;
+    const uint32_t raw = 4 * w + 4 <= len ? ld32(s + 4 * w) : 0u;
+    uint64_t nx = 0;
+    const uint32_t st = ix_mark(raw, w, len, maxlen, &nx);
+    node[i] = st ? (st << 26) : (static_cast<uint32_t>(nx - w0) | (1u << 13));
+  }
+  __syncthreads();
+  // In place: a node read mid-round is either state, each a correct jump.
+  for (uint32_t k = 0; k < kIxLog; ++k) {
+    for (uint32_t i = threadIdx.x; i < kIxSW; i += 256) {
+      const uint32_t v = node[i];
+      const uint32_t t = v & 0x1fffu;
+      if ((v >> 26) == 0 && t < kIxSW) {
+        const uint32_t u = node[t];
+        const uint32_t c = ((v >> 13) & 0x1fffu) + ((u >> 13) & 0x1fffu);
+        node[i] = (u & ~(0x1fffu << 13)) | (c << 13);
+      }
+    }
+    __syncthreads();
+  }
+  for (uint32_t e = threadIdx.x; e < K; e += 256) {
+    const uint32_t v = node[e];
+    const uint64_t st = v >> 26, c = (v >> 13) & 0x1fffu;
+    tab[static_cast<uint64_t>(blockIdx.x) * K + e] =
+        st ? (st << 56 | c) : (static_cast<uint64_t>((v & 0x1fffu) - kIxSW) << 40 | c);
+  }
+}
+
+// One node of the next level per workgroup: F children composed for
+// every entry.  LDS: the children's tables staged first.
+template <bool LDS>
+__global__ __launch_bounds__(256) void k_ix_up(const uint64_t *__restrict__ in, uint64_t nin,
+                                               uint32_t K, uint32_t F, uint64_t *__restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t stg[];
+  const uint64_t c0 = static_cast<uint64_t>(blockIdx.x) * F;
+  const uint32_t nc = static_cast<uint32_t>(min<uint64_t>(F, nin - c0));
+  const uint64_t *src = in + c0 * K;
+  if (LDS) {
+    for (uint32_t i = threadIdx.x; i < nc * K; i += 256) stg[i] = src[i];
+    __syncthreads();
+  }
+  for (uint32_t e = threadIdx.x; e < K; e += 256) {
+    uint64_t x = e, c = 0, res = 0;
+    bool term = false;
+    for (uint32_t j = 0; j < nc && !term; ++j) {
+      const uint64_t t = LDS ? stg[j * K + x] : src[static_cast<uint64_t>(j) * K + x];
+      c += t & kIxCnt;
+      if (t >> 56) { res = (t >> 56) << 56 | c; term = true; }
+      else x = (t >> 40) & 0xffffu;
+    }
+    out[static_cast<uint64_t>(blockIdx.x) * K + e] = term ? res : (x << 40 | c);
+  }
+}
+
+// Entry word of a node: bit 63 = off the chain; entry << 40; messages
+// before the node (40 bits).  One workgroup per parent: its children's
+// entries in order, from the parent's.
+template <bool LDS>
+__global__ __launch_bounds__(64) void k_ix_down(const uint64_t *__restrict__ tab, uint64_t nin,
+                                                uint32_t K, uint32_t F,
+                                                const uint64_t *__restrict__ up,
+                                                uint64_t *__restrict__ ent) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t stg[];
+  const uint64_t c0 = static_cast<uint64_t>(blockIdx.x) * F;
+  const uint32_t nc = static_cast<uint32_t>(min<uint64_t>(F, nin - c0));
+  const uint64_t e = up[blockIdx.x];
+  if (e >> 63) {
+    for (uint32_t j = threadIdx.x; j < nc; j += 64) ent[c0 + j] = 1ull << 63;
+    return;
+  }
+  const uint64_t *src = tab + c0 * K;
+  if (LDS) {
+    for (uint32_t i = threadIdx.x; i < nc * K; i += 64) stg[i] = src[i];
+    __syncthreads();
+  }
+  if (threadIdx.x != 0) return;
+  uint64_t x = (e >> 40) & 0xffffu, b = e & kIxCnt;
+  bool dead = false;
+  for (uint32_t j = 0; j < nc; ++j) {
+    ent[c0 + j] = dead ? (1ull << 63) : (x << 40 | b);
+    if (dead) continue;
+    const uint64_t t = LDS ? stg[j * K + x] : src[static_cast<uint64_t>(j) * K + x];
+    b += t & kIxCnt;
+    if (t >> 56) dead = true;
+    else x = (t >> 40) & 0xffffu;
+  }
+}
+
+// Segments on the chain: lane 0 walks the segment's marks (words staged in
+// LDS) from its entry and writes their offsets; the segment where the
+// chain ends writes offsets[count] and the count.
+__global__ __launch_bounds__(256) void k_ix_emit(const uint8_t *__restrict__ s, uint64_t len,
+                                                 uint32_t maxlen, const uint64_t *__restrict__ ent,
+                                                 uint64_t *__restrict__ offsets, uint64_t max_msgs,
+                                                 unsigned long long *count,
+                                                 unsigned long long *err) {
+  __shared__ uint32_t wd[kIxSW];
+  const uint64_t e = ent[blockIdx.x];
+  if (e >> 63) return;
+  uint64_t b = e & kIxCnt;
+  if (b > max_msgs) return;  // past the index's capacity: reported where it ran out
+  const uint64_t w0 = static_cast<uint64_t>(blockIdx.x) * kIxSW;
+  for (uint32_t i = threadIdx.x; i < kIxSW; i += 256) {
+    const uint64_t w = w0 + i;
+    wd[i] = 4 * w + 4 <= len ? ld32(s + 4 * w) : 0u;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  uint64_t i = (e >> 40) & 0xffffu;
+  while (i < kIxSW) {
+    const uint64_t w = w0 + i;
+    uint64_t nx = 0;
+    const uint32_t st = ix_mark(wd[i], w, len, maxlen, &nx);
+    offsets[b] = 4 * w;
+    if (st == IX_END) { atomicMin(count, b); return; }
+    if (b == max_msgs) {
+      report(err, b, kOpRecordLevel, XDRG_ERR_MSG_COUNT);
+      atomicMin(count, b);
+      return;
+    }
+    if (st != IX_RUN) {
+      report(err, b, kOpRecordLevel, ix_error(st));
+      atomicMin(count, b);
+      return;
+    }
+    ++b;
+    i = nx - w0;
+  }
 }
 
 // ------------------------------------------------------------------ swaps
@@ -1460,20 +1698,194 @@ uint64_t decode_heap_bytes(const xdrg_plan &p, uint64_t len) {
 
 // Size pass (xdr_size per record + 64-record block sums).
 hipError_t launch_size_pass(const xdrg_plan &p, const uint8_t *nat, uint64_t n, uint32_t *sizes,
-                            unsigned long long *bsum, unsigned long long *err, hipStream_t s) {
+                            unsigned long long *bsum, uint32_t mark, unsigned long long *err,
+                            hipStream_t s) {
   const uint64_t nb = (n + 63) / 64;
   const size_t tile = 64ull * p.stride;
   if (tile <= kVarLdsBudget)
     k_var_size<true><<<nb, 64, tile, s>>>(nat, n, p.stride, p.d_ops, uint32_t(p.ops.size()),
-                                          p.d_table, sizes, bsum, err);
+                                          p.d_table, sizes, bsum, mark, err);
   else
     k_var_size<false><<<nb, 64, 0, s>>>(nat, n, p.stride, p.d_ops, uint32_t(p.ops.size()),
-                                        p.d_table, sizes, bsum, err);
+                                        p.d_table, sizes, bsum, mark, err);
   return hipGetLastError();
 }
 
 unsigned long long *err_ptr(xdrg_status *st) {
   return reinterpret_cast<unsigned long long *>(&st->first_error);
+}
+
+// Interpreter-path encode of n records: size pass, block scan, then the
+// record kernel.  mark = 4 puts each record in a message (its record mark
+// first, xdrg_encode_msgs); mark = 0 is xdrg_encode of a var plan.
+int var_encode(const xdrg_plan &P, const void *d_native, uint64_t n, const uint8_t *d_heap,
+               uint64_t heap_len, void *d_xdr, uint64_t cap, uint64_t *d_offsets,
+               uint32_t stack_limit, void *d_ws, size_t ws_bytes, xdrg_status *d_status,
+               uint32_t mark, hipStream_t s) {
+  const xdrg_plan *p = &P;
+  unsigned long long *err = err_ptr(d_status);
+  if (!d_offsets) return XDRG_EINVAL;
+  if (d_heap && !aligned(d_heap, 4)) return XDRG_EALIGN;
+  if (!aligned(d_native, 8) || !aligned(d_xdr, 4) || !aligned(d_offsets, 8)) return XDRG_EALIGN;
+  if (n == 0) {
+    HIPCHK(hipMemsetAsync(d_offsets, 0, 8, s));
+    return XDRG_OK;
+  }
+  size_t so, bo;
+  const size_t need = var_ws_layout(n, &so, &bo);
+  if (!d_ws || ws_bytes < need) return XDRG_ESPACE;
+  uint32_t *sizes = reinterpret_cast<uint32_t *>(static_cast<char *>(d_ws) + so);
+  unsigned long long *bsum = reinterpret_cast<unsigned long long *>(static_cast<char *>(d_ws) + bo);
+  const uint64_t max_rec = p->max_record_bytes + mark;
+  // chunk-map image encode (64-record workgroups); chunk map entries are
+  // u16 (lane 6 | slot 2 | chunk 8 bits)
+  const uint32_t MC = static_cast<uint32_t>(std::min<uint64_t>(64ull * p->max_chunks16, 1u << 20));
+  const uint32_t Ci = static_cast<uint32_t>(std::min<uint64_t>(
+      g_img_bytes, (64ull * std::max<uint64_t>(max_rec, 16) + 15u) & ~15ull));
+  const uint32_t KI = p->max_var_slots <= 1 ? 1u : p->max_var_slots <= 2 ? 2u : 4u;
+  const enc_i_lds LI = enc_i_layout(p->stride, KI, MC, Ci);
+  const bool ok_I = p->max_var_slots <= 4 && p->max_slot_len <= 4096u &&
+                    64ull * max_rec < (1ull << 31) && LI.total <= kVarLdsBudget &&
+                    aligned(d_native, 16);
+  const enc_lds EL = enc_lds_layout(uint32_t(p->ops.size()), p->stride, p->max_scalar_words);
+  const bool ok_C = EL.total <= kVarLdsBudget && aligned(d_native, 16) && p->max_var_slots <= 4 &&
+                    !p->has_vector &&  // its per-lane scalar-word array cannot bound element words
+                    !mark;
+  int kern = g_force_enc;
+  if (kern == 3 && !ok_I) kern = 0;
+  if (kern == 2 && !ok_C) kern = 0;
+  if (kern == 0) kern = ok_I ? 3 : ok_C ? 2 : 1;
+  const uint64_t nb = (n + 63) / 64;  // 64-record blocks for the size pass, scan and kernel 3
+  if (nb > 0xffffffffull) return XDRG_EUNSUPPORTED;
+  const size_t lds_ops = p->ops.size() * sizeof(xdrg_op);
+  const uint8_t *nat8 = static_cast<const uint8_t *>(d_native);
+  uint8_t *xdr8 = static_cast<uint8_t *>(d_xdr);
+  const uint32_t nops = uint32_t(p->ops.size());
+  HIPCHK(launch_size_pass(*p, nat8, n, sizes, bsum, mark, err, s));
+  k_scan_blocks<<<1, 1024, 0, s>>>(bsum, uint32_t(nb), d_status, d_offsets, n);
+  HIPCHK(hipGetLastError());
+  if (kern == 3) {
+#define LAUNCH_ENC_I(K)                                                                        \
+  k_var_encode_i<K, 16><<<nb, 64, LI.total, s>>>(nat8, n, p->stride, d_heap, heap_len, xdr8,  \
+                                                 cap, d_offsets, sizes, bsum, p->d_ops, nops,  \
+                                                 p->d_table, stack_limit, MC, Ci, mark, err,   \
+                                                 g_stamps_enc)
+    if (KI == 1) LAUNCH_ENC_I(1);
+    else if (KI == 2) LAUNCH_ENC_I(2);
+    else LAUNCH_ENC_I(4);
+#undef LAUNCH_ENC_I
+    HIPCHK(hipGetLastError());
+    return XDRG_OK;
+  }
+  const uint64_t nb256 = (n + 255) / 256;
+  if (kern == 2) {
+#define LAUNCH_ENC_C(K)                                                                        \
+  k_var_encode_c<K><<<nb256, 256, EL.total, s>>>(nat8, n, p->stride, d_heap, heap_len, xdr8, cap, \
+                                              d_offsets, sizes, bsum, p->d_ops, nops,          \
+                                              p->d_table, stack_limit, p->max_scalar_words,   \
+                                              err, g_stamps_enc)
+    if (p->max_var_slots <= 1) LAUNCH_ENC_C(1);
+    else if (p->max_var_slots <= 2) LAUNCH_ENC_C(2);
+    else LAUNCH_ENC_C(4);
+#undef LAUNCH_ENC_C
+  } else {
+    k_var_encode<<<nb256, 256, lds_ops, s>>>(nat8, n, p->stride, d_heap, heap_len, xdr8, cap,
+                                          d_offsets, sizes, bsum, p->d_ops, nops, p->d_table,
+                                          stack_limit, mark, err);
+  }
+  HIPCHK(hipGetLastError());
+  return XDRG_OK;
+}
+
+// Index pass levels and workspace: per level L (n[L] nodes) a table of
+// n[L] * K words (below the top) and n[L] entry words.
+struct ix_layout {
+  uint64_t nseg = 0;
+  uint32_t K = 0, F = 0;
+  bool lds = false;
+  int top = 0;
+  uint64_t n[24] = {};
+  size_t tab[24] = {}, ent[24] = {};
+  size_t total = 0;
+};
+constexpr size_t kIxLdsBytes = 64u << 10;
+
+ix_layout ix_plan(uint64_t len, uint32_t maxlen) {
+  ix_layout L;
+  L.nseg = (len / 4) / kIxSW + 1;  // covers the end-of-stream word
+  L.K = maxlen / 4 + 1;
+  L.F = L.K <= 128 ? 64 : 16;
+  L.lds = static_cast<size_t>(L.F) * L.K * 8 <= kIxLdsBytes;
+  L.n[0] = L.nseg;
+  while (L.n[L.top] > 1) {
+    L.n[L.top + 1] = (L.n[L.top] + L.F - 1) / L.F;
+    ++L.top;
+  }
+  size_t off = 0;
+  for (int l = 0; l <= L.top; ++l) {
+    if (l < L.top) { L.tab[l] = off; off += align_up(L.n[l] * L.K * 8, 256); }
+    L.ent[l] = off;
+    off += align_up(L.n[l] * 8, 256);
+  }
+  L.total = off;
+  return L;
+}
+
+// Heap bytes a decode needs; plans without payload or element fields need
+// none when decoding messages (the decoded records hold no heap refs).
+bool plan_has_payload(const xdrg_plan &p) { return p.max_var_slots > 0 || p.has_vector; }
+
+// Interpreter-path decode of n records indexed by d_offsets (mark = 4:
+// each record is a message whose mark is checked, xdrg_decode_msgs).
+int var_decode(const xdrg_plan &P, const void *d_xdr, uint64_t len, const uint64_t *d_offsets,
+               uint64_t n, void *d_native, uint8_t *d_heap_out, uint64_t heap_cap,
+               uint32_t stack_limit, xdrg_status *d_status, uint32_t mark, hipStream_t s) {
+  const xdrg_plan *p = &P;
+  unsigned long long *err = err_ptr(d_status);
+  if (n == 0) {
+    if (len) return launch_report(err, 0, kOpRecordLevel, XDRG_ERR_TRAILING, s);
+    return XDRG_OK;
+  }
+  bool no_heap = false;
+  if (mark && !d_heap_out && !plan_has_payload(*p)) {  // nothing points into a heap
+    d_heap_out = static_cast<uint8_t *>(const_cast<void *>(d_xdr));
+    no_heap = true;
+  }
+  if (!no_heap && (heap_cap < decode_heap_bytes(*p, len) || (len && !d_heap_out)))
+    return XDRG_ESPACE;
+  const uint64_t ebase = p->has_vector ? align_up(len, 16) : 0;  // decoded element arrays
+  if (!aligned(d_xdr, 4) || !aligned(d_native, 8) || (d_heap_out && !aligned(d_heap_out, 4)))
+    return XDRG_EALIGN;
+  const uint8_t *xdr8 = static_cast<const uint8_t *>(d_xdr);
+  uint8_t *nat8 = static_cast<uint8_t *>(d_native);
+  const uint32_t nops = uint32_t(p->ops.size());
+  const bool copy = d_heap_out != d_xdr;  // heap_out == d_xdr: zero-copy (refs into the stream)
+  const uint32_t Cw = static_cast<uint32_t>(std::min<uint64_t>(
+      g_win_bytes, (64ull * std::max<uint64_t>(p->max_record_bytes + mark, 16) + 15u) & ~15ull));
+  const uint32_t lw = dec_w_lds(p->stride, Cw);
+  const bool ok_W = lw <= kVarLdsBudget && aligned(d_native, 16);
+  int kern = g_force_dec;
+  if (kern == 2 && !ok_W) kern = 0;
+  if (kern == 0) kern = ok_W ? 2 : 1;
+  if (kern == 2) {
+    const uint64_t nb = (n + 63) / 64;
+    if (copy)
+      k_var_decode_w<true><<<nb, 64, lw, s>>>(xdr8, len, d_offsets, n, nat8, p->stride, d_heap_out,
+                                              p->d_ops, nops, p->d_table, stack_limit, Cw, ebase,
+                                              p->heap_factor, mark, err, g_stamps);
+    else
+      k_var_decode_w<false><<<nb, 64, lw, s>>>(xdr8, len, d_offsets, n, nat8, p->stride, d_heap_out,
+                                               p->d_ops, nops, p->d_table, stack_limit, Cw, ebase,
+                                               p->heap_factor, mark, err, g_stamps);
+  } else {
+    if (copy && len) HIPCHK(hipMemcpyAsync(d_heap_out, d_xdr, len, hipMemcpyDeviceToDevice, s));
+    const uint64_t nb = (n + 255) / 256;
+    k_var_decode<<<nb, 256, p->ops.size() * sizeof(xdrg_op), s>>>(
+        xdr8, len, d_offsets, n, nat8, p->stride, p->d_ops, nops, p->d_table, stack_limit,
+        d_heap_out, ebase, p->heap_factor, mark, err);
+  }
+  HIPCHK(hipGetLastError());
+  return XDRG_OK;
 }
 
 }  // namespace
@@ -1576,6 +1988,7 @@ int xdrg_plan_get_info(const xdrg_plan *p, xdrg_plan_info *info) {
   info->max_depth = p->max_depth;
   info->nops = uint32_t(p->ops.size());
   info->has_checks = p->has_checks ? 1u : 0u;
+  info->max_record_bytes = p->max_record_bytes;
   return XDRG_OK;
 }
 
@@ -1584,7 +1997,7 @@ uint64_t xdrg_decode_heap_size(const xdrg_plan *p, uint64_t len) {
 }
 
 size_t xdrg_workspace_size(const xdrg_plan *p, uint64_t n) {
-  if (!p || p->path != XDRG_PATH_VAR) return 0;
+  if (!p) return 0;  // var encode of any plan; encode_msgs of every plan
   size_t a, b;
   return var_ws_layout(n, &a, &b);
 }
@@ -1635,75 +2048,8 @@ int xdrg_encode(const xdrg_plan *p, const void *d_native, uint64_t n, const uint
     return run_fixed(*p, false, d_native, d_xdr, nrec, err, s);
   }
   // ---- variable plans
-  if (!d_offsets) return XDRG_EINVAL;
-  if (d_heap && !aligned(d_heap, 4)) return XDRG_EALIGN;
-  if (!aligned(d_native, 8) || !aligned(d_xdr, 4) || !aligned(d_offsets, 8)) return XDRG_EALIGN;
-  if (n == 0) {
-    HIPCHK(hipMemsetAsync(d_offsets, 0, 8, s));
-    return XDRG_OK;
-  }
-  size_t so, bo;
-  const size_t need = var_ws_layout(n, &so, &bo);
-  if (!d_ws || ws_bytes < need) return XDRG_ESPACE;
-  uint32_t *sizes = reinterpret_cast<uint32_t *>(static_cast<char *>(d_ws) + so);
-  unsigned long long *bsum = reinterpret_cast<unsigned long long *>(static_cast<char *>(d_ws) + bo);
-  // chunk-map image encode (64-record workgroups); chunk map entries are
-  // u16 (lane 6 | slot 2 | chunk 8 bits)
-  const uint32_t MC = static_cast<uint32_t>(std::min<uint64_t>(64ull * p->max_chunks16, 1u << 20));
-  const uint32_t Ci = static_cast<uint32_t>(std::min<uint64_t>(
-      g_img_bytes, (64ull * std::max<uint64_t>(p->max_record_bytes, 16) + 15u) & ~15ull));
-  const uint32_t KI = p->max_var_slots <= 1 ? 1u : p->max_var_slots <= 2 ? 2u : 4u;
-  const enc_i_lds LI = enc_i_layout(p->stride, KI, MC, Ci);
-  const bool ok_I = p->max_var_slots <= 4 && p->max_slot_len <= 4096u &&
-                    64ull * p->max_record_bytes < (1ull << 31) && LI.total <= kVarLdsBudget &&
-                    aligned(d_native, 16);
-  const enc_lds EL = enc_lds_layout(uint32_t(p->ops.size()), p->stride, p->max_scalar_words);
-  const bool ok_C = EL.total <= kVarLdsBudget && aligned(d_native, 16) && p->max_var_slots <= 4 &&
-                    !p->has_vector;  // its per-lane scalar-word array cannot bound element words
-  int kern = g_force_enc;
-  if (kern == 3 && !ok_I) kern = 0;
-  if (kern == 2 && !ok_C) kern = 0;
-  if (kern == 0) kern = ok_I ? 3 : ok_C ? 2 : 1;
-  const uint64_t nb = (n + 63) / 64;  // 64-record blocks for the size pass, scan and kernel 3
-  if (nb > 0xffffffffull) return XDRG_EUNSUPPORTED;
-  const size_t lds_ops = p->ops.size() * sizeof(xdrg_op);
-  const uint8_t *nat8 = static_cast<const uint8_t *>(d_native);
-  uint8_t *xdr8 = static_cast<uint8_t *>(d_xdr);
-  const uint32_t nops = uint32_t(p->ops.size());
-  HIPCHK(launch_size_pass(*p, nat8, n, sizes, bsum, err, s));
-  k_scan_blocks<<<1, 1024, 0, s>>>(bsum, uint32_t(nb), d_status, d_offsets, n);
-  HIPCHK(hipGetLastError());
-  if (kern == 3) {
-#define LAUNCH_ENC_I(K)                                                                        \
-  k_var_encode_i<K, 16><<<nb, 64, LI.total, s>>>(nat8, n, p->stride, d_heap, heap_len, xdr8,  \
-                                                 cap, d_offsets, sizes, bsum, p->d_ops, nops,  \
-                                                 p->d_table, stack_limit, MC, Ci, err,         \
-                                                 g_stamps_enc)
-    if (KI == 1) LAUNCH_ENC_I(1);
-    else if (KI == 2) LAUNCH_ENC_I(2);
-    else LAUNCH_ENC_I(4);
-#undef LAUNCH_ENC_I
-    HIPCHK(hipGetLastError());
-    return XDRG_OK;
-  }
-  const uint64_t nb256 = (n + 255) / 256;
-  if (kern == 2) {
-#define LAUNCH_ENC_C(K)                                                                        \
-  k_var_encode_c<K><<<nb256, 256, EL.total, s>>>(nat8, n, p->stride, d_heap, heap_len, xdr8, cap, \
-                                              d_offsets, sizes, bsum, p->d_ops, nops,          \
-                                              p->d_table, stack_limit, p->max_scalar_words,   \
-                                              err, g_stamps_enc)
-    if (p->max_var_slots <= 1) LAUNCH_ENC_C(1);
-    else if (p->max_var_slots <= 2) LAUNCH_ENC_C(2);
-    else LAUNCH_ENC_C(4);
-#undef LAUNCH_ENC_C
-  } else {
-    k_var_encode<<<nb256, 256, lds_ops, s>>>(nat8, n, p->stride, d_heap, heap_len, xdr8, cap,
-                                          d_offsets, sizes, bsum, p->d_ops, nops, p->d_table,
-                                          stack_limit, err);
-  }
-  HIPCHK(hipGetLastError());
-  return XDRG_OK;
+  return var_encode(*p, d_native, n, d_heap, heap_len, d_xdr, cap, d_offsets, stack_limit, d_ws,
+                    ws_bytes, d_status, 0u, s);
 }
 
 int xdrg_decode(const xdrg_plan *p, const void *d_xdr, uint64_t len, const uint64_t *d_offsets,
@@ -1738,44 +2084,8 @@ int xdrg_decode(const xdrg_plan *p, const void *d_xdr, uint64_t len, const uint6
     return run_fixed(*p, true, d_xdr, d_native, nrec, err, s);
   }
   if (!d_offsets) return XDRG_EUNSUPPORTED;  // var decode needs a record index
-  if (n == 0) {
-    if (len) return launch_report(err, 0, kOpRecordLevel, XDRG_ERR_TRAILING, s);
-    return XDRG_OK;
-  }
-  if (heap_cap < decode_heap_bytes(*p, len) || (len && !d_heap_out)) return XDRG_ESPACE;
-  const uint64_t ebase = p->has_vector ? align_up(len, 16) : 0;  // decoded element arrays
-  if (!aligned(d_xdr, 4) || !aligned(d_native, 8) || (d_heap_out && !aligned(d_heap_out, 4)))
-    return XDRG_EALIGN;
-  const uint8_t *xdr8 = static_cast<const uint8_t *>(d_xdr);
-  uint8_t *nat8 = static_cast<uint8_t *>(d_native);
-  const uint32_t nops = uint32_t(p->ops.size());
-  const bool copy = d_heap_out != d_xdr;  // heap_out == d_xdr: zero-copy (refs into the stream)
-  const uint32_t Cw = static_cast<uint32_t>(std::min<uint64_t>(
-      g_win_bytes, (64ull * std::max<uint64_t>(p->max_record_bytes, 16) + 15u) & ~15ull));
-  const uint32_t lw = dec_w_lds(p->stride, Cw);
-  const bool ok_W = lw <= kVarLdsBudget && aligned(d_native, 16);
-  int kern = g_force_dec;
-  if (kern == 2 && !ok_W) kern = 0;
-  if (kern == 0) kern = ok_W ? 2 : 1;
-  if (kern == 2) {
-    const uint64_t nb = (n + 63) / 64;
-    if (copy)
-      k_var_decode_w<true><<<nb, 64, lw, s>>>(xdr8, len, d_offsets, n, nat8, p->stride, d_heap_out,
-                                              p->d_ops, nops, p->d_table, stack_limit, Cw, ebase,
-                                              p->heap_factor, err, g_stamps);
-    else
-      k_var_decode_w<false><<<nb, 64, lw, s>>>(xdr8, len, d_offsets, n, nat8, p->stride, d_heap_out,
-                                               p->d_ops, nops, p->d_table, stack_limit, Cw, ebase,
-                                               p->heap_factor, err, g_stamps);
-  } else {
-    if (copy && len) HIPCHK(hipMemcpyAsync(d_heap_out, d_xdr, len, hipMemcpyDeviceToDevice, s));
-    const uint64_t nb = (n + 255) / 256;
-    k_var_decode<<<nb, 256, p->ops.size() * sizeof(xdrg_op), s>>>(
-        xdr8, len, d_offsets, n, nat8, p->stride, p->d_ops, nops, p->d_table, stack_limit,
-        d_heap_out, ebase, p->heap_factor, err);
-  }
-  HIPCHK(hipGetLastError());
-  return XDRG_OK;
+  return var_decode(*p, d_xdr, len, d_offsets, n, d_native, d_heap_out, heap_cap, stack_limit,
+                    d_status, 0u, s);
 }
 
 int xdrg_serial_sizes(const xdrg_plan *p, const void *d_native, uint64_t n, uint32_t *d_sizes,
@@ -1789,9 +2099,80 @@ int xdrg_serial_sizes(const xdrg_plan *p, const void *d_native, uint64_t n, uint
     HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_sizes), int(p->fixed_size), n, s));
     return XDRG_OK;
   }
-  HIPCHK(launch_size_pass(*p, static_cast<const uint8_t *>(d_native), n, d_sizes, nullptr,
+  HIPCHK(launch_size_pass(*p, static_cast<const uint8_t *>(d_native), n, d_sizes, nullptr, 0u,
                           err_ptr(d_status), s));
   return XDRG_OK;
+}
+
+int xdrg_encode_msgs(const xdrg_plan *p, const void *d_native, uint64_t n, const uint8_t *d_heap,
+                     uint64_t heap_len, void *d_out, uint64_t cap, uint64_t *d_offsets,
+                     uint32_t stack_limit, void *d_ws, size_t ws_bytes, xdrg_status *d_status,
+                     void *stream) {
+  if (!p || !d_status || (n && (!d_native || !d_out))) return XDRG_EINVAL;
+  if (int rc = plan_upload(p)) return rc;
+  return var_encode(*p, d_native, n, d_heap, heap_len, d_out, cap, d_offsets, stack_limit, d_ws,
+                    ws_bytes, d_status, 4u, static_cast<hipStream_t>(stream));
+}
+
+size_t xdrg_index_workspace_size(uint64_t len, uint32_t max_msg_len) {
+  if (max_msg_len > XDRG_INDEX_MAX_MSG) return 0;
+  return ix_plan(len, max_msg_len).total;
+}
+
+int xdrg_index_msgs(const void *d_stream, uint64_t len, uint32_t max_msg_len, uint64_t max_msgs,
+                    uint64_t *d_offsets, uint64_t *d_count, void *d_ws, size_t ws_bytes,
+                    xdrg_status *d_status, void *stream) {
+  if (!d_offsets || !d_count || !d_status || (len && !d_stream)) return XDRG_EINVAL;
+  if (max_msg_len > XDRG_INDEX_MAX_MSG) return XDRG_EUNSUPPORTED;
+  if ((d_stream && !aligned(d_stream, 4)) || !aligned(d_offsets, 8) || !aligned(d_count, 8))
+    return XDRG_EALIGN;
+  if (max_msgs >= (1ull << 40)) return XDRG_EUNSUPPORTED;  // entry words hold 40-bit counts
+  const ix_layout L = ix_plan(len, max_msg_len);
+  if (!d_ws || ws_bytes < L.total) return XDRG_ESPACE;
+  if (L.nseg > 0xffffffffull) return XDRG_EUNSUPPORTED;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  unsigned long long *err = err_ptr(d_status);
+  char *ws = static_cast<char *>(d_ws);
+  auto tab = [&](int l) { return reinterpret_cast<uint64_t *>(ws + L.tab[l]); };
+  auto ent = [&](int l) { return reinterpret_cast<uint64_t *>(ws + L.ent[l]); };
+  const uint8_t *s8 = static_cast<const uint8_t *>(d_stream);
+  HIPCHK(hipMemsetAsync(d_count, 0xff, 8, s));
+  if (L.top > 0) {
+    k_ix_seg<<<L.nseg, 256, 0, s>>>(s8, len, max_msg_len, L.K, tab(0));
+    HIPCHK(hipGetLastError());
+  }
+  const size_t stg = L.lds ? static_cast<size_t>(L.F) * L.K * 8 : 0;
+  for (int l = 0; l + 1 < L.top; ++l) {
+    if (L.lds)
+      k_ix_up<true><<<L.n[l + 1], 256, stg, s>>>(tab(l), L.n[l], L.K, L.F, tab(l + 1));
+    else
+      k_ix_up<false><<<L.n[l + 1], 256, 0, s>>>(tab(l), L.n[l], L.K, L.F, tab(l + 1));
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(hipMemsetAsync(ent(L.top), 0, 8, s));  // the chain starts at word 0 with 0 messages
+  for (int l = L.top - 1; l >= 0; --l) {
+    if (L.lds)
+      k_ix_down<true><<<L.n[l + 1], 64, stg, s>>>(tab(l), L.n[l], L.K, L.F, ent(l + 1), ent(l));
+    else
+      k_ix_down<false><<<L.n[l + 1], 64, 0, s>>>(tab(l), L.n[l], L.K, L.F, ent(l + 1), ent(l));
+    HIPCHK(hipGetLastError());
+  }
+  k_ix_emit<<<L.nseg, 256, 0, s>>>(s8, len, max_msg_len, ent(0), d_offsets, max_msgs,
+                                   reinterpret_cast<unsigned long long *>(d_count), err);
+  HIPCHK(hipGetLastError());
+  return XDRG_OK;
+}
+
+int xdrg_decode_msgs(const xdrg_plan *p, const void *d_stream, uint64_t len,
+                     const uint64_t *d_offsets, uint64_t n, void *d_native, uint8_t *d_heap_out,
+                     uint64_t heap_cap, uint32_t stack_limit, void *d_ws, size_t ws_bytes,
+                     xdrg_status *d_status, void *stream) {
+  (void)d_ws;
+  (void)ws_bytes;
+  if (!p || !d_status || !d_offsets || (n && (!d_native || (len && !d_stream)))) return XDRG_EINVAL;
+  if (int rc = plan_upload(p)) return rc;
+  return var_decode(*p, d_stream, len, d_offsets, n, d_native, d_heap_out, heap_cap, stack_limit,
+                    d_status, 4u, static_cast<hipStream_t>(stream));
 }
 
 int xdrg_swap32(const uint32_t *in, uint32_t *out, uint64_t n, void *stream) {
@@ -1827,6 +2208,12 @@ const char *xdrg_error_message(int code) {
   case XDRG_ERR_SIZE_NOT_MULT4: return "xdr_generic_get: message size not multiple of 4";
   case XDRG_ERR_TRAILING: return "unmarshaling did not consume whole message";
   case XDRG_ERR_POINTER_BOUND: return "xdr::pointer size must be 0 or 1";
+  case XDRG_ERR_MSG_EOF: return "read_message: premature EOF";
+  case XDRG_ERR_MSG_SIZE4: return "read_message: received size not multiple of 4";
+  case XDRG_ERR_MSG_FRAGMENT: return "read_message: message fragments unimplemented";
+  case XDRG_ERR_MSG_TOO_LONG: return "msg_sock: rejecting message (too long)";
+  case XDRG_ERR_MSG_MISMATCH: return "record mark does not match the record index";
+  case XDRG_ERR_MSG_COUNT: return "more messages than the record index holds";
   default: return "unknown xdrgpu error";
   }
 }
@@ -1840,6 +2227,11 @@ int xdrg_error_exception(int code) {
   case XDRG_ERR_INVALID_ENUM: return XDRG_EXC_INVARIANT_FAILED;
   case XDRG_ERR_STACK_PUT: case XDRG_ERR_STACK_GET: return XDRG_EXC_STACK_OVERFLOW;
   case XDRG_ERR_SIZE_NOT_MULT4: case XDRG_ERR_TRAILING: return XDRG_EXC_BAD_MESSAGE_SIZE;
+  // read_message throws xdr_bad_message_size (srpc.cc:36-52); msg_sock's
+  // rejections (no exception there, msgsock.cc:86-117) map to the same class
+  case XDRG_ERR_MSG_EOF: case XDRG_ERR_MSG_SIZE4: case XDRG_ERR_MSG_FRAGMENT:
+  case XDRG_ERR_MSG_TOO_LONG: case XDRG_ERR_MSG_MISMATCH: case XDRG_ERR_MSG_COUNT:
+    return XDRG_EXC_BAD_MESSAGE_SIZE;
   default: return XDRG_EXC_NONE;
   }
 }

@@ -82,6 +82,7 @@ class Plan:
         self.stride = info.native_stride
         self.max_depth = info.max_depth
         self.has_checks = bool(info.has_checks)
+        self.max_record_bytes = int(info.max_record_bytes)
 
     @property
     def is_fixed(self) -> bool:
@@ -185,6 +186,22 @@ class Marshaler:
             _ptr(heap_out), 0 if heap_out is None else heap_out.numel(), stack_limit, None, 0,
             self.status.ptr, _stream() if stream is None else stream), "xdrg_decode")
 
+    def launch_encode_msgs(self, native, n, out, offsets, heap=None,
+                           stack_limit=A.DEFAULT_STACK_LIMIT, stream=None):
+        ws = self._workspace(n)
+        A.check(A.lib().xdrg_encode_msgs(
+            self.plan.handle, _ptr(native), n, _ptr(heap), 0 if heap is None else heap.numel(),
+            _ptr(out), out.numel(), _ptr(offsets), stack_limit, _ptr(ws), ws.numel(),
+            self.status.ptr, _stream() if stream is None else stream), "xdrg_encode_msgs")
+
+    def launch_decode_msgs(self, stream_bytes, n, native_out, offsets, heap_out=None,
+                           stack_limit=A.DEFAULT_STACK_LIMIT, stream=None):
+        A.check(A.lib().xdrg_decode_msgs(
+            self.plan.handle, _ptr(stream_bytes), stream_bytes.numel(), _ptr(offsets), n,
+            _ptr(native_out), _ptr(heap_out), 0 if heap_out is None else heap_out.numel(),
+            stack_limit, None, 0, self.status.ptr, _stream() if stream is None else stream),
+            "xdrg_decode_msgs")
+
     def check(self, stream=None) -> A.XdrgError:
         e = self.status.read(_stream() if stream is None else stream)
         err = error_from(self.plan, e)
@@ -240,6 +257,106 @@ class Marshaler:
                            stack_limit=stack_limit, stream=s)
         self.check(s)
         return native[:n * self.plan.stride], (None if heap is None else heap[:hsize])
+
+
+    # ---- record-marked messages (message_t, RFC 5531) -----------------------
+    def message_sizes(self, native, n, stack_limit=A.DEFAULT_STACK_LIMIT) -> torch.Tensor:
+        """raw_size() of xdr_to_msg(r) per record: 4 + xdr_size(r)."""
+        return self.serial_sizes(native, n, stack_limit) + 4
+
+    def encode_msgs(self, native: torch.Tensor, n: int, heap: torch.Tensor | None = None,
+                    stack_limit: int = A.DEFAULT_STACK_LIMIT,
+                    capacity: int | None = None) -> EncodeResult:
+        """Message r = xdr_to_msg(record r) (marshal.h:252-260), back to back:
+        a 4-byte mark BE(size | 0x80000000) then the record's bytes.
+        offsets[r] = message r's mark, offsets[n] = total."""
+        s = _stream()
+        if capacity is None:
+            if self.plan.is_fixed:
+                capacity = n * (self.plan.fixed_size + 4)
+            else:
+                capacity = int(self.serial_sizes(native, n, stack_limit).to(torch.int64).sum().item()) + 4 * n
+        out = torch.empty(max(capacity, 4), dtype=torch.uint8, device=self.device)
+        offsets = torch.empty(n + 1, dtype=torch.int64, device=self.device)
+        self.status.init(s)
+        self.launch_encode_msgs(native, n, out, offsets, heap=heap, stack_limit=stack_limit, stream=s)
+        e = self.check(s)
+        return EncodeResult(out[:e.total_bytes], offsets)
+
+    def decode_msgs(self, stream_bytes: torch.Tensor, n: int | None = None,
+                    offsets: torch.Tensor | None = None, max_msg_len: int | None = None,
+                    stack_limit: int = A.DEFAULT_STACK_LIMIT):
+        """xdr_from_msg(m_r, r) for every message of the stream
+        (marshal.h:278-284).  Without `offsets` the record index comes from
+        the marks (index_messages, on the device; the message bound
+        defaults to the plan's largest record).  Returns (native, heap)."""
+        if offsets is None:
+            if max_msg_len is None:
+                max_msg_len = min(self.plan.max_record_bytes, A.INDEX_MAX_MSG)
+            offsets = index_messages(stream_bytes, max_msg_len)
+        if n is None:
+            n = offsets.numel() - 1
+        s = _stream()
+        native = torch.zeros(max(n, 1) * self.plan.stride, dtype=torch.uint8, device=self.device)
+        heap = None  # fixed plans: the decoded records point into no heap
+        if not self.plan.is_fixed:
+            hsize = self.plan.decode_heap_bytes(stream_bytes.numel())
+            heap = torch.zeros(max(hsize, 4), dtype=torch.uint8, device=self.device)[:hsize]
+        self.status.init(s)
+        self.launch_decode_msgs(stream_bytes, n, native, offsets, heap_out=heap,
+                                stack_limit=stack_limit, stream=s)
+        self.check(s)
+        return native[:n * self.plan.stride], heap
+
+
+class _IndexErrorPlan:
+    """error_from() needs only the bad-discriminant messages of a plan;
+    framing errors have none."""
+
+    class cp:  # noqa: N801
+        @staticmethod
+        def bad_discriminant_message(op):
+            return "bad value of discriminant"
+
+
+def index_messages(stream_bytes: torch.Tensor, max_msg_len: int = A.INDEX_MAX_MSG,
+                   max_msgs: int | None = None) -> torch.Tensor:
+    """Record index of a stream of record-marked messages, on the device
+    (xdrg_index_msgs): the framing read_message / msg_sock::input apply
+    (srpc.cc:29-55, msgsock.cc:38-119).  Returns int64 offsets[count + 1]
+    (mark of each message, then the end); raises XdrBadMessageSize with
+    the reference's what() on a framing error."""
+    dev = stream_bytes.device
+    L = A.lib()
+    total = stream_bytes.numel()
+    if max_msgs is None:
+        max_msgs = total // 4
+    ws_n = L.xdrg_index_workspace_size(total, max_msg_len)
+    ws = torch.empty(max(ws_n, 16), dtype=torch.uint8, device=dev)
+    offs = torch.empty(max_msgs + 1, dtype=torch.int64, device=dev)
+    cnt = torch.empty(1, dtype=torch.int64, device=dev)
+    st = Status(dev)
+    s = _stream()
+    st.init(s)
+    A.check(L.xdrg_index_msgs(_ptr(stream_bytes), total, max_msg_len, max_msgs, _ptr(offs),
+                              cnt.data_ptr(), _ptr(ws), ws.numel(), st.ptr, s), "xdrg_index_msgs")
+    e = st.read(s)
+    err = error_from(_IndexErrorPlan, e)
+    if err is not None:
+        raise err
+    return offs[:int(cnt.item()) + 1]
+
+
+def to_msg_batch(plan: Plan, native: torch.Tensor, n: int, heap: torch.Tensor | None = None,
+                 **kw) -> EncodeResult:
+    """xdr_to_msg of every record, messages back to back (marshal.h:252-260)."""
+    return Marshaler(plan, native.device).encode_msgs(native, n, heap, **kw)
+
+
+def from_msg_batch(plan: Plan, stream_bytes: torch.Tensor, n: int | None = None,
+                   offsets: torch.Tensor | None = None, **kw):
+    """xdr_from_msg of every message of the stream (marshal.h:278-284)."""
+    return Marshaler(plan, stream_bytes.device).decode_msgs(stream_bytes, n, offsets, **kw)
 
 
 def to_opaque_batch(plan: Plan, native: torch.Tensor, n: int, heap: torch.Tensor | None = None,
