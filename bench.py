@@ -49,6 +49,9 @@ def parse():
                     help="also time each kernel alone after evicting the caches")
     ap.add_argument("--gather", action="store_true",
                     help="also time an RCCL gather of encoded shards to rank 0 (reported apart)")
+    ap.add_argument("--msgs", action="store_true",
+                    help="also time the record-marked message path (xdr_to_msg per record, the "
+                         "device record index from the marks, xdr_from_msg per message)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--schema", default="rec128",
                     choices=["rec128", "numerics", "recvar", "rpc", "vecrec"],
@@ -188,6 +191,76 @@ def cold_cache(mar, nat, xdr, back, n, alg_bytes, reps=5):
                         f"median of {reps}"}
 
 
+def messages_leg(schema, plan, mar, nat, heap, n, reps=20):
+    """Record-marked messages (message_t, RFC 5531): encode_msgs = xdr_to_msg
+    per record, the device index of the stream's marks (read_message framing),
+    decode_msgs = xdr_from_msg per message.  Each timed alone with HIP events
+    on the launch stream; reported apart from the headline."""
+    dev = nat.device
+    stream = torch.cuda.current_stream()
+    s = stream.cuda_stream
+    X = n * plan.fixed_size if plan.is_fixed else \
+        int(mar.serial_sizes(nat, n).to(torch.int64).sum().item())
+    total = X + 4 * n
+    out = torch.empty(total, dtype=torch.uint8, device=dev)
+    offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    idx = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    cnt = torch.empty(1, dtype=torch.int64, device=dev)
+    back = torch.empty(n * plan.stride, dtype=torch.uint8, device=dev)
+    hout = None if plan.is_fixed else torch.empty(plan.decode_heap_bytes(total), dtype=torch.uint8,
+                                                  device=dev)
+    L = A.lib()
+    maxlen = min(plan.max_record_bytes, A.INDEX_MAX_MSG)
+    ws = torch.empty(max(L.xdrg_index_workspace_size(total, maxlen), 16), dtype=torch.uint8, device=dev)
+    st = M.Status(dev)
+    st.init(s)
+    mar.status.init(s)
+
+    def index():
+        A.check(L.xdrg_index_msgs(out.data_ptr(), total, maxlen, n, idx.data_ptr(), cnt.data_ptr(),
+                                  ws.data_ptr(), ws.numel(), st.ptr, s), "xdrg_index_msgs")
+
+    legs = {"encode_msgs": lambda: mar.launch_encode_msgs(nat, n, out, offs, heap=heap, stream=s),
+            "index_msgs": index,
+            "decode_msgs": lambda: mar.launch_decode_msgs(out, n, back, idx, heap_out=hout, stream=s)}
+    for f in legs.values():
+        f()
+    torch.cuda.synchronize()
+    times = {k: [] for k in legs}
+    for _ in range(reps):
+        for k, f in legs.items():
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            ev[0].record(stream)
+            f()
+            ev[1].record(stream)
+            torch.cuda.synchronize()
+            times[k].append(ev[0].elapsed_time(ev[1]))
+    mar.check(s)
+    e = st.read(s)
+    ok_index = e.code == 0 and int(cnt.item()) == n and bool(torch.equal(idx, offs))
+    x2 = torch.empty_like(out)
+    o2 = torch.empty_like(offs)
+    mar.status.init(s)
+    mar.launch_encode_msgs(back, n, x2, o2, heap=hout if hout is not None else heap, stream=s)
+    mar.check(s)
+    r = {k: round(float(np.mean(v)), 4) for k, v in times.items()}
+    ms = r["encode_msgs"] + r["index_msgs"] + r["decode_msgs"]
+    res = {"stream_bytes": total,
+           "encode_msgs_ms": r["encode_msgs"], "index_msgs_ms": r["index_msgs"],
+           "decode_msgs_ms": r["decode_msgs"],
+           "encode_index_decode_gib_s": round(2 * total / GIB / (ms * 1e-3), 2),
+           "index_gb_s": round((total + 8 * (n + 1)) / (r["index_msgs"] * 1e-3) / 1e9, 1),
+           "index_ok": ok_index, "round_trip_ok": bool(torch.equal(x2, out)),
+           "protocol": f"HIP events around each launch, mean of {reps}"}
+    man = os.path.join(ROOT, "tests", "golden", "manifest.json")
+    if os.path.exists(man):
+        h = json.load(open(man))["hashes"].get(f"{schema}_{n}", {})
+        if "msgs" in h:
+            res["bit_exact_vs_reference"] = (
+                hashlib.sha256(out.cpu().numpy().tobytes()).hexdigest() == h["msgs"])
+    return res
+
+
 def setup(schema, n, dev, rank, world):
     """Plan, resident inputs and preallocated outputs for one rank."""
     plan = M.Plan(S.ALL[schema])
@@ -320,9 +393,10 @@ def main():
     if os.path.exists(tf):
         try:
             tj = json.load(open(tf))
-            if tj.get("records") == n and tj.get("schema", "rec128") == args.schema \
-                    and tj.get("kernel") == kern:
-                traffic = tj.get("hbm_bytes_per_launch")
+            tab = tj.get("hbm_bytes_per_launch", {})
+            parts = [tab.get(f"{args.schema}:{k}") for k in kern.split("+")]
+            if tj.get("records") == n and all(p is not None for p in parts):
+                traffic = int(sum(parts))  # multi-kernel phases: sum of their launches
         except Exception:
             traffic = None
     wl = {"rec128": "rec128: 1M fixed-width 128-byte XDR records per GPU",
@@ -362,6 +436,8 @@ def main():
     if world == 1 and args.cold and plan.is_fixed:
         line["cold_cache"] = cold_cache(mar, nat, xdr, back, n, alg_bytes)
         mar.check(s)
+    if world == 1 and args.msgs:
+        line["messages"] = messages_leg(args.schema, plan, mar, nat, heap, n)
     if world == 1 and args.host_inclusive and plan.is_fixed:
         try:
             line["host_inclusive"] = host_inclusive(mar, plan, nat, n, plan.fixed_size)

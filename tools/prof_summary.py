@@ -1,17 +1,22 @@
 """Summarise rocprofv3 outputs of bench.py into profiles/ (committed).
 
-    python tools/prof_summary.py <round tag> <stats dir> <fetch dir> <write dir> [records]
+    python tools/prof_summary.py <round tag> <prof dir> [schemas...]
 
-Writes profiles/<tag>_kernel_stats.csv (the rocprofv3 --stats table as
-produced), profiles/<tag>_pmc.json (per-kernel FETCH_SIZE / WRITE_SIZE per
-launch and HBM bytes with the gfx950 correction: FETCH_SIZE reads half the
-bytes of a wide coalesced stream, so hbm = 2*FETCH_SIZE + WRITE_SIZE, KiB),
-and profiles/pmc_traffic.json for bench.py's roofline.traffic.
+<prof dir> is what tools/gpu/r01_prof.sh leaves: stats_<schema>/,
+fetch_<schema>/, write_<schema>/ per schema.  Writes, per schema,
+profiles/<tag>_<schema>_kernel_stats.csv (the rocprofv3 --stats table as
+produced) and one profiles/<tag>_pmc.json with per-kernel FETCH_SIZE /
+WRITE_SIZE per launch and HBM bytes with the gfx950 correction
+(MI355X_MICROARCH.md "HBM": FETCH_SIZE reports half the bytes of a wide
+coalesced stream, so hbm = 2*FETCH_SIZE + WRITE_SIZE; both in KiB), plus
+profiles/pmc_traffic.json, the per-(schema, kernel) traffic table bench.py
+reads for roofline.traffic.
 """
 import collections
 import csv
 import json
 import os
+import re
 import shutil
 import sys
 
@@ -26,31 +31,41 @@ def counters(d):
     return agg
 
 
+def short(kname):
+    m = re.search(r"(k_\w+)", kname)
+    return m.group(1) if m else kname.split("(")[0][:60]
+
+
 def main():
-    tag, sd, fd, wd = sys.argv[1:5]
-    records = int(sys.argv[5]) if len(sys.argv) > 5 else 1 << 20
+    tag, pd = sys.argv[1:3]
+    schemas = sys.argv[3:] or ["rec128", "numerics", "recvar", "rpc", "vecrec"]
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
-    stats = [os.path.join(sd, x) for x in os.listdir(sd) if x.endswith("kernel_stats.csv")][0]
-    shutil.copy(stats, os.path.join(prof, f"{tag}_kernel_stats.csv"))
-    f, w = counters(fd), counters(wd)
-    out = {}
-    for (k, c), v in list(f.items()) + list(w.items()):
-        e = out.setdefault(k, {"launches": len(v)})
-        e[c + "_KiB_per_launch"] = sum(v) / len(v)
-    for k, e in out.items():
-        if "FETCH_SIZE_KiB_per_launch" in e and "WRITE_SIZE_KiB_per_launch" in e:
-            e["hbm_bytes_per_launch"] = int(1024 * (2 * e["FETCH_SIZE_KiB_per_launch"]
-                                                    + e["WRITE_SIZE_KiB_per_launch"]))
-    json.dump(out, open(os.path.join(prof, f"{tag}_pmc.json"), "w"), indent=1)
-    for k, e in out.items():
-        if "k_fixed_reg" in k and "hbm_bytes_per_launch" in e:
-            json.dump({"kernel": "k_fixed_reg", "schema": "rec128", "records": records,
-                       "hbm_bytes_per_launch": e["hbm_bytes_per_launch"],
-                       "source": f"profiles/{tag}_pmc.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
-                                 "passes of bench.py; 2*FETCH_SIZE+WRITE_SIZE, gfx950 correction)"},
-                      open(os.path.join(prof, "pmc_traffic.json"), "w"), indent=1)
-    print(json.dumps(out, indent=1)[:3000])
+    allpmc, traffic = {}, {}
+    for sch in schemas:
+        sd = os.path.join(pd, f"stats_{sch}")
+        stats = [os.path.join(sd, x) for x in os.listdir(sd) if x.endswith("kernel_stats.csv")][0]
+        shutil.copy(stats, os.path.join(prof, f"{tag}_{sch}_kernel_stats.csv"))
+        f, w = counters(os.path.join(pd, f"fetch_{sch}")), counters(os.path.join(pd, f"write_{sch}"))
+        out = {}
+        for (k, c), v in list(f.items()) + list(w.items()):
+            if not short(k).startswith("k_"):
+                continue  # torch / runtime kernels of the bench's own checks
+            e = out.setdefault(short(k), {"launches": len(v)})
+            e[c + "_KiB_per_launch"] = round(sum(v) / len(v), 1)
+        for k, e in out.items():
+            if "FETCH_SIZE_KiB_per_launch" in e and "WRITE_SIZE_KiB_per_launch" in e:
+                e["hbm_bytes_per_launch"] = int(1024 * (2 * e["FETCH_SIZE_KiB_per_launch"]
+                                                        + e["WRITE_SIZE_KiB_per_launch"]))
+                traffic[f"{sch}:{k}"] = e["hbm_bytes_per_launch"]
+        allpmc[sch] = out
+    json.dump(allpmc, open(os.path.join(prof, f"{tag}_pmc.json"), "w"), indent=1)
+    json.dump({"records": 1 << 20,
+               "hbm_bytes_per_launch": traffic,
+               "source": f"profiles/{tag}_pmc.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes "
+                         "of bench.py --schema <s>; 2*FETCH_SIZE+WRITE_SIZE, gfx950 correction)"},
+              open(os.path.join(prof, "pmc_traffic.json"), "w"), indent=1)
+    print(json.dumps(allpmc, indent=1)[:4000])
 
 
 if __name__ == "__main__":

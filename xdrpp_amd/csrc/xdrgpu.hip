@@ -106,6 +106,38 @@ __device__ __forceinline__ uint32_t keep_bytes(int32_t k) {  // mask of the low 
 
 constexpr uint32_t kSizeErr = 0x80000000u;
 
+// Single-wave workgroups: LDS written by some lanes and read by others needs
+// only ordering within the wave (LDS executes a wave's instructions in
+// order), not __syncthreads(), whose workgroup-scope release would also
+// wait for every outstanding global store of the wave (s_waitcnt vmcnt(0)).
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Stage nbytes (a multiple of 4) of native records from a 16-byte aligned
+// global address to LDS: 16-byte loads, up to 4 per lane in flight before
+// any LDS store (one memory round trip per 4 KiB per wave).
+__device__ __forceinline__ void stage_tile(uint8_t *tile, const uint8_t *src, uint32_t nbytes,
+                                           uint32_t lane, uint32_t nthreads) {
+  const uint32_t n16 = nbytes / 16u;
+  for (uint32_t i0 = 0; i0 < n16; i0 += 4u * nthreads) {
+    u32x4 t[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t i = i0 + k * nthreads + lane;
+      if (i < n16) t[k] = reinterpret_cast<const u32x4 *>(src)[i];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t i = i0 + k * nthreads + lane;
+      if (i < n16) reinterpret_cast<u32x4 *>(tile)[i] = t[k];
+    }
+  }
+  for (uint32_t i = n16 * 4u + lane; i < nbytes / 4u; i += nthreads)
+    reinterpret_cast<uint32_t *>(tile)[i] = reinterpret_cast<const uint32_t *>(src)[i];
+}
+
 // ------------------------------------------- record marks (RFC 5531)
 // message_t keeps a 4-byte mark BE(size | 0x80000000) in front of the
 // message bytes (message_t::alloc, xdrpp/marshal.cc:15-31: always one
@@ -282,16 +314,13 @@ __global__ __launch_bounds__(64) void k_var_size(const uint8_t *__restrict__ nat
     const uint32_t nbytes = nrec * stride;
     const uint8_t *nsrc = native + wr0 * stride;
     if ((reinterpret_cast<uintptr_t>(nsrc) & 15u) == 0) {
-      for (uint32_t i = lane; i < nbytes / 16u; i += 64u)
-        reinterpret_cast<u32x4 *>(tile)[i] = reinterpret_cast<const u32x4 *>(nsrc)[i];
-      for (uint32_t i = (nbytes / 16u) * 4u + lane; i < nbytes / 4u; i += 64u)
-        reinterpret_cast<uint32_t *>(tile)[i] = reinterpret_cast<const uint32_t *>(nsrc)[i];
+      stage_tile(tile, nsrc, nbytes, lane, 64u);
     } else {
       for (uint32_t i = lane; i < nbytes / 4u; i += 64u)
         reinterpret_cast<uint32_t *>(tile)[i] = reinterpret_cast<const uint32_t *>(nsrc)[i];
     }
   }
-  __syncthreads();
+  wave_sync();
   const uint8_t *nat = TILE ? tile + lane * stride : native + r * stride;
   uint64_t s = mark;  // record-marked batches: the message's 4-byte mark
   uint32_t pc = r < n ? 0u : kPcDone, bad_op = kPcDone;
@@ -906,7 +935,10 @@ __global__ __launch_bounds__(64) void k_var_encode_i(
   const uint32_t nrec = static_cast<uint32_t>(min<uint64_t>(64, n - wr0));
 
   // ---- record offsets: wave scan of the sizes on top of the block base
+  // (sizes, block base and the native tile are loaded in one round trip)
   const uint32_t sz = r < n ? sizes[r] : kSizeErr;
+  const uint64_t wave_out = block_base[blockIdx.x];
+  stage_tile(tile, native + wr0 * stride, nrec * stride, lane, 64u);
   const bool szok = !(sz & kSizeErr);
   const unsigned long long v = szok ? sz : 0ull;
   unsigned long long incl = v;
@@ -914,19 +946,10 @@ __global__ __launch_bounds__(64) void k_var_encode_i(
     const unsigned long long x = __shfl_up(incl, o, 64);
     if (lane >= static_cast<uint32_t>(o)) incl += x;
   }
-  const uint64_t wave_out = block_base[blockIdx.x];
   const uint64_t off = wave_out + incl - v;
   const uint64_t T = rl64(incl, 63);  // bytes of the wave's stretch
   if (r < n) offsets[r] = off;
-  {
-    const uint32_t nbytes = nrec * stride;
-    const uint8_t *nsrc = native + wr0 * stride;
-    for (uint32_t i = lane; i < nbytes / 16u; i += 64u)
-      reinterpret_cast<u32x4 *>(tile)[i] = reinterpret_cast<const u32x4 *>(nsrc)[i];
-    for (uint32_t i = (nbytes / 16u) * 4u + lane; i < nbytes / 4u; i += 64u)
-      reinterpret_cast<uint32_t *>(tile)[i] = reinterpret_cast<const uint32_t *>(nsrc)[i];
-  }
-  __syncthreads();
+  wave_sync();
   XDRG_STAMP(1);
   XDRG_STAMP(2);
 
@@ -1059,60 +1082,69 @@ __global__ __launch_bounds__(64) void k_var_encode_i(
       e += nq;
     }
   }
-  __syncthreads();
+  wave_sync();
 
-  // ---- payload chunks: heap -> image, U chunks in flight per lane
+  // ---- payload chunks: heap -> image, U chunks in flight per lane.  Three
+  // passes per batch: the chunk descriptors (LDS), then the U loads with no
+  // use of a loaded value in between (so none waits for another), then the
+  // rare chunk that ends past the heap, the pad masks and the stores.
   for (uint32_t c0 = 0; c0 < M; c0 += 64u * U) {
     u32x4 val[U];
-    uint32_t at[U], nb[U];
+    uint64_t hs[U];
+    uint32_t at[U], nb[U], rem[U];
+    bool fast[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t c = c0 + 64u * u + lane;
       nb[u] = 0u;
       at[u] = 0u;
-      val[u] = u32x4{0u, 0u, 0u, 0u};
+      hs[u] = 0u;
+      rem[u] = 16u;
+      fast[u] = false;
       if (c < M) {
         const uint32_t m = map[c];
         const echunk_desc d = desc[(m >> 10) * KMAX + ((m >> 8) & 3u)];
         const uint32_t q16 = (m & 0xffu) << 4;
-        const uint64_t hs = d.src + q16;
-        u32x4 x;
-        if (hs + 16u <= heap_len) {
-          x = ld16u(heap + hs);
-        } else {
-          x = u32x4{unaligned_word(heap, heap_len, hs), unaligned_word(heap, heap_len, hs + 4),
-                    unaligned_word(heap, heap_len, hs + 8), unaligned_word(heap, heap_len, hs + 12)};
-        }
-        const int32_t rem = static_cast<int32_t>(d.len - q16);
-        if (rem < 16) {  // zero the pad bytes after the payload (put_bytes)
-          x.x &= keep_bytes(rem);
-          x.y &= keep_bytes(rem - 4);
-          x.z &= keep_bytes(rem - 8);
-          x.w &= keep_bytes(rem - 12);
-        }
-        val[u] = x;
+        hs[u] = d.src + q16;
+        rem[u] = d.len - q16;
         at[u] = d.dst + q16;
         nb[u] = min(16u, ((d.len + 3u) & ~3u) - q16);
+        fast[u] = hs[u] + 16u <= heap_len;
       }
     }
 #pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (fast[u]) val[u] = ld16u(heap + hs[u]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
     for (int u = 0; u < U; ++u) {
       if (!nb[u]) continue;
+      u32x4 x = val[u];
+      if (!fast[u])
+        x = u32x4{unaligned_word(heap, heap_len, hs[u]), unaligned_word(heap, heap_len, hs[u] + 4),
+                  unaligned_word(heap, heap_len, hs[u] + 8), unaligned_word(heap, heap_len, hs[u] + 12)};
+      const int32_t r = static_cast<int32_t>(rem[u]);
+      if (r < 16) {  // zero the pad bytes after the payload (put_bytes)
+        x.x &= keep_bytes(r);
+        x.y &= keep_bytes(r - 4);
+        x.z &= keep_bytes(r - 8);
+        x.w &= keep_bytes(r - 12);
+      }
       if (at[u] + 16u <= C) {
         uint32_t *w = reinterpret_cast<uint32_t *>(im + at[u]);
-        w[0] = val[u].x;
-        if (nb[u] > 4u) w[1] = val[u].y;
-        if (nb[u] > 8u) w[2] = val[u].z;
-        if (nb[u] > 12u) w[3] = val[u].w;
+        w[0] = x.x;
+        if (nb[u] > 4u) w[1] = x.y;
+        if (nb[u] > 8u) w[2] = x.z;
+        if (nb[u] > 12u) w[3] = x.w;
       } else {
-        img_put(im, C, gout, at[u], val[u].x);
-        if (nb[u] > 4u) img_put(im, C, gout, at[u] + 4, val[u].y);
-        if (nb[u] > 8u) img_put(im, C, gout, at[u] + 8, val[u].z);
-        if (nb[u] > 12u) img_put(im, C, gout, at[u] + 12, val[u].w);
+        img_put(im, C, gout, at[u], x.x);
+        if (nb[u] > 4u) img_put(im, C, gout, at[u] + 4, x.y);
+        if (nb[u] > 8u) img_put(im, C, gout, at[u] + 8, x.z);
+        if (nb[u] > 12u) img_put(im, C, gout, at[u] + 12, x.w);
       }
     }
   }
-  __syncthreads();
+  wave_sync();
   XDRG_STAMP(4);
 
   // ---- image -> global: aligned 16-byte chunks, partial words at the edges
@@ -1228,7 +1260,7 @@ __global__ __launch_bounds__(64) void k_var_decode_w(
       }
     }
   }
-  __syncthreads();
+  wave_sync();
   XDRG_STAMP(1);
 
   // word reader: window for stream bytes in [ws, ws + wc), global otherwise
@@ -1353,7 +1385,7 @@ __global__ __launch_bounds__(64) void k_var_decode_w(
     }
     if (ok && p != b) report(err, r, kOpRecordLevel, XDRG_ERR_TRAILING);
   }
-  __syncthreads();
+  wave_sync();
   XDRG_STAMP(2);
   uint8_t *ndst = native + wr0 * stride;
   const uint32_t nbytes = nrec * stride;
@@ -1372,17 +1404,21 @@ __global__ __launch_bounds__(64) void k_var_decode_w(
 // position), so finding the messages is list ranking.  The stream is cut
 // into segments of kIxSW words; a message is at most max_msg_len bytes,
 // so the chain enters every segment within its first K = max_msg_len/4 + 1
-// words.
-//   k_ix_seg   per segment, pointer jumping in LDS over all its words: the
-//              exit (entry word of the next segment) and the number of
-//              marks passed, or the terminal state (end of stream or a
-//              framing error), for each of the K entries;
+// words.  Only words that read as a well-formed mark ("valid" nodes: a
+// last-fragment mark of a bounded, 4-aligned size that fits the stream)
+// can continue a chain; every other word ends any chain that reaches it.
+//   k_ix_seg   per segment: the valid nodes (written out as a list), then
+//              pointer jumping over them in LDS: the exit (entry word of
+//              the next segment) and the marks passed, or "ends here", for
+//              each of the K entries;
 //   k_ix_up    composes F consecutive tables into one (levels until one
 //              node remains);
 //   k_ix_down  from the top: each node's entry and the count of messages
 //              before it, which reach every segment;
-//   k_ix_emit  per segment on the chain, one lane walks it from its entry
-//              through an LDS copy and writes the offsets.
+//   k_ix_emit  per segment on the chain: the nodes reachable from its
+//              entry (doubling over the valid-node list), ranked by
+//              position, give the offsets; the word where the chain ends
+//              is classified exactly as read_message would (ix_mark).
 constexpr uint32_t kIxSW = 4096;  // words per segment (16 KiB)
 constexpr uint32_t kIxLog = 12;   // log2(kIxSW) pointer-jumping rounds
 constexpr uint64_t kIxCnt = (1ull << 40) - 1;  // table / entry word: count bits
@@ -1423,40 +1459,120 @@ __device__ __forceinline__ uint32_t ix_mark(uint32_t raw, uint64_t w, uint64_t l
   return IX_RUN;
 }
 
-// LDS node: target (13 bits: < kIxSW a word of this segment, kIxSW + e =
-// entry e of the next one) | marks passed << 13 (13 bits) | state << 26.
-// Table word: marks (40 bits) | exit entry << 40 (16 bits) | state << 56.
+// 16 words of a segment per thread (4 x 16 bytes, all in flight at once):
+// raw[4g + j] = word 4 * (tid + 256 g) + j of the segment (0 past the stream).
+__device__ __forceinline__ void ix_load16(const uint8_t *__restrict__ s, uint64_t len, uint64_t w0,
+                                          uint32_t tid, uint32_t raw[16]) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const uint64_t w = w0 + 4u * (tid + 256u * g);
+    if (4 * w + 16 <= len) {
+      const u32x4 q = ld16u(s + 4 * w);
+      raw[4 * g] = q.x; raw[4 * g + 1] = q.y; raw[4 * g + 2] = q.z; raw[4 * g + 3] = q.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) raw[4 * g + j] = 4 * (w + j) + 4 <= len ? ld32(s + 4 * (w + j)) : 0u;
+    }
+  }
+}
+
+// Valid-node test with segment-local 32-bit arithmetic: node i of a segment
+// whose stream bytes end `lim` bytes after its start (lim >= 4 * i).  A
+// valid mark's first two bytes are 0x80 0x00 (last-fragment bit, size <
+// 2^16 and the pre-swap size test passes), so one compare rejects almost
+// every other word.  Returns the next mark's node index (may be past the
+// segment) or 0xffffffff when a chain reaching node i ends there.
+__device__ __forceinline__ uint32_t ix_next(uint32_t raw, uint32_t i, uint32_t lim, uint32_t maxlen) {
+  const uint32_t at = 4u * i;
+  if ((raw & 0xffffu) != 0x80u || lim - at < 4u) return 0xffffffffu;
+  const uint32_t size = ((raw >> 8) & 0xff00u) | (raw >> 24);
+  if (size > maxlen || (size & 3u) || lim - at - 4u < size) return 0xffffffffu;
+  return i + 1u + size / 4u;
+}
+
+// LDS node: target (13 bits: < kIxSW a node of this segment, kIxSW + e =
+// entry e of the next one) | marks passed << 13 (13 bits) | ends << 26.
+// Table word: marks (40 bits) | exit entry << 40 (16 bits) | ends << 56.
+// List word of a valid node: node index | target << 12.
+constexpr uint32_t kIxEnds = 1u << 26;
+
 __global__ __launch_bounds__(256) void k_ix_seg(const uint8_t *__restrict__ s, uint64_t len,
                                                 uint32_t maxlen, uint32_t K,
-                                                uint64_t *__restrict__ tab) {
-  __shared__ uint32_t node[kIxSW];
+                                                uint64_t *__restrict__ tab,
+                                                uint32_t *__restrict__ list,
+                                                uint32_t *__restrict__ lcount) {
+  __shared__ __attribute__((aligned(16))) uint32_t node[kIxSW];
+  __shared__ uint16_t lst[kIxSW];
+  __shared__ uint32_t wtot[4];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
   const uint64_t w0 = static_cast<uint64_t>(blockIdx.x) * kIxSW;
-  for (uint32_t i = threadIdx.x; i < kIxSW; i += 256) {
-    const uint64_t w = w0 + i;
-    const uint32_t raw = 4 * w + 4 <= len ? ld32(s + 4 * w) : 0u;
-    uint64_t nx = 0;
-    const uint32_t st = ix_mark(raw, w, len, maxlen, &nx);
-    node[i] = st ? (st << 26) : (static_cast<uint32_t>(nx - w0) | (1u << 13));
+  const uint32_t lim = static_cast<uint32_t>(min<uint64_t>(len - 4 * w0, 0xfffffff0ull));
+  uint32_t raw[16];
+  ix_load16(s, len, w0, tid, raw);
+  uint32_t vmask = 0, vnext[16];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    uint32_t nv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int q = 4 * g + j;
+      const uint32_t i = 4u * (tid + 256u * g) + j;
+      vnext[q] = ix_next(raw[q], i, lim, maxlen);
+      if (vnext[q] != 0xffffffffu) vmask |= 1u << q;
+      nv[j] = vnext[q] != 0xffffffffu ? (vnext[q] | (1u << 13)) : kIxEnds;
+    }
+    reinterpret_cast<u32x4 *>(node)[tid + 256u * g] = u32x4{nv[0], nv[1], nv[2], nv[3]};
   }
+  // compact the valid nodes: block-wide exclusive scan of the counts
+  const uint32_t cnt = __popc(vmask);
+  uint32_t incl = cnt;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(incl, o, 64);
+    if (lane >= static_cast<uint32_t>(o)) incl += y;
+  }
+  if (lane == 63) wtot[wid] = incl;
   __syncthreads();
-  // In place: a node read mid-round is either state, each a correct jump.
-  for (uint32_t k = 0; k < kIxLog; ++k) {
-    for (uint32_t i = threadIdx.x; i < kIxSW; i += 256) {
+  uint32_t base = incl - cnt, nvalid = 0;
+  for (uint32_t w = 0; w < 4; ++w) {
+    if (w < wid) base += wtot[w];
+    nvalid += wtot[w];
+  }
+  uint32_t *gl = list + static_cast<uint64_t>(blockIdx.x) * kIxSW;
+#pragma unroll
+  for (int q = 0; q < 16; ++q)
+    if (vmask & (1u << q)) {
+      const uint32_t i = 4u * (tid + 256u * (q >> 2)) + (q & 3);
+      lst[base] = static_cast<uint16_t>(i);
+      gl[base] = i | (vnext[q] << 12);
+      ++base;
+    }
+  if (tid == 0) lcount[blockIdx.x] = nvalid;
+  __syncthreads();
+  // Pointer jumping over the valid nodes, in place: a node read mid-round
+  // is either state, each a correct jump.  Stops once no valid node points
+  // inside the segment.
+  for (uint32_t k = 0; k < kIxLog + 1; ++k) {
+    bool inside = false;
+    for (uint32_t j = tid; j < nvalid; j += 256) {
+      const uint32_t i = lst[j];
       const uint32_t v = node[i];
       const uint32_t t = v & 0x1fffu;
-      if ((v >> 26) == 0 && t < kIxSW) {
+      if (!(v & kIxEnds) && t < kIxSW) {
         const uint32_t u = node[t];
         const uint32_t c = ((v >> 13) & 0x1fffu) + ((u >> 13) & 0x1fffu);
-        node[i] = (u & ~(0x1fffu << 13)) | (c << 13);
+        const uint32_t nv = (u & ~(0x1fffu << 13)) | (c << 13);
+        node[i] = nv;
+        inside |= !(nv & kIxEnds) && (nv & 0x1fffu) < kIxSW;
       }
     }
-    __syncthreads();
+    if (!__syncthreads_or(inside)) break;
   }
-  for (uint32_t e = threadIdx.x; e < K; e += 256) {
+  if (!tab) return;
+  for (uint32_t e = tid; e < K; e += 256) {
     const uint32_t v = node[e];
-    const uint64_t st = v >> 26, c = (v >> 13) & 0x1fffu;
+    const uint64_t c = (v >> 13) & 0x1fffu;
     tab[static_cast<uint64_t>(blockIdx.x) * K + e] =
-        st ? (st << 56 | c) : (static_cast<uint64_t>((v & 0x1fffu) - kIxSW) << 40 | c);
+        (v & kIxEnds) ? (1ull << 56 | c) : (static_cast<uint64_t>((v & 0x1fffu) - kIxSW) << 40 | c);
   }
 }
 
@@ -1505,7 +1621,7 @@ __global__ __launch_bounds__(64) void k_ix_down(const uint64_t *__restrict__ tab
   const uint64_t *src = tab + c0 * K;
   if (LDS) {
     for (uint32_t i = threadIdx.x; i < nc * K; i += 64) stg[i] = src[i];
-    __syncthreads();
+    wave_sync();
   }
   if (threadIdx.x != 0) return;
   uint64_t x = (e >> 40) & 0xffffu, b = e & kIxCnt;
@@ -1520,45 +1636,146 @@ __global__ __launch_bounds__(64) void k_ix_down(const uint64_t *__restrict__ tab
   }
 }
 
-// Segments on the chain: lane 0 walks the segment's marks (words staged in
-// LDS) from its entry and writes their offsets; the segment where the
-// chain ends writes offsets[count] and the count.
+// Segments on the chain.  The nodes reachable from the entry x are found by
+// doubling over the segment's valid-node list (Reach_{k+1} = Reach_k plus
+// the 2^k-th successors of Reach_k); since positions grow along the chain,
+// a node's message index is b + (reachable nodes before it).  The node
+// where the chain ends (the last reachable one, unless the chain leaves the
+// segment) is classified exactly as read_message would (ix_mark).
+__device__ void ix_final(const uint8_t *__restrict__ s, uint64_t len, uint32_t maxlen, uint64_t w,
+                         uint64_t m, uint64_t max_msgs, uint64_t *__restrict__ offsets,
+                         unsigned long long *count, unsigned long long *err) {
+  if (m > max_msgs) return;
+  offsets[m] = 4 * w;
+  uint64_t nx = 0;
+  const uint32_t st = ix_mark(4 * w + 4 <= len ? ld32(s + 4 * w) : 0u, w, len, maxlen, &nx);
+  if (st != IX_END) report(err, m, kOpRecordLevel, m == max_msgs ? XDRG_ERR_MSG_COUNT : ix_error(st));
+  atomicMin(count, m);
+}
+
 __global__ __launch_bounds__(256) void k_ix_emit(const uint8_t *__restrict__ s, uint64_t len,
                                                  uint32_t maxlen, const uint64_t *__restrict__ ent,
+                                                 const uint32_t *__restrict__ list,
+                                                 const uint32_t *__restrict__ lcount,
                                                  uint64_t *__restrict__ offsets, uint64_t max_msgs,
                                                  unsigned long long *count,
                                                  unsigned long long *err) {
-  __shared__ uint32_t wd[kIxSW];
+  // J: successor of a valid node (0xffff: not a valid node); lst: the valid
+  // nodes; nj / mk: a round's new successors and marks (double buffer)
+  __shared__ __attribute__((aligned(16))) uint16_t J[kIxSW];
+  __shared__ uint16_t lst[kIxSW], nj[kIxSW], mk[kIxSW];
+  __shared__ __attribute__((aligned(16))) uint8_t on[kIxSW];  // reachable from the entry
+  __shared__ uint32_t seen[kIxSW / 32];                       // successor of a node >= x
+  __shared__ uint32_t wtot[4];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+  // the entry, the list length and the list's first 256 words in one round trip
+  const uint32_t *gl = list + static_cast<uint64_t>(blockIdx.x) * kIxSW;
   const uint64_t e = ent[blockIdx.x];
+  const uint32_t nvalid = lcount[blockIdx.x];
+  const uint32_t v0 = gl[tid];  // inside the workspace; used only when tid < nvalid
   if (e >> 63) return;
-  uint64_t b = e & kIxCnt;
+  const uint64_t b = e & kIxCnt;
   if (b > max_msgs) return;  // past the index's capacity: reported where it ran out
+  const uint32_t x = static_cast<uint32_t>((e >> 40) & 0xffffu);
   const uint64_t w0 = static_cast<uint64_t>(blockIdx.x) * kIxSW;
-  for (uint32_t i = threadIdx.x; i < kIxSW; i += 256) {
-    const uint64_t w = w0 + i;
-    wd[i] = 4 * w + 4 <= len ? ld32(s + 4 * w) : 0u;
-  }
+  const u32x4 ones = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+  reinterpret_cast<u32x4 *>(J)[tid] = ones;
+  reinterpret_cast<u32x4 *>(J)[tid + 256] = ones;
+  reinterpret_cast<u32x4 *>(on)[tid] = u32x4{0, 0, 0, 0};
+  if (tid < kIxSW / 32) seen[tid] = 0;
   __syncthreads();
-  if (threadIdx.x != 0) return;
-  uint64_t i = (e >> 40) & 0xffffu;
-  while (i < kIxSW) {
-    const uint64_t w = w0 + i;
-    uint64_t nx = 0;
-    const uint32_t st = ix_mark(wd[i], w, len, maxlen, &nx);
-    offsets[b] = 4 * w;
-    if (st == IX_END) { atomicMin(count, b); return; }
-    if (b == max_msgs) {
-      report(err, b, kOpRecordLevel, XDRG_ERR_MSG_COUNT);
-      atomicMin(count, b);
-      return;
+  for (uint32_t j = tid; j < nvalid; j += 256) {
+    const uint32_t v = j == tid ? v0 : gl[j];
+    J[v & 0xfffu] = static_cast<uint16_t>(v >> 12);
+    lst[j] = static_cast<uint16_t>(v & 0xfffu);
+  }
+  if (tid == 0) on[x] = 1;
+  __syncthreads();
+  if (J[x] == 0xffffu) {  // the chain ends at its entry
+    if (tid == 0) ix_final(s, len, maxlen, w0 + x, b, max_msgs, offsets, count, err);
+    return;
+  }
+  // Fast path: when the valid nodes from x on form one path (no node is the
+  // successor of two of them and each but x is the successor of one), the
+  // chain is exactly those nodes plus the word where it ends; true unless
+  // message bodies hold words that read as marks.
+  bool slow = false;
+  for (uint32_t j = tid; j < nvalid; j += 256) {
+    const uint32_t i = lst[j];
+    if (i < x) continue;
+    on[i] = 1;
+    const uint32_t t = J[i];
+    if (t < kIxSW) {
+      const uint32_t bit = 1u << (t & 31u);
+      if (atomicOr(&seen[t >> 5], bit) & bit) slow = true;  // two predecessors
+      if (J[t] == 0xffffu) on[t] = 1;                        // the chain ends at t
     }
-    if (st != IX_RUN) {
-      report(err, b, kOpRecordLevel, ix_error(st));
-      atomicMin(count, b);
-      return;
+  }
+  slow = __syncthreads_or(slow);
+  if (!slow) {
+    for (uint32_t j = tid; j < nvalid; j += 256) {
+      const uint32_t i = lst[j];
+      if (i > x && !(seen[i >> 5] & (1u << (i & 31u)))) slow = true;  // a second path
     }
-    ++b;
-    i = nx - w0;
+    slow = __syncthreads_or(slow);
+  }
+  if (slow) {
+    reinterpret_cast<u32x4 *>(on)[tid] = u32x4{0, 0, 0, 0};
+    __syncthreads();
+    if (tid == 0) on[x] = 1;
+    __syncthreads();
+  }
+  // slow path, doubling: read phase into nj / mk, barrier, write phase (Jacobi)
+  for (uint32_t k = 0; slow && k < 2 * kIxLog + 2; ++k) {
+    for (uint32_t j = tid; j < nvalid; j += 256) {
+      const uint32_t i = lst[j];
+      const uint32_t ji = J[i];
+      const uint32_t jj = ji < kIxSW ? J[ji] : 0xffffu;
+      nj[j] = static_cast<uint16_t>(jj != 0xffffu ? jj : ji);
+      mk[j] = static_cast<uint16_t>(on[i] && ji < kIxSW ? ji : 0xffffu);
+    }
+    __syncthreads();
+    bool changed = false;
+    for (uint32_t j = tid; j < nvalid; j += 256) {
+      const uint32_t i = lst[j], m = mk[j], v = nj[j];
+      if (m != 0xffffu && !on[m]) { on[m] = 1; changed = true; }
+      if (v != J[i]) { J[i] = static_cast<uint16_t>(v); changed = true; }
+    }
+    if (!__syncthreads_or(changed)) break;
+  }
+  // rank the reachable nodes by position: thread t owns nodes [16t, 16t + 16)
+  const u32x4 f = reinterpret_cast<const u32x4 *>(on)[tid];
+  const uint32_t fw[4] = {f.x, f.y, f.z, f.w};
+  uint32_t cnt = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) cnt += __popc(fw[q] & 0x01010101u);
+  uint32_t incl = cnt;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(incl, o, 64);
+    if (lane >= static_cast<uint32_t>(o)) incl += y;
+  }
+  if (lane == 63) wtot[wid] = incl;
+  __syncthreads();
+  uint32_t r = incl - cnt, total = 0;
+  for (uint32_t w = 0; w < 4; ++w) {
+    if (w < wid) r += wtot[w];
+    total += wtot[w];
+  }
+  for (uint32_t q = 0; q < 16; ++q) {
+    if (!((fw[q >> 2] >> (8 * (q & 3))) & 1u)) continue;
+    const uint32_t i = 16u * tid + q;
+    const uint64_t m = b + r;
+    ++r;
+    if (r == total && J[i] == 0xffffu) {  // the chain ends at this node
+      ix_final(s, len, maxlen, w0 + i, m, max_msgs, offsets, count, err);
+      continue;
+    }
+    if (m > max_msgs) continue;
+    offsets[m] = 4 * (w0 + i);
+    if (m == max_msgs) {  // a message past the index's capacity
+      report(err, m, kOpRecordLevel, XDRG_ERR_MSG_COUNT);
+      atomicMin(count, m);
+    }
   }
 }
 
@@ -1801,6 +2018,7 @@ int var_encode(const xdrg_plan &P, const void *d_native, uint64_t n, const uint8
 // n[L] * K words (below the top) and n[L] entry words.
 struct ix_layout {
   uint64_t nseg = 0;
+  size_t list = 0, lcount = 0;  // valid-node lists (kIxSW words per segment) and their lengths
   uint32_t K = 0, F = 0;
   bool lds = false;
   int top = 0;
@@ -1822,6 +2040,10 @@ ix_layout ix_plan(uint64_t len, uint32_t maxlen) {
     ++L.top;
   }
   size_t off = 0;
+  L.list = off;
+  off += align_up(L.nseg * kIxSW * 4, 256);
+  L.lcount = off;
+  off += align_up(L.nseg * 4, 256);
   for (int l = 0; l <= L.top; ++l) {
     if (l < L.top) { L.tab[l] = off; off += align_up(L.n[l] * L.K * 8, 256); }
     L.ent[l] = off;
@@ -2137,10 +2359,12 @@ int xdrg_index_msgs(const void *d_stream, uint64_t len, uint32_t max_msg_len, ui
   auto ent = [&](int l) { return reinterpret_cast<uint64_t *>(ws + L.ent[l]); };
   const uint8_t *s8 = static_cast<const uint8_t *>(d_stream);
   HIPCHK(hipMemsetAsync(d_count, 0xff, 8, s));
-  if (L.top > 0) {
-    k_ix_seg<<<L.nseg, 256, 0, s>>>(s8, len, max_msg_len, L.K, tab(0));
-    HIPCHK(hipGetLastError());
-  }
+  uint32_t *vlist = reinterpret_cast<uint32_t *>(ws + L.list);
+  uint32_t *vcount = reinterpret_cast<uint32_t *>(ws + L.lcount);
+  // the tables are needed above one segment; the valid-node lists always
+  k_ix_seg<<<L.nseg, 256, 0, s>>>(s8, len, max_msg_len, L.K, L.top > 0 ? tab(0) : nullptr, vlist,
+                                  vcount);
+  HIPCHK(hipGetLastError());
   const size_t stg = L.lds ? static_cast<size_t>(L.F) * L.K * 8 : 0;
   for (int l = 0; l + 1 < L.top; ++l) {
     if (L.lds)
@@ -2157,8 +2381,8 @@ int xdrg_index_msgs(const void *d_stream, uint64_t len, uint32_t max_msg_len, ui
       k_ix_down<false><<<L.n[l + 1], 64, 0, s>>>(tab(l), L.n[l], L.K, L.F, ent(l + 1), ent(l));
     HIPCHK(hipGetLastError());
   }
-  k_ix_emit<<<L.nseg, 256, 0, s>>>(s8, len, max_msg_len, ent(0), d_offsets, max_msgs,
-                                   reinterpret_cast<unsigned long long *>(d_count), err);
+  k_ix_emit<<<L.nseg, 256, 0, s>>>(s8, len, max_msg_len, ent(0), vlist, vcount, d_offsets,
+                                   max_msgs, reinterpret_cast<unsigned long long *>(d_count), err);
   HIPCHK(hipGetLastError());
   return XDRG_OK;
 }
