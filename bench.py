@@ -52,6 +52,9 @@ def parse():
     ap.add_argument("--msgs", action="store_true",
                     help="also time the record-marked message path (xdr_to_msg per record, the "
                          "device record index from the marks, xdr_from_msg per message)")
+    ap.add_argument("--rpc", action="store_true",
+                    help="also time the RPC header batch (xdrg_rpc_dispatch routing of 1M "
+                         "record-marked calls + xdrg_rpc_replies error replies)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--schema", default="rec128",
                     choices=["rec128", "numerics", "recvar", "rpc", "vecrec"],
@@ -261,6 +264,65 @@ def messages_leg(schema, plan, mar, nat, heap, n, reps=20):
     return res
 
 
+def rpc_leg(dev, n=1 << 20, reps=20):
+    """RPC header batches: xdrg_rpc_dispatch over n
+    record-marked CALL messages (workloads.rpc_calls: mixed routes and
+    malformed headers) and xdrg_rpc_replies of the batch's error replies.
+    HIP events on the launch stream, mean of reps; reported apart from the
+    headline.  Algorithmic bytes of dispatch: the header bytes each lane
+    reads (mark .. end of header) + its two offsets + the 64-byte record."""
+    from xdrpp_amd import rpc as R
+    stream = torch.cuda.current_stream()
+    s = stream.cuda_stream
+    sb, ob = W.rpc_calls(n)
+    st = torch.from_numpy(sb).to(dev)
+    od = torch.from_numpy(ob.view(np.int64)).to(dev)
+    procs = torch.from_numpy(W.RPC_PROCS.view(np.int32)).to(dev)
+    hd = torch.empty(n * A.RPC_HDR_BYTES, dtype=torch.uint8, device=dev)
+    rw = R.ReplyWriter(dev)
+    rout = torch.empty(36 * n, dtype=torch.uint8, device=dev)
+    roffs = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    L = A.lib()
+    rw.status.init(s)
+
+    def disp():
+        A.check(L.xdrg_rpc_dispatch(st.data_ptr(), st.numel(), od.data_ptr(), n, procs.data_ptr(),
+                                    procs.numel() // 4, hd.data_ptr(), s), "xdrg_rpc_dispatch")
+
+    legs = {"dispatch": disp, "replies": lambda: rw.launch(hd, rout, roffs, s)}
+    for f in legs.values():
+        f()
+    torch.cuda.synchronize()
+    times = {k: [] for k in legs}
+    for _ in range(reps):
+        for k, f in legs.items():
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            ev[0].record(stream)
+            f()
+            ev[1].record(stream)
+            torch.cuda.synchronize()
+            times[k].append(ev[0].elapsed_time(ev[1]))
+    e = rw.status.read(s)
+    h = hd.cpu().numpy().view(R.HDR_DTYPE)
+    hdr_bytes = int(np.where(h["err"] == 0, h["body_off"] - ob[:-1], h["end"] - ob[:-1]).sum())
+    r = {k: round(float(np.mean(v)), 4) for k, v in times.items()}
+    alg = hdr_bytes + 16 * n + A.RPC_HDR_BYTES * n
+    res = {"messages": n, "stream_bytes": int(sb.size), "dispatch_ms": r["dispatch"],
+           "replies_ms": r["replies"], "reply_bytes": int(e.total_bytes),
+           "dispatch_mmsg_s": round(n / (r["dispatch"] * 1e-3) / 1e6, 1),
+           "dispatch_alg_bytes": alg, "dispatch_gb_s": round(alg / (r["dispatch"] * 1e-3) / 1e9, 1),
+           "protocol": f"HIP events around each launch, mean of {reps}"}
+    man = os.path.join(ROOT, "tests", "golden", "manifest.json")
+    if os.path.exists(man):
+        hh = json.load(open(man))["hashes"].get(f"rpccall_{n}", {})
+        if "hdrs" in hh:
+            res["bit_exact_vs_reference"] = (
+                hashlib.sha256(h.tobytes()).hexdigest() == hh["hdrs"] and
+                hashlib.sha256(rout[:int(e.total_bytes)].cpu().numpy().tobytes()).hexdigest()
+                == hh["replies"])
+    return res
+
+
 def setup(schema, n, dev, rank, world):
     """Plan, resident inputs and preallocated outputs for one rank."""
     plan = M.Plan(S.ALL[schema])
@@ -438,6 +500,8 @@ def main():
         mar.check(s)
     if world == 1 and args.msgs:
         line["messages"] = messages_leg(args.schema, plan, mar, nat, heap, n)
+    if world == 1 and args.rpc:
+        line["rpc_headers"] = rpc_leg(nat.device)
     if world == 1 and args.host_inclusive and plan.is_fixed:
         try:
             line["host_inclusive"] = host_inclusive(mar, plan, nat, n, plan.fixed_size)

@@ -22,6 +22,11 @@
  *   xdrg_serial_sizes     <- xdr_argpack_size / xdr_size     xdrpp/marshal.h:223-234,
  *                                                            xdrpp/types.h:240-244
  *   xdrg_swap32/xdrg_swap64 <- swap32 / swap64               xdrpp/endian.h:56-68
+ *   xdrg_rpc_dispatch     <- rpc_server_base::dispatch header decode + routing
+ *                            xdrpp/server.cc:78-117, srpc.h:121-128
+ *   xdrg_rpc_check_replies <- check_call_hdr + xid test      xdrpp/rpc_msg.cc:115-131,
+ *                                                            xdrpp/srpc.h:61-66
+ *   xdrg_rpc_replies      <- rpc_*_msg error replies         xdrpp/server.cc:8-67
  *   xdrg_error_message    <- the what() strings of the exception types
  *                            xdrpp/types.h:57-99, marshal.h:104-108,152-170,
  *                            :131-136,:207-210, marshal.cc:43-57
@@ -52,7 +57,7 @@
 extern "C" {
 #endif
 
-#define XDRG_ABI_VERSION 2
+#define XDRG_ABI_VERSION 3
 
 /* ---------------------------------------------------------------------- */
 /* Plan ops: a flat, wire-ordered walk of xdr_traits<T>::save.             */
@@ -342,6 +347,127 @@ int xdrg_index_msgs(const void *d_stream, uint64_t len, uint32_t max_msg_len,
                     void *d_workspace, size_t workspace_bytes, xdrg_status *d_status,
                     void *stream);
 size_t xdrg_index_workspace_size(uint64_t len, uint32_t max_msg_len);
+
+/* ---------------------------------------------------------------------- */
+/* RPC header batches (RFC 5531 rpc_msg, xdrpp/rpc_msg.x)                  */
+/* ---------------------------------------------------------------------- */
+/*
+ * A batch of record-marked messages (indexed by xdrg_index_msgs: message k
+ * = [d_offsets[k], d_offsets[k+1]), mark first) has its rpc_msg headers
+ * decoded, one lane per message, into xdrg_rpc_hdr records:
+ *
+ *   xdrg_rpc_dispatch      <- rpc_server_base::dispatch, header decode and
+ *                             routing (xdrpp/server.cc:78-117) plus the
+ *                             procedure lookup of srpc_service::process /
+ *                             arpc_service::process (srpc.h:121-128,
+ *                             arpc.h:175-182)
+ *   xdrg_rpc_check_replies <- the client side: archive(g, hdr),
+ *                             check_call_hdr (rpc_msg.cc:115-131) and the
+ *                             xid test of synchronous_client_base::invoke
+ *                             (srpc.h:61-66)
+ *   xdrg_rpc_replies       <- rpc_accepted_error_msg, rpc_prog_mismatch_msg,
+ *                             rpc_auth_error_msg, rpc_rpc_mismatch_msg
+ *                             (server.cc:8-67): the error replies of a batch
+ *                             as record-marked messages
+ *
+ * Success replies are xdr_to_msg(rpc_success_hdr(xid), res) (srpc.h:152,
+ * server.h:27-49), i.e. an argument pack: encode them with xdrg_encode_msgs
+ * and a plan whose record is {xid, REPLY, MSG_ACCEPTED, AUTH_NONE, 0,
+ * SUCCESS, res...} (the Python/C++ layers build it).
+ *
+ * The header is decoded exactly as xdr_get decodes rpc_msg: a short message
+ * is xdr_overflow, an opaque_auth body over 400 bytes is the xvector bound,
+ * nonzero padding is xdr_should_be_zero, an unknown msg_type / reply_stat /
+ * reject_stat is a bad discriminant (accept_stat has a default arm).  Enum
+ * fields are not range-checked (no xdr_validate_enum in rpc_msg.x).  A
+ * header that fails is not an error of the call: its record carries the
+ * XDRG_ERR_* code in `err` and the action says what the reference does
+ * with it (drop it, or raise in the client).
+ */
+enum xdrg_rpc_action {          /* server side (xdrg_rpc_dispatch)             */
+  XDRG_RPC_DISPATCH = 0,        /* registered procedure: args at body_off     */
+  XDRG_RPC_DROP_MALFORMED = 1,  /* header did not decode: dropped, no reply   server.cc:84-89 */
+  XDRG_RPC_DROP_NONCALL = 2,    /* mtype != CALL: dropped, no reply           server.cc:90-93 */
+  XDRG_RPC_RPC_MISMATCH = 3,    /* rpcvers != 2 -> rpc_rpc_mismatch_msg       server.cc:95-96 */
+  XDRG_RPC_PROG_UNAVAIL = 4,    /* unknown prog                               server.cc:98-100 */
+  XDRG_RPC_PROG_MISMATCH = 5,   /* unknown vers: low/high = registered range  server.cc:102-107 */
+  XDRG_RPC_PROC_UNAVAIL = 6,    /* call_dispatch found no such proc           srpc.h:125-127 */
+  XDRG_RPC_GARBAGE_ARGS = 7,    /* set by the caller when the args fail       srpc.h:132-134, server.cc:109-116 */
+  XDRG_RPC_SYSTEM_ERR = 8,      /* set by the caller (accept_stat SYSTEM_ERR) */
+  XDRG_RPC_AUTH_ERROR = 9       /* set by the caller: why in w[2]             server.cc:42-53 */
+};
+enum xdrg_rpc_status {          /* client side (xdrg_rpc_check_replies)        */
+  XDRG_RPCR_OK = 0,             /* MSG_ACCEPTED + SUCCESS: result at body_off  */
+  XDRG_RPCR_ACCEPT_STAT = 1,    /* xdr_call_error(accept_stat w[1])   rpc_msg.cc:120-122 */
+  XDRG_RPCR_AUTH_STAT = 2,      /* xdr_call_error(auth_stat w[2])     rpc_msg.cc:124-125 */
+  XDRG_RPCR_RPCVERS_MISMATCH = 3,/* xdr_call_error(RPCVERS_MISMATCH)  rpc_msg.cc:126 */
+  XDRG_RPCR_NOT_REPLY = 4,      /* "call received when reply expected" rpc_msg.cc:117-118 */
+  XDRG_RPCR_MALFORMED = 5,      /* archive(g, hdr) threw: code in err           srpc.h:62 */
+  XDRG_RPCR_BAD_XID = 6         /* "synchronous_client: unexpected xid"         srpc.h:64-65 */
+};
+/* w[] slots of xdrg_rpc_hdr */
+#define XDRG_RPC_W_RPCVERS 0     /* CALL  */
+#define XDRG_RPC_W_PROG 1
+#define XDRG_RPC_W_VERS 2
+#define XDRG_RPC_W_PROC 3
+#define XDRG_RPC_W_CRED_FLAVOR 4
+#define XDRG_RPC_W_REPLY_STAT 0  /* REPLY */
+#define XDRG_RPC_W_STAT 1        /*   accept_stat (MSG_ACCEPTED) or reject_stat (MSG_DENIED) */
+#define XDRG_RPC_W_WHY 2         /*   auth_stat (AUTH_ERROR) */
+#define XDRG_RPC_W_VERF_FLAVOR 5 /* both */
+#define XDRG_RPC_W_LOW 6         /* PROG_MISMATCH / RPC_MISMATCH mismatch_info */
+#define XDRG_RPC_W_HIGH 7
+
+typedef struct xdrg_rpc_hdr {   /* 64 bytes */
+  uint32_t xid;
+  uint16_t action;   /* xdrg_rpc_action or xdrg_rpc_status */
+  uint8_t err;       /* XDRG_ERR_* of a malformed header, else 0.  A malformed
+                        header keeps only action, err, end and, for
+                        XDRG_ERR_BAD_DISCRIMINANT, the union in w[0]
+                        (0 _body_t, 1 reply_body, 2 rejected_reply) */
+  uint8_t mtype;     /* msg_type as decoded */
+  uint32_t w[8];     /* XDRG_RPC_W_* */
+  uint32_t cred_len; /* CALL: cred body bytes (body at mark + 36) */
+  uint32_t verf_len; /* verf body bytes (CALL: body ends at body_off; REPLY: at mark + 24) */
+  uint64_t body_off; /* stream offset after the header: args (CALL) / results (REPLY) */
+  uint64_t end;      /* stream offset of the message end */
+} xdrg_rpc_hdr;
+
+/* A registered procedure (prog, vers, proc).  The table passed to
+ * xdrg_rpc_dispatch lists every procedure of every registered interface,
+ * sorted by (prog, vers, proc), no duplicates: the servers_ map of
+ * rpc_server_base (server.h:218-219) plus each interface's call_dispatch
+ * switch (xdrc/gen_hh.cc:757-774). */
+typedef struct xdrg_rpc_proc {
+  uint32_t prog, vers, proc;
+  uint32_t flags; /* 0, or XDRG_RPC_PROC_IFACE_ONLY: (prog, vers) is registered
+                     but this entry names no procedure (an interface whose
+                     call_dispatch has no case) */
+} xdrg_rpc_proc;
+#define XDRG_RPC_PROC_IFACE_ONLY 1u
+#define XDRG_RPC_MAX_PROCS 4096u
+
+int xdrg_rpc_dispatch(const void *d_stream, uint64_t len, const uint64_t *d_offsets,
+                      uint64_t n, const xdrg_rpc_proc *d_procs, uint32_t nprocs,
+                      xdrg_rpc_hdr *d_hdrs, void *stream);
+
+/* d_xids: the xid each reply must carry (NULL: no xid test). */
+int xdrg_rpc_check_replies(const void *d_stream, uint64_t len, const uint64_t *d_offsets,
+                           uint64_t n, const uint32_t *d_xids, xdrg_rpc_hdr *d_hdrs,
+                           void *stream);
+
+/* Error replies of a dispatched batch, in message order: for every header
+ * whose action is RPC_MISMATCH / PROG_UNAVAIL / PROG_MISMATCH /
+ * PROC_UNAVAIL / GARBAGE_ARGS / SYSTEM_ERR / AUTH_ERROR one record-marked
+ * message (28, 36 or 24 bytes with its mark); other actions add nothing.
+ * d_offsets[i] = offset of header i's reply (== d_offsets[i+1] when it has
+ * none), d_offsets[n] = total, also in d_status->total_bytes.  An output
+ * capacity below the total is XDRG_ERR_OVERFLOW_PUT at the first reply that
+ * does not fit.  Workspace: xdrg_rpc_replies_workspace_size(n) bytes. */
+int xdrg_rpc_replies(const xdrg_rpc_hdr *d_hdrs, uint64_t n, void *d_out, uint64_t out_capacity,
+                     uint64_t *d_offsets, void *d_workspace, size_t workspace_bytes,
+                     xdrg_status *d_status, void *stream);
+size_t xdrg_rpc_replies_workspace_size(uint64_t n);
 
 /* Size pass alone: d_sizes[i] = xdr_size(record i) (uint32). */
 int xdrg_serial_sizes(const xdrg_plan *plan, const void *d_native, uint64_t n,

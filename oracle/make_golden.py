@@ -41,7 +41,54 @@ def sha(path: str) -> str:
     return h.hexdigest()
 
 
+RPC_SMALL = 1024
+RPC_FULL = 1 << 20
+
+
+def rpc_fixtures(manifest: dict) -> None:
+    """RPC header batches: the dispatch stream comes from
+    xdrpp_amd.workloads.rpc_calls (inputs), the expected headers, client
+    statuses and error replies from the reference (ref_golden rpc)."""
+    import numpy as np
+    sys.path.insert(0, ROOT)
+    from xdrpp_amd import workloads as W
+    procs = os.path.join(GOLD, "rpc_procs.bin")
+    W.RPC_PROCS.astype("<u4").tofile(procs)
+    stream, offs = W.rpc_calls(RPC_SMALL)
+    pre = os.path.join(GOLD, f"rpccall_{RPC_SMALL}")
+    stream.tofile(pre + ".stream")
+    offs.astype("<u8").tofile(pre + ".msgoffs")
+    subprocess.check_call([BIN, "rpc", pre + ".stream", pre + ".msgoffs", procs, "-", pre])
+    # client side over the config-4 messages: expected xid = the message's
+    # own xid, every 7th one flipped
+    msgs = np.fromfile(os.path.join(GOLD, f"rpc_{SMALL['rpc']}.msgs"), dtype=np.uint8)
+    moff = np.fromfile(os.path.join(GOLD, f"rpc_{SMALL['rpc']}.msgoffs"), dtype="<u8")
+    xids = msgs.view(">u4")[(moff[:-1] // 4 + 1).astype(np.int64)].astype("<u4")
+    xids[::7] ^= 1
+    cpre = os.path.join(GOLD, f"rpc_{SMALL['rpc']}")
+    xids.tofile(cpre + ".xids")
+    with tempfile.TemporaryDirectory() as td:
+        subprocess.check_call([BIN, "rpc", cpre + ".msgs", cpre + ".msgoffs", procs,
+                               cpre + ".xids", os.path.join(td, "c")])
+        shutil.copy(os.path.join(td, "c.chk"), cpre + ".chk")
+        stream, offs = W.rpc_calls(RPC_FULL)
+        fp = os.path.join(td, "full")
+        stream.tofile(fp + ".stream")
+        offs.astype("<u8").tofile(fp + ".msgoffs")
+        subprocess.check_call([BIN, "rpc", fp + ".stream", fp + ".msgoffs", procs, "-", fp])
+        manifest["hashes"][f"rpccall_{RPC_FULL}"] = {
+            "n": RPC_FULL, **{e: sha(fp + "." + e) for e in ("stream", "hdrs", "chk", "replies")},
+            "stream_bytes": os.path.getsize(fp + ".stream")}
+
+
 def main() -> int:
+    if "--only-rpc" in sys.argv:
+        mp = os.path.join(GOLD, "manifest.json")
+        manifest = json.load(open(mp))
+        rpc_fixtures(manifest)
+        with open(mp, "w") as f:
+            json.dump(manifest, f, indent=1, sort_keys=True)
+        return 0
     if not os.path.exists(BIN):
         print("build oracle/_ref/ref_golden first (make -C oracle)", file=sys.stderr)
         return 2
@@ -66,6 +113,7 @@ def main() -> int:
                     "xdr_bytes": os.path.getsize(pre + ".xdr")}
                 for e in exts:
                     os.remove(pre + "." + e)
+    rpc_fixtures(manifest)
     with open(os.path.join(GOLD, "manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1, sort_keys=True)
     print("wrote", GOLD)

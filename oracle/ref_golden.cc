@@ -317,12 +317,231 @@ static void bench_one(const char *name, const vector<T> &v, int threads, int rep
          2 * gib / (te[0] + td[0]));
 }
 
+// ------------------------------------------------------------ RPC headers
+// ref_golden rpc <stream> <offsets> <procs> <xids|-> <outprefix>
+//
+// Every message [off[k], off[k+1]) of the stream goes through the REAL
+// reference decode of its rpc_msg header (xdr_get over the message body,
+// archive(g, hdr): xdrpp/marshal.h:142-211 with the rpc_msg traits of
+// ref_schemas.hh), then
+//  * the server's routing, restated line for line from
+//    rpc_server_base::dispatch (xdrpp/server.cc:84-107) over a servers_-shaped
+//    map (server.h:218-219), plus call_dispatch's case test (srpc.h:125-127);
+//  * the client's check_call_hdr (rpc_msg.cc:115-131) + xid test (srpc.h:61-66);
+//  * the error replies, built exactly as server.cc:8-67 builds them (real
+//    message_t::alloc + xdr_put).
+// Writes <outprefix>.hdrs / .chk (xdrg_rpc_hdr per message, server / client
+// classification) and .replies / .replyoffs.
+#include <map>
+#include <set>
+
+static vector<uint8_t> slurp(const string &path) {
+  FILE *f = fopen(path.c_str(), "rb");
+  if (!f) die("cannot open " + path);
+  vector<uint8_t> b;
+  uint8_t buf[1 << 16];
+  size_t k;
+  while ((k = fread(buf, 1, sizeof buf, f)) > 0) b.insert(b.end(), buf, buf + k);
+  fclose(f);
+  return b;
+}
+
+namespace rpcref {
+using namespace rpcx;
+// server.cc:8-22
+static xdr::msg_ptr accepted_error_msg(uint32_t xid, int32_t stat) {
+  xdr::msg_ptr buf(xdr::message_t::alloc(24));
+  xdr::xdr_put p(buf);
+  p(xid); p(int32_t(REPLY)); p(int32_t(MSG_ACCEPTED)); p(int32_t(AUTH_NONE)); p(uint32_t(0)); p(stat);
+  if (p.p_ != p.e_) die("accepted_error_msg size");
+  return buf;
+}
+// server.cc:24-39
+static xdr::msg_ptr prog_mismatch_msg(uint32_t xid, uint32_t low, uint32_t high) {
+  xdr::msg_ptr buf(xdr::message_t::alloc(32));
+  xdr::xdr_put p(buf);
+  p(xid); p(int32_t(REPLY)); p(int32_t(MSG_ACCEPTED)); p(int32_t(AUTH_NONE)); p(uint32_t(0));
+  p(int32_t(PROG_MISMATCH)); p(low); p(high);
+  if (p.p_ != p.e_) die("prog_mismatch_msg size");
+  return buf;
+}
+// server.cc:41-53
+static xdr::msg_ptr auth_error_msg(uint32_t xid, int32_t stat) {
+  xdr::msg_ptr buf(xdr::message_t::alloc(20));
+  xdr::xdr_put p(buf);
+  p(xid); p(int32_t(REPLY)); p(int32_t(MSG_DENIED)); p(int32_t(AUTH_ERROR)); p(stat);
+  if (p.p_ != p.e_) die("auth_error_msg size");
+  return buf;
+}
+// server.cc:55-68
+static xdr::msg_ptr rpc_mismatch_msg(uint32_t xid) {
+  xdr::msg_ptr buf(xdr::message_t::alloc(24));
+  xdr::xdr_put p(buf);
+  p(xid); p(int32_t(REPLY)); p(int32_t(MSG_DENIED)); p(int32_t(RPC_MISMATCH)); p(uint32_t(2));
+  p(uint32_t(2));
+  if (p.p_ != p.e_) die("rpc_mismatch_msg size");
+  return buf;
+}
+
+static uint8_t err_code(const std::exception &e, const string &w, uint32_t *site) {
+  *site = 0;
+  if (dynamic_cast<const xdr::xdr_bad_discriminant *>(&e)) {
+    if (w.find("reply_body") != string::npos) *site = 1;
+    else if (w.find("rejected_reply") != string::npos) *site = 2;
+    return XDRG_ERR_BAD_DISCRIMINANT;
+  }
+  if (dynamic_cast<const xdr::xdr_should_be_zero *>(&e)) return XDRG_ERR_NONZERO_PAD;
+  if (w == "xvector overflow") return XDRG_ERR_XVECTOR_BOUND;
+  if (dynamic_cast<const xdr::xdr_overflow *>(&e)) return XDRG_ERR_OVERFLOW_GET;
+  if (dynamic_cast<const xdr::xdr_bad_message_size *>(&e)) return XDRG_ERR_SIZE_NOT_MULT4;
+  die("unexpected exception " + w);
+  return 0;
+}
+}  // namespace rpcref
+
+static void rpc_mode(const string &sp, const string &op, const string &pp, const string &xp,
+                     const string &pre) {
+  using namespace rpcx;
+  vector<uint8_t> sb = slurp(sp), ob = slurp(op), pb = slurp(pp), xb;
+  if (xp != "-") xb = slurp(xp);
+  // 4-byte aligned copy of the stream (xdr_get asserts an aligned start)
+  vector<uint32_t> words((sb.size() + 3) / 4);
+  memcpy(words.data(), sb.data(), sb.size());
+  const uint8_t *s = reinterpret_cast<const uint8_t *>(words.data());
+  const uint64_t *off = reinterpret_cast<const uint64_t *>(ob.data());
+  const size_t n = ob.size() / 8 - 1;
+  const xdrg_rpc_proc *pt = reinterpret_cast<const xdrg_rpc_proc *>(pb.data());
+  const size_t np = pb.size() / sizeof(xdrg_rpc_proc);
+  // servers_: prog -> vers -> the service's procedure set (call_dispatch cases)
+  std::map<uint32_t, std::map<uint32_t, std::set<uint32_t>>> servers;
+  for (size_t i = 0; i < np; ++i) {
+    auto &procs = servers[pt[i].prog][pt[i].vers];
+    if (!(pt[i].flags & XDRG_RPC_PROC_IFACE_ONLY)) procs.insert(pt[i].proc);
+  }
+  vector<xdrg_rpc_hdr> hs(n), cs(n);
+  vector<uint8_t> rep;
+  vector<uint64_t> roff(n + 1, 0);
+  for (size_t k = 0; k < n; ++k) {
+    const uint64_t m0 = off[k], m1 = off[k + 1];
+    xdrg_rpc_hdr h;
+    memset(&h, 0, sizeof h);
+    h.end = m1;
+    rpc_msg hdr{};
+    uint8_t err = 0;
+    uint32_t site = 0;
+    try {
+      xdr::xdr_get g(s + m0 + 4, s + m1);
+      archive(g, hdr);
+      h.body_off = reinterpret_cast<const uint8_t *>(g.p_) - s;
+    } catch (const std::exception &e) {
+      err = rpcref::err_code(e, e.what(), &site);
+    }
+    if (!err) {
+      h.xid = hdr.xid;
+      h.mtype = uint8_t(hdr.body.mtype);
+      if (hdr.body.mtype == CALL) {
+        const call_body &cb = hdr.body.cbody;
+        h.w[XDRG_RPC_W_RPCVERS] = cb.rpcvers; h.w[XDRG_RPC_W_PROG] = cb.prog;
+        h.w[XDRG_RPC_W_VERS] = cb.vers; h.w[XDRG_RPC_W_PROC] = cb.proc;
+        h.w[XDRG_RPC_W_CRED_FLAVOR] = uint32_t(cb.cred.flavor);
+        h.w[XDRG_RPC_W_VERF_FLAVOR] = uint32_t(cb.verf.flavor);
+        h.cred_len = uint32_t(cb.cred.body.size());
+        h.verf_len = uint32_t(cb.verf.body.size());
+      } else {
+        const reply_body &rb = hdr.body.rbody;
+        h.w[XDRG_RPC_W_REPLY_STAT] = uint32_t(rb.stat);
+        if (rb.stat == MSG_ACCEPTED) {
+          h.w[XDRG_RPC_W_VERF_FLAVOR] = uint32_t(rb.areply.verf.flavor);
+          h.verf_len = uint32_t(rb.areply.verf.body.size());
+          h.w[XDRG_RPC_W_STAT] = uint32_t(rb.areply.reply_data.stat);
+          if (rb.areply.reply_data.stat == PROG_MISMATCH) {
+            h.w[XDRG_RPC_W_LOW] = rb.areply.reply_data.mismatch_info_.low;
+            h.w[XDRG_RPC_W_HIGH] = rb.areply.reply_data.mismatch_info_.high;
+          }
+        } else {
+          h.w[XDRG_RPC_W_STAT] = uint32_t(rb.rreply.stat);
+          if (rb.rreply.stat == RPC_MISMATCH) {
+            h.w[XDRG_RPC_W_LOW] = rb.rreply.mismatch_info_.low;
+            h.w[XDRG_RPC_W_HIGH] = rb.rreply.mismatch_info_.high;
+          } else {
+            h.w[XDRG_RPC_W_WHY] = uint32_t(rb.rreply.rj_why);
+          }
+        }
+      }
+    } else {
+      h.err = err;
+      h.w[0] = site;
+    }
+    // ---- server: rpc_server_base::dispatch (server.cc:84-107)
+    xdrg_rpc_hdr sv = h;
+    xdr::msg_ptr reply;
+    if (err) sv.action = XDRG_RPC_DROP_MALFORMED;
+    else if (hdr.body.mtype != CALL) sv.action = XDRG_RPC_DROP_NONCALL;
+    else if (hdr.body.cbody.rpcvers != 2) {
+      sv.action = XDRG_RPC_RPC_MISMATCH;
+      reply = rpcref::rpc_mismatch_msg(hdr.xid);
+    } else {
+      auto prog = servers.find(hdr.body.cbody.prog);
+      if (prog == servers.end()) {
+        sv.action = XDRG_RPC_PROG_UNAVAIL;
+        reply = rpcref::accepted_error_msg(hdr.xid, PROG_UNAVAIL);
+      } else {
+        auto vers = prog->second.find(hdr.body.cbody.vers);
+        if (vers == prog->second.end()) {
+          uint32_t low = prog->second.cbegin()->first;
+          uint32_t high = prog->second.crbegin()->first;
+          sv.action = XDRG_RPC_PROG_MISMATCH;
+          sv.w[XDRG_RPC_W_LOW] = low;
+          sv.w[XDRG_RPC_W_HIGH] = high;
+          reply = rpcref::prog_mismatch_msg(hdr.xid, low, high);
+        } else if (!vers->second.count(hdr.body.cbody.proc)) {  // call_dispatch false
+          sv.action = XDRG_RPC_PROC_UNAVAIL;
+          reply = rpcref::accepted_error_msg(hdr.xid, 3 /* PROC_UNAVAIL */);
+        } else {
+          sv.action = XDRG_RPC_DISPATCH;
+        }
+      }
+    }
+    hs[k] = sv;
+    if (reply)
+      rep.insert(rep.end(), reinterpret_cast<const uint8_t *>(reply->raw_data()),
+                 reinterpret_cast<const uint8_t *>(reply->raw_data()) + reply->raw_size());
+    roff[k + 1] = rep.size();
+    // ---- client: archive(g, hdr); check_call_hdr(hdr); xid (srpc.h:61-66)
+    xdrg_rpc_hdr cl = h;
+    if (err) cl.action = XDRG_RPCR_MALFORMED;
+    else if (hdr.body.mtype != REPLY) cl.action = XDRG_RPCR_NOT_REPLY;
+    else if (hdr.body.rbody.stat == MSG_ACCEPTED)
+      cl.action = hdr.body.rbody.areply.reply_data.stat == SUCCESS ? XDRG_RPCR_OK
+                                                                  : XDRG_RPCR_ACCEPT_STAT;
+    else
+      cl.action = hdr.body.rbody.rreply.stat == AUTH_ERROR ? XDRG_RPCR_AUTH_STAT
+                                                            : XDRG_RPCR_RPCVERS_MISMATCH;
+    if (cl.action == XDRG_RPCR_OK && !xb.empty() &&
+        reinterpret_cast<const uint32_t *>(xb.data())[k] != hdr.xid)
+      cl.action = XDRG_RPCR_BAD_XID;
+    cs[k] = cl;
+  }
+  write_file(pre + ".hdrs", hs.data(), hs.size() * sizeof(xdrg_rpc_hdr));
+  write_file(pre + ".chk", cs.data(), cs.size() * sizeof(xdrg_rpc_hdr));
+  write_file(pre + ".replies", rep.data(), rep.size());
+  write_file(pre + ".replyoffs", roff.data(), roff.size() * 8);
+  // the auth-error reply has no dispatch route; one known answer of it
+  xdr::msg_ptr ae = rpcref::auth_error_msg(0x01020304u, 5);
+  write_file(pre + ".autherr", ae->raw_data(), ae->raw_size());
+}
+
 int main(int argc, char **argv) {
   if (argc < 2) die("usage: gen|kat|bench ...");
   string mode = argv[1];
   if (mode == "kat") {
     if (argc != 3) die("kat <out.json>");
     kat(argv[2]);
+    return 0;
+  }
+  if (mode == "rpc") {
+    if (argc != 7) die("rpc <stream> <offsets> <procs> <xids|-> <outprefix>");
+    rpc_mode(argv[2], argv[3], argv[4], argv[5], argv[6]);
     return 0;
   }
   if (argc < 4) die("missing args");

@@ -522,3 +522,165 @@ int xdro_index_msgs(const uint8_t *s, uint64_t len, uint32_t maxlen, uint64_t ma
     ++k;
   }
 }
+
+/* ------------------------------------------------------------ RPC headers
+ * rpc_msg header decode (xdrpp/rpc_msg.x through xdr_get: check(4) per
+ * word, opaque body<400>: length, check(size), bound, pad check —
+ * marshal.h:163-196, marshal.cc:43-57), then
+ *   server: rpc_server_base::dispatch (xdrpp/server.cc:84-107) and the
+ *           call_dispatch switch of the service (srpc.h:121-128);
+ *   client: check_call_hdr (rpc_msg.cc:115-131) + xid test (srpc.h:61-66).
+ * A malformed header keeps only action, err, end and, for a bad
+ * discriminant, the union in w[0] (0 _body_t, 1 reply_body, 2
+ * rejected_reply); other fields are zero. */
+typedef struct { const uint8_t *s; uint64_t p, e; } rcur;
+
+static int rword(rcur *c, uint32_t *v) {
+  if (c->e - c->p < 4) return 0;
+  *v = bswap32(rd32(c->s + c->p));
+  c->p += 4;
+  return 1;
+}
+
+static uint32_t rauth(rcur *c, uint32_t *len) {
+  if (!rword(c, len)) return XDRG_ERR_OVERFLOW_GET;
+  if (*len > c->e - c->p) return XDRG_ERR_OVERFLOW_GET;
+  if (*len > 400) return XDRG_ERR_XVECTOR_BOUND;
+  for (uint64_t j = *len; j & 3; ++j)
+    if (c->s[c->p + j]) return XDRG_ERR_NONZERO_PAD;
+  c->p += pad4(*len);
+  return 0;
+}
+
+static uint32_t rwalk(rcur *c, xdrg_rpc_hdr *h) {
+  uint32_t v, e;
+  if (!rword(c, &h->xid) || !rword(c, &v)) return XDRG_ERR_OVERFLOW_GET;
+  h->mtype = (uint8_t)v;
+  if (v == 0) { /* CALL: call_body */
+    for (int k = 0; k < 5; ++k)
+      if (!rword(c, &h->w[k])) return XDRG_ERR_OVERFLOW_GET;
+    if ((e = rauth(c, &h->cred_len))) return e;
+    if (!rword(c, &h->w[XDRG_RPC_W_VERF_FLAVOR])) return XDRG_ERR_OVERFLOW_GET;
+    return rauth(c, &h->verf_len);
+  }
+  if (v != 1) return XDRG_ERR_BAD_DISCRIMINANT;
+  if (!rword(c, &h->w[XDRG_RPC_W_REPLY_STAT])) return XDRG_ERR_OVERFLOW_GET;
+  if (h->w[XDRG_RPC_W_REPLY_STAT] == 0) { /* MSG_ACCEPTED: accepted_reply */
+    if (!rword(c, &h->w[XDRG_RPC_W_VERF_FLAVOR])) return XDRG_ERR_OVERFLOW_GET;
+    if ((e = rauth(c, &h->verf_len))) return e;
+    if (!rword(c, &h->w[XDRG_RPC_W_STAT])) return XDRG_ERR_OVERFLOW_GET;
+    if (h->w[XDRG_RPC_W_STAT] == 2 &&
+        (!rword(c, &h->w[XDRG_RPC_W_LOW]) || !rword(c, &h->w[XDRG_RPC_W_HIGH])))
+      return XDRG_ERR_OVERFLOW_GET;
+    return 0;
+  }
+  if (h->w[XDRG_RPC_W_REPLY_STAT] != 1) return XDRG_ERR_BAD_DISCRIMINANT | (1u << 8);
+  if (!rword(c, &h->w[XDRG_RPC_W_STAT])) return XDRG_ERR_OVERFLOW_GET;
+  if (h->w[XDRG_RPC_W_STAT] == 0)
+    return rword(c, &h->w[XDRG_RPC_W_LOW]) && rword(c, &h->w[XDRG_RPC_W_HIGH])
+               ? 0 : XDRG_ERR_OVERFLOW_GET;
+  if (h->w[XDRG_RPC_W_STAT] != 1) return XDRG_ERR_BAD_DISCRIMINANT | (2u << 8);
+  return rword(c, &h->w[XDRG_RPC_W_WHY]) ? 0 : XDRG_ERR_OVERFLOW_GET;
+}
+
+static uint32_t rroute(const xdrg_rpc_proc *t, uint32_t nt, xdrg_rpc_hdr *h) {
+  const uint32_t P = h->w[XDRG_RPC_W_PROG], V = h->w[XDRG_RPC_W_VERS], Q = h->w[XDRG_RPC_W_PROC];
+  int64_t first = -1, last = -1, vhit = 0;
+  for (uint32_t i = 0; i < nt; ++i) {
+    if (t[i].prog != P) continue;
+    if (first < 0) first = i;
+    last = i;
+    if (t[i].vers == V) {
+      vhit = 1;
+      if (t[i].proc == Q && !(t[i].flags & XDRG_RPC_PROC_IFACE_ONLY)) return XDRG_RPC_DISPATCH;
+    }
+  }
+  if (first < 0) return XDRG_RPC_PROG_UNAVAIL;
+  if (!vhit) {
+    h->w[XDRG_RPC_W_LOW] = t[first].vers;
+    h->w[XDRG_RPC_W_HIGH] = t[last].vers;
+    return XDRG_RPC_PROG_MISMATCH;
+  }
+  return XDRG_RPC_PROC_UNAVAIL;
+}
+
+int xdro_rpc_headers(const uint8_t *s, uint64_t len, const uint64_t *offs, uint64_t n,
+                     const xdrg_rpc_proc *procs, uint32_t nprocs, const uint32_t *xids,
+                     int client, xdrg_rpc_hdr *out) {
+  for (uint64_t i = 0; i < n; ++i) {
+    xdrg_rpc_hdr h;
+    memset(&h, 0, sizeof h);
+    const uint64_t m0 = offs[i], m1 = offs[i + 1];
+    uint32_t err;
+    if (m1 > len || m1 < m0 + 4 || (m0 & 3)) err = XDRG_ERR_MSG_MISMATCH;
+    else if ((m1 - m0) & 3) err = XDRG_ERR_SIZE_NOT_MULT4;
+    else {
+      rcur c = {s, m0 + 4, m1};
+      err = rwalk(&c, &h);
+      h.body_off = c.p;
+    }
+    if (err) {
+      memset(&h, 0, sizeof h);
+      h.w[0] = err >> 8; /* bad discriminant: 0 _body_t, 1 reply_body, 2 rejected_reply */
+      err &= 0xff;
+    }
+    h.err = (uint8_t)err;
+    h.end = m1;
+    if (!client) {
+      if (err) h.action = XDRG_RPC_DROP_MALFORMED;
+      else if (h.mtype != 0) h.action = XDRG_RPC_DROP_NONCALL;
+      else if (h.w[XDRG_RPC_W_RPCVERS] != 2) h.action = XDRG_RPC_RPC_MISMATCH;
+      else h.action = (uint16_t)rroute(procs, nprocs, &h);
+    } else {
+      if (err) h.action = XDRG_RPCR_MALFORMED;
+      else if (h.mtype != 1) h.action = XDRG_RPCR_NOT_REPLY;
+      else if (h.w[XDRG_RPC_W_REPLY_STAT] == 0)
+        h.action = h.w[XDRG_RPC_W_STAT] == 0 ? XDRG_RPCR_OK : XDRG_RPCR_ACCEPT_STAT;
+      else
+        h.action = h.w[XDRG_RPC_W_STAT] == 1 ? XDRG_RPCR_AUTH_STAT : XDRG_RPCR_RPCVERS_MISMATCH;
+      if (h.action == XDRG_RPCR_OK && xids && xids[i] != h.xid) h.action = XDRG_RPCR_BAD_XID;
+    }
+    out[i] = h;
+  }
+  return 0;
+}
+
+/* Error replies (server.cc:8-67) as record-marked messages, message order.
+ * Returns 0, or XDRG_ERR_OVERFLOW_PUT with *erec = the first reply that
+ * does not fit in cap. */
+int xdro_rpc_replies(const xdrg_rpc_hdr *h, uint64_t n, uint8_t *out, uint64_t cap,
+                     uint64_t *offs, uint64_t *total, uint64_t *erec) {
+  uint64_t pos = 0;
+  int rc = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    uint32_t w[9], k = 0, a = h[i].action;
+    offs[i] = pos;
+    w[k++] = 0; /* mark, below */
+    w[k++] = h[i].xid;
+    w[k++] = 1; /* REPLY */
+    if (a == XDRG_RPC_RPC_MISMATCH) {
+      w[k++] = 1; w[k++] = 0; w[k++] = 2; w[k++] = 2;
+    } else if (a == XDRG_RPC_AUTH_ERROR) {
+      w[k++] = 1; w[k++] = 1; w[k++] = h[i].w[XDRG_RPC_W_WHY];
+    } else if (a == XDRG_RPC_PROG_UNAVAIL || a == XDRG_RPC_PROG_MISMATCH ||
+               a == XDRG_RPC_PROC_UNAVAIL || a == XDRG_RPC_GARBAGE_ARGS ||
+               a == XDRG_RPC_SYSTEM_ERR) {
+      w[k++] = 0; w[k++] = 0; w[k++] = 0;
+      w[k++] = a == XDRG_RPC_PROG_UNAVAIL ? 1 : a == XDRG_RPC_PROG_MISMATCH ? 2
+             : a == XDRG_RPC_PROC_UNAVAIL ? 3 : a == XDRG_RPC_GARBAGE_ARGS ? 4 : 5;
+      if (a == XDRG_RPC_PROG_MISMATCH) { w[k++] = h[i].w[XDRG_RPC_W_LOW]; w[k++] = h[i].w[XDRG_RPC_W_HIGH]; }
+    } else {
+      continue;
+    }
+    w[0] = (4 * (k - 1)) | XDRG_MARK_LAST;
+    if (pos + 4 * k > cap) {
+      if (!rc) { rc = XDRG_ERR_OVERFLOW_PUT; *erec = i; }
+    } else {
+      for (uint32_t j = 0; j < k; ++j) wr32(out + pos + 4 * j, bswap32(w[j]));
+    }
+    pos += 4 * k;
+  }
+  offs[n] = pos;
+  *total = pos;
+  return rc;
+}

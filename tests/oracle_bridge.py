@@ -147,3 +147,41 @@ def index_msgs(stream: np.ndarray, max_msg_len: int, max_msgs: int | None = None
     rc = lib().xdro_index_msgs(_p(x), stream.size, max_msg_len, max_msgs, _p(offs),
                                C.byref(cnt), C.byref(erec))
     return rc, int(cnt.value), offs[:cnt.value + 1]
+
+
+# ------------------------------------------------------------ RPC headers
+def _rpc_lib():
+    L = lib()
+    if not getattr(L, "_rpc_bound", False):
+        vp, u64, u32 = C.c_void_p, C.c_uint64, C.c_uint32
+        L.xdro_rpc_headers.argtypes = [vp, u64, vp, u64, vp, u32, vp, C.c_int, vp]
+        L.xdro_rpc_replies.argtypes = [vp, u64, vp, u64, vp, C.POINTER(u64), C.POINTER(u64)]
+        L._rpc_bound = True
+    return L
+
+
+def rpc_headers(stream: np.ndarray, offsets: np.ndarray, procs: np.ndarray | None,
+                client: bool = False, xids: np.ndarray | None = None) -> np.ndarray:
+    """xdrg_rpc_hdr records (numpy structured, xdrpp_amd.rpc.HDR_DTYPE)."""
+    from xdrpp_amd.rpc import HDR_DTYPE
+    n = offsets.size - 1
+    out = np.zeros(max(n, 1), dtype=HDR_DTYPE)
+    s = np.ascontiguousarray(stream, dtype=np.uint8)
+    o = np.ascontiguousarray(offsets, dtype=np.uint64)
+    p = None if procs is None else np.ascontiguousarray(procs, dtype=np.uint32)
+    x = None if xids is None else np.ascontiguousarray(xids, dtype=np.uint32)
+    _rpc_lib().xdro_rpc_headers(_p(s), s.size, _p(o), n, _p(p), 0 if p is None else p.size // 4,
+                                _p(x), int(client), _p(out))
+    return out[:n]
+
+
+def rpc_replies(hdrs: np.ndarray, cap: int | None = None):
+    """(reply stream, offsets[n+1], error code, failing record)."""
+    n = hdrs.size
+    cap = 36 * n if cap is None else cap
+    out = np.zeros(max(cap, 4), dtype=np.uint8)
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    tot, er = C.c_uint64(0), C.c_uint64(0)
+    h = np.ascontiguousarray(hdrs)
+    rc = _rpc_lib().xdro_rpc_replies(_p(h), n, _p(out), cap, _p(offs), C.byref(tot), C.byref(er))
+    return out[:min(tot.value, cap)], offs, rc, er.value

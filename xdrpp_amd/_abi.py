@@ -14,7 +14,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libxdrgpu.s
 
 # enum xdrg_op_kind
 OP_U32, OP_U64, OP_BOOL, OP_ENUM, OP_OPAQUE, OP_VAROPAQUE, OP_STRING, OP_UNION, OP_JUMP, OP_END, OP_VECTOR = range(1, 12)
-ABI_VERSION = 2  # XDRG_ABI_VERSION, include/xdrgpu.h
+ABI_VERSION = 3  # XDRG_ABI_VERSION, include/xdrgpu.h
 F_VALIDATE = 1
 F_DEFAULT = 2
 F_POINTER = 4
@@ -104,8 +104,21 @@ EXPORTED = (
     "xdrg_decode", "xdrg_serial_sizes", "xdrg_swap32", "xdrg_swap64",
     "xdrg_error_message", "xdrg_error_exception", "xdrg_last_hip_error",
     "xdrg_decode_heap_size", "xdrg_encode_msgs", "xdrg_decode_msgs", "xdrg_index_msgs",
-    "xdrg_index_workspace_size",
+    "xdrg_index_workspace_size", "xdrg_rpc_dispatch", "xdrg_rpc_check_replies",
+    "xdrg_rpc_replies", "xdrg_rpc_replies_workspace_size",
 )
+
+# RPC header batches (include/xdrgpu.h "RPC header batches")
+RPC_DISPATCH, RPC_DROP_MALFORMED, RPC_DROP_NONCALL, RPC_RPC_MISMATCH, RPC_PROG_UNAVAIL, \
+    RPC_PROG_MISMATCH, RPC_PROC_UNAVAIL, RPC_GARBAGE_ARGS, RPC_SYSTEM_ERR, RPC_AUTH_ERROR = range(10)
+RPCR_OK, RPCR_ACCEPT_STAT, RPCR_AUTH_STAT, RPCR_RPCVERS_MISMATCH, RPCR_NOT_REPLY, RPCR_MALFORMED, \
+    RPCR_BAD_XID = range(7)
+RPC_W_RPCVERS, RPC_W_PROG, RPC_W_VERS, RPC_W_PROC, RPC_W_CRED_FLAVOR = range(5)
+RPC_W_REPLY_STAT, RPC_W_STAT, RPC_W_WHY = range(3)
+RPC_W_VERF_FLAVOR, RPC_W_LOW, RPC_W_HIGH = 5, 6, 7
+RPC_PROC_IFACE_ONLY = 1
+RPC_MAX_PROCS = 4096
+RPC_HDR_BYTES = 64
 
 _lib = None
 
@@ -150,6 +163,14 @@ def lib() -> C.CDLL:
     L.xdrg_index_msgs.restype = C.c_int
     L.xdrg_index_workspace_size.argtypes = [u64, u32]
     L.xdrg_index_workspace_size.restype = sz
+    L.xdrg_rpc_dispatch.argtypes = [vp, u64, vp, u64, vp, u32, vp, vp]
+    L.xdrg_rpc_dispatch.restype = C.c_int
+    L.xdrg_rpc_check_replies.argtypes = [vp, u64, vp, u64, vp, vp, vp]
+    L.xdrg_rpc_check_replies.restype = C.c_int
+    L.xdrg_rpc_replies.argtypes = [vp, u64, vp, u64, vp, vp, sz, vp, vp]
+    L.xdrg_rpc_replies.restype = C.c_int
+    L.xdrg_rpc_replies_workspace_size.argtypes = [u64]
+    L.xdrg_rpc_replies_workspace_size.restype = sz
     L.xdrg_serial_sizes.argtypes = [vp, vp, u64, vp, u32, vp, vp]
     L.xdrg_serial_sizes.restype = C.c_int
     L.xdrg_swap32.argtypes = [vp, vp, u64, vp]

@@ -11,7 +11,8 @@ import sys
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
-SOURCES = [os.path.join(CSRC, "plan.cpp"), os.path.join(CSRC, "xdrgpu.hip")]
+SOURCES = [os.path.join(CSRC, "plan.cpp"), os.path.join(CSRC, "xdrgpu.hip"),
+           os.path.join(CSRC, "rpc.hip")]
 DEPS = SOURCES + [os.path.join(CSRC, "plan.h"), os.path.join(CSRC, "kernels.h"),
                   os.path.join(ROOT, "include", "xdrgpu.h")]
 OUT = os.path.join(PKG, "libxdrgpu.so")

@@ -98,6 +98,14 @@ struct xdrg_plan {
 };
 
 namespace xdrg {
+// Shared by the kernels' translation units (xdrgpu.hip, rpc.hip):
+// exclusive scan of nb u64 block sums in place, writing the total to
+// status->total_bytes and offsets[n] (one workgroup, stream-ordered), and
+// the thread's last-HIP-error record behind xdrg_last_hip_error.
+int launch_block_scan(unsigned long long *v, uint32_t nb, xdrg_status *status,
+                      uint64_t *offsets, uint64_t n, void *stream);
+int record_hip_error(int hip_error, const char *what);
+
 // Validates ops and builds all host-side programs.  Returns XDRG_OK or an
 // API error.  Does not touch the device.
 int compile_plan(xdrg_plan &p);

@@ -369,45 +369,63 @@ __global__ __launch_bounds__(64) void k_var_size(const uint8_t *__restrict__ nat
   if (block_sums && lane == 0) block_sums[blockIdx.x] = v;
 }
 
-// Exclusive scan of nb block sums in place; writes the total.  Tiles of
-// 16 x 1024 values: every thread loads its 16 contiguous values with
-// independent loads (one round trip per tile), scans them, and the block
-// scans the thread totals.
+// Exclusive scan of nb block sums in place; writes the total.  One
+// workgroup of 16 waves; tiles of 16 x 1024 values.  Loads and stores are
+// coalesced (value k of thread t is element t0 + 1024 k + t): each of the
+// 16 rows is scanned per wave with shuffles, wave 0 scans the 256 row/wave
+// totals in (row, wave) order, and every value adds its row/wave base.
+// (A thread-contiguous layout costs a cache line per lane per load: 18 us
+// for 16K values on MI355X, against a few us for this one.)
 __global__ __launch_bounds__(1024) void k_scan_blocks(unsigned long long *__restrict__ v,
                                                       uint32_t nb, xdrg_status *status,
                                                       uint64_t *__restrict__ offsets, uint64_t n) {
-  constexpr uint32_t PER = 16;
-  __shared__ unsigned long long wtot[16];
+  constexpr uint32_t PER = 16, NT = 1024, NW = NT / 64;
+  __shared__ unsigned long long part[PER * NW];  // (row k, wave w) totals -> bases
+  __shared__ unsigned long long tile_total;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   unsigned long long carry = 0;
-  for (uint64_t t0 = 0; t0 < nb; t0 += 1024ull * PER) {
-    unsigned long long x[PER];
-    const uint64_t b0 = t0 + static_cast<uint64_t>(tid) * PER;
-#pragma unroll
-    for (uint32_t k = 0; k < PER; ++k) x[k] = b0 + k < nb ? v[b0 + k] : 0ull;
-    unsigned long long tsum = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < PER; ++k) tsum += x[k];
-    unsigned long long incl = tsum;
-    for (int o = 1; o < 64; o <<= 1) {
-      const unsigned long long y = __shfl_up(incl, o, 64);
-      if (lane >= static_cast<uint32_t>(o)) incl += y;
-    }
-    if (lane == 63) wtot[wid] = incl;
-    __syncthreads();
-    unsigned long long wbase = 0, all = 0;
-    for (uint32_t w = 0; w < 16; ++w) {
-      if (w < wid) wbase += wtot[w];
-      all += wtot[w];
-    }
-    unsigned long long run = carry + wbase + incl - tsum;
+  for (uint64_t t0 = 0; t0 < nb; t0 += static_cast<uint64_t>(NT) * PER) {
+    unsigned long long x[PER], incl[PER];
 #pragma unroll
     for (uint32_t k = 0; k < PER; ++k) {
-      if (b0 + k < nb) v[b0 + k] = run;
-      run += x[k];
+      const uint64_t j = t0 + static_cast<uint64_t>(k) * NT + tid;
+      x[k] = j < nb ? v[j] : 0ull;
     }
-    carry += all;
-    __syncthreads();  // wtot reused by the next tile
+#pragma unroll
+    for (uint32_t k = 0; k < PER; ++k) {
+      unsigned long long a = x[k];
+      for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long y = __shfl_up(a, o, 64);
+        if (lane >= static_cast<uint32_t>(o)) a += y;
+      }
+      incl[k] = a;
+      if (lane == 63) part[k * NW + wid] = a;
+    }
+    __syncthreads();
+    if (wid == 0) {  // exclusive scan of the 256 (row, wave) totals, 4 per lane
+      unsigned long long p0 = part[4 * lane], p1 = part[4 * lane + 1], p2 = part[4 * lane + 2],
+                         p3 = part[4 * lane + 3];
+      const unsigned long long sum = p0 + p1 + p2 + p3;
+      unsigned long long a = sum;
+      for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long y = __shfl_up(a, o, 64);
+        if (lane >= static_cast<uint32_t>(o)) a += y;
+      }
+      unsigned long long b = carry + a - sum;
+      part[4 * lane] = b; b += p0;
+      part[4 * lane + 1] = b; b += p1;
+      part[4 * lane + 2] = b; b += p2;
+      part[4 * lane + 3] = b;
+      if (lane == 63) tile_total = a;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < PER; ++k) {
+      const uint64_t j = t0 + static_cast<uint64_t>(k) * NT + tid;
+      if (j < nb) v[j] = part[k * NW + wid] + incl[k] - x[k];
+    }
+    carry += tile_total;
+    __syncthreads();  // part / tile_total reused by the next tile
   }
   if (tid == 0) {
     status->total_bytes = carry;
@@ -1935,6 +1953,20 @@ unsigned long long *err_ptr(xdrg_status *st) {
 // Interpreter-path encode of n records: size pass, block scan, then the
 // record kernel.  mark = 4 puts each record in a message (its record mark
 // first, xdrg_encode_msgs); mark = 0 is xdrg_encode of a var plan.
+}  // namespace
+
+namespace xdrg {
+int launch_block_scan(unsigned long long *v, uint32_t nb, xdrg_status *status, uint64_t *offsets,
+                      uint64_t n, void *stream) {
+  k_scan_blocks<<<1, 1024, 0, static_cast<hipStream_t>(stream)>>>(v, nb, status, offsets, n);
+  HIPCHK(hipGetLastError());
+  return XDRG_OK;
+}
+int record_hip_error(int e, const char *what) { return hip_fail(static_cast<hipError_t>(e), what); }
+}  // namespace xdrg
+
+namespace {
+
 int var_encode(const xdrg_plan &P, const void *d_native, uint64_t n, const uint8_t *d_heap,
                uint64_t heap_len, void *d_xdr, uint64_t cap, uint64_t *d_offsets,
                uint32_t stack_limit, void *d_ws, size_t ws_bytes, xdrg_status *d_status,

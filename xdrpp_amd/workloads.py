@@ -257,3 +257,128 @@ def generate(schema: str, n: int, chunk: int = 1 << 16) -> tuple[np.ndarray, np.
     if schema in ("numerics", "rec128") or n <= chunk:
         return GENERATORS[schema](n)
     raise NotImplementedError("chunked generation of var schemas: use generate_var")
+
+
+# ------------------------------------------------------ RPC call batches
+SEED_RPCCALL = 0x5EED0007
+
+# Registered procedures (prog, vers, proc, flags) of the dispatch workload,
+# sorted: the servers_ map of rpc_server_base (xdrpp/server.h:218-219) with
+# each interface's call_dispatch cases (xdrc/gen_hh.cc:757-774).  Program
+# 100005 is an interface with no procedure (flag 1 = XDRG_RPC_PROC_IFACE_ONLY).
+RPC_PROCS = np.array(
+    [(100000, 2, p, 0) for p in (0, 1, 2, 3, 5, 8)]
+    + [(100000, 3, p, 0) for p in range(10)]
+    + [(100003, 3, p, 0) for p in range(22)]
+    + [(100003, 4, p, 0) for p in range(22)]
+    + [(100005, 1, 0, 1)]
+    + [(0x20000001, 1, 0, 0)],
+    dtype=np.uint32)
+
+
+def _be(v: np.ndarray) -> np.ndarray:
+    """uint32 values -> their XDR (big-endian) words as little-endian uint32."""
+    return v.astype(np.uint32).byteswap()
+
+
+def rpc_calls(n: int, seed: int = SEED_RPCCALL, first: int = 0) -> tuple[np.ndarray, np.ndarray]:
+    """A record-marked stream of n RPC messages for the dispatch path
+    (SURVEY.md §8 f1).  Returns (stream bytes, offsets[n+1] of the marks).
+
+    Per message i (draws d0..d5 of stream seed, message first+i):
+      sel = d2 % 32
+        0-23  CALL of a registered procedure (entry d3 % nreal of RPC_PROCS)
+        24    rpcvers 3                          -> RPC_MISMATCH reply
+        25    d3 odd: unknown prog (0x30000000 + d3 % 1000)  -> PROG_UNAVAIL
+              d3 even: prog 100005 (interface with no proc) -> PROC_UNAVAIL
+        26    registered prog, vers 100 + d3 % 7  -> PROG_MISMATCH
+        27    registered prog/vers, proc 5000 + d3 % 50 -> PROC_UNAVAIL
+        28    REPLY (MSG_ACCEPTED, SUCCESS) + result words -> dropped
+        29    msg_type 2 + d3 % 5 (bad discriminant) -> malformed
+        30    cred body length 401 + d3 % 8 (over opaque<400>) -> malformed
+        31    d3 % 3 == 0: truncated after prog (xdr_overflow)
+              d3 % 3 == 1: cred length 4k+1..3 with a nonzero pad byte
+              d3 % 3 == 2: cred length 0x10000 beyond the message
+      xid = lo32(d1); cred flavor d4 % 2, cred length (d4 >> 8) % 101;
+      verf flavor 0, verf length (d5 >> 8) % 9; (d5 >> 32) % 25 argument
+      words.  Body and argument words are lo32 of draw(seed ^ PAYLOAD_XOR,
+      64 * first + word position in the batch), pad bytes zero.
+    """
+    d = _draws(seed, n, 6, first)
+    u = lambda x: x.astype(np.int64)  # noqa: E731
+    sel = u(d[:, 2] % np.uint64(32))
+    d3 = u(d[:, 3] % np.uint64(1 << 30))
+    real = RPC_PROCS[RPC_PROCS[:, 3] == 0]
+    ent = real[d3 % len(real)]
+    prog, vers, proc = ent[:, 0].astype(np.int64), ent[:, 1].astype(np.int64), ent[:, 2].astype(np.int64)
+    rpcvers = np.where(sel == 24, 3, 2)
+    s25 = sel == 25
+    prog = np.where(s25 & (d3 % 2 == 1), 0x30000000 + d3 % 1000, np.where(s25, 100005, prog))
+    vers = np.where(s25 & (d3 % 2 == 0), 1, vers)
+    proc = np.where(s25 & (d3 % 2 == 0), d3 % 4, proc)
+    vers = np.where(sel == 26, 100 + d3 % 7, vers)
+    proc = np.where(sel == 27, 5000 + d3 % 50, proc)
+    reply = sel == 28
+    mtype = np.where(sel == 29, 2 + d3 % 5, np.where(reply, 1, 0))
+    trunc = (sel == 31) & (d3 % 3 == 0)
+    badpad = (sel == 31) & (d3 % 3 == 1)
+    huge = (sel == 31) & (d3 % 3 == 2)
+    cred_len = u((d[:, 4] >> np.uint64(8)) % np.uint64(101))
+    cred_len = np.where(sel == 30, 401 + d3 % 8, cred_len)
+    cred_len = np.where(badpad, 4 * (cred_len // 8) + 1 + d3 % 3, cred_len)
+    cred_wire = np.where(huge, 0, (cred_len + 3) // 4)  # body words present in the stream
+    cred_len = np.where(huge, 0x10000, cred_len)
+    verf_len = u((d[:, 5] >> np.uint64(8)) % np.uint64(9))
+    verf_wire = (verf_len + 3) // 4
+    nargs = u((d[:, 5] >> np.uint64(32)) % np.uint64(25))
+    # words per message: mark + xid + mtype + [call: 5 + 1 + cred + 2 + verf]
+    # or [reply: stat + flavor + len(0) + accept_stat] + args
+    call_words = 1 + 1 + 1 + 5 + 1 + cred_wire + 2 + verf_wire + nargs
+    reply_words = 1 + 1 + 1 + 4 + nargs
+    words = np.where(reply, reply_words, np.where(trunc, 5, call_words))
+    off = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(words, out=off[1:])
+    total = int(off[-1])
+    # every word starts as payload (lo32 of the payload stream, by global word)
+    gw = np.arange(total, dtype=np.uint64)
+    base = int(first) * 64  # disjoint payload words per message batch position
+    out = (draw(seed ^ PAYLOAD_XOR, gw + np.uint64(base)) & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    o = off[:-1]
+
+    def put(mask, pos, val):
+        idx = np.nonzero(mask)[0]
+        out[o[idx] + pos[idx] if isinstance(pos, np.ndarray) else o[idx] + pos] = _be(
+            np.asarray(val)[idx] if np.ndim(val) else np.full(len(idx), val))
+
+    allm = np.ones(n, dtype=bool)
+    put(allm, 0, (words - 1) * 4 | 0x80000000)
+    put(allm, 1, d[:, 1] & np.uint64(0xFFFFFFFF))
+    put(allm, 2, mtype)
+    call = ~reply
+    put(call, 3, rpcvers)
+    put(call, 4, prog)
+    put(call & ~trunc, 5, vers)
+    put(call & ~trunc, 6, proc)
+    put(call & ~trunc, 7, d[:, 4] % np.uint64(2))
+    put(call & ~trunc, 8, cred_len)
+    # zero the pad bytes of the last cred / verf word (badpad keeps a nonzero one)
+    cl = np.where(call & ~trunc & ~huge & (cred_len % 4 != 0), cred_len, 0)
+    m = np.nonzero(cl)[0]
+    last = o[m] + 9 + (cl[m] - 1) // 4
+    keep = (np.uint64(1) << (np.uint64(8) * (cl[m] % 4).astype(np.uint64))) - np.uint64(1)
+    lw = out[last].astype(np.uint64) & keep
+    lw = np.where(badpad[m], lw | np.uint64(0xFF000000), lw)
+    out[last] = lw.astype(np.uint32)
+    vpos = 9 + cred_wire
+    put(call & ~trunc, vpos, np.zeros(n, dtype=np.int64))
+    put(call & ~trunc, vpos + 1, verf_len)
+    vl = np.where(call & ~trunc & (verf_len % 4 != 0), verf_len, 0)
+    m = np.nonzero(vl)[0]
+    last = o[m] + vpos[m] + 2 + (vl[m] - 1) // 4
+    keep = (np.uint64(1) << (np.uint64(8) * (vl[m] % 4).astype(np.uint64))) - np.uint64(1)
+    out[last] = (out[last].astype(np.uint64) & keep).astype(np.uint32)
+    put(reply, 3, 0)  # MSG_ACCEPTED
+    put(reply, 4, 0)  # verf AUTH_NONE
+    put(reply, 5, 0)  # verf body<> length 0
+    put(reply, 6, 0)  # SUCCESS
+    return out.view(np.uint8), (off * 4).astype(np.uint64)
