@@ -21,6 +21,7 @@
  *                                                            xdrpp/msgsock.cc:38-119
  *   xdrg_serial_sizes     <- xdr_argpack_size / xdr_size     xdrpp/marshal.h:223-234,
  *                                                            xdrpp/types.h:240-244
+ *   xdrg_record_depths    <- check_xdr_depth / depth_checker xdrpp/depth_checker.h:10-79
  *   xdrg_swap32/xdrg_swap64 <- swap32 / swap64               xdrpp/endian.h:56-68
  *   xdrg_rpc_dispatch     <- rpc_server_base::dispatch header decode + routing
  *                            xdrpp/server.cc:78-117, srpc.h:121-128
@@ -468,6 +469,14 @@ int xdrg_rpc_replies(const xdrg_rpc_hdr *d_hdrs, uint64_t n, void *d_out, uint64
                      uint64_t *d_offsets, void *d_workspace, size_t workspace_bytes,
                      xdrg_status *d_status, void *stream);
 size_t xdrg_rpc_replies_workspace_size(uint64_t n);
+
+/* Recursion depth per record: d_depths[i] = the deepest class/container
+ * level record i's walk enters (the record itself is level 1), so
+ * xdr::check_xdr_depth(r_i, limit) (xdrpp/depth_checker.h:72-79) is
+ * d_depths[i] <= limit.  A bad union discriminant stops the walk and is
+ * reported through d_status like the size pass. */
+int xdrg_record_depths(const xdrg_plan *plan, const void *d_native, uint64_t n,
+                       uint32_t *d_depths, xdrg_status *d_status, void *stream);
 
 /* Size pass alone: d_sizes[i] = xdr_size(record i) (uint32). */
 int xdrg_serial_sizes(const xdrg_plan *plan, const void *d_native, uint64_t n,

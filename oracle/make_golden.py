@@ -81,7 +81,18 @@ def rpc_fixtures(manifest: dict) -> None:
             "stream_bytes": os.path.getsize(fp + ".stream")}
 
 
+def depth_fixtures() -> None:
+    """depth_checker (xdrpp/depth_checker.h): the smallest passing limit of
+    every record of the small batches, from the real check_xdr_depth."""
+    for schema, n in SMALL.items():
+        subprocess.check_call([BIN, "depths", schema, str(n),
+                               os.path.join(GOLD, f"{schema}_{n}.depths")])
+
+
 def main() -> int:
+    if "--only-depths" in sys.argv:
+        depth_fixtures()
+        return 0
     if "--only-rpc" in sys.argv:
         mp = os.path.join(GOLD, "manifest.json")
         manifest = json.load(open(mp))
@@ -114,6 +125,7 @@ def main() -> int:
                 for e in exts:
                     os.remove(pre + "." + e)
     rpc_fixtures(manifest)
+    depth_fixtures()
     with open(os.path.join(GOLD, "manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1, sort_keys=True)
     print("wrote", GOLD)

@@ -531,6 +531,21 @@ static void rpc_mode(const string &sp, const string &op, const string &pp, const
   write_file(pre + ".autherr", ae->raw_data(), ae->raw_size());
 }
 
+// ------------------------------------------------------------ depths
+// ref_golden depths <schema> <n> <out>: per record the smallest limit L for
+// which the REAL xdr::check_xdr_depth(r, L) holds (xdrpp/depth_checker.h).
+#include <xdrpp/depth_checker.h>
+
+template <typename T> static void depths_of(const vector<T> &v, const string &out) {
+  vector<uint32_t> d(v.size());
+  for (size_t r = 0; r < v.size(); ++r) {
+    uint32_t L = 0;
+    while (!xdr::check_xdr_depth(v[r], L)) ++L;
+    d[r] = L;
+  }
+  write_file(out, d.data(), d.size() * 4);
+}
+
 int main(int argc, char **argv) {
   if (argc < 2) die("usage: gen|kat|bench ...");
   string mode = argv[1];
@@ -557,6 +572,17 @@ int main(int argc, char **argv) {
     else if (schema == "recvar") { vector<recvar> v; gen_recvar(n, WG_SEED_RECVAR, v); emit(v, pre, wm); }
     else if (schema == "vecrec") { vector<vecrec> v; gen_vecrec(n, WG_SEED_VECREC, v); emit(v, pre, wm); }
     else if (schema == "rpc") { vector<rpcx::rpc_msg> v; gen_rpc(n, WG_SEED_RPC, v); emit(v, pre, wm); }
+    else die("unknown schema " + schema);
+    return 0;
+  }
+  if (mode == "depths") {
+    if (argc != 5) die("depths <schema> <n> <out>");
+    string o = argv[4];
+    if (schema == "numerics") { vector<testns::numerics> v; gen_numerics(n, WG_SEED_NUMERICS, v); depths_of(v, o); }
+    else if (schema == "rec128") { vector<rec128> v; gen_rec128(n, WG_SEED_REC128, 0, v); depths_of(v, o); }
+    else if (schema == "recvar") { vector<recvar> v; gen_recvar(n, WG_SEED_RECVAR, v); depths_of(v, o); }
+    else if (schema == "vecrec") { vector<vecrec> v; gen_vecrec(n, WG_SEED_VECREC, v); depths_of(v, o); }
+    else if (schema == "rpc") { vector<rpcx::rpc_msg> v; gen_rpc(n, WG_SEED_RPC, v); depths_of(v, o); }
     else die("unknown schema " + schema);
     return 0;
   }

@@ -259,6 +259,44 @@ int xdro_sizes(const xdrg_op *ops, uint32_t nops, const uint32_t *table, uint32_
   return 0;
 }
 
+/* depth_checker (xdrpp/depth_checker.h:10-79): per record, the deepest
+ * class/container level its walk enters (the record is level 1; a union
+ * and a container count their own level, a non-empty xvector/pointer its
+ * element's).  check_xdr_depth(r, L) == depths[r] <= L. */
+int xdro_depths(const xdrg_op *ops, uint32_t nops, const uint32_t *table, uint32_t stride,
+                const uint8_t *native, uint64_t n, uint32_t *depths, uint64_t *erec,
+                uint32_t *eop) {
+  plan_t P = {ops, nops, table, stride};
+  for (uint64_t r = 0; r < n; ++r) {
+    const uint8_t *nat = native + r * stride;
+    uint32_t pc = 0, d = 0;
+    for (;;) {
+      const xdrg_op *op = &P.ops[pc];
+      if (op->kind == XDRG_OP_END) break;
+      if (op->kind != XDRG_OP_JUMP && op->depth > d) d = op->depth;
+      if (op->kind == XDRG_OP_UNION) {
+        int64_t t = union_target(&P, op, rd32(nat + op->noff));
+        if (t < 0) { *erec = r; *eop = pc; return XDRG_ERR_BAD_DISCRIMINANT; }
+        pc = (uint32_t)t;
+      } else if (op->kind == XDRG_OP_JUMP) {
+        pc = op->arg0;
+      } else if (op->kind == XDRG_OP_VECTOR) {
+        xdrg_bytes_ref ref;
+        memcpy(&ref, nat + op->noff, sizeof ref);
+        if (ref.len)
+          for (uint32_t k = 1; k <= op->arg2; ++k)
+            if (P.ops[pc + k].depth > d) d = P.ops[pc + k].depth;
+        pc += 1 + op->arg2;
+      } else {
+        ++pc;
+      }
+    }
+    depths[r] = d;
+  }
+  (void)nops;
+  return 0;
+}
+
 /* ---------------------------------------------------------------- decode */
 /* Decode one record from [p, e); returns 0 or an error code (op in *eop).
  * *pp is advanced.  Native record is zero-filled first.  A payload's

@@ -185,3 +185,17 @@ def rpc_replies(hdrs: np.ndarray, cap: int | None = None):
     h = np.ascontiguousarray(hdrs)
     rc = _rpc_lib().xdro_rpc_replies(_p(h), n, _p(out), cap, _p(offs), C.byref(tot), C.byref(er))
     return out[:min(tot.value, cap)], offs, rc, er.value
+
+
+def depths(plan, native: np.ndarray, n: int) -> np.ndarray:
+    """depth_checker per record (xdro_depths); raises OracleError."""
+    L = lib()
+    vp, u64, u32 = C.c_void_p, C.c_uint64, C.c_uint32
+    L.xdro_depths.argtypes = [vp, u32, vp, u32, vp, u64, vp, C.POINTER(u64), C.POINTER(u32)]
+    out = np.zeros(max(n, 1), dtype=np.uint32)
+    er, eo = C.c_uint64(0), C.c_uint32(0)
+    rc = L.xdro_depths(_p(plan.ops), len(plan.ops), _p(plan.table), plan.stride, _p(native), n,
+                       _p(out), C.byref(er), C.byref(eo))
+    if rc:
+        raise OracleError(rc, er.value, eo.value)
+    return out[:n]

@@ -392,3 +392,27 @@ def test_var_kernels_capacity_and_stack(dev, forced, name):
         want = _oracle_err(lambda: O.encode(p.cp, nat, n, heap, stack_limit=limit))
         got = _gpu_err(lambda: mar.encode(to_dev(nat, dev), n, to_dev(heap, dev), stack_limit=limit))
         assert got == want
+
+
+# ------------------------------------------------------------ depth_checker
+@pytest.mark.parametrize("name", SCHEMAS)
+def test_record_depths_golden(dev, name):
+    """xdrg_record_depths vs the real check_xdr_depth (xdrpp/depth_checker.h):
+    depths[i] is the smallest limit record i passes, so check_xdr_depth(r, L)
+    == depths <= L at every L."""
+    n = SMALL_N[name]
+    mar = M.Marshaler(plan(name), dev)
+    nat = to_dev(golden(name, n, "native"), dev)
+    want = golden(name, n, "depths", np.uint32)
+    got = mar.record_depths(nat, n).cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, want)
+    for lim in range(int(want.max()) + 2):
+        assert np.array_equal(mar.check_xdr_depth(nat, n, lim).cpu().numpy(), want <= lim)
+
+
+@pytest.mark.parametrize("name,n", [("rpc", 1 << 20), ("vecrec", 1 << 16)])
+def test_record_depths_full_size(dev, name, n):
+    p = plan(name)
+    nat, _ = W.GENERATORS[name](n)
+    got = M.Marshaler(p, dev).record_depths(to_dev(nat, dev), n).cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, O.depths(p.cp, nat, n))

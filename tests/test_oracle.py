@@ -199,3 +199,13 @@ def test_oracle_stack_limit():
     with pytest.raises(O.OracleError) as ei:
         O.decode(CP["rpc"], x, 4, offs, stack_limit=1)
     assert ei.value.code == A.ERR_STACK_GET
+
+
+@pytest.mark.parametrize("name", SCHEMAS)
+def test_oracle_depths_golden(name):
+    """depth_checker: the C restatement vs the real check_xdr_depth
+    (oracle/ref_golden depths: the smallest passing limit per record)."""
+    n = SMALL_N[name]
+    cp = compile_plan(S.ALL[name])
+    d = O.depths(cp, golden(name, n, "native"), n)
+    assert np.array_equal(d, golden(name, n, "depths", np.uint32))

@@ -105,7 +105,7 @@ EXPORTED = (
     "xdrg_error_message", "xdrg_error_exception", "xdrg_last_hip_error",
     "xdrg_decode_heap_size", "xdrg_encode_msgs", "xdrg_decode_msgs", "xdrg_index_msgs",
     "xdrg_index_workspace_size", "xdrg_rpc_dispatch", "xdrg_rpc_check_replies",
-    "xdrg_rpc_replies", "xdrg_rpc_replies_workspace_size",
+    "xdrg_rpc_replies", "xdrg_rpc_replies_workspace_size", "xdrg_record_depths",
 )
 
 # RPC header batches (include/xdrgpu.h "RPC header batches")
@@ -171,6 +171,8 @@ def lib() -> C.CDLL:
     L.xdrg_rpc_replies.restype = C.c_int
     L.xdrg_rpc_replies_workspace_size.argtypes = [u64]
     L.xdrg_rpc_replies_workspace_size.restype = sz
+    L.xdrg_record_depths.argtypes = [vp, vp, u64, vp, vp, vp]
+    L.xdrg_record_depths.restype = C.c_int
     L.xdrg_serial_sizes.argtypes = [vp, vp, u64, vp, u32, vp, vp]
     L.xdrg_serial_sizes.restype = C.c_int
     L.xdrg_swap32.argtypes = [vp, vp, u64, vp]

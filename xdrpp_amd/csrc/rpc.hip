@@ -3,17 +3,17 @@
 // check) and the batch's error replies.  SURVEY.md §8 f1.
 //
 // Kernels
-//   k_rpc_hdr<CLIENT, LDS>  one message per lane: decodes the rpc_msg header
+//   k_rpc_hdr<CLIENT>  one message per lane: decodes the rpc_msg header
 //       exactly as xdr_get over xdr_traits<rpc_msg> does (xdrpp/rpc_msg.x,
 //       xdrpp/marshal.h:142-211, marshal.cc:43-57) and routes it:
 //       server  rpc_server_base::dispatch (xdrpp/server.cc:78-117) + the
 //               procedure switch of srpc_service::process (srpc.h:121-128)
-//               against a sorted (prog, vers, proc) table staged in LDS;
+//               by binary search of a sorted (prog, vers, proc) table;
 //       client  check_call_hdr (xdrpp/rpc_msg.cc:115-131) and the xid test
 //               of synchronous_client_base::invoke (srpc.h:61-66).
-//       The first eight payload words are fetched as independent loads, so
-//       a CALL header costs one memory round trip plus one for the verf and
-//       pad words; the 64-byte result is written as four 16-byte stores.
+//       A wave stages its 64 messages' stretch of the stream in LDS with
+//       coalesced 16-byte loads and walks the headers from there; the
+//       64-byte results leave through LDS as coalesced 16-byte stores.
 //   k_rpc_reply_sizes / launch_block_scan / k_rpc_reply_emit  the error
 //       replies (server.cc:8-67) as record-marked messages in message order:
 //       per-256-header byte sums, the shared block scan, then each lane
@@ -27,7 +27,6 @@ namespace {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr uint32_t kMaxAuth = 400;  // opaque_auth body<400> (rpc_msg.x)
-constexpr uint32_t kLdsProcs = 1024;
 
 enum : uint32_t { CALL = 0, REPLY = 1 };
 enum : uint32_t { MSG_ACCEPTED = 0, MSG_DENIED = 1 };
@@ -78,13 +77,19 @@ struct hdr_out {
   uint64_t body_off = 0, end = 0;
 };
 
-// Payload cursor over [p, e) of the stream.
+// Payload cursor over [p, e) of the stream.  Words inside the wave's LDS
+// window [wb, we) of the stream come from LDS, the rest from global memory.
 struct cursor {
   const uint8_t *s;
+  const uint32_t *win;
+  uint64_t wb, we;
   uint64_t p, e;
+  __device__ __forceinline__ uint32_t raw(uint64_t q) const {
+    return q >= wb && q + 4 <= we ? win[(q - wb) >> 2] : ld32(s, q);
+  }
   __device__ bool word(uint32_t &v) {  // xdr_generic_get::check(4) + get32
     if (e - p < 4) return false;
-    v = bswap(ld32(s, p));
+    v = bswap(raw(p));
     p += 4;
     return true;
   }
@@ -96,7 +101,7 @@ __device__ uint32_t auth_body(cursor &c, uint32_t len) {
   if (len > c.e - c.p) return XDRG_ERR_OVERFLOW_GET;
   if (len > kMaxAuth) return XDRG_ERR_XVECTOR_BOUND;
   if (len & 3u) {
-    const uint32_t w = ld32(c.s, c.p + (len & ~3u));
+    const uint32_t w = c.raw(c.p + (len & ~3u));
     if (w & (0xffffffffu << (8u * (len & 3u)))) return XDRG_ERR_NONZERO_PAD;
   }
   c.p += (len + 3u) & ~3u;
@@ -163,47 +168,67 @@ __device__ uint32_t walk(cursor &c, const uint32_t (&pre)[8], uint32_t nw, hdr_o
   return 0;
 }
 
-template <bool CLIENT, bool LDS>
-__global__ __launch_bounds__(256) void k_rpc_hdr(const uint8_t *__restrict__ s, uint64_t len,
-                                                 const uint64_t *__restrict__ offs, uint64_t n,
-                                                 const xdrg_rpc_proc *__restrict__ g_procs,
-                                                 uint32_t nprocs, const uint32_t *__restrict__ xids,
-                                                 xdrg_rpc_hdr *__restrict__ out) {
-  __shared__ xdrg_rpc_proc sp[LDS ? kLdsProcs : 1];
-  const xdrg_rpc_proc *procs = g_procs;
-  if (!CLIENT && LDS) {
-    for (uint32_t i = threadIdx.x; i < nprocs; i += blockDim.x) sp[i] = g_procs[i];
-    __syncthreads();
-    procs = sp;
+// One wave per workgroup, 64 consecutive messages.  Their bytes are one
+// contiguous stretch of the stream: the wave loads up to kWinBytes of it
+// into LDS with coalesced 16-byte loads, then every lane walks its header
+// from LDS (words past the window are read from global memory).  The 64
+// 64-byte records are transposed through LDS and stored as coalesced
+// 16-byte chunks.
+constexpr uint32_t kWinBytes = 12288;
+
+template <bool CLIENT>
+__global__ __launch_bounds__(64) void k_rpc_hdr(const uint8_t *__restrict__ s, uint64_t len,
+                                                const uint64_t *__restrict__ offs, uint64_t n,
+                                                const xdrg_rpc_proc *__restrict__ procs,
+                                                uint32_t nprocs, const uint32_t *__restrict__ xids,
+                                                xdrg_rpc_hdr *__restrict__ out) {
+  __shared__ u32x4 win4[kWinBytes / 16];
+  const uint32_t lane = threadIdx.x;
+  const uint64_t b0 = static_cast<uint64_t>(blockIdx.x) * 64u;
+  const uint64_t i = b0 + lane;
+  const uint32_t nmsg = static_cast<uint32_t>(min<uint64_t>(64, n - b0));
+  const uint64_t m0 = i < n ? offs[i] : 0, m1 = i < n ? offs[i + 1] : 0;
+  // the wave's stretch [lo, hi) and its window (16-byte aligned stream)
+  const uint64_t lo = __shfl(m0, 0, 64), hi = __shfl(m1, nmsg - 1, 64);
+  uint64_t wb = lo & ~15ull, we = wb;
+  if ((reinterpret_cast<uintptr_t>(s) & 15u) == 0 && lo <= hi && hi <= len) {
+    we = min(min(hi, wb + kWinBytes), len);
+    we = wb + ((we - wb) & ~15ull);
+    const uint32_t nc = static_cast<uint32_t>((we - wb) >> 4);
+    const u32x4 *src = reinterpret_cast<const u32x4 *>(s + wb);
+    for (uint32_t c = lane; c < nc; c += 64) win4[c] = src[c];
   }
-  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  __syncthreads();
   hdr_out h;
-  const uint64_t m0 = offs[i], m1 = offs[i + 1];
   h.end = m1;
   uint32_t err = 0;
-  if (m1 > len || m1 < m0 + 4 || (m0 & 3u)) {
-    err = XDRG_ERR_MSG_MISMATCH;  // not a message of an xdrg_index_msgs index
-  } else if ((m1 - m0) & 3u) {
-    err = XDRG_ERR_SIZE_NOT_MULT4;  // xdr_generic_get ctor, marshal.h:157-159
-  } else {
-    cursor c;
-    c.s = s;
-    c.p = m0 + 4;
-    c.e = m1;
-    const uint64_t pw = (m1 - m0 - 4) >> 2;
-    const uint32_t nw = pw < 8 ? static_cast<uint32_t>(pw) : 8u;
-    uint32_t pre[8];
+  if (i < n) {
+    if (m1 > len || m1 < m0 + 4 || (m0 & 3u)) {
+      err = XDRG_ERR_MSG_MISMATCH;  // not a message of an xdrg_index_msgs index
+    } else if ((m1 - m0) & 3u) {
+      err = XDRG_ERR_SIZE_NOT_MULT4;  // xdr_generic_get ctor, marshal.h:157-159
+    } else {
+      cursor c;
+      c.s = s;
+      c.win = reinterpret_cast<const uint32_t *>(win4);
+      c.wb = wb;
+      c.we = we;
+      c.p = m0 + 4;
+      c.e = m1;
+      const uint64_t pw = (m1 - m0 - 4) >> 2;
+      const uint32_t nw = pw < 8 ? static_cast<uint32_t>(pw) : 8u;
+      uint32_t pre[8];
 #pragma unroll
-    for (uint32_t k = 0; k < 8; ++k) pre[k] = k < nw ? bswap(ld32(s, c.p + 4u * k)) : 0u;
-    err = walk(c, pre, nw, h);
-    h.body_off = c.p;
-  }
-  if (err) {  // a malformed header keeps only action, err, the union site and end
-    h = hdr_out{};
-    h.end = m1;
-    h.w[0] = err >> 8;
-    err &= 0xffu;
+      for (uint32_t k = 0; k < 8; ++k) pre[k] = k < nw ? bswap(c.raw(c.p + 4u * k)) : 0u;
+      err = walk(c, pre, nw, h);
+      h.body_off = c.p;
+    }
+    if (err) {  // a malformed header keeps only action, err, the union site and end
+      h = hdr_out{};
+      h.end = m1;
+      h.w[0] = err >> 8;
+      err &= 0xffu;
+    }
   }
   h.err = err;
   if (!CLIENT) {
@@ -242,12 +267,20 @@ __global__ __launch_bounds__(256) void k_rpc_hdr(const uint8_t *__restrict__ s, 
                                                     : XDRG_RPCR_RPCVERS_MISMATCH;
     if (h.action == XDRG_RPCR_OK && xids && xids[i] != h.xid) h.action = XDRG_RPCR_BAD_XID;
   }
-  u32x4 *o = reinterpret_cast<u32x4 *>(out + i);
-  o[0] = u32x4{h.xid, h.action | (h.err << 16) | (h.mtype << 24), h.w[0], h.w[1]};
-  o[1] = u32x4{h.w[2], h.w[3], h.w[4], h.w[5]};
-  o[2] = u32x4{h.w[6], h.w[7], h.cred_len, h.verf_len};
-  o[3] = u32x4{static_cast<uint32_t>(h.body_off), static_cast<uint32_t>(h.body_off >> 32),
-               static_cast<uint32_t>(h.end), static_cast<uint32_t>(h.end >> 32)};
+  // transpose the 64 records through LDS, then coalesced 16-byte stores
+  __syncthreads();  // window fully consumed
+  win4[4 * lane + 0] = u32x4{h.xid, h.action | (h.err << 16) | (h.mtype << 24), h.w[0], h.w[1]};
+  win4[4 * lane + 1] = u32x4{h.w[2], h.w[3], h.w[4], h.w[5]};
+  win4[4 * lane + 2] = u32x4{h.w[6], h.w[7], h.cred_len, h.verf_len};
+  win4[4 * lane + 3] = u32x4{static_cast<uint32_t>(h.body_off), static_cast<uint32_t>(h.body_off >> 32),
+                             static_cast<uint32_t>(h.end), static_cast<uint32_t>(h.end >> 32)};
+  __syncthreads();
+  u32x4 *o = reinterpret_cast<u32x4 *>(out + b0);
+#pragma unroll
+  for (uint32_t q = 0; q < 4; ++q) {
+    const uint32_t c = q * 64u + lane;
+    if (c < 4u * nmsg) o[c] = win4[c];
+  }
 }
 
 // -------------------------------------------------------------- replies
@@ -354,17 +387,13 @@ int hdr_launch(bool client, const void *d_stream, uint64_t len, const uint64_t *
       (reinterpret_cast<uintptr_t>(d_hdrs) & 15u) || (d_procs && (reinterpret_cast<uintptr_t>(d_procs) & 15u)) ||
       (d_xids && (reinterpret_cast<uintptr_t>(d_xids) & 3u)))
     return XDRG_EALIGN;
-  const uint64_t blocks = (n + 255) / 256;
+  const uint64_t blocks = (n + 63) / 64;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const uint8_t *s8 = static_cast<const uint8_t *>(d_stream);
   if (client)
-    k_rpc_hdr<true, false><<<blocks, 256, 0, s>>>(s8, len, d_offsets, n, nullptr, 0, d_xids, d_hdrs);
-  else if (nprocs <= kLdsProcs)
-    k_rpc_hdr<false, true><<<blocks, 256, 0, s>>>(s8, len, d_offsets, n, d_procs, nprocs, nullptr,
-                                                  d_hdrs);
+    k_rpc_hdr<true><<<blocks, 64, 0, s>>>(s8, len, d_offsets, n, nullptr, 0, d_xids, d_hdrs);
   else
-    k_rpc_hdr<false, false><<<blocks, 256, 0, s>>>(s8, len, d_offsets, n, d_procs, nprocs,
-                                                   nullptr, d_hdrs);
+    k_rpc_hdr<false><<<blocks, 64, 0, s>>>(s8, len, d_offsets, n, d_procs, nprocs, nullptr, d_hdrs);
   HIPCHK(hipGetLastError());
   return XDRG_OK;
 }

@@ -298,13 +298,16 @@ constexpr uint32_t kPcDone = 0xffffffffu;
 // One 64-thread workgroup = 64 consecutive records.  The native records are
 // staged in LDS with coalesced 16-byte loads, so the walk reads fields from
 // LDS instead of issuing one dependent global load per op.
-template <bool TILE>
+// DEPTH: also the deepest class/container level the record's walk enters
+// (depth_checker, xdrpp/depth_checker.h:41-54), into depths[r].
+template <bool TILE, bool DEPTH = false>
 __global__ __launch_bounds__(64) void k_var_size(const uint8_t *__restrict__ native, uint64_t n,
                                                  uint32_t stride, const xdrg_op *__restrict__ ops,
                                                  uint32_t nops, const uint32_t *__restrict__ table,
                                                  uint32_t *__restrict__ sizes,
                                                  unsigned long long *__restrict__ block_sums,
-                                                 uint32_t mark, unsigned long long *err) {
+                                                 uint32_t mark, unsigned long long *err,
+                                                 uint32_t *__restrict__ depths = nullptr) {
   extern __shared__ __attribute__((aligned(16))) uint8_t tile[];
   const uint32_t lane = threadIdx.x;
   const uint64_t wr0 = static_cast<uint64_t>(blockIdx.x) * 64u;
@@ -323,11 +326,17 @@ __global__ __launch_bounds__(64) void k_var_size(const uint8_t *__restrict__ nat
   wave_sync();
   const uint8_t *nat = TILE ? tile + lane * stride : native + r * stride;
   uint64_t s = mark;  // record-marked batches: the message's 4-byte mark
-  uint32_t pc = r < n ? 0u : kPcDone, bad_op = kPcDone;
+  uint32_t pc = r < n ? 0u : kPcDone, bad_op = kPcDone, dmax = 0;
   for (uint32_t upc = 0; upc < nops; ++upc) {
     if (!__any(pc == upc)) continue;
     const xdrg_op op = ops[upc];
     if (pc != upc) continue;
+    if (DEPTH && op.kind != XDRG_OP_JUMP && op.kind != XDRG_OP_END) {
+      dmax = max(dmax, static_cast<uint32_t>(op.depth));
+      // a non-empty xvector / pointer enters its element's levels
+      if (op.kind == XDRG_OP_VECTOR && *reinterpret_cast<const uint32_t *>(nat + op.noff + 8))
+        for (uint32_t k = 1; k <= op.arg2; ++k) dmax = max(dmax, static_cast<uint32_t>(ops[upc + k].depth));
+    }
     switch (op.kind) {
     case XDRG_OP_END: pc = kPcDone; break;
     case XDRG_OP_JUMP: pc = op.arg0; break;
@@ -362,7 +371,8 @@ __global__ __launch_bounds__(64) void k_var_size(const uint8_t *__restrict__ nat
     } else {
       size = static_cast<uint32_t>(s);
     }
-    sizes[r] = size;
+    if (sizes) sizes[r] = size;
+    if (DEPTH) depths[r] = dmax;
   }
   unsigned long long v = (size & kSizeErr) ? 0ull : size;
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -2340,6 +2350,30 @@ int xdrg_decode(const xdrg_plan *p, const void *d_xdr, uint64_t len, const uint6
   if (!d_offsets) return XDRG_EUNSUPPORTED;  // var decode needs a record index
   return var_decode(*p, d_xdr, len, d_offsets, n, d_native, d_heap_out, heap_cap, stack_limit,
                     d_status, 0u, s);
+}
+
+int xdrg_record_depths(const xdrg_plan *p, const void *d_native, uint64_t n, uint32_t *d_depths,
+                       xdrg_status *d_status, void *stream) {
+  if (!p || !d_status || (n && (!d_native || !d_depths))) return XDRG_EINVAL;
+  if (n == 0) return XDRG_OK;
+  if (int rc = plan_upload(p)) return rc;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (p->path != XDRG_PATH_VAR) {  // every record walks every op
+    HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_depths), int(p->max_depth), n, s));
+    return XDRG_OK;
+  }
+  const uint64_t nb = (n + 63) / 64;
+  const size_t tile = 64ull * p->stride;
+  const uint8_t *nat = static_cast<const uint8_t *>(d_native);
+  unsigned long long *err = err_ptr(d_status);
+  if (tile <= kVarLdsBudget)
+    k_var_size<true, true><<<nb, 64, tile, s>>>(nat, n, p->stride, p->d_ops, uint32_t(p->ops.size()),
+                                                p->d_table, nullptr, nullptr, 0u, err, d_depths);
+  else
+    k_var_size<false, true><<<nb, 64, 0, s>>>(nat, n, p->stride, p->d_ops, uint32_t(p->ops.size()),
+                                              p->d_table, nullptr, nullptr, 0u, err, d_depths);
+  HIPCHK(hipGetLastError());
+  return XDRG_OK;
 }
 
 int xdrg_serial_sizes(const xdrg_plan *p, const void *d_native, uint64_t n, uint32_t *d_sizes,

@@ -220,6 +220,22 @@ class Marshaler:
         self.check(s)
         return sizes[:n]
 
+    def record_depths(self, native, n) -> torch.Tensor:
+        """Deepest class/container level of every record's walk
+        (depth_checker, xdrpp/depth_checker.h:10-79); int32 [n]."""
+        d = torch.empty(max(n, 1), dtype=torch.int32, device=self.device)
+        s = _stream()
+        self.status.init(s)
+        A.check(A.lib().xdrg_record_depths(self.plan.handle, _ptr(native), n, _ptr(d),
+                                           self.status.ptr, s), "xdrg_record_depths")
+        self.check(s)
+        return d[:n]
+
+    def check_xdr_depth(self, native, n, depth_limit: int) -> torch.Tensor:
+        """xdr::check_xdr_depth(r_i, depth_limit) for every record
+        (xdrpp/depth_checker.h:72-79): bool [n]."""
+        return self.record_depths(native, n) <= depth_limit
+
     def encode(self, native: torch.Tensor, n: int, heap: torch.Tensor | None = None,
                stack_limit: int = A.DEFAULT_STACK_LIMIT, capacity: int | None = None) -> EncodeResult:
         """= xdr_to_opaque(r0, ..., rn-1) (marshal.h:264-272)."""
