@@ -1,0 +1,661 @@
+"""XDR-language front end and plan back end.
+
+The reference's xdrc parses a .x file (RFC 4506 §6 plus xdrc's `namespace`
+and `%` pass-through lines: xdrc/parse.yy, xdrc/scan.ll) and emits C++
+xdr_traits<T> (xdrc/gen_hh.cc).  Its front end needs bison/flex, which this
+image lacks, so the grammar is re-stated here as a recursive-descent parser;
+the back end emits what the device path needs instead of C++ traits:
+
+  load(text)                       -> Spec: the types as xdrpp_amd.xdr_types
+                                      descriptors (Struct / Union / Enum / ...),
+                                      constants, programs
+  Spec.plan(name)                  -> CompiledPlan (ops + table for
+                                      xdrg_plan_create), no runtime recorder
+  Spec.proc_table()                -> the sorted (prog, vers, proc) table of
+                                      the .x file's program definitions, for
+                                      xdrg_rpc_dispatch (xdrc/gen_hh.cc:757-774
+                                      call_dispatch cases)
+  emit_plan_header(spec, names)    -> a C header with static xdrg_op tables,
+                                      strides and a create function per type:
+                                      the plan emitted at generation time
+
+    python -m xdrpp_amd.xdrc file.x -o file_plan.h [type ...]
+
+Names follow xdrc: an anonymous struct/union/enum declared inline for field
+`f` is named `_f_t` (xdrc/xdrc.cc:47), so bad-discriminant messages equal
+the reference's ("bad value of <tag> in <union>", gen_hh.cc:479-481).
+Input is expected after the C preprocessor as xdrc expects it; comments
+(/* */, //) and preprocessor lines are dropped here too.
+"""
+from __future__ import annotations
+
+import re
+import sys
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _abi as A
+from .xdr_types import (Bool, CompiledPlan, Double, Enum, Float, Hyper, Int, Opaque, OpaqueArray,
+                        Pointer, String, Struct, UHyper, UInt, Union, Void, XArray, XdrType,
+                        XVector, compile_plan)
+
+XDR_UNBOUNDED = A.XDR_MAX_LEN
+
+_KEYWORDS = {"const", "struct", "union", "enum", "typedef", "program", "namespace", "bool",
+             "unsigned", "int", "hyper", "float", "double", "quadruple", "void", "version",
+             "switch", "case", "default", "opaque", "string"}
+_RESERVED = {"char", "short", "inline", "sizeof"}  # scan.ll:66-69
+
+_TOKEN = re.compile(r"""
+    (?P<ws>\s+)
+  | (?P<num>[+-]?0x[0-9a-fA-F]+|[+-]?[0-9]+)
+  | (?P<qid>(?:::)?[A-Za-z_][A-Za-z_0-9]*(?:::[A-Za-z_][A-Za-z_0-9]*)+|::[A-Za-z_][A-Za-z_0-9]*)
+  | (?P<id>[A-Za-z_][A-Za-z_0-9]*)
+  | (?P<punct>[=;{}<>\[\]*,:()])
+""", re.X)
+
+
+class XdrcError(ValueError):
+    pass
+
+
+def _strip(text: str) -> tuple[str, list[str]]:
+    """Drop comments, preprocessor lines and %-pass-through lines (kept)."""
+    text = re.sub(r"/\*.*?\*/", lambda m: "\n" * m.group(0).count("\n"), text, flags=re.S)
+    text = re.sub(r"//[^\n]*", "", text)
+    out, lits = [], []
+    for line in text.split("\n"):
+        if line.startswith("%"):
+            lits.append(line[1:])
+            out.append("")
+        elif line.lstrip().startswith("#"):
+            out.append("")
+        else:
+            out.append(line)
+    return "\n".join(out), lits
+
+
+def tokenize(text: str) -> list[tuple[str, str, int]]:
+    body, _ = _strip(text)
+    toks, pos, line = [], 0, 1
+    while pos < len(body):
+        m = _TOKEN.match(body, pos)
+        if not m:
+            raise XdrcError(f"line {line}: syntax error at {body[pos:pos + 20]!r}")
+        kind = m.lastgroup
+        s = m.group(0)
+        if kind == "ws":
+            line += s.count("\n")
+        else:
+            if kind == "id" and s in _RESERVED:
+                raise XdrcError(f"line {line}: illegal use of reserved word {s!r}")
+            if kind == "id" and s in _KEYWORDS:
+                kind = s
+            toks.append((kind, s, line))
+        pos = m.end()
+    toks.append(("eof", "", line))
+    return toks
+
+
+# ----------------------------------------------------------------- AST
+@dataclass
+class Decl:
+    """rpc_decl: a type spec, an id and a qualifier (xdrc_internal.h)."""
+    id: str
+    type: object            # str (base type / name) or an inline EnumDef/StructDef/UnionDef
+    qual: str = "scalar"    # scalar | array | vec | ptr
+    bound: object = None    # value (str) for array/vec; XDR_UNBOUNDED for <>
+
+
+@dataclass
+class EnumDef:
+    id: str
+    tags: list              # [(name, value-string or None)]
+
+
+@dataclass
+class StructDef:
+    id: str
+    decls: list
+
+
+@dataclass
+class UnionDef:
+    id: str
+    tag_type: object
+    tag_id: str
+    arms: list              # [(case value strings or None for default, Decl or None for void)]
+
+
+@dataclass
+class ProcDef:
+    id: str
+    val: int
+    args: list
+    res: str
+
+
+@dataclass
+class VersDef:
+    id: str
+    val: int
+    procs: list = field(default_factory=list)
+
+
+@dataclass
+class ProgDef:
+    id: str
+    val: int
+    vers: list = field(default_factory=list)
+
+
+class _Parser:
+    def __init__(self, toks):
+        self.t, self.i = toks, 0
+
+    def peek(self, k=0):
+        return self.t[self.i + k]
+
+    def take(self, kind=None, value=None):
+        tk = self.t[self.i]
+        if (kind and tk[0] != kind) or (value and tk[1] != value):
+            want = value or kind
+            raise XdrcError(f"line {tk[2]}: expected {want!r}, got {tk[1] or tk[0]!r}")
+        self.i += 1
+        return tk
+
+    def accept(self, value):
+        if self.peek()[1] == value and self.peek()[0] in (value, "punct"):
+            self.i += 1
+            return True
+        return False
+
+    # file: definition*
+    def file(self, until_brace=False):
+        defs = []
+        while True:
+            k, v, _ = self.peek()
+            if k == "eof" or (until_brace and v == "}"):
+                return defs
+            defs.extend(self.definition())
+
+    def definition(self):
+        k, v, ln = self.peek()
+        if k == "const":
+            self.take()
+            name = self.take("id")[1]
+            self.take("punct", "=")
+            val = self.value()
+            self.take("punct", ";")
+            return [("const", name, val)]
+        if k == "enum":
+            self.take()
+            name = self.take("id")[1]
+            e = EnumDef(name, self.enum_body())
+            self.take("punct", ";")
+            return [("enum", e)]
+        if k == "struct":
+            self.take()
+            name = self.take("id")[1]
+            s = StructDef(name, self.struct_body())
+            self.take("punct", ";")
+            return [("struct", s)]
+        if k == "union":
+            self.take()
+            name = self.take("id")[1]
+            u = self.union_body(name)
+            self.take("punct", ";")
+            return [("union", u)]
+        if k == "typedef":
+            self.take()
+            if self.peek()[0] == "struct" and self.peek(1)[0] in ("id", "qid") and \
+                    self.peek(2)[1] != "{":
+                self.take()  # typedef struct foo bar;  (parse.yy def_type)
+            d = self.declaration()
+            return [("typedef", d)]
+        if k == "program":
+            return [("program", self.program())]
+        if k == "namespace":
+            self.take()
+            self.take("id")
+            self.take("punct", "{")
+            defs = self.file(until_brace=True)
+            self.take("punct", "}")
+            return defs
+        raise XdrcError(f"line {ln}: unexpected {v!r}")
+
+    def value(self):
+        k, v, ln = self.peek()
+        if k in ("num", "id", "qid"):
+            self.i += 1
+            return v
+        raise XdrcError(f"line {ln}: expected a value, got {v!r}")
+
+    def enum_body(self):
+        self.take("punct", "{")
+        tags = []
+        while True:
+            name = self.take("id")[1]
+            val = None
+            if self.accept("="):
+                val = self.value()
+            tags.append((name, val))
+            if self.accept(","):
+                if self.peek()[1] == "}":
+                    break  # comma after the last tag (xdrc warns)
+                continue
+            break
+        self.take("punct", "}")
+        return tags
+
+    def struct_body(self):
+        self.take("punct", "{")
+        decls = [self.declaration()]
+        while self.peek()[1] != "}":
+            decls.append(self.declaration())
+        self.take("punct", "}")
+        return decls
+
+    def union_body(self, name):
+        self.take("switch")
+        self.take("punct", "(")
+        tag_type = self.type_name()
+        tag_id = self.take("id")[1]
+        self.take("punct", ")")
+        self.take("punct", "{")
+        arms = []
+        while self.peek()[1] != "}":
+            cases = []
+            while self.peek()[0] in ("case", "default"):
+                if self.peek()[0] == "case":
+                    self.take()
+                    cases.append(self.value())
+                else:
+                    self.take()
+                    cases.append(None)
+                self.take("punct", ":")
+            if not cases:
+                raise XdrcError(f"line {self.peek()[2]}: expected case")
+            if self.peek()[0] == "void":
+                self.take()
+                self.take("punct", ";")
+                arms.append((cases, None))
+            else:
+                arms.append((cases, self.declaration()))
+        self.take("punct", "}")
+        if sum(c is None for cs, _ in arms for c in cs) > 1:
+            raise XdrcError(f"union {name}: duplicate default statement")
+        return UnionDef(name, tag_type, tag_id, arms)
+
+    def type_name(self):
+        k, v, ln = self.peek()
+        if k == "unsigned":
+            self.take()
+            if self.peek()[0] == "int":
+                self.take()
+                return "unsigned"
+            if self.peek()[0] == "hyper":
+                self.take()
+                return "unsigned hyper"
+            return "unsigned"
+        if k in ("int", "hyper", "float", "double", "quadruple", "bool"):
+            self.take()
+            return k
+        if k in ("id", "qid"):
+            self.take()
+            return v
+        raise XdrcError(f"line {ln}: expected a type, got {v!r}")
+
+    def type_specifier(self, anon_for=None):
+        k = self.peek()[0]
+        if k == "enum" and self.peek(1)[1] == "{":
+            self.take()
+            return EnumDef("", self.enum_body())
+        if k == "struct" and self.peek(1)[1] == "{":
+            self.take()
+            return StructDef("", self.struct_body())
+        if k == "union" and self.peek(1)[0] == "switch":
+            self.take()
+            return self.union_body("")
+        if k == "struct":  # "struct foo" as a type name
+            self.take()
+        return self.type_name()
+
+    def vec_len(self):
+        self.take("punct", "<")
+        if self.accept(">"):
+            return XDR_UNBOUNDED
+        v = self.value()
+        self.take("punct", ">")
+        return v
+
+    def declaration(self):
+        k = self.peek()[0]
+        if k in ("opaque", "string"):
+            base = self.take()[0]
+            ident = self.take("id")[1]
+            if base == "opaque" and self.peek()[1] == "[":
+                self.take()
+                b = self.value()
+                self.take("punct", "]")
+                self.take("punct", ";")
+                return Decl(ident, "opaque", "array", b)
+            if base == "string" and self.peek()[1] == ";":
+                self.take()
+                return Decl(ident, "string", "vec", XDR_UNBOUNDED)
+            b = self.vec_len()
+            self.take("punct", ";")
+            return Decl(ident, base, "vec", b)
+        ts = self.type_specifier()
+        if self.accept("*"):
+            ident = self.take("id")[1]
+            self.take("punct", ";")
+            return Decl(ident, ts, "ptr")
+        ident = self.take("id")[1]
+        if self.accept("["):
+            b = self.value()
+            self.take("punct", "]")
+            self.take("punct", ";")
+            return Decl(ident, ts, "array", b)
+        if self.peek()[1] == "<":
+            b = self.vec_len()
+            self.take("punct", ";")
+            return Decl(ident, ts, "vec", b)
+        self.take("punct", ";")
+        return Decl(ident, ts)
+
+    def program(self):
+        self.take("program")
+        p = ProgDef(self.take("id")[1], 0)
+        self.take("punct", "{")
+        while self.peek()[0] == "version":
+            self.take()
+            vd = VersDef(self.take("id")[1], 0)
+            self.take("punct", "{")
+            while self.peek()[1] != "}":
+                res = "void" if self.peek()[0] == "void" else None
+                if res:
+                    self.take()
+                else:
+                    res = self.type_name()
+                pid = self.take("id")[1]
+                self.take("punct", "(")
+                args = []
+                if self.peek()[0] == "void":
+                    self.take()
+                else:
+                    args.append(self.type_name())
+                    while self.accept(","):
+                        args.append(self.type_name())
+                self.take("punct", ")")
+                self.take("punct", "=")
+                val = int(self.take("num")[1], 0)
+                self.take("punct", ";")
+                vd.procs.append(ProcDef(pid, val, args, res))
+            self.take("punct", "}")
+            self.take("punct", "=")
+            vd.val = int(self.take("num")[1], 0)
+            self.take("punct", ";")
+            vd.procs.sort(key=lambda q: q.val)
+            p.vers.append(vd)
+        self.take("punct", "}")
+        self.take("punct", "=")
+        p.val = int(self.take("num")[1], 0)
+        self.take("punct", ";")
+        p.vers.sort(key=lambda v: v.val)
+        return p
+
+
+# -------------------------------------------------------------- resolve
+_BASE = {"int": Int, "unsigned": UInt, "hyper": Hyper, "unsigned hyper": UHyper,
+         "float": Float, "double": Double, "bool": Bool}
+
+
+def _local(name: str) -> str:
+    return name.split("::")[-1]
+
+
+class _Unsupported(XdrType):
+    """A type the .x file defines but device plans cannot express: a
+    reference to a type from inside its own definition (tests/xdrtest.x has
+    lists and trees; plans are flat DAGs bounded at plan creation), or a
+    counted/optional container of variable-size elements.  It parses, and
+    only compiling a plan that contains it fails."""
+
+    size = 16  # staged as an xdrg_bytes_ref
+    align = 8
+
+    def __init__(self, name, why):
+        self.name, self.why = name, why
+
+    def emit(self, ctx, noff, depth, path):
+        raise XdrcError(f"{self.name}: {self.why}")
+
+
+def _Recursive(name):
+    return _Unsupported(name, "recursive type: no flat device plan (the reference marshals it "
+                              "with unbounded recursion)")
+
+
+class Spec:
+    """The resolved contents of a .x file."""
+
+    def __init__(self, defs, literals, validate_enums=()):
+        self.consts: dict[str, int] = {"TRUE": 1, "FALSE": 0}
+        self.types: dict[str, XdrType] = {}
+        self.programs: list[ProgDef] = []
+        self.literals = literals
+        self._validate = set(validate_enums)
+        self._ast: dict[str, tuple] = {}
+        self._busy: set[str] = set()
+        order = []
+        for d in defs:
+            if d[0] == "const":
+                self.consts[d[1]] = self._val(d[2])
+            elif d[0] == "enum":
+                self.types[d[1].id] = self._enum(d[1])  # tags are constants from here on
+            elif d[0] in ("struct", "union", "typedef"):
+                self._ast[d[1].id] = d
+                order.append(d[1].id)
+            elif d[0] == "program":
+                self.programs.append(d[1])
+        for name in order:
+            self._resolve(name)
+
+    def _resolve(self, name: str) -> XdrType:
+        if name in self.types:
+            return self.types[name]
+        if name in self._busy:
+            return _Recursive(name)  # a self-referential type (e.g. a linked list)
+        kind, d = self._ast[name]
+        self._busy.add(name)
+        try:
+            t = self._struct(d) if kind == "struct" else self._union(d) if kind == "union" \
+                else self._decl_type(d)
+        finally:
+            self._busy.discard(name)
+        self.types[name] = t
+        return t
+
+    def _val(self, v) -> int:
+        if isinstance(v, int):
+            return v
+        try:
+            return int(v, 0)
+        except ValueError:
+            pass
+        n = _local(v)
+        if n in self.consts:
+            return self.consts[n]
+        raise XdrcError(f"unknown constant {v!r}")
+
+    def _enum(self, e: EnumDef) -> Enum:
+        tags, nxt = {}, 0
+        for name, val in e.tags:
+            v = self._val(val) if val is not None else nxt
+            tags[name] = v
+            self.consts[name] = v
+            nxt = v + 1
+        return Enum(e.id, tags, validate=e.id in self._validate)
+
+    def _named(self, n: str) -> XdrType:
+        ln = _local(n)
+        if ln in _BASE:
+            return _BASE[ln]
+        if n == "quadruple":
+            raise XdrcError("quadruple is not supported (no xdr_traits in xdrpp)")
+        if ln in self.types:
+            return self.types[ln]
+        if ln in self._ast:
+            return self._resolve(ln)
+        raise XdrcError(f"unknown type {n!r}")
+
+    def _spec(self, ts, field_id: str) -> XdrType:
+        anon = f"_{field_id}_t"  # xdrc/xdrc.cc:47
+        if isinstance(ts, EnumDef):
+            return self._enum(EnumDef(anon, ts.tags))
+        if isinstance(ts, StructDef):
+            return self._struct(StructDef(anon, ts.decls))
+        if isinstance(ts, UnionDef):
+            return self._union(UnionDef(anon, ts.tag_type, ts.tag_id, ts.arms))
+        return self._named(ts)
+
+    def _decl_type(self, d: Decl) -> XdrType:
+        if d.type == "opaque":
+            if d.qual == "array":
+                return OpaqueArray(self._val(d.bound))
+            return Opaque(self._val(d.bound))
+        if d.type == "string":
+            return String(self._val(d.bound))
+        t = self._spec(d.type, d.id)
+        try:
+            if d.qual == "array":
+                return XArray(t, self._val(d.bound))
+            if d.qual == "vec":
+                return XVector(t, self._val(d.bound))
+            if d.qual == "ptr":
+                return Pointer(t)
+        except NotImplementedError as e:
+            return _Unsupported(d.id, str(e))
+        return t
+
+    def _struct(self, s: StructDef) -> Struct:
+        return Struct(s.id, [(d.id, self._decl_type(d)) for d in s.decls])
+
+    def _union(self, u: UnionDef) -> Union:
+        tag_t = self._named(u.tag_type) if isinstance(u.tag_type, str) else self._spec(u.tag_type, u.tag_id)
+        arms, default = [], None
+        for cases, d in u.arms:
+            t = Void if d is None else self._decl_type(d)
+            fname = "" if d is None else d.id
+            vals = [self._val(c) for c in cases if c is not None]
+            if vals:
+                arms.append((vals, fname, t))
+            if any(c is None for c in cases):
+                default = (fname, t)
+        return Union(u.id, u.tag_id, tag_t, arms, default=default)
+
+    # ------------------------------------------------------------ outputs
+    def plan(self, name: str) -> CompiledPlan:
+        return compile_plan(self.types[name])
+
+    def proc_table(self) -> np.ndarray:
+        """Every procedure of every program/version, sorted, as the table
+        xdrg_rpc_dispatch takes (rpc.proc_table)."""
+        from . import rpc as R
+        svc: dict[int, dict[int, list[int]]] = {}
+        for p in self.programs:
+            for v in p.vers:
+                svc.setdefault(p.val, {})[v.val] = [q.val for q in v.procs]
+        return R.proc_table(svc)
+
+
+def load(text: str, validate_enums=()) -> Spec:
+    """Parse .x source.  ``validate_enums``: enum names that opt in to
+    xdr_validate_enum (xdrpp/types.h:157-173)."""
+    _, lits = _strip(text)
+    return Spec(_Parser(tokenize(text)).file(), lits, validate_enums)
+
+
+def load_file(path: str, validate_enums=()) -> Spec:
+    with open(path) as f:
+        return load(f.read(), validate_enums)
+
+
+# ---------------------------------------------------------- C back end
+def _c_ident(name: str) -> str:
+    return re.sub(r"[^A-Za-z0-9_]", "_", name)
+
+
+def emit_plan_header(spec: Spec, names=None, guard: str = "XDRG_EMITTED_PLANS_H") -> str:
+    """A C header holding, per type, the plan xdrg_plan_create takes: the
+    op array, the shared table, the native stride, the fixed wire size, the
+    bad-discriminant message of every union op, and a create function."""
+    names = list(names) if names else [n for n, t in spec.types.items()
+                                       if isinstance(t, (Struct, Union))]
+    out = [f"/* Generated by xdrpp_amd.xdrc (plan back end) -- do not edit. */",
+           f"#ifndef {guard}", f"#define {guard} 1", '#include "xdrgpu.h"', ""]
+    for n in names:
+        cp = spec.plan(n)
+        c = _c_ident(n)
+        out.append(f"/* {n}: {len(cp.ops)} ops, stride {cp.stride}, "
+                   f"{'fixed ' + str(cp.fixed_size) + ' wire bytes' if cp.fixed_size is not None else 'variable length'} */")
+        out.append(f"static const xdrg_op xdrg_plan_{c}_ops[{len(cp.ops)}] = {{")
+        for o in cp.ops:
+            out.append("  {%d, %d, %d, %du, %du, %du, %du, %du, %du, %du}," % (
+                o["kind"], o["flags"], o["depth"], o["noff"], o["arg0"], o["arg1"], o["arg2"],
+                o["arg3"], o["arg4"], o["name"]))
+        out.append("};")
+        tab = [int(x) for x in cp.table] or [0]
+        out.append(f"static const uint32_t xdrg_plan_{c}_table[{len(tab)}] = {{")
+        for i in range(0, len(tab), 8):
+            out.append("  " + ", ".join(f"{v}u" for v in tab[i:i + 8]) + ",")
+        out.append("};")
+        out.append(f"#define XDRG_PLAN_{c.upper()}_NOPS {len(cp.ops)}u")
+        out.append(f"#define XDRG_PLAN_{c.upper()}_NTABLE {len(cp.table)}u")
+        out.append(f"#define XDRG_PLAN_{c.upper()}_STRIDE {cp.stride}u")
+        out.append(f"#define XDRG_PLAN_{c.upper()}_FIXED_SIZE {cp.fixed_size or 0}u")
+        msgs = sorted(cp.messages.items())
+        if msgs:
+            out.append(f"static const struct {{ uint32_t op; const char *what; }} "
+                       f"xdrg_plan_{c}_union_msgs[{len(msgs)}] = {{")
+            for op, m in msgs:
+                out.append(f'  {{{op}u, "{m}"}},')
+            out.append("};")
+        out.append(f"static inline int xdrg_plan_create_{c}(xdrg_plan **out) {{")
+        out.append(f"  return xdrg_plan_create(xdrg_plan_{c}_ops, XDRG_PLAN_{c.upper()}_NOPS, "
+                   f"xdrg_plan_{c}_table, XDRG_PLAN_{c.upper()}_NTABLE, "
+                   f"XDRG_PLAN_{c.upper()}_STRIDE, out);")
+        out.append("}")
+        out.append("")
+    procs = spec.proc_table() if spec.programs else None
+    if procs is not None and len(procs):
+        out.append(f"static const xdrg_rpc_proc xdrg_emitted_procs[{len(procs)}] = {{")
+        for r in procs:
+            out.append("  {%du, %du, %du, %du}," % tuple(int(x) for x in r))
+        out.append("};")
+        out.append(f"#define XDRG_EMITTED_NPROCS {len(procs)}u")
+    out.append(f"#endif /* {guard} */")
+    return "\n".join(out) + "\n"
+
+
+def main(argv=None) -> int:
+    import argparse
+    ap = argparse.ArgumentParser(prog="python -m xdrpp_amd.xdrc")
+    ap.add_argument("x")
+    ap.add_argument("-o", "--output", default="-")
+    ap.add_argument("types", nargs="*")
+    a = ap.parse_intermixed_args(argv)
+    spec = load_file(a.x)
+    text = emit_plan_header(spec, a.types or None)
+    if a.output == "-":
+        sys.stdout.write(text)
+    else:
+        with open(a.output, "w") as f:
+            f.write(text)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
