@@ -44,6 +44,7 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <tuple>
 #include <type_traits>
 #include <utility>
 #include <vector>
@@ -814,6 +815,248 @@ void from_opaque_batch(const void *bytes, std::size_t len, T *out, std::size_t n
   detail::abicheck(xdrg_status_read(d_st.p, s, &e), "xdrg_status_read");
   if (e.code) P.raise(e);
   unstage(nat.data(), heap.data(), n, out);
+}
+
+// ---------------------------------------------------- record-marked messages
+namespace detail {
+// Device encode of n staged records as n record-marked messages.  Returns
+// the stream and fills off[n+1] (mark of each message, then the total).
+template <typename T>
+std::vector<std::uint8_t> encode_msgs(const T *recs, std::size_t n, std::vector<std::uint64_t> &off,
+                                      hipStream_t s) {
+  const batch_plan<T> &P = plan_for<T>();
+  staged_batch b = stage(recs, n);
+  dev_buf<std::uint8_t> d_nat(b.native.size()), d_heap(b.heap.size());
+  dev_buf<xdrg_status> d_st(1);
+  hipcheck(hipMemcpyAsync(d_nat.p, b.native.data(), b.native.size(), hipMemcpyHostToDevice, s), "H2D");
+  if (!b.heap.empty())
+    hipcheck(hipMemcpyAsync(d_heap.p, b.heap.data(), b.heap.size(), hipMemcpyHostToDevice, s), "H2D");
+  abicheck(xdrg_status_init(d_st.p, s), "xdrg_status_init");
+  std::size_t total = (std::size_t(P.fixed_size()) + 4) * n;
+  if (!P.fixed()) {  // size pass for the capacity: xdr_argpack_size + the marks
+    dev_buf<std::uint32_t> d_sz(n);
+    abicheck(xdrg_serial_sizes(P.handle(), d_nat.p, n, d_sz.p, marshaling_stack_limit, d_st.p, s),
+             "xdrg_serial_sizes");
+    std::vector<std::uint32_t> sz(n);
+    if (n) hipcheck(hipMemcpyAsync(sz.data(), d_sz.p, n * 4, hipMemcpyDeviceToHost, s), "D2H");
+    xdrg_error e{};
+    abicheck(xdrg_status_read(d_st.p, s, &e), "xdrg_status_read");
+    if (e.code) P.raise(e);
+    total = 4 * n;
+    for (auto v : sz) total += v;
+  }
+  const std::size_t ws_bytes = xdrg_workspace_size(P.handle(), n);
+  dev_buf<std::uint8_t> ws(ws_bytes), d_out(total);
+  dev_buf<std::uint64_t> d_off(n + 1);
+  abicheck(xdrg_encode_msgs(P.handle(), d_nat.p, n, b.heap.empty() ? nullptr : d_heap.p,
+                            b.heap.size(), d_out.p, total, d_off.p, marshaling_stack_limit, ws.p,
+                            ws_bytes, d_st.p, s),
+           "xdrg_encode_msgs");
+  std::vector<std::uint8_t> out(total);
+  off.assign(n + 1, 0);
+  if (total) hipcheck(hipMemcpyAsync(out.data(), d_out.p, total, hipMemcpyDeviceToHost, s), "D2H");
+  hipcheck(hipMemcpyAsync(off.data(), d_off.p, (n + 1) * 8, hipMemcpyDeviceToHost, s), "D2H");
+  xdrg_error e{};
+  abicheck(xdrg_status_read(d_st.p, s, &e), "xdrg_status_read");
+  if (e.code) P.raise(e);
+  return out;
+}
+
+// Device decode of the n messages of a stream indexed by off[n+1].
+template <typename T>
+void decode_msgs(const std::uint8_t *x, std::size_t len, const std::vector<std::uint64_t> &off,
+                 T *out, std::size_t n, hipStream_t s) {
+  const batch_plan<T> &P = plan_for<T>();
+  dev_buf<std::uint8_t> d_x(len), d_nat(n * P.stride());
+  dev_buf<std::uint64_t> d_off(n + 1);
+  dev_buf<xdrg_status> d_st(1);
+  if (len) hipcheck(hipMemcpyAsync(d_x.p, x, len, hipMemcpyHostToDevice, s), "H2D");
+  hipcheck(hipMemcpyAsync(d_off.p, off.data(), (n + 1) * 8, hipMemcpyHostToDevice, s), "H2D");
+  abicheck(xdrg_status_init(d_st.p, s), "xdrg_status_init");
+  const std::uint64_t hcap = P.fixed() ? 0 : xdrg_decode_heap_size(P.handle(), len);
+  dev_buf<std::uint8_t> d_heap(hcap);
+  const std::size_t ws_bytes = xdrg_workspace_size(P.handle(), n);
+  dev_buf<std::uint8_t> ws(ws_bytes);
+  abicheck(xdrg_decode_msgs(P.handle(), d_x.p, len, d_off.p, n, d_nat.p, d_heap.p, hcap,
+                            marshaling_stack_limit, ws.p, ws_bytes, d_st.p, s),
+           "xdrg_decode_msgs");
+  std::vector<std::uint8_t> nat(n * P.stride()), heap(hcap);
+  if (!nat.empty())
+    hipcheck(hipMemcpyAsync(nat.data(), d_nat.p, nat.size(), hipMemcpyDeviceToHost, s), "D2H");
+  if (!heap.empty())
+    hipcheck(hipMemcpyAsync(heap.data(), d_heap.p, heap.size(), hipMemcpyDeviceToHost, s), "D2H");
+  xdrg_error e{};
+  abicheck(xdrg_status_read(d_st.p, s, &e), "xdrg_status_read");
+  if (e.code) P.raise(e);
+  unstage(nat.data(), heap.data(), n, out);
+}
+
+// The raw bytes (mark + body) of a vector of messages, back to back.
+inline std::vector<std::uint8_t> concat(const std::vector<msg_ptr> &msgs,
+                                        std::vector<std::uint64_t> &off) {
+  off.assign(msgs.size() + 1, 0);
+  for (std::size_t i = 0; i < msgs.size(); ++i) off[i + 1] = off[i] + msgs[i]->raw_size();
+  std::vector<std::uint8_t> x(off.back());
+  for (std::size_t i = 0; i < msgs.size(); ++i)
+    std::memcpy(x.data() + off[i], msgs[i]->raw_data(), msgs[i]->raw_size());
+  return x;
+}
+}  // namespace detail
+
+//! xdr::xdr_to_msg(recs[i]) for every record (marshal.h:252-260) in one
+//! device pass: the messages back to back, as msg_sock::output writes a
+//! queue of them (msgsock.cc:158-188).
+template <typename T>
+std::vector<std::uint8_t> to_msg_stream(const T *recs, std::size_t n, hipStream_t s = nullptr) {
+  std::vector<std::uint64_t> off;
+  return detail::encode_msgs(recs, n, off, s);
+}
+
+//! The same messages, one message_t per record: msgs[i] holds the bytes
+//! xdr::xdr_to_msg(recs[i]) produces (message_t::alloc, marshal.cc:15-31).
+template <typename T>
+std::vector<msg_ptr> to_msg_batch(const T *recs, std::size_t n, hipStream_t s = nullptr) {
+  std::vector<std::uint64_t> off;
+  const std::vector<std::uint8_t> x = detail::encode_msgs(recs, n, off, s);
+  std::vector<msg_ptr> out;
+  out.reserve(n);
+  for (std::size_t i = 0; i < n; ++i) {
+    msg_ptr m = message_t::alloc(off[i + 1] - off[i] - 4);
+    std::memcpy(m->data(), x.data() + off[i] + 4, m->size());
+    out.push_back(std::move(m));
+  }
+  return out;
+}
+
+//! xdr::xdr_from_msg(msgs[i], out[i]) for every message (marshal.h:278-284);
+//! the first failing message raises the reference's exception.
+template <typename T>
+void from_msg_batch(const std::vector<msg_ptr> &msgs, T *out, hipStream_t s = nullptr) {
+  std::vector<std::uint64_t> off;
+  const std::vector<std::uint8_t> x = detail::concat(msgs, off);
+  detail::decode_msgs(x.data(), x.size(), off, out, msgs.size(), s);
+}
+
+//! Every message of a stream of record-marked messages, decoded: the
+//! framing of read_message / msg_sock::input (srpc.cc:29-55,
+//! msgsock.cc:38-119) applied on the device (xdrg_index_msgs), then
+//! xdr_from_msg per message.  A framing error raises xdr_bad_message_size.
+template <typename T>
+std::vector<T> from_msg_stream(const void *bytes, std::size_t len,
+                               std::uint32_t max_msg_len = XDRG_INDEX_MAX_MSG,
+                               hipStream_t s = nullptr) {
+  const auto *x = static_cast<const std::uint8_t *>(bytes);
+  const std::uint64_t max_msgs = len / 4;
+  detail::dev_buf<std::uint8_t> d_x(len);
+  detail::dev_buf<std::uint64_t> d_off(max_msgs + 1), d_cnt(1);
+  detail::dev_buf<xdrg_status> d_st(1);
+  const std::size_t ws_bytes = xdrg_index_workspace_size(len, max_msg_len);
+  detail::dev_buf<std::uint8_t> ws(ws_bytes);
+  if (len) detail::hipcheck(hipMemcpyAsync(d_x.p, x, len, hipMemcpyHostToDevice, s), "H2D");
+  detail::abicheck(xdrg_status_init(d_st.p, s), "xdrg_status_init");
+  detail::abicheck(xdrg_index_msgs(d_x.p, len, max_msg_len, max_msgs, d_off.p, d_cnt.p, ws.p,
+                                   ws_bytes, d_st.p, s),
+                   "xdrg_index_msgs");
+  std::uint64_t cnt = 0;
+  detail::hipcheck(hipMemcpyAsync(&cnt, d_cnt.p, 8, hipMemcpyDeviceToHost, s), "D2H");
+  xdrg_error e{};
+  detail::abicheck(xdrg_status_read(d_st.p, s, &e), "xdrg_status_read");
+  if (e.code) throw xdr_bad_message_size(xdrg_error_message(e.code));
+  std::vector<std::uint64_t> off(cnt + 1);
+  detail::hipcheck(hipMemcpy(off.data(), d_off.p, (cnt + 1) * 8, hipMemcpyDeviceToHost), "D2H");
+  std::vector<T> out(cnt);
+  detail::decode_msgs(x, len, off, out.data(), cnt, s);
+  return out;
+}
+
+// ------------------------------------------------------- RPC header batches
+//! The procedures a server has registered: rpc_server_base::servers_
+//! (server.h:218-219) with each interface's call_dispatch cases
+//! (xdrc/gen_hh.cc:757-774), as the sorted table xdrg_rpc_dispatch takes.
+class rpc_registry {
+  std::vector<xdrg_rpc_proc> t_;
+
+ public:
+  //! register_service for (prog, vers) with these procedure numbers
+  void add(std::uint32_t prog, std::uint32_t vers, const std::vector<std::uint32_t> &procs) {
+    if (procs.empty()) t_.push_back({prog, vers, 0, XDRG_RPC_PROC_IFACE_ONLY});
+    for (std::uint32_t p : procs) t_.push_back({prog, vers, p, 0});
+    std::sort(t_.begin(), t_.end(), [](const xdrg_rpc_proc &a, const xdrg_rpc_proc &b) {
+      return std::tie(a.prog, a.vers, a.proc) < std::tie(b.prog, b.vers, b.proc);
+    });
+    t_.erase(std::unique(t_.begin(), t_.end(),
+                         [](const xdrg_rpc_proc &a, const xdrg_rpc_proc &b) {
+                           return a.prog == b.prog && a.vers == b.vers && a.proc == b.proc;
+                         }),
+             t_.end());
+    if (t_.size() > XDRG_RPC_MAX_PROCS) throw std::length_error("rpc_registry: too many procedures");
+  }
+  const std::vector<xdrg_rpc_proc> &table() const { return t_; }
+};
+
+//! rpc_server_base::dispatch's header decode and routing (server.cc:78-117)
+//! for a batch of received messages, on the device.  hdrs[i].body_off and
+//! .end are rebased to offsets into msgs[i]->data(), so the arguments of a
+//! DISPATCH message decode with xdr_get(m->data() + body_off, m->end()).
+inline std::vector<xdrg_rpc_hdr> rpc_dispatch_batch(const std::vector<msg_ptr> &msgs,
+                                                    const rpc_registry &reg,
+                                                    hipStream_t s = nullptr) {
+  std::vector<std::uint64_t> off;
+  const std::vector<std::uint8_t> x = detail::concat(msgs, off);
+  const std::size_t n = msgs.size();
+  std::vector<xdrg_rpc_hdr> h(n);
+  if (!n) return h;
+  detail::dev_buf<std::uint8_t> d_x(x.size());
+  detail::dev_buf<std::uint64_t> d_off(n + 1);
+  detail::dev_buf<xdrg_rpc_proc> d_p(reg.table().size());
+  detail::dev_buf<xdrg_rpc_hdr> d_h(n);
+  detail::hipcheck(hipMemcpyAsync(d_x.p, x.data(), x.size(), hipMemcpyHostToDevice, s), "H2D");
+  detail::hipcheck(hipMemcpyAsync(d_off.p, off.data(), (n + 1) * 8, hipMemcpyHostToDevice, s), "H2D");
+  if (!reg.table().empty())
+    detail::hipcheck(hipMemcpyAsync(d_p.p, reg.table().data(), reg.table().size() * sizeof(xdrg_rpc_proc),
+                                    hipMemcpyHostToDevice, s), "H2D");
+  detail::abicheck(xdrg_rpc_dispatch(d_x.p, x.size(), d_off.p, n, d_p.p,
+                                     std::uint32_t(reg.table().size()), d_h.p, s),
+                   "xdrg_rpc_dispatch");
+  detail::hipcheck(hipMemcpyAsync(h.data(), d_h.p, n * sizeof(xdrg_rpc_hdr), hipMemcpyDeviceToHost, s), "D2H");
+  detail::hipcheck(hipStreamSynchronize(s), "sync");
+  for (std::size_t i = 0; i < n; ++i) {
+    if (!h[i].err) h[i].body_off -= off[i] + 4;
+    h[i].end -= off[i] + 4;
+  }
+  return h;
+}
+
+//! The error reply dispatch sends for each header (rpc_rpc_mismatch_msg,
+//! rpc_accepted_error_msg, rpc_prog_mismatch_msg, rpc_auth_error_msg;
+//! server.cc:8-67), or nullptr for DISPATCH and dropped messages.
+inline std::vector<msg_ptr> rpc_error_replies(const std::vector<xdrg_rpc_hdr> &h,
+                                              hipStream_t s = nullptr) {
+  const std::size_t n = h.size();
+  std::vector<msg_ptr> out(n);
+  if (!n) return out;
+  const std::size_t ws_bytes = xdrg_rpc_replies_workspace_size(n);
+  detail::dev_buf<xdrg_rpc_hdr> d_h(n);
+  detail::dev_buf<std::uint8_t> d_out(36 * n), ws(ws_bytes);
+  detail::dev_buf<std::uint64_t> d_off(n + 1);
+  detail::dev_buf<xdrg_status> d_st(1);
+  detail::hipcheck(hipMemcpyAsync(d_h.p, h.data(), n * sizeof(xdrg_rpc_hdr), hipMemcpyHostToDevice, s), "H2D");
+  detail::abicheck(xdrg_status_init(d_st.p, s), "xdrg_status_init");
+  detail::abicheck(xdrg_rpc_replies(d_h.p, n, d_out.p, 36 * n, d_off.p, ws.p, ws_bytes, d_st.p, s),
+                   "xdrg_rpc_replies");
+  std::vector<std::uint64_t> off(n + 1);
+  detail::hipcheck(hipMemcpyAsync(off.data(), d_off.p, (n + 1) * 8, hipMemcpyDeviceToHost, s), "D2H");
+  xdrg_error e{};
+  detail::abicheck(xdrg_status_read(d_st.p, s, &e), "xdrg_status_read");
+  std::vector<std::uint8_t> x(e.total_bytes);
+  if (!x.empty())
+    detail::hipcheck(hipMemcpy(x.data(), d_out.p, x.size(), hipMemcpyDeviceToHost), "D2H");
+  for (std::size_t i = 0; i < n; ++i) {
+    if (off[i + 1] == off[i]) continue;
+    out[i] = message_t::alloc(off[i + 1] - off[i] - 4);
+    std::memcpy(out[i]->data(), x.data() + off[i] + 4, out[i]->size());
+  }
+  return out;
 }
 
 }  // namespace gpu

@@ -11,9 +11,13 @@
 //   dropin_test stage         (CPU)  stage() == the reference-side staged layout,
 //                                    unstage(stage(x)) == x, index_records ==
 //                                    the reference's record offsets
-//   dropin_test gpu           (GPU)  to_opaque_batch == xdr_put stream,
+//   dropin_test gpu [golden]  (GPU)  to_opaque_batch == xdr_put stream,
 //                                    from_opaque_batch round trip, and the
-//                                    reference's exceptions on bad input
+//                                    reference's exceptions on bad input;
+//                                    to_msg_batch == xdr_to_msg per record,
+//                                    from_msg_batch / from_msg_stream back;
+//                                    rpc_dispatch_batch / rpc_error_replies
+//                                    against the reference's RPC fixtures
 #include "ref_objects.hh"
 #include "xdrpp_gpu.hh"
 
@@ -125,6 +129,98 @@ static void check_gpu(const char *name, const std::vector<T> &v) {
   xdr::opaque_vec<> one = xdr::gpu::to_opaque_batch(&v[1], 1);
   CHECK(one == xdr::xdr_to_opaque(v[1]), "%s: batch of one differs from xdr_to_opaque", name);
   std::printf("gpu %s: %zu records, %zu bytes bit-exact, round trip ok\n", name, v.size(), want.size());
+}
+
+// Record-marked messages: to_msg_batch / to_msg_stream against the
+// reference's xdr_to_msg per record; from_msg_batch / from_msg_stream back.
+template <typename T>
+static void check_msgs(const char *name, const std::vector<T> &v) {
+  std::vector<std::uint8_t> want;
+  std::vector<xdr::msg_ptr> ref;
+  for (const T &x : v) {
+    ref.push_back(xdr::xdr_to_msg(x));
+    want.insert(want.end(), ref.back()->raw_data(), ref.back()->raw_data() + ref.back()->raw_size());
+  }
+  std::vector<xdr::msg_ptr> got = xdr::gpu::to_msg_batch(v.data(), v.size());
+  bool ok = got.size() == ref.size();
+  for (std::size_t i = 0; ok && i < ref.size(); ++i)
+    ok = got[i]->raw_size() == ref[i]->raw_size() &&
+         !memcmp(got[i]->raw_data(), ref[i]->raw_data(), ref[i]->raw_size());
+  CHECK(ok, "%s: to_msg_batch differs from xdr_to_msg", name);
+  CHECK(xdr::gpu::to_msg_stream(v.data(), v.size()) == want, "%s: to_msg_stream differs", name);
+  std::vector<T> back(v.size());
+  xdr::gpu::from_msg_batch(ref, back.data());
+  std::vector<T> back2 = xdr::gpu::from_msg_stream<T>(want.data(), want.size());
+  ok = back2.size() == v.size();
+  for (std::size_t i = 0; ok && i < v.size(); ++i) ok = same(v[i], back[i]) && same(v[i], back2[i]);
+  CHECK(ok, "%s: from_msg_batch / from_msg_stream != records", name);
+  // xdr_from_msg's errors: record 3's message one word short
+  if (v.size() > 4) {
+    std::vector<xdr::msg_ptr> bad;
+    for (std::size_t i = 0; i < 5; ++i) bad.push_back(xdr::xdr_to_msg(v[i]));
+    bad[3]->shrink(bad[3]->size() - 4);
+    std::vector<T> a(1), b(5);
+    std::string rw, gw;
+    try { xdr::xdr_from_msg(bad[3], a[0]); } catch (const xdr::xdr_runtime_error &e) { rw = e.what(); }
+    try { xdr::gpu::from_msg_batch(bad, b.data()); } catch (const xdr::xdr_runtime_error &e) { gw = e.what(); }
+    CHECK(!rw.empty() && rw == gw, "%s: short message: reference \"%s\" vs gpu \"%s\"", name,
+          rw.c_str(), gw.c_str());
+  }
+  std::printf("msgs %s: %zu messages bit-exact, both decodes ok\n", name, v.size());
+}
+
+static std::vector<std::uint8_t> slurp(const std::string &path) {
+  std::ifstream f(path, std::ios::binary);
+  return std::vector<std::uint8_t>((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+}
+
+// RPC header batches: rpc_dispatch_batch / rpc_error_replies on msg_ptrs
+// against the reference-generated fixtures (tests/golden/rpccall_1024.*).
+static void check_rpc(const std::string &gold) {
+  const auto stream = slurp(gold + "/rpccall_1024.stream");
+  const auto offb = slurp(gold + "/rpccall_1024.msgoffs");
+  const auto procb = slurp(gold + "/rpc_procs.bin");
+  const auto want = slurp(gold + "/rpccall_1024.hdrs");
+  const auto wrep = slurp(gold + "/rpccall_1024.replies");
+  CHECK(!stream.empty() && !want.empty(), "rpc fixtures missing under %s", gold.c_str());
+  if (stream.empty() || want.empty()) return;
+  const auto *off = reinterpret_cast<const std::uint64_t *>(offb.data());
+  const std::size_t n = offb.size() / 8 - 1;
+  std::vector<xdr::msg_ptr> msgs;
+  for (std::size_t i = 0; i < n; ++i) {
+    xdr::msg_ptr m = xdr::message_t::alloc(off[i + 1] - off[i] - 4);
+    memcpy(m->data(), stream.data() + off[i] + 4, m->size());
+    msgs.push_back(std::move(m));
+  }
+  xdr::gpu::rpc_registry reg;
+  const auto *pt = reinterpret_cast<const xdrg_rpc_proc *>(procb.data());
+  for (std::size_t i = 0; i < procb.size() / sizeof(xdrg_rpc_proc); ++i)
+    reg.add(pt[i].prog, pt[i].vers,
+            pt[i].flags & XDRG_RPC_PROC_IFACE_ONLY ? std::vector<std::uint32_t>{}
+                                                   : std::vector<std::uint32_t>{pt[i].proc});
+  CHECK(reg.table().size() == procb.size() / sizeof(xdrg_rpc_proc), "rpc registry size");
+  std::vector<xdrg_rpc_hdr> h = xdr::gpu::rpc_dispatch_batch(msgs, reg);
+  const auto *w = reinterpret_cast<const xdrg_rpc_hdr *>(want.data());
+  bool ok = true;
+  for (std::size_t i = 0; i < n; ++i) {
+    xdrg_rpc_hdr g = h[i];
+    if (!g.err) g.body_off += off[i] + 4;  // back to stream offsets
+    g.end += off[i] + 4;
+    ok = ok && !memcmp(&g, &w[i], sizeof g);
+  }
+  CHECK(ok, "rpc_dispatch_batch differs from the reference's routing");
+  std::vector<xdr::msg_ptr> rep = xdr::gpu::rpc_error_replies(h);
+  std::vector<std::uint8_t> cat;
+  for (const auto &m : rep)
+    if (m) cat.insert(cat.end(), m->raw_data(), m->raw_data() + m->raw_size());
+  CHECK(cat == wrep, "rpc_error_replies differ from server.cc's replies");
+  // a DISPATCH message's arguments decode from data() + body_off
+  for (std::size_t i = 0; i < n; ++i)
+    if (h[i].action == XDRG_RPC_DISPATCH) {
+      CHECK(h[i].body_off <= h[i].end && h[i].end == msgs[i]->size(), "rpc body offsets");
+      break;
+    }
+  std::printf("rpc: %zu headers routed, %zu reply bytes bit-exact\n", n, cat.size());
 }
 
 // Run `f`; return the exception's class name and what(), as the reference would.
@@ -250,6 +346,12 @@ int main(int argc, char **argv) {
     check_gpu("rpc", rp);
     check_gpu("vecrec", vr);
     gpu_errors();
+    check_msgs("numerics", nu);
+    check_msgs("rec128", rc);
+    check_msgs("recvar", rv);
+    check_msgs("rpc", rp);
+    check_msgs("vecrec", vr);
+    check_rpc(argc > 2 ? argv[2] : "tests/golden");
   } else {
     std::fprintf(stderr, "usage: dropin_test plans <dir> | stage | gpu\n");
     return 2;

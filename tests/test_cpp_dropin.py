@@ -68,6 +68,6 @@ def test_recorded_plan_equals_compiled_plan(tmp_path, name):
 
 @pytest.mark.gpu
 def test_cpp_dropin_on_gpu():
-    r = run("gpu", timeout=600)
+    r = run("gpu", os.path.join(ROOT, "tests", "golden"), timeout=600)
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
