@@ -20,6 +20,7 @@ from xdrpp_amd import marshal as M  # noqa: E402
 from xdrpp_amd import schemas as S  # noqa: E402
 from xdrpp_amd import workloads as W  # noqa: E402
 import oracle_bridge as O  # noqa: E402
+from xdrpp_amd.xdr_types import compile_plan  # noqa: E402
 
 SCHEMAS = ["numerics", "rec128", "recvar", "rpc", "vecrec"]
 _plans = {}
@@ -416,3 +417,53 @@ def test_record_depths_full_size(dev, name, n):
     nat, _ = W.GENERATORS[name](n)
     got = M.Marshaler(p, dev).record_depths(to_dev(nat, dev), n).cpu().numpy().view(np.uint32)
     assert np.array_equal(got, O.depths(p.cp, nat, n))
+
+
+# ------------------------------------- fixed non-identity paths (group / LDS)
+FIXED_PATHS = {"auto": 0, "lds": 2}
+BOOLS = S.Struct("boolrec", [("a", S.Bool), ("b", S.Bool), ("c", S.Int), ("d", S.Bool)])
+
+
+@pytest.fixture(params=list(FIXED_PATHS))
+def fixed_path(request):
+    import ctypes as C
+    L = A.lib()
+    L.xdrg__force_fixed_path.argtypes = [C.c_int]
+    L.xdrg__force_fixed_path(FIXED_PATHS[request.param])
+    yield request.param
+    L.xdrg__force_fixed_path(0)
+
+
+@pytest.mark.parametrize("n", [1, 3, 4, 5, 1000, 4099, 1 << 16])
+def test_fixed_group_numerics(dev, fixed_path, n):
+    """numerics (56-byte native, 44-byte wire): full groups of 4 records on
+    the group kernel, the tail on the LDS kernel; both paths bit-exact."""
+    p = plan("numerics")
+    nat, _ = W.numerics(n)
+    want, _ = O.encode(p.cp, nat, n)
+    mar = M.Marshaler(p, dev)
+    res = mar.encode(to_dev(nat, dev), n)
+    assert np.array_equal(res.xdr.cpu().numpy(), want)
+    back, _ = mar.decode(res.xdr, n)
+    assert np.array_equal(back.cpu().numpy(), nat)
+
+
+@pytest.mark.parametrize("n", [1, 4, 7, 4096, 10001])
+def test_fixed_group_bools(dev, fixed_path, n):
+    """Several bools per native word (decode: 2 terms per word) and a bool
+    in the record's last word (encode: the window's high word)."""
+    cp = compile_plan(BOOLS)
+    p = M.Plan(BOOLS)
+    rng = np.random.default_rng(n)
+    nat = rng.integers(0, 256, size=n * cp.stride, dtype=np.uint8)
+    want, _ = O.encode(cp, nat, n)
+    mar = M.Marshaler(p, dev)
+    res = mar.encode(to_dev(nat, dev), n)
+    assert np.array_equal(res.xdr.cpu().numpy(), want)
+    # decode arbitrary nonzero wire bools (xdr_traits<bool>: nonzero is true)
+    wire = want.view("<u4").copy().reshape(n, 4)
+    wire[:, [0, 1, 3]] = rng.integers(0, 3, size=(n, 3)).astype(">u4").view("<u4")
+    wire = wire.reshape(-1).view(np.uint8)
+    o_nat, _ = O.decode(cp, wire, n, None)
+    back, _ = mar.decode(to_dev(wire, dev), n)
+    assert np.array_equal(back.cpu().numpy(), o_nat)

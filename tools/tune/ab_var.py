@@ -40,7 +40,7 @@ for schema in sys.argv[1:] or ["recvar", "rpc"]:
     xdr = torch.empty(total, dtype=torch.uint8, device=dev)
     offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
     back = torch.empty_like(nat)
-    hout = torch.empty(total, dtype=torch.uint8, device=dev)
+    hout = torch.empty(plan.decode_heap_bytes(total), dtype=torch.uint8, device=dev)
     ref = None
     s = torch.cuda.current_stream().cuda_stream
     times = {v: ([], []) for v in VARIANTS}

@@ -197,5 +197,75 @@ __global__ __launch_bounds__(256) void k_fixed_lds(
 }
 
 
+// ----------------------------------------------------------- fixed: group
+// Non-identity fixed layouts (numerics: 56-byte native, 44-byte wire).  G
+// records form a group whose input and output are whole 16-byte chunks; a
+// lane owns output chunk position q of every group it visits (the grid
+// stride is a multiple of the chunks per group), keeps its 4 x KT term
+// program in registers, reads its terms' 8-byte windows straight from
+// global memory (4-byte aligned dwordx2 loads; the wave's loads cover a
+// contiguous stretch, so they coalesce in L1/L2), and stores one 16-byte
+// chunk.  U chunks in flight per lane.  Full groups only; the host runs the
+// tail (< G records) through k_fixed_lds.
+typedef uint32_t u32x2a __attribute__((ext_vector_type(2), aligned(4)));
+
+template <int KT, int U, bool NT = false>
+__global__ __launch_bounds__(256) void k_fixed_grp(const uint8_t *__restrict__ in,
+                                                   u32x4 *__restrict__ out, uint64_t nchunks,
+                                                   uint32_t C, uint32_t in_g,
+                                                   const grp_term *__restrict__ prog) {
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  const uint64_t c0 = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const uint32_t q = static_cast<uint32_t>(c0 % C);
+  const uint64_t gstep = stride / C;
+  uint32_t off[4][KT], sel[4][KT];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int k = 0; k < KT; ++k) {
+      const grp_term t = prog[(q * 4u + i) * KT + k];
+      off[i][k] = t.off;
+      sel[i][k] = t.sel;
+    }
+  uint64_t g = c0 / C;
+  for (uint64_t c = c0; c < nchunks; c += U * stride, g += U * gstep) {
+    u32x2a w[U][4][KT];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint8_t *base = in + (g + u * gstep) * in_g;
+      if (c + u * stride < nchunks) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int k = 0; k < KT; ++k)
+            w[u][i][k] = *reinterpret_cast<const u32x2a *>(base + off[i][k]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t cc = c + u * stride;
+      if (cc < nchunks) {
+        uint32_t o[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          uint32_t v = 0;
+#pragma unroll
+          for (int k = 0; k < KT; ++k) {
+            const uint32_t s = sel[i][k];
+            const u32x2a x = w[u][i][k];
+            if (s & kGrpBool)
+              v |= bool_term((s & kGrpHi) ? x.y : x.x, s & 0xffffffu);
+            else
+              v |= perm(x.y, x.x, s);
+          }
+          o[i] = v;
+        }
+        const u32x4 ov = u32x4{o[0], o[1], o[2], o[3]};
+        if (NT) __builtin_nontemporal_store(ov, out + cc); else out[cc] = ov;
+      }
+    }
+  }
+}
+
 }  // namespace dev
 }  // namespace xdrg

@@ -42,6 +42,43 @@ uint32_t native_size(const xdrg_op &op) {
 // Build a byte-permutation program: out word w takes bytes from the input
 // record per `src[4w + i]` (input byte index, kNone for zero, or a bool
 // marker).  `prefer_pair` asks for window base (w & ~1) when possible.
+// Group path (see plan.h grp_term): G = the fewest records whose input and
+// output are both whole 16-byte chunks.  Terms keep their 8-byte windows
+// inside the record, so a group's loads stay inside its G records.
+void build_group(fixed_prog &pg) {
+  pg.grp_G = pg.grp_C = pg.grp_KT = 0;
+  pg.grp.clear();
+  const uint32_t ib = 4 * pg.in_words, ob = 4 * pg.out_words;
+  if (pg.in_words < 2 || pg.out_words == 0) return;
+  uint32_t kt = 0;
+  for (const term_idx &x : pg.idx) kt = std::max<uint32_t>(kt, x.count);
+  if (kt == 0 || kt > 4) return;
+  kt = kt <= 1 ? 1 : kt <= 2 ? 2 : 4;
+  uint32_t G = 1;
+  while ((G * ib) % 16 || (G * ob) % 16) ++G;  // G <= 4
+  const uint32_t C = G * ob / 16;
+  if (C > 1024) return;
+  pg.grp.assign(size_t(C) * 4 * kt, grp_term{0, 0x0C0C0C0Cu});
+  for (uint32_t c = 0; c < C; ++c)
+    for (uint32_t i = 0; i < 4; ++i) {
+      const uint32_t wg = 4 * c + i, r = wg / pg.out_words, j = wg % pg.out_words;
+      const term_idx x = pg.idx[j];
+      for (uint32_t q = 0; q < x.count; ++q) {
+        const term &t = pg.terms[x.start + q];
+        grp_term &g = pg.grp[(size_t(c) * 4 + i) * kt + q];
+        g.off = r * ib + 4u * t.src;
+        g.sel = t.kind == T_BOOL ? (t.sel | kGrpBool) : t.sel;
+        if (t.kind == T_BOOL && t.src + 1u >= pg.in_words) {  // window ends at the record's end
+          g.off -= 4u;
+          g.sel |= kGrpHi;
+        }
+      }
+    }
+  pg.grp_G = G;
+  pg.grp_C = C;
+  pg.grp_KT = kt;
+}
+
 void build_prog(const std::vector<int> &src, uint32_t in_words, uint32_t out_words,
                 fixed_prog &pg) {
   pg.in_words = in_words;
@@ -117,6 +154,7 @@ void build_prog(const std::vector<int> &src, uint32_t in_words, uint32_t out_wor
     }
   }
   pg.reg_ok = reg_ok;
+  build_group(pg);
 }
 
 }  // namespace

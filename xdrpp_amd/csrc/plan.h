@@ -51,6 +51,20 @@ struct reg_word {
   uint32_t ck_b;
 };
 
+// Group-path program (non-identity fixed layouts, e.g. numerics): G records
+// form a group whose input and output are whole 16-byte chunks; a lane owns
+// one output chunk position q of every group it visits, and each of its 4
+// output words is the OR of KT terms, each an 8-byte window at byte `off`
+// of the group's input (4-byte aligned) picked with a v_perm selector, or a
+// bool term (sel bit 31 set; low bits as term::sel of T_BOOL).  Unused
+// terms select zero (sel 0x0C0C0C0C).
+struct grp_term {
+  uint32_t off;
+  uint32_t sel;
+};
+constexpr uint32_t kGrpBool = 0x80000000u;
+constexpr uint32_t kGrpHi = 0x40000000u;  // bool term reads the window's high word
+
 struct fixed_prog {
   uint32_t in_words;   // words per input record
   uint32_t out_words;  // words per output record
@@ -58,6 +72,10 @@ struct fixed_prog {
   std::vector<term> terms;
   bool reg_ok = false;         // eligible for the register path
   std::vector<reg_word> reg;   // [out_words] when reg_ok
+  uint32_t grp_G = 0;          // group path: records per group (0 = not eligible)
+  uint32_t grp_C = 0;          //   output chunks per group
+  uint32_t grp_KT = 0;         //   terms per output word
+  std::vector<grp_term> grp;   //   [grp_C][4][grp_KT]
   bool has_bool = false;
 };
 
@@ -94,6 +112,7 @@ struct xdrg_plan {
   const xdrg::term_idx *d_enc_idx = nullptr, *d_dec_idx = nullptr;
   const xdrg::term *d_enc_terms = nullptr, *d_dec_terms = nullptr;
   const xdrg::reg_word *d_enc_reg = nullptr, *d_dec_reg = nullptr;
+  const xdrg::grp_term *d_enc_grp = nullptr, *d_dec_grp = nullptr;
   const xdrg::check *d_checks = nullptr;
 };
 

@@ -1164,6 +1164,8 @@ __global__ __launch_bounds__(64) void k_var_encode_i(
         if (nb[u] > 4u) w[1] = x.y;
         if (nb[u] > 8u) w[2] = x.z;
         if (nb[u] > 12u) w[3] = x.w;
+      } else if (at[u] >= C && nb[u] == 16u) {
+        st16u(gout + at[u], x);  // a whole chunk past the image: one (4-aligned) 16-byte store
       } else {
         img_put(im, C, gout, at[u], x.x);
         if (nb[u] > 4u) img_put(im, C, gout, at[u] + 4, x.y);
@@ -1826,6 +1828,8 @@ constexpr uint32_t kVarLdsBudget = 64u << 10;  // wave-cooperative var kernels
 // (tools/tune A/B, tests): encode 1 = per-lane, 2 = record image,
 // 3 = chunk-map image; decode 1 = per-lane, 2 = window.
 int g_force_enc = 0, g_force_dec = 0;
+int g_fixed_path = 0;  // 0 automatic, 2 = force k_fixed_lds for non-identity fixed plans
+int g_grp_u = 0, g_grp_blocks = 0, g_grp_nt = 0;  // group-path launch overrides (tools/tune)
 uint32_t g_img_bytes = 4u << 10;   // encode LDS image per wave (tools/tune/ab_var.py)
 uint32_t g_win_bytes = 4u << 10;   // decode LDS window per wave (tools/tune/ab_var.py)
 unsigned long long *g_stamps = nullptr;      // diagnostic phase stamps, decode (tuning)
@@ -1900,6 +1904,42 @@ int run_fixed(const xdrg_plan &p, bool decode, const void *in, void *out, uint64
     return XDRG_OK;
   }
   if (!aligned(in, 4) || !aligned(out, 4)) return XDRG_EALIGN;
+  if (pg.grp_G && !checks && g_fixed_path != 2 && aligned(in, 16) && aligned(out, 16) &&
+      nrec >= pg.grp_G) {
+    // Group path over the full groups; the tail (< G records) below.
+    const uint64_t ngroups = nrec / pg.grp_G;
+    const uint64_t nchunks = ngroups * pg.grp_C;
+    const uint32_t in_g = pg.grp_G * pg.in_words * 4u;
+    const uint64_t cap = g_grp_blocks ? uint64_t(g_grp_blocks) : 2048u;
+    uint64_t blocks = std::min<uint64_t>((nchunks + 255) / 256, cap);
+    blocks = align_up(std::max<uint64_t>(blocks, 1), pg.grp_C / gcd32(pg.grp_C, 256));
+    const grp_term *prog = decode ? p.d_dec_grp : p.d_enc_grp;
+    const uint8_t *i8 = static_cast<const uint8_t *>(in);
+    u32x4 *o4 = static_cast<u32x4 *>(out);
+    // tools/tune/tune_grp.py (numerics 1M): U=4 / 2048 workgroups best, within 10 %
+    const int U = g_grp_u ? g_grp_u : (pg.grp_KT == 1 ? 4 : pg.grp_KT == 2 ? 2 : 1);
+#define LAUNCH_GRP(KT, UU)                                                                   \
+  do {                                                                                       \
+    if (g_grp_nt)                                                                            \
+      k_fixed_grp<KT, UU, true><<<blocks, 256, 0, s>>>(i8, o4, nchunks, pg.grp_C, in_g, prog); \
+    else                                                                                     \
+      k_fixed_grp<KT, UU, false><<<blocks, 256, 0, s>>>(i8, o4, nchunks, pg.grp_C, in_g, prog); \
+  } while (0)
+    if (pg.grp_KT == 1) {
+      if (U == 1) LAUNCH_GRP(1, 1); else if (U == 2) LAUNCH_GRP(1, 2); else LAUNCH_GRP(1, 4);
+    } else if (pg.grp_KT == 2) {
+      if (U == 1) LAUNCH_GRP(2, 1); else LAUNCH_GRP(2, 2);
+    } else {
+      LAUNCH_GRP(4, 1);
+    }
+#undef LAUNCH_GRP
+    HIPCHK(hipGetLastError());
+    const uint64_t done = ngroups * pg.grp_G;
+    if (done == nrec) return XDRG_OK;
+    in = static_cast<const uint8_t *>(in) + done * pg.in_words * 4u;
+    out = static_cast<uint8_t *>(out) + done * pg.out_words * 4u;
+    nrec -= done;
+  }
   const uint32_t in_words = pg.in_words, out_words = pg.out_words;
   if (in_words > 8192) return XDRG_EUNSUPPORTED;  // > 32 KiB records: tile won't fit
   uint32_t T = std::min<uint32_t>(256, std::max<uint32_t>(4, 8192 / in_words));
@@ -2162,6 +2202,12 @@ int xdrg_abi_version(void) { return XDRG_ABI_VERSION; }
 const char *xdrg_last_hip_error(void) { return g_hip_err; }
 
 // Internal A/B hooks for tools/tune and the tests (not part of include/xdrgpu.h).
+void xdrg__force_fixed_path(int path) { g_fixed_path = path; }
+void xdrg__set_fixed_grp(int u, int blocks, int nt) {
+  g_grp_u = u;
+  g_grp_blocks = blocks;
+  g_grp_nt = nt;
+}
 void xdrg__force_var_kernels(int enc, int dec) {
   g_force_enc = enc;
   g_force_dec = dec;
@@ -2202,7 +2248,7 @@ static int plan_upload(const xdrg_plan *cp) {
   std::lock_guard<std::mutex> g(p->upload_mu);
   if (p->uploaded.load(std::memory_order_relaxed)) return XDRG_OK;
   struct part { const void *src; size_t bytes; size_t off; };
-  part parts[10] = {
+  part parts[12] = {
       {p->ops.data(), p->ops.size() * sizeof(xdrg_op), 0},
       {p->table.data(), p->table.size() * 4, 0},
       {p->enc.idx.data(), p->enc.idx.size() * sizeof(term_idx), 0},
@@ -2212,6 +2258,8 @@ static int plan_upload(const xdrg_plan *cp) {
       {p->enc.reg.data(), p->enc.reg.size() * sizeof(reg_word), 0},
       {p->dec.reg.data(), p->dec.reg.size() * sizeof(reg_word), 0},
       {p->checks.data(), p->checks.size() * sizeof(check), 0},
+      {p->enc.grp.data(), p->enc.grp.size() * sizeof(grp_term), 0},
+      {p->dec.grp.data(), p->dec.grp.size() * sizeof(grp_term), 0},
       {nullptr, 16, 0}};
   size_t total = 0;
   for (part &q : parts) { q.off = total; total += align_up(q.bytes, 256); }
@@ -2234,6 +2282,8 @@ static int plan_upload(const xdrg_plan *cp) {
   p->d_enc_reg = reinterpret_cast<const reg_word *>(base + parts[6].off);
   p->d_dec_reg = reinterpret_cast<const reg_word *>(base + parts[7].off);
   p->d_checks = reinterpret_cast<const check *>(base + parts[8].off);
+  p->d_enc_grp = reinterpret_cast<const grp_term *>(base + parts[9].off);
+  p->d_dec_grp = reinterpret_cast<const grp_term *>(base + parts[10].off);
   p->uploaded.store(true, std::memory_order_release);
   return XDRG_OK;
 }
