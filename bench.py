@@ -431,7 +431,10 @@ def main():
     if plan.is_fixed:
         # dominant kernel: k_fixed_reg / k_fixed_lds (encode and decode are
         # the same kernel with the encode / decode permutation programs)
-        kern = "k_fixed_reg" if plan.path == A.PATH_FIXED_REG else "k_fixed_lds"
+        info = A.XdrgPlanInfo()
+        A.check(A.lib().xdrg_plan_get_info(plan.handle, A.C.byref(info)), "xdrg_plan_get_info")
+        kern = ("k_fixed_reg" if plan.path == A.PATH_FIXED_REG else
+                "k_fixed_grp" if info.group_records else "k_fixed_lds")
         alg_bytes = n * S_ + X  # read one side + write the other, per launch
         launches = enc_ms + dec_ms
     else:

@@ -145,6 +145,9 @@ typedef struct xdrg_plan_info {
   uint32_t has_checks;    /* decode validates something (pads, enums) */
   uint64_t max_record_bytes; /* largest wire record the plan's bounds allow
                               * (fixed: fixed_size); a message's body bound */
+  uint32_t group_records;    /* FIXED_LDS plans run by the group kernel: records
+                              * per group (0: the LDS kernel, or not fixed) */
+  uint32_t rsv;
 } xdrg_plan_info;
 
 /* ---------------------------------------------------------------------- */

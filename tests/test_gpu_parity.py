@@ -467,3 +467,31 @@ def test_fixed_group_bools(dev, fixed_path, n):
     o_nat, _ = O.decode(cp, wire, n, None)
     back, _ = mar.decode(to_dev(wire, dev), n)
     assert np.array_equal(back.cpu().numpy(), o_nat)
+
+
+# ----------------------- chunk-map encode: LDS image sizes and unroll depths
+@pytest.fixture(params=[(-1, 8), (0, 8), (1024, 4), (4096, 16)], ids=lambda v: f"img{v[0]}_u{v[1]}")
+def enc_shape(request):
+    import ctypes as C
+    L = A.lib()
+    L.xdrg__set_image_bytes.argtypes = [C.c_int]
+    L.xdrg__set_enc_unroll.argtypes = [C.c_int]
+    L.xdrg__set_image_bytes(request.param[0])
+    old = L.xdrg__set_enc_unroll(request.param[1])
+    yield request.param
+    L.xdrg__set_image_bytes(-1)
+    L.xdrg__set_enc_unroll(old)
+
+
+@pytest.mark.parametrize("name", ["recvar", "rpc", "vecrec"])
+@pytest.mark.parametrize("n", [1, 64, 1000, 4099])
+def test_encode_image_shapes(dev, enc_shape, name, n):
+    """Every stretch byte goes through the LDS image or the direct global
+    path (whole 16-byte chunks as one store); both, at every image size and
+    unroll depth, give the reference's bytes."""
+    p = plan(name)
+    nat, heap = W.GENERATORS[name](n)
+    want, offs = O.encode(p.cp, nat, n, heap)
+    res = M.Marshaler(p, dev).encode(to_dev(nat, dev), n, to_dev(heap, dev) if heap.size else None)
+    assert np.array_equal(res.xdr.cpu().numpy(), want)
+    assert np.array_equal(res.offsets.cpu().numpy().view(np.uint64), offs)

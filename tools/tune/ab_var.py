@@ -23,10 +23,16 @@ VARIANTS = [tuple(int(x) for x in v.split(",")) for v in
             os.environ.get("VARIANTS", "2,2,4096,4096 3,2,4096,4096 3,2,2048,4096 3,2,0,4096 3,2,4096,2048").split()]
 
 
+L.xdrg__set_enc_unroll.argtypes = [C.c_int]
+L.xdrg__set_dec_readahead.argtypes = [C.c_int]
+
+
 def select(v):
     L.xdrg__force_var_kernels(v[0], v[1])
     L.xdrg__set_image_bytes(v[2])
     L.xdrg__set_window_bytes(v[3])
+    L.xdrg__set_enc_unroll(v[4] if len(v) > 4 else 8)
+    L.xdrg__set_dec_readahead(v[5] if len(v) > 5 else 1)
 dev = torch.device("cuda:0")
 out = {}
 for schema in sys.argv[1:] or ["recvar", "rpc"]:
@@ -71,10 +77,10 @@ for schema in sys.argv[1:] or ["recvar", "rpc"]:
             torch.cuda.synchronize()
             times[v][0].append(ev[0].elapsed_time(ev[1]) / 5)
             times[v][1].append(ev[1].elapsed_time(ev[2]) / 5)
-    select((0, 0, 4096, 16384))
+    select((0, 0, -1, 4096, 8))
     mar.check()
     for v in VARIANTS:
-        name = f"e{v[0]}d{v[1]}_i{v[2] // 1024}K_w{v[3] // 1024}K"
+        name = f"e{v[0]}d{v[1]}_i{v[2] // 1024}K_w{v[3] // 1024}K" + (f"_u{v[4]}" if len(v) > 4 else "") + (f"_ra{v[5]}" if len(v) > 5 else "")
         e, d = float(np.median(times[v][0])), float(np.median(times[v][1]))
         out[f"{schema}_{name}"] = {"encode_ms": round(e, 4), "decode_ms": round(d, 4),
                                    "gib_s": round(2 * total / 2**30 / ((e + d) * 1e-3), 1)}

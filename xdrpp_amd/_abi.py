@@ -79,6 +79,8 @@ class XdrgPlanInfo(C.Structure):
         ("nops", C.c_uint32),
         ("has_checks", C.c_uint32),
         ("max_record_bytes", C.c_uint64),
+        ("group_records", C.c_uint32),
+        ("rsv", C.c_uint32),
     ]
 
 

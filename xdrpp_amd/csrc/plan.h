@@ -118,11 +118,12 @@ struct xdrg_plan {
 
 namespace xdrg {
 // Shared by the kernels' translation units (xdrgpu.hip, rpc.hip):
-// exclusive scan of nb u64 block sums in place, writing the total to
+// exclusive scan of nb u64 block sums (in -> out; in != out lets it run on
+// several workgroups), writing the total to
 // status->total_bytes and offsets[n] (one workgroup, stream-ordered), and
 // the thread's last-HIP-error record behind xdrg_last_hip_error.
-int launch_block_scan(unsigned long long *v, uint32_t nb, xdrg_status *status,
-                      uint64_t *offsets, uint64_t n, void *stream);
+int launch_block_scan(const unsigned long long *in, unsigned long long *out, uint32_t nb,
+                      xdrg_status *status, uint64_t *offsets, uint64_t n, void *stream);
 int record_hip_error(int hip_error, const char *what);
 
 // Validates ops and builds all host-side programs.  Returns XDRG_OK or an

@@ -368,7 +368,9 @@ __global__ __launch_bounds__(256) void k_rpc_reply_emit(
   for (uint32_t j = 0; j < k; ++j) o[j] = bswap(w[j]);
 }
 
-size_t replies_ws_bytes(uint64_t n) { return ((n + 255) / 256 + 1) * 8; }
+// block sums, then their exclusive scan
+size_t replies_ws_half(uint64_t n) { return (((n + 255) / 256 + 1) * 8 + 255) / 256 * 256; }
+size_t replies_ws_bytes(uint64_t n) { return 2 * replies_ws_half(n); }
 
 #define HIPCHK(x)                                                             \
   do {                                                                        \
@@ -434,12 +436,13 @@ int xdrg_rpc_replies(const xdrg_rpc_hdr *d_hdrs, uint64_t n, void *d_out, uint64
   const uint64_t nb = (n + 255) / 256;
   if (nb > 0xffffffffull) return XDRG_EUNSUPPORTED;
   auto *bsum = static_cast<unsigned long long *>(d_workspace);
+  auto *bbase = bsum + replies_ws_half(n) / 8;
   k_rpc_reply_sizes<<<nb, 256, 0, s>>>(d_hdrs, n, bsum);
   HIPCHK(hipGetLastError());
-  const int rc = xdrg::launch_block_scan(bsum, uint32_t(nb), d_status, d_offsets, n, stream);
+  const int rc = xdrg::launch_block_scan(bsum, bbase, uint32_t(nb), d_status, d_offsets, n, stream);
   if (rc != XDRG_OK) return rc;
   k_rpc_reply_emit<<<nb, 256, 0, s>>>(d_hdrs, n, static_cast<uint8_t *>(d_out), out_capacity,
-                                      d_offsets, bsum,
+                                      d_offsets, bbase,
                                       reinterpret_cast<unsigned long long *>(&d_status->first_error));
   HIPCHK(hipGetLastError());
   return XDRG_OK;

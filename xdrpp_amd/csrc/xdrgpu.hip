@@ -379,64 +379,109 @@ __global__ __launch_bounds__(64) void k_var_size(const uint8_t *__restrict__ nat
   if (block_sums && lane == 0) block_sums[blockIdx.x] = v;
 }
 
-// Exclusive scan of nb block sums in place; writes the total.  One
-// workgroup of 16 waves; tiles of 16 x 1024 values.  Loads and stores are
-// coalesced (value k of thread t is element t0 + 1024 k + t): each of the
-// 16 rows is scanned per wave with shuffles, wave 0 scans the 256 row/wave
-// totals in (row, wave) order, and every value adds its row/wave base.
-// (A thread-contiguous layout costs a cache line per lane per load: 18 us
-// for 16K values on MI355X, against a few us for this one.)
-__global__ __launch_bounds__(1024) void k_scan_blocks(unsigned long long *__restrict__ v,
-                                                      uint32_t nb, xdrg_status *status,
-                                                      uint64_t *__restrict__ offsets, uint64_t n) {
-  constexpr uint32_t PER = 16, NT = 1024, NW = NT / 64;
-  __shared__ unsigned long long part[PER * NW];  // (row k, wave w) totals -> bases
-  __shared__ unsigned long long tile_total;
+// Exclusive scan of nb block sums in place; writes the total to
+// status->total_bytes and offsets[n].  Workgroups of 16 waves, each owning
+// tiles of 4096 values.  A tile's loads are coalesced into LDS; each thread
+// scans 4 contiguous values serially, the thread totals take one 64-bit
+// wave scan, the 16 wave totals one more pass.  With nb <= kScanMulti
+// every tile has its own workgroup, which first sums all values before its
+// tile (coalesced, all loads in flight; at most 15 x 4096 values) -- no
+// inter-workgroup communication, one memory round trip per workgroup.
+// Larger nb: one workgroup walks the tiles carrying the running total.
+// (Measured on MI355X: per-row wave scans of 16 x 1024 values took ~12 us
+// for any nb; the single-workgroup tile walk takes ~3.5 us per tile.)
+constexpr uint32_t kScanNT = 1024, kScanSub = 4, kScanTile = kScanNT * kScanSub;
+constexpr uint32_t kScanMulti = 16u * kScanTile;
+
+__device__ __forceinline__ unsigned long long scan_tile(const unsigned long long *in,
+                                                        unsigned long long *out,
+                                                        uint64_t t0, uint32_t nb,
+                                                        unsigned long long carry,
+                                                        unsigned long long *buf,
+                                                        unsigned long long *wtot) {
+  constexpr uint32_t NW = kScanNT / 64;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  unsigned long long carry = 0;
-  for (uint64_t t0 = 0; t0 < nb; t0 += static_cast<uint64_t>(NT) * PER) {
-    unsigned long long x[PER], incl[PER];
+  auto sk = [](uint32_t e) { return e + (e >> 5); };  // skew: fewer bank conflicts
 #pragma unroll
-    for (uint32_t k = 0; k < PER; ++k) {
-      const uint64_t j = t0 + static_cast<uint64_t>(k) * NT + tid;
-      x[k] = j < nb ? v[j] : 0ull;
-    }
-#pragma unroll
-    for (uint32_t k = 0; k < PER; ++k) {
-      unsigned long long a = x[k];
-      for (int o = 1; o < 64; o <<= 1) {
-        const unsigned long long y = __shfl_up(a, o, 64);
-        if (lane >= static_cast<uint32_t>(o)) a += y;
-      }
-      incl[k] = a;
-      if (lane == 63) part[k * NW + wid] = a;
-    }
-    __syncthreads();
-    if (wid == 0) {  // exclusive scan of the 256 (row, wave) totals, 4 per lane
-      unsigned long long p0 = part[4 * lane], p1 = part[4 * lane + 1], p2 = part[4 * lane + 2],
-                         p3 = part[4 * lane + 3];
-      const unsigned long long sum = p0 + p1 + p2 + p3;
-      unsigned long long a = sum;
-      for (int o = 1; o < 64; o <<= 1) {
-        const unsigned long long y = __shfl_up(a, o, 64);
-        if (lane >= static_cast<uint32_t>(o)) a += y;
-      }
-      unsigned long long b = carry + a - sum;
-      part[4 * lane] = b; b += p0;
-      part[4 * lane + 1] = b; b += p1;
-      part[4 * lane + 2] = b; b += p2;
-      part[4 * lane + 3] = b;
-      if (lane == 63) tile_total = a;
-    }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t k = 0; k < PER; ++k) {
-      const uint64_t j = t0 + static_cast<uint64_t>(k) * NT + tid;
-      if (j < nb) v[j] = part[k * NW + wid] + incl[k] - x[k];
-    }
-    carry += tile_total;
-    __syncthreads();  // part / tile_total reused by the next tile
+  for (uint32_t k = 0; k < kScanSub; ++k) {
+    const uint32_t e = k * kScanNT + tid;
+    buf[sk(e)] = t0 + e < nb ? in[t0 + e] : 0ull;
   }
+  __syncthreads();
+  unsigned long long x[kScanSub], tsum = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kScanSub; ++k) {
+    x[k] = buf[sk(kScanSub * tid + k)];
+    tsum += x[k];
+  }
+  unsigned long long incl = tsum;
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long y = __shfl_up(incl, o, 64);
+    if (lane >= static_cast<uint32_t>(o)) incl += y;
+  }
+  if (lane == 63) wtot[wid] = incl;
+  __syncthreads();
+  unsigned long long wbase = 0, all = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < NW; ++w) {
+    const unsigned long long t = wtot[w];
+    if (w < wid) wbase += t;
+    all += t;
+  }
+  unsigned long long run = carry + wbase + incl - tsum;
+#pragma unroll
+  for (uint32_t k = 0; k < kScanSub; ++k) {
+    buf[sk(kScanSub * tid + k)] = run;
+    run += x[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t k = 0; k < kScanSub; ++k) {
+    const uint32_t e = k * kScanNT + tid;
+    if (t0 + e < nb) out[t0 + e] = buf[sk(e)];
+  }
+  __syncthreads();  // buf / wtot reused by the next tile
+  return carry + all;
+}
+
+// MULTI reads `in` and writes `out` (distinct: other workgroups still read
+// `in`); the single-workgroup walk may scan in place.
+template <bool MULTI>
+__global__ __launch_bounds__(1024) void k_scan_blocks(const unsigned long long *in,
+                                                      unsigned long long *out, uint32_t nb,
+                                                      xdrg_status *status,
+                                                      uint64_t *__restrict__ offsets, uint64_t n) {
+  __shared__ unsigned long long buf[kScanTile + kScanTile / 32];
+  __shared__ unsigned long long wtot[kScanNT / 64];
+  const uint32_t tid = threadIdx.x;
+  unsigned long long carry = 0;
+  if (MULTI) {
+    // this workgroup's tile; its carry = the sum of every value before it
+    const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * kScanTile;
+    unsigned long long part = 0;
+    uint64_t j = tid;
+    for (; j + 7u * kScanNT < t0; j += 8u * kScanNT) {  // 8 loads in flight per thread
+      unsigned long long q[8];
+#pragma unroll
+      for (uint32_t k = 0; k < 8; ++k) q[k] = in[j + k * kScanNT];
+#pragma unroll
+      for (uint32_t k = 0; k < 8; ++k) part += q[k];
+    }
+    for (; j < t0; j += kScanNT) part += in[j];
+    for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+    if ((tid & 63) == 0) wtot[tid >> 6] = part;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t w = 0; w < kScanNT / 64; ++w) carry += wtot[w];
+    __syncthreads();
+    carry = scan_tile(in, out, t0, nb, carry, buf, wtot);
+    if (tid == 0 && blockIdx.x == gridDim.x - 1) {
+      status->total_bytes = carry;
+      offsets[n] = carry;
+    }
+    return;
+  }
+  for (uint64_t t0 = 0; t0 < nb; t0 += kScanTile) carry = scan_tile(in, out, t0, nb, carry, buf, wtot);
   if (tid == 0) {
     status->total_bytes = carry;
     offsets[n] = carry;
@@ -1220,7 +1265,7 @@ __host__ __device__ inline uint32_t dec_w_lds(uint32_t stride, uint32_t C) {
   return ((64u * stride + 15u) & ~15u) + C + 32u;
 }
 
-template <bool COPY>
+template <bool COPY, bool RA = true>
 __global__ __launch_bounds__(64) void k_var_decode_w(
     const uint8_t *__restrict__ xdr, uint64_t len, const uint64_t *__restrict__ offsets, uint64_t n,
     uint8_t *__restrict__ native, uint32_t stride, uint8_t *__restrict__ heap,
@@ -1293,7 +1338,16 @@ __global__ __launch_bounds__(64) void k_var_decode_w(
   wave_sync();
   XDRG_STAMP(1);
 
-  // word reader: window for stream bytes in [ws, ws + wc), global otherwise
+  // word reader: window for stream bytes in [ws, ws + wc), global otherwise.
+  // Past the window a lane keeps a 32-byte read-ahead of the stream (two
+  // aligned 16-byte chunks loaded together): consecutive fields are
+  // adjacent, so one round trip serves up to 8 words instead of 1.  The
+  // second chunk is loaded only when it holds stream bytes (an aligned
+  // chunk with a stream byte never leaves the stream's pages).
+  const uintptr_t xbase = reinterpret_cast<uintptr_t>(xdr);
+  const uintptr_t xend = xbase + len;
+  uintptr_t ra_line = ~uintptr_t(0);
+  u32x4 ra0 = u32x4{0u, 0u, 0u, 0u}, ra1 = ra0;
   auto rd = [&](uint64_t pos) -> uint32_t {
     const uint64_t rel = pos - ws;
     if (pos >= ws && rel + 4 <= wc) {
@@ -1301,7 +1355,17 @@ __global__ __launch_bounds__(64) void k_var_decode_w(
       if (((sh + rel) & 3u) == 0) return *reinterpret_cast<const uint32_t *>(q);
       return uint32_t(q[0]) | (uint32_t(q[1]) << 8) | (uint32_t(q[2]) << 16) | (uint32_t(q[3]) << 24);
     }
-    return unaligned_word(xdr, len, pos);
+    const uintptr_t ga = xbase + pos;
+    if (!RA || (ga & 3u) || pos + 4 > len) return unaligned_word(xdr, len, pos);
+    if (ga - ra_line >= 32u) {
+      ra_line = ga & ~uintptr_t(15);
+      ra0 = *reinterpret_cast<const u32x4 *>(ra_line);
+      ra1 = ra_line + 16u < xend ? *reinterpret_cast<const u32x4 *>(ra_line + 16u) : u32x4{0u, 0u, 0u, 0u};
+    }
+    const uint32_t k = static_cast<uint32_t>(ga - ra_line) >> 2;
+    const u32x4 h = k < 4u ? ra0 : ra1;
+    const uint32_t j = k & 3u;
+    return j == 0 ? h.x : j == 1 ? h.y : j == 2 ? h.z : h.w;
   };
 
   {
@@ -1830,7 +1894,10 @@ constexpr uint32_t kVarLdsBudget = 64u << 10;  // wave-cooperative var kernels
 int g_force_enc = 0, g_force_dec = 0;
 int g_fixed_path = 0;  // 0 automatic, 2 = force k_fixed_lds for non-identity fixed plans
 int g_grp_u = 0, g_grp_blocks = 0, g_grp_nt = 0;  // group-path launch overrides (tools/tune)
-uint32_t g_img_bytes = 4u << 10;   // encode LDS image per wave (tools/tune/ab_var.py)
+uint32_t g_img_bytes = 4u << 10;   // encode LDS image per wave when not automatic
+bool g_img_auto = true;            // per-plan image size (var_encode)
+int g_enc_u = 8;                   // payload chunks in flight per lane, chunk-map encode
+int g_dec_ra = 1;                  // window decode: 32-byte read-ahead past the window
 uint32_t g_win_bytes = 4u << 10;   // decode LDS window per wave (tools/tune/ab_var.py)
 unsigned long long *g_stamps = nullptr;      // diagnostic phase stamps, decode (tuning)
 unsigned long long *g_stamps_enc = nullptr;  // diagnostic phase stamps, encode (tuning)
@@ -1969,11 +2036,16 @@ int run_fixed(const xdrg_plan &p, bool decode, const void *in, void *out, uint64
   return XDRG_OK;
 }
 
-size_t var_ws_layout(uint64_t n, size_t *sizes_off, size_t *bsum_off) {
+// Var workspace: u32 sizes[n], the 64-record block sums, then their
+// exclusive scan (a separate array: the multi-workgroup scan reads the sums
+// while other workgroups write the bases).
+size_t var_ws_layout(uint64_t n, size_t *sizes_off, size_t *bsum_off, size_t *base_off = nullptr) {
   const uint64_t nb = (n + 63) / 64;  // block sums at the finest block size (64)
   *sizes_off = 0;
   *bsum_off = align_up(n * 4, 256);
-  return *bsum_off + align_up((nb + 1) * 8, 256);  // block sums / look-back flags + ticket
+  const size_t b2 = *bsum_off + align_up((nb + 1) * 8, 256);
+  if (base_off) *base_off = b2;
+  return b2 + align_up((nb + 1) * 8, 256);
 }
 
 // Heap bytes xdrg_decode needs (include/xdrgpu.h xdrg_decode_heap_size).
@@ -2006,9 +2078,14 @@ unsigned long long *err_ptr(xdrg_status *st) {
 }  // namespace
 
 namespace xdrg {
-int launch_block_scan(unsigned long long *v, uint32_t nb, xdrg_status *status, uint64_t *offsets,
-                      uint64_t n, void *stream) {
-  k_scan_blocks<<<1, 1024, 0, static_cast<hipStream_t>(stream)>>>(v, nb, status, offsets, n);
+int launch_block_scan(const unsigned long long *in, unsigned long long *out, uint32_t nb,
+                      xdrg_status *status, uint64_t *offsets, uint64_t n, void *stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (nb <= kScanMulti && in != out)
+    k_scan_blocks<true><<<(nb + kScanTile - 1) / kScanTile, 1024, 0, s>>>(in, out, nb, status,
+                                                                          offsets, n);
+  else
+    k_scan_blocks<false><<<1, 1024, 0, s>>>(in, out, nb, status, offsets, n);
   HIPCHK(hipGetLastError());
   return XDRG_OK;
 }
@@ -2031,17 +2108,25 @@ int var_encode(const xdrg_plan &P, const void *d_native, uint64_t n, const uint8
     return XDRG_OK;
   }
   size_t so, bo;
-  const size_t need = var_ws_layout(n, &so, &bo);
+  size_t bbo;
+  const size_t need = var_ws_layout(n, &so, &bo, &bbo);
   if (!d_ws || ws_bytes < need) return XDRG_ESPACE;
   uint32_t *sizes = reinterpret_cast<uint32_t *>(static_cast<char *>(d_ws) + so);
   unsigned long long *bsum = reinterpret_cast<unsigned long long *>(static_cast<char *>(d_ws) + bo);
+  unsigned long long *bbase = reinterpret_cast<unsigned long long *>(static_cast<char *>(d_ws) + bbo);
   const uint64_t max_rec = p->max_record_bytes + mark;
   // chunk-map image encode (64-record workgroups); chunk map entries are
   // u16 (lane 6 | slot 2 | chunk 8 bits)
   const uint32_t MC = static_cast<uint32_t>(std::min<uint64_t>(64ull * p->max_chunks16, 1u << 20));
-  const uint32_t Ci = static_cast<uint32_t>(std::min<uint64_t>(
-      g_img_bytes, (64ull * std::max<uint64_t>(max_rec, 16) + 15u) & ~15ull));
   const uint32_t KI = p->max_var_slots <= 1 ? 1u : p->max_var_slots <= 2 ? 2u : 4u;
+  // LDS image: tools/tune/ab_var.py (MI355X, 1M records, U=8): an 8 KiB
+  // image helps plans whose other LDS is small (recvar 0.208 -> 0.179 ms,
+  // vecrec 0.373 -> 0.305 ms); plans with a large chunk map and tile run
+  // better with no image and the occupancy it costs (rpc 0.349 -> 0.318 ms).
+  uint32_t img = g_img_bytes;
+  if (g_img_auto) img = enc_i_layout(p->stride, KI, MC, 0).total >= (12u << 10) ? 0u : (8u << 10);
+  const uint32_t Ci = static_cast<uint32_t>(std::min<uint64_t>(
+      img, (64ull * std::max<uint64_t>(max_rec, 16) + 15u) & ~15ull));
   const enc_i_lds LI = enc_i_layout(p->stride, KI, MC, Ci);
   const bool ok_I = p->max_var_slots <= 4 && p->max_slot_len <= 4096u &&
                     64ull * max_rec < (1ull << 31) && LI.total <= kVarLdsBudget &&
@@ -2061,18 +2146,24 @@ int var_encode(const xdrg_plan &P, const void *d_native, uint64_t n, const uint8
   uint8_t *xdr8 = static_cast<uint8_t *>(d_xdr);
   const uint32_t nops = uint32_t(p->ops.size());
   HIPCHK(launch_size_pass(*p, nat8, n, sizes, bsum, mark, err, s));
-  k_scan_blocks<<<1, 1024, 0, s>>>(bsum, uint32_t(nb), d_status, d_offsets, n);
-  HIPCHK(hipGetLastError());
+  if (int rc = xdrg::launch_block_scan(bsum, bbase, uint32_t(nb), d_status, d_offsets, n, s)) return rc;
   if (kern == 3) {
-#define LAUNCH_ENC_I(K)                                                                        \
-  k_var_encode_i<K, 16><<<nb, 64, LI.total, s>>>(nat8, n, p->stride, d_heap, heap_len, xdr8,  \
-                                                 cap, d_offsets, sizes, bsum, p->d_ops, nops,  \
+#define LAUNCH_ENC_IU(K, UU)                                                                   \
+  k_var_encode_i<K, UU><<<nb, 64, LI.total, s>>>(nat8, n, p->stride, d_heap, heap_len, xdr8,  \
+                                                 cap, d_offsets, sizes, bbase, p->d_ops, nops,  \
                                                  p->d_table, stack_limit, MC, Ci, mark, err,   \
                                                  g_stamps_enc)
+#define LAUNCH_ENC_I(K)                                     \
+  do {                                                      \
+    if (g_enc_u == 16) LAUNCH_ENC_IU(K, 16);                \
+    else if (g_enc_u == 8) LAUNCH_ENC_IU(K, 8);             \
+    else LAUNCH_ENC_IU(K, 4);                               \
+  } while (0)
     if (KI == 1) LAUNCH_ENC_I(1);
     else if (KI == 2) LAUNCH_ENC_I(2);
     else LAUNCH_ENC_I(4);
 #undef LAUNCH_ENC_I
+#undef LAUNCH_ENC_IU
     HIPCHK(hipGetLastError());
     return XDRG_OK;
   }
@@ -2080,7 +2171,7 @@ int var_encode(const xdrg_plan &P, const void *d_native, uint64_t n, const uint8
   if (kern == 2) {
 #define LAUNCH_ENC_C(K)                                                                        \
   k_var_encode_c<K><<<nb256, 256, EL.total, s>>>(nat8, n, p->stride, d_heap, heap_len, xdr8, cap, \
-                                              d_offsets, sizes, bsum, p->d_ops, nops,          \
+                                              d_offsets, sizes, bbase, p->d_ops, nops,          \
                                               p->d_table, stack_limit, p->max_scalar_words,   \
                                               err, g_stamps_enc)
     if (p->max_var_slots <= 1) LAUNCH_ENC_C(1);
@@ -2089,7 +2180,7 @@ int var_encode(const xdrg_plan &P, const void *d_native, uint64_t n, const uint8
 #undef LAUNCH_ENC_C
   } else {
     k_var_encode<<<nb256, 256, lds_ops, s>>>(nat8, n, p->stride, d_heap, heap_len, xdr8, cap,
-                                          d_offsets, sizes, bsum, p->d_ops, nops, p->d_table,
+                                          d_offsets, sizes, bbase, p->d_ops, nops, p->d_table,
                                           stack_limit, mark, err);
   }
   HIPCHK(hipGetLastError());
@@ -2173,14 +2264,16 @@ int var_decode(const xdrg_plan &P, const void *d_xdr, uint64_t len, const uint64
   if (kern == 0) kern = ok_W ? 2 : 1;
   if (kern == 2) {
     const uint64_t nb = (n + 63) / 64;
-    if (copy)
-      k_var_decode_w<true><<<nb, 64, lw, s>>>(xdr8, len, d_offsets, n, nat8, p->stride, d_heap_out,
-                                              p->d_ops, nops, p->d_table, stack_limit, Cw, ebase,
-                                              p->heap_factor, mark, err, g_stamps);
-    else
-      k_var_decode_w<false><<<nb, 64, lw, s>>>(xdr8, len, d_offsets, n, nat8, p->stride, d_heap_out,
-                                               p->d_ops, nops, p->d_table, stack_limit, Cw, ebase,
-                                               p->heap_factor, mark, err, g_stamps);
+#define LAUNCH_DEC_W(CP, RA)                                                                      \
+  k_var_decode_w<CP, RA><<<nb, 64, lw, s>>>(xdr8, len, d_offsets, n, nat8, p->stride, d_heap_out, \
+                                            p->d_ops, nops, p->d_table, stack_limit, Cw, ebase,   \
+                                            p->heap_factor, mark, err, g_stamps)
+    if (copy) {
+      if (g_dec_ra) LAUNCH_DEC_W(true, true); else LAUNCH_DEC_W(true, false);
+    } else {
+      if (g_dec_ra) LAUNCH_DEC_W(false, true); else LAUNCH_DEC_W(false, false);
+    }
+#undef LAUNCH_DEC_W
   } else {
     if (copy && len) HIPCHK(hipMemcpyAsync(d_heap_out, d_xdr, len, hipMemcpyDeviceToDevice, s));
     const uint64_t nb = (n + 255) / 256;
@@ -2203,6 +2296,16 @@ const char *xdrg_last_hip_error(void) { return g_hip_err; }
 
 // Internal A/B hooks for tools/tune and the tests (not part of include/xdrgpu.h).
 void xdrg__force_fixed_path(int path) { g_fixed_path = path; }
+int xdrg__set_dec_readahead(int on) {
+  const int old = g_dec_ra;
+  g_dec_ra = on ? 1 : 0;
+  return old;
+}
+int xdrg__set_enc_unroll(int u) {
+  const int old = g_enc_u;
+  if (u == 4 || u == 8 || u == 16) g_enc_u = u;
+  return old;
+}
 void xdrg__set_fixed_grp(int u, int blocks, int nt) {
   g_grp_u = u;
   g_grp_blocks = blocks;
@@ -2219,9 +2322,10 @@ int xdrg__set_window_bytes(int bytes) {
   g_win_bytes = static_cast<uint32_t>(bytes) & ~15u;
   return old;
 }
-int xdrg__set_image_bytes(int bytes) {
-  const int old = static_cast<int>(g_img_bytes);
-  g_img_bytes = static_cast<uint32_t>(bytes) & ~15u;
+int xdrg__set_image_bytes(int bytes) {  // < 0: back to the per-plan choice
+  const int old = g_img_auto ? -1 : static_cast<int>(g_img_bytes);
+  g_img_auto = bytes < 0;
+  if (bytes >= 0) g_img_bytes = static_cast<uint32_t>(bytes) & ~15u;
   return old;
 }
 
@@ -2303,6 +2407,8 @@ int xdrg_plan_get_info(const xdrg_plan *p, xdrg_plan_info *info) {
   info->nops = uint32_t(p->ops.size());
   info->has_checks = p->has_checks ? 1u : 0u;
   info->max_record_bytes = p->max_record_bytes;
+  info->group_records = p->path == XDRG_PATH_FIXED_LDS && !p->has_checks ? p->enc.grp_G : 0u;
+  info->rsv = 0;
   return XDRG_OK;
 }
 

@@ -83,6 +83,7 @@ class Plan:
         self.max_depth = info.max_depth
         self.has_checks = bool(info.has_checks)
         self.max_record_bytes = int(info.max_record_bytes)
+        self.group_records = int(info.group_records)
 
     @property
     def is_fixed(self) -> bool:
