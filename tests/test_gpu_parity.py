@@ -495,3 +495,31 @@ def test_encode_image_shapes(dev, enc_shape, name, n):
     res = M.Marshaler(p, dev).encode(to_dev(nat, dev), n, to_dev(heap, dev) if heap.size else None)
     assert np.array_equal(res.xdr.cpu().numpy(), want)
     assert np.array_equal(res.offsets.cpu().numpy().view(np.uint64), offs)
+
+
+@pytest.fixture(params=[(-1, 1), (2048, 0), (16384, 1)], ids=lambda v: f"win{v[0]}_ra{v[1]}")
+def dec_shape(request):
+    import ctypes as C
+    L = A.lib()
+    L.xdrg__set_window_bytes.argtypes = [C.c_int]
+    L.xdrg__set_dec_readahead.argtypes = [C.c_int]
+    L.xdrg__set_window_bytes(request.param[0])
+    old = L.xdrg__set_dec_readahead(request.param[1])
+    yield request.param
+    L.xdrg__set_window_bytes(-1)
+    L.xdrg__set_dec_readahead(old)
+
+
+@pytest.mark.parametrize("name", ["recvar", "rpc", "vecrec"])
+@pytest.mark.parametrize("n", [1, 64, 1000, 4099])
+def test_decode_window_shapes(dev, dec_shape, name, n):
+    """Stream words inside the LDS window, past it through the 32-byte
+    read-ahead, or past it word by word: the same records as the C
+    restatement."""
+    p = plan(name)
+    nat, heap = W.GENERATORS[name](n)
+    want, offs = O.encode(p.cp, nat, n, heap)
+    back, bheap = M.Marshaler(p, dev).decode(to_dev(want, dev), n, to_dev(offs.view(np.int64), dev))
+    o_nat, o_heap = O.decode(p.cp, want, n, offs)
+    assert np.array_equal(back.cpu().numpy(), o_nat)
+    assert np.array_equal(bheap.cpu().numpy(), o_heap)

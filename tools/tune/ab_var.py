@@ -77,7 +77,7 @@ for schema in sys.argv[1:] or ["recvar", "rpc"]:
             torch.cuda.synchronize()
             times[v][0].append(ev[0].elapsed_time(ev[1]) / 5)
             times[v][1].append(ev[1].elapsed_time(ev[2]) / 5)
-    select((0, 0, -1, 4096, 8))
+    select((0, 0, -1, -1, 8))
     mar.check()
     for v in VARIANTS:
         name = f"e{v[0]}d{v[1]}_i{v[2] // 1024}K_w{v[3] // 1024}K" + (f"_u{v[4]}" if len(v) > 4 else "") + (f"_ra{v[5]}" if len(v) > 5 else "")

@@ -50,7 +50,7 @@ for schema in sys.argv[1:] or ["recvar"]:
     back = torch.empty_like(nat)
     hout = torch.empty(total, dtype=torch.uint8, device=dev)
     L.xdrg__force_var_kernels(int(os.environ.get('VENC', '0')), int(os.environ.get('VDEC', '0')))
-    L.xdrg__set_window_bytes(int(os.environ.get('WIN', '8192')))
+    L.xdrg__set_window_bytes(int(os.environ.get('WIN', '-1')))
     mar.status.init(torch.cuda.current_stream().cuda_stream)
     nwaves = (n + 63) // 64
     se = torch.zeros(nwaves * 8, dtype=torch.int64, device=dev)

@@ -81,6 +81,27 @@ __device__ __forceinline__ uint32_t keep_mask(uint32_t nbytes) {  // nbytes in 1
   return nbytes >= 4 ? 0xffffffffu : ((1u << (8u * nbytes)) - 1u);
 }
 
+// A plan op at a wave-uniform index, read as 8 dwords through the scalar
+// cache (s_load_dwordx8) and unpacked.  Reading the struct directly makes
+// the compiler fetch the byte fields (kind, flags) with a vector
+// global_load_ubyte and wait on it: one memory round trip per op visited.
+__device__ __forceinline__ xdrg_op load_op(const xdrg_op *__restrict__ ops, uint32_t i) {
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(ops) + 8u * i;
+  const uint32_t w0 = w[0];
+  xdrg_op op;
+  op.kind = static_cast<uint8_t>(w0);
+  op.flags = static_cast<uint8_t>(w0 >> 8);
+  op.depth = static_cast<uint16_t>(w0 >> 16);
+  op.noff = w[1];
+  op.arg0 = w[2];
+  op.arg1 = w[3];
+  op.arg2 = w[4];
+  op.arg3 = w[5];
+  op.arg4 = w[6];
+  op.name = w[7];
+  return op;
+}
+
 __device__ __forceinline__ int union_target(const xdrg_op &op, const uint32_t *__restrict__ table,
                                             uint32_t d) {
   for (uint32_t i = 0; i < op.arg3; ++i)
@@ -178,7 +199,7 @@ __device__ bool enc_vector_elems(const xdrg_op *__restrict__ ops, uint32_t b0, u
   for (uint32_t i = 0; i < cnt; ++i) {
     const uint64_t eb = eoff + static_cast<uint64_t>(i) * es;
     for (uint32_t k = 0; k < nb; ++k) {
-      const xdrg_op e = ops[b0 + k];
+      const xdrg_op e = load_op(ops, b0 + k);
       if (e.depth > stack_limit) { report(err, r, b0 + k, XDRG_ERR_STACK_PUT); return false; }
       const uint32_t wb = elem_wire_bytes(e);
       if (wb > cap - min(pos, cap)) { report(err, r, b0 + k, XDRG_ERR_OVERFLOW_PUT); return false; }
@@ -222,7 +243,7 @@ __device__ bool dec_vector_elems(const xdrg_op *__restrict__ ops, const uint32_t
     if (w4) for (uint32_t z = 0; z < es; z += 4) st32(el + z, 0u);
     else for (uint32_t z = 0; z < es; ++z) el[z] = 0;
     for (uint32_t k = 0; k < nb; ++k) {
-      const xdrg_op e = ops[b0 + k];
+      const xdrg_op e = load_op(ops, b0 + k);
       if (e.depth > stack_limit) { report(err, r, b0 + k, XDRG_ERR_STACK_GET); return false; }
       const uint32_t need = e.kind == XDRG_OP_U64 ? 8u : e.kind == XDRG_OP_OPAQUE ? e.arg0 : 4u;
       if (b - p < need) { report(err, r, b0 + k, XDRG_ERR_OVERFLOW_GET); return false; }
@@ -329,13 +350,13 @@ __global__ __launch_bounds__(64) void k_var_size(const uint8_t *__restrict__ nat
   uint32_t pc = r < n ? 0u : kPcDone, bad_op = kPcDone, dmax = 0;
   for (uint32_t upc = 0; upc < nops; ++upc) {
     if (!__any(pc == upc)) continue;
-    const xdrg_op op = ops[upc];
+    const xdrg_op op = load_op(ops, upc);
     if (pc != upc) continue;
     if (DEPTH && op.kind != XDRG_OP_JUMP && op.kind != XDRG_OP_END) {
       dmax = max(dmax, static_cast<uint32_t>(op.depth));
       // a non-empty xvector / pointer enters its element's levels
       if (op.kind == XDRG_OP_VECTOR && *reinterpret_cast<const uint32_t *>(nat + op.noff + 8))
-        for (uint32_t k = 1; k <= op.arg2; ++k) dmax = max(dmax, static_cast<uint32_t>(ops[upc + k].depth));
+        for (uint32_t k = 1; k <= op.arg2; ++k) dmax = max(dmax, static_cast<uint32_t>(load_op(ops, upc + k).depth));
     }
     switch (op.kind) {
     case XDRG_OP_END: pc = kPcDone; break;
@@ -821,7 +842,7 @@ __global__ __launch_bounds__(256) void k_var_encode_c(
     bool ok = pc == 0u;
     for (uint32_t upc = 0; upc < nops; ++upc) {
       if (!__any(pc == upc)) continue;
-      const xdrg_op op = ops[upc];
+      const xdrg_op op = load_op(ops, upc);
       if (pc != upc) continue;
       if (op.kind == XDRG_OP_END) { pc = kPcDone; continue; }
       if (op.kind == XDRG_OP_JUMP) { pc = op.arg0; continue; }
@@ -1056,7 +1077,7 @@ __global__ __launch_bounds__(64) void k_var_encode_i(
     }
     for (uint32_t upc = 0; upc < nops; ++upc) {
       if (!__any(pc == upc)) continue;
-      const xdrg_op op = ops[upc];
+      const xdrg_op op = load_op(ops, upc);
       if (pc != upc) continue;
       if (op.kind == XDRG_OP_END) { pc = kPcDone; continue; }
       if (op.kind == XDRG_OP_JUMP) { pc = op.arg0; continue; }
@@ -1386,7 +1407,7 @@ __global__ __launch_bounds__(64) void k_var_decode_w(
     bool ok = pc == 0u;
     for (uint32_t upc = 0; upc < nops; ++upc) {
       if (!__any(pc == upc)) continue;
-      const xdrg_op op = ops[upc];
+      const xdrg_op op = load_op(ops, upc);
       if (pc != upc) continue;
       if (op.kind == XDRG_OP_END) { pc = kPcDone; continue; }
       if (op.kind == XDRG_OP_JUMP) { pc = op.arg0; continue; }
@@ -1898,7 +1919,8 @@ uint32_t g_img_bytes = 4u << 10;   // encode LDS image per wave when not automat
 bool g_img_auto = true;            // per-plan image size (var_encode)
 int g_enc_u = 8;                   // payload chunks in flight per lane, chunk-map encode
 int g_dec_ra = 1;                  // window decode: 32-byte read-ahead past the window
-uint32_t g_win_bytes = 4u << 10;   // decode LDS window per wave (tools/tune/ab_var.py)
+uint32_t g_win_bytes = 4u << 10;   // decode LDS window per wave when not automatic
+bool g_win_auto = true;            // per-call window size (var_decode)
 unsigned long long *g_stamps = nullptr;      // diagnostic phase stamps, decode (tuning)
 unsigned long long *g_stamps_enc = nullptr;  // diagnostic phase stamps, encode (tuning)
 
@@ -2255,8 +2277,14 @@ int var_decode(const xdrg_plan &P, const void *d_xdr, uint64_t len, const uint64
   uint8_t *nat8 = static_cast<uint8_t *>(d_native);
   const uint32_t nops = uint32_t(p->ops.size());
   const bool copy = d_heap_out != d_xdr;  // heap_out == d_xdr: zero-copy (refs into the stream)
+  // LDS window: tools/tune/ab_var.py (MI355X, 1M records): an 8 KiB window
+  // pays when it holds a wave's whole stretch (vecrec, ~6.6 KiB per 64
+  // records: 0.37 -> 0.30 ms); for longer stretches the occupancy it costs
+  // outweighs it (rpc, ~15 KiB: 0.199 -> 0.220 ms), so they keep 4 KiB.
+  uint32_t win = g_win_bytes;
+  if (g_win_auto) win = n && 64ull * (len / n) <= (8u << 10) ? (8u << 10) : (4u << 10);
   const uint32_t Cw = static_cast<uint32_t>(std::min<uint64_t>(
-      g_win_bytes, (64ull * std::max<uint64_t>(p->max_record_bytes + mark, 16) + 15u) & ~15ull));
+      win, (64ull * std::max<uint64_t>(p->max_record_bytes + mark, 16) + 15u) & ~15ull));
   const uint32_t lw = dec_w_lds(p->stride, Cw);
   const bool ok_W = lw <= kVarLdsBudget && aligned(d_native, 16);
   int kern = g_force_dec;
@@ -2317,9 +2345,10 @@ void xdrg__force_var_kernels(int enc, int dec) {
 }
 void xdrg__set_stamps(void *buf) { g_stamps = static_cast<unsigned long long *>(buf); }
 void xdrg__set_stamps_enc(void *buf) { g_stamps_enc = static_cast<unsigned long long *>(buf); }
-int xdrg__set_window_bytes(int bytes) {
-  const int old = static_cast<int>(g_win_bytes);
-  g_win_bytes = static_cast<uint32_t>(bytes) & ~15u;
+int xdrg__set_window_bytes(int bytes) {  // < 0: back to the per-call choice
+  const int old = g_win_auto ? -1 : static_cast<int>(g_win_bytes);
+  g_win_auto = bytes < 0;
+  if (bytes >= 0) g_win_bytes = static_cast<uint32_t>(bytes) & ~15u;
   return old;
 }
 int xdrg__set_image_bytes(int bytes) {  // < 0: back to the per-plan choice
