@@ -37,11 +37,12 @@ __device__ __forceinline__ void report(unsigned long long *err, uint64_t rec, ui
   atomicMin(err, key);
 }
 
+// Uniform trip count, no per-lane exit: the table reads stay scalar.
 __device__ __forceinline__ bool enum_ok(const uint32_t *__restrict__ table, uint32_t idx,
                                         uint32_t cnt, uint32_t v) {
-  for (uint32_t i = 0; i < cnt; ++i)
-    if (table[idx + i] == v) return true;
-  return false;
+  bool ok = false;
+  for (uint32_t i = 0; i < cnt; ++i) ok |= table[idx + i] == v;
+  return ok;
 }
 
 // Decode-time word checks: padding of fixed opaque (marshal.cc:52-55) and

@@ -102,11 +102,18 @@ __device__ __forceinline__ xdrg_op load_op(const xdrg_op *__restrict__ ops, uint
   return op;
 }
 
+// The case table of a union op: (value, target pc) pairs with distinct
+// values.  The loop has a wave-uniform trip count and no per-lane exit, so
+// the table reads stay scalar (an early per-lane return made them vector
+// loads, one memory round trip per union visited).
 __device__ __forceinline__ int union_target(const xdrg_op &op, const uint32_t *__restrict__ table,
                                             uint32_t d) {
-  for (uint32_t i = 0; i < op.arg3; ++i)
-    if (table[op.arg2 + 2 * i] == d) return static_cast<int>(table[op.arg2 + 2 * i + 1]);
-  return (op.flags & XDRG_F_DEFAULT) ? static_cast<int>(op.arg4) : -1;
+  int t = (op.flags & XDRG_F_DEFAULT) ? static_cast<int>(op.arg4) : -1;
+  for (uint32_t i = 0; i < op.arg3; ++i) {
+    const uint32_t cv = table[op.arg2 + 2 * i], tg = table[op.arg2 + 2 * i + 1];
+    t = cv == d ? static_cast<int>(tg) : t;
+  }
+  return t;
 }
 
 __device__ __forceinline__ void load_ops(xdrg_op *sops, const xdrg_op *__restrict__ ops,
