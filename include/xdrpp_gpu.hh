@@ -817,6 +817,52 @@ void from_opaque_batch(const void *bytes, std::size_t len, T *out, std::size_t n
   unstage(nat.data(), heap.data(), n, out);
 }
 
+// ------------------------------------------------------ sizes and depths
+//! xdr::xdr_size(recs[i]) for every record (xdrpp/types.h:240-244), one
+//! device size pass (xdrg_serial_sizes).
+template <typename T>
+std::vector<std::uint32_t> xdr_size_batch(const T *recs, std::size_t n, hipStream_t s = nullptr) {
+  const batch_plan<T> &P = plan_for<T>();
+  staged_batch b = stage(recs, n);
+  detail::dev_buf<std::uint8_t> d_nat(b.native.size());
+  detail::dev_buf<std::uint32_t> d_sz(n);
+  detail::dev_buf<xdrg_status> d_st(1);
+  detail::hipcheck(hipMemcpyAsync(d_nat.p, b.native.data(), b.native.size(), hipMemcpyHostToDevice, s), "H2D");
+  detail::abicheck(xdrg_status_init(d_st.p, s), "xdrg_status_init");
+  detail::abicheck(xdrg_serial_sizes(P.handle(), d_nat.p, n, d_sz.p, marshaling_stack_limit, d_st.p, s),
+                   "xdrg_serial_sizes");
+  std::vector<std::uint32_t> out(n);
+  if (n) detail::hipcheck(hipMemcpyAsync(out.data(), d_sz.p, n * 4, hipMemcpyDeviceToHost, s), "D2H");
+  xdrg_error e{};
+  detail::abicheck(xdrg_status_read(d_st.p, s, &e), "xdrg_status_read");
+  if (e.code) P.raise(e);
+  return out;
+}
+
+//! xdr::check_xdr_depth(recs[i], depth_limit) for every record
+//! (xdrpp/depth_checker.h:72-79), from the device's per-record depths
+//! (xdrg_record_depths).
+template <typename T>
+std::vector<bool> check_xdr_depth_batch(const T *recs, std::size_t n, std::uint32_t depth_limit,
+                                        hipStream_t s = nullptr) {
+  const batch_plan<T> &P = plan_for<T>();
+  staged_batch b = stage(recs, n);
+  detail::dev_buf<std::uint8_t> d_nat(b.native.size());
+  detail::dev_buf<std::uint32_t> d_d(n);
+  detail::dev_buf<xdrg_status> d_st(1);
+  detail::hipcheck(hipMemcpyAsync(d_nat.p, b.native.data(), b.native.size(), hipMemcpyHostToDevice, s), "H2D");
+  detail::abicheck(xdrg_status_init(d_st.p, s), "xdrg_status_init");
+  detail::abicheck(xdrg_record_depths(P.handle(), d_nat.p, n, d_d.p, d_st.p, s), "xdrg_record_depths");
+  std::vector<std::uint32_t> d(n);
+  if (n) detail::hipcheck(hipMemcpyAsync(d.data(), d_d.p, n * 4, hipMemcpyDeviceToHost, s), "D2H");
+  xdrg_error e{};
+  detail::abicheck(xdrg_status_read(d_st.p, s, &e), "xdrg_status_read");
+  if (e.code) P.raise(e);
+  std::vector<bool> ok(n);
+  for (std::size_t i = 0; i < n; ++i) ok[i] = d[i] <= depth_limit;
+  return ok;
+}
+
 // ---------------------------------------------------- record-marked messages
 namespace detail {
 // Device encode of n staged records as n record-marked messages.  Returns

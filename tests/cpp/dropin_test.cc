@@ -21,6 +21,8 @@
 #include "ref_objects.hh"
 #include "xdrpp_gpu.hh"
 
+#include <xdrpp/depth_checker.h>
+
 #include <cstdio>
 #include <fstream>
 #include <functional>
@@ -167,6 +169,23 @@ static void check_msgs(const char *name, const std::vector<T> &v) {
           rw.c_str(), gw.c_str());
   }
   std::printf("msgs %s: %zu messages bit-exact, both decodes ok\n", name, v.size());
+}
+
+// xdr_size_batch == xdr::xdr_size per record; check_xdr_depth_batch ==
+// xdr::check_xdr_depth per record at every limit that matters.
+template <typename T>
+static void check_sizes_depths(const char *name, const std::vector<T> &v) {
+  std::vector<std::uint32_t> sz = xdr::gpu::xdr_size_batch(v.data(), v.size());
+  bool ok = sz.size() == v.size();
+  for (std::size_t i = 0; ok && i < v.size(); ++i) ok = sz[i] == xdr::xdr_size(v[i]);
+  CHECK(ok, "%s: xdr_size_batch differs from xdr_size", name);
+  for (std::uint32_t lim = 0; lim <= 7; ++lim) {
+    std::vector<bool> d = xdr::gpu::check_xdr_depth_batch(v.data(), v.size(), lim);
+    bool okd = d.size() == v.size();
+    for (std::size_t i = 0; okd && i < v.size(); ++i) okd = d[i] == xdr::check_xdr_depth(v[i], lim);
+    CHECK(okd, "%s: check_xdr_depth_batch differs from check_xdr_depth at limit %u", name, lim);
+  }
+  std::printf("sizes+depths %s: %zu records match xdr_size / check_xdr_depth\n", name, v.size());
 }
 
 static std::vector<std::uint8_t> slurp(const std::string &path) {
@@ -352,6 +371,11 @@ int main(int argc, char **argv) {
     check_msgs("rpc", rp);
     check_msgs("vecrec", vr);
     check_rpc(argc > 2 ? argv[2] : "tests/golden");
+    check_sizes_depths("numerics", nu);
+    check_sizes_depths("rec128", rc);
+    check_sizes_depths("recvar", rv);
+    check_sizes_depths("rpc", rp);
+    check_sizes_depths("vecrec", vr);
   } else {
     std::fprintf(stderr, "usage: dropin_test plans <dir> | stage | gpu\n");
     return 2;
