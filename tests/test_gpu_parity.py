@@ -523,3 +523,28 @@ def test_decode_window_shapes(dev, dec_shape, name, n):
     o_nat, o_heap = O.decode(p.cp, want, n, offs)
     assert np.array_equal(back.cpu().numpy(), o_nat)
     assert np.array_equal(bheap.cpu().numpy(), o_heap)
+
+
+@pytest.mark.parametrize("linear", [1, 0])
+@pytest.mark.parametrize("n", [1, 63, 65, 300, 4099])
+def test_size_pass_linear(dev, linear, n):
+    """recvar is a linear plan (no unions/containers): its size pass reads
+    the length words without a walk; both passes give xdr_size and the
+    same encode."""
+    import ctypes as C
+    L = A.lib()
+    L.xdrg__set_size_linear.argtypes = [C.c_int]
+    old = L.xdrg__set_size_linear(linear)
+    try:
+        p = plan("recvar")
+        nat, heap = W.recvar(n)
+        want, offs = O.encode(p.cp, nat, n, heap)
+        mar = M.Marshaler(p, dev)
+        sz = mar.serial_sizes(to_dev(nat, dev), n).cpu().numpy().astype(np.uint64)
+        assert np.array_equal(sz, np.diff(offs))
+        res = mar.encode(to_dev(nat, dev), n, to_dev(heap, dev))
+        assert np.array_equal(res.xdr.cpu().numpy(), want)
+        msgs = mar.encode_msgs(to_dev(nat, dev), n, to_dev(heap, dev))
+        assert np.array_equal(msgs.xdr.cpu().numpy(), O.encode_msgs(p.cp, nat, n, heap)[0])
+    finally:
+        L.xdrg__set_size_linear(old)

@@ -299,6 +299,22 @@ int compile_plan(xdrg_plan &p) {
   if (!fixed) {
     p.fixed_size = 0;
     p.path = XDRG_PATH_VAR;
+    p.linear = true;
+    p.lin_base = 0;
+    p.lin_n = 0;
+    for (const xdrg_op &op : p.ops) {
+      switch (op.kind) {
+      case XDRG_OP_U32: case XDRG_OP_BOOL: case XDRG_OP_ENUM: p.lin_base += 4; break;
+      case XDRG_OP_U64: p.lin_base += 8; break;
+      case XDRG_OP_OPAQUE: p.lin_base += (op.arg0 + 3u) & ~3u; break;
+      case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING:
+        if (p.lin_n == 8) p.linear = false;
+        else { p.lin_off[p.lin_n++] = op.noff; p.lin_base += 4; }
+        break;
+      case XDRG_OP_END: break;
+      default: p.linear = false; break;  // UNION, JUMP, VECTOR
+      }
+    }
     for (const xdrg_op &op : p.ops)
       if (op.kind == XDRG_OP_VAROPAQUE || op.kind == XDRG_OP_STRING || op.kind == XDRG_OP_UNION ||
           op.kind == XDRG_OP_VECTOR ||

@@ -98,6 +98,12 @@ struct xdrg_plan {
   uint32_t heap_factor = 0;       // decode element-area factor (xdrg_decode_heap_size)
   bool has_checks = false;
   bool has_bool = false;
+  // var plans whose walk never branches (scalars, opaque[n], opaque<>,
+  // string<>; no unions or containers): xdr_size = lin_base + the padded
+  // lengths of the lin_n bytes fields whose xdrg_bytes_ref sit at lin_off[]
+  bool linear = false;
+  uint32_t lin_base = 0, lin_n = 0;
+  uint32_t lin_off[8] = {};
   // fixed plans
   std::vector<uint32_t> op_wire_off;  // wire byte offset of each op (fixed)
   xdrg::fixed_prog enc, dec;

@@ -1926,6 +1926,7 @@ uint32_t g_img_bytes = 4u << 10;   // encode LDS image per wave when not automat
 bool g_img_auto = true;            // per-plan image size (var_encode)
 int g_enc_u = 8;                   // payload chunks in flight per lane, chunk-map encode
 int g_dec_ra = 1;                  // window decode: 32-byte read-ahead past the window
+int g_size_linear = 1;             // size pass without a walk for linear plans
 uint32_t g_win_bytes = 4u << 10;   // decode LDS window per wave when not automatic
 bool g_win_auto = true;            // per-call window size (var_decode)
 unsigned long long *g_stamps = nullptr;      // diagnostic phase stamps, decode (tuning)
@@ -2083,9 +2084,54 @@ uint64_t decode_heap_bytes(const xdrg_plan &p, uint64_t len) {
 }
 
 // Size pass (xdr_size per record + 64-record block sums).
+// Size pass of a linear plan (xdrg_plan::linear): no walk.  One lane per
+// record reads the length words of its bytes fields (independent loads);
+// 256-record workgroups, one 64-record block sum per wave.
+struct lin_args {
+  uint32_t base, n;
+  uint32_t off[8];
+};
+__global__ __launch_bounds__(256) void k_size_linear(const uint8_t *__restrict__ native, uint64_t n,
+                                                     uint32_t stride, lin_args L,
+                                                     uint32_t *__restrict__ sizes,
+                                                     unsigned long long *__restrict__ block_sums,
+                                                     uint32_t mark, unsigned long long *err) {
+  const uint64_t r = static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x;
+  uint32_t size = 0;
+  if (r < n) {
+    const uint8_t *rec = native + r * stride;
+    uint32_t len[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      len[k] = static_cast<uint32_t>(k) < L.n ? *reinterpret_cast<const uint32_t *>(rec + L.off[k] + 8) : 0u;
+    uint64_t sz = static_cast<uint64_t>(L.base) + mark;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sz += (static_cast<uint64_t>(len[k]) + 3u) & ~3ull;
+    if (sz >= kSizeErr) {
+      report(err, r, 0, XDRG_ERR_OVERFLOW_PUT);
+      size = kSizeErr;
+    } else {
+      size = static_cast<uint32_t>(sz);
+    }
+    sizes[r] = size;
+  }
+  unsigned long long v = (size & kSizeErr) ? 0ull : size;
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  const uint64_t blk = r / 64u;
+  if (block_sums && (threadIdx.x & 63u) == 0 && blk * 64u < n) block_sums[blk] = v;
+}
+
 hipError_t launch_size_pass(const xdrg_plan &p, const uint8_t *nat, uint64_t n, uint32_t *sizes,
                             unsigned long long *bsum, uint32_t mark, unsigned long long *err,
                             hipStream_t s) {
+  if (p.linear && g_size_linear) {
+    lin_args L;
+    L.base = p.lin_base;
+    L.n = p.lin_n;
+    for (int k = 0; k < 8; ++k) L.off[k] = p.lin_off[k];
+    k_size_linear<<<(n + 255) / 256, 256, 0, s>>>(nat, n, p.stride, L, sizes, bsum, mark, err);
+    return hipGetLastError();
+  }
   const uint64_t nb = (n + 63) / 64;
   const size_t tile = 64ull * p.stride;
   if (tile <= kVarLdsBudget)
@@ -2331,6 +2377,11 @@ const char *xdrg_last_hip_error(void) { return g_hip_err; }
 
 // Internal A/B hooks for tools/tune and the tests (not part of include/xdrgpu.h).
 void xdrg__force_fixed_path(int path) { g_fixed_path = path; }
+int xdrg__set_size_linear(int on) {
+  const int old = g_size_linear;
+  g_size_linear = on ? 1 : 0;
+  return old;
+}
 int xdrg__set_dec_readahead(int on) {
   const int old = g_dec_ra;
   g_dec_ra = on ? 1 : 0;
@@ -2550,7 +2601,7 @@ int xdrg_record_depths(const xdrg_plan *p, const void *d_native, uint64_t n, uin
   if (n == 0) return XDRG_OK;
   if (int rc = plan_upload(p)) return rc;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (p->path != XDRG_PATH_VAR) {  // every record walks every op
+  if (p->path != XDRG_PATH_VAR || p->linear) {  // every record walks every op
     HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_depths), int(p->max_depth), n, s));
     return XDRG_OK;
   }
