@@ -185,7 +185,8 @@ enum xdrg_err {
   XDRG_ERR_MSG_FRAGMENT = 15,   /* xdr_bad_message_size srpc.cc:42-45    */
   XDRG_ERR_MSG_TOO_LONG = 16,   /* msg_sock maxmsglen_  msgsock.cc:99-111 */
   XDRG_ERR_MSG_MISMATCH = 17,   /* mark disagrees with the record index  */
-  XDRG_ERR_MSG_COUNT = 18       /* more messages than the index can hold */
+  XDRG_ERR_MSG_COUNT = 18,      /* more messages than the index can hold */
+  XDRG_ERR_INTERNAL = 19        /* a device-side wait gave up (the kernel still ends) */
 };
 
 /* Exception class a data error maps to (for host-side rethrow). */

@@ -548,3 +548,52 @@ def test_size_pass_linear(dev, linear, n):
         assert np.array_equal(msgs.xdr.cpu().numpy(), O.encode_msgs(p.cp, nat, n, heap)[0])
     finally:
         L.xdrg__set_size_linear(old)
+
+
+@pytest.mark.parametrize("fused", [1, 0])
+@pytest.mark.parametrize("name", ["recvar", "rpc", "vecrec"])
+@pytest.mark.parametrize("n", [1, 64, 65, 4099, 100003])
+def test_encode_fused_lookback(dev, fused, name, n):
+    """The one-kernel encode (in-kernel sizes + decoupled look-back over
+    64-record blocks) and the three-kernel one give the reference's bytes,
+    record index and total."""
+    import ctypes as C
+    L = A.lib()
+    L.xdrg__set_enc_fused.argtypes = [C.c_int]
+    old = L.xdrg__set_enc_fused(fused)
+    try:
+        p = plan(name)
+        nat, heap = W.GENERATORS[name](n)
+        want, offs = O.encode(p.cp, nat, n, heap)
+        mar = M.Marshaler(p, dev)
+        res = mar.encode(to_dev(nat, dev), n, to_dev(heap, dev) if heap.size else None)
+        assert np.array_equal(res.xdr.cpu().numpy(), want)
+        assert np.array_equal(res.offsets.cpu().numpy().view(np.uint64), offs)
+        m = mar.encode_msgs(to_dev(nat, dev), n, to_dev(heap, dev) if heap.size else None)
+        assert np.array_equal(m.xdr.cpu().numpy(), O.encode_msgs(p.cp, nat, n, heap)[0])
+    finally:
+        L.xdrg__set_enc_fused(old)
+
+
+@pytest.mark.parametrize("fused", [1, 0])
+def test_encode_fused_bad_discriminant(dev, fused):
+    """A bad discriminant found by the in-kernel size walk is reported at the
+    lowest failing record, as the size pass reports it."""
+    import ctypes as C
+    L = A.lib()
+    L.xdrg__set_enc_fused.argtypes = [C.c_int]
+    old = L.xdrg__set_enc_fused(fused)
+    try:
+        p = plan("rpc")
+        n = 5000
+        nat, heap = W.rpc(n)
+        rec = nat.reshape(n, p.stride).copy()
+        off = S.rpc_msg.offset_of("body")
+        for bad in (4321, 777):
+            rec[bad, off:off + 4] = np.frombuffer(np.uint32(9).tobytes(), np.uint8)
+        with pytest.raises(M.XdrBadDiscriminant) as ei:
+            M.Marshaler(p, dev).encode(to_dev(rec.reshape(-1), dev), n, to_dev(heap, dev))
+        assert ei.value.record == 777
+        assert str(ei.value) == "bad value of mtype in _body_t"
+    finally:
+        L.xdrg__set_enc_fused(old)

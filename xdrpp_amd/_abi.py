@@ -44,6 +44,7 @@ ERR_MSG_FRAGMENT = 15
 ERR_MSG_TOO_LONG = 16
 ERR_MSG_MISMATCH = 17
 ERR_MSG_COUNT = 18
+ERR_INTERNAL = 19
 
 MARK_LAST = 0x80000000  # XDRG_MARK_LAST: last-fragment bit of a record mark
 INDEX_MAX_MSG = 16380   # XDRG_INDEX_MAX_MSG

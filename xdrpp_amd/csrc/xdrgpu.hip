@@ -323,6 +323,112 @@ constexpr uint32_t kPcDone = 0xffffffffu;
       for (int q_ = 0; q_ < 8; ++q_) stamps[(wave_id) * 8 + q_] = stv[q_];         \
   } while (0)
 
+// xdr_size of the record at `nat` (a lane-per-record walk; every lane of
+// the wave calls it, `active` lanes walk).  Returns the wire bytes, or sets
+// bad_op on an unknown discriminant.
+__device__ uint64_t size_walk(const uint8_t *nat, bool active, const xdrg_op *__restrict__ ops,
+                              uint32_t nops, const uint32_t *__restrict__ table, uint32_t &bad_op) {
+  uint64_t s = 0;
+  uint32_t pc = active ? 0u : kPcDone;
+  bad_op = kPcDone;
+  for (uint32_t upc = 0; upc < nops; ++upc) {
+    if (!__any(pc == upc)) continue;
+    const xdrg_op op = load_op(ops, upc);
+    if (pc != upc) continue;
+    switch (op.kind) {
+    case XDRG_OP_END: pc = kPcDone; break;
+    case XDRG_OP_JUMP: pc = op.arg0; break;
+    case XDRG_OP_U64: s += 8; ++pc; break;
+    case XDRG_OP_OPAQUE: s += (op.arg0 + 3u) & ~3u; ++pc; break;
+    case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING:
+      s += 4u + ((static_cast<uint64_t>(*reinterpret_cast<const uint32_t *>(nat + op.noff + 8)) + 3u) & ~3ull);
+      ++pc;
+      break;
+    case XDRG_OP_UNION: {
+      const int t = union_target(op, table, *reinterpret_cast<const uint32_t *>(nat + op.noff));
+      s += 4;
+      if (t < 0) { bad_op = upc; pc = kPcDone; }
+      else pc = static_cast<uint32_t>(t);
+      break;
+    }
+    case XDRG_OP_VECTOR:
+      s += 4ull + static_cast<uint64_t>(*reinterpret_cast<const uint32_t *>(nat + op.noff + 8)) * op.arg3;
+      pc = upc + 1 + op.arg2;
+      break;
+    default: s += 4; ++pc; break;
+    }
+  }
+  return s;
+}
+
+// ---------------------------------------------- decoupled look-back (waves)
+// One flag word per 64-record block: status (bits 63-62: 1 = aggregate,
+// 2 = inclusive prefix) | value (62 bits).  Flags and the block ticket are
+// zeroed by the host before the launch.  A wave takes its block by ticket
+// (so it only ever waits on blocks that already run), publishes its
+// aggregate at once, then walks back 64 flags at a time: the nearest
+// inclusive prefix plus the aggregates after it.  Every block publishes
+// its aggregate without waiting on anything, so the wait always ends; a
+// bounded poll count keeps a bug from hanging the GPU (XDRG_ERR_INTERNAL).
+constexpr unsigned long long kLbAgg = 1ull << 62, kLbInc = 2ull << 62;
+constexpr unsigned long long kLbVal = (1ull << 62) - 1;
+
+// Relaxed, device-coherent accesses: the flag word carries its own value,
+// so no other memory is ordered through it.  (Release/acquire at agent
+// scope made every publish write back the XCD's L2: 1.9 ms for 16K blocks.)
+__device__ __forceinline__ unsigned long long lb_load(const unsigned long long *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void lb_store(unsigned long long *p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Exclusive prefix of block `bid` whose aggregate is `agg`; publishes the
+// block's inclusive prefix.  All 64 lanes call it.
+__device__ uint64_t lookback(unsigned long long *flags, uint64_t bid, uint64_t agg,
+                             unsigned long long *err) {
+  const uint32_t lane = threadIdx.x & 63u;
+  if (bid == 0) {
+    if (lane == 0) lb_store(&flags[0], kLbInc | agg);
+    return 0;
+  }
+  if (lane == 0) lb_store(&flags[bid], kLbAgg | agg);
+  uint64_t prefix = 0;
+  int64_t j = static_cast<int64_t>(bid) - 1;
+  for (;;) {
+    const int64_t idx = j - static_cast<int64_t>(lane);
+    unsigned long long f = idx >= 0 ? 0ull : kLbInc;  // below block 0: nothing
+    uint32_t polls = 0;
+    bool gave_up = false;
+    for (;;) {
+      if (idx >= 0 && (f >> 62) == 0) f = lb_load(&flags[idx]);
+      if (!__any(idx >= 0 && (f >> 62) == 0)) break;
+      if (++polls > (1u << 22)) { gave_up = true; break; }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (gave_up) {
+      if (lane == 0) report(err, bid * 64u, kOpRecordLevel, XDRG_ERR_INTERNAL);
+      break;
+    }
+    const bool inc = (f >> 62) == 2;
+    const unsigned long long b = __ballot(inc);
+    const uint64_t val = f & kLbVal;
+    if (b) {
+      const uint32_t l0 = __builtin_ctzll(b);  // nearest block with an inclusive prefix
+      uint64_t v = lane <= l0 ? val : 0ull;
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      prefix += v;
+      break;
+    }
+    uint64_t v = val;
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    prefix += v;
+    j -= 64;
+  }
+  if (lane == 0) lb_store(&flags[bid], kLbInc | ((prefix + agg) & kLbVal));
+  return prefix;
+}
+
 // One 64-thread workgroup = 64 consecutive records.  The native records are
 // staged in LDS with coalesced 16-byte loads, so the walk reads fields from
 // LDS instead of issuing one dependent global load per op.
@@ -1014,14 +1120,19 @@ __device__ __forceinline__ void img_put(uint8_t *im, uint32_t C, uint8_t *gout, 
   else st32(gout + at, v);
 }
 
-template <int KMAX, int U>
+// FUSED: no separate size pass and scan.  The wave takes its block by
+// ticket, sizes its records from the staged tile (size_walk) and gets its
+// stretch offset by decoupled look-back (`lb` = flags[nb] + ticket, zeroed
+// by the host); the last block writes the total.
+template <int KMAX, int U, bool FUSED = false>
 __global__ __launch_bounds__(64) void k_var_encode_i(
     const uint8_t *__restrict__ native, uint64_t n, uint32_t stride, const uint8_t *__restrict__ heap,
     uint64_t heap_len, uint8_t *__restrict__ xdr, uint64_t cap, uint64_t *__restrict__ offsets,
     const uint32_t *__restrict__ sizes, const unsigned long long *__restrict__ block_base,
     const xdrg_op *__restrict__ ops, uint32_t nops, const uint32_t *__restrict__ table,
     uint32_t stack_limit, uint32_t MC, uint32_t C, uint32_t mark, unsigned long long *err,
-    unsigned long long *stamps) {
+    unsigned long long *stamps, unsigned long long *lb = nullptr,
+    unsigned long long *total = nullptr) {
   extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
   unsigned long long stv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   XDRG_STAMP(0);
@@ -1031,15 +1142,37 @@ __global__ __launch_bounds__(64) void k_var_encode_i(
   uint16_t *map = reinterpret_cast<uint16_t *>(sm + L.map);
   uint8_t *img = sm + L.img;
   const uint32_t lane = threadIdx.x;
-  const uint64_t wr0 = static_cast<uint64_t>(blockIdx.x) * 64u;
+  const uint64_t nblk = (n + 63) / 64;
+  uint64_t bid = blockIdx.x;
+  if (FUSED) {  // block by ticket: waits only ever target blocks that already run
+    uint64_t t = 0;
+    if (lane == 0) t = atomicAdd(&lb[nblk], 1ull);
+    bid = __shfl(t, 0, 64);
+  }
+  const uint64_t wr0 = bid * 64u;
   const uint64_t r = wr0 + lane;
   const uint32_t nrec = static_cast<uint32_t>(min<uint64_t>(64, n - wr0));
 
   // ---- record offsets: wave scan of the sizes on top of the block base
   // (sizes, block base and the native tile are loaded in one round trip)
-  const uint32_t sz = r < n ? sizes[r] : kSizeErr;
-  const uint64_t wave_out = block_base[blockIdx.x];
-  stage_tile(tile, native + wr0 * stride, nrec * stride, lane, 64u);
+  uint32_t sz;
+  uint64_t wave_out;
+  if (FUSED) {
+    stage_tile(tile, native + wr0 * stride, nrec * stride, lane, 64u);
+    wave_sync();
+    uint32_t bad_op;
+    const uint64_t s0 = size_walk(tile + lane * stride, r < n, ops, nops, table, bad_op) + mark;
+    sz = kSizeErr;
+    if (r < n) {  // k_var_size's reports (gen_hh.cc:639-648; marshal.h:104-108)
+      if (bad_op != kPcDone) report(err, r, bad_op, XDRG_ERR_BAD_DISCRIMINANT);
+      else if (s0 >= kSizeErr) report(err, r, 0, XDRG_ERR_OVERFLOW_PUT);
+      else sz = static_cast<uint32_t>(s0);
+    }
+  } else {
+    sz = r < n ? sizes[r] : kSizeErr;
+    wave_out = block_base[blockIdx.x];
+    stage_tile(tile, native + wr0 * stride, nrec * stride, lane, 64u);
+  }
   const bool szok = !(sz & kSizeErr);
   const unsigned long long v = szok ? sz : 0ull;
   unsigned long long incl = v;
@@ -1047,8 +1180,15 @@ __global__ __launch_bounds__(64) void k_var_encode_i(
     const unsigned long long x = __shfl_up(incl, o, 64);
     if (lane >= static_cast<uint32_t>(o)) incl += x;
   }
-  const uint64_t off = wave_out + incl - v;
   const uint64_t T = rl64(incl, 63);  // bytes of the wave's stretch
+  if (FUSED) {
+    wave_out = lookback(lb, bid, T, err);
+    if (bid == nblk - 1 && lane == 0) {  // the scan's outputs (k_scan_blocks)
+      *total = wave_out + T;
+      offsets[n] = wave_out + T;
+    }
+  }
+  const uint64_t off = wave_out + incl - v;
   if (r < n) offsets[r] = off;
   wave_sync();
   XDRG_STAMP(1);
@@ -1927,6 +2067,12 @@ bool g_img_auto = true;            // per-plan image size (var_encode)
 int g_enc_u = 8;                   // payload chunks in flight per lane, chunk-map encode
 int g_dec_ra = 1;                  // window decode: 32-byte read-ahead past the window
 int g_size_linear = 1;             // size pass without a walk for linear plans
+// Chunk-map encode with in-kernel sizes + decoupled look-back instead of the
+// size pass and the block scan.  Off: measured slower on MI355X (recvar
+// 1M: 269 us vs 170 us for the three kernels).  ~5000 waves run at once,
+// so the inclusive-prefix frontier lags far behind and each wave sums
+// thousands of aggregates through device-coherent (L2-bypassing) loads.
+int g_enc_fused = 0;
 uint32_t g_win_bytes = 4u << 10;   // decode LDS window per wave when not automatic
 bool g_win_auto = true;            // per-call window size (var_decode)
 unsigned long long *g_stamps = nullptr;      // diagnostic phase stamps, decode (tuning)
@@ -2220,6 +2366,22 @@ int var_encode(const xdrg_plan &P, const void *d_native, uint64_t n, const uint8
   const uint8_t *nat8 = static_cast<const uint8_t *>(d_native);
   uint8_t *xdr8 = static_cast<uint8_t *>(d_xdr);
   const uint32_t nops = uint32_t(p->ops.size());
+  if (kern == 3 && g_enc_fused) {
+    // one kernel: sizes, decoupled look-back and emission (flags + ticket
+    // in the block-sum area, zeroed here)
+    HIPCHK(hipMemsetAsync(bsum, 0, (nb + 1) * 8, s));
+    unsigned long long *tot = reinterpret_cast<unsigned long long *>(&d_status->total_bytes);
+#define LAUNCH_ENC_F(K, UU)                                                                      \
+  k_var_encode_i<K, UU, true><<<nb, 64, LI.total, s>>>(                                          \
+      nat8, n, p->stride, d_heap, heap_len, xdr8, cap, d_offsets, nullptr, nullptr, p->d_ops,    \
+      nops, p->d_table, stack_limit, MC, Ci, mark, err, g_stamps_enc, bsum, tot)
+    if (KI == 1) LAUNCH_ENC_F(1, 8);
+    else if (KI == 2) LAUNCH_ENC_F(2, 8);
+    else LAUNCH_ENC_F(4, 8);
+#undef LAUNCH_ENC_F
+    HIPCHK(hipGetLastError());
+    return XDRG_OK;
+  }
   HIPCHK(launch_size_pass(*p, nat8, n, sizes, bsum, mark, err, s));
   if (int rc = xdrg::launch_block_scan(bsum, bbase, uint32_t(nb), d_status, d_offsets, n, s)) return rc;
   if (kern == 3) {
@@ -2377,6 +2539,11 @@ const char *xdrg_last_hip_error(void) { return g_hip_err; }
 
 // Internal A/B hooks for tools/tune and the tests (not part of include/xdrgpu.h).
 void xdrg__force_fixed_path(int path) { g_fixed_path = path; }
+int xdrg__set_enc_fused(int on) {
+  const int old = g_enc_fused;
+  g_enc_fused = on ? 1 : 0;
+  return old;
+}
 int xdrg__set_size_linear(int on) {
   const int old = g_size_linear;
   g_size_linear = on ? 1 : 0;
@@ -2747,6 +2914,7 @@ const char *xdrg_error_message(int code) {
   case XDRG_ERR_MSG_TOO_LONG: return "msg_sock: rejecting message (too long)";
   case XDRG_ERR_MSG_MISMATCH: return "record mark does not match the record index";
   case XDRG_ERR_MSG_COUNT: return "more messages than the record index holds";
+  case XDRG_ERR_INTERNAL: return "xdrgpu internal error (device wait gave up)";
   default: return "unknown xdrgpu error";
   }
 }
