@@ -163,6 +163,61 @@ def host_inclusive(mar, plan, nat_dev, n, W_, reps=5, nstreams=2, chunk_records=
             "chunk_records": chunk_records, "streams": nstreams}
 
 
+def host_inclusive_var(mar, plan, nat_dev, heap_dev, n, reps=3):
+    """Var schemas, whole batch on one stream: pinned native records + payload
+    heap H2D -> encode -> stream + record index D2H, and the decode mirror
+    (stream + index H2D -> decode -> native records + decoded heap D2H).
+    PCIe-bound; reported apart, never as `value`."""
+    dev = nat_dev.device
+    s = torch.cuda.current_stream()
+    h_nat = nat_dev.cpu().pin_memory()
+    h_heap = heap_dev.cpu().pin_memory()
+    X = int(mar.serial_sizes(nat_dev, n).to(torch.int64).sum().item())
+    d_nat, d_heap = torch.empty_like(nat_dev), torch.empty_like(heap_dev)
+    d_xdr = torch.empty(X, dtype=torch.uint8, device=dev)
+    d_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    h_xdr = torch.empty(X, dtype=torch.uint8, pin_memory=True)
+    h_off = torch.empty(n + 1, dtype=torch.int64, pin_memory=True)
+    d_back = torch.empty_like(nat_dev)
+    d_hout = torch.empty(plan.decode_heap_bytes(X), dtype=torch.uint8, device=dev)
+    h_back = torch.empty(d_back.numel(), dtype=torch.uint8, pin_memory=True)
+    h_hout = torch.empty(d_hout.numel(), dtype=torch.uint8, pin_memory=True)
+    mar.status.init(s.cuda_stream)
+
+    def enc():
+        d_nat.copy_(h_nat, non_blocking=True)
+        d_heap.copy_(h_heap, non_blocking=True)
+        mar.launch_encode(d_nat, n, d_xdr, heap=d_heap, offsets=d_off, stream=s.cuda_stream)
+        h_xdr.copy_(d_xdr, non_blocking=True)
+        h_off.copy_(d_off, non_blocking=True)
+
+    def dec():
+        d_xdr.copy_(h_xdr, non_blocking=True)
+        d_off.copy_(h_off, non_blocking=True)
+        mar.launch_decode(d_xdr, n, d_back, offsets=d_off, heap_out=d_hout, stream=s.cuda_stream)
+        h_back.copy_(d_back, non_blocking=True)
+        h_hout.copy_(d_hout, non_blocking=True)
+
+    def timed(f):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        f()
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0
+
+    timed(enc), timed(dec)
+    te = min(timed(enc) for _ in range(reps))
+    td = min(timed(dec) for _ in range(reps))
+    mar.check(s.cuda_stream)
+    x2 = torch.empty_like(d_xdr)
+    mar.launch_encode(d_back, n, x2, heap=d_hout, offsets=torch.empty_like(d_off), stream=s.cuda_stream)
+    mar.check(s.cuda_stream)
+    return {"encode_gib_s": round(X / GIB / te, 2), "decode_gib_s": round(X / GIB / td, 2),
+            "encode_decode_gib_s": round(2 * X / GIB / (te + td), 2),
+            "round_trip_ok": bool(torch.equal(x2, d_xdr)), "streams": 1,
+            "note": "whole batch, copies and kernel serialized on one stream"}
+
+
 def cold_cache(mar, nat, xdr, back, n, alg_bytes, reps=5):
     """Each kernel timed alone after a 1 GiB streaming READ that evicts the
     256 MiB Infinity Cache and the L2s without leaving dirty lines whose
@@ -505,9 +560,10 @@ def main():
         line["messages"] = messages_leg(args.schema, plan, mar, nat, heap, n)
     if world == 1 and args.rpc:
         line["rpc_headers"] = rpc_leg(nat.device)
-    if world == 1 and args.host_inclusive and plan.is_fixed:
+    if world == 1 and args.host_inclusive:
         try:
-            line["host_inclusive"] = host_inclusive(mar, plan, nat, n, plan.fixed_size)
+            line["host_inclusive"] = (host_inclusive(mar, plan, nat, n, plan.fixed_size) if plan.is_fixed
+                                      else host_inclusive_var(mar, plan, nat, heap, n))
         except Exception as e:  # reported, never fatal
             line["host_inclusive"] = {"error": str(e)[:200]}
     if world == 1 and not args.no_cpu_baseline:

@@ -183,3 +183,38 @@ def test_success_replies_are_xdr_to_msg(dev):
     chk = R.hdrs_numpy(R.check_replies(enc.xdr, enc.offsets, to_dev(xid.view(np.int32), dev)))
     assert (chk["action"] == A.RPCR_OK).all()
     assert np.array_equal(chk["body_off"], enc.offsets.cpu().numpy()[:-1].astype(np.uint64) + 28)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_fuzzed_headers_vs_oracle(dev, seed):
+    """Random word corruptions of the call stream (lengths, discriminants,
+    pads, flavors) and random message lengths: every header's route,
+    client status and error replies equal the C restatement."""
+    rng = np.random.default_rng(1234 + seed)
+    s, o = W.rpc_calls(3000, first=7 * seed)
+    s = s.copy()
+    w = s.view("<u4")
+    marks = (o[:-1] // 4).astype(np.int64)
+    for _ in range(1500):  # corrupt header words (never the marks)
+        k = int(rng.integers(0, len(marks)))
+        pos = int(marks[k] + 1 + rng.integers(0, 12))
+        if pos >= len(w) or pos in set(marks[k:k + 2].tolist()):
+            continue
+        w[pos] = np.uint32(rng.choice([0, 1, 2, 3, 400, 401, 0xFFFFFFFF,
+                                       int(rng.integers(0, 1 << 32))])).byteswap()
+    # some messages cut short: move an offset down (the index would reject
+    # such framing; dispatch sees the shorter message and must not read past it)
+    o2 = o.copy()
+    for k in rng.integers(1, len(o) - 1, size=50):
+        o2[k] = max(o2[k - 1] + 4, o2[k] - 4 * int(rng.integers(1, 8)))
+    t = W.RPC_PROCS
+    want = O.rpc_headers(s, o2, t)
+    got = R.hdrs_numpy(R.dispatch(to_dev(s, dev), offs_dev(o2, dev), t))
+    assert got.tobytes() == want.tobytes()
+    wc = O.rpc_headers(s, o2, None, client=True)
+    gc = R.hdrs_numpy(R.check_replies(to_dev(s, dev), offs_dev(o2, dev)))
+    assert gc.tobytes() == wc.tobytes()
+    rs, roffs, rc, _ = O.rpc_replies(want)
+    out, goffs = R.error_replies(to_dev(want.view(np.uint8), dev))
+    assert rc == 0 and out.cpu().numpy().tobytes() == rs.tobytes()
+    assert np.array_equal(goffs.cpu().numpy().view(np.uint64), roffs)
