@@ -9,4 +9,4 @@ for sch in recvar rpc vecrec; do
   timeout -k 10 300 python bench.py --schema $sch --steps 20 --warmup 3 --no-cpu-baseline > $O/bench_$sch.log 2>&1 || { tail $O/bench_$sch.log; exit 1; }
   python -c "import json;d=json.loads(open('$O/bench_$sch.log').read().strip().split('\n')[-1]);print('$sch', d['value'], d['encode_ms'],d['decode_ms'],d['roofline']['frac'])"
 done
-OUT=prof9 bash tools/gpu/prof8.sh 2>&1 | grep -v "^\[" | grep "==\|k_var\|k_scan"
+OUT=${PROF_OUT:-prof9} bash tools/gpu/prof8.sh 2>&1 | grep -v "^\[" | grep "==\|k_var\|k_scan"

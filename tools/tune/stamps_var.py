@@ -48,7 +48,7 @@ for schema in sys.argv[1:] or ["recvar"]:
     xdr = torch.empty(total, dtype=torch.uint8, device=dev)
     offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
     back = torch.empty_like(nat)
-    hout = torch.empty(total, dtype=torch.uint8, device=dev)
+    hout = torch.empty(plan.decode_heap_bytes(total), dtype=torch.uint8, device=dev)
     L.xdrg__force_var_kernels(int(os.environ.get('VENC', '0')), int(os.environ.get('VDEC', '0')))
     L.xdrg__set_window_bytes(int(os.environ.get('WIN', '-1')))
     mar.status.init(torch.cuda.current_stream().cuda_stream)

@@ -245,6 +245,56 @@ __device__ bool dec_vector_elems(const xdrg_op *__restrict__ ops, const uint32_t
                                  uint64_t &p, uint64_t b, uint32_t stack_limit, uint64_t r,
                                  unsigned long long *err, const RD &rd) {
   const bool w4 = (es & 3u) == 0;  // 4-byte stores (dst is 8-aligned)
+  // Elements of at most 16 bytes made of word-aligned scalars and bools are
+  // assembled in four registers and written with one or two 8-byte stores:
+  // the byte-wise path below zero-fills first and stores each field on its
+  // own, up to 7 scattered stores per 16-byte element.  The test is on plan
+  // ops only, so it is wave-uniform.
+  bool staged = w4 && es <= 16u;
+  for (uint32_t k = 0; k < nb && staged; ++k) {
+    const xdrg_op e = load_op(ops, b0 + k);
+    staged = e.kind == XDRG_OP_BOOL ||
+             ((e.kind == XDRG_OP_U32 || e.kind == XDRG_OP_ENUM || e.kind == XDRG_OP_U64) &&
+              (e.noff & 3u) == 0);
+  }
+  if (staged) {
+    for (uint32_t i = 0; i < cnt; ++i) {
+      uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+      auto put = [&](uint32_t j, uint32_t v) {
+        w0 |= j == 0 ? v : 0u; w1 |= j == 1 ? v : 0u; w2 |= j == 2 ? v : 0u; w3 |= j == 3 ? v : 0u;
+      };
+      for (uint32_t k = 0; k < nb; ++k) {
+        const xdrg_op e = load_op(ops, b0 + k);
+        if (e.depth > stack_limit) { report(err, r, b0 + k, XDRG_ERR_STACK_GET); return false; }
+        const uint32_t need = e.kind == XDRG_OP_U64 ? 8u : 4u;
+        if (b - p < need) { report(err, r, b0 + k, XDRG_ERR_OVERFLOW_GET); return false; }
+        const uint32_t j = e.noff >> 2;
+        if (e.kind == XDRG_OP_BOOL) {
+          put(j, (rd(p) != 0u ? 1u : 0u) << (8u * (e.noff & 3u)));
+        } else if (e.kind == XDRG_OP_U64) {
+          put(j, bswap32(rd(p + 4)));
+          put(j + 1, bswap32(rd(p)));
+        } else {
+          const uint32_t v = bswap32(rd(p));
+          put(j, v);
+          if (e.kind == XDRG_OP_ENUM && (e.flags & XDRG_F_VALIDATE) && !enum_ok(table, e.arg0, e.arg1, v)) {
+            report(err, r, b0 + k, XDRG_ERR_INVALID_ENUM);
+            return false;
+          }
+        }
+        p += need;
+      }
+      uint8_t *el = dst + static_cast<uint64_t>(i) * es;
+      if (es == 4u) {
+        st32(el, w0);
+      } else {
+        *reinterpret_cast<uint2 *>(el) = make_uint2(w0, w1);
+        if (es == 12u) st32(el + 8, w2);
+        else if (es == 16u) *reinterpret_cast<uint2 *>(el + 8) = make_uint2(w2, w3);
+      }
+    }
+    return true;
+  }
   for (uint32_t i = 0; i < cnt; ++i) {
     uint8_t *el = dst + static_cast<uint64_t>(i) * es;
     if (w4) for (uint32_t z = 0; z < es; z += 4) st32(el + z, 0u);
