@@ -597,3 +597,65 @@ def test_encode_fused_bad_discriminant(dev, fused):
         assert str(ei.value) == "bad value of mtype in _body_t"
     finally:
         L.xdrg__set_enc_fused(old)
+
+
+# ------------------------------------------------- vector element layouts
+# Element structs that take the register-staged element path (<= 16 bytes of
+# word-aligned scalars and bools, bools sharing a word, 12-byte strides) and
+# ones that take the per-field path (an opaque field, > 16 bytes).
+_e_opq = S.Struct("e_opq", [("a", S.Int), ("t", S.OpaqueArray(3)), ("f", S.Bool)])
+_e_wide = S.Struct("e_wide", [("a", S.Hyper), ("b", S.Hyper), ("c", S.UInt)])
+_e_bools = S.Struct("e_bools", [("a", S.Bool), ("b", S.Bool), ("c", S.Int)])
+_e_three = S.Struct("e_three", [("a", S.Int), ("b", S.UInt), ("c", S.Int)])
+_e_ih = S.Struct("e_ih", [("a", S.Int), ("b", S.Hyper)])
+vshapes = S.Struct("vshapes", [("v1", S.XVector(_e_opq, 5)), ("v2", S.XVector(_e_wide, 3)),
+                               ("v3", S.XVector(_e_bools, 4)), ("v4", S.XVector(_e_three, 6)),
+                               ("v5", S.XVector(_e_ih, 3)), ("v6", S.XVector(S.Hyper, 4)),
+                               ("tail", S.UInt)])
+_VS = [("v1", _e_opq, 5), ("v2", _e_wide, 3), ("v3", _e_bools, 4), ("v4", _e_three, 6),
+       ("v5", _e_ih, 3), ("v6", S.Hyper, 4)]
+
+
+def _vshapes_batch(n, seed, straddle=False):
+    """Random records; element bytes random (bools included), arrays 8-byte
+    aligned in the heap.  With `straddle` the last record's v4 array starts
+    5 bytes before the end of the heap, so its elements are read past it."""
+    rng = np.random.default_rng(seed)
+    o = vshapes.offsets
+    nat = np.zeros((n, vshapes.size), dtype=np.uint8)
+    heap = bytearray()
+    for r in range(n):
+        for f, et, mx in _VS:
+            cnt = int(rng.integers(0, mx + 1))
+            start = len(heap)
+            heap += rng.integers(0, 256, cnt * et.size, dtype=np.uint8).tobytes()
+            heap += bytes(-len(heap) % 8)
+            _ref(nat, r, o[f], start, cnt)
+        nat[r, o["tail"]:o["tail"] + 4] = rng.integers(0, 256, 4, dtype=np.uint8)
+    if straddle:
+        heap += rng.integers(0, 256, 8, dtype=np.uint8).tobytes()
+        _ref(nat, n - 1, o["v4"], len(heap) - 5, 2)
+    return nat.reshape(-1), np.frombuffer(bytes(heap), np.uint8).copy()
+
+
+def _ref(nat, r, off, start, cnt):
+    nat[r, off:off + 8] = np.frombuffer(np.uint64(start).tobytes(), np.uint8)
+    nat[r, off + 8:off + 12] = np.frombuffer(np.uint32(cnt).tobytes(), np.uint8)
+
+
+@pytest.mark.parametrize("straddle", [False, True])
+@pytest.mark.parametrize("n", [1, 64, 257])
+def test_vector_element_layouts(dev, forced, n, straddle):
+    p = M.Plan(vshapes)
+    mar = M.Marshaler(p, dev)
+    nat, heap = _vshapes_batch(n, 900 + n, straddle)
+    # the oracle reads the heap unclamped: give it the zeros the GPU reads
+    # past heap_len
+    want, offs = O.encode(p.cp, nat, n, np.concatenate([heap, np.zeros(64, np.uint8)]))
+    res = mar.encode(to_dev(nat, dev), n, to_dev(heap, dev))
+    assert np.array_equal(res.xdr.cpu().numpy(), want)
+    assert np.array_equal(res.offsets.cpu().numpy().view(np.uint64), offs)
+    back, bheap = mar.decode(res.xdr, n, res.offsets)
+    o_nat, o_heap = O.decode(p.cp, want, n, offs)
+    assert np.array_equal(back.cpu().numpy(), o_nat)
+    assert np.array_equal(bheap.cpu().numpy(), o_heap)

@@ -203,6 +203,57 @@ __device__ bool enc_vector_elems(const xdrg_op *__restrict__ ops, uint32_t b0, u
                                  uint32_t cnt, uint32_t es, uint64_t &pos, uint64_t cap,
                                  uint32_t &at, uint32_t stack_limit, uint64_t r,
                                  unsigned long long *err, const PUT &put) {
+  // Elements of at most 16 bytes made of word-aligned scalars and bools are
+  // read with one or two loads and taken apart in registers (the per-field
+  // path below issues a load per field word).  Wave-uniform test.
+  bool staged = (es & 3u) == 0 && es <= 16u;
+  for (uint32_t k = 0; k < nb && staged; ++k) {
+    const xdrg_op e = load_op(ops, b0 + k);
+    staged = e.kind == XDRG_OP_BOOL ||
+             ((e.kind == XDRG_OP_U32 || e.kind == XDRG_OP_ENUM || e.kind == XDRG_OP_U64) &&
+              (e.noff & 3u) == 0);
+  }
+  if (staged) {
+    for (uint32_t i = 0; i < cnt; ++i) {
+      const uint64_t eb = eoff + static_cast<uint64_t>(i) * es;
+      uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+      if (eb <= heap_len && es <= heap_len - eb) {  // any byte alignment (ld16u note)
+        const uint8_t *q = heap + eb;
+        if (es == 4u) {
+          w0 = *reinterpret_cast<const uint32_t *>(q);
+        } else {
+          const uint2 a = *reinterpret_cast<const uint2 *>(q);
+          w0 = a.x; w1 = a.y;
+          if (es == 12u) w2 = *reinterpret_cast<const uint32_t *>(q + 8);
+          else if (es == 16u) { const uint2 c = *reinterpret_cast<const uint2 *>(q + 8); w2 = c.x; w3 = c.y; }
+        }
+      } else {  // past the heap: bytes read as 0, as unaligned_word does
+        w0 = unaligned_word(heap, heap_len, eb);
+        if (es > 4u) w1 = unaligned_word(heap, heap_len, eb + 4);
+        if (es > 8u) w2 = unaligned_word(heap, heap_len, eb + 8);
+        if (es > 12u) w3 = unaligned_word(heap, heap_len, eb + 12);
+      }
+      auto get = [&](uint32_t j) { return j == 0 ? w0 : j == 1 ? w1 : j == 2 ? w2 : w3; };
+      for (uint32_t k = 0; k < nb; ++k) {
+        const xdrg_op e = load_op(ops, b0 + k);
+        if (e.depth > stack_limit) { report(err, r, b0 + k, XDRG_ERR_STACK_PUT); return false; }
+        const uint32_t wb = e.kind == XDRG_OP_U64 ? 8u : 4u;
+        if (wb > cap - min(pos, cap)) { report(err, r, b0 + k, XDRG_ERR_OVERFLOW_PUT); return false; }
+        const uint32_t j = e.noff >> 2;
+        if (e.kind == XDRG_OP_BOOL) {
+          put(at, ((get(j) >> (8u * (e.noff & 3u))) & 0xffu) ? 0x01000000u : 0u);
+        } else if (e.kind == XDRG_OP_U64) {
+          put(at, bswap32(get(j + 1)));
+          put(at + 4, bswap32(get(j)));
+        } else {
+          put(at, bswap32(get(j)));
+        }
+        at += wb;
+        pos += wb;
+      }
+    }
+    return true;
+  }
   for (uint32_t i = 0; i < cnt; ++i) {
     const uint64_t eb = eoff + static_cast<uint64_t>(i) * es;
     for (uint32_t k = 0; k < nb; ++k) {
