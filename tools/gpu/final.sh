@@ -19,4 +19,4 @@ for sch in numerics recvar rpc vecrec; do
 done
 timeout -k 10 300 python bench.py --n 16777216 --steps 10 --warmup 3 --no-cpu-baseline --cold > $O/bench_16m.log 2>&1 || { tail $O/bench_16m.log; exit 1; }
 tail -1 $O/bench_16m.log | cut -c1-120
-PROF_TAG=$T bash tools/gpu/r01_prof.sh
+[ -n "$NO_PROF" ] || PROF_TAG=$T bash tools/gpu/r01_prof.sh
