@@ -9,6 +9,14 @@ Inputs are resident in HBM before timing.  Multi-GPU: one process per GPU
 bracketed by barrier + synchronize and the max over ranks is reported.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--n RECORDS]
+
+With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py starts
+the N rank processes itself (torch.distributed.run as a child process,
+before anything touches the GPU) and exits with its status; under an
+external launcher WORLD_SIZE must equal N.  Records per GPU default to
+1,048,576 at N = 1 (BASELINE.json config 2) and 2,097,152 at N > 1
+(config 5: 16M records over 8 GPUs, seed 0x5EED0005 over the global
+record index).
 """
 from __future__ import annotations
 
@@ -16,6 +24,7 @@ import argparse
 import hashlib
 import json
 import os
+import socket
 import subprocess
 import sys
 import time
@@ -41,14 +50,15 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--n", type=int, default=1 << 20, help="records per GPU")
+    ap.add_argument("--n", type=int, default=None,
+                    help="records per GPU (default 1M at N=1, 2M at N>1: BASELINE.json configs 2 and 5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--host-inclusive", action="store_true",
                     help="also measure pinned host->device->host rates (PCIe-bound, reported apart)")
     ap.add_argument("--cold", action="store_true",
                     help="also time each kernel alone after evicting the caches")
-    ap.add_argument("--gather", action="store_true",
-                    help="also time an RCCL gather of encoded shards to rank 0 (reported apart)")
+    ap.add_argument("--no-gather", action="store_true",
+                    help="N>1: skip the RCCL gather of the encoded shards to rank 0 (timed apart)")
     ap.add_argument("--msgs", action="store_true",
                     help="also time the record-marked message path (xdr_to_msg per record, the "
                          "device record index from the marks, xdr_from_msg per message)")
@@ -61,6 +71,31 @@ def parse():
                     help="rec128 is the headline; numerics/recvar/rpc measure BASELINE.json "
                          "configs 1, 3, 4; vecrec covers xvector<T>/pointer<T>")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def rank_command(gpus: int, port: int, argv: list[str]) -> list[str]:
+    """The torch.distributed.run command that starts one bench rank per GPU."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + argv
+
+
+def launch_ranks(args) -> int | None:
+    """--gpus N > 1 without a launcher: run the N ranks as a child process
+    group and return its exit status (None: this process is a rank)."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        return subprocess.call(rank_command(args.gpus, _free_port(), sys.argv[1:]), env=env)
+    world = int(env_world or "1")
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    return None
 
 
 def dist_init(args):
@@ -81,44 +116,147 @@ def barrier(dist):
         dist.barrier()
 
 
-def cpu_baseline(schema: str, n_records: int, threads: int) -> dict | None:
-    """The reference's CPU marshaler on this host: oracle/_ref/ref_golden
-    (xdrpp/marshal.cc compiled from the reference sources) when present,
-    else the C restatement in oracle/ (single thread)."""
-    ref = os.path.join(ROOT, "oracle", "_ref", "ref_golden")
-    if os.path.exists(ref) and os.access(ref, os.X_OK):
-        reps = 10
-        out = subprocess.run([ref, "bench", schema, str(n_records), str(threads), str(reps)],
-                             capture_output=True, text=True, timeout=600)
-        if out.returncode == 0:
-            r = json.loads(out.stdout.strip().splitlines()[-1])
-            return {"value": round(r["encode_decode_gib_s"], 4), "unit": "GiB/s", "cores": threads,
-                    "kind": "reference",
-                    "sample": f"{schema} x {n_records} (the full batch), xdr_put/xdr_get streams over "
-                              f"{threads} contiguous slices, best of {reps}; per-record "
-                              f"xdr_to_opaque {r['to_opaque_gib_s']:.3f} GiB/s",
-                    "encode_gib_s": round(r["encode_gib_s"], 4),
-                    "decode_gib_s": round(r["decode_gib_s"], 4)}
+def host_cpus() -> dict:
+    """The host's CPUs as this process sees them: nproc, the affinity mask,
+    the cgroup CPU quota (cores), and the model name."""
+    info = {"nproc": os.cpu_count() or 1, "affinity": len(os.sched_getaffinity(0)), "cgroup_quota": None,
+            "cpu_model": None}
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            info["cgroup_quota"] = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                info["cpu_model"] = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return info
+
+
+def _port_baseline(schema: str, n: int, threads: int, reps: int, nat, heap) -> dict:
+    """The committed C restatement (oracle/xdr_oracle.c) on `threads`
+    pthreads over contiguous slices (oracle/cpu_bench.c)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_bridge as O
-
     plan = __import__("xdrpp_amd.xdr_types", fromlist=["compile_plan"]).compile_plan(S.ALL[schema])
-    ns = min(n_records, 1 << 18)
-    nat, heap = W.GENERATORS[schema](ns)
-    t0 = time.perf_counter()
-    x, offs = O.encode(plan, nat, ns, heap)
-    t1 = time.perf_counter()
-    O.decode(plan, x, ns, None if plan.fixed_size else offs)
-    t2 = time.perf_counter()
-    return {"value": round(2 * x.size / GIB / (t2 - t0), 4), "unit": "GiB/s", "cores": 1,
-            "kind": "port", "sample": f"{schema} x {ns}, oracle/xdr_oracle.c, 1 thread",
-            "encode_gib_s": round(x.size / GIB / (t1 - t0), 4),
-            "decode_gib_s": round(x.size / GIB / (t2 - t1), 4)}
+    L = O.lib()
+    vp, u32, u64 = A.C.c_void_p, A.C.c_uint32, A.C.c_uint64
+    L.xdro_bench.argtypes = [vp, u32, vp, u32, vp, u64, vp, u64, vp, u64, vp, u32, u32, vp]
+    L.xdro_bench.restype = A.C.c_int
+    sizes = np.zeros(n, dtype=np.uint32)
+    X = n * plan.fixed_size if plan.fixed_size else None
+    if X is None:
+        X = int(O.sizes(plan, nat, n).astype(np.int64).sum())
+    out = np.zeros(max(X, 4), dtype=np.uint8)
+    back = np.zeros(n * plan.stride, dtype=np.uint8)
+    res = np.zeros(8, dtype=np.float64)
+    p = lambda a: a.ctypes.data if a is not None and a.size else None  # noqa: E731
+    rc = L.xdro_bench(p(plan.ops), len(plan.ops), p(plan.table), plan.stride, p(nat), n, p(heap),
+                      0 if heap is None else heap.size, p(out), out.size, p(back), threads, reps, p(res))
+    if rc != 0:
+        raise RuntimeError(f"xdro_bench failed ({rc})")
+    del sizes
+    gib = res[6] / GIB
+    r = {"encode_gib_s": gib / res[0], "decode_gib_s": gib / res[2], "to_opaque_gib_s": gib / res[4],
+         "encode_decode_gib_s": 2 * gib / (res[0] + res[2]),
+         "encode_decode_gib_s_median": 2 * gib / (res[1] + res[3]), "threads": threads}
+    man = os.path.join(ROOT, "tests", "golden", "manifest.json")
+    h = json.load(open(man))["hashes"].get(f"{schema}_{n}") if os.path.exists(man) else None
+    if h is not None:
+        r["bit_exact_vs_reference"] = hashlib.sha256(out[:X].tobytes()).hexdigest() == h["xdr"]
+    return r
 
 
-def host_inclusive(mar, plan, nat_dev, n, W_, reps=5, nstreams=2, chunk_records=1 << 17):
-    """Pinned host -> device -> encode -> host, chunked over streams (and the
-    decode direction).  PCIe-bound; reported apart, never as `value`."""
+def _ref_baseline(schema: str, n: int, threads: int, reps: int) -> dict | None:
+    """The real reference (oracle/_ref/ref_golden: xdrpp/marshal.cc compiled
+    by build() in the container, shipped with the tree) on `threads`
+    std::threads."""
+    ref = os.path.join(ROOT, "oracle", "_ref", "ref_golden")
+    if not (os.path.exists(ref) and os.access(ref, os.X_OK)):
+        return None
+    out = subprocess.run([ref, "bench", schema, str(n), str(threads), str(reps)],
+                         capture_output=True, text=True, timeout=600)
+    if out.returncode != 0:
+        return {"error": out.stderr[-200:]}
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    return {k: r[k] for k in ("encode_gib_s", "decode_gib_s", "to_opaque_gib_s", "encode_decode_gib_s",
+                              "threads")}
+
+
+def cpu_baseline(schema: str, n_records: int, threads: int = 0) -> dict:
+    """The reference's CPU marshaler on this host, on the same workload:
+    the real reference (oracle/_ref) when the tree carries it, and always
+    the committed C restatement (oracle/cpu_bench.c).  One thread per host
+    core (the affinity mask; also the cgroup quota when that is smaller),
+    best of `reps` over the whole batch."""
+    cpus = host_cpus()
+    counts = [threads] if threads else sorted({cpus["affinity"], cpus["cgroup_quota"] or cpus["affinity"], 1})
+    reps = 5
+    nat, heap = W.GENERATORS[schema](n_records)
+    runs = {"port": {}, "reference": {}}
+    for t in counts:
+        runs["port"][t] = _port_baseline(schema, n_records, t, reps, nat, heap)
+        ref = _ref_baseline(schema, n_records, t, reps)
+        if ref is not None:
+            runs["reference"][t] = ref
+    kind = "reference" if runs["reference"] and all("error" not in v for v in runs["reference"].values()) \
+        else "port"
+    best_t = max(runs[kind], key=lambda t: runs[kind][t]["encode_decode_gib_s"])
+    best = runs[kind][best_t]
+    return {"value": round(best["encode_decode_gib_s"], 3), "unit": "GiB/s", "cores": best_t, "kind": kind,
+            "sample": f"{schema} x {n_records} (the whole batch): xdr_put / xdr_get streams over {best_t} "
+                      f"contiguous slices, one thread each, best of {reps}",
+            "nproc": cpus["nproc"], "affinity_cpus": cpus["affinity"], "cgroup_quota_cpus": cpus["cgroup_quota"],
+            "cpu_model": cpus["cpu_model"],
+            "encode_gib_s": round(best["encode_gib_s"], 3), "decode_gib_s": round(best["decode_gib_s"], 3),
+            "to_opaque_gib_s": round(best["to_opaque_gib_s"], 3),
+            "by_threads": {k: {str(t): round(v["encode_decode_gib_s"], 3) for t, v in runs[k].items()}
+                           for k in runs if runs[k]},
+            "port_bit_exact_vs_reference": runs["port"][best_t if best_t in runs["port"] else counts[0]]
+            .get("bit_exact_vs_reference")}
+
+
+def pcie_ceiling(nbytes: int, dev, reps=5, chunk=16 << 20, nstreams=4) -> dict:
+    """Raw pinned hipMemcpyAsync bandwidth on this box, chunked over
+    `nstreams` streams like the host-inclusive legs: H2D alone, D2H alone
+    and both directions at once (full duplex).  GiB/s, best of reps."""
+    h_src = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    h_dst = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    d_a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    d_b = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    streams = [torch.cuda.Stream() for _ in range(nstreams)]
+
+    def run(h2d: bool, d2h: bool) -> float:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for ci, o in enumerate(range(0, nbytes, chunk)):
+            e = min(o + chunk, nbytes)
+            with torch.cuda.stream(streams[ci % nstreams]):
+                if h2d:
+                    d_a[o:e].copy_(h_src[o:e], non_blocking=True)
+                if d2h:
+                    h_dst[o:e].copy_(d_b[o:e], non_blocking=True)
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0
+
+    run(True, True)
+    g = nbytes / GIB
+    h2d = g / min(run(True, False) for _ in range(reps))
+    d2h = g / min(run(False, True) for _ in range(reps))
+    both = 2 * g / min(run(True, True) for _ in range(reps))
+    return {"h2d_gib_s": round(h2d, 2), "d2h_gib_s": round(d2h, 2), "duplex_gib_s": round(both, 2),
+            "bytes": nbytes, "chunk_bytes": chunk, "streams": nstreams}
+
+
+def host_inclusive(mar, plan, nat_dev, n, W_, reps=5, nstreams=4, chunk_records=1 << 17):
+    """Pinned host -> device -> encode -> host, chunked over `nstreams`
+    streams so that chunk k's D2H runs while chunk k+1's H2D and kernel run
+    (both copy directions at once), and the decode mirror.  PCIe-bound;
+    reported apart, never as `value`, next to the raw copy ceiling."""
     S_ = plan.stride
     h_nat = torch.empty(n * S_, dtype=torch.uint8, pin_memory=True)
     h_nat.copy_(nat_dev.cpu())
@@ -160,7 +298,9 @@ def host_inclusive(mar, plan, nat_dev, n, W_, reps=5, nstreams=2, chunk_records=
     xb = n * W_
     return {"encode_gib_s": round(xb / GIB / te, 2), "decode_gib_s": round(xb / GIB / td, 2),
             "encode_decode_gib_s": round(2 * xb / GIB / (te + td), 2), "round_trip_ok": bool(ok),
-            "chunk_records": chunk_records, "streams": nstreams}
+            "chunk_records": chunk_records, "streams": nstreams,
+            "pcie_ceiling": pcie_ceiling(max(n * S_, xb), nat_dev.device, chunk=chunk_records * W_,
+                                         nstreams=nstreams)}
 
 
 def host_inclusive_var(mar, plan, nat_dev, heap_dev, n, reps=3):
@@ -398,9 +538,12 @@ def setup(schema, n, dev, rank, world):
 
 def main():
     args = parse()
+    rc = launch_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
     dist, world, rank, local = dist_init(args)
     dev = torch.device("cuda", local)
-    n = args.n
+    n = args.n if args.n is not None else (1 << 20 if world == 1 else 1 << 21)
     plan, mar, nat, heap, xdr, back, offsets, heap_out = setup(args.schema, n, dev, rank, world)
     S_ = plan.stride
     X = xdr.numel()
@@ -432,10 +575,6 @@ def main():
     torch.cuda.synchronize()
     barrier(dist)
     elapsed = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
     mar.check(s)
     enc_ms = [e[0].elapsed_time(e[1]) for e in evs]
     dec_ms = [e[1].elapsed_time(e[2]) for e in evs]
@@ -452,40 +591,17 @@ def main():
         mar.launch_encode(back, n, x2, heap=heap_out, offsets=o2, stream=s)
         mar.check(s)
         ok_rt = bool(torch.equal(x2, xdr))
-    bit_exact = None
+        del x2, o2
     man = os.path.join(ROOT, "tests", "golden", "manifest.json")
-    key = f"{args.schema}_{n}"
-    if world == 1 and os.path.exists(man):
-        hashes = json.load(open(man))["hashes"]
-        if key in hashes:
-            bit_exact = hashlib.sha256(xdr.cpu().numpy().tobytes()).hexdigest() == hashes[key]["xdr"]
+    hashes = json.load(open(man))["hashes"] if os.path.exists(man) else {}
+    bit_exact = None
+    if world == 1 and f"{args.schema}_{n}" in hashes:
+        bit_exact = hashlib.sha256(xdr.cpu().numpy().tobytes()).hexdigest() == hashes[f"{args.schema}_{n}"]["xdr"]
 
-    gather_ms = None
-    if args.gather and dist is not None:
-        torch.cuda.synchronize()
-        barrier(dist)
-        g0 = time.perf_counter()
-        SH.gather_streams(dist, xdr, offsets, rank, world)
-        torch.cuda.synchronize()
-        gather_ms = (time.perf_counter() - g0) * 1e3
-
-    # whole-job bytes: shards of var-length schemas differ in size
-    X_all = X * world
-    if dist is not None:
-        t = torch.tensor([X], dtype=torch.int64, device=dev)
-        dist.all_reduce(t)
-        X_all = int(t.item())
-
-    if rank != 0:
-        if dist is not None:
-            dist.destroy_process_group()
-        return
-
-    xdr_bytes_step = 2 * X_all
-    value = xdr_bytes_step / GIB / (elapsed / args.steps)
+    # dominant kernel and its algorithmic bytes per launch
     if plan.is_fixed:
-        # dominant kernel: k_fixed_reg / k_fixed_lds (encode and decode are
-        # the same kernel with the encode / decode permutation programs)
+        # encode and decode are the same kernel with the encode / decode
+        # permutation programs
         info = A.XdrgPlanInfo()
         A.check(A.lib().xdrg_plan_get_info(plan.handle, A.C.byref(info)), "xdrg_plan_get_info")
         kern = ("k_fixed_reg" if plan.path == A.PATH_FIXED_REG else
@@ -505,9 +621,55 @@ def main():
             kern, alg_bytes, launches = "k_var_size+k_scan_blocks+k_var_encode_i", enc_alg, enc_ms
         else:
             kern, alg_bytes, launches = "k_var_decode_w", dec_alg, dec_ms
-    med = float(np.median(launches))
     avg = float(np.mean(launches))
     achieved = alg_bytes / (avg * 1e-3) / 1e9
+
+    # per-rank figures (max over ranks for the step time)
+    mine = torch.tensor([elapsed, float(np.mean(enc_ms)), float(np.mean(dec_ms)), float(X), achieved,
+                         float(ok_rt)], dtype=torch.float64, device=dev)
+    if dist is not None:
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        ranks = torch.stack(allr).cpu().numpy()
+    else:
+        ranks = mine.cpu().numpy()[None, :]
+    elapsed = float(ranks[:, 0].max())
+    X_all = int(ranks[:, 3].sum())
+    ok_rt = bool(ranks[:, 5].all())
+
+    gather = None
+    if dist is not None and not args.no_gather:
+        # the one collective: every shard's stream (and
+        # record index) to rank 0 over RCCL, timed apart from the marshal step
+        torch.cuda.synchronize()
+        barrier(dist)
+        g0 = time.perf_counter()
+        g_stream, g_index = SH.gather_streams(dist, xdr, offsets, rank, world)
+        torch.cuda.synchronize()
+        g_s = time.perf_counter() - g0
+        t = torch.tensor([g_s], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        g_s = float(t.item())
+        if rank == 0:
+            recv = X_all - X
+            gather = {"gather_ms": round(g_s * 1e3, 3), "bytes_to_root": recv,
+                      "root_inbound_gib_s": round(recv / GIB / g_s, 2),
+                      "encode_plus_gather_gib_s": round(X_all / GIB / (float(ranks[:, 1].max()) * 1e-3 + g_s), 2),
+                      "collective": "torch.distributed.gather (RCCL over xGMI)"}
+            key = f"{args.schema}_mgpu_{n * world}"
+            if key in hashes:
+                gather["bit_exact_vs_reference"] = (
+                    hashlib.sha256(g_stream.cpu().numpy().tobytes()).hexdigest() == hashes[key]["xdr"])
+                bit_exact = gather["bit_exact_vs_reference"]
+        del g_stream, g_index
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    xdr_bytes_step = 2 * X_all
+    value = xdr_bytes_step / GIB / (elapsed / args.steps)
     traffic = None
     tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tf):
@@ -519,7 +681,7 @@ def main():
                 traffic = int(sum(parts))  # multi-kernel phases: sum of their launches
         except Exception:
             traffic = None
-    wl = {"rec128": "rec128: 1M fixed-width 128-byte XDR records per GPU",
+    wl = {"rec128": "rec128: fixed-width 128-byte XDR records",
           "numerics": "numerics (tests/xdrtest.x) fixed 44-byte records, 56-byte native",
           "recvar": "recvar: opaque<256> + string<64> variable-length records",
           "rpc": "rpc_msg (xdrpp/rpc_msg.x) nested discriminated unions",
@@ -539,20 +701,26 @@ def main():
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic (splitmix64 seeds 0x5EED000x per SURVEY.md §8(d); FP fields as raw bit patterns)",
-        "config": {"workload": wl + ", encode (xdr_to_opaque) + decode (xdr_from_opaque), device-resident",
-                   "schema": args.schema, "records_per_gpu": n, "xdr_bytes_per_gpu": X,
-                   "native_stride": S_, "parallelism": f"dp{world}"},
+        "config": {"workload": f"{wl}, {n} records per GPU x {world} GPU(s), encode (xdr_to_opaque) + "
+                               "decode (xdr_from_opaque), device-resident",
+                   "schema": args.schema, "records_per_gpu": n, "records_total": n * world,
+                   "xdr_bytes_per_gpu": X, "native_stride": S_, "parallelism": f"dp{world}"},
         "encode_ms": round(float(np.mean(enc_ms)), 4),
         "decode_ms": round(float(np.mean(dec_ms)), 4),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "kernel": kern, "median_launch_ms": round(med, 4),
+                     "traffic": traffic, "kernel": kern, "median_launch_ms": round(float(np.median(launches)), 4),
                      "alg_bytes_per_launch": alg_bytes},
         "round_trip_ok": ok_rt,
         "bit_exact_vs_reference": bit_exact,
     }
-    if gather_ms is not None:
-        line["gather_ms"] = round(gather_ms, 3)
+    if world > 1:
+        line["per_rank"] = [{"rank": r, "gib_s": round(2 * row[3] / GIB / (row[0] / args.steps), 2),
+                             "encode_ms": round(row[1], 4), "decode_ms": round(row[2], 4),
+                             "roofline_frac": round(row[4] / HBM_PEAK_GBS, 4)}
+                            for r, row in enumerate(ranks)]
+    if gather is not None:
+        line["gather"] = gather
     if world == 1 and args.cold and plan.is_fixed:
         line["cold_cache"] = cold_cache(mar, nat, xdr, back, n, alg_bytes)
         mar.check(s)
@@ -567,9 +735,8 @@ def main():
         except Exception as e:  # reported, never fatal
             line["host_inclusive"] = {"error": str(e)[:200]}
     if world == 1 and not args.no_cpu_baseline:
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         try:
-            line["cpu_baseline"] = cpu_baseline(args.schema, n, threads)
+            line["cpu_baseline"] = cpu_baseline(args.schema, n, args.cpu_threads)
         except Exception as e:
             line["cpu_baseline"] = {"error": str(e)[:200]}
     print(json.dumps(line), flush=True)

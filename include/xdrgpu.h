@@ -58,7 +58,7 @@
 extern "C" {
 #endif
 
-#define XDRG_ABI_VERSION 3
+#define XDRG_ABI_VERSION 4
 
 /* ---------------------------------------------------------------------- */
 /* Plan ops: a flat, wire-ordered walk of xdr_traits<T>::save.             */
@@ -230,13 +230,34 @@ int xdrg_abi_version(void);
 /* Validate and compile an immutable plan.  `table` holds enum value lists
  * and union case tables referenced by the ops.  native_stride is the byte
  * distance between consecutive native records.  Host-only: the plan's
- * device tables are uploaded (synchronously, to the current device) by its
- * first encode/decode/serial_sizes call, so run one launch before capturing
- * a plan's launches into a hipGraph. */
+ * device tables are uploaded (synchronously) to each device by its first
+ * launch on that device, so run one launch per device before capturing a
+ * plan's launches into a hipGraph.  A plan of 65535 or more ops is
+ * XDRG_EUNSUPPORTED (status keys hold a 16-bit op index). */
 int xdrg_plan_create(const xdrg_op *ops, uint32_t nops, const uint32_t *table,
                      uint32_t ntable, uint32_t native_stride, xdrg_plan **out);
 void xdrg_plan_destroy(xdrg_plan *plan);
 int xdrg_plan_get_info(const xdrg_plan *plan, xdrg_plan_info *info);
+
+/* Launch options of one plan (no reference counterpart: kernel choices and
+ * launch shapes, for tests and tuning).  Every option defaults to the
+ * automatic choice.  Options belong to the plan, not to the process; set
+ * them before the plan is shared between threads.  Returns XDRG_EINVAL for
+ * an unknown option or value. */
+enum xdrg_plan_option {
+  XDRG_OPT_VAR_ENCODE_KERNEL = 1, /* 0 auto, 1 per-lane walk, 3 chunk-map image   */
+  XDRG_OPT_VAR_DECODE_KERNEL = 2, /* 0 auto, 1 per-lane walk, 2 LDS window         */
+  XDRG_OPT_FIXED_PATH = 3,        /* 0 auto, 2 LDS kernel for non-identity layouts */
+  XDRG_OPT_IMAGE_BYTES = 4,       /* var encode LDS image per wave, -1 auto        */
+  XDRG_OPT_WINDOW_BYTES = 5,      /* var decode LDS window per wave, -1 auto       */
+  XDRG_OPT_ENC_UNROLL = 6,        /* payload chunks in flight per lane: 4, 8, 16   */
+  XDRG_OPT_DEC_READAHEAD = 7,     /* window decode 32-byte read-ahead: 0 / 1       */
+  XDRG_OPT_SIZE_LINEAR = 8,       /* walk-free size pass for linear plans: 0 / 1   */
+  XDRG_OPT_GRP_UNROLL = 9,        /* fixed group kernel chunks in flight, 0 auto   */
+  XDRG_OPT_GRP_BLOCKS = 10,       /* fixed group kernel workgroups, 0 auto         */
+  XDRG_OPT_GRP_NONTEMPORAL = 11   /* fixed group kernel non-temporal stores: 0 / 1 */
+};
+int xdrg_plan_set_option(xdrg_plan *plan, int option, int64_t value);
 
 /* Workspace bytes encode (var plans), encode_msgs (any plan) and
  * serial_sizes need for n records. */

@@ -28,6 +28,7 @@ BIN = os.path.join(HERE, "_ref", "ref_golden")
 SMALL = {"numerics": 1000, "rec128": 1024, "recvar": 1024, "rpc": 1024, "vecrec": 1024}
 FULL = {"rec128": 1 << 20, "recvar": 1 << 20, "rpc": 1 << 20, "numerics": 1 << 16,
         "rec128_mgpu": 1 << 24}
+FULL2 = {"numerics": 1 << 20}  # second full-size entries (dict keys are unique per schema)
 MID = {"recvar": 1 << 16, "rpc": 1 << 16, "vecrec": 1 << 16}
 EXTS = ("native", "heap", "xdr", "offsets", "msgs", "msgoffs")
 NOMSGS = {"rec128_mgpu"}  # 16M records: messages hashed only where they are tested
@@ -89,7 +90,30 @@ def depth_fixtures() -> None:
                                os.path.join(GOLD, f"{schema}_{n}.depths")])
 
 
+def full_hashes(manifest: dict, entries) -> None:
+    """sha256 of the reference's outputs for (schema, n) batches."""
+    with tempfile.TemporaryDirectory() as td:
+        for schema, n in entries:
+            pre = os.path.join(td, f"{schema}_{n}")
+            extra = ["nomsgs"] if schema in NOMSGS else []
+            subprocess.check_call([BIN, "gen", schema, str(n), pre] + extra)
+            exts = [e for e in EXTS if os.path.exists(pre + "." + e)]
+            manifest["hashes"][f"{schema}_{n}"] = {
+                "n": n, **{e: sha(pre + "." + e) for e in exts},
+                "xdr_bytes": os.path.getsize(pre + ".xdr")}
+            for e in exts:
+                os.remove(pre + "." + e)
+
+
 def main() -> int:
+    if "--only-full" in sys.argv:  # --only-full schema:n [schema:n ...]
+        mp = os.path.join(GOLD, "manifest.json")
+        manifest = json.load(open(mp))
+        i = sys.argv.index("--only-full")
+        full_hashes(manifest, [(a.split(":")[0], int(a.split(":")[1])) for a in sys.argv[i + 1:]])
+        with open(mp, "w") as f:
+            json.dump(manifest, f, indent=1, sort_keys=True)
+        return 0
     if "--only-depths" in sys.argv:
         depth_fixtures()
         return 0
@@ -112,18 +136,7 @@ def main() -> int:
         manifest["small"][schema] = {"n": n, "files": {e: f"{schema}_{n}.{e}" for e in EXTS},
                                      "xdr_bytes": os.path.getsize(pre + ".xdr")}
     subprocess.check_call([BIN, "kat", os.path.join(GOLD, "kat.json")])
-    with tempfile.TemporaryDirectory() as td:
-        for table in (FULL, MID):
-            for schema, n in table.items():
-                pre = os.path.join(td, f"{schema}_{n}")
-                extra = ["nomsgs"] if schema in NOMSGS else []
-                subprocess.check_call([BIN, "gen", schema, str(n), pre] + extra)
-                exts = [e for e in EXTS if os.path.exists(pre + "." + e)]
-                manifest["hashes"][f"{schema}_{n}"] = {
-                    "n": n, **{e: sha(pre + "." + e) for e in exts},
-                    "xdr_bytes": os.path.getsize(pre + ".xdr")}
-                for e in exts:
-                    os.remove(pre + "." + e)
+    full_hashes(manifest, [kv for table in (FULL, FULL2, MID) for kv in table.items()])
     rpc_fixtures(manifest)
     depth_fixtures()
     with open(os.path.join(GOLD, "manifest.json"), "w") as f:

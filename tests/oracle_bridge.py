@@ -20,17 +20,18 @@ REF_BIN = os.path.join(ORACLE_DIR, "_ref", "ref_golden")
 _lib = None
 
 
+SOURCES = [os.path.join(ORACLE_DIR, "xdr_oracle.c"), os.path.join(ORACLE_DIR, "cpu_bench.c")]
+
+
 def build() -> None:
-    src = os.path.join(ORACLE_DIR, "xdr_oracle.c")
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
-    subprocess.check_call(["gcc", "-O2", "-fPIC", "-shared", "-std=c11", "-o", LIB, src])
+    subprocess.check_call(["gcc", "-O2", "-fPIC", "-shared", "-std=gnu11", "-pthread", "-o", LIB] + SOURCES)
 
 
 def lib() -> C.CDLL:
     global _lib
     if _lib is None:
-        src = os.path.join(ORACLE_DIR, "xdr_oracle.c")
-        if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(src):
+        if not os.path.exists(LIB) or any(os.path.getmtime(LIB) < os.path.getmtime(f) for f in SOURCES):
             build()
         L = C.CDLL(LIB)
         vp, u64, u32 = C.c_void_p, C.c_uint64, C.c_uint32
@@ -56,6 +57,17 @@ class OracleError(Exception):
     def __init__(self, code: int, record: int, op: int):
         super().__init__(f"oracle error code={code} record={record} op={op}")
         self.code, self.record, self.op = code, record, op
+
+
+def sizes(plan, native: np.ndarray, n: int) -> np.ndarray:
+    """xdr_size of every record (uint32 [n]) or raises OracleError."""
+    out = np.zeros(max(n, 1), dtype=np.uint32)
+    er, eo = C.c_uint64(0), C.c_uint32(0)
+    rc = lib().xdro_sizes(_p(plan.ops), len(plan.ops), _p(plan.table), plan.stride, _p(native), n,
+                          _p(out), C.byref(er), C.byref(eo))
+    if rc:
+        raise OracleError(rc, er.value, eo.value)
+    return out[:n]
 
 
 def encode(plan, native: np.ndarray, n: int, heap: np.ndarray | None = None,

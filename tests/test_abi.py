@@ -114,3 +114,51 @@ def test_no_oracle_in_product_package():
                 txt = open(os.path.join(dp, f)).read()
                 assert "oracle_bridge" not in txt and "liboracle" not in txt, f
                 assert "/root/reference" not in txt, f
+
+
+def _create(ops: np.ndarray, stride: int):
+    L = A.lib()
+    h = C.c_void_p()
+    rc = L.xdrg_plan_create(ops.ctypes.data_as(C.POINTER(A.XdrgOp)), len(ops), None, 0, stride,
+                            C.byref(h))
+    return rc, h
+
+
+def test_plan_op_count_limit():
+    """Status keys carry a 16-bit op index (0xffff = record level): a plan of
+    65535 or more ops is refused, one just below the limit is accepted."""
+    L = A.lib()
+    for nops, want in ((0xFFFE, A.OK), (0xFFFF, -3), (0x10000, -3)):
+        ops = np.zeros(nops, dtype=OP_DTYPE)
+        ops["kind"] = A.OP_U32
+        ops["noff"] = 0
+        ops["depth"] = 1
+        ops[-1]["kind"] = A.OP_END
+        rc, h = _create(ops, 4)
+        assert rc == want, (nops, rc)
+        if rc == A.OK:
+            L.xdrg_plan_destroy(h)
+
+
+def test_plan_options_are_per_plan_and_validated():
+    """Launch options live on the plan (no process-global knobs): unknown
+    options and out-of-range values are refused."""
+    from xdrpp_amd import marshal as M
+    from xdrpp_amd import schemas as S
+    L = A.lib()
+    p = M.Plan(S.recvar, {"var_encode_kernel": 1, "image_bytes": 2048})
+    assert L.xdrg_plan_set_option(p.handle, 999, 0) == -1
+    assert L.xdrg_plan_set_option(p.handle, A.PLAN_OPTIONS["var_encode_kernel"], 2) == -1
+    assert L.xdrg_plan_set_option(p.handle, A.PLAN_OPTIONS["enc_unroll"], 5) == -1
+    assert L.xdrg_plan_set_option(p.handle, A.PLAN_OPTIONS["enc_unroll"], 16) == A.OK
+    with pytest.raises(A.AbiError):
+        M.Plan(S.recvar, {"var_decode_kernel": 7})
+
+
+def test_no_tuning_hooks_exported():
+    """Nothing but the header's entry points is exported with the xdrg_
+    prefix (no process-global tuning knobs)."""
+    out = subprocess.run(["nm", "-D", "--defined-only", A.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    syms = {line.split()[-1] for line in out.splitlines() if line.strip()}
+    assert {s for s in syms if s.startswith("xdrg")} == set(A.EXPORTED)

@@ -28,10 +28,12 @@ SCHEMAS = ["numerics", "rec128", "recvar", "rpc", "vecrec"]
 _plans = {}
 
 
-def plan(name):
-    if name not in _plans:
-        _plans[name] = M.Plan(S.ALL[name])
-    return _plans[name]
+def plan(name, **options):
+    """The plan of a schema, with launch options (xdrg_plan_set_option)."""
+    key = (name, tuple(sorted(options.items())))
+    if key not in _plans:
+        _plans[key] = M.Plan(S.ALL[name], options)
+    return _plans[key]
 
 
 def to_dev(a, dev):
@@ -225,19 +227,16 @@ KERNELS = {"per_lane": (1, 1), "image_window": (3, 2)}
 
 @pytest.fixture(params=list(KERNELS))
 def forced(request):
-    import ctypes as C
-    L = A.lib()
-    L.xdrg__force_var_kernels.argtypes = [C.c_int, C.c_int]
-    L.xdrg__force_var_kernels(*KERNELS[request.param])
-    yield request.param
-    L.xdrg__force_var_kernels(0, 0)
+    """Plan options forcing one encode and one decode kernel."""
+    enc, dec = KERNELS[request.param]
+    return {"var_encode_kernel": enc, "var_decode_kernel": dec}
 
 
 @pytest.mark.parametrize("name", ["recvar", "rpc", "vecrec", "rec128"])
 @pytest.mark.parametrize("seed", range(3))
 def test_decode_msgs_fuzzed_vs_oracle(dev, forced, name, seed):
     n = SMALL_N[name]
-    p = plan(name)
+    p = plan(name, **forced)
     mar = M.Marshaler(p, dev)
     x = golden(name, n, "msgs").copy()
     mo = golden(name, n, "msgoffs", np.uint64)
@@ -253,7 +252,7 @@ def test_decode_msgs_fuzzed_vs_oracle(dev, forced, name, seed):
 @pytest.mark.parametrize("name", ["recvar", "rpc", "vecrec", "numerics"])
 @pytest.mark.parametrize("n", [1, 63, 65, 1000])
 def test_msgs_kernels_vs_oracle(dev, forced, name, n):
-    p = plan(name)
+    p = plan(name, **forced)
     mar = M.Marshaler(p, dev)
     N = SMALL_N[name]
     heap = golden(name, N, "heap")
@@ -270,7 +269,7 @@ def test_msgs_kernels_vs_oracle(dev, forced, name, n):
 
 
 def test_encode_msgs_capacity(dev, forced):
-    p = plan("recvar")
+    p = plan("recvar", **forced)
     mar = M.Marshaler(p, dev)
     n = 300
     nat, heap = W.recvar(n)

@@ -26,11 +26,13 @@ SCHEMAS = ["numerics", "rec128", "recvar", "rpc", "vecrec"]
 _plans = {}
 
 
-def plan(name):
-    if name not in _plans:
+def plan(name, **options):
+    """The plan of a schema, with launch options (xdrg_plan_set_option)."""
+    key = (name, tuple(sorted(options.items())))
+    if key not in _plans:
         t = S.numerics_validated if name == "numerics_v" else S.ALL[name]
-        _plans[name] = M.Plan(t)
-    return _plans[name]
+        _plans[key] = M.Plan(t, options)
+    return _plans[key]
 
 
 def to_dev(a, dev):
@@ -80,7 +82,7 @@ def test_golden_decode(dev, name):
 # ------------------------------------------------------------- full size
 @pytest.mark.parametrize("name,n", [("rec128", 1 << 20), ("numerics", 1 << 16),
                                     ("recvar", 1 << 16), ("rpc", 1 << 16), ("vecrec", 1 << 16),
-                                    ("recvar", 1 << 20), ("rpc", 1 << 20)])
+                                    ("recvar", 1 << 20), ("rpc", 1 << 20), ("numerics", 1 << 20)])
 def test_full_size_hash(dev, manifest, name, n):
     h = manifest["hashes"][f"{name}_{n}"]
     p = plan(name)
@@ -99,6 +101,40 @@ def test_full_size_hash(dev, manifest, name, n):
         assert sha(res.offsets) == h["offsets"]
         res2 = mar.encode(back, n, bheap)
         assert torch.equal(res2.xdr, res.xdr)  # round trip is the identity on the wire
+
+
+def test_config5_16m_sharded(dev, manifest):
+    """BASELINE.json config 5 on one GPU: 16M rec128 records (seed
+    0x5EED0005 over the global record index), generated as the 8 shards of
+    2M records bench.py gives 8 ranks.  Encoding the shards one by one into
+    their slices of one stream (what 8 GPUs + the gather produce) and
+    encoding the whole batch in one launch both give the reference's bytes
+    (sha256 of xdr_to_opaque over all 16M records); decode round-trips."""
+    from xdrpp_amd import shard as SH
+    h = manifest["hashes"]["rec128_mgpu_16777216"]
+    world, per = 8, 1 << 21
+    p = plan("rec128")
+    mar = M.Marshaler(p, dev)
+    W_ = p.fixed_size
+    nat = torch.empty(world * per * p.stride, dtype=torch.uint8, device=dev)
+    hn = hashlib.sha256()
+    for r in range(world):
+        shard, _ = SH.shard_inputs("rec128", per, r, world)
+        hn.update(shard.tobytes())
+        nat[r * per * p.stride:(r + 1) * per * p.stride] = to_dev(shard, dev)
+    assert hn.hexdigest() == h["native"]
+    out = torch.empty(world * per * W_, dtype=torch.uint8, device=dev)
+    for r in range(world):
+        mar.status.init(M._stream())
+        mar.launch_encode(nat[r * per * p.stride:(r + 1) * per * p.stride], per,
+                          out[r * per * W_:(r + 1) * per * W_])
+        mar.check()
+    assert sha(out) == h["xdr"]
+    whole = mar.encode(nat, world * per)
+    assert torch.equal(whole.xdr, out)
+    del whole
+    back, _ = mar.decode(out, world * per)
+    assert torch.equal(back, nat)
 
 
 # -------------------------------------------------------------- KAT
@@ -329,23 +365,20 @@ def test_swaps(dev):
 
 
 # ------------------------------------- every var kernel, forced in turn
-KERNELS = {"per_lane": (1, 1), "record_image_window": (2, 2), "chunk_image_window": (3, 2)}
+KERNELS = {"per_lane": (1, 1), "chunk_image_window": (3, 2)}
 
 
 @pytest.fixture(params=list(KERNELS))
 def forced(request):
-    import ctypes as C
-    L = A.lib()
-    L.xdrg__force_var_kernels.argtypes = [C.c_int, C.c_int]
-    L.xdrg__force_var_kernels(*KERNELS[request.param])
-    yield request.param
-    L.xdrg__force_var_kernels(0, 0)
+    """Plan options forcing one encode and one decode kernel."""
+    enc, dec = KERNELS[request.param]
+    return {"var_encode_kernel": enc, "var_decode_kernel": dec}
 
 
 @pytest.mark.parametrize("name", ["recvar", "rpc", "vecrec"])
 @pytest.mark.parametrize("n", [1, 63, 65, 1024])
 def test_var_kernels_golden(dev, forced, name, n):
-    p = plan(name)
+    p = plan(name, **forced)
     mar = M.Marshaler(p, dev)
     N = SMALL_N[name]
     nat_all = golden(name, N, "native")
@@ -365,7 +398,7 @@ def test_var_kernels_golden(dev, forced, name, n):
 @pytest.mark.parametrize("seed", range(3))
 def test_var_kernels_fuzzed_errors(dev, forced, name, seed):
     n = SMALL_N[name]
-    p = plan(name)
+    p = plan(name, **forced)
     mar = M.Marshaler(p, dev)
     x = golden(name, n, "xdr").copy()
     offs = golden(name, n, "offsets", np.uint64)
@@ -381,7 +414,7 @@ def test_var_kernels_fuzzed_errors(dev, forced, name, seed):
 @pytest.mark.parametrize("name", ["recvar", "rpc", "vecrec"])
 def test_var_kernels_capacity_and_stack(dev, forced, name):
     n = 300
-    p = plan(name)
+    p = plan(name, **forced)
     mar = M.Marshaler(p, dev)
     nat, heap = W.GENERATORS[name](n)
     full, offs = O.encode(p.cp, nat, n, heap)
@@ -426,19 +459,14 @@ BOOLS = S.Struct("boolrec", [("a", S.Bool), ("b", S.Bool), ("c", S.Int), ("d", S
 
 @pytest.fixture(params=list(FIXED_PATHS))
 def fixed_path(request):
-    import ctypes as C
-    L = A.lib()
-    L.xdrg__force_fixed_path.argtypes = [C.c_int]
-    L.xdrg__force_fixed_path(FIXED_PATHS[request.param])
-    yield request.param
-    L.xdrg__force_fixed_path(0)
+    return {"fixed_path": FIXED_PATHS[request.param]}
 
 
 @pytest.mark.parametrize("n", [1, 3, 4, 5, 1000, 4099, 1 << 16])
 def test_fixed_group_numerics(dev, fixed_path, n):
     """numerics (56-byte native, 44-byte wire): full groups of 4 records on
     the group kernel, the tail on the LDS kernel; both paths bit-exact."""
-    p = plan("numerics")
+    p = plan("numerics", **fixed_path)
     nat, _ = W.numerics(n)
     want, _ = O.encode(p.cp, nat, n)
     mar = M.Marshaler(p, dev)
@@ -453,7 +481,7 @@ def test_fixed_group_bools(dev, fixed_path, n):
     """Several bools per native word (decode: 2 terms per word) and a bool
     in the record's last word (encode: the window's high word)."""
     cp = compile_plan(BOOLS)
-    p = M.Plan(BOOLS)
+    p = M.Plan(BOOLS, fixed_path)
     rng = np.random.default_rng(n)
     nat = rng.integers(0, 256, size=n * cp.stride, dtype=np.uint8)
     want, _ = O.encode(cp, nat, n)
@@ -472,15 +500,7 @@ def test_fixed_group_bools(dev, fixed_path, n):
 # ----------------------- chunk-map encode: LDS image sizes and unroll depths
 @pytest.fixture(params=[(-1, 8), (0, 8), (1024, 4), (4096, 16)], ids=lambda v: f"img{v[0]}_u{v[1]}")
 def enc_shape(request):
-    import ctypes as C
-    L = A.lib()
-    L.xdrg__set_image_bytes.argtypes = [C.c_int]
-    L.xdrg__set_enc_unroll.argtypes = [C.c_int]
-    L.xdrg__set_image_bytes(request.param[0])
-    old = L.xdrg__set_enc_unroll(request.param[1])
-    yield request.param
-    L.xdrg__set_image_bytes(-1)
-    L.xdrg__set_enc_unroll(old)
+    return {"image_bytes": request.param[0], "enc_unroll": request.param[1]}
 
 
 @pytest.mark.parametrize("name", ["recvar", "rpc", "vecrec"])
@@ -489,7 +509,7 @@ def test_encode_image_shapes(dev, enc_shape, name, n):
     """Every stretch byte goes through the LDS image or the direct global
     path (whole 16-byte chunks as one store); both, at every image size and
     unroll depth, give the reference's bytes."""
-    p = plan(name)
+    p = plan(name, **enc_shape)
     nat, heap = W.GENERATORS[name](n)
     want, offs = O.encode(p.cp, nat, n, heap)
     res = M.Marshaler(p, dev).encode(to_dev(nat, dev), n, to_dev(heap, dev) if heap.size else None)
@@ -499,15 +519,7 @@ def test_encode_image_shapes(dev, enc_shape, name, n):
 
 @pytest.fixture(params=[(-1, 1), (2048, 0), (16384, 1)], ids=lambda v: f"win{v[0]}_ra{v[1]}")
 def dec_shape(request):
-    import ctypes as C
-    L = A.lib()
-    L.xdrg__set_window_bytes.argtypes = [C.c_int]
-    L.xdrg__set_dec_readahead.argtypes = [C.c_int]
-    L.xdrg__set_window_bytes(request.param[0])
-    old = L.xdrg__set_dec_readahead(request.param[1])
-    yield request.param
-    L.xdrg__set_window_bytes(-1)
-    L.xdrg__set_dec_readahead(old)
+    return {"window_bytes": request.param[0], "dec_readahead": request.param[1]}
 
 
 @pytest.mark.parametrize("name", ["recvar", "rpc", "vecrec"])
@@ -516,7 +528,7 @@ def test_decode_window_shapes(dev, dec_shape, name, n):
     """Stream words inside the LDS window, past it through the 32-byte
     read-ahead, or past it word by word: the same records as the C
     restatement."""
-    p = plan(name)
+    p = plan(name, **dec_shape)
     nat, heap = W.GENERATORS[name](n)
     want, offs = O.encode(p.cp, nat, n, heap)
     back, bheap = M.Marshaler(p, dev).decode(to_dev(want, dev), n, to_dev(offs.view(np.int64), dev))
@@ -531,72 +543,49 @@ def test_size_pass_linear(dev, linear, n):
     """recvar is a linear plan (no unions/containers): its size pass reads
     the length words without a walk; both passes give xdr_size and the
     same encode."""
-    import ctypes as C
-    L = A.lib()
-    L.xdrg__set_size_linear.argtypes = [C.c_int]
-    old = L.xdrg__set_size_linear(linear)
-    try:
-        p = plan("recvar")
-        nat, heap = W.recvar(n)
-        want, offs = O.encode(p.cp, nat, n, heap)
-        mar = M.Marshaler(p, dev)
-        sz = mar.serial_sizes(to_dev(nat, dev), n).cpu().numpy().astype(np.uint64)
-        assert np.array_equal(sz, np.diff(offs))
-        res = mar.encode(to_dev(nat, dev), n, to_dev(heap, dev))
-        assert np.array_equal(res.xdr.cpu().numpy(), want)
-        msgs = mar.encode_msgs(to_dev(nat, dev), n, to_dev(heap, dev))
-        assert np.array_equal(msgs.xdr.cpu().numpy(), O.encode_msgs(p.cp, nat, n, heap)[0])
-    finally:
-        L.xdrg__set_size_linear(old)
+    p = plan("recvar", size_linear=linear)
+    nat, heap = W.recvar(n)
+    want, offs = O.encode(p.cp, nat, n, heap)
+    mar = M.Marshaler(p, dev)
+    sz = mar.serial_sizes(to_dev(nat, dev), n).cpu().numpy().astype(np.uint64)
+    assert np.array_equal(sz, np.diff(offs))
+    res = mar.encode(to_dev(nat, dev), n, to_dev(heap, dev))
+    assert np.array_equal(res.xdr.cpu().numpy(), want)
+    msgs = mar.encode_msgs(to_dev(nat, dev), n, to_dev(heap, dev))
+    assert np.array_equal(msgs.xdr.cpu().numpy(), O.encode_msgs(p.cp, nat, n, heap)[0])
 
 
-@pytest.mark.parametrize("fused", [1, 0])
 @pytest.mark.parametrize("name", ["recvar", "rpc", "vecrec"])
-@pytest.mark.parametrize("n", [1, 64, 65, 4099, 100003])
-def test_encode_fused_lookback(dev, fused, name, n):
-    """The one-kernel encode (in-kernel sizes + decoupled look-back over
-    64-record blocks) and the three-kernel one give the reference's bytes,
-    record index and total."""
-    import ctypes as C
-    L = A.lib()
-    L.xdrg__set_enc_fused.argtypes = [C.c_int]
-    old = L.xdrg__set_enc_fused(fused)
-    try:
-        p = plan(name)
-        nat, heap = W.GENERATORS[name](n)
-        want, offs = O.encode(p.cp, nat, n, heap)
-        mar = M.Marshaler(p, dev)
-        res = mar.encode(to_dev(nat, dev), n, to_dev(heap, dev) if heap.size else None)
-        assert np.array_equal(res.xdr.cpu().numpy(), want)
-        assert np.array_equal(res.offsets.cpu().numpy().view(np.uint64), offs)
-        m = mar.encode_msgs(to_dev(nat, dev), n, to_dev(heap, dev) if heap.size else None)
-        assert np.array_equal(m.xdr.cpu().numpy(), O.encode_msgs(p.cp, nat, n, heap)[0])
-    finally:
-        L.xdrg__set_enc_fused(old)
+@pytest.mark.parametrize("n", [64, 65, 4099, 100003])
+def test_encode_sizes_scan_index(dev, name, n):
+    """Size pass + block scan + encode: the reference's bytes, record index
+    and total, for batches that end inside a 64-record block and span
+    several scan tiles."""
+    p = plan(name)
+    nat, heap = W.GENERATORS[name](n)
+    want, offs = O.encode(p.cp, nat, n, heap)
+    mar = M.Marshaler(p, dev)
+    res = mar.encode(to_dev(nat, dev), n, to_dev(heap, dev) if heap.size else None)
+    assert np.array_equal(res.xdr.cpu().numpy(), want)
+    assert np.array_equal(res.offsets.cpu().numpy().view(np.uint64), offs)
+    m = mar.encode_msgs(to_dev(nat, dev), n, to_dev(heap, dev) if heap.size else None)
+    assert np.array_equal(m.xdr.cpu().numpy(), O.encode_msgs(p.cp, nat, n, heap)[0])
 
 
-@pytest.mark.parametrize("fused", [1, 0])
-def test_encode_fused_bad_discriminant(dev, fused):
-    """A bad discriminant found by the in-kernel size walk is reported at the
-    lowest failing record, as the size pass reports it."""
-    import ctypes as C
-    L = A.lib()
-    L.xdrg__set_enc_fused.argtypes = [C.c_int]
-    old = L.xdrg__set_enc_fused(fused)
-    try:
-        p = plan("rpc")
-        n = 5000
-        nat, heap = W.rpc(n)
-        rec = nat.reshape(n, p.stride).copy()
-        off = S.rpc_msg.offset_of("body")
-        for bad in (4321, 777):
-            rec[bad, off:off + 4] = np.frombuffer(np.uint32(9).tobytes(), np.uint8)
-        with pytest.raises(M.XdrBadDiscriminant) as ei:
-            M.Marshaler(p, dev).encode(to_dev(rec.reshape(-1), dev), n, to_dev(heap, dev))
-        assert ei.value.record == 777
-        assert str(ei.value) == "bad value of mtype in _body_t"
-    finally:
-        L.xdrg__set_enc_fused(old)
+def test_encode_bad_discriminant_lowest_record(dev):
+    """A bad discriminant found by the size pass is reported at the lowest
+    failing record, with the reference's what()."""
+    p = plan("rpc")
+    n = 5000
+    nat, heap = W.rpc(n)
+    rec = nat.reshape(n, p.stride).copy()
+    off = S.rpc_msg.offset_of("body")
+    for bad in (4321, 777):
+        rec[bad, off:off + 4] = np.frombuffer(np.uint32(9).tobytes(), np.uint8)
+    with pytest.raises(M.XdrBadDiscriminant) as ei:
+        M.Marshaler(p, dev).encode(to_dev(rec.reshape(-1), dev), n, to_dev(heap, dev))
+    assert ei.value.record == 777
+    assert str(ei.value) == "bad value of mtype in _body_t"
 
 
 # ------------------------------------------------- vector element layouts
@@ -646,7 +635,7 @@ def _ref(nat, r, off, start, cnt):
 @pytest.mark.parametrize("straddle", [False, True])
 @pytest.mark.parametrize("n", [1, 64, 257])
 def test_vector_element_layouts(dev, forced, n, straddle):
-    p = M.Plan(vshapes)
+    p = M.Plan(vshapes, forced)
     mar = M.Marshaler(p, dev)
     nat, heap = _vshapes_batch(n, 900 + n, straddle)
     # the oracle reads the heap unclamped: give it the zeros the GPU reads

@@ -1,6 +1,5 @@
 """A/B the var-path kernel families (group-copy vs record-image) in one
 process, interleaved (cdna_hip_programming.md §5.4 rule 24)."""
-import ctypes as C
 import json
 import os
 import sys
@@ -12,33 +11,27 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, ROOT)
 from xdrpp_amd import _abi as A, marshal as M, schemas as S, workloads as W  # noqa: E402
 
-L = A.lib()
-L.xdrg__force_var_kernels.argtypes = [C.c_int, C.c_int]
-L.xdrg__set_image_bytes.argtypes = [C.c_int]
-L.xdrg__set_window_bytes.argtypes = [C.c_int]
 # (encode kernel, decode kernel, encode LDS image bytes, decode LDS window
-# bytes); kernels as in xdrgpu.hip g_force_enc/g_force_dec: 0 auto,
-# 1 per-lane, 2 record image, 3 chunk-map image (encode) / 2 window (decode)
+# bytes[, encode unroll, decode read-ahead]) as plan options
+# (xdrg_plan_set_option): kernels 0 auto, 1 per-lane, 3 chunk-map image
+# (encode) / 2 window (decode); -1 bytes = automatic
 VARIANTS = [tuple(int(x) for x in v.split(",")) for v in
-            os.environ.get("VARIANTS", "2,2,4096,4096 3,2,4096,4096 3,2,2048,4096 3,2,0,4096 3,2,4096,2048").split()]
+            os.environ.get("VARIANTS", "3,2,-1,-1 3,2,4096,4096 3,2,0,4096 3,2,4096,2048 1,1,-1,-1").split()]
 
 
-L.xdrg__set_enc_unroll.argtypes = [C.c_int]
-L.xdrg__set_dec_readahead.argtypes = [C.c_int]
+def options(v):
+    return {"var_encode_kernel": v[0], "var_decode_kernel": v[1], "image_bytes": v[2],
+            "window_bytes": v[3], "enc_unroll": v[4] if len(v) > 4 else 8,
+            "dec_readahead": v[5] if len(v) > 5 else 1}
 
 
-def select(v):
-    L.xdrg__force_var_kernels(v[0], v[1])
-    L.xdrg__set_image_bytes(v[2])
-    L.xdrg__set_window_bytes(v[3])
-    L.xdrg__set_enc_unroll(v[4] if len(v) > 4 else 8)
-    L.xdrg__set_dec_readahead(v[5] if len(v) > 5 else 1)
 dev = torch.device("cuda:0")
 out = {}
 for schema in sys.argv[1:] or ["recvar", "rpc"]:
     n = 1 << 20
     plan = M.Plan(S.ALL[schema])
     mar = M.Marshaler(plan, dev)
+    mars = {v: M.Marshaler(M.Plan(S.ALL[schema], options(v)), dev) for v in VARIANTS}
     nat_np, heap_np = W.GENERATORS[schema](n)
     nat = torch.from_numpy(nat_np).to(dev)
     heap = torch.from_numpy(heap_np).to(dev)
@@ -51,7 +44,7 @@ for schema in sys.argv[1:] or ["recvar", "rpc"]:
     s = torch.cuda.current_stream().cuda_stream
     times = {v: ([], []) for v in VARIANTS}
     for v in VARIANTS:  # correctness + warmup
-        select(v)
+        mar = mars[v]
         mar.status.init(s)
         mar.launch_encode(nat, n, xdr, heap=heap, offsets=offs)
         mar.launch_decode(xdr, n, back, offsets=offs, heap_out=hout)
@@ -65,7 +58,7 @@ for schema in sys.argv[1:] or ["recvar", "rpc"]:
         assert torch.equal(x2, ref), f"{schema}: variant {v} decode->encode differs"
     for rnd in range(5):
         for v in VARIANTS:
-            select(v)
+            mar = mars[v]
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
             ev[0].record()
             for _ in range(5):
@@ -77,8 +70,8 @@ for schema in sys.argv[1:] or ["recvar", "rpc"]:
             torch.cuda.synchronize()
             times[v][0].append(ev[0].elapsed_time(ev[1]) / 5)
             times[v][1].append(ev[1].elapsed_time(ev[2]) / 5)
-    select((0, 0, -1, -1, 8))
-    mar.check()
+    for m in mars.values():
+        m.check()
     for v in VARIANTS:
         name = f"e{v[0]}d{v[1]}_i{v[2] // 1024}K_w{v[3] // 1024}K" + (f"_u{v[4]}" if len(v) > 4 else "") + (f"_ra{v[5]}" if len(v) > 5 else "")
         e, d = float(np.median(times[v][0])), float(np.median(times[v][1]))

@@ -1,7 +1,6 @@
 """A/B the group-path launch shape (k_fixed_grp) on numerics 1M encode and
 decode: U chunks in flight, workgroup cap, nontemporal stores.  Interleaved
 rounds in one process; HIP events around each launch, median."""
-import ctypes as C
 import os
 import sys
 
@@ -10,10 +9,8 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
-from xdrpp_amd import _abi as A, marshal as M, schemas as S, workloads as W  # noqa: E402
+from xdrpp_amd import marshal as M, schemas as S, workloads as W  # noqa: E402
 
-L = A.lib()
-L.xdrg__set_fixed_grp.argtypes = [C.c_int, C.c_int, C.c_int]
 dev = torch.device("cuda:0")
 n = int(os.environ.get("TUNE_N", 1 << 20))
 p = M.Plan(S.numerics)
@@ -25,11 +22,13 @@ s = torch.cuda.current_stream().cuda_stream
 ref = mar.encode(nat, n).xdr.clone()
 variants = [(u, b, nt) for u in (1, 2, 4) for b in (1024, 2048, 4096, 8192, 16384) for nt in (0, 1)]
 res = {v: ([], []) for v in variants}
+mars = {v: M.Marshaler(M.Plan(S.numerics, {"grp_unroll": v[0], "grp_blocks": v[1], "grp_nontemporal": v[2]}),
+                       dev) for v in variants}
 for rnd in range(15):
     for v in variants:
-        L.xdrg__set_fixed_grp(*v)
-        for k, f in ((0, lambda: mar.launch_encode(nat, n, xdr, stream=s)),
-                     (1, lambda: mar.launch_decode(xdr, n, back, stream=s))):
+        m = mars[v]
+        for k, f in ((0, lambda: m.launch_encode(nat, n, xdr, stream=s)),
+                     (1, lambda: m.launch_decode(xdr, n, back, stream=s))):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             f()
@@ -38,7 +37,6 @@ for rnd in range(15):
             res[v][k].append(e0.elapsed_time(e1))
         if rnd == 0:
             assert torch.equal(xdr, ref) and torch.equal(back, nat), v
-L.xdrg__set_fixed_grp(0, 0, 0)
 alg = n * 100
 rows = sorted(((np.median(a) + np.median(b)) / 2, v, np.median(a), np.median(b)) for v, (a, b) in res.items())
 for t, v, a, b in rows:

@@ -14,12 +14,17 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libxdrgpu.s
 
 # enum xdrg_op_kind
 OP_U32, OP_U64, OP_BOOL, OP_ENUM, OP_OPAQUE, OP_VAROPAQUE, OP_STRING, OP_UNION, OP_JUMP, OP_END, OP_VECTOR = range(1, 12)
-ABI_VERSION = 3  # XDRG_ABI_VERSION, include/xdrgpu.h
+ABI_VERSION = 4  # XDRG_ABI_VERSION, include/xdrgpu.h
 F_VALIDATE = 1
 F_DEFAULT = 2
 F_POINTER = 4
 
 PATH_FIXED_REG, PATH_FIXED_LDS, PATH_VAR = 1, 2, 3
+
+# enum xdrg_plan_option (xdrg_plan_set_option)
+PLAN_OPTIONS = {"var_encode_kernel": 1, "var_decode_kernel": 2, "fixed_path": 3, "image_bytes": 4,
+                "window_bytes": 5, "enc_unroll": 6, "dec_readahead": 7, "size_linear": 8,
+                "grp_unroll": 9, "grp_blocks": 10, "grp_nontemporal": 11}
 
 OK = 0
 API_ERRORS = {-1: "EINVAL", -2: "EALIGN", -3: "EUNSUPPORTED", -4: "EHIP", -5: "ENOMEM", -6: "ESPACE"}
@@ -109,6 +114,7 @@ EXPORTED = (
     "xdrg_decode_heap_size", "xdrg_encode_msgs", "xdrg_decode_msgs", "xdrg_index_msgs",
     "xdrg_index_workspace_size", "xdrg_rpc_dispatch", "xdrg_rpc_check_replies",
     "xdrg_rpc_replies", "xdrg_rpc_replies_workspace_size", "xdrg_record_depths",
+    "xdrg_plan_set_option",
 )
 
 # RPC header batches (include/xdrgpu.h "RPC header batches")
@@ -148,6 +154,8 @@ def lib() -> C.CDLL:
     L.xdrg_plan_destroy.restype = None
     L.xdrg_plan_get_info.argtypes = [vp, C.POINTER(XdrgPlanInfo)]
     L.xdrg_plan_get_info.restype = C.c_int
+    L.xdrg_plan_set_option.argtypes = [vp, C.c_int, C.c_int64]
+    L.xdrg_plan_set_option.restype = C.c_int
     L.xdrg_workspace_size.argtypes = [vp, u64]
     L.xdrg_workspace_size.restype = sz
     L.xdrg_status_init.argtypes = [vp, vp]

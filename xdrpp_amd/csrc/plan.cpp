@@ -336,6 +336,7 @@ int compile_plan(xdrg_plan &p) {
   if (p.stride % 4) return XDRG_EUNSUPPORTED;  // word-granular native records
   if (W == 0) return XDRG_EUNSUPPORTED;
   const uint32_t S = p.stride;
+  if (S / 4 > 0xffffu || W / 4 > 0xffffu) return XDRG_EUNSUPPORTED;  // u16 word indices
 
   std::vector<int> enc_src(W, kNone), dec_src(S, kNone);
   for (uint32_t i = 0; i + 1 < n; ++i) {
@@ -384,6 +385,7 @@ int compile_plan(xdrg_plan &p) {
     }
   build_prog(enc_src, S / 4, W / 4, p.enc);
   build_prog(dec_src, W / 4, S / 4, p.dec);
+  if (p.enc.terms.size() > 0xffffu || p.dec.terms.size() > 0xffffu) return XDRG_EUNSUPPORTED;
 
   // decode checks
   for (uint32_t i = 0; i + 1 < n; ++i) {

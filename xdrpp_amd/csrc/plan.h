@@ -79,6 +79,34 @@ struct fixed_prog {
   bool has_bool = false;
 };
 
+// A plan's tables in one device's memory.
+struct dev_tables {
+  void *d_mem = nullptr;
+  const xdrg_op *d_ops = nullptr;
+  const uint32_t *d_table = nullptr;
+  const term_idx *d_enc_idx = nullptr, *d_dec_idx = nullptr;
+  const term *d_enc_terms = nullptr, *d_dec_terms = nullptr;
+  const reg_word *d_enc_reg = nullptr, *d_dec_reg = nullptr;
+  const grp_term *d_enc_grp = nullptr, *d_dec_grp = nullptr;
+  const check *d_checks = nullptr;
+};
+constexpr int kMaxDevices = 64;
+
+// Launch options of one plan (enum xdrg_plan_option); 0 / -1 = automatic.
+struct plan_opts {
+  int enc_kernel = 0;      // var encode: 0 auto, 1 per-lane, 3 chunk-map image
+  int dec_kernel = 0;      // var decode: 0 auto, 1 per-lane, 2 window
+  int fixed_path = 0;      // 0 auto, 2 = k_fixed_lds for non-identity fixed plans
+  int image_bytes = -1;    // var encode LDS image per wave (-1: per plan)
+  int window_bytes = -1;   // var decode LDS window per wave (-1: per call)
+  int enc_unroll = 8;      // payload chunks in flight per lane (4, 8, 16)
+  int dec_readahead = 1;   // window decode: 32-byte read-ahead past the window
+  int size_linear = 1;     // size pass without a walk for linear plans
+  int grp_unroll = 0;      // group kernel: chunks in flight (0: per plan)
+  int grp_blocks = 0;      // group kernel: workgroups (0: 2048)
+  int grp_nontemporal = 0; // group kernel: non-temporal stores
+};
+
 }  // namespace xdrg
 
 struct xdrg_plan {
@@ -108,18 +136,15 @@ struct xdrg_plan {
   std::vector<uint32_t> op_wire_off;  // wire byte offset of each op (fixed)
   xdrg::fixed_prog enc, dec;
   std::vector<xdrg::check> checks;
-  // device copies (one allocation), made by the plan's first launch so that
-  // plan creation and validation never touch the device
+  // Per-plan launch options (xdrg_plan_set_option): kernel choices and
+  // launch shapes.  Set before the plan is shared between threads.
+  xdrg::plan_opts opts;
+  // Device copies of the tables, one allocation per device, made by the
+  // plan's first launch on that device (plan creation never touches a
+  // device).  Indexed by the HIP device ordinal current at the launch.
   std::mutex upload_mu;
-  std::atomic<bool> uploaded{false};
-  void *d_mem = nullptr;
-  const xdrg_op *d_ops = nullptr;
-  const uint32_t *d_table = nullptr;
-  const xdrg::term_idx *d_enc_idx = nullptr, *d_dec_idx = nullptr;
-  const xdrg::term *d_enc_terms = nullptr, *d_dec_terms = nullptr;
-  const xdrg::reg_word *d_enc_reg = nullptr, *d_dec_reg = nullptr;
-  const xdrg::grp_term *d_enc_grp = nullptr, *d_dec_grp = nullptr;
-  const xdrg::check *d_checks = nullptr;
+  std::atomic<bool> uploaded[xdrg::kMaxDevices] = {};
+  xdrg::dev_tables dev[xdrg::kMaxDevices];
 };
 
 namespace xdrg {

@@ -406,130 +406,6 @@ __device__ bool dec_vector_elems(const xdrg_op *__restrict__ ops, const uint32_t
 // the lanes whose own pc equals upc do the field work (and jump forward).
 constexpr uint32_t kPcDone = 0xffffffffu;
 
-// Diagnostic phase stamps (in-kernel s_memtime, one row of 8 per wave);
-// only when the stamp buffer is set (tools/tune), never in timed runs.
-#define XDRG_STAMP(i)                                                              \
-  do {                                                                             \
-    if (stamps) {                                                                  \
-      __builtin_amdgcn_sched_barrier(0);                                           \
-      unsigned long long t_;                                                       \
-      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");  \
-      __builtin_amdgcn_sched_barrier(0);                                           \
-      stv[i] = t_;                                                                 \
-    }                                                                              \
-  } while (0)
-#define XDRG_STAMP_FLUSH(wave_id)                                                  \
-  do {                                                                             \
-    if (stamps && (threadIdx.x & 63) == 0)                                         \
-      for (int q_ = 0; q_ < 8; ++q_) stamps[(wave_id) * 8 + q_] = stv[q_];         \
-  } while (0)
-
-// xdr_size of the record at `nat` (a lane-per-record walk; every lane of
-// the wave calls it, `active` lanes walk).  Returns the wire bytes, or sets
-// bad_op on an unknown discriminant.
-__device__ uint64_t size_walk(const uint8_t *nat, bool active, const xdrg_op *__restrict__ ops,
-                              uint32_t nops, const uint32_t *__restrict__ table, uint32_t &bad_op) {
-  uint64_t s = 0;
-  uint32_t pc = active ? 0u : kPcDone;
-  bad_op = kPcDone;
-  for (uint32_t upc = 0; upc < nops; ++upc) {
-    if (!__any(pc == upc)) continue;
-    const xdrg_op op = load_op(ops, upc);
-    if (pc != upc) continue;
-    switch (op.kind) {
-    case XDRG_OP_END: pc = kPcDone; break;
-    case XDRG_OP_JUMP: pc = op.arg0; break;
-    case XDRG_OP_U64: s += 8; ++pc; break;
-    case XDRG_OP_OPAQUE: s += (op.arg0 + 3u) & ~3u; ++pc; break;
-    case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING:
-      s += 4u + ((static_cast<uint64_t>(*reinterpret_cast<const uint32_t *>(nat + op.noff + 8)) + 3u) & ~3ull);
-      ++pc;
-      break;
-    case XDRG_OP_UNION: {
-      const int t = union_target(op, table, *reinterpret_cast<const uint32_t *>(nat + op.noff));
-      s += 4;
-      if (t < 0) { bad_op = upc; pc = kPcDone; }
-      else pc = static_cast<uint32_t>(t);
-      break;
-    }
-    case XDRG_OP_VECTOR:
-      s += 4ull + static_cast<uint64_t>(*reinterpret_cast<const uint32_t *>(nat + op.noff + 8)) * op.arg3;
-      pc = upc + 1 + op.arg2;
-      break;
-    default: s += 4; ++pc; break;
-    }
-  }
-  return s;
-}
-
-// ---------------------------------------------- decoupled look-back (waves)
-// One flag word per 64-record block: status (bits 63-62: 1 = aggregate,
-// 2 = inclusive prefix) | value (62 bits).  Flags and the block ticket are
-// zeroed by the host before the launch.  A wave takes its block by ticket
-// (so it only ever waits on blocks that already run), publishes its
-// aggregate at once, then walks back 64 flags at a time: the nearest
-// inclusive prefix plus the aggregates after it.  Every block publishes
-// its aggregate without waiting on anything, so the wait always ends; a
-// bounded poll count keeps a bug from hanging the GPU (XDRG_ERR_INTERNAL).
-constexpr unsigned long long kLbAgg = 1ull << 62, kLbInc = 2ull << 62;
-constexpr unsigned long long kLbVal = (1ull << 62) - 1;
-
-// Relaxed, device-coherent accesses: the flag word carries its own value,
-// so no other memory is ordered through it.  (Release/acquire at agent
-// scope made every publish write back the XCD's L2: 1.9 ms for 16K blocks.)
-__device__ __forceinline__ unsigned long long lb_load(const unsigned long long *p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void lb_store(unsigned long long *p, unsigned long long v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Exclusive prefix of block `bid` whose aggregate is `agg`; publishes the
-// block's inclusive prefix.  All 64 lanes call it.
-__device__ uint64_t lookback(unsigned long long *flags, uint64_t bid, uint64_t agg,
-                             unsigned long long *err) {
-  const uint32_t lane = threadIdx.x & 63u;
-  if (bid == 0) {
-    if (lane == 0) lb_store(&flags[0], kLbInc | agg);
-    return 0;
-  }
-  if (lane == 0) lb_store(&flags[bid], kLbAgg | agg);
-  uint64_t prefix = 0;
-  int64_t j = static_cast<int64_t>(bid) - 1;
-  for (;;) {
-    const int64_t idx = j - static_cast<int64_t>(lane);
-    unsigned long long f = idx >= 0 ? 0ull : kLbInc;  // below block 0: nothing
-    uint32_t polls = 0;
-    bool gave_up = false;
-    for (;;) {
-      if (idx >= 0 && (f >> 62) == 0) f = lb_load(&flags[idx]);
-      if (!__any(idx >= 0 && (f >> 62) == 0)) break;
-      if (++polls > (1u << 22)) { gave_up = true; break; }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    if (gave_up) {
-      if (lane == 0) report(err, bid * 64u, kOpRecordLevel, XDRG_ERR_INTERNAL);
-      break;
-    }
-    const bool inc = (f >> 62) == 2;
-    const unsigned long long b = __ballot(inc);
-    const uint64_t val = f & kLbVal;
-    if (b) {
-      const uint32_t l0 = __builtin_ctzll(b);  // nearest block with an inclusive prefix
-      uint64_t v = lane <= l0 ? val : 0ull;
-      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-      prefix += v;
-      break;
-    }
-    uint64_t v = val;
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    prefix += v;
-    j -= 64;
-  }
-  if (lane == 0) lb_store(&flags[bid], kLbInc | ((prefix + agg) & kLbVal));
-  return prefix;
-}
-
 // One 64-thread workgroup = 64 consecutive records.  The native records are
 // staged in LDS with coalesced 16-byte loads, so the walk reads fields from
 // LDS instead of issuing one dependent global load per op.
@@ -962,223 +838,13 @@ overflow:
   report(err, r, pc, XDRG_ERR_OVERFLOW_GET);
 }
 
-// ------------------------------------------- var: record-image kernels
-// Encode, record-image form.  The lane walk (one lane per record) writes
-// nothing to global memory: it leaves each record's scalar wire words in
-// LDS and keeps the record's size and payload table in its own registers.
-// The wave then emits whole records: pass p of record j stores words
-// [64p, 64p+64) of the record, one per lane, fully contiguous, with
-// kEmitBatch records' loads in flight per lane.  Record j's table reaches
-// every lane through v_readlane (j is wave-uniform), so the emission loop
-// has no LDS round trips except the scalar words themselves, and no
-// partially written line is ever left for the L2 to evict.
-struct enc_lds {
-  uint32_t ops_bytes, tile_bytes, sw_words, per_wave, total;
-};
-__host__ __device__ inline enc_lds enc_lds_layout(uint32_t nops, uint32_t stride, uint32_t MSW) {
-  enc_lds L;
-  (void)nops;
-  L.ops_bytes = 0;  // ops are read through the scalar cache
-  L.tile_bytes = (64u * stride + 15u) & ~15u;
-  L.sw_words = MSW ? MSW : 1u;
-  L.per_wave = L.tile_bytes + ((64u * L.sw_words * 4u + 15u) & ~15u);  // tile | sw u32[64*MSW]
-  L.total = L.ops_bytes + 4u * L.per_wave;
-  return L;
-}
-
-constexpr int kEmitBatch = 8;
-
+// Registers of one lane read by the whole wave (v_readlane).
 __device__ __forceinline__ uint32_t rl32(uint32_t v, uint32_t lane) {
   return __builtin_amdgcn_readlane(v, lane);
 }
 __device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t lane) {
   return static_cast<uint64_t>(rl32(static_cast<uint32_t>(v), lane)) |
          (static_cast<uint64_t>(rl32(static_cast<uint32_t>(v >> 32), lane)) << 32);
-}
-
-template <int KMAX>
-__global__ __launch_bounds__(256) void k_var_encode_c(
-    const uint8_t *__restrict__ native, uint64_t n, uint32_t stride, const uint8_t *__restrict__ heap,
-    uint64_t heap_len, uint8_t *__restrict__ xdr, uint64_t cap, uint64_t *__restrict__ offsets,
-    const uint32_t *__restrict__ sizes, const unsigned long long *__restrict__ block_base,
-    const xdrg_op *__restrict__ ops, uint32_t nops, const uint32_t *__restrict__ table,
-    uint32_t stack_limit, uint32_t MSW, unsigned long long *err, unsigned long long *stamps) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
-  __shared__ unsigned long long wsum[4];
-  unsigned long long stv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  XDRG_STAMP(0);
-  const enc_lds L = enc_lds_layout(nops, stride, MSW);
-  const uint32_t msw = L.sw_words;
-  xdrg_op *sops = reinterpret_cast<xdrg_op *>(sm);
-  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  uint8_t *wb = sm + L.ops_bytes + wid * L.per_wave;
-  uint8_t *tile = wb;
-  uint32_t *sw = reinterpret_cast<uint32_t *>(wb + L.tile_bytes);
-  (void)sops;
-
-  const uint64_t r = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  const uint32_t sz = r < n ? sizes[r] : 0u;
-  unsigned long long v = (sz & kSizeErr) ? 0ull : sz;
-  unsigned long long incl = v;
-  for (int o = 1; o < 64; o <<= 1) {
-    const unsigned long long x = __shfl_up(incl, o, 64);
-    if (lane >= static_cast<uint32_t>(o)) incl += x;
-  }
-  if (lane == 63) wsum[wid] = incl;
-  XDRG_STAMP(1);
-
-  const uint64_t wr0 = static_cast<uint64_t>(blockIdx.x) * blockDim.x + wid * 64u;
-  const uint32_t wn = wr0 < n ? static_cast<uint32_t>(min<uint64_t>(64, n - wr0)) : 0u;
-  const uint32_t nbytes = wn * stride;
-  const uint8_t *nsrc = native + wr0 * stride;
-  for (uint32_t i = lane; i < nbytes / 16u; i += 64u)
-    reinterpret_cast<u32x4 *>(tile)[i] = reinterpret_cast<const u32x4 *>(nsrc)[i];
-  for (uint32_t i = (nbytes / 16u) * 4u + lane; i < nbytes / 4u; i += 64u)
-    reinterpret_cast<uint32_t *>(tile)[i] = reinterpret_cast<const uint32_t *>(nsrc)[i];
-  __syncthreads();
-  XDRG_STAMP(2);
-
-  const uint64_t off = block_base[blockIdx.x * 4u + wid] + incl - v;  // 64-record block bases
-
-  // per-record table, in this lane's registers
-  uint32_t rsize = 0;
-  uint32_t pst[KMAX], pln[KMAX];
-  uint64_t psr[KMAX];
-#pragma unroll
-  for (int k = 0; k < KMAX; ++k) { pst[k] = 0xffffffffu; pln[k] = 0; psr[k] = 0; }
-  if (r < n) offsets[r] = off;
-  {
-    const uint8_t *nat = tile + lane * stride;
-    uint32_t *mysw = sw + lane * msw;
-    uint32_t nsw = 0, wpos = 0, nslot = 0;  // wpos: record word index
-    uint64_t pos = off;
-    uint32_t pc = (r < n && !(sz & kSizeErr)) ? 0u : kPcDone;
-    bool ok = pc == 0u;
-    for (uint32_t upc = 0; upc < nops; ++upc) {
-      if (!__any(pc == upc)) continue;
-      const xdrg_op op = load_op(ops, upc);
-      if (pc != upc) continue;
-      if (op.kind == XDRG_OP_END) { pc = kPcDone; continue; }
-      if (op.kind == XDRG_OP_JUMP) { pc = op.arg0; continue; }
-      if (op.depth > stack_limit) { report(err, r, upc, XDRG_ERR_STACK_PUT); ok = false; pc = kPcDone; continue; }
-      const uint32_t *nw = reinterpret_cast<const uint32_t *>(nat + op.noff);
-      uint32_t blen = 0;
-      uint64_t need = 4;
-      if (op.kind == XDRG_OP_U64) need = 8;
-      else if (op.kind == XDRG_OP_OPAQUE) need = op.arg0;
-      else if (op.kind == XDRG_OP_VAROPAQUE || op.kind == XDRG_OP_STRING) {
-        blen = nw[2];
-        need = 4ull + blen;
-      }
-      if (need > cap - min(pos, cap)) { report(err, r, upc, XDRG_ERR_OVERFLOW_PUT); ok = false; pc = kPcDone; continue; }
-      switch (op.kind) {
-      case XDRG_OP_U32: case XDRG_OP_ENUM:
-        mysw[nsw++] = bswap32(nw[0]); pos += 4; ++wpos; ++pc; break;
-      case XDRG_OP_BOOL:
-        mysw[nsw++] = nat[op.noff] ? 0x01000000u : 0u; pos += 4; ++wpos; ++pc; break;
-      case XDRG_OP_U64:
-        mysw[nsw++] = bswap32(nw[1]);
-        mysw[nsw++] = bswap32(nw[0]);
-        pos += 8; wpos += 2; ++pc; break;
-      case XDRG_OP_OPAQUE: {
-        const uint32_t BL = op.arg0, nwd = (BL + 3u) >> 2;
-        for (uint32_t k = 0; k < nwd; ++k) {
-          uint32_t w = 0;
-          for (uint32_t bb = 0; bb < 4u && 4u * k + bb < BL; ++bb)
-            w |= static_cast<uint32_t>(nat[op.noff + 4u * k + bb]) << (8u * bb);
-          mysw[nsw++] = w;
-        }
-        pos += 4ull * nwd; wpos += nwd; ++pc; break;
-      }
-      case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
-        mysw[nsw++] = bswap32(blen);
-        ++wpos;
-        const uint32_t nwd = (blen + 3u) >> 2;
-        if (blen) {
-          const uint64_t hsrc = *reinterpret_cast<const uint64_t *>(nw);
-#pragma unroll
-          for (int k = 0; k < KMAX; ++k)
-            if (static_cast<uint32_t>(k) == nslot) { pst[k] = wpos; pln[k] = blen; psr[k] = hsrc; }
-          ++nslot;
-        }
-        wpos += nwd;
-        pos += 4ull + 4ull * nwd; ++pc; break;
-      }
-      case XDRG_OP_UNION: {
-        const uint32_t d = nw[0];
-        mysw[nsw++] = bswap32(d);
-        pos += 4; ++wpos;
-        pc = static_cast<uint32_t>(union_target(op, table, d));  // validated by k_var_size
-        break;
-      }
-      default: ++pc; break;
-      }
-    }
-    if (ok) rsize = wpos;  // a failing record emits nothing (never past `cap`)
-  }
-  __syncthreads();
-  XDRG_STAMP(3);
-
-  // ---- emission: whole records, kEmitBatch records per step
-  for (uint32_t j0 = 0; j0 < wn; j0 += kEmitBatch) {
-    uint32_t rs[kEmitBatch];
-    uint32_t passes = 0;
-#pragma unroll
-    for (int u = 0; u < kEmitBatch; ++u) {
-      rs[u] = (j0 + u < wn) ? rl32(rsize, j0 + u) : 0u;
-      passes = max(passes, (rs[u] + 63u) >> 6);
-    }
-    for (uint32_t pss = 0; pss < passes; ++pss) {
-      const uint32_t w = pss * 64u + lane;
-      uint32_t val[kEmitBatch];
-#pragma unroll
-      for (int u = 0; u < kEmitBatch; ++u) {
-        const uint32_t j = j0 + u;
-        val[u] = 0u;
-        if (w < rs[u]) {
-          // which payload (if any) holds word w of record j; scalar index otherwise
-          uint32_t skip = 0;
-          int slot = -1;
-          uint32_t st = 0, bl = 0;
-          uint64_t src = 0;
-#pragma unroll
-          for (int k = 0; k < KMAX; ++k) {
-            const uint32_t stk = rl32(pst[k], j), blk = rl32(pln[k], j);
-            const uint32_t nwk = (blk + 3u) >> 2;
-            if (slot < 0 && stk != 0xffffffffu) {
-              if (w >= stk + nwk) skip += nwk;
-              else if (w >= stk) { slot = k; st = stk; bl = blk; src = rl64(psr[k], j); }
-            }
-          }
-          if (slot < 0) {
-            val[u] = sw[j * msw + (w - skip)];
-          } else {
-            const uint32_t kw = w - st;
-            const uint64_t hs = src + 4ull * kw;
-            const uint64_t a = hs & ~3ull;
-            const uint32_t sh = static_cast<uint32_t>(hs & 3u);
-            uint32_t x;
-            if (a + 8 <= heap_len) {
-              const uint32_t lo = ld32(heap + a);
-              x = sh ? __builtin_amdgcn_alignbyte(ld32(heap + a + 4), lo, sh) : lo;
-            } else {
-              x = unaligned_word(heap, heap_len, hs);
-            }
-            if (4u * kw + 4u > bl) x &= keep_mask(bl - 4u * kw);
-            val[u] = x;
-          }
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < kEmitBatch; ++u) {
-        const uint32_t j = j0 + u;
-        if (w < rs[u]) st32(xdr + rl64(off, j) + 4ull * w, val[u]);
-      }
-    }
-  }
-  XDRG_STAMP(4);
-  XDRG_STAMP(5);
-  XDRG_STAMP_FLUSH(wr0 / 64u);
 }
 
 // -------------------------------------------- var: image encode (chunk map)
@@ -1221,59 +887,29 @@ __device__ __forceinline__ void img_put(uint8_t *im, uint32_t C, uint8_t *gout, 
   else st32(gout + at, v);
 }
 
-// FUSED: no separate size pass and scan.  The wave takes its block by
-// ticket, sizes its records from the staged tile (size_walk) and gets its
-// stretch offset by decoupled look-back (`lb` = flags[nb] + ticket, zeroed
-// by the host); the last block writes the total.
-template <int KMAX, int U, bool FUSED = false>
+template <int KMAX, int U>
 __global__ __launch_bounds__(64) void k_var_encode_i(
     const uint8_t *__restrict__ native, uint64_t n, uint32_t stride, const uint8_t *__restrict__ heap,
     uint64_t heap_len, uint8_t *__restrict__ xdr, uint64_t cap, uint64_t *__restrict__ offsets,
     const uint32_t *__restrict__ sizes, const unsigned long long *__restrict__ block_base,
     const xdrg_op *__restrict__ ops, uint32_t nops, const uint32_t *__restrict__ table,
-    uint32_t stack_limit, uint32_t MC, uint32_t C, uint32_t mark, unsigned long long *err,
-    unsigned long long *stamps, unsigned long long *lb = nullptr,
-    unsigned long long *total = nullptr) {
+    uint32_t stack_limit, uint32_t MC, uint32_t C, uint32_t mark, unsigned long long *err) {
   extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
-  unsigned long long stv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  XDRG_STAMP(0);
   const enc_i_lds L = enc_i_layout(stride, KMAX, MC, C);
   uint8_t *tile = sm + L.tile;
   echunk_desc *desc = reinterpret_cast<echunk_desc *>(sm + L.desc);
   uint16_t *map = reinterpret_cast<uint16_t *>(sm + L.map);
   uint8_t *img = sm + L.img;
   const uint32_t lane = threadIdx.x;
-  const uint64_t nblk = (n + 63) / 64;
-  uint64_t bid = blockIdx.x;
-  if (FUSED) {  // block by ticket: waits only ever target blocks that already run
-    uint64_t t = 0;
-    if (lane == 0) t = atomicAdd(&lb[nblk], 1ull);
-    bid = __shfl(t, 0, 64);
-  }
-  const uint64_t wr0 = bid * 64u;
+  const uint64_t wr0 = static_cast<uint64_t>(blockIdx.x) * 64u;
   const uint64_t r = wr0 + lane;
   const uint32_t nrec = static_cast<uint32_t>(min<uint64_t>(64, n - wr0));
 
   // ---- record offsets: wave scan of the sizes on top of the block base
   // (sizes, block base and the native tile are loaded in one round trip)
-  uint32_t sz;
-  uint64_t wave_out;
-  if (FUSED) {
-    stage_tile(tile, native + wr0 * stride, nrec * stride, lane, 64u);
-    wave_sync();
-    uint32_t bad_op;
-    const uint64_t s0 = size_walk(tile + lane * stride, r < n, ops, nops, table, bad_op) + mark;
-    sz = kSizeErr;
-    if (r < n) {  // k_var_size's reports (gen_hh.cc:639-648; marshal.h:104-108)
-      if (bad_op != kPcDone) report(err, r, bad_op, XDRG_ERR_BAD_DISCRIMINANT);
-      else if (s0 >= kSizeErr) report(err, r, 0, XDRG_ERR_OVERFLOW_PUT);
-      else sz = static_cast<uint32_t>(s0);
-    }
-  } else {
-    sz = r < n ? sizes[r] : kSizeErr;
-    wave_out = block_base[blockIdx.x];
-    stage_tile(tile, native + wr0 * stride, nrec * stride, lane, 64u);
-  }
+  const uint32_t sz = r < n ? sizes[r] : kSizeErr;
+  const uint64_t wave_out = block_base[blockIdx.x];
+  stage_tile(tile, native + wr0 * stride, nrec * stride, lane, 64u);
   const bool szok = !(sz & kSizeErr);
   const unsigned long long v = szok ? sz : 0ull;
   unsigned long long incl = v;
@@ -1282,18 +918,9 @@ __global__ __launch_bounds__(64) void k_var_encode_i(
     if (lane >= static_cast<uint32_t>(o)) incl += x;
   }
   const uint64_t T = rl64(incl, 63);  // bytes of the wave's stretch
-  if (FUSED) {
-    wave_out = lookback(lb, bid, T, err);
-    if (bid == nblk - 1 && lane == 0) {  // the scan's outputs (k_scan_blocks)
-      *total = wave_out + T;
-      offsets[n] = wave_out + T;
-    }
-  }
   const uint64_t off = wave_out + incl - v;
   if (r < n) offsets[r] = off;
   wave_sync();
-  XDRG_STAMP(1);
-  XDRG_STAMP(2);
 
   const uint32_t sh = static_cast<uint32_t>(wave_out & 15u);
   uint8_t *im = img + sh;               // image byte j <-> global wave_out + j
@@ -1399,7 +1026,6 @@ __global__ __launch_bounds__(64) void k_var_encode_i(
     }
     if (!ok) nslot = 0;  // a failing record's bytes are unspecified (never past `cap`)
   }
-  XDRG_STAMP(3);
 
   // ---- chunk map: u16 lane << 10 | slot << 8 | chunk
   uint32_t nch = 0;
@@ -1489,7 +1115,6 @@ __global__ __launch_bounds__(64) void k_var_encode_i(
     }
   }
   wave_sync();
-  XDRG_STAMP(4);
 
   // ---- image -> global: aligned 16-byte chunks, partial words at the edges
   {
@@ -1513,8 +1138,6 @@ __global__ __launch_bounds__(64) void k_var_encode_i(
       }
     }
   }
-  XDRG_STAMP(5);
-  XDRG_STAMP_FLUSH(blockIdx.x);
 }
 
 // -------------------------------------------------- var: window decode
@@ -1540,10 +1163,8 @@ __global__ __launch_bounds__(64) void k_var_decode_w(
     uint8_t *__restrict__ native, uint32_t stride, uint8_t *__restrict__ heap,
     const xdrg_op *__restrict__ ops, uint32_t nops, const uint32_t *__restrict__ table,
     uint32_t stack_limit, uint32_t C, uint64_t ebase, uint32_t F, uint32_t mark,
-    unsigned long long *err, unsigned long long *stamps) {
+    unsigned long long *err) {
   extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
-  unsigned long long stv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  XDRG_STAMP(0);
   const uint32_t lane = threadIdx.x;
   const uint32_t tile_bytes = (64u * stride + 15u) & ~15u;
   uint8_t *tile = sm;
@@ -1605,7 +1226,6 @@ __global__ __launch_bounds__(64) void k_var_decode_w(
     }
   }
   wave_sync();
-  XDRG_STAMP(1);
 
   // word reader: window for stream bytes in [ws, ws + wc), global otherwise.
   // Past the window a lane keeps a 32-byte read-ahead of the stream (two
@@ -1749,17 +1369,12 @@ __global__ __launch_bounds__(64) void k_var_decode_w(
     if (ok && p != b) report(err, r, kOpRecordLevel, XDRG_ERR_TRAILING);
   }
   wave_sync();
-  XDRG_STAMP(2);
   uint8_t *ndst = native + wr0 * stride;
   const uint32_t nbytes = nrec * stride;
   for (uint32_t i = lane; i < nbytes / 16u; i += 64u)
     reinterpret_cast<u32x4 *>(ndst)[i] = reinterpret_cast<const u32x4 *>(tile)[i];
   for (uint32_t i = (nbytes / 16u) * 4u + lane; i < nbytes / 4u; i += 64u)
     reinterpret_cast<uint32_t *>(ndst)[i] = reinterpret_cast<const uint32_t *>(tile)[i];
-  XDRG_STAMP(3);
-  XDRG_STAMP(4);
-  XDRG_STAMP(5);
-  XDRG_STAMP_FLUSH(blockIdx.x);
 }
 
 // ------------------------------------------- record marks: the index pass
@@ -2157,28 +1772,6 @@ __global__ void k_swap64(const uint64_t *__restrict__ in, uint64_t *__restrict__
 // ------------------------------------------------------------------ host
 constexpr uint64_t kMallBytes = 256ull << 20;  // MI355X Infinity Cache
 constexpr uint32_t kVarLdsBudget = 64u << 10;  // wave-cooperative var kernels
-// Var-kernel choice: 0 = automatic (the fastest eligible kernel).  Forcing
-// (tools/tune A/B, tests): encode 1 = per-lane, 2 = record image,
-// 3 = chunk-map image; decode 1 = per-lane, 2 = window.
-int g_force_enc = 0, g_force_dec = 0;
-int g_fixed_path = 0;  // 0 automatic, 2 = force k_fixed_lds for non-identity fixed plans
-int g_grp_u = 0, g_grp_blocks = 0, g_grp_nt = 0;  // group-path launch overrides (tools/tune)
-uint32_t g_img_bytes = 4u << 10;   // encode LDS image per wave when not automatic
-bool g_img_auto = true;            // per-plan image size (var_encode)
-int g_enc_u = 8;                   // payload chunks in flight per lane, chunk-map encode
-int g_dec_ra = 1;                  // window decode: 32-byte read-ahead past the window
-int g_size_linear = 1;             // size pass without a walk for linear plans
-// Chunk-map encode with in-kernel sizes + decoupled look-back instead of the
-// size pass and the block scan.  Off: measured slower on MI355X (recvar
-// 1M: 269 us vs 170 us for the three kernels).  ~5000 waves run at once,
-// so the inclusive-prefix frontier lags far behind and each wave sums
-// thousands of aggregates through device-coherent (L2-bypassing) loads.
-int g_enc_fused = 0;
-uint32_t g_win_bytes = 4u << 10;   // decode LDS window per wave when not automatic
-bool g_win_auto = true;            // per-call window size (var_decode)
-unsigned long long *g_stamps = nullptr;      // diagnostic phase stamps, decode (tuning)
-unsigned long long *g_stamps_enc = nullptr;  // diagnostic phase stamps, encode (tuning)
-
 uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 bool aligned(const void *p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) % a) == 0; }
 uint32_t gcd32(uint32_t a, uint32_t b) { while (b) { uint32_t t = a % b; a = b; b = t; } return a; }
@@ -2207,8 +1800,9 @@ int launch_report(unsigned long long *err, uint64_t rec, uint32_t op, uint32_t c
 }
 
 // Runs one fixed program (encode or decode) over nrec records.
-int run_fixed(const xdrg_plan &p, bool decode, const void *in, void *out, uint64_t nrec,
-              unsigned long long *err, hipStream_t s) {
+int run_fixed(const xdrg_plan &p, const dev_tables &T, bool decode, const void *in, void *out,
+              uint64_t nrec, unsigned long long *err, hipStream_t s) {
+  const plan_opts &O = p.opts;
   if (nrec == 0) return XDRG_OK;
   const fixed_prog &pg = decode ? p.dec : p.enc;
   const bool checks = decode && p.has_checks;
@@ -2228,16 +1822,16 @@ int run_fixed(const xdrg_plan &p, bool decode, const void *in, void *out, uint64
     blocks = std::min<uint64_t>(blocks, streaming ? 512 : 1024);
     const uint32_t g0 = cpr / gcd32(cpr, 256);
     blocks = align_up(std::max<uint64_t>(blocks, 1), g0);
-    const reg_word *prog = decode ? p.d_dec_reg : p.d_enc_reg;
+    const reg_word *prog = decode ? T.d_dec_reg : T.d_enc_reg;
     const bool bools = pg.has_bool;
     const u32x4 *i4 = static_cast<const u32x4 *>(in);
     u32x4 *o4 = static_cast<u32x4 *>(out);
 #define LAUNCH_REG(B, C)                                                                         \
   do {                                                                                           \
     if (streaming)                                                                               \
-      k_fixed_reg<B, C, 2, true><<<blocks, 256, 0, s>>>(i4, o4, nchunks, cpr, prog, p.d_table, err); \
+      k_fixed_reg<B, C, 2, true><<<blocks, 256, 0, s>>>(i4, o4, nchunks, cpr, prog, T.d_table, err); \
     else                                                                                         \
-      k_fixed_reg<B, C, 1, false><<<blocks, 256, 0, s>>>(i4, o4, nchunks, cpr, prog, p.d_table, err); \
+      k_fixed_reg<B, C, 1, false><<<blocks, 256, 0, s>>>(i4, o4, nchunks, cpr, prog, T.d_table, err); \
   } while (0)
     if (!bools && !checks) LAUNCH_REG(false, false);
     else if (bools && !checks) LAUNCH_REG(true, false);
@@ -2248,23 +1842,23 @@ int run_fixed(const xdrg_plan &p, bool decode, const void *in, void *out, uint64
     return XDRG_OK;
   }
   if (!aligned(in, 4) || !aligned(out, 4)) return XDRG_EALIGN;
-  if (pg.grp_G && !checks && g_fixed_path != 2 && aligned(in, 16) && aligned(out, 16) &&
+  if (pg.grp_G && !checks && O.fixed_path != 2 && aligned(in, 16) && aligned(out, 16) &&
       nrec >= pg.grp_G) {
     // Group path over the full groups; the tail (< G records) below.
     const uint64_t ngroups = nrec / pg.grp_G;
     const uint64_t nchunks = ngroups * pg.grp_C;
     const uint32_t in_g = pg.grp_G * pg.in_words * 4u;
-    const uint64_t cap = g_grp_blocks ? uint64_t(g_grp_blocks) : 2048u;
+    const uint64_t cap = O.grp_blocks ? uint64_t(O.grp_blocks) : 2048u;
     uint64_t blocks = std::min<uint64_t>((nchunks + 255) / 256, cap);
     blocks = align_up(std::max<uint64_t>(blocks, 1), pg.grp_C / gcd32(pg.grp_C, 256));
-    const grp_term *prog = decode ? p.d_dec_grp : p.d_enc_grp;
+    const grp_term *prog = decode ? T.d_dec_grp : T.d_enc_grp;
     const uint8_t *i8 = static_cast<const uint8_t *>(in);
     u32x4 *o4 = static_cast<u32x4 *>(out);
     // tools/tune/tune_grp.py (numerics 1M): U=4 / 2048 workgroups best, within 10 %
-    const int U = g_grp_u ? g_grp_u : (pg.grp_KT == 1 ? 4 : pg.grp_KT == 2 ? 2 : 1);
+    const int U = O.grp_unroll ? O.grp_unroll : (pg.grp_KT == 1 ? 4 : pg.grp_KT == 2 ? 2 : 1);
 #define LAUNCH_GRP(KT, UU)                                                                   \
   do {                                                                                       \
-    if (g_grp_nt)                                                                            \
+    if (O.grp_nontemporal)                                                                            \
       k_fixed_grp<KT, UU, true><<<blocks, 256, 0, s>>>(i8, o4, nchunks, pg.grp_C, in_g, prog); \
     else                                                                                     \
       k_fixed_grp<KT, UU, false><<<blocks, 256, 0, s>>>(i8, o4, nchunks, pg.grp_C, in_g, prog); \
@@ -2286,23 +1880,23 @@ int run_fixed(const xdrg_plan &p, bool decode, const void *in, void *out, uint64
   }
   const uint32_t in_words = pg.in_words, out_words = pg.out_words;
   if (in_words > 8192) return XDRG_EUNSUPPORTED;  // > 32 KiB records: tile won't fit
-  uint32_t T = std::min<uint32_t>(256, std::max<uint32_t>(4, 8192 / in_words));
-  T &= ~3u;
-  const bool vec = aligned(in, 16) && aligned(out, 16) && (T * in_words) % 4 == 0 &&
-                   (T * out_words) % 4 == 0;
-  const size_t lds = 4ull * (T * in_words + 4) + 4ull * ((out_words + 3u) & ~3u) +
+  uint32_t TR = std::min<uint32_t>(256, std::max<uint32_t>(4, 8192 / in_words));
+  TR &= ~3u;
+  const bool vec = aligned(in, 16) && aligned(out, 16) && (TR * in_words) % 4 == 0 &&
+                   (TR * out_words) % 4 == 0;
+  const size_t lds = 4ull * (TR * in_words + 4) + 4ull * ((out_words + 3u) & ~3u) +
                      sizeof(term) * pg.terms.size();
-  const uint64_t tiles = (nrec + T - 1) / T;
+  const uint64_t tiles = (nrec + TR - 1) / TR;
   const uint64_t blocks = std::min<uint64_t>(tiles, 4096);
-  const term_idx *idx = decode ? p.d_dec_idx : p.d_enc_idx;
-  const term *terms = decode ? p.d_dec_terms : p.d_enc_terms;
+  const term_idx *idx = decode ? T.d_dec_idx : T.d_enc_idx;
+  const term *terms = decode ? T.d_dec_terms : T.d_enc_terms;
   const uint32_t nterms = uint32_t(pg.terms.size());
   const uint32_t nchecks = checks ? uint32_t(p.checks.size()) : 0u;
   auto *i32 = static_cast<const uint32_t *>(in);
   auto *o32 = static_cast<uint32_t *>(out);
 #define LAUNCH_LDS(C, V)                                                                   \
-  k_fixed_lds<C, V><<<blocks, 256, lds, s>>>(i32, o32, nrec, in_words, out_words, T, idx, \
-                                             terms, nterms, p.d_checks, nchecks, p.d_table, err)
+  k_fixed_lds<C, V><<<blocks, 256, lds, s>>>(i32, o32, nrec, in_words, out_words, TR, idx, \
+                                             terms, nterms, T.d_checks, nchecks, T.d_table, err)
   if (checks) {
     if (vec) LAUNCH_LDS(true, true); else LAUNCH_LDS(true, false);
   } else {
@@ -2368,10 +1962,10 @@ __global__ __launch_bounds__(256) void k_size_linear(const uint8_t *__restrict__
   if (block_sums && (threadIdx.x & 63u) == 0 && blk * 64u < n) block_sums[blk] = v;
 }
 
-hipError_t launch_size_pass(const xdrg_plan &p, const uint8_t *nat, uint64_t n, uint32_t *sizes,
-                            unsigned long long *bsum, uint32_t mark, unsigned long long *err,
-                            hipStream_t s) {
-  if (p.linear && g_size_linear) {
+hipError_t launch_size_pass(const xdrg_plan &p, const dev_tables &T, const uint8_t *nat, uint64_t n,
+                            uint32_t *sizes, unsigned long long *bsum, uint32_t mark,
+                            unsigned long long *err, hipStream_t s) {
+  if (p.linear && p.opts.size_linear) {
     lin_args L;
     L.base = p.lin_base;
     L.n = p.lin_n;
@@ -2382,21 +1976,17 @@ hipError_t launch_size_pass(const xdrg_plan &p, const uint8_t *nat, uint64_t n, 
   const uint64_t nb = (n + 63) / 64;
   const size_t tile = 64ull * p.stride;
   if (tile <= kVarLdsBudget)
-    k_var_size<true><<<nb, 64, tile, s>>>(nat, n, p.stride, p.d_ops, uint32_t(p.ops.size()),
-                                          p.d_table, sizes, bsum, mark, err);
+    k_var_size<true><<<nb, 64, tile, s>>>(nat, n, p.stride, T.d_ops, uint32_t(p.ops.size()),
+                                          T.d_table, sizes, bsum, mark, err);
   else
-    k_var_size<false><<<nb, 64, 0, s>>>(nat, n, p.stride, p.d_ops, uint32_t(p.ops.size()),
-                                        p.d_table, sizes, bsum, mark, err);
+    k_var_size<false><<<nb, 64, 0, s>>>(nat, n, p.stride, T.d_ops, uint32_t(p.ops.size()),
+                                        T.d_table, sizes, bsum, mark, err);
   return hipGetLastError();
 }
 
 unsigned long long *err_ptr(xdrg_status *st) {
   return reinterpret_cast<unsigned long long *>(&st->first_error);
 }
-
-// Interpreter-path encode of n records: size pass, block scan, then the
-// record kernel.  mark = 4 puts each record in a message (its record mark
-// first, xdrg_encode_msgs); mark = 0 is xdrg_encode of a var plan.
 }  // namespace
 
 namespace xdrg {
@@ -2416,11 +2006,15 @@ int record_hip_error(int e, const char *what) { return hip_fail(static_cast<hipE
 
 namespace {
 
-int var_encode(const xdrg_plan &P, const void *d_native, uint64_t n, const uint8_t *d_heap,
-               uint64_t heap_len, void *d_xdr, uint64_t cap, uint64_t *d_offsets,
-               uint32_t stack_limit, void *d_ws, size_t ws_bytes, xdrg_status *d_status,
-               uint32_t mark, hipStream_t s) {
+// Var-plan encode of n records: size pass, block scan, then the record
+// kernel.  mark = 4 puts each record in a message (its record mark first,
+// xdrg_encode_msgs); mark = 0 is xdrg_encode of a var plan.
+int var_encode(const xdrg_plan &P, const dev_tables &T, const void *d_native, uint64_t n,
+               const uint8_t *d_heap, uint64_t heap_len, void *d_xdr, uint64_t cap,
+               uint64_t *d_offsets, uint32_t stack_limit, void *d_ws, size_t ws_bytes,
+               xdrg_status *d_status, uint32_t mark, hipStream_t s) {
   const xdrg_plan *p = &P;
+  const plan_opts &O = P.opts;
   unsigned long long *err = err_ptr(d_status);
   if (!d_offsets) return XDRG_EINVAL;
   if (d_heap && !aligned(d_heap, 4)) return XDRG_EALIGN;
@@ -2429,8 +2023,7 @@ int var_encode(const xdrg_plan &P, const void *d_native, uint64_t n, const uint8
     HIPCHK(hipMemsetAsync(d_offsets, 0, 8, s));
     return XDRG_OK;
   }
-  size_t so, bo;
-  size_t bbo;
+  size_t so, bo, bbo;
   const size_t need = var_ws_layout(n, &so, &bo, &bbo);
   if (!d_ws || ws_bytes < need) return XDRG_ESPACE;
   uint32_t *sizes = reinterpret_cast<uint32_t *>(static_cast<char *>(d_ws) + so);
@@ -2445,57 +2038,35 @@ int var_encode(const xdrg_plan &P, const void *d_native, uint64_t n, const uint8
   // image helps plans whose other LDS is small (recvar 0.208 -> 0.179 ms,
   // vecrec 0.373 -> 0.305 ms); plans with a large chunk map and tile run
   // better with no image and the occupancy it costs (rpc 0.349 -> 0.318 ms).
-  uint32_t img = g_img_bytes;
-  if (g_img_auto) img = enc_i_layout(p->stride, KI, MC, 0).total >= (12u << 10) ? 0u : (8u << 10);
+  uint32_t img = O.image_bytes >= 0 ? static_cast<uint32_t>(O.image_bytes) & ~15u
+                 : enc_i_layout(p->stride, KI, MC, 0).total >= (12u << 10) ? 0u : (8u << 10);
   const uint32_t Ci = static_cast<uint32_t>(std::min<uint64_t>(
       img, (64ull * std::max<uint64_t>(max_rec, 16) + 15u) & ~15ull));
   const enc_i_lds LI = enc_i_layout(p->stride, KI, MC, Ci);
   const bool ok_I = p->max_var_slots <= 4 && p->max_slot_len <= 4096u &&
                     64ull * max_rec < (1ull << 31) && LI.total <= kVarLdsBudget &&
                     aligned(d_native, 16);
-  const enc_lds EL = enc_lds_layout(uint32_t(p->ops.size()), p->stride, p->max_scalar_words);
-  const bool ok_C = EL.total <= kVarLdsBudget && aligned(d_native, 16) && p->max_var_slots <= 4 &&
-                    !p->has_vector &&  // its per-lane scalar-word array cannot bound element words
-                    !mark;
-  int kern = g_force_enc;
+  int kern = O.enc_kernel;
   if (kern == 3 && !ok_I) kern = 0;
-  if (kern == 2 && !ok_C) kern = 0;
-  if (kern == 0) kern = ok_I ? 3 : ok_C ? 2 : 1;
+  if (kern == 0) kern = ok_I ? 3 : 1;
   const uint64_t nb = (n + 63) / 64;  // 64-record blocks for the size pass, scan and kernel 3
   if (nb > 0xffffffffull) return XDRG_EUNSUPPORTED;
   const size_t lds_ops = p->ops.size() * sizeof(xdrg_op);
   const uint8_t *nat8 = static_cast<const uint8_t *>(d_native);
   uint8_t *xdr8 = static_cast<uint8_t *>(d_xdr);
   const uint32_t nops = uint32_t(p->ops.size());
-  if (kern == 3 && g_enc_fused) {
-    // one kernel: sizes, decoupled look-back and emission (flags + ticket
-    // in the block-sum area, zeroed here)
-    HIPCHK(hipMemsetAsync(bsum, 0, (nb + 1) * 8, s));
-    unsigned long long *tot = reinterpret_cast<unsigned long long *>(&d_status->total_bytes);
-#define LAUNCH_ENC_F(K, UU)                                                                      \
-  k_var_encode_i<K, UU, true><<<nb, 64, LI.total, s>>>(                                          \
-      nat8, n, p->stride, d_heap, heap_len, xdr8, cap, d_offsets, nullptr, nullptr, p->d_ops,    \
-      nops, p->d_table, stack_limit, MC, Ci, mark, err, g_stamps_enc, bsum, tot)
-    if (KI == 1) LAUNCH_ENC_F(1, 8);
-    else if (KI == 2) LAUNCH_ENC_F(2, 8);
-    else LAUNCH_ENC_F(4, 8);
-#undef LAUNCH_ENC_F
-    HIPCHK(hipGetLastError());
-    return XDRG_OK;
-  }
-  HIPCHK(launch_size_pass(*p, nat8, n, sizes, bsum, mark, err, s));
+  HIPCHK(launch_size_pass(*p, T, nat8, n, sizes, bsum, mark, err, s));
   if (int rc = xdrg::launch_block_scan(bsum, bbase, uint32_t(nb), d_status, d_offsets, n, s)) return rc;
   if (kern == 3) {
 #define LAUNCH_ENC_IU(K, UU)                                                                   \
   k_var_encode_i<K, UU><<<nb, 64, LI.total, s>>>(nat8, n, p->stride, d_heap, heap_len, xdr8,  \
-                                                 cap, d_offsets, sizes, bbase, p->d_ops, nops,  \
-                                                 p->d_table, stack_limit, MC, Ci, mark, err,   \
-                                                 g_stamps_enc)
+                                                 cap, d_offsets, sizes, bbase, T.d_ops, nops,   \
+                                                 T.d_table, stack_limit, MC, Ci, mark, err)
 #define LAUNCH_ENC_I(K)                                     \
   do {                                                      \
-    if (g_enc_u == 16) LAUNCH_ENC_IU(K, 16);                \
-    else if (g_enc_u == 8) LAUNCH_ENC_IU(K, 8);             \
-    else LAUNCH_ENC_IU(K, 4);                               \
+    if (O.enc_unroll == 16) LAUNCH_ENC_IU(K, 16);           \
+    else if (O.enc_unroll == 4) LAUNCH_ENC_IU(K, 4);        \
+    else LAUNCH_ENC_IU(K, 8);                               \
   } while (0)
     if (KI == 1) LAUNCH_ENC_I(1);
     else if (KI == 2) LAUNCH_ENC_I(2);
@@ -2506,21 +2077,9 @@ int var_encode(const xdrg_plan &P, const void *d_native, uint64_t n, const uint8
     return XDRG_OK;
   }
   const uint64_t nb256 = (n + 255) / 256;
-  if (kern == 2) {
-#define LAUNCH_ENC_C(K)                                                                        \
-  k_var_encode_c<K><<<nb256, 256, EL.total, s>>>(nat8, n, p->stride, d_heap, heap_len, xdr8, cap, \
-                                              d_offsets, sizes, bbase, p->d_ops, nops,          \
-                                              p->d_table, stack_limit, p->max_scalar_words,   \
-                                              err, g_stamps_enc)
-    if (p->max_var_slots <= 1) LAUNCH_ENC_C(1);
-    else if (p->max_var_slots <= 2) LAUNCH_ENC_C(2);
-    else LAUNCH_ENC_C(4);
-#undef LAUNCH_ENC_C
-  } else {
-    k_var_encode<<<nb256, 256, lds_ops, s>>>(nat8, n, p->stride, d_heap, heap_len, xdr8, cap,
-                                          d_offsets, sizes, bbase, p->d_ops, nops, p->d_table,
-                                          stack_limit, mark, err);
-  }
+  k_var_encode<<<nb256, 256, lds_ops, s>>>(nat8, n, p->stride, d_heap, heap_len, xdr8, cap, d_offsets,
+                                           sizes, bbase, T.d_ops, nops, T.d_table, stack_limit, mark,
+                                           err);
   HIPCHK(hipGetLastError());
   return XDRG_OK;
 }
@@ -2568,12 +2127,14 @@ ix_layout ix_plan(uint64_t len, uint32_t maxlen) {
 // none when decoding messages (the decoded records hold no heap refs).
 bool plan_has_payload(const xdrg_plan &p) { return p.max_var_slots > 0 || p.has_vector; }
 
-// Interpreter-path decode of n records indexed by d_offsets (mark = 4:
-// each record is a message whose mark is checked, xdrg_decode_msgs).
-int var_decode(const xdrg_plan &P, const void *d_xdr, uint64_t len, const uint64_t *d_offsets,
-               uint64_t n, void *d_native, uint8_t *d_heap_out, uint64_t heap_cap,
-               uint32_t stack_limit, xdrg_status *d_status, uint32_t mark, hipStream_t s) {
+// Var-plan decode of n records indexed by d_offsets (mark = 4: each record
+// is a message whose mark is checked, xdrg_decode_msgs).
+int var_decode(const xdrg_plan &P, const dev_tables &T, const void *d_xdr, uint64_t len,
+               const uint64_t *d_offsets, uint64_t n, void *d_native, uint8_t *d_heap_out,
+               uint64_t heap_cap, uint32_t stack_limit, xdrg_status *d_status, uint32_t mark,
+               hipStream_t s) {
   const xdrg_plan *p = &P;
+  const plan_opts &O = P.opts;
   unsigned long long *err = err_ptr(d_status);
   if (n == 0) {
     if (len) return launch_report(err, 0, kOpRecordLevel, XDRG_ERR_TRAILING, s);
@@ -2597,32 +2158,32 @@ int var_decode(const xdrg_plan &P, const void *d_xdr, uint64_t len, const uint64
   // pays when it holds a wave's whole stretch (vecrec, ~6.6 KiB per 64
   // records: 0.37 -> 0.30 ms); for longer stretches the occupancy it costs
   // outweighs it (rpc, ~15 KiB: 0.199 -> 0.220 ms), so they keep 4 KiB.
-  uint32_t win = g_win_bytes;
-  if (g_win_auto) win = n && 64ull * (len / n) <= (8u << 10) ? (8u << 10) : (4u << 10);
+  const uint32_t win = O.window_bytes >= 0 ? static_cast<uint32_t>(O.window_bytes) & ~15u
+                       : 64ull * (len / n) <= (8u << 10) ? (8u << 10) : (4u << 10);
   const uint32_t Cw = static_cast<uint32_t>(std::min<uint64_t>(
       win, (64ull * std::max<uint64_t>(p->max_record_bytes + mark, 16) + 15u) & ~15ull));
   const uint32_t lw = dec_w_lds(p->stride, Cw);
   const bool ok_W = lw <= kVarLdsBudget && aligned(d_native, 16);
-  int kern = g_force_dec;
+  int kern = O.dec_kernel;
   if (kern == 2 && !ok_W) kern = 0;
   if (kern == 0) kern = ok_W ? 2 : 1;
   if (kern == 2) {
     const uint64_t nb = (n + 63) / 64;
 #define LAUNCH_DEC_W(CP, RA)                                                                      \
   k_var_decode_w<CP, RA><<<nb, 64, lw, s>>>(xdr8, len, d_offsets, n, nat8, p->stride, d_heap_out, \
-                                            p->d_ops, nops, p->d_table, stack_limit, Cw, ebase,   \
-                                            p->heap_factor, mark, err, g_stamps)
+                                            T.d_ops, nops, T.d_table, stack_limit, Cw, ebase,     \
+                                            p->heap_factor, mark, err)
     if (copy) {
-      if (g_dec_ra) LAUNCH_DEC_W(true, true); else LAUNCH_DEC_W(true, false);
+      if (O.dec_readahead) LAUNCH_DEC_W(true, true); else LAUNCH_DEC_W(true, false);
     } else {
-      if (g_dec_ra) LAUNCH_DEC_W(false, true); else LAUNCH_DEC_W(false, false);
+      if (O.dec_readahead) LAUNCH_DEC_W(false, true); else LAUNCH_DEC_W(false, false);
     }
 #undef LAUNCH_DEC_W
   } else {
     if (copy && len) HIPCHK(hipMemcpyAsync(d_heap_out, d_xdr, len, hipMemcpyDeviceToDevice, s));
     const uint64_t nb = (n + 255) / 256;
     k_var_decode<<<nb, 256, p->ops.size() * sizeof(xdrg_op), s>>>(
-        xdr8, len, d_offsets, n, nat8, p->stride, p->d_ops, nops, p->d_table, stack_limit,
+        xdr8, len, d_offsets, n, nat8, p->stride, T.d_ops, nops, T.d_table, stack_limit,
         d_heap_out, ebase, p->heap_factor, mark, err);
   }
   HIPCHK(hipGetLastError());
@@ -2638,56 +2199,12 @@ int xdrg_abi_version(void) { return XDRG_ABI_VERSION; }
 
 const char *xdrg_last_hip_error(void) { return g_hip_err; }
 
-// Internal A/B hooks for tools/tune and the tests (not part of include/xdrgpu.h).
-void xdrg__force_fixed_path(int path) { g_fixed_path = path; }
-int xdrg__set_enc_fused(int on) {
-  const int old = g_enc_fused;
-  g_enc_fused = on ? 1 : 0;
-  return old;
-}
-int xdrg__set_size_linear(int on) {
-  const int old = g_size_linear;
-  g_size_linear = on ? 1 : 0;
-  return old;
-}
-int xdrg__set_dec_readahead(int on) {
-  const int old = g_dec_ra;
-  g_dec_ra = on ? 1 : 0;
-  return old;
-}
-int xdrg__set_enc_unroll(int u) {
-  const int old = g_enc_u;
-  if (u == 4 || u == 8 || u == 16) g_enc_u = u;
-  return old;
-}
-void xdrg__set_fixed_grp(int u, int blocks, int nt) {
-  g_grp_u = u;
-  g_grp_blocks = blocks;
-  g_grp_nt = nt;
-}
-void xdrg__force_var_kernels(int enc, int dec) {
-  g_force_enc = enc;
-  g_force_dec = dec;
-}
-void xdrg__set_stamps(void *buf) { g_stamps = static_cast<unsigned long long *>(buf); }
-void xdrg__set_stamps_enc(void *buf) { g_stamps_enc = static_cast<unsigned long long *>(buf); }
-int xdrg__set_window_bytes(int bytes) {  // < 0: back to the per-call choice
-  const int old = g_win_auto ? -1 : static_cast<int>(g_win_bytes);
-  g_win_auto = bytes < 0;
-  if (bytes >= 0) g_win_bytes = static_cast<uint32_t>(bytes) & ~15u;
-  return old;
-}
-int xdrg__set_image_bytes(int bytes) {  // < 0: back to the per-plan choice
-  const int old = g_img_auto ? -1 : static_cast<int>(g_img_bytes);
-  g_img_auto = bytes < 0;
-  if (bytes >= 0) g_img_bytes = static_cast<uint32_t>(bytes) & ~15u;
-  return old;
-}
-
 int xdrg_plan_create(const xdrg_op *ops, uint32_t nops, const uint32_t *table, uint32_t ntable,
                      uint32_t native_stride, xdrg_plan **out) {
   if (!ops || !out || nops == 0 || (ntable && !table)) return XDRG_EINVAL;
   *out = nullptr;
+  // status keys carry 16 bits of op index, 0xffff meaning "record level"
+  if (nops >= kOpRecordLevel) return XDRG_EUNSUPPORTED;
   xdrg_plan *p = new (std::nothrow) xdrg_plan();
   if (!p) return XDRG_ENOMEM;
   p->ops.assign(ops, ops + nops);
@@ -2700,12 +2217,54 @@ int xdrg_plan_create(const xdrg_op *ops, uint32_t nops, const uint32_t *table, u
   return XDRG_OK;
 }
 
-// First launch of a plan: one device allocation holding every table.
-static int plan_upload(const xdrg_plan *cp) {
-  if (cp->uploaded.load(std::memory_order_acquire)) return XDRG_OK;
+int xdrg_plan_set_option(xdrg_plan *p, int option, int64_t value) {
+  if (!p) return XDRG_EINVAL;
+  plan_opts &O = p->opts;
+  const int v = static_cast<int>(value);
+  if (value != v) return XDRG_EINVAL;
+  switch (option) {
+  case XDRG_OPT_VAR_ENCODE_KERNEL:
+    if (v != 0 && v != 1 && v != 3) return XDRG_EINVAL;
+    O.enc_kernel = v; return XDRG_OK;
+  case XDRG_OPT_VAR_DECODE_KERNEL:
+    if (v < 0 || v > 2) return XDRG_EINVAL;
+    O.dec_kernel = v; return XDRG_OK;
+  case XDRG_OPT_FIXED_PATH:
+    if (v != 0 && v != 2) return XDRG_EINVAL;
+    O.fixed_path = v; return XDRG_OK;
+  case XDRG_OPT_IMAGE_BYTES:
+    if (v > (32 << 10)) return XDRG_EINVAL;
+    O.image_bytes = v < 0 ? -1 : v; return XDRG_OK;
+  case XDRG_OPT_WINDOW_BYTES:
+    if (v > (32 << 10)) return XDRG_EINVAL;
+    O.window_bytes = v < 0 ? -1 : v; return XDRG_OK;
+  case XDRG_OPT_ENC_UNROLL:
+    if (v != 4 && v != 8 && v != 16) return XDRG_EINVAL;
+    O.enc_unroll = v; return XDRG_OK;
+  case XDRG_OPT_DEC_READAHEAD: O.dec_readahead = v ? 1 : 0; return XDRG_OK;
+  case XDRG_OPT_SIZE_LINEAR: O.size_linear = v ? 1 : 0; return XDRG_OK;
+  case XDRG_OPT_GRP_UNROLL:
+    if (v != 0 && v != 1 && v != 2 && v != 4) return XDRG_EINVAL;
+    O.grp_unroll = v; return XDRG_OK;
+  case XDRG_OPT_GRP_BLOCKS:
+    if (v < 0) return XDRG_EINVAL;
+    O.grp_blocks = v; return XDRG_OK;
+  case XDRG_OPT_GRP_NONTEMPORAL: O.grp_nontemporal = v ? 1 : 0; return XDRG_OK;
+  default: return XDRG_EINVAL;
+  }
+}
+
+// The plan's tables on the current device: one allocation holding every
+// table, made by the plan's first launch on that device.
+static int plan_upload(const xdrg_plan *cp, const dev_tables **out) {
+  int dev = 0;
+  HIPCHK(hipGetDevice(&dev));
+  if (dev < 0 || dev >= kMaxDevices) return XDRG_EUNSUPPORTED;
   xdrg_plan *p = const_cast<xdrg_plan *>(cp);
+  *out = &p->dev[dev];
+  if (p->uploaded[dev].load(std::memory_order_acquire)) return XDRG_OK;
   std::lock_guard<std::mutex> g(p->upload_mu);
-  if (p->uploaded.load(std::memory_order_relaxed)) return XDRG_OK;
+  if (p->uploaded[dev].load(std::memory_order_relaxed)) return XDRG_OK;
   struct part { const void *src; size_t bytes; size_t off; };
   part parts[12] = {
       {p->ops.data(), p->ops.size() * sizeof(xdrg_op), 0},
@@ -2731,25 +2290,33 @@ static int plan_upload(const xdrg_plan *cp) {
       e = hipMemcpy(base + q.off, q.src, q.bytes, hipMemcpyHostToDevice);
       if (e != hipSuccess) { (void)hipFree(mem); return hip_fail(e, "hipMemcpy(plan)"); }
     }
-  p->d_mem = mem;
-  p->d_ops = reinterpret_cast<const xdrg_op *>(base + parts[0].off);
-  p->d_table = reinterpret_cast<const uint32_t *>(base + parts[1].off);
-  p->d_enc_idx = reinterpret_cast<const term_idx *>(base + parts[2].off);
-  p->d_enc_terms = reinterpret_cast<const term *>(base + parts[3].off);
-  p->d_dec_idx = reinterpret_cast<const term_idx *>(base + parts[4].off);
-  p->d_dec_terms = reinterpret_cast<const term *>(base + parts[5].off);
-  p->d_enc_reg = reinterpret_cast<const reg_word *>(base + parts[6].off);
-  p->d_dec_reg = reinterpret_cast<const reg_word *>(base + parts[7].off);
-  p->d_checks = reinterpret_cast<const check *>(base + parts[8].off);
-  p->d_enc_grp = reinterpret_cast<const grp_term *>(base + parts[9].off);
-  p->d_dec_grp = reinterpret_cast<const grp_term *>(base + parts[10].off);
-  p->uploaded.store(true, std::memory_order_release);
+  dev_tables &T = p->dev[dev];
+  T.d_mem = mem;
+  T.d_ops = reinterpret_cast<const xdrg_op *>(base + parts[0].off);
+  T.d_table = reinterpret_cast<const uint32_t *>(base + parts[1].off);
+  T.d_enc_idx = reinterpret_cast<const term_idx *>(base + parts[2].off);
+  T.d_enc_terms = reinterpret_cast<const term *>(base + parts[3].off);
+  T.d_dec_idx = reinterpret_cast<const term_idx *>(base + parts[4].off);
+  T.d_dec_terms = reinterpret_cast<const term *>(base + parts[5].off);
+  T.d_enc_reg = reinterpret_cast<const reg_word *>(base + parts[6].off);
+  T.d_dec_reg = reinterpret_cast<const reg_word *>(base + parts[7].off);
+  T.d_checks = reinterpret_cast<const check *>(base + parts[8].off);
+  T.d_enc_grp = reinterpret_cast<const grp_term *>(base + parts[9].off);
+  T.d_dec_grp = reinterpret_cast<const grp_term *>(base + parts[10].off);
+  p->uploaded[dev].store(true, std::memory_order_release);
   return XDRG_OK;
 }
 
 void xdrg_plan_destroy(xdrg_plan *p) {
   if (!p) return;
-  if (p->d_mem) (void)hipFree(p->d_mem);
+  int cur = 0;
+  const bool restore = hipGetDevice(&cur) == hipSuccess;
+  for (int d = 0; d < kMaxDevices; ++d)
+    if (p->dev[d].d_mem) {
+      (void)hipSetDevice(d);
+      (void)hipFree(p->dev[d].d_mem);
+    }
+  if (restore) (void)hipSetDevice(cur);
   delete p;
 }
 
@@ -2805,7 +2372,8 @@ int xdrg_encode(const xdrg_plan *p, const void *d_native, uint64_t n, const uint
                 uint32_t stack_limit, void *d_ws, size_t ws_bytes, xdrg_status *d_status,
                 void *stream) {
   if (!p || !d_status || (n && (!d_native || !d_xdr))) return XDRG_EINVAL;
-  if (int rc = plan_upload(p)) return rc;
+  const dev_tables *T = nullptr;
+  if (int rc = plan_upload(p, &T)) return rc;
   hipStream_t s = static_cast<hipStream_t>(stream);
   unsigned long long *err = err_ptr(d_status);
   if (p->path != XDRG_PATH_VAR) {
@@ -2820,10 +2388,10 @@ int xdrg_encode(const xdrg_plan *p, const void *d_native, uint64_t n, const uint
       if (rc) return rc;
     }
     if (d_offsets) return XDRG_EINVAL;  // fixed plans: offsets are implied
-    return run_fixed(*p, false, d_native, d_xdr, nrec, err, s);
+    return run_fixed(*p, *T, false, d_native, d_xdr, nrec, err, s);
   }
   // ---- variable plans
-  return var_encode(*p, d_native, n, d_heap, heap_len, d_xdr, cap, d_offsets, stack_limit, d_ws,
+  return var_encode(*p, *T, d_native, n, d_heap, heap_len, d_xdr, cap, d_offsets, stack_limit, d_ws,
                     ws_bytes, d_status, 0u, s);
 }
 
@@ -2834,7 +2402,8 @@ int xdrg_decode(const xdrg_plan *p, const void *d_xdr, uint64_t len, const uint6
   (void)d_ws;
   (void)ws_bytes;
   if (!p || !d_status || (n && (!d_native || (len && !d_xdr)))) return XDRG_EINVAL;
-  if (int rc = plan_upload(p)) return rc;
+  const dev_tables *T = nullptr;
+  if (int rc = plan_upload(p, &T)) return rc;
   hipStream_t s = static_cast<hipStream_t>(stream);
   unsigned long long *err = err_ptr(d_status);
   if (p->path != XDRG_PATH_VAR) {
@@ -2856,10 +2425,10 @@ int xdrg_decode(const xdrg_plan *p, const void *d_xdr, uint64_t len, const uint6
       int rc = launch_report(err, n, kOpRecordLevel, XDRG_ERR_TRAILING, s);
       if (rc) return rc;
     }
-    return run_fixed(*p, true, d_xdr, d_native, nrec, err, s);
+    return run_fixed(*p, *T, true, d_xdr, d_native, nrec, err, s);
   }
   if (!d_offsets) return XDRG_EUNSUPPORTED;  // var decode needs a record index
-  return var_decode(*p, d_xdr, len, d_offsets, n, d_native, d_heap_out, heap_cap, stack_limit,
+  return var_decode(*p, *T, d_xdr, len, d_offsets, n, d_native, d_heap_out, heap_cap, stack_limit,
                     d_status, 0u, s);
 }
 
@@ -2867,7 +2436,8 @@ int xdrg_record_depths(const xdrg_plan *p, const void *d_native, uint64_t n, uin
                        xdrg_status *d_status, void *stream) {
   if (!p || !d_status || (n && (!d_native || !d_depths))) return XDRG_EINVAL;
   if (n == 0) return XDRG_OK;
-  if (int rc = plan_upload(p)) return rc;
+  const dev_tables *T = nullptr;
+  if (int rc = plan_upload(p, &T)) return rc;
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (p->path != XDRG_PATH_VAR || p->linear) {  // every record walks every op
     HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_depths), int(p->max_depth), n, s));
@@ -2878,27 +2448,29 @@ int xdrg_record_depths(const xdrg_plan *p, const void *d_native, uint64_t n, uin
   const uint8_t *nat = static_cast<const uint8_t *>(d_native);
   unsigned long long *err = err_ptr(d_status);
   if (tile <= kVarLdsBudget)
-    k_var_size<true, true><<<nb, 64, tile, s>>>(nat, n, p->stride, p->d_ops, uint32_t(p->ops.size()),
-                                                p->d_table, nullptr, nullptr, 0u, err, d_depths);
+    k_var_size<true, true><<<nb, 64, tile, s>>>(nat, n, p->stride, T->d_ops, uint32_t(p->ops.size()),
+                                                T->d_table, nullptr, nullptr, 0u, err, d_depths);
   else
-    k_var_size<false, true><<<nb, 64, 0, s>>>(nat, n, p->stride, p->d_ops, uint32_t(p->ops.size()),
-                                              p->d_table, nullptr, nullptr, 0u, err, d_depths);
+    k_var_size<false, true><<<nb, 64, 0, s>>>(nat, n, p->stride, T->d_ops, uint32_t(p->ops.size()),
+                                              T->d_table, nullptr, nullptr, 0u, err, d_depths);
   HIPCHK(hipGetLastError());
   return XDRG_OK;
 }
 
 int xdrg_serial_sizes(const xdrg_plan *p, const void *d_native, uint64_t n, uint32_t *d_sizes,
                       uint32_t stack_limit, xdrg_status *d_status, void *stream) {
+  (void)stack_limit;
   if (!p || !d_status || (n && (!d_native || !d_sizes))) return XDRG_EINVAL;
   if (n == 0) return XDRG_OK;
-  if (int rc = plan_upload(p)) return rc;
+  const dev_tables *T = nullptr;
+  if (int rc = plan_upload(p, &T)) return rc;
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (p->path != XDRG_PATH_VAR) {
     // fixed_size for every record (xdr_struct_base_fs, types.h:691-700)
     HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_sizes), int(p->fixed_size), n, s));
     return XDRG_OK;
   }
-  HIPCHK(launch_size_pass(*p, static_cast<const uint8_t *>(d_native), n, d_sizes, nullptr, 0u,
+  HIPCHK(launch_size_pass(*p, *T, static_cast<const uint8_t *>(d_native), n, d_sizes, nullptr, 0u,
                           err_ptr(d_status), s));
   return XDRG_OK;
 }
@@ -2908,8 +2480,9 @@ int xdrg_encode_msgs(const xdrg_plan *p, const void *d_native, uint64_t n, const
                      uint32_t stack_limit, void *d_ws, size_t ws_bytes, xdrg_status *d_status,
                      void *stream) {
   if (!p || !d_status || (n && (!d_native || !d_out))) return XDRG_EINVAL;
-  if (int rc = plan_upload(p)) return rc;
-  return var_encode(*p, d_native, n, d_heap, heap_len, d_out, cap, d_offsets, stack_limit, d_ws,
+  const dev_tables *T = nullptr;
+  if (int rc = plan_upload(p, &T)) return rc;
+  return var_encode(*p, *T, d_native, n, d_heap, heap_len, d_out, cap, d_offsets, stack_limit, d_ws,
                     ws_bytes, d_status, 4u, static_cast<hipStream_t>(stream));
 }
 
@@ -2971,8 +2544,9 @@ int xdrg_decode_msgs(const xdrg_plan *p, const void *d_stream, uint64_t len,
   (void)d_ws;
   (void)ws_bytes;
   if (!p || !d_status || !d_offsets || (n && (!d_native || (len && !d_stream)))) return XDRG_EINVAL;
-  if (int rc = plan_upload(p)) return rc;
-  return var_decode(*p, d_stream, len, d_offsets, n, d_native, d_heap_out, heap_cap, stack_limit,
+  const dev_tables *T = nullptr;
+  if (int rc = plan_upload(p, &T)) return rc;
+  return var_decode(*p, *T, d_stream, len, d_offsets, n, d_native, d_heap_out, heap_cap, stack_limit,
                     d_status, 4u, static_cast<hipStream_t>(stream));
 }
 

@@ -62,9 +62,11 @@ _EXC = {1: XdrOverflow, 2: XdrStackOverflow, 3: XdrBadMessageSize, 4: XdrBadDisc
 
 # ---------------------------------------------------------------------- plan
 class Plan:
-    """A compiled, device-resident plan for one XDR type (xdrg_plan_create)."""
+    """A compiled, device-resident plan for one XDR type (xdrg_plan_create).
+    ``options``: launch options of this plan (xdrg_plan_set_option; names
+    in _abi.PLAN_OPTIONS), e.g. {"var_encode_kernel": 1}."""
 
-    def __init__(self, t: XdrType | CompiledPlan):
+    def __init__(self, t: XdrType | CompiledPlan, options: dict | None = None):
         self.cp = t if isinstance(t, CompiledPlan) else compile_plan(t)
         L = A.lib()
         ops = self.cp.ops
@@ -75,6 +77,8 @@ class Plan:
             None if table is None else table.ctypes.data_as(C.POINTER(C.c_uint32)),
             0 if table is None else table.size, self.cp.stride, C.byref(h)), "xdrg_plan_create")
         self.handle = h
+        for k, v in (options or {}).items():
+            A.check(L.xdrg_plan_set_option(h, A.PLAN_OPTIONS[k], int(v)), f"xdrg_plan_set_option({k})")
         info = A.XdrgPlanInfo()
         A.check(L.xdrg_plan_get_info(h, C.byref(info)), "xdrg_plan_get_info")
         self.path = info.path
