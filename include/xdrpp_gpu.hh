@@ -51,6 +51,27 @@
 
 #include "xdrgpu.h"
 
+// Does a user validate() hook exist for T?  xdrc's load() ends every struct
+// and union with `using xdr::validate; validate(obj);` (xdrc/gen_hh.cc:
+// 244-247, :671-672): an overload found by argument-dependent lookup, or a
+// T::validate() member that xdr::validate calls (xdrpp/types.h:109-140).
+// Ordinary lookup here finds only the probe's own template, so the call
+// resolves to a user overload when there is one (a non-template exact
+// match) and to the probe (or ambiguously, for types in namespace xdr, to
+// xdr::validate) when there is none.
+namespace xdrg_validate_probe {
+struct no_hook {};
+template <typename T> no_hook validate(const T &);
+template <typename T, typename = void> struct adl : std::false_type {};
+template <typename T>
+struct adl<T, std::void_t<decltype(validate(std::declval<const T &>()))>>
+    : std::bool_constant<!std::is_same_v<decltype(validate(std::declval<const T &>())), no_hook>> {};
+template <typename T, typename = void> struct member : std::false_type {};
+template <typename T>
+struct member<T, std::void_t<decltype(std::declval<const T &>().validate())>> : std::true_type {};
+template <typename T> constexpr bool has_hook = adl<T>::value || member<T>::value;
+}  // namespace xdrg_validate_probe
+
 namespace xdr {
 namespace gpu {
 
@@ -131,6 +152,7 @@ struct subplan {
   std::uint32_t size = 0, align = 1;
   bool identity = true;  // staged layout == C++ layout of the type
   bool fixed = true;     // fixed wire size (xdr_traits<T>::has_fixed_size)
+  bool validates = false;  // some struct/union in the type has a validate() hook
 
   bool same_ops(const subplan &o) const {
     if (ops.size() != o.ops.size() || table != o.table) return false;
@@ -193,6 +215,7 @@ struct struct_recorder {
     off += fp.size;
     sp->align = std::max(sp->align, fp.align);
     sp->fixed = sp->fixed && fp.fixed;
+    sp->validates = sp->validates || fp.validates;
   }
 };
 
@@ -293,8 +316,13 @@ template <typename U> subplan record_union() {
   sp.fixed = false;
   sp.identity = false;
   std::uint32_t aal = 4, asz = 0;
+  sp.validates = xdrg_validate_probe::has_hook<U>;
   auto grow = [&](const arm_rec &a) {
-    if (!a.is_void) { aal = std::max(aal, a.sp.align); asz = std::max(asz, a.sp.size); }
+    if (!a.is_void) {
+      aal = std::max(aal, a.sp.align);
+      asz = std::max(asz, a.sp.size);
+      sp.validates = sp.validates || a.sp.validates;
+    }
   };
   for (auto &c : cases) grow(c.second);
   if (have_dflt) grow(dflt);
@@ -399,6 +427,7 @@ template <typename T> subplan record_type() {
     sp.align = alignof(xdrg_bytes_ref);
     sp.identity = false;
     sp.fixed = false;
+    sp.validates = e.validates;
   } else if constexpr (xarray_info<T>::value) {
     using E = typename xarray_info<T>::elem;
     const subplan e = record_type<E>();
@@ -408,6 +437,7 @@ template <typename T> subplan record_type() {
     sp.align = e.align;
     sp.identity = e.identity && sizeof(E) == step && sizeof(T) == sp.size;
     sp.fixed = e.fixed;
+    sp.validates = e.validates;
   } else if constexpr (TR::is_union) {
     sp = record_union<T>();
   } else if constexpr (TR::is_struct || TR::is_class) {
@@ -415,6 +445,7 @@ template <typename T> subplan record_type() {
     struct_recorder r{&sp, reinterpret_cast<const char *>(&proto)};
     TR::save(r, proto);
     sp.size = align_up(std::max<std::uint32_t>(r.off, 1), sp.align);
+    sp.validates = sp.validates || xdrg_validate_probe::has_hook<T>;
     if (sizeof(T) != sp.size || !std::is_trivially_copyable_v<T>) sp.identity = false;
   } else {
     static_assert(!sizeof(T *), "xdr::gpu: xvector<T>/pointer<T> of non-bytes T is not supported yet");
@@ -498,33 +529,57 @@ struct stager : cursor {
   }
 };
 
+// Thrown by an unstager that reaches its stop op (the op a device decode
+// failed at): the caller raises the device's error there.
+struct stop_reached {};
+constexpr std::uint32_t kNoStop = 0xffffffffu;
+
+// Unstage: xdr_traits<T>::load reads the staged record back, so every
+// struct and union ends with its validate() hook, in the reference's order.
+// With `stop` set, the walk throws stop_reached on reaching that op: the
+// hooks of everything decoded before it have run, as they would have in
+// xdr_generic_get before the failing field.
 struct unstager : cursor {
   const std::uint8_t *rec;
   const std::uint8_t *heap;
+  std::uint32_t stop = kNoStop;
+  void at_op() const {
+    if (pc == stop) throw stop_reached{};
+  }
   template <typename F> void operator()(F &f) {
     using P = plain<F>;
     using TR = xdr_traits<P>;
     if constexpr (std::is_same_v<P, bool>) {
       f = rec[next().noff] != 0;
+      at_op();
       ++pc;
     } else if constexpr (bytes_kind<P>::kind == XDRG_OP_OPAQUE) {
-      std::memcpy(f.data(), rec + next().noff, f.size());
+      const xdrg_op &o = next();
+      at_op();
+      std::memcpy(f.data(), rec + o.noff, f.size());
       ++pc;
     } else if constexpr (bytes_kind<P>::kind != 0) {
+      const xdrg_op &o = next();
+      at_op();
       xdrg_bytes_ref r;
-      std::memcpy(&r, rec + next().noff, sizeof r);
+      std::memcpy(&r, rec + o.noff, sizeof r);
       const char *p = reinterpret_cast<const char *>(heap + r.off);
       f.assign(p, p + r.len);
       ++pc;
     } else if constexpr (TR::is_enum || TR::is_numeric) {
       const xdrg_op &o = next();
+      at_op();
       std::memcpy(&f, rec + o.noff, sizeof(P));
       if (o.kind == XDRG_OP_UNION) branch(o, static_cast<std::int32_t>(f));
       else ++pc;
     } else if constexpr (vector_info<P>::value) {
       const xdrg_op &o = next();
+      at_op();
       xdrg_bytes_ref r;
       std::memcpy(&r, rec + o.noff, sizeof r);
+      // a decode that failed inside element r.rsv decoded the ones before it
+      const bool inside = stop != kNoStop && stop > pc && stop <= pc + o.arg2;
+      const std::uint32_t whole = inside ? std::min(r.rsv, r.len) : r.len;
       if constexpr (vector_info<P>::pointer) {
         if (r.len) f.activate(); else f.reset();
       } else {
@@ -532,14 +587,18 @@ struct unstager : cursor {
       }
       std::uint32_t i = 0;
       for (auto &e : f) {
+        if (i > whole || (i == whole && !inside)) break;
         unstager u2;
         u2.ops = ops;
         u2.table = table;
         u2.pc = pc + 1;
-        u2.rec = heap + r.off + std::uint64_t(i++) * o.arg1;
+        u2.rec = heap + r.off + std::uint64_t(i) * o.arg1;
         u2.heap = heap;
+        if (i == whole) u2.stop = stop;
         u2(e);
+        ++i;
       }
+      if (inside) throw stop_reached{};
       pc += 1 + o.arg2;
     } else if constexpr (xarray_info<P>::value) {
       for (auto &e : f) (*this)(e);
@@ -592,6 +651,8 @@ template <typename T> class batch_plan {
   bool identity() const { return identity_; }
   bool fixed() const { return fixed_; }
   std::uint32_t fixed_size() const { return fixed_size_; }
+  //! Some struct or union of T has a user validate() hook.
+  bool validates() const { return validates_; }
 
   //! Throw the reference's exception for a device status.
   [[noreturn]] void raise(const xdrg_error &e) const {
@@ -623,6 +684,7 @@ template <typename T> class batch_plan {
     stride_ = detail::align_up(std::max<std::uint32_t>(sp.size, 1), std::max<std::uint32_t>(sp.align, 4));
     identity_ = sp.identity && sp.fixed && sizeof(T) == stride_;
     fixed_ = sp.fixed;
+    validates_ = sp.validates;
     xdrg_plan *h = nullptr;
     detail::abicheck(xdrg_plan_create(ops_.data(), static_cast<std::uint32_t>(ops_.size()),
                                       table_.empty() ? nullptr : table_.data(),
@@ -638,7 +700,7 @@ template <typename T> class batch_plan {
   std::vector<std::uint32_t> table_;
   std::vector<std::pair<std::uint32_t, std::string>> msgs_;
   std::uint32_t stride_ = 0, fixed_size_ = 0;
-  bool identity_ = false, fixed_ = false;
+  bool identity_ = false, fixed_ = false, validates_ = false;
 };
 
 template <typename T> const batch_plan<T> &plan_for() { return batch_plan<T>::get(); }
@@ -672,7 +734,7 @@ template <typename T> staged_batch stage(const T *recs, std::size_t n) {
 template <typename T>
 void unstage(const std::uint8_t *native, const std::uint8_t *heap, std::size_t n, T *out) {
   const batch_plan<T> &P = plan_for<T>();
-  if (P.identity()) {
+  if (P.identity() && !P.validates()) {
     std::memcpy(static_cast<void *>(out), native, n * sizeof(T));
     return;
   }
@@ -684,6 +746,41 @@ void unstage(const std::uint8_t *native, const std::uint8_t *heap, std::size_t n
     u.heap = heap;
     u(out[i]);
   }
+}
+
+//! The records of a device decode whose status is `e`, in the order
+//! xdr_from_opaque / xdr_from_msg would load them: records before the
+//! failing one are unstaged in full (their validate() hooks run and the
+//! first hook that throws wins, xdrc/gen_hh.cc:244-247), then the failing
+//! record up to the op the device failed at, then the device's error is
+//! raised.  A record-level error (op 0xffffffff) at record r < n raises
+//! before record r; one at record n (trailing bytes, seen by done() after
+//! every record loaded) raises after all of them.
+template <typename T>
+void unstage_checked(const std::uint8_t *native, const std::uint8_t *heap, std::size_t n, T *out,
+                     const xdrg_error &e) {
+  const batch_plan<T> &P = plan_for<T>();
+  if (!e.code) {
+    unstage(native, heap, n, out);
+    return;
+  }
+  const std::size_t bad = static_cast<std::size_t>(std::min<std::uint64_t>(e.record, n));
+  if (P.validates()) {
+    unstage(native, heap, bad, out);
+    if (bad < n && e.op != 0xffffffffu) {
+      detail::unstager u;
+      u.ops = P.ops().data();
+      u.table = P.table().data();
+      u.rec = native + bad * P.stride();
+      u.heap = heap;
+      u.stop = e.op;
+      try {
+        u(out[bad]);
+      } catch (const detail::stop_reached &) {
+      }
+    }
+  }
+  P.raise(e);
 }
 
 //! Record index of a concatenated batch (host walk of lengths and
@@ -813,8 +910,7 @@ void from_opaque_batch(const void *bytes, std::size_t len, T *out, std::size_t n
     detail::hipcheck(hipMemcpyAsync(heap.data(), d_heap.p, heap.size(), hipMemcpyDeviceToHost, s), "D2H");
   xdrg_error e{};
   detail::abicheck(xdrg_status_read(d_st.p, s, &e), "xdrg_status_read");
-  if (e.code) P.raise(e);
-  unstage(nat.data(), heap.data(), n, out);
+  unstage_checked(nat.data(), heap.data(), n, out, e);
 }
 
 // ------------------------------------------------------ sizes and depths
@@ -933,8 +1029,7 @@ void decode_msgs(const std::uint8_t *x, std::size_t len, const std::vector<std::
     hipcheck(hipMemcpyAsync(heap.data(), d_heap.p, heap.size(), hipMemcpyDeviceToHost, s), "D2H");
   xdrg_error e{};
   abicheck(xdrg_status_read(d_st.p, s, &e), "xdrg_status_read");
-  if (e.code) P.raise(e);
-  unstage(nat.data(), heap.data(), n, out);
+  unstage_checked(nat.data(), heap.data(), n, out, e);
 }
 
 // The raw bytes (mark + body) of a vector of messages, back to back.

@@ -18,6 +18,58 @@
 //                                    from_msg_batch / from_msg_stream back;
 //                                    rpc_dispatch_batch / rpc_error_replies
 //                                    against the reference's RPC fixtures
+// Types with user validate() hooks, in the shape xdrc emits them: load()
+// ends with `using xdr::validate; validate(obj);` (xdrc/gen_hh.cc:244-247),
+// and the hook is declared before the traits, as tests/validate.cc does for
+// fix_4 (tests/validate.cc:7-9,21-26).
+#include <xdrpp/types.h>
+struct vfix {  // tests/xdrtest.x fix_4: struct fix_4 { int i; };
+  std::int32_t i;
+};
+struct vnest {  // struct vnest { string pre<8>; fix_4 inner; string name<16>; };
+  xdr::xstring<8> pre;
+  vfix inner;
+  xdr::xstring<16> name;
+};
+void validate(const vfix &f);
+void validate(const vnest &v);
+namespace xdr {
+template <>
+struct xdr_traits<::vfix> : xdr_struct_base<field_ptr<::vfix, decltype(::vfix::i), &::vfix::i>> {
+  template <typename Archive> static void save(Archive &ar, const ::vfix &obj) { archive(ar, obj.i, "i"); }
+  template <typename Archive> static void load(Archive &ar, ::vfix &obj) {
+    archive(ar, obj.i, "i");
+    using xdr::validate;
+    validate(obj);
+  }
+};
+template <>
+struct xdr_traits<::vnest>
+    : xdr_struct_base<field_ptr<::vnest, decltype(::vnest::pre), &::vnest::pre>,
+                      field_ptr<::vnest, decltype(::vnest::inner), &::vnest::inner>,
+                      field_ptr<::vnest, decltype(::vnest::name), &::vnest::name>> {
+  template <typename Archive> static void save(Archive &ar, const ::vnest &obj) {
+    archive(ar, obj.pre, "pre");
+    archive(ar, obj.inner, "inner");
+    archive(ar, obj.name, "name");
+  }
+  template <typename Archive> static void load(Archive &ar, ::vnest &obj) {
+    archive(ar, obj.pre, "pre");
+    archive(ar, obj.inner, "inner");
+    archive(ar, obj.name, "name");
+    using xdr::validate;
+    validate(obj);
+  }
+};
+}  // namespace xdr
+// tests/validate.cc:21-26
+void validate(const vfix &f) {
+  if (f.i == 0) throw xdr::xdr_invariant_failed("fix_4::i has value 0");
+}
+void validate(const vnest &v) {
+  if (v.name == "bad") throw xdr::xdr_invariant_failed("vnest::name is bad");
+}
+
 #include "ref_objects.hh"
 #include "xdrpp_gpu.hh"
 
@@ -332,6 +384,79 @@ static void gpu_errors() {
   check_error<rec128>("rec128 short", fs, f.size());
 }
 
+// User validate() hooks in batch decode (xdrc/gen_hh.cc:244-247): the
+// first failing hook or device error in the reference's load order wins.
+static void gpu_validate() {
+  CHECK(xdr::gpu::plan_for<vfix>().validates() && xdr::gpu::plan_for<vfix>().identity(),
+        "vfix: identity layout with a validate hook");
+  CHECK(!xdr::gpu::plan_for<rec128>().validates(), "rec128 has no validate hook");
+  std::vector<std::uint64_t> off;
+  std::vector<vfix> f(1000);
+  for (std::size_t i = 0; i < f.size(); ++i) f[i].i = std::int32_t(i + 1);
+  {  // all valid: decodes, hooks pass
+    auto x = ref_stream(f, off);
+    std::vector<vfix> back(f.size());
+    xdr::gpu::from_opaque_batch(x.data(), x.size(), back.data(), back.size());
+    CHECK(std::memcmp(back.data(), f.data(), f.size() * sizeof(vfix)) == 0, "vfix round trip");
+  }
+  f[3].i = 0;
+  check_error<vfix>("vfix hook at record 3", ref_stream(f, off), f.size());
+  {  // hook at record 3 and the stream ends inside record 500: the hook first
+    auto x = ref_stream(f, off);
+    x.resize(off[500]);
+    check_error<vfix>("vfix hook at 3 before short stream at 500", x, f.size());
+  }
+  f[3].i = 4;
+  f[700].i = 0;
+  {  // device error at 500 before the hook at 700
+    auto x = ref_stream(f, off);
+    x.resize(off[500]);
+    check_error<vfix>("vfix short stream at 500 before hook at 700", x, f.size());
+  }
+  std::vector<vnest> v(300);
+  for (std::size_t i = 0; i < v.size(); ++i) {
+    v[i].pre = std::string(i % 9, 'p');
+    v[i].inner.i = std::int32_t(i + 1);
+    v[i].name = std::string(i % 17, 'n');
+  }
+  {
+    auto x = ref_stream(v, off);
+    std::vector<vnest> back(v.size());
+    xdr::gpu::from_opaque_batch(x.data(), x.size(), back.data(), back.size());
+    bool same = true;
+    for (std::size_t i = 0; i < v.size(); ++i)
+      same = same && back[i].pre == v[i].pre && back[i].inner.i == v[i].inner.i && back[i].name == v[i].name;
+    CHECK(same, "vnest round trip");
+  }
+  v[10].inner.i = 0;
+  {  // inner hook at record 10, then name over its bound in record 10: the hook
+    auto x = ref_stream(v, off);
+    const std::size_t at = off[10] + 4 + ((v[10].pre.size() + 3) & ~std::size_t(3)) + 4;
+    x[at + 3] = 17;  // name length 17 > 16
+    check_error<vnest>("vnest inner hook before name bound", x, v.size());
+  }
+  {  // pre over its bound in record 10, before the inner hook: the bound
+    auto x = ref_stream(v, off);
+    x[off[10] + 3] = 9;
+    check_error<vnest>("vnest pre bound before inner hook", x, v.size());
+  }
+  v[10].inner.i = 11;
+  v[20].name = "bad";
+  check_error<vnest>("vnest outer hook at 20", ref_stream(v, off), v.size());
+  {  // messages: xdr_from_msg per message, the same order
+    std::vector<xdr::msg_ptr> msgs;
+    for (const vnest &r : v) msgs.push_back(xdr::xdr_to_msg(r));
+    std::vector<vnest> a(v.size()), b(v.size());
+    auto ref = catch_what([&] {
+      for (std::size_t i = 0; i < msgs.size(); ++i) xdr::xdr_from_msg(msgs[i], a[i]);
+    });
+    auto gpu = catch_what([&] { xdr::gpu::from_msg_batch(msgs, b.data()); });
+    CHECK(ref == gpu, "vnest msgs: reference %s(\"%s\") vs gpu %s(\"%s\")", ref.first.c_str(),
+          ref.second.c_str(), gpu.first.c_str(), gpu.second.c_str());
+    std::printf("error vnest msgs hook at 20: %s(\"%s\") matches\n", ref.first.c_str(), ref.second.c_str());
+  }
+}
+
 int main(int argc, char **argv) {
   const std::string mode = argc > 1 ? argv[1] : "stage";
   std::vector<testns::numerics> nu;
@@ -365,6 +490,7 @@ int main(int argc, char **argv) {
     check_gpu("rpc", rp);
     check_gpu("vecrec", vr);
     gpu_errors();
+    gpu_validate();
     check_msgs("numerics", nu);
     check_msgs("rec128", rc);
     check_msgs("recvar", rv);

@@ -294,7 +294,7 @@ template <typename RD>
 __device__ bool dec_vector_elems(const xdrg_op *__restrict__ ops, const uint32_t *__restrict__ table,
                                  uint32_t b0, uint32_t nb, uint32_t cnt, uint32_t es, uint8_t *dst,
                                  uint64_t &p, uint64_t b, uint32_t stack_limit, uint64_t r,
-                                 unsigned long long *err, const RD &rd) {
+                                 unsigned long long *err, const RD &rd, uint32_t *done) {
   const bool w4 = (es & 3u) == 0;  // 4-byte stores (dst is 8-aligned)
   // Elements of at most 16 bytes made of word-aligned scalars and bools are
   // assembled in four registers and written with one or two 8-byte stores:
@@ -316,9 +316,9 @@ __device__ bool dec_vector_elems(const xdrg_op *__restrict__ ops, const uint32_t
       };
       for (uint32_t k = 0; k < nb; ++k) {
         const xdrg_op e = load_op(ops, b0 + k);
-        if (e.depth > stack_limit) { report(err, r, b0 + k, XDRG_ERR_STACK_GET); return false; }
+        if (e.depth > stack_limit) { report(err, r, b0 + k, XDRG_ERR_STACK_GET); *done = i; return false; }
         const uint32_t need = e.kind == XDRG_OP_U64 ? 8u : 4u;
-        if (b - p < need) { report(err, r, b0 + k, XDRG_ERR_OVERFLOW_GET); return false; }
+        if (b - p < need) { report(err, r, b0 + k, XDRG_ERR_OVERFLOW_GET); *done = i; return false; }
         const uint32_t j = e.noff >> 2;
         if (e.kind == XDRG_OP_BOOL) {
           put(j, (rd(p) != 0u ? 1u : 0u) << (8u * (e.noff & 3u)));
@@ -330,6 +330,7 @@ __device__ bool dec_vector_elems(const xdrg_op *__restrict__ ops, const uint32_t
           put(j, v);
           if (e.kind == XDRG_OP_ENUM && (e.flags & XDRG_F_VALIDATE) && !enum_ok(table, e.arg0, e.arg1, v)) {
             report(err, r, b0 + k, XDRG_ERR_INVALID_ENUM);
+            *done = i;
             return false;
           }
         }
@@ -352,9 +353,9 @@ __device__ bool dec_vector_elems(const xdrg_op *__restrict__ ops, const uint32_t
     else for (uint32_t z = 0; z < es; ++z) el[z] = 0;
     for (uint32_t k = 0; k < nb; ++k) {
       const xdrg_op e = load_op(ops, b0 + k);
-      if (e.depth > stack_limit) { report(err, r, b0 + k, XDRG_ERR_STACK_GET); return false; }
+      if (e.depth > stack_limit) { report(err, r, b0 + k, XDRG_ERR_STACK_GET); *done = i; return false; }
       const uint32_t need = e.kind == XDRG_OP_U64 ? 8u : e.kind == XDRG_OP_OPAQUE ? e.arg0 : 4u;
-      if (b - p < need) { report(err, r, b0 + k, XDRG_ERR_OVERFLOW_GET); return false; }
+      if (b - p < need) { report(err, r, b0 + k, XDRG_ERR_OVERFLOW_GET); *done = i; return false; }
       uint8_t *f = el + e.noff;
       switch (e.kind) {
       case XDRG_OP_BOOL:
@@ -374,6 +375,7 @@ __device__ bool dec_vector_elems(const xdrg_op *__restrict__ ops, const uint32_t
         }
         if ((BL & 3u) && (rd(p + (BL & ~3u)) & ~keep_mask(BL & 3u))) {
           report(err, r, b0 + k, XDRG_ERR_NONZERO_PAD);
+          *done = i;
           return false;
         }
         break;
@@ -384,6 +386,7 @@ __device__ bool dec_vector_elems(const xdrg_op *__restrict__ ops, const uint32_t
         else for (int q = 0; q < 4; ++q) f[q] = uint8_t(v >> (8 * q));
         if (e.kind == XDRG_OP_ENUM && (e.flags & XDRG_F_VALIDATE) && !enum_ok(table, e.arg0, e.arg1, v)) {
           report(err, r, b0 + k, XDRG_ERR_INVALID_ENUM);
+          *done = i;
           return false;
         }
         break;
@@ -823,7 +826,7 @@ __global__ __launch_bounds__(256) void k_var_decode(
       st32(nat + op.noff + 8, cnt);
       auto rd = [&](uint64_t q) { return ld32(xdr + q); };
       if (!dec_vector_elems(sops, table, pc + 1, op.arg2, cnt, op.arg1, heap + ecur, p, b,
-                            stack_limit, r, err, rd))
+                            stack_limit, r, err, rd, reinterpret_cast<uint32_t *>(nat + op.noff + 12)))
         return;
       ecur += static_cast<uint64_t>(cnt) * op.arg1;
       pc += 1 + op.arg2;
@@ -1356,7 +1359,7 @@ __global__ __launch_bounds__(64) void k_var_decode_w(
         *reinterpret_cast<uint64_t *>(nat + op.noff) = ecur;
         nw[2] = cnt;
         if (!dec_vector_elems(ops, table, upc + 1, op.arg2, cnt, op.arg1, heap + ecur, p, b,
-                              stack_limit, r, err, rd)) {
+                              stack_limit, r, err, rd, &nw[3])) {
           ok = false; pc = kPcDone; break;
         }
         ecur += static_cast<uint64_t>(cnt) * op.arg1;
