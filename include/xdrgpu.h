@@ -51,8 +51,12 @@
 #ifndef XDRGPU_H_INCLUDED
 #define XDRGPU_H_INCLUDED 1
 
+#ifdef __HIPCC_RTC__ /* plan-specialized kernels compiled by hiprtc */
+#include <stdint.h>
+#else
 #include <stddef.h>
 #include <stdint.h>
+#endif
 
 #ifdef __cplusplus
 extern "C" {

@@ -13,8 +13,8 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 SOURCES = [os.path.join(CSRC, "plan.cpp"), os.path.join(CSRC, "xdrgpu.hip"),
            os.path.join(CSRC, "rpc.hip")]
-DEPS = SOURCES + [os.path.join(CSRC, "plan.h"), os.path.join(CSRC, "kernels.h"),
-                  os.path.join(ROOT, "include", "xdrgpu.h")]
+DEPS = SOURCES + [os.path.join(CSRC, h) for h in ("plan.h", "kernels.h", "dev_common.h", "var_kernels.h")] \
+    + [os.path.join(ROOT, "include", "xdrgpu.h")]
 OUT = os.path.join(PKG, "libxdrgpu.so")
 ARCH = os.environ.get("XDRG_OFFLOAD_ARCH", "gfx950")
 
@@ -37,7 +37,7 @@ def build(force: bool = False, verbose: bool = True) -> str:
     if not force and up_to_date():
         return OUT
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-           "-o", OUT] + SOURCES
+           "-I", os.path.join(ROOT, "include"), "-o", OUT] + SOURCES
     if verbose:
         print("[xdrpp_amd.build]", " ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd)

@@ -1,0 +1,142 @@
+// Device helpers shared by the library's kernels (xdrgpu.hip, rpc.hip) and
+// by the plan-specialized kernels compiled at plan time (hiprtc, see
+// spec.cpp): byte swaps, error reports, unaligned and clamped loads, LDS
+// staging, record marks, cross-lane reads.  Self-contained so hiprtc can
+// compile it (no C++ standard headers).
+#pragma once
+#ifndef __HIPCC_RTC__
+#include <hip/hip_runtime.h>
+#endif
+#include "xdrgpu.h"
+
+namespace xdrg {
+namespace dev {
+
+constexpr uint32_t kOpRecordLevel = 0xffff;  // op field for record-level errors
+constexpr uint32_t kSizeErr = 0x80000000u;  // size-pass marker of a failed record
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t v) { return __builtin_bswap32(v); }
+
+// D = bytes of {hi:lo} picked by sel (v_perm_b32): 0-3 from lo, 4-7 from hi,
+// 0x0C -> 0x00.
+__device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
+  return __builtin_amdgcn_perm(hi, lo, sel);
+}
+
+// The lowest failing (record, op) wins: the record at which the
+// reference's sequential archive would have thrown.
+__device__ __forceinline__ void report(unsigned long long *err, uint64_t rec, uint32_t op,
+                                       uint32_t code) {
+  const unsigned long long key =
+      (static_cast<unsigned long long>(rec) << 24) |
+      (static_cast<unsigned long long>(op & 0xffffu) << 8) | code;
+  atomicMin(err, key);
+}
+
+// Uniform trip count, no per-lane exit: the table reads stay scalar.
+__device__ __forceinline__ bool enum_ok(const uint32_t *__restrict__ table, uint32_t idx,
+                                        uint32_t cnt, uint32_t v) {
+  bool ok = false;
+  for (uint32_t i = 0; i < cnt; ++i) ok |= table[idx + i] == v;
+  return ok;
+}
+
+__device__ __forceinline__ uint32_t ld32(const uint8_t *p) {
+  return *reinterpret_cast<const uint32_t *>(p);
+}
+__device__ __forceinline__ void st32(uint8_t *p, uint32_t v) {
+  *reinterpret_cast<uint32_t *>(p) = v;
+}
+
+// Little-endian word made of the 4 bytes at [p + off, p + off + 4) of a
+// 4-byte-aligned buffer of `len` bytes; bytes at or past `len` read as 0.
+__device__ __forceinline__ uint32_t partial_word(const uint8_t *p, uint64_t len, uint64_t a) {
+  uint32_t v = 0;
+  for (uint32_t k = 0; k < 4; ++k)
+    if (a + k < len) v |= static_cast<uint32_t>(p[a + k]) << (8 * k);
+  return v;
+}
+__device__ __forceinline__ uint32_t unaligned_word(const uint8_t *p, uint64_t len, uint64_t off) {
+  const uint64_t a = off & ~3ull;
+  const uint32_t sh = static_cast<uint32_t>(off & 3u);
+  const uint32_t lo = (a + 4 <= len) ? ld32(p + a) : partial_word(p, len, a);
+  if (sh == 0) return lo;
+  const uint32_t hi = (a + 8 <= len) ? ld32(p + a + 4) : partial_word(p, len, a + 4);
+  return __builtin_amdgcn_alignbyte(hi, lo, sh);
+}
+__device__ __forceinline__ uint32_t keep_mask(uint32_t nbytes) {  // nbytes in 1..4
+  return nbytes >= 4 ? 0xffffffffu : ((1u << (8u * nbytes)) - 1u);
+}
+__device__ __forceinline__ uint32_t keep_bytes(int32_t k) {  // mask of the low k bytes, k clamped
+  return k <= 0 ? 0u : k >= 4 ? 0xffffffffu : ((1u << (8 * k)) - 1u);
+}
+
+// Unaligned 16-byte global access: correct at any byte alignment on gfx950
+// (tools/probe/unaligned.hip).
+__device__ __forceinline__ u32x4 ld16u(const uint8_t *p) { return *reinterpret_cast<const u32x4 *>(p); }
+__device__ __forceinline__ void st16u(uint8_t *p, u32x4 v) { *reinterpret_cast<u32x4 *>(p) = v; }
+
+// Single-wave workgroups: LDS written by some lanes and read by others needs
+// only ordering within the wave (LDS executes a wave's instructions in
+// order), not __syncthreads(), whose workgroup-scope release would also
+// wait for every outstanding global store of the wave (s_waitcnt vmcnt(0)).
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Stage nbytes (a multiple of 4) of native records from a 16-byte aligned
+// global address to LDS: 16-byte loads, up to 4 per lane in flight before
+// any LDS store (one memory round trip per 4 KiB per wave).
+__device__ __forceinline__ void stage_tile(uint8_t *tile, const uint8_t *src, uint32_t nbytes,
+                                           uint32_t lane, uint32_t nthreads) {
+  const uint32_t n16 = nbytes / 16u;
+  for (uint32_t i0 = 0; i0 < n16; i0 += 4u * nthreads) {
+    u32x4 t[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t i = i0 + k * nthreads + lane;
+      if (i < n16) t[k] = reinterpret_cast<const u32x4 *>(src)[i];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t i = i0 + k * nthreads + lane;
+      if (i < n16) reinterpret_cast<u32x4 *>(tile)[i] = t[k];
+    }
+  }
+  for (uint32_t i = n16 * 4u + lane; i < nbytes / 4u; i += nthreads)
+    reinterpret_cast<uint32_t *>(tile)[i] = reinterpret_cast<const uint32_t *>(src)[i];
+}
+
+// ------------------------------------------- record marks (RFC 5531)
+// message_t keeps a 4-byte mark BE(size | 0x80000000) in front of the
+// message bytes (message_t::alloc, xdrpp/marshal.cc:15-31: always one
+// last-fragment record).
+__device__ __forceinline__ uint32_t mark_word(uint32_t size) { return bswap32(size | XDRG_MARK_LAST); }
+
+// Framing checks of a message whose record index gives it `body` bytes
+// after the mark, in read_message's order (xdrpp/srpc.cc:29-55).  The
+// first test reads the mark before swap32le, so on a little-endian host it
+// looks at the low bits of the mark's first byte (bits 24-25 of the size),
+// which is what the reference does on this platform.  0 = well framed.
+__device__ __forceinline__ uint32_t mark_code(uint32_t raw, uint64_t body) {
+  if (raw & 3u) return XDRG_ERR_MSG_SIZE4;          // srpc.cc:38-39
+  const uint32_t v = bswap32(raw);
+  if (!(v & XDRG_MARK_LAST)) return XDRG_ERR_MSG_FRAGMENT;  // srpc.cc:41-45
+  if ((v & ~XDRG_MARK_LAST) != body) return XDRG_ERR_MSG_MISMATCH;
+  return 0u;
+}
+
+// Registers of one lane read by the whole wave (v_readlane).
+__device__ __forceinline__ uint32_t rl32(uint32_t v, uint32_t lane) {
+  return __builtin_amdgcn_readlane(v, lane);
+}
+__device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t lane) {
+  return static_cast<uint64_t>(rl32(static_cast<uint32_t>(v), lane)) |
+         (static_cast<uint64_t>(rl32(static_cast<uint32_t>(v >> 32), lane)) << 32);
+}
+
+}  // namespace dev
+}  // namespace xdrg

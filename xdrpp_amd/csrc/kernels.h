@@ -4,45 +4,17 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "dev_common.h"
 #include "plan.h"
 
 namespace xdrg {
 namespace dev {
-
-constexpr uint32_t kOpRecordLevel = 0xffff;  // op field for record-level errors
-
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-// ------------------------------------------------------------------ device
-__device__ __forceinline__ uint32_t bswap32(uint32_t v) { return __builtin_bswap32(v); }
-
-// D = bytes of {hi:lo} picked by sel (v_perm_b32): 0-3 from lo, 4-7 from hi,
-// 0x0C -> 0x00.
-__device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
-  return __builtin_amdgcn_perm(hi, lo, sel);
-}
 
 // xdr_traits<bool> (xdrpp/types.h:335-349).  sel: src byte | dst byte << 8 |
 // whole-word test << 16.
 __device__ __forceinline__ uint32_t bool_term(uint32_t v, uint32_t sel) {
   const bool nz = (sel & 0x10000u) ? (v != 0u) : (((v >> (8u * (sel & 3u))) & 0xffu) != 0u);
   return nz ? (1u << (8u * ((sel >> 8) & 3u))) : 0u;
-}
-
-__device__ __forceinline__ void report(unsigned long long *err, uint64_t rec, uint32_t op,
-                                       uint32_t code) {
-  const unsigned long long key =
-      (static_cast<unsigned long long>(rec) << 24) |
-      (static_cast<unsigned long long>(op & 0xffffu) << 8) | code;
-  atomicMin(err, key);
-}
-
-// Uniform trip count, no per-lane exit: the table reads stay scalar.
-__device__ __forceinline__ bool enum_ok(const uint32_t *__restrict__ table, uint32_t idx,
-                                        uint32_t cnt, uint32_t v) {
-  bool ok = false;
-  for (uint32_t i = 0; i < cnt; ++i) ok |= table[idx + i] == v;
-  return ok;
 }
 
 // Decode-time word checks: padding of fixed opaque (marshal.cc:52-55) and

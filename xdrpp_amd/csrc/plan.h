@@ -6,7 +6,7 @@
 #include <mutex>
 #include <vector>
 
-#include "../../include/xdrgpu.h"
+#include "xdrgpu.h"
 
 namespace xdrg {
 

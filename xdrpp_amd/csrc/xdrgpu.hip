@@ -49,38 +49,12 @@ int hip_fail(hipError_t e, const char *what) {
 }  // namespace
 
 #include "kernels.h"
+#include "var_kernels.h"
 using namespace xdrg::dev;
 
 namespace {
 
 // ------------------------------------------------------------ var: helpers
-__device__ __forceinline__ uint32_t ld32(const uint8_t *p) {
-  return *reinterpret_cast<const uint32_t *>(p);
-}
-__device__ __forceinline__ void st32(uint8_t *p, uint32_t v) {
-  *reinterpret_cast<uint32_t *>(p) = v;
-}
-
-// Little-endian word made of the 4 bytes at [p + off, p + off + 4) of a
-// 4-byte-aligned buffer of `len` bytes; bytes at or past `len` read as 0.
-__device__ __forceinline__ uint32_t partial_word(const uint8_t *p, uint64_t len, uint64_t a) {
-  uint32_t v = 0;
-  for (uint32_t k = 0; k < 4; ++k)
-    if (a + k < len) v |= static_cast<uint32_t>(p[a + k]) << (8 * k);
-  return v;
-}
-__device__ __forceinline__ uint32_t unaligned_word(const uint8_t *p, uint64_t len, uint64_t off) {
-  const uint64_t a = off & ~3ull;
-  const uint32_t sh = static_cast<uint32_t>(off & 3u);
-  const uint32_t lo = (a + 4 <= len) ? ld32(p + a) : partial_word(p, len, a);
-  if (sh == 0) return lo;
-  const uint32_t hi = (a + 8 <= len) ? ld32(p + a + 4) : partial_word(p, len, a + 4);
-  return __builtin_amdgcn_alignbyte(hi, lo, sh);
-}
-__device__ __forceinline__ uint32_t keep_mask(uint32_t nbytes) {  // nbytes in 1..4
-  return nbytes >= 4 ? 0xffffffffu : ((1u << (8u * nbytes)) - 1u);
-}
-
 // A plan op at a wave-uniform index, read as 8 dwords through the scalar
 // cache (s_load_dwordx8) and unpacked.  Reading the struct directly makes
 // the compiler fetch the byte fields (kind, flags) with a vector
@@ -123,68 +97,6 @@ __device__ __forceinline__ void load_ops(xdrg_op *sops, const xdrg_op *__restric
   for (uint32_t i = threadIdx.x; i < nops * 8u; i += blockDim.x) d[i] = s[i];
   __syncthreads();
 }
-
-// Unaligned 16-byte global access: correct at any byte alignment on gfx950
-// (tools/probe/unaligned.hip).
-__device__ __forceinline__ u32x4 ld16u(const uint8_t *p) { return *reinterpret_cast<const u32x4 *>(p); }
-__device__ __forceinline__ void st16u(uint8_t *p, u32x4 v) { *reinterpret_cast<u32x4 *>(p) = v; }
-__device__ __forceinline__ uint32_t keep_bytes(int32_t k) {  // mask of the low k bytes, k clamped
-  return k <= 0 ? 0u : k >= 4 ? 0xffffffffu : ((1u << (8 * k)) - 1u);
-}
-
-constexpr uint32_t kSizeErr = 0x80000000u;
-
-// Single-wave workgroups: LDS written by some lanes and read by others needs
-// only ordering within the wave (LDS executes a wave's instructions in
-// order), not __syncthreads(), whose workgroup-scope release would also
-// wait for every outstanding global store of the wave (s_waitcnt vmcnt(0)).
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-}
-
-// Stage nbytes (a multiple of 4) of native records from a 16-byte aligned
-// global address to LDS: 16-byte loads, up to 4 per lane in flight before
-// any LDS store (one memory round trip per 4 KiB per wave).
-__device__ __forceinline__ void stage_tile(uint8_t *tile, const uint8_t *src, uint32_t nbytes,
-                                           uint32_t lane, uint32_t nthreads) {
-  const uint32_t n16 = nbytes / 16u;
-  for (uint32_t i0 = 0; i0 < n16; i0 += 4u * nthreads) {
-    u32x4 t[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t i = i0 + k * nthreads + lane;
-      if (i < n16) t[k] = reinterpret_cast<const u32x4 *>(src)[i];
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t i = i0 + k * nthreads + lane;
-      if (i < n16) reinterpret_cast<u32x4 *>(tile)[i] = t[k];
-    }
-  }
-  for (uint32_t i = n16 * 4u + lane; i < nbytes / 4u; i += nthreads)
-    reinterpret_cast<uint32_t *>(tile)[i] = reinterpret_cast<const uint32_t *>(src)[i];
-}
-
-// ------------------------------------------- record marks (RFC 5531)
-// message_t keeps a 4-byte mark BE(size | 0x80000000) in front of the
-// message bytes (message_t::alloc, xdrpp/marshal.cc:15-31: always one
-// last-fragment record).
-__device__ __forceinline__ uint32_t mark_word(uint32_t size) { return bswap32(size | XDRG_MARK_LAST); }
-
-// Framing checks of a message whose record index gives it `body` bytes
-// after the mark, in read_message's order (xdrpp/srpc.cc:29-55).  The
-// first test reads the mark before swap32le, so on a little-endian host it
-// looks at the low bits of the mark's first byte (bits 24-25 of the size),
-// which is what the reference does on this platform.  0 = well framed.
-__device__ __forceinline__ uint32_t mark_code(uint32_t raw, uint64_t body) {
-  if (raw & 3u) return XDRG_ERR_MSG_SIZE4;          // srpc.cc:38-39
-  const uint32_t v = bswap32(raw);
-  if (!(v & XDRG_MARK_LAST)) return XDRG_ERR_MSG_FRAGMENT;  // srpc.cc:41-45
-  if ((v & ~XDRG_MARK_LAST) != body) return XDRG_ERR_MSG_MISMATCH;
-  return 0u;
-}
-
 
 // ------------------------------------------- var: xvector<T> / pointer<T>
 // Elements of a VECTOR op (fixed-size element plans; ops [b0, b0+nb)).
@@ -294,7 +206,7 @@ template <typename RD>
 __device__ bool dec_vector_elems(const xdrg_op *__restrict__ ops, const uint32_t *__restrict__ table,
                                  uint32_t b0, uint32_t nb, uint32_t cnt, uint32_t es, uint8_t *dst,
                                  uint64_t &p, uint64_t b, uint32_t stack_limit, uint64_t r,
-                                 unsigned long long *err, const RD &rd, uint32_t *done) {
+                                 unsigned long long *err, RD &rd, uint32_t *done) {
   const bool w4 = (es & 3u) == 0;  // 4-byte stores (dst is 8-aligned)
   // Elements of at most 16 bytes made of word-aligned scalars and bools are
   // assembled in four registers and written with one or two 8-byte stores:
@@ -841,125 +753,28 @@ overflow:
   report(err, r, pc, XDRG_ERR_OVERFLOW_GET);
 }
 
-// Registers of one lane read by the whole wave (v_readlane).
-__device__ __forceinline__ uint32_t rl32(uint32_t v, uint32_t lane) {
-  return __builtin_amdgcn_readlane(v, lane);
-}
-__device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t lane) {
-  return static_cast<uint64_t>(rl32(static_cast<uint32_t>(v), lane)) |
-         (static_cast<uint64_t>(rl32(static_cast<uint32_t>(v >> 32), lane)) << 32);
-}
+// ------------------------------------------ var: the plan interpreter walk
+// The walker of var_kernels.h for any plan: a wave-uniform sweep over the
+// op DAG (jumps are forward-only, so one sweep upc = 0..nops-1 visits every
+// op a lane can reach).  At each upc the op is read through the scalar cache
+// and dispatched with scalar branches; only the lanes whose own pc equals
+// upc do the field work.  Plans compiled to straight-line code (spec.cpp)
+// replace this walk; the interpreter serves every plan, and any plan on a
+// device where its specialized kernels are not loaded.
+struct interp_walk {
+  const xdrg_op *__restrict__ ops;
+  uint32_t nops;
+  const uint32_t *__restrict__ table;
 
-// -------------------------------------------- var: image encode (chunk map)
-// One workgroup = one wave = 64 consecutive records.  The wave's output
-// stretch [wave_out, wave_out + T) is assembled in an LDS image:
-//   * the lane-per-record walk of the plan (native fields from an LDS tile)
-//     writes each scalar wire word straight into the image;
-//   * payloads are cut into 16-byte chunks listed in a flat chunk map
-//     (u16: lane | slot | chunk), so every lane copies one chunk per step
-//     -- consecutive lanes take consecutive chunks of the same payload
-//     (coalesced heap reads) and no lane idles on a short record;
-//   * the image leaves with aligned 16-byte stores (image byte j sits at
-//     LDS j + (wave_out & 15), so LDS and global 16-byte chunks coincide).
-// Bytes past the image capacity C are written straight to global memory,
-// so a stretch of any size is handled in one pass.
-struct enc_i_lds {
-  uint32_t tile, desc, map, img, total;
-};
-__host__ __device__ inline enc_i_lds enc_i_layout(uint32_t stride, uint32_t KMAX, uint32_t MC,
-                                                 uint32_t C) {
-  enc_i_lds L;
-  L.tile = 0;
-  L.desc = (64u * stride + 15u) & ~15u;
-  L.map = L.desc + 64u * KMAX * 16u;
-  L.img = L.map + ((MC * 2u + 15u) & ~15u);
-  L.total = L.img + C + 32u;  // phase shift + the last (partial) chunk read
-  return L;
-}
-
-struct echunk_desc {  // 16 bytes: one payload slot of one lane
-  uint64_t src;       // heap byte offset
-  uint32_t dst;       // byte offset in the wave's stretch
-  uint32_t len;       // payload bytes
-};
-
-// Store word `v` at stretch offset `at`: image if it fits, else global.
-__device__ __forceinline__ void img_put(uint8_t *im, uint32_t C, uint8_t *gout, uint32_t at,
-                                        uint32_t v) {
-  if (at < C) *reinterpret_cast<uint32_t *>(im + at) = v;
-  else st32(gout + at, v);
-}
-
-template <int KMAX, int U>
-__global__ __launch_bounds__(64) void k_var_encode_i(
-    const uint8_t *__restrict__ native, uint64_t n, uint32_t stride, const uint8_t *__restrict__ heap,
-    uint64_t heap_len, uint8_t *__restrict__ xdr, uint64_t cap, uint64_t *__restrict__ offsets,
-    const uint32_t *__restrict__ sizes, const unsigned long long *__restrict__ block_base,
-    const xdrg_op *__restrict__ ops, uint32_t nops, const uint32_t *__restrict__ table,
-    uint32_t stack_limit, uint32_t MC, uint32_t C, uint32_t mark, unsigned long long *err) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
-  const enc_i_lds L = enc_i_layout(stride, KMAX, MC, C);
-  uint8_t *tile = sm + L.tile;
-  echunk_desc *desc = reinterpret_cast<echunk_desc *>(sm + L.desc);
-  uint16_t *map = reinterpret_cast<uint16_t *>(sm + L.map);
-  uint8_t *img = sm + L.img;
-  const uint32_t lane = threadIdx.x;
-  const uint64_t wr0 = static_cast<uint64_t>(blockIdx.x) * 64u;
-  const uint64_t r = wr0 + lane;
-  const uint32_t nrec = static_cast<uint32_t>(min<uint64_t>(64, n - wr0));
-
-  // ---- record offsets: wave scan of the sizes on top of the block base
-  // (sizes, block base and the native tile are loaded in one round trip)
-  const uint32_t sz = r < n ? sizes[r] : kSizeErr;
-  const uint64_t wave_out = block_base[blockIdx.x];
-  stage_tile(tile, native + wr0 * stride, nrec * stride, lane, 64u);
-  const bool szok = !(sz & kSizeErr);
-  const unsigned long long v = szok ? sz : 0ull;
-  unsigned long long incl = v;
-  for (int o = 1; o < 64; o <<= 1) {
-    const unsigned long long x = __shfl_up(incl, o, 64);
-    if (lane >= static_cast<uint32_t>(o)) incl += x;
-  }
-  const uint64_t T = rl64(incl, 63);  // bytes of the wave's stretch
-  const uint64_t off = wave_out + incl - v;
-  if (r < n) offsets[r] = off;
-  wave_sync();
-
-  const uint32_t sh = static_cast<uint32_t>(wave_out & 15u);
-  uint8_t *im = img + sh;               // image byte j <-> global wave_out + j
-  uint8_t *gout = xdr + wave_out;       // direct path for j >= C
-  const uint32_t rel = static_cast<uint32_t>(off - wave_out);
-
-  // ---- walk: scalar words -> image, payload slots -> registers
-  uint64_t psr[KMAX];
-  uint32_t pds[KMAX], pln[KMAX];
-#pragma unroll
-  for (int k = 0; k < KMAX; ++k) { psr[k] = 0; pds[k] = 0; pln[k] = 0; }
-  uint32_t nslot = 0;
-  {
-    const uint8_t *nat = tile + lane * stride;
-    uint32_t at = rel;  // stretch offset of the next wire word
-    uint64_t pos = off;
-    uint32_t pc = szok ? 0u : kPcDone;
-    bool ok = szok;
-    if (ok && mark) {  // the message's record mark (message_t::alloc, marshal.cc:15-31)
-      if (4 > cap - min(pos, cap)) {
-        report(err, r, kOpRecordLevel, XDRG_ERR_OVERFLOW_PUT);
-        ok = false;
-        pc = kPcDone;
-      } else {
-        img_put(im, C, gout, at, mark_word(sz - 4u));
-        at += 4;
-        pos += 4;
-      }
-    }
+  template <int KMAX>
+  __device__ bool enc(enc_ctx<KMAX> &c, const uint8_t *nat, bool ok) const {
+    uint32_t pc = ok ? 0u : kPcDone, nslot = 0;
     for (uint32_t upc = 0; upc < nops; ++upc) {
       if (!__any(pc == upc)) continue;
       const xdrg_op op = load_op(ops, upc);
       if (pc != upc) continue;
       if (op.kind == XDRG_OP_END) { pc = kPcDone; continue; }
       if (op.kind == XDRG_OP_JUMP) { pc = op.arg0; continue; }
-      if (op.depth > stack_limit) { report(err, r, upc, XDRG_ERR_STACK_PUT); ok = false; pc = kPcDone; continue; }
       const uint32_t *nw = reinterpret_cast<const uint32_t *>(nat + op.noff);
       uint32_t blen = 0;
       uint64_t need = 4;
@@ -969,54 +784,51 @@ __global__ __launch_bounds__(64) void k_var_encode_i(
         blen = nw[2];
         need = 4ull + blen;
       }
-      if (need > cap - min(pos, cap)) { report(err, r, upc, XDRG_ERR_OVERFLOW_PUT); ok = false; pc = kPcDone; continue; }
+      if (!c.field(upc, op.depth, need)) { ok = false; pc = kPcDone; continue; }
       switch (op.kind) {
-      case XDRG_OP_U32: case XDRG_OP_ENUM:
-        img_put(im, C, gout, at, bswap32(nw[0])); at += 4; pos += 4; ++pc; break;
-      case XDRG_OP_BOOL:
-        img_put(im, C, gout, at, nat[op.noff] ? 0x01000000u : 0u); at += 4; pos += 4; ++pc; break;
+      case XDRG_OP_U32: case XDRG_OP_ENUM: c.put(bswap32(nw[0])); ++pc; break;
+      case XDRG_OP_BOOL: c.put(nat[op.noff] ? 0x01000000u : 0u); ++pc; break;
       case XDRG_OP_U64:
-        img_put(im, C, gout, at, bswap32(nw[1]));
-        img_put(im, C, gout, at + 4, bswap32(nw[0]));
-        at += 8; pos += 8; ++pc; break;
+        c.put(bswap32(nw[1]));
+        c.put(bswap32(nw[0]));
+        ++pc;
+        break;
       case XDRG_OP_OPAQUE: {
         const uint32_t BL = op.arg0, nwd = (BL + 3u) >> 2;
         for (uint32_t k = 0; k < nwd; ++k) {
           uint32_t w = 0;
           for (uint32_t bb = 0; bb < 4u && 4u * k + bb < BL; ++bb)
             w |= static_cast<uint32_t>(nat[op.noff + 4u * k + bb]) << (8u * bb);
-          img_put(im, C, gout, at + 4u * k, w);
+          c.put(w);
         }
-        at += 4u * nwd; pos += 4ull * nwd; ++pc; break;
+        ++pc;
+        break;
       }
       case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
-        img_put(im, C, gout, at, bswap32(blen));
-        at += 4;
-        if (blen) {
-          const uint64_t hsrc = *reinterpret_cast<const uint64_t *>(nw);
-#pragma unroll
-          for (int k = 0; k < KMAX; ++k)
-            if (static_cast<uint32_t>(k) == nslot) { psr[k] = hsrc; pds[k] = at; pln[k] = blen; }
-          ++nslot;
+        c.put(bswap32(blen));
+        const uint64_t hsrc = *reinterpret_cast<const uint64_t *>(nw);
+        if (!blen) {
+        } else if (nslot < static_cast<uint32_t>(KMAX) && blen <= 4096u) {
+          c.slot_dyn(nslot++, hsrc, blen);
+        } else {
+          c.copy(hsrc, blen);
         }
-        at += (blen + 3u) & ~3u;
-        pos += 4ull + ((static_cast<uint64_t>(blen) + 3u) & ~3ull); ++pc; break;
+        ++pc;
+        break;
       }
       case XDRG_OP_UNION: {
         const uint32_t d = nw[0];
-        img_put(im, C, gout, at, bswap32(d));
-        at += 4; pos += 4;
-        pc = static_cast<uint32_t>(union_target(op, table, d));  // validated by k_var_size
+        c.put(bswap32(d));
+        pc = static_cast<uint32_t>(union_target(op, table, d));  // validated by the size pass
         break;
       }
       case XDRG_OP_VECTOR: {
         const uint64_t eoff = *reinterpret_cast<const uint64_t *>(nw);
         const uint32_t cnt = nw[2];
-        img_put(im, C, gout, at, bswap32(cnt));
-        at += 4; pos += 4;
-        auto put = [&](uint32_t a, uint32_t w) { img_put(im, C, gout, a, w); };
-        if (!enc_vector_elems(ops, upc + 1, op.arg2, heap, heap_len, eoff, cnt, op.arg1, pos, cap,
-                              at, stack_limit, r, err, put)) {
+        c.put(bswap32(cnt));
+        auto put = [&](uint32_t a, uint32_t w) { img_put(c.im, c.C, c.gout, a, w); };
+        if (!enc_vector_elems(ops, upc + 1, op.arg2, c.heap, c.heap_len, eoff, cnt, op.arg1, c.pos,
+                              c.cap, c.at, c.stack_limit, c.r, c.err, put)) {
           ok = false;
           pc = kPcDone;
           break;
@@ -1027,137 +839,116 @@ __global__ __launch_bounds__(64) void k_var_encode_i(
       default: ++pc; break;
       }
     }
-    if (!ok) nslot = 0;  // a failing record's bytes are unspecified (never past `cap`)
+    return ok;
   }
 
-  // ---- chunk map: u16 lane << 10 | slot << 8 | chunk
-  uint32_t nch = 0;
-#pragma unroll
-  for (int k = 0; k < KMAX; ++k)
-    if (static_cast<uint32_t>(k) < nslot) nch += (pln[k] + 15u) >> 4;
-  uint32_t cincl = nch;
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t x = __shfl_up(cincl, o, 64);
-    if (lane >= static_cast<uint32_t>(o)) cincl += x;
-  }
-  const uint32_t M = __shfl(cincl, 63, 64);
-  {
-    uint32_t e = cincl - nch;
-#pragma unroll
-    for (int k = 0; k < KMAX; ++k) {
-      if (static_cast<uint32_t>(k) >= nslot) break;
-      desc[lane * KMAX + k] = echunk_desc{psr[k], pds[k], pln[k]};
-      const uint32_t nq = (pln[k] + 15u) >> 4;
-      const uint32_t tag = (lane << 10) | (static_cast<uint32_t>(k) << 8);
-      for (uint32_t q = 0; q < nq; ++q) map[e + q] = static_cast<uint16_t>(tag | q);
-      e += nq;
-    }
-  }
-  wave_sync();
-
-  // ---- payload chunks: heap -> image, U chunks in flight per lane.  Three
-  // passes per batch: the chunk descriptors (LDS), then the U loads with no
-  // use of a loaded value in between (so none waits for another), then the
-  // rare chunk that ends past the heap, the pad masks and the stores.
-  for (uint32_t c0 = 0; c0 < M; c0 += 64u * U) {
-    u32x4 val[U];
-    uint64_t hs[U];
-    uint32_t at[U], nb[U], rem[U];
-    bool fast[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t c = c0 + 64u * u + lane;
-      nb[u] = 0u;
-      at[u] = 0u;
-      hs[u] = 0u;
-      rem[u] = 16u;
-      fast[u] = false;
-      if (c < M) {
-        const uint32_t m = map[c];
-        const echunk_desc d = desc[(m >> 10) * KMAX + ((m >> 8) & 3u)];
-        const uint32_t q16 = (m & 0xffu) << 4;
-        hs[u] = d.src + q16;
-        rem[u] = d.len - q16;
-        at[u] = d.dst + q16;
-        nb[u] = min(16u, ((d.len + 3u) & ~3u) - q16);
-        fast[u] = hs[u] + 16u <= heap_len;
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      if (fast[u]) val[u] = ld16u(heap + hs[u]);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (!nb[u]) continue;
-      u32x4 x = val[u];
-      if (!fast[u])
-        x = u32x4{unaligned_word(heap, heap_len, hs[u]), unaligned_word(heap, heap_len, hs[u] + 4),
-                  unaligned_word(heap, heap_len, hs[u] + 8), unaligned_word(heap, heap_len, hs[u] + 12)};
-      const int32_t r = static_cast<int32_t>(rem[u]);
-      if (r < 16) {  // zero the pad bytes after the payload (put_bytes)
-        x.x &= keep_bytes(r);
-        x.y &= keep_bytes(r - 4);
-        x.z &= keep_bytes(r - 8);
-        x.w &= keep_bytes(r - 12);
-      }
-      if (at[u] + 16u <= C) {
-        uint32_t *w = reinterpret_cast<uint32_t *>(im + at[u]);
-        w[0] = x.x;
-        if (nb[u] > 4u) w[1] = x.y;
-        if (nb[u] > 8u) w[2] = x.z;
-        if (nb[u] > 12u) w[3] = x.w;
-      } else if (at[u] >= C && nb[u] == 16u) {
-        st16u(gout + at[u], x);  // a whole chunk past the image: one (4-aligned) 16-byte store
-      } else {
-        img_put(im, C, gout, at[u], x.x);
-        if (nb[u] > 4u) img_put(im, C, gout, at[u] + 4, x.y);
-        if (nb[u] > 8u) img_put(im, C, gout, at[u] + 8, x.z);
-        if (nb[u] > 12u) img_put(im, C, gout, at[u] + 12, x.w);
-      }
-    }
-  }
-  wave_sync();
-
-  // ---- image -> global: aligned 16-byte chunks, partial words at the edges
-  {
-    const uint64_t gs = wave_out;
-    const uint64_t ge = min<uint64_t>(gs + min<uint64_t>(T, C), cap);
-    if (ge > gs) {
-      const uint64_t c0 = gs & ~15ull;
-      const uint32_t nc = static_cast<uint32_t>((ge - c0 + 15u) >> 4);
-      for (uint32_t c = lane; c < nc; c += 64u) {
-        const uint64_t ca = c0 + 16ull * c;
-        const uint8_t *lsrc = img + 16u * c;  // img + sh <-> gs, and gs - sh = c0
-        if (ca >= gs && ca + 16u <= ge) {
-          *reinterpret_cast<u32x4 *>(xdr + ca) = *reinterpret_cast<const u32x4 *>(lsrc);
-        } else {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const uint64_t wa = ca + 4u * q;
-            if (wa >= gs && wa + 4u <= ge) st32(xdr + wa, *reinterpret_cast<const uint32_t *>(lsrc + 4 * q));
-          }
+  template <bool RA>
+  __device__ bool dec(dec_ctx<RA> &c, uint8_t *nat, bool ok) const {
+    uint32_t pc = ok ? 0u : kPcDone;
+    for (uint32_t upc = 0; upc < nops; ++upc) {
+      if (!__any(pc == upc)) continue;
+      const xdrg_op op = load_op(ops, upc);
+      if (pc != upc) continue;
+      if (op.kind == XDRG_OP_END) { pc = kPcDone; continue; }
+      if (op.kind == XDRG_OP_JUMP) { pc = op.arg0; continue; }
+      uint32_t *nw = reinterpret_cast<uint32_t *>(nat + op.noff);
+      const uint32_t need = op.kind == XDRG_OP_U64 ? 8u : op.kind == XDRG_OP_OPAQUE ? op.arg0 : 4u;
+      if (!c.field(upc, op.depth, need)) { ok = false; pc = kPcDone; continue; }
+      uint64_t &p = c.p;
+      switch (op.kind) {
+      case XDRG_OP_U32: nw[0] = bswap32(c.word()); ++pc; break;
+      case XDRG_OP_ENUM: {
+        const uint32_t v = bswap32(c.word());
+        nw[0] = v;
+        ++pc;
+        if ((op.flags & XDRG_F_VALIDATE) && !enum_ok(table, op.arg0, op.arg1, v)) {
+          ok = c.fail(upc, XDRG_ERR_INVALID_ENUM); pc = kPcDone;
         }
+        break;
+      }
+      case XDRG_OP_BOOL: nat[op.noff] = c.word() != 0u; ++pc; break;
+      case XDRG_OP_U64:
+        nw[1] = bswap32(c.rd(p));
+        nw[0] = bswap32(c.rd(p + 4));
+        p += 8;
+        ++pc;
+        break;
+      case XDRG_OP_OPAQUE: {
+        const uint32_t BL = op.arg0;
+        for (uint32_t k = 0; k < BL; k += 4) {
+          const uint32_t w = c.rd(p + k);
+          for (uint32_t bb = 0; bb < 4u && k + bb < BL; ++bb) nat[op.noff + k + bb] = uint8_t(w >> (8 * bb));
+        }
+        ++pc;
+        if ((BL & 3u) && (c.rd(p + (BL & ~3u)) & ~keep_mask(BL & 3u))) {
+          ok = c.fail(upc, XDRG_ERR_NONZERO_PAD); pc = kPcDone;
+        }
+        p += (BL + 3u) & ~3u;
+        break;
+      }
+      case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
+        const uint32_t BL = bswap32(c.word());
+        if (BL > c.b - p) { ok = c.fail(upc, XDRG_ERR_OVERFLOW_GET); pc = kPcDone; break; }
+        if (BL > op.arg0) {
+          ok = c.fail(upc, op.kind == XDRG_OP_STRING ? XDRG_ERR_XSTRING_BOUND : XDRG_ERR_XVECTOR_BOUND);
+          pc = kPcDone;
+          break;
+        }
+        if ((BL & 3u) && (c.rd(p + (BL & ~3u)) & ~keep_mask(BL & 3u))) {  // get_bytes pad check
+          ok = c.fail(upc, XDRG_ERR_NONZERO_PAD); pc = kPcDone; break;
+        }
+        *reinterpret_cast<uint64_t *>(nat + op.noff) = p;  // the payload stays in the stream
+        nw[2] = BL;
+        p += (static_cast<uint64_t>(BL) + 3u) & ~3ull;
+        ++pc;
+        break;
+      }
+      case XDRG_OP_UNION: {
+        const uint32_t d = bswap32(c.word());
+        if ((op.flags & XDRG_F_VALIDATE) && !enum_ok(table, op.arg0, op.arg1, d)) {
+          ok = c.fail(upc, XDRG_ERR_INVALID_ENUM); pc = kPcDone; break;
+        }
+        const int t = union_target(op, table, d);
+        if (t < 0) { ok = c.fail(upc, XDRG_ERR_BAD_DISCRIMINANT); pc = kPcDone; break; }
+        nw[0] = d;
+        pc = static_cast<uint32_t>(t);
+        break;
+      }
+      case XDRG_OP_VECTOR: {
+        const uint32_t cnt = bswap32(c.word());
+        if (cnt > op.arg0) {  // check_size (types.h:486-489, 605-608)
+          ok = c.fail(upc, (op.flags & XDRG_F_POINTER) ? XDRG_ERR_POINTER_BOUND : XDRG_ERR_XVECTOR_BOUND);
+          pc = kPcDone;
+          break;
+        }
+        c.ecur = (c.ecur + 7u) & ~7ull;
+        *reinterpret_cast<uint64_t *>(nat + op.noff) = c.ecur;
+        nw[2] = cnt;
+        if (!dec_vector_elems(ops, table, upc + 1, op.arg2, cnt, op.arg1, c.heap + c.ecur, p, c.b,
+                              c.stack_limit, c.r, c.err, c.rd, &nw[3])) {
+          ok = false; pc = kPcDone; break;
+        }
+        c.ecur += static_cast<uint64_t>(cnt) * op.arg1;
+        pc = upc + 1 + op.arg2;
+        break;
+      }
+      default: ++pc; break;
       }
     }
+    return ok;
   }
-}
+};
 
-// -------------------------------------------------- var: window decode
-// One workgroup = one wave = 64 consecutive records.  The decoded heap is
-// the stream itself (xdrg_decode contract), so decode never gathers
-// payloads:
-//   * the wave's input stretch [a0, a_end) is read once with aligned
-//     16-byte loads into an LDS window (window byte j sits at LDS
-//     j + ((xdr + a0) & 15)) and written to heap_out at the same offsets;
-//     bytes past the window capacity C are copied global -> global;
-//   * the lane-per-record walk parses from the window (global for bytes
-//     past C): fields into a zeroed LDS native tile, payloads as
-//     xdrg_bytes_ref {stream offset, len}, with every bound / pad /
-//     discriminant / enum check of xdr_generic_get;
-//   * the tile leaves with 16-byte stores.
-__host__ __device__ inline uint32_t dec_w_lds(uint32_t stride, uint32_t C) {
-  return ((64u * stride + 15u) & ~15u) + C + 32u;
+template <int KMAX, int U>
+__global__ __launch_bounds__(64) void k_var_encode_i(
+    const uint8_t *__restrict__ native, uint64_t n, uint32_t stride, const uint8_t *__restrict__ heap,
+    uint64_t heap_len, uint8_t *__restrict__ xdr, uint64_t cap, uint64_t *__restrict__ offsets,
+    const uint32_t *__restrict__ sizes, const unsigned long long *__restrict__ block_base,
+    const xdrg_op *__restrict__ ops, uint32_t nops, const uint32_t *__restrict__ table,
+    uint32_t stack_limit, uint32_t MC, uint32_t C, uint32_t mark, unsigned long long *err) {
+  var_encode_body<interp_walk, KMAX, U>(interp_walk{ops, nops, table}, native, n, stride, heap,
+                                        heap_len, xdr, cap, offsets, sizes, block_base, stack_limit,
+                                        MC, C, mark, err);
 }
 
 template <bool COPY, bool RA = true>
@@ -1167,217 +958,8 @@ __global__ __launch_bounds__(64) void k_var_decode_w(
     const xdrg_op *__restrict__ ops, uint32_t nops, const uint32_t *__restrict__ table,
     uint32_t stack_limit, uint32_t C, uint64_t ebase, uint32_t F, uint32_t mark,
     unsigned long long *err) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
-  const uint32_t lane = threadIdx.x;
-  const uint32_t tile_bytes = (64u * stride + 15u) & ~15u;
-  uint8_t *tile = sm;
-  uint8_t *win = sm + tile_bytes;
-  const uint64_t wr0 = static_cast<uint64_t>(blockIdx.x) * 64u;
-  const uint32_t nrec = static_cast<uint32_t>(min<uint64_t>(64, n - wr0));
-  const uint64_t r = wr0 + lane;
-  uint64_t a = 0, b = 0;
-  if (lane < nrec) {
-    a = offsets[r];
-    b = offsets[r + 1];
-  }
-  // the wave's stretch, clamped to the stream (bad indices are reported by
-  // the per-record checks below; the window just gets smaller)
-  const uint64_t ws = min<uint64_t>(rl64(a, 0), len);
-  const uint64_t we = max<uint64_t>(ws, min<uint64_t>(rl64(b, nrec - 1), len));
-  const uint64_t wc = min<uint64_t>(we - ws, C);  // bytes held in the window
-  const uintptr_t gbase = reinterpret_cast<uintptr_t>(xdr) + ws;
-  const uint32_t sh = static_cast<uint32_t>(gbase & 15u);
-  const uint8_t *wnd = win + sh;  // window byte j <-> stream byte ws + j
-
-  for (uint32_t i = lane; i < tile_bytes / 16u; i += 64u)
-    reinterpret_cast<u32x4 *>(tile)[i] = u32x4{0u, 0u, 0u, 0u};
-  {
-    // Aligned 16-byte chunks covering the stretch [ws, we), 8 loads in
-    // flight per lane.  A chunk never leaves the pages that hold stream
-    // bytes, so edge chunks load whole; only in-range words reach the heap.
-    // Chunks inside [ws, ws + wc) also fill the window.
-    const uint32_t nwin = static_cast<uint32_t>((sh + wc + 15u) >> 4);
-    const uint64_t nall = COPY ? (sh + (we - ws) + 15u) >> 4 : nwin;
-    const uint8_t *g0 = xdr + ws - sh;
-    constexpr int UL = 8;
-    for (uint64_t c0 = 0; c0 < nall; c0 += 64u * UL) {
-      u32x4 v[UL];
-#pragma unroll
-      for (int u = 0; u < UL; ++u) {
-        const uint64_t c = c0 + 64u * u + lane;
-        if (c < nall) v[u] = *reinterpret_cast<const u32x4 *>(g0 + 16u * c);
-      }
-#pragma unroll
-      for (int u = 0; u < UL; ++u) {
-        const uint64_t c = c0 + 64u * u + lane;
-        if (c >= nall) continue;
-        if (c < nwin) reinterpret_cast<u32x4 *>(win)[c] = v[u];
-        if (COPY) {
-          const int64_t o = static_cast<int64_t>(16u * c) - sh;  // stream offset - ws
-          const int64_t lim = static_cast<int64_t>(we - ws);
-          uint8_t *hd = heap + ws + o;
-          if (o >= 0 && o + 16 <= lim) {
-            st16u(hd, v[u]);
-          } else {
-            const uint32_t w4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-              if (o + 4 * q >= 0 && o + 4 * q + 4 <= lim) st32(hd + 4 * q, w4[q]);
-          }
-        }
-      }
-    }
-  }
-  wave_sync();
-
-  // word reader: window for stream bytes in [ws, ws + wc), global otherwise.
-  // Past the window a lane keeps a 32-byte read-ahead of the stream (two
-  // aligned 16-byte chunks loaded together): consecutive fields are
-  // adjacent, so one round trip serves up to 8 words instead of 1.  The
-  // second chunk is loaded only when it holds stream bytes (an aligned
-  // chunk with a stream byte never leaves the stream's pages).
-  const uintptr_t xbase = reinterpret_cast<uintptr_t>(xdr);
-  const uintptr_t xend = xbase + len;
-  uintptr_t ra_line = ~uintptr_t(0);
-  u32x4 ra0 = u32x4{0u, 0u, 0u, 0u}, ra1 = ra0;
-  auto rd = [&](uint64_t pos) -> uint32_t {
-    const uint64_t rel = pos - ws;
-    if (pos >= ws && rel + 4 <= wc) {
-      const uint8_t *q = wnd + rel;
-      if (((sh + rel) & 3u) == 0) return *reinterpret_cast<const uint32_t *>(q);
-      return uint32_t(q[0]) | (uint32_t(q[1]) << 8) | (uint32_t(q[2]) << 16) | (uint32_t(q[3]) << 24);
-    }
-    const uintptr_t ga = xbase + pos;
-    if (!RA || (ga & 3u) || pos + 4 > len) return unaligned_word(xdr, len, pos);
-    if (ga - ra_line >= 32u) {
-      ra_line = ga & ~uintptr_t(15);
-      ra0 = *reinterpret_cast<const u32x4 *>(ra_line);
-      ra1 = ra_line + 16u < xend ? *reinterpret_cast<const u32x4 *>(ra_line + 16u) : u32x4{0u, 0u, 0u, 0u};
-    }
-    const uint32_t k = static_cast<uint32_t>(ga - ra_line) >> 2;
-    const u32x4 h = k < 4u ? ra0 : ra1;
-    const uint32_t j = k & 3u;
-    return j == 0 ? h.x : j == 1 ? h.y : j == 2 ? h.z : h.w;
-  };
-
-  {
-    uint8_t *nat = tile + lane * stride;
-    uint32_t pc = kPcDone;
-    if (lane < nrec) {
-      // xdr_from_msg: the message read_message framed (srpc.cc:29-55)
-      const uint32_t mc = !mark || b < a || b > len ? 0u
-                          : b - a < 4 ? XDRG_ERR_MSG_EOF : mark_code(rd(a), b - a - 4);
-      if (r == n - 1 && b != len) report(err, n, kOpRecordLevel, XDRG_ERR_TRAILING);
-      if (b < a || b > len) report(err, r, 0, XDRG_ERR_OVERFLOW_GET);
-      else if (mc) report(err, r, kOpRecordLevel, mc);
-      else if ((b - a) & 3u) report(err, r, kOpRecordLevel, XDRG_ERR_SIZE_NOT_MULT4);
-      else pc = 0;
-    }
-    uint64_t p = a + mark;
-    uint64_t ecur = ebase + static_cast<uint64_t>(F) * a;  // this record's element arrays
-    bool ok = pc == 0u;
-    for (uint32_t upc = 0; upc < nops; ++upc) {
-      if (!__any(pc == upc)) continue;
-      const xdrg_op op = load_op(ops, upc);
-      if (pc != upc) continue;
-      if (op.kind == XDRG_OP_END) { pc = kPcDone; continue; }
-      if (op.kind == XDRG_OP_JUMP) { pc = op.arg0; continue; }
-      if (op.depth > stack_limit) { report(err, r, upc, XDRG_ERR_STACK_GET); ok = false; pc = kPcDone; continue; }
-      const uint64_t rem = b - p;
-      uint32_t *nw = reinterpret_cast<uint32_t *>(nat + op.noff);
-      const uint32_t need = op.kind == XDRG_OP_U64 ? 8u : op.kind == XDRG_OP_OPAQUE ? op.arg0 : 4u;
-      if (rem < need) { report(err, r, upc, XDRG_ERR_OVERFLOW_GET); ok = false; pc = kPcDone; continue; }
-      switch (op.kind) {
-      case XDRG_OP_U32:
-        nw[0] = bswap32(rd(p)); p += 4; ++pc; break;
-      case XDRG_OP_ENUM: {
-        const uint32_t v = bswap32(rd(p));
-        nw[0] = v; p += 4; ++pc;
-        if ((op.flags & XDRG_F_VALIDATE) && !enum_ok(table, op.arg0, op.arg1, v)) {
-          report(err, r, upc, XDRG_ERR_INVALID_ENUM); ok = false; pc = kPcDone;
-        }
-        break;
-      }
-      case XDRG_OP_BOOL:
-        nat[op.noff] = rd(p) != 0u; p += 4; ++pc; break;
-      case XDRG_OP_U64:
-        nw[1] = bswap32(rd(p));
-        nw[0] = bswap32(rd(p + 4));
-        p += 8; ++pc; break;
-      case XDRG_OP_OPAQUE: {
-        const uint32_t BL = op.arg0;
-        for (uint32_t k = 0; k < BL; k += 4) {
-          const uint32_t w = rd(p + k);
-          for (uint32_t bb = 0; bb < 4u && k + bb < BL; ++bb) nat[op.noff + k + bb] = uint8_t(w >> (8 * bb));
-        }
-        ++pc;
-        if ((BL & 3u) && (rd(p + (BL & ~3u)) & ~keep_mask(BL & 3u))) {
-          report(err, r, upc, XDRG_ERR_NONZERO_PAD); ok = false; pc = kPcDone;
-        }
-        p += (BL + 3u) & ~3u;
-        break;
-      }
-      case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
-        const uint32_t BL = bswap32(rd(p));
-        p += 4;
-        if (BL > b - p) { report(err, r, upc, XDRG_ERR_OVERFLOW_GET); ok = false; pc = kPcDone; break; }
-        if (BL > op.arg0) {
-          report(err, r, upc,
-                 op.kind == XDRG_OP_STRING ? XDRG_ERR_XSTRING_BOUND : XDRG_ERR_XVECTOR_BOUND);
-          ok = false;
-          pc = kPcDone;
-          break;
-        }
-        if ((BL & 3u) && (rd(p + (BL & ~3u)) & ~keep_mask(BL & 3u))) {  // get_bytes pad check
-          report(err, r, upc, XDRG_ERR_NONZERO_PAD); ok = false; pc = kPcDone; break;
-        }
-        *reinterpret_cast<uint64_t *>(nat + op.noff) = p;  // the payload stays in the stream
-        nw[2] = BL;
-        p += (static_cast<uint64_t>(BL) + 3u) & ~3ull; ++pc;
-        break;
-      }
-      case XDRG_OP_UNION: {
-        const uint32_t d = bswap32(rd(p));
-        p += 4;
-        if ((op.flags & XDRG_F_VALIDATE) && !enum_ok(table, op.arg0, op.arg1, d)) {
-          report(err, r, upc, XDRG_ERR_INVALID_ENUM); ok = false; pc = kPcDone; break;
-        }
-        const int t = union_target(op, table, d);
-        if (t < 0) { report(err, r, upc, XDRG_ERR_BAD_DISCRIMINANT); ok = false; pc = kPcDone; break; }
-        nw[0] = d;
-        pc = static_cast<uint32_t>(t);
-        break;
-      }
-      case XDRG_OP_VECTOR: {
-        const uint32_t cnt = bswap32(rd(p));
-        p += 4;
-        if (cnt > op.arg0) {  // check_size (types.h:486-489, 605-608)
-          report(err, r, upc, (op.flags & XDRG_F_POINTER) ? XDRG_ERR_POINTER_BOUND : XDRG_ERR_XVECTOR_BOUND);
-          ok = false; pc = kPcDone; break;
-        }
-        ecur = (ecur + 7u) & ~7ull;
-        *reinterpret_cast<uint64_t *>(nat + op.noff) = ecur;
-        nw[2] = cnt;
-        if (!dec_vector_elems(ops, table, upc + 1, op.arg2, cnt, op.arg1, heap + ecur, p, b,
-                              stack_limit, r, err, rd, &nw[3])) {
-          ok = false; pc = kPcDone; break;
-        }
-        ecur += static_cast<uint64_t>(cnt) * op.arg1;
-        pc = upc + 1 + op.arg2;
-        break;
-      }
-      default: ++pc; break;
-      }
-    }
-    if (ok && p != b) report(err, r, kOpRecordLevel, XDRG_ERR_TRAILING);
-  }
-  wave_sync();
-  uint8_t *ndst = native + wr0 * stride;
-  const uint32_t nbytes = nrec * stride;
-  for (uint32_t i = lane; i < nbytes / 16u; i += 64u)
-    reinterpret_cast<u32x4 *>(ndst)[i] = reinterpret_cast<const u32x4 *>(tile)[i];
-  for (uint32_t i = (nbytes / 16u) * 4u + lane; i < nbytes / 4u; i += 64u)
-    reinterpret_cast<uint32_t *>(ndst)[i] = reinterpret_cast<const uint32_t *>(tile)[i];
+  var_decode_body<interp_walk, COPY, RA>(interp_walk{ops, nops, table}, xdr, len, offsets, n, native,
+                                         stride, heap, stack_limit, C, ebase, F, mark, err);
 }
 
 // ------------------------------------------- record marks: the index pass
