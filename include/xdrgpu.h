@@ -151,7 +151,8 @@ typedef struct xdrg_plan_info {
                               * (fixed: fixed_size); a message's body bound */
   uint32_t group_records;    /* FIXED_LDS plans run by the group kernel: records
                               * per group (0: the LDS kernel, or not fixed) */
-  uint32_t rsv;
+  uint32_t specialized;      /* var plans: 1 when the plan's specialized kernels
+                              * are built (xdrg_plan_build_kernels) */
 } xdrg_plan_info;
 
 /* ---------------------------------------------------------------------- */
@@ -259,9 +260,39 @@ enum xdrg_plan_option {
   XDRG_OPT_SIZE_LINEAR = 8,       /* walk-free size pass for linear plans: 0 / 1   */
   XDRG_OPT_GRP_UNROLL = 9,        /* fixed group kernel chunks in flight, 0 auto   */
   XDRG_OPT_GRP_BLOCKS = 10,       /* fixed group kernel workgroups, 0 auto         */
-  XDRG_OPT_GRP_NONTEMPORAL = 11   /* fixed group kernel non-temporal stores: 0 / 1 */
+  XDRG_OPT_GRP_NONTEMPORAL = 11,  /* fixed group kernel non-temporal stores: 0 / 1 */
+  XDRG_OPT_SPECIALIZE = 12        /* var plans: 1 (default) run the plan-specialized
+                                     kernels (built by the first launch, or
+                                     xdrg_plan_build_kernels); 0 the interpreter */
 };
 int xdrg_plan_set_option(xdrg_plan *plan, int option, int64_t value);
+
+/* ---------------------------------------------------------------------- */
+/* Plan-specialized kernels (var plans)                                    */
+/* ---------------------------------------------------------------------- */
+/*
+ * The generation-time form of xdr_traits<T>::save/load (xdrc/gen_hh.cc:
+ * 212-250, :575-675): a plan's walk emitted as straight-line HIP source --
+ * every field's checks, swaps and bytes, unions as switch statements,
+ * containers as loops -- over the library's var kernels, compiled for
+ * gfx950.  No reference interface corresponds one to one: this is the back
+ * end xdrc would run beside gen_hh.
+ *
+ *   xdrg_plan_kernel_source  the plan's source (NUL-terminated into buf when
+ *                            cap > 0; *len = its length).  XDRG_EUNSUPPORTED
+ *                            for fixed plans (their kernels are generic).
+ *   xdrg_plan_build_kernels  compile now: from the kernel cache (files named
+ *                            by a hash of the source under $XDRG_KERNEL_CACHE,
+ *                            default kernel_cache/ beside libxdrgpu.so) or
+ *                            with hiprtc.  The first var launch does this on
+ *                            its own; XDRG_EHIP carries the compile log.
+ *   xdrg_plan_load_kernels   attach a code object compiled ahead of time
+ *                            from xdrg_plan_kernel_source (before the plan's
+ *                            first launch).
+ */
+int xdrg_plan_kernel_source(const xdrg_plan *plan, char *buf, size_t cap, size_t *len);
+int xdrg_plan_build_kernels(xdrg_plan *plan);
+int xdrg_plan_load_kernels(xdrg_plan *plan, const void *code_object, size_t size);
 
 /* Workspace bytes encode (var plans), encode_msgs (any plan) and
  * serial_sizes need for n records. */

@@ -57,7 +57,7 @@ int main(void) {
   Z(xdrg_plan_info); F(xdrg_plan_info, path); F(xdrg_plan_info, native_stride);
   F(xdrg_plan_info, fixed_size); F(xdrg_plan_info, max_depth); F(xdrg_plan_info, nops);
   F(xdrg_plan_info, has_checks); F(xdrg_plan_info, max_record_bytes);
-  F(xdrg_plan_info, group_records); F(xdrg_plan_info, rsv);
+  F(xdrg_plan_info, group_records); F(xdrg_plan_info, specialized);
   Z(xdrg_status); F(xdrg_status, first_error); F(xdrg_status, total_bytes);
   Z(xdrg_error); F(xdrg_error, code); F(xdrg_error, exc); F(xdrg_error, record);
   F(xdrg_error, op); F(xdrg_error, rsv); F(xdrg_error, total_bytes);

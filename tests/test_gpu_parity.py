@@ -365,14 +365,15 @@ def test_swaps(dev):
 
 
 # ------------------------------------- every var kernel, forced in turn
-KERNELS = {"per_lane": (1, 1), "chunk_image_window": (3, 2)}
+KERNELS = {"per_lane": (1, 1, 0), "chunk_image_window": (3, 2, 0), "specialized": (0, 0, 1)}
 
 
 @pytest.fixture(params=list(KERNELS))
 def forced(request):
-    """Plan options forcing one encode and one decode kernel."""
-    enc, dec = KERNELS[request.param]
-    return {"var_encode_kernel": enc, "var_decode_kernel": dec}
+    """Plan options forcing one encode and one decode kernel: the plan
+    interpreter's, or the plan-specialized ones (codegen.cpp + hiprtc)."""
+    enc, dec, spec = KERNELS[request.param]
+    return {"var_encode_kernel": enc, "var_decode_kernel": dec, "specialize": spec}
 
 
 @pytest.mark.parametrize("name", ["recvar", "rpc", "vecrec"])

@@ -24,7 +24,7 @@ PATH_FIXED_REG, PATH_FIXED_LDS, PATH_VAR = 1, 2, 3
 # enum xdrg_plan_option (xdrg_plan_set_option)
 PLAN_OPTIONS = {"var_encode_kernel": 1, "var_decode_kernel": 2, "fixed_path": 3, "image_bytes": 4,
                 "window_bytes": 5, "enc_unroll": 6, "dec_readahead": 7, "size_linear": 8,
-                "grp_unroll": 9, "grp_blocks": 10, "grp_nontemporal": 11}
+                "grp_unroll": 9, "grp_blocks": 10, "grp_nontemporal": 11, "specialize": 12}
 
 OK = 0
 API_ERRORS = {-1: "EINVAL", -2: "EALIGN", -3: "EUNSUPPORTED", -4: "EHIP", -5: "ENOMEM", -6: "ESPACE"}
@@ -86,7 +86,7 @@ class XdrgPlanInfo(C.Structure):
         ("has_checks", C.c_uint32),
         ("max_record_bytes", C.c_uint64),
         ("group_records", C.c_uint32),
-        ("rsv", C.c_uint32),
+        ("specialized", C.c_uint32),
     ]
 
 
@@ -114,7 +114,8 @@ EXPORTED = (
     "xdrg_decode_heap_size", "xdrg_encode_msgs", "xdrg_decode_msgs", "xdrg_index_msgs",
     "xdrg_index_workspace_size", "xdrg_rpc_dispatch", "xdrg_rpc_check_replies",
     "xdrg_rpc_replies", "xdrg_rpc_replies_workspace_size", "xdrg_record_depths",
-    "xdrg_plan_set_option",
+    "xdrg_plan_set_option", "xdrg_plan_kernel_source", "xdrg_plan_build_kernels",
+    "xdrg_plan_load_kernels",
 )
 
 # RPC header batches (include/xdrgpu.h "RPC header batches")
@@ -156,6 +157,12 @@ def lib() -> C.CDLL:
     L.xdrg_plan_get_info.restype = C.c_int
     L.xdrg_plan_set_option.argtypes = [vp, C.c_int, C.c_int64]
     L.xdrg_plan_set_option.restype = C.c_int
+    L.xdrg_plan_kernel_source.argtypes = [vp, C.c_char_p, sz, C.POINTER(sz)]
+    L.xdrg_plan_kernel_source.restype = C.c_int
+    L.xdrg_plan_build_kernels.argtypes = [vp]
+    L.xdrg_plan_build_kernels.restype = C.c_int
+    L.xdrg_plan_load_kernels.argtypes = [vp, vp, sz]
+    L.xdrg_plan_load_kernels.restype = C.c_int
     L.xdrg_workspace_size.argtypes = [vp, u64]
     L.xdrg_workspace_size.restype = sz
     L.xdrg_status_init.argtypes = [vp, vp]

@@ -1,0 +1,573 @@
+// Plan-specialized kernel source.
+//
+// xdrc turns a type into straight-line C++ — xdr_traits<T>::save/load call
+// archive() field by field in declaration order (xdrc/gen_hh.cc:212-250,
+// unions :575-675).  This back end does the same from a plan: it emits a
+// *walker* for var_kernels.h with one block of code per op — the bounds and
+// stack checks of xdr_generic_put/get (marshal.h:104-136, :166-205), the
+// swaps, the bytes fields — unions as switch statements over their case
+// tables, containers as loops.  Compiled (hiprtc at plan time, spec.cpp, or
+// ahead of time from the emitted source) the walk carries no op table, no
+// per-op dispatch and no wave-uniform sweep: the interpreter's cost.
+//
+// Control structure comes from the plan's DAG (jumps are forward-only): the
+// end of a union is its immediate post-dominator, so every arm is emitted as
+// the block from its target to that end.
+#include <algorithm>
+#include <cstdio>
+#include <map>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "plan.h"
+#include "spec.h"
+
+namespace xdrg {
+namespace {
+
+constexpr uint32_t kNoPc = 0xffffffffu;
+constexpr uint32_t kSlotMax = 4;        // chunk-map slots per record (var_kernels.h)
+constexpr uint32_t kSlotBytes = 4096;   // largest payload one chunk-map slot addresses
+
+std::string u32(uint32_t v) {
+  char b[16];
+  snprintf(b, sizeof b, "%uu", v);
+  return b;
+}
+
+struct gen {
+  const xdrg_plan &p;
+  std::vector<uint32_t> ipdom;
+  std::ostringstream o;
+  int ind = 1;
+  uint32_t max_slots = 0;  // static chunk-map slots used on the longest path
+  uint64_t max_chunks = 0; // 16-byte chunks those slots can hold (per record)
+
+  explicit gen(const xdrg_plan &plan) : p(plan) { post_dominators(); }
+
+  const xdrg_op &op(uint32_t pc) const { return p.ops[pc]; }
+  uint32_t nops() const { return static_cast<uint32_t>(p.ops.size()); }
+
+  // Immediate post-dominators over the control-flow DAG (successors always
+  // have a larger pc, so one reverse sweep suffices; END is the exit).
+  void post_dominators() {
+    const uint32_t n = nops();
+    ipdom.assign(n, kNoPc);
+    auto meet = [&](uint32_t a, uint32_t b) {
+      while (a != b && a != kNoPc && b != kNoPc) {
+        if (a < b) a = ipdom[a];
+        else b = ipdom[b];
+      }
+      return a == b ? a : kNoPc;
+    };
+    for (uint32_t i = n; i-- > 0;) {
+      const xdrg_op &o = op(i);
+      std::vector<uint32_t> succ;
+      switch (o.kind) {
+      case XDRG_OP_END: continue;
+      case XDRG_OP_JUMP: succ.push_back(o.arg0); break;
+      case XDRG_OP_VECTOR: succ.push_back(i + 1 + o.arg2); break;
+      case XDRG_OP_UNION:
+        for (uint32_t c = 0; c < o.arg3; ++c) succ.push_back(p.table[o.arg2 + 2 * c + 1]);
+        if (o.flags & XDRG_F_DEFAULT) succ.push_back(o.arg4);
+        break;
+      default: succ.push_back(i + 1); break;
+      }
+      uint32_t d = kNoPc;
+      bool first = true;
+      for (uint32_t s : succ) {
+        d = first ? s : meet(d, s);
+        first = false;
+      }
+      ipdom[i] = d;
+    }
+  }
+
+  void line(const std::string &s) { o << std::string(2 * ind, ' ') << s << "\n"; }
+
+  static uint32_t wire_words(const xdrg_op &e) {
+    return e.kind == XDRG_OP_U64 ? 2u : e.kind == XDRG_OP_OPAQUE ? (e.arg0 + 3u) / 4u : 1u;
+  }
+  std::string enum_test(const std::string &v, uint32_t idx, uint32_t cnt) const {
+    if (!cnt) return "false";
+    std::string t;
+    for (uint32_t i = 0; i < cnt; ++i) t += (i ? " || " : "") + v + " == " + u32(p.table[idx + i]);
+    return "(" + t + ")";
+  }
+  // distinct case targets of a union, in table order, with their values
+  std::vector<std::pair<uint32_t, std::vector<uint32_t>>> arms(const xdrg_op &u) const {
+    std::vector<std::pair<uint32_t, std::vector<uint32_t>>> out;
+    for (uint32_t c = 0; c < u.arg3; ++c) {
+      const uint32_t v = p.table[u.arg2 + 2 * c], t = p.table[u.arg2 + 2 * c + 1];
+      auto it = std::find_if(out.begin(), out.end(), [&](auto &a) { return a.first == t; });
+      if (it == out.end()) out.push_back({t, {v}});
+      else it->second.push_back(v);
+    }
+    return out;
+  }
+
+  // ------------------------------------------------------------------ size
+  // xdr_size (types.h:240-244; unions gen_hh.cc:639-648): returns through s.
+  void size_block(uint32_t pc, uint32_t stop, const std::string &base) {
+    while (pc != stop) {
+      const xdrg_op &e = op(pc);
+      const std::string f = base + " + " + u32(e.noff);
+      switch (e.kind) {
+      case XDRG_OP_END: return;
+      case XDRG_OP_JUMP: pc = e.arg0; continue;
+      case XDRG_OP_U32: case XDRG_OP_ENUM: case XDRG_OP_BOOL: line("s += 4;"); break;
+      case XDRG_OP_U64: line("s += 8;"); break;
+      case XDRG_OP_OPAQUE: line("s += " + u32((e.arg0 + 3u) & ~3u) + ";"); break;
+      case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING:
+        line("s += 4ull + ((static_cast<uint64_t>(ld32(" + f + " + 8)) + 3u) & ~3ull);");
+        break;
+      case XDRG_OP_VECTOR:
+        line("s += 4ull + static_cast<uint64_t>(ld32(" + f + " + 8)) * " + u32(e.arg3) + ";");
+        pc += 1 + e.arg2;
+        continue;
+      case XDRG_OP_UNION: {
+        const uint32_t end = ipdom[pc];
+        line("s += 4;");
+        line("switch (ld32(" + f + ")) {");
+        for (auto &a : arms(e)) {
+          std::string lab;
+          for (uint32_t v : a.second) lab += "case " + u32(v) + ": ";
+          line(lab + "{");
+          ++ind;
+          size_block(a.first, end, base);
+          --ind;
+          line("} break;");
+        }
+        line("default: {");
+        ++ind;
+        if (e.flags & XDRG_F_DEFAULT) size_block(e.arg4, end, base);
+        else line("bad_op = " + u32(pc) + "; return s;");
+        --ind;
+        line("} break;");
+        line("}");
+        pc = end;
+        continue;
+      }
+      default: break;
+      }
+      ++pc;
+    }
+  }
+
+  // ---------------------------------------------------------------- encode
+  // xdr_generic_put field by field (marshal.h:84-137).  Returns the static
+  // slots used after the block (slots count along the path).
+  uint32_t enc_block(uint32_t pc, uint32_t stop, uint32_t slot, uint64_t &chunks) {
+    while (pc != stop) {
+      const xdrg_op &e = op(pc);
+      const std::string f = "nat + " + u32(e.noff), P = u32(pc), D = u32(e.depth);
+      switch (e.kind) {
+      case XDRG_OP_END: return slot;
+      case XDRG_OP_JUMP: pc = e.arg0; continue;
+      case XDRG_OP_U32: case XDRG_OP_ENUM:
+        line("if (!c.field(" + P + ", " + D + ", 4)) return false;");
+        line("c.put(bswap32(ld32(" + f + ")));");
+        break;
+      case XDRG_OP_BOOL:
+        line("if (!c.field(" + P + ", " + D + ", 4)) return false;");
+        line("c.put(nat[" + u32(e.noff) + "] ? 0x01000000u : 0u);");
+        break;
+      case XDRG_OP_U64:
+        line("if (!c.field(" + P + ", " + D + ", 8)) return false;");
+        line("c.put(bswap32(ld32(" + f + " + 4)));");
+        line("c.put(bswap32(ld32(" + f + ")));");
+        break;
+      case XDRG_OP_OPAQUE: {
+        line("if (!c.field(" + P + ", " + D + ", " + u32(e.arg0) + ")) return false;");
+        for (uint32_t k = 0; 4 * k < e.arg0; ++k) {
+          std::string w;
+          for (uint32_t b = 0; b < 4 && 4 * k + b < e.arg0; ++b)
+            w += std::string(b ? " | " : "") + "(uint32_t(nat[" + u32(e.noff + 4 * k + b) + "]) << " +
+                 std::to_string(8 * b) + ")";
+          line("c.put(" + w + ");");
+        }
+        break;
+      }
+      case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
+        line("{");
+        ++ind;
+        line("const uint32_t len = ld32(" + f + " + 8);");
+        line("if (!c.field(" + P + ", " + D + ", 4ull + len)) return false;");
+        line("c.put(bswap32(len));");
+        line("const uint64_t src = *reinterpret_cast<const uint64_t *>(" + f + ");");
+        if (slot < kSlotMax) {
+          const uint32_t cap = std::min(e.arg0, kSlotBytes);
+          if (e.arg0 > kSlotBytes)
+            line("if (len > " + u32(kSlotBytes) + ") c.copy(src, len); else c.template slot<" +
+                 std::to_string(slot) + ">(src, len);");
+          else
+            line("c.template slot<" + std::to_string(slot) + ">(src, len);");
+          chunks += (cap + 15u) / 16u;
+          ++slot;
+        } else {
+          line("c.copy(src, len);");
+        }
+        --ind;
+        line("}");
+        break;
+      }
+      case XDRG_OP_UNION: {
+        const uint32_t end = ipdom[pc];
+        line("if (!c.field(" + P + ", " + D + ", 4)) return false;");
+        line("{");
+        ++ind;
+        line("const uint32_t d = ld32(" + f + ");");
+        line("c.put(bswap32(d));");
+        line("switch (d) {");
+        uint32_t smax = slot;
+        uint64_t cmax = chunks;
+        for (auto &a : arms(e)) {
+          std::string lab;
+          for (uint32_t v : a.second) lab += "case " + u32(v) + ": ";
+          line(lab + "{");
+          ++ind;
+          uint64_t ch = chunks;
+          smax = std::max(smax, enc_block(a.first, end, slot, ch));
+          cmax = std::max(cmax, ch);
+          --ind;
+          line("} break;");
+        }
+        if (e.flags & XDRG_F_DEFAULT) {
+          line("default: {");
+          ++ind;
+          uint64_t ch = chunks;
+          smax = std::max(smax, enc_block(e.arg4, end, slot, ch));
+          cmax = std::max(cmax, ch);
+          --ind;
+          line("} break;");
+        } else {
+          line("default: return false;  // the size pass reported it");
+        }
+        line("}");
+        --ind;
+        line("}");
+        slot = smax;
+        chunks = cmax;
+        pc = end;
+        continue;
+      }
+      case XDRG_OP_VECTOR: {
+        line("{");
+        ++ind;
+        line("const uint64_t eoff = *reinterpret_cast<const uint64_t *>(" + f + ");");
+        line("const uint32_t cnt = ld32(" + f + " + 8);");
+        line("if (!c.field(" + P + ", " + D + ", 4)) return false;");
+        line("c.put(bswap32(cnt));");
+        line("for (uint32_t i = 0; i < cnt; ++i) {");
+        ++ind;
+        line("const uint64_t eb = eoff + static_cast<uint64_t>(i) * " + u32(e.arg1) + ";");
+        enc_elem(pc + 1, pc + 1 + e.arg2);
+        --ind;
+        line("}");
+        --ind;
+        line("}");
+        pc += 1 + e.arg2;
+        continue;
+      }
+      default: break;
+      }
+      ++pc;
+    }
+    return slot;
+  }
+  // Elements of a container (enc_vector_elems of xdrgpu.hip): fixed-size
+  // fields read from the heap (bytes past heap_len read as 0).
+  void enc_elem(uint32_t b0, uint32_t b1) {
+    for (uint32_t k = b0; k < b1; ++k) {
+      const xdrg_op &e = op(k);
+      const std::string P = u32(k), D = u32(e.depth), a = "eb + " + u32(e.noff);
+      const uint32_t wb = 4u * wire_words(e);
+      line("if (!c.field(" + P + ", " + D + ", " + u32(e.kind == XDRG_OP_OPAQUE ? wb : wb) + ")) return false;");
+      switch (e.kind) {
+      case XDRG_OP_BOOL: line("c.put((c.hword(" + a + ") & 0xffu) ? 0x01000000u : 0u);"); break;
+      case XDRG_OP_U64:
+        line("c.put(bswap32(c.hword(" + a + " + 4)));");
+        line("c.put(bswap32(c.hword(" + a + ")));");
+        break;
+      case XDRG_OP_OPAQUE:
+        for (uint32_t w = 0; 4 * w < e.arg0; ++w) {
+          std::string x = "c.hword(" + a + " + " + u32(4 * w) + ")";
+          if (4 * w + 4 > e.arg0) x = "(" + x + " & " + u32((1u << (8 * (e.arg0 - 4 * w))) - 1u) + ")";
+          line("c.put(" + x + ");");
+        }
+        break;
+      default: line("c.put(bswap32(c.hword(" + a + ")));"); break;
+      }
+    }
+  }
+
+  // ---------------------------------------------------------------- decode
+  // xdr_generic_get field by field (marshal.h:142-211).
+  void dec_block(uint32_t pc, uint32_t stop) {
+    while (pc != stop) {
+      const xdrg_op &e = op(pc);
+      const std::string f = "nat + " + u32(e.noff), P = u32(pc), D = u32(e.depth);
+      switch (e.kind) {
+      case XDRG_OP_END: return;
+      case XDRG_OP_JUMP: pc = e.arg0; continue;
+      case XDRG_OP_U32:
+        line("if (!c.field(" + P + ", " + D + ", 4)) return false;");
+        line("st32(" + f + ", bswap32(c.word()));");
+        break;
+      case XDRG_OP_ENUM:
+        line("if (!c.field(" + P + ", " + D + ", 4)) return false;");
+        if (e.flags & XDRG_F_VALIDATE) {
+          line("{");
+          ++ind;
+          line("const uint32_t v = bswap32(c.word());");
+          line("st32(" + f + ", v);");
+          line("if (!" + enum_test("v", e.arg0, e.arg1) + ") return c.fail(" + P + ", XDRG_ERR_INVALID_ENUM);");
+          --ind;
+          line("}");
+        } else {
+          line("st32(" + f + ", bswap32(c.word()));");
+        }
+        break;
+      case XDRG_OP_BOOL:
+        line("if (!c.field(" + P + ", " + D + ", 4)) return false;");
+        line("nat[" + u32(e.noff) + "] = c.word() != 0u;");
+        break;
+      case XDRG_OP_U64:
+        line("if (!c.field(" + P + ", " + D + ", 8)) return false;");
+        line("st32(" + f + " + 4, bswap32(c.word()));");
+        line("st32(" + f + ", bswap32(c.word()));");
+        break;
+      case XDRG_OP_OPAQUE: {
+        const uint32_t L = e.arg0;
+        line("if (!c.field(" + P + ", " + D + ", " + u32(L) + ")) return false;");
+        line("{");
+        ++ind;
+        for (uint32_t k = 0; k < L; k += 4) {
+          line("{ const uint32_t w = c.peek(c.p + " + u32(k) + ");");
+          for (uint32_t b = 0; b < 4 && k + b < L; ++b)
+            line("  nat[" + u32(e.noff + k + b) + "] = uint8_t(w >> " + std::to_string(8 * b) + "); ");
+          line("}");
+        }
+        if (L & 3u)
+          line("if (c.peek(c.p + " + u32(L & ~3u) + ") & " + u32(~((1u << (8 * (L & 3u))) - 1u)) +
+               ") return c.fail(" + P + ", XDRG_ERR_NONZERO_PAD);");
+        line("c.p += " + u32((L + 3u) & ~3u) + ";");
+        --ind;
+        line("}");
+        break;
+      }
+      case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
+        line("if (!c.field(" + P + ", " + D + ", 4)) return false;");
+        line("{");
+        ++ind;
+        line("const uint32_t len = bswap32(c.word());");
+        line("if (len > c.b - c.p) return c.fail(" + P + ", XDRG_ERR_OVERFLOW_GET);");
+        line("if (len > " + u32(e.arg0) + ") return c.fail(" + P + ", " +
+             (e.kind == XDRG_OP_STRING ? "XDRG_ERR_XSTRING_BOUND" : "XDRG_ERR_XVECTOR_BOUND") + ");");
+        line("if ((len & 3u) && (c.peek(c.p + (len & ~3u)) & ~keep_mask(len & 3u)))"
+             " return c.fail(" + P + ", XDRG_ERR_NONZERO_PAD);");
+        line("*reinterpret_cast<uint64_t *>(" + f + ") = c.p;  // the payload stays in the stream");
+        line("st32(" + f + " + 8, len);");
+        line("c.p += (static_cast<uint64_t>(len) + 3u) & ~3ull;");
+        --ind;
+        line("}");
+        break;
+      }
+      case XDRG_OP_UNION: {
+        const uint32_t end = ipdom[pc];
+        line("if (!c.field(" + P + ", " + D + ", 4)) return false;");
+        line("{");
+        ++ind;
+        line("const uint32_t d = bswap32(c.word());");
+        if (e.flags & XDRG_F_VALIDATE)
+          line("if (!" + enum_test("d", e.arg0, e.arg1) + ") return c.fail(" + P + ", XDRG_ERR_INVALID_ENUM);");
+        line("switch (d) {");
+        for (auto &a : arms(e)) {
+          std::string lab;
+          for (uint32_t v : a.second) lab += "case " + u32(v) + ": ";
+          line(lab + "{");
+          ++ind;
+          line("st32(" + f + ", d);");
+          dec_block(a.first, end);
+          --ind;
+          line("} break;");
+        }
+        line("default: {");
+        ++ind;
+        if (e.flags & XDRG_F_DEFAULT) {
+          line("st32(" + f + ", d);");
+          dec_block(e.arg4, end);
+        } else {
+          line("return c.fail(" + P + ", XDRG_ERR_BAD_DISCRIMINANT);");
+        }
+        --ind;
+        line("} break;");
+        line("}");
+        --ind;
+        line("}");
+        pc = end;
+        continue;
+      }
+      case XDRG_OP_VECTOR: {
+        line("if (!c.field(" + P + ", " + D + ", 4)) return false;");
+        line("{");
+        ++ind;
+        line("const uint32_t cnt = bswap32(c.word());");
+        line("if (cnt > " + u32(e.arg0) + ") return c.fail(" + P + ", " +
+             ((e.flags & XDRG_F_POINTER) ? "XDRG_ERR_POINTER_BOUND" : "XDRG_ERR_XVECTOR_BOUND") + ");");
+        line("c.ecur = (c.ecur + 7u) & ~7ull;");
+        line("*reinterpret_cast<uint64_t *>(" + f + ") = c.ecur;");
+        line("st32(" + f + " + 8, cnt);");
+        line("for (uint32_t i = 0; i < cnt; ++i) {");
+        ++ind;
+        line("uint8_t *el = c.heap + c.ecur + static_cast<uint64_t>(i) * " + u32(e.arg1) + ";");
+        dec_elem(pc, pc + 1, pc + 1 + e.arg2, e.arg1);
+        --ind;
+        line("}");
+        line("c.ecur += static_cast<uint64_t>(cnt) * " + u32(e.arg1) + ";");
+        --ind;
+        line("}");
+        pc += 1 + e.arg2;
+        continue;
+      }
+      default: break;
+      }
+      ++pc;
+    }
+  }
+  // One element of a container (dec_vector_elems of xdrgpu.hip): zero the
+  // element, then its fields; an error in element i records i in the
+  // container's xdrg_bytes_ref.rsv (the elements before it are decoded).
+  void dec_elem(uint32_t vpc, uint32_t b0, uint32_t b1, uint32_t es) {
+    const std::string fail_done = "st32(nat + " + u32(op(vpc).noff) + " + 12, i); ";
+    const bool w4 = (es & 3u) == 0;  // 4-byte stores (element arrays are 8-aligned)
+    if (w4)
+      for (uint32_t z = 0; z < es; z += 4) line("st32(el + " + u32(z) + ", 0u);");
+    else
+      line("for (uint32_t z = 0; z < " + u32(es) + "; ++z) el[z] = 0;");
+    for (uint32_t k = b0; k < b1; ++k) {
+      const xdrg_op &e = op(k);
+      const std::string P = u32(k), D = u32(e.depth), f = "el + " + u32(e.noff);
+      const uint32_t need = e.kind == XDRG_OP_U64 ? 8u : e.kind == XDRG_OP_OPAQUE ? e.arg0 : 4u;
+      line("if (!c.field(" + P + ", " + D + ", " + u32(need) + ")) { " + fail_done + "return false; }");
+      switch (e.kind) {
+      case XDRG_OP_BOOL: line("el[" + u32(e.noff) + "] = c.word() != 0u;"); break;
+      case XDRG_OP_U64:
+        line("{ const uint32_t hi = bswap32(c.word()), lo = bswap32(c.word());");
+        if (w4 && !(e.noff & 3u)) {
+          line("  st32(" + f + ", lo); st32(" + f + " + 4, hi);");
+        } else {
+          for (int q = 0; q < 4; ++q)
+            line("  el[" + u32(e.noff + q) + "] = uint8_t(lo >> " + std::to_string(8 * q) + "); el[" +
+                 u32(e.noff + 4 + q) + "] = uint8_t(hi >> " + std::to_string(8 * q) + ");");
+        }
+        line("}");
+        break;
+      case XDRG_OP_OPAQUE: {
+        const uint32_t L = e.arg0;
+        for (uint32_t q = 0; q < L; q += 4) {
+          line("{ const uint32_t w = c.peek(c.p + " + u32(q) + ");");
+          for (uint32_t b = 0; b < 4 && q + b < L; ++b)
+            line("  el[" + u32(e.noff + q + b) + "] = uint8_t(w >> " + std::to_string(8 * b) + ");");
+          line("}");
+        }
+        if (L & 3u)
+          line("if (c.peek(c.p + " + u32(L & ~3u) + ") & " + u32(~((1u << (8 * (L & 3u))) - 1u)) + ") { " +
+               fail_done + "return c.fail(" + P + ", XDRG_ERR_NONZERO_PAD); }");
+        line("c.p += " + u32((L + 3u) & ~3u) + ";");
+        break;
+      }
+      default: {
+        line("{ const uint32_t v = bswap32(c.word());");
+        if (w4 && !(e.noff & 3u))
+          line("  st32(" + f + ", v);");
+        else
+          line("  for (int q = 0; q < 4; ++q) el[" + u32(e.noff) + " + q] = uint8_t(v >> (8 * q));");
+        if (e.kind == XDRG_OP_ENUM && (e.flags & XDRG_F_VALIDATE))
+          line("  if (!" + enum_test("v", e.arg0, e.arg1) + ") { " + fail_done + "return c.fail(" + P +
+               ", XDRG_ERR_INVALID_ENUM); }");
+        line("}");
+        break;
+      }
+      }
+    }
+  }
+};
+
+// A plan the generator handles: every construct of the op set, with the
+// unions' post-dominators defined and inside the plan.
+bool supported(const gen &g) {
+  for (uint32_t i = 0; i < g.nops(); ++i)
+    if (g.op(i).kind == XDRG_OP_UNION && (g.ipdom[i] == kNoPc || g.ipdom[i] >= g.nops())) return false;
+  return true;
+}
+
+}  // namespace
+
+bool spec_source(const xdrg_plan &p, spec_info &info) {
+  if (p.path != XDRG_PATH_VAR) return false;
+  gen g(p);
+  if (!supported(g)) return false;
+  std::ostringstream body;
+  // size
+  g.o.str("");
+  g.ind = 2;
+  g.size_block(0, kNoPc, "nat");
+  const std::string size_code = g.o.str();
+  // encode
+  g.o.str("");
+  g.ind = 2;
+  uint64_t chunks = 0;
+  const uint32_t slots = g.enc_block(0, kNoPc, 0, chunks);
+  const std::string enc_code = g.o.str();
+  // decode
+  g.o.str("");
+  g.ind = 2;
+  g.dec_block(0, kNoPc);
+  const std::string dec_code = g.o.str();
+
+  info.slots = std::max<uint32_t>(1, slots);
+  info.max_chunks = chunks;
+  std::ostringstream s;
+  s << "// Generated by libxdrgpu (codegen.cpp) from a plan of " << p.ops.size()
+    << " ops: straight-line walker for var_kernels.h.\n"
+    << "#include \"var_kernels.h\"\n"
+    << "using namespace xdrg::dev;\n\n"
+    << "struct plan_walk {\n"
+    << "  __device__ __forceinline__ uint64_t size(const uint8_t *nat, uint32_t &bad_op) const {\n"
+    << "    uint64_t s = 0;\n"
+    << size_code << "    return s;\n  }\n"
+    << "  template <int K>\n"
+    << "  __device__ __forceinline__ bool enc(enc_ctx<K> &c, const uint8_t *nat, bool ok) const {\n"
+    << "    if (!ok) return false;\n"
+    << enc_code << "    return true;\n  }\n"
+    << "  template <bool RA>\n"
+    << "  __device__ __forceinline__ bool dec(dec_ctx<RA> &c, uint8_t *nat, bool ok) const {\n"
+    << "    if (!ok) return false;\n"
+    << dec_code << "    return true;\n  }\n"
+    << "};\n\n"
+    << "extern \"C\" __global__ __launch_bounds__(64) void xdrg_spec_size(\n"
+    << "    const uint8_t *native, uint64_t n, uint32_t stride, uint32_t *sizes,\n"
+    << "    unsigned long long *block_sums, uint32_t mark, unsigned long long *err) {\n"
+    << "  var_size_body(plan_walk{}, native, n, stride, sizes, block_sums, mark, err);\n}\n\n"
+    << "extern \"C\" __global__ __launch_bounds__(64) void xdrg_spec_encode(\n"
+    << "    const uint8_t *native, uint64_t n, uint32_t stride, const uint8_t *heap, uint64_t heap_len,\n"
+    << "    uint8_t *xdr, uint64_t cap, uint64_t *offsets, const uint32_t *sizes,\n"
+    << "    const unsigned long long *block_base, uint32_t stack_limit, uint32_t MC, uint32_t C,\n"
+    << "    uint32_t mark, unsigned long long *err) {\n"
+    << "  var_encode_body<plan_walk, " << info.slots << ", 8>(plan_walk{}, native, n, stride, heap, heap_len,\n"
+    << "      xdr, cap, offsets, sizes, block_base, stack_limit, MC, C, mark, err);\n}\n\n";
+  for (int cp = 0; cp < 2; ++cp)
+    s << "extern \"C\" __global__ __launch_bounds__(64) void xdrg_spec_decode" << (cp ? "_copy" : "") << "(\n"
+      << "    const uint8_t *xdr, uint64_t len, const uint64_t *offsets, uint64_t n, uint8_t *native,\n"
+      << "    uint32_t stride, uint8_t *heap, uint32_t stack_limit, uint32_t C, uint64_t ebase,\n"
+      << "    uint32_t F, uint32_t mark, unsigned long long *err) {\n"
+      << "  var_decode_body<plan_walk, " << (cp ? "true" : "false")
+      << ", true>(plan_walk{}, xdr, len, offsets, n, native, stride, heap,\n"
+      << "      stack_limit, C, ebase, F, mark, err);\n}\n\n";
+  info.source = s.str();
+  return true;
+}
+
+}  // namespace xdrg

@@ -6,6 +6,7 @@
 #include <mutex>
 #include <vector>
 
+#include "spec.h"
 #include "xdrgpu.h"
 
 namespace xdrg {
@@ -105,6 +106,7 @@ struct plan_opts {
   int grp_unroll = 0;      // group kernel: chunks in flight (0: per plan)
   int grp_blocks = 0;      // group kernel: workgroups (0: 2048)
   int grp_nontemporal = 0; // group kernel: non-temporal stores
+  int specialize = 1;      // var plans: plan-specialized kernels (spec.cpp) when built
 };
 
 }  // namespace xdrg
@@ -145,6 +147,9 @@ struct xdrg_plan {
   std::mutex upload_mu;
   std::atomic<bool> uploaded[xdrg::kMaxDevices] = {};
   xdrg::dev_tables dev[xdrg::kMaxDevices];
+  // plan-specialized kernels (var plans): generated source, code object,
+  // per-device modules
+  xdrg::spec_state spec;
 };
 
 namespace xdrg {

@@ -1,0 +1,58 @@
+// Plan-specialized kernels: source generation
+// (codegen.cpp) and the code objects a plan carries (spec.cpp).
+#pragma once
+#include <atomic>
+#include <cstdint>
+#include <mutex>
+#include <string>
+#include <vector>
+
+struct xdrg_plan;
+
+namespace xdrg {
+
+constexpr int kSpecDevices = 64;
+
+// The generated source of a plan and the launch facts it fixes.
+struct spec_info {
+  std::string source;     // HIP source over var_kernels.h
+  uint32_t slots = 1;     // chunk-map slots per record the encode kernel uses
+  uint64_t max_chunks = 0;  // 16-byte chunks those slots hold per record (bounds)
+};
+
+// Kernels of one plan on one device.
+struct spec_module {
+  void *module = nullptr;  // hipModule_t
+  void *f_size = nullptr, *f_enc = nullptr, *f_dec = nullptr, *f_dec_copy = nullptr;  // hipFunction_t
+};
+
+// A plan's specialized kernels: state 0 = not built yet, 1 = code object
+// ready, -1 = unavailable (plan shape not generated, or the compile
+// failed: the interpreter serves the plan).
+struct spec_state {
+  std::mutex mu;
+  std::atomic<int> state{0};
+  spec_info info;
+  std::vector<char> code;  // gfx950 code object (ELF)
+  std::string log;         // compile log of a failed build
+  std::atomic<bool> loaded[kSpecDevices] = {};
+  spec_module dev[kSpecDevices];
+};
+
+// Generate the specialized source of a var plan; false if the plan's shape
+// is not handled (the interpreter runs it).
+bool spec_source(const xdrg_plan &p, spec_info &info);
+
+// Build (or find in the kernel cache) the plan's code object: 1 ready,
+// -1 the plan runs on the interpreter.
+int spec_build(const xdrg_plan &p);
+
+// Ensure the plan's code object exists (cache, or hiprtc), then its module
+// on the current device.  Returns the module, or nullptr when the plan runs
+// on the interpreter.
+const spec_module *spec_get(const xdrg_plan &p);
+
+// Release the plan's modules (every device).
+void spec_release(spec_state &s);
+
+}  // namespace xdrg

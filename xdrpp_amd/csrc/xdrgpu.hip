@@ -1640,8 +1640,37 @@ int var_encode(const xdrg_plan &P, const dev_tables &T, const void *d_native, ui
   const uint8_t *nat8 = static_cast<const uint8_t *>(d_native);
   uint8_t *xdr8 = static_cast<uint8_t *>(d_xdr);
   const uint32_t nops = uint32_t(p->ops.size());
-  HIPCHK(launch_size_pass(*p, T, nat8, n, sizes, bsum, mark, err, s));
+  // plan-specialized kernels (spec.cpp): straight-line size and encode walks
+  const spec_module *SM = O.specialize && O.enc_kernel == 0 ? spec_get(*p) : nullptr;
+  uint32_t MCs = 0, Cs = 0, lds_s = 0;
+  if (SM) {
+    const uint32_t KS = p->spec.info.slots;
+    MCs = static_cast<uint32_t>(std::min<uint64_t>(64ull * p->spec.info.max_chunks, 1u << 20));
+    const uint32_t imgs = O.image_bytes >= 0 ? static_cast<uint32_t>(O.image_bytes) & ~15u
+                          : enc_i_layout(p->stride, KS, MCs, 0).total >= (12u << 10) ? 0u : (8u << 10);
+    Cs = static_cast<uint32_t>(std::min<uint64_t>(imgs, (64ull * std::max<uint64_t>(max_rec, 16) + 15u) & ~15ull));
+    lds_s = enc_i_layout(p->stride, KS, MCs, Cs).total;
+    if (lds_s > kVarLdsBudget || 64ull * max_rec >= (1ull << 31) || !aligned(d_native, 16)) SM = nullptr;
+  }
+  if (SM && !p->linear) {
+    const size_t tile = 64ull * p->stride;
+    uint32_t n_mark = mark;
+    void *args[] = {&nat8, &n, const_cast<uint32_t *>(&p->stride), &sizes, &bsum, &n_mark, &err};
+    HIPCHK(hipModuleLaunchKernel(static_cast<hipFunction_t>(SM->f_size), static_cast<uint32_t>(nb), 1, 1,
+                                 64, 1, 1, static_cast<uint32_t>(tile), s, args, nullptr));
+  } else {
+    HIPCHK(launch_size_pass(*p, T, nat8, n, sizes, bsum, mark, err, s));
+  }
   if (int rc = xdrg::launch_block_scan(bsum, bbase, uint32_t(nb), d_status, d_offsets, n, s)) return rc;
+  if (SM) {
+    const unsigned long long *bb = bbase;
+    uint32_t sl = stack_limit, mc = MCs, cc = Cs, mk = mark;
+    void *args[] = {&nat8, &n, const_cast<uint32_t *>(&p->stride), &d_heap, &heap_len, &xdr8, &cap,
+                    &d_offsets, &sizes, &bb, &sl, &mc, &cc, &mk, &err};
+    HIPCHK(hipModuleLaunchKernel(static_cast<hipFunction_t>(SM->f_enc), static_cast<uint32_t>(nb), 1, 1, 64, 1,
+                                 1, lds_s, s, args, nullptr));
+    return XDRG_OK;
+  }
   if (kern == 3) {
 #define LAUNCH_ENC_IU(K, UU)                                                                   \
   k_var_encode_i<K, UU><<<nb, 64, LI.total, s>>>(nat8, n, p->stride, d_heap, heap_len, xdr8,  \
@@ -1752,6 +1781,16 @@ int var_decode(const xdrg_plan &P, const dev_tables &T, const void *d_xdr, uint6
   int kern = O.dec_kernel;
   if (kern == 2 && !ok_W) kern = 0;
   if (kern == 0) kern = ok_W ? 2 : 1;
+  const spec_module *SM = O.specialize && O.dec_kernel == 0 && kern == 2 ? spec_get(*p) : nullptr;
+  if (SM) {  // plan-specialized decode walk (spec.cpp)
+    const uint64_t nb = (n + 63) / 64;
+    uint32_t st = p->stride, sl = stack_limit, cw = Cw, F = p->heap_factor, mk = mark;
+    uint64_t eb = ebase;
+    void *args[] = {&xdr8, &len, &d_offsets, &n, &nat8, &st, &d_heap_out, &sl, &cw, &eb, &F, &mk, &err};
+    HIPCHK(hipModuleLaunchKernel(static_cast<hipFunction_t>(copy ? SM->f_dec_copy : SM->f_dec),
+                                 static_cast<uint32_t>(nb), 1, 1, 64, 1, 1, lw, s, args, nullptr));
+    return XDRG_OK;
+  }
   if (kern == 2) {
     const uint64_t nb = (n + 63) / 64;
 #define LAUNCH_DEC_W(CP, RA)                                                                      \
@@ -1835,6 +1874,7 @@ int xdrg_plan_set_option(xdrg_plan *p, int option, int64_t value) {
     if (v < 0) return XDRG_EINVAL;
     O.grp_blocks = v; return XDRG_OK;
   case XDRG_OPT_GRP_NONTEMPORAL: O.grp_nontemporal = v ? 1 : 0; return XDRG_OK;
+  case XDRG_OPT_SPECIALIZE: O.specialize = v ? 1 : 0; return XDRG_OK;
   default: return XDRG_EINVAL;
   }
 }
@@ -1894,6 +1934,7 @@ static int plan_upload(const xdrg_plan *cp, const dev_tables **out) {
 
 void xdrg_plan_destroy(xdrg_plan *p) {
   if (!p) return;
+  xdrg::spec_release(p->spec);
   int cur = 0;
   const bool restore = hipGetDevice(&cur) == hipSuccess;
   for (int d = 0; d < kMaxDevices; ++d)
@@ -1915,7 +1956,7 @@ int xdrg_plan_get_info(const xdrg_plan *p, xdrg_plan_info *info) {
   info->has_checks = p->has_checks ? 1u : 0u;
   info->max_record_bytes = p->max_record_bytes;
   info->group_records = p->path == XDRG_PATH_FIXED_LDS && !p->has_checks ? p->enc.grp_G : 0u;
-  info->rsv = 0;
+  info->specialized = p->spec.state.load() == 1 ? 1u : 0u;
   return XDRG_OK;
 }
 
