@@ -1,10 +1,20 @@
-"""XDR-language front end and plan back end.
+"""ORACLE / TEST INFRASTRUCTURE ONLY: an XDR-language front end.
 
 The reference's xdrc parses a .x file (RFC 4506 §6 plus xdrc's `namespace`
 and `%` pass-through lines: xdrc/parse.yy, xdrc/scan.ll) and emits C++
 xdr_traits<T> (xdrc/gen_hh.cc).  Its front end needs bison/flex, which this
-image lacks, so the grammar is re-stated here as a recursive-descent parser;
-the back end emits what the device path needs instead of C++ traits:
+image lacks, so the grammar is re-stated here as a recursive-descent parser
+that feeds
+
+  emit_ast_cc(defs)                -> C++ that builds xdrc's own AST (symlist,
+                                      xdrc/xdrc_internal.h) exactly as the
+                                      grammar actions of parse.yy do; linked
+                                      with the REAL xdrc back end
+                                      (xdrc/gen_hh.cc) by oracle/Makefile it
+                                      yields genuine xdrc output (.hh) for the
+                                      oracle and the C++ drop-in tests
+
+and resolves the types to xdrpp_amd.xdr_types descriptors for the tests:
 
   load(text)                       -> Spec: the types as xdrpp_amd.xdr_types
                                       descriptors (Struct / Union / Enum / ...),
@@ -19,7 +29,8 @@ the back end emits what the device path needs instead of C++ traits:
                                       strides and a create function per type:
                                       the plan emitted at generation time
 
-    python -m xdrpp_amd.xdrc file.x -o file_plan.h [type ...]
+    python oracle/xdrc_front.py file.x -o file_plan.h [type ...]
+    python oracle/xdrc_front.py --ast-cc file.x -o file_ast.cc
 
 Names follow xdrc: an anonymous struct/union/enum declared inline for field
 `f` is named `_f_t` (xdrc/xdrc.cc:47), so bad-discriminant messages equal
@@ -29,16 +40,18 @@ Input is expected after the C preprocessor as xdrc expects it; comments
 """
 from __future__ import annotations
 
+import os
 import re
 import sys
 from dataclasses import dataclass, field
 
 import numpy as np
 
-from . import _abi as A
-from .xdr_types import (Bool, CompiledPlan, Double, Enum, Float, Hyper, Int, Opaque, OpaqueArray,
-                        Pointer, String, Struct, UHyper, UInt, Union, Void, XArray, XdrType,
-                        XVector, compile_plan)
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from xdrpp_amd import _abi as A  # noqa: E402
+from xdrpp_amd.xdr_types import (Bool, CompiledPlan, Double, Enum, Float, Hyper, Int, Opaque,  # noqa: E402
+                                 OpaqueArray, Pointer, String, Struct, UHyper, UInt, Union, Void,
+                                 XArray, XdrType, XVector, compile_plan)
 
 XDR_UNBOUNDED = A.XDR_MAX_LEN
 
@@ -76,7 +89,25 @@ def _strip(text: str) -> tuple[str, list[str]]:
     return "\n".join(out), lits
 
 
+def _literal_lines(text: str) -> list[tuple[int, str]]:
+    """(line, text) of the `%` pass-through lines (scan.ll: ^%.*)."""
+    text = re.sub(r"/\*.*?\*/", lambda m: "\n" * m.group(0).count("\n"), text, flags=re.S)
+    return [(i + 1, ln[1:]) for i, ln in enumerate(text.split("\n")) if ln.startswith("%")]
+
+
 def tokenize(text: str) -> list[tuple[str, str, int]]:
+    toks = _tokens(text)
+    lits = _literal_lines(text)
+    out, k = [], 0
+    for t in toks:  # a literal line goes before the first token after it
+        while k < len(lits) and lits[k][0] < t[2]:
+            out.append(("lit", lits[k][1], lits[k][0]))
+            k += 1
+        out.append(t)
+    return out
+
+
+def _tokens(text: str) -> list[tuple[str, str, int]]:
     body, _ = _strip(text)
     toks, pos, line = [], 0, 1
     while pos < len(body):
@@ -106,6 +137,7 @@ class Decl:
     type: object            # str (base type / name) or an inline EnumDef/StructDef/UnionDef
     qual: str = "scalar"    # scalar | array | vec | ptr
     bound: object = None    # value (str) for array/vec; XDR_UNBOUNDED for <>
+    struct_kw: bool = False  # `typedef struct foo bar;` (parse.yy def_type, second form)
 
 
 @dataclass
@@ -176,8 +208,12 @@ class _Parser:
         defs = []
         while True:
             k, v, _ = self.peek()
-            if k == "eof" or (until_brace and v == "}"):
+            if k == "eof" or (until_brace and v == "}" and k == "punct"):
                 return defs
+            if k == "lit":
+                self.take()
+                defs.append(("literal", v))
+                continue
             defs.extend(self.definition())
 
     def definition(self):
@@ -209,20 +245,23 @@ class _Parser:
             return [("union", u)]
         if k == "typedef":
             self.take()
+            kw = False
             if self.peek()[0] == "struct" and self.peek(1)[0] in ("id", "qid") and \
                     self.peek(2)[1] != "{":
                 self.take()  # typedef struct foo bar;  (parse.yy def_type)
+                kw = True
             d = self.declaration()
+            d.struct_kw = kw
             return [("typedef", d)]
         if k == "program":
             return [("program", self.program())]
         if k == "namespace":
             self.take()
-            self.take("id")
+            name = self.take("id")[1]
             self.take("punct", "{")
             defs = self.file(until_brace=True)
             self.take("punct", "}")
-            return defs
+            return [("namespace", name, defs)]
         raise XdrcError(f"line {ln}: unexpected {v!r}")
 
     def value(self):
@@ -438,6 +477,15 @@ def _Recursive(name):
                               "with unbounded recursion)")
 
 
+def _flat(defs):
+    """Definitions with namespaces opened and pass-through lines dropped."""
+    for d in defs:
+        if d[0] == "namespace":
+            yield from _flat(d[2])
+        elif d[0] != "literal":
+            yield d
+
+
 class Spec:
     """The resolved contents of a .x file."""
 
@@ -450,7 +498,7 @@ class Spec:
         self._ast: dict[str, tuple] = {}
         self._busy: set[str] = set()
         order = []
-        for d in defs:
+        for d in _flat(defs):
             if d[0] == "const":
                 self.consts[d[1]] = self._val(d[2])
             elif d[0] == "enum":
@@ -563,7 +611,7 @@ class Spec:
     def proc_table(self) -> np.ndarray:
         """Every procedure of every program/version, sorted, as the table
         xdrg_rpc_dispatch takes (rpc.proc_table)."""
-        from . import rpc as R
+        from xdrpp_amd import rpc as R
         svc: dict[int, dict[int, list[int]]] = {}
         for p in self.programs:
             for v in p.vers:
@@ -571,16 +619,183 @@ class Spec:
         return R.proc_table(svc)
 
 
+def parse(text: str) -> list:
+    """The definitions of .x source, in file order (namespaces nested,
+    `%` lines as ("literal", text))."""
+    return _Parser(tokenize(text)).file()
+
+
 def load(text: str, validate_enums=()) -> Spec:
     """Parse .x source.  ``validate_enums``: enum names that opt in to
     xdr_validate_enum (xdrpp/types.h:157-173)."""
     _, lits = _strip(text)
-    return Spec(_Parser(tokenize(text)).file(), lits, validate_enums)
+    return Spec(parse(text), lits, validate_enums)
 
 
 def load_file(path: str, validate_enums=()) -> Spec:
     with open(path) as f:
         return load(f.read(), validate_enums)
+
+
+# ------------------------------------------------ xdrc AST (the real back end)
+def _cstr(v: str) -> str:
+    return '"' + str(v).replace("\\", "\\\\").replace('"', '\\"') + '"'
+
+
+class _AstCC:
+    """C++ statements that build xdrc's symlist (xdrc/xdrc_internal.h) the
+    way parse.yy's grammar actions do, for gen_hh (oracle/xdrc_driver.cc)."""
+
+    def __init__(self):
+        self.lines, self.n = [], 0
+
+    def var(self, stem):
+        self.n += 1
+        return f"{stem}{self.n}"
+
+    def out(self, s, ind):
+        self.lines.append("  " * ind + s)
+
+    def bound(self, b):
+        return '""' if b == XDR_UNBOUNDED else _cstr(b)  # xdr_unbounded = "" (parse.yy)
+
+    def enum(self, e: EnumDef, ind) -> str:
+        v = self.var("en")
+        self.out(f"rpc_enum *{v} = new rpc_enum;", ind)
+        self.out(f"{v}->id = {_cstr(e.id)};", ind)
+        for name, val in e.tags:
+            self.out(f"{{ rpc_const &c = {v}->tags.push_back(); c.id = {_cstr(name)};"
+                     + (f" c.val = {_cstr(val)};" if val is not None else "") + " }", ind)
+        return v
+
+    def struct(self, st: StructDef, ind) -> str:
+        v = self.var("st")
+        self.out(f"rpc_struct *{v} = new rpc_struct;", ind)
+        self.out(f"{v}->id = {_cstr(st.id)};", ind)
+        for d in st.decls:
+            self.out("{", ind)
+            dv = self.decl(d, ind + 1)
+            self.out(f"{v}->decls.push_back(std::move({dv}));", ind + 1)
+            self.out("}", ind)
+        return v
+
+    def union(self, u: UnionDef, ind) -> str:
+        v = self.var("un")
+        self.out(f"rpc_union *{v} = new rpc_union;", ind)
+        self.out(f"{v}->id = {_cstr(u.id)};", ind)
+        self.out(f"{v}->tagtype = {_cstr(u.tag_type)};", ind)
+        self.out(f"{v}->tagid = {_cstr(u.tag_id)};", ind)
+        nxt = 0
+        for cases, d in u.arms:
+            self.out("{", ind)
+            self.out(f"rpc_ufield &f = {v}->fields.push_back();", ind + 1)
+            for c in cases:
+                self.out(f"f.cases.push_back({_cstr('' if c is None else c)});", ind + 1)
+            if any(c is None for c in cases):
+                self.out("f.hasdefault = true;", ind + 1)
+                self.out(f"{v}->hasdefault = true;", ind + 1)
+            if d is None:  # union_decl: T_VOID ';'
+                self.out('f.decl.qual = rpc_decl::SCALAR; f.decl.ts_which = rpc_decl::TS_ID; '
+                         'f.decl.type = "void";', ind + 1)
+                self.out("f.fieldno = 0;", ind + 1)
+            else:
+                dv = self.decl(d, ind + 1)
+                self.out(f"f.decl = std::move({dv});", ind + 1)
+                nxt += 1
+                self.out(f"f.fieldno = {nxt};", ind + 1)
+            self.out("}", ind)
+        return v
+
+    def decl(self, d: Decl, ind) -> str:
+        v = self.var("d")
+        self.out(f"rpc_decl {v};", ind)
+        t = d.type
+        if isinstance(t, EnumDef):
+            e = self.enum(t, ind)
+            self.out(f"{v}.ts_which = rpc_decl::TS_ENUM; {v}.ts_enum.reset({e});", ind)
+        elif isinstance(t, StructDef):
+            st = self.struct(t, ind)
+            self.out(f"{v}.ts_which = rpc_decl::TS_STRUCT; {v}.ts_struct.reset({st});", ind)
+        elif isinstance(t, UnionDef):
+            un = self.union(t, ind)
+            self.out(f"{v}.ts_which = rpc_decl::TS_UNION; {v}.ts_union.reset({un});", ind)
+        else:
+            self.out(f"{v}.type = {_cstr(t)};", ind)
+        self.out(f"{v}.set_id({_cstr(d.id)});", ind)
+        q = {"scalar": "SCALAR", "array": "ARRAY", "vec": "VEC", "ptr": "PTR"}[d.qual]
+        self.out(f"{v}.qual = rpc_decl::{q};", ind)
+        if d.qual in ("array", "vec"):
+            self.out(f"{v}.bound = {self.bound(d.bound)};", ind)
+        if d.struct_kw:
+            self.out(f'{v}.type = std::string("struct ") + {v}.type;', ind)
+        return v
+
+    def sym(self, kind, ind):
+        self.out(f"{{ rpc_sym *s = &symlist.push_back(); s->settype(rpc_sym::{kind});", ind)
+
+    def defs(self, defs, ind):
+        for d in defs:
+            k = d[0]
+            if k == "literal":
+                self.sym("LITERAL", ind)
+                self.out(f"  *s->sliteral = {_cstr(d[1])}; }}", ind)
+            elif k == "namespace":
+                self.sym("NAMESPACE", ind)
+                self.out(f"  *s->sliteral = {_cstr(d[1])}; }}", ind)
+                self.defs(d[2], ind)
+                self.sym("CLOSEBRACE", ind)
+                self.out("}", ind)
+            elif k == "const":
+                self.sym("CONST", ind)
+                self.out(f"  s->sconst->id = {_cstr(d[1])}; s->sconst->val = {_cstr(d[2])}; }}", ind)
+            elif k == "enum":
+                self.out("{", ind)
+                e = self.enum(d[1], ind + 1)
+                self.out("rpc_sym *s = &symlist.push_back(); s->settype(rpc_sym::ENUM);", ind + 1)
+                self.out(f"*s->senum = std::move(*{e}); delete {e};", ind + 1)
+                self.out("}", ind)
+            elif k == "struct":
+                self.out("{", ind)
+                st = self.struct(d[1], ind + 1)
+                self.out("rpc_sym *s = &symlist.push_back(); s->settype(rpc_sym::STRUCT);", ind + 1)
+                self.out(f"*s->sstruct = std::move(*{st}); delete {st};", ind + 1)
+                self.out("}", ind)
+            elif k == "union":
+                self.out("{", ind)
+                un = self.union(d[1], ind + 1)
+                self.out("rpc_sym *s = &symlist.push_back(); s->settype(rpc_sym::UNION);", ind + 1)
+                self.out(f"*s->sunion = std::move(*{un}); delete {un};", ind + 1)
+                self.out("}", ind)
+            elif k == "typedef":
+                self.out("{", ind)
+                dv = self.decl(d[1], ind + 1)
+                self.out("rpc_sym *s = &symlist.push_back(); s->settype(rpc_sym::TYPEDEF);", ind + 1)
+                self.out(f"*s->stypedef = std::move({dv});", ind + 1)
+                self.out("}", ind)
+            elif k == "program":
+                p = d[1]
+                self.sym("PROGRAM", ind)
+                self.out(f"  s->sprogram->id = {_cstr(p.id)}; s->sprogram->val = {p.val}u;", ind)
+                for vd in p.vers:
+                    self.out(f"  {{ rpc_vers &v = s->sprogram->vers.push_back(); v.id = {_cstr(vd.id)}; "
+                             f"v.val = {vd.val}u;", ind)
+                    for q in vd.procs:
+                        args = "".join(f" r.arg.push_back({_cstr(a)});" for a in q.args)
+                        self.out(f"    {{ rpc_proc &r = v.procs.push_back(); r.id = {_cstr(q.id)}; "
+                                 f"r.val = {q.val}u; r.res = {_cstr(q.res)};{args} }}", ind)
+                    self.out("  }", ind)
+                self.out("}", ind)
+
+
+def emit_ast_cc(defs) -> str:
+    """A C++ translation unit defining build_ast(), which fills xdrc's
+    symlist with the definitions (oracle/xdrc_driver.cc links it with the
+    reference's xdrc/gen_hh.cc)."""
+    a = _AstCC()
+    a.defs(defs, 1)
+    return ("// Generated by oracle/xdrc_front.py --ast-cc: the xdrc AST of a .x file.\n"
+            '#include "xdrc/xdrc_internal.h"\n\n'
+            "void build_ast() {\n" + "\n".join(a.lines) + "\n}\n")
 
 
 # ---------------------------------------------------------- C back end
@@ -594,7 +809,7 @@ def emit_plan_header(spec: Spec, names=None, guard: str = "XDRG_EMITTED_PLANS_H"
     bad-discriminant message of every union op, and a create function."""
     names = list(names) if names else [n for n, t in spec.types.items()
                                        if isinstance(t, (Struct, Union))]
-    out = [f"/* Generated by xdrpp_amd.xdrc (plan back end) -- do not edit. */",
+    out = [f"/* Generated by oracle/xdrc_front.py (plan tables) -- do not edit. */",
            f"#ifndef {guard}", f"#define {guard} 1", '#include "xdrgpu.h"', ""]
     for n in names:
         cp = spec.plan(n)
@@ -642,13 +857,16 @@ def emit_plan_header(spec: Spec, names=None, guard: str = "XDRG_EMITTED_PLANS_H"
 
 def main(argv=None) -> int:
     import argparse
-    ap = argparse.ArgumentParser(prog="python -m xdrpp_amd.xdrc")
+    ap = argparse.ArgumentParser(prog="python oracle/xdrc_front.py")
     ap.add_argument("x")
     ap.add_argument("-o", "--output", default="-")
+    ap.add_argument("--ast-cc", action="store_true", help="emit the xdrc AST builder (for gen_hh)")
     ap.add_argument("types", nargs="*")
     a = ap.parse_intermixed_args(argv)
-    spec = load_file(a.x)
-    text = emit_plan_header(spec, a.types or None)
+    if a.ast_cc:
+        text = emit_ast_cc(parse(open(a.x).read()))
+    else:
+        text = emit_plan_header(load_file(a.x), a.types or None)
     if a.output == "-":
         sys.stdout.write(text)
     else:

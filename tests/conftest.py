@@ -8,7 +8,8 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 TESTS = os.path.dirname(os.path.abspath(__file__))
 GOLD = os.path.join(TESTS, "golden")
-for p in (ROOT, TESTS):
+ORACLE = os.path.join(ROOT, "oracle")  # test infrastructure (xdrc_front.py)
+for p in (ROOT, TESTS, ORACLE):
     if p not in sys.path:
         sys.path.insert(0, p)
 

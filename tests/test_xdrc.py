@@ -1,5 +1,5 @@
-"""The XDR-language front end and plan back end (xdrpp_amd.xdrc, SURVEY.md
-§8 f3).  CPU only: parsing, plan equality with the hand-written descriptors,
+"""The XDR-language front end (oracle/xdrc_front.py, test infrastructure)
+and the plans it yields.  CPU only: parsing, plan equality with the hand-written descriptors,
 the reference's own .x files when the reference tree is present, and the
 emitted C header compiled and run against libxdrgpu.so's host-only plan
 creation (no GPU call)."""
@@ -16,11 +16,11 @@ from xdrpp_amd import _abi as A
 from xdrpp_amd import marshal as M
 from xdrpp_amd import rpc as R
 from xdrpp_amd import schemas as S
-from xdrpp_amd import xdrc
+import xdrc_front as xdrc  # noqa: E402  (oracle/, test infrastructure)
 from xdrpp_amd.xdr_types import compile_plan
 
 REF = "/root/reference"
-BENCH_X = os.path.join(ROOT, "xdrpp_amd", "x", "bench.x")
+BENCH_X = os.path.join(ROOT, "oracle", "x", "bench.x")
 
 
 def same_plan(a, b):
@@ -165,6 +165,6 @@ def test_emitted_header_compiles_and_creates_plans(tmp_path):
 
 def test_cli(tmp_path):
     out = tmp_path / "b.h"
-    subprocess.check_call(["python", "-m", "xdrpp_amd.xdrc", BENCH_X, "-o", str(out), "rec128"],
-                          cwd=ROOT)
+    subprocess.check_call(["python", os.path.join(ROOT, "oracle", "xdrc_front.py"), BENCH_X, "-o",
+                           str(out), "rec128"], cwd=ROOT)
     assert "xdrg_plan_create_rec128" in out.read_text()

@@ -17,7 +17,7 @@ import csv, glob, collections, re, sys
 agg = collections.defaultdict(list)
 for f in glob.glob(sys.argv[1] + "/p*/run_counter_collection.csv"):
     for r in csv.DictReader(open(f)):
-        m = re.search(r"(k_\w+)", r["Kernel_Name"])
+        m = re.search(r"(k_\w+|xdrg_spec_\w+)", r["Kernel_Name"])
         if m:
             agg[(m.group(1), r["Counter_Name"])].append(float(r["Counter_Value"]))
 for (k, c), v in sorted(agg.items()):
