@@ -35,6 +35,10 @@ namespace xdrg {
 namespace dev {
 
 // ---------------------------------------------------------------- encode
+// LDS of an encode wave: the native tile is dead once the walk is done, so
+// the chunk descriptors and the chunk map (built after the walk) reuse it;
+// the image follows.  (Overlaying them cut recvar's LDS per wave from 16.4
+// to 12.8 KiB: more waves per CU to hide the wave's memory round trips.)
 struct enc_i_lds {
   uint32_t tile, desc, map, img, total;
 };
@@ -42,9 +46,10 @@ __host__ __device__ inline enc_i_lds enc_i_layout(uint32_t stride, uint32_t KMAX
                                                  uint32_t C) {
   enc_i_lds L;
   L.tile = 0;
-  L.desc = (64u * stride + 15u) & ~15u;
+  L.desc = 0;
   L.map = L.desc + 64u * KMAX * 16u;
-  L.img = L.map + ((MC * 2u + 15u) & ~15u);
+  const uint32_t a = (64u * stride + 15u) & ~15u, b = L.map + ((MC * 2u + 15u) & ~15u);
+  L.img = a > b ? a : b;
   L.total = L.img + C + 32u;  // phase shift + the last (partial) chunk read
   return L;
 }
@@ -204,6 +209,7 @@ __device__ __forceinline__ void var_encode_body(
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) c.pln[k] = 0;
   }
+  wave_sync();  // every lane's walk is done with the tile: the chunk map reuses it
 
   // ---- chunk map: u16 lane << 10 | slot << 8 | chunk
   uint32_t nch = 0;
