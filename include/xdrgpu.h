@@ -62,7 +62,7 @@
 extern "C" {
 #endif
 
-#define XDRG_ABI_VERSION 4
+#define XDRG_ABI_VERSION 5
 
 /* ---------------------------------------------------------------------- */
 /* Plan ops: a flat, wire-ordered walk of xdr_traits<T>::save.             */
@@ -82,14 +82,19 @@ enum xdrg_op_kind {
   XDRG_OP_VECTOR = 11    /* xvector<T,arg0> / pointer<T> (F_POINTER, arg0 = 1):  (types.h:365-414,476-512,591-665)
                           * native xdrg_bytes_ref {heap offset, count} of an
                           * element array with stride arg1; wire u32 count then
-                          * the elements.  The element's ops follow inline:
-                          * ops [pc+1, pc+1+arg2); fixed-size elements only. */
+                          * the elements.  Fixed-size elements: the element's
+                          * ops follow inline, ops [pc+1, pc+1+arg2).  Any
+                          * element (F_SUB): the element is a subroutine, ops
+                          * from pc arg4 to the next END, walked once per
+                          * element (arg2 = 0); it may be the plan's own
+                          * record (recursive types). */
 };
 
 enum xdrg_op_flags {
   XDRG_F_VALIDATE = 1,   /* ENUM / UNION: opt-in xdr_validate_enum (types.h:157-173) */
   XDRG_F_DEFAULT = 2,    /* UNION: has a default arm; arg4 = its pc             */
-  XDRG_F_POINTER = 4     /* VECTOR: xdr::pointer (count 0 or 1)                 */
+  XDRG_F_POINTER = 4,    /* VECTOR: xdr::pointer (count 0 or 1)                 */
+  XDRG_F_SUB = 8         /* VECTOR: element subroutine at pc arg4 (below)       */
 };
 
 /*
@@ -109,9 +114,24 @@ enum xdrg_op_flags {
  *   UNION      enum table idx    enum count    case table idx   ncases   default pc
  *   JUMP       target pc         -             -                -        -
  *
+ *   VECTOR     max count         elem stride   inline ops       -        F_SUB: body pc
+ *
  * The case table is a run of (int32 value, uint32 target pc) pairs in the
  * shared uint32 table.  `name` is an opaque caller id (for messages).
+ *
+ * Element subroutines (F_SUB).  The record's ops end with END; subroutine
+ * bodies follow it, each ending with its own END.  A body's field offsets
+ * are relative to the element and its depths relative to the VECTOR op:
+ * an op of a body entered from a VECTOR op at (absolute) depth d sits at
+ * depth d + op.depth, so an element struct's fields are at d + 1 exactly
+ * as if the element were written inline.  A body may be entered from
+ * itself (test_recursive, tests/xdrtest.x:29-33).  The kernels keep up to
+ * XDRG_SUB_FRAMES nested element subroutines per record; data nested
+ * deeper raises the stack-overflow error at the VECTOR op that would
+ * enter the next one (bounded recursion: what marshaling_stack_limit,
+ * marshal.h:21, guards the reference's call stack against).
  */
+#define XDRG_SUB_FRAMES 32
 typedef struct xdrg_op {
   uint8_t kind;
   uint8_t flags;
@@ -534,14 +554,18 @@ size_t xdrg_rpc_replies_workspace_size(uint64_t n);
  * level record i's walk enters (the record itself is level 1), so
  * xdr::check_xdr_depth(r_i, limit) (xdrpp/depth_checker.h:72-79) is
  * d_depths[i] <= limit.  A bad union discriminant stops the walk and is
- * reported through d_status like the size pass. */
+ * reported through d_status like the size pass.  d_heap: the staged heap
+ * (element arrays of containers of variable-size elements are read from
+ * it; NULL/0 when the plan has none). */
 int xdrg_record_depths(const xdrg_plan *plan, const void *d_native, uint64_t n,
-                       uint32_t *d_depths, xdrg_status *d_status, void *stream);
+                       const void *d_heap, uint64_t heap_len, uint32_t *d_depths,
+                       xdrg_status *d_status, void *stream);
 
-/* Size pass alone: d_sizes[i] = xdr_size(record i) (uint32). */
+/* Size pass alone: d_sizes[i] = xdr_size(record i) (uint32); d_heap as
+ * for xdrg_record_depths. */
 int xdrg_serial_sizes(const xdrg_plan *plan, const void *d_native, uint64_t n,
-                      uint32_t *d_sizes, uint32_t stack_limit,
-                      xdrg_status *d_status, void *stream);
+                      const void *d_heap, uint64_t heap_len, uint32_t *d_sizes,
+                      uint32_t stack_limit, xdrg_status *d_status, void *stream);
 
 /* Bulk big-endian swaps (endian.h swap32/swap64) over device arrays. */
 int xdrg_swap32(const uint32_t *d_in, uint32_t *d_out, uint64_t n, void *stream);

@@ -858,7 +858,8 @@ opaque_vec<> to_opaque_batch(const T *recs, std::size_t n, hipStream_t s = nullp
   detail::dev_buf<std::uint64_t> d_off(P.fixed() ? 0 : n + 1);
   if (!P.fixed()) {  // size pass for the output capacity (xdr_argpack_size)
     detail::dev_buf<std::uint32_t> d_sz(n);
-    detail::abicheck(xdrg_serial_sizes(P.handle(), d_nat.p, n, d_sz.p, marshaling_stack_limit, d_st.p, s),
+    detail::abicheck(xdrg_serial_sizes(P.handle(), d_nat.p, n, b.heap.empty() ? nullptr : d_heap.p,
+                                       b.heap.size(), d_sz.p, marshaling_stack_limit, d_st.p, s),
                      "xdrg_serial_sizes");
     std::vector<std::uint32_t> sz(n);
     if (n) detail::hipcheck(hipMemcpyAsync(sz.data(), d_sz.p, n * 4, hipMemcpyDeviceToHost, s), "D2H");
@@ -920,12 +921,15 @@ template <typename T>
 std::vector<std::uint32_t> xdr_size_batch(const T *recs, std::size_t n, hipStream_t s = nullptr) {
   const batch_plan<T> &P = plan_for<T>();
   staged_batch b = stage(recs, n);
-  detail::dev_buf<std::uint8_t> d_nat(b.native.size());
+  detail::dev_buf<std::uint8_t> d_nat(b.native.size()), d_heap(b.heap.size());
   detail::dev_buf<std::uint32_t> d_sz(n);
   detail::dev_buf<xdrg_status> d_st(1);
   detail::hipcheck(hipMemcpyAsync(d_nat.p, b.native.data(), b.native.size(), hipMemcpyHostToDevice, s), "H2D");
+  if (!b.heap.empty())
+    detail::hipcheck(hipMemcpyAsync(d_heap.p, b.heap.data(), b.heap.size(), hipMemcpyHostToDevice, s), "H2D");
   detail::abicheck(xdrg_status_init(d_st.p, s), "xdrg_status_init");
-  detail::abicheck(xdrg_serial_sizes(P.handle(), d_nat.p, n, d_sz.p, marshaling_stack_limit, d_st.p, s),
+  detail::abicheck(xdrg_serial_sizes(P.handle(), d_nat.p, n, b.heap.empty() ? nullptr : d_heap.p,
+                                     b.heap.size(), d_sz.p, marshaling_stack_limit, d_st.p, s),
                    "xdrg_serial_sizes");
   std::vector<std::uint32_t> out(n);
   if (n) detail::hipcheck(hipMemcpyAsync(out.data(), d_sz.p, n * 4, hipMemcpyDeviceToHost, s), "D2H");
@@ -943,12 +947,16 @@ std::vector<bool> check_xdr_depth_batch(const T *recs, std::size_t n, std::uint3
                                         hipStream_t s = nullptr) {
   const batch_plan<T> &P = plan_for<T>();
   staged_batch b = stage(recs, n);
-  detail::dev_buf<std::uint8_t> d_nat(b.native.size());
+  detail::dev_buf<std::uint8_t> d_nat(b.native.size()), d_heap(b.heap.size());
   detail::dev_buf<std::uint32_t> d_d(n);
   detail::dev_buf<xdrg_status> d_st(1);
   detail::hipcheck(hipMemcpyAsync(d_nat.p, b.native.data(), b.native.size(), hipMemcpyHostToDevice, s), "H2D");
+  if (!b.heap.empty())
+    detail::hipcheck(hipMemcpyAsync(d_heap.p, b.heap.data(), b.heap.size(), hipMemcpyHostToDevice, s), "H2D");
   detail::abicheck(xdrg_status_init(d_st.p, s), "xdrg_status_init");
-  detail::abicheck(xdrg_record_depths(P.handle(), d_nat.p, n, d_d.p, d_st.p, s), "xdrg_record_depths");
+  detail::abicheck(xdrg_record_depths(P.handle(), d_nat.p, n, b.heap.empty() ? nullptr : d_heap.p,
+                                      b.heap.size(), d_d.p, d_st.p, s),
+                   "xdrg_record_depths");
   std::vector<std::uint32_t> d(n);
   if (n) detail::hipcheck(hipMemcpyAsync(d.data(), d_d.p, n * 4, hipMemcpyDeviceToHost, s), "D2H");
   xdrg_error e{};
@@ -977,7 +985,8 @@ std::vector<std::uint8_t> encode_msgs(const T *recs, std::size_t n, std::vector<
   std::size_t total = (std::size_t(P.fixed_size()) + 4) * n;
   if (!P.fixed()) {  // size pass for the capacity: xdr_argpack_size + the marks
     dev_buf<std::uint32_t> d_sz(n);
-    abicheck(xdrg_serial_sizes(P.handle(), d_nat.p, n, d_sz.p, marshaling_stack_limit, d_st.p, s),
+    abicheck(xdrg_serial_sizes(P.handle(), d_nat.p, n, b.heap.empty() ? nullptr : d_heap.p, b.heap.size(),
+                               d_sz.p, marshaling_stack_limit, d_st.p, s),
              "xdrg_serial_sizes");
     std::vector<std::uint32_t> sz(n);
     if (n) hipcheck(hipMemcpyAsync(sz.data(), d_sz.p, n * 4, hipMemcpyDeviceToHost, s), "D2H");

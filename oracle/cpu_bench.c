@@ -33,7 +33,8 @@ int xdro_decode(const xdrg_op *ops, uint32_t nops, const uint32_t *table, uint32
                 uint8_t *native, uint8_t *heap_out, uint32_t stack_limit, uint64_t *erec,
                 uint32_t *eop);
 int xdro_sizes(const xdrg_op *ops, uint32_t nops, const uint32_t *table, uint32_t stride,
-               const uint8_t *native, uint64_t n, uint32_t *sizes, uint64_t *erec, uint32_t *eop);
+               const uint8_t *native, uint64_t n, const uint8_t *heap, uint64_t heap_len,
+               uint32_t *sizes, uint64_t *erec, uint32_t *eop);
 
 typedef struct {
   const xdrg_op *ops;
@@ -131,7 +132,7 @@ int xdro_bench(const xdrg_op *ops, uint32_t nops, const uint32_t *table, uint32_
   {
     uint64_t erec = 0;
     uint32_t eop = 0;
-    if (xdro_sizes(ops, nops, table, stride, native, n, sizes, &erec, &eop)) { rc = -4; goto done; }
+    if (xdro_sizes(ops, nops, table, stride, native, n, heap, heap_len, sizes, &erec, &eop)) { rc = -4; goto done; }
     off[0] = 0;
     for (uint64_t r = 0; r < n; ++r) off[r + 1] = off[r] + sizes[r];
     if (off[n] > out_cap) { rc = -5; goto done; }

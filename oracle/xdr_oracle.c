@@ -63,8 +63,31 @@ static int enum_ok(const plan_t *P, const xdrg_op *op, uint32_t v) {
   return 0;
 }
 
-/* xvector<T> / pointer<T> (XDRG_OP_VECTOR): the element's ops follow the
- * op inline, [pc+1, pc+1+arg2); elements are fixed-size. */
+/* Plan regions.  The record's ops end with END; element subroutines
+ * (XDRG_F_SUB VECTOR ops, arg4 = entry pc) follow, each ending with END.
+ * A subroutine walks one element: field offsets relative to the element,
+ * depths relative to the VECTOR op that entered it (dbase).  The reference
+ * recurses on its C++ stack; so does this restatement, with the device's
+ * bound on nested element subroutines (XDRG_SUB_FRAMES, include/xdrgpu.h)
+ * restated so both raise the stack-overflow error at the same op.
+ *
+ * Native objects are read through obj_t: the record (stride bytes) or an
+ * element in the heap; bytes at or past the end read as 0, as the kernels'
+ * clamped loads do. */
+typedef struct {
+  const uint8_t *base;
+  uint64_t len;
+  uint64_t off;
+} obj_t;
+static uint8_t o8(obj_t o, uint64_t k) { return o.off + k < o.len ? o.base[o.off + k] : 0; }
+static uint32_t o32(obj_t o, uint64_t k) {
+  uint8_t b[4];
+  for (int i = 0; i < 4; ++i) b[i] = o8(o, k + (uint64_t)i);
+  return rd32(b);
+}
+static uint64_t o64(obj_t o, uint64_t k) { return o32(o, k) | (uint64_t)o32(o, k + 4) << 32; }
+
+/* Fixed-size elements of a VECTOR op without F_SUB: ops [pc+1, pc+1+arg2). */
 static uint32_t elem_wire(const xdrg_op *e) {
   return e->kind == XDRG_OP_U64 ? 8u : e->kind == XDRG_OP_OPAQUE ? pad4(e->arg0) : 4u;
 }
@@ -73,13 +96,23 @@ static uint32_t vec_wire(const plan_t *P, uint32_t pc) {
   for (uint32_t k = 1; k <= P->ops[pc].arg2; ++k) w += elem_wire(&P->ops[pc + k]);
   return w;
 }
-/* Decoded element arrays of record r start at align16(len) + F * off[r]
- * (F = 1 + the largest native/wire size ratio of an element type). */
+/* Decoded element arrays of record r come from [align16(len) + F * off[r],
+ * align16(len) + F * off[r+1]).  Fixed elements: F = 1 + the largest
+ * native/wire size ratio of an element type.  Subroutine elements: distinct
+ * elements start at distinct wire words, so stride/4 per wire byte, plus 2
+ * for the 8-byte alignment of each array (xdrpp_amd/csrc/plan.cpp). */
 static uint32_t heap_factor(const plan_t *P) {
   uint32_t f = 0;
   for (uint32_t pc = 0; pc < P->nops; ++pc)
     if (P->ops[pc].kind == XDRG_OP_VECTOR) {
-      uint32_t we = vec_wire(P, pc), g = (P->ops[pc].arg1 + we - 1) / we + 1;
+      const xdrg_op *op = &P->ops[pc];
+      uint32_t g;
+      if (op->flags & XDRG_F_SUB) {
+        g = (op->arg1 + 3) / 4 + 2;
+      } else {
+        uint32_t we = vec_wire(P, pc);
+        g = (op->arg1 + we - 1) / we + 1;
+      }
       if (g > f) f = g;
     }
   return f;
@@ -90,45 +123,175 @@ uint64_t xdro_decode_heap_size(const xdrg_op *ops, uint32_t nops, uint64_t len) 
   return f ? ((len + 15) & ~15ull) + (uint64_t)f * len : len;
 }
 
-/* xdr_size of one record (xdr_traits<T>::serial_size).  Returns 0 and sets
- * *err and *eop on a bad discriminant. */
-static uint64_t rec_size(const plan_t *P, const uint8_t *nat, uint32_t *err, uint32_t *eop) {
+/* ------------------------------------------------------------------ size */
+/* xdr_size (xdr_traits<T>::serial_size) of the object from pc to its END,
+ * and the deepest class/container level entered (depth_checker,
+ * xdrpp/depth_checker.h:10-79: a union and a container count their own
+ * level, a non-empty xvector/pointer its element's).  A bad discriminant
+ * (or data nested past XDRG_SUB_FRAMES) sets c->err / c->eop. */
+typedef struct {
+  const plan_t *P;
+  const uint8_t *heap;
+  uint64_t heap_len;
+  uint32_t err, eop, dmax;
+} szctx;
+static uint64_t size_ops(szctx *c, uint32_t pc, obj_t o, uint32_t dbase, uint32_t frames) {
+  const plan_t *P = c->P;
   uint64_t s = 0;
-  uint32_t pc = 0;
   for (;;) {
     const xdrg_op *op = &P->ops[pc];
+    if (op->kind == XDRG_OP_END) return s;
+    if (op->kind == XDRG_OP_JUMP) { pc = op->arg0; continue; }
+    if (dbase + op->depth > c->dmax) c->dmax = dbase + op->depth;
     switch (op->kind) {
-    case XDRG_OP_U32: case XDRG_OP_BOOL: case XDRG_OP_ENUM: s += 4; ++pc; break;
     case XDRG_OP_U64: s += 8; ++pc; break;
     case XDRG_OP_OPAQUE: s += pad4(op->arg0); ++pc; break;
-    case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
-      xdrg_bytes_ref r;
-      memcpy(&r, nat + op->noff, sizeof r);
-      s += 4 + pad4(r.len);
-      ++pc;
-      break;
-    }
+    case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: s += 4 + pad4(o32(o, op->noff + 8)); ++pc; break;
     case XDRG_OP_UNION: {
-      int64_t t = union_target(P, op, rd32(nat + op->noff));
-      if (t < 0) { *err = XDRG_ERR_BAD_DISCRIMINANT; *eop = pc; return 0; }
+      int64_t t = union_target(P, op, o32(o, op->noff));
+      if (t < 0) { c->err = XDRG_ERR_BAD_DISCRIMINANT; c->eop = pc; return 0; }
       s += 4;
       pc = (uint32_t)t;
       break;
     }
-    case XDRG_OP_JUMP: pc = op->arg0; break;
     case XDRG_OP_VECTOR: {
-      xdrg_bytes_ref r;
-      memcpy(&r, nat + op->noff, sizeof r);
-      s += 4 + (uint64_t)r.len * vec_wire(P, pc);
-      pc += 1 + op->arg2;
+      const uint64_t eoff = o64(o, op->noff);
+      const uint32_t cnt = o32(o, op->noff + 8);
+      s += 4;
+      if (!(op->flags & XDRG_F_SUB)) {
+        s += (uint64_t)cnt * vec_wire(P, pc);
+        if (cnt)
+          for (uint32_t k = 1; k <= op->arg2; ++k)
+            if (dbase + P->ops[pc + k].depth > c->dmax) c->dmax = dbase + P->ops[pc + k].depth;
+        pc += 1 + op->arg2;
+        break;
+      }
+      if (cnt && frames == XDRG_SUB_FRAMES) { c->err = XDRG_ERR_STACK_PUT; c->eop = pc; return 0; }
+      for (uint32_t i = 0; i < cnt; ++i) {
+        obj_t e = {c->heap, c->heap_len, eoff + (uint64_t)i * op->arg1};
+        s += size_ops(c, op->arg4, e, dbase + op->depth, frames + 1);
+        if (c->err) return 0;
+      }
+      ++pc;
       break;
     }
-    default: return s;
+    default: s += 4; ++pc; break;
+    }
+  }
+}
+static uint64_t rec_size(const plan_t *P, const uint8_t *nat, const uint8_t *heap, uint64_t heap_len,
+                         uint32_t *err, uint32_t *eop) {
+  szctx c = {P, heap, heap_len, 0, 0, 0};
+  obj_t o = {nat, P->stride, 0};
+  uint64_t s = size_ops(&c, 0, o, 0, 0);
+  *err = c.err;
+  *eop = c.eop;
+  return s;
+}
+
+/* ---------------------------------------------------------------- encode */
+/* xdr_generic_put of the object from pc to its END: check(n) before every
+ * field (marshal.h:104-108) after the stack budget of its level
+ * (marshal.h:129-136). */
+typedef struct {
+  const plan_t *P;
+  const uint8_t *heap;
+  uint64_t heap_len;
+  uint8_t *out;
+  uint64_t cap, pos;
+  uint32_t stack_limit, eop;
+} ectx;
+static int enc_ops(ectx *c, uint32_t pc, obj_t o, uint32_t dbase, uint32_t frames) {
+  const plan_t *P = c->P;
+  for (;;) {
+    const xdrg_op *op = &P->ops[pc];
+    if (op->kind == XDRG_OP_END) return 0;
+    if (op->kind == XDRG_OP_JUMP) { pc = op->arg0; continue; }
+    if (dbase + op->depth > c->stack_limit) { c->eop = pc; return XDRG_ERR_STACK_PUT; }
+    uint64_t need = 4;
+    if (op->kind == XDRG_OP_U64) need = 8;
+    else if (op->kind == XDRG_OP_OPAQUE) need = op->arg0;
+    else if (op->kind == XDRG_OP_VAROPAQUE || op->kind == XDRG_OP_STRING) need = 4 + (uint64_t)o32(o, op->noff + 8);
+    if (need > c->cap - c->pos) { c->eop = pc; return XDRG_ERR_OVERFLOW_PUT; }
+    uint8_t *w = c->out + c->pos;
+    switch (op->kind) {
+    case XDRG_OP_U32: case XDRG_OP_ENUM: wr32(w, bswap32(o32(o, op->noff))); c->pos += 4; ++pc; break;
+    case XDRG_OP_BOOL: wr32(w, bswap32(o8(o, op->noff) != 0)); c->pos += 4; ++pc; break;
+    case XDRG_OP_U64: {
+      uint64_t v = o64(o, op->noff);
+      wr32(w, bswap32((uint32_t)(v >> 32)));
+      wr32(w + 4, bswap32((uint32_t)v));
+      c->pos += 8; ++pc; break;
+    }
+    case XDRG_OP_OPAQUE: {
+      uint32_t len = op->arg0;
+      for (uint32_t k = 0; k < len; ++k) w[k] = o8(o, op->noff + k);
+      for (uint64_t k = len; k & 3; ++k) w[k] = 0;
+      c->pos += pad4(len); ++pc; break;
+    }
+    case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
+      const uint64_t hoff = o64(o, op->noff);
+      const uint32_t len = o32(o, op->noff + 8);
+      obj_t h = {c->heap, c->heap_len, hoff};
+      wr32(w, bswap32(len));
+      for (uint32_t k = 0; k < len; ++k) w[4 + k] = o8(h, k);
+      for (uint64_t k = len; k & 3; ++k) w[4 + k] = 0;
+      c->pos += 4 + pad4(len); ++pc; break;
+    }
+    case XDRG_OP_UNION: {
+      uint32_t d = o32(o, op->noff);
+      wr32(w, bswap32(d)); c->pos += 4;
+      pc = (uint32_t)union_target(P, op, d);  /* checked by the size pass */
+      break;
+    }
+    case XDRG_OP_VECTOR: {
+      /* container save (types.h:374-379): size32 count, then each element */
+      const uint64_t eoff = o64(o, op->noff);
+      const uint32_t cnt = o32(o, op->noff + 8);
+      wr32(w, bswap32(cnt)); c->pos += 4;
+      if (!(op->flags & XDRG_F_SUB)) {  /* fixed elements, field by field */
+        for (uint32_t i = 0; i < cnt; ++i) {
+          obj_t el = {c->heap, c->heap_len, eoff + (uint64_t)i * op->arg1};
+          for (uint32_t k = 1; k <= op->arg2; ++k) {
+            const xdrg_op *e = &P->ops[pc + k];
+            if (dbase + e->depth > c->stack_limit) { c->eop = pc + k; return XDRG_ERR_STACK_PUT; }
+            uint32_t wb = elem_wire(e);
+            if (wb > c->cap - c->pos) { c->eop = pc + k; return XDRG_ERR_OVERFLOW_PUT; }
+            uint8_t *q = c->out + c->pos;
+            switch (e->kind) {
+            case XDRG_OP_BOOL: wr32(q, bswap32(o8(el, e->noff) != 0)); break;
+            case XDRG_OP_U64: {
+              uint64_t v = o64(el, e->noff);
+              wr32(q, bswap32((uint32_t)(v >> 32)));
+              wr32(q + 4, bswap32((uint32_t)v));
+              break;
+            }
+            case XDRG_OP_OPAQUE:
+              for (uint32_t b = 0; b < e->arg0; ++b) q[b] = o8(el, e->noff + b);
+              for (uint64_t b = e->arg0; b & 3; ++b) q[b] = 0;
+              break;
+            default: wr32(q, bswap32(o32(el, e->noff))); break;
+            }
+            c->pos += wb;
+          }
+        }
+        pc += 1 + op->arg2;
+        break;
+      }
+      if (cnt && frames == XDRG_SUB_FRAMES) { c->eop = pc; return XDRG_ERR_STACK_PUT; }
+      for (uint32_t i = 0; i < cnt; ++i) {
+        obj_t el = {c->heap, c->heap_len, eoff + (uint64_t)i * op->arg1};
+        int rc = enc_ops(c, op->arg4, el, dbase + op->depth, frames + 1);
+        if (rc) return rc;
+      }
+      ++pc;
+      break;
+    }
+    default: ++pc; break;
     }
   }
 }
 
-/* ---------------------------------------------------------------- encode */
 /* One xdr_generic_put over [out, out+cap) for n records.  Returns 0 or the
  * error code; *erec and *eop receive the failing record and op. */
 int xdro_encode(const xdrg_op *ops, uint32_t nops, const uint32_t *table, uint32_t stride,
@@ -136,123 +299,32 @@ int xdro_encode(const xdrg_op *ops, uint32_t nops, const uint32_t *table, uint32
                 uint8_t *out, uint64_t cap, uint64_t *offsets, uint32_t stack_limit,
                 uint64_t *erec, uint32_t *eop, uint64_t *total) {
   plan_t P = {ops, nops, table, stride};
-  uint64_t pos = 0;
-  (void)heap_len;
+  ectx c = {&P, heap, heap_len, out, cap, 0, stack_limit, 0};
   for (uint64_t r = 0; r < n; ++r) {
     const uint8_t *nat = native + r * stride;
     uint32_t err = 0, op_i = 0;
-    if (offsets) offsets[r] = pos;
+    if (offsets) offsets[r] = c.pos;
     /* xdr_to_opaque sizes the argument pack first (marshal.h:264-268):
      * a bad discriminant throws before any byte is written. */
-    rec_size(&P, nat, &err, &op_i);
+    rec_size(&P, nat, heap, heap_len, &err, &op_i);
     if (err) { *erec = r; *eop = op_i; return (int)err; }
-    uint32_t pc = 0;
-    for (;;) {
-      const xdrg_op *op = &ops[pc];
-      if (op->kind == XDRG_OP_END) break;
-      if (op->kind != XDRG_OP_JUMP && op->depth > stack_limit) {
-        *erec = r; *eop = pc; return XDRG_ERR_STACK_PUT;
-      }
-      uint64_t need = 0;
-      switch (op->kind) {
-      case XDRG_OP_U32: case XDRG_OP_ENUM: case XDRG_OP_BOOL: case XDRG_OP_UNION:
-      case XDRG_OP_VECTOR: need = 4; break;
-      case XDRG_OP_U64: need = 8; break;
-      case XDRG_OP_OPAQUE: need = op->arg0; break;
-      case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
-        xdrg_bytes_ref ref; memcpy(&ref, nat + op->noff, sizeof ref);
-        need = 4 + (uint64_t)ref.len;
-        break;
-      }
-      default: break;
-      }
-      /* check(n): marshal.h:104-108 */
-      if (need > cap - pos) { *erec = r; *eop = pc; return XDRG_ERR_OVERFLOW_PUT; }
-      switch (op->kind) {
-      case XDRG_OP_U32: case XDRG_OP_ENUM:
-        wr32(out + pos, bswap32(rd32(nat + op->noff))); pos += 4; ++pc; break;
-      case XDRG_OP_BOOL:
-        wr32(out + pos, bswap32(nat[op->noff] != 0)); pos += 4; ++pc; break;
-      case XDRG_OP_U64: {
-        uint64_t v = rd64(nat + op->noff);
-        wr32(out + pos, bswap32((uint32_t)(v >> 32)));
-        wr32(out + pos + 4, bswap32((uint32_t)v));
-        pos += 8; ++pc; break;
-      }
-      case XDRG_OP_OPAQUE: {
-        uint32_t len = op->arg0;
-        if (len) {
-          memcpy(out + pos, nat + op->noff, len);
-          for (uint64_t k = len; k & 3; ++k) out[pos + k] = 0;
-          pos += pad4(len);
-        }
-        ++pc; break;
-      }
-      case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
-        xdrg_bytes_ref ref; memcpy(&ref, nat + op->noff, sizeof ref);
-        wr32(out + pos, bswap32(ref.len)); pos += 4;
-        if (ref.len) {
-          memcpy(out + pos, heap + ref.off, ref.len);
-          for (uint64_t k = ref.len; k & 3; ++k) out[pos + k] = 0;
-          pos += pad4(ref.len);
-        }
-        ++pc; break;
-      }
-      case XDRG_OP_UNION: {
-        uint32_t d = rd32(nat + op->noff);
-        wr32(out + pos, bswap32(d)); pos += 4;
-        pc = (uint32_t)union_target(&P, op, d);
-        break;
-      }
-      case XDRG_OP_JUMP: pc = op->arg0; break;
-      case XDRG_OP_VECTOR: {
-        /* container save (types.h:374-379): size32 count, then each element
-         * archived field by field (stack + space checks per field) */
-        xdrg_bytes_ref ref; memcpy(&ref, nat + op->noff, sizeof ref);
-        wr32(out + pos, bswap32(ref.len)); pos += 4;
-        for (uint32_t i = 0; i < ref.len; ++i) {
-          const uint8_t *el = heap + ref.off + (uint64_t)i * op->arg1;
-          for (uint32_t k = 1; k <= op->arg2; ++k) {
-            const xdrg_op *e = &ops[pc + k];
-            if (e->depth > stack_limit) { *erec = r; *eop = pc + k; return XDRG_ERR_STACK_PUT; }
-            uint32_t wb = elem_wire(e);
-            if (wb > cap - pos) { *erec = r; *eop = pc + k; return XDRG_ERR_OVERFLOW_PUT; }
-            switch (e->kind) {
-            case XDRG_OP_BOOL: wr32(out + pos, bswap32(el[e->noff] != 0)); break;
-            case XDRG_OP_U64: {
-              uint64_t v = rd64(el + e->noff);
-              wr32(out + pos, bswap32((uint32_t)(v >> 32)));
-              wr32(out + pos + 4, bswap32((uint32_t)v));
-              break;
-            }
-            case XDRG_OP_OPAQUE:
-              memcpy(out + pos, el + e->noff, e->arg0);
-              for (uint64_t q = e->arg0; q & 3; ++q) out[pos + q] = 0;
-              break;
-            default: wr32(out + pos, bswap32(rd32(el + e->noff))); break;
-            }
-            pos += wb;
-          }
-        }
-        pc += 1 + op->arg2;
-        break;
-      }
-      default: ++pc; break;
-      }
-    }
+    obj_t o = {nat, stride, 0};
+    int rc = enc_ops(&c, 0, o, 0, 0);
+    if (rc) { *erec = r; *eop = c.eop; return rc; }
   }
-  if (offsets) offsets[n] = pos;
-  *total = pos;
+  if (offsets) offsets[n] = c.pos;
+  *total = c.pos;
   return 0;
 }
 
 /* Per-record xdr_size (no writes). */
 int xdro_sizes(const xdrg_op *ops, uint32_t nops, const uint32_t *table, uint32_t stride,
-               const uint8_t *native, uint64_t n, uint32_t *sizes, uint64_t *erec, uint32_t *eop) {
+               const uint8_t *native, uint64_t n, const uint8_t *heap, uint64_t heap_len,
+               uint32_t *sizes, uint64_t *erec, uint32_t *eop) {
   plan_t P = {ops, nops, table, stride};
   for (uint64_t r = 0; r < n; ++r) {
     uint32_t err = 0, op_i = 0;
-    uint64_t s = rec_size(&P, native + r * stride, &err, &op_i);
+    uint64_t s = rec_size(&P, native + r * stride, heap, heap_len, &err, &op_i);
     if (err) { *erec = r; *eop = op_i; return (int)err; }
     sizes[r] = (uint32_t)s;
   }
@@ -260,102 +332,84 @@ int xdro_sizes(const xdrg_op *ops, uint32_t nops, const uint32_t *table, uint32_
 }
 
 /* depth_checker (xdrpp/depth_checker.h:10-79): per record, the deepest
- * class/container level its walk enters (the record is level 1; a union
- * and a container count their own level, a non-empty xvector/pointer its
- * element's).  check_xdr_depth(r, L) == depths[r] <= L. */
+ * class/container level its walk enters (the record is level 1).
+ * check_xdr_depth(r, L) == depths[r] <= L. */
 int xdro_depths(const xdrg_op *ops, uint32_t nops, const uint32_t *table, uint32_t stride,
-                const uint8_t *native, uint64_t n, uint32_t *depths, uint64_t *erec,
-                uint32_t *eop) {
+                const uint8_t *native, uint64_t n, const uint8_t *heap, uint64_t heap_len,
+                uint32_t *depths, uint64_t *erec, uint32_t *eop) {
   plan_t P = {ops, nops, table, stride};
   for (uint64_t r = 0; r < n; ++r) {
-    const uint8_t *nat = native + r * stride;
-    uint32_t pc = 0, d = 0;
-    for (;;) {
-      const xdrg_op *op = &P.ops[pc];
-      if (op->kind == XDRG_OP_END) break;
-      if (op->kind != XDRG_OP_JUMP && op->depth > d) d = op->depth;
-      if (op->kind == XDRG_OP_UNION) {
-        int64_t t = union_target(&P, op, rd32(nat + op->noff));
-        if (t < 0) { *erec = r; *eop = pc; return XDRG_ERR_BAD_DISCRIMINANT; }
-        pc = (uint32_t)t;
-      } else if (op->kind == XDRG_OP_JUMP) {
-        pc = op->arg0;
-      } else if (op->kind == XDRG_OP_VECTOR) {
-        xdrg_bytes_ref ref;
-        memcpy(&ref, nat + op->noff, sizeof ref);
-        if (ref.len)
-          for (uint32_t k = 1; k <= op->arg2; ++k)
-            if (P.ops[pc + k].depth > d) d = P.ops[pc + k].depth;
-        pc += 1 + op->arg2;
-      } else {
-        ++pc;
-      }
-    }
-    depths[r] = d;
+    szctx c = {&P, heap, heap_len, 0, 0, 0};
+    obj_t o = {native + r * stride, stride, 0};
+    size_ops(&c, 0, o, 0, 0);
+    if (c.err) { *erec = r; *eop = c.eop; return (int)c.err; }
+    depths[r] = c.dmax;
   }
-  (void)nops;
   return 0;
 }
 
 /* ---------------------------------------------------------------- decode */
-/* Decode one record from [p, e); returns 0 or an error code (op in *eop).
- * *pp is advanced.  Native record is zero-filled first.  A payload's
+/* xdr_generic_get of the object from pc to its END into `nat` (zeroed by
+ * the caller); returns 0 or an error code (op in c->eop).  A payload's
  * xdrg_bytes_ref holds its byte offset in the stream (`base`): the decoded
- * heap is the stream itself (xdro_decode copies it to heap_out). */
-static int dec_record(const plan_t *P, const uint8_t **pp, const uint8_t *e, uint8_t *nat,
-                      const uint8_t *base, uint8_t *heap_out, uint64_t ecur,
-                      uint32_t stack_limit, uint32_t *eop) {
-  const uint8_t *p = *pp;
-  uint32_t pc = 0;
-  memset(nat, 0, P->stride);
-#define CHECK(nb) do { if ((uint64_t)(nb) > (uint64_t)(e - p)) { *eop = pc; *pp = p; return XDRG_ERR_OVERFLOW_GET; } } while (0)
+ * heap is the stream itself (heap_out holds a copy).  Element arrays are
+ * carved from [ecur, eend) at 8-byte alignment. */
+typedef struct {
+  const plan_t *P;
+  const uint8_t *base, *p, *e;
+  uint8_t *heap_out;
+  uint64_t ecur, eend;
+  uint32_t stack_limit, eop;
+} dctx;
+static int dec_ops(dctx *c, uint32_t pc, uint8_t *nat, uint32_t dbase, uint32_t frames) {
+  const plan_t *P = c->P;
+#define CHECK(nb) do { if ((uint64_t)(nb) > (uint64_t)(c->e - c->p)) { c->eop = pc; return XDRG_ERR_OVERFLOW_GET; } } while (0)
   for (;;) {
     const xdrg_op *op = &P->ops[pc];
-    if (op->kind == XDRG_OP_END) break;
-    if (op->kind != XDRG_OP_JUMP && op->depth > stack_limit) {
-      *eop = pc; *pp = p; return XDRG_ERR_STACK_GET;
-    }
+    if (op->kind == XDRG_OP_END) return 0;
+    if (op->kind == XDRG_OP_JUMP) { pc = op->arg0; continue; }
+    if (dbase + op->depth > c->stack_limit) { c->eop = pc; return XDRG_ERR_STACK_GET; }
     switch (op->kind) {
     case XDRG_OP_U32:
-      CHECK(4); wr32(nat + op->noff, bswap32(rd32(p))); p += 4; ++pc; break;
+      CHECK(4); wr32(nat + op->noff, bswap32(rd32(c->p))); c->p += 4; ++pc; break;
     case XDRG_OP_ENUM: {
       CHECK(4);
-      uint32_t v = bswap32(rd32(p));
-      wr32(nat + op->noff, v); p += 4;
-      if (!enum_ok(P, op, v)) { *eop = pc; *pp = p; return XDRG_ERR_INVALID_ENUM; }
+      uint32_t v = bswap32(rd32(c->p));
+      wr32(nat + op->noff, v); c->p += 4;
+      if (!enum_ok(P, op, v)) { c->eop = pc; return XDRG_ERR_INVALID_ENUM; }
       ++pc; break;
     }
     case XDRG_OP_BOOL:
-      CHECK(4); nat[op->noff] = rd32(p) != 0; p += 4; ++pc; break;
+      CHECK(4); nat[op->noff] = rd32(c->p) != 0; c->p += 4; ++pc; break;
     case XDRG_OP_U64: {
       CHECK(8);
-      uint64_t hi = bswap32(rd32(p)), lo = bswap32(rd32(p + 4));
-      wr64(nat + op->noff, hi << 32 | lo); p += 8; ++pc; break;
+      uint64_t hi = bswap32(rd32(c->p)), lo = bswap32(rd32(c->p + 4));
+      wr64(nat + op->noff, hi << 32 | lo); c->p += 8; ++pc; break;
     }
     case XDRG_OP_OPAQUE: {
       uint32_t len = op->arg0;
       CHECK(len);
       if (len) {
-        memcpy(nat + op->noff, p, len);
-        p += len;
+        memcpy(nat + op->noff, c->p, len);
+        c->p += len;
         for (uint64_t k = len; k & 3; ++k)
-          if (*p++ != 0) { *eop = pc; *pp = p; return XDRG_ERR_NONZERO_PAD; }
+          if (*c->p++ != 0) { c->eop = pc; return XDRG_ERR_NONZERO_PAD; }
       }
       ++pc; break;
     }
     case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
       CHECK(4);
-      uint32_t len = bswap32(rd32(p)); p += 4;
+      uint32_t len = bswap32(rd32(c->p)); c->p += 4;
       CHECK(len);
       if (len > op->arg0) {
-        *eop = pc; *pp = p;
+        c->eop = pc;
         return op->kind == XDRG_OP_STRING ? XDRG_ERR_XSTRING_BOUND : XDRG_ERR_XVECTOR_BOUND;
       }
-      xdrg_bytes_ref ref = {(uint64_t)(p - base), len, 0};
+      xdrg_bytes_ref ref = {(uint64_t)(c->p - c->base), len, 0};
       if (len) {
-        p += len;
+        c->p += len;
         for (uint64_t k = len; k & 3; ++k)
-          if (*p++ != 0) { *eop = pc; *pp = p; return XDRG_ERR_NONZERO_PAD; }
+          if (*c->p++ != 0) { c->eop = pc; return XDRG_ERR_NONZERO_PAD; }
       }
       memcpy(nat + op->noff, &ref, sizeof ref);
       ++pc; break;
@@ -363,65 +417,97 @@ static int dec_record(const plan_t *P, const uint8_t **pp, const uint8_t *e, uin
     case XDRG_OP_VECTOR: {
       /* container load (types.h:380-392): count, check_size, elements */
       CHECK(4);
-      uint32_t cnt = bswap32(rd32(p)); p += 4;
+      uint32_t cnt = bswap32(rd32(c->p)); c->p += 4;
       if (cnt > op->arg0) {
-        *eop = pc; *pp = p;
+        c->eop = pc;
         return (op->flags & XDRG_F_POINTER) ? XDRG_ERR_POINTER_BOUND : XDRG_ERR_XVECTOR_BOUND;
       }
-      ecur = (ecur + 7) & ~7ull;
-      xdrg_bytes_ref ref = {ecur, cnt, 0};
+      c->ecur = (c->ecur + 7) & ~7ull;
+      xdrg_bytes_ref ref = {c->ecur, cnt, 0};
       memcpy(nat + op->noff, &ref, sizeof ref);
-      for (uint32_t i = 0; i < cnt; ++i) {
-        uint8_t *el = heap_out + ecur + (uint64_t)i * op->arg1;
-        memset(el, 0, op->arg1);
-        for (uint32_t k = 1; k <= op->arg2; ++k) {
-          const xdrg_op *f = &P->ops[pc + k];
-          if (f->depth > stack_limit) { *eop = pc + k; *pp = p; return XDRG_ERR_STACK_GET; }
-          uint32_t need = f->kind == XDRG_OP_U64 ? 8u : f->kind == XDRG_OP_OPAQUE ? f->arg0 : 4u;
-          if ((uint64_t)need > (uint64_t)(e - p)) { *eop = pc + k; *pp = p; return XDRG_ERR_OVERFLOW_GET; }
-          switch (f->kind) {
-          case XDRG_OP_BOOL: el[f->noff] = rd32(p) != 0; break;
-          case XDRG_OP_U64: {
-            uint64_t hi = bswap32(rd32(p)), lo = bswap32(rd32(p + 4));
-            wr64(el + f->noff, hi << 32 | lo);
-            break;
+      if (!(op->flags & XDRG_F_SUB)) {  /* fixed elements, field by field */
+        for (uint32_t i = 0; i < cnt; ++i) {
+          uint8_t *el = c->heap_out + c->ecur + (uint64_t)i * op->arg1;
+          memset(el, 0, op->arg1);
+          for (uint32_t k = 1; k <= op->arg2; ++k) {
+            const xdrg_op *f = &P->ops[pc + k];
+            if (dbase + f->depth > c->stack_limit) { c->eop = pc + k; return XDRG_ERR_STACK_GET; }
+            uint32_t need = f->kind == XDRG_OP_U64 ? 8u : f->kind == XDRG_OP_OPAQUE ? f->arg0 : 4u;
+            if ((uint64_t)need > (uint64_t)(c->e - c->p)) { c->eop = pc + k; return XDRG_ERR_OVERFLOW_GET; }
+            switch (f->kind) {
+            case XDRG_OP_BOOL: el[f->noff] = rd32(c->p) != 0; break;
+            case XDRG_OP_U64: {
+              uint64_t hi = bswap32(rd32(c->p)), lo = bswap32(rd32(c->p + 4));
+              wr64(el + f->noff, hi << 32 | lo);
+              break;
+            }
+            case XDRG_OP_OPAQUE:
+              memcpy(el + f->noff, c->p, f->arg0);
+              for (uint64_t q = f->arg0; q & 3; ++q)
+                if (c->p[q] != 0) { c->eop = pc + k; return XDRG_ERR_NONZERO_PAD; }
+              break;
+            default: {
+              uint32_t v = bswap32(rd32(c->p));
+              wr32(el + f->noff, v);
+              if (f->kind == XDRG_OP_ENUM && !enum_ok(P, f, v)) { c->eop = pc + k; return XDRG_ERR_INVALID_ENUM; }
+              break;
+            }
+            }
+            c->p += elem_wire(f);
           }
-          case XDRG_OP_OPAQUE:
-            memcpy(el + f->noff, p, f->arg0);
-            for (uint64_t q = f->arg0; q & 3; ++q)
-              if (p[q] != 0) { *eop = pc + k; *pp = p; return XDRG_ERR_NONZERO_PAD; }
-            break;
-          default: {
-            uint32_t v = bswap32(rd32(p));
-            wr32(el + f->noff, v);
-            if (f->kind == XDRG_OP_ENUM && !enum_ok(P, f, v)) { *eop = pc + k; *pp = p; return XDRG_ERR_INVALID_ENUM; }
-            break;
+        }
+        c->ecur += (uint64_t)cnt * op->arg1;
+        pc += 1 + op->arg2;
+        break;
+      }
+      if (cnt) {
+        /* a count the record cannot hold may overrun the element area; it
+         * fails here (valid data never does) */
+        const uint64_t bytes = (uint64_t)cnt * op->arg1, arr = c->ecur;
+        if (bytes > c->eend - c->ecur) { c->eop = pc; return XDRG_ERR_OVERFLOW_GET; }
+        if (frames == XDRG_SUB_FRAMES) { c->eop = pc; return XDRG_ERR_STACK_GET; }
+        memset(c->heap_out + arr, 0, bytes);
+        c->ecur += bytes;
+        for (uint32_t i = 0; i < cnt; ++i) {
+          int rc = dec_ops(c, op->arg4, c->heap_out + arr + (uint64_t)i * op->arg1, dbase + op->depth,
+                           frames + 1);
+          if (rc) {  /* the element that failed (the unstager stops there) */
+            ref.rsv = i;
+            memcpy(nat + op->noff, &ref, sizeof ref);
+            return rc;
           }
-          }
-          p += elem_wire(f);
         }
       }
-      ecur += (uint64_t)cnt * op->arg1;
-      pc += 1 + op->arg2;
+      ++pc;
       break;
     }
     case XDRG_OP_UNION: {
       CHECK(4);
-      uint32_t d = bswap32(rd32(p)); p += 4;
-      if (!enum_ok(P, op, d)) { *eop = pc; *pp = p; return XDRG_ERR_INVALID_ENUM; }
+      uint32_t d = bswap32(rd32(c->p)); c->p += 4;
+      if (!enum_ok(P, op, d)) { c->eop = pc; return XDRG_ERR_INVALID_ENUM; }
       int64_t t = union_target(P, op, d);
-      if (t < 0) { *eop = pc; *pp = p; return XDRG_ERR_BAD_DISCRIMINANT; }
+      if (t < 0) { c->eop = pc; return XDRG_ERR_BAD_DISCRIMINANT; }
       wr32(nat + op->noff, d);
       pc = (uint32_t)t;
       break;
     }
-    case XDRG_OP_JUMP: pc = op->arg0; break;
     default: ++pc; break;
     }
   }
 #undef CHECK
-  *pp = p;
-  return 0;
+}
+
+/* Decode one record from [*pp, e) into nat (zero-filled first); element
+ * arrays from [ecur, eend).  *pp is advanced. */
+static int dec_record(const plan_t *P, const uint8_t **pp, const uint8_t *e, uint8_t *nat,
+                      const uint8_t *base, uint8_t *heap_out, uint64_t ecur, uint64_t eend,
+                      uint32_t stack_limit, uint32_t *eop) {
+  dctx c = {P, base, *pp, e, heap_out, ecur, eend, stack_limit, 0};
+  memset(nat, 0, P->stride);
+  int rc = dec_ops(&c, 0, nat, 0, 0);
+  *pp = c.p;
+  *eop = c.eop;
+  return rc;
 }
 
 /*
@@ -444,7 +530,8 @@ int xdro_decode(const xdrg_op *ops, uint32_t nops, const uint32_t *table, uint32
     const uint8_t *p = xdr, *e = xdr + len;
     for (uint64_t r = 0; r < n; ++r) {
       int rc = dec_record(&P, &p, e, native + r * stride, xdr, heap_out,
-                          ebase + (uint64_t)F * (uint64_t)(p - xdr), stack_limit, eop);
+                          ebase + (uint64_t)F * (uint64_t)(p - xdr), ebase + (uint64_t)F * len,
+                          stack_limit, eop);
       if (rc) { *erec = r; return rc; }
     }
     if (p != e) { *erec = n; *eop = 0xffffffffu; return XDRG_ERR_TRAILING; }
@@ -456,7 +543,7 @@ int xdro_decode(const xdrg_op *ops, uint32_t nops, const uint32_t *table, uint32
     if ((b - a) & 3) { *erec = r; *eop = 0xffffffffu; return XDRG_ERR_SIZE_NOT_MULT4; }
     const uint8_t *p = xdr + a, *e = xdr + b;
     int rc = dec_record(&P, &p, e, native + r * stride, xdr, heap_out, ebase + (uint64_t)F * a,
-                        stack_limit, eop);
+                        ebase + (uint64_t)F * b, stack_limit, eop);
     if (rc) { *erec = r; return rc; }
     if (p != e) { *erec = r; *eop = 0xffffffffu; return XDRG_ERR_TRAILING; }
   }
@@ -492,7 +579,7 @@ int xdro_encode_msgs(const xdrg_op *ops, uint32_t nops, const uint32_t *table, u
     const uint8_t *nat = native + r * stride;
     uint32_t err = 0, op_i = 0;
     if (offsets) offsets[r] = pos;
-    uint64_t size = rec_size(&P, nat, &err, &op_i);  /* xdr_argpack_size */
+    uint64_t size = rec_size(&P, nat, heap, heap_len, &err, &op_i);  /* xdr_argpack_size */
     if (err) { *erec = r; *eop = op_i; return (int)err; }
     if (4 > cap - pos) { *erec = r; *eop = 0xffffffffu; return XDRG_ERR_OVERFLOW_PUT; }
     wr32(out + pos, bswap32((uint32_t)size | XDRG_MARK_LAST));
@@ -526,7 +613,7 @@ int xdro_decode_msgs(const xdrg_op *ops, uint32_t nops, const uint32_t *table, u
     if ((b - a) & 3) { *erec = r; *eop = 0xffffffffu; return XDRG_ERR_SIZE_NOT_MULT4; }
     const uint8_t *p = xdr + a + 4, *e = xdr + b;
     int rc = dec_record(&P, &p, e, native + r * stride, xdr, heap_out, ebase + (uint64_t)F * a,
-                        stack_limit, eop);
+                        ebase + (uint64_t)F * b, stack_limit, eop);
     if (rc) { *erec = r; return rc; }
     if (p != e) { *erec = r; *eop = 0xffffffffu; return XDRG_ERR_TRAILING; }
   }

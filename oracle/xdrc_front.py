@@ -456,11 +456,11 @@ def _local(name: str) -> str:
 
 
 class _Unsupported(XdrType):
-    """A type the .x file defines but device plans cannot express: a
-    reference to a type from inside its own definition (tests/xdrtest.x has
-    lists and trees; plans are flat DAGs bounded at plan creation), or a
-    counted/optional container of variable-size elements.  It parses, and
-    only compiling a plan that contains it fails."""
+    """A type the .x file defines but device plans cannot express: a union
+    or typedef that refers to itself (a struct may: it is declared before
+    its fields resolve, and reaches itself through a container's element
+    subroutine, as test_recursive does).  It parses, and only compiling a
+    plan that contains it fails."""
 
     size = 16  # staged as an xdrg_bytes_ref
     align = 8
@@ -473,8 +473,7 @@ class _Unsupported(XdrType):
 
 
 def _Recursive(name):
-    return _Unsupported(name, "recursive type: no flat device plan (the reference marshals it "
-                              "with unbounded recursion)")
+    return _Unsupported(name, "recursive union or typedef: only structs may refer to themselves")
 
 
 def _flat(defs):
@@ -517,10 +516,12 @@ class Spec:
         if name in self._busy:
             return _Recursive(name)  # a self-referential type (e.g. a linked list)
         kind, d = self._ast[name]
+        if kind == "struct":  # declared first: its fields may refer to it
+            t = self.types[name] = Struct(d.id)
+            return t.define([(f.id, self._decl_type(f)) for f in d.decls])
         self._busy.add(name)
         try:
-            t = self._struct(d) if kind == "struct" else self._union(d) if kind == "union" \
-                else self._decl_type(d)
+            t = self._union(d) if kind == "union" else self._decl_type(d)
         finally:
             self._busy.discard(name)
         self.types[name] = t
@@ -577,15 +578,12 @@ class Spec:
         if d.type == "string":
             return String(self._val(d.bound))
         t = self._spec(d.type, d.id)
-        try:
-            if d.qual == "array":
-                return XArray(t, self._val(d.bound))
-            if d.qual == "vec":
-                return XVector(t, self._val(d.bound))
-            if d.qual == "ptr":
-                return Pointer(t)
-        except NotImplementedError as e:
-            return _Unsupported(d.id, str(e))
+        if d.qual == "array":
+            return XArray(t, self._val(d.bound))
+        if d.qual == "vec":
+            return XVector(t, self._val(d.bound))
+        if d.qual == "ptr":
+            return Pointer(t)
         return t
 
     def _struct(self, s: StructDef) -> Struct:

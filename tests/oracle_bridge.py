@@ -39,7 +39,8 @@ def lib() -> C.CDLL:
                                   C.POINTER(u64), C.POINTER(u32), C.POINTER(u64)]
         L.xdro_decode.argtypes = [vp, u32, vp, u32, vp, u64, vp, u64, vp, vp, u32,
                                   C.POINTER(u64), C.POINTER(u32)]
-        L.xdro_sizes.argtypes = [vp, u32, vp, u32, vp, u64, vp, C.POINTER(u64), C.POINTER(u32)]
+        L.xdro_sizes.argtypes = [vp, u32, vp, u32, vp, u64, vp, u64, vp, C.POINTER(u64), C.POINTER(u32)]
+        L.xdro_depths.argtypes = L.xdro_sizes.argtypes
         L.xdro_encode_msgs.argtypes = L.xdro_encode.argtypes
         L.xdro_decode_msgs.argtypes = L.xdro_decode.argtypes
         L.xdro_index_msgs.argtypes = [vp, u64, u32, u64, vp, C.POINTER(u64), C.POINTER(u64)]
@@ -59,12 +60,17 @@ class OracleError(Exception):
         self.code, self.record, self.op = code, record, op
 
 
-def sizes(plan, native: np.ndarray, n: int) -> np.ndarray:
+def _heap(heap):
+    return np.zeros(1, dtype=np.uint8) if heap is None or heap.size == 0 else heap
+
+
+def sizes(plan, native: np.ndarray, n: int, heap: np.ndarray | None = None) -> np.ndarray:
     """xdr_size of every record (uint32 [n]) or raises OracleError."""
     out = np.zeros(max(n, 1), dtype=np.uint32)
     er, eo = C.c_uint64(0), C.c_uint32(0)
+    h = _heap(heap)
     rc = lib().xdro_sizes(_p(plan.ops), len(plan.ops), _p(plan.table), plan.stride, _p(native), n,
-                          _p(out), C.byref(er), C.byref(eo))
+                          _p(h), 0 if heap is None else heap.size, _p(out), C.byref(er), C.byref(eo))
     if rc:
         raise OracleError(rc, er.value, eo.value)
     return out[:n]
@@ -79,7 +85,7 @@ def encode(plan, native: np.ndarray, n: int, heap: np.ndarray | None = None,
     er, eo = C.c_uint64(0), C.c_uint32(0)
     if cap is None:
         rc = lib().xdro_sizes(_p(plan.ops), len(plan.ops), _p(plan.table), plan.stride,
-                              _p(native), n, _p(sizes), C.byref(er), C.byref(eo))
+                              _p(native), n, _p(heap), heap.size, _p(sizes), C.byref(er), C.byref(eo))
         cap = int(sizes[:n].astype(np.uint64).sum()) if rc == 0 else 1 << 20
     out = np.zeros(max(cap, 4), dtype=np.uint8)
     offs = np.zeros(n + 1, dtype=np.uint64)
@@ -119,7 +125,7 @@ def encode_msgs(plan, native: np.ndarray, n: int, heap: np.ndarray | None = None
     if cap is None:
         sizes = np.zeros(max(n, 1), dtype=np.uint32)
         rc = lib().xdro_sizes(_p(plan.ops), len(plan.ops), _p(plan.table), plan.stride,
-                              _p(native), n, _p(sizes), C.byref(er), C.byref(eo))
+                              _p(native), n, _p(heap), heap.size, _p(sizes), C.byref(er), C.byref(eo))
         cap = int(sizes[:n].astype(np.uint64).sum()) + 4 * n if rc == 0 else 1 << 20
     out = np.zeros(max(cap, 4), dtype=np.uint8)
     offs = np.zeros(n + 1, dtype=np.uint64)
@@ -199,15 +205,13 @@ def rpc_replies(hdrs: np.ndarray, cap: int | None = None):
     return out[:min(tot.value, cap)], offs, rc, er.value
 
 
-def depths(plan, native: np.ndarray, n: int) -> np.ndarray:
+def depths(plan, native: np.ndarray, n: int, heap: np.ndarray | None = None) -> np.ndarray:
     """depth_checker per record (xdro_depths); raises OracleError."""
-    L = lib()
-    vp, u64, u32 = C.c_void_p, C.c_uint64, C.c_uint32
-    L.xdro_depths.argtypes = [vp, u32, vp, u32, vp, u64, vp, C.POINTER(u64), C.POINTER(u32)]
     out = np.zeros(max(n, 1), dtype=np.uint32)
     er, eo = C.c_uint64(0), C.c_uint32(0)
-    rc = L.xdro_depths(_p(plan.ops), len(plan.ops), _p(plan.table), plan.stride, _p(native), n,
-                       _p(out), C.byref(er), C.byref(eo))
+    h = _heap(heap)
+    rc = lib().xdro_depths(_p(plan.ops), len(plan.ops), _p(plan.table), plan.stride, _p(native), n,
+                           _p(h), 0 if heap is None else heap.size, _p(out), C.byref(er), C.byref(eo))
     if rc:
         raise OracleError(rc, er.value, eo.value)
     return out[:n]

@@ -45,17 +45,14 @@ def test_reference_rpc_msg_x():
 def test_reference_xdrtest_x():
     sp = xdrc.load_file(f"{REF}/tests/xdrtest.x")
     assert same_plan(sp.plan("numerics"), compile_plan(S.numerics))
-    ok, unsupported = [], []
+    # all 28 types plan: containers of variable-size elements and the
+    # recursive test_recursive through element subroutines (XDRG_F_SUB)
+    assert len(sp.types) == 28
     for n in sp.types:
-        try:
-            sp.plan(n)
-            ok.append(n)
-        except xdrc.XdrcError:
-            unsupported.append(n)
-    # recursive types and containers of variable-size elements parse but have no flat plan
-    assert set(unsupported) == {"test_recursive", "hasbytes", "containertest", "containertest1",
-                                "nested_cereal_adapter_calls"}
-    assert len(ok) >= 20
+        M.Plan(sp.plan(n)).close()
+    tr = sp.plan("test_recursive")
+    sub = [o for o in tr.ops if o["kind"] == A.OP_VECTOR]
+    assert len(sub) == 2 and all(o["flags"] & A.F_SUB and o["arg4"] == 0 for o in sub)
     t = sp.proc_table()
     assert t[:, :3].tolist() == [[0x20000000, 1, 1], [0x20000000, 1, 2], [0x20000000, 2, 1],
                                  [0x20000000, 2, 2], [0x20000000, 2, 3], [0x20000000, 2, 4],

@@ -14,10 +14,12 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libxdrgpu.s
 
 # enum xdrg_op_kind
 OP_U32, OP_U64, OP_BOOL, OP_ENUM, OP_OPAQUE, OP_VAROPAQUE, OP_STRING, OP_UNION, OP_JUMP, OP_END, OP_VECTOR = range(1, 12)
-ABI_VERSION = 4  # XDRG_ABI_VERSION, include/xdrgpu.h
+ABI_VERSION = 5  # XDRG_ABI_VERSION, include/xdrgpu.h
 F_VALIDATE = 1
 F_DEFAULT = 2
 F_POINTER = 4
+F_SUB = 8
+SUB_FRAMES = 32  # XDRG_SUB_FRAMES
 
 PATH_FIXED_REG, PATH_FIXED_LDS, PATH_VAR = 1, 2, 3
 
@@ -189,9 +191,9 @@ def lib() -> C.CDLL:
     L.xdrg_rpc_replies.restype = C.c_int
     L.xdrg_rpc_replies_workspace_size.argtypes = [u64]
     L.xdrg_rpc_replies_workspace_size.restype = sz
-    L.xdrg_record_depths.argtypes = [vp, vp, u64, vp, vp, vp]
+    L.xdrg_record_depths.argtypes = [vp, vp, u64, vp, u64, vp, vp, vp]
     L.xdrg_record_depths.restype = C.c_int
-    L.xdrg_serial_sizes.argtypes = [vp, vp, u64, vp, u32, vp, vp]
+    L.xdrg_serial_sizes.argtypes = [vp, vp, u64, vp, u64, vp, u32, vp, vp]
     L.xdrg_serial_sizes.restype = C.c_int
     L.xdrg_swap32.argtypes = [vp, vp, u64, vp]
     L.xdrg_swap32.restype = C.c_int

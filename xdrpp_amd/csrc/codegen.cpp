@@ -506,7 +506,7 @@ bool supported(const gen &g) {
 }  // namespace
 
 bool spec_source(const xdrg_plan &p, spec_info &info) {
-  if (p.path != XDRG_PATH_VAR) return false;
+  if (p.path != XDRG_PATH_VAR || p.has_sub) return false;  // element subroutines: the frame walk
   gen g(p);
   if (!supported(g)) return false;
   std::ostringstream body;
@@ -533,7 +533,6 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
   s << "// Generated by libxdrgpu (codegen.cpp) from a plan of " << p.ops.size()
     << " ops: straight-line walker for var_kernels.h.\n"
     << "#include \"var_kernels.h\"\n"
-
     << "using namespace xdrg::dev;\n\n"
     << "struct plan_walk {\n"
     << "  __device__ __forceinline__ uint64_t size(const uint8_t *nat, uint32_t &bad_op) const {\n"

@@ -157,25 +157,83 @@ void build_prog(const std::vector<int> &src, uint32_t in_words, uint32_t out_wor
   build_group(pg);
 }
 
+
+uint64_t sat_add(uint64_t a, uint64_t b) { return a > UINT64_MAX - b ? UINT64_MAX : a + b; }
+uint64_t sat_mul(uint64_t a, uint64_t b) { return a && b > UINT64_MAX / a ? UINT64_MAX : a * b; }
+
+// Regions of a plan: the record's ops up to its END, then one region per
+// element subroutine (XDRG_F_SUB), each ending with its own END.  A region's
+// ops address a native object of the region's stride: the record's, or the
+// element stride of the VECTOR ops that enter it.
+struct regions {
+  std::vector<uint32_t> id, end, stride;  // per op; per region
+};
+int split_regions(const xdrg_plan &p, regions &R) {
+  const uint32_t n = uint32_t(p.ops.size());
+  R.id.assign(n, 0);
+  uint32_t r = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    R.id[i] = r;
+    if (p.ops[i].kind == XDRG_OP_END) {
+      R.end.push_back(i);
+      ++r;
+    }
+  }
+  if (R.end.empty() || R.end.back() != n - 1) return XDRG_EINVAL;
+  R.stride.assign(R.end.size(), 0);
+  R.stride[0] = p.stride;
+  for (uint32_t i = 0; i < n; ++i) {
+    const xdrg_op &op = p.ops[i];
+    if (op.kind != XDRG_OP_VECTOR || !(op.flags & XDRG_F_SUB)) continue;
+    if (op.arg4 >= n || (op.arg4 && p.ops[op.arg4 - 1].kind != XDRG_OP_END))
+      return XDRG_EINVAL;  // a body starts a region
+    uint32_t &st = R.stride[R.id[op.arg4]];
+    if (st && st != op.arg1) return XDRG_EINVAL;  // one native layout per body
+    st = op.arg1;
+  }
+  for (uint32_t st : R.stride)
+    if (!st) return XDRG_EINVAL;  // a region nothing enters
+  return XDRG_OK;
+}
+
 }  // namespace
 
 int compile_plan(xdrg_plan &p) {
   const uint32_t n = uint32_t(p.ops.size());
   if (n == 0 || p.stride == 0) return XDRG_EINVAL;
+  for (const xdrg_op &op : p.ops)
+    if (op.kind < XDRG_OP_U32 || op.kind > XDRG_OP_VECTOR) return XDRG_EINVAL;
+  regions R;
+  if (int rc = split_regions(p, R)) return rc;
   bool fixed = true, saw_end = false;
   p.max_depth = 0;
   p.has_vector = false;
+  p.has_sub = false;
   p.heap_factor = 0;
   for (uint32_t i = 0; i < n; ++i) {
     xdrg_op &op = p.ops[i];
-    if (op.kind < XDRG_OP_U32 || op.kind > XDRG_OP_VECTOR) return XDRG_EINVAL;
+    const uint32_t rstride = R.stride[R.id[i]], rend = R.end[R.id[i]];
     if (op.kind == XDRG_OP_END) { saw_end = true; continue; }
     if (op.kind == XDRG_OP_VECTOR) {
+      if (op.arg1 == 0) return XDRG_EINVAL;
+      if ((op.flags & XDRG_F_POINTER) && op.arg0 != 1) return XDRG_EINVAL;
+      if ((op.noff & 7) || uint64_t(op.noff) + sizeof(xdrg_bytes_ref) > rstride) return XDRG_EINVAL;
+      if (op.flags & XDRG_F_SUB) {
+        // any element type: its body is a subroutine (checked as a region);
+        // decoded element arrays take at most stride bytes per element,
+        // and distinct elements start at distinct wire words, so the
+        // element area needs stride/4 bytes per wire byte, plus the
+        // 8-byte alignment of each array (one per count word)
+        if (op.arg2 != 0) return XDRG_EINVAL;
+        p.heap_factor = std::max<uint32_t>(p.heap_factor, (op.arg1 + 3u) / 4u + 2u);
+        p.has_vector = p.has_sub = true;
+        if (R.id[i] == 0) p.max_depth = std::max<uint32_t>(p.max_depth, op.depth);
+        fixed = false;
+        continue;
+      }
       // xvector<T,arg0> / pointer<T>: element ops inline in [i+1, i+1+arg2)
       const uint32_t b0 = i + 1, b1 = i + 1 + op.arg2;
-      if (op.arg2 == 0 || b1 >= n || op.arg1 == 0) return XDRG_EINVAL;
-      if ((op.flags & XDRG_F_POINTER) && op.arg0 != 1) return XDRG_EINVAL;
-      if ((op.noff & 7) || uint64_t(op.noff) + sizeof(xdrg_bytes_ref) > p.stride) return XDRG_EINVAL;
+      if (op.arg2 == 0 || b1 > rend) return XDRG_EINVAL;
       uint32_t we = 0;
       for (uint32_t k = b0; k < b1; ++k) {
         const xdrg_op &e = p.ops[k];
@@ -200,13 +258,13 @@ int compile_plan(xdrg_plan &p) {
       continue;
     }
     if (op.kind == XDRG_OP_JUMP) {
-      if (op.arg0 >= n || op.arg0 <= i) return XDRG_EINVAL;  // forward jumps only
+      if (op.arg0 > rend || op.arg0 <= i) return XDRG_EINVAL;  // forward, within the region
       fixed = false;
       continue;
     }
     if (!is_fixed_kind(op.kind)) fixed = false;
-    p.max_depth = std::max<uint32_t>(p.max_depth, op.depth);
-    if (uint64_t(op.noff) + native_size(op) > p.stride) return XDRG_EINVAL;
+    if (R.id[i] == 0) p.max_depth = std::max<uint32_t>(p.max_depth, op.depth);
+    if (uint64_t(op.noff) + native_size(op) > rstride) return XDRG_EINVAL;
     if ((op.kind == XDRG_OP_ENUM || op.kind == XDRG_OP_UNION) && (op.flags & XDRG_F_VALIDATE) &&
         uint64_t(op.arg0) + op.arg1 > p.table.size())
       return XDRG_EINVAL;
@@ -214,9 +272,9 @@ int compile_plan(xdrg_plan &p) {
       if (uint64_t(op.arg2) + 2ull * op.arg3 > p.table.size()) return XDRG_EINVAL;
       for (uint32_t c = 0; c < op.arg3; ++c) {
         uint32_t t = p.table[op.arg2 + 2 * c + 1];
-        if (t >= n || t <= i) return XDRG_EINVAL;
+        if (t > rend || t <= i) return XDRG_EINVAL;
       }
-      if ((op.flags & XDRG_F_DEFAULT) && (op.arg4 >= n || op.arg4 <= i)) return XDRG_EINVAL;
+      if ((op.flags & XDRG_F_DEFAULT) && (op.arg4 > rend || op.arg4 <= i)) return XDRG_EINVAL;
     }
     if ((op.kind == XDRG_OP_U32 || op.kind == XDRG_OP_ENUM || op.kind == XDRG_OP_UNION) &&
         (op.noff & 3))
@@ -236,22 +294,26 @@ int compile_plan(xdrg_plan &p) {
     // Computed for fixed plans too: record-marked batches of any plan run
     // on the interpreter kernels, which size themselves with these.
     std::vector<uint32_t> slots(n, 0), words(n, 0);
-    std::vector<uint64_t> pieces(n, 0), bytes(n, 0), chunks(n, 0);
+    std::vector<uint64_t> pieces(n, 0), bytes(n, 0), chunks(n, 0), minw(n, 0);
     for (uint32_t i = n; i-- > 0;) {
       const xdrg_op &op = p.ops[i];
       uint32_t best = 0, bw = 0;
-      uint64_t bp = 0, bb = 0, bc = 0;
+      uint64_t bp = 0, bb = 0, bc = 0, bm = 0;
       switch (op.kind) {
       case XDRG_OP_END: break;
       case XDRG_OP_JUMP:
         best = slots[op.arg0]; bw = words[op.arg0]; bp = pieces[op.arg0]; bb = bytes[op.arg0];
-        bc = chunks[op.arg0];
+        bc = chunks[op.arg0]; bm = minw[op.arg0];
         break;
       case XDRG_OP_VECTOR: {
         const uint32_t nx = i + 1 + op.arg2;
         best = slots[nx]; bp = pieces[nx]; bc = chunks[nx];
         bw = words[nx] + 1u;  // the count word; elements are unbounded scalar words
-        bb = bytes[nx] + 4ull + uint64_t(op.arg0) * op.arg3;
+        bm = minw[nx] + 4u;   // an empty container
+        if (op.flags & XDRG_F_SUB)  // a body entered backwards is recursive: no bound
+          bb = sat_add(bytes[nx], sat_add(4, sat_mul(op.arg0, op.arg4 > i ? bytes[op.arg4] : UINT64_MAX)));
+        else
+          bb = sat_add(bytes[nx], 4ull + uint64_t(op.arg0) * op.arg3);
         break;
       }
       case XDRG_OP_UNION:
@@ -262,6 +324,7 @@ int compile_plan(xdrg_plan &p) {
           bp = std::max(bp, pieces[t]);
           bb = std::max(bb, bytes[t]);
           bc = std::max(bc, chunks[t]);
+          bm = c ? std::min(bm, minw[t]) : minw[t];
         }
         if (op.flags & XDRG_F_DEFAULT) {
           best = std::max(best, slots[op.arg4]);
@@ -269,9 +332,11 @@ int compile_plan(xdrg_plan &p) {
           bp = std::max(bp, pieces[op.arg4]);
           bb = std::max(bb, bytes[op.arg4]);
           bc = std::max(bc, chunks[op.arg4]);
+          bm = op.arg3 ? std::min(bm, minw[op.arg4]) : minw[op.arg4];
         }
         bw += 1;
-        bb += 4;
+        bb = sat_add(bb, 4);
+        bm += 4;
         break;
       default: {
         const bool var = op.kind == XDRG_OP_VAROPAQUE || op.kind == XDRG_OP_STRING;
@@ -279,7 +344,8 @@ int compile_plan(xdrg_plan &p) {
         const uint32_t w = op.kind == XDRG_OP_U64 ? 2u : op.kind == XDRG_OP_OPAQUE ? (op.arg0 + 3u) / 4u : 1u;
         bw = words[i + 1] + w;
         bp = pieces[i + 1] + (var ? (uint64_t(op.arg0) + 255u) / 256u : 0u);
-        bb = bytes[i + 1] + 4ull * w + (var ? (uint64_t(op.arg0) + 3u) & ~3ull : 0u);
+        bb = sat_add(bytes[i + 1], 4ull * w + (var ? (uint64_t(op.arg0) + 3u) & ~3ull : 0u));
+        bm = minw[i + 1] + (var ? 4u : 4ull * w);
         bc = chunks[i + 1] + (var ? (uint64_t(op.arg0) + 15u) / 16u : 0u);
         if (var) p.max_slot_len = std::max(p.max_slot_len, op.arg0);
       }
@@ -289,7 +355,15 @@ int compile_plan(xdrg_plan &p) {
       pieces[i] = bp;
       bytes[i] = bb;
       chunks[i] = bc;
+      minw[i] = bm;
     }
+    // an element subroutine must consume wire bytes (its decoded arrays are
+    // bounded by the wire words, see the heap factor above)
+    for (xdrg_op &op : p.ops)
+      if (op.kind == XDRG_OP_VECTOR && (op.flags & XDRG_F_SUB)) {
+        if (minw[op.arg4] < 4) return XDRG_EUNSUPPORTED;
+        op.arg3 = uint32_t(std::min<uint64_t>(minw[op.arg4], 0xffffffffu));  // least element wire bytes
+      }
     p.max_chunks16 = chunks[0];
     p.max_var_slots = slots[0];
     p.max_scalar_words = words[0];

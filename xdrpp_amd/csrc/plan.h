@@ -125,6 +125,7 @@ struct xdrg_plan {
   uint64_t max_chunks16 = 0;      // var plans: most 16-byte payload chunks on one path
   uint32_t max_slot_len = 0;      // var plans: largest opaque<>/string<> bound
   bool has_vector = false;        // xvector<T>/pointer<T> fields (XDRG_OP_VECTOR)
+  bool has_sub = false;           // element subroutines (XDRG_F_SUB): the frame-walk kernels
   uint32_t heap_factor = 0;       // decode element-area factor (xdrg_decode_heap_size)
   bool has_checks = false;
   bool has_bool = false;

@@ -1,0 +1,446 @@
+// Element subroutines (XDRG_F_SUB, include/xdrgpu.h): containers of
+// variable-size elements and recursive types.
+//
+// xvector<T>/pointer<T> of a T that is not fixed-size (types.h:374-392,
+// :476-512, :591-665) archives each element with xdr_traits<T>::save/load,
+// which for a struct or union walks its fields (xdrc/gen_hh.cc:212-250,
+// :575-675) -- and T may contain the container again (test_recursive,
+// tests/xdrtest.x:29-33).  The plan gives such an element a subroutine: ops
+// after the record's END, entered once per element.  These kernels walk
+// one record per lane with an explicit stack of element frames (the
+// reference recurses on the C++ stack; marshal.h:129-136, :198-205 count
+// its levels):
+//
+//   k_sub_size     xdr_size per record (+ depth_checker levels) and the
+//                  64-record block sums;
+//   k_sub_encode   xdr_generic_put of the record (marshal.h:84-137);
+//   k_sub_decode   xdr_generic_get (marshal.h:142-211); decoded element
+//                  arrays are carved from the record's element area.
+//
+// A body's field offsets are element-relative and its depths relative to
+// the VECTOR op that entered it (frame.dbase).  Fixed-size element
+// containers inside a body keep the inline element walk of xdrgpu.hip.
+//
+// Included by xdrgpu.hip after its element helpers (load_ops, union_target,
+// enc_vector_elems, dec_vector_elems).
+#pragma once
+
+constexpr uint32_t kSubFrames = XDRG_SUB_FRAMES;
+constexpr uint32_t kReported = 0x100;  // decode: the element walk reported the error
+
+struct sub_frame {
+  uint64_t eb;     // current element: byte offset in the heap
+  uint8_t *ref;    // decode: the container's native xdrg_bytes_ref
+  uint32_t left;   // elements after the current one
+  uint32_t cnt;
+  uint32_t stride;
+  uint32_t entry;  // body pc
+  uint32_t ret;    // pc after the VECTOR op
+  uint32_t dbase;  // absolute depth of the VECTOR op
+};
+
+// The native object a lane's walk is in: its record (frame 0, `len` bytes)
+// or an element in the heap.  Heap bytes at or past heap_len read as 0.
+struct sub_src {
+  const uint8_t *nat;
+  uint32_t len;
+  const uint8_t *heap;
+  uint64_t heap_len;
+  uint64_t eb;
+  bool in_heap;
+  // a naturally aligned field word
+  __device__ __forceinline__ uint32_t w(uint32_t off) const {
+    return in_heap ? unaligned_word(heap, heap_len, eb + off) : ld32(nat + off);
+  }
+  // a word at any byte offset (opaque[n] fields)
+  __device__ __forceinline__ uint32_t wu(uint32_t off) const {
+    return in_heap ? unaligned_word(heap, heap_len, eb + off) : unaligned_word(nat, len, off);
+  }
+  __device__ __forceinline__ uint32_t b(uint32_t off) const {
+    return in_heap ? (eb + off < heap_len ? heap[eb + off] : 0u) : nat[off];
+  }
+  __device__ __forceinline__ uint64_t w64(uint32_t off) const {
+    return static_cast<uint64_t>(w(off)) | (static_cast<uint64_t>(w(off + 4)) << 32);
+  }
+};
+
+// Pop finished elements: returns false when the record's own END is
+// reached, else sets pc (and the walk's object and depth) to the next
+// element's body or the op after the container.
+__device__ __forceinline__ bool sub_next(sub_frame *st, uint32_t &fp, uint32_t &pc, uint32_t &dbase,
+                                         uint64_t &eb, bool &in_heap) {
+  if (!fp) return false;
+  sub_frame &f = st[fp - 1];
+  if (f.left) {
+    --f.left;
+    f.eb += f.stride;
+    eb = f.eb;
+    pc = f.entry;
+    return true;
+  }
+  pc = f.ret;
+  if (--fp) {
+    eb = st[fp - 1].eb;
+    dbase = st[fp - 1].dbase;
+  } else {
+    in_heap = false;
+    dbase = 0;
+  }
+  return true;
+}
+
+// ---------------------------------------------------------------- size
+// xdr_size (xdr_traits<T>::serial_size) of one record, and with DEPTH the
+// deepest class/container level its walk enters (depth_checker,
+// xdrpp/depth_checker.h:41-54).  On failure returns false with the op and
+// code: a bad discriminant, a record of 2^31 bytes or more, or data nested
+// deeper than kSubFrames element frames.
+template <bool DEPTH>
+__device__ bool sub_size(const xdrg_op *__restrict__ ops, const uint32_t *__restrict__ table,
+                         sub_src src, uint64_t &s, uint32_t &dmax, uint32_t &bad_op, uint32_t &code) {
+  sub_frame st[kSubFrames];
+  uint32_t fp = 0, pc = 0, dbase = 0;
+  for (;;) {
+    const xdrg_op &op = ops[pc];
+    if (op.kind == XDRG_OP_END) {
+      if (!sub_next(st, fp, pc, dbase, src.eb, src.in_heap)) return true;
+      continue;
+    }
+    if (op.kind == XDRG_OP_JUMP) { pc = op.arg0; continue; }
+    if (DEPTH) dmax = max(dmax, dbase + op.depth);
+    switch (op.kind) {
+    case XDRG_OP_U64: s += 8; ++pc; break;
+    case XDRG_OP_OPAQUE: s += (op.arg0 + 3u) & ~3u; ++pc; break;
+    case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING:
+      s += 4ull + ((static_cast<uint64_t>(src.w(op.noff + 8)) + 3u) & ~3ull);
+      ++pc;
+      break;
+    case XDRG_OP_UNION: {
+      const int t = union_target(op, table, src.w(op.noff));
+      s += 4;
+      if (t < 0) { bad_op = pc; code = XDRG_ERR_BAD_DISCRIMINANT; return false; }
+      pc = static_cast<uint32_t>(t);
+      break;
+    }
+    case XDRG_OP_VECTOR: {
+      const uint32_t cnt = src.w(op.noff + 8);
+      s += 4;
+      if (!(op.flags & XDRG_F_SUB)) {  // fixed-size elements (arg3 wire bytes each)
+        s += static_cast<uint64_t>(cnt) * op.arg3;
+        if (DEPTH && cnt)
+          for (uint32_t k = 1; k <= op.arg2; ++k) dmax = max(dmax, dbase + ops[pc + k].depth);
+        pc += 1 + op.arg2;
+        break;
+      }
+      if (!cnt) { ++pc; break; }
+      if (fp == kSubFrames) { bad_op = pc; code = XDRG_ERR_STACK_PUT; return false; }
+      dbase += op.depth;
+      st[fp++] = sub_frame{src.w64(op.noff), nullptr, cnt - 1, cnt, op.arg1, op.arg4, pc + 1, dbase};
+      src.eb = st[fp - 1].eb;
+      src.in_heap = true;
+      pc = op.arg4;
+      break;
+    }
+    default: s += 4; ++pc; break;
+    }
+    if (s >= kSizeErr) { bad_op = 0; code = XDRG_ERR_OVERFLOW_PUT; return false; }
+  }
+}
+
+template <bool DEPTH>
+__global__ __launch_bounds__(256) void k_sub_size(
+    const uint8_t *__restrict__ native, uint64_t n, uint32_t stride, const uint8_t *__restrict__ heap,
+    uint64_t heap_len, const xdrg_op *__restrict__ ops, uint32_t nops, const uint32_t *__restrict__ table,
+    uint32_t *__restrict__ sizes, unsigned long long *__restrict__ block_sums, uint32_t mark,
+    unsigned long long *err, uint32_t *__restrict__ depths) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  xdrg_op *sops = reinterpret_cast<xdrg_op *>(smem);
+  load_ops(sops, ops, nops);
+  const uint64_t r = static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x;
+  uint32_t size = 0;
+  if (r < n) {
+    const sub_src src{native + r * stride, stride, heap, heap_len, 0, false};
+    uint64_t s = mark;
+    uint32_t dmax = 0, bad_op = 0, code = 0;
+    if (sub_size<DEPTH>(sops, table, src, s, dmax, bad_op, code)) {
+      size = static_cast<uint32_t>(s);
+    } else {
+      report(err, r, bad_op, code);
+      size = kSizeErr;
+    }
+    if (sizes) sizes[r] = size;
+    if (DEPTH) depths[r] = dmax;
+  }
+  unsigned long long v = (size & kSizeErr) ? 0ull : size;
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  const uint64_t blk = r / 64u;
+  if (block_sums && (threadIdx.x & 63u) == 0 && blk * 64u < n) block_sums[blk] = v;
+}
+
+// -------------------------------------------------------------- encode
+// Record offsets as k_var_encode computes them (block-local scan on top of
+// the 64-record block bases), then the record's walk with check(n) and the
+// stack budget before every field (marshal.h:104-108, :129-136).
+__global__ __launch_bounds__(256) void k_sub_encode(
+    const uint8_t *__restrict__ native, uint64_t n, uint32_t stride, const uint8_t *__restrict__ heap,
+    uint64_t heap_len, uint8_t *__restrict__ xdr, uint64_t cap, uint64_t *__restrict__ offsets,
+    const uint32_t *__restrict__ sizes, const unsigned long long *__restrict__ block_base,
+    const xdrg_op *__restrict__ ops, uint32_t nops, const uint32_t *__restrict__ table,
+    uint32_t stack_limit, uint32_t mark, unsigned long long *err) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  xdrg_op *sops = reinterpret_cast<xdrg_op *>(smem);
+  load_ops(sops, ops, nops);
+  const uint64_t r = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const uint32_t sz = r < n ? sizes[r] : 0u;
+  const unsigned long long v = (sz & kSizeErr) ? 0ull : sz;
+  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  unsigned long long incl = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long x = __shfl_up(incl, o, 64);
+    if (lane >= static_cast<uint32_t>(o)) incl += x;
+  }
+  if (r >= n) return;
+  const uint64_t off = block_base[blockIdx.x * 4u + wid] + incl - v;
+  offsets[r] = off;
+  if (sz & kSizeErr) return;  // the size pass reported this record
+
+  sub_src src{native + r * stride, stride, heap, heap_len, 0, false};
+  uint64_t pos = off;
+  if (mark) {  // the message's record mark (message_t::alloc, marshal.cc:15-31)
+    if (4 > cap - min(pos, cap)) { report(err, r, kOpRecordLevel, XDRG_ERR_OVERFLOW_PUT); return; }
+    st32(xdr + pos, mark_word(sz - 4u));
+    pos += 4;
+  }
+  sub_frame st[kSubFrames];
+  uint32_t fp = 0, pc = 0, dbase = 0;
+  for (;;) {
+    const xdrg_op &op = sops[pc];
+    if (op.kind == XDRG_OP_END) {
+      if (!sub_next(st, fp, pc, dbase, src.eb, src.in_heap)) break;
+      continue;
+    }
+    if (op.kind == XDRG_OP_JUMP) { pc = op.arg0; continue; }
+    if (dbase + op.depth > stack_limit) { report(err, r, pc, XDRG_ERR_STACK_PUT); return; }
+    uint64_t need = 4;
+    uint32_t len = 0;
+    if (op.kind == XDRG_OP_U64) need = 8;
+    else if (op.kind == XDRG_OP_OPAQUE) need = op.arg0;
+    else if (op.kind == XDRG_OP_VAROPAQUE || op.kind == XDRG_OP_STRING) {
+      len = src.w(op.noff + 8);
+      need = 4ull + len;
+    }
+    if (need > cap - min(pos, cap)) { report(err, r, pc, XDRG_ERR_OVERFLOW_PUT); return; }
+    uint32_t *o = reinterpret_cast<uint32_t *>(xdr + pos);
+    switch (op.kind) {
+    case XDRG_OP_U32: case XDRG_OP_ENUM: o[0] = bswap32(src.w(op.noff)); pos += 4; ++pc; break;
+    case XDRG_OP_BOOL: o[0] = src.b(op.noff) ? 0x01000000u : 0u; pos += 4; ++pc; break;
+    case XDRG_OP_U64:
+      o[0] = bswap32(src.w(op.noff + 4));
+      o[1] = bswap32(src.w(op.noff));
+      pos += 8;
+      ++pc;
+      break;
+    case XDRG_OP_OPAQUE: {
+      const uint32_t L = op.arg0, nw = (L + 3u) >> 2;
+      for (uint32_t k = 0; k < nw; ++k) {
+        uint32_t w = src.wu(op.noff + 4u * k);
+        if (4 * k + 4 > L) w &= keep_mask(L - 4 * k);
+        o[k] = w;
+      }
+      pos += 4ull * nw;
+      ++pc;
+      break;
+    }
+    case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
+      const uint64_t hoff = src.w64(op.noff);
+      const uint32_t nw = (len + 3u) >> 2;
+      o[0] = bswap32(len);
+      for (uint32_t k = 0; k < nw; ++k) {
+        uint32_t w = unaligned_word(heap, heap_len, hoff + 4ull * k);
+        if (4 * k + 4 > len) w &= keep_mask(len - 4 * k);
+        o[1 + k] = w;
+      }
+      pos += 4ull + 4ull * nw;
+      ++pc;
+      break;
+    }
+    case XDRG_OP_UNION: {
+      const uint32_t d = src.w(op.noff);
+      o[0] = bswap32(d);
+      pos += 4;
+      pc = static_cast<uint32_t>(union_target(op, table, d));  // validated by the size pass
+      break;
+    }
+    case XDRG_OP_VECTOR: {
+      const uint64_t eoff = src.w64(op.noff);
+      const uint32_t cnt = src.w(op.noff + 8);
+      o[0] = bswap32(cnt);
+      pos += 4;
+      if (!(op.flags & XDRG_F_SUB)) {
+        uint32_t at = static_cast<uint32_t>(pos - off);
+        auto put = [&](uint32_t a, uint32_t w) { st32(xdr + off + a, w); };
+        if (!enc_vector_elems(sops, pc + 1, op.arg2, heap, heap_len, eoff, cnt, op.arg1, pos, cap, at,
+                              stack_limit - dbase, r, err, put))
+          return;
+        pc += 1 + op.arg2;
+        break;
+      }
+      if (!cnt) { ++pc; break; }
+      if (fp == kSubFrames) { report(err, r, pc, XDRG_ERR_STACK_PUT); return; }
+      dbase += op.depth;
+      st[fp++] = sub_frame{eoff, nullptr, cnt - 1, cnt, op.arg1, op.arg4, pc + 1, dbase};
+      src.eb = eoff;
+      src.in_heap = true;
+      pc = op.arg4;
+      break;
+    }
+    default: ++pc; break;
+    }
+  }
+}
+
+// -------------------------------------------------------------- decode
+// Record r = xdr_from_opaque(stream[off[r], off[r+1]), r) with check(n)
+// before every read; the native record and every element array are
+// zero-filled first.  Payloads stay in the stream (heap_out holds it at
+// [0, len)); element arrays come from the record's element area
+// [ebase + F*off[r], ebase + F*off[r+1]) at 8-byte alignment.  On a failure
+// inside elements, each open container's rsv holds the index of the
+// element that failed (the unstager stops there).
+__global__ __launch_bounds__(256) void k_sub_decode(
+    const uint8_t *__restrict__ xdr, uint64_t len, const uint64_t *__restrict__ offsets, uint64_t n,
+    uint8_t *__restrict__ native, uint32_t stride, const xdrg_op *__restrict__ ops, uint32_t nops,
+    const uint32_t *__restrict__ table, uint32_t stack_limit, uint8_t *__restrict__ heap,
+    uint64_t ebase, uint32_t F, uint32_t mark, unsigned long long *err) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  xdrg_op *sops = reinterpret_cast<xdrg_op *>(smem);
+  load_ops(sops, ops, nops);
+  const uint64_t r = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  const uint64_t a = offsets[r], b = offsets[r + 1];
+  if (r == n - 1 && b != len) report(err, n, kOpRecordLevel, XDRG_ERR_TRAILING);
+  if (b < a || b > len) { report(err, r, 0, XDRG_ERR_OVERFLOW_GET); return; }
+  if (mark) {  // xdr_from_msg: the message read_message framed (srpc.cc:29-55)
+    const uint32_t c = b - a < 4 ? XDRG_ERR_MSG_EOF : mark_code(ld32(xdr + a), b - a - 4);
+    if (c) { report(err, r, kOpRecordLevel, c); return; }
+  }
+  if ((b - a) & 3u) { report(err, r, kOpRecordLevel, XDRG_ERR_SIZE_NOT_MULT4); return; }
+  uint8_t *const rec = native + r * stride;
+  for (uint32_t k = 0; k < stride / 4; ++k) st32(rec + 4 * k, 0u);
+  uint64_t p = a + mark;
+  uint64_t ecur = ebase + static_cast<uint64_t>(F) * a;
+  const uint64_t eend = ebase + static_cast<uint64_t>(F) * b;
+  sub_frame st[kSubFrames];
+  uint32_t fp = 0, pc = 0, dbase = 0, code = 0;
+  uint64_t eb = 0;
+  bool in_heap = false;
+  for (;;) {
+    const xdrg_op &op = sops[pc];
+    if (op.kind == XDRG_OP_END) {
+      if (!sub_next(st, fp, pc, dbase, eb, in_heap)) break;
+      continue;
+    }
+    if (op.kind == XDRG_OP_JUMP) { pc = op.arg0; continue; }
+    if (dbase + op.depth > stack_limit) { code = XDRG_ERR_STACK_GET; break; }
+    uint8_t *nat = in_heap ? heap + eb : rec;
+    const uint64_t rem = b - p;
+    switch (op.kind) {
+    case XDRG_OP_U32:
+      if (rem < 4) { code = XDRG_ERR_OVERFLOW_GET; break; }
+      st32(nat + op.noff, bswap32(ld32(xdr + p))); p += 4; ++pc; break;
+    case XDRG_OP_ENUM: {
+      if (rem < 4) { code = XDRG_ERR_OVERFLOW_GET; break; }
+      const uint32_t v = bswap32(ld32(xdr + p));
+      st32(nat + op.noff, v); p += 4;
+      if ((op.flags & XDRG_F_VALIDATE) && !enum_ok(table, op.arg0, op.arg1, v)) { code = XDRG_ERR_INVALID_ENUM; break; }
+      ++pc; break;
+    }
+    case XDRG_OP_BOOL:
+      if (rem < 4) { code = XDRG_ERR_OVERFLOW_GET; break; }
+      nat[op.noff] = ld32(xdr + p) != 0u; p += 4; ++pc; break;
+    case XDRG_OP_U64:
+      if (rem < 8) { code = XDRG_ERR_OVERFLOW_GET; break; }
+      st32(nat + op.noff + 4, bswap32(ld32(xdr + p)));
+      st32(nat + op.noff, bswap32(ld32(xdr + p + 4)));
+      p += 8; ++pc; break;
+    case XDRG_OP_OPAQUE: {
+      const uint32_t L = op.arg0;
+      if (rem < L) { code = XDRG_ERR_OVERFLOW_GET; break; }
+      for (uint32_t k = 0; k < L; ++k) nat[op.noff + k] = xdr[p + k];
+      if ((L & 3u) && (ld32(xdr + p + (L & ~3u)) & ~keep_mask(L & 3u))) { code = XDRG_ERR_NONZERO_PAD; break; }
+      p += (L + 3u) & ~3u; ++pc; break;
+    }
+    case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
+      if (rem < 4) { code = XDRG_ERR_OVERFLOW_GET; break; }
+      const uint32_t L = bswap32(ld32(xdr + p));
+      if (L > rem - 4) { code = XDRG_ERR_OVERFLOW_GET; break; }
+      if (L > op.arg0) { code = op.kind == XDRG_OP_STRING ? XDRG_ERR_XSTRING_BOUND : XDRG_ERR_XVECTOR_BOUND; break; }
+      p += 4;
+      const uint32_t nw = (L + 3u) >> 2;
+      if ((L & 3u) && (ld32(xdr + p + 4ull * (nw - 1)) & ~keep_mask(L & 3u))) { code = XDRG_ERR_NONZERO_PAD; break; }
+      *reinterpret_cast<uint64_t *>(nat + op.noff) = p;  // the payload stays in the stream
+      st32(nat + op.noff + 8, L);
+      p += 4ull * nw; ++pc; break;
+    }
+    case XDRG_OP_UNION: {
+      if (rem < 4) { code = XDRG_ERR_OVERFLOW_GET; break; }
+      const uint32_t d = bswap32(ld32(xdr + p));
+      p += 4;
+      if ((op.flags & XDRG_F_VALIDATE) && !enum_ok(table, op.arg0, op.arg1, d)) { code = XDRG_ERR_INVALID_ENUM; break; }
+      const int t = union_target(op, table, d);
+      if (t < 0) { code = XDRG_ERR_BAD_DISCRIMINANT; break; }
+      st32(nat + op.noff, d);
+      pc = static_cast<uint32_t>(t);
+      break;
+    }
+    case XDRG_OP_VECTOR: {
+      if (rem < 4) { code = XDRG_ERR_OVERFLOW_GET; break; }
+      const uint32_t cnt = bswap32(ld32(xdr + p));
+      p += 4;
+      if (cnt > op.arg0) {  // check_size (types.h:486-489, 605-608)
+        code = (op.flags & XDRG_F_POINTER) ? XDRG_ERR_POINTER_BOUND : XDRG_ERR_XVECTOR_BOUND;
+        break;
+      }
+      ecur = (ecur + 7u) & ~7ull;
+      *reinterpret_cast<uint64_t *>(nat + op.noff) = ecur;
+      st32(nat + op.noff + 8, cnt);
+      if (!(op.flags & XDRG_F_SUB)) {
+        auto rd = [&](uint64_t q) { return ld32(xdr + q); };
+        if (!dec_vector_elems(sops, table, pc + 1, op.arg2, cnt, op.arg1, heap + ecur, p, b,
+                              stack_limit - dbase, r, err, rd, reinterpret_cast<uint32_t *>(nat + op.noff + 12))) {
+          code = kReported;
+          break;
+        }
+        ecur += static_cast<uint64_t>(cnt) * op.arg1;
+        pc += 1 + op.arg2;
+        break;
+      }
+      if (!cnt) { ++pc; break; }
+      // Valid data never overruns the area (distinct elements start at
+      // distinct wire words); a count the record cannot hold may, and
+      // fails here rather than at the element that runs out of bytes.
+      const uint64_t bytes = static_cast<uint64_t>(cnt) * op.arg1;
+      if (bytes > eend - ecur) { code = XDRG_ERR_OVERFLOW_GET; break; }
+      if (fp == kSubFrames) { code = XDRG_ERR_STACK_GET; break; }
+      uint8_t *arr = heap + ecur;
+      for (uint64_t z = 0; z < (bytes & ~3ull); z += 4) st32(arr + z, 0u);
+      for (uint64_t z = bytes & ~3ull; z < bytes; ++z) arr[z] = 0;
+      dbase += op.depth;
+      st[fp++] = sub_frame{ecur, nat + op.noff, cnt - 1, cnt, op.arg1, op.arg4, pc + 1, dbase};
+      eb = ecur;
+      in_heap = true;
+      ecur += bytes;
+      pc = op.arg4;
+      break;
+    }
+    default: ++pc; break;
+    }
+    if (code) break;
+  }
+  if (code) {
+    if (code != kReported) report(err, r, pc, code);
+    for (uint32_t k = 0; k < fp; ++k) st32(st[k].ref + 12, st[k].cnt - 1u - st[k].left);
+    return;
+  }
+  if (p != b) report(err, r, kOpRecordLevel, XDRG_ERR_TRAILING);
+}

@@ -962,6 +962,8 @@ __global__ __launch_bounds__(64) void k_var_decode_w(
                                          stride, heap, stack_limit, C, ebase, F, mark, err);
 }
 
+#include "sub_kernels.h"
+
 // ------------------------------------------- record marks: the index pass
 // The marks of a message stream form a chain (each names the next one's
 // position), so finding the messages is list ranking.  The stream is cut
@@ -1548,8 +1550,15 @@ __global__ __launch_bounds__(256) void k_size_linear(const uint8_t *__restrict__
 }
 
 hipError_t launch_size_pass(const xdrg_plan &p, const dev_tables &T, const uint8_t *nat, uint64_t n,
-                            uint32_t *sizes, unsigned long long *bsum, uint32_t mark,
-                            unsigned long long *err, hipStream_t s) {
+                            const uint8_t *heap, uint64_t heap_len, uint32_t *sizes,
+                            unsigned long long *bsum, uint32_t mark, unsigned long long *err,
+                            hipStream_t s) {
+  if (p.has_sub) {  // containers of variable-size elements: the frame walk
+    k_sub_size<false><<<(n + 255) / 256, 256, p.ops.size() * sizeof(xdrg_op), s>>>(
+        nat, n, p.stride, heap, heap_len, T.d_ops, uint32_t(p.ops.size()), T.d_table, sizes, bsum, mark,
+        err, nullptr);
+    return hipGetLastError();
+  }
   if (p.linear && p.opts.size_linear) {
     lin_args L;
     L.base = p.lin_base;
@@ -1641,7 +1650,7 @@ int var_encode(const xdrg_plan &P, const dev_tables &T, const void *d_native, ui
   uint8_t *xdr8 = static_cast<uint8_t *>(d_xdr);
   const uint32_t nops = uint32_t(p->ops.size());
   // plan-specialized kernels (spec.cpp): straight-line size and encode walks
-  const spec_module *SM = O.specialize && O.enc_kernel == 0 ? spec_get(*p) : nullptr;
+  const spec_module *SM = O.specialize && O.enc_kernel == 0 && !p->has_sub ? spec_get(*p) : nullptr;
   uint32_t MCs = 0, Cs = 0, lds_s = 0;
   if (SM) {
     const uint32_t KS = p->spec.info.slots;
@@ -1659,9 +1668,16 @@ int var_encode(const xdrg_plan &P, const dev_tables &T, const void *d_native, ui
     HIPCHK(hipModuleLaunchKernel(static_cast<hipFunction_t>(SM->f_size), static_cast<uint32_t>(nb), 1, 1,
                                  64, 1, 1, static_cast<uint32_t>(tile), s, args, nullptr));
   } else {
-    HIPCHK(launch_size_pass(*p, T, nat8, n, sizes, bsum, mark, err, s));
+    HIPCHK(launch_size_pass(*p, T, nat8, n, d_heap, heap_len, sizes, bsum, mark, err, s));
   }
   if (int rc = xdrg::launch_block_scan(bsum, bbase, uint32_t(nb), d_status, d_offsets, n, s)) return rc;
+  if (p->has_sub) {
+    k_sub_encode<<<(n + 255) / 256, 256, lds_ops, s>>>(nat8, n, p->stride, d_heap, heap_len, xdr8, cap,
+                                                      d_offsets, sizes, bbase, T.d_ops, nops, T.d_table,
+                                                      stack_limit, mark, err);
+    HIPCHK(hipGetLastError());
+    return XDRG_OK;
+  }
   if (SM) {
     const unsigned long long *bb = bbase;
     uint32_t sl = stack_limit, mc = MCs, cc = Cs, mk = mark;
@@ -1781,6 +1797,14 @@ int var_decode(const xdrg_plan &P, const dev_tables &T, const void *d_xdr, uint6
   int kern = O.dec_kernel;
   if (kern == 2 && !ok_W) kern = 0;
   if (kern == 0) kern = ok_W ? 2 : 1;
+  if (p->has_sub) {  // containers of variable-size elements: the frame walk
+    if (copy && len) HIPCHK(hipMemcpyAsync(d_heap_out, d_xdr, len, hipMemcpyDeviceToDevice, s));
+    k_sub_decode<<<(n + 255) / 256, 256, p->ops.size() * sizeof(xdrg_op), s>>>(
+        xdr8, len, d_offsets, n, nat8, p->stride, T.d_ops, nops, T.d_table, stack_limit, d_heap_out, ebase,
+        p->heap_factor, mark, err);
+    HIPCHK(hipGetLastError());
+    return XDRG_OK;
+  }
   const spec_module *SM = O.specialize && O.dec_kernel == 0 && kern == 2 ? spec_get(*p) : nullptr;
   if (SM) {  // plan-specialized decode walk (spec.cpp)
     const uint64_t nb = (n + 63) / 64;
@@ -2058,13 +2082,20 @@ int xdrg_decode(const xdrg_plan *p, const void *d_xdr, uint64_t len, const uint6
                     d_status, 0u, s);
 }
 
-int xdrg_record_depths(const xdrg_plan *p, const void *d_native, uint64_t n, uint32_t *d_depths,
-                       xdrg_status *d_status, void *stream) {
+int xdrg_record_depths(const xdrg_plan *p, const void *d_native, uint64_t n, const void *d_heap,
+                       uint64_t heap_len, uint32_t *d_depths, xdrg_status *d_status, void *stream) {
   if (!p || !d_status || (n && (!d_native || !d_depths))) return XDRG_EINVAL;
   if (n == 0) return XDRG_OK;
   const dev_tables *T = nullptr;
   if (int rc = plan_upload(p, &T)) return rc;
   hipStream_t s = static_cast<hipStream_t>(stream);
+  if (p->has_sub) {
+    k_sub_size<true><<<(n + 255) / 256, 256, p->ops.size() * sizeof(xdrg_op), s>>>(
+        static_cast<const uint8_t *>(d_native), n, p->stride, static_cast<const uint8_t *>(d_heap), heap_len,
+        T->d_ops, uint32_t(p->ops.size()), T->d_table, nullptr, nullptr, 0u, err_ptr(d_status), d_depths);
+    HIPCHK(hipGetLastError());
+    return XDRG_OK;
+  }
   if (p->path != XDRG_PATH_VAR || p->linear) {  // every record walks every op
     HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_depths), int(p->max_depth), n, s));
     return XDRG_OK;
@@ -2083,8 +2114,9 @@ int xdrg_record_depths(const xdrg_plan *p, const void *d_native, uint64_t n, uin
   return XDRG_OK;
 }
 
-int xdrg_serial_sizes(const xdrg_plan *p, const void *d_native, uint64_t n, uint32_t *d_sizes,
-                      uint32_t stack_limit, xdrg_status *d_status, void *stream) {
+int xdrg_serial_sizes(const xdrg_plan *p, const void *d_native, uint64_t n, const void *d_heap,
+                      uint64_t heap_len, uint32_t *d_sizes, uint32_t stack_limit, xdrg_status *d_status,
+                      void *stream) {
   (void)stack_limit;
   if (!p || !d_status || (n && (!d_native || !d_sizes))) return XDRG_EINVAL;
   if (n == 0) return XDRG_OK;
@@ -2096,7 +2128,8 @@ int xdrg_serial_sizes(const xdrg_plan *p, const void *d_native, uint64_t n, uint
     HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_sizes), int(p->fixed_size), n, s));
     return XDRG_OK;
   }
-  HIPCHK(launch_size_pass(*p, *T, static_cast<const uint8_t *>(d_native), n, d_sizes, nullptr, 0u,
+  HIPCHK(launch_size_pass(*p, *T, static_cast<const uint8_t *>(d_native), n,
+                          static_cast<const uint8_t *>(d_heap), heap_len, d_sizes, nullptr, 0u,
                           err_ptr(d_status), s));
   return XDRG_OK;
 }

@@ -215,31 +215,33 @@ class Marshaler:
         return e
 
     # ---- reference-shaped API --------------------------------------------
-    def serial_sizes(self, native, n, stack_limit=A.DEFAULT_STACK_LIMIT) -> torch.Tensor:
+    def serial_sizes(self, native, n, stack_limit=A.DEFAULT_STACK_LIMIT, heap=None) -> torch.Tensor:
         """xdr_size of every record (xdrpp/types.h:240-244)."""
         sizes = torch.empty(max(n, 1), dtype=torch.int32, device=self.device)
         s = _stream()
         self.status.init(s)
-        A.check(A.lib().xdrg_serial_sizes(self.plan.handle, _ptr(native), n, _ptr(sizes),
+        A.check(A.lib().xdrg_serial_sizes(self.plan.handle, _ptr(native), n, _ptr(heap),
+                                          0 if heap is None else heap.numel(), _ptr(sizes),
                                           stack_limit, self.status.ptr, s), "xdrg_serial_sizes")
         self.check(s)
         return sizes[:n]
 
-    def record_depths(self, native, n) -> torch.Tensor:
+    def record_depths(self, native, n, heap=None) -> torch.Tensor:
         """Deepest class/container level of every record's walk
         (depth_checker, xdrpp/depth_checker.h:10-79); int32 [n]."""
         d = torch.empty(max(n, 1), dtype=torch.int32, device=self.device)
         s = _stream()
         self.status.init(s)
-        A.check(A.lib().xdrg_record_depths(self.plan.handle, _ptr(native), n, _ptr(d),
+        A.check(A.lib().xdrg_record_depths(self.plan.handle, _ptr(native), n, _ptr(heap),
+                                           0 if heap is None else heap.numel(), _ptr(d),
                                            self.status.ptr, s), "xdrg_record_depths")
         self.check(s)
         return d[:n]
 
-    def check_xdr_depth(self, native, n, depth_limit: int) -> torch.Tensor:
+    def check_xdr_depth(self, native, n, depth_limit: int, heap=None) -> torch.Tensor:
         """xdr::check_xdr_depth(r_i, depth_limit) for every record
         (xdrpp/depth_checker.h:72-79): bool [n]."""
-        return self.record_depths(native, n) <= depth_limit
+        return self.record_depths(native, n, heap) <= depth_limit
 
     def encode(self, native: torch.Tensor, n: int, heap: torch.Tensor | None = None,
                stack_limit: int = A.DEFAULT_STACK_LIMIT, capacity: int | None = None) -> EncodeResult:
@@ -253,7 +255,7 @@ class Marshaler:
             self.check(s)
             return EncodeResult(out, None)
         if capacity is None:
-            capacity = int(self.serial_sizes(native, n, stack_limit).to(torch.int64).sum().item())
+            capacity = int(self.serial_sizes(native, n, stack_limit, heap).to(torch.int64).sum().item())
         out = torch.empty(max(capacity, 4), dtype=torch.uint8, device=self.device)
         offsets = torch.empty(n + 1, dtype=torch.int64, device=self.device)
         self.status.init(s)
@@ -281,9 +283,9 @@ class Marshaler:
 
 
     # ---- record-marked messages (message_t, RFC 5531) -----------------------
-    def message_sizes(self, native, n, stack_limit=A.DEFAULT_STACK_LIMIT) -> torch.Tensor:
+    def message_sizes(self, native, n, stack_limit=A.DEFAULT_STACK_LIMIT, heap=None) -> torch.Tensor:
         """raw_size() of xdr_to_msg(r) per record: 4 + xdr_size(r)."""
-        return self.serial_sizes(native, n, stack_limit) + 4
+        return self.serial_sizes(native, n, stack_limit, heap) + 4
 
     def encode_msgs(self, native: torch.Tensor, n: int, heap: torch.Tensor | None = None,
                     stack_limit: int = A.DEFAULT_STACK_LIMIT,
@@ -296,7 +298,7 @@ class Marshaler:
             if self.plan.is_fixed:
                 capacity = n * (self.plan.fixed_size + 4)
             else:
-                capacity = int(self.serial_sizes(native, n, stack_limit).to(torch.int64).sum().item()) + 4 * n
+                capacity = int(self.serial_sizes(native, n, stack_limit, heap).to(torch.int64).sum().item()) + 4 * n
         out = torch.empty(max(capacity, 4), dtype=torch.uint8, device=self.device)
         offsets = torch.empty(n + 1, dtype=torch.int64, device=self.device)
         self.status.init(s)

@@ -6,6 +6,9 @@
   recvar    SURVEY.md §8(d) config 3: unsigned hyper id; int kind;
             opaque blob<256>; string name<64>; double score
   rpc_msg   xdrpp/rpc_msg.x:5-140 (nested discriminated unions)
+  containers of variable-size elements and a recursive type, from
+  tests/xdrtest.x: containertest, containertest1 (:129-137), hasbytes
+  (:94-96), test_recursive (:29-33), nested_cereal_adapter_calls (:172-176)
 
 The union/type names match what xdrc generates, so bad-discriminant
 messages equal the reference's ("bad value of mtype in _body_t", ...).
@@ -13,7 +16,7 @@ messages equal the reference's ("bad value of mtype in _body_t", ...).
 from __future__ import annotations
 
 from .xdr_types import (Bool, Double, Enum, Float, Hyper, Int, Opaque, OpaqueArray, Pointer, String,
-                        Struct, UHyper, UInt, Union, Void, XVector)
+                        Struct, UHyper, UInt, Union, Void, XArray, XVector)
 
 # ------------------------------------------------------------- numerics
 _COLOR_TAGS = {"RED": 0, "REDDER": 1, "REDDEST": 2}
@@ -85,5 +88,22 @@ rpc_msg = Struct("rpc_msg", [("xid", UInt), ("body", rpc_body)])
 vpair = Struct("vpair", [("h", Hyper), ("b", Bool)])
 vecrec = Struct("vecrec", [("id", UInt), ("vals", XVector(Int, 16)), ("opt", Pointer(mismatch_info)),
                            ("pairs", XVector(vpair, 8)), ("flag", Bool)])
+
+# --------------------------------------- tests/xdrtest.x: element subroutines
+fix_4 = Struct("fix_4", [("i", Int)])
+fix_12 = Struct("fix_12", [("i", Int), ("d", Double)])
+u_4_12 = Union("u_4_12", "which", Int, [([4], "f4", fix_4), ([12], "f12", fix_12)])
+containertest = Struct("containertest", [("uvec", XVector(u_4_12)), ("sarr", XArray(String(), 2))])
+containertest1 = Struct("containertest1", [("uvec", XVector(u_4_12, 2)), ("sarr", XArray(String(), 2))])
+xbytes = Struct("bytes", [("s", String(16)), ("fixed", OpaqueArray(16)), ("variable", Opaque(16))])
+hasbytes = Struct("hasbytes", [("the_bytes", XVector(xbytes))])
+test_recursive = Struct("test_recursive")
+test_recursive.define([("elem", String()), ("next", Pointer(test_recursive)),
+                       ("nextvec", XVector(test_recursive))])
+string32 = String(32)  # typedef string string32<32>: one element subroutine for both containers
+nested_cereal_adapter_calls = Struct("nested_cereal_adapter_calls", [
+    ("strptr", Pointer(string32)), ("strvec", XVector(string32)), ("strarr", XArray(string32, 2))])
+CONTAINERS = {"containertest": containertest, "containertest1": containertest1, "hasbytes": hasbytes,
+              "test_recursive": test_recursive, "nested_cereal_adapter_calls": nested_cereal_adapter_calls}
 
 ALL = {"numerics": numerics, "rec128": rec128, "recvar": recvar, "rpc": rpc_msg, "vecrec": vecrec}

@@ -20,10 +20,18 @@ Each descriptor knows
 | Opaque(max)       | opaque_vec<N>    (opaque x<N>)         | types.h:515-524        |
 | String(max)       | xstring<N>       (string x<N>)         | types.h:530-587        |
 | XArray(t, n)      | xarray<T,N>      (T x[N])              | types.h:424-452        |
-| XVector(t, max)   | xvector<T,N>     (T x<N>), T fixed     | types.h:365-414,476-512|
-| Pointer(t)        | pointer<T>       (T *x), T fixed       | types.h:591-665        |
+| XVector(t, max)   | xvector<T,N>     (T x<N>)              | types.h:365-414,476-512|
+| Pointer(t)        | pointer<T>       (T *x)                | types.h:591-665        |
 | Struct            | xdrc struct + xdr_struct_base          | types.h:676-730, gen_hh.cc:212-250 |
 | Union             | xdrc union                             | gen_hh.cc:368-675      |
+
+Containers of fixed-size elements put the element's ops inline after the
+VECTOR op; containers of any other element type (strings, structs with
+bytes fields, unions, containers, the enclosing type itself) give the
+element a subroutine (XDRG_F_SUB): its ops follow the record's END, emitted
+once per element type.  A recursive type is declared first and given its
+fields afterwards (``Struct(name)`` then ``.define(fields)``), as the
+reference's test_recursive (tests/xdrtest.x:29-33) refers to itself.
 """
 from __future__ import annotations
 
@@ -57,6 +65,29 @@ class _Ctx:
         self.table: list[int] = []
         self.names: list[str] = []      # name id -> dotted field path
         self.messages: dict[int, str] = {}  # op index -> bad-discriminant what()
+        self.subs: dict[int, list] = {}     # id(element type) -> [type, path, entry pc, VECTOR ops]
+        self.pending: list[int] = []        # element types whose bodies are still to emit
+
+    def sub(self, t: "XdrType", path: str, vec_op: int) -> None:
+        """VECTOR op `vec_op` walks elements of `t` through t's subroutine."""
+        e = self.subs.get(id(t))
+        if e is None:
+            e = self.subs[id(t)] = [t, path, None, []]
+            self.pending.append(id(t))
+        e[3].append(vec_op)
+
+    def emit_subs(self) -> None:
+        """Element subroutines after the record's END, each ending with END;
+        a body may enter further (or its own) subroutines."""
+        while self.pending:
+            e = self.subs[self.pending.pop(0)]
+            t, path = e[0], e[1]
+            e[2] = len(self.ops)
+            t.emit(self, 0, 0, path)  # element-relative offsets and depths
+            self.emit(A.OP_END, 0, 0, "<end>")
+        for t, _, entry, vecs in self.subs.values():
+            for v in vecs:
+                self.ops[v][8] = entry  # arg4
 
     def name(self, path: str) -> int:
         self.names.append(path)
@@ -173,25 +204,31 @@ class XArray(XdrType):
 
 
 class XVector(XdrType):
-    """T x<N> for non-byte, fixed-size T (xvector<T,N>): a container level,
-    then a u32 count and the elements.  Staged as xdrg_bytes_ref {heap
-    offset, count} of an element array (stride = T's aligned size).  The
-    element's ops follow the VECTOR op inline (arg2 of them)."""
+    """T x<N> for non-byte T (xvector<T,N>): a container level, then a u32
+    count and the elements.  Staged as xdrg_bytes_ref {heap offset, count}
+    of an element array (stride = T's aligned size).  Fixed-size T: the
+    element's ops follow the VECTOR op inline (arg2 of them); any other T:
+    the element's subroutine (XDRG_F_SUB, arg4 = its pc)."""
 
     size, align = 16, 8
     fixed_wire = None
     pointer = False
 
     def __init__(self, elem: XdrType, max_len: int = A.XDR_MAX_LEN):
-        if elem.fixed_wire is None:
-            raise NotImplementedError("xvector<T>/pointer<T> of variable-size T")
         self.elem, self.max_len = elem, max_len
-        self.stride = _align_up(elem.size, elem.align)
+
+    @property
+    def stride(self) -> int:  # read late: the element may be a type still being defined
+        return _align_up(self.elem.size, self.elem.align)
 
     def emit(self, ctx, noff, depth, path):
         d = depth + 1  # container level (marshal.h:129-136)
-        upc = ctx.emit(A.OP_VECTOR, noff, d, path, A.F_POINTER if self.pointer else 0,
-                       self.max_len, self.stride)
+        flags = A.F_POINTER if self.pointer else 0
+        if self.elem.fixed_wire is None:
+            upc = ctx.emit(A.OP_VECTOR, noff, d, path, flags | A.F_SUB, self.max_len, self.stride)
+            ctx.sub(self.elem, f"{path}[]", upc)
+            return
+        upc = ctx.emit(A.OP_VECTOR, noff, d, path, flags, self.max_len, self.stride)
         start = len(ctx.ops)
         self.elem.emit(ctx, 0, d, f"{path}[]")  # element-relative offsets
         ctx.ops[upc][6] = len(ctx.ops) - start  # arg2 = number of element ops
@@ -209,8 +246,17 @@ class Pointer(XVector):
 class Struct(XdrType):
     is_class = True
 
-    def __init__(self, name: str, fields: list):
+    def __init__(self, name: str, fields: list | None = None):
         self.name = name
+        self.fields = []
+        self.size, self.align, self.fixed_wire, self.offsets = 0, 1, None, {}
+        if fields is not None:
+            self.define(fields)
+
+    def define(self, fields: list) -> "Struct":
+        """Give a declared struct its fields (a recursive type refers to
+        itself through a container, whose staged size does not depend on
+        the element's)."""
         self.fields = list(fields)
         off, al = 0, 1
         self.offsets = {}
@@ -223,6 +269,7 @@ class Struct(XdrType):
         self.size = _align_up(max(off, 1), al) if self.fields else 1
         fw = [ft.fixed_wire for _, ft in self.fields]
         self.fixed_wire = None if any(w is None for w in fw) else sum(fw)
+        return self
 
     def emit(self, ctx, noff, depth, path):
         d = depth + 1  # xdr_generic_put/get operator() on a class, marshal.h:129-136
@@ -363,11 +410,13 @@ def compile_plan(root: XdrType) -> CompiledPlan:
     """Flatten ``root`` (normally a Struct or Union) into plan ops."""
     ctx = _Ctx()
     if isinstance(root, (Struct, Union)):
+        ctx.subs[id(root)] = [root, "", 0, []]  # the record's own ops serve as its subroutine
         root.emit(ctx, 0, 0, "")
     else:
         # a bare scalar/bytes record: one field, no class level
         root.emit(ctx, 0, 0, "value")
     ctx.emit(A.OP_END, 0, 0, "<end>")
+    ctx.emit_subs()
     ops = np.zeros(len(ctx.ops), dtype=OP_DTYPE)
     for i, o in enumerate(ctx.ops):
         ops[i] = tuple(o)
