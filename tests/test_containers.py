@@ -165,7 +165,7 @@ def test_fixture_regenerates(tmp_path):
 # ------------------------------------------------------------------ GPU
 def _dev(a, dev):
     import torch
-    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    return torch.from_numpy(np.array(a)).to(dev)
 
 
 @pytest.mark.gpu
