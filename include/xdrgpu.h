@@ -129,7 +129,9 @@ enum xdrg_op_flags {
  * XDRG_SUB_FRAMES nested element subroutines per record; data nested
  * deeper raises the stack-overflow error at the VECTOR op that would
  * enter the next one (bounded recursion: what marshaling_stack_limit,
- * marshal.h:21, guards the reference's call stack against).
+ * marshal.h:21, guards the reference's call stack against).  A decode that
+ * fails inside elements leaves rsv = 1 + the failing element's index in
+ * every container on the way to the failure (0 in the others).
  */
 #define XDRG_SUB_FRAMES 32
 typedef struct xdrg_op {

@@ -29,6 +29,13 @@
 // fixed-size, trivially copyable types whose C++ layout already IS that
 // layout (e.g. structs of ints/hypers/doubles) records are passed as-is;
 // other types are staged/unstaged on the host by plan-following archives.
+//
+// Containers of variable-size elements (xvector<T>/pointer<T> of strings,
+// structs with bytes fields, unions, containers -- and recursive types such
+// as tests/xdrtest.x's test_recursive) give the element a subroutine
+// (XDRG_F_SUB): its ops are recorded once per element type and placed after
+// the record's END; a type still being recorded is referenced by key and
+// patched when the plan is assembled.
 #ifndef XDRPP_GPU_HH_INCLUDED
 #define XDRPP_GPU_HH_INCLUDED 1
 
@@ -46,6 +53,7 @@
 #include <string>
 #include <tuple>
 #include <type_traits>
+#include <typeindex>
 #include <utility>
 #include <vector>
 
@@ -200,6 +208,46 @@ inline void append(subplan &dst, const subplan &src, std::uint32_t base, std::ui
 
 template <typename T> subplan record_type();
 
+// Element subroutines of the plan being assembled (batch_plan): one body
+// per element type.  `busy` holds the struct/union types whose recording is
+// on the stack: an element of such a type (a recursive type) is known to be
+// variable-size and is referenced before its body exists.  F_SUB VECTOR ops
+// carry the body's key in arg4 until the plan is assembled.
+struct sub_registry {
+  std::vector<std::type_index> types;
+  std::vector<subplan> bodies;
+  std::vector<std::type_index> busy;
+};
+inline sub_registry *&active_subs() {
+  static thread_local sub_registry *r = nullptr;
+  return r;
+}
+struct busy_guard {
+  explicit busy_guard(std::type_index t) {
+    if (active_subs()) active_subs()->busy.push_back(t);
+  }
+  ~busy_guard() {
+    if (active_subs()) active_subs()->busy.pop_back();
+  }
+};
+template <typename E> bool recording() {
+  const sub_registry *R = active_subs();
+  return R && std::find(R->busy.begin(), R->busy.end(), std::type_index(typeid(E))) != R->busy.end();
+}
+template <typename E> std::uint32_t sub_key() {
+  sub_registry *R = active_subs();
+  if (!R) throw std::logic_error("xdr::gpu: element subroutines are recorded by plan_for<T>()");
+  const std::type_index t(typeid(E));
+  for (std::size_t k = 0; k < R->types.size(); ++k)
+    if (R->types[k] == t) return static_cast<std::uint32_t>(k);
+  const std::uint32_t k = static_cast<std::uint32_t>(R->types.size());
+  R->types.push_back(t);  // before recording: the body may refer to itself
+  R->bodies.emplace_back();
+  subplan b = record_type<E>();
+  R->bodies[k] = std::move(b);
+  return k;
+}
+
 // Walks xdr_traits<S>::save on a prototype: each archived field is placed
 // at its natural alignment (the C++ rule xdrc structs follow).
 struct struct_recorder {
@@ -263,6 +311,7 @@ std::vector<std::int64_t> union_cases<U, E>::values() {
 namespace detail {
 
 template <typename U> subplan record_union() {
+  const busy_guard busy{std::type_index(typeid(U))};
   // candidate discriminants: union_cases<U>, else the discriminant enum's tags
   std::vector<std::int64_t> cand = union_cases<U>::values();
   const bool has_default = union_cases<U>::has_default;
@@ -416,18 +465,24 @@ template <typename T> subplan record_type() {
     sp.align = alignof(T);
   } else if constexpr (vector_info<T>::value) {
     using E = typename vector_info<T>::elem;
-    const subplan e = record_type<E>();
-    if (!e.fixed) throw std::logic_error("xdr::gpu: xvector<T>/pointer<T> of variable-size T is not supported");
-    xdrg_op v = mkop(XDRG_OP_VECTOR, 0, 1, vector_info<T>::max, align_up(e.size, e.align),
-                     vector_info<T>::pointer ? XDRG_F_POINTER : 0);
-    v.arg2 = static_cast<std::uint32_t>(e.ops.size());
-    sp.ops.push_back(v);
-    append(sp, e, 0, 1);  // elements inside the container level
+    const std::uint8_t fl = vector_info<T>::pointer ? XDRG_F_POINTER : 0;
     sp.size = sizeof(xdrg_bytes_ref);
     sp.align = alignof(xdrg_bytes_ref);
     sp.identity = false;
     sp.fixed = false;
-    sp.validates = e.validates;
+    subplan e;
+    const bool inline_elems = !recording<E>() && (e = record_type<E>()).fixed;
+    if (inline_elems) {  // fixed-size elements: ops inline after the VECTOR op
+      xdrg_op v = mkop(XDRG_OP_VECTOR, 0, 1, vector_info<T>::max, align_up(e.size, e.align), fl);
+      v.arg2 = static_cast<std::uint32_t>(e.ops.size());
+      sp.ops.push_back(v);
+      append(sp, e, 0, 1);  // elements inside the container level
+      sp.validates = e.validates;
+    } else {  // the element's subroutine; stride and body pc set by batch_plan
+      xdrg_op v = mkop(XDRG_OP_VECTOR, 0, 1, vector_info<T>::max, 0, fl | XDRG_F_SUB);
+      v.arg4 = sub_key<E>();
+      sp.ops.push_back(v);
+    }
   } else if constexpr (xarray_info<T>::value) {
     using E = typename xarray_info<T>::elem;
     const subplan e = record_type<E>();
@@ -441,6 +496,7 @@ template <typename T> subplan record_type() {
   } else if constexpr (TR::is_union) {
     sp = record_union<T>();
   } else if constexpr (TR::is_struct || TR::is_class) {
+    const busy_guard busy{std::type_index(typeid(T))};
     static const T proto{};
     struct_recorder r{&sp, reinterpret_cast<const char *>(&proto)};
     TR::save(r, proto);
@@ -475,31 +531,35 @@ struct cursor {
 };
 
 struct stager : cursor {
-  std::uint8_t *rec;
+  std::uint8_t *rec = nullptr;  // the record, or (in_heap) heap offset `roff`
   std::vector<std::uint8_t> *heap;
+  bool in_heap = false;
+  std::uint64_t roff = 0;
+  // the object's bytes, looked up at every write: staging elements grows the heap
+  std::uint8_t *R() const { return in_heap ? heap->data() + roff : rec; }
   template <typename F> void operator()(const F &f) {
     using P = plain<F>;
     using TR = xdr_traits<P>;
     if constexpr (std::is_same_v<P, bool>) {
-      rec[next().noff] = f ? 1 : 0;
+      R()[next().noff] = f ? 1 : 0;
       ++pc;
     } else if constexpr (bytes_kind<P>::kind == XDRG_OP_OPAQUE) {
-      std::memcpy(rec + next().noff, f.data(), f.size());
+      std::memcpy(R() + next().noff, f.data(), f.size());
       ++pc;
     } else if constexpr (bytes_kind<P>::kind != 0) {
       xdrg_bytes_ref r{heap->size(), static_cast<std::uint32_t>(f.size()), 0};
       heap->insert(heap->end(), reinterpret_cast<const std::uint8_t *>(f.data()),
                    reinterpret_cast<const std::uint8_t *>(f.data()) + f.size());
-      std::memcpy(rec + next().noff, &r, sizeof r);
+      std::memcpy(R() + next().noff, &r, sizeof r);
       ++pc;
     } else if constexpr (TR::is_enum || TR::is_numeric) {
       const xdrg_op &o = next();
       if (o.kind == XDRG_OP_UNION) {
         const std::int32_t d = static_cast<std::int32_t>(f);
-        std::memcpy(rec + o.noff, &d, 4);
+        std::memcpy(R() + o.noff, &d, 4);
         branch(o, d);
       } else {
-        std::memcpy(rec + o.noff, &f, sizeof(P));
+        std::memcpy(R() + o.noff, &f, sizeof(P));
         ++pc;
       }
     } else if constexpr (vector_info<P>::value) {
@@ -508,18 +568,20 @@ struct stager : cursor {
       heap->resize((heap->size() + 7) & ~std::size_t(7), 0);
       const std::uint64_t off = heap->size();
       heap->resize(off + std::uint64_t(cnt) * o.arg1, 0);
+      const std::uint32_t entry = (o.flags & XDRG_F_SUB) ? o.arg4 : pc + 1;
       std::uint32_t i = 0;
-      for (const auto &e : f) {  // fixed-size elements: staging them never grows the heap
+      for (const auto &e : f) {
         stager s2;
         s2.ops = ops;
         s2.table = table;
-        s2.pc = pc + 1;
-        s2.rec = heap->data() + off + std::uint64_t(i++) * o.arg1;
+        s2.pc = entry;
         s2.heap = heap;
+        s2.in_heap = true;
+        s2.roff = off + std::uint64_t(i++) * o.arg1;
         s2(e);
       }
       const xdrg_bytes_ref r{off, cnt, 0};
-      std::memcpy(rec + o.noff, &r, sizeof r);
+      std::memcpy(R() + o.noff, &r, sizeof r);
       pc += 1 + o.arg2;
     } else if constexpr (xarray_info<P>::value) {
       for (const auto &e : f) (*this)(e);
@@ -539,12 +601,43 @@ constexpr std::uint32_t kNoStop = 0xffffffffu;
 // With `stop` set, the walk throws stop_reached on reaching that op: the
 // hooks of everything decoded before it have run, as they would have in
 // xdr_generic_get before the failing field.
+// Does the failure of a decoded object (walked from pc) lie inside one of
+// its element subroutines?  Those containers carry rsv = 1 + the failing
+// element (xdrgpu.h); the walk follows the object's own discriminants.
+inline bool failure_deeper(const xdrg_op *ops, const std::uint32_t *table, const std::uint8_t *rec,
+                           std::uint32_t pc) {
+  for (;;) {
+    const xdrg_op &o = ops[pc];
+    switch (o.kind) {
+    case XDRG_OP_END: return false;
+    case XDRG_OP_JUMP: pc = o.arg0; break;
+    case XDRG_OP_UNION: {
+      std::int32_t d;
+      std::memcpy(&d, rec + o.noff, 4);
+      cursor c{ops, table, pc};
+      try { c.branch(o, d); } catch (const xdr_bad_discriminant &) { return false; }
+      pc = c.pc;
+      break;
+    }
+    case XDRG_OP_VECTOR: {
+      xdrg_bytes_ref r;
+      std::memcpy(&r, rec + o.noff, sizeof r);
+      if ((o.flags & XDRG_F_SUB) && r.rsv) return true;
+      pc += 1 + o.arg2;
+      break;
+    }
+    default: ++pc; break;
+    }
+  }
+}
+
 struct unstager : cursor {
   const std::uint8_t *rec;
   const std::uint8_t *heap;
   std::uint32_t stop = kNoStop;
+  bool here = true;  // the stop op is in this object's own walk, not in an element's
   void at_op() const {
-    if (pc == stop) throw stop_reached{};
+    if (pc == stop && here) throw stop_reached{};
   }
   template <typename F> void operator()(F &f) {
     using P = plain<F>;
@@ -577,9 +670,15 @@ struct unstager : cursor {
       at_op();
       xdrg_bytes_ref r;
       std::memcpy(&r, rec + o.noff, sizeof r);
-      // a decode that failed inside element r.rsv decoded the ones before it
-      const bool inside = stop != kNoStop && stop > pc && stop <= pc + o.arg2;
-      const std::uint32_t whole = inside ? std::min(r.rsv, r.len) : r.len;
+      // A decode that failed inside an element decoded the ones before it:
+      // inline (fixed) elements when the failing op is one of theirs
+      // (rsv = the failing element), subroutine elements on the marked
+      // path (rsv = 1 + the failing element).
+      const bool sub = (o.flags & XDRG_F_SUB) != 0;
+      const bool inside = stop != kNoStop &&
+                          (sub ? r.rsv != 0 : here && stop > pc && stop <= pc + o.arg2);
+      const std::uint32_t whole = !inside ? r.len : std::min(sub ? r.rsv - 1 : r.rsv, r.len);
+      const std::uint32_t entry = sub ? o.arg4 : pc + 1;
       if constexpr (vector_info<P>::pointer) {
         if (r.len) f.activate(); else f.reset();
       } else {
@@ -591,10 +690,13 @@ struct unstager : cursor {
         unstager u2;
         u2.ops = ops;
         u2.table = table;
-        u2.pc = pc + 1;
+        u2.pc = entry;
         u2.rec = heap + r.off + std::uint64_t(i) * o.arg1;
         u2.heap = heap;
-        if (i == whole) u2.stop = stop;
+        if (i == whole) {
+          u2.stop = stop;
+          u2.here = !sub || !failure_deeper(ops, table, u2.rec, entry);
+        }
         u2(e);
         ++i;
       }
@@ -674,17 +776,60 @@ template <typename T> class batch_plan {
  private:
   struct deleter { void operator()(xdrg_plan *p) const { xdrg_plan_destroy(p); } };
   batch_plan() {
-    detail::subplan sp = detail::record_type<T>();
+    // the record's ops, END, then one element subroutine per element type
+    // (each ending with END); F_SUB VECTOR ops get the body's stride and pc
+    detail::sub_registry subs;
+    subs.types.push_back(std::type_index(typeid(T)));  // key 0: the record's own ops (pc 0)
+    subs.bodies.emplace_back();
+    detail::sub_registry *outer = detail::active_subs();
+    detail::active_subs() = &subs;
+    detail::subplan sp;
+    try {
+      sp = detail::record_type<T>();
+    } catch (...) {
+      detail::active_subs() = outer;
+      throw;
+    }
+    detail::active_subs() = outer;
+    subs.bodies[0] = sp;
     detail::subplan top;
     detail::append(top, sp, 0, 0);
     top.ops.push_back(detail::mkop(XDRG_OP_END, 0, 0));
+    // bodies in order of first reference, breadth first from the record
+    // (the order xdrpp_amd/xdr_types.py emits them in)
+    const std::size_t nk = subs.bodies.size();
+    std::vector<std::uint32_t> entry(nk, 0xffffffffu), order;
+    entry[0] = 0;
+    auto refs = [&](const detail::subplan &b) {
+      for (const xdrg_op &o : b.ops)
+        if (o.kind == XDRG_OP_VECTOR && (o.flags & XDRG_F_SUB) && entry[o.arg4] == 0xffffffffu) {
+          entry[o.arg4] = 0;  // queued
+          order.push_back(o.arg4);
+        }
+    };
+    refs(sp);
+    bool validates = sp.validates;
+    for (std::size_t q = 0; q < order.size(); ++q) {
+      const std::uint32_t k = order[q];
+      entry[k] = static_cast<std::uint32_t>(top.ops.size());
+      detail::append(top, subs.bodies[k], 0, 0);
+      top.ops.push_back(detail::mkop(XDRG_OP_END, 0, 0));
+      validates = validates || subs.bodies[k].validates;
+      refs(subs.bodies[k]);
+    }
+    for (xdrg_op &o : top.ops)
+      if (o.kind == XDRG_OP_VECTOR && (o.flags & XDRG_F_SUB)) {
+        const detail::subplan &b = subs.bodies[o.arg4];
+        o.arg1 = detail::align_up(std::max<std::uint32_t>(b.size, 1), b.align);
+        o.arg4 = entry[o.arg4];
+      }
     ops_ = std::move(top.ops);
     table_ = std::move(top.table);
     msgs_ = std::move(top.msgs);
     stride_ = detail::align_up(std::max<std::uint32_t>(sp.size, 1), std::max<std::uint32_t>(sp.align, 4));
     identity_ = sp.identity && sp.fixed && sizeof(T) == stride_;
     fixed_ = sp.fixed;
-    validates_ = sp.validates;
+    validates_ = validates;
     xdrg_plan *h = nullptr;
     detail::abicheck(xdrg_plan_create(ops_.data(), static_cast<std::uint32_t>(ops_.size()),
                                       table_.empty() ? nullptr : table_.data(),
@@ -774,6 +919,7 @@ void unstage_checked(const std::uint8_t *native, const std::uint8_t *heap, std::
       u.rec = native + bad * P.stride();
       u.heap = heap;
       u.stop = e.op;
+      u.here = !detail::failure_deeper(u.ops, u.table, u.rec, 0);
       try {
         u(out[bad]);
       } catch (const detail::stop_reached &) {
@@ -787,52 +933,68 @@ void unstage_checked(const std::uint8_t *native, const std::uint8_t *heap, std::
 //! discriminants only).  Records that would overrun `len` or carry a bad
 //! discriminant end the walk; the remaining offsets are `len`, and the
 //! device decode then reports the reference's error for that record.
+namespace detail {
+// Step p over one object's wire bytes (the walk from pc to its END): false
+// when the bytes run out, a discriminant is bad, or elements nest deeper
+// than the device walks them.
+inline bool skip_object(const xdrg_op *ops, const std::uint32_t *tab, const std::uint8_t *xdr,
+                        std::size_t len, std::uint64_t &p, std::uint32_t pc, std::uint32_t frames) {
+  for (;;) {
+    const xdrg_op &o = ops[pc];
+    switch (o.kind) {
+    case XDRG_OP_END: return true;
+    case XDRG_OP_JUMP: pc = o.arg0; continue;
+    case XDRG_OP_U64: p += 8; break;
+    case XDRG_OP_OPAQUE: p += align_up(o.arg0, 4); break;
+    case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING:
+      if (p + 4 > len) return false;
+      p += 4 + ((std::uint64_t(be32(xdr + p)) + 3) & ~3ull);
+      break;
+    case XDRG_OP_VECTOR: {
+      if (p + 4 > len) return false;
+      const std::uint32_t cnt = be32(xdr + p);
+      p += 4;
+      if (o.flags & XDRG_F_SUB) {
+        if (cnt && frames == XDRG_SUB_FRAMES) return false;
+        for (std::uint32_t i = 0; i < cnt; ++i)
+          if (p > len || !skip_object(ops, tab, xdr, len, p, o.arg4, frames + 1)) return false;
+        ++pc;
+        continue;
+      }
+      std::uint64_t we = 0;
+      for (std::uint32_t k = 1; k <= o.arg2; ++k) {
+        const xdrg_op &e = ops[pc + k];
+        we += e.kind == XDRG_OP_U64 ? 8u : e.kind == XDRG_OP_OPAQUE ? align_up(e.arg0, 4) : 4u;
+      }
+      p += cnt * we;
+      pc += 1 + o.arg2;
+      continue;
+    }
+    case XDRG_OP_UNION: {
+      if (p + 4 > len) return false;
+      const std::int32_t d = static_cast<std::int32_t>(be32(xdr + p));
+      p += 4;
+      cursor c{ops, tab, pc};
+      try { c.branch(o, d); } catch (const xdr_bad_discriminant &) { return false; }
+      pc = c.pc;
+      continue;
+    }
+    default: p += 4; break;
+    }
+    ++pc;
+  }
+}
+}  // namespace detail
+
 template <typename T>
 std::vector<std::uint64_t> index_records(const std::uint8_t *xdr, std::size_t len, std::size_t n) {
   const batch_plan<T> &P = plan_for<T>();
   std::vector<std::uint64_t> off(n + 1, len);
   std::uint64_t p = 0;
-  const xdrg_op *ops = P.ops().data();
-  const std::uint32_t *tab = P.table().data();
   for (std::size_t r = 0; r < n; ++r) {
     off[r] = std::min<std::uint64_t>(p, len);
-    std::uint32_t pc = 0;
-    bool bad = false;
-    while (!bad && ops[pc].kind != XDRG_OP_END) {
-      const xdrg_op &o = ops[pc];
-      switch (o.kind) {
-      case XDRG_OP_JUMP: pc = o.arg0; continue;
-      case XDRG_OP_U64: p += 8; break;
-      case XDRG_OP_OPAQUE: p += detail::align_up(o.arg0, 4); break;
-      case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING:
-        if (p + 4 > len) { bad = true; break; }
-        p += 4 + ((std::uint64_t(detail::be32(xdr + p)) + 3) & ~3ull);
-        break;
-      case XDRG_OP_VECTOR: {
-        if (p + 4 > len) { bad = true; break; }
-        std::uint64_t we = 0;
-        for (std::uint32_t k = 1; k <= o.arg2; ++k) {
-          const xdrg_op &e = ops[pc + k];
-          we += e.kind == XDRG_OP_U64 ? 8u : e.kind == XDRG_OP_OPAQUE ? detail::align_up(e.arg0, 4) : 4u;
-        }
-        p += 4 + detail::be32(xdr + p) * we;
-        pc += 1 + o.arg2;
-        continue;
-      }
-      case XDRG_OP_UNION: {
-        if (p + 4 > len) { bad = true; break; }
-        const std::int32_t d = static_cast<std::int32_t>(detail::be32(xdr + p));
-        p += 4;
-        detail::cursor c{ops, tab, pc};
-        try { c.branch(o, d); } catch (const xdr_bad_discriminant &) { bad = true; break; }
-        pc = c.pc;
-        continue;
-      }
-      default: p += 4; break;
-      }
-      ++pc;
-    }
-    if (bad || p > len) return off;  // off[r] is set; the rest stay at len
+    if (!detail::skip_object(P.ops().data(), P.table().data(), xdr, len, p, 0, 0) || p > len)
+      return off;  // off[r] is set; the rest stay at len
   }
   off[n] = p;  // p < len: trailing bytes, which decode reports at record n
   return off;

@@ -30,24 +30,13 @@
 #include <xdrpp/marshal.h>
 
 #include "tests/xdrtest.hh"
+#include "xdrtest_gen.hh"
 
 using namespace testns;
 using std::string;
 using std::vector;
 
 namespace {
-
-struct rng {  // splitmix64
-  uint64_t s;
-  uint64_t next() {
-    uint64_t z = (s += 0x9E3779B97F4A7C15ull);
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-  }
-  uint32_t below(uint32_t n) { return n ? uint32_t(next() % n) : 0; }
-  bool coin() { return next() & 1; }
-};
 
 string hex(const void *p, size_t n) {
   static const char *d = "0123456789abcdef";
@@ -104,60 +93,6 @@ template <typename T, uint32_t N> string J(const xdr::xarray<T, N> &v) {
   return s + "]";
 }
 
-// ---- random values
-template <typename S> void rbytes(rng &g, S &s, uint32_t maxlen) {
-  s.resize(g.below(maxlen + 1));
-  for (auto &c : s) c = static_cast<char>(g.below(256));
-}
-u_4_12 ru(rng &g) {
-  u_4_12 u(g.coin() ? 4 : 12);
-  if (u.which() == 4) u.f4().i = int32_t(g.next());
-  else { u.f12().i = int32_t(g.next()); u.f12().d = double(int32_t(g.next())) / 8.0; }
-  return u;
-}
-containertest r_containertest(rng &g) {
-  containertest c;
-  c.uvec.resize(g.below(7));
-  for (auto &u : c.uvec) u = ru(g);
-  for (auto &s : c.sarr) rbytes(g, s, 40);
-  return c;
-}
-containertest1 r_containertest1(rng &g) {
-  containertest1 c;
-  c.uvec.resize(g.below(3));
-  for (auto &u : c.uvec) u = ru(g);
-  for (auto &s : c.sarr) rbytes(g, s, 40);
-  return c;
-}
-hasbytes r_hasbytes(rng &g) {
-  hasbytes h;
-  h.the_bytes.resize(g.below(6));
-  for (auto &b : h.the_bytes) {
-    rbytes(g, b.s, 16);
-    for (auto &c : b.fixed) c = uint8_t(g.below(256));
-    rbytes(g, b.variable, 16);
-  }
-  return h;
-}
-test_recursive r_recursive(rng &g, int depth) {
-  test_recursive t;
-  rbytes(g, t.elem, 12);
-  if (depth > 0 && g.coin()) t.next.activate() = r_recursive(g, depth - 1);
-  if (depth > 0) {
-    t.nextvec.resize(g.below(4));
-    for (auto &e : t.nextvec) e = r_recursive(g, depth - 1);
-  }
-  return t;
-}
-nested_cereal_adapter_calls r_nested(rng &g) {
-  nested_cereal_adapter_calls c;
-  if (g.coin()) rbytes(g, c.strptr.activate(), 32);
-  c.strvec.resize(g.below(6));
-  for (auto &s : c.strvec) rbytes(g, s, 32);
-  for (auto &s : c.strarr) rbytes(g, s, 32);
-  return c;
-}
-
 // The smallest marshaling_stack_limit under which f() does not throw
 // xdr_stack_overflow.
 template <typename F> uint32_t min_limit(F f) {
@@ -199,38 +134,12 @@ int main(int argc, char **argv) {
     fprintf(stderr, "usage: ref_containers <out.json>\n");
     return 2;
   }
-  rng g{0x5EED0A8ull};
-  vector<containertest> ct;
-  vector<containertest1> ct1;
-  vector<hasbytes> hb;
-  vector<test_recursive> tr;
-  vector<nested_cereal_adapter_calls> nc;
-  // edge cases first: every container empty, then the reference's own value
-  ct.emplace_back();
-  {
-    containertest c;  // tests/marshal.cc:551-553
-    c.uvec = {u_4_12(4), u_4_12(12), u_4_12(4), u_4_12(4)};
-    c.sarr[0] = "hello";
-    c.sarr[1] = "world";
-    ct.push_back(c);
-  }
-  ct1.emplace_back();
-  hb.emplace_back();
-  tr.emplace_back();
-  nc.emplace_back();
-  for (int i = 0; i < 200; ++i) {
-    ct.push_back(r_containertest(g));
-    ct1.push_back(r_containertest1(g));
-    hb.push_back(r_hasbytes(g));
-    tr.push_back(r_recursive(g, 1 + int(g.below(5))));
-    nc.push_back(r_nested(g));
-  }
-  {
-    test_recursive deep;  // a chain 12 deep through `next`
-    test_recursive *t = &deep;
-    for (int d = 0; d < 12; ++d) { t->elem = "n" + std::to_string(d); t = &t->next.activate(); }
-    tr.push_back(deep);
-  }
+  xdrtest_gen::batches B = xdrtest_gen::make_batches();
+  auto &ct = B.ct;
+  auto &ct1 = B.ct1;
+  auto &hb = B.hb;
+  auto &tr = B.tr;
+  auto &nc = B.nc;
 
   // tests/marshal.cc:548-573: containertest with 4 uvec elements read as
   // containertest1 (uvec<2>) throws xdr_overflow

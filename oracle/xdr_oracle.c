@@ -471,8 +471,8 @@ static int dec_ops(dctx *c, uint32_t pc, uint8_t *nat, uint32_t dbase, uint32_t 
         for (uint32_t i = 0; i < cnt; ++i) {
           int rc = dec_ops(c, op->arg4, c->heap_out + arr + (uint64_t)i * op->arg1, dbase + op->depth,
                            frames + 1);
-          if (rc) {  /* the element that failed (the unstager stops there) */
-            ref.rsv = i;
+          if (rc) {  /* 1 + the element that failed (the unstager follows it) */
+            ref.rsv = i + 1;
             memcpy(nat + op->noff, &ref, sizeof ref);
             return rc;
           }

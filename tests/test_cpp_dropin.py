@@ -71,3 +71,41 @@ def test_cpp_dropin_on_gpu():
     r = run("gpu", os.path.join(ROOT, "tests", "golden"), timeout=600)
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+# ------------------------------------- genuine xdrc output: containers_test
+CBIN = os.path.join(ROOT, "oracle", "_ref", "containers_test")
+needs_cbin = pytest.mark.skipif(not os.path.exists(CBIN), reason="oracle/_ref/containers_test not built")
+
+
+def crun(*args, timeout=300):
+    return subprocess.run([CBIN, *args], capture_output=True, text=True, timeout=timeout)
+
+
+@needs_cbin
+@pytest.mark.parametrize("name", list(S.CONTAINERS))
+def test_containers_recorded_plan_equals_compiled_plan(tmp_path, name):
+    """Element subroutines recorded from the generated xdr_traits equal the
+    Python mirror's, op for op (bodies after the record's END, breadth
+    first; test_recursive's elements enter the record's own ops)."""
+    r = crun("plans", str(tmp_path))
+    assert r.returncode == 0, r.stderr
+    ops, tab, stride, identity = read_plan(tmp_path / f"{name}.plan")
+    cp = compile_plan(S.CONTAINERS[name])
+    assert stride == cp.stride and not identity
+    assert np.array_equal(normalized(ops), normalized(cp.ops))
+    assert np.array_equal(tab, cp.table)
+
+
+@needs_cbin
+def test_containers_staging_round_trip():
+    r = crun("stage")
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+@needs_cbin
+@pytest.mark.gpu
+def test_containers_dropin_on_gpu():
+    r = crun("gpu", timeout=600)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr

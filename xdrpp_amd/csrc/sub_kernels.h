@@ -305,8 +305,8 @@ __global__ __launch_bounds__(256) void k_sub_encode(
 // zero-filled first.  Payloads stay in the stream (heap_out holds it at
 // [0, len)); element arrays come from the record's element area
 // [ebase + F*off[r], ebase + F*off[r+1]) at 8-byte alignment.  On a failure
-// inside elements, each open container's rsv holds the index of the
-// element that failed (the unstager stops there).
+// inside elements, each open container's rsv holds 1 + the index of the
+// element that failed, the others 0 (the unstager follows these marks).
 __global__ __launch_bounds__(256) void k_sub_decode(
     const uint8_t *__restrict__ xdr, uint64_t len, const uint64_t *__restrict__ offsets, uint64_t n,
     uint8_t *__restrict__ native, uint32_t stride, const xdrg_op *__restrict__ ops, uint32_t nops,
@@ -439,7 +439,7 @@ __global__ __launch_bounds__(256) void k_sub_decode(
   }
   if (code) {
     if (code != kReported) report(err, r, pc, code);
-    for (uint32_t k = 0; k < fp; ++k) st32(st[k].ref + 12, st[k].cnt - 1u - st[k].left);
+    for (uint32_t k = 0; k < fp; ++k) st32(st[k].ref + 12, st[k].cnt - st[k].left);  // 1 + element
     return;
   }
   if (p != b) report(err, r, kOpRecordLevel, XDRG_ERR_TRAILING);
