@@ -16,6 +16,8 @@
  *   xdrg_encode_msgs      <- xdr_to_msg(r) per record       xdrpp/marshal.h:252-260
  *                            (record mark: message_t::alloc, xdrpp/marshal.cc:15-31)
  *   xdrg_decode_msgs      <- xdr_from_msg(m, r) per message  xdrpp/marshal.h:278-284
+ *   xdrg_index_records    <- the record boundaries of xdr_from_opaque's walk
+ *                                                            xdrpp/marshal.h:299-306
  *   xdrg_index_msgs       <- the record-mark framing of read_message /
  *                            msg_sock::input                 xdrpp/srpc.cc:29-55,
  *                                                            xdrpp/msgsock.cc:38-119
@@ -213,7 +215,8 @@ enum xdrg_err {
   XDRG_ERR_MSG_TOO_LONG = 16,   /* msg_sock maxmsglen_  msgsock.cc:99-111 */
   XDRG_ERR_MSG_MISMATCH = 17,   /* mark disagrees with the record index  */
   XDRG_ERR_MSG_COUNT = 18,      /* more messages than the index can hold */
-  XDRG_ERR_INTERNAL = 19        /* a device-side wait gave up (the kernel still ends) */
+  XDRG_ERR_INTERNAL = 19,       /* a device-side wait gave up (the kernel still ends) */
+  XDRG_ERR_INDEX_LONG = 20      /* xdrg_index_records: a record longer than its bound */
 };
 
 /* Exception class a data error maps to (for host-side rethrow). */
@@ -430,6 +433,29 @@ int xdrg_index_msgs(const void *d_stream, uint64_t len, uint32_t max_msg_len,
                     void *d_workspace, size_t workspace_bytes, xdrg_status *d_status,
                     void *stream);
 size_t xdrg_index_workspace_size(uint64_t len, uint32_t max_msg_len);
+
+/*
+ * Record index of n records of `plan` concatenated in one stream, the
+ * input of xdr_from_opaque(bytes, r0, ..., rn-1) (xdrpp/marshal.h:299-306),
+ * computed on the device: every word position is parsed as a possible
+ * record start (lengths, counts and discriminants only) and the chain of
+ * record ends from byte 0 is ranked as for xdrg_index_msgs.  Writes
+ * d_offsets[0..n] for xdrg_decode: record r = [off[r], off[r+1]).  Where
+ * the records stop parsing -- a bad discriminant, a length past its bound
+ * or past the stream -- record k gets [off[k], len) and the rest [len, len),
+ * so xdrg_decode reports the reference's error for record k; fewer than n
+ * records end at len likewise, more leave off[n] < len (trailing bytes).
+ * *d_count = the records the chain holds before it ends (all-ones when
+ * it goes past record n).  A record longer than max_rec_len (<= XDRG_INDEX_MAX_MSG)
+ * is reported as XDRG_ERR_INDEX_LONG at its index: the caller indexes that
+ * stream another way (the C++ layer walks it on the host).  Plans whose
+ * records can be empty are XDRG_EUNSUPPORTED.  Workspace:
+ * xdrg_index_workspace_size(len, max_rec_len).
+ */
+int xdrg_index_records(const xdrg_plan *plan, const void *d_xdr, uint64_t len, uint64_t n,
+                       uint32_t max_rec_len, uint64_t *d_offsets, uint64_t *d_count,
+                       void *d_workspace, size_t workspace_bytes, xdrg_status *d_status,
+                       void *stream);
 
 /* ---------------------------------------------------------------------- */
 /* RPC header batches (RFC 5531 rpc_msg, xdrpp/rpc_msg.x)                  */

@@ -753,6 +753,8 @@ template <typename T> class batch_plan {
   bool identity() const { return identity_; }
   bool fixed() const { return fixed_; }
   std::uint32_t fixed_size() const { return fixed_size_; }
+  //! Largest wire record the plan's bounds allow (all-ones: unbounded).
+  std::uint64_t max_record_bytes() const { return max_record_bytes_; }
   //! Some struct or union of T has a user validate() hook.
   bool validates() const { return validates_; }
 
@@ -839,12 +841,14 @@ template <typename T> class batch_plan {
     xdrg_plan_info info{};
     detail::abicheck(xdrg_plan_get_info(h, &info), "xdrg_plan_get_info");
     fixed_size_ = info.fixed_size;
+    max_record_bytes_ = info.max_record_bytes;
   }
   std::unique_ptr<xdrg_plan, deleter> h_;
   std::vector<xdrg_op> ops_;
   std::vector<std::uint32_t> table_;
   std::vector<std::pair<std::uint32_t, std::string>> msgs_;
   std::uint32_t stride_ = 0, fixed_size_ = 0;
+  std::uint64_t max_record_bytes_ = 0;
   bool identity_ = false, fixed_ = false, validates_ = false;
 };
 
@@ -1060,8 +1064,29 @@ void from_opaque_batch(const void *bytes, std::size_t len, T *out, std::size_t n
   const std::uint64_t hcap = P.fixed() ? 0 : xdrg_decode_heap_size(P.handle(), len);
   detail::dev_buf<std::uint8_t> d_heap(hcap);
   if (!P.fixed()) {
-    idx = index_records<T>(x, len, n);
-    detail::hipcheck(hipMemcpyAsync(d_off.p, idx.data(), (n + 1) * 8, hipMemcpyHostToDevice, s), "H2D");
+    // the record index on the device (xdrg_index_records); a stream with a
+    // record longer than the index window is walked on the host instead
+    const std::uint32_t win = static_cast<std::uint32_t>(
+        std::min<std::uint64_t>(std::max<std::uint64_t>(P.max_record_bytes(), 16), XDRG_INDEX_MAX_MSG));
+    const std::size_t wsb = xdrg_index_workspace_size(len, win);
+    detail::dev_buf<std::uint8_t> ws(wsb);
+    detail::dev_buf<std::uint64_t> d_cnt(1);
+    const int rc = xdrg_index_records(P.handle(), d_xdr.p, len, n, win, d_off.p, d_cnt.p, ws.p, wsb, d_st.p, s);
+    bool host = rc == XDRG_EUNSUPPORTED;
+    if (!host) {
+      detail::abicheck(rc, "xdrg_index_records");
+      xdrg_error ie{};
+      detail::abicheck(xdrg_status_read(d_st.p, s, &ie), "xdrg_status_read");
+      if (ie.code) {
+        if (ie.code != XDRG_ERR_INDEX_LONG) P.raise(ie);
+        host = true;
+        detail::abicheck(xdrg_status_init(d_st.p, s), "xdrg_status_init");
+      }
+    }
+    if (host) {
+      idx = index_records<T>(x, len, n);
+      detail::hipcheck(hipMemcpyAsync(d_off.p, idx.data(), (n + 1) * 8, hipMemcpyHostToDevice, s), "H2D");
+    }
   }
   detail::abicheck(xdrg_decode(P.handle(), d_xdr.p, len, d_off.p, n, d_nat.p, d_heap.p, hcap,
                                marshaling_stack_limit, nullptr, 0, d_st.p, s),

@@ -648,6 +648,110 @@ int xdro_index_msgs(const uint8_t *s, uint64_t len, uint32_t maxlen, uint64_t ma
   }
 }
 
+/* ------------------------------------------------ concatenated records
+ * xdrg_index_records restated: the record boundaries xdr_from_opaque
+ * (marshal.h:299-306) walks, record after record from byte 0.  A record
+ * is parsed for its structure -- lengths, counts, discriminants -- with
+ * the checks that make its decode fail (bounds, unknown discriminants,
+ * unlisted values of validated enums): where it fails to parse, record k
+ * gets [off[k], len) and the rest [len, len).  A record running past
+ * a + maxlen (but not past the stream) is XDRG_ERR_INDEX_LONG at k. */
+#define RX_BAD 0xffffffffu
+#define RX_LONG 0xfffffffeu
+typedef struct {
+  const plan_t *P;
+  const uint8_t *s;
+  uint64_t lim;
+  uint32_t past;
+} rxctx;
+static uint32_t rx_walk(rxctx *c, uint64_t *pp, uint32_t pc, uint32_t frames) {
+  const plan_t *P = c->P;
+  uint64_t p = *pp;
+  for (;;) {
+    const xdrg_op *op = &P->ops[pc];
+    if (op->kind == XDRG_OP_END) { *pp = p; return 0; }
+    if (op->kind == XDRG_OP_JUMP) { pc = op->arg0; continue; }
+    if (op->kind == XDRG_OP_U64) {
+      if (c->lim - p < 8) return c->past;
+      p += 8; ++pc; continue;
+    }
+    if (op->kind == XDRG_OP_OPAQUE) {
+      if (c->lim - p < op->arg0) return c->past;
+      p += pad4(op->arg0); ++pc; continue;
+    }
+    if (c->lim - p < 4) return c->past;
+    const uint32_t v = bswap32(rd32(c->s + p));
+    p += 4;
+    switch (op->kind) {
+    case XDRG_OP_ENUM:
+      if (!enum_ok(P, op, v)) return RX_BAD;
+      ++pc; break;
+    case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING:
+      if (v > op->arg0) return RX_BAD;
+      if (c->lim - p < v) return c->past;
+      p += pad4(v); ++pc; break;
+    case XDRG_OP_UNION: {
+      if (!enum_ok(P, op, v)) return RX_BAD;
+      int64_t t = union_target(P, op, v);
+      if (t < 0) return RX_BAD;
+      pc = (uint32_t)t;
+      break;
+    }
+    case XDRG_OP_VECTOR:
+      if (v > op->arg0) return RX_BAD;
+      if (!(op->flags & XDRG_F_SUB)) {
+        const uint64_t b = (uint64_t)v * vec_wire(P, pc);
+        if (c->lim - p < b) return c->past;
+        p += b;
+        pc += 1 + op->arg2;
+        break;
+      }
+      if (v && frames == XDRG_SUB_FRAMES) return RX_BAD;
+      for (uint32_t i = 0; i < v; ++i) {
+        uint32_t rc = rx_walk(c, &p, op->arg4, frames + 1);
+        if (rc) return rc;
+      }
+      ++pc;
+      break;
+    default: ++pc; break;
+    }
+  }
+}
+
+int xdro_index_records(const xdrg_op *ops, uint32_t nops, const uint32_t *table, const uint8_t *s,
+                       uint64_t len, uint64_t n, uint32_t maxlen, uint64_t *offsets, uint64_t *count,
+                       uint64_t *erec) {
+  plan_t P = {ops, nops, table, 0};
+  uint64_t p = 0, k = 0;
+  *count = UINT64_MAX;
+  for (; k < n && p < len; ++k) {
+    offsets[k] = p;
+    const int capped = p + maxlen < len;
+    rxctx c = {&P, s, capped ? p + maxlen : len, capped ? RX_LONG : RX_BAD};
+    uint64_t q = p;
+    uint32_t rc = rx_walk(&c, &q, 0, 0);
+    if (rc) {
+      *count = k;
+      for (uint64_t i = k + 1; i <= n; ++i) offsets[i] = len;
+      if (rc == RX_LONG) { *erec = k; return XDRG_ERR_INDEX_LONG; }
+      return 0;
+    }
+    p = q;
+  }
+  offsets[k] = p;
+  if (p == len || k < n) {  /* the stream ends at record k */
+    *count = k;
+    for (uint64_t i = k + 1; i <= n; ++i) offsets[i] = len;
+    return 0;
+  }
+  /* n records and more bytes: the chain ends at record n unless it parses */
+  const int capped = p + maxlen < len;
+  rxctx c = {&P, s, capped ? p + maxlen : len, capped ? RX_LONG : RX_BAD};
+  uint64_t q = p;
+  if (rx_walk(&c, &q, 0, 0)) *count = n;
+  return 0;
+}
+
 /* ------------------------------------------------------------ RPC headers
  * rpc_msg header decode (xdrpp/rpc_msg.x through xdr_get: check(4) per
  * word, opaque body<400>: length, check(size), bound, pad check —

@@ -205,6 +205,19 @@ def rpc_replies(hdrs: np.ndarray, cap: int | None = None):
     return out[:min(tot.value, cap)], offs, rc, er.value
 
 
+def index_records(plan, xdr: np.ndarray, n: int, maxlen: int):
+    """xdro_index_records: (offsets[n+1], count, error code, error record)."""
+    L = lib()
+    vp, u64, u32 = C.c_void_p, C.c_uint64, C.c_uint32
+    L.xdro_index_records.argtypes = [vp, u32, vp, vp, u64, u64, u32, vp, C.POINTER(u64), C.POINTER(u64)]
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    cnt, er = C.c_uint64(0), C.c_uint64(0)
+    x = xdr if xdr.size else np.zeros(4, dtype=np.uint8)
+    rc = L.xdro_index_records(_p(plan.ops), len(plan.ops), _p(plan.table), _p(x), xdr.size, n, maxlen,
+                              _p(offs), C.byref(cnt), C.byref(er))
+    return offs, cnt.value, rc, er.value
+
+
 def depths(plan, native: np.ndarray, n: int, heap: np.ndarray | None = None) -> np.ndarray:
     """depth_checker per record (xdro_depths); raises OracleError."""
     out = np.zeros(max(n, 1), dtype=np.uint32)

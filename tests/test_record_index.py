@@ -1,0 +1,169 @@
+"""The device record index of concatenated var records (xdrg_index_records):
+the record boundaries xdr_from_opaque walks (xdrpp/marshal.h:299-306).
+
+CPU: the C restatement (oracle/xdr_oracle.c xdro_index_records) against
+the reference's own record offsets (golden fixtures written by the real
+xdr_put, oracle/ref_golden.cc; containers.json from genuine xdrc output).
+GPU: the list-ranking index against the restatement -- goldens, full-size
+encoded batches (offsets of the encode == the index of its output), and
+damaged streams (bad lengths and discriminants, truncation, extra records,
+trailing garbage, a record past the index window).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLD, golden
+
+from xdrpp_amd import _abi as A
+from xdrpp_amd import schemas as S
+from xdrpp_amd.xdr_types import compile_plan
+import oracle_bridge as O
+
+VAR = ["recvar", "rpc", "vecrec"]
+
+
+def window(cp):
+    return min(int(max(cp_max(cp), 16)), A.INDEX_MAX_MSG)
+
+
+def cp_max(cp):
+    from xdrpp_amd import marshal as M
+    return M.Plan(cp).max_record_bytes
+
+
+def gold_stream(name):
+    n = 1024
+    return golden(name, n, "xdr"), golden(name, n, "offsets", np.uint64), n
+
+
+def containers_stream(name):
+    with open(os.path.join(GOLD, "containers.json")) as f:
+        recs = json.load(f)["types"][name]["records"]
+    wire = [bytes.fromhex(r["xdr"]) for r in recs]
+    offs = np.zeros(len(wire) + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(w) for w in wire])
+    return np.frombuffer(b"".join(wire), dtype=np.uint8).copy(), offs, len(wire)
+
+
+def damaged(x, offs, n, seed):
+    """(label, stream, n) cases around a good stream of n records."""
+    rng = np.random.default_rng(seed)
+    out = [("good", x, n), ("fewer", x[:int(offs[n // 2])], n), ("more", x, n // 2),
+           ("cut", x[:int(offs[n // 3]) + 4], n), ("trailing", np.concatenate([x, np.full(8, 0xff, np.uint8)]), n)]
+    for t in range(4):
+        y = x.copy()
+        r = int(rng.integers(0, n))
+        w = int(offs[r]) // 4 + int(rng.integers(0, max(1, (int(offs[r + 1]) - int(offs[r])) // 4)))
+        y[4 * w:4 * w + 4] = np.frombuffer(rng.integers(0, 2**32, 1, dtype=np.uint64).astype(">u4").tobytes(),
+                                           dtype=np.uint8)
+        out.append((f"word{t}", y, n))
+    return out
+
+
+# ------------------------------------------------------------------ CPU
+@pytest.mark.parametrize("name", VAR)
+def test_oracle_index_matches_reference(name):
+    x, offs, n = gold_stream(name)
+    cp = compile_plan(S.ALL[name])
+    got, cnt, rc, _ = O.index_records(cp, x, n, window(cp))
+    assert rc == 0 and cnt == n and np.array_equal(got, offs)
+
+
+@pytest.mark.parametrize("name", list(S.CONTAINERS))
+def test_oracle_index_matches_reference_containers(name):
+    x, offs, n = containers_stream(name)
+    cp = compile_plan(S.CONTAINERS[name])
+    got, cnt, rc, _ = O.index_records(cp, x, n, A.INDEX_MAX_MSG)
+    assert rc == 0 and cnt == n and np.array_equal(got, offs)
+
+
+def test_oracle_index_semantics():
+    x, offs, n = gold_stream("recvar")
+    cp = compile_plan(S.recvar)
+    W = window(cp)
+    got, cnt, rc, _ = O.index_records(cp, x[:int(offs[10])], n, W)  # 10 records, then the end
+    assert rc == 0 and cnt == 10 and np.array_equal(got[:11], offs[:11]) and (got[11:] == offs[10]).all()
+    got, cnt, rc, _ = O.index_records(cp, x, 5, W)  # more records than asked for
+    assert rc == 0 and cnt == 2**64 - 1 and np.array_equal(got, offs[:6])
+    y = x.copy()
+    y[int(offs[7]) + 12:int(offs[7]) + 16] = 0xff  # record 7's blob length: past its bound
+    got, cnt, rc, _ = O.index_records(cp, y, n, W)
+    assert rc == 0 and cnt == 7 and np.array_equal(got[:8], offs[:8]) and (got[8:] == x.size).all()
+    got, cnt, rc, er = O.index_records(cp, x, n, 64)  # a window shorter than the records
+    assert rc == A.ERR_INDEX_LONG and er == 0
+
+
+# ------------------------------------------------------------------ GPU
+def _dev(a, dev):
+    import torch
+    return torch.from_numpy(np.array(a)).to(dev)
+
+
+def _gpu_index(mar, x, n, maxlen, dev):
+    """(offsets, count, error) of the device index."""
+    import torch
+    from xdrpp_amd import marshal as M
+    L = A.lib()
+    dx = _dev(x if x.size else np.zeros(4, np.uint8), dev)
+    ws = torch.empty(max(L.xdrg_index_workspace_size(x.size, maxlen), 16), dtype=torch.uint8, device=dev)
+    offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    cnt = torch.empty(1, dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    mar.status.init(s)
+    A.check(L.xdrg_index_records(mar.plan.handle, dx.data_ptr(), x.size, n, maxlen, offs.data_ptr(),
+                                 cnt.data_ptr(), ws.data_ptr(), ws.numel(), mar.status.ptr, s),
+            "xdrg_index_records")
+    e = M.error_from(mar.plan, mar.status.read(s))
+    return offs.cpu().numpy().view(np.uint64), int(cnt.cpu().numpy().view(np.uint64)[0]), e
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", VAR + list(S.CONTAINERS))
+def test_gpu_index_matches_oracle(dev, name):
+    from xdrpp_amd import marshal as M
+    t = S.ALL.get(name) or S.CONTAINERS[name]
+    cp = compile_plan(t)
+    x, offs, n = gold_stream(name) if name in VAR else containers_stream(name)
+    mar = M.Marshaler(M.Plan(cp), dev)
+    W = window(cp)
+    for label, y, k in damaged(x, offs, n, 7):
+        want, wcnt, wrc, wer = O.index_records(cp, y, k, W)
+        got, gcnt, err = _gpu_index(mar, y, k, W, dev)
+        assert np.array_equal(got, want), label
+        assert gcnt == wcnt, label
+        assert (err.code if err else 0) == wrc, label
+
+
+@pytest.mark.gpu
+def test_gpu_index_long_record(dev):
+    from xdrpp_amd import marshal as M
+    x, offs, n = gold_stream("recvar")
+    cp = compile_plan(S.recvar)
+    mar = M.Marshaler(M.Plan(cp), dev)
+    got, cnt, err = _gpu_index(mar, x, n, 64, dev)
+    want, wcnt, wrc, wer = O.index_records(cp, x, n, 64)
+    assert err is not None and err.code == A.ERR_INDEX_LONG == wrc and err.record == wer
+    assert np.array_equal(got, want) and cnt == wcnt
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["recvar", "rpc"])
+def test_gpu_index_full_size(dev, name):
+    """1M records: the index of the encode's output is the encode's offsets,
+    and decode without offsets (device index) equals decode with them."""
+    import torch
+    from xdrpp_amd import marshal as M
+    from xdrpp_amd import workloads as W
+    n = 1 << 20
+    nat, heap = getattr(W, name)(n)
+    nat, heap = _dev(nat, dev), _dev(heap, dev)
+    mar = M.Marshaler(M.Plan(S.ALL[name]), dev)
+    r = mar.encode(nat, n, heap)
+    offs = mar.index_records(r.xdr, n)
+    assert torch.equal(offs, r.offsets)
+    a, ha = mar.decode(r.xdr, n, r.offsets)
+    b, hb = mar.decode(r.xdr, n)
+    assert torch.equal(a, b) and torch.equal(ha, hb)

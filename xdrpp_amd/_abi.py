@@ -52,6 +52,7 @@ ERR_MSG_TOO_LONG = 16
 ERR_MSG_MISMATCH = 17
 ERR_MSG_COUNT = 18
 ERR_INTERNAL = 19
+ERR_INDEX_LONG = 20
 
 MARK_LAST = 0x80000000  # XDRG_MARK_LAST: last-fragment bit of a record mark
 INDEX_MAX_MSG = 16380   # XDRG_INDEX_MAX_MSG
@@ -117,7 +118,7 @@ EXPORTED = (
     "xdrg_index_workspace_size", "xdrg_rpc_dispatch", "xdrg_rpc_check_replies",
     "xdrg_rpc_replies", "xdrg_rpc_replies_workspace_size", "xdrg_record_depths",
     "xdrg_plan_set_option", "xdrg_plan_kernel_source", "xdrg_plan_build_kernels",
-    "xdrg_plan_load_kernels",
+    "xdrg_plan_load_kernels", "xdrg_index_records",
 )
 
 # RPC header batches (include/xdrgpu.h "RPC header batches")
@@ -181,6 +182,8 @@ def lib() -> C.CDLL:
     L.xdrg_decode_msgs.restype = C.c_int
     L.xdrg_index_msgs.argtypes = [vp, u64, u32, u64, vp, vp, vp, sz, vp, vp]
     L.xdrg_index_msgs.restype = C.c_int
+    L.xdrg_index_records.argtypes = [vp, vp, u64, u64, u32, vp, vp, vp, sz, vp, vp]
+    L.xdrg_index_records.restype = C.c_int
     L.xdrg_index_workspace_size.argtypes = [u64, u32]
     L.xdrg_index_workspace_size.restype = sz
     L.xdrg_rpc_dispatch.argtypes = [vp, u64, vp, u64, vp, u32, vp, vp]

@@ -369,6 +369,7 @@ int compile_plan(xdrg_plan &p) {
     p.max_scalar_words = words[0];
     p.max_pieces = uint32_t(std::min<uint64_t>(pieces[0], 0xffffffffu));
     p.max_record_bytes = bytes[0];
+    p.min_record_bytes = minw[0];
   }
   if (!fixed) {
     p.fixed_size = 0;

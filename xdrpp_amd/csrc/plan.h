@@ -122,6 +122,7 @@ struct xdrg_plan {
   uint32_t max_scalar_words = 0;  // var plans: most non-payload wire words on one path
   uint32_t max_pieces = 0;  // var plans: most 256-byte payload pieces on one path (by bounds)
   uint64_t max_record_bytes = 0;  // var plans: largest wire record the bounds allow
+  uint64_t min_record_bytes = 0;  // smallest wire record (the record index needs >= 4)
   uint64_t max_chunks16 = 0;      // var plans: most 16-byte payload chunks on one path
   uint32_t max_slot_len = 0;      // var plans: largest opaque<>/string<> bound
   bool has_vector = false;        // xvector<T>/pointer<T> fields (XDRG_OP_VECTOR)

@@ -1055,25 +1055,126 @@ __device__ __forceinline__ uint32_t ix_next(uint32_t raw, uint32_t i, uint32_t l
   return i + 1u + size / 4u;
 }
 
+// ------------------------------------- concatenated records: the index pass
+// xdrg_index_records runs the same list ranking over record starts: node w
+// is "a record starts at word w", its successor the word after that
+// record.  rx_len parses one record from byte a -- lengths, counts and
+// discriminants only, the structure xdr_generic_get would walk
+// (marshal.h:142-211) -- with every check that makes its decode fail
+// (bounds of strings, opaques and containers, unknown discriminants,
+// unlisted values of validated enums), so a node that does not parse is a
+// record the decode rejects.  RX_LONG: the record runs past a + maxlen (but
+// not past the stream), beyond what one segment window can index.
+constexpr uint32_t RX_BAD = 0xffffffffu, RX_LONG = 0xfffffffeu;
+
+// Stream words through global memory.  (Staging a segment's reachable
+// window in LDS first measured slower on MI355X: 0.69 -> 0.96 ms for 1M
+// recvar records, the occupancy it costs outweighing L2-hit latency.)
+struct rx_global {
+  const uint8_t *s;
+  __device__ __forceinline__ uint32_t operator()(uint64_t p) const { return ld32(s + p); }
+};
+
+template <class RD>
+__device__ uint32_t rx_len(const xdrg_op *__restrict__ ops, const uint32_t *__restrict__ table,
+                           const RD &rd, uint64_t len, uint64_t a, uint32_t maxlen) {
+  const bool capped = a + maxlen < len;
+  const uint64_t lim = capped ? a + maxlen : len;
+  const uint32_t past = capped ? RX_LONG : RX_BAD;
+  struct frame { uint32_t left, entry, ret; };
+  frame st[XDRG_SUB_FRAMES];
+  uint32_t fp = 0, pc = 0;
+  uint64_t p = a;
+  for (;;) {
+    const xdrg_op &op = ops[pc];
+    switch (op.kind) {
+    case XDRG_OP_END:
+      if (!fp) return static_cast<uint32_t>(p - a);
+      if (st[fp - 1].left) { --st[fp - 1].left; pc = st[fp - 1].entry; }
+      else pc = st[--fp].ret;
+      continue;
+    case XDRG_OP_JUMP: pc = op.arg0; continue;
+    case XDRG_OP_U64:
+      if (lim - p < 8) return past;
+      p += 8; ++pc; continue;
+    case XDRG_OP_OPAQUE:
+      if (lim - p < op.arg0) return past;
+      p += (op.arg0 + 3u) & ~3u; ++pc; continue;
+    default: break;
+    }
+    if (lim - p < 4) return past;
+    const uint32_t v = bswap32(rd(p));
+    p += 4;
+    switch (op.kind) {
+    case XDRG_OP_ENUM:
+      if ((op.flags & XDRG_F_VALIDATE) && !enum_ok(table, op.arg0, op.arg1, v)) return RX_BAD;
+      ++pc;
+      break;
+    case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING:
+      if (v > op.arg0) return RX_BAD;
+      if (lim - p < v) return past;
+      p += (static_cast<uint64_t>(v) + 3u) & ~3ull;
+      ++pc;
+      break;
+    case XDRG_OP_UNION: {
+      if ((op.flags & XDRG_F_VALIDATE) && !enum_ok(table, op.arg0, op.arg1, v)) return RX_BAD;
+      const int t = union_target(op, table, v);
+      if (t < 0) return RX_BAD;
+      pc = static_cast<uint32_t>(t);
+      break;
+    }
+    case XDRG_OP_VECTOR:
+      if (v > op.arg0) return RX_BAD;
+      if (!(op.flags & XDRG_F_SUB)) {
+        const uint64_t b = static_cast<uint64_t>(v) * op.arg3;
+        if (lim - p < b) return past;
+        p += b;
+        pc += 1 + op.arg2;
+      } else if (!v) {
+        ++pc;
+      } else {
+        if (fp == XDRG_SUB_FRAMES) return RX_BAD;
+        st[fp++] = frame{v - 1, op.arg4, pc + 1};
+        pc = op.arg4;
+      }
+      break;
+    default: ++pc; break;  // U32, BOOL
+    }
+  }
+}
+
+// The plan of a record index, for the segment and emit kernels.
+struct rx_plan {
+  const xdrg_op *ops;
+  const uint32_t *table;
+  uint32_t nops;
+};
+
 // LDS node: target (13 bits: < kIxSW a node of this segment, kIxSW + e =
 // entry e of the next one) | marks passed << 13 (13 bits) | ends << 26.
 // Table word: marks (40 bits) | exit entry << 40 (16 bits) | ends << 56.
 // List word of a valid node: node index | target << 12.
 constexpr uint32_t kIxEnds = 1u << 26;
 
+// REC: record starts (xdrg_index_records, rx_len over the plan in LDS);
+// otherwise record marks (xdrg_index_msgs).
+template <bool REC>
 __global__ __launch_bounds__(256) void k_ix_seg(const uint8_t *__restrict__ s, uint64_t len,
                                                 uint32_t maxlen, uint32_t K,
                                                 uint64_t *__restrict__ tab,
                                                 uint32_t *__restrict__ list,
-                                                uint32_t *__restrict__ lcount) {
+                                                uint32_t *__restrict__ lcount, rx_plan rp) {
   __shared__ __attribute__((aligned(16))) uint32_t node[kIxSW];
   __shared__ uint16_t lst[kIxSW];
   __shared__ uint32_t wtot[4];
+  extern __shared__ __attribute__((aligned(16))) uint32_t rx_smem[];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
   const uint64_t w0 = static_cast<uint64_t>(blockIdx.x) * kIxSW;
   const uint32_t lim = static_cast<uint32_t>(min<uint64_t>(len - 4 * w0, 0xfffffff0ull));
   uint32_t raw[16];
-  ix_load16(s, len, w0, tid, raw);
+  if (REC) load_ops(reinterpret_cast<xdrg_op *>(rx_smem), rp.ops, rp.nops);
+  else ix_load16(s, len, w0, tid, raw);
+  const rx_global rd{s};
   uint32_t vmask = 0, vnext[16];
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
@@ -1082,7 +1183,14 @@ __global__ __launch_bounds__(256) void k_ix_seg(const uint8_t *__restrict__ s, u
     for (int j = 0; j < 4; ++j) {
       const int q = 4 * g + j;
       const uint32_t i = 4u * (tid + 256u * g) + j;
-      vnext[q] = ix_next(raw[q], i, lim, maxlen);
+      if (REC) {
+        const uint64_t a = 4 * (w0 + i);
+        const uint32_t L =
+            a < len ? rx_len(reinterpret_cast<const xdrg_op *>(rx_smem), rp.table, rd, len, a, maxlen) : RX_BAD;
+        vnext[q] = L < RX_LONG ? i + L / 4u : 0xffffffffu;
+      } else {
+        vnext[q] = ix_next(raw[q], i, lim, maxlen);
+      }
       if (vnext[q] != 0xffffffffu) vmask |= 1u << q;
       nv[j] = vnext[q] != 0xffffffffu ? (vnext[q] | (1u << 13)) : kIxEnds;
     }
@@ -1207,24 +1315,34 @@ __global__ __launch_bounds__(64) void k_ix_down(const uint64_t *__restrict__ tab
 // a node's message index is b + (reachable nodes before it).  The node
 // where the chain ends (the last reachable one, unless the chain leaves the
 // segment) is classified exactly as read_message would (ix_mark).
+// REC: the chain of records ends at w: the end of the stream, or a record
+// that does not parse (its decode reports why) -- or one longer than the
+// index window, XDRG_ERR_INDEX_LONG.
+template <bool REC>
 __device__ void ix_final(const uint8_t *__restrict__ s, uint64_t len, uint32_t maxlen, uint64_t w,
                          uint64_t m, uint64_t max_msgs, uint64_t *__restrict__ offsets,
-                         unsigned long long *count, unsigned long long *err) {
+                         unsigned long long *count, unsigned long long *err, const rx_plan &rp) {
   if (m > max_msgs) return;
   offsets[m] = 4 * w;
-  uint64_t nx = 0;
-  const uint32_t st = ix_mark(4 * w + 4 <= len ? ld32(s + 4 * w) : 0u, w, len, maxlen, &nx);
-  if (st != IX_END) report(err, m, kOpRecordLevel, m == max_msgs ? XDRG_ERR_MSG_COUNT : ix_error(st));
+  if (REC) {
+    if (4 * w < len && m < max_msgs && rx_len(rp.ops, rp.table, rx_global{s}, len, 4 * w, maxlen) == RX_LONG)
+      report(err, m, kOpRecordLevel, XDRG_ERR_INDEX_LONG);
+  } else {
+    uint64_t nx = 0;
+    const uint32_t st = ix_mark(4 * w + 4 <= len ? ld32(s + 4 * w) : 0u, w, len, maxlen, &nx);
+    if (st != IX_END) report(err, m, kOpRecordLevel, m == max_msgs ? XDRG_ERR_MSG_COUNT : ix_error(st));
+  }
   atomicMin(count, m);
 }
 
+template <bool REC>
 __global__ __launch_bounds__(256) void k_ix_emit(const uint8_t *__restrict__ s, uint64_t len,
                                                  uint32_t maxlen, const uint64_t *__restrict__ ent,
                                                  const uint32_t *__restrict__ list,
                                                  const uint32_t *__restrict__ lcount,
                                                  uint64_t *__restrict__ offsets, uint64_t max_msgs,
                                                  unsigned long long *count,
-                                                 unsigned long long *err) {
+                                                 unsigned long long *err, rx_plan rp) {
   // J: successor of a valid node (0xffff: not a valid node); lst: the valid
   // nodes; nj / mk: a round's new successors and marks (double buffer)
   __shared__ __attribute__((aligned(16))) uint16_t J[kIxSW];
@@ -1257,7 +1375,7 @@ __global__ __launch_bounds__(256) void k_ix_emit(const uint8_t *__restrict__ s, 
   if (tid == 0) on[x] = 1;
   __syncthreads();
   if (J[x] == 0xffffu) {  // the chain ends at its entry
-    if (tid == 0) ix_final(s, len, maxlen, w0 + x, b, max_msgs, offsets, count, err);
+    if (tid == 0) ix_final<REC>(s, len, maxlen, w0 + x, b, max_msgs, offsets, count, err, rp);
     return;
   }
   // Fast path: when the valid nodes from x on form one path (no node is the
@@ -1332,16 +1450,26 @@ __global__ __launch_bounds__(256) void k_ix_emit(const uint8_t *__restrict__ s, 
     const uint64_t m = b + r;
     ++r;
     if (r == total && J[i] == 0xffffu) {  // the chain ends at this node
-      ix_final(s, len, maxlen, w0 + i, m, max_msgs, offsets, count, err);
+      ix_final<REC>(s, len, maxlen, w0 + i, m, max_msgs, offsets, count, err, rp);
       continue;
     }
     if (m > max_msgs) continue;
     offsets[m] = 4 * (w0 + i);
-    if (m == max_msgs) {  // a message past the index's capacity
+    if (m == max_msgs && !REC) {  // a message past the index's capacity
       report(err, m, kOpRecordLevel, XDRG_ERR_MSG_COUNT);
       atomicMin(count, m);
     }
   }
+}
+
+// Records after the one where the chain ended: [len, len).
+__global__ void k_rx_fill(uint64_t *__restrict__ offsets, const unsigned long long *__restrict__ count,
+                          uint64_t n, uint64_t len) {
+  const uint64_t c = *count;  // all-ones: the chain went past record n
+  if (c >= n) return;
+  for (uint64_t i = c + 1 + static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i <= n;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
+    offsets[i] = len;
 }
 
 // ------------------------------------------------------------------ swaps
@@ -1840,6 +1968,57 @@ int var_decode(const xdrg_plan &P, const dev_tables &T, const void *d_xdr, uint6
 
 }  // namespace
 
+namespace {
+template <bool REC>
+int run_index(const xdrg_plan *p, const dev_tables *T, const void *d_stream, uint64_t len,
+              uint32_t max_msg_len, uint64_t max_msgs, uint64_t *d_offsets, uint64_t *d_count,
+              void *d_ws, size_t ws_bytes, xdrg_status *d_status, hipStream_t s) {
+  const ix_layout L = ix_plan(len, max_msg_len);
+  if (!d_ws || ws_bytes < L.total) return XDRG_ESPACE;
+  if (L.nseg > 0xffffffffull) return XDRG_EUNSUPPORTED;
+  rx_plan rp{REC ? T->d_ops : nullptr, REC ? T->d_table : nullptr, REC ? uint32_t(p->ops.size()) : 0u};
+  const size_t ops_lds = REC ? p->ops.size() * sizeof(xdrg_op) : 0;
+  if (ops_lds > (38u << 10)) return XDRG_EUNSUPPORTED;  // + 25 KiB static: the 64 KiB workgroup LDS
+  unsigned long long *err = err_ptr(d_status);
+  char *ws = static_cast<char *>(d_ws);
+  auto tab = [&](int l) { return reinterpret_cast<uint64_t *>(ws + L.tab[l]); };
+  auto ent = [&](int l) { return reinterpret_cast<uint64_t *>(ws + L.ent[l]); };
+  const uint8_t *s8 = static_cast<const uint8_t *>(d_stream);
+  HIPCHK(hipMemsetAsync(d_count, 0xff, 8, s));
+  uint32_t *vlist = reinterpret_cast<uint32_t *>(ws + L.list);
+  uint32_t *vcount = reinterpret_cast<uint32_t *>(ws + L.lcount);
+  // the tables are needed above one segment; the valid-node lists always
+  k_ix_seg<REC><<<L.nseg, 256, ops_lds, s>>>(s8, len, max_msg_len, L.K, L.top > 0 ? tab(0) : nullptr,
+                                             vlist, vcount, rp);
+  HIPCHK(hipGetLastError());
+  const size_t stg = L.lds ? static_cast<size_t>(L.F) * L.K * 8 : 0;
+  for (int l = 0; l + 1 < L.top; ++l) {
+    if (L.lds)
+      k_ix_up<true><<<L.n[l + 1], 256, stg, s>>>(tab(l), L.n[l], L.K, L.F, tab(l + 1));
+    else
+      k_ix_up<false><<<L.n[l + 1], 256, 0, s>>>(tab(l), L.n[l], L.K, L.F, tab(l + 1));
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(hipMemsetAsync(ent(L.top), 0, 8, s));  // the chain starts at word 0 with 0 messages
+  for (int l = L.top - 1; l >= 0; --l) {
+    if (L.lds)
+      k_ix_down<true><<<L.n[l + 1], 64, stg, s>>>(tab(l), L.n[l], L.K, L.F, ent(l + 1), ent(l));
+    else
+      k_ix_down<false><<<L.n[l + 1], 64, 0, s>>>(tab(l), L.n[l], L.K, L.F, ent(l + 1), ent(l));
+    HIPCHK(hipGetLastError());
+  }
+  k_ix_emit<REC><<<L.nseg, 256, 0, s>>>(s8, len, max_msg_len, ent(0), vlist, vcount, d_offsets,
+                                        max_msgs, reinterpret_cast<unsigned long long *>(d_count), err, rp);
+  HIPCHK(hipGetLastError());
+  if (REC) {
+    k_rx_fill<<<static_cast<uint32_t>(std::min<uint64_t>((max_msgs + 256) / 256, 4096)), 256, 0, s>>>(
+        d_offsets, reinterpret_cast<const unsigned long long *>(d_count), max_msgs, len);
+    HIPCHK(hipGetLastError());
+  }
+  return XDRG_OK;
+}
+}  // namespace
+
 // ==================================================================== C ABI
 extern "C" {
 
@@ -2158,43 +2337,25 @@ int xdrg_index_msgs(const void *d_stream, uint64_t len, uint32_t max_msg_len, ui
   if ((d_stream && !aligned(d_stream, 4)) || !aligned(d_offsets, 8) || !aligned(d_count, 8))
     return XDRG_EALIGN;
   if (max_msgs >= (1ull << 40)) return XDRG_EUNSUPPORTED;  // entry words hold 40-bit counts
-  const ix_layout L = ix_plan(len, max_msg_len);
-  if (!d_ws || ws_bytes < L.total) return XDRG_ESPACE;
-  if (L.nseg > 0xffffffffull) return XDRG_EUNSUPPORTED;
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  unsigned long long *err = err_ptr(d_status);
-  char *ws = static_cast<char *>(d_ws);
-  auto tab = [&](int l) { return reinterpret_cast<uint64_t *>(ws + L.tab[l]); };
-  auto ent = [&](int l) { return reinterpret_cast<uint64_t *>(ws + L.ent[l]); };
-  const uint8_t *s8 = static_cast<const uint8_t *>(d_stream);
-  HIPCHK(hipMemsetAsync(d_count, 0xff, 8, s));
-  uint32_t *vlist = reinterpret_cast<uint32_t *>(ws + L.list);
-  uint32_t *vcount = reinterpret_cast<uint32_t *>(ws + L.lcount);
-  // the tables are needed above one segment; the valid-node lists always
-  k_ix_seg<<<L.nseg, 256, 0, s>>>(s8, len, max_msg_len, L.K, L.top > 0 ? tab(0) : nullptr, vlist,
-                                  vcount);
-  HIPCHK(hipGetLastError());
-  const size_t stg = L.lds ? static_cast<size_t>(L.F) * L.K * 8 : 0;
-  for (int l = 0; l + 1 < L.top; ++l) {
-    if (L.lds)
-      k_ix_up<true><<<L.n[l + 1], 256, stg, s>>>(tab(l), L.n[l], L.K, L.F, tab(l + 1));
-    else
-      k_ix_up<false><<<L.n[l + 1], 256, 0, s>>>(tab(l), L.n[l], L.K, L.F, tab(l + 1));
-    HIPCHK(hipGetLastError());
-  }
-  HIPCHK(hipMemsetAsync(ent(L.top), 0, 8, s));  // the chain starts at word 0 with 0 messages
-  for (int l = L.top - 1; l >= 0; --l) {
-    if (L.lds)
-      k_ix_down<true><<<L.n[l + 1], 64, stg, s>>>(tab(l), L.n[l], L.K, L.F, ent(l + 1), ent(l));
-    else
-      k_ix_down<false><<<L.n[l + 1], 64, 0, s>>>(tab(l), L.n[l], L.K, L.F, ent(l + 1), ent(l));
-    HIPCHK(hipGetLastError());
-  }
-  k_ix_emit<<<L.nseg, 256, 0, s>>>(s8, len, max_msg_len, ent(0), vlist, vcount, d_offsets,
-                                   max_msgs, reinterpret_cast<unsigned long long *>(d_count), err);
-  HIPCHK(hipGetLastError());
-  return XDRG_OK;
+  return run_index<false>(nullptr, nullptr, d_stream, len, max_msg_len, max_msgs, d_offsets, d_count,
+                          d_ws, ws_bytes, d_status, static_cast<hipStream_t>(stream));
 }
+
+int xdrg_index_records(const xdrg_plan *p, const void *d_xdr, uint64_t len, uint64_t n,
+                       uint32_t max_rec_len, uint64_t *d_offsets, uint64_t *d_count, void *d_ws,
+                       size_t ws_bytes, xdrg_status *d_status, void *stream) {
+  if (!p || !d_offsets || !d_count || !d_status || (len && !d_xdr)) return XDRG_EINVAL;
+  if (max_rec_len > XDRG_INDEX_MAX_MSG) return XDRG_EUNSUPPORTED;
+  if ((d_xdr && !aligned(d_xdr, 4)) || !aligned(d_offsets, 8) || !aligned(d_count, 8)) return XDRG_EALIGN;
+  if (n >= (1ull << 40)) return XDRG_EUNSUPPORTED;
+  if (p->min_record_bytes < 4) return XDRG_EUNSUPPORTED;  // the chain must advance
+  const dev_tables *T = nullptr;
+  if (int rc = plan_upload(p, &T)) return rc;
+  return run_index<true>(p, T, d_xdr, len, max_rec_len, n, d_offsets, d_count, d_ws, ws_bytes, d_status,
+                         static_cast<hipStream_t>(stream));
+}
+
+
 
 int xdrg_decode_msgs(const xdrg_plan *p, const void *d_stream, uint64_t len,
                      const uint64_t *d_offsets, uint64_t n, void *d_native, uint8_t *d_heap_out,
@@ -2249,6 +2410,7 @@ const char *xdrg_error_message(int code) {
   case XDRG_ERR_MSG_MISMATCH: return "record mark does not match the record index";
   case XDRG_ERR_MSG_COUNT: return "more messages than the record index holds";
   case XDRG_ERR_INTERNAL: return "xdrgpu internal error (device wait gave up)";
+  case XDRG_ERR_INDEX_LONG: return "record longer than the device record index window";
   default: return "unknown xdrgpu error";
   }
 }

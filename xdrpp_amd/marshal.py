@@ -264,10 +264,36 @@ class Marshaler:
         e = self.check(s)
         return EncodeResult(out[:e.total_bytes], offsets)
 
+    def index_records(self, xdr: torch.Tensor, n: int, max_rec_len: int | None = None) -> torch.Tensor:
+        """Record index of n records concatenated in `xdr`, on the device
+        (xdrg_index_records): int64 offsets[n + 1] for decode.  Raises
+        XdrRuntimeError (XDRG_ERR_INDEX_LONG) when a record is longer than
+        the index window (max_rec_len, default the plan's largest record
+        up to XDRG_INDEX_MAX_MSG)."""
+        if max_rec_len is None:
+            max_rec_len = min(self.plan.max_record_bytes, A.INDEX_MAX_MSG)
+        L = A.lib()
+        total = xdr.numel()
+        ws = torch.empty(max(L.xdrg_index_workspace_size(total, max_rec_len), 16), dtype=torch.uint8,
+                         device=self.device)
+        offs = torch.empty(n + 1, dtype=torch.int64, device=self.device)
+        cnt = torch.empty(1, dtype=torch.int64, device=self.device)
+        s = _stream()
+        self.status.init(s)
+        A.check(L.xdrg_index_records(self.plan.handle, _ptr(xdr), total, n, max_rec_len, _ptr(offs),
+                                     cnt.data_ptr(), _ptr(ws), ws.numel(), self.status.ptr, s),
+                "xdrg_index_records")
+        self.check(s)
+        return offs
+
     def decode(self, xdr: torch.Tensor, n: int, offsets: torch.Tensor | None = None,
                stack_limit: int = A.DEFAULT_STACK_LIMIT):
         """= xdr_from_opaque(bytes, r0, ..., rn-1) (marshal.h:299-306).
-        Returns (native uint8 tensor [n*stride], heap uint8 tensor or None)."""
+        Var plans without `offsets` index the records on the device first
+        (index_records).  Returns (native uint8 tensor [n*stride], heap
+        uint8 tensor or None)."""
+        if offsets is None and not self.plan.is_fixed:
+            offsets = self.index_records(xdr, n)
         s = _stream()
         native = torch.zeros(max(n, 1) * self.plan.stride, dtype=torch.uint8, device=self.device)
         heap = None
