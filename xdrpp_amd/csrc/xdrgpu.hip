@@ -1100,6 +1100,13 @@ __device__ uint32_t rx_len(const xdrg_op *__restrict__ ops, const uint32_t *__re
     case XDRG_OP_OPAQUE:
       if (lim - p < op.arg0) return past;
       p += (op.arg0 + 3u) & ~3u; ++pc; continue;
+    case XDRG_OP_U32: case XDRG_OP_BOOL:  // any value decodes: no load
+      if (lim - p < 4) return past;
+      p += 4; ++pc; continue;
+    case XDRG_OP_ENUM:
+      if (op.flags & XDRG_F_VALIDATE) break;
+      if (lim - p < 4) return past;
+      p += 4; ++pc; continue;
     default: break;
     }
     if (lim - p < 4) return past;
@@ -1138,17 +1145,34 @@ __device__ uint32_t rx_len(const xdrg_op *__restrict__ ops, const uint32_t *__re
         pc = op.arg4;
       }
       break;
-    default: ++pc; break;  // U32, BOOL
+    default: ++pc; break;
     }
   }
 }
 
-// The plan of a record index, for the segment and emit kernels.
+// The plan of a record index, for the segment and emit kernels.  fpc /
+// fd: the first op whose word is checked (a length, count, discriminant or
+// validated enum) and its byte offset in the record -- every op before it
+// has a fixed size -- or fpc = RX_BAD.  Its check is a necessary condition
+// for a word to start a record: the segment kernel loads that word for all
+// of a thread's candidate starts at once and walks only the ones that pass.
 struct rx_plan {
   const xdrg_op *ops;
   const uint32_t *table;
   uint32_t nops;
+  uint32_t fpc, fd;
 };
+
+__device__ __forceinline__ bool rx_first_ok(const xdrg_op &op, const uint32_t *__restrict__ table,
+                                            uint32_t v) {
+  switch (op.kind) {
+  case XDRG_OP_ENUM: return enum_ok(table, op.arg0, op.arg1, v);
+  case XDRG_OP_UNION:
+    return (!(op.flags & XDRG_F_VALIDATE) || enum_ok(table, op.arg0, op.arg1, v)) &&
+           union_target(op, table, v) >= 0;
+  default: return v <= op.arg0;  // VAROPAQUE, STRING, VECTOR
+  }
+}
 
 // LDS node: target (13 bits: < kIxSW a node of this segment, kIxSW + e =
 // entry e of the next one) | marks passed << 13 (13 bits) | ends << 26.
@@ -1175,6 +1199,16 @@ __global__ __launch_bounds__(256) void k_ix_seg(const uint8_t *__restrict__ s, u
   if (REC) load_ops(reinterpret_cast<xdrg_op *>(rx_smem), rp.ops, rp.nops);
   else ix_load16(s, len, w0, tid, raw);
   const rx_global rd{s};
+  // REC: the first checked word of every candidate start, all in flight
+  // at once; only starts that pass it are walked
+  uint32_t first[16];
+  if (REC) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const uint64_t a = 4 * (w0 + 4u * (tid + 256u * (q >> 2)) + (q & 3));
+      first[q] = rp.fpc == RX_BAD || a + rp.fd + 4 > len ? 0u : ld32(s + a + rp.fd);
+    }
+  }
   uint32_t vmask = 0, vnext[16];
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
@@ -1184,9 +1218,12 @@ __global__ __launch_bounds__(256) void k_ix_seg(const uint8_t *__restrict__ s, u
       const int q = 4 * g + j;
       const uint32_t i = 4u * (tid + 256u * g) + j;
       if (REC) {
+        const xdrg_op *sops = reinterpret_cast<const xdrg_op *>(rx_smem);
         const uint64_t a = 4 * (w0 + i);
-        const uint32_t L =
-            a < len ? rx_len(reinterpret_cast<const xdrg_op *>(rx_smem), rp.table, rd, len, a, maxlen) : RX_BAD;
+        const bool cand = a < len && (rp.fpc == RX_BAD ||
+                                      (a + rp.fd + 4 <= len && rp.fd + 4 <= maxlen &&
+                                       rx_first_ok(sops[rp.fpc], rp.table, bswap32(first[q]))));
+        const uint32_t L = cand ? rx_len(sops, rp.table, rd, len, a, maxlen) : RX_BAD;
         vnext[q] = L < RX_LONG ? i + L / 4u : 0xffffffffu;
       } else {
         vnext[q] = ix_next(raw[q], i, lim, maxlen);
@@ -1976,7 +2013,22 @@ int run_index(const xdrg_plan *p, const dev_tables *T, const void *d_stream, uin
   const ix_layout L = ix_plan(len, max_msg_len);
   if (!d_ws || ws_bytes < L.total) return XDRG_ESPACE;
   if (L.nseg > 0xffffffffull) return XDRG_EUNSUPPORTED;
-  rx_plan rp{REC ? T->d_ops : nullptr, REC ? T->d_table : nullptr, REC ? uint32_t(p->ops.size()) : 0u};
+  rx_plan rp{REC ? T->d_ops : nullptr, REC ? T->d_table : nullptr, REC ? uint32_t(p->ops.size()) : 0u,
+             RX_BAD, 0};
+  if (REC) {  // the first checked op: fixed-size ops before it, no branch
+    uint32_t d = 0;
+    for (uint32_t pc = 0; pc < p->ops.size(); ++pc) {
+      const xdrg_op &o = p->ops[pc];
+      if (o.kind == XDRG_OP_END || o.kind == XDRG_OP_JUMP) break;
+      if (o.kind == XDRG_OP_U64) { d += 8; continue; }
+      if (o.kind == XDRG_OP_OPAQUE) { d += (o.arg0 + 3u) & ~3u; continue; }
+      if (o.kind == XDRG_OP_U32 || o.kind == XDRG_OP_BOOL ||
+          (o.kind == XDRG_OP_ENUM && !(o.flags & XDRG_F_VALIDATE))) { d += 4; continue; }
+      rp.fpc = pc;
+      rp.fd = d;
+      break;
+    }
+  }
   const size_t ops_lds = REC ? p->ops.size() * sizeof(xdrg_op) : 0;
   if (ops_lds > (38u << 10)) return XDRG_EUNSUPPORTED;  // + 25 KiB static: the 64 KiB workgroup LDS
   unsigned long long *err = err_ptr(d_status);
