@@ -150,6 +150,16 @@ struct has_case_values<U, std::void_t<decltype(U::_xdr_case_values())>> : std::t
 
 template <typename T> using plain = std::remove_cv_t<std::remove_reference_t<T>>;
 
+// The declared discriminant type of a union: xdr_traits<U>::discriminant_type
+// (xdrc emits it, gen_hh.cc), else what _xdr_discriminant() returns.
+template <typename U, typename = void> struct discriminant_of {
+  using type = decltype(std::declval<U>()._xdr_discriminant());
+};
+template <typename U>
+struct discriminant_of<U, std::void_t<typename xdr_traits<U>::discriminant_type>> {
+  using type = typename xdr_traits<U>::discriminant_type;
+};
+
 // ---------------------------------------------------------------- sub-plans
 // Ops of one type placed at offset 0, pcs relative to the sub-plan start,
 // depths relative to the level the type is placed at.
@@ -316,13 +326,14 @@ template <typename U> subplan record_union() {
   std::vector<std::int64_t> cand = union_cases<U>::values();
   const bool has_default = union_cases<U>::has_default;
   if constexpr (has_case_values<U>::value) {
-    if (cand.empty()) {  // xdrc lists no cases for unions with a default arm
-      using D = plain<decltype(std::declval<U>()._xdr_discriminant())>;
+    if (cand.empty()) {  // xdrc lists no cases for unions with a default arm:
+      // the tags of the discriminant's enum (xdr_traits<U>::discriminant_type)
+      using D = plain<typename discriminant_of<U>::type>;
       if constexpr (xdr_traits<D>::is_enum)
         for (auto v : xdr_traits<D>::enum_values()) cand.push_back(v);
     }
   }
-  if (cand.empty() && !has_default)
+  if (cand.empty())
     throw std::logic_error("xdr::gpu: cannot enumerate the cases of a union (specialize xdr::gpu::union_cases)");
   std::int64_t probe = 0;
   for (auto v : cand) probe = std::max(probe, v + 1);

@@ -128,7 +128,7 @@ def main() -> int:
         print("build oracle/_ref/ref_golden first (make -C oracle)", file=sys.stderr)
         return 2
     os.makedirs(GOLD, exist_ok=True)
-    manifest = {"generator": "oracle/ref_golden.cc (reference xdrpp/marshal.cc compiled in place)",
+    manifest = {"generator": "oracle/ref_golden.cc (reference xdrpp/marshal.cc + server side compiled in place, genuine xdrc-generated types)",
                 "small": {}, "hashes": {}}
     for schema, n in SMALL.items():
         pre = os.path.join(GOLD, f"{schema}_{n}")

@@ -166,7 +166,7 @@ static void kat(const string &path) {
     o << "  \"recvar_len" << bl << "\": \"" << enc(x) << "\",\n";
   }
   // rpc: one of each arm
-  vector<rpcx::rpc_msg> pv;
+  vector<xdr::rpc_msg> pv;
   gen_rpc(64, WG_SEED_RPC, pv);
   o << "  \"rpc_first64\": [";
   for (size_t i = 0; i < pv.size(); ++i) o << (i ? ", " : "") << "\"" << enc(pv[i]) << "\"";
@@ -218,30 +218,30 @@ static void kat(const string &path) {
   o << "    \"recvar_len_past_end\": "
     << try_decode<recvar>(good_rv, [](xdr::opaque_vec<> &m) { m[15] = 200; }) << ",\n";
   string good_rpc = enc(pv[0]);
-  o << "    \"rpc_ok\": " << try_decode<rpcx::rpc_msg>(good_rpc) << ",\n";
+  o << "    \"rpc_ok\": " << try_decode<xdr::rpc_msg>(good_rpc) << ",\n";
   o << "    \"rpc_bad_mtype\": "
-    << try_decode<rpcx::rpc_msg>(good_rpc, [](xdr::opaque_vec<> &m) { m[7] = 7; }) << ",\n";
+    << try_decode<xdr::rpc_msg>(good_rpc, [](xdr::opaque_vec<> &m) { m[7] = 7; }) << ",\n";
   {
     // a MSG_DENIED reply with a bad reject_stat
-    rpcx::rpc_msg d{};
+    xdr::rpc_msg d{};
     d.xid = 9;
-    d.body.mtype = rpcx::REPLY;
-    d.body.rbody.stat = rpcx::MSG_DENIED;
-    d.body.rbody.rreply.stat = rpcx::AUTH_ERROR;
-    d.body.rbody.rreply.rj_why = 3;
+    d.body.mtype(xdr::REPLY);
+    d.body.rbody().stat(xdr::MSG_DENIED);
+    d.body.rbody().rreply().stat(xdr::AUTH_ERROR);
+    d.body.rbody().rreply().rj_why() = xdr::auth_stat(3);
     string h = enc(d);
-    o << "    \"rpc_denied_ok\": " << try_decode<rpcx::rpc_msg>(h) << ",\n";
+    o << "    \"rpc_denied_ok\": " << try_decode<xdr::rpc_msg>(h) << ",\n";
     o << "    \"rpc_bad_reject_stat\": "
-      << try_decode<rpcx::rpc_msg>(h, [](xdr::opaque_vec<> &m) { m[15] = 5; }) << ",\n";
+      << try_decode<xdr::rpc_msg>(h, [](xdr::opaque_vec<> &m) { m[15] = 5; }) << ",\n";
     o << "    \"rpc_bad_reply_stat\": "
-      << try_decode<rpcx::rpc_msg>(h, [](xdr::opaque_vec<> &m) { m[11] = 2; }) << ",\n";
+      << try_decode<xdr::rpc_msg>(h, [](xdr::opaque_vec<> &m) { m[11] = 2; }) << ",\n";
   }
   {
     // vecrec: id, vals<16> = {5, -6}, opt = {7, 8}, pairs<8> = {(9, true)}, flag
     vecrec x{};
     x.id = 1;
     x.vals = {5, -6};
-    x.opt.activate() = rpcx::mismatch_info{7, 8};
+    x.opt.activate() = ::mismatch_info{7, 8};
     x.pairs.resize(1);
     x.pairs[0].h = 9;
     x.pairs[0].b = true;
@@ -321,17 +321,24 @@ static void bench_one(const char *name, const vector<T> &v, int threads, int rep
 // ref_golden rpc <stream> <offsets> <procs> <xids|-> <outprefix>
 //
 // Every message [off[k], off[k+1]) of the stream goes through the REAL
-// reference decode of its rpc_msg header (xdr_get over the message body,
-// archive(g, hdr): xdrpp/marshal.h:142-211 with the rpc_msg traits of
-// ref_schemas.hh), then
-//  * the server's routing, restated line for line from
-//    rpc_server_base::dispatch (xdrpp/server.cc:84-107) over a servers_-shaped
-//    map (server.h:218-219), plus call_dispatch's case test (srpc.h:125-127);
-//  * the client's check_call_hdr (rpc_msg.cc:115-131) + xid test (srpc.h:61-66);
-//  * the error replies, built exactly as server.cc:8-67 builds them (real
-//    message_t::alloc + xdr_put).
+// reference paths, compiled from /root/reference against the generated
+// xdrpp/rpc_msg.hh (oracle/Makefile):
+//  * the header decode, archive(g, hdr) with xdr_get over the message body
+//    (xdrpp/marshal.h:142-211), for the fields of xdrg_rpc_hdr;
+//  * the server: rpc_server_base::dispatch (xdrpp/server.cc:78-117) with a
+//    service registered for every (prog, vers) of the procedure table; a
+//    service's process() is srpc_service::process (xdrpp/srpc.h:121-128)
+//    whose call_dispatch knows the table's procedures.  The reply dispatch
+//    sends -- built by the real rpc_*_msg, server.cc:8-67 -- is the
+//    fixture's reply, and its words name the action;
+//  * the client: the real check_call_hdr (xdrpp/rpc_msg.cc:114-131) + the
+//    xid test of srpc.h:61-66.
 // Writes <outprefix>.hdrs / .chk (xdrg_rpc_hdr per message, server / client
 // classification) and .replies / .replyoffs.
+#include <xdrpp/exception.h>
+#include <xdrpp/server.h>
+
+#include <iostream>
 #include <map>
 #include <set>
 
@@ -347,41 +354,25 @@ static vector<uint8_t> slurp(const string &path) {
 }
 
 namespace rpcref {
-using namespace rpcx;
-// server.cc:8-22
-static xdr::msg_ptr accepted_error_msg(uint32_t xid, int32_t stat) {
-  xdr::msg_ptr buf(xdr::message_t::alloc(24));
-  xdr::xdr_put p(buf);
-  p(xid); p(int32_t(REPLY)); p(int32_t(MSG_ACCEPTED)); p(int32_t(AUTH_NONE)); p(uint32_t(0)); p(stat);
-  if (p.p_ != p.e_) die("accepted_error_msg size");
-  return buf;
-}
-// server.cc:24-39
-static xdr::msg_ptr prog_mismatch_msg(uint32_t xid, uint32_t low, uint32_t high) {
-  xdr::msg_ptr buf(xdr::message_t::alloc(32));
-  xdr::xdr_put p(buf);
-  p(xid); p(int32_t(REPLY)); p(int32_t(MSG_ACCEPTED)); p(int32_t(AUTH_NONE)); p(uint32_t(0));
-  p(int32_t(PROG_MISMATCH)); p(low); p(high);
-  if (p.p_ != p.e_) die("prog_mismatch_msg size");
-  return buf;
-}
-// server.cc:41-53
-static xdr::msg_ptr auth_error_msg(uint32_t xid, int32_t stat) {
-  xdr::msg_ptr buf(xdr::message_t::alloc(20));
-  xdr::xdr_put p(buf);
-  p(xid); p(int32_t(REPLY)); p(int32_t(MSG_DENIED)); p(int32_t(AUTH_ERROR)); p(stat);
-  if (p.p_ != p.e_) die("auth_error_msg size");
-  return buf;
-}
-// server.cc:55-68
-static xdr::msg_ptr rpc_mismatch_msg(uint32_t xid) {
-  xdr::msg_ptr buf(xdr::message_t::alloc(24));
-  xdr::xdr_put p(buf);
-  p(xid); p(int32_t(REPLY)); p(int32_t(MSG_DENIED)); p(int32_t(RPC_MISMATCH)); p(uint32_t(2));
-  p(uint32_t(2));
-  if (p.p_ != p.e_) die("rpc_mismatch_msg size");
-  return buf;
-}
+// srpc_service::process (srpc.h:121-128) for an interface whose
+// call_dispatch has a case for each procedure in `procs`.
+struct table_service : xdr::service_base {
+  std::set<uint32_t> procs;
+  bool *dispatched;
+  table_service(uint32_t prog, uint32_t vers, std::set<uint32_t> p, bool *d)
+      : service_base(prog, vers), procs(std::move(p)), dispatched(d) {}
+  void process(void *, xdr::rpc_msg &hdr, xdr::xdr_get &, cb_t reply) override {
+    if (!check_call(hdr)) reply(nullptr);
+    if (procs.count(hdr.body.cbody().proc)) {
+      *dispatched = true;  // call_dispatch's case: the procedure runs
+      return;
+    }
+    reply(xdr::rpc_accepted_error_msg(hdr.xid, xdr::PROC_UNAVAIL));
+  }
+};
+struct table_server : xdr::rpc_server_base {
+  void add(table_service *s) { register_service_base(s); }
+};
 
 static uint8_t err_code(const std::exception &e, const string &w, uint32_t *site) {
   *site = 0;
@@ -401,7 +392,6 @@ static uint8_t err_code(const std::exception &e, const string &w, uint32_t *site
 
 static void rpc_mode(const string &sp, const string &op, const string &pp, const string &xp,
                      const string &pre) {
-  using namespace rpcx;
   vector<uint8_t> sb = slurp(sp), ob = slurp(op), pb = slurp(pp), xb;
   if (xp != "-") xb = slurp(xp);
   // 4-byte aligned copy of the stream (xdr_get asserts an aligned start)
@@ -412,12 +402,15 @@ static void rpc_mode(const string &sp, const string &op, const string &pp, const
   const size_t n = ob.size() / 8 - 1;
   const xdrg_rpc_proc *pt = reinterpret_cast<const xdrg_rpc_proc *>(pb.data());
   const size_t np = pb.size() / sizeof(xdrg_rpc_proc);
-  // servers_: prog -> vers -> the service's procedure set (call_dispatch cases)
-  std::map<uint32_t, std::map<uint32_t, std::set<uint32_t>>> servers;
+  std::map<std::pair<uint32_t, uint32_t>, std::set<uint32_t>> ifaces;
   for (size_t i = 0; i < np; ++i) {
-    auto &procs = servers[pt[i].prog][pt[i].vers];
+    auto &procs = ifaces[{pt[i].prog, pt[i].vers}];
     if (!(pt[i].flags & XDRG_RPC_PROC_IFACE_ONLY)) procs.insert(pt[i].proc);
   }
+  bool dispatched = false;
+  rpcref::table_server server;
+  for (auto &f : ifaces) server.add(new rpcref::table_service(f.first.first, f.first.second, f.second, &dispatched));
+  std::streambuf *cerr_buf = std::cerr.rdbuf(nullptr);  // dispatch's diagnostics
   vector<xdrg_rpc_hdr> hs(n), cs(n);
   vector<uint8_t> rep;
   vector<uint64_t> roff(n + 1, 0);
@@ -426,7 +419,7 @@ static void rpc_mode(const string &sp, const string &op, const string &pp, const
     xdrg_rpc_hdr h;
     memset(&h, 0, sizeof h);
     h.end = m1;
-    rpc_msg hdr{};
+    xdr::rpc_msg hdr;
     uint8_t err = 0;
     uint32_t site = 0;
     try {
@@ -438,9 +431,9 @@ static void rpc_mode(const string &sp, const string &op, const string &pp, const
     }
     if (!err) {
       h.xid = hdr.xid;
-      h.mtype = uint8_t(hdr.body.mtype);
-      if (hdr.body.mtype == CALL) {
-        const call_body &cb = hdr.body.cbody;
+      h.mtype = uint8_t(hdr.body.mtype());
+      if (hdr.body.mtype() == xdr::CALL) {
+        const xdr::call_body &cb = hdr.body.cbody();
         h.w[XDRG_RPC_W_RPCVERS] = cb.rpcvers; h.w[XDRG_RPC_W_PROG] = cb.prog;
         h.w[XDRG_RPC_W_VERS] = cb.vers; h.w[XDRG_RPC_W_PROC] = cb.proc;
         h.w[XDRG_RPC_W_CRED_FLAVOR] = uint32_t(cb.cred.flavor);
@@ -448,23 +441,23 @@ static void rpc_mode(const string &sp, const string &op, const string &pp, const
         h.cred_len = uint32_t(cb.cred.body.size());
         h.verf_len = uint32_t(cb.verf.body.size());
       } else {
-        const reply_body &rb = hdr.body.rbody;
-        h.w[XDRG_RPC_W_REPLY_STAT] = uint32_t(rb.stat);
-        if (rb.stat == MSG_ACCEPTED) {
-          h.w[XDRG_RPC_W_VERF_FLAVOR] = uint32_t(rb.areply.verf.flavor);
-          h.verf_len = uint32_t(rb.areply.verf.body.size());
-          h.w[XDRG_RPC_W_STAT] = uint32_t(rb.areply.reply_data.stat);
-          if (rb.areply.reply_data.stat == PROG_MISMATCH) {
-            h.w[XDRG_RPC_W_LOW] = rb.areply.reply_data.mismatch_info_.low;
-            h.w[XDRG_RPC_W_HIGH] = rb.areply.reply_data.mismatch_info_.high;
+        const xdr::reply_body &rb = hdr.body.rbody();
+        h.w[XDRG_RPC_W_REPLY_STAT] = uint32_t(rb.stat());
+        if (rb.stat() == xdr::MSG_ACCEPTED) {
+          h.w[XDRG_RPC_W_VERF_FLAVOR] = uint32_t(rb.areply().verf.flavor);
+          h.verf_len = uint32_t(rb.areply().verf.body.size());
+          h.w[XDRG_RPC_W_STAT] = uint32_t(rb.areply().reply_data.stat());
+          if (rb.areply().reply_data.stat() == xdr::PROG_MISMATCH) {
+            h.w[XDRG_RPC_W_LOW] = rb.areply().reply_data.mismatch_info().low;
+            h.w[XDRG_RPC_W_HIGH] = rb.areply().reply_data.mismatch_info().high;
           }
         } else {
-          h.w[XDRG_RPC_W_STAT] = uint32_t(rb.rreply.stat);
-          if (rb.rreply.stat == RPC_MISMATCH) {
-            h.w[XDRG_RPC_W_LOW] = rb.rreply.mismatch_info_.low;
-            h.w[XDRG_RPC_W_HIGH] = rb.rreply.mismatch_info_.high;
+          h.w[XDRG_RPC_W_STAT] = uint32_t(rb.rreply().stat());
+          if (rb.rreply().stat() == xdr::RPC_MISMATCH) {
+            h.w[XDRG_RPC_W_LOW] = rb.rreply().mismatch_info().low;
+            h.w[XDRG_RPC_W_HIGH] = rb.rreply().mismatch_info().high;
           } else {
-            h.w[XDRG_RPC_W_WHY] = uint32_t(rb.rreply.rj_why);
+            h.w[XDRG_RPC_W_WHY] = uint32_t(rb.rreply().rj_why());
           }
         }
       }
@@ -472,62 +465,72 @@ static void rpc_mode(const string &sp, const string &op, const string &pp, const
       h.err = err;
       h.w[0] = site;
     }
-    // ---- server: rpc_server_base::dispatch (server.cc:84-107)
+    // ---- server: the real rpc_server_base::dispatch
     xdrg_rpc_hdr sv = h;
+    xdr::msg_ptr m = xdr::message_t::alloc(m1 - m0 - 4);
+    memcpy(m->data(), s + m0 + 4, m1 - m0 - 4);
     xdr::msg_ptr reply;
-    if (err) sv.action = XDRG_RPC_DROP_MALFORMED;
-    else if (hdr.body.mtype != CALL) sv.action = XDRG_RPC_DROP_NONCALL;
-    else if (hdr.body.cbody.rpcvers != 2) {
-      sv.action = XDRG_RPC_RPC_MISMATCH;
-      reply = rpcref::rpc_mismatch_msg(hdr.xid);
-    } else {
-      auto prog = servers.find(hdr.body.cbody.prog);
-      if (prog == servers.end()) {
-        sv.action = XDRG_RPC_PROG_UNAVAIL;
-        reply = rpcref::accepted_error_msg(hdr.xid, PROG_UNAVAIL);
+    dispatched = false;
+    server.dispatch(nullptr, std::move(m), [&](xdr::msg_ptr r) { reply = std::move(r); });
+    if (dispatched) {
+      sv.action = XDRG_RPC_DISPATCH;
+    } else if (reply) {  // words: xid REPLY reply_stat ...
+      auto w = [&](size_t i) { return __builtin_bswap32(reinterpret_cast<const uint32_t *>(reply->data())[i]); };
+      if (w(2) == xdr::MSG_DENIED) {
+        if (w(3) != xdr::RPC_MISMATCH) die("unexpected denied reply");
+        sv.action = XDRG_RPC_RPC_MISMATCH;
       } else {
-        auto vers = prog->second.find(hdr.body.cbody.vers);
-        if (vers == prog->second.end()) {
-          uint32_t low = prog->second.cbegin()->first;
-          uint32_t high = prog->second.crbegin()->first;
+        switch (w(5)) {  // accept_stat after the AUTH_NONE verifier
+        case xdr::PROG_UNAVAIL: sv.action = XDRG_RPC_PROG_UNAVAIL; break;
+        case xdr::PROG_MISMATCH:
           sv.action = XDRG_RPC_PROG_MISMATCH;
-          sv.w[XDRG_RPC_W_LOW] = low;
-          sv.w[XDRG_RPC_W_HIGH] = high;
-          reply = rpcref::prog_mismatch_msg(hdr.xid, low, high);
-        } else if (!vers->second.count(hdr.body.cbody.proc)) {  // call_dispatch false
-          sv.action = XDRG_RPC_PROC_UNAVAIL;
-          reply = rpcref::accepted_error_msg(hdr.xid, 3 /* PROC_UNAVAIL */);
-        } else {
-          sv.action = XDRG_RPC_DISPATCH;
+          sv.w[XDRG_RPC_W_LOW] = w(6);
+          sv.w[XDRG_RPC_W_HIGH] = w(7);
+          break;
+        case xdr::PROC_UNAVAIL: sv.action = XDRG_RPC_PROC_UNAVAIL; break;
+        case xdr::GARBAGE_ARGS: sv.action = XDRG_RPC_GARBAGE_ARGS; break;
+        default: die("unexpected accepted reply");
         }
       }
+    } else {  // dispatch dropped the message
+      sv.action = err ? XDRG_RPC_DROP_MALFORMED : XDRG_RPC_DROP_NONCALL;
     }
     hs[k] = sv;
     if (reply)
       rep.insert(rep.end(), reinterpret_cast<const uint8_t *>(reply->raw_data()),
                  reinterpret_cast<const uint8_t *>(reply->raw_data()) + reply->raw_size());
     roff[k + 1] = rep.size();
-    // ---- client: archive(g, hdr); check_call_hdr(hdr); xid (srpc.h:61-66)
+    // ---- client: archive(g, hdr); the real check_call_hdr; xid (srpc.h:61-66)
     xdrg_rpc_hdr cl = h;
-    if (err) cl.action = XDRG_RPCR_MALFORMED;
-    else if (hdr.body.mtype != REPLY) cl.action = XDRG_RPCR_NOT_REPLY;
-    else if (hdr.body.rbody.stat == MSG_ACCEPTED)
-      cl.action = hdr.body.rbody.areply.reply_data.stat == SUCCESS ? XDRG_RPCR_OK
-                                                                  : XDRG_RPCR_ACCEPT_STAT;
-    else
-      cl.action = hdr.body.rbody.rreply.stat == AUTH_ERROR ? XDRG_RPCR_AUTH_STAT
-                                                            : XDRG_RPCR_RPCVERS_MISMATCH;
+    if (err) {
+      cl.action = XDRG_RPCR_MALFORMED;
+    } else {
+      try {
+        xdr::check_call_hdr(hdr);
+        cl.action = XDRG_RPCR_OK;
+      } catch (const xdr::xdr_call_error &e) {
+        switch (e.stat_.type_) {
+        case xdr::rpc_call_stat::ACCEPT_STAT: cl.action = XDRG_RPCR_ACCEPT_STAT; break;
+        case xdr::rpc_call_stat::AUTH_STAT: cl.action = XDRG_RPCR_AUTH_STAT; break;
+        case xdr::rpc_call_stat::RPCVERS_MISMATCH: cl.action = XDRG_RPCR_RPCVERS_MISMATCH; break;
+        default: die("unexpected call error");
+        }
+      } catch (const xdr::xdr_runtime_error &) {
+        cl.action = XDRG_RPCR_NOT_REPLY;  // "call received when reply expected"
+      }
+    }
     if (cl.action == XDRG_RPCR_OK && !xb.empty() &&
         reinterpret_cast<const uint32_t *>(xb.data())[k] != hdr.xid)
       cl.action = XDRG_RPCR_BAD_XID;
     cs[k] = cl;
   }
+  std::cerr.rdbuf(cerr_buf);
   write_file(pre + ".hdrs", hs.data(), hs.size() * sizeof(xdrg_rpc_hdr));
   write_file(pre + ".chk", cs.data(), cs.size() * sizeof(xdrg_rpc_hdr));
   write_file(pre + ".replies", rep.data(), rep.size());
   write_file(pre + ".replyoffs", roff.data(), roff.size() * 8);
   // the auth-error reply has no dispatch route; one known answer of it
-  xdr::msg_ptr ae = rpcref::auth_error_msg(0x01020304u, 5);
+  xdr::msg_ptr ae = xdr::rpc_auth_error_msg(0x01020304u, xdr::auth_stat(5));
   write_file(pre + ".autherr", ae->raw_data(), ae->raw_size());
 }
 
@@ -571,7 +574,7 @@ int main(int argc, char **argv) {
     else if (schema == "rec128_mgpu") { vector<rec128> v; gen_rec128(n, WG_SEED_REC128_MGPU, 0, v); emit(v, pre, wm); }
     else if (schema == "recvar") { vector<recvar> v; gen_recvar(n, WG_SEED_RECVAR, v); emit(v, pre, wm); }
     else if (schema == "vecrec") { vector<vecrec> v; gen_vecrec(n, WG_SEED_VECREC, v); emit(v, pre, wm); }
-    else if (schema == "rpc") { vector<rpcx::rpc_msg> v; gen_rpc(n, WG_SEED_RPC, v); emit(v, pre, wm); }
+    else if (schema == "rpc") { vector<xdr::rpc_msg> v; gen_rpc(n, WG_SEED_RPC, v); emit(v, pre, wm); }
     else die("unknown schema " + schema);
     return 0;
   }
@@ -582,7 +585,7 @@ int main(int argc, char **argv) {
     else if (schema == "rec128") { vector<rec128> v; gen_rec128(n, WG_SEED_REC128, 0, v); depths_of(v, o); }
     else if (schema == "recvar") { vector<recvar> v; gen_recvar(n, WG_SEED_RECVAR, v); depths_of(v, o); }
     else if (schema == "vecrec") { vector<vecrec> v; gen_vecrec(n, WG_SEED_VECREC, v); depths_of(v, o); }
-    else if (schema == "rpc") { vector<rpcx::rpc_msg> v; gen_rpc(n, WG_SEED_RPC, v); depths_of(v, o); }
+    else if (schema == "rpc") { vector<xdr::rpc_msg> v; gen_rpc(n, WG_SEED_RPC, v); depths_of(v, o); }
     else die("unknown schema " + schema);
     return 0;
   }
@@ -593,7 +596,7 @@ int main(int argc, char **argv) {
     else if (schema == "numerics") { vector<testns::numerics> v; gen_numerics(n, WG_SEED_NUMERICS, v); bench_one("numerics", v, threads, reps); }
     else if (schema == "recvar") { vector<recvar> v; gen_recvar(n, WG_SEED_RECVAR, v); bench_one("recvar", v, threads, reps); }
     else if (schema == "vecrec") { vector<vecrec> v; gen_vecrec(n, WG_SEED_VECREC, v); bench_one("vecrec", v, threads, reps); }
-    else if (schema == "rpc") { vector<rpcx::rpc_msg> v; gen_rpc(n, WG_SEED_RPC, v); bench_one("rpc", v, threads, reps); }
+    else if (schema == "rpc") { vector<xdr::rpc_msg> v; gen_rpc(n, WG_SEED_RPC, v); bench_one("rpc", v, threads, reps); }
     else die("unknown schema " + schema);
     return 0;
   }

@@ -1,12 +1,13 @@
 // ORACLE / TEST INFRASTRUCTURE ONLY.
 //
-// C++ record objects of the four benchmark schemas (oracle/ref_schemas.hh)
-// built from the synthetic generator (oracle/workload_gen.h), their staged
-// device layout, and equality helpers.  Shared by ref_golden.cc and the
-// C++ drop-in test (tests/cpp/dropin_test.cc).
+// C++ record objects of the benchmark schemas -- genuine xdrc-generated
+// types (oracle/ref_types.hh) -- built from the synthetic generator
+// (oracle/workload_gen.h), their staged device layout, and equality
+// helpers.  Shared by ref_golden.cc and the C++ drop-in test
+// (tests/cpp/dropin_test.cc).
 #ifndef XDRG_REF_OBJECTS_HH
 #define XDRG_REF_OBJECTS_HH
-#include "ref_schemas.hh"
+#include "ref_types.hh"
 #include "workload_gen.h"
 
 #include <cstdio>
@@ -115,7 +116,7 @@ template <typename T> [[maybe_unused]] static T bits_as(uint64_t v) {
     for (uint32_t j = 0; j < nv; ++j) x.vals[j] = (int32_t)(uint32_t)wg_draw(ps, r * 32 + j);
     if (d[2] & 1) {
       const uint64_t w = wg_draw(ps, r * 32 + 16);
-      x.opt.activate() = rpcx::mismatch_info{(uint32_t)w, (uint32_t)(w >> 32)};
+      x.opt.activate() = ::mismatch_info{(uint32_t)w, (uint32_t)(w >> 32)};
     } else {
       x.opt.reset();
     }
@@ -128,26 +129,26 @@ template <typename T> [[maybe_unused]] static T bits_as(uint64_t v) {
   }
 }
 
-[[maybe_unused]] static void fill_auth(rpcx::opaque_auth &a, int32_t flavor, uint32_t len, uint64_t ps,
+[[maybe_unused]] static void fill_auth(xdr::opaque_auth &a, int32_t flavor, uint32_t len, uint64_t ps,
                       uint64_t word0) {
-  a.flavor = flavor;
+  a.flavor = xdr::auth_flavor(flavor);
   a.body.resize(len);
   for (uint32_t j = 0; j < len; ++j) a.body[j] = wg_byte(ps, word0 + j / 8, j);
 }
 
-[[maybe_unused]] static void gen_rpc(size_t n, uint64_t seed, vector<rpcx::rpc_msg> &v) {
+[[maybe_unused]] static void gen_rpc(size_t n, uint64_t seed, vector<xdr::rpc_msg> &v) {
   v.resize(n);
   const uint64_t ps = seed ^ WG_PAYLOAD_XOR;
   for (size_t r = 0; r < n; ++r) {
     uint64_t d[16];
     for (int k = 0; k < 16; ++k) d[k] = wg_draw(seed, r * 16 + k);
-    rpcx::rpc_msg &m = v[r];
-    m = rpcx::rpc_msg{};
+    xdr::rpc_msg &m = v[r];
+    m = xdr::rpc_msg{};
     m.xid = (uint32_t)d[0];
     unsigned sel = d[1] % 10;
     if (sel <= WG_RPC_CALL_MAX) {
-      m.body.mtype = rpcx::CALL;
-      rpcx::call_body &c = m.body.cbody;
+      m.body.mtype(xdr::CALL);
+      xdr::call_body &c = m.body.cbody();
       c.rpcvers = 2;
       c.prog = (uint32_t)d[2];
       c.vers = (uint32_t)d[3];
@@ -155,27 +156,27 @@ template <typename T> [[maybe_unused]] static T bits_as(uint64_t v) {
       fill_auth(c.cred, int32_t(d[5] % 2), d[6] % 401, ps, r * 128);
       fill_auth(c.verf, int32_t(d[7] % 2), d[8] % 401, ps, r * 128 + 64);
     } else {
-      m.body.mtype = rpcx::REPLY;
-      rpcx::reply_body &b = m.body.rbody;
+      m.body.mtype(xdr::REPLY);
+      xdr::reply_body &b = m.body.rbody();
       if (sel <= WG_RPC_PROG_UNAVAIL) {
-        b.stat = rpcx::MSG_ACCEPTED;
-        fill_auth(b.areply.verf, int32_t(d[5] % 2), d[6] % 41, ps, r * 128 + 64);
-        rpcx::reply_data_u &rd = b.areply.reply_data;
-        if (sel == WG_RPC_SUCCESS) rd.stat = rpcx::SUCCESS;
+        b.stat(xdr::MSG_ACCEPTED);
+        fill_auth(b.areply().verf, int32_t(d[5] % 2), d[6] % 41, ps, r * 128 + 64);
+        auto &rd = b.areply().reply_data;
+        if (sel == WG_RPC_SUCCESS) rd.stat(xdr::SUCCESS);
         else if (sel == WG_RPC_PROG_MISMATCH) {
-          rd.stat = rpcx::PROG_MISMATCH;
-          rd.mismatch_info_.low = (uint32_t)d[9];
-          rd.mismatch_info_.high = (uint32_t)d[10];
-        } else rd.stat = rpcx::PROG_UNAVAIL;
+          rd.stat(xdr::PROG_MISMATCH);
+          rd.mismatch_info().low = (uint32_t)d[9];
+          rd.mismatch_info().high = (uint32_t)d[10];
+        } else rd.stat(xdr::PROG_UNAVAIL);
       } else {
-        b.stat = rpcx::MSG_DENIED;
+        b.stat(xdr::MSG_DENIED);
         if (sel == WG_RPC_RPC_MISMATCH) {
-          b.rreply.stat = rpcx::RPC_MISMATCH;
-          b.rreply.mismatch_info_.low = (uint32_t)d[9];
-          b.rreply.mismatch_info_.high = (uint32_t)d[10];
+          b.rreply().stat(xdr::RPC_MISMATCH);
+          b.rreply().mismatch_info().low = (uint32_t)d[9];
+          b.rreply().mismatch_info().high = (uint32_t)d[10];
         } else {
-          b.rreply.stat = rpcx::AUTH_ERROR;
-          b.rreply.rj_why = int32_t(d[11] % 15);
+          b.rreply().stat(xdr::AUTH_ERROR);
+          b.rreply().rj_why() = xdr::auth_stat(d[11] % 15);
         }
       }
     }
@@ -221,44 +222,46 @@ struct heap_t {
     s[r].score = v[r].score;
   }
 }
-[[maybe_unused]] static void stage_auth(const rpcx::opaque_auth &a, st_opaque_auth &s, heap_t &h) {
+[[maybe_unused]] static void stage_auth(const xdr::opaque_auth &a, st_opaque_auth &s, heap_t &h) {
   s.flavor = a.flavor;
   s.body = h.put(a.body.data(), a.body.size());
 }
-[[maybe_unused]] static void stage(const vector<rpcx::rpc_msg> &v, vector<uint8_t> &nat, heap_t &h) {
+[[maybe_unused]] static void stage(const vector<xdr::rpc_msg> &v, vector<uint8_t> &nat, heap_t &h) {
   nat.assign(v.size() * sizeof(st_rpc_msg), 0);
   st_rpc_msg *s = reinterpret_cast<st_rpc_msg *>(nat.data());
   for (size_t r = 0; r < v.size(); ++r) {
-    const rpcx::rpc_msg &m = v[r];
+    const xdr::rpc_msg &m = v[r];
     s[r].xid = m.xid;
-    s[r].body.mtype = m.body.mtype;
-    if (m.body.mtype == rpcx::CALL) {
+    s[r].body.mtype = m.body.mtype();
+    if (m.body.mtype() == xdr::CALL) {
+      const xdr::call_body &mc = m.body.cbody();
       st_call_body &c = s[r].body.u.cbody;
-      c.rpcvers = m.body.cbody.rpcvers;
-      c.prog = m.body.cbody.prog;
-      c.vers = m.body.cbody.vers;
-      c.proc = m.body.cbody.proc;
-      stage_auth(m.body.cbody.cred, c.cred, h);
-      stage_auth(m.body.cbody.verf, c.verf, h);
+      c.rpcvers = mc.rpcvers;
+      c.prog = mc.prog;
+      c.vers = mc.vers;
+      c.proc = mc.proc;
+      stage_auth(mc.cred, c.cred, h);
+      stage_auth(mc.verf, c.verf, h);
     } else {
+      const xdr::reply_body &mb = m.body.rbody();
       st_reply_body &b = s[r].body.u.rbody;
-      b.stat = m.body.rbody.stat;
-      if (b.stat == rpcx::MSG_ACCEPTED) {
-        const rpcx::accepted_reply &a = m.body.rbody.areply;
+      b.stat = mb.stat();
+      if (mb.stat() == xdr::MSG_ACCEPTED) {
+        const xdr::accepted_reply &a = mb.areply();
         stage_auth(a.verf, b.u.areply.verf, h);
-        b.u.areply.reply_data.stat = a.reply_data.stat;
-        if (a.reply_data.stat == rpcx::PROG_MISMATCH) {
-          b.u.areply.reply_data.u.mismatch_info.low = a.reply_data.mismatch_info_.low;
-          b.u.areply.reply_data.u.mismatch_info.high = a.reply_data.mismatch_info_.high;
+        b.u.areply.reply_data.stat = a.reply_data.stat();
+        if (a.reply_data.stat() == xdr::PROG_MISMATCH) {
+          b.u.areply.reply_data.u.mismatch_info.low = a.reply_data.mismatch_info().low;
+          b.u.areply.reply_data.u.mismatch_info.high = a.reply_data.mismatch_info().high;
         }
       } else {
-        const rpcx::rejected_reply &j = m.body.rbody.rreply;
-        b.u.rreply.stat = j.stat;
-        if (j.stat == rpcx::RPC_MISMATCH) {
-          b.u.rreply.u.mismatch_info.low = j.mismatch_info_.low;
-          b.u.rreply.u.mismatch_info.high = j.mismatch_info_.high;
+        const xdr::rejected_reply &j = mb.rreply();
+        b.u.rreply.stat = j.stat();
+        if (j.stat() == xdr::RPC_MISMATCH) {
+          b.u.rreply.u.mismatch_info.low = j.mismatch_info().low;
+          b.u.rreply.u.mismatch_info.high = j.mismatch_info().high;
         } else
-          b.u.rreply.u.rj_why = j.rj_why;
+          b.u.rreply.u.rj_why = j.rj_why();
       }
     }
   }
@@ -298,7 +301,7 @@ struct heap_t {
 [[maybe_unused]] static bool same(const vecrec &a, const vecrec &b) {
   return xdr::xdr_to_opaque(a) == xdr::xdr_to_opaque(b);
 }
-[[maybe_unused]] static bool same(const rpcx::rpc_msg &a, const rpcx::rpc_msg &b) {
+[[maybe_unused]] static bool same(const xdr::rpc_msg &a, const xdr::rpc_msg &b) {
   return xdr::xdr_to_opaque(a) == xdr::xdr_to_opaque(b);
 }
 

@@ -81,30 +81,9 @@ void validate(const vnest &v) {
 
 using namespace refobj;
 
-// The hand-expanded unions of oracle/ref_schemas.hh are plain structs with
-// switch-based traits (no xdrc union helpers): name their cases here.
-namespace xdr {
-namespace gpu {
-template <> struct union_cases<rpcx::body_u> {
-  static std::vector<std::int64_t> values() { return {rpcx::CALL, rpcx::REPLY}; }
-  static constexpr bool has_default = false;
-};
-template <> struct union_cases<rpcx::reply_body> {
-  static std::vector<std::int64_t> values() { return {rpcx::MSG_ACCEPTED, rpcx::MSG_DENIED}; }
-  static constexpr bool has_default = false;
-};
-template <> struct union_cases<rpcx::reply_data_u> {
-  static std::vector<std::int64_t> values() {
-    return {rpcx::SUCCESS, rpcx::PROG_UNAVAIL, rpcx::PROG_MISMATCH};
-  }
-  static constexpr bool has_default = true;
-};
-template <> struct union_cases<rpcx::rejected_reply> {
-  static std::vector<std::int64_t> values() { return {rpcx::RPC_MISMATCH, rpcx::AUTH_ERROR}; }
-  static constexpr bool has_default = false;
-};
-}  // namespace gpu
-}  // namespace xdr
+// The record types are genuine xdrc output (oracle/ref_types.hh): the
+// recorder enumerates their unions' cases from _xdr_case_values()
+// (xdrc/gen_hh.cc:410-432) -- no union_cases specializations.
 
 static int failures = 0;
 #define CHECK(c, ...)                                  \
@@ -330,24 +309,24 @@ static void check_error(const char *label, const std::vector<std::uint8_t> &byte
 }
 
 static void gpu_errors() {
-  std::vector<rpcx::rpc_msg> m;
+  std::vector<xdr::rpc_msg> m;
   gen_rpc(64, WG_SEED_RPC, m);
   std::vector<std::uint64_t> off;
   std::vector<std::uint8_t> s = ref_stream(m, off);
   {  // unknown mtype in record 5
     auto x = s;
     x[off[5] + 7] = 7;
-    check_error<rpcx::rpc_msg>("rpc bad mtype", x, m.size());
+    check_error<xdr::rpc_msg>("rpc bad mtype", x, m.size());
   }
   {  // trailing bytes
     auto x = s;
     x.insert(x.end(), {0, 0, 0, 0});
-    check_error<rpcx::rpc_msg>("rpc trailing", x, m.size());
+    check_error<xdr::rpc_msg>("rpc trailing", x, m.size());
   }
   {  // truncated stream
     auto x = s;
     x.resize(x.size() - 8);
-    check_error<rpcx::rpc_msg>("rpc short", x, m.size());
+    check_error<xdr::rpc_msg>("rpc short", x, m.size());
   }
   std::vector<recvar> r;
   gen_recvar(32, WG_SEED_RECVAR, r);
@@ -462,7 +441,7 @@ int main(int argc, char **argv) {
   std::vector<testns::numerics> nu;
   std::vector<rec128> rc;
   std::vector<recvar> rv;
-  std::vector<rpcx::rpc_msg> rp;
+  std::vector<xdr::rpc_msg> rp;
   std::vector<vecrec> vr;
   gen_vecrec(1024, WG_SEED_VECREC, vr);
   gen_numerics(1000, WG_SEED_NUMERICS, nu);
@@ -475,7 +454,7 @@ int main(int argc, char **argv) {
     write_plan<testns_v::numerics>(dir, "numerics_validated");
     write_plan<rec128>(dir, "rec128");
     write_plan<recvar>(dir, "recvar");
-    write_plan<rpcx::rpc_msg>(dir, "rpc");
+    write_plan<xdr::rpc_msg>(dir, "rpc");
     write_plan<vecrec>(dir, "vecrec");
   } else if (mode == "stage") {
     check_stage("numerics", nu);
