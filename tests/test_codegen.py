@@ -3,6 +3,7 @@ codegen.cpp emits for a plan, and its compile for gfx950 with hiprtc (no
 device needed).  The GPU parity of the compiled kernels is in
 tests/test_gpu_parity.py / test_gpu_messages.py ("specialized")."""
 import ctypes as C
+import os
 
 import pytest
 
@@ -49,5 +50,40 @@ def test_source_compiles_for_gfx950(name):
     rc = L.xdrg_plan_build_kernels(p.handle)
     assert rc == A.OK, L.xdrg_last_hip_error().decode()
     info = A.XdrgPlanInfo()
+    A.check(L.xdrg_plan_get_info(p.handle, C.byref(info)), "xdrg_plan_get_info")
+    assert info.specialized == 1
+
+
+# ------------------------------------------------- ahead-of-time code objects
+AOT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "xdrpp_amd", "aot")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["recvar", "rpc", "vecrec"])
+def test_aot_code_object_runs(dev, name):
+    """The emitted source compiled ahead of time by hipcc --genco
+    (xdrpp_amd/build.py aot_kernels), attached with xdrg_plan_load_kernels:
+    its encode reproduces the reference's bytes, its decode reads them back."""
+    import numpy as np
+    import torch
+    from conftest import golden
+    co = os.path.join(AOT, f"{name}.co")
+    if not os.path.exists(co):
+        pytest.skip("aot code objects not built")
+    code = open(co, "rb").read()
+    p = M.Plan(S.ALL[name])
+    L = A.lib()
+    assert L.xdrg_plan_load_kernels(p.handle, code, len(code)) == A.OK
+    info = A.XdrgPlanInfo()
+    A.check(L.xdrg_plan_get_info(p.handle, C.byref(info)), "xdrg_plan_get_info")
+    n = 1024
+    nat, heap = golden(name, n, "native"), golden(name, n, "heap")
+    want = golden(name, n, "xdr")
+    mar = M.Marshaler(p, dev)
+    r = mar.encode(torch.from_numpy(nat.copy()).to(dev), n, torch.from_numpy(heap.copy()).to(dev))
+    assert np.array_equal(r.xdr.cpu().numpy(), want)
+    nat2, heap2 = mar.decode(r.xdr, n, r.offsets)
+    r2 = mar.encode(nat2, n, heap2)
+    assert np.array_equal(r2.xdr.cpu().numpy(), want)
     A.check(L.xdrg_plan_get_info(p.handle, C.byref(info)), "xdrg_plan_get_info")
     assert info.specialized == 1
