@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--n", type=int, default=None,
                     help="records per GPU (default 1M at N=1, 2M at N>1: BASELINE.json configs 2 and 5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-large", action="store_true",
+                    help="skip the 16M-record fixed-path leg (large_batch_16m)")
     ap.add_argument("--host-inclusive", action="store_true",
                     help="also measure pinned host->device->host rates (PCIe-bound, reported apart)")
     ap.add_argument("--cold", action="store_true",
@@ -252,7 +254,7 @@ def pcie_ceiling(nbytes: int, dev, reps=5, chunk=16 << 20, nstreams=4) -> dict:
             "bytes": nbytes, "chunk_bytes": chunk, "streams": nstreams}
 
 
-def host_inclusive(mar, plan, nat_dev, n, W_, reps=5, nstreams=4, chunk_records=1 << 17):
+def host_inclusive(mar, plan, nat_dev, n, W_, reps=5, nstreams=4, chunk_records=1 << 15):
     """Pinned host -> device -> encode -> host, chunked over `nstreams`
     streams so that chunk k's D2H runs while chunk k+1's H2D and kernel run
     (both copy directions at once), and the decode mirror.  PCIe-bound;
@@ -387,6 +389,43 @@ def cold_cache(mar, nat, xdr, back, n, alg_bytes, reps=5):
             "achieved_GBps": round(alg_bytes / ((e + d) / 2 * 1e-3) / 1e9, 1),
             "protocol": "1 GiB read sweep before each kernel, HIP events around the kernel, "
                         f"median of {reps}"}
+
+
+def large_batch(mar, dev, reps=5, n=1 << 24):
+    """The fixed path at 16M records (2 GiB in, 2 GiB out per kernel): a
+    working set eight times the 256 MiB Infinity Cache, so the rate is HBM's,
+    not the cache's (the 1M headline fits in it).  Synthetic record bytes
+    made on the device; parity at this size is tests/test_gpu_parity.py
+    (test_config5_16m_sharded)."""
+    S_ = mar.plan.stride
+    nat = torch.randint(0, 256, (n * S_,), dtype=torch.uint8, device=dev)
+    xdr = torch.empty(n * mar.plan.fixed_size, dtype=torch.uint8, device=dev)
+    back = torch.empty_like(nat)
+    stream = torch.cuda.current_stream()
+    s = stream.cuda_stream
+    mar.status.init(s)
+    enc, dec = [], []
+    for r in range(reps + 1):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        ev[0].record(stream)
+        mar.launch_encode(nat, n, xdr, stream=s)
+        ev[1].record(stream)
+        mar.launch_decode(xdr, n, back, stream=s)
+        ev[2].record(stream)
+        torch.cuda.synchronize()
+        if r:
+            enc.append(ev[0].elapsed_time(ev[1]))
+            dec.append(ev[1].elapsed_time(ev[2]))
+    mar.check(s)
+    ok = bool(torch.equal(back, nat))
+    e, d = float(np.median(enc)), float(np.median(dec))
+    alg = n * (S_ + mar.plan.fixed_size)  # bytes in + out per kernel
+    ach = alg / ((e + d) / 2 * 1e-3) / 1e9
+    del nat, xdr, back
+    return {"records": n, "encode_ms": round(e, 4), "decode_ms": round(d, 4),
+            "encode_decode_gib_s": round(2 * n * mar.plan.fixed_size / GIB / ((e + d) * 1e-3), 2),
+            "achieved_GBps": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4), "round_trip_ok": ok,
+            "protocol": f"HIP events around each kernel, median of {reps}, device-made record bytes"}
 
 
 def messages_leg(schema, plan, mar, nat, heap, n, reps=20):
@@ -721,6 +760,11 @@ def main():
                             for r, row in enumerate(ranks)]
     if gather is not None:
         line["gather"] = gather
+    if world == 1 and plan.is_fixed and args.schema == "rec128" and not args.no_large:
+        try:
+            line["large_batch_16m"] = large_batch(mar, nat.device)
+        except Exception as e:  # reported, never fatal
+            line["large_batch_16m"] = {"error": str(e)[:200]}
     if world == 1 and args.cold and plan.is_fixed:
         line["cold_cache"] = cold_cache(mar, nat, xdr, back, n, alg_bytes)
         mar.check(s)

@@ -79,13 +79,19 @@ typedef struct {
   uint64_t len;
   uint64_t off;
 } obj_t;
-static uint8_t o8(obj_t o, uint64_t k) { return o.off + k < o.len ? o.base[o.off + k] : 0; }
-static uint32_t o32(obj_t o, uint64_t k) {
+static inline uint8_t o8(obj_t o, uint64_t k) { return o.off + k < o.len ? o.base[o.off + k] : 0; }
+static inline uint32_t o32(obj_t o, uint64_t k) {
+  if (o.off + k + 4 <= o.len) return rd32(o.base + o.off + k);
   uint8_t b[4];
   for (int i = 0; i < 4; ++i) b[i] = o8(o, k + (uint64_t)i);
   return rd32(b);
 }
-static uint64_t o64(obj_t o, uint64_t k) { return o32(o, k) | (uint64_t)o32(o, k + 4) << 32; }
+/* n bytes of o from k into w (bytes past the end read 0) */
+static inline void obytes(obj_t o, uint64_t k, uint8_t *w, uint64_t n) {
+  if (o.off + k + n <= o.len) { memcpy(w, o.base + o.off + k, n); return; }
+  for (uint64_t i = 0; i < n; ++i) w[i] = o8(o, k + i);
+}
+static inline uint64_t o64(obj_t o, uint64_t k) { return o32(o, k) | (uint64_t)o32(o, k + 4) << 32; }
 
 /* Fixed-size elements of a VECTOR op without F_SUB: ops [pc+1, pc+1+arg2). */
 static uint32_t elem_wire(const xdrg_op *e) {
@@ -225,7 +231,7 @@ static int enc_ops(ectx *c, uint32_t pc, obj_t o, uint32_t dbase, uint32_t frame
     }
     case XDRG_OP_OPAQUE: {
       uint32_t len = op->arg0;
-      for (uint32_t k = 0; k < len; ++k) w[k] = o8(o, op->noff + k);
+      obytes(o, op->noff, w, len);
       for (uint64_t k = len; k & 3; ++k) w[k] = 0;
       c->pos += pad4(len); ++pc; break;
     }
@@ -234,7 +240,7 @@ static int enc_ops(ectx *c, uint32_t pc, obj_t o, uint32_t dbase, uint32_t frame
       const uint32_t len = o32(o, op->noff + 8);
       obj_t h = {c->heap, c->heap_len, hoff};
       wr32(w, bswap32(len));
-      for (uint32_t k = 0; k < len; ++k) w[4 + k] = o8(h, k);
+      obytes(h, 0, w + 4, len);
       for (uint64_t k = len; k & 3; ++k) w[4 + k] = 0;
       c->pos += 4 + pad4(len); ++pc; break;
     }
@@ -267,7 +273,7 @@ static int enc_ops(ectx *c, uint32_t pc, obj_t o, uint32_t dbase, uint32_t frame
               break;
             }
             case XDRG_OP_OPAQUE:
-              for (uint32_t b = 0; b < e->arg0; ++b) q[b] = o8(el, e->noff + b);
+              obytes(el, e->noff, q, e->arg0);
               for (uint64_t b = e->arg0; b & 3; ++b) q[b] = 0;
               break;
             default: wr32(q, bswap32(o32(el, e->noff))); break;

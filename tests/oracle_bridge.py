@@ -25,7 +25,7 @@ SOURCES = [os.path.join(ORACLE_DIR, "xdr_oracle.c"), os.path.join(ORACLE_DIR, "c
 
 def build() -> None:
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
-    subprocess.check_call(["gcc", "-O2", "-fPIC", "-shared", "-std=gnu11", "-pthread", "-o", LIB] + SOURCES)
+    subprocess.check_call(["gcc", "-O3", "-fPIC", "-shared", "-std=gnu11", "-pthread", "-o", LIB] + SOURCES)
 
 
 def lib() -> C.CDLL:
