@@ -391,6 +391,15 @@ def cold_cache(mar, nat, xdr, back, n, alg_bytes, reps=5):
                         f"median of {reps}"}
 
 
+def plan_linear(plan) -> bool:
+    """Var plans whose walk never branches size without a walk (k_size_linear):
+    scalars, opaque[n] and opaque<>/string<> fields only, at most 8 of them."""
+    ops = plan.cp.ops
+    k = ops["kind"]
+    nvar = int(((k == A.OP_VAROPAQUE) | (k == A.OP_STRING)).sum())
+    return not plan.is_fixed and nvar <= 8 and not np.isin(k, [A.OP_UNION, A.OP_JUMP, A.OP_VECTOR]).any()
+
+
 def large_batch(mar, dev, reps=5, n=1 << 24):
     """The fixed path at 16M records (2 GiB in, 2 GiB out per kernel): a
     working set eight times the 256 MiB Infinity Cache, so the rate is HBM's,
@@ -656,10 +665,15 @@ def main():
         H = 0 if heap is None else heap.numel()
         enc_alg = n * S_ + H + X + 8 * (n + 1)
         dec_alg = X + 8 * (n + 1) + n * S_ + X
+        info = A.XdrgPlanInfo()
+        A.check(A.lib().xdrg_plan_get_info(plan.handle, A.C.byref(info)), "xdrg_plan_get_info")
+        spec = bool(info.specialized)  # plan-specialized kernels ran (built at warmup)
+        size_k = "k_size_linear" if plan_linear(plan) else ("xdrg_spec_size" if spec else "k_var_size")
         if np.mean(enc_ms) >= np.mean(dec_ms):
-            kern, alg_bytes, launches = "k_var_size+k_scan_blocks+k_var_encode_i", enc_alg, enc_ms
+            kern = f"{size_k}+k_scan_blocks+" + ("xdrg_spec_encode" if spec else "k_var_encode_i")
+            alg_bytes, launches = enc_alg, enc_ms
         else:
-            kern, alg_bytes, launches = "k_var_decode_w", dec_alg, dec_ms
+            kern, alg_bytes, launches = ("xdrg_spec_decode_copy" if spec else "k_var_decode_w"), dec_alg, dec_ms
     avg = float(np.mean(launches))
     achieved = alg_bytes / (avg * 1e-3) / 1e9
 

@@ -2,7 +2,7 @@
 
     python tools/prof_summary.py <round tag> <prof dir> [schemas...]
 
-<prof dir> is what tools/gpu/r01_prof.sh leaves: stats_<schema>/,
+<prof dir> is what tools/gpu/prof_round.sh leaves: stats_<schema>/,
 fetch_<schema>/, write_<schema>/ per schema.  Writes, per schema,
 profiles/<tag>_<schema>_kernel_stats.csv (the rocprofv3 --stats table as
 produced) and one profiles/<tag>_pmc.json with per-kernel FETCH_SIZE /
@@ -24,7 +24,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def counters(d):
-    f = [os.path.join(d, x) for x in os.listdir(d) if x.endswith("counter_collection.csv")][0]
+    f = [os.path.join(r, x) for r, _, fs in os.walk(d) for x in fs if x.endswith("counter_collection.csv")][0]
     agg = collections.defaultdict(list)
     for r in csv.DictReader(open(f)):
         agg[(r["Kernel_Name"], r["Counter_Name"])].append(float(r["Counter_Value"]))
@@ -32,7 +32,7 @@ def counters(d):
 
 
 def short(kname):
-    m = re.search(r"(k_\w+)", kname)
+    m = re.search(r"(k_\w+|xdrg_spec_\w+)", kname)
     return m.group(1) if m else kname.split("(")[0][:60]
 
 
@@ -44,12 +44,12 @@ def main():
     allpmc, traffic = {}, {}
     for sch in schemas:
         sd = os.path.join(pd, f"stats_{sch}")
-        stats = [os.path.join(sd, x) for x in os.listdir(sd) if x.endswith("kernel_stats.csv")][0]
+        stats = [os.path.join(r, x) for r, _, fs in os.walk(sd) for x in fs if x.endswith("kernel_stats.csv")][0]
         shutil.copy(stats, os.path.join(prof, f"{tag}_{sch}_kernel_stats.csv"))
         f, w = counters(os.path.join(pd, f"fetch_{sch}")), counters(os.path.join(pd, f"write_{sch}"))
         out = {}
         for (k, c), v in list(f.items()) + list(w.items()):
-            if not short(k).startswith("k_"):
+            if not short(k).startswith(("k_", "xdrg_spec_")):
                 continue  # torch / runtime kernels of the bench's own checks
             e = out.setdefault(short(k), {"launches": len(v)})
             e[c + "_KiB_per_launch"] = round(sum(v) / len(v), 1)
