@@ -28,7 +28,7 @@ namespace {
 
 constexpr uint32_t kNoPc = 0xffffffffu;
 constexpr uint32_t kSlotMax = 4;        // chunk-map slots per record (var_kernels.h)
-constexpr uint32_t kSlotBytes = 4096;   // largest payload one chunk-map slot addresses
+constexpr uint32_t kSlotBytes = 1u << 30;  // longer payloads are copied by their lane
 
 std::string u32(uint32_t v) {
   char b[16];
@@ -534,6 +534,7 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
     << " ops: straight-line walker for var_kernels.h.\n"
     << "#include \"var_kernels.h\"\n"
     << "using namespace xdrg::dev;\n\n"
+    << "extern \"C\" __device__ __attribute__((used)) unsigned xdrg_spec_iface = " << kSpecIface << "u;\n\n"
     << "struct plan_walk {\n"
     << "  __device__ __forceinline__ uint64_t size(const uint8_t *nat, uint32_t &bad_op) const {\n"
     << "    uint64_t s = 0;\n"
@@ -554,10 +555,10 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
     << "extern \"C\" __global__ __launch_bounds__(64) void xdrg_spec_encode(\n"
     << "    const uint8_t *native, uint64_t n, uint32_t stride, const uint8_t *heap, uint64_t heap_len,\n"
     << "    uint8_t *xdr, uint64_t cap, uint64_t *offsets, const uint32_t *sizes,\n"
-    << "    const unsigned long long *block_base, uint32_t stack_limit, uint32_t MC, uint32_t C,\n"
+    << "    const unsigned long long *block_base, uint32_t stack_limit, uint32_t C,\n"
     << "    uint32_t mark, unsigned long long *err) {\n"
     << "  var_encode_body<plan_walk, " << info.slots << ", 8>(plan_walk{}, native, n, stride, heap, heap_len,\n"
-    << "      xdr, cap, offsets, sizes, block_base, stack_limit, MC, C, mark, err);\n}\n\n";
+    << "      xdr, cap, offsets, sizes, block_base, stack_limit, C, mark, err);\n}\n\n";
   for (int cp = 0; cp < 2; ++cp)
     s << "extern \"C\" __global__ __launch_bounds__(64) void xdrg_spec_decode" << (cp ? "_copy" : "") << "(\n"
       << "    const uint8_t *xdr, uint64_t len, const uint64_t *offsets, uint64_t n, uint8_t *native,\n"

@@ -138,5 +138,23 @@ __device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t lane) {
          (static_cast<uint64_t>(rl32(static_cast<uint32_t>(v >> 32), lane)) << 32);
 }
 
+// Inclusive prefix sum over the 64 lanes of a wave with DPP moves (no LDS
+// round trip, unlike __shfl_up's ds_bpermute): row_shr 1/2/4/8 scans each
+// row of 16 lanes, row_bcast:15 and row_bcast:31 carry row totals into the
+// rows above.  Every lane of the wave must be active.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp_add(uint32_t x) {
+  return x + static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), CTRL, ROWS, 0xf, true));
+}
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+  x = dpp_add<0x111, 0xf>(x);  // row_shr:1
+  x = dpp_add<0x112, 0xf>(x);  // row_shr:2
+  x = dpp_add<0x114, 0xf>(x);  // row_shr:4
+  x = dpp_add<0x118, 0xf>(x);  // row_shr:8
+  x = dpp_add<0x142, 0xa>(x);  // row_bcast:15 -> rows 1, 3
+  x = dpp_add<0x143, 0xc>(x);  // row_bcast:31 -> rows 2, 3
+  return x;
+}
+
 }  // namespace dev
 }  // namespace xdrg

@@ -154,6 +154,17 @@ const spec_module *spec_get(const xdrg_plan &cp) {
       (void)hipModuleUnload(m);
       return nullptr;
     }
+  // a code object of another kernel interface (an older build's AOT file)
+  void *iv = nullptr;
+  size_t ib = 0;
+  unsigned iface = 0;
+  if (hipModuleGetGlobal(&iv, &ib, m, "xdrg_spec_iface") != hipSuccess || ib != sizeof iface ||
+      hipMemcpyDtoH(&iface, iv, sizeof iface) != hipSuccess || iface != kSpecIface) {
+    (void)hipModuleUnload(m);
+    s.log = "specialized kernels: code object of another kernel interface (rebuild it from xdrg_plan_kernel_source)";
+    s.state.store(-1, std::memory_order_release);
+    return nullptr;
+  }
   d.module = m;
   d.f_size = f[0];
   d.f_enc = f[1];

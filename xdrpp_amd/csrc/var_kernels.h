@@ -31,52 +31,49 @@
 #pragma once
 #include "dev_common.h"
 
+// Phase timestamps of a wave for tuning harnesses (tools/tune/enc_stamps.py
+// defines XDRG_STAMP(k) before including the kernels); nothing in the
+// library.
+#ifndef XDRG_STAMP
+#define XDRG_STAMP(k) ((void)0)
+#endif
+
 namespace xdrg {
 namespace dev {
 
 // ---------------------------------------------------------------- encode
-// LDS of an encode wave: the native tile is dead once the walk is done, so
-// the chunk descriptors and the chunk map (built after the walk) reuse it;
-// the image follows.  (Overlaying them cut recvar's LDS per wave from 16.4
-// to 12.8 KiB: more waves per CU to hide the wave's memory round trips.)
-struct enc_i_lds {
-  uint32_t tile, desc, map, img, total;
+// LDS of an encode wave: the native tile (kept for every window round), the
+// payload slots of the 64 lanes, their inclusive chunk counts, and the image
+// of one window of the wave's output stretch.
+struct enc_lds {
+  uint32_t tile, desc, cum, img, total;
 };
-__host__ __device__ inline enc_i_lds enc_i_layout(uint32_t stride, uint32_t KMAX, uint32_t MC,
-                                                 uint32_t C) {
-  enc_i_lds L;
+__host__ __device__ inline enc_lds enc_layout(uint32_t stride, uint32_t KMAX, uint32_t C) {
+  enc_lds L;
   L.tile = 0;
-  L.desc = 0;
-  L.map = L.desc + 64u * KMAX * 16u;
-  const uint32_t a = (64u * stride + 15u) & ~15u, b = L.map + ((MC * 2u + 15u) & ~15u);
-  L.img = a > b ? a : b;
-  L.total = L.img + C + 32u;  // phase shift + the last (partial) chunk read
+  L.desc = (64u * stride + 15u) & ~15u;
+  L.cum = L.desc + 64u * KMAX * 16u;
+  L.img = L.cum + 64u * 4u;
+  L.total = L.img + C + 32u;  // + the last (partial) chunk read
   return L;
 }
 
 struct echunk_desc {  // 16 bytes: one payload slot of one lane
   uint64_t src;       // heap byte offset
-  uint32_t dst;       // byte offset in the wave's stretch
+  uint32_t dst;       // image-space byte offset of the payload (below)
   uint32_t len;       // payload bytes
 };
 
-// Store word `v` at stretch offset `at`: image if it fits, else global.
-__device__ __forceinline__ void img_put(uint8_t *im, uint32_t C, uint8_t *gout, uint32_t at,
-                                        uint32_t v) {
-  if (at < C) *reinterpret_cast<uint32_t *>(im + at) = v;
-  else st32(gout + at, v);
-}
-
-// One lane's encode state: where its next wire word goes (stretch offset
-// `at`, stream offset `pos`), the checks of xdr_generic_put, and up to KMAX
-// payload slots for the chunk map.  Payloads that do not take a slot (no
-// slot left, longer than a chunk map entry can address, inside a container
-// element) are copied by the lane itself.
+// One lane's encode state.  Positions are *image-space* offsets: stretch
+// offset + the wave's 16-byte phase, so that window w = [w0, w0 + C) of
+// image space maps onto whole aligned 16-byte chunks of the stream.  The
+// walk stores only the words of the current window (LDS image); payloads
+// in registered slots are copied by the wave's chunk pass; the rest
+// (container elements, payloads past the slots) word by word by the lane.
 template <int KMAX>
 struct enc_ctx {
-  uint8_t *im;
-  uint32_t C;
-  uint8_t *gout;
+  uint8_t *img;
+  uint32_t w0, C;
   const uint8_t *heap;
   uint64_t heap_len;
   uint64_t cap;
@@ -88,6 +85,10 @@ struct enc_ctx {
   uint64_t psr[KMAX];
   uint32_t pds[KMAX], pln[KMAX];
 
+  // word `v` at image-space offset `a`, if it lies in the window
+  __device__ __forceinline__ void wput(uint32_t a, uint32_t v) {
+    if (a - w0 < C) *reinterpret_cast<uint32_t *>(img + (a - w0)) = v;
+  }
   // check(n) of xdr_generic_put (marshal.h:104-108) after the stack budget
   // of the field's class level (marshal.h:129-136)
   __device__ __forceinline__ bool field(uint32_t op, uint32_t depth, uint64_t need) {
@@ -102,7 +103,7 @@ struct enc_ctx {
     return true;
   }
   __device__ __forceinline__ void put(uint32_t v) {
-    img_put(im, C, gout, at, v);
+    wput(at, v);
     at += 4;
     pos += 4;
   }
@@ -111,7 +112,7 @@ struct enc_ctx {
     at += p4;
     pos += p4;
   }
-  // payload of `len` bytes at heap offset `src`, copied by the chunk map
+  // payload of `len` bytes at heap offset `src`, copied by the chunk pass
   template <int K> __device__ __forceinline__ void slot(uint64_t src, uint32_t len) {
     if (len) {
       psr[K] = src;
@@ -127,13 +128,16 @@ struct enc_ctx {
       if (static_cast<uint32_t>(q) == k) { psr[q] = src; pds[q] = at; pln[q] = len; }
     skip(len);
   }
-  // payload copied word by word by this lane (put_bytes, marshal.cc:59-72)
+  // payload copied word by word by this lane (put_bytes, marshal.cc:59-72):
+  // only the words of the window are read
   __device__ void copy(uint64_t src, uint32_t len) {
     const uint32_t nw = (len + 3u) >> 2;
-    for (uint32_t k = 0; k < nw; ++k) {
+    const uint32_t k0 = w0 > at ? (w0 - at) >> 2 : 0u;
+    const uint32_t k1 = min(nw, w0 + C > at ? (w0 + C - at + 3u) >> 2 : 0u);
+    for (uint32_t k = k0; k < k1; ++k) {
       uint32_t w = unaligned_word(heap, heap_len, src + 4ull * k);
       if (4u * k + 4u > len) w &= keep_mask(len - 4u * k);
-      img_put(im, C, gout, at + 4u * k, w);
+      wput(at + 4u * k, w);
     }
     skip(len);
   }
@@ -141,23 +145,51 @@ struct enc_ctx {
   __device__ __forceinline__ uint32_t hword(uint64_t off) const { return unaligned_word(heap, heap_len, off); }
 };
 
+// Chunks of a lane's slots that end at or before image-space offset `a`,
+// and that start before `a` (the slots' chunks are in stream order).
+template <int KMAX>
+__device__ __forceinline__ uint32_t chunks_ending_by(const enc_ctx<KMAX> &c, uint32_t a) {
+  uint32_t s = 0;
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k)
+    if (c.pln[k] && a >= c.pds[k] + 16u) s += min((c.pln[k] + 15u) >> 4, (a - c.pds[k]) >> 4);
+  return s;
+}
+template <int KMAX>
+__device__ __forceinline__ uint32_t chunks_starting_before(const enc_ctx<KMAX> &c, uint32_t a) {
+  uint32_t s = 0;
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k)
+    if (c.pln[k] && a > c.pds[k]) s += min((c.pln[k] + 15u) >> 4, (a - c.pds[k] + 15u) >> 4);
+  return s;
+}
+
+// One wave = 64 consecutive records (xdr_generic_put, marshal.h:84-137).
+// The output stretch of the wave is produced in windows of C bytes of LDS
+// image: per window the lanes whose record reaches into it walk it (scalar
+// words of the window into the image), the wave copies the payload chunks
+// that land in it (16-byte loads, consecutive lanes on consecutive chunks),
+// and the window leaves as aligned, whole-line 16-byte stores.  No partial
+// or scattered global store, so each 64-byte line of the stream is one
+// write request to L2.
 template <class W, int KMAX, int U>
 __device__ __forceinline__ void var_encode_body(
     const W &w, const uint8_t *__restrict__ native, uint64_t n, uint32_t stride,
     const uint8_t *__restrict__ heap, uint64_t heap_len, uint8_t *__restrict__ xdr, uint64_t cap,
     uint64_t *__restrict__ offsets, const uint32_t *__restrict__ sizes,
-    const unsigned long long *__restrict__ block_base, uint32_t stack_limit, uint32_t MC,
-    uint32_t C, uint32_t mark, unsigned long long *err) {
+    const unsigned long long *__restrict__ block_base, uint32_t stack_limit, uint32_t C,
+    uint32_t mark, unsigned long long *err) {
   extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
-  const enc_i_lds L = enc_i_layout(stride, KMAX, MC, C);
+  const enc_lds L = enc_layout(stride, KMAX, C);
   uint8_t *tile = sm + L.tile;
   echunk_desc *desc = reinterpret_cast<echunk_desc *>(sm + L.desc);
-  uint16_t *map = reinterpret_cast<uint16_t *>(sm + L.map);
+  uint32_t *cum = reinterpret_cast<uint32_t *>(sm + L.cum);
   uint8_t *img = sm + L.img;
   const uint32_t lane = threadIdx.x;
   const uint64_t wr0 = static_cast<uint64_t>(blockIdx.x) * 64u;
   const uint64_t r = wr0 + lane;
   const uint32_t nrec = static_cast<uint32_t>(min<uint64_t>(64, n - wr0));
+  XDRG_STAMP(0);
 
   // ---- record offsets: wave scan of the sizes on top of the block base
   // (sizes, block base and the native tile are loaded in one round trip)
@@ -165,162 +197,185 @@ __device__ __forceinline__ void var_encode_body(
   const uint64_t wave_out = block_base[blockIdx.x];
   stage_tile(tile, native + wr0 * stride, nrec * stride, lane, 64u);
   const bool szok = !(sz & kSizeErr);
-  const unsigned long long v = szok ? sz : 0ull;
-  unsigned long long incl = v;
-  for (int o = 1; o < 64; o <<= 1) {
-    const unsigned long long x = __shfl_up(incl, o, 64);
-    if (lane >= static_cast<uint32_t>(o)) incl += x;
-  }
-  const uint64_t T = rl64(incl, 63);  // bytes of the wave's stretch
-  const uint64_t off = wave_out + incl - v;
+  const uint32_t v = szok ? sz : 0u;
+  const uint32_t incl = wave_incl_scan(v);  // a wave's stretch < 2^31 bytes (launch condition)
+  const uint32_t T = rl32(incl, 63);        // bytes of the wave's stretch
+  const uint64_t off = wave_out + (incl - v);
   if (r < n) offsets[r] = off;
   wave_sync();
+  XDRG_STAMP(1);
 
+  // image space: byte j <-> stream byte g0 + j, g0 = wave_out rounded down to 16
   const uint32_t sh = static_cast<uint32_t>(wave_out & 15u);
-  uint8_t *im = img + sh;          // image byte j <-> global wave_out + j
-  uint8_t *gout = xdr + wave_out;  // direct path for j >= C
+  const uint64_t g0 = wave_out - sh;
+  const uint32_t a0 = static_cast<uint32_t>(off - wave_out) + sh;  // this record's first byte
+  const uint32_t span = sh + T;
+  const uint32_t rounds = T ? (span + C - 1u) / C : 1u;
+  const uint64_t ge = min<uint64_t>(wave_out + T, cap);  // last stream byte + 1 to write
 
-  // ---- walk: scalar words -> image, payload slots -> registers
   enc_ctx<KMAX> c;
-  c.im = im;
+  c.img = img;
   c.C = C;
-  c.gout = gout;
   c.heap = heap;
   c.heap_len = heap_len;
   c.cap = cap;
   c.stack_limit = stack_limit;
   c.r = r;
   c.err = err;
-  c.at = static_cast<uint32_t>(off - wave_out);
-  c.pos = off;
 #pragma unroll
   for (int k = 0; k < KMAX; ++k) { c.psr[k] = 0; c.pds[k] = 0; c.pln[k] = 0; }
   bool ok = szok;
-  if (ok && mark) {  // the message's record mark (message_t::alloc, marshal.cc:15-31)
-    if (4 > cap - min(c.pos, cap)) {
-      report(err, r, kOpRecordLevel, XDRG_ERR_OVERFLOW_PUT);
-      ok = false;
-    } else {
-      c.put(mark_word(sz - 4u));
-    }
-  }
-  ok = w.enc(c, tile + lane * stride, ok);
-  if (!ok) {  // a failing record's bytes are unspecified (never past `cap`)
+  uint32_t M = 0;
+  for (uint32_t rd = 0; rd < rounds; ++rd) {
+    const uint32_t w0 = rd * C;
+    c.w0 = w0;
+    // ---- walk: the window's scalar words -> image, payload slots -> registers
+    // (every lane walks in the first round: it reports the record's errors)
+    if (rd == 0 || (ok && a0 < w0 + C && a0 + v > w0)) {
+      c.at = a0;
+      c.pos = off;
+      bool okr = szok;
+      if (okr && mark) {  // the message's record mark (message_t::alloc, marshal.cc:15-31)
+        if (4 > cap - min(c.pos, cap)) {
+          report(err, r, kOpRecordLevel, XDRG_ERR_OVERFLOW_PUT);
+          okr = false;
+        } else {
+          c.put(mark_word(sz - 4u));
+        }
+      }
+      okr = w.enc(c, tile + lane * stride, okr);
+      if (rd == 0) {
+        ok = okr;
+        if (!ok) {  // a failing record's bytes are unspecified (never past `cap`)
 #pragma unroll
-    for (int k = 0; k < KMAX; ++k) c.pln[k] = 0;
-  }
-  wave_sync();  // every lane's walk is done with the tile: the chunk map reuses it
-
-  // ---- chunk map: u16 lane << 10 | slot << 8 | chunk
-  uint32_t nch = 0;
-#pragma unroll
-  for (int k = 0; k < KMAX; ++k) nch += (c.pln[k] + 15u) >> 4;
-  uint32_t cincl = nch;
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t x = __shfl_up(cincl, o, 64);
-    if (lane >= static_cast<uint32_t>(o)) cincl += x;
-  }
-  const uint32_t M = __shfl(cincl, 63, 64);
-  {
-    uint32_t e = cincl - nch;
-#pragma unroll
-    for (int k = 0; k < KMAX; ++k) {
-      if (!c.pln[k]) continue;
-      desc[lane * KMAX + k] = echunk_desc{c.psr[k], c.pds[k], c.pln[k]};
-      const uint32_t nq = (c.pln[k] + 15u) >> 4;
-      const uint32_t tag = (lane << 10) | (static_cast<uint32_t>(k) << 8);
-      for (uint32_t q = 0; q < nq; ++q) map[e + q] = static_cast<uint16_t>(tag | q);
-      e += nq;
-    }
-  }
-  wave_sync();
-
-  // ---- payload chunks: heap -> image, U chunks in flight per lane.  Three
-  // passes per batch: the chunk descriptors (LDS), then the U loads with no
-  // use of a loaded value in between (so none waits for another), then the
-  // rare chunk that ends past the heap, the pad masks and the stores.
-  for (uint32_t c0 = 0; c0 < M; c0 += 64u * U) {
-    u32x4 val[U];
-    uint64_t hs[U];
-    uint32_t at[U], nb[U], rem[U];
-    bool fast[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t ci = c0 + 64u * u + lane;
-      nb[u] = 0u;
-      at[u] = 0u;
-      hs[u] = 0u;
-      rem[u] = 16u;
-      fast[u] = false;
-      if (ci < M) {
-        const uint32_t m = map[ci];
-        const echunk_desc d = desc[(m >> 10) * KMAX + ((m >> 8) & 3u)];
-        const uint32_t q16 = (m & 0xffu) << 4;
-        hs[u] = d.src + q16;
-        rem[u] = d.len - q16;
-        at[u] = d.dst + q16;
-        nb[u] = min(16u, ((d.len + 3u) & ~3u) - q16);
-        fast[u] = hs[u] + 16u <= heap_len;
+          for (int k = 0; k < KMAX; ++k) c.pln[k] = 0;
+        }
       }
     }
+    if (rd == 0) {
+      XDRG_STAMP(2);
+      // ---- the lanes' slots and inclusive chunk counts, for the chunk pass
+      uint32_t nch = 0;
 #pragma unroll
-    for (int u = 0; u < U; ++u)
-      if (fast[u]) val[u] = ld16u(heap + hs[u]);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (!nb[u]) continue;
-      u32x4 x = val[u];
-      if (!fast[u])
-        x = u32x4{unaligned_word(heap, heap_len, hs[u]), unaligned_word(heap, heap_len, hs[u] + 4),
-                  unaligned_word(heap, heap_len, hs[u] + 8), unaligned_word(heap, heap_len, hs[u] + 12)};
-      const int32_t rm = static_cast<int32_t>(rem[u]);
-      if (rm < 16) {  // zero the pad bytes after the payload (put_bytes)
-        x.x &= keep_bytes(rm);
-        x.y &= keep_bytes(rm - 4);
-        x.z &= keep_bytes(rm - 8);
-        x.w &= keep_bytes(rm - 12);
+      for (int k = 0; k < KMAX; ++k) {
+        desc[lane * KMAX + k] = echunk_desc{c.psr[k], c.pds[k], c.pln[k]};
+        nch += (c.pln[k] + 15u) >> 4;
       }
-      if (at[u] + 16u <= C) {
-        uint32_t *wp = reinterpret_cast<uint32_t *>(im + at[u]);
-        wp[0] = x.x;
-        if (nb[u] > 4u) wp[1] = x.y;
-        if (nb[u] > 8u) wp[2] = x.z;
-        if (nb[u] > 12u) wp[3] = x.w;
-      } else if (at[u] >= C && nb[u] == 16u) {
-        st16u(gout + at[u], x);  // a whole chunk past the image: one (4-aligned) 16-byte store
-      } else {
-        img_put(im, C, gout, at[u], x.x);
-        if (nb[u] > 4u) img_put(im, C, gout, at[u] + 4, x.y);
-        if (nb[u] > 8u) img_put(im, C, gout, at[u] + 8, x.z);
-        if (nb[u] > 12u) img_put(im, C, gout, at[u] + 12, x.w);
+      const uint32_t ci = wave_incl_scan(nch);
+      cum[lane] = ci;
+      M = rl32(ci, 63);
+      XDRG_STAMP(3);
+    }
+    wave_sync();
+
+    // ---- payload chunks of the window: heap -> image, U per lane in flight.
+    // Chunk i of the wave (stream order) belongs to the lane L with
+    // cum[L-1] <= i < cum[L] (binary search) and to the first of its slots
+    // whose chunks reach past i - cum[L-1].
+    const uint32_t clo = rl32(wave_incl_scan(chunks_ending_by(c, w0)), 63);
+    const uint32_t chi = min(M, rl32(wave_incl_scan(chunks_starting_before(c, w0 + C)), 63));
+    for (uint32_t c0 = clo; c0 < chi; c0 += 64u * U) {
+      uint32_t lo[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) lo[u] = 0;
+      uint32_t ix[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) ix[u] = min(c0 + 64u * u + lane, chi - 1u);
+#pragma unroll
+      for (uint32_t s = 32; s; s >>= 1) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (cum[lo[u] + s - 1u] <= ix[u]) lo[u] += s;
+      }
+      echunk_desc d[U];
+      uint32_t q[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        uint32_t rem = ix[u] - (lo[u] ? cum[lo[u] - 1u] : 0u);
+        const echunk_desc *dl = desc + lo[u] * KMAX;
+        d[u] = dl[0];
+#pragma unroll
+        for (int k = 0; k + 1 < KMAX; ++k) {
+          const uint32_t nq = (d[u].len + 15u) >> 4;
+          if (rem >= nq) {
+            rem -= nq;
+            d[u] = dl[k + 1];
+          }
+        }
+        q[u] = rem;
+      }
+      u32x4 val[U];
+      uint64_t hs[U];
+      uint32_t at[U], nb[U], rm[U];
+      bool fast[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bool live = c0 + 64u * u + lane < chi;
+        const uint32_t q16 = q[u] << 4;
+        hs[u] = d[u].src + q16;
+        rm[u] = live ? d[u].len - q16 : 16u;
+        at[u] = d[u].dst + q16;
+        nb[u] = live ? min(16u, ((d[u].len + 3u) & ~3u) - q16) : 0u;
+        fast[u] = live && hs[u] + 16u <= heap_len;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (fast[u]) val[u] = ld16u(heap + hs[u]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (!nb[u]) continue;
+        u32x4 x = val[u];
+        if (!fast[u])
+          x = u32x4{unaligned_word(heap, heap_len, hs[u]), unaligned_word(heap, heap_len, hs[u] + 4),
+                    unaligned_word(heap, heap_len, hs[u] + 8), unaligned_word(heap, heap_len, hs[u] + 12)};
+        const int32_t rr = static_cast<int32_t>(rm[u]);
+        if (rr < 16) {  // zero the pad bytes after the payload (put_bytes)
+          x.x &= keep_bytes(rr);
+          x.y &= keep_bytes(rr - 4);
+          x.z &= keep_bytes(rr - 8);
+          x.w &= keep_bytes(rr - 12);
+        }
+        const uint32_t j = at[u] - w0;
+        if (j + 16u <= C && at[u] >= w0) {
+          uint32_t *wp = reinterpret_cast<uint32_t *>(img + j);
+          wp[0] = x.x;
+          if (nb[u] > 4u) wp[1] = x.y;
+          if (nb[u] > 8u) wp[2] = x.z;
+          if (nb[u] > 12u) wp[3] = x.w;
+        } else {  // a chunk across a window edge
+          c.wput(at[u], x.x);
+          if (nb[u] > 4u) c.wput(at[u] + 4, x.y);
+          if (nb[u] > 8u) c.wput(at[u] + 8, x.z);
+          if (nb[u] > 12u) c.wput(at[u] + 12, x.w);
+        }
       }
     }
-  }
-  wave_sync();
+    wave_sync();
+    if (rd + 1 == rounds) XDRG_STAMP(4);
 
-  // ---- image -> global: aligned 16-byte chunks, partial words at the edges
-  {
-    const uint64_t gs = wave_out;
-    const uint64_t ge = min<uint64_t>(gs + min<uint64_t>(T, C), cap);
-    if (ge > gs) {
-      const uint64_t c0 = gs & ~15ull;
-      const uint32_t nc = static_cast<uint32_t>((ge - c0 + 15u) >> 4);
-      for (uint32_t ci = lane; ci < nc; ci += 64u) {
-        const uint64_t ca = c0 + 16ull * ci;
-        const uint8_t *lsrc = img + 16u * ci;  // img + sh <-> gs, and gs - sh = c0
-        if (ca >= gs && ca + 16u <= ge) {
+    // ---- window -> stream: aligned 16-byte chunks, words at the stretch's edges
+    const uint64_t ws = g0 + w0;
+    const uint64_t we = min<uint64_t>(ws + C, ge);
+    if (we > ws) {
+      const uint32_t nc = static_cast<uint32_t>((we - ws + 15u) >> 4);
+      for (uint32_t k = lane; k < nc; k += 64u) {
+        const uint64_t ca = ws + 16ull * k;
+        const uint8_t *lsrc = img + 16u * k;
+        if (ca >= wave_out && ca + 16u <= we) {
           *reinterpret_cast<u32x4 *>(xdr + ca) = *reinterpret_cast<const u32x4 *>(lsrc);
         } else {
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const uint64_t wa = ca + 4u * q;
-            if (wa >= gs && wa + 4u <= ge) st32(xdr + wa, *reinterpret_cast<const uint32_t *>(lsrc + 4 * q));
+          for (int t = 0; t < 4; ++t) {
+            const uint64_t wa = ca + 4u * t;
+            if (wa >= wave_out && wa + 4u <= we) st32(xdr + wa, *reinterpret_cast<const uint32_t *>(lsrc + 4 * t));
           }
         }
       }
     }
+    wave_sync();  // the next window's walk reuses the image
   }
+  XDRG_STAMP(5);
 }
 
 // ---------------------------------------------------------------- decode
@@ -356,10 +411,13 @@ struct win_reader {
       ra0 = *reinterpret_cast<const u32x4 *>(ra_line);
       ra1 = ra_line + 16u < xend ? *reinterpret_cast<const u32x4 *>(ra_line + 16u) : u32x4{0u, 0u, 0u, 0u};
     }
+    // word k (0..7) of the 32 bytes, by selects on its bits (a variable
+    // vector index would put ra0/ra1 in scratch memory)
     const uint32_t k = static_cast<uint32_t>(ga - ra_line) >> 2;
-    const u32x4 h = k < 4u ? ra0 : ra1;
-    const uint32_t j = k & 3u;
-    return j == 0 ? h.x : j == 1 ? h.y : j == 2 ? h.z : h.w;
+    const bool b0 = k & 1u, b1 = k & 2u, b2 = k & 4u;
+    const uint32_t x0 = b2 ? ra1.x : ra0.x, x1 = b2 ? ra1.y : ra0.y;
+    const uint32_t x2 = b2 ? ra1.z : ra0.z, x3 = b2 ? ra1.w : ra0.w;
+    return b1 ? (b0 ? x3 : x2) : (b0 ? x1 : x0);
   }
 };
 
@@ -457,10 +515,10 @@ __device__ __forceinline__ void var_decode_body(
           if (o >= 0 && o + 16 <= lim) {
             st16u(hd, v[u]);
           } else {
-            const uint32_t w4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-              if (o + 4 * q >= 0 && o + 4 * q + 4 <= lim) st32(hd + 4 * q, w4[q]);
+            if (o >= 0 && o + 4 <= lim) st32(hd, v[u].x);
+            if (o + 4 >= 0 && o + 8 <= lim) st32(hd + 4, v[u].y);
+            if (o + 8 >= 0 && o + 12 <= lim) st32(hd + 8, v[u].z);
+            if (o + 12 >= 0 && o + 16 <= lim) st32(hd + 12, v[u].w);
           }
         }
       }

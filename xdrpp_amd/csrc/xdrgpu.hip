@@ -808,7 +808,7 @@ struct interp_walk {
         c.put(bswap32(blen));
         const uint64_t hsrc = *reinterpret_cast<const uint64_t *>(nw);
         if (!blen) {
-        } else if (nslot < static_cast<uint32_t>(KMAX) && blen <= 4096u) {
+        } else if (nslot < static_cast<uint32_t>(KMAX) && blen <= (1u << 30)) {
           c.slot_dyn(nslot++, hsrc, blen);
         } else {
           c.copy(hsrc, blen);
@@ -826,7 +826,7 @@ struct interp_walk {
         const uint64_t eoff = *reinterpret_cast<const uint64_t *>(nw);
         const uint32_t cnt = nw[2];
         c.put(bswap32(cnt));
-        auto put = [&](uint32_t a, uint32_t w) { img_put(c.im, c.C, c.gout, a, w); };
+        auto put = [&](uint32_t a, uint32_t w) { c.wput(a, w); };
         if (!enc_vector_elems(ops, upc + 1, op.arg2, c.heap, c.heap_len, eoff, cnt, op.arg1, c.pos,
                               c.cap, c.at, c.stack_limit, c.r, c.err, put)) {
           ok = false;
@@ -945,10 +945,10 @@ __global__ __launch_bounds__(64) void k_var_encode_i(
     uint64_t heap_len, uint8_t *__restrict__ xdr, uint64_t cap, uint64_t *__restrict__ offsets,
     const uint32_t *__restrict__ sizes, const unsigned long long *__restrict__ block_base,
     const xdrg_op *__restrict__ ops, uint32_t nops, const uint32_t *__restrict__ table,
-    uint32_t stack_limit, uint32_t MC, uint32_t C, uint32_t mark, unsigned long long *err) {
+    uint32_t stack_limit, uint32_t C, uint32_t mark, unsigned long long *err) {
   var_encode_body<interp_walk, KMAX, U>(interp_walk{ops, nops, table}, native, n, stride, heap,
                                         heap_len, xdr, cap, offsets, sizes, block_base, stack_limit,
-                                        MC, C, mark, err);
+                                        C, mark, err);
 }
 
 template <bool COPY, bool RA = true>
@@ -1789,21 +1789,18 @@ int var_encode(const xdrg_plan &P, const dev_tables &T, const void *d_native, ui
   unsigned long long *bsum = reinterpret_cast<unsigned long long *>(static_cast<char *>(d_ws) + bo);
   unsigned long long *bbase = reinterpret_cast<unsigned long long *>(static_cast<char *>(d_ws) + bbo);
   const uint64_t max_rec = p->max_record_bytes + mark;
-  // chunk-map image encode (64-record workgroups); chunk map entries are
-  // u16 (lane 6 | slot 2 | chunk 8 bits)
-  const uint32_t MC = static_cast<uint32_t>(std::min<uint64_t>(64ull * p->max_chunks16, 1u << 20));
   const uint32_t KI = p->max_var_slots <= 1 ? 1u : p->max_var_slots <= 2 ? 2u : 4u;
-  // LDS image: tools/tune/ab_var.py (MI355X, 1M records, U=8): an 8 KiB
-  // image helps plans whose other LDS is small (recvar 0.208 -> 0.179 ms,
-  // vecrec 0.373 -> 0.305 ms); plans with a large chunk map and tile run
-  // better with no image and the occupancy it costs (rpc 0.349 -> 0.318 ms).
-  uint32_t img = O.image_bytes >= 0 ? static_cast<uint32_t>(O.image_bytes) & ~15u
-                 : enc_i_layout(p->stride, KI, MC, 0).total >= (12u << 10) ? 0u : (8u << 10);
-  const uint32_t Ci = static_cast<uint32_t>(std::min<uint64_t>(
-      img, (64ull * std::max<uint64_t>(max_rec, 16) + 15u) & ~15ull));
-  const enc_i_lds LI = enc_i_layout(p->stride, KI, MC, Ci);
-  const bool ok_I = p->max_var_slots <= 4 && p->max_slot_len <= 4096u &&
-                    64ull * max_rec < (1ull << 31) && LI.total <= kVarLdsBudget &&
+  // LDS window of the wave's output stretch (var_kernels.h): the stretch
+  // leaves in rounds of C bytes.  8 KiB by default, never more than the
+  // longest stretch needs.
+  auto window = [&](void) -> uint32_t {
+    const uint32_t want = O.image_bytes > 0 ? std::max(static_cast<uint32_t>(O.image_bytes) & ~15u, 256u)
+                                            : (8u << 10);
+    return static_cast<uint32_t>(std::min<uint64_t>(want, (64ull * std::max<uint64_t>(max_rec, 16) + 31u) & ~15ull));
+  };
+  const uint32_t Ci = window();
+  const enc_lds LI = enc_layout(p->stride, KI, Ci);
+  const bool ok_I = p->max_var_slots <= 4 && 64ull * max_rec < (1ull << 31) && LI.total <= kVarLdsBudget &&
                     aligned(d_native, 16);
   int kern = O.enc_kernel;
   if (kern == 3 && !ok_I) kern = 0;
@@ -1816,14 +1813,10 @@ int var_encode(const xdrg_plan &P, const dev_tables &T, const void *d_native, ui
   const uint32_t nops = uint32_t(p->ops.size());
   // plan-specialized kernels (spec.cpp): straight-line size and encode walks
   const spec_module *SM = O.specialize && O.enc_kernel == 0 && !p->has_sub ? spec_get(*p) : nullptr;
-  uint32_t MCs = 0, Cs = 0, lds_s = 0;
+  uint32_t Cs = 0, lds_s = 0;
   if (SM) {
-    const uint32_t KS = p->spec.info.slots;
-    MCs = static_cast<uint32_t>(std::min<uint64_t>(64ull * p->spec.info.max_chunks, 1u << 20));
-    const uint32_t imgs = O.image_bytes >= 0 ? static_cast<uint32_t>(O.image_bytes) & ~15u
-                          : enc_i_layout(p->stride, KS, MCs, 0).total >= (12u << 10) ? 0u : (8u << 10);
-    Cs = static_cast<uint32_t>(std::min<uint64_t>(imgs, (64ull * std::max<uint64_t>(max_rec, 16) + 15u) & ~15ull));
-    lds_s = enc_i_layout(p->stride, KS, MCs, Cs).total;
+    Cs = window();
+    lds_s = enc_layout(p->stride, p->spec.info.slots, Cs).total;
     if (lds_s > kVarLdsBudget || 64ull * max_rec >= (1ull << 31) || !aligned(d_native, 16)) SM = nullptr;
   }
   if (SM && !p->linear) {
@@ -1845,9 +1838,9 @@ int var_encode(const xdrg_plan &P, const dev_tables &T, const void *d_native, ui
   }
   if (SM) {
     const unsigned long long *bb = bbase;
-    uint32_t sl = stack_limit, mc = MCs, cc = Cs, mk = mark;
+    uint32_t sl = stack_limit, cc = Cs, mk = mark;
     void *args[] = {&nat8, &n, const_cast<uint32_t *>(&p->stride), &d_heap, &heap_len, &xdr8, &cap,
-                    &d_offsets, &sizes, &bb, &sl, &mc, &cc, &mk, &err};
+                    &d_offsets, &sizes, &bb, &sl, &cc, &mk, &err};
     HIPCHK(hipModuleLaunchKernel(static_cast<hipFunction_t>(SM->f_enc), static_cast<uint32_t>(nb), 1, 1, 64, 1,
                                  1, lds_s, s, args, nullptr));
     return XDRG_OK;
@@ -1856,7 +1849,7 @@ int var_encode(const xdrg_plan &P, const dev_tables &T, const void *d_native, ui
 #define LAUNCH_ENC_IU(K, UU)                                                                   \
   k_var_encode_i<K, UU><<<nb, 64, LI.total, s>>>(nat8, n, p->stride, d_heap, heap_len, xdr8,  \
                                                  cap, d_offsets, sizes, bbase, T.d_ops, nops,   \
-                                                 T.d_table, stack_limit, MC, Ci, mark, err)
+                                                 T.d_table, stack_limit, Ci, mark, err)
 #define LAUNCH_ENC_I(K)                                     \
   do {                                                      \
     if (O.enc_unroll == 16) LAUNCH_ENC_IU(K, 16);           \
