@@ -30,14 +30,20 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, ROOT)
 from xdrpp_amd import _abi as A, build as B, marshal as M, schemas as S  # noqa: E402
 
-OUT = os.path.join(ROOT, "tools", "tune", "_stamps" + os.environ.get("U", "") + ("n" if os.environ.get("NOSTAMP") else ""))
+OUT = os.path.join(ROOT, "tools", "tune", "_stamps" + os.environ.get("U", "") + ("n" if os.environ.get("NOSTAMP") else "")
+                   + os.environ.get("TAG", ""))
 NST = 8
 IMAGES = [int(x) for x in os.environ.get("IMAGES", "-1").split()]  # LDS image bytes (-1 auto)
 PHASES = ["sizes+tile+scan", "first walk", "slots+scan", "windows up to the last copy", "last flush"]
 STAMP = ("#define XDRG_STAMP(k) do { if (threadIdx.x == 0) { const unsigned long long t_ = "
          "__builtin_amdgcn_s_memtime(); *reinterpret_cast<volatile unsigned long long *>(xdr + "
          "((cap + 15ull) & ~15ull) + (static_cast<unsigned long long>(blockIdx.x) * " + str(NST) +
+         "ull + (k)) * 8ull) = t_; } } while (0)\n"
+         "#define XDRG_DSTAMP(k) do { if (threadIdx.x == 0) { const unsigned long long t_ = "
+         "__builtin_amdgcn_s_memtime(); *reinterpret_cast<volatile unsigned long long *>(native + "
+         "((n * stride + 15ull) & ~15ull) + (static_cast<unsigned long long>(blockIdx.x) * " + str(NST) +
          "ull + (k)) * 8ull) = t_; } } while (0)\n")
+DPHASES = ["offsets", "window load+heap copy", "walk", "tile out"]
 
 
 def source(plan):
@@ -58,8 +64,8 @@ def build(schemas):
             text = text.replace(", 8>(plan_walk{}", ", " + os.environ["U"] + ">(plan_walk{}")
         with open(src, "w") as f:
             f.write(("" if os.environ.get("NOSTAMP") else STAMP) + text)
-        subprocess.check_call([B.hipcc(), "--genco", f"--offload-arch={B.ARCH}", "-O3", "-std=c++17",
-                               "-I", B.CSRC, "-I", os.path.join(ROOT, "include"),
+        subprocess.check_call([B.hipcc(), "--genco", f"--offload-arch={B.ARCH}", "-O3", "-std=c++17"]
+                              + os.environ.get("CFLAGS", "").split() + ["-I", B.CSRC, "-I", os.path.join(ROOT, "include"),
                                "-o", os.path.join(OUT, f"{name}.co"), src])
         print("built", name)
 
@@ -114,6 +120,34 @@ def run(schemas):
                 t[k].append(e0.elapsed_time(e1) / 5)
         d["encode_ms_library"] = round(float(np.median(t["library"])), 4)
         d["encode_ms_stamped"] = round(float(np.median(t["stamped"])), 4)
+        # decode: the same code object's decode_copy, stamps past the natives
+        nb_nat = nat.numel()
+        nbig = torch.zeros(((nb_nat + 15) & ~15) + nw * NST * 8, dtype=torch.uint8, device=dev)
+        hout = torch.empty(p.decode_heap_bytes(total), dtype=torch.uint8, device=dev)
+        for _ in range(2):
+            mar.status.init(s)
+            mar.launch_decode(want.xdr, n, nbig[:nb_nat], offsets=want.offsets, heap_out=hout)
+            mar.check()
+        if not os.environ.get("NOSTAMP"):
+            st = nbig[((nb_nat + 15) & ~15):].cpu().numpy().view(np.uint64).reshape(nw, NST)[:, :5].astype(np.int64)
+            for i, ph in enumerate(DPHASES):
+                d["dec " + ph] = int(np.median(st[:, i + 1] - st[:, i]))
+            d["dec wave_lifetime_median"] = int(np.median(st[:, 4] - st[:, 0]))
+        t = {"library": [], "variant": []}
+        back = torch.empty_like(nat)
+        for _ in range(5):
+            for k, m in (("library", ref), ("variant", mar)):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(5):
+                    own = (k == "variant") != bool(os.environ.get("SWAP"))  # SWAP: trade output buffers
+                    m.launch_decode(want.xdr, n, nbig[:nb_nat] if own else back, offsets=want.offsets,
+                                    heap_out=hout)
+                e1.record()
+                torch.cuda.synchronize()
+                t[k].append(e0.elapsed_time(e1) / 5)
+        d["decode_ms_library"] = round(float(np.median(t["library"])), 4)
+        d["decode_ms_variant"] = round(float(np.median(t["variant"])), 4)
         res[f"{name}_img{img}"] = d
         print(name, img, json.dumps(d))
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)

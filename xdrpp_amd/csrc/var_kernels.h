@@ -37,6 +37,9 @@
 #ifndef XDRG_STAMP
 #define XDRG_STAMP(k) ((void)0)
 #endif
+#ifndef XDRG_DSTAMP
+#define XDRG_DSTAMP(k) ((void)0)
+#endif
 
 namespace xdrg {
 namespace dev {
@@ -472,6 +475,7 @@ __device__ __forceinline__ void var_decode_body(
   const uint64_t wr0 = static_cast<uint64_t>(blockIdx.x) * 64u;
   const uint32_t nrec = static_cast<uint32_t>(min<uint64_t>(64, n - wr0));
   const uint64_t r = wr0 + lane;
+  XDRG_DSTAMP(0);
   uint64_t a = 0, b = 0;
   if (lane < nrec) {
     a = offsets[r];
@@ -484,47 +488,35 @@ __device__ __forceinline__ void var_decode_body(
   const uint64_t wc = min<uint64_t>(we - ws, C);  // bytes held in the window
   const uintptr_t gbase = reinterpret_cast<uintptr_t>(xdr) + ws;
   const uint32_t sh = static_cast<uint32_t>(gbase & 15u);
+  XDRG_DSTAMP(1);
 
   for (uint32_t i = lane; i < tile_bytes / 16u; i += 64u)
     reinterpret_cast<u32x4 *>(tile)[i] = u32x4{0u, 0u, 0u, 0u};
+  // The window: aligned 16-byte chunks covering [ws, ws + wc), 16 loads in
+  // flight per lane, into LDS.  A chunk never leaves the pages that hold
+  // stream bytes, so edge chunks load whole.  No global store is issued
+  // before the walk: on gfx9 loads and stores share one counter, so a load
+  // issued after a store would also wait for the store to complete.
+  const uint32_t nwin = static_cast<uint32_t>((sh + wc + 15u) >> 4);
+  const uint8_t *g0 = xdr + ws - sh;
   {
-    // Aligned 16-byte chunks covering the stretch [ws, we), 8 loads in
-    // flight per lane.  A chunk never leaves the pages that hold stream
-    // bytes, so edge chunks load whole; only in-range words reach the heap.
-    // Chunks inside [ws, ws + wc) also fill the window.
-    const uint32_t nwin = static_cast<uint32_t>((sh + wc + 15u) >> 4);
-    const uint64_t nall = COPY ? (sh + (we - ws) + 15u) >> 4 : nwin;
-    const uint8_t *g0 = xdr + ws - sh;
-    constexpr int UL = 8;
-    for (uint64_t c0 = 0; c0 < nall; c0 += 64u * UL) {
+    constexpr int UL = 16;
+    for (uint32_t c0 = 0; c0 < nwin; c0 += 64u * UL) {
       u32x4 v[UL];
 #pragma unroll
       for (int u = 0; u < UL; ++u) {
-        const uint64_t ci = c0 + 64u * u + lane;
-        if (ci < nall) v[u] = *reinterpret_cast<const u32x4 *>(g0 + 16u * ci);
+        const uint32_t ci = c0 + 64u * u + lane;
+        if (ci < nwin) v[u] = *reinterpret_cast<const u32x4 *>(g0 + 16u * ci);
       }
 #pragma unroll
       for (int u = 0; u < UL; ++u) {
-        const uint64_t ci = c0 + 64u * u + lane;
-        if (ci >= nall) continue;
+        const uint32_t ci = c0 + 64u * u + lane;
         if (ci < nwin) reinterpret_cast<u32x4 *>(win)[ci] = v[u];
-        if (COPY) {
-          const int64_t o = static_cast<int64_t>(16u * ci) - sh;  // stream offset - ws
-          const int64_t lim = static_cast<int64_t>(we - ws);
-          uint8_t *hd = heap + ws + o;
-          if (o >= 0 && o + 16 <= lim) {
-            st16u(hd, v[u]);
-          } else {
-            if (o >= 0 && o + 4 <= lim) st32(hd, v[u].x);
-            if (o + 4 >= 0 && o + 8 <= lim) st32(hd + 4, v[u].y);
-            if (o + 8 >= 0 && o + 12 <= lim) st32(hd + 8, v[u].z);
-            if (o + 12 >= 0 && o + 16 <= lim) st32(hd + 12, v[u].w);
-          }
-        }
       }
     }
   }
   wave_sync();
+  XDRG_DSTAMP(2);
 
   dec_ctx<RA> c;
   c.rd.xdr = xdr;
@@ -562,12 +554,51 @@ __device__ __forceinline__ void var_decode_body(
     if (ok && c.p != b) report(err, r, kOpRecordLevel, XDRG_ERR_TRAILING);
   }
   wave_sync();
+  XDRG_DSTAMP(3);
+  if (COPY) {
+    // The decoded heap is the stream: the stretch [ws, we) to heap + ws.
+    // Chunks past the window are loaded first (all in flight), then the
+    // window's chunks leave from LDS, then those.
+    const uint64_t nall = (sh + (we - ws) + 15u) >> 4;
+    const int64_t lim = static_cast<int64_t>(we - ws);
+    uint8_t *h0 = heap + ws - sh;
+    auto put = [&](uint64_t ci, const u32x4 &x) {
+      const int64_t o = static_cast<int64_t>(16u * ci) - sh;  // stream offset - ws
+      if (o >= 0 && o + 16 <= lim) {
+        st16u(h0 + 16u * ci, x);
+      } else {
+        uint8_t *hd = h0 + 16u * ci;
+        if (o >= 0 && o + 4 <= lim) st32(hd, x.x);
+        if (o + 4 >= 0 && o + 8 <= lim) st32(hd + 4, x.y);
+        if (o + 8 >= 0 && o + 12 <= lim) st32(hd + 8, x.z);
+        if (o + 12 >= 0 && o + 16 <= lim) st32(hd + 12, x.w);
+      }
+    };
+    constexpr int UB = 8;
+    for (uint64_t c0 = nwin; c0 < nall || c0 == nwin; c0 += 64u * UB) {
+      u32x4 v[UB];
+#pragma unroll
+      for (int u = 0; u < UB; ++u) {
+        const uint64_t ci = c0 + 64u * u + lane;
+        if (ci < nall) v[u] = *reinterpret_cast<const u32x4 *>(g0 + 16u * ci);
+      }
+      if (c0 == nwin)
+        for (uint32_t ci = lane; ci < nwin; ci += 64u) put(ci, reinterpret_cast<const u32x4 *>(win)[ci]);
+#pragma unroll
+      for (int u = 0; u < UB; ++u) {
+        const uint64_t ci = c0 + 64u * u + lane;
+        if (ci < nall) put(ci, v[u]);
+      }
+      if (c0 + 64u * UB >= nall) break;
+    }
+  }
   uint8_t *ndst = native + wr0 * stride;
   const uint32_t nbytes = nrec * stride;
   for (uint32_t i = lane; i < nbytes / 16u; i += 64u)
     reinterpret_cast<u32x4 *>(ndst)[i] = reinterpret_cast<const u32x4 *>(tile)[i];
   for (uint32_t i = (nbytes / 16u) * 4u + lane; i < nbytes / 4u; i += 64u)
     reinterpret_cast<uint32_t *>(ndst)[i] = reinterpret_cast<const uint32_t *>(tile)[i];
+  XDRG_DSTAMP(4);
 }
 
 // ------------------------------------------------------------------ size
