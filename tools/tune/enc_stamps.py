@@ -33,7 +33,7 @@ from xdrpp_amd import _abi as A, build as B, marshal as M, schemas as S  # noqa:
 OUT = os.path.join(ROOT, "tools", "tune", "_stamps" + os.environ.get("U", "") + ("n" if os.environ.get("NOSTAMP") else "")
                    + os.environ.get("TAG", ""))
 NST = 8
-IMAGES = [int(x) for x in os.environ.get("IMAGES", "-1").split()]  # LDS image bytes (-1 auto)
+IMAGES = [int(x) for x in os.environ.get("IMAGES", "-1").split()]  # values of plan option OPT (-1 auto)
 PHASES = ["sizes+tile+scan", "first walk", "slots+scan", "windows up to the last copy", "last flush"]
 STAMP = ("#define XDRG_STAMP(k) do { if (threadIdx.x == 0) { const unsigned long long t_ = "
          "__builtin_amdgcn_s_memtime(); *reinterpret_cast<volatile unsigned long long *>(xdr + "
@@ -60,8 +60,8 @@ def build(schemas):
     for name in schemas:
         src = os.path.join(OUT, f"{name}.hip")
         text = source(M.Plan(S.ALL[name]))
-        if os.environ.get("U"):  # payload chunks in flight per lane (the library's default: 8)
-            text = text.replace(", 8>(plan_walk{}", ", " + os.environ["U"] + ">(plan_walk{}")
+        if os.environ.get("U"):  # payload chunks in flight per lane (the library's default: 4)
+            text = text.replace(", 4>(plan_walk{}", ", " + os.environ["U"] + ">(plan_walk{}")
         with open(src, "w") as f:
             f.write(("" if os.environ.get("NOSTAMP") else STAMP) + text)
         subprocess.check_call([B.hipcc(), "--genco", f"--offload-arch={B.ARCH}", "-O3", "-std=c++17"]
@@ -79,7 +79,7 @@ def run(schemas):
     for name, img in [(nm, i) for nm in schemas for i in IMAGES]:
         n = 1 << 20
         ref = M.Marshaler(M.Plan(S.ALL[name]), dev)
-        p = M.Plan(S.ALL[name], {"image_bytes": img})
+        p = M.Plan(S.ALL[name], {os.environ.get("OPT", "image_bytes"): img})
         code = open(os.path.join(OUT, f"{name}.co"), "rb").read()
         A.check(L.xdrg_plan_load_kernels(p.handle, code, len(code)), "xdrg_plan_load_kernels")
         mar = M.Marshaler(p, dev)

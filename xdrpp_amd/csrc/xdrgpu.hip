@@ -1791,11 +1791,16 @@ int var_encode(const xdrg_plan &P, const dev_tables &T, const void *d_native, ui
   const uint64_t max_rec = p->max_record_bytes + mark;
   const uint32_t KI = p->max_var_slots <= 1 ? 1u : p->max_var_slots <= 2 ? 2u : 4u;
   // LDS window of the wave's output stretch (var_kernels.h): the stretch
-  // leaves in rounds of C bytes.  8 KiB by default, never more than the
-  // longest stretch needs.
+  // leaves in rounds of C bytes, each round walking the records that reach
+  // into it.  tools/tune/enc_stamps.py (MI355X, 1M records, plan-specialized
+  // kernels): a cheap walk wants occupancy -- recvar (6 ops) 4 KiB 0.128 ms,
+  // 8 KiB 0.139; a walk that loads container elements from the heap must not
+  // repeat -- vecrec 8 KiB 0.159, 4 KiB 0.198; rpc (30 ops) 8 KiB 0.214,
+  // 4 KiB 0.216.  Never more than the longest stretch needs.
   auto window = [&](void) -> uint32_t {
     const uint32_t want = O.image_bytes > 0 ? std::max(static_cast<uint32_t>(O.image_bytes) & ~15u, 256u)
-                                            : (8u << 10);
+                          : !p->has_vector && p->ops.size() <= 16 ? (4u << 10)
+                                                                  : (8u << 10);
     return static_cast<uint32_t>(std::min<uint64_t>(want, (64ull * std::max<uint64_t>(max_rec, 16) + 31u) & ~15ull));
   };
   const uint32_t Ci = window();
@@ -1942,11 +1947,14 @@ int var_decode(const xdrg_plan &P, const dev_tables &T, const void *d_xdr, uint6
   uint8_t *nat8 = static_cast<uint8_t *>(d_native);
   const uint32_t nops = uint32_t(p->ops.size());
   const bool copy = d_heap_out != d_xdr;  // heap_out == d_xdr: zero-copy (refs into the stream)
-  // LDS window: tools/tune/ab_var.py (MI355X, 1M records): an 8 KiB window
-  // pays when it holds a wave's whole stretch (vecrec, ~6.6 KiB per 64
-  // records: 0.37 -> 0.30 ms); for longer stretches the occupancy it costs
-  // outweighs it (rpc, ~15 KiB: 0.199 -> 0.220 ms), so they keep 4 KiB.
+  // LDS window: tools/tune/enc_stamps.py (OPT=window_bytes, MI355X, 1M
+  // records).  Plans with a short walk are bound by the global reads of the
+  // records past the window: a 16 KiB window (recvar's whole ~12 KiB
+  // stretch) cut recvar's decode 0.120 -> 0.089 ms, vecrec's 0.222 ->
+  // 0.216.  A long walk (rpc, 30 ops) wants the occupancy instead: 4 KiB
+  // (0.142 ms) beats 8 KiB (0.154) and 16 KiB (0.164).
   const uint32_t win = O.window_bytes >= 0 ? static_cast<uint32_t>(O.window_bytes) & ~15u
+                       : p->ops.size() <= 16 ? (16u << 10)
                        : 64ull * (len / n) <= (8u << 10) ? (8u << 10) : (4u << 10);
   const uint32_t Cw = static_cast<uint32_t>(std::min<uint64_t>(
       win, (64ull * std::max<uint64_t>(p->max_record_bytes + mark, 16) + 15u) & ~15ull));
