@@ -175,7 +175,11 @@ __device__ __forceinline__ uint32_t chunks_starting_before(const enc_ctx<KMAX> &
 // and the window leaves as aligned, whole-line 16-byte stores.  No partial
 // or scattered global store, so each 64-byte line of the stream is one
 // write request to L2.
-template <class W, int KMAX, int U>
+// NW > 0 (plan-specialized walks, whose field offsets are constants): the
+// lane's record (NW words) is copied from the tile into registers before
+// the walk, so the walk issues no LDS read -- its reads no longer wait
+// behind its own image writes.  NW = 0: the walk reads the tile.
+template <class W, int KMAX, int U, int NW = 0>
 __device__ __forceinline__ void var_encode_body(
     const W &w, const uint8_t *__restrict__ native, uint64_t n, uint32_t stride,
     const uint8_t *__restrict__ heap, uint64_t heap_len, uint8_t *__restrict__ xdr, uint64_t cap,
@@ -246,7 +250,15 @@ __device__ __forceinline__ void var_encode_body(
           c.put(mark_word(sz - 4u));
         }
       }
-      okr = w.enc(c, tile + lane * stride, okr);
+      if constexpr (NW > 0) {
+        uint32_t rec[NW];
+        const uint32_t *t32 = reinterpret_cast<const uint32_t *>(tile + lane * stride);
+#pragma unroll
+        for (int k = 0; k < NW; ++k) rec[k] = t32[k];
+        okr = w.enc(c, reinterpret_cast<const uint8_t *>(rec), okr);
+      } else {
+        okr = w.enc(c, tile + lane * stride, okr);
+      }
       if (rd == 0) {
         ok = okr;
         if (!ok) {  // a failing record's bytes are unspecified (never past `cap`)
