@@ -32,7 +32,7 @@ from xdrpp_amd import _abi as A, build as B, marshal as M, schemas as S  # noqa:
 
 OUT = os.path.join(ROOT, "tools", "tune", "_stamps" + os.environ.get("U", "") + ("n" if os.environ.get("NOSTAMP") else "")
                    + os.environ.get("TAG", ""))
-NST = 8
+NST = 10
 IMAGES = [int(x) for x in os.environ.get("IMAGES", "-1").split()]  # values of plan option OPT (-1 auto)
 PHASES = ["sizes+tile+scan", "first walk", "slots+scan", "windows up to the last copy", "last flush"]
 STAMP = ("#define XDRG_STAMP(k) do { if (threadIdx.x == 0) { const unsigned long long t_ = "
@@ -103,10 +103,14 @@ def run(schemas):
         torch.cuda.synchronize()
         d = {}
         if not os.environ.get("NOSTAMP"):
-            st = big[((total + 15) & ~15):].cpu().numpy().view(np.uint64).reshape(nw, NST)[:, :6].astype(np.int64)
-            life = st[:, 5] - st[:, 0]
-            d = {ph: int(np.median(st[:, i + 1] - st[:, i])) for i, ph in enumerate(PHASES)}
-            d["wave_lifetime_median"] = int(np.median(life))
+            st = big[((total + 15) & ~15):].cpu().numpy().view(np.uint64).reshape(nw, NST).astype(np.int64)
+            # 0 start, 1 offsets, 2 first walk, 3 slots, 4 last payload window, 5 end
+            seq = [(0, 1, "sizes+tile+scan"), (1, 2, "first walk"), (2, 3, "slots"),
+                   (3, 4, "windows up to the last copy"), (4, 5, "last flush")]
+            for a, b_, ph in seq:
+                dd = st[:, b_] - st[:, a]
+                d[ph] = [int(np.median(dd)), int(np.percentile(dd, 90))]
+            d["wave_lifetime_median"] = int(np.median(st[:, 5] - st[:, 0]))
         d["encode_ms_all_passes"] = round(ev[0].elapsed_time(ev[1]), 4)
         t = {"library": [], "stamped": []}
         for _ in range(5):
