@@ -528,6 +528,8 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
   g.dec_block(0, kNoPc);
   const std::string dec_code = g.o.str();
 
+  uint32_t maxd = 0;  // deepest field: the stack budget a wave must have to skip the checks
+  for (const xdrg_op &o : p.ops) maxd = std::max<uint32_t>(maxd, o.depth);
   info.slots = std::max<uint32_t>(1, slots);
   info.max_chunks = chunks;
   std::ostringstream s;
@@ -540,8 +542,10 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
     << "  __device__ __forceinline__ uint64_t size(const uint8_t *nat, uint32_t &bad_op) const {\n"
     << "    uint64_t s = 0;\n"
     << size_code << "    return s;\n  }\n"
-    << "  template <int K>\n"
-    << "  __device__ __forceinline__ bool enc(enc_ctx<K> &c, const uint8_t *nat, bool ok) const {\n"
+    << "  static constexpr bool kFastWalk = true;  // enc() also runs on an unchecked context\n"
+    << "  static constexpr uint32_t kMaxDepth = " << maxd << "u;\n"
+    << "  template <class CTX>\n"
+    << "  __device__ __forceinline__ bool enc(CTX &c, const uint8_t *nat, bool ok) const {\n"
     << "    if (!ok) return false;\n"
     << enc_code << "    return true;\n  }\n"
     << "  template <bool RA>\n"

@@ -24,7 +24,7 @@
 // Walkers: the plan interpreter (xdrgpu.hip, any plan) and the plan-
 // specialized walkers that spec.cpp generates as straight-line code per
 // plan and compiles with hiprtc.  A walker provides
-//   bool enc(enc_ctx<K> &, const uint8_t *nat)
+//   bool enc(CTX &, const uint8_t *nat)  (CTX: an enc_ctx, checked or not)
 //   bool dec(dec_ctx<RA> &, uint8_t *nat)
 //   uint64_t size(const uint8_t *nat, uint32_t &bad_op)
 // and reports its own field errors through the context.
@@ -73,7 +73,7 @@ struct echunk_desc {  // 16 bytes: one payload slot of one lane
 // walk stores only the words of the current window (LDS image); payloads
 // in registered slots are copied by the wave's chunk pass; the rest
 // (container elements, payloads past the slots) word by word by the lane.
-template <int KMAX>
+template <int KMAX, bool CHECK = true>
 struct enc_ctx {
   uint8_t *img;
   uint32_t w0, C;
@@ -95,6 +95,7 @@ struct enc_ctx {
   // check(n) of xdr_generic_put (marshal.h:104-108) after the stack budget
   // of the field's class level (marshal.h:129-136)
   __device__ __forceinline__ bool field(uint32_t op, uint32_t depth, uint64_t need) {
+    if constexpr (!CHECK) return true;  // the wave fits `cap` and the plan's depth fits the budget
     if (depth > stack_limit) {
       report(err, r, op, XDRG_ERR_STACK_PUT);
       return false;
@@ -146,6 +147,24 @@ struct enc_ctx {
   }
   // a word of the heap (container elements), bytes past heap_len read 0
   __device__ __forceinline__ uint32_t hword(uint64_t off) const { return unaligned_word(heap, heap_len, off); }
+
+  // the same state under the other checking mode, and back
+  template <bool B>
+  __device__ __forceinline__ enc_ctx<KMAX, B> as() const {
+    enc_ctx<KMAX, B> o;
+    o.img = img; o.w0 = w0; o.C = C; o.heap = heap; o.heap_len = heap_len; o.cap = cap;
+    o.stack_limit = stack_limit; o.r = r; o.err = err; o.at = at; o.pos = pos;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) { o.psr[k] = psr[k]; o.pds[k] = pds[k]; o.pln[k] = pln[k]; }
+    return o;
+  }
+  template <bool B>
+  __device__ __forceinline__ void take(const enc_ctx<KMAX, B> &o) {
+    at = o.at;
+    pos = o.pos;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) { psr[k] = o.psr[k]; pds[k] = o.pds[k]; pln[k] = o.pln[k]; }
+  }
 };
 
 // Chunks of a lane's slots that end at or before image-space offset `a`,
@@ -242,22 +261,39 @@ __device__ __forceinline__ void var_encode_body(
       c.at = a0;
       c.pos = off;
       bool okr = szok;
-      if (okr && mark) {  // the message's record mark (message_t::alloc, marshal.cc:15-31)
-        if (4 > cap - min(c.pos, cap)) {
-          report(err, r, kOpRecordLevel, XDRG_ERR_OVERFLOW_PUT);
-          okr = false;
+      auto walk = [&](auto &cc, bool o) -> bool {
+        if constexpr (NW > 0) {
+          uint32_t rec[NW];
+          const uint32_t *t32 = reinterpret_cast<const uint32_t *>(tile + lane * stride);
+#pragma unroll
+          for (int k = 0; k < NW; ++k) rec[k] = t32[k];
+          return w.enc(cc, reinterpret_cast<const uint8_t *>(rec), o);
         } else {
-          c.put(mark_word(sz - 4u));
+          return w.enc(cc, tile + lane * stride, o);
+        }
+      };
+      bool checked = true;
+      if constexpr (W::kFastWalk) {
+        // the wave's bytes fit `cap` and the plan's depth fits the stack
+        // budget: no field can fail a check -- walk without them
+        if (wave_out + T <= cap && W::kMaxDepth <= stack_limit) {
+          checked = false;
+          enc_ctx<KMAX, false> f = c.template as<false>();
+          if (okr && mark) f.put(mark_word(sz - 4u));
+          okr = walk(f, okr);
+          c.take(f);
         }
       }
-      if constexpr (NW > 0) {
-        uint32_t rec[NW];
-        const uint32_t *t32 = reinterpret_cast<const uint32_t *>(tile + lane * stride);
-#pragma unroll
-        for (int k = 0; k < NW; ++k) rec[k] = t32[k];
-        okr = w.enc(c, reinterpret_cast<const uint8_t *>(rec), okr);
-      } else {
-        okr = w.enc(c, tile + lane * stride, okr);
+      if (checked) {
+        if (okr && mark) {  // the message's record mark (message_t::alloc, marshal.cc:15-31)
+          if (4 > cap - min(c.pos, cap)) {
+            report(err, r, kOpRecordLevel, XDRG_ERR_OVERFLOW_PUT);
+            okr = false;
+          } else {
+            c.put(mark_word(sz - 4u));
+          }
+        }
+        okr = walk(c, okr);
       }
       if (rd == 0) {
         ok = okr;

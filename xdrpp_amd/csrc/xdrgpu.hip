@@ -762,6 +762,8 @@ overflow:
 // replace this walk; the interpreter serves every plan, and any plan on a
 // device where its specialized kernels are not loaded.
 struct interp_walk {
+  static constexpr bool kFastWalk = false;  // enc() takes the checked context only
+  static constexpr uint32_t kMaxDepth = 0;
   const xdrg_op *__restrict__ ops;
   uint32_t nops;
   const uint32_t *__restrict__ table;
