@@ -30,6 +30,7 @@ constexpr uint32_t kNoPc = 0xffffffffu;
 constexpr uint32_t kSlotMax = 4;        // chunk-map slots per record (var_kernels.h)
 constexpr uint32_t kSlotBytes = 1u << 30;  // longer payloads are copied by their lane
 constexpr uint32_t kRegRecordBytes = 128;  // records up to this size are walked from registers
+constexpr uint32_t kMaxListWords = 24;     // word-list walks: register budget of emit_words
 
 std::string u32(uint32_t v) {
   char b[16];
@@ -44,6 +45,7 @@ struct gen {
   int ind = 1;
   uint32_t max_slots = 0;  // static chunk-map slots used on the longest path
   uint64_t max_chunks = 0; // 16-byte chunks those slots can hold (per record)
+  bool word_list = true;   // every payload takes a slot, no container loop (var_kernels.h WL)
 
   explicit gen(const xdrg_plan &plan) : p(plan) { post_dominators(); }
 
@@ -158,8 +160,9 @@ struct gen {
 
   // ---------------------------------------------------------------- encode
   // xdr_generic_put field by field (marshal.h:84-137).  Returns the static
-  // slots used after the block (slots count along the path).
-  uint32_t enc_block(uint32_t pc, uint32_t stop, uint32_t slot, uint64_t &chunks) {
+  // slots used after the block (slots count along the path); `words` = the
+  // most scalar words a path through the block puts.
+  uint32_t enc_block(uint32_t pc, uint32_t stop, uint32_t slot, uint64_t &chunks, uint32_t &words) {
     while (pc != stop) {
       const xdrg_op &e = op(pc);
       const std::string f = "nat + " + u32(e.noff), P = u32(pc), D = u32(e.depth);
@@ -169,18 +172,22 @@ struct gen {
       case XDRG_OP_U32: case XDRG_OP_ENUM:
         line("if (!c.field(" + P + ", " + D + ", 4)) return false;");
         line("c.put(bswap32(ld32(" + f + ")));");
+        words += 1;
         break;
       case XDRG_OP_BOOL:
         line("if (!c.field(" + P + ", " + D + ", 4)) return false;");
         line("c.put(nat[" + u32(e.noff) + "] ? 0x01000000u : 0u);");
+        words += 1;
         break;
       case XDRG_OP_U64:
         line("if (!c.field(" + P + ", " + D + ", 8)) return false;");
         line("c.put(bswap32(ld32(" + f + " + 4)));");
         line("c.put(bswap32(ld32(" + f + ")));");
+        words += 2;
         break;
       case XDRG_OP_OPAQUE: {
         line("if (!c.field(" + P + ", " + D + ", " + u32(e.arg0) + ")) return false;");
+        words += (e.arg0 + 3u) / 4u;
         for (uint32_t k = 0; 4 * k < e.arg0; ++k) {
           std::string w;
           for (uint32_t b = 0; b < 4 && 4 * k + b < e.arg0; ++b)
@@ -196,18 +203,22 @@ struct gen {
         line("const uint32_t len = ld32(" + f + " + 8);");
         line("if (!c.field(" + P + ", " + D + ", 4ull + len)) return false;");
         line("c.put(bswap32(len));");
+        words += 1;
         line("const uint64_t src = *reinterpret_cast<const uint64_t *>(" + f + ");");
         if (slot < kSlotMax) {
           const uint32_t cap = std::min(e.arg0, kSlotBytes);
-          if (e.arg0 > kSlotBytes)
+          if (e.arg0 > kSlotBytes) {
             line("if (len > " + u32(kSlotBytes) + ") c.copy(src, len); else c.template slot<" +
                  std::to_string(slot) + ">(src, len);");
-          else
+            word_list = false;
+          } else {
             line("c.template slot<" + std::to_string(slot) + ">(src, len);");
+          }
           chunks += (cap + 15u) / 16u;
           ++slot;
         } else {
           line("c.copy(src, len);");
+          word_list = false;
         }
         --ind;
         line("}");
@@ -220,8 +231,9 @@ struct gen {
         ++ind;
         line("const uint32_t d = ld32(" + f + ");");
         line("c.put(bswap32(d));");
+        words += 1;
         line("switch (d) {");
-        uint32_t smax = slot;
+        uint32_t smax = slot, wmax = words;
         uint64_t cmax = chunks;
         for (auto &a : arms(e)) {
           std::string lab;
@@ -229,8 +241,10 @@ struct gen {
           line(lab + "{");
           ++ind;
           uint64_t ch = chunks;
-          smax = std::max(smax, enc_block(a.first, end, slot, ch));
+          uint32_t wd = words;
+          smax = std::max(smax, enc_block(a.first, end, slot, ch, wd));
           cmax = std::max(cmax, ch);
+          wmax = std::max(wmax, wd);
           --ind;
           line("} break;");
         }
@@ -238,8 +252,10 @@ struct gen {
           line("default: {");
           ++ind;
           uint64_t ch = chunks;
-          smax = std::max(smax, enc_block(e.arg4, end, slot, ch));
+          uint32_t wd = words;
+          smax = std::max(smax, enc_block(e.arg4, end, slot, ch, wd));
           cmax = std::max(cmax, ch);
+          wmax = std::max(wmax, wd);
           --ind;
           line("} break;");
         } else {
@@ -250,10 +266,12 @@ struct gen {
         line("}");
         slot = smax;
         chunks = cmax;
+        words = wmax;
         pc = end;
         continue;
       }
       case XDRG_OP_VECTOR: {
+        word_list = false;
         line("{");
         ++ind;
         line("const uint64_t eoff = *reinterpret_cast<const uint64_t *>(" + f + ");");
@@ -520,7 +538,12 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
   g.o.str("");
   g.ind = 2;
   uint64_t chunks = 0;
-  const uint32_t slots = g.enc_block(0, kNoPc, 0, chunks);
+  uint32_t words = 0;
+  const uint32_t slots = g.enc_block(0, kNoPc, 0, chunks, words);
+  // the word list (mark + words, 4 bytes each per lane) must fit in the
+  // tile it aliases, and the walk must run from registers
+  const bool regs = p.stride <= kRegRecordBytes && p.stride % 4 == 0;
+  const uint32_t kwords = g.word_list && regs && words + 1 <= kMaxListWords && 4 * (words + 1) <= p.stride ? words : 0;
   const std::string enc_code = g.o.str();
   // decode
   g.o.str("");
@@ -531,6 +554,7 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
   uint32_t maxd = 0;  // deepest field: the stack budget a wave must have to skip the checks
   for (const xdrg_op &o : p.ops) maxd = std::max<uint32_t>(maxd, o.depth);
   info.slots = std::max<uint32_t>(1, slots);
+  info.dec_regs = regs;
   info.max_chunks = chunks;
   std::ostringstream s;
   s << "// Generated by libxdrgpu (codegen.cpp) from a plan of " << p.ops.size()
@@ -544,6 +568,7 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
     << size_code << "    return s;\n  }\n"
     << "  static constexpr bool kFastWalk = true;  // enc() also runs on an unchecked context\n"
     << "  static constexpr uint32_t kMaxDepth = " << maxd << "u;\n"
+    << "  static constexpr uint32_t kWords = " << kwords << "u;  // scalar words per record (0: no word list)\n"
     << "  template <class CTX>\n"
     << "  __device__ __forceinline__ bool enc(CTX &c, const uint8_t *nat, bool ok) const {\n"
     << "    if (!ok) return false;\n"
@@ -562,7 +587,7 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
     << "    uint8_t *xdr, uint64_t cap, uint64_t *offsets, const uint32_t *sizes,\n"
     << "    const unsigned long long *block_base, uint32_t stack_limit, uint32_t C,\n"
     << "    uint32_t mark, unsigned long long *err) {\n"
-    << "  var_encode_body<plan_walk, " << info.slots << ", 4, " << (p.stride <= kRegRecordBytes && p.stride % 4 == 0 ? p.stride / 4 : 0)
+    << "  var_encode_body<plan_walk, " << info.slots << ", 4, " << (regs ? p.stride / 4 : 0)
     << ">(plan_walk{}, native, n, stride, heap, heap_len,\n"
     << "      xdr, cap, offsets, sizes, block_base, stack_limit, C, mark, err);\n}\n\n";
   for (int cp = 0; cp < 2; ++cp)
@@ -571,7 +596,7 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
       << "    uint32_t stride, uint8_t *heap, uint32_t stack_limit, uint32_t C, uint64_t ebase,\n"
       << "    uint32_t F, uint32_t mark, unsigned long long *err) {\n"
       << "  var_decode_body<plan_walk, " << (cp ? "true" : "false")
-      << ", true>(plan_walk{}, xdr, len, offsets, n, native, stride, heap,\n"
+      << ", true, " << (regs ? p.stride / 4 : 0) << ">(plan_walk{}, xdr, len, offsets, n, native, stride, heap,\n"
       << "      stack_limit, C, ebase, F, mark, err);\n}\n\n";
   info.source = s.str();
   return true;

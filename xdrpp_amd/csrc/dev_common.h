@@ -88,20 +88,21 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 // Stage nbytes (a multiple of 4) of native records from a 16-byte aligned
-// global address to LDS: 16-byte loads, up to 4 per lane in flight before
-// any LDS store (one memory round trip per 4 KiB per wave).
+// global address to LDS: 16-byte loads, up to UL per lane in flight before
+// any LDS store (one memory round trip per UL KiB per 64 threads).
+template <int UL = 4>
 __device__ __forceinline__ void stage_tile(uint8_t *tile, const uint8_t *src, uint32_t nbytes,
                                            uint32_t lane, uint32_t nthreads) {
   const uint32_t n16 = nbytes / 16u;
-  for (uint32_t i0 = 0; i0 < n16; i0 += 4u * nthreads) {
-    u32x4 t[4];
+  for (uint32_t i0 = 0; i0 < n16; i0 += UL * nthreads) {
+    u32x4 t[UL];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < UL; ++k) {
       const uint32_t i = i0 + k * nthreads + lane;
       if (i < n16) t[k] = reinterpret_cast<const u32x4 *>(src)[i];
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < UL; ++k) {
       const uint32_t i = i0 + k * nthreads + lane;
       if (i < n16) reinterpret_cast<u32x4 *>(tile)[i] = t[k];
     }

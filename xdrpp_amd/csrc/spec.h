@@ -16,13 +16,14 @@ constexpr int kSpecDevices = 64;
 // Interface version of the generated kernels (their parameter lists and
 // LDS layout, var_kernels.h): the source defines xdrg_spec_iface with it,
 // and a code object that carries another value is refused at load.
-constexpr unsigned kSpecIface = 3;
+constexpr unsigned kSpecIface = 4;
 
 // The generated source of a plan and the launch facts it fixes.
 struct spec_info {
   std::string source;     // HIP source over var_kernels.h
   uint32_t slots = 1;     // chunk-map slots per record the encode kernel uses
   uint64_t max_chunks = 0;  // 16-byte chunks those slots hold per record (bounds)
+  bool dec_regs = false;  // the decode walks into registers: no native tile in LDS
 };
 
 // Kernels of one plan on one device.

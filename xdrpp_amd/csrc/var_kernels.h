@@ -73,7 +73,12 @@ struct echunk_desc {  // 16 bytes: one payload slot of one lane
 // walk stores only the words of the current window (LDS image); payloads
 // in registered slots are copied by the wave's chunk pass; the rest
 // (container elements, payloads past the slots) word by word by the lane.
-template <int KMAX, bool CHECK = true>
+// WL > 0 (word-list walk, plans whose scalar words per record are bounded
+// by WL and whose payloads all take slots): the walk runs once and puts the
+// record's scalar words in a list (LDS, word-major: word j of the lane at
+// sw[64 j]); `rb[k]` = words before slot k.  Each window then places the
+// list's words that land in it (emit_words) instead of walking again.
+template <int KMAX, bool CHECK = true, int WL = 0>
 struct enc_ctx {
   uint8_t *img;
   uint32_t w0, C;
@@ -87,6 +92,9 @@ struct enc_ctx {
   uint64_t pos;
   uint64_t psr[KMAX];
   uint32_t pds[KMAX], pln[KMAX];
+  uint32_t *sw;  // WL: this lane's column of the word list
+  uint32_t nw;   // WL: words listed
+  uint32_t rb[KMAX > 0 ? KMAX : 1];
 
   // word `v` at image-space offset `a`, if it lies in the window
   __device__ __forceinline__ void wput(uint32_t a, uint32_t v) {
@@ -107,7 +115,12 @@ struct enc_ctx {
     return true;
   }
   __device__ __forceinline__ void put(uint32_t v) {
-    wput(at, v);
+    if constexpr (WL > 0) {
+      sw[64u * nw] = v;
+      ++nw;
+    } else {
+      wput(at, v);
+    }
     at += 4;
     pos += 4;
   }
@@ -123,6 +136,7 @@ struct enc_ctx {
       pds[K] = at;
       pln[K] = len;
     }
+    if constexpr (WL > 0) rb[K] = nw;
     skip(len);
   }
   // the same, slot chosen at run time (interpreter walk)
@@ -150,35 +164,56 @@ struct enc_ctx {
 
   // the same state under the other checking mode, and back
   template <bool B>
-  __device__ __forceinline__ enc_ctx<KMAX, B> as() const {
-    enc_ctx<KMAX, B> o;
+  __device__ __forceinline__ enc_ctx<KMAX, B, WL> as() const {
+    enc_ctx<KMAX, B, WL> o;
     o.img = img; o.w0 = w0; o.C = C; o.heap = heap; o.heap_len = heap_len; o.cap = cap;
     o.stack_limit = stack_limit; o.r = r; o.err = err; o.at = at; o.pos = pos;
+    o.sw = sw; o.nw = nw;
 #pragma unroll
-    for (int k = 0; k < KMAX; ++k) { o.psr[k] = psr[k]; o.pds[k] = pds[k]; o.pln[k] = pln[k]; }
+    for (int k = 0; k < KMAX; ++k) { o.psr[k] = psr[k]; o.pds[k] = pds[k]; o.pln[k] = pln[k]; o.rb[k] = rb[k]; }
     return o;
   }
   template <bool B>
-  __device__ __forceinline__ void take(const enc_ctx<KMAX, B> &o) {
+  __device__ __forceinline__ void take(const enc_ctx<KMAX, B, WL> &o) {
     at = o.at;
     pos = o.pos;
+    nw = o.nw;
 #pragma unroll
-    for (int k = 0; k < KMAX; ++k) { psr[k] = o.psr[k]; pds[k] = o.pds[k]; pln[k] = o.pln[k]; }
+    for (int k = 0; k < KMAX; ++k) { psr[k] = o.psr[k]; pds[k] = o.pds[k]; pln[k] = o.pln[k]; rb[k] = o.rb[k]; }
   }
 };
 
+// Word-list walk: the listed words of a lane's record (first byte at
+// image-space offset a0) that land in the window [w0, w0 + C) -> image.
+// Word j sits after the padded payloads of the slots listed before it.
+template <int KMAX, bool B, int WL>
+__device__ __forceinline__ void emit_words(const enc_ctx<KMAX, B, WL> &c, uint32_t a0) {
+  uint32_t v[WL];
+#pragma unroll
+  for (int j = 0; j < WL; ++j)
+    if (static_cast<uint32_t>(j) < c.nw) v[j] = c.sw[64u * j];
+#pragma unroll
+  for (int j = 0; j < WL; ++j) {
+    uint32_t a = a0 + 4u * j;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k)
+      if (static_cast<uint32_t>(j) >= c.rb[k]) a += (c.pln[k] + 3u) & ~3u;
+    if (static_cast<uint32_t>(j) < c.nw && a - c.w0 < c.C) *reinterpret_cast<uint32_t *>(c.img + (a - c.w0)) = v[j];
+  }
+}
+
 // Chunks of a lane's slots that end at or before image-space offset `a`,
 // and that start before `a` (the slots' chunks are in stream order).
-template <int KMAX>
-__device__ __forceinline__ uint32_t chunks_ending_by(const enc_ctx<KMAX> &c, uint32_t a) {
+template <int KMAX, bool B, int WL>
+__device__ __forceinline__ uint32_t chunks_ending_by(const enc_ctx<KMAX, B, WL> &c, uint32_t a) {
   uint32_t s = 0;
 #pragma unroll
   for (int k = 0; k < KMAX; ++k)
     if (c.pln[k] && a >= c.pds[k] + 16u) s += min((c.pln[k] + 15u) >> 4, (a - c.pds[k]) >> 4);
   return s;
 }
-template <int KMAX>
-__device__ __forceinline__ uint32_t chunks_starting_before(const enc_ctx<KMAX> &c, uint32_t a) {
+template <int KMAX, bool B, int WL>
+__device__ __forceinline__ uint32_t chunks_starting_before(const enc_ctx<KMAX, B, WL> &c, uint32_t a) {
   uint32_t s = 0;
 #pragma unroll
   for (int k = 0; k < KMAX; ++k)
@@ -198,6 +233,9 @@ __device__ __forceinline__ uint32_t chunks_starting_before(const enc_ctx<KMAX> &
 // lane's record (NW words) is copied from the tile into registers before
 // the walk, so the walk issues no LDS read -- its reads no longer wait
 // behind its own image writes.  NW = 0: the walk reads the tile.
+// WL (plans with a bounded scalar word list, W::kWords > 0, walked from
+// registers): the list aliases the tile, which the walk no longer reads once
+// the lane's record is in registers; the walk runs once, in the first round.
 template <class W, int KMAX, int U, int NW = 0>
 __device__ __forceinline__ void var_encode_body(
     const W &w, const uint8_t *__restrict__ native, uint64_t n, uint32_t stride,
@@ -221,7 +259,7 @@ __device__ __forceinline__ void var_encode_body(
   // (sizes, block base and the native tile are loaded in one round trip)
   const uint32_t sz = r < n ? sizes[r] : kSizeErr;
   const uint64_t wave_out = block_base[blockIdx.x];
-  stage_tile(tile, native + wr0 * stride, nrec * stride, lane, 64u);
+  stage_tile<8>(tile, native + wr0 * stride, nrec * stride, lane, 64u);
   const bool szok = !(sz & kSizeErr);
   const uint32_t v = szok ? sz : 0u;
   const uint32_t incl = wave_incl_scan(v);  // a wave's stretch < 2^31 bytes (launch condition)
@@ -239,7 +277,10 @@ __device__ __forceinline__ void var_encode_body(
   const uint32_t rounds = T ? (span + C - 1u) / C : 1u;
   const uint64_t ge = min<uint64_t>(wave_out + T, cap);  // last stream byte + 1 to write
 
-  enc_ctx<KMAX> c;
+  constexpr int WL = (W::kWords > 0 && NW > 0) ? static_cast<int>(W::kWords) + 1 : 0;  // + the mark
+  enc_ctx<KMAX, true, WL> c;
+  c.sw = reinterpret_cast<uint32_t *>(tile) + lane;
+  c.nw = 0;
   c.img = img;
   c.C = C;
   c.heap = heap;
@@ -249,7 +290,7 @@ __device__ __forceinline__ void var_encode_body(
   c.r = r;
   c.err = err;
 #pragma unroll
-  for (int k = 0; k < KMAX; ++k) { c.psr[k] = 0; c.pds[k] = 0; c.pln[k] = 0; }
+  for (int k = 0; k < KMAX; ++k) { c.psr[k] = 0; c.pds[k] = 0; c.pln[k] = 0; c.rb[k] = 0; }
   bool ok = szok;
   uint32_t M = 0;
   for (uint32_t rd = 0; rd < rounds; ++rd) {
@@ -257,16 +298,19 @@ __device__ __forceinline__ void var_encode_body(
     c.w0 = w0;
     // ---- walk: the window's scalar words -> image, payload slots -> registers
     // (every lane walks in the first round: it reports the record's errors)
-    if (rd == 0 || (ok && a0 < w0 + C && a0 + v > w0)) {
+    if (rd == 0 || (WL == 0 && ok && a0 < w0 + C && a0 + v > w0)) {
       c.at = a0;
       c.pos = off;
       bool okr = szok;
+      uint32_t rec[NW > 0 ? NW : 1];
+      if constexpr (NW > 0) {
+        const uint32_t *t32 = reinterpret_cast<const uint32_t *>(tile + lane * stride);
+#pragma unroll
+        for (int k = 0; k < NW; ++k) rec[k] = t32[k];
+        if constexpr (WL > 0) wave_sync();  // every tile read before the list (mark included) overwrites it
+      }
       auto walk = [&](auto &cc, bool o) -> bool {
         if constexpr (NW > 0) {
-          uint32_t rec[NW];
-          const uint32_t *t32 = reinterpret_cast<const uint32_t *>(tile + lane * stride);
-#pragma unroll
-          for (int k = 0; k < NW; ++k) rec[k] = t32[k];
           return w.enc(cc, reinterpret_cast<const uint8_t *>(rec), o);
         } else {
           return w.enc(cc, tile + lane * stride, o);
@@ -278,7 +322,7 @@ __device__ __forceinline__ void var_encode_body(
         // budget: no field can fail a check -- walk without them
         if (wave_out + T <= cap && W::kMaxDepth <= stack_limit) {
           checked = false;
-          enc_ctx<KMAX, false> f = c.template as<false>();
+          enc_ctx<KMAX, false, WL> f = c.template as<false>();
           if (okr && mark) f.put(mark_word(sz - 4u));
           okr = walk(f, okr);
           c.take(f);
@@ -318,6 +362,8 @@ __device__ __forceinline__ void var_encode_body(
       XDRG_STAMP(3);
     }
     wave_sync();
+    if constexpr (WL > 0)
+      if (ok && a0 < w0 + C && a0 + v > w0) emit_words(c, a0);
 
     // ---- payload chunks of the window: heap -> image, U per lane in flight.
     // Chunk i of the wave (stream order) belongs to the lane L with
@@ -430,8 +476,10 @@ __device__ __forceinline__ void var_encode_body(
 }
 
 // ---------------------------------------------------------------- decode
-__host__ __device__ inline uint32_t dec_w_lds(uint32_t stride, uint32_t C) {
-  return ((64u * stride + 15u) & ~15u) + C + 32u;
+// LDS of a decode wave: the native tile (none when the walk decodes into
+// registers, NWD > 0) and the window.
+__host__ __device__ inline uint32_t dec_w_lds(uint32_t stride, uint32_t C, bool regs = false) {
+  return (regs ? 0u : ((64u * stride + 15u) & ~15u)) + C + 32u;
 }
 
 // Stream reader of a wave: the window for stream bytes in [ws, ws + wc),
@@ -509,7 +557,10 @@ struct dec_ctx {
   }
 };
 
-template <class W, bool COPY, bool RA>
+// NWD > 0 (plan-specialized walks, whose native offsets are constants): the
+// lane decodes its record into NWD registers and stores them itself, so the
+// wave keeps no native tile in LDS (more waves per CU, or a larger window).
+template <class W, bool COPY, bool RA, int NWD = 0>
 __device__ __forceinline__ void var_decode_body(
     const W &w, const uint8_t *__restrict__ xdr, uint64_t len, const uint64_t *__restrict__ offsets,
     uint64_t n, uint8_t *__restrict__ native, uint32_t stride, uint8_t *__restrict__ heap,
@@ -517,7 +568,7 @@ __device__ __forceinline__ void var_decode_body(
     unsigned long long *err) {
   extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
   const uint32_t lane = threadIdx.x;
-  const uint32_t tile_bytes = (64u * stride + 15u) & ~15u;
+  const uint32_t tile_bytes = NWD > 0 ? 0u : (64u * stride + 15u) & ~15u;
   uint8_t *tile = sm;
   uint8_t *win = sm + tile_bytes;
   const uint64_t wr0 = static_cast<uint64_t>(blockIdx.x) * 64u;
@@ -585,8 +636,11 @@ __device__ __forceinline__ void var_decode_body(
   c.err = err;
   c.heap = heap;
   c.ecur = ebase + static_cast<uint64_t>(F) * a;  // this record's element arrays
+  uint32_t rec[NWD > 0 ? NWD : 1];
+#pragma unroll
+  for (int k = 0; k < (NWD > 0 ? NWD : 1); ++k) rec[k] = 0u;
   {
-    uint8_t *nat = tile + lane * stride;
+    uint8_t *nat = NWD > 0 ? reinterpret_cast<uint8_t *>(rec) : tile + lane * stride;
     bool ok = false;
     if (lane < nrec) {
       // xdr_from_msg: the message read_message framed (srpc.cc:29-55)
@@ -641,11 +695,30 @@ __device__ __forceinline__ void var_decode_body(
     }
   }
   uint8_t *ndst = native + wr0 * stride;
-  const uint32_t nbytes = nrec * stride;
-  for (uint32_t i = lane; i < nbytes / 16u; i += 64u)
-    reinterpret_cast<u32x4 *>(ndst)[i] = reinterpret_cast<const u32x4 *>(tile)[i];
-  for (uint32_t i = (nbytes / 16u) * 4u + lane; i < nbytes / 4u; i += 64u)
-    reinterpret_cast<uint32_t *>(ndst)[i] = reinterpret_cast<const uint32_t *>(tile)[i];
+  if constexpr (NWD > 0) {
+    if (lane < nrec) {
+      uint8_t *d = ndst + lane * stride;
+      if constexpr (NWD % 4 == 0) {
+#pragma unroll
+        for (int k = 0; k < NWD; k += 4)
+          *reinterpret_cast<u32x4 *>(d + 4 * k) = u32x4{rec[k], rec[k + 1], rec[k + 2], rec[k + 3]};
+      } else if constexpr (NWD % 2 == 0) {
+#pragma unroll
+        for (int k = 0; k < NWD; k += 2)
+          *reinterpret_cast<unsigned long long *>(d + 4 * k) =
+              static_cast<unsigned long long>(rec[k]) | (static_cast<unsigned long long>(rec[k + 1]) << 32);
+      } else {
+#pragma unroll
+        for (int k = 0; k < NWD; ++k) st32(d + 4 * k, rec[k]);
+      }
+    }
+  } else {
+    const uint32_t nbytes = nrec * stride;
+    for (uint32_t i = lane; i < nbytes / 16u; i += 64u)
+      reinterpret_cast<u32x4 *>(ndst)[i] = reinterpret_cast<const u32x4 *>(tile)[i];
+    for (uint32_t i = (nbytes / 16u) * 4u + lane; i < nbytes / 4u; i += 64u)
+      reinterpret_cast<uint32_t *>(ndst)[i] = reinterpret_cast<const uint32_t *>(tile)[i];
+  }
   XDRG_DSTAMP(4);
 }
 
@@ -666,7 +739,7 @@ __device__ __forceinline__ void var_size_body(const W &w, const uint8_t *__restr
   const uint32_t nrec = static_cast<uint32_t>(min<uint64_t>(64, n - wr0));
   const uint8_t *nsrc = native + wr0 * stride;
   if ((reinterpret_cast<uintptr_t>(nsrc) & 15u) == 0) {
-    stage_tile(tile, nsrc, nrec * stride, lane, 64u);
+    stage_tile<8>(tile, nsrc, nrec * stride, lane, 64u);
   } else {
     for (uint32_t i = lane; i < nrec * stride / 4u; i += 64u)
       reinterpret_cast<uint32_t *>(tile)[i] = reinterpret_cast<const uint32_t *>(nsrc)[i];

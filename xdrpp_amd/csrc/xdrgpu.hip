@@ -764,6 +764,7 @@ overflow:
 struct interp_walk {
   static constexpr bool kFastWalk = false;  // enc() takes the checked context only
   static constexpr uint32_t kMaxDepth = 0;
+  static constexpr uint32_t kWords = 0;  // walks every window (no word list)
   const xdrg_op *__restrict__ ops;
   uint32_t nops;
   const uint32_t *__restrict__ table;
@@ -1976,11 +1977,22 @@ int var_decode(const xdrg_plan &P, const dev_tables &T, const void *d_xdr, uint6
   const spec_module *SM = O.specialize && O.dec_kernel == 0 && kern == 2 ? spec_get(*p) : nullptr;
   if (SM) {  // plan-specialized decode walk (spec.cpp)
     const uint64_t nb = (n + 63) / 64;
-    uint32_t st = p->stride, sl = stack_limit, cw = Cw, F = p->heap_factor, mk = mark;
+    uint32_t st = p->stride, sl = stack_limit, cw = Cw, F = p->heap_factor, mk = mark, lws = lw;
+    if (p->spec.info.dec_regs) {
+      // no native tile in LDS: the window gets its room.  tools/tune/
+      // enc_stamps.py (OPT=window_bytes, MI355X, 1M records,
+      // profiles/r02s/ab_dec_window*.log): rpc 4 KiB 0.159 ms, 8 KiB 0.146,
+      // 16 KiB 0.126, 20 KiB 0.128, 32 KiB 0.177; recvar and vecrec are
+      // flat from 16 KiB (0.089, 0.226) and slower below
+      const uint32_t want = O.window_bytes >= 0 ? static_cast<uint32_t>(O.window_bytes) & ~15u : (16u << 10);
+      cw = static_cast<uint32_t>(std::min<uint64_t>(
+          want, (64ull * std::max<uint64_t>(p->max_record_bytes + mark, 16) + 15u) & ~15ull));
+      lws = dec_w_lds(p->stride, cw, true);
+    }
     uint64_t eb = ebase;
     void *args[] = {&xdr8, &len, &d_offsets, &n, &nat8, &st, &d_heap_out, &sl, &cw, &eb, &F, &mk, &err};
     HIPCHK(hipModuleLaunchKernel(static_cast<hipFunction_t>(copy ? SM->f_dec_copy : SM->f_dec),
-                                 static_cast<uint32_t>(nb), 1, 1, 64, 1, 1, lw, s, args, nullptr));
+                                 static_cast<uint32_t>(nb), 1, 1, 64, 1, 1, lws, s, args, nullptr));
     return XDRG_OK;
   }
   if (kern == 2) {
