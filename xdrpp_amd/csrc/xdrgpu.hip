@@ -1212,6 +1212,43 @@ __global__ __launch_bounds__(256) void k_ix_seg(const uint8_t *__restrict__ s, u
       first[q] = rp.fpc == RX_BAD || a + rp.fd + 4 > len ? 0u : ld32(s + a + rp.fd);
     }
   }
+  // REC: the wave's candidates that pass their first word are walked as one
+  // queue (64 lanes per round, lst holds the wave's queue: 1024 entries), not
+  // candidate slot by candidate slot -- a slot where a few lanes pass would
+  // otherwise walk with the rest idle.  A walk leaves its successor in
+  // node[i]; the owner lane reads it back below.
+  uint32_t pmask = 0;
+  if (REC) {
+    const xdrg_op *sops = reinterpret_cast<const xdrg_op *>(rx_smem);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const uint32_t i = 4u * (tid + 256u * (q >> 2)) + (q & 3);
+      const uint64_t a = 4 * (w0 + i);
+      const bool cand = a < len && (rp.fpc == RX_BAD ||
+                                    (a + rp.fd + 4 <= len && rp.fd + 4 <= maxlen &&
+                                     rx_first_ok(sops[rp.fpc], rp.table, bswap32(first[q]))));
+      if (cand) pmask |= 1u << q;
+    }
+    const uint32_t pc = __popc(pmask);
+    uint32_t pin = pc;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(pin, o, 64);
+      if (lane >= static_cast<uint32_t>(o)) pin += y;
+    }
+    const uint32_t ptot = rl32(pin, 63);
+    uint16_t *queue = lst + 1024u * wid;
+    uint32_t qb = pin - pc;
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+      if (pmask & (1u << q)) queue[qb++] = static_cast<uint16_t>(4u * (tid + 256u * (q >> 2)) + (q & 3));
+    wave_sync();
+    for (uint32_t k = lane; k < ptot; k += 64u) {
+      const uint32_t i = queue[k];
+      const uint32_t L = rx_len(sops, rp.table, rd, len, 4 * (w0 + i), maxlen);
+      node[i] = L < RX_LONG ? i + L / 4u : 0xffffffffu;
+    }
+    wave_sync();
+  }
   uint32_t vmask = 0, vnext[16];
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
@@ -1221,13 +1258,7 @@ __global__ __launch_bounds__(256) void k_ix_seg(const uint8_t *__restrict__ s, u
       const int q = 4 * g + j;
       const uint32_t i = 4u * (tid + 256u * g) + j;
       if (REC) {
-        const xdrg_op *sops = reinterpret_cast<const xdrg_op *>(rx_smem);
-        const uint64_t a = 4 * (w0 + i);
-        const bool cand = a < len && (rp.fpc == RX_BAD ||
-                                      (a + rp.fd + 4 <= len && rp.fd + 4 <= maxlen &&
-                                       rx_first_ok(sops[rp.fpc], rp.table, bswap32(first[q]))));
-        const uint32_t L = cand ? rx_len(sops, rp.table, rd, len, a, maxlen) : RX_BAD;
-        vnext[q] = L < RX_LONG ? i + L / 4u : 0xffffffffu;
+        vnext[q] = (pmask & (1u << q)) ? node[i] : 0xffffffffu;
       } else {
         vnext[q] = ix_next(raw[q], i, lim, maxlen);
       }
