@@ -555,6 +555,7 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
   for (const xdrg_op &o : p.ops) maxd = std::max<uint32_t>(maxd, o.depth);
   info.slots = std::max<uint32_t>(1, slots);
   info.dec_regs = regs;
+  info.word_list = kwords > 0;
   info.max_chunks = chunks;
   std::ostringstream s;
   s << "// Generated by libxdrgpu (codegen.cpp) from a plan of " << p.ops.size()

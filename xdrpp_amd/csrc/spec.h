@@ -24,6 +24,7 @@ struct spec_info {
   uint32_t slots = 1;     // chunk-map slots per record the encode kernel uses
   uint64_t max_chunks = 0;  // 16-byte chunks those slots hold per record (bounds)
   bool dec_regs = false;  // the decode walks into registers: no native tile in LDS
+  bool word_list = false; // the encode walks once into a word list (no walk per window)
 };
 
 // Kernels of one plan on one device.

@@ -1854,7 +1854,12 @@ int var_encode(const xdrg_plan &P, const dev_tables &T, const void *d_native, ui
   const spec_module *SM = O.specialize && O.enc_kernel == 0 && !p->has_sub ? spec_get(*p) : nullptr;
   uint32_t Cs = 0, lds_s = 0;
   if (SM) {
-    Cs = window();
+    // a word-list walk (var_kernels.h WL) does not repeat per window, so
+    // small windows cost no walks: rpc 4 KiB 0.169 ms vs 8 KiB 0.181,
+    // recvar 4 KiB (profiles/r02s/ab_enc_wordlist_u*.log)
+    Cs = p->spec.info.word_list && O.image_bytes <= 0
+             ? static_cast<uint32_t>(std::min<uint64_t>(4u << 10, (64ull * std::max<uint64_t>(max_rec, 16) + 31u) & ~15ull))
+             : window();
     lds_s = enc_layout(p->stride, p->spec.info.slots, Cs).total;
     if (lds_s > kVarLdsBudget || 64ull * max_rec >= (1ull << 31) || !aligned(d_native, 16)) SM = nullptr;
   }
