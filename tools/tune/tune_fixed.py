@@ -16,7 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 SO = os.path.join(HERE, "libtune.so")
 if not os.path.exists(SO):
     subprocess.check_call(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-                           "-o", SO, os.path.join(HERE, "tune_fixed.hip")])
+                           "-I", os.path.join(ROOT, "include"), "-o", SO, os.path.join(HERE, "tune_fixed.hip")])
 L = C.CDLL(SO)
 vp, u64, i32, u32 = C.c_void_p, C.c_uint64, C.c_int, C.c_uint32
 L.tune_copy.argtypes = [vp, vp, u64, i32, i32, i32, vp]
