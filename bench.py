@@ -599,33 +599,35 @@ def main():
     s = stream.cuda_stream
     mar.status.init(s)
 
+    # One event at every kernel boundary of the timed region: ev[2k] before
+    # step k's encode, ev[2k+1] between its encode and decode, ev[2k+2]
+    # after its decode (= before the next step's encode).
     def step(ev=None):
-        if ev is not None:
-            ev[0].record(stream)
         mar.launch_encode(nat, n, xdr, heap=heap, offsets=offsets, stream=s)
         if ev is not None:
-            ev[1].record(stream)
+            ev[0].record(stream)
         mar.launch_decode(xdr, n, back, offsets=offsets, heap_out=heap_out, stream=s)
         if ev is not None:
-            ev[2].record(stream)
+            ev[1].record(stream)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     mar.check(s)
 
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(2 * args.steps + 1)]
     barrier(dist)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    evs[0].record(stream)
     for k in range(args.steps):
-        step(evs[k])
+        step(evs[2 * k + 1:2 * k + 3])
     torch.cuda.synchronize()
     barrier(dist)
     elapsed = time.perf_counter() - t0
     mar.check(s)
-    enc_ms = [e[0].elapsed_time(e[1]) for e in evs]
-    dec_ms = [e[1].elapsed_time(e[2]) for e in evs]
+    enc_ms = [evs[2 * k].elapsed_time(evs[2 * k + 1]) for k in range(args.steps)]
+    dec_ms = [evs[2 * k + 1].elapsed_time(evs[2 * k + 2]) for k in range(args.steps)]
 
     # correctness of what was timed: decode(encode(x)) == x (fixed) or
     # encode(decode(encode(x))) == encode(x) (var); on the 1-GPU headline
