@@ -458,7 +458,71 @@ struct gen {
   // One element of a container (dec_vector_elems of xdrgpu.hip): zero the
   // element, then its fields; an error in element i records i in the
   // container's xdrg_bytes_ref.rsv (the elements before it are decoded).
+  // Elements of up to 64 bytes whose word fields are 4-aligned are built in
+  // registers and leave as whole 8- or 4-byte stores (a lane's scattered
+  // byte and word stores were most of vecrec's decode); a failing field
+  // stores what was built so far, as the store-by-store form leaves it.
+  bool dec_elem_regs(uint32_t vpc, uint32_t b0, uint32_t b1, uint32_t es) {
+    if ((es & 3u) || es == 0 || es > 64) return false;
+    for (uint32_t k = b0; k < b1; ++k) {
+      const xdrg_op &e = op(k);
+      if (e.kind != XDRG_OP_BOOL && e.kind != XDRG_OP_OPAQUE && (e.noff & 3u)) return false;
+    }
+    const uint32_t nw = es / 4;
+    std::string store;
+    if ((es & 7u) == 0) {
+      for (uint32_t z = 0; z < nw; z += 2)
+        store += "*reinterpret_cast<unsigned long long *>(el + " + u32(4 * z) + ") = ew[" + u32(z) +
+                 "] | (static_cast<unsigned long long>(ew[" + u32(z + 1) + "]) << 32); ";
+    } else {
+      for (uint32_t z = 0; z < nw; ++z) store += "st32(el + " + u32(4 * z) + ", ew[" + u32(z) + "]); ";
+    }
+    const std::string fail_done = store + "st32(nat + " + u32(op(vpc).noff) + " + 12, i); ";
+    line("uint32_t ew[" + u32(nw) + "] = {};");
+    auto byte_in = [&](uint32_t at, const std::string &v) {
+      return "ew[" + u32(at / 4) + "] |= (" + v + ") << " + std::to_string(8 * (at % 4)) + ";";
+    };
+    for (uint32_t k = b0; k < b1; ++k) {
+      const xdrg_op &e = op(k);
+      const std::string P = u32(k), D = u32(e.depth);
+      const uint32_t need = e.kind == XDRG_OP_U64 ? 8u : e.kind == XDRG_OP_OPAQUE ? e.arg0 : 4u;
+      line("if (!c.field(" + P + ", " + D + ", " + u32(need) + ")) { " + fail_done + "return false; }");
+      switch (e.kind) {
+      case XDRG_OP_BOOL: line(byte_in(e.noff, "c.word() != 0u ? 1u : 0u")); break;
+      case XDRG_OP_U64:
+        line("{ const uint32_t hi = bswap32(c.word()), lo = bswap32(c.word());");
+        line("  ew[" + u32(e.noff / 4) + "] = lo; ew[" + u32(e.noff / 4 + 1) + "] = hi; }");
+        break;
+      case XDRG_OP_OPAQUE: {
+        const uint32_t L = e.arg0;
+        for (uint32_t q = 0; q < L; q += 4) {
+          line("{ const uint32_t w = c.peek(c.p + " + u32(q) + ");");
+          for (uint32_t b = 0; b < 4 && q + b < L; ++b)
+            line("  " + byte_in(e.noff + q + b, "(w >> " + std::to_string(8 * b) + ") & 0xffu"));
+          line("}");
+        }
+        if (L & 3u)
+          line("if (c.peek(c.p + " + u32(L & ~3u) + ") & " + u32(~((1u << (8 * (L & 3u))) - 1u)) + ") { " +
+               fail_done + "return c.fail(" + P + ", XDRG_ERR_NONZERO_PAD); }");
+        line("c.p += " + u32((L + 3u) & ~3u) + ";");
+        break;
+      }
+      default: {
+        line("{ const uint32_t v = bswap32(c.word());");
+        line("  ew[" + u32(e.noff / 4) + "] = v;");
+        if (e.kind == XDRG_OP_ENUM && (e.flags & XDRG_F_VALIDATE))
+          line("  if (!" + enum_test("v", e.arg0, e.arg1) + ") { " + fail_done + "return c.fail(" + P +
+               ", XDRG_ERR_INVALID_ENUM); }");
+        line("}");
+        break;
+      }
+      }
+    }
+    line(store);
+    return true;
+  }
   void dec_elem(uint32_t vpc, uint32_t b0, uint32_t b1, uint32_t es) {
+    if (dec_elem_regs(vpc, b0, b1, es)) return;
     const std::string fail_done = "st32(nat + " + u32(op(vpc).noff) + " + 12, i); ";
     const bool w4 = (es & 3u) == 0;  // 4-byte stores (element arrays are 8-aligned)
     if (w4)
