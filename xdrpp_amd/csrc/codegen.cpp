@@ -281,7 +281,7 @@ struct gen {
         line("for (uint32_t i = 0; i < cnt; ++i) {");
         ++ind;
         line("const uint64_t eb = eoff + static_cast<uint64_t>(i) * " + u32(e.arg1) + ";");
-        enc_elem(pc + 1, pc + 1 + e.arg2);
+        enc_elem(pc + 1, pc + 1 + e.arg2, e.arg1);
         --ind;
         line("}");
         --ind;
@@ -296,8 +296,50 @@ struct gen {
     return slot;
   }
   // Elements of a container (enc_vector_elems of xdrgpu.hip): fixed-size
-  // fields read from the heap (bytes past heap_len read as 0).
-  void enc_elem(uint32_t b0, uint32_t b1) {
+  // fields read from the heap (bytes past heap_len read as 0).  An element
+  // of 16-byte multiples whose word fields are 4-aligned is loaded whole
+  // (16-byte loads) into registers first, its fields taken from there.
+  bool enc_elem_regs(uint32_t b0, uint32_t b1, uint32_t es) {
+    if (es == 0 || (es & 15u) || es > 64) return false;
+    for (uint32_t k = b0; k < b1; ++k) {
+      const xdrg_op &e = op(k);
+      if (e.kind != XDRG_OP_BOOL && (e.noff & 3u)) return false;
+    }
+    const uint32_t nw = es / 4;
+    line("uint32_t ew[" + u32(nw) + "];");
+    line("if (eb + " + u32(es) + " <= c.heap_len) {");
+    for (uint32_t q = 0; q < nw; q += 4)
+      line("  { const u32x4 t = ld16u(c.heap + eb + " + u32(4 * q) + "); ew[" + u32(q) + "] = t.x; ew[" +
+           u32(q + 1) + "] = t.y; ew[" + u32(q + 2) + "] = t.z; ew[" + u32(q + 3) + "] = t.w; }");
+    line("} else {");
+    for (uint32_t q = 0; q < nw; ++q) line("  ew[" + u32(q) + "] = c.hword(eb + " + u32(4 * q) + ");");
+    line("}");
+    for (uint32_t k = b0; k < b1; ++k) {
+      const xdrg_op &e = op(k);
+      const std::string P = u32(k), D = u32(e.depth), w = "ew[" + u32(e.noff / 4) + "]";
+      line("if (!c.field(" + P + ", " + D + ", " + u32(4u * wire_words(e)) + ")) return false;");
+      switch (e.kind) {
+      case XDRG_OP_BOOL:
+        line("c.put(((" + w + " >> " + std::to_string(8 * (e.noff % 4)) + ") & 0xffu) ? 0x01000000u : 0u);");
+        break;
+      case XDRG_OP_U64:
+        line("c.put(bswap32(ew[" + u32(e.noff / 4 + 1) + "]));");
+        line("c.put(bswap32(" + w + "));");
+        break;
+      case XDRG_OP_OPAQUE:
+        for (uint32_t q = 0; 4 * q < e.arg0; ++q) {
+          std::string x = "ew[" + u32(e.noff / 4 + q) + "]";
+          if (4 * q + 4 > e.arg0) x = "(" + x + " & " + u32((1u << (8 * (e.arg0 - 4 * q))) - 1u) + ")";
+          line("c.put(" + x + ");");
+        }
+        break;
+      default: line("c.put(bswap32(" + w + "));"); break;
+      }
+    }
+    return true;
+  }
+  void enc_elem(uint32_t b0, uint32_t b1, uint32_t es) {
+    if (enc_elem_regs(b0, b1, es)) return;
     for (uint32_t k = b0; k < b1; ++k) {
       const xdrg_op &e = op(k);
       const std::string P = u32(k), D = u32(e.depth), a = "eb + " + u32(e.noff);
