@@ -1321,14 +1321,20 @@ __global__ __launch_bounds__(256) void k_ix_seg(const uint8_t *__restrict__ s, u
 }
 
 // One node of the next level per workgroup: F children composed for
-// every entry.  LDS: the children's tables staged first.
+// every entry.  Also writes each child's inclusive prefix composition
+// (pf: the group's first child up to this one, from every entry), so that
+// the down pass hands every child its entry with one lookup.  out may be
+// null (the top level needs only the prefixes).  LDS: the children's
+// tables staged first.
 template <bool LDS>
 __global__ __launch_bounds__(256) void k_ix_up(const uint64_t *__restrict__ in, uint64_t nin,
-                                               uint32_t K, uint32_t F, uint64_t *__restrict__ out) {
+                                               uint32_t K, uint32_t F, uint64_t *__restrict__ out,
+                                               uint64_t *__restrict__ pf) {
   extern __shared__ __attribute__((aligned(16))) uint64_t stg[];
   const uint64_t c0 = static_cast<uint64_t>(blockIdx.x) * F;
   const uint32_t nc = static_cast<uint32_t>(min<uint64_t>(F, nin - c0));
   const uint64_t *src = in + c0 * K;
+  uint64_t *pre = pf + c0 * K;
   if (LDS) {
     for (uint32_t i = threadIdx.x; i < nc * K; i += 256) stg[i] = src[i];
     __syncthreads();
@@ -1336,48 +1342,43 @@ __global__ __launch_bounds__(256) void k_ix_up(const uint64_t *__restrict__ in, 
   for (uint32_t e = threadIdx.x; e < K; e += 256) {
     uint64_t x = e, c = 0, res = 0;
     bool term = false;
-    for (uint32_t j = 0; j < nc && !term; ++j) {
-      const uint64_t t = LDS ? stg[j * K + x] : src[static_cast<uint64_t>(j) * K + x];
-      c += t & kIxCnt;
-      if (t >> 56) { res = (t >> 56) << 56 | c; term = true; }
-      else x = (t >> 40) & 0xffffu;
+    for (uint32_t j = 0; j < nc; ++j) {
+      if (!term) {
+        const uint64_t t = LDS ? stg[j * K + x] : src[static_cast<uint64_t>(j) * K + x];
+        c += t & kIxCnt;
+        if (t >> 56) { res = (t >> 56) << 56 | c; term = true; }
+        else x = (t >> 40) & 0xffffu;
+      }
+      pre[static_cast<uint64_t>(j) * K + e] = term ? res : (x << 40 | c);
     }
-    out[static_cast<uint64_t>(blockIdx.x) * K + e] = term ? res : (x << 40 | c);
+    if (out) out[static_cast<uint64_t>(blockIdx.x) * K + e] = term ? res : (x << 40 | c);
   }
 }
 
 // Entry word of a node: bit 63 = off the chain; entry << 40; messages
-// before the node (40 bits).  One workgroup per parent: its children's
-// entries in order, from the parent's.
-template <bool LDS>
-__global__ __launch_bounds__(64) void k_ix_down(const uint64_t *__restrict__ tab, uint64_t nin,
+// before the node (40 bits).  One workgroup per parent, one thread per
+// child: the child's entry is the parent's through the prefix composition
+// of the children before it (k_ix_up's pf).
+__global__ __launch_bounds__(64) void k_ix_down(const uint64_t *__restrict__ pf, uint64_t nin,
                                                 uint32_t K, uint32_t F,
                                                 const uint64_t *__restrict__ up,
                                                 uint64_t *__restrict__ ent) {
-  extern __shared__ __attribute__((aligned(16))) uint64_t stg[];
   const uint64_t c0 = static_cast<uint64_t>(blockIdx.x) * F;
   const uint32_t nc = static_cast<uint32_t>(min<uint64_t>(F, nin - c0));
+  const uint32_t j = threadIdx.x;
+  if (j >= nc) return;
   const uint64_t e = up[blockIdx.x];
   if (e >> 63) {
-    for (uint32_t j = threadIdx.x; j < nc; j += 64) ent[c0 + j] = 1ull << 63;
+    ent[c0 + j] = 1ull << 63;
     return;
   }
-  const uint64_t *src = tab + c0 * K;
-  if (LDS) {
-    for (uint32_t i = threadIdx.x; i < nc * K; i += 64) stg[i] = src[i];
-    wave_sync();
+  const uint64_t x = (e >> 40) & 0xffffu, b = e & kIxCnt;
+  if (j == 0) {
+    ent[c0] = x << 40 | b;
+    return;
   }
-  if (threadIdx.x != 0) return;
-  uint64_t x = (e >> 40) & 0xffffu, b = e & kIxCnt;
-  bool dead = false;
-  for (uint32_t j = 0; j < nc; ++j) {
-    ent[c0 + j] = dead ? (1ull << 63) : (x << 40 | b);
-    if (dead) continue;
-    const uint64_t t = LDS ? stg[j * K + x] : src[static_cast<uint64_t>(j) * K + x];
-    b += t & kIxCnt;
-    if (t >> 56) dead = true;
-    else x = (t >> 40) & 0xffffu;
-  }
+  const uint64_t t = pf[(c0 + j - 1) * K + x];
+  ent[c0 + j] = (t >> 56) ? (1ull << 63) : (((t >> 40) & 0xffffu) << 40 | (b + (t & kIxCnt)));
 }
 
 // Segments on the chain.  The nodes reachable from the entry x are found by
@@ -1925,7 +1926,7 @@ struct ix_layout {
   bool lds = false;
   int top = 0;
   uint64_t n[24] = {};
-  size_t tab[24] = {}, ent[24] = {};
+  size_t tab[24] = {}, pf[24] = {}, ent[24] = {};
   size_t total = 0;
 };
 constexpr size_t kIxLdsBytes = 64u << 10;
@@ -1947,7 +1948,12 @@ ix_layout ix_plan(uint64_t len, uint32_t maxlen) {
   L.lcount = off;
   off += align_up(L.nseg * 4, 256);
   for (int l = 0; l <= L.top; ++l) {
-    if (l < L.top) { L.tab[l] = off; off += align_up(L.n[l] * L.K * 8, 256); }
+    if (l < L.top) {
+      L.tab[l] = off;
+      off += align_up(L.n[l] * L.K * 8, 256);
+      L.pf[l] = off;  // prefix compositions (k_ix_up) of the same shape
+      off += align_up(L.n[l] * L.K * 8, 256);
+    }
     L.ent[l] = off;
     off += align_up(L.n[l] * 8, 256);
   }
@@ -2095,19 +2101,18 @@ int run_index(const xdrg_plan *p, const dev_tables *T, const void *d_stream, uin
                                              vlist, vcount, rp);
   HIPCHK(hipGetLastError());
   const size_t stg = L.lds ? static_cast<size_t>(L.F) * L.K * 8 : 0;
-  for (int l = 0; l + 1 < L.top; ++l) {
+  auto pfx = [&](int l) { return reinterpret_cast<uint64_t *>(ws + L.pf[l]); };
+  for (int l = 0; l < L.top; ++l) {  // the top level: prefixes only
+    uint64_t *o = l + 1 < L.top ? tab(l + 1) : nullptr;
     if (L.lds)
-      k_ix_up<true><<<L.n[l + 1], 256, stg, s>>>(tab(l), L.n[l], L.K, L.F, tab(l + 1));
+      k_ix_up<true><<<L.n[l + 1], 256, stg, s>>>(tab(l), L.n[l], L.K, L.F, o, pfx(l));
     else
-      k_ix_up<false><<<L.n[l + 1], 256, 0, s>>>(tab(l), L.n[l], L.K, L.F, tab(l + 1));
+      k_ix_up<false><<<L.n[l + 1], 256, 0, s>>>(tab(l), L.n[l], L.K, L.F, o, pfx(l));
     HIPCHK(hipGetLastError());
   }
   HIPCHK(hipMemsetAsync(ent(L.top), 0, 8, s));  // the chain starts at word 0 with 0 messages
   for (int l = L.top - 1; l >= 0; --l) {
-    if (L.lds)
-      k_ix_down<true><<<L.n[l + 1], 64, stg, s>>>(tab(l), L.n[l], L.K, L.F, ent(l + 1), ent(l));
-    else
-      k_ix_down<false><<<L.n[l + 1], 64, 0, s>>>(tab(l), L.n[l], L.K, L.F, ent(l + 1), ent(l));
+    k_ix_down<<<L.n[l + 1], 64, 0, s>>>(pfx(l), L.n[l], L.K, L.F, ent(l + 1), ent(l));
     HIPCHK(hipGetLastError());
   }
   k_ix_emit<REC><<<L.nseg, 256, 0, s>>>(s8, len, max_msg_len, ent(0), vlist, vcount, d_offsets,
