@@ -278,7 +278,6 @@ struct gen {
         line("const uint32_t cnt = ld32(" + f + " + 8);");
         line("if (!c.field(" + P + ", " + D + ", 4)) return false;");
         line("c.put(bswap32(cnt));");
-        line("#pragma unroll 4");  // the loads of later elements go out before this one's puts
         line("for (uint32_t i = 0; i < cnt; ++i) {");
         ++ind;
         line("const uint64_t eb = eoff + static_cast<uint64_t>(i) * " + u32(e.arg1) + ";");
