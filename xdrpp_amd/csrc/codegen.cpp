@@ -278,7 +278,23 @@ struct gen {
         line("const uint32_t cnt = ld32(" + f + " + 8);");
         line("if (!c.field(" + P + ", " + D + ", 4)) return false;");
         line("c.put(bswap32(cnt));");
-        line("for (uint32_t i = 0; i < cnt; ++i) {");
+        line("uint32_t i = 0;");
+        if (e.arg1 == 4 && e.arg2 == 1 && op(pc + 1).noff == 0 &&
+            (op(pc + 1).kind == XDRG_OP_U32 || op(pc + 1).kind == XDRG_OP_ENUM || op(pc + 1).kind == XDRG_OP_BOOL)) {
+          // 4-byte elements four at a time: one 16-byte load per four
+          const xdrg_op &el = op(pc + 1);
+          const std::string chk = "if (!c.field(" + u32(pc + 1) + ", " + u32(el.depth) + ", 4)) return false;";
+          auto cv = [&](const std::string &w) {
+            return el.kind == XDRG_OP_BOOL ? "((" + w + " & 0xffu) ? 0x01000000u : 0u)" : "bswap32(" + w + ")";
+          };
+          line("for (; i + 4u <= cnt && eoff + 4ull * (i + 4u) <= c.heap_len; i += 4u) {");
+          ++ind;
+          line("const u32x4 t = ld16u(c.heap + eoff + 4ull * i);");
+          for (const char *w : {"t.x", "t.y", "t.z", "t.w"}) line(chk + " c.put(" + cv(w) + ");");
+          --ind;
+          line("}");
+        }
+        line("for (; i < cnt; ++i) {");
         ++ind;
         line("const uint64_t eb = eoff + static_cast<uint64_t>(i) * " + u32(e.arg1) + ";");
         enc_elem(pc + 1, pc + 1 + e.arg2, e.arg1);
