@@ -40,6 +40,13 @@
 #ifndef XDRG_DSTAMP
 #define XDRG_DSTAMP(k) ((void)0)
 #endif
+// Memory hints of the encode (tools/tune/enc_stamps.py CFLAGS A/B,
+// profiles/r02s/nt_hints/): bit 0 non-temporal payload loads, bit 1
+// non-temporal stream stores.  Stores: encode kernel -7 % recvar, -3 % rpc
+// alone; enc+dec bench lines +0-2 %.
+#ifndef XDRG_ENC_NT
+#define XDRG_ENC_NT 2
+#endif
 
 namespace xdrg {
 namespace dev {
@@ -417,7 +424,12 @@ __device__ __forceinline__ void var_encode_body(
       }
 #pragma unroll
       for (int u = 0; u < U; ++u)
-        if (fast[u]) val[u] = ld16u(heap + hs[u]);
+        if (fast[u]) {
+          if constexpr ((XDRG_ENC_NT & 1) != 0)
+            val[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(heap + hs[u]));
+          else
+            val[u] = ld16u(heap + hs[u]);
+        }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -460,7 +472,10 @@ __device__ __forceinline__ void var_encode_body(
         const uint64_t ca = ws + 16ull * k;
         const uint8_t *lsrc = img + 16u * k;
         if (ca >= wave_out && ca + 16u <= we) {
-          *reinterpret_cast<u32x4 *>(xdr + ca) = *reinterpret_cast<const u32x4 *>(lsrc);
+          if constexpr ((XDRG_ENC_NT & 2) != 0)
+            __builtin_nontemporal_store(*reinterpret_cast<const u32x4 *>(lsrc), reinterpret_cast<u32x4 *>(xdr + ca));
+          else
+            *reinterpret_cast<u32x4 *>(xdr + ca) = *reinterpret_cast<const u32x4 *>(lsrc);
         } else {
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
