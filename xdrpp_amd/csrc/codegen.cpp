@@ -158,6 +158,100 @@ struct gen {
     }
   }
 
+  // ----------------------------------------------------- record parse
+  // The record-start parse of the plain-stream index (rx_len of
+  // xdrgpu.hip, straight-line): lengths, counts and discriminants only,
+  // with every check that makes a decode fail.  Returns through p, or
+  // `past` when the record runs past lim, or RX_BAD.
+  void rx_block(uint32_t pc, uint32_t stop) {
+    auto need = [&](const std::string &n) { line("if (lim - p < " + n + ") return past;"); };
+    auto word = [&]() { need("4"); line("{ const uint32_t v = bswap32(ld32(s + p)); p += 4;"); };
+    while (pc != stop) {
+      const xdrg_op &e = op(pc);
+      switch (e.kind) {
+      case XDRG_OP_END: return;
+      case XDRG_OP_JUMP: pc = e.arg0; continue;
+      case XDRG_OP_U64: need("8"); line("p += 8;"); break;
+      case XDRG_OP_OPAQUE: need(u32(e.arg0)); line("p += " + u32((e.arg0 + 3u) & ~3u) + ";"); break;
+      case XDRG_OP_U32: case XDRG_OP_BOOL: need("4"); line("p += 4;"); break;
+      case XDRG_OP_ENUM:
+        if (e.flags & XDRG_F_VALIDATE) {
+          word();
+          line("  if (!" + enum_test("v", e.arg0, e.arg1) + ") return RX_BAD; }");
+        } else {
+          need("4");
+          line("p += 4;");
+        }
+        break;
+      case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING:
+        word();
+        line("  if (v > " + u32(e.arg0) + ") return RX_BAD;");
+        line("  if (lim - p < v) return past;");
+        line("  p += (static_cast<uint64_t>(v) + 3u) & ~3ull; }");
+        break;
+      case XDRG_OP_VECTOR:  // fixed-size elements (element subroutines are not generated)
+        word();
+        line("  if (v > " + u32(e.arg0) + ") return RX_BAD;");
+        line("  const uint64_t b = static_cast<uint64_t>(v) * " + u32(e.arg3) + ";");
+        line("  if (lim - p < b) return past;");
+        line("  p += b; }");
+        pc += 1 + e.arg2;
+        continue;
+      case XDRG_OP_UNION: {
+        const uint32_t end = ipdom[pc];
+        word();
+        if (e.flags & XDRG_F_VALIDATE) line("  if (!" + enum_test("v", e.arg0, e.arg1) + ") return RX_BAD;");
+        line("  switch (v) {");
+        for (auto &a : arms(e)) {
+          std::string lab;
+          for (uint32_t v : a.second) lab += "case " + u32(v) + ": ";
+          line("  " + lab + "{");
+          ind += 2;
+          rx_block(a.first, end);
+          ind -= 2;
+          line("  } break;");
+        }
+        line("  default: {");
+        ind += 2;
+        if (e.flags & XDRG_F_DEFAULT) rx_block(e.arg4, end);
+        else line("return RX_BAD;");
+        ind -= 2;
+        line("  } break;");
+        line("  }");
+        line("}");
+        pc = end;
+        continue;
+      }
+      default: break;
+      }
+      ++pc;
+    }
+  }
+  // The first op whose word is checked (every op before it fixed-size, no
+  // branch) and the test of that word: what the index loads for every
+  // candidate start before parsing it (run_index in xdrgpu.hip finds the
+  // same op).
+  std::string first_test() {
+    for (uint32_t pc = 0; pc < nops(); ++pc) {
+      const xdrg_op &o = op(pc);
+      if (o.kind == XDRG_OP_END || o.kind == XDRG_OP_JUMP) break;
+      if (o.kind == XDRG_OP_U64 || o.kind == XDRG_OP_OPAQUE || o.kind == XDRG_OP_U32 || o.kind == XDRG_OP_BOOL ||
+          (o.kind == XDRG_OP_ENUM && !(o.flags & XDRG_F_VALIDATE)))
+        continue;
+      if (o.kind == XDRG_OP_ENUM) return enum_test("v", o.arg0, o.arg1);
+      if (o.kind == XDRG_OP_UNION) {
+        if (o.flags & XDRG_F_DEFAULT) return (o.flags & XDRG_F_VALIDATE) ? enum_test("v", o.arg0, o.arg1) : "true";
+        std::string t;
+        for (auto &a : arms(o))
+          for (uint32_t v : a.second) t += (t.empty() ? "" : " || ") + std::string("v == ") + u32(v);
+        if (t.empty()) t = "false";
+        return (o.flags & XDRG_F_VALIDATE) ? "(" + enum_test("v", o.arg0, o.arg1) + " && (" + t + "))" : "(" + t + ")";
+      }
+      return "v <= " + u32(o.arg0);  // VAROPAQUE, STRING, VECTOR
+    }
+    return "true";
+  }
+
   // ---------------------------------------------------------------- encode
   // xdr_generic_put field by field (marshal.h:84-137).  Returns the static
   // slots used after the block (slots count along the path); `words` = the
@@ -672,6 +766,12 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
   g.ind = 2;
   g.dec_block(0, kNoPc);
   const std::string dec_code = g.o.str();
+  // record parse of the plain-stream index
+  g.o.str("");
+  g.ind = 2;
+  g.rx_block(0, kNoPc);
+  const std::string rx_code = g.o.str();
+  const std::string first = g.first_test();
 
   uint32_t maxd = 0;  // deepest field: the stack budget a wave must have to skip the checks
   for (const xdrg_op &o : p.ops) maxd = std::max<uint32_t>(maxd, o.depth);
@@ -683,6 +783,7 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
   s << "// Generated by libxdrgpu (codegen.cpp) from a plan of " << p.ops.size()
     << " ops: straight-line walker for var_kernels.h.\n"
     << "#include \"var_kernels.h\"\n"
+    << "#include \"index_kernels.h\"\n"
     << "using namespace xdrg::dev;\n\n"
     << "extern \"C\" __device__ __attribute__((used)) unsigned xdrg_spec_iface = " << kSpecIface << "u;\n\n"
     << "struct plan_walk {\n"
@@ -701,6 +802,21 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
     << "    if (!ok) return false;\n"
     << dec_code << "    return true;\n  }\n"
     << "};\n\n"
+    << "struct plan_rx {  // index_kernels.h ix_seg_body's parser\n"
+    << "  __device__ __forceinline__ void init(uint32_t *) const {}\n"
+    << "  __device__ __forceinline__ bool first_ok(const uint32_t *, uint32_t v) const { return " << first << "; }\n"
+    << "  __device__ __forceinline__ uint32_t rlen(const uint32_t *, const uint8_t *__restrict__ s, uint64_t len,\n"
+    << "                                           uint64_t a, uint32_t maxlen) const {\n"
+    << "    const bool capped = a + maxlen < len;\n"
+    << "    const uint64_t lim = capped ? a + maxlen : len;\n"
+    << "    const uint32_t past = capped ? RX_LONG : RX_BAD;\n"
+    << "    uint64_t p = a;\n"
+    << rx_code << "    return static_cast<uint32_t>(p - a);\n  }\n"
+    << "};\n\n"
+    << "extern \"C\" __global__ __launch_bounds__(256) void xdrg_spec_ix_seg(\n"
+    << "    const uint8_t *s, uint64_t len, uint32_t maxlen, uint32_t K, uint64_t *tab, uint32_t *list,\n"
+    << "    uint32_t *lcount, uint32_t has_first, uint32_t fd) {\n"
+    << "  ix_seg_body<true>(plan_rx{}, s, len, maxlen, K, tab, list, lcount, has_first != 0, fd);\n}\n\n"
     << "extern \"C\" __global__ __launch_bounds__(64) void xdrg_spec_size(\n"
     << "    const uint8_t *native, uint64_t n, uint32_t stride, uint32_t *sizes,\n"
     << "    unsigned long long *block_sums, uint32_t mark, unsigned long long *err) {\n"

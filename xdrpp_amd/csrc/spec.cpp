@@ -147,9 +147,10 @@ const spec_module *spec_get(const xdrg_plan &cp) {
   hipModule_t m = nullptr;
   if (hipModuleLoadData(&m, s.code.data()) != hipSuccess) return nullptr;
   spec_module &d = s.dev[dev];
-  hipFunction_t f[4] = {};
-  const char *names[4] = {"xdrg_spec_size", "xdrg_spec_encode", "xdrg_spec_decode", "xdrg_spec_decode_copy"};
-  for (int i = 0; i < 4; ++i)
+  hipFunction_t f[5] = {};
+  const char *names[5] = {"xdrg_spec_size", "xdrg_spec_encode", "xdrg_spec_decode", "xdrg_spec_decode_copy",
+                          "xdrg_spec_ix_seg"};
+  for (int i = 0; i < 5; ++i)
     if (hipModuleGetFunction(&f[i], m, names[i]) != hipSuccess) {
       (void)hipModuleUnload(m);
       return nullptr;
@@ -170,6 +171,7 @@ const spec_module *spec_get(const xdrg_plan &cp) {
   d.f_enc = f[1];
   d.f_dec = f[2];
   d.f_dec_copy = f[3];
+  d.f_ix_seg = f[4];
   s.loaded[dev].store(true, std::memory_order_release);
   return &d;
 }
