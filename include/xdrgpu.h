@@ -300,8 +300,9 @@ int xdrg_plan_set_option(xdrg_plan *plan, int option, int64_t value);
  * 212-250, :575-675): a plan's walk emitted as straight-line HIP source --
  * every field's checks, swaps and bytes, unions as switch statements,
  * containers as loops -- over the library's var kernels, compiled for
- * gfx950.  No reference interface corresponds one to one: this is the back
- * end xdrc would run beside gen_hh.
+ * gfx950; also the plan's record-start parse for xdrg_index_records.  No
+ * reference interface corresponds one to one: this is the back end xdrc
+ * would run beside gen_hh.
  *
  *   xdrg_plan_kernel_source  the plan's source (NUL-terminated into buf when
  *                            cap > 0; *len = its length).  XDRG_EUNSUPPORTED
