@@ -590,7 +590,33 @@ struct gen {
         line("c.ecur = (c.ecur + 7u) & ~7ull;");
         line("*reinterpret_cast<uint64_t *>(" + f + ") = c.ecur;");
         line("st32(" + f + " + 8, cnt);");
-        line("for (uint32_t i = 0; i < cnt; ++i) {");
+        line("uint32_t i = 0;");
+        {
+          const xdrg_op &el = op(pc + 1);
+          if (e.arg1 == 4 && e.arg2 == 1 && el.noff == 0 &&
+              (el.kind == XDRG_OP_U32 || el.kind == XDRG_OP_BOOL ||
+               (el.kind == XDRG_OP_ENUM && !(el.flags & XDRG_F_VALIDATE)))) {
+            // 4-byte elements two at a time: one 8-byte store per pair (the
+            // array starts 8-aligned); a failing element leaves what the
+            // one-by-one form leaves (the element before it stored, it zeroed)
+            const std::string chk = "c.field(" + u32(pc + 1) + ", " + u32(el.depth) + ", 4)";
+            const std::string rsv = "st32(nat + " + u32(e.noff) + " + 12, ";
+            auto cv = [&](const std::string &w) {
+              return el.kind == XDRG_OP_BOOL ? "(" + w + " != 0u ? 1u : 0u)" : "bswap32(" + w + ")";
+            };
+            line("for (; i + 2u <= cnt; i += 2u) {");
+            ++ind;
+            line("uint8_t *ep = c.heap + c.ecur + 4ull * i;");
+            line("if (!" + chk + ") { st32(ep, 0u); " + rsv + "i); return false; }");
+            line("const uint32_t v0 = " + cv("c.word()") + ";");
+            line("if (!" + chk + ") { st32(ep, v0); st32(ep + 4, 0u); " + rsv + "i + 1u); return false; }");
+            line("const uint32_t v1 = " + cv("c.word()") + ";");
+            line("*reinterpret_cast<unsigned long long *>(ep) = v0 | (static_cast<unsigned long long>(v1) << 32);");
+            --ind;
+            line("}");
+          }
+        }
+        line("for (; i < cnt; ++i) {");
         ++ind;
         line("uint8_t *el = c.heap + c.ecur + static_cast<uint64_t>(i) * " + u32(e.arg1) + ";");
         dec_elem(pc, pc + 1, pc + 1 + e.arg2, e.arg1);
