@@ -121,13 +121,17 @@ def _gpu_index(mar, x, n, maxlen, dev):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("spec", [1, 0], ids=["generated", "interpreted"])
 @pytest.mark.parametrize("name", VAR + list(S.CONTAINERS))
-def test_gpu_index_matches_oracle(dev, name):
+def test_gpu_index_matches_oracle(dev, name, spec):
+    """Both record-start parses of the segment pass -- the plan's generated
+    plan_rx and the interpreted rx_len -- against the C restatement, on
+    damaged streams."""
     from xdrpp_amd import marshal as M
     t = S.ALL.get(name) or S.CONTAINERS[name]
     cp = compile_plan(t)
     x, offs, n = gold_stream(name) if name in VAR else containers_stream(name)
-    mar = M.Marshaler(M.Plan(cp), dev)
+    mar = M.Marshaler(M.Plan(cp, {"specialize": spec}), dev)
     W = window(cp)
     for label, y, k in damaged(x, offs, n, 7):
         want, wcnt, wrc, wer = O.index_records(cp, y, k, W)
