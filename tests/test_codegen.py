@@ -29,12 +29,25 @@ def test_source_is_straight_line(name):
     src = source(p)
     assert "struct plan_walk" in src and "xdrg_spec_encode" in src
     assert "load_op" not in src and "ops[" not in src  # no op table, no dispatch
+    # the record-start parse of the plain-stream index (index_kernels.h)
+    assert "struct plan_rx" in src and "xdrg_spec_ix_seg" in src
     if name == "rpc":
         # nested unions become switch statements with the reference's case values
-        assert src.count("switch (") >= 2 * 4
+        # (size, encode, decode, record parse)
+        assert src.count("switch (") >= 3 * 4
         assert "XDRG_ERR_BAD_DISCRIMINANT" in src
+        # every payload takes a slot, no container: the encode walks once into
+        # a word list (xid, mtype, 4 call words, 2 x flavor + length)
+        assert "kWords = 10u" in src
+        assert "return (v == 0u || v == 1u);" in src  # first checked word: mtype
+    if name == "recvar":
+        assert "kWords = 7u" in src
     if name == "vecrec":
-        assert "for (uint32_t i = 0; i < cnt; ++i)" in src
+        assert "kWords = 0u" in src  # containers: the walk runs per window
+        assert "for (; i < cnt; ++i)" in src
+        # int vals<16>: four elements per 16-byte load (encode), two per
+        # 8-byte store (decode)
+        assert "i + 4u <= cnt" in src and "i + 2u <= cnt" in src
 
 
 def test_fixed_plans_have_no_specialized_source():
