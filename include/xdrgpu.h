@@ -127,15 +127,22 @@ enum xdrg_op_flags {
  * an op of a body entered from a VECTOR op at (absolute) depth d sits at
  * depth d + op.depth, so an element struct's fields are at d + 1 exactly
  * as if the element were written inline.  A body may be entered from
- * itself (test_recursive, tests/xdrtest.x:29-33).  The kernels keep up to
- * XDRG_SUB_FRAMES nested element subroutines per record; data nested
- * deeper raises the stack-overflow error at the VECTOR op that would
- * enter the next one (bounded recursion: what marshaling_stack_limit,
- * marshal.h:21, guards the reference's call stack against).  A decode that
- * fails inside elements leaves rsv = 1 + the failing element's index in
- * every container on the way to the failure (0 in the others).
+ * itself (test_recursive, tests/xdrtest.x:29-33; rpcbind's rp__list,
+ * xdrpp/rpcb_prot.x:34).  Nesting is bounded by the data and by
+ * marshaling_stack_limit only: a walk keeps XDRG_SUB_FRAMES element frames
+ * in private memory, and records nested deeper are walked again by deep
+ * passes whose frames live in a library-owned frame pool (one per device,
+ * allocated by the first launch of a plan that can nest that deep: about
+ * 128 MiB + 8 bytes per record; launches that use it are ordered across
+ * streams).  A record that needs more than XDRG_MAX_FRAMES nested element
+ * frames raises the stack-overflow error at the VECTOR op that would open
+ * the next one; the reference's own recursion ends far earlier, in a
+ * segmentation fault of its 8 MiB call stack.  A decode that fails inside
+ * elements leaves rsv = 1 + the failing element's index in every container
+ * on the way to the failure (0 in the others).
  */
 #define XDRG_SUB_FRAMES 32
+#define XDRG_MAX_FRAMES (1u << 19)
 typedef struct xdrg_op {
   uint8_t kind;
   uint8_t flags;
@@ -387,8 +394,11 @@ uint64_t xdrg_decode_heap_size(const xdrg_plan *plan, uint64_t xdr_len);
  * msg_sock::input read (xdrpp/srpc.cc:29-55, msgsock.cc:38-119).
  */
 #define XDRG_MARK_LAST 0x80000000u
-/* Largest max_msg_len xdrg_index_msgs accepts (its segment window). */
+/* Longest message one list-ranking window of the stream indexes holds (a
+ * 16 KiB segment); xdrg_index_records' record bound. */
 #define XDRG_INDEX_MAX_MSG 16380u
+/* Longest message a record mark can state (31 size bits). */
+#define XDRG_MAX_MSG 0x7fffffffu
 
 /*
  * Encode n records as n messages: message i = xdr_to_msg(r_i)
@@ -427,7 +437,13 @@ int xdrg_decode_msgs(const xdrg_plan *plan, const void *d_stream, uint64_t len,
  * *d_count = k and d_offsets[k] = the failing mark's offset.  At most
  * max_msgs messages are indexed (d_offsets holds max_msgs + 1 entries);
  * more is XDRG_ERR_MSG_COUNT at record max_msgs.  Entries past count are
- * unspecified.  max_msg_len <= XDRG_INDEX_MAX_MSG.
+ * unspecified.  Any max_msg_len up to XDRG_MAX_MSG: msg_sock's is 1 MiB by
+ * default (msgsock.h:29), read_message has none.  Up to XDRG_INDEX_MAX_MSG
+ * the call is one asynchronous list-ranking pass; past it the messages
+ * longer than that are walked mark by mark on the device between
+ * list-ranking windows over the rest, and the call waits on the stream
+ * once or twice per window (every byte is read about twice at most).
+ * Workspace: xdrg_index_workspace_size(len, max_msg_len).
  */
 int xdrg_index_msgs(const void *d_stream, uint64_t len, uint32_t max_msg_len,
                     uint64_t max_msgs, uint64_t *d_offsets, uint64_t *d_count,

@@ -950,14 +950,29 @@ void unstage_checked(const std::uint8_t *native, const std::uint8_t *heap, std::
 //! device decode then reports the reference's error for that record.
 namespace detail {
 // Step p over one object's wire bytes (the walk from pc to its END): false
-// when the bytes run out, a discriminant is bad, or elements nest deeper
-// than the device walks them.
+// when the bytes run out or a discriminant is bad.  Element subroutines are
+// walked with an explicit stack, so nesting is bounded by the bytes only
+// (every element consumes at least 4 of them).
 inline bool skip_object(const xdrg_op *ops, const std::uint32_t *tab, const std::uint8_t *xdr,
-                        std::size_t len, std::uint64_t &p, std::uint32_t pc, std::uint32_t frames) {
+                        std::size_t len, std::uint64_t &p, std::uint32_t pc) {
+  struct frame {
+    std::uint32_t left, vpc;  // elements after the current one; the VECTOR op
+  };
+  std::vector<frame> st;
   for (;;) {
     const xdrg_op &o = ops[pc];
     switch (o.kind) {
-    case XDRG_OP_END: return true;
+    case XDRG_OP_END:
+      if (st.empty()) return true;
+      if (st.back().left) {
+        --st.back().left;
+        pc = ops[st.back().vpc].arg4;
+        if (p > len) return false;
+      } else {
+        pc = st.back().vpc + 1;
+        st.pop_back();
+      }
+      continue;
     case XDRG_OP_JUMP: pc = o.arg0; continue;
     case XDRG_OP_U64: p += 8; break;
     case XDRG_OP_OPAQUE: p += align_up(o.arg0, 4); break;
@@ -970,10 +985,13 @@ inline bool skip_object(const xdrg_op *ops, const std::uint32_t *tab, const std:
       const std::uint32_t cnt = be32(xdr + p);
       p += 4;
       if (o.flags & XDRG_F_SUB) {
-        if (cnt && frames == XDRG_SUB_FRAMES) return false;
-        for (std::uint32_t i = 0; i < cnt; ++i)
-          if (p > len || !skip_object(ops, tab, xdr, len, p, o.arg4, frames + 1)) return false;
-        ++pc;
+        if (cnt) {
+          if (p > len) return false;
+          st.push_back(frame{cnt - 1, pc});
+          pc = o.arg4;
+        } else {
+          ++pc;
+        }
         continue;
       }
       std::uint64_t we = 0;
@@ -1008,7 +1026,7 @@ std::vector<std::uint64_t> index_records(const std::uint8_t *xdr, std::size_t le
   std::uint64_t p = 0;
   for (std::size_t r = 0; r < n; ++r) {
     off[r] = std::min<std::uint64_t>(p, len);
-    if (!detail::skip_object(P.ops().data(), P.table().data(), xdr, len, p, 0, 0) || p > len)
+    if (!detail::skip_object(P.ops().data(), P.table().data(), xdr, len, p, 0) || p > len)
       return off;  // off[r] is set; the rest stay at len
   }
   off[n] = p;  // p < len: trailing bytes, which decode reports at record n
@@ -1291,7 +1309,7 @@ void from_msg_batch(const std::vector<msg_ptr> &msgs, T *out, hipStream_t s = nu
 //! xdr_from_msg per message.  A framing error raises xdr_bad_message_size.
 template <typename T>
 std::vector<T> from_msg_stream(const void *bytes, std::size_t len,
-                               std::uint32_t max_msg_len = XDRG_INDEX_MAX_MSG,
+                               std::uint32_t max_msg_len = 0x100000,  // msg_sock::default_maxmsglen
                                hipStream_t s = nullptr) {
   const auto *x = static_cast<const std::uint8_t *>(bytes);
   const std::uint64_t max_msgs = len / 4;

@@ -165,6 +165,52 @@ static void kat(const string &path) {
     x.name = string(size_t((bl * 3) % 7), 'h');
     o << "  \"recvar_len" << bl << "\": \"" << enc(x) << "\",\n";
   }
+  // SURVEY §8(c) known answers over oracle/x/kat.x.  The union and the
+  // xvector alone encode as the one-field structs the plans describe.
+  {
+    katns::ku u(katns::KRED);
+    u.i() = -1;
+    katns::ku_rec ur;
+    ur.u = u;
+    if (enc(u) != enc(ur)) die("kat: union alone != in a struct");
+    o << "  \"union_red_m1\": \"" << enc(ur) << "\",\n";
+    katns::ku h(katns::KREDDER);
+    h.h() = 0x0102030405060708ull;
+    katns::ku_rec hr;
+    hr.u = h;
+    o << "  \"union_redder\": \"" << enc(hr) << "\",\n";
+    katns::ku_rec dr;
+    dr.u = katns::ku(katns::KREDDEST);  // the default (void) arm
+    o << "  \"union_default\": \"" << enc(dr) << "\",\n";
+    xdr::xvector<int32_t> xv{1, 2};
+    katns::kint_vec kv;
+    kv.v = xv;
+    if (enc(xv) != enc(kv)) die("kat: xvector alone != in a struct");
+    o << "  \"xvector_int_1_2\": \"" << enc(kv) << "\",\n";
+    katns::kstruct ks;
+    ks.i = -2;
+    ks.u = 0x0102030405060708ull;
+    ks.d = 1.5;
+    ks.blob = {1, 2, 3};
+    ks.name = "hello";
+    o << "  \"struct_hello\": \"" << enc(ks) << "\",\n";
+    // a4: xdr_generic_put checks capacity, not bounds (marshal.h:118-127):
+    // past-bound fields encode; their decode throws (types.h:486-489, :539-542)
+    auto bounded = [](size_t nb, size_t ns, size_t nv) {
+      katns::kbounded b;
+      for (size_t j = 0; j < nb; ++j) b.blob.push_back(uint8_t(j + 1));  // std::vector: unchecked
+      for (size_t j = 0; j < ns; ++j) static_cast<std::string &>(b.s).push_back(char('a' + j));  // xstring::push_back checks
+      for (size_t j = 0; j < nv; ++j) b.v.push_back(int32_t(j + 10));
+      return b;
+    };
+    const katns::kbounded over_all = bounded(65, 9, 3), over_blob = bounded(65, 8, 2),
+                          over_s = bounded(64, 9, 2), over_v = bounded(64, 8, 3), in = bounded(64, 8, 2);
+    o << "  \"bounded_in\": \"" << enc(in) << "\",\n";
+    o << "  \"bounded_over_all\": \"" << enc(over_all) << "\",\n";
+    o << "  \"bounded_over_blob\": \"" << enc(over_blob) << "\",\n";
+    o << "  \"bounded_over_s\": \"" << enc(over_s) << "\",\n";
+    o << "  \"bounded_over_v\": \"" << enc(over_v) << "\",\n";
+  }
   // rpc: one of each arm
   vector<xdr::rpc_msg> pv;
   gen_rpc(64, WG_SEED_RPC, pv);
@@ -257,7 +303,22 @@ static void kat(const string &path) {
     o << "    \"vecrec_pairs_past_end\": "
       << try_decode<vecrec>(h, [](xdr::opaque_vec<> &m) { m[31] = 3; }) << ",\n";
     o << "    \"vecrec_bool2\": "
-      << try_decode<vecrec>(h, [](xdr::opaque_vec<> &m) { m[43] = 2; }) << "\n";
+      << try_decode<vecrec>(h, [](xdr::opaque_vec<> &m) { m[43] = 2; }) << ",\n";
+  }
+  {
+    // the past-bound encodes of kat.x kbounded (above), decoded
+    auto bounded = [](size_t nb, size_t ns, size_t nv) {
+      katns::kbounded b;
+      for (size_t j = 0; j < nb; ++j) b.blob.push_back(uint8_t(j + 1));
+      for (size_t j = 0; j < ns; ++j) static_cast<std::string &>(b.s).push_back(char('a' + j));  // xstring::push_back checks
+      for (size_t j = 0; j < nv; ++j) b.v.push_back(int32_t(j + 10));
+      return enc(b);
+    };
+    o << "    \"kbounded_in\": " << try_decode<katns::kbounded>(bounded(64, 8, 2)) << ",\n";
+    o << "    \"kbounded_over_blob\": " << try_decode<katns::kbounded>(bounded(65, 8, 2)) << ",\n";
+    o << "    \"kbounded_over_s\": " << try_decode<katns::kbounded>(bounded(64, 9, 2)) << ",\n";
+    o << "    \"kbounded_over_v\": " << try_decode<katns::kbounded>(bounded(64, 8, 3)) << ",\n";
+    o << "    \"kbounded_over_all\": " << try_decode<katns::kbounded>(bounded(65, 9, 3)) << "\n";
   }
   o << "  }\n}\n";
   std::ofstream f(path);
@@ -549,9 +610,56 @@ template <typename T> static void depths_of(const vector<T> &v, const string &ou
   write_file(out, d.data(), d.size() * 4);
 }
 
+// frame <stream file> <maxmsglen> <out.json>: the messages of a stream as
+// the REAL read_message (srpc.cc:29-55) reads them from a file descriptor,
+// message after message, with msg_sock's length rule in front of each
+// (msgsock.cc:97-111: a message longer than maxmsglen is rejected).  Out:
+// {"offsets": [mark of each message, then where the framing stopped],
+//  "what": the exception's what() or "too long" or null at a clean end}.
+// A clean end is the stream's end reached exactly at a mark.
+#include <fcntl.h>
+#include <unistd.h>
+#include <xdrpp/srpc.h>
+
+static void frame_mode(const string &in, uint64_t maxlen, const string &out) {
+  const int fd = open(in.c_str(), O_RDONLY);
+  if (fd < 0) die("open " + in);
+  const off_t len = lseek(fd, 0, SEEK_END);
+  lseek(fd, 0, SEEK_SET);
+  std::ostringstream o;
+  o << "{\"offsets\": [";
+  uint64_t pos = 0;
+  string what = "null";
+  for (bool first = true;; first = false) {
+    o << (first ? "" : ", ") << pos;
+    if (pos == static_cast<uint64_t>(len)) break;
+    uint32_t raw = 0;
+    if (pread(fd, &raw, 4, pos) == 4) {  // msg_sock's rule needs the size first
+      const uint32_t v = xdr::swap32le(raw);
+      if (!(raw & 3) && (v & 0x80000000u) && (v & 0x7fffffffu) > maxlen) { what = "\"too long\""; break; }
+    }
+    try {
+      xdr::msg_ptr m = xdr::read_message(fd);
+      pos += m->raw_size();
+    } catch (const std::exception &e) {
+      what = string("\"") + e.what() + "\"";
+      break;
+    }
+  }
+  o << "], \"what\": " << what << "}\n";
+  close(fd);
+  std::ofstream f(out);
+  f << o.str();
+}
+
 int main(int argc, char **argv) {
-  if (argc < 2) die("usage: gen|kat|bench ...");
+  if (argc < 2) die("usage: gen|kat|bench|rpc|frame ...");
   string mode = argv[1];
+  if (mode == "frame") {
+    if (argc != 5) die("frame <stream> <maxmsglen> <out.json>");
+    frame_mode(argv[2], std::stoull(argv[3]), argv[4]);
+    return 0;
+  }
   if (mode == "kat") {
     if (argc != 3) die("kat <out.json>");
     kat(argv[2]);

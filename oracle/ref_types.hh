@@ -7,6 +7,7 @@
 //   xdrpp/rpc_msg.x     -> xdrpp/rpc_msg.hh   rpc_msg (also what server.h uses)
 //   oracle/x/bench.x    -> bench.hh           rec128, recvar, vecrec
 //   oracle/x/validated.x -> validated.hh      numerics in testns_v
+//   oracle/x/kat.x      -> kat.hh             the SURVEY §8(c) known-answer types
 // testns_v opts in to enum validation with the idiom of the reference's
 // tests/validate.cc:18-20.
 #ifndef XDRG_REF_TYPES_HH
@@ -15,6 +16,7 @@
 #include <xdrpp/rpc_msg.hh>
 
 #include "bench.hh"
+#include "kat.hh"
 #include "tests/xdrtest.hh"
 #include "validated.hh"
 

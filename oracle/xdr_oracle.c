@@ -45,6 +45,7 @@ typedef struct {
   uint32_t nops;
   const uint32_t *table;
   uint32_t stride;
+  const uint64_t *minw; /* decode: least wire bytes from each pc to its END */
 } plan_t;
 
 /* Find the target pc of a union discriminant, or -1. */
@@ -67,9 +68,10 @@ static int enum_ok(const plan_t *P, const xdrg_op *op, uint32_t v) {
  * (XDRG_F_SUB VECTOR ops, arg4 = entry pc) follow, each ending with END.
  * A subroutine walks one element: field offsets relative to the element,
  * depths relative to the VECTOR op that entered it (dbase).  The reference
- * recurses on its C++ stack; so does this restatement, with the device's
- * bound on nested element subroutines (XDRG_SUB_FRAMES, include/xdrgpu.h)
- * restated so both raise the stack-overflow error at the same op.
+ * recurses on its C++ stack (types.h:374-392, marshal.h:129-136); so does
+ * this restatement, with no bound on the nesting but marshaling_stack_limit
+ * (the device's XDRG_MAX_FRAMES lies past the depth at which the
+ * reference's own recursion overflows its call stack, and past this one's).
  *
  * Native objects are read through obj_t: the record (stride bytes) or an
  * element in the heap; bytes at or past the end read as 0, as the kernels'
@@ -107,6 +109,42 @@ static uint32_t vec_wire(const plan_t *P, uint32_t pc) {
  * native/wire size ratio of an element type.  Subroutine elements: distinct
  * elements start at distinct wire words, so stride/4 per wire byte, plus 2
  * for the 8-byte alignment of each array (xdrpp_amd/csrc/plan.cpp). */
+/* Least wire bytes of the walk from each pc to its region's END (unions:
+ * the cheapest arm; containers: empty), as plan.cpp computes them: an
+ * element subroutine consumes at least minw[body] bytes per element. */
+static uint64_t *min_wires(const xdrg_op *ops, uint32_t nops, const uint32_t *table) {
+  uint64_t *m = (uint64_t *)calloc((size_t)nops + 1, sizeof *m);
+  if (!m) abort();
+  for (uint32_t i = nops; i-- > 0;) {
+    const xdrg_op *op = &ops[i];
+    uint64_t v = 0;
+    switch (op->kind) {
+    case XDRG_OP_END: v = 0; break;
+    case XDRG_OP_JUMP: v = m[op->arg0]; break;
+    case XDRG_OP_VECTOR: v = m[i + 1 + op->arg2] + 4; break;
+    case XDRG_OP_UNION: {
+      int any = 0;
+      for (uint32_t c = 0; c < op->arg3; ++c) {
+        const uint64_t t = m[table[op->arg2 + 2 * c + 1]];
+        if (!any || t < v) v = t;
+        any = 1;
+      }
+      if (op->flags & XDRG_F_DEFAULT) {
+        const uint64_t t = m[op->arg4];
+        if (!any || t < v) v = t;
+      }
+      v += 4;
+      break;
+    }
+    case XDRG_OP_U64: v = m[i + 1] + 8; break;
+    case XDRG_OP_OPAQUE: v = m[i + 1] + pad4(op->arg0); break;
+    default: v = m[i + 1] + 4; break;
+    }
+    m[i] = v;
+  }
+  return m;
+}
+
 static uint32_t heap_factor(const plan_t *P) {
   uint32_t f = 0;
   for (uint32_t pc = 0; pc < P->nops; ++pc)
@@ -124,7 +162,7 @@ static uint32_t heap_factor(const plan_t *P) {
   return f;
 }
 uint64_t xdro_decode_heap_size(const xdrg_op *ops, uint32_t nops, uint64_t len) {
-  plan_t P = {ops, nops, NULL, 0};
+  plan_t P = {ops, nops, NULL, 0, NULL};
   uint32_t f = heap_factor(&P);
   return f ? ((len + 15) & ~15ull) + (uint64_t)f * len : len;
 }
@@ -134,14 +172,14 @@ uint64_t xdro_decode_heap_size(const xdrg_op *ops, uint32_t nops, uint64_t len) 
  * and the deepest class/container level entered (depth_checker,
  * xdrpp/depth_checker.h:10-79: a union and a container count their own
  * level, a non-empty xvector/pointer its element's).  A bad discriminant
- * (or data nested past XDRG_SUB_FRAMES) sets c->err / c->eop. */
+ * sets c->err / c->eop. */
 typedef struct {
   const plan_t *P;
   const uint8_t *heap;
   uint64_t heap_len;
   uint32_t err, eop, dmax;
 } szctx;
-static uint64_t size_ops(szctx *c, uint32_t pc, obj_t o, uint32_t dbase, uint32_t frames) {
+static uint64_t size_ops(szctx *c, uint32_t pc, obj_t o, uint32_t dbase) {
   const plan_t *P = c->P;
   uint64_t s = 0;
   for (;;) {
@@ -172,10 +210,9 @@ static uint64_t size_ops(szctx *c, uint32_t pc, obj_t o, uint32_t dbase, uint32_
         pc += 1 + op->arg2;
         break;
       }
-      if (cnt && frames == XDRG_SUB_FRAMES) { c->err = XDRG_ERR_STACK_PUT; c->eop = pc; return 0; }
       for (uint32_t i = 0; i < cnt; ++i) {
         obj_t e = {c->heap, c->heap_len, eoff + (uint64_t)i * op->arg1};
-        s += size_ops(c, op->arg4, e, dbase + op->depth, frames + 1);
+        s += size_ops(c, op->arg4, e, dbase + op->depth);
         if (c->err) return 0;
       }
       ++pc;
@@ -189,7 +226,7 @@ static uint64_t rec_size(const plan_t *P, const uint8_t *nat, const uint8_t *hea
                          uint32_t *err, uint32_t *eop) {
   szctx c = {P, heap, heap_len, 0, 0, 0};
   obj_t o = {nat, P->stride, 0};
-  uint64_t s = size_ops(&c, 0, o, 0, 0);
+  uint64_t s = size_ops(&c, 0, o, 0);
   *err = c.err;
   *eop = c.eop;
   return s;
@@ -207,7 +244,7 @@ typedef struct {
   uint64_t cap, pos;
   uint32_t stack_limit, eop;
 } ectx;
-static int enc_ops(ectx *c, uint32_t pc, obj_t o, uint32_t dbase, uint32_t frames) {
+static int enc_ops(ectx *c, uint32_t pc, obj_t o, uint32_t dbase) {
   const plan_t *P = c->P;
   for (;;) {
     const xdrg_op *op = &P->ops[pc];
@@ -284,10 +321,9 @@ static int enc_ops(ectx *c, uint32_t pc, obj_t o, uint32_t dbase, uint32_t frame
         pc += 1 + op->arg2;
         break;
       }
-      if (cnt && frames == XDRG_SUB_FRAMES) { c->eop = pc; return XDRG_ERR_STACK_PUT; }
       for (uint32_t i = 0; i < cnt; ++i) {
         obj_t el = {c->heap, c->heap_len, eoff + (uint64_t)i * op->arg1};
-        int rc = enc_ops(c, op->arg4, el, dbase + op->depth, frames + 1);
+        int rc = enc_ops(c, op->arg4, el, dbase + op->depth);
         if (rc) return rc;
       }
       ++pc;
@@ -304,7 +340,7 @@ int xdro_encode(const xdrg_op *ops, uint32_t nops, const uint32_t *table, uint32
                 const uint8_t *native, uint64_t n, const uint8_t *heap, uint64_t heap_len,
                 uint8_t *out, uint64_t cap, uint64_t *offsets, uint32_t stack_limit,
                 uint64_t *erec, uint32_t *eop, uint64_t *total) {
-  plan_t P = {ops, nops, table, stride};
+  plan_t P = {ops, nops, table, stride, NULL};
   ectx c = {&P, heap, heap_len, out, cap, 0, stack_limit, 0};
   for (uint64_t r = 0; r < n; ++r) {
     const uint8_t *nat = native + r * stride;
@@ -315,7 +351,7 @@ int xdro_encode(const xdrg_op *ops, uint32_t nops, const uint32_t *table, uint32
     rec_size(&P, nat, heap, heap_len, &err, &op_i);
     if (err) { *erec = r; *eop = op_i; return (int)err; }
     obj_t o = {nat, stride, 0};
-    int rc = enc_ops(&c, 0, o, 0, 0);
+    int rc = enc_ops(&c, 0, o, 0);
     if (rc) { *erec = r; *eop = c.eop; return rc; }
   }
   if (offsets) offsets[n] = c.pos;
@@ -327,7 +363,7 @@ int xdro_encode(const xdrg_op *ops, uint32_t nops, const uint32_t *table, uint32
 int xdro_sizes(const xdrg_op *ops, uint32_t nops, const uint32_t *table, uint32_t stride,
                const uint8_t *native, uint64_t n, const uint8_t *heap, uint64_t heap_len,
                uint32_t *sizes, uint64_t *erec, uint32_t *eop) {
-  plan_t P = {ops, nops, table, stride};
+  plan_t P = {ops, nops, table, stride, NULL};
   for (uint64_t r = 0; r < n; ++r) {
     uint32_t err = 0, op_i = 0;
     uint64_t s = rec_size(&P, native + r * stride, heap, heap_len, &err, &op_i);
@@ -343,11 +379,11 @@ int xdro_sizes(const xdrg_op *ops, uint32_t nops, const uint32_t *table, uint32_
 int xdro_depths(const xdrg_op *ops, uint32_t nops, const uint32_t *table, uint32_t stride,
                 const uint8_t *native, uint64_t n, const uint8_t *heap, uint64_t heap_len,
                 uint32_t *depths, uint64_t *erec, uint32_t *eop) {
-  plan_t P = {ops, nops, table, stride};
+  plan_t P = {ops, nops, table, stride, NULL};
   for (uint64_t r = 0; r < n; ++r) {
     szctx c = {&P, heap, heap_len, 0, 0, 0};
     obj_t o = {native + r * stride, stride, 0};
-    size_ops(&c, 0, o, 0, 0);
+    size_ops(&c, 0, o, 0);
     if (c.err) { *erec = r; *eop = c.eop; return (int)c.err; }
     depths[r] = c.dmax;
   }
@@ -367,7 +403,7 @@ typedef struct {
   uint64_t ecur, eend;
   uint32_t stack_limit, eop;
 } dctx;
-static int dec_ops(dctx *c, uint32_t pc, uint8_t *nat, uint32_t dbase, uint32_t frames) {
+static int dec_ops(dctx *c, uint32_t pc, uint8_t *nat, uint32_t dbase) {
   const plan_t *P = c->P;
 #define CHECK(nb) do { if ((uint64_t)(nb) > (uint64_t)(c->e - c->p)) { c->eop = pc; return XDRG_ERR_OVERFLOW_GET; } } while (0)
   for (;;) {
@@ -428,7 +464,23 @@ static int dec_ops(dctx *c, uint32_t pc, uint8_t *nat, uint32_t dbase, uint32_t 
         c->eop = pc;
         return (op->flags & XDRG_F_POINTER) ? XDRG_ERR_POINTER_BOUND : XDRG_ERR_XVECTOR_BOUND;
       }
-      c->ecur = (c->ecur + 7) & ~7ull;
+      /* Element area (the kernels' elem_area_ok and sub_kernels.h): valid
+       * data always fits; a count the bytes left cannot hold fails here
+       * with xdr_overflow -- an element subroutine's before any element,
+       * inline elements once the ones the bytes can reach would not fit. */
+      {
+        const uint64_t rem = (uint64_t)(c->e - c->p);
+        const int sub = (op->flags & XDRG_F_SUB) != 0;
+        const uint64_t w = sub ? P->minw[op->arg4] : vec_wire(P, pc);
+        uint64_t reach = cnt;
+        if (!sub && rem / w + 1 < reach) reach = rem / w + 1;
+        reach *= op->arg1;
+        c->ecur = (c->ecur + 7) & ~7ull;
+        if ((sub && (uint64_t)cnt * w > rem) || c->ecur > c->eend || reach > c->eend - c->ecur) {
+          c->eop = pc;
+          return XDRG_ERR_OVERFLOW_GET;
+        }
+      }
       xdrg_bytes_ref ref = {c->ecur, cnt, 0};
       memcpy(nat + op->noff, &ref, sizeof ref);
       if (!(op->flags & XDRG_F_SUB)) {  /* fixed elements, field by field */
@@ -467,16 +519,11 @@ static int dec_ops(dctx *c, uint32_t pc, uint8_t *nat, uint32_t dbase, uint32_t 
         break;
       }
       if (cnt) {
-        /* a count the record cannot hold may overrun the element area; it
-         * fails here (valid data never does) */
         const uint64_t bytes = (uint64_t)cnt * op->arg1, arr = c->ecur;
-        if (bytes > c->eend - c->ecur) { c->eop = pc; return XDRG_ERR_OVERFLOW_GET; }
-        if (frames == XDRG_SUB_FRAMES) { c->eop = pc; return XDRG_ERR_STACK_GET; }
         memset(c->heap_out + arr, 0, bytes);
         c->ecur += bytes;
         for (uint32_t i = 0; i < cnt; ++i) {
-          int rc = dec_ops(c, op->arg4, c->heap_out + arr + (uint64_t)i * op->arg1, dbase + op->depth,
-                           frames + 1);
+          int rc = dec_ops(c, op->arg4, c->heap_out + arr + (uint64_t)i * op->arg1, dbase + op->depth);
           if (rc) {  /* 1 + the element that failed (the unstager follows it) */
             ref.rsv = i + 1;
             memcpy(nat + op->noff, &ref, sizeof ref);
@@ -510,7 +557,7 @@ static int dec_record(const plan_t *P, const uint8_t **pp, const uint8_t *e, uin
                       uint32_t stack_limit, uint32_t *eop) {
   dctx c = {P, base, *pp, e, heap_out, ecur, eend, stack_limit, 0};
   memset(nat, 0, P->stride);
-  int rc = dec_ops(&c, 0, nat, 0, 0);
+  int rc = dec_ops(&c, 0, nat, 0);
   *pp = c.p;
   *eop = c.eop;
   return rc;
@@ -523,11 +570,24 @@ static int dec_record(const plan_t *P, const uint8_t **pp, const uint8_t *e, uin
  * slice [off[r], off[r+1]).  heap_out (if given) receives the stream
  * verbatim; every decoded xdrg_bytes_ref points at its payload in it.
  */
+static int decode_batch(const plan_t *PP, const uint8_t *xdr, uint64_t len, const uint64_t *offsets,
+                        uint64_t n, uint8_t *native, uint8_t *heap_out, uint32_t stack_limit,
+                        uint64_t *erec, uint32_t *eop);
 int xdro_decode(const xdrg_op *ops, uint32_t nops, const uint32_t *table, uint32_t stride,
                 const uint8_t *xdr, uint64_t len, const uint64_t *offsets, uint64_t n,
                 uint8_t *native, uint8_t *heap_out, uint32_t stack_limit, uint64_t *erec,
                 uint32_t *eop) {
-  plan_t P = {ops, nops, table, stride};
+  uint64_t *mw = min_wires(ops, nops, table);
+  plan_t P = {ops, nops, table, stride, mw};
+  int rc = decode_batch(&P, xdr, len, offsets, n, native, heap_out, stack_limit, erec, eop);
+  free(mw);
+  return rc;
+}
+static int decode_batch(const plan_t *PP, const uint8_t *xdr, uint64_t len, const uint64_t *offsets,
+                        uint64_t n, uint8_t *native, uint8_t *heap_out, uint32_t stack_limit,
+                        uint64_t *erec, uint32_t *eop) {
+  const plan_t P = *PP;
+  const uint32_t stride = P.stride;
   if (heap_out && len) memcpy(heap_out, xdr, len);
   const uint32_t F = heap_factor(&P);
   const uint64_t ebase = F ? ((len + 15) & ~15ull) : 0;
@@ -579,7 +639,7 @@ int xdro_encode_msgs(const xdrg_op *ops, uint32_t nops, const uint32_t *table, u
                      const uint8_t *native, uint64_t n, const uint8_t *heap, uint64_t heap_len,
                      uint8_t *out, uint64_t cap, uint64_t *offsets, uint32_t stack_limit,
                      uint64_t *erec, uint32_t *eop, uint64_t *total) {
-  plan_t P = {ops, nops, table, stride};
+  plan_t P = {ops, nops, table, stride, NULL};
   uint64_t pos = 0;
   for (uint64_t r = 0; r < n; ++r) {
     const uint8_t *nat = native + r * stride;
@@ -603,11 +663,24 @@ int xdro_encode_msgs(const xdrg_op *ops, uint32_t nops, const uint32_t *table, u
 
 /* n messages indexed by offsets (message r = [off[r], off[r+1]), mark
  * included), each decoded as xdr_from_msg. */
+static int decode_msgs_batch(const plan_t *PP, const uint8_t *xdr, uint64_t len,
+                             const uint64_t *offsets, uint64_t n, uint8_t *native, uint8_t *heap_out,
+                             uint32_t stack_limit, uint64_t *erec, uint32_t *eop);
 int xdro_decode_msgs(const xdrg_op *ops, uint32_t nops, const uint32_t *table, uint32_t stride,
                      const uint8_t *xdr, uint64_t len, const uint64_t *offsets, uint64_t n,
                      uint8_t *native, uint8_t *heap_out, uint32_t stack_limit, uint64_t *erec,
                      uint32_t *eop) {
-  plan_t P = {ops, nops, table, stride};
+  uint64_t *mw = min_wires(ops, nops, table);
+  plan_t P = {ops, nops, table, stride, mw};
+  int rc = decode_msgs_batch(&P, xdr, len, offsets, n, native, heap_out, stack_limit, erec, eop);
+  free(mw);
+  return rc;
+}
+static int decode_msgs_batch(const plan_t *PP, const uint8_t *xdr, uint64_t len,
+                             const uint64_t *offsets, uint64_t n, uint8_t *native, uint8_t *heap_out,
+                             uint32_t stack_limit, uint64_t *erec, uint32_t *eop) {
+  const plan_t P = *PP;
+  const uint32_t stride = P.stride;
   if (heap_out && len) memcpy(heap_out, xdr, len);
   const uint32_t F = heap_factor(&P);
   const uint64_t ebase = F ? ((len + 15) & ~15ull) : 0;
@@ -712,7 +785,9 @@ static uint32_t rx_walk(rxctx *c, uint64_t *pp, uint32_t pc, uint32_t frames) {
         pc += 1 + op->arg2;
         break;
       }
-      if (v && frames == XDRG_SUB_FRAMES) return RX_BAD;
+      /* the device index keeps XDRG_SUB_FRAMES frames: deeper records are
+       * left to the caller's walk, as records past the window are */
+      if (v && frames == XDRG_SUB_FRAMES) return RX_LONG;
       for (uint32_t i = 0; i < v; ++i) {
         uint32_t rc = rx_walk(c, &p, op->arg4, frames + 1);
         if (rc) return rc;
@@ -727,7 +802,7 @@ static uint32_t rx_walk(rxctx *c, uint64_t *pp, uint32_t pc, uint32_t frames) {
 int xdro_index_records(const xdrg_op *ops, uint32_t nops, const uint32_t *table, const uint8_t *s,
                        uint64_t len, uint64_t n, uint32_t maxlen, uint64_t *offsets, uint64_t *count,
                        uint64_t *erec) {
-  plan_t P = {ops, nops, table, 0};
+  plan_t P = {ops, nops, table, 0, NULL};
   uint64_t p = 0, k = 0;
   *count = UINT64_MAX;
   for (; k < n && p < len; ++k) {

@@ -136,20 +136,24 @@ def chain(depth: int):
     return v
 
 
-def test_oracle_frame_bound():
-    """Element subroutines nest at most XDRG_SUB_FRAMES deep (the device's
-    bound, restated by the oracle); one more raises xdr_stack_overflow at
-    the container that would open the next frame."""
+def test_oracle_no_frame_bound():
+    """Element subroutines nest as deep as the data goes (types.h:591-665):
+    only marshaling_stack_limit raises xdr_stack_overflow (marshal.h:131-132,
+    :200-201).  Chains just past the device's private frames and well past
+    them round-trip; the reference's own chains are in test_deep.py."""
     cp = compile_plan(S.test_recursive)
-    ok = chain(A.SUB_FRAMES + 1)  # root + SUB_FRAMES elements
-    nat, heap = OB.stage(S.test_recursive, [ok])
-    x, offs = O.encode(cp, nat, 1, heap)
-    nat2, heap2 = O.decode(cp, x, 1, offs)
-    assert OB.unstage(S.test_recursive, nat2, heap2, 1) == [ok]
-    nat, heap = OB.stage(S.test_recursive, [chain(A.SUB_FRAMES + 2)])
+    vals = [chain(A.SUB_FRAMES + 1), chain(A.SUB_FRAMES + 2), chain(A.SUB_FRAMES + 60)]
+    nat, heap = OB.stage(S.test_recursive, vals)
+    x, offs = O.encode(cp, nat, 3, heap)
+    nat2, heap2 = O.decode(cp, x, 3, offs)
+    assert OB.unstage(S.test_recursive, nat2, heap2, 3) == vals
+    # the stack budget of a chain of k nodes is 2k: the third record fails
     with pytest.raises(O.OracleError) as e:
-        O.encode(cp, nat, 1, heap)
-    assert (e.value.code, e.value.op) == (A.ERR_STACK_PUT, 1)  # `next` of the deepest frame
+        O.encode(cp, nat, 3, heap, stack_limit=2 * (A.SUB_FRAMES + 2))
+    assert (e.value.code, e.value.record) == (A.ERR_STACK_PUT, 2)
+    with pytest.raises(O.OracleError) as e:
+        O.decode(cp, x, 3, offs, stack_limit=2 * (A.SUB_FRAMES + 2))
+    assert (e.value.code, e.value.record) == (A.ERR_STACK_GET, 2)
 
 
 @pytest.mark.skipif(not os.path.exists(f"{REF}/xdrpp/marshal.cc"), reason="reference tree absent")
@@ -242,21 +246,32 @@ def test_gpu_containertest1_overflow(gold, dev):
 
 
 @pytest.mark.gpu
-def test_gpu_frame_bound(dev):
+def test_gpu_no_frame_bound(dev):
+    """Past the private frames the deep passes walk the record: same bytes
+    and decode as the oracle, and only the stack limit fails it."""
     from xdrpp_amd import marshal as M
     cp = compile_plan(S.test_recursive)
     mar = M.Marshaler(M.Plan(S.test_recursive), dev)
-    vals = [chain(A.SUB_FRAMES + 1), chain(3), chain(A.SUB_FRAMES + 2)]
-    nat, heap = OB.stage(S.test_recursive, vals[:2])
-    r = mar.encode(_dev(nat, dev), 2, _dev(heap, dev))
-    x, offs = O.encode(cp, nat, 2, heap)
-    assert bytes(r.xdr.cpu().numpy()) == bytes(x)
-    nat2, heap2 = mar.decode(r.xdr, 2, r.offsets)
-    assert OB.unstage(S.test_recursive, nat2.cpu().numpy(), heap2.cpu().numpy(), 2) == vals[:2]
+    vals = [chain(A.SUB_FRAMES + 1), chain(3), chain(A.SUB_FRAMES + 2), chain(A.SUB_FRAMES + 60)]
     nat, heap = OB.stage(S.test_recursive, vals)
+    dn, dh = _dev(nat, dev), _dev(heap, dev)
+    r = mar.encode(dn, 4, dh)
+    x, offs = O.encode(cp, nat, 4, heap)
+    assert bytes(r.xdr.cpu().numpy()) == bytes(x)
+    assert np.array_equal(mar.record_depths(dn, 4, dh).cpu().numpy(), O.depths(cp, nat, 4, heap))
+    nat2, heap2 = mar.decode(r.xdr, 4, r.offsets)
+    assert OB.unstage(S.test_recursive, nat2.cpu().numpy(), heap2.cpu().numpy(), 4) == vals
+    L = 2 * (A.SUB_FRAMES + 2)
+    with pytest.raises(O.OracleError) as want:
+        O.encode(cp, nat, 4, heap, stack_limit=L)
     with pytest.raises(M.XdrStackOverflow) as e:
-        mar.encode(_dev(nat, dev), 3, _dev(heap, dev))
-    assert (e.value.record, e.value.op) == (2, 1)
+        mar.encode(dn, 4, dh, stack_limit=L)
+    assert (e.value.record, e.value.op) == (want.value.record, want.value.op) == (3, want.value.op)
+    with pytest.raises(O.OracleError) as want:
+        O.decode(cp, x, 4, offs, stack_limit=L)
+    with pytest.raises(M.XdrStackOverflow) as e:
+        mar.decode(r.xdr, 4, r.offsets, stack_limit=L)
+    assert (e.value.record, e.value.op) == (want.value.record, want.value.op)
 
 
 @pytest.mark.gpu
@@ -285,3 +300,76 @@ def test_gpu_random_recursive_batch(dev):
     nat2, heap2 = mar.decode(r.xdr, n, r.offsets)
     onat, oheap = O.decode(cp, x, n, offs)
     assert np.array_equal(nat2.cpu().numpy(), onat) and np.array_equal(heap2.cpu().numpy(), oheap)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", NAMES + ["vecrec"])
+@pytest.mark.parametrize("seed", range(8))
+def test_gpu_malformed_streams(gold, dev, name, seed):
+    """Damaged container streams: flipped bytes, forged element counts and
+    a truncated last record.  The device reports the oracle's error (code,
+    record, op) and writes nothing past the decoded heap it was given
+    (guard bytes after it stay intact)."""
+    import torch
+    from xdrpp_amd import marshal as M
+    from xdrpp_amd import workloads as W
+    if name == "vecrec":
+        t = S.vecrec
+        nat, heap = W.GENERATORS["vecrec"](64)
+        x, offs = O.encode(compile_plan(t), nat, 64, heap)
+        x = bytes(x)
+    else:
+        t, vals, wire, offs, recs = batch(gold, name)
+        x = b"".join(wire)
+    cp = compile_plan(t)
+    n = len(offs) - 1
+    x = np.frombuffer(x, dtype=np.uint8).copy()
+    offs = offs.astype(np.uint64).copy()
+    rng = np.random.default_rng(7000 + seed)
+    mode = seed % 3
+    if mode == 0:  # flipped bytes
+        for _ in range(4):
+            x[int(rng.integers(0, x.size))] = np.uint8(rng.integers(0, 256))
+    elif mode == 1:  # a forged count or length: a big value in a random word
+        w = int(rng.integers(0, x.size // 4))
+        x[4 * w:4 * w + 4] = np.frombuffer(int(rng.integers(2, 1 << 20)).to_bytes(4, "big"), dtype=np.uint8)
+    else:  # the last record cut short, a forged count in it
+        a, b = int(offs[n - 1]), int(offs[n])
+        if b - a >= 8:
+            w = a // 4 + int(rng.integers(0, (b - a) // 4))
+            x[4 * w:4 * w + 4] = np.frombuffer(int(rng.integers(2, 64)).to_bytes(4, "big"), dtype=np.uint8)
+            cut = 4 * int(rng.integers(1, (b - a) // 4))
+            x = x[:b - cut].copy()
+            offs[n] = b - cut
+    want = _oracle_err(lambda: O.decode(cp, x, n, offs))
+    mar = M.Marshaler(M.Plan(t), dev)
+    hsize = mar.plan.decode_heap_bytes(x.size)
+    guard = 4096
+    heap = torch.full((hsize + guard,), 0xA5, dtype=torch.uint8, device=dev)
+    native = torch.zeros(n * mar.plan.stride + guard, dtype=torch.uint8, device=dev)
+    native[n * mar.plan.stride:] = 0xA5
+    s = torch.cuda.current_stream().cuda_stream
+    mar.status.init(s)
+    mar.launch_decode(_dev(x, dev), n, native[:n * mar.plan.stride], offsets=_dev(offs.view(np.int64), dev),
+                      heap_out=heap[:hsize], stream=s)
+    got = _gpu_err(lambda: mar.check(s))
+    assert got == want
+    assert bool((heap[hsize:] == 0xA5).all()), "decode wrote past its heap"
+    assert bool((native[n * mar.plan.stride:] == 0xA5).all()), "decode wrote past its records"
+
+
+def _oracle_err(fn):
+    try:
+        fn()
+    except O.OracleError as e:
+        return (e.code, e.record, e.op)
+    return None
+
+
+def _gpu_err(fn):
+    from xdrpp_amd import marshal as M
+    try:
+        fn()
+    except M.XdrRuntimeError as e:
+        return (e.code, e.record, 0xFFFFFFFF if e.op is None else e.op)
+    return None

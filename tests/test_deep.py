@@ -1,0 +1,279 @@
+"""Deeply nested element subroutines: linked lists through pointer<T>.
+
+tests/xdrtest.x's test_recursive (`test_recursive *next`, :29-33) and
+rpcbind's RPCBPROC_DUMP reply list rp__list (xdrpp/rpcb_prot.x:24-37)
+nest one element frame per node.  The reference recurses through them on
+its call stack (xdrpp/types.h:591-665, marshal.h:129-136, :198-205),
+bounded only by marshaling_stack_limit.  The device keeps XDRG_SUB_FRAMES
+frames per record in private memory and walks deeper records again in its
+deep passes (xdrpp_amd/csrc/sub_kernels.h); only XDRG_MAX_FRAMES, far past
+the depth at which the reference's own recursion crashes, is a limit of
+its own.
+
+Golden vectors: tests/golden/deep.json, written by oracle/ref_deep.cc
+(`make -C oracle deep`) -- the REAL reference marshaler over genuine xdrc
+output.  Chains are staged and read back iteratively here (no recursion
+in Python, whose limit a 3000-node chain would pass).
+"""
+import json
+import os
+import struct
+
+import numpy as np
+import pytest
+
+from conftest import GOLD, ROOT
+
+from xdrpp_amd import _abi as A
+from xdrpp_amd import objects as OB
+from xdrpp_amd import schemas as S
+from xdrpp_amd.xdr_types import compile_plan
+import oracle_bridge as O
+
+REF = "/root/reference"
+LINK = {"test_recursive": "next", "rp__list": "rpcb_next"}
+
+
+@pytest.fixture(scope="module")
+def gold():
+    with open(os.path.join(GOLD, "deep.json")) as f:
+        return json.load(f)
+
+
+def node_value(name, j):
+    """One chain node's non-link fields as objects.py holds them."""
+    if name == "test_recursive":
+        return {"elem": bytes.fromhex(j), "nextvec": []}
+    prog, vers, netid, addr, owner = j
+    return {"rpcb_map": {"r_prog": prog, "r_vers": vers, "r_netid": bytes.fromhex(netid),
+                         "r_addr": bytes.fromhex(addr), "r_owner": bytes.fromhex(owner)}}
+
+
+def stage_chains(name, chains):
+    """Native records + heap of records that are linked lists (lists of
+    node values), built iteratively: node i+1 is the single element of node
+    i's link pointer."""
+    t = S.CONTAINERS.get(name) or getattr(S, name)
+    link = LINK[name]
+    stride = OB._align_up(t.size, t.align)
+    native = bytearray(len(chains) * stride)
+    heap = OB._Heap()
+    for r, nodes in enumerate(chains):
+        buf, off = native, r * stride
+        for i, node in enumerate(nodes):
+            for fname, ft in t.fields:
+                if fname != link:
+                    OB._put(ft, buf, off + t.offsets[fname], node[fname], heap)
+            nxt = i + 1 < len(nodes)
+            arr = heap.alloc(stride if nxt else 0, 8)
+            struct.pack_into("<QII", buf, off + t.offsets[link], arr, 1 if nxt else 0, 0)
+            buf, off = heap.buf, arr
+    return np.frombuffer(bytes(native), dtype=np.uint8).copy(), np.frombuffer(bytes(heap.buf), dtype=np.uint8).copy()
+
+
+def unstage_chains(name, native, heap, n):
+    """The node lists of n decoded list records (iterative walk)."""
+    t = S.CONTAINERS.get(name) or getattr(S, name)
+    link = LINK[name]
+    stride = OB._align_up(t.size, t.align)
+    nat, hp = bytes(np.asarray(native, dtype=np.uint8)), bytes(np.asarray(heap, dtype=np.uint8))
+    out = []
+    for r in range(n):
+        buf, off, nodes = nat, r * stride, []
+        while True:
+            nodes.append({f: OB._get(ft, buf, off + t.offsets[f], hp) for f, ft in t.fields if f != link})
+            arr, cnt, _ = struct.unpack_from("<QII", buf, off + t.offsets[link])
+            if not cnt:
+                break
+            buf, off = hp, arr
+        out.append(nodes)
+    return out
+
+
+def chains_of(gold, name):
+    recs = gold[name]
+    chains = [[node_value(name, j) for j in r["nodes"]] for r in recs]
+    wire = [bytes.fromhex(r["xdr"]) for r in recs]
+    offs = np.zeros(len(recs) + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(w) for w in wire])
+    return chains, wire, offs, recs
+
+
+TYPES = ["test_recursive", "rp__list"]
+
+
+def plan_of(name):
+    return compile_plan(S.CONTAINERS.get(name) or getattr(S, name))
+
+
+# ------------------------------------------------------------------ CPU
+@pytest.mark.skipif(not os.path.exists(f"{REF}/xdrpp/rpcb_prot.x"), reason="reference tree absent")
+def test_rp_list_schema_equals_rpcb_prot_x():
+    import xdrc_front as xdrc
+    from test_xdrc import same_plan
+    sp = xdrc.load_file(f"{REF}/xdrpp/rpcb_prot.x")
+    assert same_plan(sp.plan("rp__list"), compile_plan(S.rp__list))
+
+
+@pytest.mark.parametrize("name", TYPES)
+def test_oracle_matches_reference(gold, name):
+    """The C restatement (no nesting bound but the stack limit) reproduces
+    the reference's bytes, sizes, depths and decodes of every chain."""
+    chains, wire, offs, recs = chains_of(gold, name)
+    cp, n = plan_of(name), len(chains)
+    nat, heap = stage_chains(name, chains)
+    x, o = O.encode(cp, nat, n, heap)
+    assert bytes(x) == b"".join(wire)
+    assert np.array_equal(o, offs)
+    assert np.array_equal(O.sizes(cp, nat, n, heap), [len(w) for w in wire])
+    assert np.array_equal(O.depths(cp, nat, n, heap), [r["depth"] for r in recs])
+    nat2, heap2 = O.decode(cp, np.frombuffer(b"".join(wire), dtype=np.uint8), n, offs)
+    assert unstage_chains(name, nat2, heap2, n) == chains
+
+
+@pytest.mark.parametrize("name", TYPES)
+def test_oracle_stack_limits(gold, name):
+    """Only marshaling_stack_limit stops a deep record (marshal.h:131-132,
+    :200-201): the first record whose limit exceeds L fails."""
+    chains, wire, offs, recs = chains_of(gold, name)
+    cp, n = plan_of(name), len(chains)
+    nat, heap = stage_chains(name, chains)
+    x = np.frombuffer(b"".join(wire), dtype=np.uint8)
+    for L in sorted({r["put_limit"] for r in recs})[-3:]:
+        first = next(i for i, r in enumerate(recs) if r["put_limit"] > L - 1)
+        with pytest.raises(O.OracleError) as e:
+            O.encode(cp, nat, n, heap, stack_limit=L - 1)
+        assert (e.value.code, e.value.record) == (A.ERR_STACK_PUT, first)
+        first = next(i for i, r in enumerate(recs) if r["get_limit"] > L - 1)
+        with pytest.raises(O.OracleError) as e:
+            O.decode(cp, x, n, offs, stack_limit=L - 1)
+        assert (e.value.code, e.value.record) == (A.ERR_STACK_GET, first)
+
+
+@pytest.mark.skipif(not os.path.exists(f"{REF}/xdrpp/marshal.cc"), reason="reference tree absent")
+def test_fixture_regenerates(tmp_path):
+    """deep.json is what the reference produces today (empty diff)."""
+    import subprocess
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "_ref/ref_deep"], check=True)
+    out = tmp_path / "d.json"
+    subprocess.run([os.path.join(ROOT, "oracle", "_ref", "ref_deep"), str(out)], check=True)
+    assert out.read_bytes() == open(os.path.join(GOLD, "deep.json"), "rb").read()
+
+
+def chain_stream(depth):
+    """xdr_to_opaque of a test_recursive chain of `depth` nodes with empty
+    elems: depth x (elem len 0, pointer flag) then depth x (nextvec count 0),
+    with the last flag 0."""
+    w = np.zeros(3 * depth, dtype=">u4")
+    w[1:2 * depth:2] = 1
+    w[2 * depth - 1] = 0
+    return w.view(np.uint8).copy()
+
+
+# ------------------------------------------------------------------ GPU
+def _dev(a, dev):
+    import torch
+    return torch.from_numpy(np.array(a)).to(dev)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", TYPES)
+def test_gpu_matches_reference(gold, dev, name):
+    """Every chain, 1 to 3000 nodes: bytes, offsets, sizes, depths and the
+    decode, through the main pass and both deep passes."""
+    from xdrpp_amd import marshal as M
+    chains, wire, offs, recs = chains_of(gold, name)
+    cp, n = plan_of(name), len(chains)
+    mar = M.Marshaler(M.Plan(S.CONTAINERS.get(name) or getattr(S, name)), dev)
+    nat, heap = stage_chains(name, chains)
+    dn, dh = _dev(nat, dev), _dev(heap, dev)
+    r = mar.encode(dn, n, dh)
+    assert bytes(r.xdr.cpu().numpy()) == b"".join(wire)
+    assert np.array_equal(r.offsets.cpu().numpy().astype(np.uint64), offs)
+    assert np.array_equal(mar.serial_sizes(dn, n, heap=dh).cpu().numpy(), [len(w) for w in wire])
+    assert np.array_equal(mar.record_depths(dn, n, dh).cpu().numpy(), [r_["depth"] for r_ in recs])
+    x = np.frombuffer(b"".join(wire), dtype=np.uint8)
+    nat2, heap2 = mar.decode(_dev(x, dev), n, _dev(offs.astype(np.int64), dev))
+    assert unstage_chains(name, nat2.cpu().numpy(), heap2.cpu().numpy(), n) == chains
+    onat, oheap = O.decode(cp, x, n, offs)
+    assert np.array_equal(nat2.cpu().numpy(), onat)
+    assert np.array_equal(heap2.cpu().numpy(), oheap)
+    # record-marked messages take the same walks
+    m = mar.encode_msgs(dn, n, dh)
+    assert bytes(m.xdr.cpu().numpy()) == b"".join((len(w) | 0x80000000).to_bytes(4, "big") + w for w in wire)
+    nat3, heap3 = mar.decode_msgs(m.xdr)
+    assert unstage_chains(name, nat3.cpu().numpy(), heap3.cpu().numpy(), n) == chains
+
+
+@pytest.mark.gpu
+def test_gpu_stack_limits(gold, dev):
+    """marshaling_stack_limit is the only limit the reference's data meets:
+    xdr_stack_overflow at the first record past it, whichever pass walks it."""
+    from xdrpp_amd import marshal as M
+    chains, wire, offs, recs = chains_of(gold, "test_recursive")
+    n = len(chains)
+    mar = M.Marshaler(M.Plan(S.test_recursive), dev)
+    nat, heap = stage_chains("test_recursive", chains)
+    dn, dh = _dev(nat, dev), _dev(heap, dev)
+    dx, do = _dev(np.frombuffer(b"".join(wire), dtype=np.uint8), dev), _dev(offs.astype(np.int64), dev)
+    for L in (60, 66, 2000, 2049, 2052, 6000):
+        first = next((i for i, r in enumerate(recs) if r["put_limit"] > L), None)
+        if first is None:
+            assert bytes(mar.encode(dn, n, dh, stack_limit=L).xdr.cpu().numpy()) == b"".join(wire)
+            continue
+        with pytest.raises(M.XdrStackOverflow) as e:
+            mar.encode(dn, n, dh, stack_limit=L, capacity=int(offs[-1]))
+        assert e.value.record == first
+        with pytest.raises(M.XdrStackOverflow) as e:
+            mar.decode(dx, n, do, stack_limit=L)
+        assert e.value.record == next(i for i, r in enumerate(recs) if r["get_limit"] > L)
+
+
+@pytest.mark.gpu
+def test_gpu_many_deep_records(gold, dev):
+    """Hundreds of deep records at once (deep pass A's lanes, the lists)
+    against the oracle, mixed with shallow ones."""
+    from xdrpp_amd import marshal as M
+    chains, wire, offs, recs = chains_of(gold, "test_recursive")
+    pick = [0, 4, 5, 7, 8, 1, 11, 2]
+    many = [chains[pick[i % len(pick)]] for i in range(400)]
+    n, cp = len(many), plan_of("test_recursive")
+    nat, heap = stage_chains("test_recursive", many)
+    mar = M.Marshaler(M.Plan(S.test_recursive), dev)
+    r = mar.encode(_dev(nat, dev), n, _dev(heap, dev))
+    x, o = O.encode(cp, nat, n, heap)
+    assert bytes(r.xdr.cpu().numpy()) == bytes(x)
+    nat2, heap2 = mar.decode(r.xdr, n, r.offsets)
+    onat, oheap = O.decode(cp, x, n, o)
+    assert np.array_equal(nat2.cpu().numpy(), onat) and np.array_equal(heap2.cpu().numpy(), oheap)
+
+
+@pytest.mark.gpu
+def test_gpu_max_frames(dev):
+    """XDRG_MAX_FRAMES: the device's own limit, past the reference's crash
+    depth.  A chain that needs one frame more fails with xdr_stack_overflow
+    at the `next` pointer that would open it, on encode (a cyclic staged heap
+    too: it would never end) and on decode; one frame less passes."""
+    from xdrpp_amd import marshal as M
+    mar = M.Marshaler(M.Plan(S.test_recursive), dev)
+    ok, bad = A.MAX_FRAMES + 1, A.MAX_FRAMES + 2  # nodes = frames + 1
+    xs = [chain_stream(ok), chain_stream(bad)]
+    for x, fails in zip(xs, (False, True)):
+        offs = np.array([0, x.size], dtype=np.int64)
+        if fails:
+            with pytest.raises(M.XdrStackOverflow) as e:
+                mar.decode(_dev(x, dev), 1, _dev(offs, dev))
+            assert (e.value.record, e.value.op) == (0, 1)
+        else:
+            nat, heap = mar.decode(_dev(x, dev), 1, _dev(offs, dev))
+            r = mar.encode(nat, 1, heap)
+            assert np.array_equal(r.xdr.cpu().numpy(), x)
+    # a node whose `next` is itself: the walk ends at the frame limit
+    t = S.test_recursive
+    nat = np.zeros(OB._align_up(t.size, t.align), dtype=np.uint8)
+    struct.pack_into("<QII", nat, t.offsets["next"], 0, 1, 0)
+    struct.pack_into("<QII", nat, t.offsets["nextvec"], 0, 0, 0)
+    heap = nat.copy()  # element 0 of the pointer is the record's own image
+    with pytest.raises(M.XdrStackOverflow) as e:
+        mar.encode(_dev(nat, dev), 1, _dev(heap, dev))
+    assert (e.value.record, e.value.op) == (0, 1)

@@ -1,0 +1,24 @@
+# One GPU-box pass of chosen steps, each under its own time limit, chained
+# so that the first failure ends the pass.  Output under gpurun_out/$TAG.
+#   gpurun -- 'TAG=x STEPS="copy tests:tests/test_deep.py bench" bash tools/gpu/step.sh'
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+O=gpurun_out/${TAG:-step}
+mkdir -p "$O"
+for st in ${STEPS:-tests bench}; do
+  name=${st%%:*}; arg=${st#*:}; [ "$arg" = "$st" ] && arg=""
+  echo "[step] $st $(date +%T)"
+  case $name in
+    copy) timeout -k 10 120 ./tools/probe/copy_ceiling 256 2048 4096 > "$O/copy_ceiling.log" 2>&1 ;;
+    tests) timeout -k 10 900 python3 -u -m pytest ${arg:-tests} -m gpu -x -v --timeout 300 --timeout-method thread > "$O/pytest_${arg//\//_}.log" 2>&1 ;;
+    smoke) timeout -k 10 300 python3 -u -c 'import __graft_entry__ as g; g.smoke()' > "$O/smoke.log" 2>&1 ;;
+    bench) timeout -k 10 400 python3 -u bench.py ${arg//,/ } > "$O/bench_${arg//[ ,-]/_}.log" 2>&1 ;;
+    prof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_${arg//[ ,-]/_}" -o run --output-format csv -- python3 bench.py --no-cpu-baseline ${arg//,/ } > "$O/prof_${arg//[ ,-]/_}.log" 2>&1 ;;
+    *) echo "unknown step $st"; exit 2 ;;
+  esac
+  rc=$?
+  echo "[step] $st rc=$rc $(date +%T)"
+  [ $rc -ne 0 ] && { tail -30 "$O"/*.log; exit $rc; }
+done
+tail -3 "$O"/*.log

@@ -1,0 +1,131 @@
+// Probe (not part of the product): the device-copy ceiling of the box,
+// against which the fixed-record kernels are judged (VERDICT r02 "What's
+// weak" 3).  MI355X_MICROARCH.md quotes 6.29 TB/s for a float4 copy; this
+// measures plain 16-byte copies of several shapes past the 256 MiB Infinity
+// Cache (2 GiB and 4 GiB per buffer), plus read-only and write-only streams
+// and hipMemcpy D2D, all interleaved in one process, median of 15 reps.
+//   hipcc --offload-arch=gfx950 -O3 -o copy_ceiling copy_ceiling.hip
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <string>
+#include <vector>
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// one 16-byte chunk per thread, one-shot grid
+template <bool NT>
+__global__ __launch_bounds__(256) void k_flat(const u32x4 *__restrict__ in, u32x4 *__restrict__ out, uint64_t n) {
+  const uint64_t i = uint64_t(blockIdx.x) * 256u + threadIdx.x;
+  if (i < n) {
+    u32x4 v = NT ? __builtin_nontemporal_load(in + i) : in[i];
+    if (NT) __builtin_nontemporal_store(v, out + i); else out[i] = v;
+  }
+}
+// U chunks per thread, one-shot grid (block-contiguous: a block covers 256*U chunks)
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void k_flatU(const u32x4 *__restrict__ in, u32x4 *__restrict__ out, uint64_t n) {
+  const uint64_t b = uint64_t(blockIdx.x) * 256u * U + threadIdx.x;
+  u32x4 v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (b + 256u * u < n) v[u] = NT ? __builtin_nontemporal_load(in + b + 256u * u) : in[b + 256u * u];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (b + 256u * u < n) {
+      if (NT) __builtin_nontemporal_store(v[u], out + b + 256u * u); else out[b + 256u * u] = v[u];
+    }
+}
+// grid-stride, U chunks in flight
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void k_gs(const u32x4 *__restrict__ in, u32x4 *__restrict__ out, uint64_t n) {
+  const uint64_t stride = uint64_t(gridDim.x) * 256u;
+  for (uint64_t c = uint64_t(blockIdx.x) * 256u + threadIdx.x; c < n; c += U * stride) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (c + u * stride < n) v[u] = NT ? __builtin_nontemporal_load(in + c + u * stride) : in[c + u * stride];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (c + u * stride < n) {
+        if (NT) __builtin_nontemporal_store(v[u], out + c + u * stride); else out[c + u * stride] = v[u];
+      }
+  }
+}
+__global__ __launch_bounds__(256) void k_read(const u32x4 *__restrict__ in, uint64_t n, uint32_t *sink) {
+  const uint64_t stride = uint64_t(gridDim.x) * 256u;
+  uint32_t acc = 0;
+  for (uint64_t c = uint64_t(blockIdx.x) * 256u + threadIdx.x; c < n; c += 4 * stride) {
+    u32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = c + u * stride < n ? in[c + u * stride] : u32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+__global__ __launch_bounds__(256) void k_write(u32x4 *__restrict__ out, uint64_t n) {
+  const uint64_t i = uint64_t(blockIdx.x) * 256u + threadIdx.x;
+  if (i < n) out[i] = u32x4{uint32_t(i), 1u, 2u, 3u};
+}
+
+int main(int argc, char **argv) {
+  std::vector<uint64_t> sizes_mib = {256, 2048, 4096};
+  if (argc > 1) { sizes_mib.clear(); for (int i = 1; i < argc; ++i) sizes_mib.push_back(strtoull(argv[i], 0, 10)); }
+  hipDeviceProp_t prop;
+  hipGetDeviceProperties(&prop, 0);
+  printf("device %s CUs %d\n", prop.gcnArchName, prop.multiProcessorCount);
+  const uint64_t maxb = *std::max_element(sizes_mib.begin(), sizes_mib.end()) << 20;
+  u32x4 *a, *b;
+  uint32_t *sink;
+  if (hipMalloc(&a, maxb) || hipMalloc(&b, maxb) || hipMalloc(&sink, 64)) { printf("alloc failed\n"); return 1; }
+  hipMemset(a, 1, maxb);
+  hipMemset(b, 0, maxb);
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  for (uint64_t mib : sizes_mib) {
+    const uint64_t bytes = mib << 20, n = bytes / 16;
+    struct V { std::string name; double mult; std::function<void()> go; std::vector<float> t; };
+    std::vector<V> vs;
+    auto flat = [&](uint64_t blocks) { return uint32_t(blocks); };
+    vs.push_back({"flat_1chunk", 2, [&] { k_flat<false><<<flat((n + 255) / 256), 256>>>(a, b, n); }, {}});
+    vs.push_back({"flat_1chunk_nt", 2, [&] { k_flat<true><<<flat((n + 255) / 256), 256>>>(a, b, n); }, {}});
+    vs.push_back({"flat_2chunk", 2, [&] { k_flatU<2, false><<<flat((n + 511) / 512), 256>>>(a, b, n); }, {}});
+    vs.push_back({"flat_4chunk", 2, [&] { k_flatU<4, false><<<flat((n + 1023) / 1024), 256>>>(a, b, n); }, {}});
+    vs.push_back({"flat_4chunk_nt", 2, [&] { k_flatU<4, true><<<flat((n + 1023) / 1024), 256>>>(a, b, n); }, {}});
+    for (int blocks : {1024, 2048, 4096, 8192}) {
+      vs.push_back({"gs_U1_b" + std::to_string(blocks), 2, [&, blocks] { k_gs<1, false><<<blocks, 256>>>(a, b, n); }, {}});
+      vs.push_back({"gs_U2_b" + std::to_string(blocks), 2, [&, blocks] { k_gs<2, false><<<blocks, 256>>>(a, b, n); }, {}});
+      vs.push_back({"gs_U4_b" + std::to_string(blocks), 2, [&, blocks] { k_gs<4, false><<<blocks, 256>>>(a, b, n); }, {}});
+      vs.push_back({"gs_U2nt_b" + std::to_string(blocks), 2, [&, blocks] { k_gs<2, true><<<blocks, 256>>>(a, b, n); }, {}});
+    }
+    vs.push_back({"memcpy_d2d", 2, [&] { hipMemcpyAsync(b, a, bytes, hipMemcpyDeviceToDevice, 0); }, {}});
+    vs.push_back({"read_only", 1, [&] { k_read<<<4096, 256>>>(a, n, sink); }, {}});
+    vs.push_back({"write_only", 1, [&] { k_write<<<uint32_t((n + 255) / 256), 256>>>(b, n); }, {}});
+    for (auto &v : vs) for (int w = 0; w < 2; ++w) v.go();
+    hipDeviceSynchronize();
+    for (int rep = 0; rep < 15; ++rep)
+      for (auto &v : vs) {
+        hipEventRecord(e0, 0);
+        v.go();
+        hipEventRecord(e1, 0);
+        hipEventSynchronize(e1);
+        float ms;
+        hipEventElapsedTime(&ms, e0, e1);
+        v.t.push_back(ms);
+      }
+    printf("== %lu MiB per buffer ==\n", (unsigned long)mib);
+    for (auto &v : vs) {
+      std::sort(v.t.begin(), v.t.end());
+      const double med = v.t[v.t.size() / 2], best = v.t[0];
+      printf("%-18s median %8.3f ms  %6.3f TB/s   best %6.3f TB/s\n", v.name.c_str(), med,
+             v.mult * bytes / (med * 1e-3) / 1e12, v.mult * bytes / (best * 1e-3) / 1e12);
+    }
+    fflush(stdout);
+  }
+  if (hipGetLastError() != hipSuccess) { printf("hip error\n"); return 1; }
+  return 0;
+}

@@ -19,7 +19,8 @@ F_VALIDATE = 1
 F_DEFAULT = 2
 F_POINTER = 4
 F_SUB = 8
-SUB_FRAMES = 32  # XDRG_SUB_FRAMES
+SUB_FRAMES = 32  # XDRG_SUB_FRAMES (private frames of the element-subroutine walks)
+MAX_FRAMES = 1 << 19  # XDRG_MAX_FRAMES
 
 PATH_FIXED_REG, PATH_FIXED_LDS, PATH_VAR = 1, 2, 3
 
@@ -55,7 +56,9 @@ ERR_INTERNAL = 19
 ERR_INDEX_LONG = 20
 
 MARK_LAST = 0x80000000  # XDRG_MARK_LAST: last-fragment bit of a record mark
-INDEX_MAX_MSG = 16380   # XDRG_INDEX_MAX_MSG
+INDEX_MAX_MSG = 16380   # XDRG_INDEX_MAX_MSG (one list-ranking window)
+MAX_MSG = 0x7FFFFFFF    # XDRG_MAX_MSG
+MSG_SOCK_MAXMSGLEN = 0x100000  # msg_sock::default_maxmsglen, xdrpp/msgsock.h:29
 
 XDR_MAX_LEN = 0xFFFFFFFC  # xdrpp/types.h:360
 DEFAULT_STACK_LIMIT = 0xFFFFFFFF  # xdrpp/marshal.cc:6

@@ -587,7 +587,7 @@ struct gen {
         line("const uint32_t cnt = bswap32(c.word());");
         line("if (cnt > " + u32(e.arg0) + ") return c.fail(" + P + ", " +
              ((e.flags & XDRG_F_POINTER) ? "XDRG_ERR_POINTER_BOUND" : "XDRG_ERR_XVECTOR_BOUND") + ");");
-        line("c.ecur = (c.ecur + 7u) & ~7ull;");
+        line("if (!c.area(" + P + ", cnt, " + u32(e.arg1) + ", " + u32(e.arg3) + ")) return false;");
         line("*reinterpret_cast<uint64_t *>(" + f + ") = c.ecur;");
         line("st32(" + f + " + 8, cnt);");
         line("uint32_t i = 0;");

@@ -66,6 +66,20 @@ __device__ __forceinline__ uint32_t unaligned_word(const uint8_t *p, uint64_t le
   const uint32_t hi = (a + 8 <= len) ? ld32(p + a + 4) : partial_word(p, len, a + 4);
   return __builtin_amdgcn_alignbyte(hi, lo, sh);
 }
+// Decode: the element area of one container of `cnt` inline elements of
+// `stride` native and `wire` wire bytes, `rem` wire bytes left after its
+// count.  Aligns the bump pointer to 8 and checks that the elements the
+// bytes left can reach (the ones before the first that runs out, and that
+// one) fit before `eend`.  Valid data always fits (the heap factor,
+// xdrg_decode_heap_size); a forged count in a truncated record fails here
+// with xdr_overflow, the error the reference raises at the element that
+// runs out, instead of writing past the record's area.
+__device__ __forceinline__ bool elem_area_ok(uint64_t &ecur, uint64_t eend, uint32_t cnt, uint32_t stride,
+                                             uint32_t wire, uint64_t rem) {
+  ecur = (ecur + 7u) & ~7ull;
+  const uint64_t reach = min(static_cast<uint64_t>(cnt), rem / wire + 1) * stride;
+  return ecur <= eend && reach <= eend - ecur;
+}
 __device__ __forceinline__ uint32_t keep_mask(uint32_t nbytes) {  // nbytes in 1..4
   return nbytes >= 4 ? 0xffffffffu : ((1u << (8u * nbytes)) - 1u);
 }

@@ -364,6 +364,43 @@ int compile_plan(xdrg_plan &p) {
         if (minw[op.arg4] < 4) return XDRG_EUNSUPPORTED;
         op.arg3 = uint32_t(std::min<uint64_t>(minw[op.arg4], 0xffffffffu));  // least element wire bytes
       }
+    // Nesting of element subroutines: frames[r] = the most frames a walk
+    // that enters region r can open below it (UINT32_MAX: a region that can
+    // enter itself, i.e. a recursive type).  Past XDRG_SUB_FRAMES the frame
+    // walks need their deep passes.
+    {
+      const uint32_t nreg = uint32_t(R.end.size());
+      std::vector<uint32_t> frames(nreg, 0);
+      std::vector<uint8_t> state(nreg, 0);  // 0 new, 1 on the DFS path, 2 done
+      std::vector<std::pair<uint32_t, uint32_t>> stk;  // (region, next op to look at)
+      stk.push_back({0, 0});
+      state[0] = 1;
+      while (!stk.empty()) {
+        auto &top = stk.back();
+        const uint32_t reg = top.first, first = reg ? R.end[reg - 1] + 1 : 0;
+        uint32_t i = std::max(top.second, first);
+        bool pushed = false;
+        for (; i < R.end[reg]; ++i) {
+          const xdrg_op &op = p.ops[i];
+          if (op.kind != XDRG_OP_VECTOR || !(op.flags & XDRG_F_SUB)) continue;
+          const uint32_t body = R.id[op.arg4];
+          if (state[body] == 1) { frames[reg] = UINT32_MAX; continue; }
+          if (state[body] == 0) {
+            top.second = i;
+            state[body] = 1;
+            stk.push_back({body, 0});
+            pushed = true;
+            break;
+          }
+          const uint32_t f = frames[body] == UINT32_MAX ? UINT32_MAX : frames[body] + 1;
+          frames[reg] = std::max(frames[reg], f);
+        }
+        if (pushed) continue;
+        state[reg] = 2;
+        stk.pop_back();
+      }
+      p.deep = frames[0] > XDRG_SUB_FRAMES;
+    }
     p.max_chunks16 = chunks[0];
     p.max_var_slots = slots[0];
     p.max_scalar_words = words[0];

@@ -5,11 +5,11 @@
 // :476-512, :591-665) archives each element with xdr_traits<T>::save/load,
 // which for a struct or union walks its fields (xdrc/gen_hh.cc:212-250,
 // :575-675) -- and T may contain the container again (test_recursive,
-// tests/xdrtest.x:29-33).  The plan gives such an element a subroutine: ops
-// after the record's END, entered once per element.  These kernels walk
-// one record per lane with an explicit stack of element frames (the
-// reference recurses on the C++ stack; marshal.h:129-136, :198-205 count
-// its levels):
+// tests/xdrtest.x:29-33; rpcbind's rp__list, xdrpp/rpcb_prot.x:34).  The
+// plan gives such an element a subroutine: ops after the record's END,
+// entered once per element.  These kernels walk one record per lane with an
+// explicit stack of element frames (the reference recurses on the C++
+// stack; marshal.h:129-136, :198-205 count its levels):
 //
 //   k_sub_size     xdr_size per record (+ depth_checker levels) and the
 //                  64-record block sums;
@@ -17,27 +17,75 @@
 //   k_sub_decode   xdr_generic_get (marshal.h:142-211); decoded element
 //                  arrays are carved from the record's element area.
 //
+// Nesting is bounded only by the data (and marshaling_stack_limit).  Each
+// kernel runs as up to three passes over the same walk:
+//   main   one lane per record, kSubFrames frames in private memory; a
+//          record that needs more is appended to list A and left alone;
+//   deep A a fixed grid of kDeepLanesA lanes walks list A, kDeepSlabA frames
+//          per lane in the frame pool (global memory); a record that needs
+//          more goes to list B;
+//   deep B kDeepLanesB lanes walk list B with kDeepSlabB frames each; a
+//          record that needs more is xdr_stack_overflow at the VECTOR op
+//          that would open the frame (the reference's own recursion ends in
+//          a segmentation fault far earlier: xdr_from_opaque of a
+//          test_recursive chain between 60K and 100K levels, xdr_to_opaque
+//          between 100K and 200K, g++ -O2 on an 8 MiB stack).
+// The encode pass reuses the lists its size pass built (the two walks visit
+// the same frames), so it defers nothing itself.  A deferred record is
+// walked again from its start by the next pass: every write it makes is
+// deterministic, so the main pass's partial output is simply overwritten.
+//
 // A body's field offsets are element-relative and its depths relative to
-// the VECTOR op that entered it (frame.dbase).  Fixed-size element
-// containers inside a body keep the inline element walk of xdrgpu.hip.
+// the VECTOR op that entered it.  Fixed-size element containers inside a
+// body keep the inline element walk of xdrgpu.hip.
 //
 // Included by xdrgpu.hip after its element helpers (load_ops, union_target,
 // enc_vector_elems, dec_vector_elems).
 #pragma once
 
-constexpr uint32_t kSubFrames = XDRG_SUB_FRAMES;
+constexpr uint32_t kSubFrames = XDRG_SUB_FRAMES;  // private frames of the main pass
 constexpr uint32_t kReported = 0x100;  // decode: the element walk reported the error
 
+// One open container: its current element (heap byte offset), the elements
+// after it and the VECTOR op (stride, body pc, return pc and depth come
+// from the op).
 struct sub_frame {
-  uint64_t eb;     // current element: byte offset in the heap
-  uint8_t *ref;    // decode: the container's native xdrg_bytes_ref
-  uint32_t left;   // elements after the current one
-  uint32_t cnt;
-  uint32_t stride;
-  uint32_t entry;  // body pc
-  uint32_t ret;    // pc after the VECTOR op
-  uint32_t dbase;  // absolute depth of the VECTOR op
+  uint64_t eb;
+  uint32_t left;
+  uint32_t vpc;
 };
+
+struct priv_stack {
+  sub_frame f[kSubFrames];
+  __device__ __forceinline__ sub_frame &operator[](uint32_t i) { return f[i]; }
+  __device__ __forceinline__ uint32_t cap() const { return kSubFrames; }
+};
+struct slab_stack {
+  sub_frame *f;
+  uint32_t n;
+  __device__ __forceinline__ sub_frame &operator[](uint32_t i) { return f[i]; }
+  __device__ __forceinline__ uint32_t cap() const { return n; }
+};
+
+// The pass a launch runs (see the top of the file).
+struct sub_pass {
+  const uint32_t *list;            // deep: the records to walk (nullptr: main pass, every record)
+  const unsigned long long *count; //       and their number
+  uint32_t *defer;                 // where records that need more frames go (nullptr: see last)
+  unsigned long long *defer_count;
+  sub_frame *slabs;                // deep: `slab` frames per lane
+  uint32_t slab;
+  uint32_t last;                   // 1: running out of frames is xdr_stack_overflow
+};
+
+enum : int { kWalkOk = 0, kWalkErr = 1, kWalkFull = 2 };
+
+// A running out of frames: defer the record to the next pass, or report.
+__device__ __forceinline__ void sub_full(const sub_pass &P, uint64_t r, uint32_t pc, uint32_t code,
+                                         unsigned long long *err) {
+  if (P.defer) P.defer[atomicAdd(P.defer_count, 1ull)] = static_cast<uint32_t>(r);
+  else if (P.last) report(err, r, pc, code);
+}
 
 // The native object a lane's walk is in: its record (frame 0, `len` bytes)
 // or an element in the heap.  Heap bytes at or past heap_len read as 0.
@@ -67,43 +115,57 @@ struct sub_src {
 // Pop finished elements: returns false when the record's own END is
 // reached, else sets pc (and the walk's object and depth) to the next
 // element's body or the op after the container.
-__device__ __forceinline__ bool sub_next(sub_frame *st, uint32_t &fp, uint32_t &pc, uint32_t &dbase,
-                                         uint64_t &eb, bool &in_heap) {
+template <class ST>
+__device__ __forceinline__ bool sub_next(const xdrg_op *__restrict__ ops, ST &st, uint32_t &fp, uint32_t &pc,
+                                         uint32_t &dbase, uint64_t &eb, bool &in_heap) {
   if (!fp) return false;
   sub_frame &f = st[fp - 1];
+  const xdrg_op &v = ops[f.vpc];
   if (f.left) {
     --f.left;
-    f.eb += f.stride;
+    f.eb += v.arg1;
     eb = f.eb;
-    pc = f.entry;
+    pc = v.arg4;
     return true;
   }
-  pc = f.ret;
-  if (--fp) {
-    eb = st[fp - 1].eb;
-    dbase = st[fp - 1].dbase;
-  } else {
-    in_heap = false;
-    dbase = 0;
-  }
+  pc = f.vpc + 1;
+  dbase -= v.depth;
+  if (--fp) eb = st[fp - 1].eb;
+  else in_heap = false;
   return true;
+}
+
+// The walk of one record for a pass: the main pass walks record gid, a
+// deep pass every listed record its lane owns.
+template <class F>
+__device__ __forceinline__ void sub_records(const sub_pass &P, uint64_t n, F &&walk) {
+  const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (!P.list) {
+    if (gid < n) {
+      priv_stack st;
+      walk(gid, st);
+    }
+    return;
+  }
+  const uint64_t cnt = *P.count, lanes = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  slab_stack st{P.slabs + gid * P.slab, P.slab};
+  for (uint64_t i = gid; i < cnt; i += lanes) walk(static_cast<uint64_t>(P.list[i]), st);
 }
 
 // ---------------------------------------------------------------- size
 // xdr_size (xdr_traits<T>::serial_size) of one record, and with DEPTH the
 // deepest class/container level its walk enters (depth_checker,
-// xdrpp/depth_checker.h:41-54).  On failure returns false with the op and
-// code: a bad discriminant, a record of 2^31 bytes or more, or data nested
-// deeper than kSubFrames element frames.
-template <bool DEPTH>
-__device__ bool sub_size(const xdrg_op *__restrict__ ops, const uint32_t *__restrict__ table,
-                         sub_src src, uint64_t &s, uint32_t &dmax, uint32_t &bad_op, uint32_t &code) {
-  sub_frame st[kSubFrames];
+// xdrpp/depth_checker.h:41-54).  kWalkErr with the op and code: a bad
+// discriminant or a record of 2^31 bytes or more; kWalkFull (op in bad_op):
+// the stack ran out.
+template <bool DEPTH, class ST>
+__device__ int sub_size(const xdrg_op *__restrict__ ops, const uint32_t *__restrict__ table, sub_src src,
+                        uint64_t &s, uint32_t &dmax, uint32_t &bad_op, uint32_t &code, ST &st) {
   uint32_t fp = 0, pc = 0, dbase = 0;
   for (;;) {
     const xdrg_op &op = ops[pc];
     if (op.kind == XDRG_OP_END) {
-      if (!sub_next(st, fp, pc, dbase, src.eb, src.in_heap)) return true;
+      if (!sub_next(ops, st, fp, pc, dbase, src.eb, src.in_heap)) return kWalkOk;
       continue;
     }
     if (op.kind == XDRG_OP_JUMP) { pc = op.arg0; continue; }
@@ -118,7 +180,7 @@ __device__ bool sub_size(const xdrg_op *__restrict__ ops, const uint32_t *__rest
     case XDRG_OP_UNION: {
       const int t = union_target(op, table, src.w(op.noff));
       s += 4;
-      if (t < 0) { bad_op = pc; code = XDRG_ERR_BAD_DISCRIMINANT; return false; }
+      if (t < 0) { bad_op = pc; code = XDRG_ERR_BAD_DISCRIMINANT; return kWalkErr; }
       pc = static_cast<uint32_t>(t);
       break;
     }
@@ -133,9 +195,9 @@ __device__ bool sub_size(const xdrg_op *__restrict__ ops, const uint32_t *__rest
         break;
       }
       if (!cnt) { ++pc; break; }
-      if (fp == kSubFrames) { bad_op = pc; code = XDRG_ERR_STACK_PUT; return false; }
+      if (fp == st.cap()) { bad_op = pc; return kWalkFull; }
       dbase += op.depth;
-      st[fp++] = sub_frame{src.w64(op.noff), nullptr, cnt - 1, cnt, op.arg1, op.arg4, pc + 1, dbase};
+      st[fp++] = sub_frame{src.w64(op.noff), cnt - 1, pc};
       src.eb = st[fp - 1].eb;
       src.in_heap = true;
       pc = op.arg4;
@@ -143,7 +205,9 @@ __device__ bool sub_size(const xdrg_op *__restrict__ ops, const uint32_t *__rest
     }
     default: s += 4; ++pc; break;
     }
-    if (s >= kSizeErr) { bad_op = 0; code = XDRG_ERR_OVERFLOW_PUT; return false; }
+    // every frame adds a count word, so a walk that never ends (a cycle in
+    // the staged heap) fails here or at its last frame
+    if (s >= kSizeErr) { bad_op = 0; code = XDRG_ERR_OVERFLOW_PUT; return kWalkErr; }
   }
 }
 
@@ -152,25 +216,31 @@ __global__ __launch_bounds__(256) void k_sub_size(
     const uint8_t *__restrict__ native, uint64_t n, uint32_t stride, const uint8_t *__restrict__ heap,
     uint64_t heap_len, const xdrg_op *__restrict__ ops, uint32_t nops, const uint32_t *__restrict__ table,
     uint32_t *__restrict__ sizes, unsigned long long *__restrict__ block_sums, uint32_t mark,
-    unsigned long long *err, uint32_t *__restrict__ depths) {
+    unsigned long long *err, uint32_t *__restrict__ depths, sub_pass P) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   xdrg_op *sops = reinterpret_cast<xdrg_op *>(smem);
   load_ops(sops, ops, nops);
-  const uint64_t r = static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x;
-  uint32_t size = 0;
-  if (r < n) {
+  uint32_t size = 0;  // main pass: this lane's contribution to its block sum
+  sub_records(P, n, [&](uint64_t r, auto &st) {
     const sub_src src{native + r * stride, stride, heap, heap_len, 0, false};
     uint64_t s = mark;
-    uint32_t dmax = 0, bad_op = 0, code = 0;
-    if (sub_size<DEPTH>(sops, table, src, s, dmax, bad_op, code)) {
-      size = static_cast<uint32_t>(s);
-    } else {
+    uint32_t dmax = 0, bad_op = 0, code = 0, sz = kSizeErr;
+    const int rc = sub_size<DEPTH>(sops, table, src, s, dmax, bad_op, code, st);
+    if (rc == kWalkOk) {
+      sz = static_cast<uint32_t>(s);
+    } else if (rc == kWalkErr) {
       report(err, r, bad_op, code);
-      size = kSizeErr;
+    } else {  // the stack ran out
+      sub_full(P, r, bad_op, XDRG_ERR_STACK_PUT, err);
+      if (!P.last) return;  // the next pass sizes it
     }
-    if (sizes) sizes[r] = size;
+    if (sizes) sizes[r] = sz;
     if (DEPTH) depths[r] = dmax;
-  }
+    if (!P.list) size = sz;
+    else if (block_sums && !(sz & kSizeErr)) atomicAdd(&block_sums[r / 64u], static_cast<unsigned long long>(sz));
+  });
+  if (P.list) return;
+  const uint64_t r = static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x;
   unsigned long long v = (size & kSizeErr) ? 0ull : size;
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   const uint64_t blk = r / 64u;
@@ -178,49 +248,31 @@ __global__ __launch_bounds__(256) void k_sub_size(
 }
 
 // -------------------------------------------------------------- encode
-// Record offsets as k_var_encode computes them (block-local scan on top of
-// the 64-record block bases), then the record's walk with check(n) and the
-// stack budget before every field (marshal.h:104-108, :129-136).
-__global__ __launch_bounds__(256) void k_sub_encode(
-    const uint8_t *__restrict__ native, uint64_t n, uint32_t stride, const uint8_t *__restrict__ heap,
-    uint64_t heap_len, uint8_t *__restrict__ xdr, uint64_t cap, uint64_t *__restrict__ offsets,
-    const uint32_t *__restrict__ sizes, const unsigned long long *__restrict__ block_base,
-    const xdrg_op *__restrict__ ops, uint32_t nops, const uint32_t *__restrict__ table,
-    uint32_t stack_limit, uint32_t mark, unsigned long long *err) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  xdrg_op *sops = reinterpret_cast<xdrg_op *>(smem);
-  load_ops(sops, ops, nops);
-  const uint64_t r = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  const uint32_t sz = r < n ? sizes[r] : 0u;
-  const unsigned long long v = (sz & kSizeErr) ? 0ull : sz;
-  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  unsigned long long incl = v;
-  for (int o = 1; o < 64; o <<= 1) {
-    const unsigned long long x = __shfl_up(incl, o, 64);
-    if (lane >= static_cast<uint32_t>(o)) incl += x;
-  }
-  if (r >= n) return;
-  const uint64_t off = block_base[blockIdx.x * 4u + wid] + incl - v;
-  offsets[r] = off;
-  if (sz & kSizeErr) return;  // the size pass reported this record
-
-  sub_src src{native + r * stride, stride, heap, heap_len, 0, false};
+// The record's walk from stream offset `off` with check(n) and the stack
+// budget before every field (marshal.h:104-108, :129-136).  Errors are
+// reported; kWalkFull when the stack ran out (op in *full_op).
+template <class ST>
+__device__ int sub_encode_rec(const xdrg_op *__restrict__ sops, const uint32_t *__restrict__ table, sub_src src,
+                              uint8_t *__restrict__ xdr, uint64_t cap, uint64_t off, uint32_t sz, uint32_t mark,
+                              uint32_t stack_limit, uint64_t r, unsigned long long *err, uint32_t *full_op,
+                              ST &st) {
+  const uint8_t *heap = src.heap;
+  const uint64_t heap_len = src.heap_len;
   uint64_t pos = off;
   if (mark) {  // the message's record mark (message_t::alloc, marshal.cc:15-31)
-    if (4 > cap - min(pos, cap)) { report(err, r, kOpRecordLevel, XDRG_ERR_OVERFLOW_PUT); return; }
+    if (4 > cap - min(pos, cap)) { report(err, r, kOpRecordLevel, XDRG_ERR_OVERFLOW_PUT); return kWalkErr; }
     st32(xdr + pos, mark_word(sz - 4u));
     pos += 4;
   }
-  sub_frame st[kSubFrames];
   uint32_t fp = 0, pc = 0, dbase = 0;
   for (;;) {
     const xdrg_op &op = sops[pc];
     if (op.kind == XDRG_OP_END) {
-      if (!sub_next(st, fp, pc, dbase, src.eb, src.in_heap)) break;
+      if (!sub_next(sops, st, fp, pc, dbase, src.eb, src.in_heap)) return kWalkOk;
       continue;
     }
     if (op.kind == XDRG_OP_JUMP) { pc = op.arg0; continue; }
-    if (dbase + op.depth > stack_limit) { report(err, r, pc, XDRG_ERR_STACK_PUT); return; }
+    if (dbase + op.depth > stack_limit) { report(err, r, pc, XDRG_ERR_STACK_PUT); return kWalkErr; }
     uint64_t need = 4;
     uint32_t len = 0;
     if (op.kind == XDRG_OP_U64) need = 8;
@@ -229,7 +281,7 @@ __global__ __launch_bounds__(256) void k_sub_encode(
       len = src.w(op.noff + 8);
       need = 4ull + len;
     }
-    if (need > cap - min(pos, cap)) { report(err, r, pc, XDRG_ERR_OVERFLOW_PUT); return; }
+    if (need > cap - min(pos, cap)) { report(err, r, pc, XDRG_ERR_OVERFLOW_PUT); return kWalkErr; }
     uint32_t *o = reinterpret_cast<uint32_t *>(xdr + pos);
     switch (op.kind) {
     case XDRG_OP_U32: case XDRG_OP_ENUM: o[0] = bswap32(src.w(op.noff)); pos += 4; ++pc; break;
@@ -281,14 +333,14 @@ __global__ __launch_bounds__(256) void k_sub_encode(
         auto put = [&](uint32_t a, uint32_t w) { st32(xdr + off + a, w); };
         if (!enc_vector_elems(sops, pc + 1, op.arg2, heap, heap_len, eoff, cnt, op.arg1, pos, cap, at,
                               stack_limit - dbase, r, err, put))
-          return;
+          return kWalkErr;
         pc += 1 + op.arg2;
         break;
       }
       if (!cnt) { ++pc; break; }
-      if (fp == kSubFrames) { report(err, r, pc, XDRG_ERR_STACK_PUT); return; }
+      if (fp == st.cap()) { *full_op = pc; return kWalkFull; }
       dbase += op.depth;
-      st[fp++] = sub_frame{eoff, nullptr, cnt - 1, cnt, op.arg1, op.arg4, pc + 1, dbase};
+      st[fp++] = sub_frame{eoff, cnt - 1, pc};
       src.eb = eoff;
       src.in_heap = true;
       pc = op.arg4;
@@ -299,45 +351,67 @@ __global__ __launch_bounds__(256) void k_sub_encode(
   }
 }
 
-// -------------------------------------------------------------- decode
-// Record r = xdr_from_opaque(stream[off[r], off[r+1]), r) with check(n)
-// before every read; the native record and every element array are
-// zero-filled first.  Payloads stay in the stream (heap_out holds it at
-// [0, len)); element arrays come from the record's element area
-// [ebase + F*off[r], ebase + F*off[r+1]) at 8-byte alignment.  On a failure
-// inside elements, each open container's rsv holds 1 + the index of the
-// element that failed, the others 0 (the unstager follows these marks).
-__global__ __launch_bounds__(256) void k_sub_decode(
-    const uint8_t *__restrict__ xdr, uint64_t len, const uint64_t *__restrict__ offsets, uint64_t n,
-    uint8_t *__restrict__ native, uint32_t stride, const xdrg_op *__restrict__ ops, uint32_t nops,
-    const uint32_t *__restrict__ table, uint32_t stack_limit, uint8_t *__restrict__ heap,
-    uint64_t ebase, uint32_t F, uint32_t mark, unsigned long long *err) {
+// Record offsets as k_var_encode computes them (block-local scan on top of
+// the 64-record block bases); a deep pass reads them back.
+__global__ __launch_bounds__(256) void k_sub_encode(
+    const uint8_t *__restrict__ native, uint64_t n, uint32_t stride, const uint8_t *__restrict__ heap,
+    uint64_t heap_len, uint8_t *__restrict__ xdr, uint64_t cap, uint64_t *__restrict__ offsets,
+    const uint32_t *__restrict__ sizes, const unsigned long long *__restrict__ block_base,
+    const xdrg_op *__restrict__ ops, uint32_t nops, const uint32_t *__restrict__ table,
+    uint32_t stack_limit, uint32_t mark, unsigned long long *err, sub_pass P) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   xdrg_op *sops = reinterpret_cast<xdrg_op *>(smem);
   load_ops(sops, ops, nops);
-  const uint64_t r = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (r >= n) return;
-  const uint64_t a = offsets[r], b = offsets[r + 1];
-  if (r == n - 1 && b != len) report(err, n, kOpRecordLevel, XDRG_ERR_TRAILING);
-  if (b < a || b > len) { report(err, r, 0, XDRG_ERR_OVERFLOW_GET); return; }
-  if (mark) {  // xdr_from_msg: the message read_message framed (srpc.cc:29-55)
-    const uint32_t c = b - a < 4 ? XDRG_ERR_MSG_EOF : mark_code(ld32(xdr + a), b - a - 4);
-    if (c) { report(err, r, kOpRecordLevel, c); return; }
+  uint64_t off = 0;
+  if (!P.list) {
+    const uint64_t r = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const uint32_t sz = r < n ? sizes[r] : 0u;
+    const unsigned long long v = (sz & kSizeErr) ? 0ull : sz;
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    unsigned long long incl = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned long long x = __shfl_up(incl, o, 64);
+      if (lane >= static_cast<uint32_t>(o)) incl += x;
+    }
+    if (r >= n) return;
+    off = block_base[blockIdx.x * 4u + wid] + incl - v;
+    offsets[r] = off;
   }
-  if ((b - a) & 3u) { report(err, r, kOpRecordLevel, XDRG_ERR_SIZE_NOT_MULT4); return; }
-  uint8_t *const rec = native + r * stride;
+  sub_records(P, n, [&](uint64_t r, auto &st) {
+    const uint32_t sz = sizes[r];
+    if (sz & kSizeErr) return;  // the size pass reported this record
+    const uint64_t o = P.list ? offsets[r] : off;
+    const sub_src src{native + r * stride, stride, heap, heap_len, 0, false};
+    uint32_t full_op = 0;
+    if (sub_encode_rec(sops, table, src, xdr, cap, o, sz, mark, stack_limit, r, err, &full_op, st) == kWalkFull)
+      sub_full(P, r, full_op, XDRG_ERR_STACK_PUT, err);
+  });
+}
+
+// -------------------------------------------------------------- decode
+// Record r = xdr_from_opaque(stream[a, b), r) with check(n) before every
+// read; the native record and every element array are zero-filled first.
+// Payloads stay in the stream (heap_out holds it at [0, len)); element
+// arrays come from the record's element area [ecur, eend) at 8-byte
+// alignment.  On a failure inside elements, each open container's rsv
+// holds 1 + the index of the element that failed, the others 0 (the
+// unstager follows these marks).  kWalkFull: the stack ran out (op in
+// *full_op), nothing reported.
+template <class ST>
+__device__ int sub_decode_rec(const xdrg_op *__restrict__ sops, const uint32_t *__restrict__ table,
+                              const uint8_t *__restrict__ xdr, uint64_t a, uint64_t b, uint8_t *__restrict__ rec,
+                              uint32_t stride, uint8_t *__restrict__ heap, uint64_t ecur, uint64_t eend,
+                              uint32_t stack_limit, uint64_t r, unsigned long long *err, uint32_t *full_op,
+                              ST &st) {
   for (uint32_t k = 0; k < stride / 4; ++k) st32(rec + 4 * k, 0u);
-  uint64_t p = a + mark;
-  uint64_t ecur = ebase + static_cast<uint64_t>(F) * a;
-  const uint64_t eend = ebase + static_cast<uint64_t>(F) * b;
-  sub_frame st[kSubFrames];
+  uint64_t p = a;
   uint32_t fp = 0, pc = 0, dbase = 0, code = 0;
   uint64_t eb = 0;
   bool in_heap = false;
   for (;;) {
     const xdrg_op &op = sops[pc];
     if (op.kind == XDRG_OP_END) {
-      if (!sub_next(st, fp, pc, dbase, eb, in_heap)) break;
+      if (!sub_next(sops, st, fp, pc, dbase, eb, in_heap)) break;
       continue;
     }
     if (op.kind == XDRG_OP_JUMP) { pc = op.arg0; continue; }
@@ -401,7 +475,25 @@ __global__ __launch_bounds__(256) void k_sub_decode(
         code = (op.flags & XDRG_F_POINTER) ? XDRG_ERR_POINTER_BOUND : XDRG_ERR_XVECTOR_BOUND;
         break;
       }
+      // Element area.  Valid data never overruns it (distinct elements
+      // start at distinct wire words, include/xdrgpu.h heap factor); a
+      // forged count could, so every reservation is checked.  Every element
+      // takes at least arg3 wire bytes (the inline element size, or the
+      // least an element subroutine consumes): an element subroutine's count
+      // the bytes left cannot hold fails here, before any area is reserved,
+      // with the xdr_overflow the reference raises at the element that runs
+      // out; inline elements fail at that element, so only the ones that
+      // can be reached are reserved.
+      const uint64_t bytes = static_cast<uint64_t>(cnt) * op.arg1;
+      const uint64_t reach = (op.flags & XDRG_F_SUB)
+                                 ? bytes
+                                 : min(static_cast<uint64_t>(cnt), (b - p) / op.arg3 + 1) * op.arg1;
       ecur = (ecur + 7u) & ~7ull;
+      if (((op.flags & XDRG_F_SUB) && static_cast<uint64_t>(cnt) * op.arg3 > b - p) || ecur > eend ||
+          reach > eend - ecur) {
+        code = XDRG_ERR_OVERFLOW_GET;
+        break;
+      }
       *reinterpret_cast<uint64_t *>(nat + op.noff) = ecur;
       st32(nat + op.noff + 8, cnt);
       if (!(op.flags & XDRG_F_SUB)) {
@@ -411,22 +503,17 @@ __global__ __launch_bounds__(256) void k_sub_decode(
           code = kReported;
           break;
         }
-        ecur += static_cast<uint64_t>(cnt) * op.arg1;
+        ecur += bytes;
         pc += 1 + op.arg2;
         break;
       }
       if (!cnt) { ++pc; break; }
-      // Valid data never overruns the area (distinct elements start at
-      // distinct wire words); a count the record cannot hold may, and
-      // fails here rather than at the element that runs out of bytes.
-      const uint64_t bytes = static_cast<uint64_t>(cnt) * op.arg1;
-      if (bytes > eend - ecur) { code = XDRG_ERR_OVERFLOW_GET; break; }
-      if (fp == kSubFrames) { code = XDRG_ERR_STACK_GET; break; }
+      if (fp == st.cap()) { *full_op = pc; return kWalkFull; }
       uint8_t *arr = heap + ecur;
       for (uint64_t z = 0; z < (bytes & ~3ull); z += 4) st32(arr + z, 0u);
       for (uint64_t z = bytes & ~3ull; z < bytes; ++z) arr[z] = 0;
       dbase += op.depth;
-      st[fp++] = sub_frame{ecur, nat + op.noff, cnt - 1, cnt, op.arg1, op.arg4, pc + 1, dbase};
+      st[fp++] = sub_frame{ecur, cnt - 1, pc};
       eb = ecur;
       in_heap = true;
       ecur += bytes;
@@ -439,8 +526,41 @@ __global__ __launch_bounds__(256) void k_sub_decode(
   }
   if (code) {
     if (code != kReported) report(err, r, pc, code);
-    for (uint32_t k = 0; k < fp; ++k) st32(st[k].ref + 12, st[k].cnt - st[k].left);  // 1 + element
-    return;
+    // 1 + the failing element in every open container: the container's ref
+    // sits in the object that encloses it (the record, or the frame below)
+    for (uint32_t k = 0; k < fp; ++k) {
+      uint8_t *ref = (k ? heap + st[k - 1].eb : rec) + sops[st[k].vpc].noff;
+      st32(ref + 12, ld32(ref + 8) - st[k].left);
+    }
+    return kWalkErr;
   }
   if (p != b) report(err, r, kOpRecordLevel, XDRG_ERR_TRAILING);
+  return kWalkOk;
+}
+
+__global__ __launch_bounds__(256) void k_sub_decode(
+    const uint8_t *__restrict__ xdr, uint64_t len, const uint64_t *__restrict__ offsets, uint64_t n,
+    uint8_t *__restrict__ native, uint32_t stride, const xdrg_op *__restrict__ ops, uint32_t nops,
+    const uint32_t *__restrict__ table, uint32_t stack_limit, uint8_t *__restrict__ heap,
+    uint64_t ebase, uint32_t F, uint32_t mark, unsigned long long *err, sub_pass P) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  xdrg_op *sops = reinterpret_cast<xdrg_op *>(smem);
+  load_ops(sops, ops, nops);
+  sub_records(P, n, [&](uint64_t r, auto &st) {
+    const uint64_t a = offsets[r], b = offsets[r + 1];
+    if (!P.list) {  // record-level checks: the main pass reports them once
+      if (r == n - 1 && b != len) report(err, n, kOpRecordLevel, XDRG_ERR_TRAILING);
+      if (b < a || b > len) { report(err, r, 0, XDRG_ERR_OVERFLOW_GET); return; }
+      if (mark) {  // xdr_from_msg: the message read_message framed (srpc.cc:29-55)
+        const uint32_t c = b - a < 4 ? XDRG_ERR_MSG_EOF : mark_code(ld32(xdr + a), b - a - 4);
+        if (c) { report(err, r, kOpRecordLevel, c); return; }
+      }
+      if ((b - a) & 3u) { report(err, r, kOpRecordLevel, XDRG_ERR_SIZE_NOT_MULT4); return; }
+    }
+    uint32_t full_op = 0;
+    if (sub_decode_rec(sops, table, xdr, a + mark, b, native + r * stride, stride, heap,
+                       ebase + static_cast<uint64_t>(F) * a, ebase + static_cast<uint64_t>(F) * b, stack_limit, r,
+                       err, &full_op, st) == kWalkFull)
+      sub_full(P, r, full_op, XDRG_ERR_STACK_GET, err);
+  });
 }

@@ -551,8 +551,8 @@ struct dec_ctx {
   uint32_t stack_limit;
   uint64_t r;
   unsigned long long *err;
-  uint8_t *heap;  // decoded heap (element arrays live at ecur)
-  uint64_t ecur;
+  uint8_t *heap;  // decoded heap (element arrays live at [ecur, eend))
+  uint64_t ecur, eend;
 
   // stack budget, then check(n) of xdr_generic_get (marshal.h:166-170)
   __device__ __forceinline__ bool field(uint32_t op, uint32_t depth, uint64_t need) {
@@ -575,6 +575,11 @@ struct dec_ctx {
   __device__ __forceinline__ bool fail(uint32_t op, uint32_t code) {
     report(err, r, op, code);
     return false;
+  }
+  // the element area of a container of inline elements (elem_area_ok)
+  __device__ __forceinline__ bool area(uint32_t op, uint32_t cnt, uint32_t stride, uint32_t wire) {
+    if (elem_area_ok(ecur, eend, cnt, stride, wire, b - p)) return true;
+    return fail(op, XDRG_ERR_OVERFLOW_GET);
   }
 };
 
@@ -657,6 +662,7 @@ __device__ __forceinline__ void var_decode_body(
   c.err = err;
   c.heap = heap;
   c.ecur = ebase + static_cast<uint64_t>(F) * a;  // this record's element arrays
+  c.eend = ebase + static_cast<uint64_t>(F) * b;
   uint32_t rec[NWD > 0 ? NWD : 1];
 #pragma unroll
   for (int k = 0; k < (NWD > 0 ? NWD : 1); ++k) rec[k] = 0u;

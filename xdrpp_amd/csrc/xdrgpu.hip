@@ -734,7 +734,7 @@ __global__ __launch_bounds__(256) void k_var_decode(
         report(err, r, pc, (op.flags & XDRG_F_POINTER) ? XDRG_ERR_POINTER_BOUND : XDRG_ERR_XVECTOR_BOUND);
         return;
       }
-      ecur = (ecur + 7u) & ~7ull;
+      if (!elem_area_ok(ecur, ebase + static_cast<uint64_t>(F) * b, cnt, op.arg1, op.arg3, b - p)) goto overflow;
       *reinterpret_cast<uint64_t *>(nat + op.noff) = ecur;
       st32(nat + op.noff + 8, cnt);
       auto rd = [&](uint64_t q) { return ld32(xdr + q); };
@@ -925,7 +925,7 @@ struct interp_walk {
           pc = kPcDone;
           break;
         }
-        c.ecur = (c.ecur + 7u) & ~7ull;
+        if (!c.area(upc, cnt, op.arg1, op.arg3)) { ok = false; pc = kPcDone; break; }
         *reinterpret_cast<uint64_t *>(nat + op.noff) = c.ecur;
         nw[2] = cnt;
         if (!dec_vector_elems(ops, table, upc + 1, op.arg2, cnt, op.arg1, c.heap + c.ecur, p, c.b,
@@ -1109,7 +1109,9 @@ __device__ uint32_t rx_len(const xdrg_op *__restrict__ ops, const uint32_t *__re
       } else if (!v) {
         ++pc;
       } else {
-        if (fp == XDRG_SUB_FRAMES) return RX_BAD;
+        // deeper records are left to the caller's walk, as records past
+        // the window are (include/xdrgpu.h xdrg_index_records)
+        if (fp == XDRG_SUB_FRAMES) return RX_LONG;
         st[fp++] = frame{v - 1, op.arg4, pc + 1};
         pc = op.arg4;
       }
@@ -1238,21 +1240,48 @@ __global__ __launch_bounds__(64) void k_ix_down(const uint64_t *__restrict__ pf,
 // REC: the chain of records ends at w: the end of the stream, or a record
 // that does not parse (its decode reports why) -- or one longer than the
 // index window, XDRG_ERR_INDEX_LONG.
+// A message index over a window of a longer stream (xdrg_index_msgs with a
+// max_msg_len past XDRG_INDEX_MAX_MSG, ix_window below): the window's
+// place in the stream, and where the chain leaves it.  For any other index
+// m0 = base = 0, next = nullptr and the window is the stream.
+struct ix_cont {
+  uint64_t m0;               // messages before the window
+  uint64_t base;             // byte offset of the window in the stream
+  const uint8_t *s;          // the whole stream
+  uint64_t len;              // its length
+  uint32_t maxlen;           // the caller's max_msg_len
+  unsigned long long *next;  // the chain leaves at: [mark word, message index]
+};
+
 template <bool REC>
 __device__ void ix_final(const uint8_t *__restrict__ s, uint64_t len, uint32_t maxlen, uint64_t w,
                          uint64_t m, uint64_t max_msgs, uint64_t *__restrict__ offsets,
-                         unsigned long long *count, unsigned long long *err, const rx_plan &rp) {
+                         unsigned long long *count, unsigned long long *err, const rx_plan &rp,
+                         const ix_cont &C) {
   if (m > max_msgs) return;
-  offsets[m] = 4 * w;
+  offsets[m] = C.base + 4 * w;
   if (REC) {
     if (4 * w < len && m < max_msgs && rx_len(rp.ops, rp.table, rx_global{s}, len, 4 * w, maxlen) == RX_LONG)
       report(err, m, kOpRecordLevel, XDRG_ERR_INDEX_LONG);
   } else {
     uint64_t nx = 0;
-    const uint32_t st = ix_mark(4 * w + 4 <= len ? ld32(s + 4 * w) : 0u, w, len, maxlen, &nx);
-    if (st != IX_END) report(err, m, kOpRecordLevel, m == max_msgs ? XDRG_ERR_MSG_COUNT : ix_error(st));
+    uint32_t st = ix_mark(4 * w + 4 <= len ? ld32(s + 4 * w) : 0u, w, len, maxlen, &nx);
+    if (C.next && !(st == IX_END && C.base + len == C.len)) {
+      // a mark the window cannot hold (a longer message, or one past the
+      // window's end), or the window's end: the chain goes on there unless
+      // the stream itself says otherwise (classified as read_message would)
+      const uint64_t aw = C.base / 4 + w;
+      const uint32_t rs = ix_mark(4 * aw + 4 <= C.len ? ld32(C.s + 4 * aw) : 0u, aw, C.len, C.maxlen, &nx);
+      if (m < max_msgs && (rs == IX_RUN || st == IX_END)) {
+        C.next[0] = aw;
+        C.next[1] = C.m0 + m;
+        return;
+      }
+      st = m == max_msgs ? IX_LONG : rs;  // the capacity (MSG_COUNT below), or what the stream says
+    }
+    if (st != IX_END) report(err, C.m0 + m, kOpRecordLevel, m == max_msgs ? XDRG_ERR_MSG_COUNT : ix_error(st));
   }
-  atomicMin(count, m);
+  atomicMin(count, C.m0 + m);
 }
 
 template <bool REC>
@@ -1262,7 +1291,7 @@ __global__ __launch_bounds__(256) void k_ix_emit(const uint8_t *__restrict__ s, 
                                                  const uint32_t *__restrict__ lcount,
                                                  uint64_t *__restrict__ offsets, uint64_t max_msgs,
                                                  unsigned long long *count,
-                                                 unsigned long long *err, rx_plan rp) {
+                                                 unsigned long long *err, rx_plan rp, ix_cont C) {
   // J: successor of a valid node (0xffff: not a valid node); lst: the valid
   // nodes; nj / mk: a round's new successors and marks (double buffer)
   __shared__ __attribute__((aligned(16))) uint16_t J[kIxSW];
@@ -1295,7 +1324,7 @@ __global__ __launch_bounds__(256) void k_ix_emit(const uint8_t *__restrict__ s, 
   if (tid == 0) on[x] = 1;
   __syncthreads();
   if (J[x] == 0xffffu) {  // the chain ends at its entry
-    if (tid == 0) ix_final<REC>(s, len, maxlen, w0 + x, b, max_msgs, offsets, count, err, rp);
+    if (tid == 0) ix_final<REC>(s, len, maxlen, w0 + x, b, max_msgs, offsets, count, err, rp, C);
     return;
   }
   // Fast path: when the valid nodes from x on form one path (no node is the
@@ -1370,14 +1399,14 @@ __global__ __launch_bounds__(256) void k_ix_emit(const uint8_t *__restrict__ s, 
     const uint64_t m = b + r;
     ++r;
     if (r == total && J[i] == 0xffffu) {  // the chain ends at this node
-      ix_final<REC>(s, len, maxlen, w0 + i, m, max_msgs, offsets, count, err, rp);
+      ix_final<REC>(s, len, maxlen, w0 + i, m, max_msgs, offsets, count, err, rp, C);
       continue;
     }
     if (m > max_msgs) continue;
-    offsets[m] = 4 * (w0 + i);
+    offsets[m] = C.base + 4 * (w0 + i);
     if (m == max_msgs && !REC) {  // a message past the index's capacity
-      report(err, m, kOpRecordLevel, XDRG_ERR_MSG_COUNT);
-      atomicMin(count, m);
+      report(err, C.m0 + m, kOpRecordLevel, XDRG_ERR_MSG_COUNT);
+      atomicMin(count, C.m0 + m);
     }
   }
 }
@@ -1390,6 +1419,43 @@ __global__ void k_rx_fill(uint64_t *__restrict__ offsets, const unsigned long lo
   for (uint64_t i = c + 1 + static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i <= n;
        i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
     offsets[i] = len;
+}
+
+// Messages longer than one index window, walked mark after mark as
+// read_message frames them (srpc.cc:29-55): from next = [mark word,
+// message index] while the message there is longer than
+// XDRG_INDEX_MAX_MSG, at most `hops` of them.  Leaves next at the first
+// shorter message (next[2] = 1) or at the hop budget (next[2] = 0); the
+// end of the stream, a framing error or the index's capacity ends the
+// index here (next[0] = all ones).
+__global__ void k_ix_long(const uint8_t *__restrict__ s, uint64_t len, uint32_t maxlen, uint64_t max_msgs,
+                          uint64_t *__restrict__ offsets, unsigned long long *count, unsigned long long *err,
+                          unsigned long long *next, uint32_t hops) {
+  if (threadIdx.x || blockIdx.x) return;
+  uint64_t w = next[0], m = next[1];
+  for (uint32_t h = 0; h < hops; ++h) {
+    uint64_t nx = 0;
+    const uint32_t st = ix_mark(4 * w + 4 <= len ? ld32(s + 4 * w) : 0u, w, len, maxlen, &nx);
+    if (st == IX_RUN && 4 * (nx - w - 1) <= XDRG_INDEX_MAX_MSG) {  // a window takes it
+      next[0] = w;
+      next[1] = m;
+      next[2] = 1;
+      return;
+    }
+    if (m > max_msgs) break;  // not reached: the capacity is checked below
+    offsets[m] = 4 * w;
+    if (st != IX_RUN || m == max_msgs) {
+      if (st != IX_END) report(err, m, kOpRecordLevel, m == max_msgs ? XDRG_ERR_MSG_COUNT : ix_error(st));
+      atomicMin(count, m);
+      next[0] = ~0ull;
+      return;
+    }
+    ++m;
+    w = nx;
+  }
+  next[0] = w;
+  next[1] = m;
+  next[2] = 0;
 }
 
 // ------------------------------------------------------------------ swaps
@@ -1597,16 +1663,119 @@ __global__ __launch_bounds__(256) void k_size_linear(const uint8_t *__restrict__
   if (block_sums && (threadIdx.x & 63u) == 0 && blk * 64u < n) block_sums[blk] = v;
 }
 
+// ------------------------------------------------------------ frame pool
+// The deep passes of the element-subroutine walks (sub_kernels.h): per
+// device, the lists of deferred records and the frame slabs of the two deep
+// passes.  A plan that can nest past XDRG_SUB_FRAMES (plan.deep) leases the
+// pool for the launches of one API call; the pool's event orders its users
+// across streams (no host wait, except when the lists must grow).
+constexpr uint32_t kDeepLanesA = 4096, kDeepSlabA = 1024;           // 64 MiB of frames
+constexpr uint32_t kDeepLanesB = 8, kDeepSlabB = XDRG_MAX_FRAMES;   // 64 MiB
+static_assert(kDeepLanesA % 256 == 0, "deep pass A runs 256-lane workgroups");
+struct frame_pool {
+  std::mutex mu;
+  uint8_t *d = nullptr;
+  uint64_t records = 0;       // capacity of each list
+  hipEvent_t last = nullptr;  // the last lease's launches
+};
+frame_pool g_pool[kMaxDevices];
+
+struct deep_passes {
+  sub_pass main{nullptr, nullptr, nullptr, nullptr, nullptr, 0, 1};
+  sub_pass A{}, B{};
+  bool on = false;  // the plan needs the deep passes
+};
+
+class pool_lease {
+ public:
+  ~pool_lease() {
+    if (!pool_) return;
+    if (!capturing_) (void)hipEventRecord(pool_->last, s_);
+    pool_->mu.unlock();
+  }
+  // The passes of plan p over n records on stream s.  For encode, `reuse`:
+  // the encode walks the lists its size pass built, deferring nothing.
+  int acquire(const xdrg_plan &p, uint64_t n, hipStream_t s, deep_passes &dp) {
+    if (!p.deep) return XDRG_OK;
+    if (n > 0xffffffffull) return XDRG_EUNSUPPORTED;  // u32 list entries
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev));
+    if (dev < 0 || dev >= kMaxDevices) return XDRG_EUNSUPPORTED;
+    frame_pool &P = g_pool[dev];
+    P.mu.lock();
+    pool_ = &P;
+    s_ = s;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    HIPCHK(hipStreamIsCapturing(s, &cs));
+    capturing_ = cs != hipStreamCaptureStatusNone;
+    if (!P.last) HIPCHK(hipEventCreateWithFlags(&P.last, hipEventDisableTiming));
+    const uint64_t slabs = 16ull * (uint64_t(kDeepLanesA) * kDeepSlabA + uint64_t(kDeepLanesB) * kDeepSlabB);
+    if (n > P.records) {
+      if (capturing_) return XDRG_EUNSUPPORTED;  // run one launch of this size before capturing
+      if (P.d) {
+        HIPCHK(hipEventSynchronize(P.last));
+        HIPCHK(hipFree(P.d));
+        P.d = nullptr;
+        P.records = 0;
+      }
+      const uint64_t cap = align_up(std::max<uint64_t>(n, 1u << 16), 1u << 16);
+      HIPCHK(hipMalloc(&P.d, 256 + 8 * cap + slabs));
+      P.records = cap;
+    }
+    if (!capturing_) HIPCHK(hipStreamWaitEvent(s, P.last, 0));
+    HIPCHK(hipMemsetAsync(P.d, 0, 16, s));
+    auto *cnt = reinterpret_cast<unsigned long long *>(P.d);
+    uint32_t *la = reinterpret_cast<uint32_t *>(P.d + 256), *lb = la + P.records;
+    sub_frame *sa = reinterpret_cast<sub_frame *>(P.d + 256 + 8 * P.records);
+    sub_frame *sb = sa + uint64_t(kDeepLanesA) * kDeepSlabA;
+    dp.on = true;
+    dp.main = sub_pass{nullptr, nullptr, la, cnt, nullptr, 0, 0};
+    dp.A = sub_pass{la, cnt, lb, cnt + 1, sa, kDeepSlabA, 0};
+    dp.B = sub_pass{lb, cnt + 1, nullptr, nullptr, sb, kDeepSlabB, 1};
+    return XDRG_OK;
+  }
+
+ private:
+  frame_pool *pool_ = nullptr;
+  hipStream_t s_ = nullptr;
+  bool capturing_ = false;
+};
+
+// The encode walk reuses the size pass's lists: it defers nothing.
+deep_passes encode_passes(deep_passes dp) {
+  if (!dp.on) return dp;
+  dp.main.defer = nullptr;
+  dp.main.defer_count = nullptr;
+  dp.A.defer = nullptr;
+  dp.A.defer_count = nullptr;
+  return dp;
+}
+
+// The frame-walk size pass (k_sub_size) with its deep passes.
+template <bool DEPTH>
+hipError_t launch_sub_size(const xdrg_plan &p, const dev_tables &T, const uint8_t *nat, uint64_t n,
+                           const uint8_t *heap, uint64_t heap_len, uint32_t *sizes, unsigned long long *bsum,
+                           uint32_t mark, unsigned long long *err, uint32_t *depths, const deep_passes &dp,
+                           hipStream_t s) {
+  const size_t lds = p.ops.size() * sizeof(xdrg_op);
+  const uint32_t nops = uint32_t(p.ops.size());
+  k_sub_size<DEPTH><<<(n + 255) / 256, 256, lds, s>>>(nat, n, p.stride, heap, heap_len, T.d_ops, nops, T.d_table,
+                                                      sizes, bsum, mark, err, depths, dp.main);
+  if (dp.on) {
+    k_sub_size<DEPTH><<<kDeepLanesA / 256, 256, lds, s>>>(nat, n, p.stride, heap, heap_len, T.d_ops, nops,
+                                                          T.d_table, sizes, bsum, mark, err, depths, dp.A);
+    k_sub_size<DEPTH><<<1, kDeepLanesB, lds, s>>>(nat, n, p.stride, heap, heap_len, T.d_ops, nops, T.d_table,
+                                                  sizes, bsum, mark, err, depths, dp.B);
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_size_pass(const xdrg_plan &p, const dev_tables &T, const uint8_t *nat, uint64_t n,
                             const uint8_t *heap, uint64_t heap_len, uint32_t *sizes,
                             unsigned long long *bsum, uint32_t mark, unsigned long long *err,
-                            hipStream_t s) {
-  if (p.has_sub) {  // containers of variable-size elements: the frame walk
-    k_sub_size<false><<<(n + 255) / 256, 256, p.ops.size() * sizeof(xdrg_op), s>>>(
-        nat, n, p.stride, heap, heap_len, T.d_ops, uint32_t(p.ops.size()), T.d_table, sizes, bsum, mark,
-        err, nullptr);
-    return hipGetLastError();
-  }
+                            hipStream_t s, const deep_passes &dp = deep_passes{}) {
+  if (p.has_sub)  // containers of variable-size elements: the frame walk
+    return launch_sub_size<false>(p, T, nat, n, heap, heap_len, sizes, bsum, mark, err, nullptr, dp, s);
   if (p.linear && p.opts.size_linear) {
     lin_args L;
     L.base = p.lin_base;
@@ -1712,6 +1881,10 @@ int var_encode(const xdrg_plan &P, const dev_tables &T, const void *d_native, ui
     lds_s = enc_layout(p->stride, p->spec.info.slots, Cs).total;
     if (lds_s > kVarLdsBudget || 64ull * max_rec >= (1ull << 31) || !aligned(d_native, 16)) SM = nullptr;
   }
+  pool_lease lease;  // element subroutines nested past XDRG_SUB_FRAMES
+  deep_passes dp;
+  if (p->has_sub)
+    if (int rc = lease.acquire(*p, n, s, dp)) return rc;
   if (SM && !p->linear) {
     const size_t tile = 64ull * p->stride;
     uint32_t n_mark = mark;
@@ -1719,13 +1892,22 @@ int var_encode(const xdrg_plan &P, const dev_tables &T, const void *d_native, ui
     HIPCHK(hipModuleLaunchKernel(static_cast<hipFunction_t>(SM->f_size), static_cast<uint32_t>(nb), 1, 1,
                                  64, 1, 1, static_cast<uint32_t>(tile), s, args, nullptr));
   } else {
-    HIPCHK(launch_size_pass(*p, T, nat8, n, d_heap, heap_len, sizes, bsum, mark, err, s));
+    HIPCHK(launch_size_pass(*p, T, nat8, n, d_heap, heap_len, sizes, bsum, mark, err, s, dp));
   }
   if (int rc = xdrg::launch_block_scan(bsum, bbase, uint32_t(nb), d_status, d_offsets, n, s)) return rc;
   if (p->has_sub) {
+    const deep_passes ep = encode_passes(dp);
     k_sub_encode<<<(n + 255) / 256, 256, lds_ops, s>>>(nat8, n, p->stride, d_heap, heap_len, xdr8, cap,
                                                       d_offsets, sizes, bbase, T.d_ops, nops, T.d_table,
-                                                      stack_limit, mark, err);
+                                                      stack_limit, mark, err, ep.main);
+    if (ep.on) {
+      k_sub_encode<<<kDeepLanesA / 256, 256, lds_ops, s>>>(nat8, n, p->stride, d_heap, heap_len, xdr8, cap,
+                                                           d_offsets, sizes, bbase, T.d_ops, nops, T.d_table,
+                                                           stack_limit, mark, err, ep.A);
+      k_sub_encode<<<1, kDeepLanesB, lds_ops, s>>>(nat8, n, p->stride, d_heap, heap_len, xdr8, cap, d_offsets,
+                                                   sizes, bbase, T.d_ops, nops, T.d_table, stack_limit, mark,
+                                                   err, ep.B);
+    }
     HIPCHK(hipGetLastError());
     return XDRG_OK;
   }
@@ -1778,6 +1960,7 @@ struct ix_layout {
   size_t total = 0;
 };
 constexpr size_t kIxLdsBytes = 64u << 10;
+constexpr size_t kIxNextBytes = 256;  // ix_windows' continuation block
 
 ix_layout ix_plan(uint64_t len, uint32_t maxlen) {
   ix_layout L;
@@ -1857,10 +2040,22 @@ int var_decode(const xdrg_plan &P, const dev_tables &T, const void *d_xdr, uint6
   if (kern == 2 && !ok_W) kern = 0;
   if (kern == 0) kern = ok_W ? 2 : 1;
   if (p->has_sub) {  // containers of variable-size elements: the frame walk
+    pool_lease lease;  // element subroutines nested past XDRG_SUB_FRAMES
+    deep_passes dp;
+    if (int rc = lease.acquire(*p, n, s, dp)) return rc;
     if (copy && len) HIPCHK(hipMemcpyAsync(d_heap_out, d_xdr, len, hipMemcpyDeviceToDevice, s));
-    k_sub_decode<<<(n + 255) / 256, 256, p->ops.size() * sizeof(xdrg_op), s>>>(
-        xdr8, len, d_offsets, n, nat8, p->stride, T.d_ops, nops, T.d_table, stack_limit, d_heap_out, ebase,
-        p->heap_factor, mark, err);
+    const size_t lds = p->ops.size() * sizeof(xdrg_op);
+    k_sub_decode<<<(n + 255) / 256, 256, lds, s>>>(xdr8, len, d_offsets, n, nat8, p->stride, T.d_ops, nops,
+                                                  T.d_table, stack_limit, d_heap_out, ebase, p->heap_factor,
+                                                  mark, err, dp.main);
+    if (dp.on) {
+      k_sub_decode<<<kDeepLanesA / 256, 256, lds, s>>>(xdr8, len, d_offsets, n, nat8, p->stride, T.d_ops, nops,
+                                                       T.d_table, stack_limit, d_heap_out, ebase,
+                                                       p->heap_factor, mark, err, dp.A);
+      k_sub_decode<<<1, kDeepLanesB, lds, s>>>(xdr8, len, d_offsets, n, nat8, p->stride, T.d_ops, nops,
+                                               T.d_table, stack_limit, d_heap_out, ebase, p->heap_factor, mark,
+                                               err, dp.B);
+    }
     HIPCHK(hipGetLastError());
     return XDRG_OK;
   }
@@ -1911,10 +2106,13 @@ int var_decode(const xdrg_plan &P, const dev_tables &T, const void *d_xdr, uint6
 }  // namespace
 
 namespace {
+// C: the window of a longer stream this index covers (ix_cont); the
+// offsets, count and errors are the whole stream's.
 template <bool REC>
 int run_index(const xdrg_plan *p, const dev_tables *T, const void *d_stream, uint64_t len,
               uint32_t max_msg_len, uint64_t max_msgs, uint64_t *d_offsets, uint64_t *d_count,
-              void *d_ws, size_t ws_bytes, xdrg_status *d_status, hipStream_t s) {
+              void *d_ws, size_t ws_bytes, xdrg_status *d_status, hipStream_t s,
+              const ix_cont &C = ix_cont{}) {
   const ix_layout L = ix_plan(len, max_msg_len);
   if (!d_ws || ws_bytes < L.total) return XDRG_ESPACE;
   if (L.nseg > 0xffffffffull) return XDRG_EUNSUPPORTED;
@@ -1941,7 +2139,7 @@ int run_index(const xdrg_plan *p, const dev_tables *T, const void *d_stream, uin
   auto tab = [&](int l) { return reinterpret_cast<uint64_t *>(ws + L.tab[l]); };
   auto ent = [&](int l) { return reinterpret_cast<uint64_t *>(ws + L.ent[l]); };
   const uint8_t *s8 = static_cast<const uint8_t *>(d_stream);
-  HIPCHK(hipMemsetAsync(d_count, 0xff, 8, s));
+  if (!C.next) HIPCHK(hipMemsetAsync(d_count, 0xff, 8, s));  // (a window's caller sets it once)
   uint32_t *vlist = reinterpret_cast<uint32_t *>(ws + L.list);
   uint32_t *vcount = reinterpret_cast<uint32_t *>(ws + L.lcount);
   // the tables are needed above one segment; the valid-node lists always
@@ -1974,8 +2172,9 @@ int run_index(const xdrg_plan *p, const dev_tables *T, const void *d_stream, uin
     k_ix_down<<<L.n[l + 1], 64, 0, s>>>(pfx(l), L.n[l], L.K, L.F, ent(l + 1), ent(l));
     HIPCHK(hipGetLastError());
   }
-  k_ix_emit<REC><<<L.nseg, 256, 0, s>>>(s8, len, max_msg_len, ent(0), vlist, vcount, d_offsets,
-                                        max_msgs, reinterpret_cast<unsigned long long *>(d_count), err, rp);
+  k_ix_emit<REC><<<L.nseg, 256, 0, s>>>(s8, len, max_msg_len, ent(0), vlist, vcount, d_offsets + C.m0,
+                                        max_msgs - C.m0, reinterpret_cast<unsigned long long *>(d_count), err,
+                                        rp, C);
   HIPCHK(hipGetLastError());
   if (REC) {
     k_rx_fill<<<static_cast<uint32_t>(std::min<uint64_t>((max_msgs + 256) / 256, 4096)), 256, 0, s>>>(
@@ -1983,6 +2182,54 @@ int run_index(const xdrg_plan *p, const dev_tables *T, const void *d_stream, uin
     HIPCHK(hipGetLastError());
   }
   return XDRG_OK;
+}
+
+// Message index of a stream whose messages may be longer than one index
+// window (max_msg_len > XDRG_INDEX_MAX_MSG; msg_sock's default is 1 MiB,
+// msgsock.h:29, and read_message has no limit, srpc.cc:29-55).  Rounds,
+// each picking up where the chain left the last one:
+//   k_ix_long  walks the long messages from there, mark after mark;
+//   a window   the list-ranking index (run_index, messages up to
+//              XDRG_INDEX_MAX_MSG) over the stream from the first short
+//              message on, until its chain reaches a long message or the
+//              window's end (ix_final leaves the continuation).
+// The first window is the whole stream, so a stream without long messages
+// takes one round.  A window that its chain left early is followed by one
+// twice as long as the stretch the chain covered (at least kIxMinWindow):
+// the index reads each byte about twice at most, plus two host waits per
+// round (the continuation is read back).
+constexpr uint64_t kIxMinWindow = 1ull << 20;
+int ix_windows(const uint8_t *s8, uint64_t len, uint32_t max_msg_len, uint64_t max_msgs, uint64_t *d_offsets,
+               uint64_t *d_count, void *d_ws, size_t ws_bytes, xdrg_status *d_status, hipStream_t s) {
+  const size_t need = xdrg_index_workspace_size(len, max_msg_len);
+  if (!d_ws || ws_bytes < need) return XDRG_ESPACE;
+  auto *next = reinterpret_cast<unsigned long long *>(static_cast<char *>(d_ws) + need - kIxNextBytes);
+  unsigned long long *err = err_ptr(d_status);
+  unsigned long long *count = reinterpret_cast<unsigned long long *>(d_count);
+  HIPCHK(hipMemsetAsync(d_count, 0xff, 8, s));
+  HIPCHK(hipMemsetAsync(next, 0, 24, s));  // the chain starts at word 0, message 0
+  unsigned long long h[3] = {0, 0, 0};
+  uint64_t window = len;
+  for (;;) {
+    k_ix_long<<<1, 64, 0, s>>>(s8, len, max_msg_len, max_msgs, d_offsets, count, err, next, 4096u);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(h, next, 24, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (h[0] == ~0ull) return XDRG_OK;
+    if (!h[2]) continue;  // the hop budget ran out among long messages
+    const uint64_t start = 4 * h[0], m0 = h[1];
+    const uint64_t wl = std::min<uint64_t>(window, len - start);
+    HIPCHK(hipMemsetAsync(next, 0xff, 8, s));
+    const ix_cont C{m0, start, s8, len, max_msg_len, next};
+    if (int rc = run_index<false>(nullptr, nullptr, s8 + start, wl, XDRG_INDEX_MAX_MSG, max_msgs, d_offsets,
+                                  d_count, d_ws, ws_bytes, d_status, s, C))
+      return rc;
+    HIPCHK(hipMemcpyAsync(h, next, 16, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (h[0] == ~0ull) return XDRG_OK;
+    const uint64_t covered = 4 * h[0] - start;
+    window = covered < wl ? std::max<uint64_t>(2 * covered, kIxMinWindow) : 2 * wl;
+  }
 }
 }  // namespace
 
@@ -2236,10 +2483,12 @@ int xdrg_record_depths(const xdrg_plan *p, const void *d_native, uint64_t n, con
   if (int rc = plan_upload(p, &T)) return rc;
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (p->has_sub) {
-    k_sub_size<true><<<(n + 255) / 256, 256, p->ops.size() * sizeof(xdrg_op), s>>>(
-        static_cast<const uint8_t *>(d_native), n, p->stride, static_cast<const uint8_t *>(d_heap), heap_len,
-        T->d_ops, uint32_t(p->ops.size()), T->d_table, nullptr, nullptr, 0u, err_ptr(d_status), d_depths);
-    HIPCHK(hipGetLastError());
+    pool_lease lease;  // element subroutines nested past XDRG_SUB_FRAMES
+    deep_passes dp;
+    if (int rc = lease.acquire(*p, n, s, dp)) return rc;
+    HIPCHK(launch_sub_size<true>(*p, *T, static_cast<const uint8_t *>(d_native), n,
+                                 static_cast<const uint8_t *>(d_heap), heap_len, nullptr, nullptr, 0u,
+                                 err_ptr(d_status), d_depths, dp, s));
     return XDRG_OK;
   }
   if (p->path != XDRG_PATH_VAR || p->linear) {  // every record walks every op
@@ -2274,9 +2523,13 @@ int xdrg_serial_sizes(const xdrg_plan *p, const void *d_native, uint64_t n, cons
     HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_sizes), int(p->fixed_size), n, s));
     return XDRG_OK;
   }
+  pool_lease lease;  // element subroutines nested past XDRG_SUB_FRAMES
+  deep_passes dp;
+  if (p->has_sub)
+    if (int rc = lease.acquire(*p, n, s, dp)) return rc;
   HIPCHK(launch_size_pass(*p, *T, static_cast<const uint8_t *>(d_native), n,
                           static_cast<const uint8_t *>(d_heap), heap_len, d_sizes, nullptr, 0u,
-                          err_ptr(d_status), s));
+                          err_ptr(d_status), s, dp));
   return XDRG_OK;
 }
 
@@ -2292,20 +2545,25 @@ int xdrg_encode_msgs(const xdrg_plan *p, const void *d_native, uint64_t n, const
 }
 
 size_t xdrg_index_workspace_size(uint64_t len, uint32_t max_msg_len) {
-  if (max_msg_len > XDRG_INDEX_MAX_MSG) return 0;
-  return ix_plan(len, max_msg_len).total;
+  if (max_msg_len > XDRG_MAX_MSG) return 0;
+  if (max_msg_len <= XDRG_INDEX_MAX_MSG) return ix_plan(len, max_msg_len).total;
+  return ix_plan(len, XDRG_INDEX_MAX_MSG).total + kIxNextBytes;  // + ix_windows' continuation
 }
 
 int xdrg_index_msgs(const void *d_stream, uint64_t len, uint32_t max_msg_len, uint64_t max_msgs,
                     uint64_t *d_offsets, uint64_t *d_count, void *d_ws, size_t ws_bytes,
                     xdrg_status *d_status, void *stream) {
   if (!d_offsets || !d_count || !d_status || (len && !d_stream)) return XDRG_EINVAL;
-  if (max_msg_len > XDRG_INDEX_MAX_MSG) return XDRG_EUNSUPPORTED;
+  if (max_msg_len > XDRG_MAX_MSG) return XDRG_EINVAL;
   if ((d_stream && !aligned(d_stream, 4)) || !aligned(d_offsets, 8) || !aligned(d_count, 8))
     return XDRG_EALIGN;
   if (max_msgs >= (1ull << 40)) return XDRG_EUNSUPPORTED;  // entry words hold 40-bit counts
-  return run_index<false>(nullptr, nullptr, d_stream, len, max_msg_len, max_msgs, d_offsets, d_count,
-                          d_ws, ws_bytes, d_status, static_cast<hipStream_t>(stream));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (max_msg_len <= XDRG_INDEX_MAX_MSG)
+    return run_index<false>(nullptr, nullptr, d_stream, len, max_msg_len, max_msgs, d_offsets, d_count,
+                            d_ws, ws_bytes, d_status, s);
+  return ix_windows(static_cast<const uint8_t *>(d_stream), len, max_msg_len, max_msgs, d_offsets, d_count,
+                    d_ws, ws_bytes, d_status, s);
 }
 
 int xdrg_index_records(const xdrg_plan *p, const void *d_xdr, uint64_t len, uint64_t n,

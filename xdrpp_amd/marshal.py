@@ -338,10 +338,10 @@ class Marshaler:
         """xdr_from_msg(m_r, r) for every message of the stream
         (marshal.h:278-284).  Without `offsets` the record index comes from
         the marks (index_messages, on the device; the message bound
-        defaults to the plan's largest record).  Returns (native, heap)."""
+        defaults to msg_sock's, msgsock.h:29).  Returns (native, heap)."""
         if offsets is None:
             if max_msg_len is None:
-                max_msg_len = min(self.plan.max_record_bytes, A.INDEX_MAX_MSG)
+                max_msg_len = A.MSG_SOCK_MAXMSGLEN
             offsets = index_messages(stream_bytes, max_msg_len)
         if n is None:
             n = offsets.numel() - 1
@@ -368,13 +368,14 @@ class _IndexErrorPlan:
             return "bad value of discriminant"
 
 
-def index_messages(stream_bytes: torch.Tensor, max_msg_len: int = A.INDEX_MAX_MSG,
+def index_messages(stream_bytes: torch.Tensor, max_msg_len: int = A.MSG_SOCK_MAXMSGLEN,
                    max_msgs: int | None = None) -> torch.Tensor:
     """Record index of a stream of record-marked messages, on the device
     (xdrg_index_msgs): the framing read_message / msg_sock::input apply
-    (srpc.cc:29-55, msgsock.cc:38-119).  Returns int64 offsets[count + 1]
-    (mark of each message, then the end); raises XdrBadMessageSize with
-    the reference's what() on a framing error."""
+    (srpc.cc:29-55, msgsock.cc:38-119), messages up to max_msg_len (msg_sock's
+    1 MiB by default; any length up to 2^31 - 1).  Returns int64
+    offsets[count + 1] (mark of each message, then the end); raises
+    XdrBadMessageSize with the reference's what() on a framing error."""
     dev = stream_bytes.device
     L = A.lib()
     total = stream_bytes.numel()

@@ -9,6 +9,7 @@
   containers of variable-size elements and a recursive type, from
   tests/xdrtest.x: containertest, containertest1 (:129-137), hasbytes
   (:94-96), test_recursive (:29-33), nested_cereal_adapter_calls (:172-176)
+  rp__list  xdrpp/rpcb_prot.x:24-37, a linked list of rpcb entries
 
 The union/type names match what xdrc generates, so bad-discriminant
 messages equal the reference's ("bad value of mtype in _body_t", ...).
@@ -105,5 +106,13 @@ nested_cereal_adapter_calls = Struct("nested_cereal_adapter_calls", [
     ("strptr", Pointer(string32)), ("strvec", XVector(string32)), ("strarr", XArray(string32, 2))])
 CONTAINERS = {"containertest": containertest, "containertest1": containertest1, "hasbytes": hasbytes,
               "test_recursive": test_recursive, "nested_cereal_adapter_calls": nested_cereal_adapter_calls}
+
+# ------------------------------------------ xdrpp/rpcb_prot.x: linked lists
+# The RPCBPROC_DUMP reply list (rpcb_prot.x:24-37): nested one pointer per
+# entry, as deep as the list is long.
+rpcb = Struct("rpcb", [("r_prog", UInt), ("r_vers", UInt), ("r_netid", String()), ("r_addr", String()),
+                       ("r_owner", String())])
+rp__list = Struct("rp__list")
+rp__list.define([("rpcb_map", rpcb), ("rpcb_next", Pointer(rp__list))])
 
 ALL = {"numerics": numerics, "rec128": rec128, "recvar": recvar, "rpc": rpc_msg, "vecrec": vecrec}
