@@ -8,7 +8,7 @@ Inputs are resident in HBM before timing.  Multi-GPU: one process per GPU
 (weak scaling, no collective on the data path); the timed region is
 bracketed by barrier + synchronize and the max over ranks is reported.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--n RECORDS]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--records N]
 
 With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py starts
 the N rank processes itself (torch.distributed.run as a child process,
@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--n", type=int, default=None,
+    ap.add_argument("--records", "--n", dest="n", type=int, default=None,
                     help="records per GPU (default 1M at N=1, 2M at N>1: BASELINE.json configs 2 and 5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-large", action="store_true",
@@ -70,6 +70,9 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--event-every", type=int, default=4,
                     help="HIP events around the kernels of every E-th timed step (1: every step)")
+    ap.add_argument("--engine", default=None,
+                    help="a file defining Engine, in place of the GPU step (tests only: "
+                         "tests/bench_cpu_engine.py rehearses the multi-rank plumbing on CPU over gloo)")
     ap.add_argument("--schema", default="rec128",
                     choices=["rec128", "numerics", "recvar", "rpc", "vecrec"],
                     help="rec128 is the headline; numerics/recvar/rpc measure BASELINE.json "
@@ -84,7 +87,10 @@ def _free_port() -> int:
 
 
 def rank_command(gpus: int, port: int, argv: list[str]) -> list[str]:
-    """The torch.distributed.run command that starts one bench rank per GPU."""
+    """The torch.distributed.run command that starts one bench rank per GPU.
+    (--n is passed on as --records: torch.distributed.run's own parser would
+    take it for an abbreviation of its options.)"""
+    argv = ["--records" if a == "--n" else "--records=" + a[4:] if a.startswith("--n=") else a for a in argv]
     return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
             "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + argv
 
@@ -102,16 +108,20 @@ def launch_ranks(args) -> int | None:
     return None
 
 
-def dist_init(args):
+def dist_init(args, backend="nccl"):
+    """One process per GPU: RCCL ("nccl") between the ranks; the tests'
+    CPU engine rehearses the same plumbing over gloo."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
         return dist, world, rank, local
-    torch.cuda.set_device(local)
     return None, 1, 0, local
 
 
@@ -586,151 +596,198 @@ def setup(schema, n, dev, rank, world):
     return plan, mar, nat, heap, xdr, back, offsets, heap_out
 
 
-def main():
-    args = parse()
-    rc = launch_ranks(args)
-    if rc is not None:
-        sys.exit(rc)
-    dist, world, rank, local = dist_init(args)
-    dev = torch.device("cuda", local)
-    n = args.n if args.n is not None else (1 << 20 if world == 1 else 1 << 21)
-    plan, mar, nat, heap, xdr, back, offsets, heap_out = setup(args.schema, n, dev, rank, world)
-    S_ = plan.stride
-    X = xdr.numel()
-    stream = torch.cuda.current_stream()
-    s = stream.cuda_stream
-    mar.status.init(s)
+class GpuEngine:
+    """One rank's marshal step on its GPU: encode the rank's batch, decode it
+    back (libxdrgpu through xdrpp_amd.marshal), with HIP events around the
+    kernels of the steps the caller marks.  The multi-rank plumbing of
+    main() only sees this interface (tests/bench_cpu_engine.py gives it a
+    CPU stand-in to rehearse that plumbing over gloo)."""
+
+    backend = "nccl"
+
+    def __init__(self, args, n, rank, world, local):
+        torch.cuda.set_device(local)
+        self.dev = torch.device("cuda", local)
+        self.schema, self.n = args.schema, n
+        (self.plan, self.mar, self.nat, self.heap, self.xdr, self.back, self.offsets,
+         self.heap_out) = setup(args.schema, n, self.dev, rank, world)
+        self.stream = torch.cuda.current_stream()
+        self.s = self.stream.cuda_stream
+        self.mar.status.init(self.s)
+        self.evs = []
+
+    def sync(self):
+        torch.cuda.synchronize()
 
     # HIP events bracket the kernels of every E-th step of the timed region
     # (--event-every E): before its encode, between encode and decode, after
     # its decode.  An event between two kernels is itself a command on the
     # stream that widens the gap between them; the other steps run without.
-    def step(ev=None):
+    def step(self, record=False):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if record else None
         if ev is not None:
-            ev[0].record(stream)
-        mar.launch_encode(nat, n, xdr, heap=heap, offsets=offsets, stream=s)
+            ev[0].record(self.stream)
+        self.mar.launch_encode(self.nat, self.n, self.xdr, heap=self.heap, offsets=self.offsets, stream=self.s)
         if ev is not None:
-            ev[1].record(stream)
-        mar.launch_decode(xdr, n, back, offsets=offsets, heap_out=heap_out, stream=s)
+            ev[1].record(self.stream)
+        self.mar.launch_decode(self.xdr, self.n, self.back, offsets=self.offsets, heap_out=self.heap_out,
+                               stream=self.s)
         if ev is not None:
-            ev[2].record(stream)
+            ev[2].record(self.stream)
+            self.evs.append(ev)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    mar.check(s)
+    def launch_ms(self):
+        """(encode ms, decode ms) of every recorded step."""
+        return ([e[0].elapsed_time(e[1]) for e in self.evs], [e[1].elapsed_time(e[2]) for e in self.evs])
 
-    E = max(1, args.event_every)
-    timed = [k for k in range(args.steps) if k % E == E - 1] or [args.steps - 1]
-    evs = {k: [torch.cuda.Event(enable_timing=True) for _ in range(3)] for k in timed}
-    barrier(dist)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(evs.get(k))
-    torch.cuda.synchronize()
-    barrier(dist)
-    elapsed = time.perf_counter() - t0
-    mar.check(s)
-    enc_ms = [evs[k][0].elapsed_time(evs[k][1]) for k in timed]
-    dec_ms = [evs[k][1].elapsed_time(evs[k][2]) for k in timed]
+    def check(self):
+        self.mar.check(self.s)
 
-    # correctness of what was timed: decode(encode(x)) == x (fixed) or
-    # encode(decode(encode(x))) == encode(x) (var); on the 1-GPU headline
-    # config the stream also hashes to the reference's output.
-    if plan.is_fixed:
-        ok_rt = bool(torch.equal(back, nat))
-    else:
-        x2 = torch.empty_like(xdr)
-        o2 = torch.empty_like(offsets)
-        mar.status.init(s)
-        mar.launch_encode(back, n, x2, heap=heap_out, offsets=o2, stream=s)
-        mar.check(s)
-        ok_rt = bool(torch.equal(x2, xdr))
-        del x2, o2
-    man = os.path.join(ROOT, "tests", "golden", "manifest.json")
-    hashes = json.load(open(man))["hashes"] if os.path.exists(man) else {}
-    bit_exact = None
-    if world == 1 and f"{args.schema}_{n}" in hashes:
-        bit_exact = hashlib.sha256(xdr.cpu().numpy().tobytes()).hexdigest() == hashes[f"{args.schema}_{n}"]["xdr"]
+    def round_trip_ok(self) -> bool:
+        """decode(encode(x)) == x (fixed) or encode(decode(encode(x))) ==
+        encode(x) (var)."""
+        if self.plan.is_fixed:
+            return bool(torch.equal(self.back, self.nat))
+        x2 = torch.empty_like(self.xdr)
+        o2 = torch.empty_like(self.offsets)
+        self.mar.status.init(self.s)
+        self.mar.launch_encode(self.back, self.n, x2, heap=self.heap_out, offsets=o2, stream=self.s)
+        self.mar.check(self.s)
+        return bool(torch.equal(x2, self.xdr))
 
-    # dominant kernel and its algorithmic bytes per launch
-    if plan.is_fixed:
-        # encode and decode are the same kernel with the encode / decode
-        # permutation programs
+    def dominant(self, enc_ms, dec_ms):
+        """The dominant kernel (or phase) and its algorithmic bytes per launch
+        (DESIGN.md §4), and the launch times it is timed by."""
+        plan, n, S_, X = self.plan, self.n, self.plan.stride, self.xdr.numel()
         info = A.XdrgPlanInfo()
         A.check(A.lib().xdrg_plan_get_info(plan.handle, A.C.byref(info)), "xdrg_plan_get_info")
-        kern = ("k_fixed_reg" if plan.path == A.PATH_FIXED_REG else
-                "k_fixed_grp" if info.group_records else "k_fixed_lds")
-        alg_bytes = n * S_ + X  # read one side + write the other, per launch
-        launches = enc_ms + dec_ms
-    else:
-        # dominant phase: encode (size pass + block scan + chunk-map image
-        # encode) vs decode (window decode).  Encode reads the native
-        # records and the payload heap and writes the stream + record index;
-        # decode reads stream + index and writes native records + the heap
-        # (= the stream verbatim).  Scratch (sizes, block sums) is excluded.
-        H = 0 if heap is None else heap.numel()
+        if plan.is_fixed:
+            # encode and decode are the same kernel with the encode / decode
+            # permutation programs: read one side, write the other
+            kern = ("k_fixed_reg" if plan.path == A.PATH_FIXED_REG else
+                    "k_fixed_grp" if info.group_records else "k_fixed_lds")
+            return kern, n * S_ + X, enc_ms + dec_ms
+        # dominant phase: encode (size pass + block scan + window encode) vs
+        # decode (window decode).  Encode reads the native records and the
+        # payload heap and writes the stream + record index; decode reads
+        # stream + index and writes the native records, the heap (= the
+        # stream verbatim) and the decoded element arrays past it (the
+        # element area the decode filled: every container's elements, read
+        # back from the decoded records' refs).  Scratch (sizes, block sums)
+        # is excluded.
+        H = 0 if self.heap is None else self.heap.numel()
         enc_alg = n * S_ + H + X + 8 * (n + 1)
-        dec_alg = X + 8 * (n + 1) + n * S_ + X
-        info = A.XdrgPlanInfo()
-        A.check(A.lib().xdrg_plan_get_info(plan.handle, A.C.byref(info)), "xdrg_plan_get_info")
+        dec_alg = X + 8 * (n + 1) + n * S_ + X + self.element_bytes()
         spec = bool(info.specialized)  # plan-specialized kernels ran (built at warmup)
         size_k = "k_size_linear" if plan_linear(plan) else ("xdrg_spec_size" if spec else "k_var_size")
         if np.mean(enc_ms) >= np.mean(dec_ms):
-            kern = f"{size_k}+k_scan_blocks+" + ("xdrg_spec_encode" if spec else "k_var_encode_i")
-            alg_bytes, launches = enc_alg, enc_ms
-        else:
-            kern, alg_bytes, launches = ("xdrg_spec_decode_copy" if spec else "k_var_decode_w"), dec_alg, dec_ms
+            return f"{size_k}+k_scan_blocks+" + ("xdrg_spec_encode" if spec else "k_var_encode_i"), enc_alg, enc_ms
+        return ("xdrg_spec_decode_copy" if spec else "k_var_decode_w"), dec_alg, dec_ms
+
+    def element_bytes(self) -> int:
+        """Native bytes of the element arrays a decode writes: count x stride
+        of every xvector/pointer field of every record (plans whose
+        containers hold fixed-size elements, read from the decoded records)."""
+        ops = self.plan.cp.ops
+        vec = np.nonzero(ops["kind"] == A.OP_VECTOR)[0]
+        if not vec.size:
+            return 0
+        nat = self.back.view(-1, self.plan.stride)
+        total = 0
+        for i in vec:
+            off, stride = int(ops["noff"][i]), int(ops["arg1"][i])
+            cnt = nat[:, off + 8:off + 12].contiguous().view(torch.int32)
+            total += int(cnt.to(torch.int64).sum().item()) * stride
+        return total
+
+    def shard(self):
+        """The rank's encoded stream and record index (for the gather)."""
+        return self.xdr, self.offsets
+
+
+def load_engine(path: str):
+    """--engine FILE: a module defining Engine (the tests' CPU stand-in)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_engine", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod.Engine
+
+
+def measure(engine, args):
+    """Warmup, then exactly args.steps steps bracketed by barrier + sync;
+    events around the kernels of every E-th.  Returns (elapsed s, encode
+    ms, decode ms)."""
+    for _ in range(args.warmup):
+        engine.step()
+    engine.sync()
+    engine.check()
+    E = max(1, args.event_every)
+    timed = {k for k in range(args.steps) if k % E == E - 1} or {args.steps - 1}
+    barrier(engine.dist)
+    engine.sync()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        engine.step(k in timed)
+    engine.sync()
+    barrier(engine.dist)
+    elapsed = time.perf_counter() - t0
+    engine.check()
+    enc_ms, dec_ms = engine.launch_ms()
+    return elapsed, enc_ms, dec_ms
+
+
+def rank_rows(dist, world, mine: list[float], dev):
+    """Every rank's row [elapsed, encode ms, decode ms, XDR bytes, achieved
+    GB/s, round trip ok] on every rank (one all_gather)."""
+    t = torch.tensor(mine, dtype=torch.float64, device=dev)
+    if dist is None:
+        return t.cpu().numpy()[None, :]
+    allr = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(allr, t)
+    return torch.stack(allr).cpu().numpy()
+
+
+def gather_leg(engine, dist, rank, world, X_all, X, rows, hashes, key):
+    """The one collective: every shard's stream (and
+    record index) to rank 0, timed apart from the marshal step.  Rank 0
+    gets the report dict; the others None."""
+    xdr, offsets = engine.shard()
+    engine.sync()
+    barrier(dist)
+    g0 = time.perf_counter()
+    g_stream, g_index = SH.gather_streams(dist, xdr, offsets, rank, world)
+    engine.sync()
+    g_s = time.perf_counter() - g0
+    t = torch.tensor([g_s], dtype=torch.float64, device=engine.dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    g_s = float(t.item())
+    if rank != 0:
+        return None
+    recv = X_all - X
+    sha = hashlib.sha256(g_stream.cpu().numpy().tobytes()).hexdigest()
+    gather = {"gather_ms": round(g_s * 1e3, 3), "bytes_to_root": recv, "stream_bytes": int(g_stream.numel()),
+              "root_inbound_gib_s": round(recv / GIB / g_s, 2),
+              "encode_plus_gather_gib_s": round(X_all / GIB / (float(rows[:, 1].max()) * 1e-3 + g_s), 2),
+              "sha256": sha,
+              "collective": f"exact-size point-to-point sends to rank 0 ({engine.backend}; RCCL over xGMI on "
+                            "MI355X)"}
+    if g_index is not None:
+        gather["index_sha256"] = hashlib.sha256(g_index.cpu().numpy().tobytes()).hexdigest()
+    if key in hashes:
+        gather["bit_exact_vs_reference"] = sha == hashes[key]["xdr"]
+    return gather
+
+
+def report(args, engine, world, rows, X, kern, alg_bytes, launches, enc_ms, dec_ms, bit_exact, gather):
+    """Rank 0's JSON line (the bench contract) from the per-rank rows."""
+    n, S_ = engine.n, engine.plan.stride
+    elapsed = float(rows[:, 0].max())
+    X_all = int(rows[:, 3].sum())
+    value = 2 * X_all / GIB / (elapsed / args.steps)
     avg = float(np.mean(launches))
     achieved = alg_bytes / (avg * 1e-3) / 1e9
-
-    # per-rank figures (max over ranks for the step time)
-    mine = torch.tensor([elapsed, float(np.mean(enc_ms)), float(np.mean(dec_ms)), float(X), achieved,
-                         float(ok_rt)], dtype=torch.float64, device=dev)
-    if dist is not None:
-        allr = [torch.zeros_like(mine) for _ in range(world)]
-        dist.all_gather(allr, mine)
-        ranks = torch.stack(allr).cpu().numpy()
-    else:
-        ranks = mine.cpu().numpy()[None, :]
-    elapsed = float(ranks[:, 0].max())
-    X_all = int(ranks[:, 3].sum())
-    ok_rt = bool(ranks[:, 5].all())
-
-    gather = None
-    if dist is not None and not args.no_gather:
-        # the one collective: every shard's stream (and
-        # record index) to rank 0 over RCCL, timed apart from the marshal step
-        torch.cuda.synchronize()
-        barrier(dist)
-        g0 = time.perf_counter()
-        g_stream, g_index = SH.gather_streams(dist, xdr, offsets, rank, world)
-        torch.cuda.synchronize()
-        g_s = time.perf_counter() - g0
-        t = torch.tensor([g_s], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        g_s = float(t.item())
-        if rank == 0:
-            recv = X_all - X
-            gather = {"gather_ms": round(g_s * 1e3, 3), "bytes_to_root": recv,
-                      "root_inbound_gib_s": round(recv / GIB / g_s, 2),
-                      "encode_plus_gather_gib_s": round(X_all / GIB / (float(ranks[:, 1].max()) * 1e-3 + g_s), 2),
-                      "collective": "torch.distributed.gather (RCCL over xGMI)"}
-            key = f"{args.schema}_mgpu_{n * world}"
-            if key in hashes:
-                gather["bit_exact_vs_reference"] = (
-                    hashlib.sha256(g_stream.cpu().numpy().tobytes()).hexdigest() == hashes[key]["xdr"])
-                bit_exact = gather["bit_exact_vs_reference"]
-        del g_stream, g_index
-
-    if rank != 0:
-        if dist is not None:
-            dist.destroy_process_group()
-        return
-
-    xdr_bytes_step = 2 * X_all
-    value = xdr_bytes_step / GIB / (elapsed / args.steps)
+    E = max(1, args.event_every)
     traffic = None
     tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tf):
@@ -774,42 +831,92 @@ def main():
                      "alg_bytes_per_launch": alg_bytes,
                      "timed_launches": len(launches),
                      "protocol": f"HIP events on the launch stream around both kernels of every {E}th timed step"},
-        "round_trip_ok": ok_rt,
+        "round_trip_ok": bool(rows[:, 5].all()),
         "bit_exact_vs_reference": bit_exact,
     }
     if world > 1:
         line["per_rank"] = [{"rank": r, "gib_s": round(2 * row[3] / GIB / (row[0] / args.steps), 2),
                              "encode_ms": round(row[1], 4), "decode_ms": round(row[2], 4),
                              "roofline_frac": round(row[4] / HBM_PEAK_GBS, 4)}
-                            for r, row in enumerate(ranks)]
+                            for r, row in enumerate(rows)]
     if gather is not None:
         line["gather"] = gather
-    if world == 1 and plan.is_fixed and args.schema == "rec128" and not args.no_large:
+    return line
+
+
+def main():
+    args = parse()
+    rc = launch_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
+    Engine = load_engine(args.engine) if args.engine else GpuEngine
+    dist, world, rank, local = dist_init(args, Engine.backend)
+    n = args.n if args.n is not None else (1 << 20 if world == 1 else 1 << 21)
+    engine = Engine(args, n, rank, world, local)
+    engine.dist = dist
+    elapsed, enc_ms, dec_ms = measure(engine, args)
+
+    # correctness of what was timed; on the 1-GPU headline config the stream
+    # also hashes to the reference's output
+    ok_rt = engine.round_trip_ok()
+    xdr, _ = engine.shard()
+    X = xdr.numel()
+    man = os.path.join(ROOT, "tests", "golden", "manifest.json")
+    hashes = json.load(open(man))["hashes"] if os.path.exists(man) else {}
+    bit_exact = None
+    if world == 1 and f"{args.schema}_{n}" in hashes:
+        bit_exact = hashlib.sha256(xdr.cpu().numpy().tobytes()).hexdigest() == hashes[f"{args.schema}_{n}"]["xdr"]
+
+    kern, alg_bytes, launches = engine.dominant(enc_ms, dec_ms)
+    achieved = alg_bytes / (float(np.mean(launches)) * 1e-3) / 1e9
+    rows = rank_rows(dist, world, [elapsed, float(np.mean(enc_ms)), float(np.mean(dec_ms)), float(X), achieved,
+                                   float(ok_rt)], engine.dev)
+    X_all = int(rows[:, 3].sum())
+    gather = None
+    if dist is not None and not args.no_gather:
+        gather = gather_leg(engine, dist, rank, world, X_all, X, rows, hashes, f"{args.schema}_mgpu_{n * world}")
+        if gather is not None and "bit_exact_vs_reference" in gather:
+            bit_exact = gather["bit_exact_vs_reference"]
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+    line = report(args, engine, world, rows, X, kern, alg_bytes, launches, enc_ms, dec_ms, bit_exact, gather)
+    if isinstance(engine, GpuEngine) and world == 1:
+        extra_legs(args, engine, line, alg_bytes)
+    print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def extra_legs(args, engine, line, alg_bytes):
+    """The legs beside the headline (1 GPU): the fixed path past the cache,
+    cold caches, record-marked messages, RPC headers, host-inclusive rates
+    with the PCIe ceiling, and the CPU reference on this host's cores."""
+    plan, mar, nat, heap, n = engine.plan, engine.mar, engine.nat, engine.heap, engine.n
+    if plan.is_fixed and args.schema == "rec128" and not args.no_large:
         try:
             line["large_batch_16m"] = large_batch(mar, nat.device)
         except Exception as e:  # reported, never fatal
             line["large_batch_16m"] = {"error": str(e)[:200]}
-    if world == 1 and args.cold and plan.is_fixed:
-        line["cold_cache"] = cold_cache(mar, nat, xdr, back, n, alg_bytes)
-        mar.check(s)
-    if world == 1 and args.msgs:
+    if args.cold and plan.is_fixed:
+        line["cold_cache"] = cold_cache(mar, nat, engine.xdr, engine.back, n, alg_bytes)
+        engine.check()
+    if args.msgs:
         line["messages"] = messages_leg(args.schema, plan, mar, nat, heap, n)
-    if world == 1 and args.rpc:
+    if args.rpc:
         line["rpc_headers"] = rpc_leg(nat.device)
-    if world == 1 and args.host_inclusive:
+    if args.host_inclusive:
         try:
             line["host_inclusive"] = (host_inclusive(mar, plan, nat, n, plan.fixed_size) if plan.is_fixed
                                       else host_inclusive_var(mar, plan, nat, heap, n))
         except Exception as e:  # reported, never fatal
             line["host_inclusive"] = {"error": str(e)[:200]}
-    if world == 1 and not args.no_cpu_baseline:
+    if not args.no_cpu_baseline:
         try:
             line["cpu_baseline"] = cpu_baseline(args.schema, n, args.cpu_threads)
         except Exception as e:
             line["cpu_baseline"] = {"error": str(e)[:200]}
-    print(json.dumps(line), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

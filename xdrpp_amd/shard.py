@@ -47,35 +47,53 @@ def gather_streams(dist, xdr, offsets, rank: int, world: int):
     """Gather every rank's XDR stream (uint8 tensor) and, for var-length
     plans, its record index (int64 tensor of n + 1 entries, or None) on
     rank 0.  Returns (stream, index) on rank 0 and (None, None) elsewhere;
-    index is None when `offsets` is None.  Shards may differ in length:
-    lengths are exchanged first and streams padded to the longest."""
+    index is None when `offsets` is None.
+
+    Shards may differ in length and record count: both are exchanged first
+    (one all_gather of two words), then every rank sends exactly its bytes
+    and rank 0 receives them straight into their place in the whole stream
+    (point-to-point sends and receives issued as one batch, so the root's
+    links work at once; no padding, no concatenation copy).  Each rank
+    rebases its own record index by the stream bytes of the ranks before it
+    and sends its entries (the last rank also the end), so rank 0 receives
+    the whole batch's index in place too."""
     import torch
 
     dev = xdr.device
-    ln = torch.tensor([xdr.numel()], dtype=torch.int64, device=dev)
-    lens = [torch.zeros_like(ln) for _ in range(world)]
-    dist.all_gather(lens, ln)
-    lens = [int(x.item()) for x in lens]
-    mx = max(lens)
-    buf = xdr
-    if xdr.numel() < mx:
-        buf = torch.zeros(mx, dtype=torch.uint8, device=dev)
-        buf[: xdr.numel()] = xdr
-    got = [torch.empty(mx, dtype=torch.uint8, device=dev) for _ in range(world)] if rank == 0 else None
-    dist.gather(buf, got, dst=0)
-    idx_parts = None
+    nrec = (offsets.numel() - 1) if offsets is not None else 0
+    mine = torch.tensor([xdr.numel(), nrec], dtype=torch.int64, device=dev)
+    every = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(every, mine)
+    lens = [int(e[0].item()) for e in every]
+    recs = [int(e[1].item()) for e in every]
+    base = sum(lens[:rank])
+    idx = None
     if offsets is not None:
-        idx_parts = ([torch.empty_like(offsets) for _ in range(world)] if rank == 0 else None)
-        dist.gather(offsets, idx_parts, dst=0)
+        last = rank == world - 1
+        idx = (offsets if last else offsets[:-1]) + base
+    ops = []
     if rank != 0:
+        if lens[rank]:
+            ops.append(dist.P2POp(dist.isend, xdr.contiguous(), 0))
+        if idx is not None and idx.numel():
+            ops.append(dist.P2POp(dist.isend, idx.contiguous(), 0))
+        for r in dist.batch_isend_irecv(ops) if ops else []:
+            r.wait()
         return None, None
-    stream = torch.cat([g[:k] for g, k in zip(got, lens)])
+    stream = torch.empty(sum(lens), dtype=torch.uint8, device=dev)
+    stream[:lens[0]].copy_(xdr)
     index = None
-    if idx_parts is not None:
-        base = 0
-        parts = []
-        for i, (part, k) in enumerate(zip(idx_parts, lens)):
-            parts.append(part[:-1] + base if i < world - 1 else part + base)
-            base += k
-        index = torch.cat(parts)
+    if offsets is not None:
+        index = torch.empty(sum(recs) + 1, dtype=torch.int64, device=dev)
+        index[:idx.numel()].copy_(idx)
+    for k in range(1, world):
+        b, rb = sum(lens[:k]), sum(recs[:k])
+        if lens[k]:
+            ops.append(dist.P2POp(dist.irecv, stream[b:b + lens[k]], k))
+        if index is not None:
+            cnt = recs[k] + (1 if k == world - 1 else 0)
+            if cnt:
+                ops.append(dist.P2POp(dist.irecv, index[rb:rb + cnt], k))
+    for r in dist.batch_isend_irecv(ops) if ops else []:
+        r.wait()
     return stream, index
