@@ -100,3 +100,28 @@ def test_aot_code_object_runs(dev, name):
     assert np.array_equal(r2.xdr.cpu().numpy(), want)
     A.check(L.xdrg_plan_get_info(p.handle, C.byref(info)), "xdrg_plan_get_info")
     assert info.specialized == 1
+
+
+@pytest.mark.gpu
+def test_foreign_code_object_refused(dev):
+    """A code object compiled from another plan's source (here rpc's, given
+    to recvar) is refused at load: the plan runs on the interpreter and its
+    bytes stay the reference's (spec.cpp checks xdrg_spec_src_hash)."""
+    import numpy as np
+    import torch
+    from conftest import golden
+    co = os.path.join(AOT, "rpc.co")
+    if not os.path.exists(co):
+        pytest.skip("aot code objects not built")
+    code = open(co, "rb").read()
+    p = M.Plan(S.ALL["recvar"])
+    L = A.lib()
+    assert L.xdrg_plan_load_kernels(p.handle, code, len(code)) == A.OK
+    n = 1024
+    mar = M.Marshaler(p, dev)
+    r = mar.encode(torch.from_numpy(golden("recvar", n, "native").copy()).to(dev), n,
+                   torch.from_numpy(golden("recvar", n, "heap").copy()).to(dev))
+    assert np.array_equal(r.xdr.cpu().numpy(), golden("recvar", n, "xdr"))
+    info = A.XdrgPlanInfo()
+    A.check(L.xdrg_plan_get_info(p.handle, C.byref(info)), "xdrg_plan_get_info")
+    assert info.specialized == 0

@@ -277,3 +277,34 @@ def test_gpu_max_frames(dev):
     with pytest.raises(M.XdrStackOverflow) as e:
         mar.encode(_dev(nat, dev), 1, _dev(heap, dev))
     assert (e.value.record, e.value.op) == (0, 1)
+
+
+@pytest.mark.parametrize("name", TYPES)
+def test_host_index_records(gold, name):
+    """decode()'s host fallback finds the same record boundaries as the
+    encoder (the device index hands streams of records nested deeper than
+    its frames, or longer than its window, back to it)."""
+    from xdrpp_amd import marshal as M
+    chains, wire, offs, recs = chains_of(gold, name)
+    x = np.frombuffer(b"".join(wire), dtype=np.uint8)
+    got = M.host_index_records(plan_of(name), x, len(chains))
+    assert np.array_equal(got, offs)
+    # a stream cut short: the record it runs out in gets [off, len), the rest [len, len)
+    cut = x[:int(offs[1]) + 8]
+    got = M.host_index_records(plan_of(name), cut, len(chains))
+    assert list(got[:2]) == list(offs[:2]) and (got[2:] == cut.size).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", TYPES)
+def test_gpu_decode_without_offsets(gold, dev, name):
+    """decode() with no record index: the device index hands these chains
+    back (INDEX_LONG), the host walk indexes them, the decode matches."""
+    from xdrpp_amd import marshal as M
+    chains, wire, offs, recs = chains_of(gold, name)
+    n = len(chains)
+    mar = M.Marshaler(M.Plan(S.CONTAINERS.get(name) or getattr(S, name)), dev)
+    x = _dev(np.frombuffer(b"".join(wire), dtype=np.uint8), dev)
+    a, ha = mar.decode(x, n, _dev(offs.astype(np.int64), dev))
+    b, hb = mar.decode(x, n)
+    assert np.array_equal(a.cpu().numpy(), b.cpu().numpy()) and np.array_equal(ha.cpu().numpy(), hb.cpu().numpy())

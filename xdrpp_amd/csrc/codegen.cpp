@@ -863,7 +863,16 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
       << "  var_decode_body<plan_walk, " << (cp ? "true" : "false")
       << ", true, " << (regs ? p.stride / 4 : 0) << ">(plan_walk{}, xdr, len, offsets, n, native, stride, heap,\n"
       << "      stack_limit, C, ebase, F, mark, err);\n}\n\n";
-  info.source = s.str();
+  // the source's own hash, defined in it: spec_get refuses a code object
+  // (kernel cache file, or one attached with xdrg_plan_load_kernels) that
+  // was not compiled from this plan's source
+  std::string src = s.str();
+  uint64_t h = 1469598103934665603ull;  // FNV-1a
+  for (unsigned char ch : src) h = (h ^ ch) * 1099511628211ull;
+  info.src_hash = h;
+  src += "extern \"C\" __device__ __attribute__((used)) unsigned long long xdrg_spec_src_hash = " +
+         std::to_string(h) + "ull;\n";
+  info.source = std::move(src);
   return true;
 }
 

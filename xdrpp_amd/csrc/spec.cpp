@@ -29,13 +29,30 @@ namespace {
 // include/xdrgpu.h).
 #include "_embed.inc"
 
-const char *kOpts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+const char *kOptsBase[] = {"-O3", "-std=c++17"};
+
+// --offload-arch of the current device (gcnArchName without its feature
+// suffix); gfx950 when the device cannot be asked.
+std::string device_arch() {
+  int dev = 0;
+  hipDeviceProp_t prop;
+  if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess) {
+    std::string a = prop.gcnArchName;
+    const size_t k = a.find(':');
+    if (k != std::string::npos) a.resize(k);
+    if (!a.empty()) return a;
+  }
+  return "gfx950";
+}
 
 uint64_t fnv1a(const std::string &s, uint64_t h = 1469598103934665603ull) {
   for (unsigned char c : s) h = (h ^ c) * 1099511628211ull;
   return h;
 }
 
+// $XDRG_KERNEL_CACHE, else kernel_cache/ beside libxdrgpu.so; empty (no
+// cache) when neither is known -- never a shared directory such as /tmp,
+// where another user's file would be loaded as this plan's kernels.
 std::string cache_dir() {
   if (const char *e = getenv("XDRG_KERNEL_CACHE")) return e;
   Dl_info di;
@@ -44,13 +61,14 @@ std::string cache_dir() {
     const size_t k = so.rfind('/');
     return (k == std::string::npos ? std::string(".") : so.substr(0, k)) + "/kernel_cache";
   }
-  return "/tmp/xdrgpu_kernel_cache";
+  return "";
 }
 
-std::string cache_key(const std::string &src) {
+std::string cache_key(const std::string &src, const std::string &arch) {
   uint64_t h = fnv1a(src);
   for (const char *hd : kEmbedText) h = fnv1a(hd, h);
-  for (const char *o : kOpts) h = fnv1a(o, h);
+  for (const char *o : kOptsBase) h = fnv1a(o, h);
+  h = fnv1a(arch, h);
   char b[32];
   snprintf(b, sizeof b, "%016llx", static_cast<unsigned long long>(h));
   return b;
@@ -75,14 +93,16 @@ void write_file(const std::string &path, const char *data, size_t n) {
 }
 
 // hiprtc: source -> gfx950 code object.
-bool rtc_compile(const std::string &src, std::vector<char> &code, std::string &log) {
+bool rtc_compile(const std::string &src, const std::string &arch, std::vector<char> &code, std::string &log) {
   hiprtcProgram prog;
   if (hiprtcCreateProgram(&prog, src.c_str(), "xdrg_spec.hip", kEmbedCount, kEmbedText, kEmbedName) !=
       HIPRTC_SUCCESS) {
     log = "hiprtcCreateProgram failed";
     return false;
   }
-  const hiprtcResult rc = hiprtcCompileProgram(prog, sizeof kOpts / sizeof kOpts[0], kOpts);
+  const std::string oa = "--offload-arch=" + arch;
+  const char *opts[] = {oa.c_str(), kOptsBase[0], kOptsBase[1]};
+  const hiprtcResult rc = hiprtcCompileProgram(prog, sizeof opts / sizeof opts[0], opts);
   size_t ls = 0;
   hiprtcGetProgramLogSize(prog, &ls);
   log.assign(ls, '\0');
@@ -116,19 +136,21 @@ int spec_build(const xdrg_plan &cp) {
       s.state.store(-1, std::memory_order_release);
       return -1;
     }
-    const std::string dir = cache_dir(), key = cache_key(s.info.source);
+    const std::string arch = device_arch(), dir = cache_dir(), key = cache_key(s.info.source, arch);
     const std::string co = dir + "/" + key + ".co";
-    if (!read_file(co, s.code)) {
+    if (dir.empty() || !read_file(co, s.code)) {
       std::string log;
-      if (!rtc_compile(s.info.source, s.code, log)) {
+      if (!rtc_compile(s.info.source, arch, s.code, log)) {
         s.log = log;
         s.code.clear();
         s.state.store(-1, std::memory_order_release);
         return -1;
       }
-      mkdir(dir.c_str(), 0755);  // a read-only tree just means no cache
-      write_file(co, s.code.data(), s.code.size());
-      write_file(dir + "/" + key + ".hip", s.info.source.data(), s.info.source.size());
+      if (!dir.empty()) {
+        mkdir(dir.c_str(), 0755);  // a read-only tree just means no cache
+        write_file(co, s.code.data(), s.code.size());
+        write_file(dir + "/" + key + ".hip", s.info.source.data(), s.info.source.size());
+      }
     }
   }
   s.state.store(1, std::memory_order_release);
@@ -142,30 +164,42 @@ const spec_module *spec_get(const xdrg_plan &cp) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kSpecDevices) return nullptr;
   if (s.loaded[dev].load(std::memory_order_acquire)) return &s.dev[dev];
+  if (s.failed[dev].load(std::memory_order_acquire)) return nullptr;
   std::lock_guard<std::mutex> g(s.mu);
   if (s.loaded[dev].load(std::memory_order_relaxed)) return &s.dev[dev];
+  if (s.failed[dev].load(std::memory_order_relaxed)) return nullptr;
+  // a load that fails is not retried on every launch: the plan runs on the
+  // interpreter on this device from now on
+  auto fail = [&](hipModule_t m, const char *why) -> const spec_module * {
+    if (m) (void)hipModuleUnload(m);
+    s.log = why;
+    s.failed[dev].store(true, std::memory_order_release);
+    return nullptr;
+  };
   hipModule_t m = nullptr;
-  if (hipModuleLoadData(&m, s.code.data()) != hipSuccess) return nullptr;
+  if (hipModuleLoadData(&m, s.code.data()) != hipSuccess)
+    return fail(nullptr, "specialized kernels: the code object does not load on this device");
   spec_module &d = s.dev[dev];
   hipFunction_t f[5] = {};
   const char *names[5] = {"xdrg_spec_size", "xdrg_spec_encode", "xdrg_spec_decode", "xdrg_spec_decode_copy",
                           "xdrg_spec_ix_seg"};
   for (int i = 0; i < 5; ++i)
-    if (hipModuleGetFunction(&f[i], m, names[i]) != hipSuccess) {
-      (void)hipModuleUnload(m);
-      return nullptr;
-    }
-  // a code object of another kernel interface (an older build's AOT file)
+    if (hipModuleGetFunction(&f[i], m, names[i]) != hipSuccess)
+      return fail(m, "specialized kernels: the code object lacks a kernel");
+  // a code object of another kernel interface (an older build's AOT file),
+  // or of another plan's source (a foreign cache file or attached object,
+  // whose hard-coded offsets would silently write wrong bytes)
   void *iv = nullptr;
   size_t ib = 0;
   unsigned iface = 0;
   if (hipModuleGetGlobal(&iv, &ib, m, "xdrg_spec_iface") != hipSuccess || ib != sizeof iface ||
-      hipMemcpyDtoH(&iface, iv, sizeof iface) != hipSuccess || iface != kSpecIface) {
-    (void)hipModuleUnload(m);
-    s.log = "specialized kernels: code object of another kernel interface (rebuild it from xdrg_plan_kernel_source)";
-    s.state.store(-1, std::memory_order_release);
-    return nullptr;
-  }
+      hipMemcpyDtoH(&iface, iv, sizeof iface) != hipSuccess || iface != kSpecIface)
+    return fail(m, "specialized kernels: code object of another kernel interface (rebuild it from "
+                   "xdrg_plan_kernel_source)");
+  unsigned long long sh = 0;
+  if (hipModuleGetGlobal(&iv, &ib, m, "xdrg_spec_src_hash") != hipSuccess || ib != sizeof sh ||
+      hipMemcpyDtoH(&sh, iv, sizeof sh) != hipSuccess || sh != s.info.src_hash)
+    return fail(m, "specialized kernels: code object compiled from another plan's source");
   d.module = m;
   d.f_size = f[0];
   d.f_enc = f[1];

@@ -25,6 +25,7 @@ struct spec_info {
   uint64_t max_chunks = 0;  // 16-byte chunks those slots hold per record (bounds)
   bool dec_regs = false;  // the decode walks into registers: no native tile in LDS
   bool word_list = false; // the encode walks once into a word list (no walk per window)
+  uint64_t src_hash = 0;  // FNV-1a of the source (before the line that defines it)
 };
 
 // Kernels of one plan on one device.
@@ -44,6 +45,7 @@ struct spec_state {
   std::vector<char> code;  // gfx950 code object (ELF)
   std::string log;         // compile log of a failed build
   std::atomic<bool> loaded[kSpecDevices] = {};
+  std::atomic<bool> failed[kSpecDevices] = {};  // the module did not load there: interpreter
   spec_module dev[kSpecDevices];
 };
 

@@ -2373,7 +2373,10 @@ int xdrg_plan_get_info(const xdrg_plan *p, xdrg_plan_info *info) {
   info->has_checks = p->has_checks ? 1u : 0u;
   info->max_record_bytes = p->max_record_bytes;
   info->group_records = p->path == XDRG_PATH_FIXED_LDS && !p->has_checks ? p->enc.grp_G : 0u;
-  info->specialized = p->spec.state.load() == 1 ? 1u : 0u;
+  int dev = 0;
+  const bool failed_here = hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < kSpecDevices &&
+                           p->spec.failed[dev].load();
+  info->specialized = p->spec.state.load() == 1 && !failed_here ? 1u : 0u;
   return XDRG_OK;
 }
 

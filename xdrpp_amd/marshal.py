@@ -15,6 +15,7 @@ from __future__ import annotations
 import ctypes as C
 from dataclasses import dataclass
 
+import numpy as np
 import torch
 
 from . import _abi as A
@@ -290,10 +291,18 @@ class Marshaler:
                stack_limit: int = A.DEFAULT_STACK_LIMIT):
         """= xdr_from_opaque(bytes, r0, ..., rn-1) (marshal.h:299-306).
         Var plans without `offsets` index the records on the device first
-        (index_records).  Returns (native uint8 tensor [n*stride], heap
-        uint8 tensor or None)."""
+        (index_records); a stream the device index hands back (a record
+        longer than its window, or nested deeper than its frames) is walked
+        on the host instead, as the C++ layer does.  Returns (native uint8
+        tensor [n*stride], heap uint8 tensor or None)."""
         if offsets is None and not self.plan.is_fixed:
-            offsets = self.index_records(xdr, n)
+            try:
+                offsets = self.index_records(xdr, n)
+            except XdrRuntimeError as e:
+                if e.code != A.ERR_INDEX_LONG:
+                    raise
+                offs = host_index_records(self.plan.cp, xdr.cpu().numpy(), n)
+                offsets = torch.from_numpy(offs.view(np.int64)).to(self.device)
         s = _stream()
         native = torch.zeros(max(n, 1) * self.plan.stride, dtype=torch.uint8, device=self.device)
         heap = None
@@ -356,6 +365,104 @@ class Marshaler:
                                 stack_limit=stack_limit, stream=s)
         self.check(s)
         return native[:n * self.plan.stride], heap
+
+
+def host_index_records(cp, xdr: np.ndarray, n: int) -> np.ndarray:
+    """The record boundaries xdr_from_opaque's walk finds in n records
+    concatenated in `xdr` (marshal.h:299-306), walked on the host: lengths,
+    counts and discriminants only.  Where the bytes run out or a
+    discriminant is bad, record k gets [off[k], len) and the rest
+    [len, len), so the decode reports the reference's error for record k;
+    trailing bytes leave off[n] < len.  The fallback of decode() for the
+    streams the device index hands back (include/xdrpp_gpu.hh
+    index_records is the C++ layer's); uint64 [n + 1]."""
+    ops, table = cp.ops, cp.table
+    L = int(xdr.size)
+    buf = np.ascontiguousarray(xdr, dtype=np.uint8).tobytes()
+
+    def word(p):
+        return int.from_bytes(buf[p:p + 4], "big")
+
+    def elem_wire(e):
+        k = int(e["kind"])
+        return 8 if k == A.OP_U64 else ((int(e["arg0"]) + 3) & ~3) if k == A.OP_OPAQUE else 4
+
+    def skip(p):  # one record from p: the end, or None
+        stack = []  # [elements left, VECTOR pc]
+        pc = 0
+        while True:
+            o = ops[pc]
+            k = int(o["kind"])
+            if k == A.OP_END:
+                if not stack:
+                    return p
+                if stack[-1][0]:
+                    stack[-1][0] -= 1
+                    pc = int(ops[stack[-1][1]]["arg4"])
+                    if p > L:
+                        return None
+                else:
+                    pc = stack.pop()[1] + 1
+                continue
+            if k == A.OP_JUMP:
+                pc = int(o["arg0"])
+                continue
+            if k == A.OP_U64:
+                p += 8
+            elif k == A.OP_OPAQUE:
+                p += (int(o["arg0"]) + 3) & ~3
+            elif k in (A.OP_VAROPAQUE, A.OP_STRING):
+                if p + 4 > L:
+                    return None
+                p += 4 + ((word(p) + 3) & ~3)
+            elif k == A.OP_VECTOR:
+                if p + 4 > L:
+                    return None
+                cnt = word(p)
+                p += 4
+                if int(o["flags"]) & A.F_SUB:
+                    if cnt:
+                        if p > L:
+                            return None
+                        stack.append([cnt - 1, pc])
+                        pc = int(o["arg4"])
+                    else:
+                        pc += 1
+                    continue
+                nb = int(o["arg2"])
+                p += cnt * sum(elem_wire(ops[pc + j]) for j in range(1, nb + 1))
+                pc += 1 + nb
+                continue
+            elif k == A.OP_UNION:
+                if p + 4 > L:
+                    return None
+                d = word(p)
+                p += 4
+                tgt = None
+                for c in range(int(o["arg3"])):
+                    if int(table[int(o["arg2"]) + 2 * c]) == d:
+                        tgt = int(table[int(o["arg2"]) + 2 * c + 1])
+                        break
+                if tgt is None and int(o["flags"]) & A.F_DEFAULT:
+                    tgt = int(o["arg4"])
+                if tgt is None:
+                    return None
+                pc = tgt
+                continue
+            else:
+                p += 4
+            pc += 1
+
+    off = np.full(n + 1, L, dtype=np.uint64)
+    p = 0
+    for r in range(n):
+        off[r] = min(p, L)
+        q = skip(p)
+        if q is None or q > L:
+            return off
+        p = q
+    off[n] = p
+    return off
 
 
 class _IndexErrorPlan:
