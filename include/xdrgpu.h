@@ -11,6 +11,8 @@
  *                            :575-675 unions; xdrpp/types.h:676-730)
  *   xdrg_encode           <- xdr_to_opaque(r0, ..., rN-1)   xdrpp/marshal.h:264-272
  *                            (xdr_generic_put, xdrpp/marshal.h:84-137)
+ *   xdrg_encode_sizes /   <- its two halves: xdr_argpack_size, then the put
+ *   xdrg_encode_sized        xdrpp/marshal.h:223-234, :264-272
  *   xdrg_decode           <- xdr_from_opaque(bytes, r...)    xdrpp/marshal.h:299-306
  *                            (xdr_generic_get, xdrpp/marshal.h:142-211)
  *   xdrg_encode_msgs      <- xdr_to_msg(r) per record       xdrpp/marshal.h:252-260
@@ -64,7 +66,7 @@
 extern "C" {
 #endif
 
-#define XDRG_ABI_VERSION 5
+#define XDRG_ABI_VERSION 6
 
 /* ---------------------------------------------------------------------- */
 /* Plan ops: a flat, wire-ordered walk of xdr_traits<T>::save.             */
@@ -353,6 +355,31 @@ int xdrg_encode(const xdrg_plan *plan, const void *d_native, uint64_t n,
                 uint64_t xdr_capacity, uint64_t *d_offsets,
                 uint32_t stack_limit, void *d_workspace, size_t workspace_bytes,
                 xdrg_status *d_status, void *stream);
+
+/*
+ * xdrg_encode (msgs = 0) or xdrg_encode_msgs (msgs = 1) in two halves, for
+ * callers that size the output from the records, as xdr_to_opaque does
+ * (xdr_argpack_size, then xdr_generic_put; xdrpp/marshal.h:264-272):
+ *   xdrg_encode_sizes  the size pass alone (xdr_size of every record, their
+ *                      scan into the workspace); the total wire bytes land
+ *                      in d_status->total_bytes and size errors (a bad
+ *                      discriminant) in d_status.  No output is written.
+ *   xdrg_encode_sized  the encode over the sizes the first half left in the
+ *                      same workspace, with the same status block (not
+ *                      re-initialised), records, heap and msgs flag: the
+ *                      size pass does not run again.  Plans whose element
+ *                      subroutines can nest past XDRG_SUB_FRAMES run both
+ *                      halves here (their deep passes keep per-call lists).
+ * Arguments as xdrg_encode / xdrg_encode_msgs; d_offsets is required by the
+ * second half for every plan with msgs, for var plans without.
+ */
+int xdrg_encode_sizes(const xdrg_plan *plan, const void *d_native, uint64_t n,
+                      const uint8_t *d_heap, uint64_t heap_len, uint32_t stack_limit, int msgs,
+                      void *d_workspace, size_t workspace_bytes, xdrg_status *d_status, void *stream);
+int xdrg_encode_sized(const xdrg_plan *plan, const void *d_native, uint64_t n,
+                      const uint8_t *d_heap, uint64_t heap_len, void *d_out, uint64_t out_capacity,
+                      uint64_t *d_offsets, uint32_t stack_limit, int msgs, void *d_workspace,
+                      size_t workspace_bytes, xdrg_status *d_status, void *stream);
 
 /*
  * Decode n records from an XDR stream of xdr_len bytes.

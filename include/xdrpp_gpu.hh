@@ -45,6 +45,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstring>
 #include <memory>
@@ -99,6 +100,32 @@ struct api_error : std::runtime_error {
 namespace detail {
 
 inline std::uint32_t align_up(std::uint32_t x, std::uint32_t a) { return (x + a - 1) / a * a; }
+
+// Buffers the batch calls allocate (pinned host and device), counted so
+// that a test can see a context reach its steady state (no allocation).
+inline std::atomic<std::size_t> &alloc_count() {
+  static std::atomic<std::size_t> c{0};
+  return c;
+}
+
+//! Pinned (page-locked) host memory for std::vector: the staged records and
+//! heaps are copied to and from the device by DMA, asynchronously.
+template <typename T> struct pinned_allocator {
+  using value_type = T;
+  pinned_allocator() = default;
+  template <typename U> pinned_allocator(const pinned_allocator<U> &) {}
+  T *allocate(std::size_t n) {
+    void *p = nullptr;
+    const hipError_t e = hipHostMalloc(&p, std::max<std::size_t>(n, 1) * sizeof(T), hipHostMallocDefault);
+    if (e != hipSuccess) throw api_error(XDRG_EHIP, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+    ++alloc_count();
+    return static_cast<T *>(p);
+  }
+  void deallocate(T *p, std::size_t) { (void)hipHostFree(p); }
+  template <typename U> bool operator==(const pinned_allocator<U> &) const { return true; }
+  template <typename U> bool operator!=(const pinned_allocator<U> &) const { return false; }
+};
+using host_bytes = std::vector<std::uint8_t, pinned_allocator<std::uint8_t>>;
 
 // ---------------------------------------------------------------- type tests
 template <typename T> struct bytes_kind {
@@ -541,9 +568,9 @@ struct cursor {
   }
 };
 
-struct stager : cursor {
+template <typename V> struct stager : cursor {  // V: the heap's byte vector type
   std::uint8_t *rec = nullptr;  // the record, or (in_heap) heap offset `roff`
-  std::vector<std::uint8_t> *heap;
+  V *heap;
   bool in_heap = false;
   std::uint64_t roff = 0;
   // the object's bytes, looked up at every write: staging elements grows the heap
@@ -582,7 +609,7 @@ struct stager : cursor {
       const std::uint32_t entry = (o.flags & XDRG_F_SUB) ? o.arg4 : pc + 1;
       std::uint32_t i = 0;
       for (const auto &e : f) {
-        stager s2;
+        stager<V> s2;
         s2.ops = ops;
         s2.table = table;
         s2.pc = entry;
@@ -736,14 +763,26 @@ inline void abicheck(int rc, const char *what) {
   }
 }
 
-template <typename T> struct dev_buf {
-  T *p = nullptr;
-  explicit dev_buf(std::size_t n) {
-    if (n) hipcheck(hipMalloc(reinterpret_cast<void **>(&p), n * sizeof(T)), "hipMalloc");
+//! A device buffer that only grows: reused from call to call.
+struct grow_buf {
+  void *p = nullptr;
+  std::size_t cap = 0;
+  template <typename T> T *get(std::size_t n) {
+    const std::size_t bytes = std::max<std::size_t>(n * sizeof(T), 16);
+    if (bytes > cap) {
+      if (p) hipcheck(hipFree(p), "hipFree");  // hipFree waits for the work using it
+      p = nullptr;
+      cap = 0;
+      hipcheck(hipMalloc(&p, bytes), "hipMalloc");
+      ++alloc_count();
+      cap = bytes;
+    }
+    return static_cast<T *>(p);
   }
-  ~dev_buf() { if (p) (void)hipFree(p); }
-  dev_buf(const dev_buf &) = delete;
-  dev_buf &operator=(const dev_buf &) = delete;
+  grow_buf() = default;
+  grow_buf(const grow_buf &) = delete;
+  grow_buf &operator=(const grow_buf &) = delete;
+  ~grow_buf() { if (p) (void)hipFree(p); }
 };
 
 }  // namespace detail
@@ -867,29 +906,92 @@ template <typename T> const batch_plan<T> &plan_for() { return batch_plan<T>::ge
 
 // ---------------------------------------------------------------- staging
 //! Host staging of a batch: records in the staged layout + payload heap.
-struct staged_batch {
-  std::vector<std::uint8_t> native;
-  std::vector<std::uint8_t> heap;
+//! (A context stages into pinned memory, so that the copies to the device
+//! run asynchronously.)
+template <typename A = std::allocator<std::uint8_t>> struct basic_staged_batch {
+  std::vector<std::uint8_t, A> native;
+  std::vector<std::uint8_t, A> heap;
 };
+using staged_batch = basic_staged_batch<>;
 
-template <typename T> staged_batch stage(const T *recs, std::size_t n) {
+//! Stage n records into b, reusing its buffers' capacity.
+template <typename T, typename A> void stage_into(basic_staged_batch<A> &b, const T *recs, std::size_t n) {
   const batch_plan<T> &P = plan_for<T>();
-  staged_batch b;
   b.native.assign(n * P.stride(), 0);
+  b.heap.clear();
   if (P.identity()) {
-    std::memcpy(b.native.data(), recs, n * sizeof(T));
-    return b;
+    if (n) std::memcpy(b.native.data(), recs, n * sizeof(T));
+    return;
   }
   for (std::size_t i = 0; i < n; ++i) {
-    detail::stager s;
+    detail::stager<std::vector<std::uint8_t, A>> s;
     s.ops = P.ops().data();
     s.table = P.table().data();
     s.rec = b.native.data() + i * P.stride();
     s.heap = &b.heap;
     s(recs[i]);
   }
+}
+
+template <typename T> staged_batch stage(const T *recs, std::size_t n) {
+  staged_batch b;
+  stage_into(b, recs, n);
   return b;
 }
+
+//! The buffers of the batch calls -- device buffers and pinned host staging
+//! that only grow, so a context serving batches of a steady size allocates
+//! nothing after its first call -- used by one thread at a time.  The
+//! calls that take no context use their thread's default one (per device).
+class context {
+ public:
+  context() = default;
+  context(const context &) = delete;
+  context &operator=(const context &) = delete;
+  //! Device and pinned buffers allocated so far by every context.
+  static std::size_t allocations() { return detail::alloc_count(); }
+
+  // device buffers
+  detail::grow_buf d_nat, d_heap, d_xdr, d_off, d_ws, d_st, d_aux, d_cnt;
+  // pinned host staging
+  basic_staged_batch<detail::pinned_allocator<std::uint8_t>> staged;
+  detail::host_bytes h_in, h_out, h_heap, h_off;
+  xdrg_status *status() { return d_st.get<xdrg_status>(1); }
+};
+
+//! The calling thread's default context on the current device.  (Never
+//! destroyed: its buffers must not be freed after the HIP runtime's own
+//! teardown at exit.)
+inline context &default_context() {
+  thread_local std::vector<context *> per_device;
+  int d = 0;
+  detail::hipcheck(hipGetDevice(&d), "hipGetDevice");
+  if (per_device.size() <= static_cast<std::size_t>(d)) per_device.resize(d + 1, nullptr);
+  if (!per_device[d]) per_device[d] = new context();
+  return *per_device[d];
+}
+
+namespace detail {
+//! H2D of a staged batch into the context's device buffers.
+inline void upload(context &c, hipStream_t s, std::uint8_t **nat, std::uint8_t **heap) {
+  *nat = c.d_nat.get<std::uint8_t>(c.staged.native.size());
+  *heap = c.staged.heap.empty() ? nullptr : c.d_heap.get<std::uint8_t>(c.staged.heap.size());
+  if (!c.staged.native.empty())
+    hipcheck(hipMemcpyAsync(*nat, c.staged.native.data(), c.staged.native.size(), hipMemcpyHostToDevice, s), "H2D");
+  if (*heap)
+    hipcheck(hipMemcpyAsync(*heap, c.staged.heap.data(), c.staged.heap.size(), hipMemcpyHostToDevice, s), "H2D");
+}
+//! Stage host bytes into pinned memory and copy them to a device buffer.
+inline std::uint8_t *upload_bytes(context &c, grow_buf &d, const void *bytes, std::size_t len, hipStream_t s) {
+  std::uint8_t *p = d.get<std::uint8_t>(len);
+  if (len) {
+    c.h_in.resize(len);
+    std::memcpy(c.h_in.data(), bytes, len);
+    hipcheck(hipMemcpyAsync(p, c.h_in.data(), len, hipMemcpyHostToDevice, s), "H2D");
+  }
+  return p;
+}
+}  // namespace detail
 
 template <typename T>
 void unstage(const std::uint8_t *native, const std::uint8_t *heap, std::size_t n, T *out) {
@@ -1034,153 +1136,175 @@ std::vector<std::uint64_t> index_records(const std::uint8_t *xdr, std::size_t le
 }
 
 // ------------------------------------------------------------ batch calls
-//! xdr::xdr_to_opaque(recs[0], ..., recs[n-1]) on the GPU.  Host in, host
-//! out (pinned staging is the caller's business for peak PCIe rates; the
-//! device-resident entry point is xdrg_encode).
-template <typename T>
-opaque_vec<> to_opaque_batch(const T *recs, std::size_t n, hipStream_t s = nullptr) {
+namespace detail {
+//! Read the status block (waits for the stream); raise on a data error.
+template <typename T> xdrg_error read_status(context &c, hipStream_t s, bool raise_it = true) {
+  xdrg_error e{};
+  abicheck(xdrg_status_read(c.status(), s, &e), "xdrg_status_read");
+  if (raise_it && e.code) plan_for<T>().raise(e);
+  return e;
+}
+
+//! The batch encoded on the device: the context's d_xdr holds `total`
+//! bytes, d_off the record (msgs: message) offsets.  One size pass: the
+//! output is sized by xdrg_encode_sizes, as xdr_to_opaque sizes the
+//! argument pack (marshal.h:264-268), and xdrg_encode_sized encodes over it.
+template <typename T> std::size_t encode_on_device(context &c, const T *recs, std::size_t n, bool msgs,
+                                                   hipStream_t s) {
   const batch_plan<T> &P = plan_for<T>();
-  staged_batch b = stage(recs, n);
-  detail::dev_buf<std::uint8_t> d_nat(b.native.size()), d_heap(b.heap.size());
-  detail::dev_buf<xdrg_status> d_st(1);
-  detail::hipcheck(hipMemcpyAsync(d_nat.p, b.native.data(), b.native.size(), hipMemcpyHostToDevice, s), "H2D");
-  if (!b.heap.empty())
-    detail::hipcheck(hipMemcpyAsync(d_heap.p, b.heap.data(), b.heap.size(), hipMemcpyHostToDevice, s), "H2D");
-  detail::abicheck(xdrg_status_init(d_st.p, s), "xdrg_status_init");
-  std::size_t total = std::size_t(P.fixed_size()) * n;
+  stage_into(c.staged, recs, n);
+  std::uint8_t *nat = nullptr, *heap = nullptr;
+  upload(c, s, &nat, &heap);
+  const std::size_t hl = c.staged.heap.size();
+  abicheck(xdrg_status_init(c.status(), s), "xdrg_status_init");
   const std::size_t ws_bytes = xdrg_workspace_size(P.handle(), n);
-  detail::dev_buf<std::uint8_t> ws(ws_bytes);
-  detail::dev_buf<std::uint64_t> d_off(P.fixed() ? 0 : n + 1);
-  if (!P.fixed()) {  // size pass for the output capacity (xdr_argpack_size)
-    detail::dev_buf<std::uint32_t> d_sz(n);
-    detail::abicheck(xdrg_serial_sizes(P.handle(), d_nat.p, n, b.heap.empty() ? nullptr : d_heap.p,
-                                       b.heap.size(), d_sz.p, marshaling_stack_limit, d_st.p, s),
-                     "xdrg_serial_sizes");
-    std::vector<std::uint32_t> sz(n);
-    if (n) detail::hipcheck(hipMemcpyAsync(sz.data(), d_sz.p, n * 4, hipMemcpyDeviceToHost, s), "D2H");
-    xdrg_error e{};
-    detail::abicheck(xdrg_status_read(d_st.p, s, &e), "xdrg_status_read");
-    if (e.code) P.raise(e);
-    total = 0;
-    for (auto v : sz) total += v;
+  void *ws = c.d_ws.get<std::uint8_t>(ws_bytes);
+  std::uint64_t *off = c.d_off.get<std::uint64_t>(n + 1);
+  std::size_t total = (std::size_t(P.fixed_size()) + (msgs ? 4 : 0)) * n;
+  if (!P.fixed() || msgs) {
+    abicheck(xdrg_encode_sizes(P.handle(), nat, n, heap, hl, marshaling_stack_limit, msgs, ws, ws_bytes,
+                               c.status(), s),
+             "xdrg_encode_sizes");
+    total = read_status<T>(c, s).total_bytes;
   }
-  detail::dev_buf<std::uint8_t> d_xdr(total);
-  detail::abicheck(xdrg_encode(P.handle(), d_nat.p, n, b.heap.empty() ? nullptr : d_heap.p, b.heap.size(),
-                               d_xdr.p, total, d_off.p, marshaling_stack_limit, ws.p, ws_bytes, d_st.p, s),
-                   "xdrg_encode");
+  std::uint8_t *out = c.d_xdr.get<std::uint8_t>(total);
+  abicheck(xdrg_encode_sized(P.handle(), nat, n, heap, hl, out, total, (P.fixed() && !msgs) ? nullptr : off,
+                             marshaling_stack_limit, msgs, ws, ws_bytes, c.status(), s),
+           "xdrg_encode_sized");
+  return total;
+}
+}  // namespace detail
+
+//! xdr::xdr_to_opaque(recs[0], ..., recs[n-1]) on the GPU.  Host in, host
+//! out, through the context's pinned staging (the device-resident entry
+//! point is xdrg_encode).
+template <typename T>
+opaque_vec<> to_opaque_batch(context &c, const T *recs, std::size_t n, hipStream_t s = nullptr) {
+  const std::size_t total = detail::encode_on_device(c, recs, n, false, s);
+  c.h_out.resize(total);
+  if (total)
+    detail::hipcheck(hipMemcpyAsync(c.h_out.data(), c.d_xdr.p, total, hipMemcpyDeviceToHost, s), "D2H");
+  detail::read_status<T>(c, s);
   opaque_vec<> out;
   out.resize(total);
-  if (total) detail::hipcheck(hipMemcpyAsync(out.data(), d_xdr.p, total, hipMemcpyDeviceToHost, s), "D2H");
-  xdrg_error e{};
-  detail::abicheck(xdrg_status_read(d_st.p, s, &e), "xdrg_status_read");
-  if (e.code) P.raise(e);
+  if (total) std::memcpy(out.data(), c.h_out.data(), total);
   return out;
+}
+template <typename T>
+opaque_vec<> to_opaque_batch(const T *recs, std::size_t n, hipStream_t s = nullptr) {
+  return to_opaque_batch(default_context(), recs, n, s);
 }
 
 //! xdr::xdr_from_opaque(bytes, out[0], ..., out[n-1]) on the GPU.
 template <typename T>
-void from_opaque_batch(const void *bytes, std::size_t len, T *out, std::size_t n,
+void from_opaque_batch(context &c, const void *bytes, std::size_t len, T *out, std::size_t n,
                        hipStream_t s = nullptr) {
   const batch_plan<T> &P = plan_for<T>();
   const auto *x = static_cast<const std::uint8_t *>(bytes);
-  detail::dev_buf<std::uint8_t> d_xdr(len);
-  detail::dev_buf<std::uint8_t> d_nat(n * P.stride());
-  detail::dev_buf<xdrg_status> d_st(1);
-  if (len) detail::hipcheck(hipMemcpyAsync(d_xdr.p, x, len, hipMemcpyHostToDevice, s), "H2D");
-  detail::abicheck(xdrg_status_init(d_st.p, s), "xdrg_status_init");
-  std::vector<std::uint64_t> idx;
-  detail::dev_buf<std::uint64_t> d_off(P.fixed() ? 0 : n + 1);
+  std::uint8_t *d_x = detail::upload_bytes(c, c.d_xdr, x, len, s);
+  std::uint8_t *d_nat = c.d_nat.get<std::uint8_t>(n * P.stride());
+  detail::abicheck(xdrg_status_init(c.status(), s), "xdrg_status_init");
+  std::uint64_t *d_off = P.fixed() ? nullptr : c.d_off.get<std::uint64_t>(n + 1);
   const std::uint64_t hcap = P.fixed() ? 0 : xdrg_decode_heap_size(P.handle(), len);
-  detail::dev_buf<std::uint8_t> d_heap(hcap);
+  std::uint8_t *d_heap = hcap ? c.d_heap.get<std::uint8_t>(hcap) : nullptr;
   if (!P.fixed()) {
     // the record index on the device (xdrg_index_records); a stream with a
-    // record longer than the index window is walked on the host instead
+    // record longer than the index window, or nested deeper than its frames,
+    // is walked on the host instead
     const std::uint32_t win = static_cast<std::uint32_t>(
         std::min<std::uint64_t>(std::max<std::uint64_t>(P.max_record_bytes(), 16), XDRG_INDEX_MAX_MSG));
     const std::size_t wsb = xdrg_index_workspace_size(len, win);
-    detail::dev_buf<std::uint8_t> ws(wsb);
-    detail::dev_buf<std::uint64_t> d_cnt(1);
-    const int rc = xdrg_index_records(P.handle(), d_xdr.p, len, n, win, d_off.p, d_cnt.p, ws.p, wsb, d_st.p, s);
+    void *ws = c.d_ws.get<std::uint8_t>(wsb);
+    std::uint64_t *d_cnt = c.d_cnt.get<std::uint64_t>(1);
+    const int rc = xdrg_index_records(P.handle(), d_x, len, n, win, d_off, d_cnt, ws, wsb, c.status(), s);
     bool host = rc == XDRG_EUNSUPPORTED;
     if (!host) {
       detail::abicheck(rc, "xdrg_index_records");
-      xdrg_error ie{};
-      detail::abicheck(xdrg_status_read(d_st.p, s, &ie), "xdrg_status_read");
+      const xdrg_error ie = detail::read_status<T>(c, s, false);
       if (ie.code) {
         if (ie.code != XDRG_ERR_INDEX_LONG) P.raise(ie);
         host = true;
-        detail::abicheck(xdrg_status_init(d_st.p, s), "xdrg_status_init");
+        detail::abicheck(xdrg_status_init(c.status(), s), "xdrg_status_init");
       }
     }
     if (host) {
-      idx = index_records<T>(x, len, n);
-      detail::hipcheck(hipMemcpyAsync(d_off.p, idx.data(), (n + 1) * 8, hipMemcpyHostToDevice, s), "H2D");
+      const std::vector<std::uint64_t> idx = index_records<T>(x, len, n);
+      c.h_off.resize((n + 1) * 8);
+      std::memcpy(c.h_off.data(), idx.data(), (n + 1) * 8);
+      detail::hipcheck(hipMemcpyAsync(d_off, c.h_off.data(), (n + 1) * 8, hipMemcpyHostToDevice, s), "H2D");
     }
   }
-  detail::abicheck(xdrg_decode(P.handle(), d_xdr.p, len, d_off.p, n, d_nat.p, d_heap.p, hcap,
-                               marshaling_stack_limit, nullptr, 0, d_st.p, s),
+  detail::abicheck(xdrg_decode(P.handle(), d_x, len, d_off, n, d_nat, d_heap, hcap, marshaling_stack_limit,
+                               nullptr, 0, c.status(), s),
                    "xdrg_decode");
-  std::vector<std::uint8_t> nat(n * P.stride()), heap(hcap);
-  if (!nat.empty())
-    detail::hipcheck(hipMemcpyAsync(nat.data(), d_nat.p, nat.size(), hipMemcpyDeviceToHost, s), "D2H");
-  if (!heap.empty())
-    detail::hipcheck(hipMemcpyAsync(heap.data(), d_heap.p, heap.size(), hipMemcpyDeviceToHost, s), "D2H");
-  xdrg_error e{};
-  detail::abicheck(xdrg_status_read(d_st.p, s, &e), "xdrg_status_read");
-  unstage_checked(nat.data(), heap.data(), n, out, e);
+  c.h_out.resize(n * P.stride());
+  c.h_heap.resize(hcap);
+  if (!c.h_out.empty())
+    detail::hipcheck(hipMemcpyAsync(c.h_out.data(), d_nat, c.h_out.size(), hipMemcpyDeviceToHost, s), "D2H");
+  if (hcap) detail::hipcheck(hipMemcpyAsync(c.h_heap.data(), d_heap, hcap, hipMemcpyDeviceToHost, s), "D2H");
+  const xdrg_error e = detail::read_status<T>(c, s, false);
+  unstage_checked(c.h_out.data(), c.h_heap.data(), n, out, e);
+}
+template <typename T>
+void from_opaque_batch(const void *bytes, std::size_t len, T *out, std::size_t n, hipStream_t s = nullptr) {
+  from_opaque_batch(default_context(), bytes, len, out, n, s);
 }
 
 // ------------------------------------------------------ sizes and depths
 //! xdr::xdr_size(recs[i]) for every record (xdrpp/types.h:240-244), one
 //! device size pass (xdrg_serial_sizes).
 template <typename T>
-std::vector<std::uint32_t> xdr_size_batch(const T *recs, std::size_t n, hipStream_t s = nullptr) {
+std::vector<std::uint32_t> xdr_size_batch(context &c, const T *recs, std::size_t n, hipStream_t s = nullptr) {
   const batch_plan<T> &P = plan_for<T>();
-  staged_batch b = stage(recs, n);
-  detail::dev_buf<std::uint8_t> d_nat(b.native.size()), d_heap(b.heap.size());
-  detail::dev_buf<std::uint32_t> d_sz(n);
-  detail::dev_buf<xdrg_status> d_st(1);
-  detail::hipcheck(hipMemcpyAsync(d_nat.p, b.native.data(), b.native.size(), hipMemcpyHostToDevice, s), "H2D");
-  if (!b.heap.empty())
-    detail::hipcheck(hipMemcpyAsync(d_heap.p, b.heap.data(), b.heap.size(), hipMemcpyHostToDevice, s), "H2D");
-  detail::abicheck(xdrg_status_init(d_st.p, s), "xdrg_status_init");
-  detail::abicheck(xdrg_serial_sizes(P.handle(), d_nat.p, n, b.heap.empty() ? nullptr : d_heap.p,
-                                     b.heap.size(), d_sz.p, marshaling_stack_limit, d_st.p, s),
+  stage_into(c.staged, recs, n);
+  std::uint8_t *nat = nullptr, *heap = nullptr;
+  detail::upload(c, s, &nat, &heap);
+  std::uint32_t *d_sz = c.d_aux.get<std::uint32_t>(n);
+  detail::abicheck(xdrg_status_init(c.status(), s), "xdrg_status_init");
+  detail::abicheck(xdrg_serial_sizes(P.handle(), nat, n, heap, c.staged.heap.size(), d_sz, marshaling_stack_limit,
+                                     c.status(), s),
                    "xdrg_serial_sizes");
+  c.h_out.resize(n * 4);
+  if (n) detail::hipcheck(hipMemcpyAsync(c.h_out.data(), d_sz, n * 4, hipMemcpyDeviceToHost, s), "D2H");
+  detail::read_status<T>(c, s);
   std::vector<std::uint32_t> out(n);
-  if (n) detail::hipcheck(hipMemcpyAsync(out.data(), d_sz.p, n * 4, hipMemcpyDeviceToHost, s), "D2H");
-  xdrg_error e{};
-  detail::abicheck(xdrg_status_read(d_st.p, s, &e), "xdrg_status_read");
-  if (e.code) P.raise(e);
+  if (n) std::memcpy(out.data(), c.h_out.data(), n * 4);
   return out;
+}
+template <typename T>
+std::vector<std::uint32_t> xdr_size_batch(const T *recs, std::size_t n, hipStream_t s = nullptr) {
+  return xdr_size_batch(default_context(), recs, n, s);
 }
 
 //! xdr::check_xdr_depth(recs[i], depth_limit) for every record
 //! (xdrpp/depth_checker.h:72-79), from the device's per-record depths
 //! (xdrg_record_depths).
 template <typename T>
-std::vector<bool> check_xdr_depth_batch(const T *recs, std::size_t n, std::uint32_t depth_limit,
+std::vector<bool> check_xdr_depth_batch(context &c, const T *recs, std::size_t n, std::uint32_t depth_limit,
                                         hipStream_t s = nullptr) {
   const batch_plan<T> &P = plan_for<T>();
-  staged_batch b = stage(recs, n);
-  detail::dev_buf<std::uint8_t> d_nat(b.native.size()), d_heap(b.heap.size());
-  detail::dev_buf<std::uint32_t> d_d(n);
-  detail::dev_buf<xdrg_status> d_st(1);
-  detail::hipcheck(hipMemcpyAsync(d_nat.p, b.native.data(), b.native.size(), hipMemcpyHostToDevice, s), "H2D");
-  if (!b.heap.empty())
-    detail::hipcheck(hipMemcpyAsync(d_heap.p, b.heap.data(), b.heap.size(), hipMemcpyHostToDevice, s), "H2D");
-  detail::abicheck(xdrg_status_init(d_st.p, s), "xdrg_status_init");
-  detail::abicheck(xdrg_record_depths(P.handle(), d_nat.p, n, b.heap.empty() ? nullptr : d_heap.p,
-                                      b.heap.size(), d_d.p, d_st.p, s),
+  stage_into(c.staged, recs, n);
+  std::uint8_t *nat = nullptr, *heap = nullptr;
+  detail::upload(c, s, &nat, &heap);
+  std::uint32_t *d_d = c.d_aux.get<std::uint32_t>(n);
+  detail::abicheck(xdrg_status_init(c.status(), s), "xdrg_status_init");
+  detail::abicheck(xdrg_record_depths(P.handle(), nat, n, heap, c.staged.heap.size(), d_d, c.status(), s),
                    "xdrg_record_depths");
-  std::vector<std::uint32_t> d(n);
-  if (n) detail::hipcheck(hipMemcpyAsync(d.data(), d_d.p, n * 4, hipMemcpyDeviceToHost, s), "D2H");
-  xdrg_error e{};
-  detail::abicheck(xdrg_status_read(d_st.p, s, &e), "xdrg_status_read");
-  if (e.code) P.raise(e);
+  c.h_out.resize(n * 4);
+  if (n) detail::hipcheck(hipMemcpyAsync(c.h_out.data(), d_d, n * 4, hipMemcpyDeviceToHost, s), "D2H");
+  detail::read_status<T>(c, s);
   std::vector<bool> ok(n);
-  for (std::size_t i = 0; i < n; ++i) ok[i] = d[i] <= depth_limit;
+  for (std::size_t i = 0; i < n; ++i) {
+    std::uint32_t d;
+    std::memcpy(&d, c.h_out.data() + 4 * i, 4);
+    ok[i] = d <= depth_limit;
+  }
   return ok;
+}
+template <typename T>
+std::vector<bool> check_xdr_depth_batch(const T *recs, std::size_t n, std::uint32_t depth_limit,
+                                        hipStream_t s = nullptr) {
+  return check_xdr_depth_batch(default_context(), recs, n, depth_limit, s);
 }
 
 // ---------------------------------------------------- record-marked messages
@@ -1188,84 +1312,49 @@ namespace detail {
 // Device encode of n staged records as n record-marked messages.  Returns
 // the stream and fills off[n+1] (mark of each message, then the total).
 template <typename T>
-std::vector<std::uint8_t> encode_msgs(const T *recs, std::size_t n, std::vector<std::uint64_t> &off,
+std::vector<std::uint8_t> encode_msgs(context &c, const T *recs, std::size_t n, std::vector<std::uint64_t> &off,
                                       hipStream_t s) {
-  const batch_plan<T> &P = plan_for<T>();
-  staged_batch b = stage(recs, n);
-  dev_buf<std::uint8_t> d_nat(b.native.size()), d_heap(b.heap.size());
-  dev_buf<xdrg_status> d_st(1);
-  hipcheck(hipMemcpyAsync(d_nat.p, b.native.data(), b.native.size(), hipMemcpyHostToDevice, s), "H2D");
-  if (!b.heap.empty())
-    hipcheck(hipMemcpyAsync(d_heap.p, b.heap.data(), b.heap.size(), hipMemcpyHostToDevice, s), "H2D");
-  abicheck(xdrg_status_init(d_st.p, s), "xdrg_status_init");
-  std::size_t total = (std::size_t(P.fixed_size()) + 4) * n;
-  if (!P.fixed()) {  // size pass for the capacity: xdr_argpack_size + the marks
-    dev_buf<std::uint32_t> d_sz(n);
-    abicheck(xdrg_serial_sizes(P.handle(), d_nat.p, n, b.heap.empty() ? nullptr : d_heap.p, b.heap.size(),
-                               d_sz.p, marshaling_stack_limit, d_st.p, s),
-             "xdrg_serial_sizes");
-    std::vector<std::uint32_t> sz(n);
-    if (n) hipcheck(hipMemcpyAsync(sz.data(), d_sz.p, n * 4, hipMemcpyDeviceToHost, s), "D2H");
-    xdrg_error e{};
-    abicheck(xdrg_status_read(d_st.p, s, &e), "xdrg_status_read");
-    if (e.code) P.raise(e);
-    total = 4 * n;
-    for (auto v : sz) total += v;
-  }
-  const std::size_t ws_bytes = xdrg_workspace_size(P.handle(), n);
-  dev_buf<std::uint8_t> ws(ws_bytes), d_out(total);
-  dev_buf<std::uint64_t> d_off(n + 1);
-  abicheck(xdrg_encode_msgs(P.handle(), d_nat.p, n, b.heap.empty() ? nullptr : d_heap.p,
-                            b.heap.size(), d_out.p, total, d_off.p, marshaling_stack_limit, ws.p,
-                            ws_bytes, d_st.p, s),
-           "xdrg_encode_msgs");
-  std::vector<std::uint8_t> out(total);
+  const std::size_t total = encode_on_device(c, recs, n, true, s);
+  c.h_out.resize(total);
+  c.h_off.resize((n + 1) * 8);
+  if (total) hipcheck(hipMemcpyAsync(c.h_out.data(), c.d_xdr.p, total, hipMemcpyDeviceToHost, s), "D2H");
+  hipcheck(hipMemcpyAsync(c.h_off.data(), c.d_off.p, (n + 1) * 8, hipMemcpyDeviceToHost, s), "D2H");
+  read_status<T>(c, s);
   off.assign(n + 1, 0);
-  if (total) hipcheck(hipMemcpyAsync(out.data(), d_out.p, total, hipMemcpyDeviceToHost, s), "D2H");
-  hipcheck(hipMemcpyAsync(off.data(), d_off.p, (n + 1) * 8, hipMemcpyDeviceToHost, s), "D2H");
-  xdrg_error e{};
-  abicheck(xdrg_status_read(d_st.p, s, &e), "xdrg_status_read");
-  if (e.code) P.raise(e);
-  return out;
+  std::memcpy(off.data(), c.h_off.data(), (n + 1) * 8);
+  return std::vector<std::uint8_t>(c.h_out.begin(), c.h_out.begin() + std::ptrdiff_t(total));
 }
 
-// Device decode of the n messages of a stream indexed by off[n+1].
+// Device decode of the n messages of a stream (already on the device at
+// d_x) indexed by d_off.
 template <typename T>
-void decode_msgs(const std::uint8_t *x, std::size_t len, const std::vector<std::uint64_t> &off,
-                 T *out, std::size_t n, hipStream_t s) {
+void decode_msgs_on_device(context &c, const std::uint8_t *d_x, std::size_t len, const std::uint64_t *d_off, T *out,
+                           std::size_t n, hipStream_t s) {
   const batch_plan<T> &P = plan_for<T>();
-  dev_buf<std::uint8_t> d_x(len), d_nat(n * P.stride());
-  dev_buf<std::uint64_t> d_off(n + 1);
-  dev_buf<xdrg_status> d_st(1);
-  if (len) hipcheck(hipMemcpyAsync(d_x.p, x, len, hipMemcpyHostToDevice, s), "H2D");
-  hipcheck(hipMemcpyAsync(d_off.p, off.data(), (n + 1) * 8, hipMemcpyHostToDevice, s), "H2D");
-  abicheck(xdrg_status_init(d_st.p, s), "xdrg_status_init");
+  std::uint8_t *d_nat = c.d_nat.get<std::uint8_t>(n * P.stride());
+  abicheck(xdrg_status_init(c.status(), s), "xdrg_status_init");
   const std::uint64_t hcap = P.fixed() ? 0 : xdrg_decode_heap_size(P.handle(), len);
-  dev_buf<std::uint8_t> d_heap(hcap);
-  const std::size_t ws_bytes = xdrg_workspace_size(P.handle(), n);
-  dev_buf<std::uint8_t> ws(ws_bytes);
-  abicheck(xdrg_decode_msgs(P.handle(), d_x.p, len, d_off.p, n, d_nat.p, d_heap.p, hcap,
-                            marshaling_stack_limit, ws.p, ws_bytes, d_st.p, s),
+  std::uint8_t *d_heap = hcap ? c.d_heap.get<std::uint8_t>(hcap) : nullptr;
+  abicheck(xdrg_decode_msgs(P.handle(), d_x, len, d_off, n, d_nat, d_heap, hcap, marshaling_stack_limit, nullptr,
+                            0, c.status(), s),
            "xdrg_decode_msgs");
-  std::vector<std::uint8_t> nat(n * P.stride()), heap(hcap);
-  if (!nat.empty())
-    hipcheck(hipMemcpyAsync(nat.data(), d_nat.p, nat.size(), hipMemcpyDeviceToHost, s), "D2H");
-  if (!heap.empty())
-    hipcheck(hipMemcpyAsync(heap.data(), d_heap.p, heap.size(), hipMemcpyDeviceToHost, s), "D2H");
-  xdrg_error e{};
-  abicheck(xdrg_status_read(d_st.p, s, &e), "xdrg_status_read");
-  unstage_checked(nat.data(), heap.data(), n, out, e);
+  c.h_out.resize(n * P.stride());
+  c.h_heap.resize(hcap);
+  if (!c.h_out.empty())
+    hipcheck(hipMemcpyAsync(c.h_out.data(), d_nat, c.h_out.size(), hipMemcpyDeviceToHost, s), "D2H");
+  if (hcap) hipcheck(hipMemcpyAsync(c.h_heap.data(), d_heap, hcap, hipMemcpyDeviceToHost, s), "D2H");
+  const xdrg_error e = read_status<T>(c, s, false);
+  unstage_checked(c.h_out.data(), c.h_heap.data(), n, out, e);
 }
 
-// The raw bytes (mark + body) of a vector of messages, back to back.
-inline std::vector<std::uint8_t> concat(const std::vector<msg_ptr> &msgs,
-                                        std::vector<std::uint64_t> &off) {
+// The raw bytes (mark + body) of a vector of messages, back to back, into
+// the context's pinned staging.
+inline void concat(context &c, const std::vector<msg_ptr> &msgs, std::vector<std::uint64_t> &off) {
   off.assign(msgs.size() + 1, 0);
   for (std::size_t i = 0; i < msgs.size(); ++i) off[i + 1] = off[i] + msgs[i]->raw_size();
-  std::vector<std::uint8_t> x(off.back());
+  c.h_in.resize(off.back());
   for (std::size_t i = 0; i < msgs.size(); ++i)
-    std::memcpy(x.data() + off[i], msgs[i]->raw_data(), msgs[i]->raw_size());
-  return x;
+    std::memcpy(c.h_in.data() + off[i], msgs[i]->raw_data(), msgs[i]->raw_size());
 }
 }  // namespace detail
 
@@ -1275,20 +1364,21 @@ inline std::vector<std::uint8_t> concat(const std::vector<msg_ptr> &msgs,
 template <typename T>
 std::vector<std::uint8_t> to_msg_stream(const T *recs, std::size_t n, hipStream_t s = nullptr) {
   std::vector<std::uint64_t> off;
-  return detail::encode_msgs(recs, n, off, s);
+  return detail::encode_msgs(default_context(), recs, n, off, s);
 }
 
 //! The same messages, one message_t per record: msgs[i] holds the bytes
 //! xdr::xdr_to_msg(recs[i]) produces (message_t::alloc, marshal.cc:15-31).
 template <typename T>
 std::vector<msg_ptr> to_msg_batch(const T *recs, std::size_t n, hipStream_t s = nullptr) {
+  context &c = default_context();
   std::vector<std::uint64_t> off;
-  const std::vector<std::uint8_t> x = detail::encode_msgs(recs, n, off, s);
+  detail::encode_msgs(c, recs, n, off, s);
   std::vector<msg_ptr> out;
   out.reserve(n);
   for (std::size_t i = 0; i < n; ++i) {
     msg_ptr m = message_t::alloc(off[i + 1] - off[i] - 4);
-    std::memcpy(m->data(), x.data() + off[i] + 4, m->size());
+    std::memcpy(m->data(), c.h_out.data() + off[i] + 4, m->size());
     out.push_back(std::move(m));
   }
   return out;
@@ -1298,40 +1388,48 @@ std::vector<msg_ptr> to_msg_batch(const T *recs, std::size_t n, hipStream_t s = 
 //! the first failing message raises the reference's exception.
 template <typename T>
 void from_msg_batch(const std::vector<msg_ptr> &msgs, T *out, hipStream_t s = nullptr) {
+  context &c = default_context();
   std::vector<std::uint64_t> off;
-  const std::vector<std::uint8_t> x = detail::concat(msgs, off);
-  detail::decode_msgs(x.data(), x.size(), off, out, msgs.size(), s);
+  detail::concat(c, msgs, off);
+  const std::size_t len = off.back(), n = msgs.size();
+  std::uint8_t *d_x = c.d_xdr.get<std::uint8_t>(len);
+  std::uint64_t *d_off = c.d_off.get<std::uint64_t>(n + 1);
+  if (len) detail::hipcheck(hipMemcpyAsync(d_x, c.h_in.data(), len, hipMemcpyHostToDevice, s), "H2D");
+  c.h_off.resize((n + 1) * 8);
+  std::memcpy(c.h_off.data(), off.data(), (n + 1) * 8);
+  detail::hipcheck(hipMemcpyAsync(d_off, c.h_off.data(), (n + 1) * 8, hipMemcpyHostToDevice, s), "H2D");
+  detail::decode_msgs_on_device(c, d_x, len, d_off, out, n, s);
 }
 
 //! Every message of a stream of record-marked messages, decoded: the
 //! framing of read_message / msg_sock::input (srpc.cc:29-55,
-//! msgsock.cc:38-119) applied on the device (xdrg_index_msgs), then
-//! xdr_from_msg per message.  A framing error raises xdr_bad_message_size.
+//! msgsock.cc:38-119) applied on the device (xdrg_index_msgs), messages of
+//! up to max_msg_len bytes (msg_sock's default; any length up to 2^31 - 1),
+//! then xdr_from_msg per message.  A framing error raises
+//! xdr_bad_message_size.
 template <typename T>
 std::vector<T> from_msg_stream(const void *bytes, std::size_t len,
                                std::uint32_t max_msg_len = 0x100000,  // msg_sock::default_maxmsglen
                                hipStream_t s = nullptr) {
-  const auto *x = static_cast<const std::uint8_t *>(bytes);
+  context &c = default_context();
   const std::uint64_t max_msgs = len / 4;
-  detail::dev_buf<std::uint8_t> d_x(len);
-  detail::dev_buf<std::uint64_t> d_off(max_msgs + 1), d_cnt(1);
-  detail::dev_buf<xdrg_status> d_st(1);
+  std::uint8_t *d_x = detail::upload_bytes(c, c.d_xdr, bytes, len, s);
+  std::uint64_t *d_off = c.d_off.get<std::uint64_t>(max_msgs + 1);
+  std::uint64_t *d_cnt = c.d_cnt.get<std::uint64_t>(1);
   const std::size_t ws_bytes = xdrg_index_workspace_size(len, max_msg_len);
-  detail::dev_buf<std::uint8_t> ws(ws_bytes);
-  if (len) detail::hipcheck(hipMemcpyAsync(d_x.p, x, len, hipMemcpyHostToDevice, s), "H2D");
-  detail::abicheck(xdrg_status_init(d_st.p, s), "xdrg_status_init");
-  detail::abicheck(xdrg_index_msgs(d_x.p, len, max_msg_len, max_msgs, d_off.p, d_cnt.p, ws.p,
-                                   ws_bytes, d_st.p, s),
+  void *ws = c.d_ws.get<std::uint8_t>(ws_bytes);
+  detail::abicheck(xdrg_status_init(c.status(), s), "xdrg_status_init");
+  detail::abicheck(xdrg_index_msgs(d_x, len, max_msg_len, max_msgs, d_off, d_cnt, ws, ws_bytes, c.status(), s),
                    "xdrg_index_msgs");
-  std::uint64_t cnt = 0;
-  detail::hipcheck(hipMemcpyAsync(&cnt, d_cnt.p, 8, hipMemcpyDeviceToHost, s), "D2H");
+  c.h_off.resize(8);
+  detail::hipcheck(hipMemcpyAsync(c.h_off.data(), d_cnt, 8, hipMemcpyDeviceToHost, s), "D2H");
   xdrg_error e{};
-  detail::abicheck(xdrg_status_read(d_st.p, s, &e), "xdrg_status_read");
+  detail::abicheck(xdrg_status_read(c.status(), s, &e), "xdrg_status_read");
   if (e.code) throw xdr_bad_message_size(xdrg_error_message(e.code));
-  std::vector<std::uint64_t> off(cnt + 1);
-  detail::hipcheck(hipMemcpy(off.data(), d_off.p, (cnt + 1) * 8, hipMemcpyDeviceToHost), "D2H");
+  std::uint64_t cnt = 0;
+  std::memcpy(&cnt, c.h_off.data(), 8);
   std::vector<T> out(cnt);
-  detail::decode_msgs(x, len, off, out.data(), cnt, s);
+  detail::decode_msgs_on_device(c, d_x, len, d_off, out.data(), cnt, s);
   return out;
 }
 
@@ -1367,25 +1465,29 @@ class rpc_registry {
 inline std::vector<xdrg_rpc_hdr> rpc_dispatch_batch(const std::vector<msg_ptr> &msgs,
                                                     const rpc_registry &reg,
                                                     hipStream_t s = nullptr) {
+  context &c = default_context();
   std::vector<std::uint64_t> off;
-  const std::vector<std::uint8_t> x = detail::concat(msgs, off);
-  const std::size_t n = msgs.size();
+  detail::concat(c, msgs, off);
+  const std::size_t n = msgs.size(), len = off.back(), np = reg.table().size();
   std::vector<xdrg_rpc_hdr> h(n);
   if (!n) return h;
-  detail::dev_buf<std::uint8_t> d_x(x.size());
-  detail::dev_buf<std::uint64_t> d_off(n + 1);
-  detail::dev_buf<xdrg_rpc_proc> d_p(reg.table().size());
-  detail::dev_buf<xdrg_rpc_hdr> d_h(n);
-  detail::hipcheck(hipMemcpyAsync(d_x.p, x.data(), x.size(), hipMemcpyHostToDevice, s), "H2D");
-  detail::hipcheck(hipMemcpyAsync(d_off.p, off.data(), (n + 1) * 8, hipMemcpyHostToDevice, s), "H2D");
-  if (!reg.table().empty())
-    detail::hipcheck(hipMemcpyAsync(d_p.p, reg.table().data(), reg.table().size() * sizeof(xdrg_rpc_proc),
+  std::uint8_t *d_x = c.d_xdr.get<std::uint8_t>(len);
+  std::uint64_t *d_off = c.d_off.get<std::uint64_t>(n + 1);
+  xdrg_rpc_proc *d_p = c.d_aux.get<xdrg_rpc_proc>(np);
+  xdrg_rpc_hdr *d_h = c.d_nat.get<xdrg_rpc_hdr>(n);
+  c.h_off.resize((n + 1) * 8 + np * sizeof(xdrg_rpc_proc));
+  std::memcpy(c.h_off.data(), off.data(), (n + 1) * 8);
+  if (np) std::memcpy(c.h_off.data() + (n + 1) * 8, reg.table().data(), np * sizeof(xdrg_rpc_proc));
+  detail::hipcheck(hipMemcpyAsync(d_x, c.h_in.data(), len, hipMemcpyHostToDevice, s), "H2D");
+  detail::hipcheck(hipMemcpyAsync(d_off, c.h_off.data(), (n + 1) * 8, hipMemcpyHostToDevice, s), "H2D");
+  if (np)
+    detail::hipcheck(hipMemcpyAsync(d_p, c.h_off.data() + (n + 1) * 8, np * sizeof(xdrg_rpc_proc),
                                     hipMemcpyHostToDevice, s), "H2D");
-  detail::abicheck(xdrg_rpc_dispatch(d_x.p, x.size(), d_off.p, n, d_p.p,
-                                     std::uint32_t(reg.table().size()), d_h.p, s),
-                   "xdrg_rpc_dispatch");
-  detail::hipcheck(hipMemcpyAsync(h.data(), d_h.p, n * sizeof(xdrg_rpc_hdr), hipMemcpyDeviceToHost, s), "D2H");
+  detail::abicheck(xdrg_rpc_dispatch(d_x, len, d_off, n, d_p, std::uint32_t(np), d_h, s), "xdrg_rpc_dispatch");
+  c.h_out.resize(n * sizeof(xdrg_rpc_hdr));
+  detail::hipcheck(hipMemcpyAsync(c.h_out.data(), d_h, c.h_out.size(), hipMemcpyDeviceToHost, s), "D2H");
   detail::hipcheck(hipStreamSynchronize(s), "sync");
+  std::memcpy(h.data(), c.h_out.data(), c.h_out.size());
   for (std::size_t i = 0; i < n; ++i) {
     if (!h[i].err) h[i].body_off -= off[i] + 4;
     h[i].end -= off[i] + 4;
@@ -1398,29 +1500,32 @@ inline std::vector<xdrg_rpc_hdr> rpc_dispatch_batch(const std::vector<msg_ptr> &
 //! server.cc:8-67), or nullptr for DISPATCH and dropped messages.
 inline std::vector<msg_ptr> rpc_error_replies(const std::vector<xdrg_rpc_hdr> &h,
                                               hipStream_t s = nullptr) {
+  context &c = default_context();
   const std::size_t n = h.size();
   std::vector<msg_ptr> out(n);
   if (!n) return out;
   const std::size_t ws_bytes = xdrg_rpc_replies_workspace_size(n);
-  detail::dev_buf<xdrg_rpc_hdr> d_h(n);
-  detail::dev_buf<std::uint8_t> d_out(36 * n), ws(ws_bytes);
-  detail::dev_buf<std::uint64_t> d_off(n + 1);
-  detail::dev_buf<xdrg_status> d_st(1);
-  detail::hipcheck(hipMemcpyAsync(d_h.p, h.data(), n * sizeof(xdrg_rpc_hdr), hipMemcpyHostToDevice, s), "H2D");
-  detail::abicheck(xdrg_status_init(d_st.p, s), "xdrg_status_init");
-  detail::abicheck(xdrg_rpc_replies(d_h.p, n, d_out.p, 36 * n, d_off.p, ws.p, ws_bytes, d_st.p, s),
-                   "xdrg_rpc_replies");
-  std::vector<std::uint64_t> off(n + 1);
-  detail::hipcheck(hipMemcpyAsync(off.data(), d_off.p, (n + 1) * 8, hipMemcpyDeviceToHost, s), "D2H");
+  xdrg_rpc_hdr *d_h = c.d_nat.get<xdrg_rpc_hdr>(n);
+  std::uint8_t *d_out = c.d_xdr.get<std::uint8_t>(36 * n);
+  void *ws = c.d_ws.get<std::uint8_t>(ws_bytes);
+  std::uint64_t *d_off = c.d_off.get<std::uint64_t>(n + 1);
+  c.h_in.resize(n * sizeof(xdrg_rpc_hdr));
+  std::memcpy(c.h_in.data(), h.data(), c.h_in.size());
+  detail::hipcheck(hipMemcpyAsync(d_h, c.h_in.data(), c.h_in.size(), hipMemcpyHostToDevice, s), "H2D");
+  detail::abicheck(xdrg_status_init(c.status(), s), "xdrg_status_init");
+  detail::abicheck(xdrg_rpc_replies(d_h, n, d_out, 36 * n, d_off, ws, ws_bytes, c.status(), s), "xdrg_rpc_replies");
+  c.h_off.resize((n + 1) * 8);
+  c.h_out.resize(36 * n);
+  detail::hipcheck(hipMemcpyAsync(c.h_off.data(), d_off, (n + 1) * 8, hipMemcpyDeviceToHost, s), "D2H");
+  detail::hipcheck(hipMemcpyAsync(c.h_out.data(), d_out, 36 * n, hipMemcpyDeviceToHost, s), "D2H");
   xdrg_error e{};
-  detail::abicheck(xdrg_status_read(d_st.p, s, &e), "xdrg_status_read");
-  std::vector<std::uint8_t> x(e.total_bytes);
-  if (!x.empty())
-    detail::hipcheck(hipMemcpy(x.data(), d_out.p, x.size(), hipMemcpyDeviceToHost), "D2H");
+  detail::abicheck(xdrg_status_read(c.status(), s, &e), "xdrg_status_read");
+  std::vector<std::uint64_t> off(n + 1);
+  std::memcpy(off.data(), c.h_off.data(), (n + 1) * 8);
   for (std::size_t i = 0; i < n; ++i) {
     if (off[i + 1] == off[i]) continue;
     out[i] = message_t::alloc(off[i + 1] - off[i] - 4);
-    std::memcpy(out[i]->data(), x.data() + off[i] + 4, out[i]->size());
+    std::memcpy(out[i]->data(), c.h_out.data() + off[i] + 4, out[i]->size());
   }
   return out;
 }

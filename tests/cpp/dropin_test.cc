@@ -23,6 +23,7 @@
 // and the hook is declared before the traits, as tests/validate.cc does for
 // fix_4 (tests/validate.cc:7-9,21-26).
 #include <xdrpp/types.h>
+#include <chrono>
 struct vfix {  // tests/xdrtest.x fix_4: struct fix_4 { int i; };
   std::int32_t i;
 };
@@ -131,8 +132,9 @@ static void check_stage(const char *name, const std::vector<T> &v) {
   heap_t h;
   stage(v, nat, h);  // the reference-side staged layout (oracle/ref_objects.hh)
   CHECK(nat.size() == b.native.size(), "%s: staged size %zu vs %zu", name, b.native.size(), nat.size());
-  CHECK(nat == b.native, "%s: staged native bytes differ", name);
-  CHECK(h.b == b.heap, "%s: staged heap differs", name);
+  CHECK(std::equal(nat.begin(), nat.end(), b.native.begin()), "%s: staged native bytes differ", name);
+  CHECK(h.b.size() == b.heap.size() && std::equal(h.b.begin(), h.b.end(), b.heap.begin()),
+        "%s: staged heap differs", name);
   std::vector<T> back(v.size());
   xdr::gpu::unstage(b.native.data(), b.heap.data(), v.size(), back.data());
   bool ok = true;
@@ -162,6 +164,74 @@ static void check_gpu(const char *name, const std::vector<T> &v) {
   xdr::opaque_vec<> one = xdr::gpu::to_opaque_batch(&v[1], 1);
   CHECK(one == xdr::xdr_to_opaque(v[1]), "%s: batch of one differs from xdr_to_opaque", name);
   std::printf("gpu %s: %zu records, %zu bytes bit-exact, round trip ok\n", name, v.size(), want.size());
+}
+
+// A context in its steady state: once its buffers have grown to a batch
+// size, the calls allocate nothing (no hipMalloc, no pinned host memory),
+// and an encode sizes its output with one size pass.
+template <typename T>
+static void check_steady(const char *name, const std::vector<T> &v) {
+  std::vector<std::uint64_t> off;
+  const std::vector<std::uint8_t> want = ref_stream(v, off);
+  xdr::gpu::context c;
+  std::vector<T> back(v.size());
+  for (int i = 0; i < 2; ++i) {  // the first call grows the buffers
+    (void)xdr::gpu::to_opaque_batch(c, v.data(), v.size());
+    xdr::gpu::from_opaque_batch(c, want.data(), want.size(), back.data(), back.size());
+  }
+  const std::size_t a0 = xdr::gpu::context::allocations();
+  for (int i = 0; i < 3; ++i) {
+    xdr::opaque_vec<> got = xdr::gpu::to_opaque_batch(c, v.data(), v.size());
+    CHECK(got.size() == want.size() && std::equal(got.begin(), got.end(), want.begin()),
+          "%s: steady to_opaque_batch differs", name);
+    xdr::gpu::from_opaque_batch(c, want.data(), want.size(), back.data(), back.size());
+  }
+  CHECK(xdr::gpu::context::allocations() == a0, "%s: %zu allocations after the steady state", name,
+        xdr::gpu::context::allocations() - a0);
+  std::printf("steady %s: 3 encode + decode calls, %zu allocations\n", name, xdr::gpu::context::allocations() - a0);
+}
+
+// Host-inclusive rates of the C++ drop-in: records in host memory -> staged
+// (pinned) -> device encode -> host opaque_vec, and the decode mirror,
+// through one context in its steady state; the reference's single-thread
+// xdr_put / xdr_get stream over the same records beside it.
+template <typename T>
+static void bench_one(const char *name, const std::vector<T> &v, int reps) {
+  using clk = std::chrono::steady_clock;
+  std::vector<std::uint64_t> off;
+  const std::vector<std::uint8_t> want = ref_stream(v, off);
+  xdr::gpu::context c;
+  std::vector<T> back(v.size());
+  for (int i = 0; i < 2; ++i) {
+    (void)xdr::gpu::to_opaque_batch(c, v.data(), v.size());
+    xdr::gpu::from_opaque_batch(c, want.data(), want.size(), back.data(), back.size());
+  }
+  double te = 1e30, td = 1e30, tr = 1e30, tg = 1e30;
+  for (int r = 0; r < reps; ++r) {
+    auto t0 = clk::now();
+    xdr::opaque_vec<> got = xdr::gpu::to_opaque_batch(c, v.data(), v.size());
+    auto t1 = clk::now();
+    xdr::gpu::from_opaque_batch(c, want.data(), want.size(), back.data(), back.size());
+    auto t2 = clk::now();
+    std::vector<std::uint8_t> out(want.size());
+    xdr::xdr_put p(out.data(), out.data() + out.size());
+    for (const T &t : v) xdr::archive(p, t);
+    auto t3 = clk::now();
+    std::vector<T> rb(v.size());
+    xdr::xdr_get g(out.data(), out.data() + out.size());
+    for (T &t : rb) xdr::archive(g, t);
+    auto t4 = clk::now();
+    te = std::min(te, std::chrono::duration<double>(t1 - t0).count());
+    td = std::min(td, std::chrono::duration<double>(t2 - t1).count());
+    tr = std::min(tr, std::chrono::duration<double>(t3 - t2).count());
+    tg = std::min(tg, std::chrono::duration<double>(t4 - t3).count());
+    CHECK(got.size() == want.size() && std::equal(got.begin(), got.end(), want.begin()), "%s: bench bytes", name);
+  }
+  const double g = double(want.size()) / double(1ull << 30);
+  std::printf("{\"schema\": \"%s\", \"records\": %zu, \"xdr_bytes\": %zu, \"to_opaque_batch_gib_s\": %.3f, "
+              "\"from_opaque_batch_gib_s\": %.3f, \"encode_decode_gib_s\": %.3f, "
+              "\"reference_1thread_put_gib_s\": %.3f, \"reference_1thread_get_gib_s\": %.3f, \"reps\": %d}\n",
+              name, v.size(), want.size(), g / te, g / td, 2 * g / (te + td), g / tr, g / tg, reps);
 }
 
 // Record-marked messages: to_msg_batch / to_msg_stream against the
@@ -462,7 +532,21 @@ int main(int argc, char **argv) {
     check_stage("recvar", rv);
     check_stage("rpc", rp);
     check_stage("vecrec", vr);
+  } else if (mode == "bench") {
+    const std::size_t n = argc > 2 ? std::stoull(argv[2]) : (1u << 20);
+    std::vector<rec128> brc;
+    std::vector<recvar> brv;
+    std::vector<xdr::rpc_msg> brp;
+    gen_rec128(n, WG_SEED_REC128, 0, brc);
+    gen_recvar(n, WG_SEED_RECVAR, brv);
+    gen_rpc(n, WG_SEED_RPC, brp);
+    bench_one("rec128", brc, 5);
+    bench_one("recvar", brv, 5);
+    bench_one("rpc", brp, 5);
   } else if (mode == "gpu") {
+    check_steady("rec128", rc);
+    check_steady("recvar", rv);
+    check_steady("rpc", rp);
     check_gpu("numerics", nu);
     check_gpu("rec128", rc);
     check_gpu("recvar", rv);
@@ -482,7 +566,7 @@ int main(int argc, char **argv) {
     check_sizes_depths("rpc", rp);
     check_sizes_depths("vecrec", vr);
   } else {
-    std::fprintf(stderr, "usage: dropin_test plans <dir> | stage | gpu\n");
+    std::fprintf(stderr, "usage: dropin_test plans <dir> | stage | gpu [golden] | bench [records]\n");
     return 2;
   }
   if (failures) std::fprintf(stderr, "%d failure(s)\n", failures);

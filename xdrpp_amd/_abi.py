@@ -14,7 +14,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libxdrgpu.s
 
 # enum xdrg_op_kind
 OP_U32, OP_U64, OP_BOOL, OP_ENUM, OP_OPAQUE, OP_VAROPAQUE, OP_STRING, OP_UNION, OP_JUMP, OP_END, OP_VECTOR = range(1, 12)
-ABI_VERSION = 5  # XDRG_ABI_VERSION, include/xdrgpu.h
+ABI_VERSION = 6  # XDRG_ABI_VERSION, include/xdrgpu.h
 F_VALIDATE = 1
 F_DEFAULT = 2
 F_POINTER = 4
@@ -121,7 +121,7 @@ EXPORTED = (
     "xdrg_index_workspace_size", "xdrg_rpc_dispatch", "xdrg_rpc_check_replies",
     "xdrg_rpc_replies", "xdrg_rpc_replies_workspace_size", "xdrg_record_depths",
     "xdrg_plan_set_option", "xdrg_plan_kernel_source", "xdrg_plan_build_kernels",
-    "xdrg_plan_load_kernels", "xdrg_index_records",
+    "xdrg_plan_load_kernels", "xdrg_index_records", "xdrg_encode_sizes", "xdrg_encode_sized",
 )
 
 # RPC header batches (include/xdrgpu.h "RPC header batches")
@@ -181,6 +181,10 @@ def lib() -> C.CDLL:
     L.xdrg_decode.restype = C.c_int
     L.xdrg_encode_msgs.argtypes = [vp, vp, u64, vp, u64, vp, u64, vp, u32, vp, sz, vp, vp]
     L.xdrg_encode_msgs.restype = C.c_int
+    L.xdrg_encode_sizes.argtypes = [vp, vp, u64, vp, u64, u32, C.c_int, vp, sz, vp, vp]
+    L.xdrg_encode_sizes.restype = C.c_int
+    L.xdrg_encode_sized.argtypes = [vp, vp, u64, vp, u64, vp, u64, vp, u32, C.c_int, vp, sz, vp, vp]
+    L.xdrg_encode_sized.restype = C.c_int
     L.xdrg_decode_msgs.argtypes = [vp, vp, u64, vp, u64, vp, vp, u64, u32, vp, sz, vp, vp]
     L.xdrg_decode_msgs.restype = C.c_int
     L.xdrg_index_msgs.argtypes = [vp, u64, u32, u64, vp, vp, vp, sz, vp, vp]

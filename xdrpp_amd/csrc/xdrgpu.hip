@@ -504,14 +504,14 @@ __global__ __launch_bounds__(1024) void k_scan_blocks(const unsigned long long *
     carry = scan_tile(in, out, t0, nb, carry, buf, wtot);
     if (tid == 0 && blockIdx.x == gridDim.x - 1) {
       status->total_bytes = carry;
-      offsets[n] = carry;
+      if (offsets) offsets[n] = carry;
     }
     return;
   }
   for (uint64_t t0 = 0; t0 < nb; t0 += kScanTile) carry = scan_tile(in, out, t0, nb, carry, buf, wtot);
   if (tid == 0) {
     status->total_bytes = carry;
-    offsets[n] = carry;
+    if (offsets) offsets[n] = carry;
   }
 }
 
@@ -1458,6 +1458,11 @@ __global__ void k_ix_long(const uint8_t *__restrict__ s, uint64_t len, uint32_t 
   next[2] = 0;
 }
 
+// xdrg_encode_sizes of a fixed plan: the total is known.
+__global__ void k_set_total(xdrg_status *st, uint64_t v) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) st->total_bytes = v;
+}
+
 // ------------------------------------------------------------------ swaps
 __global__ void k_swap32(const uint32_t *__restrict__ in, uint32_t *__restrict__ out, uint64_t n) {
   for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
@@ -1819,19 +1824,27 @@ namespace {
 
 // Var-plan encode of n records: size pass, block scan, then the record
 // kernel.  mark = 4 puts each record in a message (its record mark first,
-// xdrg_encode_msgs); mark = 0 is xdrg_encode of a var plan.
+// xdrg_encode_msgs); mark = 0 is xdrg_encode of a var plan.  phase: both
+// halves (kEncBoth), the size pass and scan alone into the workspace
+// (kEncSizes, xdrg_encode_sizes: the total lands in status->total_bytes),
+// or the record kernel over a workspace kEncSizes filled (kEncSized).
+enum : int { kEncBoth = 0, kEncSizes = 1, kEncSized = 2 };
 int var_encode(const xdrg_plan &P, const dev_tables &T, const void *d_native, uint64_t n,
                const uint8_t *d_heap, uint64_t heap_len, void *d_xdr, uint64_t cap,
                uint64_t *d_offsets, uint32_t stack_limit, void *d_ws, size_t ws_bytes,
-               xdrg_status *d_status, uint32_t mark, hipStream_t s) {
+               xdrg_status *d_status, uint32_t mark, hipStream_t s, int phase = kEncBoth) {
   const xdrg_plan *p = &P;
   const plan_opts &O = P.opts;
   unsigned long long *err = err_ptr(d_status);
-  if (!d_offsets) return XDRG_EINVAL;
+  // a deep plan's lists live in the frame pool for one call: its sized half
+  // runs both halves again
+  if (phase == kEncSized && p->deep) phase = kEncBoth;
+  if (phase != kEncSizes && !d_offsets) return XDRG_EINVAL;
   if (d_heap && !aligned(d_heap, 4)) return XDRG_EALIGN;
-  if (!aligned(d_native, 8) || !aligned(d_xdr, 4) || !aligned(d_offsets, 8)) return XDRG_EALIGN;
+  if (!aligned(d_native, 8) || (phase != kEncSizes && (!aligned(d_xdr, 4) || !aligned(d_offsets, 8))))
+    return XDRG_EALIGN;
   if (n == 0) {
-    HIPCHK(hipMemsetAsync(d_offsets, 0, 8, s));
+    if (d_offsets) HIPCHK(hipMemsetAsync(d_offsets, 0, 8, s));
     return XDRG_OK;
   }
   size_t so, bo, bbo;
@@ -1885,16 +1898,21 @@ int var_encode(const xdrg_plan &P, const dev_tables &T, const void *d_native, ui
   deep_passes dp;
   if (p->has_sub)
     if (int rc = lease.acquire(*p, n, s, dp)) return rc;
-  if (SM && !p->linear) {
-    const size_t tile = 64ull * p->stride;
-    uint32_t n_mark = mark;
-    void *args[] = {&nat8, &n, const_cast<uint32_t *>(&p->stride), &sizes, &bsum, &n_mark, &err};
-    HIPCHK(hipModuleLaunchKernel(static_cast<hipFunction_t>(SM->f_size), static_cast<uint32_t>(nb), 1, 1,
-                                 64, 1, 1, static_cast<uint32_t>(tile), s, args, nullptr));
+  if (phase == kEncSized) {  // sizes and block bases from xdrg_encode_sizes
+    HIPCHK(hipMemcpyAsync(d_offsets + n, &d_status->total_bytes, 8, hipMemcpyDeviceToDevice, s));
   } else {
-    HIPCHK(launch_size_pass(*p, T, nat8, n, d_heap, heap_len, sizes, bsum, mark, err, s, dp));
+    if (SM && !p->linear) {
+      const size_t tile = 64ull * p->stride;
+      uint32_t n_mark = mark;
+      void *args[] = {&nat8, &n, const_cast<uint32_t *>(&p->stride), &sizes, &bsum, &n_mark, &err};
+      HIPCHK(hipModuleLaunchKernel(static_cast<hipFunction_t>(SM->f_size), static_cast<uint32_t>(nb), 1, 1,
+                                   64, 1, 1, static_cast<uint32_t>(tile), s, args, nullptr));
+    } else {
+      HIPCHK(launch_size_pass(*p, T, nat8, n, d_heap, heap_len, sizes, bsum, mark, err, s, dp));
+    }
+    if (int rc = xdrg::launch_block_scan(bsum, bbase, uint32_t(nb), d_status, d_offsets, n, s)) return rc;
+    if (phase == kEncSizes) return XDRG_OK;
   }
-  if (int rc = xdrg::launch_block_scan(bsum, bbase, uint32_t(nb), d_status, d_offsets, n, s)) return rc;
   if (p->has_sub) {
     const deep_passes ep = encode_passes(dp);
     k_sub_encode<<<(n + 255) / 256, 256, lds_ops, s>>>(nat8, n, p->stride, d_heap, heap_len, xdr8, cap,
@@ -2545,6 +2563,35 @@ int xdrg_encode_msgs(const xdrg_plan *p, const void *d_native, uint64_t n, const
   if (int rc = plan_upload(p, &T)) return rc;
   return var_encode(*p, *T, d_native, n, d_heap, heap_len, d_out, cap, d_offsets, stack_limit, d_ws,
                     ws_bytes, d_status, 4u, static_cast<hipStream_t>(stream));
+}
+
+int xdrg_encode_sizes(const xdrg_plan *p, const void *d_native, uint64_t n, const uint8_t *d_heap,
+                      uint64_t heap_len, uint32_t stack_limit, int msgs, void *d_ws, size_t ws_bytes,
+                      xdrg_status *d_status, void *stream) {
+  if (!p || !d_status || (n && !d_native)) return XDRG_EINVAL;
+  const dev_tables *T = nullptr;
+  if (int rc = plan_upload(p, &T)) return rc;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (p->path != XDRG_PATH_VAR && !msgs) {  // n * fixed_size (xdr_struct_base_fs, types.h:691-700)
+    k_set_total<<<1, 1, 0, s>>>(d_status, n * uint64_t(p->fixed_size));
+    HIPCHK(hipGetLastError());
+    return XDRG_OK;
+  }
+  return var_encode(*p, *T, d_native, n, d_heap, heap_len, nullptr, 0, nullptr, stack_limit, d_ws, ws_bytes,
+                    d_status, msgs ? 4u : 0u, s, kEncSizes);
+}
+
+int xdrg_encode_sized(const xdrg_plan *p, const void *d_native, uint64_t n, const uint8_t *d_heap,
+                      uint64_t heap_len, void *d_out, uint64_t cap, uint64_t *d_offsets, uint32_t stack_limit,
+                      int msgs, void *d_ws, size_t ws_bytes, xdrg_status *d_status, void *stream) {
+  if (!p || !d_status || (n && (!d_native || !d_out))) return XDRG_EINVAL;
+  if (p->path != XDRG_PATH_VAR && !msgs)
+    return xdrg_encode(p, d_native, n, d_heap, heap_len, d_out, cap, d_offsets, stack_limit, d_ws, ws_bytes,
+                       d_status, stream);
+  const dev_tables *T = nullptr;
+  if (int rc = plan_upload(p, &T)) return rc;
+  return var_encode(*p, *T, d_native, n, d_heap, heap_len, d_out, cap, d_offsets, stack_limit, d_ws, ws_bytes,
+                    d_status, msgs ? 4u : 0u, static_cast<hipStream_t>(stream), kEncSized);
 }
 
 size_t xdrg_index_workspace_size(uint64_t len, uint32_t max_msg_len) {

@@ -255,13 +255,32 @@ class Marshaler:
             self.launch_encode(native, n, out, stack_limit=stack_limit, stream=s)
             self.check(s)
             return EncodeResult(out, None)
-        if capacity is None:
-            capacity = int(self.serial_sizes(native, n, stack_limit, heap).to(torch.int64).sum().item())
-        out = torch.empty(max(capacity, 4), dtype=torch.uint8, device=self.device)
         offsets = torch.empty(n + 1, dtype=torch.int64, device=self.device)
+        if capacity is None:  # one size pass: the output is sized from it
+            return self._encode_two_halves(native, n, heap, offsets, stack_limit, msgs=0)
+        out = torch.empty(max(capacity, 4), dtype=torch.uint8, device=self.device)
         self.status.init(s)
         self.launch_encode(native, n, out, heap=heap, offsets=offsets, stack_limit=stack_limit,
                            stream=s)
+        e = self.check(s)
+        return EncodeResult(out[:e.total_bytes], offsets)
+
+    def _encode_two_halves(self, native, n, heap, offsets, stack_limit, msgs: int) -> EncodeResult:
+        """xdr_to_opaque's own order (marshal.h:264-272): xdrg_encode_sizes
+        (xdr_argpack_size) into the workspace, the output allocated from its
+        total, then xdrg_encode_sized over the same sizes: one size pass."""
+        s = _stream()
+        L = A.lib()
+        ws = self._workspace(n)
+        hl = 0 if heap is None else heap.numel()
+        self.status.init(s)
+        A.check(L.xdrg_encode_sizes(self.plan.handle, _ptr(native), n, _ptr(heap), hl, stack_limit, msgs,
+                                    _ptr(ws), ws.numel(), self.status.ptr, s), "xdrg_encode_sizes")
+        total = int(self.check(s).total_bytes)
+        out = torch.empty(max(total, 4), dtype=torch.uint8, device=self.device)
+        A.check(L.xdrg_encode_sized(self.plan.handle, _ptr(native), n, _ptr(heap), hl, _ptr(out), total,
+                                    _ptr(offsets), stack_limit, msgs, _ptr(ws), ws.numel(), self.status.ptr, s),
+                "xdrg_encode_sized")
         e = self.check(s)
         return EncodeResult(out[:e.total_bytes], offsets)
 
@@ -329,13 +348,12 @@ class Marshaler:
         a 4-byte mark BE(size | 0x80000000) then the record's bytes.
         offsets[r] = message r's mark, offsets[n] = total."""
         s = _stream()
-        if capacity is None:
-            if self.plan.is_fixed:
-                capacity = n * (self.plan.fixed_size + 4)
-            else:
-                capacity = int(self.serial_sizes(native, n, stack_limit, heap).to(torch.int64).sum().item()) + 4 * n
-        out = torch.empty(max(capacity, 4), dtype=torch.uint8, device=self.device)
         offsets = torch.empty(n + 1, dtype=torch.int64, device=self.device)
+        if capacity is None:
+            if not self.plan.is_fixed:  # one size pass: the output is sized from it
+                return self._encode_two_halves(native, n, heap, offsets, stack_limit, msgs=1)
+            capacity = n * (self.plan.fixed_size + 4)
+        out = torch.empty(max(capacity, 4), dtype=torch.uint8, device=self.device)
         self.status.init(s)
         self.launch_encode_msgs(native, n, out, offsets, heap=heap, stack_limit=stack_limit, stream=s)
         e = self.check(s)
