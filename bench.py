@@ -56,9 +56,12 @@ def parse():
     ap.add_argument("--no-large", action="store_true",
                     help="skip the 16M-record fixed-path leg (large_batch_16m)")
     ap.add_argument("--host-inclusive", action="store_true",
-                    help="also measure pinned host->device->host rates (PCIe-bound, reported apart)")
+                    help="measure pinned host->device->host rates (PCIe-bound, reported apart; "
+                         "on by default for rec128)")
+    ap.add_argument("--no-host-inclusive", action="store_true")
     ap.add_argument("--cold", action="store_true",
-                    help="also time each kernel alone after evicting the caches")
+                    help="time each kernel alone after evicting the caches (on by default for rec128)")
+    ap.add_argument("--no-cold", action="store_true")
     ap.add_argument("--no-gather", action="store_true",
                     help="N>1: skip the RCCL gather of the encoded shards to rank 0 (timed apart)")
     ap.add_argument("--msgs", action="store_true",
@@ -447,6 +450,19 @@ def large_batch(mar, dev, reps=5, n=1 << 24):
             "encode_decode_gib_s": round(2 * n * mar.plan.fixed_size / GIB / ((e + d) * 1e-3), 2),
             "achieved_GBps": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4), "round_trip_ok": ok,
             "protocol": f"HIP events around each kernel, median of {reps}, device-made record bytes"}
+
+
+def copy_ceiling(mib: int) -> dict | None:
+    """The box's device-copy ceiling past the Infinity Cache: the best of
+    four plain 16-byte copy shapes (tools/probe/copy_ceiling.hip, built by
+    build(); run as a child process), `mib` MiB per buffer, median of 7."""
+    probe = os.path.join(ROOT, "tools", "probe", "copy_ceiling")
+    if not os.access(probe, os.X_OK):
+        return None
+    out = subprocess.run([probe, "--json", str(mib)], capture_output=True, text=True, timeout=120)
+    if out.returncode != 0:
+        return {"error": out.stdout[-200:] + out.stderr[-200:]}
+    return json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
 
 
 def messages_leg(schema, plan, mar, nat, heap, n, reps=20):
@@ -897,16 +913,23 @@ def extra_legs(args, engine, line, alg_bytes):
     if plan.is_fixed and args.schema == "rec128" and not args.no_large:
         try:
             line["large_batch_16m"] = large_batch(mar, nat.device)
+            torch.cuda.empty_cache()
+            ceil = copy_ceiling(2048)  # the same bytes per buffer as 16M records
+            if ceil is not None:
+                lb = line["large_batch_16m"]
+                lb["copy_ceiling"] = ceil
+                lb["frac_of_copy_ceiling"] = round(lb["achieved_GBps"] / (ceil["best_tb_s"] * 1e3), 4)
         except Exception as e:  # reported, never fatal
             line["large_batch_16m"] = {"error": str(e)[:200]}
-    if args.cold and plan.is_fixed:
+    headline = args.schema == "rec128"
+    if (args.cold or headline) and not args.no_cold and plan.is_fixed:
         line["cold_cache"] = cold_cache(mar, nat, engine.xdr, engine.back, n, alg_bytes)
         engine.check()
     if args.msgs:
         line["messages"] = messages_leg(args.schema, plan, mar, nat, heap, n)
     if args.rpc:
         line["rpc_headers"] = rpc_leg(nat.device)
-    if args.host_inclusive:
+    if (args.host_inclusive or headline) and not args.no_host_inclusive:
         try:
             line["host_inclusive"] = (host_inclusive(mar, plan, nat, n, plan.fixed_size) if plan.is_fixed
                                       else host_inclusive_var(mar, plan, nat, heap, n))

@@ -14,6 +14,7 @@ for st in ${STEPS:-tests bench}; do
     tests) timeout -k 10 900 python3 -u -m pytest ${arg:-tests} -m gpu -x -v --timeout 300 --timeout-method thread > "$O/pytest_${arg//\//_}.log" 2>&1 ;;
     smoke) timeout -k 10 300 python3 -u -c 'import __graft_entry__ as g; g.smoke()' > "$O/smoke.log" 2>&1 ;;
     bench) timeout -k 10 400 python3 -u bench.py ${arg//,/ } > "$O/bench_${arg//[ ,-]/_}.log" 2>&1 ;;
+    cppbench) timeout -k 10 300 ./oracle/_ref/dropin_test bench ${arg:-1048576} > "$O/cppbench.log" 2>&1 ;;
     prof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_${arg//[ ,-]/_}" -o run --output-format csv -- python3 bench.py --no-cpu-baseline ${arg//,/ } > "$O/prof_${arg//[ ,-]/_}.log" 2>&1 ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac

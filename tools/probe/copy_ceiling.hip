@@ -71,9 +71,16 @@ __global__ __launch_bounds__(256) void k_write(u32x4 *__restrict__ out, uint64_t
   if (i < n) out[i] = u32x4{uint32_t(i), 1u, 2u, 3u};
 }
 
+// --json MIB: the quick form bench.py runs (the four shapes that matter at
+// one size, 7 reps): one JSON line with the best median rate.
 int main(int argc, char **argv) {
   std::vector<uint64_t> sizes_mib = {256, 2048, 4096};
-  if (argc > 1) { sizes_mib.clear(); for (int i = 1; i < argc; ++i) sizes_mib.push_back(strtoull(argv[i], 0, 10)); }
+  bool json = argc > 1 && std::string(argv[1]) == "--json";
+  if (argc > 1) {
+    sizes_mib.clear();
+    for (int i = json ? 2 : 1; i < argc; ++i) sizes_mib.push_back(strtoull(argv[i], 0, 10));
+    if (sizes_mib.empty()) sizes_mib.push_back(2048);
+  }
   hipDeviceProp_t prop;
   hipGetDeviceProperties(&prop, 0);
   printf("device %s CUs %d\n", prop.gcnArchName, prop.multiProcessorCount);
@@ -93,6 +100,10 @@ int main(int argc, char **argv) {
     auto flat = [&](uint64_t blocks) { return uint32_t(blocks); };
     vs.push_back({"flat_1chunk", 2, [&] { k_flat<false><<<flat((n + 255) / 256), 256>>>(a, b, n); }, {}});
     vs.push_back({"flat_1chunk_nt", 2, [&] { k_flat<true><<<flat((n + 255) / 256), 256>>>(a, b, n); }, {}});
+    if (json) {
+      vs.push_back({"gs_U1_b1024", 2, [&] { k_gs<1, false><<<1024, 256>>>(a, b, n); }, {}});
+      vs.push_back({"memcpy_d2d", 2, [&] { hipMemcpyAsync(b, a, bytes, hipMemcpyDeviceToDevice, 0); }, {}});
+    } else {
     vs.push_back({"flat_2chunk", 2, [&] { k_flatU<2, false><<<flat((n + 511) / 512), 256>>>(a, b, n); }, {}});
     vs.push_back({"flat_4chunk", 2, [&] { k_flatU<4, false><<<flat((n + 1023) / 1024), 256>>>(a, b, n); }, {}});
     vs.push_back({"flat_4chunk_nt", 2, [&] { k_flatU<4, true><<<flat((n + 1023) / 1024), 256>>>(a, b, n); }, {}});
@@ -105,9 +116,10 @@ int main(int argc, char **argv) {
     vs.push_back({"memcpy_d2d", 2, [&] { hipMemcpyAsync(b, a, bytes, hipMemcpyDeviceToDevice, 0); }, {}});
     vs.push_back({"read_only", 1, [&] { k_read<<<4096, 256>>>(a, n, sink); }, {}});
     vs.push_back({"write_only", 1, [&] { k_write<<<uint32_t((n + 255) / 256), 256>>>(b, n); }, {}});
+    }
     for (auto &v : vs) for (int w = 0; w < 2; ++w) v.go();
     hipDeviceSynchronize();
-    for (int rep = 0; rep < 15; ++rep)
+    for (int rep = 0; rep < (json ? 7 : 15); ++rep)
       for (auto &v : vs) {
         hipEventRecord(e0, 0);
         v.go();
@@ -117,6 +129,20 @@ int main(int argc, char **argv) {
         hipEventElapsedTime(&ms, e0, e1);
         v.t.push_back(ms);
       }
+    if (json) {
+      std::string best;
+      double bt = 0;
+      std::string all = "{";
+      for (auto &v : vs) {
+        std::sort(v.t.begin(), v.t.end());
+        const double tb = v.mult * bytes / (v.t[v.t.size() / 2] * 1e-3) / 1e12;
+        all += (all.size() > 1 ? ", \"" : "\"") + v.name + "\": " + std::to_string(tb);
+        if (tb > bt) { bt = tb; best = v.name; }
+      }
+      printf("{\"mib_per_buffer\": %lu, \"best_tb_s\": %.4f, \"best\": \"%s\", \"median_tb_s\": %s}}\n",
+             (unsigned long)mib, bt, best.c_str(), all.c_str());
+      continue;
+    }
     printf("== %lu MiB per buffer ==\n", (unsigned long)mib);
     for (auto &v : vs) {
       std::sort(v.t.begin(), v.t.end());

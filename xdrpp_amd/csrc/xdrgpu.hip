@@ -1513,19 +1513,23 @@ int run_fixed(const xdrg_plan &p, const dev_tables &T, bool decode, const void *
   const fixed_prog &pg = decode ? p.dec : p.enc;
   const bool checks = decode && p.has_checks;
   if (p.path == XDRG_PATH_FIXED_REG && aligned(in, 16) && aligned(out, 16)) {
-    // Launch shapes from tools/tune/tune_fixed.py (rec128):
+    // Launch shapes from tools/tune/tune_fixed.py (rec128) and the copy
+    // ceiling probe (tools/probe/copy_ceiling.hip, profiles/r03c):
     //  * working set (input + output) that fits the 256 MiB Infinity Cache
     //    (1M records = 256 MiB): plain 16-byte loads/stores, one chunk in
     //    flight per lane, 1024 workgroups -> 6.9 TB/s back to back;
-    //  * larger batches stream from HBM: non-temporal loads/stores, two
-    //    chunks in flight per lane, 512 workgroups -> 5.76 TB/s at 16M
-    //    records (a plain 16-byte copy of the same bytes: 5.67 TB/s).
+    //  * larger batches stream from HBM: one chunk per lane over a one-shot
+    //    grid with non-temporal loads and stores -- the box's best 16-byte
+    //    copy past the cache, 6.58 TB/s at 2 GiB per buffer, where any
+    //    grid-stride loop measured 4.6-5.6 TB/s (the old 512-workgroup,
+    //    two-in-flight shape: 5.54 TB/s at 16M records).
     const uint32_t W = p.fixed_size;
     const uint32_t cpr = W / 16;
     const uint64_t nchunks = nrec * cpr;
     const bool streaming = nchunks * 32ull > kMallBytes * 3 / 2;  // in+out bytes > 384 MiB
     uint64_t blocks = (nchunks + 255) / 256;
-    blocks = std::min<uint64_t>(blocks, streaming ? 512 : 1024);
+    if (!streaming) blocks = std::min<uint64_t>(blocks, 1024);
+    if (blocks > 0x7fffffffull) return XDRG_EUNSUPPORTED;
     const uint32_t g0 = cpr / gcd32(cpr, 256);
     blocks = align_up(std::max<uint64_t>(blocks, 1), g0);
     const reg_word *prog = decode ? T.d_dec_reg : T.d_enc_reg;
@@ -1535,7 +1539,7 @@ int run_fixed(const xdrg_plan &p, const dev_tables &T, bool decode, const void *
 #define LAUNCH_REG(B, C)                                                                         \
   do {                                                                                           \
     if (streaming)                                                                               \
-      k_fixed_reg<B, C, 2, true><<<blocks, 256, 0, s>>>(i4, o4, nchunks, cpr, prog, T.d_table, err); \
+      k_fixed_reg<B, C, 1, true><<<blocks, 256, 0, s>>>(i4, o4, nchunks, cpr, prog, T.d_table, err); \
     else                                                                                         \
       k_fixed_reg<B, C, 1, false><<<blocks, 256, 0, s>>>(i4, o4, nchunks, cpr, prog, T.d_table, err); \
   } while (0)
