@@ -224,7 +224,7 @@ enum xdrg_err {
   XDRG_ERR_MSG_TOO_LONG = 16,   /* msg_sock maxmsglen_  msgsock.cc:99-111 */
   XDRG_ERR_MSG_MISMATCH = 17,   /* mark disagrees with the record index  */
   XDRG_ERR_MSG_COUNT = 18,      /* more messages than the index can hold */
-  XDRG_ERR_INTERNAL = 19,       /* a device-side wait gave up (the kernel still ends) */
+  /* 19 is not used: no kernel waits on another workgroup */
   XDRG_ERR_INDEX_LONG = 20      /* xdrg_index_records: a record longer than its bound */
 };
 

@@ -4,7 +4,7 @@
 // reference marshaler (xdrpp/marshal.cc compiled in place) over GENUINE
 // xdrc output (oracle/Makefile):
 //   test_recursive   tests/xdrtest.x:29-33, chains through `next` of
-//                    0 .. 3000 nodes (the lengths straddle the device's
+//                    1 .. 3000 nodes (the lengths straddle the device's
 //                    private frames and both deep passes, sub_kernels.h);
 //   rp__list         xdrpp/rpcb_prot.x:24-37, the RPCBPROC_DUMP reply
 //                    list, 500 entries (plus 33, one past the old bound).

@@ -22,4 +22,4 @@ for st in ${STEPS:-tests bench}; do
   echo "[step] $st rc=$rc $(date +%T)"
   [ $rc -ne 0 ] && { tail -30 "$O"/*.log; exit $rc; }
 done
-tail -3 "$O"/*.log
+tail -n 3 "$O"/*.log

@@ -52,7 +52,6 @@ ERR_MSG_FRAGMENT = 15
 ERR_MSG_TOO_LONG = 16
 ERR_MSG_MISMATCH = 17
 ERR_MSG_COUNT = 18
-ERR_INTERNAL = 19
 ERR_INDEX_LONG = 20
 
 MARK_LAST = 0x80000000  # XDRG_MARK_LAST: last-fragment bit of a record mark

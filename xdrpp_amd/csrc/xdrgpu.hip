@@ -2688,7 +2688,6 @@ const char *xdrg_error_message(int code) {
   case XDRG_ERR_MSG_TOO_LONG: return "msg_sock: rejecting message (too long)";
   case XDRG_ERR_MSG_MISMATCH: return "record mark does not match the record index";
   case XDRG_ERR_MSG_COUNT: return "more messages than the record index holds";
-  case XDRG_ERR_INTERNAL: return "xdrgpu internal error (device wait gave up)";
   case XDRG_ERR_INDEX_LONG: return "record longer than the device record index window";
   default: return "unknown xdrgpu error";
   }
