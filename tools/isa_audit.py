@@ -1,0 +1,102 @@
+"""Audit of the pipelined encode windows in compiled code (var_kernels.h
+XDRG_ENC_PIPE): the next window's payload loads are inline asm that the
+compiler does not count, and their wait is an explicit s_waitcnt vmcnt(SW)
+after the window's SW buffer stores.  That wait is right only if, in the
+compiled kernel, exactly the SW stores (and no other vector memory
+instruction) sit between the last asm load and the wait, no compiler wait
+on vmcnt sits among them, and nothing touches the loads' destination
+registers before the wait.  This compiles a plan's generated source with
+hipcc -save-temps and checks every such sequence.
+
+    python tools/isa_audit.py recvar rpc vecrec
+"""
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+VMEM = re.compile(r"^(global_|buffer_|flat_|scratch_)")
+
+
+def regs(text):
+    out = set()
+    for m in re.finditer(r"v\[(\d+):(\d+)\]", text):
+        out |= set(range(int(m.group(1)), int(m.group(2)) + 1))
+    for m in re.finditer(r"\bv(\d+)\b", text):
+        out.add(int(m.group(1)))
+    return out
+
+
+def kernel_asm(schema, workdir):
+    import ctypes as C
+    from xdrpp_amd import _abi as A, build as B, schemas as S
+    from xdrpp_amd.build import _Plan
+    p = _Plan(S.ALL[schema])
+    L = A.lib()
+    n = C.c_size_t(0)
+    A.check(L.xdrg_plan_kernel_source(p.handle, None, 0, C.byref(n)), "xdrg_plan_kernel_source")
+    buf = C.create_string_buffer(n.value + 1)
+    A.check(L.xdrg_plan_kernel_source(p.handle, buf, n.value + 1, C.byref(n)), "xdrg_plan_kernel_source")
+    src = os.path.join(workdir, f"{schema}.hip")
+    with open(src, "w") as f:
+        f.write(buf.value.decode())
+    subprocess.check_call([B.hipcc(), "--genco", f"--offload-arch={B.ARCH}", "-O3", "-std=c++17", "-save-temps",
+                           "-I", B.CSRC, "-I", os.path.join(ROOT, "include"), "-o", os.path.join(workdir, "x.co"),
+                           src], cwd=workdir)
+    s = open([os.path.join(workdir, f) for f in os.listdir(workdir)
+              if f.startswith(schema) and f.endswith(".s") and "gfx" in f][0]).read()
+    i = s.index("xdrg_spec_encode:")
+    return s[i:s.index(".Lfunc_end", i)].splitlines()
+
+
+def audit(lines):
+    """Number of pipelined sequences checked; raises AssertionError on a bad one."""
+    ins = [ln.strip() for ln in lines]
+    asm_loads = [k for k, t in enumerate(ins) if t.startswith("global_load_dwordx4") and k > 0
+                 and ins[k - 1] == ";;#ASMSTART"]
+    if not asm_loads:
+        return 0  # no payload slots (vecrec: elements only) or XDRG_ENC_PIPE off
+    checked = 0
+    for k in asm_loads:
+        nxt = [j for j in asm_loads if j > k]
+        if nxt and not any(VMEM.match(ins[j]) or ins[j].startswith("s_waitcnt vmcnt") for j in range(k + 1, nxt[0])):
+            continue  # not the batch's last load
+        dst = regs(ins[k].split(",")[0])
+        group = [j for j in asm_loads if j <= k and j >= k - 80]
+        dsts = set().union(*(regs(ins[j].split(",")[0]) for j in group))
+        stores, wait = 0, None
+        for j in range(k + 1, len(ins)):
+            t = ins[j]
+            if not t or t.startswith(";") or t.startswith("."):
+                continue
+            m = re.match(r"s_waitcnt vmcnt\((\d+)\)", t)
+            if m:
+                assert ins[j - 1] == ";;#ASMSTART", f"compiler vmcnt wait among the stores: line {j}: {t}"
+                wait = int(m.group(1))
+                break
+            if VMEM.match(t):
+                assert t.startswith("buffer_store_dwordx4"), f"other memory op before the wait: {t}"
+                stores += 1
+            elif regs(t) & dsts and not t.startswith("buffer_store"):
+                raise AssertionError(f"asm load destination touched before its wait: {t}")
+            # the only branch allowed: the skip of the wait when nothing was
+            # prefetched, after every store (the fall-through reaches the wait)
+            assert not t.startswith("s_cbranch") or stores > 0, f"branch among the loads and stores: {t}"
+        assert wait is not None and stores == wait, f"{stores} stores before vmcnt({wait})"
+        checked += 1
+    assert checked, "asm loads without a load/store/wait sequence"
+    return checked
+
+
+def main():
+    for schema in sys.argv[1:] or ["recvar", "rpc", "vecrec"]:
+        with tempfile.TemporaryDirectory() as d:
+            print(schema, "ok:", audit(kernel_asm(schema, d)), "pipelined window sequence(s)")
+
+
+if __name__ == "__main__":
+    main()

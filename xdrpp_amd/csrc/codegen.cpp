@@ -852,8 +852,8 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
     << "    uint8_t *xdr, uint64_t cap, uint64_t *offsets, const uint32_t *sizes,\n"
     << "    const unsigned long long *block_base, uint32_t stack_limit, uint32_t C,\n"
     << "    uint32_t mark, unsigned long long *err) {\n"
-    << "  var_encode_body<plan_walk, " << info.slots << ", 4, " << (regs ? p.stride / 4 : 0)
-    << ">(plan_walk{}, native, n, stride, heap, heap_len,\n"
+    << "  var_encode_body<plan_walk, " << info.slots << ", 4, " << (regs ? p.stride / 4 : 0) << ", "
+    << (kwords > 0 ? 4096 : 8192) << "u>(plan_walk{}, native, n, stride, heap, heap_len,\n"
     << "      xdr, cap, offsets, sizes, block_base, stack_limit, C, mark, err);\n}\n\n";
   for (int cp = 0; cp < 2; ++cp)
     s << "extern \"C\" __global__ __launch_bounds__(64) void xdrg_spec_decode" << (cp ? "_copy" : "") << "(\n"

@@ -53,11 +53,69 @@
 #ifndef XDRG_DEC_NT
 #define XDRG_DEC_NT 1
 #endif
+// Encode window pipelining (A/B: tools/tune/enc_stamps.py CFLAGS
+// -DXDRG_ENC_PIPE=0/1): the next window's first payload batch is loaded
+// before the current window's stores are issued, and the stores of a full
+// window are a fixed number of buffer stores per lane (out-of-range lanes
+// dropped by the descriptor's range check), so that waiting on those loads
+// does not wait on the stores too (gfx9: loads and stores share vmcnt).
+// The loads are inline asm the compiler does not count, waited for by an
+// explicit vmcnt(SW) after the SW stores (tools/gpu/isa_audit.py checks the
+// shape in the compiled code).  MI355X, 1M records, kernel alone
+// (profiles/r03f): rpc 0.1616 -> 0.1582 ms, vecrec 0.0977 -> 0.0969,
+// recvar 0.1073 -> 0.1066.
+#ifndef XDRG_ENC_PIPE
+#define XDRG_ENC_PIPE 1
+#endif
 
 namespace xdrg {
 namespace dev {
 
 // ---------------------------------------------------------------- encode
+template <bool B> struct bool_tag { static constexpr bool value = B; };
+
+// The 16 bytes at heap offset hs, bytes at or past len reading 0, for a
+// chunk within 16 bytes of the heap's end (hs + 16 > len).  One 16-byte
+// load ending at the heap's end and a byte shift; a heap shorter than 16
+// bytes is read byte by byte, each load waited for inside its own asm
+// statement so that no load of this rare path stays pending in the
+// compiler's count (the pipelined windows count their own loads).
+__device__ __forceinline__ u32x4 heap_tail16(const uint8_t *heap, uint64_t len, uint64_t hs) {
+  if (hs >= len) return u32x4{0u, 0u, 0u, 0u};
+  if (len >= 16) {
+    const u32x4 t = ld16u(heap + len - 16);
+    const uint32_t d = static_cast<uint32_t>(hs - (len - 16));  // 1..15: bytes of t before hs
+    const uint32_t w = d >> 2, sb = d & 3u;
+    const uint32_t t0 = w == 0 ? t.x : w == 1 ? t.y : w == 2 ? t.z : t.w;
+    const uint32_t t1 = w == 0 ? t.y : w == 1 ? t.z : w == 2 ? t.w : 0u;
+    const uint32_t t2 = w == 0 ? t.z : w == 1 ? t.w : 0u;
+    const uint32_t t3 = w == 0 ? t.w : 0u;
+    return u32x4{__builtin_amdgcn_alignbyte(t1, t0, sb), __builtin_amdgcn_alignbyte(t2, t1, sb),
+                 __builtin_amdgcn_alignbyte(t3, t2, sb), __builtin_amdgcn_alignbyte(0u, t3, sb)};
+  }
+  uint32_t v[4] = {0u, 0u, 0u, 0u};
+  for (uint32_t k = 0; k < 16u && hs + k < len; ++k) {
+    uint32_t byte;
+    asm volatile("global_load_ubyte %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=&v"(byte) : "v"(heap + hs + k) : "memory");
+    v[k >> 2] |= byte << (8u * (k & 3u));
+  }
+  return u32x4{v[0], v[1], v[2], v[3]};
+}
+
+// s_waitcnt vmcnt(N) that also defines `v` (loaded by inline asm the
+// compiler does not count): nothing reads v before this wait
+template <uint32_t N, int U>
+__device__ __forceinline__ void vm_wait_after(u32x4 (&v)[U]) {
+  if constexpr (U == 2)
+    asm volatile("s_waitcnt vmcnt(%2)" : "+v"(v[0]), "+v"(v[1]) : "n"(N) : "memory");
+  else if constexpr (U == 4)
+    asm volatile("s_waitcnt vmcnt(%4)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]) : "n"(N) : "memory");
+  else if constexpr (U == 8)
+    asm volatile("s_waitcnt vmcnt(%8)"
+                 : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7])
+                 : "n"(N) : "memory");
+}
+
 // LDS of an encode wave: the native tile (kept for every window round), the
 // payload slots of the 64 lanes, their inclusive chunk counts, and the image
 // of one window of the wave's output stretch.
@@ -249,7 +307,7 @@ __device__ __forceinline__ uint32_t chunks_starting_before(const enc_ctx<KMAX, B
 // WL (plans with a bounded scalar word list, W::kWords > 0, walked from
 // registers): the list aliases the tile, which the walk no longer reads once
 // the lane's record is in registers; the walk runs once, in the first round.
-template <class W, int KMAX, int U, int NW = 0>
+template <class W, int KMAX, int U, int NW = 0, uint32_t CMAX = 0>
 __device__ __forceinline__ void var_encode_body(
     const W &w, const uint8_t *__restrict__ native, uint64_t n, uint32_t stride,
     const uint8_t *__restrict__ heap, uint64_t heap_len, uint8_t *__restrict__ xdr, uint64_t cap,
@@ -306,6 +364,106 @@ __device__ __forceinline__ void var_encode_body(
   for (int k = 0; k < KMAX; ++k) { c.psr[k] = 0; c.pds[k] = 0; c.pln[k] = 0; c.rb[k] = 0; }
   bool ok = szok;
   uint32_t M = 0;
+
+  // one batch of payload chunks: U per lane, chunks c0 + 64 u + lane
+  struct batch {
+    u32x4 val[U];
+    uint64_t hs[U];
+    uint32_t at[U], nb[U], rm[U];
+    bool fast[U];
+    uint32_t tok;  // 0, defined after the asm loads (orders the stores after them)
+  } B;
+  B.tok = 0;
+  // ASM: the loads as inline asm, which the compiler does not count: their
+  // wait is the explicit one after the window's stores (XDRG_ENC_PIPE)
+  auto issue = [&](uint32_t c0, uint32_t chi, batch &b, auto asm_tag) {
+    uint32_t lo[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) lo[u] = 0;
+    uint32_t ix[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) ix[u] = min(c0 + 64u * u + lane, chi - 1u);
+#pragma unroll
+    for (uint32_t s = 32; s; s >>= 1) {
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (cum[lo[u] + s - 1u] <= ix[u]) lo[u] += s;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      uint32_t rem = ix[u] - (lo[u] ? cum[lo[u] - 1u] : 0u);
+      const echunk_desc *dl = desc + lo[u] * KMAX;
+      echunk_desc d = dl[0];
+#pragma unroll
+      for (int k = 0; k + 1 < KMAX; ++k) {
+        const uint32_t nq = (d.len + 15u) >> 4;
+        if (rem >= nq) {
+          rem -= nq;
+          d = dl[k + 1];
+        }
+      }
+      const bool live = c0 + 64u * u + lane < chi;
+      const uint32_t q16 = rem << 4;
+      b.hs[u] = d.src + q16;
+      b.rm[u] = live ? d.len - q16 : 16u;
+      b.at[u] = d.dst + q16;
+      b.nb[u] = live ? min(16u, ((d.len + 3u) & ~3u) - q16) : 0u;
+      b.fast[u] = live && b.hs[u] + 16u <= heap_len;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (b.fast[u]) {
+        if constexpr (decltype(asm_tag)::value)
+          asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(b.val[u]) : "v"(heap + b.hs[u]));
+        else if constexpr ((XDRG_ENC_NT & 1) != 0)
+          b.val[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(heap + b.hs[u]));
+        else
+          b.val[u] = ld16u(heap + b.hs[u]);
+      }
+    if constexpr (decltype(asm_tag)::value) asm volatile("v_mov_b32 %0, 0" : "=v"(b.tok));
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto place = [&](batch &b, uint32_t w0) {
+    // every load of the batch counts as consumed here, on every path (a
+    // load left pending on some path makes the compiler wait for all
+    // memory before the next write of these registers)
+#pragma unroll
+    for (int u = 0; u < U; ++u) asm volatile("" ::"v"(b.val[u]));
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (!b.nb[u]) continue;
+      u32x4 x = b.val[u];
+      if (!b.fast[u]) x = heap_tail16(heap, heap_len, b.hs[u]);
+      const int32_t rr = static_cast<int32_t>(b.rm[u]);
+      if (rr < 16) {  // zero the pad bytes after the payload (put_bytes)
+        x.x &= keep_bytes(rr);
+        x.y &= keep_bytes(rr - 4);
+        x.z &= keep_bytes(rr - 8);
+        x.w &= keep_bytes(rr - 12);
+      }
+      const uint32_t j = b.at[u] - w0;
+      if (j + 16u <= C && b.at[u] >= w0) {
+        uint32_t *wp = reinterpret_cast<uint32_t *>(img + j);
+        wp[0] = x.x;
+        if (b.nb[u] > 4u) wp[1] = x.y;
+        if (b.nb[u] > 8u) wp[2] = x.z;
+        if (b.nb[u] > 12u) wp[3] = x.w;
+      } else {  // a chunk across a window edge
+        c.wput(b.at[u], x.x);
+        if (b.nb[u] > 4u) c.wput(b.at[u] + 4, x.y);
+        if (b.nb[u] > 8u) c.wput(b.at[u] + 8, x.z);
+        if (b.nb[u] > 12u) c.wput(b.at[u] + 12, x.w);
+      }
+    }
+  };
+  // pipelined windows (XDRG_ENC_PIPE): full windows leave as SW buffer
+  // stores per lane; the wave's head chunk (shared with the previous wave's
+  // stretch) is kept by lane 0 and written last, word by word
+  constexpr uint32_t SW = CMAX / 1024u;
+  constexpr bool kPipe = XDRG_ENC_PIPE && SW > 0 && (U == 2 || U == 4 || U == 8);  // vm_wait_after's shapes
+  const bool pipe = kPipe && C <= CMAX && wave_out + T <= cap;
+  bool pf = false;
+  u32x4 head = u32x4{0u, 0u, 0u, 0u};
   for (uint32_t rd = 0; rd < rounds; ++rd) {
     const uint32_t w0 = rd * C;
     c.w0 = w0;
@@ -384,87 +542,14 @@ __device__ __forceinline__ void var_encode_body(
     // whose chunks reach past i - cum[L-1].
     const uint32_t clo = rl32(wave_incl_scan(chunks_ending_by(c, w0)), 63);
     const uint32_t chi = min(M, rl32(wave_incl_scan(chunks_starting_before(c, w0 + C)), 63));
-    for (uint32_t c0 = clo; c0 < chi; c0 += 64u * U) {
-      uint32_t lo[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) lo[u] = 0;
-      uint32_t ix[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) ix[u] = min(c0 + 64u * u + lane, chi - 1u);
-#pragma unroll
-      for (uint32_t s = 32; s; s >>= 1) {
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-          if (cum[lo[u] + s - 1u] <= ix[u]) lo[u] += s;
-      }
-      echunk_desc d[U];
-      uint32_t q[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        uint32_t rem = ix[u] - (lo[u] ? cum[lo[u] - 1u] : 0u);
-        const echunk_desc *dl = desc + lo[u] * KMAX;
-        d[u] = dl[0];
-#pragma unroll
-        for (int k = 0; k + 1 < KMAX; ++k) {
-          const uint32_t nq = (d[u].len + 15u) >> 4;
-          if (rem >= nq) {
-            rem -= nq;
-            d[u] = dl[k + 1];
-          }
-        }
-        q[u] = rem;
-      }
-      u32x4 val[U];
-      uint64_t hs[U];
-      uint32_t at[U], nb[U], rm[U];
-      bool fast[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const bool live = c0 + 64u * u + lane < chi;
-        const uint32_t q16 = q[u] << 4;
-        hs[u] = d[u].src + q16;
-        rm[u] = live ? d[u].len - q16 : 16u;
-        at[u] = d[u].dst + q16;
-        nb[u] = live ? min(16u, ((d[u].len + 3u) & ~3u) - q16) : 0u;
-        fast[u] = live && hs[u] + 16u <= heap_len;
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (fast[u]) {
-          if constexpr ((XDRG_ENC_NT & 1) != 0)
-            val[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(heap + hs[u]));
-          else
-            val[u] = ld16u(heap + hs[u]);
-        }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (!nb[u]) continue;
-        u32x4 x = val[u];
-        if (!fast[u])
-          x = u32x4{unaligned_word(heap, heap_len, hs[u]), unaligned_word(heap, heap_len, hs[u] + 4),
-                    unaligned_word(heap, heap_len, hs[u] + 8), unaligned_word(heap, heap_len, hs[u] + 12)};
-        const int32_t rr = static_cast<int32_t>(rm[u]);
-        if (rr < 16) {  // zero the pad bytes after the payload (put_bytes)
-          x.x &= keep_bytes(rr);
-          x.y &= keep_bytes(rr - 4);
-          x.z &= keep_bytes(rr - 8);
-          x.w &= keep_bytes(rr - 12);
-        }
-        const uint32_t j = at[u] - w0;
-        if (j + 16u <= C && at[u] >= w0) {
-          uint32_t *wp = reinterpret_cast<uint32_t *>(img + j);
-          wp[0] = x.x;
-          if (nb[u] > 4u) wp[1] = x.y;
-          if (nb[u] > 8u) wp[2] = x.z;
-          if (nb[u] > 12u) wp[3] = x.w;
-        } else {  // a chunk across a window edge
-          c.wput(at[u], x.x);
-          if (nb[u] > 4u) c.wput(at[u] + 4, x.y);
-          if (nb[u] > 8u) c.wput(at[u] + 8, x.z);
-          if (nb[u] > 12u) c.wput(at[u] + 12, x.w);
-        }
-      }
+    uint32_t c0 = clo;
+    if (pf) {  // this window's first batch was loaded during the last window's stores
+      place(B, w0);
+      c0 += 64u * U;
+    }
+    for (; c0 < chi; c0 += 64u * U) {
+      issue(c0, chi, B, bool_tag<false>{});
+      place(B, w0);
     }
     wave_sync();
     if (rd + 1 == rounds) XDRG_STAMP(4);
@@ -472,7 +557,35 @@ __device__ __forceinline__ void var_encode_body(
     // ---- window -> stream: aligned 16-byte chunks, words at the stretch's edges
     const uint64_t ws = g0 + w0;
     const uint64_t we = min<uint64_t>(ws + C, ge);
-    if (we > ws) {
+    pf = false;
+    if (pipe && rd + 1 < rounds) {
+      // a full window (we = ws + C): first the next window's first batch...
+      const uint32_t w1 = w0 + C;
+      const uint32_t nlo = rl32(wave_incl_scan(chunks_ending_by(c, w1)), 63);
+      const uint32_t nhi = min(M, rl32(wave_incl_scan(chunks_starting_before(c, w1 + C)), 63));
+      if (nlo < nhi) {
+        issue(nlo, nhi, B, bool_tag<true>{});
+        pf = true;
+      }
+      // ...then SW stores per lane, none skipped by a branch
+      if (rd == 0 && sh && lane == 0) head = *reinterpret_cast<const u32x4 *>(img);
+      const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>(xdr + ws) >> 32));
+      const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>(xdr + ws)));
+      const auto rs = __builtin_amdgcn_make_buffer_rsrc(
+          reinterpret_cast<void *>((static_cast<uint64_t>(hi) << 32) | lo), 0, C, 0x00020000);
+      const uint32_t nc = C >> 4;
+#pragma unroll
+      for (uint32_t j = 0; j < SW; ++j) {
+        const uint32_t k = lane + 64u * j;
+        const bool drop = k >= nc || (rd == 0 && k == 0 && sh);
+        const u32x4 v = *reinterpret_cast<const u32x4 *>(img + 16u * min(k, nc - 1u));
+        __builtin_amdgcn_raw_buffer_store_b128(v, rs, (drop ? 0x80000000u : 16u * k) + B.tok, 0,
+                                               (XDRG_ENC_NT & 2) != 0 ? 2 : 0);
+      }
+      // the prefetched loads were issued before these SW stores and vmcnt
+      // retires in order: at most SW outstanding = every load has landed
+      if (pf) vm_wait_after<SW>(B.val);
+    } else if (we > ws) {
       const uint32_t nc = static_cast<uint32_t>((we - ws + 15u) >> 4);
       for (uint32_t k = lane; k < nc; k += 64u) {
         const uint64_t ca = ws + 16ull * k;
@@ -492,6 +605,11 @@ __device__ __forceinline__ void var_encode_body(
       }
     }
     wave_sync();  // the next window's walk reuses the image
+  }
+  if (pipe && rounds > 1 && sh && lane == 0) {  // the head chunk's words of this wave
+    if (sh <= 4) st32(xdr + g0 + 4, head.y);
+    if (sh <= 8) st32(xdr + g0 + 8, head.z);
+    st32(xdr + g0 + 12, head.w);
   }
   XDRG_STAMP(5);
 }

@@ -407,19 +407,21 @@ __global__ __launch_bounds__(64) void k_var_size(const uint8_t *__restrict__ nat
 }
 
 // Exclusive scan of nb block sums in place; writes the total to
-// status->total_bytes and offsets[n].  Workgroups of 16 waves, each owning
-// tiles of 4096 values.  A tile's loads are coalesced into LDS; each thread
-// scans 4 contiguous values serially, the thread totals take one 64-bit
-// wave scan, the 16 wave totals one more pass.  With nb <= kScanMulti
-// every tile has its own workgroup, which first sums all values before its
-// tile (coalesced, all loads in flight; at most 15 x 4096 values) -- no
-// inter-workgroup communication, one memory round trip per workgroup.
-// Larger nb: one workgroup walks the tiles carrying the running total.
-// (Measured on MI355X: per-row wave scans of 16 x 1024 values took ~12 us
-// for any nb; the single-workgroup tile walk takes ~3.5 us per tile.)
+// status->total_bytes and offsets[n].  Workgroups of 16 waves.  A tile's
+// loads are coalesced into LDS; each thread scans SUB contiguous values
+// serially, the thread totals take one 64-bit wave scan, the 16 wave totals
+// one more pass.  With nb <= kScanMulti every 1024-value tile has its own
+// workgroup, which first sums all values before its tile (coalesced, its
+// own value's load and up to 16 more per thread in flight at once) -- no
+// inter-workgroup communication, one memory round trip per workgroup for
+// nb <= 16K (1M records).  Larger nb: one workgroup walks 4096-value tiles
+// carrying the running total.  (Measured on MI355X: per-row wave scans of
+// 16 x 1024 values took ~12 us for any nb; the single-workgroup tile walk
+// ~3.5 us per tile; 4096-value tiles per workgroup 7.7 us for 16K values.)
 constexpr uint32_t kScanNT = 1024, kScanSub = 4, kScanTile = kScanNT * kScanSub;
-constexpr uint32_t kScanMulti = 16u * kScanTile;
+constexpr uint32_t kScanMulti = 64u * kScanNT;
 
+template <uint32_t SUB = kScanSub>
 __device__ __forceinline__ unsigned long long scan_tile(const unsigned long long *in,
                                                         unsigned long long *out,
                                                         uint64_t t0, uint32_t nb,
@@ -430,15 +432,15 @@ __device__ __forceinline__ unsigned long long scan_tile(const unsigned long long
   const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   auto sk = [](uint32_t e) { return e + (e >> 5); };  // skew: fewer bank conflicts
 #pragma unroll
-  for (uint32_t k = 0; k < kScanSub; ++k) {
+  for (uint32_t k = 0; k < SUB; ++k) {
     const uint32_t e = k * kScanNT + tid;
     buf[sk(e)] = t0 + e < nb ? in[t0 + e] : 0ull;
   }
   __syncthreads();
-  unsigned long long x[kScanSub], tsum = 0;
+  unsigned long long x[SUB], tsum = 0;
 #pragma unroll
-  for (uint32_t k = 0; k < kScanSub; ++k) {
-    x[k] = buf[sk(kScanSub * tid + k)];
+  for (uint32_t k = 0; k < SUB; ++k) {
+    x[k] = buf[sk(SUB * tid + k)];
     tsum += x[k];
   }
   unsigned long long incl = tsum;
@@ -457,13 +459,13 @@ __device__ __forceinline__ unsigned long long scan_tile(const unsigned long long
   }
   unsigned long long run = carry + wbase + incl - tsum;
 #pragma unroll
-  for (uint32_t k = 0; k < kScanSub; ++k) {
-    buf[sk(kScanSub * tid + k)] = run;
+  for (uint32_t k = 0; k < SUB; ++k) {
+    buf[sk(SUB * tid + k)] = run;
     run += x[k];
   }
   __syncthreads();
 #pragma unroll
-  for (uint32_t k = 0; k < kScanSub; ++k) {
+  for (uint32_t k = 0; k < SUB; ++k) {
     const uint32_t e = k * kScanNT + tid;
     if (t0 + e < nb) out[t0 + e] = buf[sk(e)];
   }
@@ -483,25 +485,27 @@ __global__ __launch_bounds__(1024) void k_scan_blocks(const unsigned long long *
   const uint32_t tid = threadIdx.x;
   unsigned long long carry = 0;
   if (MULTI) {
-    // this workgroup's tile; its carry = the sum of every value before it
-    const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * kScanTile;
+    // this workgroup's 1024-value tile; its carry = the sum of every value
+    // before it, up to 16 loads per thread in flight
+    const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * kScanNT;
     unsigned long long part = 0;
-    uint64_t j = tid;
-    for (; j + 7u * kScanNT < t0; j += 8u * kScanNT) {  // 8 loads in flight per thread
-      unsigned long long q[8];
+    for (uint64_t j0 = 0; j0 < t0; j0 += 16u * kScanNT) {
+      unsigned long long q[16];
 #pragma unroll
-      for (uint32_t k = 0; k < 8; ++k) q[k] = in[j + k * kScanNT];
+      for (uint32_t k = 0; k < 16; ++k) {
+        const uint64_t j = j0 + k * kScanNT + tid;
+        q[k] = j < t0 ? in[j] : 0ull;
+      }
 #pragma unroll
-      for (uint32_t k = 0; k < 8; ++k) part += q[k];
+      for (uint32_t k = 0; k < 16; ++k) part += q[k];
     }
-    for (; j < t0; j += kScanNT) part += in[j];
     for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
     if ((tid & 63) == 0) wtot[tid >> 6] = part;
     __syncthreads();
 #pragma unroll
     for (uint32_t w = 0; w < kScanNT / 64; ++w) carry += wtot[w];
     __syncthreads();
-    carry = scan_tile(in, out, t0, nb, carry, buf, wtot);
+    carry = scan_tile<1>(in, out, t0, nb, carry, buf, wtot);
     if (tid == 0 && blockIdx.x == gridDim.x - 1) {
       status->total_bytes = carry;
       if (offsets) offsets[n] = carry;
@@ -1814,7 +1818,7 @@ int launch_block_scan(const unsigned long long *in, unsigned long long *out, uin
                       xdrg_status *status, uint64_t *offsets, uint64_t n, void *stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (nb <= kScanMulti && in != out)
-    k_scan_blocks<true><<<(nb + kScanTile - 1) / kScanTile, 1024, 0, s>>>(in, out, nb, status,
+    k_scan_blocks<true><<<(nb + kScanNT - 1) / kScanNT, 1024, 0, s>>>(in, out, nb, status,
                                                                           offsets, n);
   else
     k_scan_blocks<false><<<1, 1024, 0, s>>>(in, out, nb, status, offsets, n);
