@@ -77,7 +77,7 @@ def parse():
                     help="a file defining Engine, in place of the GPU step (tests only: "
                          "tests/bench_cpu_engine.py rehearses the multi-rank plumbing on CPU over gloo)")
     ap.add_argument("--schema", default="rec128",
-                    choices=["rec128", "numerics", "recvar", "rpc", "vecrec"],
+                    choices=["rec128", "numerics", "recvar", "rpc", "vecrec", "containertest"],
                     help="rec128 is the headline; numerics/recvar/rpc measure BASELINE.json "
                          "configs 1, 3, 4; vecrec covers xvector<T>/pointer<T>")
     return ap.parse_args()
@@ -695,10 +695,14 @@ class GpuEngine:
         enc_alg = n * S_ + H + X + 8 * (n + 1)
         dec_alg = X + 8 * (n + 1) + n * S_ + X + self.element_bytes()
         spec = bool(info.specialized)  # plan-specialized kernels ran (built at warmup)
-        size_k = "k_size_linear" if plan_linear(plan) else ("xdrg_spec_size" if spec else "k_var_size")
+        sub = bool((plan.cp.ops["flags"] & A.F_SUB).any())  # element subroutines: the frame walk
+        size_k = ("k_sub_size" if sub and not spec else "k_size_linear" if plan_linear(plan)
+                  else "xdrg_spec_size" if spec else "k_var_size")
+        enc_k = "xdrg_spec_encode" if spec else "k_sub_encode" if sub else "k_var_encode_i"
+        dec_k = "xdrg_spec_decode_copy" if spec else "k_sub_decode" if sub else "k_var_decode_w"
         if np.mean(enc_ms) >= np.mean(dec_ms):
-            return f"{size_k}+k_scan_blocks+" + ("xdrg_spec_encode" if spec else "k_var_encode_i"), enc_alg, enc_ms
-        return ("xdrg_spec_decode_copy" if spec else "k_var_decode_w"), dec_alg, dec_ms
+            return f"{size_k}+k_scan_blocks+{enc_k}", enc_alg, enc_ms
+        return dec_k, dec_alg, dec_ms
 
     def element_bytes(self) -> int:
         """Native bytes of the element arrays a decode writes: count x stride

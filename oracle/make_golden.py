@@ -25,11 +25,12 @@ ROOT = os.path.dirname(HERE)
 GOLD = os.path.join(ROOT, "tests", "golden")
 BIN = os.path.join(HERE, "_ref", "ref_golden")
 
-SMALL = {"numerics": 1000, "rec128": 1024, "recvar": 1024, "rpc": 1024, "vecrec": 1024}
+SMALL = {"numerics": 1000, "rec128": 1024, "recvar": 1024, "rpc": 1024, "vecrec": 1024, "containertest": 1024}
 FULL = {"rec128": 1 << 20, "recvar": 1 << 20, "rpc": 1 << 20, "numerics": 1 << 16,
         "rec128_mgpu": 1 << 24}
 FULL2 = {"numerics": 1 << 20}  # second full-size entries (dict keys are unique per schema)
-MID = {"recvar": 1 << 16, "rpc": 1 << 16, "vecrec": 1 << 16}
+MID = {"recvar": 1 << 16, "rpc": 1 << 16, "vecrec": 1 << 16, "containertest": 1 << 16}
+FULL3 = {"vecrec": 1 << 20, "containertest": 1 << 20}
 EXTS = ("native", "heap", "xdr", "offsets", "msgs", "msgoffs")
 NOMSGS = {"rec128_mgpu"}  # 16M records: messages hashed only where they are tested
 
@@ -114,6 +115,19 @@ def main() -> int:
         with open(mp, "w") as f:
             json.dump(manifest, f, indent=1, sort_keys=True)
         return 0
+    if "--only-small" in sys.argv:  # --only-small schema [schema ...]: fixtures + depths of those
+        mp = os.path.join(GOLD, "manifest.json")
+        manifest = json.load(open(mp))
+        for schema in sys.argv[sys.argv.index("--only-small") + 1:]:
+            n = SMALL[schema]
+            pre = os.path.join(GOLD, f"{schema}_{n}")
+            subprocess.check_call([BIN, "gen", schema, str(n), pre])
+            manifest["small"][schema] = {"n": n, "files": {e: f"{schema}_{n}.{e}" for e in EXTS},
+                                         "xdr_bytes": os.path.getsize(pre + ".xdr")}
+            subprocess.check_call([BIN, "depths", schema, str(n), pre + ".depths"])
+        with open(mp, "w") as f:
+            json.dump(manifest, f, indent=1, sort_keys=True)
+        return 0
     if "--only-depths" in sys.argv:
         depth_fixtures()
         return 0
@@ -136,7 +150,7 @@ def main() -> int:
         manifest["small"][schema] = {"n": n, "files": {e: f"{schema}_{n}.{e}" for e in EXTS},
                                      "xdr_bytes": os.path.getsize(pre + ".xdr")}
     subprocess.check_call([BIN, "kat", os.path.join(GOLD, "kat.json")])
-    full_hashes(manifest, [kv for table in (FULL, FULL2, MID) for kv in table.items()])
+    full_hashes(manifest, [kv for table in (FULL, FULL2, MID, FULL3) for kv in table.items()])
     rpc_fixtures(manifest)
     depth_fixtures()
     with open(os.path.join(GOLD, "manifest.json"), "w") as f:

@@ -682,6 +682,7 @@ int main(int argc, char **argv) {
     else if (schema == "rec128_mgpu") { vector<rec128> v; gen_rec128(n, WG_SEED_REC128_MGPU, 0, v); emit(v, pre, wm); }
     else if (schema == "recvar") { vector<recvar> v; gen_recvar(n, WG_SEED_RECVAR, v); emit(v, pre, wm); }
     else if (schema == "vecrec") { vector<vecrec> v; gen_vecrec(n, WG_SEED_VECREC, v); emit(v, pre, wm); }
+    else if (schema == "containertest") { vector<testns::containertest> v; gen_containertest(n, WG_SEED_CONTAINERTEST, v); emit(v, pre, wm); }
     else if (schema == "rpc") { vector<xdr::rpc_msg> v; gen_rpc(n, WG_SEED_RPC, v); emit(v, pre, wm); }
     else die("unknown schema " + schema);
     return 0;
@@ -693,6 +694,7 @@ int main(int argc, char **argv) {
     else if (schema == "rec128") { vector<rec128> v; gen_rec128(n, WG_SEED_REC128, 0, v); depths_of(v, o); }
     else if (schema == "recvar") { vector<recvar> v; gen_recvar(n, WG_SEED_RECVAR, v); depths_of(v, o); }
     else if (schema == "vecrec") { vector<vecrec> v; gen_vecrec(n, WG_SEED_VECREC, v); depths_of(v, o); }
+    else if (schema == "containertest") { vector<testns::containertest> v; gen_containertest(n, WG_SEED_CONTAINERTEST, v); depths_of(v, o); }
     else if (schema == "rpc") { vector<xdr::rpc_msg> v; gen_rpc(n, WG_SEED_RPC, v); depths_of(v, o); }
     else die("unknown schema " + schema);
     return 0;
@@ -704,6 +706,7 @@ int main(int argc, char **argv) {
     else if (schema == "numerics") { vector<testns::numerics> v; gen_numerics(n, WG_SEED_NUMERICS, v); bench_one("numerics", v, threads, reps); }
     else if (schema == "recvar") { vector<recvar> v; gen_recvar(n, WG_SEED_RECVAR, v); bench_one("recvar", v, threads, reps); }
     else if (schema == "vecrec") { vector<vecrec> v; gen_vecrec(n, WG_SEED_VECREC, v); bench_one("vecrec", v, threads, reps); }
+    else if (schema == "containertest") { vector<testns::containertest> v; gen_containertest(n, WG_SEED_CONTAINERTEST, v); bench_one("containertest", v, threads, reps); }
     else if (schema == "rpc") { vector<xdr::rpc_msg> v; gen_rpc(n, WG_SEED_RPC, v); bench_one("rpc", v, threads, reps); }
     else die("unknown schema " + schema);
     return 0;

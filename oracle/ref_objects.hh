@@ -129,6 +129,40 @@ template <typename T> [[maybe_unused]] static T bits_as(uint64_t v) {
   }
 }
 
+// containertest (tests/xdrtest.x:129-132): d[0..3] = draw(seed, 4r + k);
+// nu = d0 % 9 elements, element j the f12 arm if bit j of d1 is set (else
+// f4), its int from payload word 32r + j, its double's bits from word
+// 32r + 8 + j; |sarr[0]| = d2 % 33, |sarr[1]| = (d2 >> 32) % 33, letters
+// from payload words 32r + 16 + k/8 and 32r + 21 + k/8
+[[maybe_unused]] static void gen_containertest(size_t n, uint64_t seed, vector<testns::containertest> &v) {
+  v.resize(n);
+  const uint64_t ps = seed ^ WG_PAYLOAD_XOR;
+  for (size_t r = 0; r < n; ++r) {
+    uint64_t d[4];
+    for (int k = 0; k < 4; ++k) d[k] = wg_draw(seed, r * 4 + k);
+    testns::containertest &x = v[r];
+    const uint32_t nu = d[0] % 9;
+    x.uvec.resize(nu);
+    for (uint32_t j = 0; j < nu; ++j) {
+      const int32_t i = (int32_t)(uint32_t)wg_draw(ps, r * 32 + j);
+      if ((d[1] >> j) & 1) {
+        x.uvec[j].which(12);
+        x.uvec[j].f12().i = i;
+        x.uvec[j].f12().d = bits_as<double>(wg_draw(ps, r * 32 + 8 + j));
+      } else {
+        x.uvec[j].which(4);
+        x.uvec[j].f4().i = i;
+      }
+    }
+    const uint32_t len[2] = {uint32_t(d[2] % 33), uint32_t((d[2] >> 32) % 33)};
+    for (int k = 0; k < 2; ++k) {
+      string s(len[k], '\0');
+      for (uint32_t j = 0; j < len[k]; ++j) s[j] = char(0x61 + wg_byte(ps, r * 32 + 16 + 5 * k + j / 8, j) % 26);
+      x.sarr[k] = s;
+    }
+  }
+}
+
 [[maybe_unused]] static void fill_auth(xdr::opaque_auth &a, int32_t flavor, uint32_t len, uint64_t ps,
                       uint64_t word0) {
   a.flavor = xdr::auth_flavor(flavor);
@@ -288,6 +322,41 @@ struct heap_t {
   }
 }
 
+// containertest: {uvec ref, sarr[2] refs}; per record the element array
+// (24-byte u_4_12: which, the arm at +8) then the two strings
+struct st_u_4_12 {
+  int32_t which;
+  uint32_t pad;
+  int32_t i;
+  uint32_t pad2;
+  double d;  // the f12 arm's double (0 for f4)
+};
+static_assert(sizeof(st_u_4_12) == 24, "u_4_12 staged element");
+struct st_containertest {
+  xdrg_bytes_ref uvec, sarr[2];
+};
+[[maybe_unused]] static void stage(const vector<testns::containertest> &v, vector<uint8_t> &nat, heap_t &h) {
+  nat.assign(v.size() * sizeof(st_containertest), 0);
+  st_containertest *s = reinterpret_cast<st_containertest *>(nat.data());
+  for (size_t r = 0; r < v.size(); ++r) {
+    const testns::containertest &x = v[r];
+    vector<st_u_4_12> e(x.uvec.size());
+    for (size_t j = 0; j < e.size(); ++j) {
+      e[j] = st_u_4_12{};
+      e[j].which = x.uvec[j].which();
+      if (e[j].which == 12) {
+        e[j].i = x.uvec[j].f12().i;
+        e[j].d = x.uvec[j].f12().d;
+      } else {
+        e[j].i = x.uvec[j].f4().i;
+      }
+    }
+    s[r].uvec = h.put_elems(e.data(), e.size(), sizeof(st_u_4_12));
+    for (int k = 0; k < 2; ++k)
+      s[r].sarr[k] = h.put(reinterpret_cast<const uint8_t *>(x.sarr[k].data()), x.sarr[k].size());
+  }
+}
+
 // Equality for round-trip checks (byte-level for fixed structs).
 [[maybe_unused]] static bool same(const testns::numerics &a, const testns::numerics &b) {
   return a.b == b.b && a.i1 == b.i1 && a.i2 == b.i2 && a.i3 == b.i3 && a.i4 == b.i4 &&
@@ -299,6 +368,9 @@ struct heap_t {
          !memcmp(&a.score, &b.score, 8);
 }
 [[maybe_unused]] static bool same(const vecrec &a, const vecrec &b) {
+  return xdr::xdr_to_opaque(a) == xdr::xdr_to_opaque(b);
+}
+[[maybe_unused]] static bool same(const testns::containertest &a, const testns::containertest &b) {
   return xdr::xdr_to_opaque(a) == xdr::xdr_to_opaque(b);
 }
 [[maybe_unused]] static bool same(const xdr::rpc_msg &a, const xdr::rpc_msg &b) {

@@ -26,6 +26,7 @@
 #define WG_SEED_RPC 0x5EED0004ULL
 #define WG_SEED_REC128_MGPU 0x5EED0005ULL
 #define WG_SEED_VECREC 0x5EED0006ULL
+#define WG_SEED_CONTAINERTEST 0x5EED0008ULL
 #define WG_PAYLOAD_XOR 0xB10BB10BB10BB10BULL
 
 static inline uint64_t wg_draw(uint64_t seed, uint64_t i) {

@@ -34,7 +34,8 @@ def golden(schema: str, n: int, ext: str, dtype=np.uint8) -> np.ndarray:
     return np.fromfile(os.path.join(GOLD, f"{schema}_{n}.{ext}"), dtype=dtype)
 
 
-SMALL_N = {"numerics": 1000, "rec128": 1024, "recvar": 1024, "rpc": 1024, "vecrec": 1024}
+SMALL_N = {"numerics": 1000, "rec128": 1024, "recvar": 1024, "rpc": 1024, "vecrec": 1024,
+           "containertest": 1024}
 
 
 @pytest.fixture(scope="session")

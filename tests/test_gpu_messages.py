@@ -24,7 +24,7 @@ from xdrpp_amd import schemas as S  # noqa: E402
 from xdrpp_amd import workloads as W  # noqa: E402
 import oracle_bridge as O  # noqa: E402
 
-SCHEMAS = ["numerics", "rec128", "recvar", "rpc", "vecrec"]
+SCHEMAS = ["numerics", "rec128", "recvar", "rpc", "vecrec", "containertest"]
 _plans = {}
 
 

@@ -30,7 +30,7 @@ from xdrpp_amd import schemas as S
 from xdrpp_amd import workloads as W
 from xdrpp_amd.xdr_types import compile_plan
 
-SCHEMAS = ["numerics", "rec128", "recvar", "rpc", "vecrec"]
+SCHEMAS = ["numerics", "rec128", "recvar", "rpc", "vecrec", "containertest"]
 CP = {k: compile_plan(t) for k, t in S.ALL.items()}
 
 

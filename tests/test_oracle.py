@@ -30,7 +30,7 @@ from xdrpp_amd import schemas as S
 from xdrpp_amd import workloads as W
 from xdrpp_amd.xdr_types import compile_plan
 
-SCHEMAS = ["numerics", "rec128", "recvar", "rpc", "vecrec"]
+SCHEMAS = ["numerics", "rec128", "recvar", "rpc", "vecrec", "containertest"]
 CP = {k: compile_plan(t) for k, t in S.ALL.items()}
 CP["numerics_v"] = compile_plan(S.numerics_validated)
 
@@ -49,7 +49,7 @@ def test_generator_matches_reference_fixture(name):
 
 
 @pytest.mark.parametrize("key", ["numerics_65536", "recvar_65536", "rpc_65536", "vecrec_65536",
-                                 "rec128_1048576"])
+                                 "containertest_65536", "rec128_1048576"])
 def test_generator_matches_manifest(manifest, key):
     name, n = key.rsplit("_", 1)
     h = manifest["hashes"][key]
@@ -58,7 +58,7 @@ def test_generator_matches_manifest(manifest, key):
     assert sha(heap) == h["heap"]
 
 
-@pytest.mark.parametrize("name", ["numerics", "rec128", "recvar", "rpc", "vecrec"])
+@pytest.mark.parametrize("name", SCHEMAS)
 def test_generator_first_is_a_slice(name):
     """Shard generation (first=k) reproduces records [k, k+n) of the batch."""
     nat, heap = W.GENERATORS[name](96)
@@ -101,7 +101,7 @@ def test_oracle_decode_golden(name):
 
 
 @pytest.mark.parametrize("key", ["numerics_65536", "recvar_65536", "rpc_65536", "vecrec_65536",
-                                 "rec128_1048576"])
+                                 "containertest_65536", "rec128_1048576"])
 def test_oracle_full_size_hash(manifest, key):
     name, n = key.rsplit("_", 1)
     n = int(n)
@@ -207,5 +207,5 @@ def test_oracle_depths_golden(name):
     (oracle/ref_golden depths: the smallest passing limit per record)."""
     n = SMALL_N[name]
     cp = compile_plan(S.ALL[name])
-    d = O.depths(cp, golden(name, n, "native"), n)
+    d = O.depths(cp, golden(name, n, "native"), n, golden(name, n, "heap"))
     assert np.array_equal(d, golden(name, n, "depths", np.uint32))

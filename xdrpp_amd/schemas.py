@@ -115,4 +115,5 @@ rpcb = Struct("rpcb", [("r_prog", UInt), ("r_vers", UInt), ("r_netid", String())
 rp__list = Struct("rp__list")
 rp__list.define([("rpcb_map", rpcb), ("rpcb_next", Pointer(rp__list))])
 
-ALL = {"numerics": numerics, "rec128": rec128, "recvar": recvar, "rpc": rpc_msg, "vecrec": vecrec}
+ALL = {"numerics": numerics, "rec128": rec128, "recvar": recvar, "rpc": rpc_msg, "vecrec": vecrec,
+       "containertest": containertest}

@@ -24,6 +24,7 @@ SEED_RECVAR = 0x5EED0003
 SEED_RPC = 0x5EED0004
 SEED_REC128_MGPU = 0x5EED0005
 SEED_VECREC = 0x5EED0006
+SEED_CONTAINERTEST = 0x5EED0008
 PAYLOAD_XOR = 0xB10BB10BB10BB10B
 
 _M1 = np.uint64(0xBF58476D1CE4E5B9)
@@ -249,7 +250,61 @@ def vecrec(n: int, seed: int = SEED_VECREC, first: int = 0) -> tuple[np.ndarray,
     return buf.reshape(-1), heap
 
 
-GENERATORS = {"numerics": numerics, "rec128": rec128, "recvar": recvar, "rpc": rpc, "vecrec": vecrec}
+def containertest(n: int, seed: int = SEED_CONTAINERTEST, first: int = 0) -> tuple[np.ndarray, np.ndarray]:
+    """Records [first, first + n) of tests/xdrtest.x containertest (a vector
+    of u_4_12 unions, variable-size elements, and bigstr sarr[2]); oracle/
+    ref_objects.hh gen_containertest.  d[0..3] = draw(seed, 4r + k):
+    nu = d0 % 9 elements, element j takes arm 12 if bit j of d1 is set
+    (else 4), its int from payload word 32r + j and its double's bits from
+    word 32r + 8 + j; |sarr[0]| = d2 % 33, |sarr[1]| = (d2 >> 32) % 33,
+    letters from payload words 32r + 16.. and 32r + 21...  Heap per record:
+    the element array (8-byte aligned, 24-byte u_4_12 elements: which, then
+    the arm at +8), then the two strings."""
+    t, u = S.containertest, S.u_4_12
+    o = t.offsets
+    ps = seed ^ PAYLOAD_XOR
+    d = _draws(seed, n, 4, first)
+    r = np.arange(first, first + n, dtype=np.uint64)
+    nu = (d[:, 0] % np.uint64(9)).astype(np.int64)
+    arm12 = ((d[:, 1][:, None] >> np.arange(8, dtype=np.uint64)[None, :]) & np.uint64(1)).astype(bool)
+    iv = draw(ps, r[:, None] * np.uint64(32) + np.arange(8, dtype=np.uint64)[None, :]) & np.uint64(0xFFFFFFFF)
+    dv = draw(ps, r[:, None] * np.uint64(32) + np.uint64(8) + np.arange(8, dtype=np.uint64)[None, :])
+    l0 = (d[:, 2] % np.uint64(33)).astype(np.int64)
+    l1 = ((d[:, 2] >> np.uint64(32)) % np.uint64(33)).astype(np.int64)
+    s0 = (np.uint8(0x61) + _payload_bytes(seed, n, 32, 16, 5, first) % np.uint8(26)).astype(np.uint8)
+    s1 = (np.uint8(0x61) + _payload_bytes(seed, n, 32, 21, 5, first) % np.uint8(26)).astype(np.uint8)
+    es = u.size  # 24: which @0, arm @ arms_off (8)
+    el = np.zeros((n, 8, es), dtype=np.uint8)
+    el[:, :, 0:4] = np.where(arm12, 12, 4).astype("<u4").view(np.uint8).reshape(n, 8, 4)
+    ao = u.arms_off
+    el[:, :, ao:ao + 4] = iv.astype("<u4").view(np.uint8).reshape(n, 8, 4)
+    dd = np.where(arm12, dv, np.uint64(0)).astype("<u8").view(np.uint8).reshape(n, 8, 8)
+    el[:, :, ao + S.fix_12.offsets["d"]:ao + S.fix_12.offsets["d"] + 8] = dd
+    el = el.reshape(n, 8 * es)
+    lens = np.stack([es * nu, l0, l1], axis=1)
+    reclen = lens.sum(axis=1)
+    starts = np.zeros(n, dtype=np.int64)
+    if n > 1:
+        np.cumsum((reclen[:-1] + 7) & ~7, out=starts[1:])
+    cols = np.concatenate([el, s0, s1], axis=1)                       # (n, 192 + 40 + 40)
+    widths = [8 * es, 40, 40]
+    live = np.concatenate([np.arange(w)[None, :] < lens[:, k][:, None] for k, w in enumerate(widths)], axis=1)
+    # each record's bytes, then zeros up to the next 8-byte boundary
+    padw = 8
+    pad = np.arange(padw)[None, :] < (((reclen + 7) & ~7) - reclen)[:, None]
+    heap = np.concatenate([cols, np.zeros((n, padw), dtype=np.uint8)], axis=1)[
+        np.concatenate([live, pad], axis=1)]
+    if n:  # no pad after the last record
+        heap = heap[:int(starts[-1] + reclen[-1])]
+    buf = np.zeros((n, t.size), dtype=np.uint8)
+    _put_ref(buf, o["uvec"], starts, nu)
+    _put_ref(buf, o["sarr"], starts + es * nu, l0)
+    _put_ref(buf, o["sarr"] + 16, starts + es * nu + l0, l1)
+    return buf.reshape(-1), heap
+
+
+GENERATORS = {"numerics": numerics, "rec128": rec128, "recvar": recvar, "rpc": rpc, "vecrec": vecrec,
+              "containertest": containertest}
 
 
 def generate(schema: str, n: int, chunk: int = 1 << 16) -> tuple[np.ndarray, np.ndarray]:
