@@ -46,6 +46,8 @@ struct gen {
   uint32_t max_slots = 0;  // static chunk-map slots used on the longest path
   uint64_t max_chunks = 0; // 16-byte chunks those slots can hold (per record)
   bool word_list = true;   // every payload takes a slot, no container loop (var_kernels.h WL)
+  uint32_t uid = 0;        // names of the element loops of subroutine containers
+  uint32_t maxd = 0;       // deepest absolute op depth a walk checks
 
   explicit gen(const xdrg_plan &plan) : p(plan) { post_dominators(); }
 
@@ -89,6 +91,41 @@ struct gen {
 
   void line(const std::string &s) { o << std::string(2 * ind, ' ') << s << "\n"; }
 
+  // Absolute depth of an op of a body entered with depth offset dadd
+  // (include/xdrgpu.h: a subroutine's depths are relative to its VECTOR op)
+  std::string depth(const xdrg_op &e, uint32_t dadd) {
+    maxd = std::max(maxd, e.depth + dadd);
+    return u32(e.depth + dadd);
+  }
+  // The element at heap offset `eb` of a subroutine container, loaded into
+  // registers ew<k> (stride/4 words; heap bytes past `len` read as 0) and
+  // seen through the byte pointer e<k>: the body's field reads then have
+  // constant offsets, as the record's own.
+  std::string load_elem(uint32_t k, const std::string &eb, uint32_t stride, const std::string &heap,
+                        const std::string &len) {
+    const std::string ew = "ew" + std::to_string(k), e = "e" + std::to_string(k);
+    const uint32_t nw = stride / 4;
+    line("uint32_t " + ew + "[" + u32(nw) + "];");
+    line("if (" + eb + " + " + u32(stride) + " <= " + len + ") {");
+    uint32_t q = 0;
+    for (; q + 4 <= nw; q += 4)
+      line("  { const u32x4 t = ld16u(" + heap + " + " + eb + " + " + u32(4 * q) + "); " + ew + "[" + u32(q) +
+           "] = t.x; " + ew + "[" + u32(q + 1) + "] = t.y; " + ew + "[" + u32(q + 2) + "] = t.z; " + ew + "[" +
+           u32(q + 3) + "] = t.w; }");
+    for (; q < nw; ++q) line("  " + ew + "[" + u32(q) + "] = ld32(" + heap + " + " + eb + " + " + u32(4 * q) + ");");
+    line("} else {");
+    for (q = 0; q < nw; ++q)
+      line("  " + ew + "[" + u32(q) + "] = unaligned_word(" + heap + ", " + len + ", " + eb + " + " + u32(4 * q) + ");");
+    line("}");
+    line("const uint8_t *" + e + " = reinterpret_cast<const uint8_t *>(" + ew + ");");
+    return e;
+  }
+  // the END that closes the subroutine body starting at pc
+  uint32_t body_end(uint32_t pc) const {
+    while (op(pc).kind != XDRG_OP_END) ++pc;
+    return pc;
+  }
+
   static uint32_t wire_words(const xdrg_op &e) {
     return e.kind == XDRG_OP_U64 ? 2u : e.kind == XDRG_OP_OPAQUE ? (e.arg0 + 3u) / 4u : 1u;
   }
@@ -126,6 +163,27 @@ struct gen {
         line("s += 4ull + ((static_cast<uint64_t>(ld32(" + f + " + 8)) + 3u) & ~3ull);");
         break;
       case XDRG_OP_VECTOR:
+        if (e.flags & XDRG_F_SUB) {  // element subroutine: the body's size per element
+          const uint32_t k = uid++;
+          line("{");
+          ++ind;
+          line("const uint64_t eoff" + std::to_string(k) + " = *reinterpret_cast<const uint64_t *>(" + f + ");");
+          line("const uint32_t cnt" + std::to_string(k) + " = ld32(" + f + " + 8);");
+          line("s += 4;");
+          line("for (uint32_t i" + std::to_string(k) + " = 0; i" + std::to_string(k) + " < cnt" +
+               std::to_string(k) + "; ++i" + std::to_string(k) + ") {");
+          ++ind;
+          const std::string eb = "(eoff" + std::to_string(k) + " + static_cast<uint64_t>(i" + std::to_string(k) +
+                                 ") * " + u32(e.arg1) + ")";
+          const std::string el = load_elem(k, eb, e.arg1, "heap", "heap_len");
+          size_block(e.arg4, body_end(e.arg4), el);
+          --ind;
+          line("}");
+          --ind;
+          line("}");
+          ++pc;
+          continue;
+        }
         line("s += 4ull + static_cast<uint64_t>(ld32(" + f + " + 8)) * " + u32(e.arg3) + ";");
         pc += 1 + e.arg2;
         continue;
@@ -189,7 +247,21 @@ struct gen {
         line("  if (lim - p < v) return past;");
         line("  p += (static_cast<uint64_t>(v) + 3u) & ~3ull; }");
         break;
-      case XDRG_OP_VECTOR:  // fixed-size elements (element subroutines are not generated)
+      case XDRG_OP_VECTOR:
+        if (e.flags & XDRG_F_SUB) {  // each element parsed by its body
+          const std::string k = std::to_string(uid++);
+          word();
+          line("  if (v > " + u32(e.arg0) + ") return RX_BAD;");
+          line("  if ((lim - p) / " + u32(e.arg3) + " < v) return past;  // the decode's least-wire check");
+          line("  for (uint32_t i" + k + " = 0; i" + k + " < v; ++i" + k + ") {");
+          ind += 2;
+          rx_block(e.arg4, body_end(e.arg4));
+          ind -= 2;
+          line("  }");
+          line("}");
+          ++pc;
+          continue;
+        }
         word();
         line("  if (v > " + u32(e.arg0) + ") return RX_BAD;");
         line("  const uint64_t b = static_cast<uint64_t>(v) * " + u32(e.arg3) + ";");
@@ -256,10 +328,11 @@ struct gen {
   // xdr_generic_put field by field (marshal.h:84-137).  Returns the static
   // slots used after the block (slots count along the path); `words` = the
   // most scalar words a path through the block puts.
-  uint32_t enc_block(uint32_t pc, uint32_t stop, uint32_t slot, uint64_t &chunks, uint32_t &words) {
+  uint32_t enc_block(uint32_t pc, uint32_t stop, uint32_t slot, uint64_t &chunks, uint32_t &words,
+                     const std::string &base = "nat", uint32_t dadd = 0) {
     while (pc != stop) {
       const xdrg_op &e = op(pc);
-      const std::string f = "nat + " + u32(e.noff), P = u32(pc), D = u32(e.depth);
+      const std::string f = base + " + " + u32(e.noff), P = u32(pc), D = depth(e, dadd);
       switch (e.kind) {
       case XDRG_OP_END: return slot;
       case XDRG_OP_JUMP: pc = e.arg0; continue;
@@ -270,7 +343,7 @@ struct gen {
         break;
       case XDRG_OP_BOOL:
         line("if (!c.field(" + P + ", " + D + ", 4)) return false;");
-        line("c.put(nat[" + u32(e.noff) + "] ? 0x01000000u : 0u);");
+        line("c.put(" + base + "[" + u32(e.noff) + "] ? 0x01000000u : 0u);");
         words += 1;
         break;
       case XDRG_OP_U64:
@@ -285,7 +358,7 @@ struct gen {
         for (uint32_t k = 0; 4 * k < e.arg0; ++k) {
           std::string w;
           for (uint32_t b = 0; b < 4 && 4 * k + b < e.arg0; ++b)
-            w += std::string(b ? " | " : "") + "(uint32_t(nat[" + u32(e.noff + 4 * k + b) + "]) << " +
+            w += std::string(b ? " | " : "") + "(uint32_t(" + base + "[" + u32(e.noff + 4 * k + b) + "]) << " +
                  std::to_string(8 * b) + ")";
           line("c.put(" + w + ");");
         }
@@ -336,7 +409,7 @@ struct gen {
           ++ind;
           uint64_t ch = chunks;
           uint32_t wd = words;
-          smax = std::max(smax, enc_block(a.first, end, slot, ch, wd));
+          smax = std::max(smax, enc_block(a.first, end, slot, ch, wd, base, dadd));
           cmax = std::max(cmax, ch);
           wmax = std::max(wmax, wd);
           --ind;
@@ -347,7 +420,7 @@ struct gen {
           ++ind;
           uint64_t ch = chunks;
           uint32_t wd = words;
-          smax = std::max(smax, enc_block(e.arg4, end, slot, ch, wd));
+          smax = std::max(smax, enc_block(e.arg4, end, slot, ch, wd, base, dadd));
           cmax = std::max(cmax, ch);
           wmax = std::max(wmax, wd);
           --ind;
@@ -366,6 +439,29 @@ struct gen {
       }
       case XDRG_OP_VECTOR: {
         word_list = false;
+        if (e.flags & XDRG_F_SUB) {  // each element walked by its body (payloads copied by the lane)
+          const uint32_t k = uid++;
+          const std::string ks = std::to_string(k);
+          line("{");
+          ++ind;
+          line("const uint64_t eoff" + ks + " = *reinterpret_cast<const uint64_t *>(" + f + ");");
+          line("const uint32_t cnt" + ks + " = ld32(" + f + " + 8);");
+          line("if (!c.field(" + P + ", " + D + ", 4)) return false;");
+          line("c.put(bswap32(cnt" + ks + "));");
+          line("for (uint32_t i" + ks + " = 0; i" + ks + " < cnt" + ks + "; ++i" + ks + ") {");
+          ++ind;
+          const std::string el = load_elem(k, "(eoff" + ks + " + static_cast<uint64_t>(i" + ks + ") * " + u32(e.arg1) + ")",
+                                            e.arg1, "c.heap", "c.heap_len");
+          uint64_t ch = 0;
+          uint32_t wd = 0;
+          enc_block(e.arg4, body_end(e.arg4), kSlotMax, ch, wd, el, dadd + e.depth);
+          --ind;
+          line("}");
+          --ind;
+          line("}");
+          ++pc;
+          continue;
+        }
         line("{");
         ++ind;
         line("const uint64_t eoff = *reinterpret_cast<const uint64_t *>(" + f + ");");
@@ -377,7 +473,7 @@ struct gen {
             (op(pc + 1).kind == XDRG_OP_U32 || op(pc + 1).kind == XDRG_OP_ENUM || op(pc + 1).kind == XDRG_OP_BOOL)) {
           // 4-byte elements four at a time: one 16-byte load per four
           const xdrg_op &el = op(pc + 1);
-          const std::string chk = "if (!c.field(" + u32(pc + 1) + ", " + u32(el.depth) + ", 4)) return false;";
+          const std::string chk = "if (!c.field(" + u32(pc + 1) + ", " + depth(el, dadd) + ", 4)) return false;";
           auto cv = [&](const std::string &w) {
             return el.kind == XDRG_OP_BOOL ? "((" + w + " & 0xffu) ? 0x01000000u : 0u)" : "bswap32(" + w + ")";
           };
@@ -391,7 +487,7 @@ struct gen {
         line("for (; i < cnt; ++i) {");
         ++ind;
         line("const uint64_t eb = eoff + static_cast<uint64_t>(i) * " + u32(e.arg1) + ";");
-        enc_elem(pc + 1, pc + 1 + e.arg2, e.arg1);
+        enc_elem(pc + 1, pc + 1 + e.arg2, e.arg1, dadd);
         --ind;
         line("}");
         --ind;
@@ -409,7 +505,7 @@ struct gen {
   // fields read from the heap (bytes past heap_len read as 0).  An element
   // of 16-byte multiples whose word fields are 4-aligned is loaded whole
   // (16-byte loads) into registers first, its fields taken from there.
-  bool enc_elem_regs(uint32_t b0, uint32_t b1, uint32_t es) {
+  bool enc_elem_regs(uint32_t b0, uint32_t b1, uint32_t es, uint32_t dadd) {
     if (es == 0 || (es & 15u) || es > 64) return false;
     for (uint32_t k = b0; k < b1; ++k) {
       const xdrg_op &e = op(k);
@@ -426,7 +522,7 @@ struct gen {
     line("}");
     for (uint32_t k = b0; k < b1; ++k) {
       const xdrg_op &e = op(k);
-      const std::string P = u32(k), D = u32(e.depth), w = "ew[" + u32(e.noff / 4) + "]";
+      const std::string P = u32(k), D = depth(e, dadd), w = "ew[" + u32(e.noff / 4) + "]";
       line("if (!c.field(" + P + ", " + D + ", " + u32(4u * wire_words(e)) + ")) return false;");
       switch (e.kind) {
       case XDRG_OP_BOOL:
@@ -448,11 +544,11 @@ struct gen {
     }
     return true;
   }
-  void enc_elem(uint32_t b0, uint32_t b1, uint32_t es) {
-    if (enc_elem_regs(b0, b1, es)) return;
+  void enc_elem(uint32_t b0, uint32_t b1, uint32_t es, uint32_t dadd) {
+    if (enc_elem_regs(b0, b1, es, dadd)) return;
     for (uint32_t k = b0; k < b1; ++k) {
       const xdrg_op &e = op(k);
-      const std::string P = u32(k), D = u32(e.depth), a = "eb + " + u32(e.noff);
+      const std::string P = u32(k), D = depth(e, dadd), a = "eb + " + u32(e.noff);
       const uint32_t wb = 4u * wire_words(e);
       line("if (!c.field(" + P + ", " + D + ", " + u32(e.kind == XDRG_OP_OPAQUE ? wb : wb) + ")) return false;");
       switch (e.kind) {
@@ -475,10 +571,10 @@ struct gen {
 
   // ---------------------------------------------------------------- decode
   // xdr_generic_get field by field (marshal.h:142-211).
-  void dec_block(uint32_t pc, uint32_t stop) {
+  void dec_block(uint32_t pc, uint32_t stop, const std::string &base = "nat", uint32_t dadd = 0) {
     while (pc != stop) {
       const xdrg_op &e = op(pc);
-      const std::string f = "nat + " + u32(e.noff), P = u32(pc), D = u32(e.depth);
+      const std::string f = base + " + " + u32(e.noff), P = u32(pc), D = depth(e, dadd);
       switch (e.kind) {
       case XDRG_OP_END: return;
       case XDRG_OP_JUMP: pc = e.arg0; continue;
@@ -502,7 +598,7 @@ struct gen {
         break;
       case XDRG_OP_BOOL:
         line("if (!c.field(" + P + ", " + D + ", 4)) return false;");
-        line("nat[" + u32(e.noff) + "] = c.word() != 0u;");
+        line(base + "[" + u32(e.noff) + "] = c.word() != 0u;");
         break;
       case XDRG_OP_U64:
         line("if (!c.field(" + P + ", " + D + ", 8)) return false;");
@@ -517,7 +613,7 @@ struct gen {
         for (uint32_t k = 0; k < L; k += 4) {
           line("{ const uint32_t w = c.peek(c.p + " + u32(k) + ");");
           for (uint32_t b = 0; b < 4 && k + b < L; ++b)
-            line("  nat[" + u32(e.noff + k + b) + "] = uint8_t(w >> " + std::to_string(8 * b) + "); ");
+            line("  " + base + "[" + u32(e.noff + k + b) + "] = uint8_t(w >> " + std::to_string(8 * b) + "); ");
           line("}");
         }
         if (L & 3u)
@@ -560,7 +656,7 @@ struct gen {
           line(lab + "{");
           ++ind;
           line("st32(" + f + ", d);");
-          dec_block(a.first, end);
+          dec_block(a.first, end, base, dadd);
           --ind;
           line("} break;");
         }
@@ -568,7 +664,7 @@ struct gen {
         ++ind;
         if (e.flags & XDRG_F_DEFAULT) {
           line("st32(" + f + ", d);");
-          dec_block(e.arg4, end);
+          dec_block(e.arg4, end, base, dadd);
         } else {
           line("return c.fail(" + P + ", XDRG_ERR_BAD_DISCRIMINANT);");
         }
@@ -581,6 +677,41 @@ struct gen {
         continue;
       }
       case XDRG_OP_VECTOR: {
+        if (e.flags & XDRG_F_SUB) {
+          // the element array (zeroed) from the element area, then each
+          // element by its body; an element that fails leaves 1 + its
+          // index in the container's xdrg_bytes_ref.rsv (sub_kernels.h)
+          const std::string ks = std::to_string(uid++);
+          line("if (!c.field(" + P + ", " + D + ", 4)) return false;");
+          line("{");
+          ++ind;
+          line("const uint32_t cnt" + ks + " = bswap32(c.word());");
+          line("if (cnt" + ks + " > " + u32(e.arg0) + ") return c.fail(" + P + ", " +
+               ((e.flags & XDRG_F_POINTER) ? "XDRG_ERR_POINTER_BOUND" : "XDRG_ERR_XVECTOR_BOUND") + ");");
+          line("if (!c.area_sub(" + P + ", cnt" + ks + ", " + u32(e.arg1) + ", " + u32(e.arg3) + ")) return false;");
+          line("*reinterpret_cast<uint64_t *>(" + f + ") = c.ecur;");
+          line("st32(" + f + " + 8, cnt" + ks + ");");
+          line("uint8_t *arr" + ks + " = c.heap + c.ecur;");
+          line("for (uint64_t z = 0; z < static_cast<uint64_t>(cnt" + ks + ") * " + u32(e.arg1) +
+               "; z += 4) st32(arr" + ks + " + z, 0u);");
+          line("c.ecur += static_cast<uint64_t>(cnt" + ks + ") * " + u32(e.arg1) + ";");
+          line("for (uint32_t i" + ks + " = 0; i" + ks + " < cnt" + ks + "; ++i" + ks + ") {");
+          ++ind;
+          line("uint8_t *e" + ks + " = arr" + ks + " + static_cast<uint64_t>(i" + ks + ") * " + u32(e.arg1) + ";");
+          line("auto body" + ks + " = [&]() -> bool {");
+          ++ind;
+          dec_block(e.arg4, body_end(e.arg4), "e" + ks, dadd + e.depth);
+          line("return true;");
+          --ind;
+          line("};");
+          line("if (!body" + ks + "()) { st32(" + f + " + 12, i" + ks + " + 1u); return false; }");
+          --ind;
+          line("}");
+          --ind;
+          line("}");
+          ++pc;
+          continue;
+        }
         line("if (!c.field(" + P + ", " + D + ", 4)) return false;");
         line("{");
         ++ind;
@@ -599,8 +730,8 @@ struct gen {
             // 4-byte elements two at a time: one 8-byte store per pair (the
             // array starts 8-aligned); a failing element leaves what the
             // one-by-one form leaves (the element before it stored, it zeroed)
-            const std::string chk = "c.field(" + u32(pc + 1) + ", " + u32(el.depth) + ", 4)";
-            const std::string rsv = "st32(nat + " + u32(e.noff) + " + 12, ";
+            const std::string chk = "c.field(" + u32(pc + 1) + ", " + depth(el, dadd) + ", 4)";
+            const std::string rsv = "st32(" + f + " + 12, ";
             auto cv = [&](const std::string &w) {
               return el.kind == XDRG_OP_BOOL ? "(" + w + " != 0u ? 1u : 0u)" : "bswap32(" + w + ")";
             };
@@ -619,7 +750,7 @@ struct gen {
         line("for (; i < cnt; ++i) {");
         ++ind;
         line("uint8_t *el = c.heap + c.ecur + static_cast<uint64_t>(i) * " + u32(e.arg1) + ";");
-        dec_elem(pc, pc + 1, pc + 1 + e.arg2, e.arg1);
+        dec_elem(pc, pc + 1, pc + 1 + e.arg2, e.arg1, base, dadd);
         --ind;
         line("}");
         line("c.ecur += static_cast<uint64_t>(cnt) * " + u32(e.arg1) + ";");
@@ -640,7 +771,7 @@ struct gen {
   // registers and leave as whole 8- or 4-byte stores (a lane's scattered
   // byte and word stores were most of vecrec's decode); a failing field
   // stores what was built so far, as the store-by-store form leaves it.
-  bool dec_elem_regs(uint32_t vpc, uint32_t b0, uint32_t b1, uint32_t es) {
+  bool dec_elem_regs(uint32_t vpc, uint32_t b0, uint32_t b1, uint32_t es, const std::string &base, uint32_t dadd) {
     if ((es & 3u) || es == 0 || es > 64) return false;
     for (uint32_t k = b0; k < b1; ++k) {
       const xdrg_op &e = op(k);
@@ -655,14 +786,14 @@ struct gen {
     } else {
       for (uint32_t z = 0; z < nw; ++z) store += "st32(el + " + u32(4 * z) + ", ew[" + u32(z) + "]); ";
     }
-    const std::string fail_done = store + "st32(nat + " + u32(op(vpc).noff) + " + 12, i); ";
+    const std::string fail_done = store + "st32(" + base + " + " + u32(op(vpc).noff) + " + 12, i); ";
     line("uint32_t ew[" + u32(nw) + "] = {};");
     auto byte_in = [&](uint32_t at, const std::string &v) {
       return "ew[" + u32(at / 4) + "] |= (" + v + ") << " + std::to_string(8 * (at % 4)) + ";";
     };
     for (uint32_t k = b0; k < b1; ++k) {
       const xdrg_op &e = op(k);
-      const std::string P = u32(k), D = u32(e.depth);
+      const std::string P = u32(k), D = depth(e, dadd);
       const uint32_t need = e.kind == XDRG_OP_U64 ? 8u : e.kind == XDRG_OP_OPAQUE ? e.arg0 : 4u;
       line("if (!c.field(" + P + ", " + D + ", " + u32(need) + ")) { " + fail_done + "return false; }");
       switch (e.kind) {
@@ -699,9 +830,9 @@ struct gen {
     line(store);
     return true;
   }
-  void dec_elem(uint32_t vpc, uint32_t b0, uint32_t b1, uint32_t es) {
-    if (dec_elem_regs(vpc, b0, b1, es)) return;
-    const std::string fail_done = "st32(nat + " + u32(op(vpc).noff) + " + 12, i); ";
+  void dec_elem(uint32_t vpc, uint32_t b0, uint32_t b1, uint32_t es, const std::string &base, uint32_t dadd) {
+    if (dec_elem_regs(vpc, b0, b1, es, base, dadd)) return;
+    const std::string fail_done = "st32(" + base + " + " + u32(op(vpc).noff) + " + 12, i); ";
     const bool w4 = (es & 3u) == 0;  // 4-byte stores (element arrays are 8-aligned)
     if (w4)
       for (uint32_t z = 0; z < es; z += 4) line("st32(el + " + u32(z) + ", 0u);");
@@ -709,7 +840,7 @@ struct gen {
       line("for (uint32_t z = 0; z < " + u32(es) + "; ++z) el[z] = 0;");
     for (uint32_t k = b0; k < b1; ++k) {
       const xdrg_op &e = op(k);
-      const std::string P = u32(k), D = u32(e.depth), f = "el + " + u32(e.noff);
+      const std::string P = u32(k), D = depth(e, dadd), f = "el + " + u32(e.noff);
       const uint32_t need = e.kind == XDRG_OP_U64 ? 8u : e.kind == XDRG_OP_OPAQUE ? e.arg0 : 4u;
       line("if (!c.field(" + P + ", " + D + ", " + u32(need) + ")) { " + fail_done + "return false; }");
       switch (e.kind) {
@@ -758,16 +889,24 @@ struct gen {
 
 // A plan the generator handles: every construct of the op set, with the
 // unions' post-dominators defined and inside the plan.
+// Element subroutines are emitted inline per element: none may be entered
+// from itself (recursive types run the frame walk, sub_kernels.h), and
+// their elements (read into registers, load_elem) are at most 64 bytes.
 bool supported(const gen &g) {
-  for (uint32_t i = 0; i < g.nops(); ++i)
-    if (g.op(i).kind == XDRG_OP_UNION && (g.ipdom[i] == kNoPc || g.ipdom[i] >= g.nops())) return false;
+  for (uint32_t i = 0; i < g.nops(); ++i) {
+    const xdrg_op &o = g.op(i);
+    if (o.kind == XDRG_OP_UNION && (g.ipdom[i] == kNoPc || g.ipdom[i] >= g.nops())) return false;
+    if (o.kind == XDRG_OP_VECTOR && (o.flags & XDRG_F_SUB) &&
+        (o.arg1 == 0 || o.arg1 > 64 || (o.arg1 & 3u) || o.arg4 >= g.nops() || o.arg3 == 0))
+      return false;
+  }
   return true;
 }
 
 }  // namespace
 
 bool spec_source(const xdrg_plan &p, spec_info &info) {
-  if (p.path != XDRG_PATH_VAR || p.has_sub) return false;  // element subroutines: the frame walk
+  if (p.path != XDRG_PATH_VAR || p.deep) return false;  // recursive / deep nesting: the frame walk
   gen g(p);
   if (!supported(g)) return false;
   std::ostringstream body;
@@ -799,8 +938,7 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
   const std::string rx_code = g.o.str();
   const std::string first = g.first_test();
 
-  uint32_t maxd = 0;  // deepest field: the stack budget a wave must have to skip the checks
-  for (const xdrg_op &o : p.ops) maxd = std::max<uint32_t>(maxd, o.depth);
+  const uint32_t maxd = g.maxd;  // deepest field: the stack budget a wave must have to skip the checks
   info.slots = std::max<uint32_t>(1, slots);
   info.dec_regs = regs;
   info.word_list = kwords > 0;
@@ -813,10 +951,12 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
     << "using namespace xdrg::dev;\n\n"
     << "extern \"C\" __device__ __attribute__((used)) unsigned xdrg_spec_iface = " << kSpecIface << "u;\n\n"
     << "struct plan_walk {\n"
-    << "  __device__ __forceinline__ uint64_t size(const uint8_t *nat, uint32_t &bad_op) const {\n"
+    << "  __device__ __forceinline__ uint64_t size(const uint8_t *nat, const uint8_t *heap, uint64_t heap_len,\n"
+    << "                                             uint32_t &bad_op) const {\n"
     << "    uint64_t s = 0;\n"
     << size_code << "    return s;\n  }\n"
     << "  static constexpr bool kFastWalk = true;  // enc() also runs on an unchecked context\n"
+    << "  static constexpr bool kDirect = true;    // ... and on var_kernels.h enc_direct_ctx\n"
     << "  static constexpr uint32_t kMaxDepth = " << maxd << "u;\n"
     << "  static constexpr uint32_t kWords = " << kwords << "u;  // scalar words per record (0: no word list)\n"
     << "  template <class CTX>\n"
@@ -844,9 +984,9 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
     << "    uint32_t *lcount, uint32_t has_first, uint32_t fd) {\n"
     << "  ix_seg_body<true>(plan_rx{}, s, len, maxlen, K, tab, list, lcount, has_first != 0, fd);\n}\n\n"
     << "extern \"C\" __global__ __launch_bounds__(64) void xdrg_spec_size(\n"
-    << "    const uint8_t *native, uint64_t n, uint32_t stride, uint32_t *sizes,\n"
-    << "    unsigned long long *block_sums, uint32_t mark, unsigned long long *err) {\n"
-    << "  var_size_body(plan_walk{}, native, n, stride, sizes, block_sums, mark, err);\n}\n\n"
+    << "    const uint8_t *native, uint64_t n, uint32_t stride, const uint8_t *heap, uint64_t heap_len,\n"
+    << "    uint32_t *sizes, unsigned long long *block_sums, uint32_t mark, unsigned long long *err) {\n"
+    << "  var_size_body(plan_walk{}, native, n, stride, heap, heap_len, sizes, block_sums, mark, err);\n}\n\n"
     << "extern \"C\" __global__ __launch_bounds__(64) void xdrg_spec_encode(\n"
     << "    const uint8_t *native, uint64_t n, uint32_t stride, const uint8_t *heap, uint64_t heap_len,\n"
     << "    uint8_t *xdr, uint64_t cap, uint64_t *offsets, const uint32_t *sizes,\n"

@@ -26,7 +26,7 @@
 // plan and compiles with hiprtc.  A walker provides
 //   bool enc(CTX &, const uint8_t *nat)  (CTX: an enc_ctx, checked or not)
 //   bool dec(dec_ctx<RA> &, uint8_t *nat)
-//   uint64_t size(const uint8_t *nat, uint32_t &bad_op)
+//   uint64_t size(const uint8_t *nat, const uint8_t *heap, uint64_t heap_len, uint32_t &bad_op)
 // and reports its own field errors through the context.
 #pragma once
 #include "dev_common.h"
@@ -254,6 +254,48 @@ struct enc_ctx {
   }
 };
 
+// Direct mode of an encode wave whose stretch could pass 2 GiB (some
+// record of 32 MiB or more; unbounded plans): the lane writes its record
+// straight to the stream, words and payloads alike, at 64-bit positions --
+// xdr_generic_put record by record, with no window.
+struct enc_direct_ctx {
+  uint8_t *xdr;
+  const uint8_t *heap;
+  uint64_t heap_len;
+  uint64_t cap;
+  uint32_t stack_limit;
+  uint64_t r;
+  unsigned long long *err;
+  uint64_t pos;
+
+  __device__ __forceinline__ bool field(uint32_t op, uint32_t depth, uint64_t need) {
+    if (depth > stack_limit) {
+      report(err, r, op, XDRG_ERR_STACK_PUT);
+      return false;
+    }
+    if (need > cap - min(pos, cap)) {
+      report(err, r, op, XDRG_ERR_OVERFLOW_PUT);
+      return false;
+    }
+    return true;
+  }
+  __device__ __forceinline__ void put(uint32_t v) {
+    st32(xdr + pos, v);
+    pos += 4;
+  }
+  __device__ void copy(uint64_t src, uint32_t len) {  // put_bytes (marshal.cc:59-72), pad zeroed
+    const uint32_t nw = (len + 3u) >> 2;
+    for (uint32_t k = 0; k < nw; ++k) {
+      uint32_t w = unaligned_word(heap, heap_len, src + 4ull * k);
+      if (4u * k + 4u > len) w &= keep_mask(len - 4u * k);
+      st32(xdr + pos + 4ull * k, w);
+    }
+    pos += 4ull * nw;
+  }
+  template <int K> __device__ __forceinline__ void slot(uint64_t src, uint32_t len) { copy(src, len); }
+  __device__ __forceinline__ uint32_t hword(uint64_t off) const { return unaligned_word(heap, heap_len, off); }
+};
+
 // Word-list walk: the listed words of a lane's record (first byte at
 // image-space offset a0) that land in the window [w0, w0 + C) -> image.
 // Word j sits after the padded payloads of the slots listed before it.
@@ -333,7 +375,27 @@ __device__ __forceinline__ void var_encode_body(
   stage_tile<8>(tile, native + wr0 * stride, nrec * stride, lane, 64u);
   const bool szok = !(sz & kSizeErr);
   const uint32_t v = szok ? sz : 0u;
-  const uint32_t incl = wave_incl_scan(v);  // a wave's stretch < 2^31 bytes (launch condition)
+  if constexpr (W::kDirect) {
+    if (__any(v >= (1u << 25))) {  // 64 records could pass 2^31 bytes: direct mode
+      uint64_t inc = v;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t x = __shfl_up(inc, o, 64);
+        if (lane >= static_cast<uint32_t>(o)) inc += x;
+      }
+      const uint64_t doff = wave_out + inc - v;
+      if (r < n) offsets[r] = doff;
+      wave_sync();  // the tile
+      if (r >= n || !szok) return;
+      enc_direct_ctx d{xdr, heap, heap_len, cap, stack_limit, r, err, doff};
+      if (mark) {  // the message's record mark (message_t::alloc, marshal.cc:15-31)
+        if (!d.field(kOpRecordLevel, 0, 4)) return;
+        d.put(mark_word(sz - 4u));
+      }
+      (void)w.enc(d, tile + lane * stride, true);
+      return;
+    }
+  }
+  const uint32_t incl = wave_incl_scan(v);  // a wave's stretch < 2^31 bytes (direct mode above)
   const uint32_t T = rl32(incl, 63);        // bytes of the wave's stretch
   const uint64_t off = wave_out + (incl - v);
   if (r < n) offsets[r] = off;
@@ -699,6 +761,16 @@ struct dec_ctx {
     if (elem_area_ok(ecur, eend, cnt, stride, wire, b - p)) return true;
     return fail(op, XDRG_ERR_OVERFLOW_GET);
   }
+  // ... of an element subroutine's container: every element takes at least
+  // `minw` wire bytes, so a count the bytes left cannot hold fails before
+  // any element (sub_kernels.h, oracle/xdr_oracle.c)
+  __device__ __forceinline__ bool area_sub(uint32_t op, uint32_t cnt, uint32_t stride, uint32_t minw) {
+    ecur = (ecur + 7u) & ~7ull;
+    const uint64_t bytes = static_cast<uint64_t>(cnt) * stride;
+    if (static_cast<uint64_t>(cnt) * minw > b - p || ecur > eend || bytes > eend - ecur)
+      return fail(op, XDRG_ERR_OVERFLOW_GET);
+    return true;
+  }
 };
 
 // NWD > 0 (plan-specialized walks, whose native offsets are constants): the
@@ -877,7 +949,8 @@ __device__ __forceinline__ void var_decode_body(
 // = the 64-record sums.
 template <class W>
 __device__ __forceinline__ void var_size_body(const W &w, const uint8_t *__restrict__ native, uint64_t n,
-                                              uint32_t stride, uint32_t *__restrict__ sizes,
+                                              uint32_t stride, const uint8_t *__restrict__ heap,
+                                              uint64_t heap_len, uint32_t *__restrict__ sizes,
                                               unsigned long long *__restrict__ block_sums,
                                               uint32_t mark, unsigned long long *err) {
   extern __shared__ __attribute__((aligned(16))) uint8_t tile[];
@@ -896,7 +969,7 @@ __device__ __forceinline__ void var_size_body(const W &w, const uint8_t *__restr
   uint32_t size = 0;
   if (r < n) {
     uint32_t bad_op = 0xffffffffu;
-    const uint64_t s = w.size(tile + lane * stride, bad_op) + mark;
+    const uint64_t s = w.size(tile + lane * stride, heap, heap_len, bad_op) + mark;
     if (bad_op != 0xffffffffu) {
       report(err, r, bad_op, XDRG_ERR_BAD_DISCRIMINANT);
       size = kSizeErr;

@@ -768,6 +768,7 @@ overflow:
 // device where its specialized kernels are not loaded.
 struct interp_walk {
   static constexpr bool kFastWalk = false;  // enc() takes the checked context only
+  static constexpr bool kDirect = false;    // (launched only when 64 records fit 2^31 bytes)
   static constexpr uint32_t kMaxDepth = 0;
   static constexpr uint32_t kWords = 0;  // walks every window (no word list)
   const xdrg_op *__restrict__ ops;
@@ -1890,7 +1891,7 @@ int var_encode(const xdrg_plan &P, const dev_tables &T, const void *d_native, ui
   uint8_t *xdr8 = static_cast<uint8_t *>(d_xdr);
   const uint32_t nops = uint32_t(p->ops.size());
   // plan-specialized kernels (spec.cpp): straight-line size and encode walks
-  const spec_module *SM = O.specialize && O.enc_kernel == 0 && !p->has_sub ? spec_get(*p) : nullptr;
+  const spec_module *SM = O.specialize && O.enc_kernel == 0 && !p->deep ? spec_get(*p) : nullptr;
   uint32_t Cs = 0, lds_s = 0;
   if (SM) {
     // a word-list walk (var_kernels.h WL) does not repeat per window, so
@@ -1900,7 +1901,9 @@ int var_encode(const xdrg_plan &P, const dev_tables &T, const void *d_native, ui
              ? static_cast<uint32_t>(std::min<uint64_t>(4u << 10, (64ull * std::max<uint64_t>(max_rec, 16) + 31u) & ~15ull))
              : window();
     lds_s = enc_layout(p->stride, p->spec.info.slots, Cs).total;
-    if (lds_s > kVarLdsBudget || 64ull * max_rec >= (1ull << 31) || !aligned(d_native, 16)) SM = nullptr;
+    // (a wave whose stretch could pass 2 GiB writes its records directly,
+    // var_encode_body's direct mode)
+    if (lds_s > kVarLdsBudget || !aligned(d_native, 16)) SM = nullptr;
   }
   pool_lease lease;  // element subroutines nested past XDRG_SUB_FRAMES
   deep_passes dp;
@@ -1912,7 +1915,8 @@ int var_encode(const xdrg_plan &P, const dev_tables &T, const void *d_native, ui
     if (SM && !p->linear) {
       const size_t tile = 64ull * p->stride;
       uint32_t n_mark = mark;
-      void *args[] = {&nat8, &n, const_cast<uint32_t *>(&p->stride), &sizes, &bsum, &n_mark, &err};
+      void *args[] = {&nat8, &n, const_cast<uint32_t *>(&p->stride), &d_heap, &heap_len, &sizes, &bsum, &n_mark,
+                      &err};
       HIPCHK(hipModuleLaunchKernel(static_cast<hipFunction_t>(SM->f_size), static_cast<uint32_t>(nb), 1, 1,
                                    64, 1, 1, static_cast<uint32_t>(tile), s, args, nullptr));
     } else {
@@ -1921,7 +1925,7 @@ int var_encode(const xdrg_plan &P, const dev_tables &T, const void *d_native, ui
     if (int rc = xdrg::launch_block_scan(bsum, bbase, uint32_t(nb), d_status, d_offsets, n, s)) return rc;
     if (phase == kEncSizes) return XDRG_OK;
   }
-  if (p->has_sub) {
+  if (p->has_sub && !SM) {
     const deep_passes ep = encode_passes(dp);
     k_sub_encode<<<(n + 255) / 256, 256, lds_ops, s>>>(nat8, n, p->stride, d_heap, heap_len, xdr8, cap,
                                                       d_offsets, sizes, bbase, T.d_ops, nops, T.d_table,
@@ -2065,7 +2069,8 @@ int var_decode(const xdrg_plan &P, const dev_tables &T, const void *d_xdr, uint6
   int kern = O.dec_kernel;
   if (kern == 2 && !ok_W) kern = 0;
   if (kern == 0) kern = ok_W ? 2 : 1;
-  if (p->has_sub) {  // containers of variable-size elements: the frame walk
+  const spec_module *SM = O.specialize && O.dec_kernel == 0 && kern == 2 && !p->deep ? spec_get(*p) : nullptr;
+  if (p->has_sub && !SM) {  // containers of variable-size elements: the frame walk
     pool_lease lease;  // element subroutines nested past XDRG_SUB_FRAMES
     deep_passes dp;
     if (int rc = lease.acquire(*p, n, s, dp)) return rc;
@@ -2085,7 +2090,6 @@ int var_decode(const xdrg_plan &P, const dev_tables &T, const void *d_xdr, uint6
     HIPCHK(hipGetLastError());
     return XDRG_OK;
   }
-  const spec_module *SM = O.specialize && O.dec_kernel == 0 && kern == 2 ? spec_get(*p) : nullptr;
   if (SM) {  // plan-specialized decode walk (spec.cpp)
     const uint64_t nb = (n + 63) / 64;
     uint32_t st = p->stride, sl = stack_limit, cw = Cw, F = p->heap_factor, mk = mark, lws = lw;
@@ -2171,7 +2175,7 @@ int run_index(const xdrg_plan *p, const dev_tables *T, const void *d_stream, uin
   // the tables are needed above one segment; the valid-node lists always
   // record starts: the plan's generated parse when its kernels are built
   // (codegen.cpp plan_rx), else the interpreted rx_len
-  const spec_module *SM = REC && p->opts.specialize && !p->has_sub ? spec_get(*p) : nullptr;
+  const spec_module *SM = REC && p->opts.specialize && !p->deep ? spec_get(*p) : nullptr;
   if (SM && SM->f_ix_seg) {
     uint64_t *t0 = L.top > 0 ? tab(0) : nullptr;
     uint32_t ml = max_msg_len, K = L.K, hf = rp.fpc != RX_BAD, fd = rp.fd;
