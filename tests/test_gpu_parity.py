@@ -82,7 +82,8 @@ def test_golden_decode(dev, name):
 # ------------------------------------------------------------- full size
 @pytest.mark.parametrize("name,n", [("rec128", 1 << 20), ("numerics", 1 << 16),
                                     ("recvar", 1 << 16), ("rpc", 1 << 16), ("vecrec", 1 << 16),
-                                    ("recvar", 1 << 20), ("rpc", 1 << 20), ("numerics", 1 << 20)])
+                                    ("recvar", 1 << 20), ("rpc", 1 << 20), ("numerics", 1 << 20),
+                                    ("vecrec", 1 << 20), ("containertest", 1 << 16), ("containertest", 1 << 20)])
 def test_full_size_hash(dev, manifest, name, n):
     h = manifest["hashes"][f"{name}_{n}"]
     p = plan(name)
@@ -438,11 +439,13 @@ def test_record_depths_golden(dev, name):
     n = SMALL_N[name]
     mar = M.Marshaler(plan(name), dev)
     nat = to_dev(golden(name, n, "native"), dev)
+    hp = golden(name, n, "heap")
+    heap = to_dev(hp, dev) if hp.size else None  # element arrays of subroutine containers
     want = golden(name, n, "depths", np.uint32)
-    got = mar.record_depths(nat, n).cpu().numpy().view(np.uint32)
+    got = mar.record_depths(nat, n, heap).cpu().numpy().view(np.uint32)
     assert np.array_equal(got, want)
     for lim in range(int(want.max()) + 2):
-        assert np.array_equal(mar.check_xdr_depth(nat, n, lim).cpu().numpy(), want <= lim)
+        assert np.array_equal(mar.check_xdr_depth(nat, n, lim, heap).cpu().numpy(), want <= lim)
 
 
 @pytest.mark.parametrize("name,n", [("rpc", 1 << 20), ("vecrec", 1 << 16)])
