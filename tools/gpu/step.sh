@@ -20,6 +20,6 @@ for st in ${STEPS:-tests bench}; do
   esac
   rc=$?
   echo "[step] $st rc=$rc $(date +%T)"
-  [ $rc -ne 0 ] && { tail -30 "$O"/*.log; exit $rc; }
+  [ $rc -ne 0 ] && { tail -n 30 "$O"/*.log; exit $rc; }
 done
 tail -n 3 "$O"/*.log
