@@ -329,7 +329,7 @@ def host_inclusive_var(mar, plan, nat_dev, heap_dev, n, reps=3):
     s = torch.cuda.current_stream()
     h_nat = nat_dev.cpu().pin_memory()
     h_heap = heap_dev.cpu().pin_memory()
-    X = int(mar.serial_sizes(nat_dev, n).to(torch.int64).sum().item())
+    X = int(mar.serial_sizes(nat_dev, n, heap=heap_dev).to(torch.int64).sum().item())
     d_nat, d_heap = torch.empty_like(nat_dev), torch.empty_like(heap_dev)
     d_xdr = torch.empty(X, dtype=torch.uint8, device=dev)
     d_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
@@ -474,7 +474,7 @@ def messages_leg(schema, plan, mar, nat, heap, n, reps=20):
     stream = torch.cuda.current_stream()
     s = stream.cuda_stream
     X = n * plan.fixed_size if plan.is_fixed else \
-        int(mar.serial_sizes(nat, n).to(torch.int64).sum().item())
+        int(mar.serial_sizes(nat, n, heap=heap).to(torch.int64).sum().item())
     total = X + 4 * n
     out = torch.empty(total, dtype=torch.uint8, device=dev)
     offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
@@ -605,7 +605,7 @@ def setup(schema, n, dev, rank, world):
     if plan.is_fixed:
         xdr = torch.empty(n * plan.fixed_size, dtype=torch.uint8, device=dev)
         return plan, mar, nat, heap, xdr, back, None, None
-    total = int(mar.serial_sizes(nat, n).to(torch.int64).sum().item())
+    total = int(mar.serial_sizes(nat, n, heap=heap).to(torch.int64).sum().item())
     xdr = torch.empty(total, dtype=torch.uint8, device=dev)
     offsets = torch.empty(n + 1, dtype=torch.int64, device=dev)
     heap_out = torch.empty(plan.decode_heap_bytes(total), dtype=torch.uint8, device=dev)
@@ -823,7 +823,9 @@ def report(args, engine, world, rows, X, kern, alg_bytes, launches, enc_ms, dec_
           "numerics": "numerics (tests/xdrtest.x) fixed 44-byte records, 56-byte native",
           "recvar": "recvar: opaque<256> + string<64> variable-length records",
           "rpc": "rpc_msg (xdrpp/rpc_msg.x) nested discriminated unions",
-          "vecrec": "vecrec: int<16>, mismatch_info *, vpair<8> counted/optional containers"}[args.schema]
+          "vecrec": "vecrec: int<16>, mismatch_info *, vpair<8> counted/optional containers",
+          "containertest": "containertest (tests/xdrtest.x): u_4_12 uvec<> (variable-size union "
+                           "elements, element subroutines) + string sarr[2]"}[args.schema]
     line = {
         "metric": ("XDR encode+decode GiB/s (device-resident, 1M×128B records) + %HBM roofline"
                    if args.schema == "rec128" else
