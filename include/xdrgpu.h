@@ -295,9 +295,13 @@ enum xdrg_plan_option {
   XDRG_OPT_GRP_UNROLL = 9,        /* fixed group kernel chunks in flight, 0 auto   */
   XDRG_OPT_GRP_BLOCKS = 10,       /* fixed group kernel workgroups, 0 auto         */
   XDRG_OPT_GRP_NONTEMPORAL = 11,  /* fixed group kernel non-temporal stores: 0 / 1 */
-  XDRG_OPT_SPECIALIZE = 12        /* var plans: 1 (default) run the plan-specialized
+  XDRG_OPT_SPECIALIZE = 12,       /* var plans: 1 (default) run the plan-specialized
                                      kernels (built by the first launch, or
                                      xdrg_plan_build_kernels); 0 the interpreter */
+  XDRG_OPT_INDEX_FAST = 13        /* xdrg_index_records: 1 (default) the speculative
+                                     chain walk first, the list ranking only when
+                                     its checks fail; 0 the list ranking alone.
+                                     Same offsets, count and errors either way */
 };
 int xdrg_plan_set_option(xdrg_plan *plan, int option, int64_t value);
 
@@ -481,9 +485,16 @@ size_t xdrg_index_workspace_size(uint64_t len, uint32_t max_msg_len);
 /*
  * Record index of n records of `plan` concatenated in one stream, the
  * input of xdr_from_opaque(bytes, r0, ..., rn-1) (xdrpp/marshal.h:299-306),
- * computed on the device: every word position is parsed as a possible
- * record start (lengths, counts and discriminants only) and the chain of
- * record ends from byte 0 is ranked as for xdrg_index_msgs.  Writes
+ * computed on the device.  First a speculative walk: each 16 KiB segment
+ * of the stream guesses where the chain of records enters it, walks the
+ * chain (lengths, counts and discriminants only) and every guess is
+ * checked against the previous segment's exit; when all hold and the chain
+ * ends at len with exactly n records, that is the index.  Otherwise
+ * (damaged streams, trailing or missing records, long records, or a guess
+ * that missed: XDRG_OPT_INDEX_FAST = 0 forces this) every word position is
+ * parsed as a possible record start and the chain of record ends from byte
+ * 0 is ranked as for xdrg_index_msgs.  The first u32 of the workspace's
+ * last 256 bytes says which ran (1: the speculative walk).  Writes
  * d_offsets[0..n] for xdrg_decode: record r = [off[r], off[r+1]).  Where
  * the records stop parsing -- a bad discriminant, a length past its bound
  * or past the stream -- record k gets [off[k], len) and the rest [len, len),

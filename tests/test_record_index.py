@@ -4,10 +4,12 @@ the record boundaries xdr_from_opaque walks (xdrpp/marshal.h:299-306).
 CPU: the C restatement (oracle/xdr_oracle.c xdro_index_records) against
 the reference's own record offsets (golden fixtures written by the real
 xdr_put, oracle/ref_golden.cc; containers.json from genuine xdrc output).
-GPU: the list-ranking index against the restatement -- goldens, full-size
-encoded batches (offsets of the encode == the index of its output), and
-damaged streams (bad lengths and discriminants, truncation, extra records,
-trailing garbage, a record past the index window).
+GPU: both device paths -- the speculative chain walk and the list ranking
+it falls back to -- against the restatement: goldens, full-size encoded
+batches (offsets of the encode == the index of its output, and the walk
+must hold those itself), streams whose payloads hold records, and damaged
+streams (bad lengths and discriminants, truncation, extra records, trailing
+garbage, a record past the index window).
 """
 import json
 import os
@@ -102,8 +104,9 @@ def _dev(a, dev):
     return torch.from_numpy(np.array(a)).to(dev)
 
 
-def _gpu_index(mar, x, n, maxlen, dev):
-    """(offsets, count, error) of the device index."""
+def _gpu_index(mar, x, n, maxlen, dev, ws_tail=False):
+    """(offsets, count, error) of the device index (+ the workspace's last
+    256 bytes: the fast path's flag)."""
     import torch
     from xdrpp_amd import marshal as M
     L = A.lib()
@@ -117,7 +120,8 @@ def _gpu_index(mar, x, n, maxlen, dev):
                                  cnt.data_ptr(), ws.data_ptr(), ws.numel(), mar.status.ptr, s),
             "xdrg_index_records")
     e = M.error_from(mar.plan, mar.status.read(s))
-    return offs.cpu().numpy().view(np.uint64), int(cnt.cpu().numpy().view(np.uint64)[0]), e
+    res = offs.cpu().numpy().view(np.uint64), int(cnt.cpu().numpy().view(np.uint64)[0]), e
+    return res + (ws[-256:].cpu().numpy(),) if ws_tail else res
 
 
 @pytest.mark.gpu
@@ -141,6 +145,82 @@ def test_gpu_index_matches_oracle(dev, name, spec):
         assert (err.code if err else 0) == wrc, label
 
 
+def _recvar_bytes(rid, kind, blob, name, score):
+    """One recvar record on the wire (oracle/x/bench.x), written by hand."""
+    pad = lambda b: b + b"\0" * (-len(b) % 4)
+    return (rid.to_bytes(8, "big") + kind.to_bytes(4, "big", signed=True) + len(blob).to_bytes(4, "big") +
+            pad(blob) + len(name).to_bytes(4, "big") + pad(name) + score.to_bytes(8, "big"))
+
+
+def nested_recvar_stream(n, seed):
+    """recvar records whose blobs hold encoded recvar records (one or two):
+    word positions inside a payload that parse as record chains, which the
+    speculative walk may take as its guess."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        k = int(rng.integers(0, 4))
+        if k == 0:
+            blob = bytes(rng.integers(0, 256, int(rng.integers(0, 257)), dtype=np.uint8))
+        else:
+            inner = b"".join(_recvar_bytes(int(rng.integers(0, 2**40)), int(rng.integers(-9, 9)),
+                                           bytes(int(rng.integers(0, 40))), b"in", 7) for _ in range(k))
+            blob = inner[:256]
+        name = bytes(rng.integers(97, 123, int(rng.integers(0, 65)), dtype=np.uint8))
+        out.append(_recvar_bytes(i, int(rng.integers(-5, 5)), blob, name, int(rng.integers(0, 2**63))))
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(w) for w in out])
+    return np.frombuffer(b"".join(out), dtype=np.uint8).copy(), offs, n
+
+
+def tiled(x, offs, n, reps):
+    """reps copies of a stream of n records: a stream of reps * n records."""
+    L = int(offs[n])
+    o = np.concatenate([offs[:n] + np.uint64(r * L) for r in range(reps)] + [np.array([reps * L], np.uint64)])
+    return np.tile(x[:L], reps), o, reps * n
+
+
+def _fast_flag(ws_tail):
+    return int(ws_tail[:4].view(np.uint32)[0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("spec", [1, 0], ids=["generated", "interpreted"])
+@pytest.mark.parametrize("name", VAR + list(S.CONTAINERS) + ["nested_recvar"])
+def test_gpu_index_fast_path(dev, name, spec):
+    """The speculative walk and the list ranking on the same streams, both
+    against the C restatement: streams long enough for the walk (>= 4
+    segments), good and damaged at many places, and in every case the same
+    offsets, count and error.  On the good streams the walk must hold the
+    index itself (its flag), or it would only be tested as a pass-through."""
+    import torch
+    from xdrpp_amd import marshal as M
+    if name == "nested_recvar":
+        cp = compile_plan(S.recvar)
+        x, offs, n = nested_recvar_stream(1500, 3)
+    else:
+        cp = compile_plan(S.ALL.get(name) or S.CONTAINERS[name])
+        x, offs, n = gold_stream(name) if name in VAR else containers_stream(name)
+    want0, _, _, _ = O.index_records(cp, x, n, A.INDEX_MAX_MSG)
+    assert np.array_equal(want0, offs)
+    reps = max(1, -(-(1 << 18) // int(offs[n])))  # >= 256 KiB
+    x, offs, n = tiled(x, offs, n, reps)
+    W = window(cp)
+    cases = damaged(x, offs, n, 11) + damaged(x, offs, n, 12)[5:]
+    for fast in (1, 0):
+        mar = M.Marshaler(M.Plan(cp, {"specialize": spec, "index_fast": fast}), dev)
+        for label, y, k in cases:
+            want, wcnt, wrc, wer = O.index_records(cp, y, k, W)
+            got, gcnt, err, tail = _gpu_index(mar, y, k, W, dev, ws_tail=True)
+            assert np.array_equal(got, want), (fast, label)
+            assert gcnt == wcnt, (fast, label)
+            assert (err.code if err else 0) == wrc, (fast, label)
+            if err:
+                assert err.record == wer, (fast, label)
+            if fast and label == "good" and name != "nested_recvar":
+                assert _fast_flag(tail) == 1, label  # (the flag is not written without the walk)
+
+
 @pytest.mark.gpu
 def test_gpu_index_long_record(dev):
     from xdrpp_amd import marshal as M
@@ -154,10 +234,11 @@ def test_gpu_index_long_record(dev):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["recvar", "rpc"])
+@pytest.mark.parametrize("name", ["recvar", "rpc", "vecrec", "containertest"])
 def test_gpu_index_full_size(dev, name):
-    """1M records: the index of the encode's output is the encode's offsets,
-    and decode without offsets (device index) equals decode with them."""
+    """1M records: the index of the encode's output is the encode's offsets
+    (and the speculative walk held it: its flag), and decode without offsets
+    (device index) equals decode with them."""
     import torch
     from xdrpp_amd import marshal as M
     from xdrpp_amd import workloads as W
@@ -168,6 +249,18 @@ def test_gpu_index_full_size(dev, name):
     r = mar.encode(nat, n, heap)
     offs = mar.index_records(r.xdr, n)
     assert torch.equal(offs, r.offsets)
+    L = A.lib()
+    maxlen = min(mar.plan.max_record_bytes, A.INDEX_MAX_MSG)
+    ws = torch.empty(L.xdrg_index_workspace_size(r.xdr.numel(), maxlen), dtype=torch.uint8, device=dev)
+    o2 = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    cnt = torch.empty(1, dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    mar.status.init(s)
+    A.check(L.xdrg_index_records(mar.plan.handle, r.xdr.data_ptr(), r.xdr.numel(), n, maxlen, o2.data_ptr(),
+                                 cnt.data_ptr(), ws.data_ptr(), ws.numel(), mar.status.ptr, s), "index")
+    assert mar.status.read(s).code == 0
+    assert torch.equal(o2, r.offsets) and int(cnt.item()) == n
+    assert _fast_flag(ws[-256:].cpu().numpy()) == 1
     a, ha = mar.decode(r.xdr, n, r.offsets)
     b, hb = mar.decode(r.xdr, n)
     assert torch.equal(a, b) and torch.equal(ha, hb)

@@ -1,0 +1,93 @@
+"""Per-wave phase timestamps of the speculative record index walk
+(index_kernels.h rxs_walk_body), plan-specialized.
+
+    python tools/tune/ix_stamps.py build recvar rpc   # here: stamped .co files
+    python tools/tune/ix_stamps.py run recvar rpc     # GPU box
+
+`build` compiles the plan's generated source with XDRG_XSTAMP(k) defined:
+lane 0 of every wave writes s_memtime at the phase boundaries into the
+workspace's list area past the node lists (the walk's own scratch; the
+library never sees the macro).  `run` attaches the code object to a plan,
+indexes an encoded 1M batch, checks the offsets and prints the median and
+90th-percentile cycles per phase.
+"""
+import ctypes as C
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+from xdrpp_amd import _abi as A, build as B, marshal as M, schemas as S  # noqa: E402
+
+OUT = os.path.join(ROOT, "tools", "tune", "_stamps_ix")
+NST = 8
+SEGB = 15120  # kRxsSeg
+STAMP = ("#define XDRG_XSTAMP(k) do { if (threadIdx.x == 0) { const unsigned long long t_ = "
+         "__builtin_amdgcn_s_memtime(); *reinterpret_cast<volatile unsigned long long *>("
+         "reinterpret_cast<char *>(nodes) + static_cast<unsigned long long>(gridDim.x) * (kRxsSeg / 2) + "
+         "(static_cast<unsigned long long>(blockIdx.x) * " + str(NST) + "ull + (k)) * 8ull) = t_; } } while (0)\n")
+PHASES = ["stage", "guess", "agree", "count", "write"]
+
+
+def source(plan):
+    L = A.lib()
+    n = C.c_size_t()
+    A.check(L.xdrg_plan_kernel_source(plan.handle, None, 0, C.byref(n)), "xdrg_plan_kernel_source")
+    buf = C.create_string_buffer(n.value + 1)
+    A.check(L.xdrg_plan_kernel_source(plan.handle, buf, n.value + 1, C.byref(n)), "xdrg_plan_kernel_source")
+    return buf.value.decode()
+
+
+def build(schemas):
+    os.makedirs(OUT, exist_ok=True)
+    for name in schemas:
+        src = os.path.join(OUT, f"{name}.hip")
+        with open(src, "w") as f:
+            f.write(STAMP + source(M.Plan(S.ALL[name])))
+        subprocess.check_call([B.hipcc(), "--genco", f"--offload-arch={B.ARCH}", "-O3", "-std=c++17",
+                               "-I", B.CSRC, "-I", os.path.join(ROOT, "include"),
+                               "-o", os.path.join(OUT, f"{name}.co"), src])
+        print("built", name)
+
+
+def run(schemas):
+    import torch
+    from xdrpp_amd import workloads as W
+    dev = torch.device("cuda:0")
+    L = A.lib()
+    for name in schemas:
+        n = 1 << 20
+        p = M.Plan(S.ALL[name])
+        code = open(os.path.join(OUT, f"{name}.co"), "rb").read()
+        A.check(L.xdrg_plan_load_kernels(p.handle, code, len(code)), "xdrg_plan_load_kernels")
+        mar = M.Marshaler(p, dev)
+        nat, heap = (torch.from_numpy(a).to(dev) for a in W.GENERATORS[name](n))
+        enc = mar.encode(nat, n, heap)
+        total = enc.xdr.numel()
+        maxlen = min(p.max_record_bytes, A.INDEX_MAX_MSG)
+        ws = torch.zeros(L.xdrg_index_workspace_size(total, maxlen), dtype=torch.uint8, device=dev)
+        offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        cnt = torch.empty(1, dtype=torch.int64, device=dev)
+        s = torch.cuda.current_stream().cuda_stream
+        for _ in range(3):
+            mar.status.init(s)
+            A.check(L.xdrg_index_records(p.handle, enc.xdr.data_ptr(), total, n, maxlen, offs.data_ptr(),
+                                         cnt.data_ptr(), ws.data_ptr(), ws.numel(), mar.status.ptr, s), "index")
+        torch.cuda.synchronize()
+        assert torch.equal(offs, enc.offsets), name
+        nseg = (total + SEGB - 1) // SEGB
+        o = nseg * (SEGB // 2)
+        st = ws[o:o + nseg * NST * 8].cpu().numpy().view(np.uint64).reshape(nseg, NST)[:, :6].astype(np.int64)
+        d = {}
+        for i, ph in enumerate(PHASES):
+            dd = st[:, i + 1] - st[:, i]
+            d[ph] = [int(np.median(dd)), int(np.percentile(dd, 90)), int(dd.max())]
+        d["wave"] = [int(np.median(st[:, 5] - st[:, 0])), int(np.percentile(st[:, 5] - st[:, 0], 90))]
+        print(name, "segments", nseg, "cycles [median, p90, max]:", d, flush=True)
+
+
+if __name__ == "__main__":
+    {"build": build, "run": run}[sys.argv[1]](sys.argv[2:])

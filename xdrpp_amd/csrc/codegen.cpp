@@ -223,7 +223,7 @@ struct gen {
   // `past` when the record runs past lim, or RX_BAD.
   void rx_block(uint32_t pc, uint32_t stop) {
     auto need = [&](const std::string &n) { line("if (lim - p < " + n + ") return past;"); };
-    auto word = [&]() { need("4"); line("{ const uint32_t v = bswap32(ld32(s + p)); p += 4;"); };
+    auto word = [&]() { need("4"); line("{ const uint32_t v = bswap32(rd(p)); p += 4;"); };
     while (pc != stop) {
       const xdrg_op &e = op(pc);
       switch (e.kind) {
@@ -968,11 +968,15 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
     << "    if (!ok) return false;\n"
     << dec_code << "    return true;\n  }\n"
     << "};\n\n"
-    << "struct plan_rx {  // index_kernels.h ix_seg_body's parser\n"
+    << "struct plan_rx {  // index_kernels.h ix_seg_body's and rxs_walk_body's parser\n"
     << "  __device__ __forceinline__ void init(uint32_t *) const {}\n"
     << "  __device__ __forceinline__ bool first_ok(const uint32_t *, uint32_t v) const { return " << first << "; }\n"
-    << "  __device__ __forceinline__ uint32_t rlen(const uint32_t *, const uint8_t *__restrict__ s, uint64_t len,\n"
+    << "  __device__ __forceinline__ uint32_t rlen(const uint32_t *m, const uint8_t *__restrict__ s, uint64_t len,\n"
     << "                                           uint64_t a, uint32_t maxlen) const {\n"
+    << "    return rlen_rd(m, rx_global{s}, len, a, maxlen);\n  }\n"
+    << "  template <class RD>\n"
+    << "  __device__ __forceinline__ uint32_t rlen_rd(const uint32_t *, const RD &rd, uint64_t len,\n"
+    << "                                              uint64_t a, uint32_t maxlen) const {\n"
     << "    const bool capped = a + maxlen < len;\n"
     << "    const uint64_t lim = capped ? a + maxlen : len;\n"
     << "    const uint32_t past = capped ? RX_LONG : RX_BAD;\n"
@@ -981,8 +985,13 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
     << "};\n\n"
     << "extern \"C\" __global__ __launch_bounds__(256) void xdrg_spec_ix_seg(\n"
     << "    const uint8_t *s, uint64_t len, uint32_t maxlen, uint32_t K, uint64_t *tab, uint32_t *list,\n"
-    << "    uint32_t *lcount, uint32_t has_first, uint32_t fd) {\n"
+    << "    uint32_t *lcount, uint32_t has_first, uint32_t fd, const uint32_t *skip) {\n"
+    << "  if (skip && *skip == 1u) return;  // the speculative walk holds the index\n"
     << "  ix_seg_body<true>(plan_rx{}, s, len, maxlen, K, tab, list, lcount, has_first != 0, fd);\n}\n\n"
+    << "extern \"C\" __global__ __launch_bounds__(64) void xdrg_spec_rxs_walk(\n"
+    << "    const uint8_t *s, uint64_t len, uint32_t maxlen, uint64_t *seg, uint16_t *nodes,\n"
+    << "    uint32_t *flag, uint32_t has_first, uint32_t fd) {\n"
+    << "  rxs_walk_body(plan_rx{}, s, len, maxlen, seg, nodes, flag, has_first != 0, fd);\n}\n\n"
     << "extern \"C\" __global__ __launch_bounds__(64) void xdrg_spec_size(\n"
     << "    const uint8_t *native, uint64_t n, uint32_t stride, const uint8_t *heap, uint64_t heap_len,\n"
     << "    uint32_t *sizes, unsigned long long *block_sums, uint32_t mark, unsigned long long *err) {\n"

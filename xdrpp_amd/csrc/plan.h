@@ -107,6 +107,7 @@ struct plan_opts {
   int grp_blocks = 0;      // group kernel: workgroups (0: 2048)
   int grp_nontemporal = 0; // group kernel: non-temporal stores
   int specialize = 1;      // var plans: plan-specialized kernels (spec.cpp) when built
+  int index_fast = 1;      // record index: speculative chain walk before the list ranking
 };
 
 }  // namespace xdrg

@@ -180,10 +180,10 @@ const spec_module *spec_get(const xdrg_plan &cp) {
   if (hipModuleLoadData(&m, s.code.data()) != hipSuccess)
     return fail(nullptr, "specialized kernels: the code object does not load on this device");
   spec_module &d = s.dev[dev];
-  hipFunction_t f[5] = {};
-  const char *names[5] = {"xdrg_spec_size", "xdrg_spec_encode", "xdrg_spec_decode", "xdrg_spec_decode_copy",
-                          "xdrg_spec_ix_seg"};
-  for (int i = 0; i < 5; ++i)
+  hipFunction_t f[6] = {};
+  const char *names[6] = {"xdrg_spec_size", "xdrg_spec_encode", "xdrg_spec_decode", "xdrg_spec_decode_copy",
+                          "xdrg_spec_ix_seg", "xdrg_spec_rxs_walk"};
+  for (int i = 0; i < 6; ++i)
     if (hipModuleGetFunction(&f[i], m, names[i]) != hipSuccess)
       return fail(m, "specialized kernels: the code object lacks a kernel");
   // a code object of another kernel interface (an older build's AOT file),
@@ -206,6 +206,7 @@ const spec_module *spec_get(const xdrg_plan &cp) {
   d.f_dec = f[2];
   d.f_dec_copy = f[3];
   d.f_ix_seg = f[4];
+  d.f_rxs_walk = f[5];
   s.loaded[dev].store(true, std::memory_order_release);
   return &d;
 }

@@ -16,7 +16,7 @@ constexpr int kSpecDevices = 64;
 // Interface version of the generated kernels (their parameter lists and
 // LDS layout, var_kernels.h): the source defines xdrg_spec_iface with it,
 // and a code object that carries another value is refused at load.
-constexpr unsigned kSpecIface = 6;
+constexpr unsigned kSpecIface = 7;
 
 // The generated source of a plan and the launch facts it fixes.
 struct spec_info {
@@ -32,7 +32,8 @@ struct spec_info {
 struct spec_module {
   void *module = nullptr;  // hipModule_t
   void *f_size = nullptr, *f_enc = nullptr, *f_dec = nullptr, *f_dec_copy = nullptr;  // hipFunction_t
-  void *f_ix_seg = nullptr;  // record-start parse of the plain-stream index
+  void *f_ix_seg = nullptr;  // record-start parse of the plain-stream index (list ranking)
+  void *f_rxs_walk = nullptr;  // ... and its speculative chain walk
 };
 
 // A plan's specialized kernels: state 0 = not built yet, 1 = code object

@@ -1041,13 +1041,11 @@ __device__ __forceinline__ uint32_t ix_mark(uint32_t raw, uint64_t w, uint64_t l
 // record the decode rejects.  RX_LONG: the record runs past a + maxlen (but
 // not past the stream), beyond what one segment window can index.
 
-// Stream words through global memory.  (Staging a segment's reachable
-// window in LDS first measured slower on MI355X: 0.69 -> 0.96 ms for 1M
-// recvar records, the occupancy it costs outweighing L2-hit latency.)
-struct rx_global {
-  const uint8_t *s;
-  __device__ __forceinline__ uint32_t operator()(uint64_t p) const { return ld32(s + p); }
-};
+// Stream words through global memory (rx_global, index_kernels.h) in the
+// list ranking.  (Staging a segment's reachable window in LDS first
+// measured slower on MI355X: 0.69 -> 0.96 ms for 1M recvar records, the
+// occupancy it costs outweighing L2-hit latency.)  The fast path
+// (rxs_walk_body) stages its segment: its walks are serial chains.
 
 template <class RD>
 __device__ uint32_t rx_len(const xdrg_op *__restrict__ ops, const uint32_t *__restrict__ table,
@@ -1164,15 +1162,49 @@ struct rx_interp {
                                            uint32_t maxlen) const {
     return rx_len(reinterpret_cast<const xdrg_op *>(smem), rp.table, rx_global{s}, len, a, maxlen);
   }
+  template <class RD>
+  __device__ __forceinline__ uint32_t rlen_rd(const uint32_t *smem, const RD &rd, uint64_t len, uint64_t a,
+                                              uint32_t maxlen) const {
+    return rx_len(reinterpret_cast<const xdrg_op *>(smem), rp.table, rd, len, a, maxlen);
+  }
 };
+
+// skip (record index): 1 when the fast path (rxs_*) holds the index; the
+// list ranking's kernels then return at once.
+__device__ __forceinline__ bool ix_skip(const uint32_t *skip) { return skip && *skip == 1u; }
 
 template <bool REC>
 __global__ __launch_bounds__(256) void k_ix_seg(const uint8_t *__restrict__ s, uint64_t len,
                                                 uint32_t maxlen, uint32_t K,
                                                 uint64_t *__restrict__ tab,
                                                 uint32_t *__restrict__ list,
-                                                uint32_t *__restrict__ lcount, rx_plan rp) {
+                                                uint32_t *__restrict__ lcount, rx_plan rp,
+                                                const uint32_t *__restrict__ skip) {
+  if (ix_skip(skip)) return;
   ix_seg_body<REC>(rx_interp{rp}, s, len, maxlen, K, tab, list, lcount, rp.fpc != RX_BAD, rp.fd);
+}
+
+// The fast path's kernels (index_kernels.h) with the interpreted parse.
+__global__ __launch_bounds__(64) void k_rxs_walk(const uint8_t *__restrict__ s, uint64_t len, uint32_t maxlen,
+                                                 uint64_t *__restrict__ seg, uint16_t *__restrict__ nodes,
+                                                 uint32_t *__restrict__ flag, rx_plan rp) {
+  rxs_walk_body(rx_interp{rp}, s, len, maxlen, seg, nodes, flag, rp.fpc != RX_BAD, rp.fd);
+}
+__global__ __launch_bounds__(256) void k_rxs_check(uint64_t *__restrict__ seg, const uint16_t *__restrict__ nodes,
+                                                   uint64_t nseg, uint64_t len, unsigned long long *__restrict__ cnt,
+                                                   uint32_t *__restrict__ flag) {
+  rxs_check_body(seg, nodes, nseg, len, cnt, flag);
+}
+__global__ __launch_bounds__(64) void k_rxs_final(const xdrg_status *__restrict__ tot, uint64_t len, uint64_t n,
+                                                  uint64_t *__restrict__ offsets, uint64_t *__restrict__ count,
+                                                  uint32_t *__restrict__ flag) {
+  rxs_final_body(tot, len, n, offsets, count, flag);
+}
+__global__ __launch_bounds__(64) void k_rxs_emit(const uint64_t *__restrict__ seg,
+                                                 const uint16_t *__restrict__ nodes,
+                                                 const unsigned long long *__restrict__ base,
+                                                 const uint32_t *__restrict__ flag, uint64_t *__restrict__ offsets) {
+  rxs_emit_body(seg, nodes, base, flag, offsets);
 }
 
 // One node of the next level per workgroup: F children composed for
@@ -1184,8 +1216,9 @@ __global__ __launch_bounds__(256) void k_ix_seg(const uint8_t *__restrict__ s, u
 template <bool LDS>
 __global__ __launch_bounds__(256) void k_ix_up(const uint64_t *__restrict__ in, uint64_t nin,
                                                uint32_t K, uint32_t F, uint64_t *__restrict__ out,
-                                               uint64_t *__restrict__ pf) {
+                                               uint64_t *__restrict__ pf, const uint32_t *__restrict__ skip) {
   extern __shared__ __attribute__((aligned(16))) uint64_t stg[];
+  if (ix_skip(skip)) return;
   const uint64_t c0 = static_cast<uint64_t>(blockIdx.x) * F;
   const uint32_t nc = static_cast<uint32_t>(min<uint64_t>(F, nin - c0));
   const uint64_t *src = in + c0 * K;
@@ -1217,7 +1250,8 @@ __global__ __launch_bounds__(256) void k_ix_up(const uint64_t *__restrict__ in, 
 __global__ __launch_bounds__(64) void k_ix_down(const uint64_t *__restrict__ pf, uint64_t nin,
                                                 uint32_t K, uint32_t F,
                                                 const uint64_t *__restrict__ up,
-                                                uint64_t *__restrict__ ent) {
+                                                uint64_t *__restrict__ ent, const uint32_t *__restrict__ skip) {
+  if (ix_skip(skip)) return;
   const uint64_t c0 = static_cast<uint64_t>(blockIdx.x) * F;
   const uint32_t nc = static_cast<uint32_t>(min<uint64_t>(F, nin - c0));
   const uint32_t j = threadIdx.x;
@@ -1296,7 +1330,9 @@ __global__ __launch_bounds__(256) void k_ix_emit(const uint8_t *__restrict__ s, 
                                                  const uint32_t *__restrict__ lcount,
                                                  uint64_t *__restrict__ offsets, uint64_t max_msgs,
                                                  unsigned long long *count,
-                                                 unsigned long long *err, rx_plan rp, ix_cont C) {
+                                                 unsigned long long *err, rx_plan rp, ix_cont C,
+                                                 const uint32_t *__restrict__ skip) {
+  if (ix_skip(skip)) return;
   // J: successor of a valid node (0xffff: not a valid node); lst: the valid
   // nodes; nj / mk: a round's new successors and marks (double buffer)
   __shared__ __attribute__((aligned(16))) uint16_t J[kIxSW];
@@ -1418,7 +1454,8 @@ __global__ __launch_bounds__(256) void k_ix_emit(const uint8_t *__restrict__ s, 
 
 // Records after the one where the chain ended: [len, len).
 __global__ void k_rx_fill(uint64_t *__restrict__ offsets, const unsigned long long *__restrict__ count,
-                          uint64_t n, uint64_t len) {
+                          uint64_t n, uint64_t len, const uint32_t *__restrict__ skip) {
+  if (ix_skip(skip)) return;
   const uint64_t c = *count;  // all-ones: the chain went past record n
   if (c >= n) return;
   for (uint64_t i = c + 1 + static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i <= n;
@@ -1987,6 +2024,9 @@ struct ix_layout {
   int top = 0;
   uint64_t n[24] = {};
   size_t tab[24] = {}, pf[24] = {}, ent[24] = {};
+  uint64_t rxs_nseg = 0;  // fast path (record index): segments, their records,
+  size_t rxs_seg = 0, rxs_cnt = 0, rxs_base = 0, rxs_tot = 0, rxs_flag = 0;  // counts, bases, total, flag
+                          // (its node lists: in the list area)
   size_t total = 0;
 };
 constexpr size_t kIxLdsBytes = 64u << 10;
@@ -2018,6 +2058,17 @@ ix_layout ix_plan(uint64_t len, uint32_t maxlen) {
     L.ent[l] = off;
     off += align_up(L.n[l] * 8, 256);
   }
+  L.rxs_nseg = (len + kRxsSeg - 1) / kRxsSeg;  // its u16 node lists fit the list area
+  L.rxs_seg = off;
+  off += align_up(L.rxs_nseg * kRxsSegWords * 8, 256);
+  L.rxs_cnt = off;
+  off += align_up(L.rxs_nseg * 8, 256);
+  L.rxs_base = off;
+  off += align_up(L.rxs_nseg * 8, 256);
+  L.rxs_tot = off;
+  off += 256;
+  L.rxs_flag = off;  // the workspace's last 256 bytes (include/xdrgpu.h)
+  off += 256;
   L.total = off;
   return L;
 }
@@ -2176,15 +2227,45 @@ int run_index(const xdrg_plan *p, const dev_tables *T, const void *d_stream, uin
   // record starts: the plan's generated parse when its kernels are built
   // (codegen.cpp plan_rx), else the interpreted rx_len
   const spec_module *SM = REC && p->opts.specialize && !p->deep ? spec_get(*p) : nullptr;
+  // Record index: the speculative chain walk first (index_kernels.h rxs_*);
+  // the list ranking below runs only when its checks fail.  Short streams
+  // (a few segments) go to the list ranking alone.
+  const uint32_t *skip = nullptr;
+  if (REC && p->opts.index_fast && !C.next && len >= 4ull * kRxsSeg && max_msgs > 0) {
+    uint64_t *seg = reinterpret_cast<uint64_t *>(ws + L.rxs_seg);
+    auto *cnt = reinterpret_cast<unsigned long long *>(ws + L.rxs_cnt);
+    auto *base = reinterpret_cast<unsigned long long *>(ws + L.rxs_base);
+    auto *tot = reinterpret_cast<xdrg_status *>(ws + L.rxs_tot);
+    uint32_t *flag = reinterpret_cast<uint32_t *>(ws + L.rxs_flag);
+    uint16_t *nodes = reinterpret_cast<uint16_t *>(vlist);  // the list ranking's lists, unused when it skips
+    const uint32_t ns = static_cast<uint32_t>(L.rxs_nseg);
+    if (SM && SM->f_rxs_walk) {
+      uint32_t ml = max_msg_len, hf = rp.fpc != RX_BAD, fd = rp.fd;
+      void *args[] = {&s8, &len, &ml, &seg, &nodes, &flag, &hf, &fd};
+      HIPCHK(hipModuleLaunchKernel(static_cast<hipFunction_t>(SM->f_rxs_walk), ns, 1, 1, 64, 1, 1, 0, s, args,
+                                   nullptr));
+    } else {
+      k_rxs_walk<<<ns, 64, ops_lds, s>>>(s8, len, max_msg_len, seg, nodes, flag, rp);
+      HIPCHK(hipGetLastError());
+    }
+    k_rxs_check<<<(ns + 255) / 256, 256, 0, s>>>(seg, nodes, L.rxs_nseg, len, cnt, flag);
+    HIPCHK(hipGetLastError());
+    if (int rc = launch_block_scan(cnt, base, ns, tot, nullptr, 0, s)) return rc;
+    k_rxs_final<<<1, 64, 0, s>>>(tot, len, max_msgs, d_offsets, d_count, flag);
+    HIPCHK(hipGetLastError());
+    k_rxs_emit<<<ns, 64, 0, s>>>(seg, nodes, base, flag, d_offsets);
+    HIPCHK(hipGetLastError());
+    skip = flag;
+  }
   if (SM && SM->f_ix_seg) {
     uint64_t *t0 = L.top > 0 ? tab(0) : nullptr;
     uint32_t ml = max_msg_len, K = L.K, hf = rp.fpc != RX_BAD, fd = rp.fd;
-    void *args[] = {&s8, &len, &ml, &K, &t0, &vlist, &vcount, &hf, &fd};
+    void *args[] = {&s8, &len, &ml, &K, &t0, &vlist, &vcount, &hf, &fd, &skip};
     HIPCHK(hipModuleLaunchKernel(static_cast<hipFunction_t>(SM->f_ix_seg), static_cast<uint32_t>(L.nseg), 1, 1, 256,
                                  1, 1, 0, s, args, nullptr));
   } else {
     k_ix_seg<REC><<<L.nseg, 256, ops_lds, s>>>(s8, len, max_msg_len, L.K, L.top > 0 ? tab(0) : nullptr,
-                                               vlist, vcount, rp);
+                                               vlist, vcount, rp, skip);
     HIPCHK(hipGetLastError());
   }
   const size_t stg = L.lds ? static_cast<size_t>(L.F) * L.K * 8 : 0;
@@ -2192,23 +2273,23 @@ int run_index(const xdrg_plan *p, const dev_tables *T, const void *d_stream, uin
   for (int l = 0; l < L.top; ++l) {  // the top level: prefixes only
     uint64_t *o = l + 1 < L.top ? tab(l + 1) : nullptr;
     if (L.lds)
-      k_ix_up<true><<<L.n[l + 1], 256, stg, s>>>(tab(l), L.n[l], L.K, L.F, o, pfx(l));
+      k_ix_up<true><<<L.n[l + 1], 256, stg, s>>>(tab(l), L.n[l], L.K, L.F, o, pfx(l), skip);
     else
-      k_ix_up<false><<<L.n[l + 1], 256, 0, s>>>(tab(l), L.n[l], L.K, L.F, o, pfx(l));
+      k_ix_up<false><<<L.n[l + 1], 256, 0, s>>>(tab(l), L.n[l], L.K, L.F, o, pfx(l), skip);
     HIPCHK(hipGetLastError());
   }
   HIPCHK(hipMemsetAsync(ent(L.top), 0, 8, s));  // the chain starts at word 0 with 0 messages
   for (int l = L.top - 1; l >= 0; --l) {
-    k_ix_down<<<L.n[l + 1], 64, 0, s>>>(pfx(l), L.n[l], L.K, L.F, ent(l + 1), ent(l));
+    k_ix_down<<<L.n[l + 1], 64, 0, s>>>(pfx(l), L.n[l], L.K, L.F, ent(l + 1), ent(l), skip);
     HIPCHK(hipGetLastError());
   }
   k_ix_emit<REC><<<L.nseg, 256, 0, s>>>(s8, len, max_msg_len, ent(0), vlist, vcount, d_offsets + C.m0,
                                         max_msgs - C.m0, reinterpret_cast<unsigned long long *>(d_count), err,
-                                        rp, C);
+                                        rp, C, skip);
   HIPCHK(hipGetLastError());
   if (REC) {
     k_rx_fill<<<static_cast<uint32_t>(std::min<uint64_t>((max_msgs + 256) / 256, 4096)), 256, 0, s>>>(
-        d_offsets, reinterpret_cast<const unsigned long long *>(d_count), max_msgs, len);
+        d_offsets, reinterpret_cast<const unsigned long long *>(d_count), max_msgs, len, skip);
     HIPCHK(hipGetLastError());
   }
   return XDRG_OK;
@@ -2322,6 +2403,7 @@ int xdrg_plan_set_option(xdrg_plan *p, int option, int64_t value) {
     O.grp_blocks = v; return XDRG_OK;
   case XDRG_OPT_GRP_NONTEMPORAL: O.grp_nontemporal = v ? 1 : 0; return XDRG_OK;
   case XDRG_OPT_SPECIALIZE: O.specialize = v ? 1 : 0; return XDRG_OK;
+  case XDRG_OPT_INDEX_FAST: O.index_fast = v ? 1 : 0; return XDRG_OK;
   default: return XDRG_EINVAL;
   }
 }
