@@ -299,9 +299,12 @@ enum xdrg_plan_option {
                                      kernels (built by the first launch, or
                                      xdrg_plan_build_kernels); 0 the interpreter */
   XDRG_OPT_INDEX_FAST = 13        /* xdrg_index_records: 1 (default) the speculative
-                                     chain walk first, the list ranking only when
-                                     its checks fail; 0 the list ranking alone.
-                                     Same offsets, count and errors either way */
+                                     chain walk first, then the call waits for its
+                                     verdict and runs the list ranking only when a
+                                     check failed; 2 the same without the wait (the
+                                     list ranking is queued and skips itself: the
+                                     call stays asynchronous); 0 the list ranking
+                                     alone.  Same offsets, count and errors */
 };
 int xdrg_plan_set_option(xdrg_plan *plan, int option, int64_t value);
 
@@ -494,7 +497,9 @@ size_t xdrg_index_workspace_size(uint64_t len, uint32_t max_msg_len);
  * that missed: XDRG_OPT_INDEX_FAST = 0 forces this) every word position is
  * parsed as a possible record start and the chain of record ends from byte
  * 0 is ranked as for xdrg_index_msgs.  The first u32 of the workspace's
- * last 256 bytes says which ran (1: the speculative walk).  Writes
+ * last 256 bytes says which ran (1: the speculative walk).  By default
+ * (XDRG_OPT_INDEX_FAST) the call waits on the stream once, for the walk's
+ * verdict.  Writes
  * d_offsets[0..n] for xdrg_decode: record r = [off[r], off[r+1]).  Where
  * the records stop parsing -- a bad discriminant, a length past its bound
  * or past the stream -- record k gets [off[k], len) and the rest [len, len),

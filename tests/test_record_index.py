@@ -207,7 +207,7 @@ def test_gpu_index_fast_path(dev, name, spec):
     x, offs, n = tiled(x, offs, n, reps)
     W = window(cp)
     cases = damaged(x, offs, n, 11) + damaged(x, offs, n, 12)[5:]
-    for fast in (1, 0):
+    for fast in (1, 2, 0):  # host-gated walk, asynchronous walk, list ranking alone
         mar = M.Marshaler(M.Plan(cp, {"specialize": spec, "index_fast": fast}), dev)
         for label, y, k in cases:
             want, wcnt, wrc, wer = O.index_records(cp, y, k, W)
@@ -217,7 +217,11 @@ def test_gpu_index_fast_path(dev, name, spec):
             assert (err.code if err else 0) == wrc, (fast, label)
             if err:
                 assert err.record == wer, (fast, label)
-            if fast and label == "good" and name != "nested_recvar":
+            # the walk must hold good streams of types whose payloads do not
+            # parse as records (test_recursive's elements are records, and a
+            # chain entering one need not rejoin the record chain: it may
+            # take the list ranking, which the offsets above check)
+            if fast and label == "good" and name not in ("nested_recvar", "test_recursive"):
                 assert _fast_flag(tail) == 1, label  # (the flag is not written without the walk)
 
 

@@ -24,7 +24,7 @@ from xdrpp_amd import _abi as A, build as B, marshal as M, schemas as S  # noqa:
 
 OUT = os.path.join(ROOT, "tools", "tune", "_stamps_ix")
 NST = 8
-SEGB = 15120  # kRxsSeg
+SEGB = 6944  # kRxsSeg
 STAMP = ("#define XDRG_XSTAMP(k) do { if (threadIdx.x == 0) { const unsigned long long t_ = "
          "__builtin_amdgcn_s_memtime(); *reinterpret_cast<volatile unsigned long long *>("
          "reinterpret_cast<char *>(nodes) + static_cast<unsigned long long>(gridDim.x) * (kRxsSeg / 2) + "

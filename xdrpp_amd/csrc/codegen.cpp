@@ -245,7 +245,7 @@ struct gen {
         word();
         line("  if (v > " + u32(e.arg0) + ") return RX_BAD;");
         line("  if (lim - p < v) return past;");
-        line("  p += (static_cast<uint64_t>(v) + 3u) & ~3ull; }");
+        line("  p += static_cast<U>((static_cast<uint64_t>(v) + 3u) & ~3ull); }");
         break;
       case XDRG_OP_VECTOR:
         if (e.flags & XDRG_F_SUB) {  // each element parsed by its body
@@ -265,8 +265,8 @@ struct gen {
         word();
         line("  if (v > " + u32(e.arg0) + ") return RX_BAD;");
         line("  const uint64_t b = static_cast<uint64_t>(v) * " + u32(e.arg3) + ";");
-        line("  if (lim - p < b) return past;");
-        line("  p += b; }");
+        line("  if (static_cast<uint64_t>(lim - p) < b) return past;");
+        line("  p += static_cast<U>(b); }");
         pc += 1 + e.arg2;
         continue;
       case XDRG_OP_UNION: {
@@ -973,14 +973,15 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
     << "  __device__ __forceinline__ bool first_ok(const uint32_t *, uint32_t v) const { return " << first << "; }\n"
     << "  __device__ __forceinline__ uint32_t rlen(const uint32_t *m, const uint8_t *__restrict__ s, uint64_t len,\n"
     << "                                           uint64_t a, uint32_t maxlen) const {\n"
-    << "    return rlen_rd(m, rx_global{s}, len, a, maxlen);\n  }\n"
-    << "  template <class RD>\n"
-    << "  __device__ __forceinline__ uint32_t rlen_rd(const uint32_t *, const RD &rd, uint64_t len,\n"
-    << "                                              uint64_t a, uint32_t maxlen) const {\n"
-    << "    const bool capped = a + maxlen < len;\n"
-    << "    const uint64_t lim = capped ? a + maxlen : len;\n"
+    << "    return rlen_rd<rx_global, uint64_t>(m, rx_global{s}, len, a, maxlen);\n  }\n"
+    << "  // U: the position type (uint32_t for offsets into a staged stretch)\n"
+    << "  template <class RD, class U>\n"
+    << "  __device__ __forceinline__ uint32_t rlen_rd(const uint32_t *, const RD &rd, U len,\n"
+    << "                                              U a, uint32_t maxlen) const {\n"
+    << "    const bool capped = static_cast<uint64_t>(a) + maxlen < len;\n"
+    << "    const U lim = capped ? static_cast<U>(a + maxlen) : len;\n"
     << "    const uint32_t past = capped ? RX_LONG : RX_BAD;\n"
-    << "    uint64_t p = a;\n"
+    << "    U p = a;\n"
     << rx_code << "    return static_cast<uint32_t>(p - a);\n  }\n"
     << "};\n\n"
     << "extern \"C\" __global__ __launch_bounds__(256) void xdrg_spec_ix_seg(\n"

@@ -198,20 +198,25 @@ struct rx_global {
   const uint8_t *s;
   __device__ __forceinline__ uint32_t operator()(uint64_t p) const { return ld32(s + p); }
 };
-// The staged stretch alone: a read outside it sets `out` (and reads word 0)
-// and the caller parses that record again from global memory.  Keeping the
-// two apart matters: one reader choosing between LDS and global per read
-// compiles to flat loads, which take the vector memory path for LDS too.
+// The fast path (rxs_*) parses in 32-bit offsets from the start of its
+// staged stretch: rx_lds reads the stretch alone -- a read outside it sets
+// `out` (and reads word 0) and the caller parses that record again with
+// rx_goff, from global memory.  Keeping the two apart matters: one reader
+// choosing between LDS and global per read compiles to flat loads, which
+// take the vector memory path for LDS too.
 struct rx_lds {
-  const uint32_t *w;  // LDS: stream bytes [lo, lo + nb)
-  uint64_t lo;
+  const uint32_t *w;  // LDS: the stretch's first nb bytes
   uint32_t nb;
   mutable bool out;
-  __device__ __forceinline__ uint32_t operator()(uint64_t p) const {
-    uint64_t d = p - lo;
+  __device__ __forceinline__ uint32_t operator()(uint32_t p) const {
+    uint32_t d = p;
     if (d >= nb) { out = true; d = 0; }
     return w[d >> 2];
   }
+};
+struct rx_goff {
+  const uint8_t *b;  // the stretch's start in global memory
+  __device__ __forceinline__ uint32_t operator()(uint32_t p) const { return ld32(b + p); }
 };
 
 // ---------------------------------- speculative record index (fast path)
@@ -221,11 +226,11 @@ struct rx_lds {
 // checking every guess exactly:
 //   rxs_walk   one wave per kRxsSeg-byte segment, staged in LDS with the
 //              kRxsBack bytes before it and kRxsAhead after.  Lane j takes
-//              kRxsSub bytes, lanes 0-3 the look-back: its guess is the
+//              kRxsSub bytes, the first lanes the look-back: its guess is the
 //              first word from which a chain of record parses runs past the
 //              lane's end.  The lanes then agree from lane 0 on (each
 //              re-walks from its predecessor's exit until no exit changes),
-//              so the chain enters the segment proper (lane 4) from a guess
+//              so the chain enters the segment proper (lane kRoot) from a guess
 //              a kilobyte before it, by then usually the true chain: its
 //              first node there is the segment's entry E.  The segment's
 //              lanes count their nodes and write them out (segment-relative
@@ -237,24 +242,29 @@ struct rx_lds {
 //              from it on are the segment's records.  (A record that spans
 //              a whole segment passes only when the guess agrees.)
 //   (scan)     exclusive scan of those counts (launch_block_scan).
-//   rxs_final  the last exit is the stream's end and the chain holds
-//              exactly n records: then offsets[n] and the count, and the
-//              flag says so; else the flag sends the batch down the list
-//              ranking (whose kernels skip themselves otherwise).
-//   rxs_emit   offsets[] from the node lists.
+//   rxs_emit   when the last exit is the stream's end and the chain holds
+//              exactly n records: offsets[] from the node lists, offsets[n]
+//              and the count, and the flag says so; else the flag sends the
+//              batch down the list ranking.
 // Any stream the fast path does not take (a damaged one, trailing records,
 // a record longer than the window, a guess that missed) therefore gets the
 // list ranking's exact answer; tests/test_record_index.py checks both on
 // the same streams.
-// 63 words per lane: lane j's stretch starts at LDS bank -j (mod 32), so
-// the lanes' reads at like offsets hit 32 different banks (ds_read_b32
+// 63 words per lane would start lane j's stretch at LDS bank -j (mod 32),
+// so the lanes' reads at like offsets hit 32 different banks (ds_read_b32
 // banks by (a/4) mod 32 over each half-wave; with 64 words per lane every
-// lane of a half-wave would read the same bank, a 32-way conflict)
-constexpr uint32_t kRxsSub = 252;                        // bytes per lane
-constexpr uint32_t kRxsBack = 4 * kRxsSub;               // look-back: lanes 0-3
-constexpr uint32_t kRxsSeg = 64 * kRxsSub - kRxsBack;    // bytes per segment (one wave): lanes 4-63
-constexpr uint32_t kRxsAhead = 17u * 1024 - 64 * kRxsSub;  // staged past the segment (1280)
-constexpr uint64_t kRxsBroken = ~0ull, kRxsNone = ~0ull - 1;
+// lane of a half-wave reads the same bank, a 32-way conflict, measured).
+// 31 words per lane does the same (31j = -j mod 32), and its 9 KiB stretch
+// per wave lets 17 waves share a CU's LDS (latency hiding for the walks,
+// which are chains of dependent LDS reads) where 63 words (17 KiB) let 9
+constexpr uint32_t kRxsSub = 124;                         // bytes per lane
+constexpr uint32_t kRxsBackLanes = 8;                     // look-back: lanes 0-7 (992 bytes)
+constexpr uint32_t kRxsBack = kRxsBackLanes * kRxsSub;
+constexpr uint32_t kRxsSeg = 64 * kRxsSub - kRxsBack;     // bytes per segment (one wave): lanes 8-63
+constexpr uint32_t kRxsAhead = 9u * 1024 - 64 * kRxsSub;  // staged past the segment (1280)
+constexpr uint64_t kRxsBroken = ~0ull;
+// in the walk (32-bit offsets into the stretch): a broken chain, no state
+constexpr uint32_t kBrk = 0xffffffffu, kNone = 0xfffffffeu;
 // segment record: entry E (rxs_check: the index of its first true node),
 // exit, node count (kRxsBroken: the chain broke), nodes from the true entry
 constexpr uint32_t kRxsSegWords = 4;
@@ -263,52 +273,37 @@ constexpr uint32_t kRxsSegWords = 4;
 // when the record reaches past it.
 template <class P>
 __device__ __forceinline__ uint32_t rxs_rlen(const P &parser, const uint32_t *smem, const rx_lds &st,
-                                             const uint8_t *s, uint64_t len, uint32_t maxlen, uint64_t q) {
+                                             const uint8_t *base, uint32_t lenr, uint32_t maxlen, uint32_t q) {
   st.out = false;
-  const uint32_t L = parser.rlen_rd(smem, st, len, q, maxlen);
+  const uint32_t L = parser.rlen_rd(smem, st, lenr, q, maxlen);
   if (!st.out) return L;
-  return parser.rlen_rd(smem, rx_global{s}, len, q, maxlen);
+  return parser.rlen_rd(smem, rx_goff{base}, lenr, q, maxlen);
 }
 
-// Chain of record parses from q until it reaches b: the position reached,
-// or kRxsBroken.
-template <class P>
-__device__ __forceinline__ uint64_t rxs_chain(const P &parser, const uint32_t *smem, const rx_lds &st,
-                                              const uint8_t *s, uint64_t len, uint32_t maxlen, uint64_t q,
-                                              uint64_t b) {
-  while (q < b) {
-    const uint32_t L = rxs_rlen(parser, smem, st, s, len, maxlen, q);
-    if (L >= RX_LONG) return kRxsBroken;
-    q += L;
-  }
-  return q;
-}
-
-// The nodes a walk passes, kept for the node list: the first kRxsKeep as
-// segment-relative words (meaningful at or past s0), and how many there were
-// (more than kRxsKeep: the list is walked again).
-constexpr uint32_t kRxsKeep = 4;
+// The nodes a walk passes, kept for the node list: the first kRxsKeep (as
+// stretch offsets) and how many there were (more: the list is walked again).
+constexpr uint32_t kRxsKeep = 6;
 struct rxs_nodes {
   uint32_t n = 0;
   uint32_t w[kRxsKeep];
-  __device__ __forceinline__ void add(uint64_t q, uint64_t s0) {
-    const uint32_t v = static_cast<uint32_t>((q - s0) >> 2);
+  __device__ __forceinline__ void add(uint32_t q) {
 #pragma unroll
-    for (uint32_t i = 0; i < kRxsKeep; ++i) w[i] = n == i ? v : w[i];
+    for (uint32_t i = 0; i < kRxsKeep; ++i) w[i] = n == i ? q : w[i];
     ++n;
   }
 };
 
-// rxs_chain, noting the nodes
+// Chain of record parses from q until it reaches b, noting its nodes: the
+// position reached, or kBrk.
 template <class P>
-__device__ __forceinline__ uint64_t rxs_chain_n(const P &parser, const uint32_t *smem, const rx_lds &st,
-                                                const uint8_t *s, uint64_t len, uint32_t maxlen, uint64_t q,
-                                                uint64_t b, uint64_t s0, rxs_nodes &nd) {
+__device__ __forceinline__ uint32_t rxs_chain(const P &parser, const uint32_t *smem, const rx_lds &st,
+                                              const uint8_t *base, uint32_t lenr, uint32_t maxlen, uint32_t q,
+                                              uint32_t b, rxs_nodes &nd) {
   nd.n = 0;
   while (q < b) {
-    nd.add(q, s0);
-    const uint32_t L = rxs_rlen(parser, smem, st, s, len, maxlen, q);
-    if (L >= RX_LONG) return kRxsBroken;
+    nd.add(q);
+    const uint32_t L = rxs_rlen(parser, smem, st, base, lenr, maxlen, q);
+    if (L >= RX_LONG) return kBrk;
     q += L;
   }
   return q;
@@ -330,15 +325,19 @@ __device__ __forceinline__ void rxs_walk_body(const P &parser, const uint8_t *__
   __shared__ __attribute__((aligned(16))) uint32_t stg[kStg / 4];
   extern __shared__ __attribute__((aligned(16))) uint32_t rx_smem[];
   const uint32_t lane = threadIdx.x;
-  const uint64_t s0 = static_cast<uint64_t>(blockIdx.x) * kRxsSeg;
-  const uint64_t s1 = min(len, s0 + kRxsSeg);
-  const uint64_t lo = s0 >= kRxsBack ? s0 - kRxsBack : 0;
   XDRG_XSTAMP(0);
+  const uint64_t s0 = static_cast<uint64_t>(blockIdx.x) * kRxsSeg;
+  const uint64_t lo = s0 >= kRxsBack ? s0 - kRxsBack : 0;
+  const uint8_t *base = s + lo;
+  // offsets from lo from here on (a record parse never looks past
+  // maxlen, so the clamp changes nothing)
+  const uint32_t lenr = static_cast<uint32_t>(min(len - lo, 0x7fffffffull));
+  const uint32_t r0 = static_cast<uint32_t>(s0 - lo), r1 = static_cast<uint32_t>(min(len, s0 + kRxsSeg) - lo);
   if (blockIdx.x == 0 && lane == 0) *flag = 1u;  // rxs_check clears it on a miss
   parser.init(rx_smem);
   // stage [lo, lo + kStg) within the stream: all of a lane's 16-byte loads
   // in flight before its stores
-  const uint32_t nb = static_cast<uint32_t>((len - lo < kStg ? len - lo : uint64_t(kStg)) & ~3ull);
+  const uint32_t nb = min(lenr, kStg) & ~3u;
   {
     constexpr int U = kStg / 1024;
     u32x4 t[U];
@@ -346,11 +345,11 @@ __device__ __forceinline__ void rxs_walk_body(const P &parser, const uint8_t *__
     for (int k = 0; k < U; ++k) {
       const uint32_t o = 16u * lane + 1024u * k;
       if (o + 16 <= nb) {
-        t[k] = ld16u(s + lo + o);
+        t[k] = ld16u(base + o);
       } else {
         uint32_t w[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) w[j] = o + 4 * j + 4 <= nb ? ld32(s + lo + o + 4 * j) : 0u;
+        for (int j = 0; j < 4; ++j) w[j] = o + 4 * j + 4 <= nb ? ld32(base + o + 4 * j) : 0u;
         t[k] = u32x4{w[0], w[1], w[2], w[3]};
       }
     }
@@ -359,69 +358,94 @@ __device__ __forceinline__ void rxs_walk_body(const P &parser, const uint8_t *__
   }
   wave_sync();
   XDRG_XSTAMP(1);
-  const rx_lds st{stg, lo, nb, false};
+  const rx_lds st{stg, nb, false};
   // lane j: [a, b); lanes below kRoot cover the look-back (none in the
   // first segment, whose chain starts at byte 0: lane kRoot is its root)
   const bool first = s0 == 0;
   const uint32_t root = first ? kRoot : 0;
-  const uint64_t a = s0 + static_cast<uint64_t>(kRxsSub) * lane - kRxsBack;  // (wraps below 0: inactive)
-  const uint64_t b = min(a + kRxsSub, s1);
-  const bool act = lane >= root && a < s1;
+  const uint32_t a = r0 + kRxsSub * lane - kRxsBack;  // (wraps for the first segment's look-back: inactive)
+  const uint32_t b = min(a + kRxsSub, r1);
+  const bool act = lane >= root && a < r1;
   // the lane's guess: g (its chain's first node), e (where it leaves the
   // lane), nd (its nodes)
-  uint64_t g = kRxsNone, e = kRxsNone;
+  uint32_t g = kNone, e = kNone;
   rxs_nodes nd;
   if (act && first && lane == root) {
     g = 0;
-    e = rxs_chain_n(parser, rx_smem, st, s, len, maxlen, 0, b, s0, nd);
+    e = rxs_chain(parser, rx_smem, st, base, lenr, maxlen, 0, b, nd);
   } else if (act) {
-    // the first checked word of every word of the lane: all 63 LDS reads
-    // issued before the tests (one round trip per 15, not one per word)
-    uint32_t fw[kRxsSub / 4];
-    const uint64_t f0 = a + fd - lo;
+    // candidates: the lane's words (before b, with a first checked word
+    // inside the stream) whose first checked word passes; the lane's LDS reads
+    // are issued before the tests (one round trip per 15, not per word)
+    const uint32_t nk = (b - a + 3) / 4;
+    const uint32_t nf = a + fd + 4 <= lenr ? (lenr - a - fd - 4) / 4 + 1 : 0u;
+    const uint32_t nv = min(nk, nf);
+    const uint64_t vmask = nv >= 64 ? ~0ull : (1ull << nv) - 1;
+    uint64_t mask = vmask;
+    if (has_first && fd <= 1024) {  // (fd > 1024: every word is a candidate)
+      const uint32_t i0 = (a + fd) >> 2;  // + kRxsSub / 4 stays inside stg for fd <= 1024
+      uint32_t fw[kRxsSub / 4];
 #pragma unroll
-    for (uint32_t k = 0; k < kRxsSub / 4; ++k) {
-      const uint64_t f = f0 + 4 * k;
-      fw[k] = stg[(f < nb ? f : 0) >> 2];
-    }
-    uint64_t mask = 0;  // (63 bits)
+      for (uint32_t k = 0; k < kRxsSub / 4; ++k) fw[k] = stg[i0 + k];
+      uint64_t m = 0;
 #pragma unroll
-    for (uint32_t k = 0; k < kRxsSub / 4; ++k) {
-      const uint64_t p = a + 4 * k, f = f0 + 4 * k;
-      bool cand = p < b;
-      if (has_first) cand = cand && p + fd + 4 <= len && (f >= nb || parser.first_ok(rx_smem, bswap32(fw[k])));
-      mask |= static_cast<uint64_t>(cand) << k;
+      for (uint32_t k = 0; k < kRxsSub / 4; ++k)
+        m |= static_cast<uint64_t>(parser.first_ok(rx_smem, bswap32(fw[k]))) << k;
+      // words whose first checked word is past the staged stretch stay candidates
+      const uint32_t ns = a + fd < nb ? (nb - a - fd) / 4 : 0u;
+      if (ns < 64) m |= ~0ull << ns;
+      mask &= m;
     }
     while (mask) {
       const uint32_t k = __builtin_ctzll(mask);
       mask &= mask - 1;
-      const uint64_t p = a + 4 * k;
-      const uint64_t q = rxs_chain_n(parser, rx_smem, st, s, len, maxlen, p, b, s0, nd);
-      if (q != kRxsBroken) { g = p; e = q; break; }
+      const uint32_t p = a + 4 * k;
+      const uint32_t q = rxs_chain(parser, rx_smem, st, base, lenr, maxlen, p, b, nd);
+      if (q != kBrk) { g = p; e = q; break; }
     }
-    if (g == kRxsNone) nd.n = 0;
-    if (g == kRxsNone && (lane == root || lane < kRoot)) e = kRxsBroken;  // no chain from here
+    if (g == kNone) nd.n = 0;
   }
+  if (lane == root && g == kNone) e = kBrk;  // a root without a chain
   XDRG_XSTAMP(2);
-  const uint64_t g0 = g, e0 = e;
-  uint64_t pin = g;  // the entry the lane's state follows from
+  // Agree from the root on.  A lane without a guess is transparent: no
+  // word of it starts a chain that leaves it, so the chain either passes
+  // over it (an entry at or past its end) or breaks there.  Every other
+  // lane takes its entry from the nearest such lane before it (through the
+  // transparent ones) and re-walks from it when it is not its guess; lanes
+  // are final in order, one lane with a state per round.  In the look-back
+  // a chain that breaks gives way to the lane's own guess (a wrong guess
+  // upstream must not sink the segment); in the segment proper it breaks
+  // the segment.
+  const bool stateful = act && (g != kNone || lane == root);
+  const uint64_t smask = __ballot(stateful);
+  const uint64_t below = smask & ((1ull << lane) - 1);
+  const uint32_t src = below ? 63u - static_cast<uint32_t>(__builtin_clzll(below)) : lane;
+  const uint32_t g0 = g, e0 = e;
+  uint32_t pin = g;  // the entry the lane's state follows from
+  auto entry = [&](uint32_t pe) { return pe == kBrk || pe < a ? kBrk : pe; };
   for (int it = 0; it < 64; ++it) {
-    const uint64_t pe = __shfl_up(static_cast<unsigned long long>(e), 1, 64);
+    const uint32_t pe = entry(__shfl(e, src, 64));
     bool ch = false;
-    if (lane > root && pe != kRxsNone && pe != pin) {
+    if (stateful && lane > root && pe != pin) {
       ch = true;
       pin = g = pe;
       nd.n = 0;
-      e = pe == kRxsBroken || !act || pe >= b ? pe : rxs_chain_n(parser, rx_smem, st, s, len, maxlen, pe, b, s0, nd);
-      if (e == kRxsBroken && lane < kRoot) { g = g0; e = e0; }  // (its nodes are not the segment's)
+      e = pe == kBrk || pe >= b ? pe : rxs_chain(parser, rx_smem, st, base, lenr, maxlen, pe, b, nd);
+      if (e == kBrk && lane < kRoot && g0 != kNone) { g = g0; e = e0; }  // (its nodes are not the segment's)
     }
     if (!__any(ch)) break;
   }
-  // the segment's nodes: the lanes' chains from g while inside the lane (the
-  // look-back lanes' nodes belong to the segment before), noted by the walk
-  // that set the lane's state; a lane with more than kRxsKeep walks again
+  const uint32_t pt = entry(__shfl(e, src, 64));
+  if (act && !stateful) {  // a transparent lane passes the chain over or breaks it
+    g = pt;
+    e = g == kBrk || g < b ? kBrk : g;
+    nd.n = 0;
+  }
   XDRG_XSTAMP(3);
-  const bool live = act && lane >= kRoot && e != kRxsBroken;
+  // the segment's nodes, noted by the walk that set each lane's state (the
+  // look-back lanes' nodes belong to the segment before); a lane with more
+  // than kRxsKeep walks again
+  const bool live = act && lane >= kRoot && e != kBrk;
   const uint32_t c = live ? nd.n : 0u;
   XDRG_XSTAMP(4);
   const uint32_t incl = wave_incl_scan(c);
@@ -429,24 +453,46 @@ __device__ __forceinline__ void rxs_walk_body(const P &parser, const uint8_t *__
   if (live) {
 #pragma unroll
     for (uint32_t i = 0; i < kRxsKeep; ++i)
-      if (i < c) out[i] = static_cast<uint16_t>(nd.w[i]);
+      if (i < c) out[i] = static_cast<uint16_t>((nd.w[i] - r0) >> 2);
     if (c > kRxsKeep) {
-      uint64_t q = g;
+      uint32_t q = g;
       for (uint32_t k = 0; k < c; ++k) {
-        if (k >= kRxsKeep) out[k] = static_cast<uint16_t>((q - s0) >> 2);
-        q += rxs_rlen(parser, rx_smem, st, s, len, maxlen, q);
+        if (k >= kRxsKeep) out[k] = static_cast<uint16_t>((q - r0) >> 2);
+        q += rxs_rlen(parser, rx_smem, st, base, lenr, maxlen, q);
       }
     }
   }
   XDRG_XSTAMP(5);
-  // E: the chain's first node at or past s0 = what lane kRoot starts from
-  const uint64_t x = rl64(e, 63), E = rl64(g, kRoot), eR = rl64(e, kRoot);
+  // the segment's exit: the last active lane's; E: the chain's first node
+  // at or past s0 = lane kRoot's entry
+  const uint64_t amask = __ballot(act);
+  const uint32_t last = 63u - static_cast<uint32_t>(__builtin_clzll(amask));
+  const uint32_t x = __shfl(e, last, 64), E = __shfl(g, kRoot, 64), eR = __shfl(e, kRoot, 64);
   if (lane == 0) {
     uint64_t *r = seg + static_cast<uint64_t>(blockIdx.x) * kRxsSegWords;
-    r[0] = eR == kRxsBroken ? kRxsBroken : E;
-    r[1] = x;
-    r[2] = x == kRxsBroken ? kRxsBroken : rl32(incl, 63);
+    r[0] = eR == kBrk || E == kBrk ? kRxsBroken : lo + E;
+    r[1] = x == kBrk ? kRxsBroken : lo + x;
+    r[2] = x == kBrk ? kRxsBroken : rl32(incl, 63);
   }
+}
+
+// The true entry among segment i's nodes (nodes ascend: binary search): its
+// index, or kRxsBroken when the segment's chain does not hold it.
+__device__ __forceinline__ uint64_t rxs_entry(uint64_t i, uint64_t E, uint64_t C, uint64_t prev, uint64_t len,
+                                              const uint16_t *__restrict__ nodes) {
+  if (C == kRxsBroken || prev == kRxsBroken) return kRxsBroken;
+  if (E == prev) return 0;
+  // the chain entered before the true entry: it holds it if it merged
+  const uint64_t s0 = i * kRxsSeg;
+  if (!(E < prev && prev < min(len, s0 + kRxsSeg))) return kRxsBroken;
+  const uint16_t *nd = nodes + i * (kRxsSeg / 4);
+  const uint32_t w = static_cast<uint32_t>((prev - s0) >> 2);
+  uint64_t lo = 0, hi = C;
+  while (lo < hi) {
+    const uint64_t m = (lo + hi) >> 1;
+    if (nd[m] < w) lo = m + 1; else hi = m;
+  }
+  return lo < C && nd[lo] == w ? lo : kRxsBroken;
 }
 
 // One thread per segment: the true entry among the segment's nodes.
@@ -457,50 +503,30 @@ __device__ __forceinline__ void rxs_check_body(uint64_t *__restrict__ seg, const
   const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= nseg) return;
   uint64_t *r = seg + i * kRxsSegWords;
-  const uint64_t E = r[0], C = r[2], prev = i == 0 ? 0 : seg[(i - 1) * kRxsSegWords + 1];
-  const uint64_t s0 = i * kRxsSeg;
-  bool ok = C != kRxsBroken && prev != kRxsBroken;
-  uint64_t k = 0;  // index of the true entry among the segment's nodes
-  if (ok && E != prev) {
-    // the chain entered before the true entry: it holds it if it merged
-    ok = false;
-    if (E < prev && prev < min(len, s0 + kRxsSeg)) {
-      const uint16_t *nd = nodes + i * (kRxsSeg / 4);
-      const uint32_t w = static_cast<uint32_t>((prev - s0) >> 2);
-      uint64_t lo = 0, hi = C;  // nodes ascend: binary search
-      while (lo < hi) {
-        const uint64_t m = (lo + hi) >> 1;
-        if (nd[m] < w) lo = m + 1; else hi = m;
-      }
-      ok = lo < C && nd[lo] == w;
-      k = lo;
-    }
-  }
-  if (i == nseg - 1) ok = ok && r[1] == len;
-  r[0] = k;
+  const uint64_t C = r[2], k = rxs_entry(i, r[0], C, i == 0 ? 0 : seg[(i - 1) * kRxsSegWords + 1], len, nodes);
+  const bool ok = k != kRxsBroken && (i != nseg - 1 || r[1] == len);
+  r[0] = ok ? k : 0;
   cnt[i] = ok ? C - k : 0;
   if (!ok) *flag = 0u;
 }
 
-// One thread: the count and offsets[n] when every check held and the chain
-// holds exactly n records; the flag otherwise.
-__device__ __forceinline__ void rxs_final_body(const xdrg_status *__restrict__ tot, uint64_t len, uint64_t n,
-                                               uint64_t *__restrict__ offsets, uint64_t *__restrict__ count,
-                                               uint32_t *__restrict__ flag) {
-  if (threadIdx.x || blockIdx.x) return;
-  const bool all = *flag == 1u && tot->total_bytes == n;
-  *flag = all ? 1u : 0u;
-  if (all) {
-    offsets[n] = len;
-    *count = n;
-  }
-}
-
-// One wave per segment: its records' offsets.
+// One wave per segment: its records' offsets, when every check held (the
+// flag) and the chain holds exactly n records (the scan's total); the
+// first wave also writes offsets[n], the count and the final flag.
 __device__ __forceinline__ void rxs_emit_body(const uint64_t *__restrict__ seg, const uint16_t *__restrict__ nodes,
                                               const unsigned long long *__restrict__ base,
-                                              const uint32_t *__restrict__ flag, uint64_t *__restrict__ offsets) {
-  if (*flag != 1u) return;
+                                              const xdrg_status *__restrict__ tot, uint64_t len, uint64_t n,
+                                              uint64_t *__restrict__ offsets, uint64_t *__restrict__ count,
+                                              uint32_t *__restrict__ flag) {
+  const bool all = *flag == 1u && tot->total_bytes == n;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    *flag = all ? 1u : 0u;
+    if (all) {
+      offsets[n] = len;
+      *count = n;
+    }
+  }
+  if (!all) return;
   const uint64_t *r = seg + static_cast<uint64_t>(blockIdx.x) * kRxsSegWords;
   const uint64_t k = r[0], c = r[2] - k, b0 = base[blockIdx.x], s0 = static_cast<uint64_t>(blockIdx.x) * kRxsSeg;
   const uint16_t *in = nodes + static_cast<uint64_t>(blockIdx.x) * (kRxsSeg / 4) + k;

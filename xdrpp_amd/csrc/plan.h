@@ -108,6 +108,7 @@ struct plan_opts {
   int grp_nontemporal = 0; // group kernel: non-temporal stores
   int specialize = 1;      // var plans: plan-specialized kernels (spec.cpp) when built
   int index_fast = 1;      // record index: speculative chain walk before the list ranking
+                           // (1: the host waits for its flag; 2: asynchronous; 0: off)
 };
 
 }  // namespace xdrg

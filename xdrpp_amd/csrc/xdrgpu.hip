@@ -1047,16 +1047,17 @@ __device__ __forceinline__ uint32_t ix_mark(uint32_t raw, uint64_t w, uint64_t l
 // occupancy it costs outweighing L2-hit latency.)  The fast path
 // (rxs_walk_body) stages its segment: its walks are serial chains.
 
-template <class RD>
+// U: the position type (uint32_t for offsets into a staged stretch).
+template <class RD, class U = uint64_t>
 __device__ uint32_t rx_len(const xdrg_op *__restrict__ ops, const uint32_t *__restrict__ table,
-                           const RD &rd, uint64_t len, uint64_t a, uint32_t maxlen) {
-  const bool capped = a + maxlen < len;
-  const uint64_t lim = capped ? a + maxlen : len;
+                           const RD &rd, U len, U a, uint32_t maxlen) {
+  const bool capped = static_cast<uint64_t>(a) + maxlen < len;
+  const U lim = capped ? static_cast<U>(a + maxlen) : len;
   const uint32_t past = capped ? RX_LONG : RX_BAD;
   struct frame { uint32_t left, entry, ret; };
   frame st[XDRG_SUB_FRAMES];
   uint32_t fp = 0, pc = 0;
-  uint64_t p = a;
+  U p = a;
   for (;;) {
     const xdrg_op &op = ops[pc];
     switch (op.kind) {
@@ -1092,7 +1093,7 @@ __device__ uint32_t rx_len(const xdrg_op *__restrict__ ops, const uint32_t *__re
     case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING:
       if (v > op.arg0) return RX_BAD;
       if (lim - p < v) return past;
-      p += (static_cast<uint64_t>(v) + 3u) & ~3ull;
+      p += static_cast<U>((static_cast<uint64_t>(v) + 3u) & ~3ull);
       ++pc;
       break;
     case XDRG_OP_UNION: {
@@ -1106,8 +1107,8 @@ __device__ uint32_t rx_len(const xdrg_op *__restrict__ ops, const uint32_t *__re
       if (v > op.arg0) return RX_BAD;
       if (!(op.flags & XDRG_F_SUB)) {
         const uint64_t b = static_cast<uint64_t>(v) * op.arg3;
-        if (lim - p < b) return past;
-        p += b;
+        if (static_cast<uint64_t>(lim - p) < b) return past;
+        p += static_cast<U>(b);
         pc += 1 + op.arg2;
       } else if (!v) {
         ++pc;
@@ -1162,10 +1163,10 @@ struct rx_interp {
                                            uint32_t maxlen) const {
     return rx_len(reinterpret_cast<const xdrg_op *>(smem), rp.table, rx_global{s}, len, a, maxlen);
   }
-  template <class RD>
-  __device__ __forceinline__ uint32_t rlen_rd(const uint32_t *smem, const RD &rd, uint64_t len, uint64_t a,
+  template <class RD, class U>
+  __device__ __forceinline__ uint32_t rlen_rd(const uint32_t *smem, const RD &rd, U len, U a,
                                               uint32_t maxlen) const {
-    return rx_len(reinterpret_cast<const xdrg_op *>(smem), rp.table, rd, len, a, maxlen);
+    return rx_len<RD, U>(reinterpret_cast<const xdrg_op *>(smem), rp.table, rd, len, a, maxlen);
   }
 };
 
@@ -1195,16 +1196,13 @@ __global__ __launch_bounds__(256) void k_rxs_check(uint64_t *__restrict__ seg, c
                                                    uint32_t *__restrict__ flag) {
   rxs_check_body(seg, nodes, nseg, len, cnt, flag);
 }
-__global__ __launch_bounds__(64) void k_rxs_final(const xdrg_status *__restrict__ tot, uint64_t len, uint64_t n,
-                                                  uint64_t *__restrict__ offsets, uint64_t *__restrict__ count,
-                                                  uint32_t *__restrict__ flag) {
-  rxs_final_body(tot, len, n, offsets, count, flag);
-}
 __global__ __launch_bounds__(64) void k_rxs_emit(const uint64_t *__restrict__ seg,
                                                  const uint16_t *__restrict__ nodes,
                                                  const unsigned long long *__restrict__ base,
-                                                 const uint32_t *__restrict__ flag, uint64_t *__restrict__ offsets) {
-  rxs_emit_body(seg, nodes, base, flag, offsets);
+                                                 const xdrg_status *__restrict__ tot, uint64_t len, uint64_t n,
+                                                 uint64_t *__restrict__ offsets, uint64_t *__restrict__ count,
+                                                 uint32_t *__restrict__ flag) {
+  rxs_emit_body(seg, nodes, base, tot, len, n, offsets, count, flag);
 }
 
 // One node of the next level per workgroup: F children composed for
@@ -2073,6 +2071,12 @@ ix_layout ix_plan(uint64_t len, uint32_t maxlen) {
   return L;
 }
 
+bool plan_has_union(const xdrg_plan &p) {
+  for (const xdrg_op &o : p.ops)
+    if (o.kind == XDRG_OP_UNION) return true;
+  return false;
+}
+
 // Heap bytes a decode needs; plans without payload or element fields need
 // none when decoding messages (the decoded records hold no heap refs).
 bool plan_has_payload(const xdrg_plan &p) { return p.max_var_slots > 0 || p.has_vector; }
@@ -2231,7 +2235,11 @@ int run_index(const xdrg_plan *p, const dev_tables *T, const void *d_stream, uin
   // the list ranking below runs only when its checks fail.  Short streams
   // (a few segments) go to the list ranking alone.
   const uint32_t *skip = nullptr;
-  if (REC && p->opts.index_fast && !C.next && len >= 4ull * kRxsSeg && max_msgs > 0) {
+  // (the interpreted parse serves the walk only for plans without unions
+  // and element subroutines: their divergent op loops make the walk slower
+  // than the list ranking, measured)
+  const bool walk_ok = REC && ((SM && SM->f_rxs_walk) || (!p->has_sub && !plan_has_union(*p)));
+  if (walk_ok && p->opts.index_fast && !C.next && len >= 4ull * kRxsSeg && max_msgs > 0) {
     uint64_t *seg = reinterpret_cast<uint64_t *>(ws + L.rxs_seg);
     auto *cnt = reinterpret_cast<unsigned long long *>(ws + L.rxs_cnt);
     auto *base = reinterpret_cast<unsigned long long *>(ws + L.rxs_base);
@@ -2251,11 +2259,18 @@ int run_index(const xdrg_plan *p, const dev_tables *T, const void *d_stream, uin
     k_rxs_check<<<(ns + 255) / 256, 256, 0, s>>>(seg, nodes, L.rxs_nseg, len, cnt, flag);
     HIPCHK(hipGetLastError());
     if (int rc = launch_block_scan(cnt, base, ns, tot, nullptr, 0, s)) return rc;
-    k_rxs_final<<<1, 64, 0, s>>>(tot, len, max_msgs, d_offsets, d_count, flag);
+    k_rxs_emit<<<ns, 64, 0, s>>>(seg, nodes, base, tot, len, max_msgs, d_offsets, d_count, flag);
     HIPCHK(hipGetLastError());
-    k_rxs_emit<<<ns, 64, 0, s>>>(seg, nodes, base, flag, d_offsets);
-    HIPCHK(hipGetLastError());
-    skip = flag;
+    if (p->opts.index_fast == 1) {
+      // wait for the flag: the list ranking is launched only when a check
+      // failed (its ~11 launches would otherwise cost ~45 us of skipping)
+      uint32_t h = 0;
+      HIPCHK(hipMemcpyAsync(&h, flag, sizeof h, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      if (h == 1u) return XDRG_OK;
+    } else {
+      skip = flag;  // asynchronous: the list ranking's kernels skip themselves
+    }
   }
   if (SM && SM->f_ix_seg) {
     uint64_t *t0 = L.top > 0 ? tab(0) : nullptr;
@@ -2403,7 +2418,9 @@ int xdrg_plan_set_option(xdrg_plan *p, int option, int64_t value) {
     O.grp_blocks = v; return XDRG_OK;
   case XDRG_OPT_GRP_NONTEMPORAL: O.grp_nontemporal = v ? 1 : 0; return XDRG_OK;
   case XDRG_OPT_SPECIALIZE: O.specialize = v ? 1 : 0; return XDRG_OK;
-  case XDRG_OPT_INDEX_FAST: O.index_fast = v ? 1 : 0; return XDRG_OK;
+  case XDRG_OPT_INDEX_FAST:
+    if (v < 0 || v > 2) return XDRG_EINVAL;
+    O.index_fast = static_cast<int>(v); return XDRG_OK;
   default: return XDRG_EINVAL;
   }
 }
