@@ -23,8 +23,7 @@ for name in (sys.argv[1].split(',') if len(sys.argv) > 1 else ['recvar', 'rpc', 
     enc = M.Marshaler(M.Plan(S.ALL[name]), dev).encode(nat, n, heap)
     mar_dec = M.Marshaler(M.Plan(S.ALL[name]), dev)
     dt_dec, _ = timed(lambda: mar_dec.decode(enc.xdr, n, enc.offsets))
-    for label, opts in (('fast', {"index_fast": 1}), ('list', {"index_fast": 0}),
-                        ('fast-interp', {"index_fast": 1, "specialize": 0})):
+    for label, opts in (('fast', {"index_fast": 1}), ('list', {"index_fast": 0})):
         mar = M.Marshaler(M.Plan(S.ALL[name], opts), dev)
         dt, offs = timed(lambda: mar.index_records(enc.xdr, n))
         print(name, label, 'bytes', enc.xdr.numel(), 'index_ms %.3f' % (dt * 1e3),

@@ -1163,11 +1163,6 @@ struct rx_interp {
                                            uint32_t maxlen) const {
     return rx_len(reinterpret_cast<const xdrg_op *>(smem), rp.table, rx_global{s}, len, a, maxlen);
   }
-  template <class RD, class U>
-  __device__ __forceinline__ uint32_t rlen_rd(const uint32_t *smem, const RD &rd, U len, U a,
-                                              uint32_t maxlen) const {
-    return rx_len<RD, U>(reinterpret_cast<const xdrg_op *>(smem), rp.table, rd, len, a, maxlen);
-  }
 };
 
 // skip (record index): 1 when the fast path (rxs_*) holds the index; the
@@ -1185,12 +1180,8 @@ __global__ __launch_bounds__(256) void k_ix_seg(const uint8_t *__restrict__ s, u
   ix_seg_body<REC>(rx_interp{rp}, s, len, maxlen, K, tab, list, lcount, rp.fpc != RX_BAD, rp.fd);
 }
 
-// The fast path's kernels (index_kernels.h) with the interpreted parse.
-__global__ __launch_bounds__(64) void k_rxs_walk(const uint8_t *__restrict__ s, uint64_t len, uint32_t maxlen,
-                                                 uint64_t *__restrict__ seg, uint16_t *__restrict__ nodes,
-                                                 uint32_t *__restrict__ flag, rx_plan rp) {
-  rxs_walk_body(rx_interp{rp}, s, len, maxlen, seg, nodes, flag, rp.fpc != RX_BAD, rp.fd);
-}
+// The fast path's scan-side kernels (index_kernels.h); its walk is the
+// plan's generated xdrg_spec_rxs_walk.
 __global__ __launch_bounds__(256) void k_rxs_check(uint64_t *__restrict__ seg, const uint16_t *__restrict__ nodes,
                                                    uint64_t nseg, uint64_t len, unsigned long long *__restrict__ cnt,
                                                    uint32_t *__restrict__ flag) {
@@ -2071,12 +2062,6 @@ ix_layout ix_plan(uint64_t len, uint32_t maxlen) {
   return L;
 }
 
-bool plan_has_union(const xdrg_plan &p) {
-  for (const xdrg_op &o : p.ops)
-    if (o.kind == XDRG_OP_UNION) return true;
-  return false;
-}
-
 // Heap bytes a decode needs; plans without payload or element fields need
 // none when decoding messages (the decoded records hold no heap refs).
 bool plan_has_payload(const xdrg_plan &p) { return p.max_var_slots > 0 || p.has_vector; }
@@ -2235,10 +2220,11 @@ int run_index(const xdrg_plan *p, const dev_tables *T, const void *d_stream, uin
   // the list ranking below runs only when its checks fail.  Short streams
   // (a few segments) go to the list ranking alone.
   const uint32_t *skip = nullptr;
-  // (the interpreted parse serves the walk only for plans without unions
-  // and element subroutines: their divergent op loops make the walk slower
-  // than the list ranking, measured)
-  const bool walk_ok = REC && ((SM && SM->f_rxs_walk) || (!p->has_sub && !plan_has_union(*p)));
+  // (with the plan's generated parse: the interpreted one makes the walk
+  // slower than the list ranking -- rpc 0.65 vs 0.45 ms, vecrec 0.79 vs
+  // 0.25, its op loop and frame stack on every candidate -- so a plan
+  // without specialized kernels takes the list ranking)
+  const bool walk_ok = REC && SM && SM->f_rxs_walk;
   if (walk_ok && p->opts.index_fast && !C.next && len >= 4ull * kRxsSeg && max_msgs > 0) {
     uint64_t *seg = reinterpret_cast<uint64_t *>(ws + L.rxs_seg);
     auto *cnt = reinterpret_cast<unsigned long long *>(ws + L.rxs_cnt);
@@ -2247,14 +2233,11 @@ int run_index(const xdrg_plan *p, const dev_tables *T, const void *d_stream, uin
     uint32_t *flag = reinterpret_cast<uint32_t *>(ws + L.rxs_flag);
     uint16_t *nodes = reinterpret_cast<uint16_t *>(vlist);  // the list ranking's lists, unused when it skips
     const uint32_t ns = static_cast<uint32_t>(L.rxs_nseg);
-    if (SM && SM->f_rxs_walk) {
+    {
       uint32_t ml = max_msg_len, hf = rp.fpc != RX_BAD, fd = rp.fd;
       void *args[] = {&s8, &len, &ml, &seg, &nodes, &flag, &hf, &fd};
       HIPCHK(hipModuleLaunchKernel(static_cast<hipFunction_t>(SM->f_rxs_walk), ns, 1, 1, 64, 1, 1, 0, s, args,
                                    nullptr));
-    } else {
-      k_rxs_walk<<<ns, 64, ops_lds, s>>>(s8, len, max_msg_len, seg, nodes, flag, rp);
-      HIPCHK(hipGetLastError());
     }
     k_rxs_check<<<(ns + 255) / 256, 256, 0, s>>>(seg, nodes, L.rxs_nseg, len, cnt, flag);
     HIPCHK(hipGetLastError());
