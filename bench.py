@@ -70,6 +70,9 @@ def parse():
     ap.add_argument("--rpc", action="store_true",
                     help="also time the RPC header batch (xdrg_rpc_dispatch routing of 1M "
                          "record-marked calls + xdrg_rpc_replies error replies)")
+    ap.add_argument("--no-plain", action="store_true",
+                    help="var schemas: skip the plain-stream leg (the record index xdr_from_opaque "
+                         "needs without offsets, xdrg_index_records)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--event-every", type=int, default=4,
                     help="HIP events around the kernels of every E-th timed step (1: every step)")
@@ -535,6 +538,54 @@ def messages_leg(schema, plan, mar, nat, heap, n, reps=20):
     return res
 
 
+def plain_stream_leg(schema, engine, dec_ms, reps=10):
+    """xdr_from_opaque of a plain concatenated stream (marshal.h:299-306):
+    the record index the decode needs when no offsets came with the bytes
+    (xdrg_index_records), timed with HIP events around the call -- the
+    speculative walk, whose verdict the host waits for (the gap counts), and
+    beside it the list ranking alone (XDRG_OPT_INDEX_FAST = 0) -- then the
+    decode it feeds.  The offsets must equal the encoder's."""
+    dev = engine.nat.device
+    stream = torch.cuda.current_stream()
+    s = stream.cuda_stream
+    xdr, want, n = engine.xdr, engine.offsets, engine.n
+    L = A.lib()
+    res = {}
+    for label, fast in (("index", 1), ("index_list_ranking", 0)):
+        plan = M.Plan(S.ALL[schema], {"index_fast": fast})
+        mar = M.Marshaler(plan, dev)
+        maxlen = min(plan.max_record_bytes, A.INDEX_MAX_MSG)
+        total = xdr.numel()
+        ws = torch.empty(max(L.xdrg_index_workspace_size(total, maxlen), 16), dtype=torch.uint8, device=dev)
+        offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        cnt = torch.empty(1, dtype=torch.int64, device=dev)
+        mar.status.init(s)
+
+        def run():
+            A.check(L.xdrg_index_records(plan.handle, xdr.data_ptr(), total, n, maxlen, offs.data_ptr(),
+                                         cnt.data_ptr(), ws.data_ptr(), ws.numel(), mar.status.ptr, s),
+                    "xdrg_index_records")
+        run()
+        torch.cuda.synchronize()
+        t = []
+        for _ in range(reps):
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            ev[0].record(stream)
+            run()
+            ev[1].record(stream)
+            torch.cuda.synchronize()
+            t.append(ev[0].elapsed_time(ev[1]))
+        ok = mar.status.read(s).code == 0 and int(cnt.item()) == n and bool(torch.equal(offs, want))
+        res[label + "_ms"] = round(float(np.mean(t)), 4)
+        res[label + "_ok"] = ok
+        if fast:
+            res["walk_held"] = int(ws[-256:][:4].cpu().numpy().view(np.uint32)[0]) == 1
+    res["decode_ms"] = dec_ms
+    res["index_over_decode"] = round(res["index_ms"] / dec_ms, 3)
+    res["protocol"] = f"HIP events around each xdrg_index_records call, mean of {reps}; decode: the headline's"
+    return res
+
+
 def rpc_leg(dev, n=1 << 20, reps=20):
     """RPC header batches: xdrg_rpc_dispatch over n
     record-marked CALL messages (workloads.rpc_calls: mixed routes and
@@ -931,6 +982,11 @@ def extra_legs(args, engine, line, alg_bytes):
     if (args.cold or headline) and not args.no_cold and plan.is_fixed:
         line["cold_cache"] = cold_cache(mar, nat, engine.xdr, engine.back, n, alg_bytes)
         engine.check()
+    if not plan.is_fixed and not args.no_plain:
+        try:
+            line["plain_stream"] = plain_stream_leg(args.schema, engine, line["decode_ms"])
+        except Exception as e:  # reported, never fatal
+            line["plain_stream"] = {"error": str(e)[:200]}
     if args.msgs:
         line["messages"] = messages_leg(args.schema, plan, mar, nat, heap, n)
     if args.rpc:
