@@ -151,6 +151,9 @@ def test_plan_options_are_per_plan_and_validated():
     assert L.xdrg_plan_set_option(p.handle, A.PLAN_OPTIONS["var_encode_kernel"], 2) == -1
     assert L.xdrg_plan_set_option(p.handle, A.PLAN_OPTIONS["enc_unroll"], 5) == -1
     assert L.xdrg_plan_set_option(p.handle, A.PLAN_OPTIONS["enc_unroll"], 16) == A.OK
+    for v in (0, 1, 2):  # record index: list ranking / host-gated walk / asynchronous walk
+        assert L.xdrg_plan_set_option(p.handle, A.PLAN_OPTIONS["index_fast"], v) == A.OK
+    assert L.xdrg_plan_set_option(p.handle, A.PLAN_OPTIONS["index_fast"], 3) == -1
     with pytest.raises(A.AbiError):
         M.Plan(S.recvar, {"var_decode_kernel": 7})
 
