@@ -180,6 +180,33 @@ def test_index_framing_vs_oracle(dev, case):
     check_index(x, dev, maxlen)
 
 
+@pytest.mark.parametrize("sizes", ["mixed", "zero", "max"])
+def test_index_walk_holds(dev, sizes):
+    """Well-framed streams of several segments: the speculative walk over the
+    marks (index_kernels.h mark_rx) holds the index itself -- its flag, the
+    first u32 of the workspace's last 256 bytes -- and equals the oracle's;
+    every word a mark (zero-length messages) and maximal messages included."""
+    rng = np.random.default_rng(11)
+    maxlen = 1024
+    sz = {"mixed": list(rng.integers(0, 257, 6000) * 4), "zero": [0] * 40000, "max": [maxlen] * 400}[sizes]
+    x = _messages(sz)
+    want = O.index_msgs(x, maxlen, None)
+    L = A.lib()
+    t = to_dev(x, dev)
+    ws = torch.empty(L.xdrg_index_workspace_size(x.size, maxlen), dtype=torch.uint8, device=dev)
+    offs = torch.empty(len(sz) + 1, dtype=torch.int64, device=dev)
+    cnt = torch.empty(1, dtype=torch.int64, device=dev)
+    st = M.Status(dev)
+    s = torch.cuda.current_stream().cuda_stream
+    st.init(s)
+    A.check(L.xdrg_index_msgs(t.data_ptr(), x.size, maxlen, len(sz), offs.data_ptr(), cnt.data_ptr(),
+                              ws.data_ptr(), ws.numel(), st.ptr, s), "xdrg_index_msgs")
+    assert st.read(s).code == 0 and want[0] == 0
+    assert int(cnt.item()) == want[1] == len(sz)
+    assert np.array_equal(offs.cpu().numpy().view(np.uint64), want[2])
+    assert int(ws[-256:][:4].cpu().numpy().view(np.uint32)[0]) == 1
+
+
 @pytest.mark.parametrize("maxlen", [252, 1000, 8000])
 def test_index_window_sizes(dev, maxlen):
     """Entry windows K = maxlen/4 + 1 across the level-kernel variants

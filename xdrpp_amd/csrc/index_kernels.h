@@ -309,6 +309,29 @@ __device__ __forceinline__ uint32_t rxs_chain(const P &parser, const uint32_t *s
   return q;
 }
 
+// The "parse" of a record mark (RFC 5531) for the walk over a message
+// stream (xdrg_index_msgs): a mark whose message read_message takes
+// (srpc.cc:29-55: the pre-swap size test, the last-fragment bit, a size
+// within maxmsglen_ and the stream, a multiple of 4 for xdr_from_msg) is a
+// record of 4 + size bytes; anything else ends the chain, and the list
+// ranking then classifies it as read_message would (ix_mark).
+struct mark_rx {
+  uint32_t maxlen;
+  __device__ __forceinline__ void init(uint32_t *) const {}
+  __device__ __forceinline__ bool first_ok(const uint32_t *, uint32_t v) const {
+    const uint32_t size = v & ~XDRG_MARK_LAST;
+    return !((v >> 24) & 3u) && (v & XDRG_MARK_LAST) && size <= maxlen && !(size & 3u);
+  }
+  template <class RD, class U>
+  __device__ __forceinline__ uint32_t rlen_rd(const uint32_t *, const RD &rd, U len, U a, uint32_t) const {
+    if (len - a < 4) return RX_BAD;
+    const uint32_t raw = rd(a);
+    const uint32_t v = bswap32(raw), size = v & ~XDRG_MARK_LAST;
+    if ((raw & 3u) || !(v & XDRG_MARK_LAST) || size > maxlen || (size & 3u) || len - a - 4 < size) return RX_BAD;
+    return 4u + size;
+  }
+};
+
 // Phase timestamps for tools/tune/ix_stamps.py, which compiles a copy of a
 // plan's generated source with this defined; nothing in the library does.
 #ifndef XDRG_XSTAMP
@@ -421,17 +444,28 @@ __device__ __forceinline__ void rxs_walk_body(const P &parser, const uint8_t *__
   const uint64_t below = smask & ((1ull << lane) - 1);
   const uint32_t src = below ? 63u - static_cast<uint32_t>(__builtin_clzll(below)) : lane;
   const uint32_t g0 = g, e0 = e;
+  const rxs_nodes nd0 = nd;
   uint32_t pin = g;  // the entry the lane's state follows from
   auto entry = [&](uint32_t pe) { return pe == kBrk || pe < a ? kBrk : pe; };
+  const uint64_t below_seg = ((1ull << lane) - 1) & ~((1ull << kRoot) - 1);  // lanes [kRoot, lane)
   for (int it = 0; it < 64; ++it) {
     const uint32_t pe = entry(__shfl(e, src, 64));
+    // a broken chain gives way to the lane's own guess in the look-back, and
+    // in the segment proper until the segment's chain has started (a message
+    // or record longer than the look-back can leave it without a chain); the
+    // node list stays one chain, and rxs_check decides whether it is the true one
+    const uint64_t livem = __ballot(stateful && lane >= kRoot && e != kBrk && e != kNone);
     bool ch = false;
     if (stateful && lane > root && pe != pin) {
       ch = true;
       pin = g = pe;
       nd.n = 0;
       e = pe == kBrk || pe >= b ? pe : rxs_chain(parser, rx_smem, st, base, lenr, maxlen, pe, b, nd);
-      if (e == kBrk && lane < kRoot && g0 != kNone) { g = g0; e = e0; }  // (its nodes are not the segment's)
+      if (e == kBrk && g0 != kNone && (lane < kRoot || !(livem & below_seg))) {
+        g = g0;
+        e = e0;
+        nd = nd0;
+      }
     }
     if (!__any(ch)) break;
   }
@@ -464,13 +498,16 @@ __device__ __forceinline__ void rxs_walk_body(const P &parser, const uint8_t *__
   }
   XDRG_XSTAMP(5);
   // the segment's exit: the last active lane's; E: the chain's first node
-  // at or past s0 = lane kRoot's entry
+  // at or past s0 = the entry of the first lane of the segment proper with
+  // a live state
   const uint64_t amask = __ballot(act);
   const uint32_t last = 63u - static_cast<uint32_t>(__builtin_clzll(amask));
-  const uint32_t x = __shfl(e, last, 64), E = __shfl(g, kRoot, 64), eR = __shfl(e, kRoot, 64);
+  const uint64_t livef = __ballot(act && lane >= kRoot && e != kBrk && e != kNone);
+  const uint32_t fl = livef ? static_cast<uint32_t>(__builtin_ctzll(livef)) : kRoot;
+  const uint32_t x = __shfl(e, last, 64), E = __shfl(g, fl, 64);
   if (lane == 0) {
     uint64_t *r = seg + static_cast<uint64_t>(blockIdx.x) * kRxsSegWords;
-    r[0] = eR == kBrk || E == kBrk ? kRxsBroken : lo + E;
+    r[0] = !livef || E == kBrk ? kRxsBroken : lo + E;
     r[1] = x == kBrk ? kRxsBroken : lo + x;
     r[2] = x == kBrk ? kRxsBroken : rl32(incl, 63);
   }
@@ -511,19 +548,23 @@ __device__ __forceinline__ void rxs_check_body(uint64_t *__restrict__ seg, const
 }
 
 // One wave per segment: its records' offsets, when every check held (the
-// flag) and the chain holds exactly n records (the scan's total); the
-// first wave also writes offsets[n], the count and the final flag.
+// flag) and the chain holds exactly n records (EXACT: records of
+// xdrg_index_records) or at most n (messages of xdrg_index_msgs, n = the
+// capacity) -- the scan's total; the first wave also writes offsets[total],
+// the count and the final flag.
+template <bool EXACT>
 __device__ __forceinline__ void rxs_emit_body(const uint64_t *__restrict__ seg, const uint16_t *__restrict__ nodes,
                                               const unsigned long long *__restrict__ base,
                                               const xdrg_status *__restrict__ tot, uint64_t len, uint64_t n,
                                               uint64_t *__restrict__ offsets, uint64_t *__restrict__ count,
                                               uint32_t *__restrict__ flag) {
-  const bool all = *flag == 1u && tot->total_bytes == n;
+  const uint64_t t = tot->total_bytes;
+  const bool all = *flag == 1u && (EXACT ? t == n : t <= n);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     *flag = all ? 1u : 0u;
     if (all) {
-      offsets[n] = len;
-      *count = n;
+      offsets[t] = len;
+      *count = t;
     }
   }
   if (!all) return;

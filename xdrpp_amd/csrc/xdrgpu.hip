@@ -1187,13 +1187,20 @@ __global__ __launch_bounds__(256) void k_rxs_check(uint64_t *__restrict__ seg, c
                                                    uint32_t *__restrict__ flag) {
   rxs_check_body(seg, nodes, nseg, len, cnt, flag);
 }
+template <bool EXACT>
 __global__ __launch_bounds__(64) void k_rxs_emit(const uint64_t *__restrict__ seg,
                                                  const uint16_t *__restrict__ nodes,
                                                  const unsigned long long *__restrict__ base,
                                                  const xdrg_status *__restrict__ tot, uint64_t len, uint64_t n,
                                                  uint64_t *__restrict__ offsets, uint64_t *__restrict__ count,
                                                  uint32_t *__restrict__ flag) {
-  rxs_emit_body(seg, nodes, base, tot, len, n, offsets, count, flag);
+  rxs_emit_body<EXACT>(seg, nodes, base, tot, len, n, offsets, count, flag);
+}
+// The walk over a message stream's record marks (xdrg_index_msgs).
+__global__ __launch_bounds__(64) void k_rxs_walk_msgs(const uint8_t *__restrict__ s, uint64_t len,
+                                                      uint32_t maxlen, uint64_t *__restrict__ seg,
+                                                      uint16_t *__restrict__ nodes, uint32_t *__restrict__ flag) {
+  rxs_walk_body(mark_rx{maxlen}, s, len, maxlen, seg, nodes, flag, true, 0u);
 }
 
 // One node of the next level per workgroup: F children composed for
@@ -2224,8 +2231,10 @@ int run_index(const xdrg_plan *p, const dev_tables *T, const void *d_stream, uin
   // slower than the list ranking -- rpc 0.65 vs 0.45 ms, vecrec 0.79 vs
   // 0.25, its op loop and frame stack on every candidate -- so a plan
   // without specialized kernels takes the list ranking)
-  const bool walk_ok = REC && SM && SM->f_rxs_walk;
-  if (walk_ok && p->opts.index_fast && !C.next && len >= 4ull * kRxsSeg && max_msgs > 0) {
+  // Message streams walk their marks (mark_rx) always.
+  const bool walk_ok = REC ? SM && SM->f_rxs_walk && p->opts.index_fast : true;
+  const int gate = REC ? p->opts.index_fast : 1;
+  if (walk_ok && !C.next && len >= 4ull * kRxsSeg && max_msgs > 0) {
     uint64_t *seg = reinterpret_cast<uint64_t *>(ws + L.rxs_seg);
     auto *cnt = reinterpret_cast<unsigned long long *>(ws + L.rxs_cnt);
     auto *base = reinterpret_cast<unsigned long long *>(ws + L.rxs_base);
@@ -2233,18 +2242,21 @@ int run_index(const xdrg_plan *p, const dev_tables *T, const void *d_stream, uin
     uint32_t *flag = reinterpret_cast<uint32_t *>(ws + L.rxs_flag);
     uint16_t *nodes = reinterpret_cast<uint16_t *>(vlist);  // the list ranking's lists, unused when it skips
     const uint32_t ns = static_cast<uint32_t>(L.rxs_nseg);
-    {
+    if (REC) {
       uint32_t ml = max_msg_len, hf = rp.fpc != RX_BAD, fd = rp.fd;
       void *args[] = {&s8, &len, &ml, &seg, &nodes, &flag, &hf, &fd};
       HIPCHK(hipModuleLaunchKernel(static_cast<hipFunction_t>(SM->f_rxs_walk), ns, 1, 1, 64, 1, 1, 0, s, args,
                                    nullptr));
+    } else {
+      k_rxs_walk_msgs<<<ns, 64, 0, s>>>(s8, len, max_msg_len, seg, nodes, flag);
+      HIPCHK(hipGetLastError());
     }
     k_rxs_check<<<(ns + 255) / 256, 256, 0, s>>>(seg, nodes, L.rxs_nseg, len, cnt, flag);
     HIPCHK(hipGetLastError());
     if (int rc = launch_block_scan(cnt, base, ns, tot, nullptr, 0, s)) return rc;
-    k_rxs_emit<<<ns, 64, 0, s>>>(seg, nodes, base, tot, len, max_msgs, d_offsets, d_count, flag);
+    k_rxs_emit<REC><<<ns, 64, 0, s>>>(seg, nodes, base, tot, len, max_msgs, d_offsets, d_count, flag);
     HIPCHK(hipGetLastError());
-    if (p->opts.index_fast == 1) {
+    if (gate == 1) {
       // wait for the flag: the list ranking is launched only when a check
       // failed (its ~11 launches would otherwise cost ~45 us of skipping)
       uint32_t h = 0;
