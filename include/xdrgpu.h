@@ -473,10 +473,13 @@ int xdrg_decode_msgs(const xdrg_plan *plan, const void *d_stream, uint64_t len,
  * more is XDRG_ERR_MSG_COUNT at record max_msgs.  Entries past count are
  * unspecified.  Any max_msg_len up to XDRG_MAX_MSG: msg_sock's is 1 MiB by
  * default (msgsock.h:29), read_message has none.  Up to XDRG_INDEX_MAX_MSG
- * the call is one asynchronous list-ranking pass; past it the messages
- * longer than that are walked mark by mark on the device between
- * list-ranking windows over the rest, and the call waits on the stream
- * once or twice per window (every byte is read about twice at most).
+ * the marks are walked speculatively as for xdrg_index_records (the call
+ * waits once for the walk's verdict, except on a stream being captured)
+ * and a list-ranking pass runs when a check fails (a damaged stream, more
+ * than max_msgs messages); past it the messages longer than that are
+ * walked mark by mark on the device between list-ranking windows over the
+ * rest, and the call waits on the stream once or twice per window (every
+ * byte is read about twice at most).
  * Workspace: xdrg_index_workspace_size(len, max_msg_len).
  */
 int xdrg_index_msgs(const void *d_stream, uint64_t len, uint32_t max_msg_len,
@@ -499,7 +502,8 @@ size_t xdrg_index_workspace_size(uint64_t len, uint32_t max_msg_len);
  * 0 is ranked as for xdrg_index_msgs.  The first u32 of the workspace's
  * last 256 bytes says which ran (1: the speculative walk).  By default
  * (XDRG_OPT_INDEX_FAST) the call waits on the stream once, for the walk's
- * verdict.  Writes
+ * verdict (not on a stream being captured into a graph: there it stays
+ * asynchronous, as with XDRG_OPT_INDEX_FAST = 2).  Writes
  * d_offsets[0..n] for xdrg_decode: record r = [off[r], off[r+1]).  Where
  * the records stop parsing -- a bad discriminant, a length past its bound
  * or past the stream -- record k gets [off[k], len) and the rest [len, len),

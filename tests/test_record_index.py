@@ -270,3 +270,41 @@ def test_gpu_index_full_size(dev, name):
     a, ha = mar.decode(r.xdr, n, r.offsets)
     b, hb = mar.decode(r.xdr, n)
     assert torch.equal(a, b) and torch.equal(ha, hb)
+
+
+@pytest.mark.gpu
+def test_gpu_index_graph_capture(dev):
+    """xdrg_index_records captured into a graph (torch.cuda.graph over the
+    call's stream): the walk cannot wait for its verdict there, so it stays
+    asynchronous (the list ranking is captured too and skips itself), and a
+    replay indexes the stream."""
+    import torch
+    from xdrpp_amd import marshal as M
+    cp = compile_plan(S.recvar)
+    x, offs, n = tiled(*gold_stream("recvar"), 4)
+    mar = M.Marshaler(M.Plan(cp), dev)
+    L = A.lib()
+    maxlen = window(cp)
+    dx = _dev(x, dev)
+    ws = torch.empty(L.xdrg_index_workspace_size(x.size, maxlen), dtype=torch.uint8, device=dev)
+    out = torch.full((n + 1,), -1, dtype=torch.int64, device=dev)
+    cnt = torch.empty(1, dtype=torch.int64, device=dev)
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):  # warm: plan tables and kernels uploaded outside the capture
+        mar.status.init(side.cuda_stream)
+        A.check(L.xdrg_index_records(mar.plan.handle, dx.data_ptr(), x.size, n, maxlen, out.data_ptr(),
+                                     cnt.data_ptr(), ws.data_ptr(), ws.numel(), mar.status.ptr, side.cuda_stream),
+                "index (warm)")
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    out.fill_(-1)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        s = torch.cuda.current_stream().cuda_stream
+        A.check(L.xdrg_index_records(mar.plan.handle, dx.data_ptr(), x.size, n, maxlen, out.data_ptr(),
+                                     cnt.data_ptr(), ws.data_ptr(), ws.numel(), mar.status.ptr, s), "index (capture)")
+    g.replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint64), offs) and int(cnt.item()) == n
+    assert _fast_flag(ws[-256:].cpu().numpy()) == 1

@@ -2233,7 +2233,11 @@ int run_index(const xdrg_plan *p, const dev_tables *T, const void *d_stream, uin
   // without specialized kernels takes the list ranking)
   // Message streams walk their marks (mark_rx) always.
   const bool walk_ok = REC ? SM && SM->f_rxs_walk && p->opts.index_fast : true;
-  const int gate = REC ? p->opts.index_fast : 1;
+  int gate = REC ? p->opts.index_fast : 1;
+  if (gate == 1) {  // a stream being captured into a graph cannot be waited on: stay asynchronous
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) gate = 2;
+  }
   if (walk_ok && !C.next && len >= 4ull * kRxsSeg && max_msgs > 0) {
     uint64_t *seg = reinterpret_cast<uint64_t *>(ws + L.rxs_seg);
     auto *cnt = reinterpret_cast<unsigned long long *>(ws + L.rxs_cnt);
