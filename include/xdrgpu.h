@@ -411,9 +411,16 @@ int xdrg_decode(const xdrg_plan *plan, const void *d_xdr, uint64_t xdr_len,
 
 /* Heap capacity xdrg_decode needs for a stream of xdr_len bytes: xdr_len,
  * plus, for plans with xvector<T>/pointer<T> fields, an area for the
- * decoded element arrays.  Record i's element arrays are placed from byte
- * align16(xdr_len) + F * off[i] (F = 1 + the largest native/wire size ratio
- * of an element type, so no extra pass is needed), each 8-byte aligned. */
+ * decoded element arrays, F * xdr_len bytes from byte align16(xdr_len),
+ * every array 8-byte aligned.  F = 1 + the largest native/wire size ratio
+ * of an element type.  Plans whose containers all hold fixed-size elements
+ * pack the arrays of each group of 64 records (records 64g .. 64g+63) back
+ * to back from align8(align16(xdr_len) + F * off[64g]), record by record
+ * (a record's share is what its counts ask for, each array rounded up to
+ * 8 bytes), so the arrays leave as whole cache lines; F carries 2 more for
+ * that rounding.  Plans with element subroutines place record i's arrays
+ * from align16(xdr_len) + F * off[i] (F: the subroutine bound, + 2).  Only
+ * the xdrg_bytes_ref offsets say where an array is. */
 uint64_t xdrg_decode_heap_size(const xdrg_plan *plan, uint64_t xdr_len);
 
 /* ---------------------------------------------------------------------- */

@@ -105,10 +105,12 @@ static uint32_t vec_wire(const plan_t *P, uint32_t pc) {
   return w;
 }
 /* Decoded element arrays of record r come from [align16(len) + F * off[r],
- * align16(len) + F * off[r+1]).  Fixed elements: F = 1 + the largest
- * native/wire size ratio of an element type.  Subroutine elements: distinct
- * elements start at distinct wire words, so stride/4 per wire byte, plus 2
- * for the 8-byte alignment of each array (xdrpp_amd/csrc/plan.cpp). */
+ * align16(len) + F * off[r+1]) for plans with element subroutines, packed
+ * per group of 64 records otherwise (rec_ebytes below).  Fixed elements:
+ * F = 1 + the largest native/wire size ratio of an element type (+ 2 when
+ * packed).  Subroutine elements: distinct elements start at distinct wire
+ * words, so stride/4 per wire byte, plus 2 for the 8-byte alignment of each
+ * array (xdrpp_amd/csrc/plan.cpp). */
 /* Least wire bytes of the walk from each pc to its region's END (unions:
  * the cheapest arm; containers: empty), as plan.cpp computes them: an
  * element subroutine consumes at least minw[body] bytes per element. */
@@ -145,6 +147,19 @@ static uint64_t *min_wires(const xdrg_op *ops, uint32_t nops, const uint32_t *ta
   return m;
 }
 
+/* Plans whose containers all hold fixed-size elements (no element
+ * subroutine) pack each group of 64 records' arrays back to back (below);
+ * their factor carries 2 more bytes per wire byte for the 8-byte rounding
+ * of every array (xdrpp_amd/csrc/plan.cpp). */
+static int packed_plan(const plan_t *P) {
+  int vec = 0;
+  for (uint32_t pc = 0; pc < P->nops; ++pc)
+    if (P->ops[pc].kind == XDRG_OP_VECTOR) {
+      if (P->ops[pc].flags & XDRG_F_SUB) return 0;
+      vec = 1;
+    }
+  return vec;
+}
 static uint32_t heap_factor(const plan_t *P) {
   uint32_t f = 0;
   for (uint32_t pc = 0; pc < P->nops; ++pc)
@@ -159,7 +174,66 @@ static uint32_t heap_factor(const plan_t *P) {
       }
       if (g > f) f = g;
     }
-  return f;
+  return f && packed_plan(P) ? f + 2 : f;
+}
+
+/* Packed element areas.  Records go in groups of 64 (records 64g ..
+ * 64g+63 of the batch); group g's arrays start at align8(ebase + F *
+ * off[64g]) and follow each other record by record, each array rounded up
+ * to 8 bytes.  Record r's share is E(r): a walk of its structure (lengths,
+ * counts, discriminants; no value checks) adding align8(min(cnt, rem /
+ * wire + 1) * stride) per container, rem = the record's bytes after the
+ * count, stopping where the structure stops parsing -- what the decode's
+ * area check (elem_area_ok) needs, so valid records always fit -- capped at
+ * align8-down(F * (b - a) - 8) so that no group outgrows its F-sized area.
+ * The device kernels compute the same E(r) before their walks and place
+ * the group's records by a wave scan (xdrpp_amd/csrc: dec_ebytes,
+ * codegen.cpp ebytes). */
+static uint64_t rec_ebytes(const plan_t *P, const uint8_t *s, uint64_t p, uint64_t b) {
+  uint64_t E = 0;
+  uint32_t pc = 0;
+  for (;;) {
+    const xdrg_op *op = &P->ops[pc];
+    switch (op->kind) {
+    case XDRG_OP_END: return E;
+    case XDRG_OP_JUMP: pc = op->arg0; continue;
+    case XDRG_OP_U64: if (b - p < 8) return E; p += 8; ++pc; continue;
+    case XDRG_OP_OPAQUE: if (b - p < op->arg0) return E; p += pad4(op->arg0); ++pc; continue;
+    case XDRG_OP_U32: case XDRG_OP_BOOL: case XDRG_OP_ENUM: if (b - p < 4) return E; p += 4; ++pc; continue;
+    default: break;
+    }
+    if (b - p < 4) return E;
+    const uint32_t v = bswap32(rd32(s + p));
+    p += 4;
+    switch (op->kind) {
+    case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING:
+      if (v > op->arg0 || b - p < v) return E;
+      p += pad4(v);
+      ++pc;
+      break;
+    case XDRG_OP_UNION: {
+      const int64_t t = union_target(P, op, v);
+      if (t < 0) return E;
+      pc = (uint32_t)t;
+      break;
+    }
+    case XDRG_OP_VECTOR: {
+      if (v > op->arg0) return E;
+      const uint64_t w = vec_wire(P, pc), rem = b - p;
+      const uint64_t k = rem / w + 1 < v ? rem / w + 1 : v;
+      E += (k * op->arg1 + 7) & ~7ull;
+      if (rem < (uint64_t)v * w) return E;
+      p += (uint64_t)v * w;
+      pc += 1 + op->arg2;
+      break;
+    }
+    default: ++pc; break;
+    }
+  }
+}
+static uint64_t ebudget(uint32_t F, uint64_t a, uint64_t b) {
+  const uint64_t t = (uint64_t)F * (b - a);
+  return t >= 8 ? (t - 8) & ~7ull : 0;
 }
 uint64_t xdro_decode_heap_size(const xdrg_op *ops, uint32_t nops, uint64_t len) {
   plan_t P = {ops, nops, NULL, 0, NULL};
@@ -594,22 +668,40 @@ static int decode_batch(const plan_t *PP, const uint8_t *xdr, uint64_t len, cons
   if (!offsets) {
     if (len & 3) { *erec = 0; *eop = 0xffffffffu; return XDRG_ERR_SIZE_NOT_MULT4; }
     const uint8_t *p = xdr, *e = xdr + len;
+    const int packed = packed_plan(&P);
+    uint64_t cur = 0;
     for (uint64_t r = 0; r < n; ++r) {
-      int rc = dec_record(&P, &p, e, native + r * stride, xdr, heap_out,
-                          ebase + (uint64_t)F * (uint64_t)(p - xdr), ebase + (uint64_t)F * len,
-                          stack_limit, eop);
+      const uint64_t a = (uint64_t)(p - xdr);
+      uint64_t ec = ebase + (uint64_t)F * a, ee = ebase + (uint64_t)F * len;
+      if (packed) {  /* (the record's end is found by its walk: the stream's end bounds it) */
+        if (r % 64 == 0) cur = (ebase + (uint64_t)F * a + 7) & ~7ull;
+        const uint64_t E = rec_ebytes(&P, xdr, a, len), B = ebudget(F, a, len);
+        ec = cur;
+        ee = cur + (E < B ? E : B);
+        cur = ee;
+      }
+      int rc = dec_record(&P, &p, e, native + r * stride, xdr, heap_out, ec, ee, stack_limit, eop);
       if (rc) { *erec = r; return rc; }
     }
     if (p != e) { *erec = n; *eop = 0xffffffffu; return XDRG_ERR_TRAILING; }
     return 0;
   }
+  const int packed = packed_plan(&P);
+  uint64_t cur = 0;  /* packed: the group's bump */
   for (uint64_t r = 0; r < n; ++r) {
     uint64_t a = offsets[r], b = offsets[r + 1];
     if (b < a || b > len) { *erec = r; *eop = 0; return XDRG_ERR_OVERFLOW_GET; }
     if ((b - a) & 3) { *erec = r; *eop = 0xffffffffu; return XDRG_ERR_SIZE_NOT_MULT4; }
     const uint8_t *p = xdr + a, *e = xdr + b;
-    int rc = dec_record(&P, &p, e, native + r * stride, xdr, heap_out, ebase + (uint64_t)F * a,
-                        ebase + (uint64_t)F * b, stack_limit, eop);
+    uint64_t ec = ebase + (uint64_t)F * a, ee = ebase + (uint64_t)F * b;
+    if (packed) {
+      if (r % 64 == 0) cur = (ebase + (uint64_t)F * a + 7) & ~7ull;
+      const uint64_t E = rec_ebytes(&P, xdr, a, b), B = ebudget(F, a, b);
+      ec = cur;
+      ee = cur + (E < B ? E : B);
+      cur = ee;
+    }
+    int rc = dec_record(&P, &p, e, native + r * stride, xdr, heap_out, ec, ee, stack_limit, eop);
     if (rc) { *erec = r; return rc; }
     if (p != e) { *erec = r; *eop = 0xffffffffu; return XDRG_ERR_TRAILING; }
   }
@@ -684,6 +776,8 @@ static int decode_msgs_batch(const plan_t *PP, const uint8_t *xdr, uint64_t len,
   if (heap_out && len) memcpy(heap_out, xdr, len);
   const uint32_t F = heap_factor(&P);
   const uint64_t ebase = F ? ((len + 15) & ~15ull) : 0;
+  const int packed = packed_plan(&P);
+  uint64_t cur = 0;
   for (uint64_t r = 0; r < n; ++r) {
     uint64_t a = offsets[r], b = offsets[r + 1];
     if (b < a || b > len) { *erec = r; *eop = 0; return XDRG_ERR_OVERFLOW_GET; }
@@ -691,8 +785,15 @@ static int decode_msgs_batch(const plan_t *PP, const uint8_t *xdr, uint64_t len,
     if (c) { *erec = r; *eop = 0xffffffffu; return (int)c; }
     if ((b - a) & 3) { *erec = r; *eop = 0xffffffffu; return XDRG_ERR_SIZE_NOT_MULT4; }
     const uint8_t *p = xdr + a + 4, *e = xdr + b;
-    int rc = dec_record(&P, &p, e, native + r * stride, xdr, heap_out, ebase + (uint64_t)F * a,
-                        ebase + (uint64_t)F * b, stack_limit, eop);
+    uint64_t ec = ebase + (uint64_t)F * a, ee = ebase + (uint64_t)F * b;
+    if (packed) {
+      if (r % 64 == 0) cur = (ebase + (uint64_t)F * a + 7) & ~7ull;
+      const uint64_t E = rec_ebytes(&P, xdr, a + 4, b), B = ebudget(F, a, b);
+      ec = cur;
+      ee = cur + (E < B ? E : B);
+      cur = ee;
+    }
+    int rc = dec_record(&P, &p, e, native + r * stride, xdr, heap_out, ec, ee, stack_limit, eop);
     if (rc) { *erec = r; return rc; }
     if (p != e) { *erec = r; *eop = 0xffffffffu; return XDRG_ERR_TRAILING; }
   }

@@ -299,6 +299,64 @@ struct gen {
       ++pc;
     }
   }
+  // Packed element areas: the bytes a record's arrays take, each rounded up
+  // to 8 (oracle/xdr_oracle.c rec_ebytes, var_kernels.h packed_area) -- a
+  // walk of its lengths, counts and discriminants that stops (returns E)
+  // where the structure stops parsing.  Plans without element subroutines.
+  void eb_block(uint32_t pc, uint32_t stop) {
+    auto need = [&](const std::string &n) { line("if (b - q < " + n + ") return E;"); };
+    auto word = [&]() { need("4"); line("{ const uint32_t v = bswap32(rd(q)); q += 4;"); };
+    while (pc != stop) {
+      const xdrg_op &e = op(pc);
+      switch (e.kind) {
+      case XDRG_OP_END: return;
+      case XDRG_OP_JUMP: pc = e.arg0; continue;
+      case XDRG_OP_U64: need("8"); line("q += 8;"); break;
+      case XDRG_OP_OPAQUE: need(u32(e.arg0)); line("q += " + u32((e.arg0 + 3u) & ~3u) + ";"); break;
+      case XDRG_OP_U32: case XDRG_OP_BOOL: case XDRG_OP_ENUM: need("4"); line("q += 4;"); break;
+      case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING:
+        word();
+        line("  if (v > " + u32(e.arg0) + " || v > b - q) return E;");
+        line("  q += (static_cast<uint64_t>(v) + 3u) & ~3ull; }");
+        break;
+      case XDRG_OP_VECTOR:
+        word();
+        line("  if (v > " + u32(e.arg0) + ") return E;");
+        line("  const uint64_t left = b - q;");
+        line("  E += (min<uint64_t>(v, left / " + u32(e.arg3) + " + 1u) * " + u32(e.arg1) + " + 7u) & ~7ull;");
+        line("  if (left < static_cast<uint64_t>(v) * " + u32(e.arg3) + ") return E;");
+        line("  q += static_cast<uint64_t>(v) * " + u32(e.arg3) + "; }");
+        pc += 1 + e.arg2;
+        continue;
+      case XDRG_OP_UNION: {
+        const uint32_t end = ipdom[pc];
+        word();
+        line("  switch (v) {");
+        for (auto &a : arms(e)) {
+          std::string lab;
+          for (uint32_t v : a.second) lab += "case " + u32(v) + ": ";
+          line("  " + lab + "{");
+          ind += 2;
+          eb_block(a.first, end);
+          ind -= 2;
+          line("  } break;");
+        }
+        line("  default: {");
+        ind += 2;
+        if (e.flags & XDRG_F_DEFAULT) eb_block(e.arg4, end);
+        else line("return E;");
+        ind -= 2;
+        line("  } break;");
+        line("  }");
+        line("}");
+        pc = end;
+        continue;
+      }
+      default: break;
+      }
+      ++pc;
+    }
+  }
   // The first op whose word is checked (every op before it fixed-size, no
   // branch) and the test of that word: what the index loads for every
   // candidate start before parsing it (run_index in xdrgpu.hip finds the
@@ -937,6 +995,11 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
   g.rx_block(0, kNoPc);
   const std::string rx_code = g.o.str();
   const std::string first = g.first_test();
+  // element-area shares of packed plans
+  g.o.str("");
+  g.ind = 4;
+  if (p.packed) g.eb_block(0, kNoPc);
+  const std::string eb_code = g.o.str();
 
   const uint32_t maxd = g.maxd;  // deepest field: the stack budget a wave must have to skip the checks
   info.slots = std::max<uint32_t>(1, slots);
@@ -967,6 +1030,13 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
     << "  __device__ __forceinline__ bool dec(dec_ctx<RA> &c, uint8_t *nat, bool ok) const {\n"
     << "    if (!ok) return false;\n"
     << dec_code << "    return true;\n  }\n"
+    << "  __device__ __forceinline__ bool packed() const { return " << (p.packed ? "true" : "false") << "; }\n"
+    << "  template <class RD>\n"
+    << "  __device__ __forceinline__ uint64_t ebytes(RD &rd, uint64_t q, uint64_t b, bool on) const {\n"
+    << "    uint64_t E = 0;\n"
+    << "    if (!on) return E;\n"
+    << "    {\n" << eb_code << "    }\n"
+    << "    return E;\n  }\n"
     << "};\n\n"
     << "struct plan_rx {  // index_kernels.h ix_seg_body's and rxs_walk_body's parser\n"
     << "  __device__ __forceinline__ void init(uint32_t *) const {}\n"

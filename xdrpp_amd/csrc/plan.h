@@ -129,6 +129,7 @@ struct xdrg_plan {
   uint32_t max_slot_len = 0;      // var plans: largest opaque<>/string<> bound
   bool has_vector = false;        // xvector<T>/pointer<T> fields (XDRG_OP_VECTOR)
   bool has_sub = false;           // element subroutines (XDRG_F_SUB): the frame-walk kernels
+  bool packed = false;            // decoded element arrays packed per 64-record group (no F_SUB)
   bool deep = false;              // subroutines can nest past XDRG_SUB_FRAMES (recursive types):
                                   // the frame walks add their deep passes (sub_kernels.h)
   uint32_t heap_factor = 0;       // decode element-area factor (xdrg_decode_heap_size)

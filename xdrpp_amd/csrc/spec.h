@@ -16,7 +16,7 @@ constexpr int kSpecDevices = 64;
 // Interface version of the generated kernels (their parameter lists and
 // LDS layout, var_kernels.h): the source defines xdrg_spec_iface with it,
 // and a code object that carries another value is refused at load.
-constexpr unsigned kSpecIface = 7;
+constexpr unsigned kSpecIface = 8;
 
 // The generated source of a plan and the launch facts it fixes.
 struct spec_info {

@@ -99,6 +99,67 @@ __device__ __forceinline__ void load_ops(xdrg_op *sops, const xdrg_op *__restric
   __syncthreads();
 }
 
+// Packed element areas (oracle/xdr_oracle.c rec_ebytes): the bytes the
+// element arrays of the record at [p, b) take, each rounded up to 8 -- a
+// walk of its lengths, counts and discriminants (no value checks) that
+// stops where the structure stops parsing.  Jumps and arms go forward only,
+// so one wave-uniform sweep of the ops reaches every op a lane can reach
+// (interp_walk); every lane of the wave calls it, `on` or not.
+template <class RD>
+__device__ uint64_t ebytes_sweep(const xdrg_op *ops, uint32_t nops, const uint32_t *__restrict__ table,
+                                 RD &rd, uint64_t p, uint64_t b, bool on) {
+  constexpr uint32_t kDone = 0xffffffffu;
+  uint64_t E = 0;
+  uint32_t pc = on ? 0u : kDone;
+  for (uint32_t upc = 0; upc < nops; ++upc) {
+    if (!__any(pc == upc)) continue;
+    const xdrg_op op = load_op(ops, upc);
+    if (pc != upc) continue;
+    const uint64_t rem = b - p;
+    switch (op.kind) {
+    case XDRG_OP_END: pc = kDone; break;
+    case XDRG_OP_JUMP: pc = op.arg0; break;
+    case XDRG_OP_U64:
+      if (rem < 8) { pc = kDone; break; }
+      p += 8; ++pc; break;
+    case XDRG_OP_OPAQUE:
+      if (rem < op.arg0) { pc = kDone; break; }
+      p += (op.arg0 + 3u) & ~3u; ++pc; break;
+    case XDRG_OP_U32: case XDRG_OP_BOOL: case XDRG_OP_ENUM:
+      if (rem < 4) { pc = kDone; break; }
+      p += 4; ++pc; break;
+    case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
+      if (rem < 4) { pc = kDone; break; }
+      const uint32_t v = bswap32(rd(p));
+      p += 4;
+      if (v > op.arg0 || v > b - p) { pc = kDone; break; }
+      p += (static_cast<uint64_t>(v) + 3u) & ~3ull; ++pc; break;
+    }
+    case XDRG_OP_UNION: {
+      if (rem < 4) { pc = kDone; break; }
+      const int t = union_target(op, table, bswap32(rd(p)));
+      p += 4;
+      pc = t < 0 ? kDone : static_cast<uint32_t>(t);
+      break;
+    }
+    case XDRG_OP_VECTOR: {
+      if (rem < 4) { pc = kDone; break; }
+      const uint32_t v = bswap32(rd(p));
+      p += 4;
+      if (v > op.arg0) { pc = kDone; break; }
+      const uint64_t left = b - p, w = op.arg3;
+      E += (min<uint64_t>(v, left / w + 1) * op.arg1 + 7u) & ~7ull;
+      if (left < static_cast<uint64_t>(v) * w) { pc = kDone; break; }
+      p += static_cast<uint64_t>(v) * w;
+      pc += 1 + op.arg2;
+      break;
+    }
+    default: ++pc; break;
+    }
+  }
+  return E;
+}
+
 // ------------------------------------------- var: xvector<T> / pointer<T>
 // Elements of a VECTOR op (fixed-size element plans; ops [b0, b0+nb)).
 // Each element field checks the stack budget (the element's class level)
@@ -642,13 +703,22 @@ __global__ __launch_bounds__(256) void k_var_decode(
     const uint8_t *__restrict__ xdr, uint64_t len, const uint64_t *__restrict__ offsets, uint64_t n,
     uint8_t *__restrict__ native, uint32_t stride, const xdrg_op *__restrict__ ops, uint32_t nops,
     const uint32_t *__restrict__ table, uint32_t stack_limit, uint8_t *__restrict__ heap,
-    uint64_t ebase, uint32_t F, uint32_t mark, unsigned long long *err) {
+    uint64_t ebase, uint32_t F, uint32_t mark, uint32_t packed, unsigned long long *err) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   xdrg_op *sops = reinterpret_cast<xdrg_op *>(smem);
   load_ops(sops, ops, nops);
   const uint64_t r = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const uint64_t a = r < n ? offsets[r] : 0u, b = r < n ? offsets[r + 1] : 0u;
+  uint64_t ecur = ebase + static_cast<uint64_t>(F) * a;  // this record's element arrays
+  uint64_t eend = ebase + static_cast<uint64_t>(F) * b;
+  if (packed) {  // ... packed with its wave's (var_kernels.h packed_area)
+    const bool bad = r < n && (b < a || b > len);
+    const bool on = r < n && !bad && a + mark <= b;
+    auto rd = [&](uint64_t q) { return ld32(xdr + q); };
+    const uint64_t e = ebytes_sweep(sops, nops, table, rd, a + mark, b, on);
+    packed_area(on ? min(e, ebudget(F, a, b)) : 0u, bad, rl64(a, 0), ebase, F, ecur, eend);
+  }
   if (r >= n) return;
-  const uint64_t a = offsets[r], b = offsets[r + 1];
   if (r == n - 1 && b != len) report(err, n, kOpRecordLevel, XDRG_ERR_TRAILING);
   if (b < a || b > len) { report(err, r, 0, XDRG_ERR_OVERFLOW_GET); return; }
   if (mark) {  // xdr_from_msg: the message read_message framed (srpc.cc:29-55)
@@ -659,7 +729,6 @@ __global__ __launch_bounds__(256) void k_var_decode(
   uint8_t *nat = native + r * stride;
   for (uint32_t k = 0; k < stride / 4; ++k) st32(nat + 4 * k, 0u);
   uint64_t p = a + mark;
-  uint64_t ecur = ebase + static_cast<uint64_t>(F) * a;  // this record's element arrays
   uint32_t pc = 0;
   for (;;) {
     const xdrg_op &op = sops[pc];
@@ -738,7 +807,7 @@ __global__ __launch_bounds__(256) void k_var_decode(
         report(err, r, pc, (op.flags & XDRG_F_POINTER) ? XDRG_ERR_POINTER_BOUND : XDRG_ERR_XVECTOR_BOUND);
         return;
       }
-      if (!elem_area_ok(ecur, ebase + static_cast<uint64_t>(F) * b, cnt, op.arg1, op.arg3, b - p)) goto overflow;
+      if (!elem_area_ok(ecur, eend, cnt, op.arg1, op.arg3, b - p)) goto overflow;
       *reinterpret_cast<uint64_t *>(nat + op.noff) = ecur;
       st32(nat + op.noff + 8, cnt);
       auto rd = [&](uint64_t q) { return ld32(xdr + q); };
@@ -774,6 +843,13 @@ struct interp_walk {
   const xdrg_op *__restrict__ ops;
   uint32_t nops;
   const uint32_t *__restrict__ table;
+  bool pk = false;  // decode: packed element areas (var_kernels.h packed_area)
+
+  __device__ bool packed() const { return pk; }
+  template <class RD>
+  __device__ uint64_t ebytes(RD &rd, uint64_t p, uint64_t b, bool on) const {
+    return ebytes_sweep(ops, nops, table, rd, p, b, on);
+  }
 
   template <int KMAX>
   __device__ bool enc(enc_ctx<KMAX> &c, const uint8_t *nat, bool ok) const {
@@ -965,9 +1041,9 @@ __global__ __launch_bounds__(64) void k_var_decode_w(
     const uint8_t *__restrict__ xdr, uint64_t len, const uint64_t *__restrict__ offsets, uint64_t n,
     uint8_t *__restrict__ native, uint32_t stride, uint8_t *__restrict__ heap,
     const xdrg_op *__restrict__ ops, uint32_t nops, const uint32_t *__restrict__ table,
-    uint32_t stack_limit, uint32_t C, uint64_t ebase, uint32_t F, uint32_t mark,
+    uint32_t stack_limit, uint32_t C, uint64_t ebase, uint32_t F, uint32_t mark, uint32_t packed,
     unsigned long long *err) {
-  var_decode_body<interp_walk, COPY, RA>(interp_walk{ops, nops, table}, xdr, len, offsets, n, native,
+  var_decode_body<interp_walk, COPY, RA>(interp_walk{ops, nops, table, packed != 0}, xdr, len, offsets, n, native,
                                          stride, heap, stack_limit, C, ebase, F, mark, err);
 }
 
@@ -2162,7 +2238,7 @@ int var_decode(const xdrg_plan &P, const dev_tables &T, const void *d_xdr, uint6
 #define LAUNCH_DEC_W(CP, RA)                                                                      \
   k_var_decode_w<CP, RA><<<nb, 64, lw, s>>>(xdr8, len, d_offsets, n, nat8, p->stride, d_heap_out, \
                                             T.d_ops, nops, T.d_table, stack_limit, Cw, ebase,     \
-                                            p->heap_factor, mark, err)
+                                            p->heap_factor, mark, p->packed, err)
     if (copy) {
       if (O.dec_readahead) LAUNCH_DEC_W(true, true); else LAUNCH_DEC_W(true, false);
     } else {
@@ -2174,7 +2250,7 @@ int var_decode(const xdrg_plan &P, const dev_tables &T, const void *d_xdr, uint6
     const uint64_t nb = (n + 255) / 256;
     k_var_decode<<<nb, 256, p->ops.size() * sizeof(xdrg_op), s>>>(
         xdr8, len, d_offsets, n, nat8, p->stride, T.d_ops, nops, T.d_table, stack_limit,
-        d_heap_out, ebase, p->heap_factor, mark, err);
+        d_heap_out, ebase, p->heap_factor, mark, p->packed, err);
   }
   HIPCHK(hipGetLastError());
   return XDRG_OK;
