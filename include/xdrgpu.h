@@ -298,6 +298,10 @@ enum xdrg_plan_option {
   XDRG_OPT_SPECIALIZE = 12,       /* var plans: 1 (default) run the plan-specialized
                                      kernels (built by the first launch, or
                                      xdrg_plan_build_kernels); 0 the interpreter */
+  XDRG_OPT_STAGE_BYTES = 14,     /* window decode, plans with fixed-element
+                                     containers: LDS stage of a 64-record group's
+                                     element arrays (written out as whole lines
+                                     after the walk), -1 auto, 0 none           */
   XDRG_OPT_INDEX_FAST = 13        /* xdrg_index_records: 1 (default) the speculative
                                      chain walk first, then the call waits for its
                                      verdict and runs the list ranking only when a

@@ -156,6 +156,36 @@ def test_oracle_no_frame_bound():
     assert (e.value.code, e.value.record) == (A.ERR_STACK_GET, 2)
 
 
+@pytest.mark.parametrize("n", [1, 64, 200])
+def test_oracle_packed_element_areas(n):
+    """Fixed-element containers pack per group of 64 records (xdr_oracle.c
+    rec_ebytes; include/xdrgpu.h xdrg_decode_heap_size): the arrays follow
+    each other, 8-aligned, in record and field order from align8(ebase +
+    F * off[64g]), inside the group's F-sized area, and the values are
+    unchanged (the native records round-trip through the encoder)."""
+    from xdrpp_amd import workloads as W
+    cp = compile_plan(S.vecrec)
+    nat, heap = W.GENERATORS["vecrec"](n)
+    x, offs = O.encode(cp, nat, n, heap)
+    dn, dh = O.decode(cp, x, n, offs)
+    assert np.array_equal(O.encode(cp, dn, n, dh)[0], x)
+    vec = [int(o["noff"]) for o in cp.ops if o["kind"] == A.OP_VECTOR]
+    strides = [int(o["arg1"]) for o in cp.ops if o["kind"] == A.OP_VECTOR]
+    ebase = (x.size + 15) & ~15
+    F = (dh.size - ebase) // x.size
+    recs = dn.reshape(n, cp.stride)
+    for g in range(0, n, 64):
+        cur = (ebase + F * int(offs[g]) + 7) & ~7
+        end = ebase + F * int(offs[min(g + 64, n)])
+        for r in range(g, min(g + 64, n)):
+            for no, st in zip(vec, strides):
+                off = int(recs[r, no:no + 8].view(np.uint64)[0])
+                cnt = int(recs[r, no + 8:no + 12].view(np.uint32)[0])
+                assert off == cur
+                cur = (cur + cnt * st + 7) & ~7
+        assert cur <= end
+
+
 @pytest.mark.skipif(not os.path.exists(f"{REF}/xdrpp/marshal.cc"), reason="reference tree absent")
 def test_fixture_regenerates(tmp_path):
     """containers.json is what the reference produces today (empty diff)."""

@@ -17,6 +17,7 @@ pytestmark = pytest.mark.gpu
 
 from xdrpp_amd import _abi as A  # noqa: E402
 from xdrpp_amd import marshal as M  # noqa: E402
+from xdrpp_amd import objects as OB  # noqa: E402
 from xdrpp_amd import schemas as S  # noqa: E402
 from xdrpp_amd import workloads as W  # noqa: E402
 import oracle_bridge as O  # noqa: E402
@@ -366,15 +367,21 @@ def test_swaps(dev):
 
 
 # ------------------------------------- every var kernel, forced in turn
-KERNELS = {"per_lane": (1, 1, 0), "chunk_image_window": (3, 2, 0), "specialized": (0, 0, 1)}
+# (encode kernel, decode kernel, specialize, stage_bytes): the window decode
+# of plans with fixed-element containers (vecrec) stages a group's element
+# arrays in LDS when they fit (-1: the default 8 KiB), writes them straight
+# from the walk otherwise (0: never staged; 1024: some groups staged, some not)
+KERNELS = {"per_lane": (1, 1, 0, -1), "chunk_image_window": (3, 2, 0, -1), "window_mixed_stage": (3, 2, 0, 1024),
+           "specialized": (0, 0, 1, -1), "specialized_no_stage": (0, 0, 1, 0),
+           "specialized_mixed_stage": (0, 0, 1, 1024)}
 
 
 @pytest.fixture(params=list(KERNELS))
 def forced(request):
     """Plan options forcing one encode and one decode kernel: the plan
     interpreter's, or the plan-specialized ones (codegen.cpp + hiprtc)."""
-    enc, dec, spec = KERNELS[request.param]
-    return {"var_encode_kernel": enc, "var_decode_kernel": dec, "specialize": spec}
+    enc, dec, spec, stage = KERNELS[request.param]
+    return {"var_encode_kernel": enc, "var_decode_kernel": dec, "specialize": spec, "stage_bytes": stage}
 
 
 @pytest.mark.parametrize("name", ["recvar", "rpc", "vecrec"])
@@ -411,6 +418,38 @@ def test_var_kernels_fuzzed_errors(dev, forced, name, seed):
     want = _oracle_err(lambda: O.decode(p.cp, x, n, offs))
     got = _gpu_err(lambda: mar.decode(to_dev(x, dev), n, to_dev(offs.view(np.int64), dev)))
     assert got == want
+
+
+@pytest.mark.parametrize("bad", ["reversed", "past_end"])
+def test_var_kernels_bad_offsets(dev, forced, bad):
+    """Offsets the decode refuses (record 70: b < a, or b past the stream)
+    inside a group of packed element arrays: the oracle's error, the records
+    before it decoded identically, nothing written past the heap."""
+    n = 200
+    p = plan("vecrec", **forced)
+    mar = M.Marshaler(p, dev)
+    nat, heap = W.GENERATORS["vecrec"](n)
+    x, offs = O.encode(p.cp, nat, n, heap)
+    offs = offs.copy()
+    offs[71] = offs[70] - 8 if bad == "reversed" else x.size + 64
+    want = _oracle_err(lambda: O.decode(p.cp, x, n, offs))
+    assert want[:2] == (A.ERR_OVERFLOW_GET, 70)
+    H = p.decode_heap_bytes(x.size)
+    guard = 4096
+    hout = torch.full((H + guard,), 0xA5, dtype=torch.uint8, device=dev)
+    back = torch.zeros(n * p.stride, dtype=torch.uint8, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    mar.status.init(s)
+    mar.launch_decode(to_dev(x, dev), n, back, offsets=to_dev(offs.view(np.int64), dev), heap_out=hout[:H],
+                      stream=s)
+    assert _gpu_err(lambda: mar.check(s)) == want
+    assert bool((hout[H:] == 0xA5).all()), "decode wrote past its heap"
+    # records 0..69 hold what the oracle decodes from them alone (values:
+    # the element arrays' places depend on the batch's length)
+    o_nat, o_heap = O.decode(p.cp, x[:int(offs[70])], 70, offs[:71])
+    t = S.ALL["vecrec"]
+    assert OB.unstage(t, back.cpu().numpy()[:70 * p.stride], hout[:H].cpu().numpy(), 70) == \
+        OB.unstage(t, o_nat, o_heap, 70)
 
 
 @pytest.mark.parametrize("name", ["recvar", "rpc", "vecrec"])

@@ -1079,10 +1079,10 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
     s << "extern \"C\" __global__ __launch_bounds__(64) void xdrg_spec_decode" << (cp ? "_copy" : "") << "(\n"
       << "    const uint8_t *xdr, uint64_t len, const uint64_t *offsets, uint64_t n, uint8_t *native,\n"
       << "    uint32_t stride, uint8_t *heap, uint32_t stack_limit, uint32_t C, uint64_t ebase,\n"
-      << "    uint32_t F, uint32_t mark, unsigned long long *err) {\n"
+      << "    uint32_t F, uint32_t mark, uint32_t S, unsigned long long *err) {\n"
       << "  var_decode_body<plan_walk, " << (cp ? "true" : "false")
       << ", true, " << (regs ? p.stride / 4 : 0) << ">(plan_walk{}, xdr, len, offsets, n, native, stride, heap,\n"
-      << "      stack_limit, C, ebase, F, mark, err);\n}\n\n";
+      << "      stack_limit, C, ebase, F, mark, S, err);\n}\n\n";
   // the source's own hash, defined in it: spec_get refuses a code object
   // (kernel cache file, or one attached with xdrg_plan_load_kernels) that
   // was not compiled from this plan's source

@@ -109,6 +109,7 @@ struct plan_opts {
   int specialize = 1;      // var plans: plan-specialized kernels (spec.cpp) when built
   int index_fast = 1;      // record index: speculative chain walk before the list ranking
                            // (1: the host waits for its flag; 2: asynchronous; 0: off)
+  int stage_bytes = -1;    // window decode of packed plans: LDS stage of a group's arrays
 };
 
 }  // namespace xdrg

@@ -679,8 +679,8 @@ __device__ __forceinline__ void var_encode_body(
 // ---------------------------------------------------------------- decode
 // LDS of a decode wave: the native tile (none when the walk decodes into
 // registers, NWD > 0) and the window.
-__host__ __device__ inline uint32_t dec_w_lds(uint32_t stride, uint32_t C, bool regs = false) {
-  return (regs ? 0u : ((64u * stride + 15u) & ~15u)) + C + 32u;
+__host__ __device__ inline uint32_t dec_w_lds(uint32_t stride, uint32_t C, bool regs = false, uint32_t S = 0) {
+  return (regs ? 0u : ((64u * stride + 15u) & ~15u)) + C + 32u + S;
 }
 
 // Stream reader of a wave: the window for stream bytes in [ws, ws + wc),
@@ -787,8 +787,8 @@ __device__ __forceinline__ uint64_t ebudget(uint32_t F, uint64_t a, uint64_t b) 
   const uint64_t t = static_cast<uint64_t>(F) * (b - a);
   return t >= 8u ? (t - 8u) & ~7ull : 0u;
 }
-__device__ __forceinline__ void packed_area(uint64_t E, bool bad, uint64_t a0, uint64_t ebase, uint32_t F,
-                                            uint64_t &ecur, uint64_t &eend) {
+__device__ __forceinline__ uint64_t packed_area(uint64_t E, bool bad, uint64_t a0, uint64_t ebase, uint32_t F,
+                                                uint64_t &ecur, uint64_t &eend) {
   const uint32_t lane = __lane_id();
   const unsigned long long bm = __ballot(bad);
   if (bm & ((2ull << lane) - 1ull)) E = 0;  // a bad record at or before this one
@@ -800,6 +800,7 @@ __device__ __forceinline__ void packed_area(uint64_t E, bool bad, uint64_t a0, u
   const uint64_t g0 = (ebase + static_cast<uint64_t>(F) * a0 + 7u) & ~7ull;
   ecur = g0 + inc - E;
   eend = g0 + inc;
+  return g0;
 }
 
 // NWD > 0 (plan-specialized walks, whose native offsets are constants): the
@@ -809,13 +810,14 @@ template <class W, bool COPY, bool RA, int NWD = 0>
 __device__ __forceinline__ void var_decode_body(
     const W &w, const uint8_t *__restrict__ xdr, uint64_t len, const uint64_t *__restrict__ offsets,
     uint64_t n, uint8_t *__restrict__ native, uint32_t stride, uint8_t *__restrict__ heap,
-    uint32_t stack_limit, uint32_t C, uint64_t ebase, uint32_t F, uint32_t mark,
+    uint32_t stack_limit, uint32_t C, uint64_t ebase, uint32_t F, uint32_t mark, uint32_t S,
     unsigned long long *err) {
   extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
   const uint32_t lane = threadIdx.x;
   const uint32_t tile_bytes = NWD > 0 ? 0u : (64u * stride + 15u) & ~15u;
   uint8_t *tile = sm;
   uint8_t *win = sm + tile_bytes;
+  uint8_t *stage = win + C + 32u;  // S bytes: the group's element arrays (packed plans)
   const uint64_t wr0 = static_cast<uint64_t>(blockIdx.x) * 64u;
   const uint32_t nrec = static_cast<uint32_t>(min<uint64_t>(64, n - wr0));
   const uint64_t r = wr0 + lane;
@@ -882,12 +884,27 @@ __device__ __forceinline__ void var_decode_body(
   c.heap = heap;
   c.ecur = ebase + static_cast<uint64_t>(F) * a;  // this record's element arrays
   c.eend = ebase + static_cast<uint64_t>(F) * b;
-  if (w.packed()) {  // ... packed with the group's (packed_area)
+  // ... packed with the group's (packed_area).  When the group's arrays fit
+  // the stage (S bytes of LDS) the walk writes them there and the wave
+  // stores them after it as whole lines: written straight from the walk,
+  // each lane's stores land in lines its neighbours fill at other steps of
+  // the walk, and L2 evicts many of them half-written (vecrec: 350 MiB
+  // written per launch for ~280 MiB of data, profiles/r03p).
+  uint64_t ga = 0, gtot = 0;  // the group's arrays: [ga, ga + gtot)
+  bool staged = false;
+  if (w.packed()) {
     const bool bad = lane < nrec && (b < a || b > len);
     const bool on = lane < nrec && !bad && a + mark <= b;
     const uint64_t e = w.ebytes(c.rd, a + mark, b, on);
     const uint64_t E = on ? min(e, ebudget(F, a, b)) : 0u;
-    packed_area(E, bad, rl64(a, 0), ebase, F, c.ecur, c.eend);
+    ga = packed_area(E, bad, rl64(a, 0), ebase, F, c.ecur, c.eend);
+    gtot = rl64(c.eend, 63) - ga;
+    staged = gtot <= S;
+    if (staged) {  // zeroed: the stage leaves whole, gaps and all
+      for (uint32_t i = lane; i < (gtot + 15u) / 16u; i += 64u)
+        reinterpret_cast<u32x4 *>(stage)[i] = u32x4{0u, 0u, 0u, 0u};
+      wave_sync();
+    }
   }
   uint32_t rec[NWD > 0 ? NWD : 1];
 #pragma unroll
@@ -905,10 +922,20 @@ __device__ __forceinline__ void var_decode_body(
       else if ((b - a) & 3u) report(err, r, kOpRecordLevel, XDRG_ERR_SIZE_NOT_MULT4);
       else ok = true;
     }
-    ok = w.dec(c, nat, ok);
+    if (staged) {  // the same walk, its arrays into the stage
+      c.heap = stage - ga;
+      ok = w.dec(c, nat, ok);
+    } else {
+      ok = w.dec(c, nat, ok);
+    }
     if (ok && c.p != b) report(err, r, kOpRecordLevel, XDRG_ERR_TRAILING);
   }
   wave_sync();
+  if (staged) {  // [ga, ga + gtot): 8-aligned, a multiple of 8 bytes
+    const uint64_t *src = reinterpret_cast<const uint64_t *>(stage);
+    uint64_t *dst = reinterpret_cast<uint64_t *>(heap + ga);
+    for (uint32_t i = lane; i < gtot / 8u; i += 64u) dst[i] = src[i];
+  }
   XDRG_DSTAMP(3);
   if (COPY) {
     // The decoded heap is the stream: the stretch [ws, we) to heap + ws.

@@ -1042,9 +1042,9 @@ __global__ __launch_bounds__(64) void k_var_decode_w(
     uint8_t *__restrict__ native, uint32_t stride, uint8_t *__restrict__ heap,
     const xdrg_op *__restrict__ ops, uint32_t nops, const uint32_t *__restrict__ table,
     uint32_t stack_limit, uint32_t C, uint64_t ebase, uint32_t F, uint32_t mark, uint32_t packed,
-    unsigned long long *err) {
+    uint32_t S, unsigned long long *err) {
   var_decode_body<interp_walk, COPY, RA>(interp_walk{ops, nops, table, packed != 0}, xdr, len, offsets, n, native,
-                                         stride, heap, stack_limit, C, ebase, F, mark, err);
+                                         stride, heap, stack_limit, C, ebase, F, mark, S, err);
 }
 
 #include "sub_kernels.h"
@@ -2187,7 +2187,16 @@ int var_decode(const xdrg_plan &P, const dev_tables &T, const void *d_xdr, uint6
                        : 64ull * (len / n) <= (8u << 10) ? (8u << 10) : (4u << 10);
   const uint32_t Cw = static_cast<uint32_t>(std::min<uint64_t>(
       win, (64ull * std::max<uint64_t>(p->max_record_bytes + mark, 16) + 15u) & ~15ull));
-  const uint32_t lw = dec_w_lds(p->stride, Cw);
+  // Stage of a group's element arrays (packed plans, var_kernels.h
+  // var_decode_body).  tools/tune/dec_ab.py (MI355X, vecrec 1M records,
+  // profiles/r03q): no stage 0.137 ms and 348 MiB written per launch; an
+  // 8 KiB stage (every group's arrays fit) with an 8 KiB window 0.138 ms and
+  // 276 MiB -- the algorithmic bytes; a 12 KiB stage or a 16 KiB window
+  // cost occupancy (0.148-0.182 ms), a window below the 64 records' ~6.6
+  // KiB stretch sends the walk to global memory (0.188 ms at 6 KiB).
+  const uint32_t S = !p->packed ? 0u
+                     : O.stage_bytes >= 0 ? static_cast<uint32_t>(O.stage_bytes) & ~15u : (8u << 10);
+  const uint32_t lw = dec_w_lds(p->stride, Cw, false, S);
   const bool ok_W = lw <= kVarLdsBudget && aligned(d_native, 16);
   int kern = O.dec_kernel;
   if (kern == 2 && !ok_W) kern = 0;
@@ -2222,13 +2231,17 @@ int var_decode(const xdrg_plan &P, const dev_tables &T, const void *d_xdr, uint6
       // profiles/r02s/ab_dec_window*.log): rpc 4 KiB 0.159 ms, 8 KiB 0.146,
       // 16 KiB 0.126, 20 KiB 0.128, 32 KiB 0.177; recvar and vecrec are
       // flat from 16 KiB (0.089, 0.226) and slower below
-      const uint32_t want = O.window_bytes >= 0 ? static_cast<uint32_t>(O.window_bytes) & ~15u : (16u << 10);
+      const uint32_t want = O.window_bytes >= 0 ? static_cast<uint32_t>(O.window_bytes) & ~15u
+                            : S ? (8u << 10) : (16u << 10);  // (packed: the stage above)
       cw = static_cast<uint32_t>(std::min<uint64_t>(
           want, (64ull * std::max<uint64_t>(p->max_record_bytes + mark, 16) + 15u) & ~15ull));
-      lws = dec_w_lds(p->stride, cw, true);
+      lws = dec_w_lds(p->stride, cw, true, S);
+    } else {
+      lws = dec_w_lds(p->stride, cw, false, S);
     }
     uint64_t eb = ebase;
-    void *args[] = {&xdr8, &len, &d_offsets, &n, &nat8, &st, &d_heap_out, &sl, &cw, &eb, &F, &mk, &err};
+    uint32_t sb = S;
+    void *args[] = {&xdr8, &len, &d_offsets, &n, &nat8, &st, &d_heap_out, &sl, &cw, &eb, &F, &mk, &sb, &err};
     HIPCHK(hipModuleLaunchKernel(static_cast<hipFunction_t>(copy ? SM->f_dec_copy : SM->f_dec),
                                  static_cast<uint32_t>(nb), 1, 1, 64, 1, 1, lws, s, args, nullptr));
     return XDRG_OK;
@@ -2238,7 +2251,7 @@ int var_decode(const xdrg_plan &P, const dev_tables &T, const void *d_xdr, uint6
 #define LAUNCH_DEC_W(CP, RA)                                                                      \
   k_var_decode_w<CP, RA><<<nb, 64, lw, s>>>(xdr8, len, d_offsets, n, nat8, p->stride, d_heap_out, \
                                             T.d_ops, nops, T.d_table, stack_limit, Cw, ebase,     \
-                                            p->heap_factor, mark, p->packed, err)
+                                            p->heap_factor, mark, p->packed, S, err)
     if (copy) {
       if (O.dec_readahead) LAUNCH_DEC_W(true, true); else LAUNCH_DEC_W(true, false);
     } else {
@@ -2496,6 +2509,9 @@ int xdrg_plan_set_option(xdrg_plan *p, int option, int64_t value) {
   case XDRG_OPT_INDEX_FAST:
     if (v < 0 || v > 2) return XDRG_EINVAL;
     O.index_fast = static_cast<int>(v); return XDRG_OK;
+  case XDRG_OPT_STAGE_BYTES:
+    if (v > (32 << 10)) return XDRG_EINVAL;
+    O.stage_bytes = v < 0 ? -1 : v; return XDRG_OK;
   default: return XDRG_EINVAL;
   }
 }
