@@ -2191,7 +2191,8 @@ int var_decode(const xdrg_plan &P, const dev_tables &T, const void *d_xdr, uint6
   // var_decode_body).  tools/tune/dec_ab.py (MI355X, vecrec 1M records,
   // profiles/r03q): no stage 0.137 ms and 348 MiB written per launch; an
   // 8 KiB stage (every group's arrays fit) with an 8 KiB window 0.138 ms and
-  // 276 MiB -- the algorithmic bytes; a 12 KiB stage or a 16 KiB window
+  // 276 MiB -- the algorithmic bytes (0.128 ms once the stage leaves with
+  // non-temporal stores, profiles/r03s); a 12 KiB stage or a 16 KiB window
   // cost occupancy (0.148-0.182 ms), a window below the 64 records' ~6.6
   // KiB stretch sends the walk to global memory (0.188 ms at 6 KiB).
   const uint32_t S = !p->packed ? 0u
