@@ -224,7 +224,9 @@ enum xdrg_err {
   XDRG_ERR_MSG_TOO_LONG = 16,   /* msg_sock maxmsglen_  msgsock.cc:99-111 */
   XDRG_ERR_MSG_MISMATCH = 17,   /* mark disagrees with the record index  */
   XDRG_ERR_MSG_COUNT = 18,      /* more messages than the index can hold */
-  /* 19 is not used: no kernel waits on another workgroup */
+  XDRG_ERR_LOOKBACK = 19,      /* internal: a block of the one-pass encode waited
+                                   too long for the byte total of the blocks before
+                                   it (never expected; the output is not written) */
   XDRG_ERR_INDEX_LONG = 20      /* xdrg_index_records: a record longer than its bound */
 };
 
@@ -302,6 +304,12 @@ enum xdrg_plan_option {
                                      containers: LDS stage of a 64-record group's
                                      element arrays (written out as whole lines
                                      after the walk), -1 auto, 0 none           */
+  XDRG_OPT_ENC_STREAM = 15,      /* plan-specialized word-list plans: 1 (default)
+                                     xdrg_encode in one kernel (each wave's base by a
+                                     look-back over the byte totals of the waves
+                                     before it), 0 the size pass + scan + encode    */
+  XDRG_OPT_STREAM_HEAP = 16,     /* the one-pass encode's LDS heap window per wave,
+                                     bytes (<= 16 KiB), -1 auto                      */
   XDRG_OPT_INDEX_FAST = 13        /* xdrg_index_records: 1 (default) the speculative
                                      chain walk first, then the call waits for its
                                      verdict and runs the list ranking only when a

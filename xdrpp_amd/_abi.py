@@ -28,7 +28,8 @@ PATH_FIXED_REG, PATH_FIXED_LDS, PATH_VAR = 1, 2, 3
 PLAN_OPTIONS = {"var_encode_kernel": 1, "var_decode_kernel": 2, "fixed_path": 3, "image_bytes": 4,
                 "window_bytes": 5, "enc_unroll": 6, "dec_readahead": 7, "size_linear": 8,
                 "grp_unroll": 9, "grp_blocks": 10, "grp_nontemporal": 11, "specialize": 12,
-                "index_fast": 13, "stage_bytes": 14}
+                "index_fast": 13, "stage_bytes": 14,
+                "enc_stream": 15, "stream_heap": 16}
 
 OK = 0
 API_ERRORS = {-1: "EINVAL", -2: "EALIGN", -3: "EUNSUPPORTED", -4: "EHIP", -5: "ENOMEM", -6: "ESPACE"}
@@ -53,6 +54,7 @@ ERR_MSG_FRAGMENT = 15
 ERR_MSG_TOO_LONG = 16
 ERR_MSG_MISMATCH = 17
 ERR_MSG_COUNT = 18
+ERR_LOOKBACK = 19
 ERR_INDEX_LONG = 20
 
 MARK_LAST = 0x80000000  # XDRG_MARK_LAST: last-fragment bit of a record mark

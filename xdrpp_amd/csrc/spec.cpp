@@ -207,6 +207,14 @@ const spec_module *spec_get(const xdrg_plan &cp) {
   d.f_dec_copy = f[3];
   d.f_ix_seg = f[4];
   d.f_rxs_walk = f[5];
+  if (s.info.word_list) {  // the one-pass encode, generated for word-list plans only
+    hipFunction_t a = nullptr, b = nullptr;
+    if (hipModuleGetFunction(&a, m, "xdrg_spec_encode_stream") != hipSuccess ||
+        hipModuleGetFunction(&b, m, "xdrg_spec_encode_stream_sized") != hipSuccess)
+      return fail(m, "specialized kernels: the code object lacks the one-pass encode");
+    d.f_enc_stream = a;
+    d.f_enc_stream_sized = b;
+  }
   s.loaded[dev].store(true, std::memory_order_release);
   return &d;
 }

@@ -16,7 +16,7 @@ constexpr int kSpecDevices = 64;
 // Interface version of the generated kernels (their parameter lists and
 // LDS layout, var_kernels.h): the source defines xdrg_spec_iface with it,
 // and a code object that carries another value is refused at load.
-constexpr unsigned kSpecIface = 8;
+constexpr unsigned kSpecIface = 9;
 
 // The generated source of a plan and the launch facts it fixes.
 struct spec_info {
@@ -34,6 +34,7 @@ struct spec_module {
   void *f_size = nullptr, *f_enc = nullptr, *f_dec = nullptr, *f_dec_copy = nullptr;  // hipFunction_t
   void *f_ix_seg = nullptr;  // record-start parse of the plain-stream index (list ranking)
   void *f_rxs_walk = nullptr;  // ... and its speculative chain walk
+  void *f_enc_stream = nullptr, *f_enc_stream_sized = nullptr;  // one-pass encode (word-list plans)
 };
 
 // A plan's specialized kernels: state 0 = not built yet, 1 = code object

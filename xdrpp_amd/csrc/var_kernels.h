@@ -676,6 +676,381 @@ __device__ __forceinline__ void var_encode_body(
   XDRG_STAMP(5);
 }
 
+// ------------------------------------------------- encode, one pass (stream)
+// xdr_to_opaque(r0..rn-1) (xdrpp/marshal.h:264-272) for word-list plans (every
+// payload takes a slot, no container loop: W::kWords > 0) in ONE kernel, with
+// no size pass and no scan.  One wave = 64 consecutive records:
+//   1. (LB) a ticket from an atomic counter names the wave's block, so every
+//      block before it belongs to a wave already running;
+//   2. the native tile (coalesced), the walk from registers into the word
+//      list (xdr_generic_put's words, marshal.h:110-127) and the payload
+//      slots; the walk's byte counts are the sizes (xdr_size, types.h:240-244),
+//      and a wave scan of them the records' offsets within the wave;
+//   3. (LB) the wave's byte total is published at once, then a decoupled
+//      look-back over the totals of the blocks before it (4 per lane, 256 per
+//      step) finds the wave's base -- while the loads of its heap bytes are
+//      in flight: the payloads of a wave lie in one heap range when the heap
+//      is staged in record order (every stager here does that), so the range
+//      is loaded as aligned 16-byte chunks into LDS (up to H bytes;
+//      otherwise payload words are read from global memory);
+//   4. the wave's output stretch is assembled chunk by chunk in registers --
+//      each lane owns 16-byte output chunks, consecutive lanes consecutive
+//      chunks; a chunk's words come from the word list or the heap window,
+//      found by a binary search over the records' offsets -- and leaves as
+//      aligned 16-byte stores (words at the stretch's two edges, shared with
+//      the neighbour waves, as single-word stores).
+// Without LB (xdrg_encode_sized) the block's base comes from the size pass's
+// scan and nothing is published.  Every field check of xdr_generic_put is
+// kept: the walk runs unchecked only when the plan's depth fits the stack
+// budget (the host's condition for this kernel), and a wave whose bytes pass
+// `cap` walks again with the capacity check to report the failing record.
+constexpr unsigned long long kLbAgg = 1ull << 62;     // block total published
+constexpr unsigned long long kLbIncl = 2ull << 62;    // block total + everything before it
+constexpr unsigned long long kLbVal = (1ull << 62) - 1;
+constexpr uint32_t kLbSpinLimit = 1u << 16;           // polls before a look-back gives up
+
+struct senc_lds {
+  uint32_t tile, a0, slots, heap, total;
+};
+__host__ __device__ inline senc_lds senc_layout(uint32_t stride, uint32_t KMAX, uint32_t H) {
+  senc_lds L;
+  L.tile = 0;  // 64 native records, then the word list (4 * words <= stride)
+  L.a0 = (64u * stride + 15u) & ~15u;
+  L.slots = L.a0 + 272u;  // 65 record offsets (+ pad)
+  L.heap = L.slots + 64u * KMAX * 16u;
+  L.total = L.heap + H + 32u;
+  return L;
+}
+struct sslot {  // a record's payload slot: heap offset, record-relative wire offset, bytes
+  uint64_t src;
+  uint32_t ps, len;
+};
+
+typedef __attribute__((address_space(1))) unsigned long long lb_u64;
+typedef __attribute__((address_space(1))) unsigned int lb_u32;
+// generic -> global address space (agent-scope atomics on global, never flat)
+__device__ __forceinline__ lb_u64 *lb_global(unsigned long long *p) { return (lb_u64 *)p; }
+
+// Sum over the lanes of a wave (every lane active).
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t x) {
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+  return x;
+}
+__device__ __forceinline__ uint64_t wave_min64(uint64_t x) {
+  for (int o = 32; o > 0; o >>= 1) x = min(x, static_cast<uint64_t>(__shfl_xor(x, o, 64)));
+  return x;
+}
+__device__ __forceinline__ uint64_t wave_max64(uint64_t x) {
+  for (int o = 32; o > 0; o >>= 1) x = max(x, static_cast<uint64_t>(__shfl_xor(x, o, 64)));
+  return x;
+}
+
+// Decoupled look-back (single-pass chained scan): the exclusive prefix of
+// block `blk`'s total.  desc[i] = state | value, one 8-byte word written by
+// one store (the data is the flag).  Lane l reads blocks top - l - 64u, u < 4.
+// Returns false when a predecessor never published (kLbSpinLimit polls).
+__device__ __forceinline__ bool lookback(lb_u64 *desc, uint32_t blk, uint64_t &excl) {
+  const uint32_t lane = __lane_id();
+  excl = 0;
+  int64_t top = static_cast<int64_t>(blk) - 1;
+  for (uint32_t spins = 0; top >= 0;) {
+    uint64_t d[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t i = top - lane - 64 * u;
+      d[u] = i >= 0 ? __hip_atomic_load(desc + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kLbIncl;
+    }
+    // first block (in look-back order) that has not published, and the
+    // first that holds an inclusive prefix
+    uint32_t dn = 256, dp = 256;
+#pragma unroll
+    for (int u = 3; u >= 0; --u) {
+      const unsigned long long mn = __ballot((d[u] >> 62) == 0u);
+      const unsigned long long mp = __ballot((d[u] >> 62) == 2u);
+      if (mn) dn = 64u * u + __builtin_ctzll(mn);
+      if (mp) dp = 64u * u + __builtin_ctzll(mp);
+    }
+    const uint32_t lim = dp < dn ? dp + 1u : dn;  // blocks accounted by this step
+    uint64_t part = 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (lane + 64u * u < lim) part += d[u] & kLbVal;
+    excl += wave_sum64(part);
+    if (dp < dn) return true;
+    top -= lim;
+    if (dn < 256) {  // a block before this one is still walking its records
+      if (++spins > kLbSpinLimit) return false;
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  return true;
+}
+
+template <class W, int KMAX, int NW, int WL, bool LB>
+__device__ __forceinline__ void var_encode_stream_body(
+    const W &w, const uint8_t *__restrict__ native, uint64_t n, uint32_t stride,
+    const uint8_t *__restrict__ heap, uint64_t heap_len, uint8_t *__restrict__ xdr, uint64_t cap,
+    uint64_t *__restrict__ offsets, const unsigned long long *__restrict__ block_base,
+    unsigned long long *desc, uint32_t nb, uint64_t *total, uint32_t stack_limit, uint32_t H,
+    uint32_t mark, unsigned long long *err) {
+  static_assert(WL > 0 && NW > 0, "word-list plans walked from registers");
+  extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
+  const senc_lds L = senc_layout(stride, KMAX, H);
+  uint8_t *tile = sm + L.tile;
+  uint32_t *a0s = reinterpret_cast<uint32_t *>(sm + L.a0);
+  sslot *slt = reinterpret_cast<sslot *>(sm + L.slots);
+  uint8_t *hw = sm + L.heap;
+  const uint32_t lane = threadIdx.x;
+
+  uint32_t blk = blockIdx.x;
+  if constexpr (LB) {
+    uint32_t t = 0;
+    if (lane == 0)
+      t = __hip_atomic_fetch_add((lb_u32 *)(desc + nb), 1u, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+    blk = rl32(t, 0);
+  }
+  const uint64_t wr0 = static_cast<uint64_t>(blk) * 64u;
+  const uint64_t r = wr0 + lane;
+  const uint32_t nrec = static_cast<uint32_t>(min<uint64_t>(64, n - wr0));
+  uint64_t wave_out = 0;
+  if constexpr (!LB) wave_out = block_base[blk];
+  stage_tile<8>(tile, native + wr0 * stride, nrec * stride, lane, 64u);
+  wave_sync();
+  uint32_t rec[NW];
+  {
+    const uint32_t *t32 = reinterpret_cast<const uint32_t *>(tile + lane * stride);
+#pragma unroll
+    for (int k = 0; k < NW; ++k) rec[k] = lane < nrec ? t32[k] : 0u;
+  }
+  wave_sync();  // every tile read before the word list overwrites it
+
+  // ---- the walk: words into the list, payloads into slots, byte count
+  enc_ctx<KMAX, false, WL> c;
+  c.sw = reinterpret_cast<uint32_t *>(tile) + lane;
+  c.nw = 0;
+  c.img = nullptr;
+  c.w0 = 0;
+  c.C = 0;
+  c.heap = heap;
+  c.heap_len = heap_len;
+  c.cap = cap;
+  c.stack_limit = stack_limit;
+  c.r = r;
+  c.err = err;
+  c.at = 0;
+  c.pos = 0;
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) { c.psr[k] = 0; c.pds[k] = 0; c.pln[k] = 0; c.rb[k] = 0; }
+  bool ok = r < n;
+  if (ok && mark) c.put(0u);  // the record mark (message_t::alloc, marshal.cc:15-31), set below
+  ok = w.enc(c, reinterpret_cast<const uint8_t *>(rec), ok);
+  if (r < n && !ok) {  // an unchecked walk fails only at a bad discriminant (gen_hh.cc:645,658)
+    uint32_t bad = 0xffffffffu;
+    (void)w.size(reinterpret_cast<const uint8_t *>(rec), heap, heap_len, bad);
+    report(err, r, bad == 0xffffffffu ? 0u : bad, XDRG_ERR_BAD_DISCRIMINANT);
+  }
+  const uint32_t v = ok ? c.at : 0u;
+  if (ok && mark) c.sw[0] = mark_word(v - 4u);
+  if (!ok) {
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) c.pln[k] = 0;
+  }
+  const uint32_t incl = wave_incl_scan(v);
+  const uint32_t T = rl32(incl, 63);
+  const uint32_t a0 = incl - v;
+  a0s[lane] = a0;
+  if (lane == 0) a0s[64] = T;
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) slt[lane * KMAX + k] = sslot{c.psr[k], c.pds[k], c.pln[k]};
+  // the wave's heap range
+  uint64_t hlo = ~0ull, hhi = 0;
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k)
+    if (c.pln[k]) {
+      hlo = min(hlo, c.psr[k]);
+      hhi = max(hhi, c.psr[k] + c.pln[k]);
+    }
+  hlo = wave_min64(hlo);
+  hhi = wave_max64(hhi);
+  if constexpr (LB) {
+    if (lane == 0)
+      __hip_atomic_store(lb_global(desc) + blk, (blk == 0 ? kLbIncl : kLbAgg) | T,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+
+  // ---- the heap window: aligned 16-byte chunks covering [hlo, hhi) (loads
+  // in flight during the look-back)
+  // Chunks are 16-byte aligned in the address space, so one that holds a
+  // heap byte never leaves that byte's page (the first may start before the
+  // heap, which is only 4-byte aligned); heap bytes past heap_len read 0.
+  const uintptr_t hb = reinterpret_cast<uintptr_t>(heap);
+  const int64_t hbase = hlo < hhi && hlo < heap_len
+                            ? static_cast<int64_t>((hb + hlo) & ~uintptr_t(15)) - static_cast<int64_t>(hb)
+                            : 0;  // heap offset of hw[0] (-15..)
+  const uint64_t hspan = hlo < hhi ? hhi - static_cast<uint64_t>(hbase) : 0u;
+  const bool local = hlo >= hhi || (hlo < heap_len && hspan <= H);
+  const uint32_t nh = local ? static_cast<uint32_t>((hspan + 15u) >> 4) : 0u;
+  const int64_t hlen = static_cast<int64_t>(heap_len);
+  constexpr int UH = 16;
+  u32x4 hv[UH];
+  if (nh) {  // one batch: H <= 64 * UH * 16 bytes
+#pragma unroll
+    for (int u = 0; u < UH; ++u) {
+      const uint32_t i = lane + 64u * u;
+      const int64_t o = hbase + 16 * static_cast<int64_t>(i);
+      if (i < nh && o < hlen && o + 16 > 0) hv[u] = *reinterpret_cast<const u32x4 *>(heap + o);
+    }
+  }
+  uint64_t excl = wave_out;
+  bool live = true;
+  if constexpr (LB) {
+    live = lookback(lb_global(desc), blk, excl);
+    if (!live) report(err, wr0, kOpRecordLevel, XDRG_ERR_LOOKBACK);
+    if (blk > 0 && lane == 0)
+      __hip_atomic_store(lb_global(desc) + blk, kLbIncl | ((excl + T) & kLbVal),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    wave_out = excl;
+    if (r + 1 == n) {  // offsets[n] and the total (k_scan_blocks' job in two passes)
+      offsets[n] = wave_out + T;
+      *total = wave_out + T;
+    }
+  }
+  if (nh) {
+#pragma unroll
+    for (int u = 0; u < UH; ++u) {
+      const uint32_t i = lane + 64u * u;
+      const int64_t o = hbase + 16 * static_cast<int64_t>(i);
+      if (i < nh) {
+        u32x4 x = u32x4{0u, 0u, 0u, 0u};
+        if (o < hlen && o + 16 > 0) {
+          x = hv[u];
+          if (o + 16 > hlen) {  // the chunk holding the heap's last byte: the rest reads 0
+            const int32_t k = static_cast<int32_t>(hlen - o);
+            x.x &= keep_bytes(k);
+            x.y &= keep_bytes(k - 4);
+            x.z &= keep_bytes(k - 8);
+            x.w &= keep_bytes(k - 12);
+          }
+        }
+        reinterpret_cast<u32x4 *>(hw)[i] = x;
+      }
+    }
+  }
+  if (r < n) offsets[r] = wave_out + a0;
+  if (!live) return;
+
+  // ---- a wave whose bytes pass `cap`: the capacity checks, in the
+  // reference's order (xdr_generic_put::check, marshal.h:104-108)
+  const uint64_t ge = min<uint64_t>(wave_out + T, cap);
+  if (wave_out + T > cap && r < n && ok) {
+    enc_ctx<KMAX, true, WL> k;
+    k.sw = c.sw;
+    k.nw = 0;
+    k.img = nullptr;
+    k.w0 = 0;
+    k.C = 0;
+    k.heap = heap;
+    k.heap_len = heap_len;
+    k.cap = cap;
+    k.stack_limit = stack_limit;
+    k.r = r;
+    k.err = err;
+    k.at = 0;
+    k.pos = wave_out + a0;
+#pragma unroll
+    for (int q = 0; q < KMAX; ++q) { k.psr[q] = 0; k.pds[q] = 0; k.pln[q] = 0; k.rb[q] = 0; }
+    bool okc = true;
+    if (mark) {
+      if (4 > cap - min(k.pos, cap)) {
+        report(err, r, kOpRecordLevel, XDRG_ERR_OVERFLOW_PUT);
+        okc = false;
+      } else {
+        k.put(mark_word(v - 4u));
+      }
+    }
+    (void)w.enc(k, reinterpret_cast<const uint8_t *>(rec), okc);
+  }
+  wave_sync();
+
+  // ---- output: lane-owned 16-byte chunks of the stretch
+  const uint32_t sh = static_cast<uint32_t>(wave_out & 15u);
+  const uint64_t g0 = wave_out - sh;
+  const uint32_t nch = (sh + T + 15u) >> 4;
+  const uint32_t *sw = reinterpret_cast<const uint32_t *>(tile);
+  const uint32_t *h32 = reinterpret_cast<const uint32_t *>(hw);
+  for (uint32_t ck = lane; ck < nch; ck += 64u) {
+    const int32_t t0 = static_cast<int32_t>(16u * ck) - static_cast<int32_t>(sh);
+    // the record holding the chunk's first byte of this wave
+    const uint32_t tq = t0 < 0 ? 0u : static_cast<uint32_t>(t0);
+    uint32_t rr = 0;
+#pragma unroll
+    for (uint32_t s = 32; s; s >>= 1)
+      if (a0s[rr + s] <= tq) rr += s;  // last record starting at or before tq (a0s[64] = T)
+    uint32_t nxt = a0s[rr + 1], base = a0s[rr];
+    sslot e[KMAX];
+#pragma unroll
+    for (int q = 0; q < KMAX; ++q) e[q] = slt[rr * KMAX + q];
+    uint32_t wv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int32_t t = t0 + 4 * i;
+      wv[i] = 0u;
+      if (t < 0 || static_cast<uint32_t>(t) >= T) continue;
+      while (static_cast<uint32_t>(t) >= nxt) {  // the next record(s)
+        ++rr;
+        base = nxt;
+        nxt = a0s[rr + 1];
+#pragma unroll
+        for (int q = 0; q < KMAX; ++q) e[q] = slt[rr * KMAX + q];
+      }
+      const uint32_t qb = static_cast<uint32_t>(t) - base;  // byte of the record
+      uint32_t j4 = qb;
+      bool pay = false;
+      uint64_t src = 0;
+      uint32_t left = 0;
+#pragma unroll
+      for (int q = 0; q < KMAX; ++q) {
+        const uint32_t pe = e[q].ps + ((e[q].len + 3u) & ~3u);
+        if (e[q].len && qb >= e[q].ps && qb < pe) {
+          pay = true;
+          src = e[q].src + (qb - e[q].ps);
+          left = e[q].len - (qb - e[q].ps);
+        } else if (e[q].len && qb >= pe) {
+          j4 -= pe - e[q].ps;
+        }
+      }
+      uint32_t x;
+      if (pay) {
+        if (local) {
+          const uint32_t o = static_cast<uint32_t>(static_cast<int64_t>(src) - hbase);
+          x = __builtin_amdgcn_alignbyte(h32[(o >> 2) + 1], h32[o >> 2], o & 3u);
+        } else {
+          x = unaligned_word(heap, heap_len, src);
+        }
+        if (left < 4u) x &= keep_mask(left);  // put_bytes' zero pad (marshal.cc:59-72)
+      } else {
+        x = sw[64u * (j4 >> 2) + rr];
+      }
+      wv[i] = x;
+    }
+    const uint64_t ca = g0 + 16ull * ck;
+    if (t0 >= 0 && ca + 16u <= ge) {
+      const u32x4 o4 = u32x4{wv[0], wv[1], wv[2], wv[3]};
+      if constexpr ((XDRG_ENC_NT & 2) != 0)
+        __builtin_nontemporal_store(o4, reinterpret_cast<u32x4 *>(xdr + ca));
+      else
+        *reinterpret_cast<u32x4 *>(xdr + ca) = o4;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int32_t t = t0 + 4 * i;
+        if (t >= 0 && static_cast<uint32_t>(t) < T && ca + 4u * i + 4u <= ge) st32(xdr + ca + 4u * i, wv[i]);
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------- decode
 // LDS of a decode wave: the native tile (none when the walk decodes into
 // registers, NWD > 0) and the window.

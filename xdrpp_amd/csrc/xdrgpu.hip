@@ -1592,6 +1592,7 @@ __global__ void k_swap64(const uint64_t *__restrict__ in, uint64_t *__restrict__
 // ------------------------------------------------------------------ host
 constexpr uint64_t kMallBytes = 256ull << 20;  // MI355X Infinity Cache
 constexpr uint32_t kVarLdsBudget = 64u << 10;  // wave-cooperative var kernels
+constexpr uint32_t kStreamHeapBytes = 16u << 10;  // one-pass encode: heap window per wave
 uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 bool aligned(const void *p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) % a) == 0; }
 uint32_t gcd32(uint32_t a, uint32_t b) { while (b) { uint32_t t = a % b; a = b; b = t; } return a; }
@@ -2014,6 +2015,35 @@ int var_encode(const xdrg_plan &P, const dev_tables &T, const void *d_native, ui
     // var_encode_body's direct mode)
     if (lds_s > kVarLdsBudget || !aligned(d_native, 16)) SM = nullptr;
   }
+  // The one-pass encode of word-list plans (var_kernels.h
+  // var_encode_stream_body): no size pass and no scan; each wave finds its
+  // base by a look-back over the byte totals of the waves before it
+  // (xdrg_encode), or reads it from the scan xdrg_encode_sizes left
+  // (xdrg_encode_sized).  Its walk runs without the stack checks, so the
+  // plan's depth must fit the budget; a wave stays under 2^31 bytes.
+  if (SM && SM->f_enc_stream && O.enc_stream && phase != kEncSizes && p->max_depth <= stack_limit &&
+      64ull * max_rec < (1ull << 31)) {
+    const uint32_t H = O.stream_heap >= 0 ? static_cast<uint32_t>(O.stream_heap) : kStreamHeapBytes;
+    const uint32_t lds = senc_layout(p->stride, p->spec.info.slots, H).total;
+    if (lds <= kVarLdsBudget) {
+      uint64_t *total = &d_status->total_bytes;
+      unsigned long long *desc = bsum;  // nb block totals + the ticket counter (bsum[nb])
+      const unsigned long long *bb = bbase;
+      uint32_t nb32 = static_cast<uint32_t>(nb), sl = stack_limit, hh = H, mk = mark;
+      void *args[] = {&nat8, &n, const_cast<uint32_t *>(&p->stride), &d_heap, &heap_len, &xdr8, &cap,
+                      &d_offsets, &bb, &desc, &nb32, &total, &sl, &hh, &mk, &err};
+      hipFunction_t f;
+      if (phase == kEncBoth) {
+        HIPCHK(hipMemsetAsync(desc, 0, align_up((nb + 1) * 8, 16), s));
+        f = static_cast<hipFunction_t>(SM->f_enc_stream);
+      } else {  // sizes and block bases from xdrg_encode_sizes
+        HIPCHK(hipMemcpyAsync(d_offsets + n, &d_status->total_bytes, 8, hipMemcpyDeviceToDevice, s));
+        f = static_cast<hipFunction_t>(SM->f_enc_stream_sized);
+      }
+      HIPCHK(hipModuleLaunchKernel(f, nb32, 1, 1, 64, 1, 1, lds, s, args, nullptr));
+      return XDRG_OK;
+    }
+  }
   pool_lease lease;  // element subroutines nested past XDRG_SUB_FRAMES
   deep_passes dp;
   if (p->has_sub)
@@ -2273,13 +2303,16 @@ int var_decode(const xdrg_plan &P, const dev_tables &T, const void *d_xdr, uint6
 }  // namespace
 
 namespace {
+constexpr int kIxNotHeld = 1;  // run_index(fast_only): the speculative walk did not hold
 // C: the window of a longer stream this index covers (ix_cont); the
-// offsets, count and errors are the whole stream's.
+// offsets, count and errors are the whole stream's.  fast_only: the
+// speculative walk alone (XDRG_OK when it holds the index, kIxNotHeld when
+// it did not run or a check failed; nothing reported either way).
 template <bool REC>
 int run_index(const xdrg_plan *p, const dev_tables *T, const void *d_stream, uint64_t len,
               uint32_t max_msg_len, uint64_t max_msgs, uint64_t *d_offsets, uint64_t *d_count,
               void *d_ws, size_t ws_bytes, xdrg_status *d_status, hipStream_t s,
-              const ix_cont &C = ix_cont{}) {
+              const ix_cont &C = ix_cont{}, bool fast_only = false) {
   const ix_layout L = ix_plan(len, max_msg_len);
   if (!d_ws || ws_bytes < L.total) return XDRG_ESPACE;
   if (L.nseg > 0xffffffffull) return XDRG_EUNSUPPORTED;
@@ -2328,7 +2361,12 @@ int run_index(const xdrg_plan *p, const dev_tables *T, const void *d_stream, uin
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) gate = 2;
   }
-  if (walk_ok && !C.next && len >= 4ull * kRxsSeg && max_msgs > 0) {
+  if (fast_only) gate = 1;  // ix_windows: the walk's verdict, nothing else
+  const bool walk_runs = walk_ok && !C.next && len >= 4ull * kRxsSeg && max_msgs > 0;
+  if (fast_only && !walk_runs) return kIxNotHeld;
+  if (REC && !C.next && !walk_runs)  // the flag says which path ran (include/xdrgpu.h)
+    HIPCHK(hipMemsetAsync(ws + L.rxs_flag, 0, 4, s));
+  if (walk_runs) {
     uint64_t *seg = reinterpret_cast<uint64_t *>(ws + L.rxs_seg);
     auto *cnt = reinterpret_cast<unsigned long long *>(ws + L.rxs_cnt);
     auto *base = reinterpret_cast<unsigned long long *>(ws + L.rxs_base);
@@ -2357,6 +2395,7 @@ int run_index(const xdrg_plan *p, const dev_tables *T, const void *d_stream, uin
       HIPCHK(hipMemcpyAsync(&h, flag, sizeof h, hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
       if (h == 1u) return XDRG_OK;
+      if (fast_only) return kIxNotHeld;
     } else {
       skip = flag;  // asynchronous: the list ranking's kernels skip themselves
     }
@@ -2418,6 +2457,19 @@ int ix_windows(const uint8_t *s8, uint64_t len, uint32_t max_msg_len, uint64_t m
                uint64_t *d_count, void *d_ws, size_t ws_bytes, xdrg_status *d_status, hipStream_t s) {
   const size_t need = xdrg_index_workspace_size(len, max_msg_len);
   if (!d_ws || ws_bytes < need) return XDRG_ESPACE;
+  {  // the rounds wait on the stream: a stream being captured cannot be waited on
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return XDRG_EUNSUPPORTED;
+  }
+  // A stream whose messages all fit one index window (the usual case under
+  // msg_sock's 1 MiB default) is indexed by the speculative mark walk of
+  // run_index alone; any long message, or a check that fails, leaves it to
+  // the rounds below, which rewrite the count and every offset.
+  {
+    const int rc = run_index<false>(nullptr, nullptr, s8, len, XDRG_INDEX_MAX_MSG, max_msgs, d_offsets, d_count,
+                                    d_ws, ws_bytes, d_status, s, ix_cont{}, true);
+    if (rc != kIxNotHeld) return rc;
+  }
   auto *next = reinterpret_cast<unsigned long long *>(static_cast<char *>(d_ws) + need - kIxNextBytes);
   unsigned long long *err = err_ptr(d_status);
   unsigned long long *count = reinterpret_cast<unsigned long long *>(d_count);
@@ -2513,6 +2565,10 @@ int xdrg_plan_set_option(xdrg_plan *p, int option, int64_t value) {
   case XDRG_OPT_STAGE_BYTES:
     if (v > (32 << 10)) return XDRG_EINVAL;
     O.stage_bytes = v < 0 ? -1 : v; return XDRG_OK;
+  case XDRG_OPT_ENC_STREAM: O.enc_stream = v ? 1 : 0; return XDRG_OK;
+  case XDRG_OPT_STREAM_HEAP:
+    if (v > (16 << 10)) return XDRG_EINVAL;
+    O.stream_heap = v < 0 ? -1 : (v & ~15); return XDRG_OK;
   default: return XDRG_EINVAL;
   }
 }
@@ -2888,6 +2944,7 @@ const char *xdrg_error_message(int code) {
   case XDRG_ERR_MSG_MISMATCH: return "record mark does not match the record index";
   case XDRG_ERR_MSG_COUNT: return "more messages than the record index holds";
   case XDRG_ERR_INDEX_LONG: return "record longer than the device record index window";
+  case XDRG_ERR_LOOKBACK: return "one-pass encode: look-back timed out (internal error)";
   default: return "unknown xdrgpu error";
   }
 }

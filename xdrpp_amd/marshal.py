@@ -116,10 +116,13 @@ class Plan:
 
 # -------------------------------------------------------------------- status
 class Status:
-    """Device-resident xdrg_status (16 bytes)."""
+    """Device-resident xdrg_status (16 bytes), born initialised: first_error
+    all ones (no error), total 0 -- what xdrg_status_init writes -- so a raw
+    launch whose caller skipped init() cannot read allocator garbage as an
+    error."""
 
     def __init__(self, device: torch.device):
-        self.buf = torch.empty(2, dtype=torch.int64, device=device)
+        self.buf = torch.tensor([-1, 0], dtype=torch.int64, device=device)
 
     @property
     def ptr(self) -> int:
