@@ -66,7 +66,7 @@
 extern "C" {
 #endif
 
-#define XDRG_ABI_VERSION 6
+#define XDRG_ABI_VERSION 7
 
 /* ---------------------------------------------------------------------- */
 /* Plan ops: a flat, wire-ordered walk of xdr_traits<T>::save.             */
@@ -133,10 +133,9 @@ enum xdrg_op_flags {
  * xdrpp/rpcb_prot.x:34).  Nesting is bounded by the data and by
  * marshaling_stack_limit only: a walk keeps XDRG_SUB_FRAMES element frames
  * in private memory, and records nested deeper are walked again by deep
- * passes whose frames live in a library-owned frame pool (one per device,
- * allocated by the first launch of a plan that can nest that deep: about
- * 128 MiB + 8 bytes per record; launches that use it are ordered across
- * streams).  A record that needs more than XDRG_MAX_FRAMES nested element
+ * passes whose frames live in the caller's workspace
+ * (xdrg_deep_workspace_size: about 128 MiB + 8 bytes per record for a plan
+ * that can nest that deep, 0 for any other).  A record that needs more than XDRG_MAX_FRAMES nested element
  * frames raises the stack-overflow error at the VECTOR op that would open
  * the next one; the reference's own recursion ends far earlier, in a
  * segmentation fault of its 8 MiB call stack.  A decode that fails inside
@@ -348,9 +347,18 @@ int xdrg_plan_kernel_source(const xdrg_plan *plan, char *buf, size_t cap, size_t
 int xdrg_plan_build_kernels(xdrg_plan *plan);
 int xdrg_plan_load_kernels(xdrg_plan *plan, const void *code_object, size_t size);
 
-/* Workspace bytes encode (var plans), encode_msgs (any plan) and
- * serial_sizes need for n records. */
+/* Workspace bytes encode (var plans) and encode_msgs (any plan) need for n
+ * records; it includes xdrg_deep_workspace_size. */
 size_t xdrg_workspace_size(const xdrg_plan *plan, uint64_t n);
+/* Workspace bytes decode, decode_msgs, serial_sizes and record_depths need
+ * for n records: 0 except for plans whose element subroutines can nest past
+ * XDRG_SUB_FRAMES, whose deep passes keep their lists of deferred records
+ * and their frame slabs there (about 128 MiB + 8 bytes per record; 256-byte
+ * aligned).  The memory is the caller's: no call allocates, locks or keeps
+ * state between calls, so calls on different streams with different
+ * workspaces run side by side, and graph capture records plain memsets and
+ * kernels. */
+size_t xdrg_deep_workspace_size(const xdrg_plan *plan, uint64_t n);
 
 /* Zero a status block (first_error = all ones) on `stream`. */
 int xdrg_status_init(xdrg_status *d_status, void *stream);
@@ -414,6 +422,8 @@ int xdrg_encode_sized(const xdrg_plan *plan, const void *d_native, uint64_t n,
  *   offset of its payload (so payloads are never gathered one by one).
  *   Passing d_heap_out == d_xdr decodes without copying: the refs then
  *   point into the input stream, which must outlive the decoded records.
+ * Workspace: xdrg_deep_workspace_size(plan, n) bytes (NULL/0 for plans
+ * that need none).
  */
 int xdrg_decode(const xdrg_plan *plan, const void *d_xdr, uint64_t xdr_len,
                 const uint64_t *d_offsets, uint64_t n, void *d_native,
@@ -670,13 +680,16 @@ size_t xdrg_rpc_replies_workspace_size(uint64_t n);
  * it; NULL/0 when the plan has none). */
 int xdrg_record_depths(const xdrg_plan *plan, const void *d_native, uint64_t n,
                        const void *d_heap, uint64_t heap_len, uint32_t *d_depths,
+                       void *d_workspace, size_t workspace_bytes,
                        xdrg_status *d_status, void *stream);
 
 /* Size pass alone: d_sizes[i] = xdr_size(record i) (uint32); d_heap as
- * for xdrg_record_depths. */
+ * for xdrg_record_depths.  Both take xdrg_deep_workspace_size(plan, n)
+ * bytes of workspace (NULL/0 for every plan that needs none). */
 int xdrg_serial_sizes(const xdrg_plan *plan, const void *d_native, uint64_t n,
                       const void *d_heap, uint64_t heap_len, uint32_t *d_sizes,
-                      uint32_t stack_limit, xdrg_status *d_status, void *stream);
+                      uint32_t stack_limit, void *d_workspace, size_t workspace_bytes,
+                      xdrg_status *d_status, void *stream);
 
 /* Bulk big-endian swaps (endian.h swap32/swap64) over device arrays. */
 int xdrg_swap32(const uint32_t *d_in, uint32_t *d_out, uint64_t n, void *stream);

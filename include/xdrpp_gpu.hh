@@ -1234,8 +1234,10 @@ void from_opaque_batch(context &c, const void *bytes, std::size_t len, T *out, s
       detail::hipcheck(hipMemcpyAsync(d_off, c.h_off.data(), (n + 1) * 8, hipMemcpyHostToDevice, s), "H2D");
     }
   }
+  const std::size_t dws = xdrg_deep_workspace_size(P.handle(), n);  // deep plans' passes
+  void *dw = dws ? c.d_ws.get<std::uint8_t>(dws) : nullptr;
   detail::abicheck(xdrg_decode(P.handle(), d_x, len, d_off, n, d_nat, d_heap, hcap, marshaling_stack_limit,
-                               nullptr, 0, c.status(), s),
+                               dw, dws, c.status(), s),
                    "xdrg_decode");
   c.h_out.resize(n * P.stride());
   c.h_heap.resize(hcap);
@@ -1261,8 +1263,10 @@ std::vector<std::uint32_t> xdr_size_batch(context &c, const T *recs, std::size_t
   detail::upload(c, s, &nat, &heap);
   std::uint32_t *d_sz = c.d_aux.get<std::uint32_t>(n);
   detail::abicheck(xdrg_status_init(c.status(), s), "xdrg_status_init");
+  const std::size_t dws = xdrg_deep_workspace_size(P.handle(), n);
+  void *dw = dws ? c.d_ws.get<std::uint8_t>(dws) : nullptr;
   detail::abicheck(xdrg_serial_sizes(P.handle(), nat, n, heap, c.staged.heap.size(), d_sz, marshaling_stack_limit,
-                                     c.status(), s),
+                                     dw, dws, c.status(), s),
                    "xdrg_serial_sizes");
   c.h_out.resize(n * 4);
   if (n) detail::hipcheck(hipMemcpyAsync(c.h_out.data(), d_sz, n * 4, hipMemcpyDeviceToHost, s), "D2H");
@@ -1288,7 +1292,9 @@ std::vector<bool> check_xdr_depth_batch(context &c, const T *recs, std::size_t n
   detail::upload(c, s, &nat, &heap);
   std::uint32_t *d_d = c.d_aux.get<std::uint32_t>(n);
   detail::abicheck(xdrg_status_init(c.status(), s), "xdrg_status_init");
-  detail::abicheck(xdrg_record_depths(P.handle(), nat, n, heap, c.staged.heap.size(), d_d, c.status(), s),
+  const std::size_t dws = xdrg_deep_workspace_size(P.handle(), n);
+  void *dw = dws ? c.d_ws.get<std::uint8_t>(dws) : nullptr;
+  detail::abicheck(xdrg_record_depths(P.handle(), nat, n, heap, c.staged.heap.size(), d_d, dw, dws, c.status(), s),
                    "xdrg_record_depths");
   c.h_out.resize(n * 4);
   if (n) detail::hipcheck(hipMemcpyAsync(c.h_out.data(), d_d, n * 4, hipMemcpyDeviceToHost, s), "D2H");
@@ -1335,8 +1341,10 @@ void decode_msgs_on_device(context &c, const std::uint8_t *d_x, std::size_t len,
   abicheck(xdrg_status_init(c.status(), s), "xdrg_status_init");
   const std::uint64_t hcap = P.fixed() ? 0 : xdrg_decode_heap_size(P.handle(), len);
   std::uint8_t *d_heap = hcap ? c.d_heap.get<std::uint8_t>(hcap) : nullptr;
-  abicheck(xdrg_decode_msgs(P.handle(), d_x, len, d_off, n, d_nat, d_heap, hcap, marshaling_stack_limit, nullptr,
-                            0, c.status(), s),
+  const std::size_t dws = xdrg_deep_workspace_size(P.handle(), n);  // deep plans' passes
+  void *dw = dws ? c.d_ws.get<std::uint8_t>(dws) : nullptr;
+  abicheck(xdrg_decode_msgs(P.handle(), d_x, len, d_off, n, d_nat, d_heap, hcap, marshaling_stack_limit, dw,
+                            dws, c.status(), s),
            "xdrg_decode_msgs");
   c.h_out.resize(n * P.stride());
   c.h_heap.resize(hcap);

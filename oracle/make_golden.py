@@ -83,6 +83,17 @@ def rpc_fixtures(manifest: dict) -> None:
             "stream_bytes": os.path.getsize(fp + ".stream")}
 
 
+SUCCESS_N = 512
+
+
+def success_fixtures() -> None:
+    """Success replies xdr_to_msg(rpc_success_hdr(xid), res) of rec128
+    results from the reference (ref_golden success; xdrpp/server.h:27-49,
+    srpc.h:152), and rpc_success_hdr(7)'s message, which ref_golden checks
+    equals rpc_msg(7, REPLY)'s as tests/arpc.cc:35-43 does."""
+    subprocess.check_call([BIN, "success", str(SUCCESS_N), os.path.join(GOLD, f"success_rec128_{SUCCESS_N}")])
+
+
 def depth_fixtures() -> None:
     """depth_checker (xdrpp/depth_checker.h): the smallest passing limit of
     every record of the small batches, from the real check_xdr_depth."""
@@ -128,6 +139,9 @@ def main() -> int:
         with open(mp, "w") as f:
             json.dump(manifest, f, indent=1, sort_keys=True)
         return 0
+    if "--only-success" in sys.argv:
+        success_fixtures()
+        return 0
     if "--only-depths" in sys.argv:
         depth_fixtures()
         return 0
@@ -152,6 +166,7 @@ def main() -> int:
     subprocess.check_call([BIN, "kat", os.path.join(GOLD, "kat.json")])
     full_hashes(manifest, [kv for table in (FULL, FULL2, MID, FULL3) for kv in table.items()])
     rpc_fixtures(manifest)
+    success_fixtures()
     depth_fixtures()
     with open(os.path.join(GOLD, "manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1, sort_keys=True)

@@ -652,8 +652,37 @@ static void frame_mode(const string &in, uint64_t maxlen, const string &out) {
   f << o.str();
 }
 
+// ---- success replies: xdr_to_msg(rpc_success_hdr(xid), res) (the reply
+// srpc_service::dispatch sends, xdrpp/srpc.h:152, header xdrpp/server.h:
+// 27-49) for rec128 results r (the config-2 generator) and xid_r = r *
+// 2654435761, back to back; and the reference's own byte assertion
+// (tests/arpc.cc:35-43): xdr_to_msg(rpc_msg(7, REPLY)) == xdr_to_msg(
+// rpc_success_hdr(7)), both messages written after it.
+static void success_mode(size_t n, const string &pre) {
+  vector<rec128> v;
+  gen_rec128(n, WG_SEED_REC128, 0, v);
+  std::vector<uint8_t> out;
+  for (size_t r = 0; r < n; ++r) {
+    const uint32_t xid = static_cast<uint32_t>(r * 2654435761u);
+    xdr::msg_ptr m = xdr::xdr_to_msg(xdr::rpc_success_hdr(xid), v[r]);
+    const uint8_t *b = reinterpret_cast<const uint8_t *>(m->raw_data());
+    out.insert(out.end(), b, b + m->raw_size());
+  }
+  write_file(pre + ".msgs", out.data(), out.size());
+  xdr::msg_ptr m1(xdr::xdr_to_msg(xdr::rpc_msg(7, xdr::REPLY)));
+  xdr::msg_ptr m2(xdr::xdr_to_msg(xdr::rpc_success_hdr(7)));
+  if (m1->size() != m2->size() || memcmp(m1->data(), m2->data(), m1->size()))
+    die("rpc_msg(7, REPLY) and rpc_success_hdr(7) differ");
+  write_file(pre + ".hdr7", m2->raw_data(), m2->raw_size());
+}
+
 int main(int argc, char **argv) {
-  if (argc < 2) die("usage: gen|kat|bench|rpc|frame ...");
+  if (argc < 2) die("usage: gen|kat|bench|rpc|frame|success ...");
+  if (string(argv[1]) == "success") {
+    if (argc != 4) die("success <n> <outprefix>");
+    success_mode(std::stoull(argv[2]), argv[3]);
+    return 0;
+  }
   string mode = argv[1];
   if (mode == "frame") {
     if (argc != 5) die("frame <stream> <maxmsglen> <out.json>");

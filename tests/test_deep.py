@@ -308,3 +308,64 @@ def test_gpu_decode_without_offsets(gold, dev, name):
     a, ha = mar.decode(x, n, _dev(offs.astype(np.int64), dev))
     b, hb = mar.decode(x, n)
     assert np.array_equal(a.cpu().numpy(), b.cpu().numpy()) and np.array_equal(ha.cpu().numpy(), hb.cpu().numpy())
+
+
+@pytest.mark.gpu
+def test_gpu_deep_two_streams_and_capture(gold, dev):
+    """The deep passes' lists and frame slabs live in each caller's workspace
+    (xdrg_deep_workspace_size): two marshalers encode and decode deep chains
+    on two streams at once, each with its own workspace, and an encode and a
+    decode of a deep plan captured into a graph replay to the reference's
+    bytes (no allocation, lock or host wait inside the calls)."""
+    import torch
+    from xdrpp_amd import marshal as M
+    chains, wire, offs, recs = chains_of(gold, "test_recursive")
+    pick = [0, 4, 5, 7, 8, 1, 11, 2]
+    many = [chains[pick[i % len(pick)]] for i in range(300)]
+    n, cp = len(many), plan_of("test_recursive")
+    nat, heap = stage_chains("test_recursive", many)
+    x, o = O.encode(cp, nat, n, heap)
+    onat, oheap = O.decode(cp, x, n, o)
+    plan = M.Plan(S.test_recursive)
+    assert A.lib().xdrg_deep_workspace_size(plan.handle, n) > 0
+    dn, dh = _dev(nat, dev), _dev(heap, dev)
+    mars = [M.Marshaler(plan, dev) for _ in range(2)]
+    streams = [torch.cuda.Stream(dev) for _ in range(2)]
+    outs = [torch.empty(x.size, dtype=torch.uint8, device=dev) for _ in range(2)]
+    offsets = [torch.empty(n + 1, dtype=torch.int64, device=dev) for _ in range(2)]
+    backs = [torch.zeros(n * plan.stride, dtype=torch.uint8, device=dev) for _ in range(2)]
+    hcap = plan.decode_heap_bytes(x.size)
+    houts = [torch.zeros(hcap, dtype=torch.uint8, device=dev) for _ in range(2)]
+    torch.cuda.synchronize()
+    for _ in range(3):
+        for k in range(2):
+            s = streams[k].cuda_stream
+            mars[k].status.init(s)
+            mars[k].launch_encode(dn, n, outs[k], heap=dh, offsets=offsets[k], stream=s)
+            mars[k].launch_decode(outs[k], n, backs[k], offsets=offsets[k], heap_out=houts[k], stream=s)
+        for k in range(2):
+            assert mars[k].check(streams[k].cuda_stream).code == 0
+            assert bytes(outs[k].cpu().numpy()) == bytes(x)
+            assert np.array_equal(backs[k].cpu().numpy(), onat)
+            assert np.array_equal(houts[k].cpu().numpy(), oheap)
+    # graph capture: encode then decode of the deep plan
+    mar = mars[0]
+    cap_s = torch.cuda.Stream(dev)
+    out, back, hout = outs[0], backs[0], houts[0]
+    mar.status.init(cap_s.cuda_stream)
+    mar.launch_encode(dn, n, out, heap=dh, offsets=offsets[0], stream=cap_s.cuda_stream)  # warm (tables, kernels)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=cap_s):
+        mar.launch_encode(dn, n, out, heap=dh, offsets=offsets[0], stream=cap_s.cuda_stream)
+        mar.launch_decode(out, n, back, offsets=offsets[0], heap_out=hout, stream=cap_s.cuda_stream)
+    for _ in range(2):
+        out.zero_()
+        back.zero_()
+        hout.zero_()
+        mar.status.init(cap_s.cuda_stream)
+        g.replay()
+        assert mar.check(cap_s.cuda_stream).code == 0
+        assert bytes(out.cpu().numpy()) == bytes(x)
+        assert np.array_equal(back.cpu().numpy(), onat)
+        assert np.array_equal(hout.cpu().numpy(), oheap)

@@ -185,6 +185,33 @@ def test_success_replies_are_xdr_to_msg(dev):
     assert np.array_equal(chk["body_off"], enc.offsets.cpu().numpy()[:-1].astype(np.uint64) + 28)
 
 
+def test_success_replies_match_reference(dev):
+    """xdr_to_msg(rpc_success_hdr(xid), res) as the REAL reference writes it
+    (tests/golden/success_rec128_512.msgs from oracle/ref_golden success:
+    xdrpp/server.h:27-49, the reply srpc_service::dispatch sends at
+    srpc.h:152) equals encode_msgs of the success-reply record type; and the
+    header alone equals the reference's rpc_success_hdr(7) message, which
+    ref_golden asserts is rpc_msg(7, REPLY)'s (tests/arpc.cc:35-43)."""
+    n = 512
+    want = np.fromfile(os.path.join(GOLD, f"success_rec128_{n}.msgs"), dtype=np.uint8)
+    t = R.success_reply_type(S.rec128)
+    p = M.Plan(t)
+    res, _ = W.rec128(n)
+    xid = (np.arange(n, dtype=np.uint64) * 2654435761 & 0xFFFFFFFF).astype(np.uint32)
+    nat = np.zeros((n, p.stride), dtype=np.uint8)
+    hdr = np.zeros((n, 6), dtype="<u4")
+    hdr[:, 0], hdr[:, 1] = xid, 1  # xid, REPLY (MSG_ACCEPTED, AUTH_NONE, empty body, SUCCESS: 0)
+    nat[:, :24] = hdr.view(np.uint8).reshape(n, 24)
+    nat[:, 24:] = res.reshape(n, 128)
+    enc = M.Marshaler(p, dev).encode_msgs(to_dev(nat.reshape(-1), dev), n)
+    assert np.array_equal(enc.xdr.cpu().numpy(), want)
+    h7 = np.fromfile(os.path.join(GOLD, f"success_rec128_{n}.hdr7"), dtype=np.uint8)
+    hdr_t = S.Struct("rpc_success_hdr", [(f, S.UInt) for f in ("xid", "mtype", "stat", "flavor", "body", "accept")])
+    one = np.array([7, 1, 0, 0, 0, 0], dtype="<u4").view(np.uint8)
+    got7 = M.Marshaler(M.Plan(hdr_t), dev).encode_msgs(to_dev(one, dev), 1).xdr.cpu().numpy()
+    assert np.array_equal(got7, h7)
+
+
 @pytest.mark.parametrize("seed", range(4))
 def test_fuzzed_headers_vs_oracle(dev, seed):
     """Random word corruptions of the call stream (lengths, discriminants,

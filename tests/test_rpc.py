@@ -15,7 +15,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLD
+from conftest import GOLD, ROOT
 
 from xdrpp_amd import _abi as A
 from xdrpp_amd import rpc as R
@@ -135,3 +135,27 @@ def test_raise_for_reply_messages():
         with pytest.raises(cls) as ei:
             R.raise_for_reply(h)
         assert str(ei.value) == what
+
+
+@pytest.mark.skipif(not os.path.exists("/root/reference/xdrpp/server.h"), reason="reference tree absent")
+def test_success_fixture_regenerates(tmp_path):
+    """success_rec128_512.{msgs,hdr7} are what the reference writes today
+    (ref_golden success also asserts tests/arpc.cc:35-43: rpc_msg(7, REPLY)
+    and rpc_success_hdr(7) marshal to the same message)."""
+    import subprocess
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "_ref/ref_golden"], check=True)
+    pre = str(tmp_path / "s")
+    subprocess.run([os.path.join(ROOT, "oracle", "_ref", "ref_golden"), "success", "512", pre], check=True)
+    for ext in ("msgs", "hdr7"):
+        assert open(pre + "." + ext, "rb").read() == open(os.path.join(GOLD, "success_rec128_512." + ext), "rb").read()
+
+
+def test_success_fixture_layout():
+    """The fixture's messages: mark BE(152 | last), xid r * 2654435761,
+    REPLY, MSG_ACCEPTED, AUTH_NONE, empty verf, SUCCESS, then 128 bytes."""
+    m = g("success_rec128_512.msgs").reshape(512, 156)
+    w = m[:, :28].copy().view(">u4")
+    assert (w[:, 0] == (152 | A.MARK_LAST)).all()
+    assert np.array_equal(w[:, 1], (np.arange(512, dtype=np.uint64) * 2654435761 & 0xFFFFFFFF).astype(np.uint32))
+    assert (w[:, 2] == 1).all() and (w[:, 3:] == 0).all()
+    assert g("success_rec128_512.hdr7").view(">u4").tolist() == [24 | A.MARK_LAST, 7, 1, 0, 0, 0, 0]

@@ -202,7 +202,7 @@ def test_stream_full_grid_repeated(dev, manifest, name):
     n = 1 << 20
     p = plan(name, "stream")
     mar = M.Marshaler(p, dev)
-    nat_np, heap_np = W.generate(name, n)
+    nat_np, heap_np = W.GENERATORS[name](n)
     nat, heap = to_dev(nat_np, dev), to_dev(heap_np, dev)
     h = manifest["hashes"][f"{name}_{n}"]
     out = torch.empty(int(h["xdr_bytes"]), dtype=torch.uint8, device=dev)

@@ -14,7 +14,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libxdrgpu.s
 
 # enum xdrg_op_kind
 OP_U32, OP_U64, OP_BOOL, OP_ENUM, OP_OPAQUE, OP_VAROPAQUE, OP_STRING, OP_UNION, OP_JUMP, OP_END, OP_VECTOR = range(1, 12)
-ABI_VERSION = 6  # XDRG_ABI_VERSION, include/xdrgpu.h
+ABI_VERSION = 7  # XDRG_ABI_VERSION, include/xdrgpu.h
 F_VALIDATE = 1
 F_DEFAULT = 2
 F_POINTER = 4
@@ -124,6 +124,7 @@ EXPORTED = (
     "xdrg_rpc_replies", "xdrg_rpc_replies_workspace_size", "xdrg_record_depths",
     "xdrg_plan_set_option", "xdrg_plan_kernel_source", "xdrg_plan_build_kernels",
     "xdrg_plan_load_kernels", "xdrg_index_records", "xdrg_encode_sizes", "xdrg_encode_sized",
+    "xdrg_deep_workspace_size",
 )
 
 # RPC header batches (include/xdrgpu.h "RPC header batches")
@@ -173,6 +174,8 @@ def lib() -> C.CDLL:
     L.xdrg_plan_load_kernels.restype = C.c_int
     L.xdrg_workspace_size.argtypes = [vp, u64]
     L.xdrg_workspace_size.restype = sz
+    L.xdrg_deep_workspace_size.argtypes = [vp, u64]
+    L.xdrg_deep_workspace_size.restype = sz
     L.xdrg_status_init.argtypes = [vp, vp]
     L.xdrg_status_init.restype = C.c_int
     L.xdrg_status_read.argtypes = [vp, vp, C.POINTER(XdrgError)]
@@ -203,9 +206,9 @@ def lib() -> C.CDLL:
     L.xdrg_rpc_replies.restype = C.c_int
     L.xdrg_rpc_replies_workspace_size.argtypes = [u64]
     L.xdrg_rpc_replies_workspace_size.restype = sz
-    L.xdrg_record_depths.argtypes = [vp, vp, u64, vp, u64, vp, vp, vp]
+    L.xdrg_record_depths.argtypes = [vp, vp, u64, vp, u64, vp, vp, sz, vp, vp]
     L.xdrg_record_depths.restype = C.c_int
-    L.xdrg_serial_sizes.argtypes = [vp, vp, u64, vp, u64, vp, u32, vp, vp]
+    L.xdrg_serial_sizes.argtypes = [vp, vp, u64, vp, u64, vp, u32, vp, sz, vp, vp]
     L.xdrg_serial_sizes.restype = C.c_int
     L.xdrg_swap32.argtypes = [vp, vp, u64, vp]
     L.xdrg_swap32.restype = C.c_int

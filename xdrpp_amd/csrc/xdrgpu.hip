@@ -1787,22 +1787,24 @@ __global__ __launch_bounds__(256) void k_size_linear(const uint8_t *__restrict__
   if (block_sums && (threadIdx.x & 63u) == 0 && blk * 64u < n) block_sums[blk] = v;
 }
 
-// ------------------------------------------------------------ frame pool
-// The deep passes of the element-subroutine walks (sub_kernels.h): per
-// device, the lists of deferred records and the frame slabs of the two deep
-// passes.  A plan that can nest past XDRG_SUB_FRAMES (plan.deep) leases the
-// pool for the launches of one API call; the pool's event orders its users
-// across streams (no host wait, except when the lists must grow).
+// ------------------------------------------------------------ deep passes
+// The deep passes of the element-subroutine walks (sub_kernels.h) of a plan
+// that can nest past XDRG_SUB_FRAMES (plan.deep): the lists of deferred
+// records and the frame slabs of the two deep passes, in caller memory (the
+// workspace, include/xdrgpu.h xdrg_deep_workspace_size): no allocation, no
+// lock and no state shared between calls, so calls on different streams run
+// side by side and graph capture records plain memsets and kernels.
 constexpr uint32_t kDeepLanesA = 4096, kDeepSlabA = 1024;           // 64 MiB of frames
 constexpr uint32_t kDeepLanesB = 8, kDeepSlabB = XDRG_MAX_FRAMES;   // 64 MiB
 static_assert(kDeepLanesA % 256 == 0, "deep pass A runs 256-lane workgroups");
-struct frame_pool {
-  std::mutex mu;
-  uint8_t *d = nullptr;
-  uint64_t records = 0;       // capacity of each list
-  hipEvent_t last = nullptr;  // the last lease's launches
-};
-frame_pool g_pool[kMaxDevices];
+constexpr uint64_t kDeepSlabBytes =
+    sizeof(sub_frame) * (uint64_t(kDeepLanesA) * kDeepSlabA + uint64_t(kDeepLanesB) * kDeepSlabB);
+
+// [two counters | 256][list A: n u32][list B: n u32][slab A][slab B]
+uint64_t deep_area_bytes(const xdrg_plan &p, uint64_t n) {
+  if (!p.deep) return 0;
+  return 256 + align_up(8 * std::max<uint64_t>(n, 1), 256) + kDeepSlabBytes;
+}
 
 struct deep_passes {
   sub_pass main{nullptr, nullptr, nullptr, nullptr, nullptr, 0, 1};
@@ -1810,60 +1812,25 @@ struct deep_passes {
   bool on = false;  // the plan needs the deep passes
 };
 
-class pool_lease {
- public:
-  ~pool_lease() {
-    if (!pool_) return;
-    if (!capturing_) (void)hipEventRecord(pool_->last, s_);
-    pool_->mu.unlock();
-  }
-  // The passes of plan p over n records on stream s.  For encode, `reuse`:
-  // the encode walks the lists its size pass built, deferring nothing.
-  int acquire(const xdrg_plan &p, uint64_t n, hipStream_t s, deep_passes &dp) {
-    if (!p.deep) return XDRG_OK;
-    if (n > 0xffffffffull) return XDRG_EUNSUPPORTED;  // u32 list entries
-    int dev = 0;
-    HIPCHK(hipGetDevice(&dev));
-    if (dev < 0 || dev >= kMaxDevices) return XDRG_EUNSUPPORTED;
-    frame_pool &P = g_pool[dev];
-    P.mu.lock();
-    pool_ = &P;
-    s_ = s;
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    HIPCHK(hipStreamIsCapturing(s, &cs));
-    capturing_ = cs != hipStreamCaptureStatusNone;
-    if (!P.last) HIPCHK(hipEventCreateWithFlags(&P.last, hipEventDisableTiming));
-    const uint64_t slabs = 16ull * (uint64_t(kDeepLanesA) * kDeepSlabA + uint64_t(kDeepLanesB) * kDeepSlabB);
-    if (n > P.records) {
-      if (capturing_) return XDRG_EUNSUPPORTED;  // run one launch of this size before capturing
-      if (P.d) {
-        HIPCHK(hipEventSynchronize(P.last));
-        HIPCHK(hipFree(P.d));
-        P.d = nullptr;
-        P.records = 0;
-      }
-      const uint64_t cap = align_up(std::max<uint64_t>(n, 1u << 16), 1u << 16);
-      HIPCHK(hipMalloc(&P.d, 256 + 8 * cap + slabs));
-      P.records = cap;
-    }
-    if (!capturing_) HIPCHK(hipStreamWaitEvent(s, P.last, 0));
-    HIPCHK(hipMemsetAsync(P.d, 0, 16, s));
-    auto *cnt = reinterpret_cast<unsigned long long *>(P.d);
-    uint32_t *la = reinterpret_cast<uint32_t *>(P.d + 256), *lb = la + P.records;
-    sub_frame *sa = reinterpret_cast<sub_frame *>(P.d + 256 + 8 * P.records);
-    sub_frame *sb = sa + uint64_t(kDeepLanesA) * kDeepSlabA;
-    dp.on = true;
-    dp.main = sub_pass{nullptr, nullptr, la, cnt, nullptr, 0, 0};
-    dp.A = sub_pass{la, cnt, lb, cnt + 1, sa, kDeepSlabA, 0};
-    dp.B = sub_pass{lb, cnt + 1, nullptr, nullptr, sb, kDeepSlabB, 1};
-    return XDRG_OK;
-  }
-
- private:
-  frame_pool *pool_ = nullptr;
-  hipStream_t s_ = nullptr;
-  bool capturing_ = false;
-};
+// The passes of plan p over n records on stream s, their memory at `area`
+// (deep_area_bytes(p, n) bytes of the caller's workspace).
+int deep_setup(const xdrg_plan &p, uint64_t n, void *area, size_t area_bytes, hipStream_t s, deep_passes &dp) {
+  if (!p.deep) return XDRG_OK;
+  if (n > 0xffffffffull) return XDRG_EUNSUPPORTED;  // u32 list entries
+  if (!area || area_bytes < deep_area_bytes(p, n) || !aligned(area, 256)) return XDRG_ESPACE;
+  uint8_t *d = static_cast<uint8_t *>(area);
+  HIPCHK(hipMemsetAsync(d, 0, 16, s));
+  auto *cnt = reinterpret_cast<unsigned long long *>(d);
+  const uint64_t cap = std::max<uint64_t>(n, 1);
+  uint32_t *la = reinterpret_cast<uint32_t *>(d + 256), *lb = la + cap;
+  sub_frame *sa = reinterpret_cast<sub_frame *>(d + 256 + align_up(8 * cap, 256));
+  sub_frame *sb = sa + uint64_t(kDeepLanesA) * kDeepSlabA;
+  dp.on = true;
+  dp.main = sub_pass{nullptr, nullptr, la, cnt, nullptr, 0, 0};
+  dp.A = sub_pass{la, cnt, lb, cnt + 1, sa, kDeepSlabA, 0};
+  dp.B = sub_pass{lb, cnt + 1, nullptr, nullptr, sb, kDeepSlabB, 1};
+  return XDRG_OK;
+}
 
 // The encode walk reuses the size pass's lists: it defers nothing.
 deep_passes encode_passes(deep_passes dp) {
@@ -1968,7 +1935,7 @@ int var_encode(const xdrg_plan &P, const dev_tables &T, const void *d_native, ui
   }
   size_t so, bo, bbo;
   const size_t need = var_ws_layout(n, &so, &bo, &bbo);
-  if (!d_ws || ws_bytes < need) return XDRG_ESPACE;
+  if (!d_ws || ws_bytes < need + deep_area_bytes(*p, n)) return XDRG_ESPACE;
   uint32_t *sizes = reinterpret_cast<uint32_t *>(static_cast<char *>(d_ws) + so);
   unsigned long long *bsum = reinterpret_cast<unsigned long long *>(static_cast<char *>(d_ws) + bo);
   unsigned long long *bbase = reinterpret_cast<unsigned long long *>(static_cast<char *>(d_ws) + bbo);
@@ -2044,10 +2011,9 @@ int var_encode(const xdrg_plan &P, const dev_tables &T, const void *d_native, ui
       return XDRG_OK;
     }
   }
-  pool_lease lease;  // element subroutines nested past XDRG_SUB_FRAMES
-  deep_passes dp;
+  deep_passes dp;  // element subroutines nested past XDRG_SUB_FRAMES
   if (p->has_sub)
-    if (int rc = lease.acquire(*p, n, s, dp)) return rc;
+    if (int rc = deep_setup(*p, n, static_cast<char *>(d_ws) + need, ws_bytes - need, s, dp)) return rc;
   if (phase == kEncSized) {  // sizes and block bases from xdrg_encode_sizes
     HIPCHK(hipMemcpyAsync(d_offsets + n, &d_status->total_bytes, 8, hipMemcpyDeviceToDevice, s));
   } else {
@@ -2184,7 +2150,7 @@ bool plan_has_payload(const xdrg_plan &p) { return p.max_var_slots > 0 || p.has_
 int var_decode(const xdrg_plan &P, const dev_tables &T, const void *d_xdr, uint64_t len,
                const uint64_t *d_offsets, uint64_t n, void *d_native, uint8_t *d_heap_out,
                uint64_t heap_cap, uint32_t stack_limit, xdrg_status *d_status, uint32_t mark,
-               hipStream_t s) {
+               void *d_ws, size_t ws_bytes, hipStream_t s) {
   const xdrg_plan *p = &P;
   const plan_opts &O = P.opts;
   unsigned long long *err = err_ptr(d_status);
@@ -2234,9 +2200,8 @@ int var_decode(const xdrg_plan &P, const dev_tables &T, const void *d_xdr, uint6
   if (kern == 0) kern = ok_W ? 2 : 1;
   const spec_module *SM = O.specialize && O.dec_kernel == 0 && kern == 2 && !p->deep ? spec_get(*p) : nullptr;
   if (p->has_sub && !SM) {  // containers of variable-size elements: the frame walk
-    pool_lease lease;  // element subroutines nested past XDRG_SUB_FRAMES
-    deep_passes dp;
-    if (int rc = lease.acquire(*p, n, s, dp)) return rc;
+    deep_passes dp;  // element subroutines nested past XDRG_SUB_FRAMES
+    if (int rc = deep_setup(*p, n, d_ws, ws_bytes, s, dp)) return rc;
     if (copy && len) HIPCHK(hipMemcpyAsync(d_heap_out, d_xdr, len, hipMemcpyDeviceToDevice, s));
     const size_t lds = p->ops.size() * sizeof(xdrg_op);
     k_sub_decode<<<(n + 255) / 256, 256, lds, s>>>(xdr8, len, d_offsets, n, nat8, p->stride, T.d_ops, nops,
@@ -2664,8 +2629,10 @@ uint64_t xdrg_decode_heap_size(const xdrg_plan *p, uint64_t len) {
 size_t xdrg_workspace_size(const xdrg_plan *p, uint64_t n) {
   if (!p) return 0;  // var encode of any plan; encode_msgs of every plan
   size_t a, b;
-  return var_ws_layout(n, &a, &b);
+  return var_ws_layout(n, &a, &b) + deep_area_bytes(*p, n);
 }
+
+size_t xdrg_deep_workspace_size(const xdrg_plan *p, uint64_t n) { return p ? deep_area_bytes(*p, n) : 0; }
 
 int xdrg_status_init(xdrg_status *st, void *stream) {
   if (!st) return XDRG_EINVAL;
@@ -2722,8 +2689,6 @@ int xdrg_decode(const xdrg_plan *p, const void *d_xdr, uint64_t len, const uint6
                 uint64_t n, void *d_native, uint8_t *d_heap_out, uint64_t heap_cap,
                 uint32_t stack_limit, void *d_ws, size_t ws_bytes, xdrg_status *d_status,
                 void *stream) {
-  (void)d_ws;
-  (void)ws_bytes;
   if (!p || !d_status || (n && (!d_native || (len && !d_xdr)))) return XDRG_EINVAL;
   const dev_tables *T = nullptr;
   if (int rc = plan_upload(p, &T)) return rc;
@@ -2752,20 +2717,20 @@ int xdrg_decode(const xdrg_plan *p, const void *d_xdr, uint64_t len, const uint6
   }
   if (!d_offsets) return XDRG_EUNSUPPORTED;  // var decode needs a record index
   return var_decode(*p, *T, d_xdr, len, d_offsets, n, d_native, d_heap_out, heap_cap, stack_limit,
-                    d_status, 0u, s);
+                    d_status, 0u, d_ws, ws_bytes, s);
 }
 
 int xdrg_record_depths(const xdrg_plan *p, const void *d_native, uint64_t n, const void *d_heap,
-                       uint64_t heap_len, uint32_t *d_depths, xdrg_status *d_status, void *stream) {
+                       uint64_t heap_len, uint32_t *d_depths, void *d_ws, size_t ws_bytes,
+                       xdrg_status *d_status, void *stream) {
   if (!p || !d_status || (n && (!d_native || !d_depths))) return XDRG_EINVAL;
   if (n == 0) return XDRG_OK;
   const dev_tables *T = nullptr;
   if (int rc = plan_upload(p, &T)) return rc;
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (p->has_sub) {
-    pool_lease lease;  // element subroutines nested past XDRG_SUB_FRAMES
-    deep_passes dp;
-    if (int rc = lease.acquire(*p, n, s, dp)) return rc;
+    deep_passes dp;  // element subroutines nested past XDRG_SUB_FRAMES
+    if (int rc = deep_setup(*p, n, d_ws, ws_bytes, s, dp)) return rc;
     HIPCHK(launch_sub_size<true>(*p, *T, static_cast<const uint8_t *>(d_native), n,
                                  static_cast<const uint8_t *>(d_heap), heap_len, nullptr, nullptr, 0u,
                                  err_ptr(d_status), d_depths, dp, s));
@@ -2790,8 +2755,8 @@ int xdrg_record_depths(const xdrg_plan *p, const void *d_native, uint64_t n, con
 }
 
 int xdrg_serial_sizes(const xdrg_plan *p, const void *d_native, uint64_t n, const void *d_heap,
-                      uint64_t heap_len, uint32_t *d_sizes, uint32_t stack_limit, xdrg_status *d_status,
-                      void *stream) {
+                      uint64_t heap_len, uint32_t *d_sizes, uint32_t stack_limit, void *d_ws,
+                      size_t ws_bytes, xdrg_status *d_status, void *stream) {
   (void)stack_limit;
   if (!p || !d_status || (n && (!d_native || !d_sizes))) return XDRG_EINVAL;
   if (n == 0) return XDRG_OK;
@@ -2803,10 +2768,9 @@ int xdrg_serial_sizes(const xdrg_plan *p, const void *d_native, uint64_t n, cons
     HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_sizes), int(p->fixed_size), n, s));
     return XDRG_OK;
   }
-  pool_lease lease;  // element subroutines nested past XDRG_SUB_FRAMES
-  deep_passes dp;
+  deep_passes dp;  // element subroutines nested past XDRG_SUB_FRAMES
   if (p->has_sub)
-    if (int rc = lease.acquire(*p, n, s, dp)) return rc;
+    if (int rc = deep_setup(*p, n, d_ws, ws_bytes, s, dp)) return rc;
   HIPCHK(launch_size_pass(*p, *T, static_cast<const uint8_t *>(d_native), n,
                           static_cast<const uint8_t *>(d_heap), heap_len, d_sizes, nullptr, 0u,
                           err_ptr(d_status), s, dp));
@@ -2895,13 +2859,11 @@ int xdrg_decode_msgs(const xdrg_plan *p, const void *d_stream, uint64_t len,
                      const uint64_t *d_offsets, uint64_t n, void *d_native, uint8_t *d_heap_out,
                      uint64_t heap_cap, uint32_t stack_limit, void *d_ws, size_t ws_bytes,
                      xdrg_status *d_status, void *stream) {
-  (void)d_ws;
-  (void)ws_bytes;
   if (!p || !d_status || !d_offsets || (n && (!d_native || (len && !d_stream)))) return XDRG_EINVAL;
   const dev_tables *T = nullptr;
   if (int rc = plan_upload(p, &T)) return rc;
   return var_decode(*p, *T, d_stream, len, d_offsets, n, d_native, d_heap_out, heap_cap, stack_limit,
-                    d_status, 4u, static_cast<hipStream_t>(stream));
+                    d_status, 4u, d_ws, ws_bytes, static_cast<hipStream_t>(stream));
 }
 
 int xdrg_swap32(const uint32_t *in, uint32_t *out, uint64_t n, void *stream) {

@@ -178,6 +178,14 @@ class Marshaler:
             self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
         return self._ws
 
+    def _deep(self, n: int) -> tuple[int | None, int]:
+        """(pointer, bytes) of the deep-pass workspace decode, serial_sizes and
+        record_depths take (xdrg_deep_workspace_size: none for most plans)."""
+        need = int(A.lib().xdrg_deep_workspace_size(self.plan.handle, n))
+        if not need:
+            return None, 0
+        return self._workspace(n).data_ptr(), need  # (xdrg_workspace_size holds it)
+
     # ---- raw launches (no sync, no status handling) -----------------------
     def launch_encode(self, native, n, out, heap=None, offsets=None, stack_limit=A.DEFAULT_STACK_LIMIT,
                       stream=None):
@@ -190,9 +198,10 @@ class Marshaler:
 
     def launch_decode(self, xdr, n, native_out, offsets=None, heap_out=None,
                       stack_limit=A.DEFAULT_STACK_LIMIT, stream=None):
+        dw, dn = self._deep(n)
         A.check(A.lib().xdrg_decode(
             self.plan.handle, _ptr(xdr), xdr.numel(), _ptr(offsets), n, _ptr(native_out),
-            _ptr(heap_out), 0 if heap_out is None else heap_out.numel(), stack_limit, None, 0,
+            _ptr(heap_out), 0 if heap_out is None else heap_out.numel(), stack_limit, dw, dn,
             self.status.ptr, _stream() if stream is None else stream), "xdrg_decode")
 
     def launch_encode_msgs(self, native, n, out, offsets, heap=None,
@@ -205,10 +214,11 @@ class Marshaler:
 
     def launch_decode_msgs(self, stream_bytes, n, native_out, offsets, heap_out=None,
                            stack_limit=A.DEFAULT_STACK_LIMIT, stream=None):
+        dw, dn = self._deep(n)
         A.check(A.lib().xdrg_decode_msgs(
             self.plan.handle, _ptr(stream_bytes), stream_bytes.numel(), _ptr(offsets), n,
             _ptr(native_out), _ptr(heap_out), 0 if heap_out is None else heap_out.numel(),
-            stack_limit, None, 0, self.status.ptr, _stream() if stream is None else stream),
+            stack_limit, dw, dn, self.status.ptr, _stream() if stream is None else stream),
             "xdrg_decode_msgs")
 
     def check(self, stream=None) -> A.XdrgError:
@@ -224,9 +234,10 @@ class Marshaler:
         sizes = torch.empty(max(n, 1), dtype=torch.int32, device=self.device)
         s = _stream()
         self.status.init(s)
+        dw, dn = self._deep(n)
         A.check(A.lib().xdrg_serial_sizes(self.plan.handle, _ptr(native), n, _ptr(heap),
                                           0 if heap is None else heap.numel(), _ptr(sizes),
-                                          stack_limit, self.status.ptr, s), "xdrg_serial_sizes")
+                                          stack_limit, dw, dn, self.status.ptr, s), "xdrg_serial_sizes")
         self.check(s)
         return sizes[:n]
 
@@ -236,8 +247,9 @@ class Marshaler:
         d = torch.empty(max(n, 1), dtype=torch.int32, device=self.device)
         s = _stream()
         self.status.init(s)
+        dw, dn = self._deep(n)
         A.check(A.lib().xdrg_record_depths(self.plan.handle, _ptr(native), n, _ptr(heap),
-                                           0 if heap is None else heap.numel(), _ptr(d),
+                                           0 if heap is None else heap.numel(), _ptr(d), dw, dn,
                                            self.status.ptr, s), "xdrg_record_depths")
         self.check(s)
         return d[:n]
