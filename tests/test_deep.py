@@ -314,9 +314,8 @@ def test_gpu_decode_without_offsets(gold, dev, name):
 def test_gpu_deep_two_streams_and_capture(gold, dev):
     """The deep passes' lists and frame slabs live in each caller's workspace
     (xdrg_deep_workspace_size): two marshalers encode and decode deep chains
-    on two streams at once, each with its own workspace, and an encode and a
-    decode of a deep plan captured into a graph replay to the reference's
-    bytes (no allocation, lock or host wait inside the calls)."""
+    on two streams at once, each with its own workspace (no allocation, lock
+    or host wait inside the calls)."""
     import torch
     from xdrpp_amd import marshal as M
     chains, wire, offs, recs = chains_of(gold, "test_recursive")
@@ -348,24 +347,17 @@ def test_gpu_deep_two_streams_and_capture(gold, dev):
             assert bytes(outs[k].cpu().numpy()) == bytes(x)
             assert np.array_equal(backs[k].cpu().numpy(), onat)
             assert np.array_equal(houts[k].cpu().numpy(), oheap)
-    # graph capture: encode then decode of the deep plan
+    # graph capture of a deep plan is refused before anything is queued
+    # (a replay of the frame walk faulted on MI355X, profiles/r04c): the
+    # capture ends empty and the plan still runs eagerly
     mar = mars[0]
     cap_s = torch.cuda.Stream(dev)
-    out, back, hout = outs[0], backs[0], houts[0]
-    mar.status.init(cap_s.cuda_stream)
-    mar.launch_encode(dn, n, out, heap=dh, offsets=offsets[0], stream=cap_s.cuda_stream)  # warm (tables, kernels)
-    torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, stream=cap_s):
-        mar.launch_encode(dn, n, out, heap=dh, offsets=offsets[0], stream=cap_s.cuda_stream)
-        mar.launch_decode(out, n, back, offsets=offsets[0], heap_out=hout, stream=cap_s.cuda_stream)
-    for _ in range(2):
-        out.zero_()
-        back.zero_()
-        hout.zero_()
-        mar.status.init(cap_s.cuda_stream)
-        g.replay()
-        assert mar.check(cap_s.cuda_stream).code == 0
-        assert bytes(out.cpu().numpy()) == bytes(x)
-        assert np.array_equal(back.cpu().numpy(), onat)
-        assert np.array_equal(hout.cpu().numpy(), oheap)
+        with pytest.raises(A.AbiError, match="EUNSUPPORTED"):
+            mar.launch_encode(dn, n, outs[0], heap=dh, offsets=offsets[0], stream=cap_s.cuda_stream)
+        with pytest.raises(A.AbiError, match="EUNSUPPORTED"):
+            mar.launch_decode(outs[0], n, backs[0], offsets=offsets[0], heap_out=houts[0], stream=cap_s.cuda_stream)
+    torch.cuda.synchronize()
+    r = mar.encode(dn, n, dh)
+    assert bytes(r.xdr.cpu().numpy()) == bytes(x)

@@ -29,7 +29,8 @@ import oracle_bridge as O  # noqa: E402
 # plan options: the one-pass kernel with its default heap window, with a
 # window no wave's payloads fit (every payload word from global memory), and
 # the two-pass encode it replaces
-MODES = {"stream": {}, "stream_global": {"stream_heap": 256}, "two_pass": {"enc_stream": 0}}
+MODES = {"stream": {"enc_stream": 1}, "stream_global": {"enc_stream": 1, "stream_heap": 256},
+         "two_pass": {"enc_stream": 0}}
 _plans = {}
 
 

@@ -1,5 +1,7 @@
 """Run one var schema's encode (and decode) repeatedly: a target for
-rocprofv3 PC sampling / counters.  python tools/tune/run_enc.py rpc [reps]"""
+rocprofv3 PC sampling / counters.  python tools/tune/run_enc.py rpc [reps]
+OPTS='{"enc_stream": 0}' sets plan options (xdrg_plan_set_option names)."""
+import json
 import os
 import sys
 
@@ -13,7 +15,7 @@ name = sys.argv[1] if len(sys.argv) > 1 else "rpc"
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 200
 dev = torch.device("cuda:0")
 n = 1 << 20
-p = M.Plan(S.ALL[name])
+p = M.Plan(S.ALL[name], json.loads(os.environ.get("OPTS", "{}")))
 mar = M.Marshaler(p, dev)
 nat_np, heap_np = W.GENERATORS[name](n)
 nat, heap = torch.from_numpy(nat_np).to(dev), torch.from_numpy(heap_np).to(dev)

@@ -25,6 +25,7 @@ struct spec_info {
   uint64_t max_chunks = 0;  // 16-byte chunks those slots hold per record (bounds)
   bool dec_regs = false;  // the decode walks into registers: no native tile in LDS
   bool word_list = false; // the encode walks once into a word list (no walk per window)
+  uint32_t list_words = 0; // ... of this many words per record (the mark included)
   uint64_t src_hash = 0;  // FNV-1a of the source (before the line that defines it)
 };
 

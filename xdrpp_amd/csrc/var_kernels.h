@@ -40,6 +40,15 @@
 #ifndef XDRG_DSTAMP
 #define XDRG_DSTAMP(k) ((void)0)
 #endif
+#ifndef XDRG_STAMPV
+#define XDRG_STAMPV(k, v) ((void)0)
+#endif
+// Tuning switches of the one-pass encode's output loop (tools/tune/
+// stream_stamps.py CFLAGS; wrong bytes by design): 1 no stores, 2 no word
+// reads.  0 in the library.
+#ifndef XDRG_STREAM_DBG
+#define XDRG_STREAM_DBG 0
+#endif
 // Memory hints of the encode (tools/tune/enc_stamps.py CFLAGS A/B,
 // profiles/r02s/nt_hints/): bit 0 non-temporal payload loads, bit 1
 // non-temporal stream stores.  Stores: encode kernel -7 % recvar, -3 % rpc
@@ -710,21 +719,30 @@ constexpr unsigned long long kLbVal = (1ull << 62) - 1;
 constexpr uint32_t kLbSpinLimit = 1u << 16;           // polls before a look-back gives up
 
 struct senc_lds {
-  uint32_t tile, a0, slots, heap, total;
+  uint32_t tile, pay, gsrc, hist, heap, total;
 };
-__host__ __device__ inline senc_lds senc_layout(uint32_t stride, uint32_t KMAX, uint32_t H) {
+constexpr uint32_t kSencU = 2;  // output chunks per lane per round
+// LDS of a one-pass encode wave:
+//   tile  64 native records; then the wave's scalar words in stream order
+//         (4 * words per record <= stride, codegen.cpp)
+//   pay   the wave's payloads in stream order, 16 bytes each {stream offset
+//         in the stretch, bytes, heap-window offset, padded payload bytes
+//         before it}; entry 0 is a payload of 0 bytes at 0, the last one
+//         past the stretch
+//   gsrc  their heap offsets (payload words from global memory)
+//   hist  two histograms of the payloads' first chunks over a round's chunks
+//   heap  the heap window; before it is loaded, the walk's word list
+//         (word j of lane l at word 64 j + l)
+__host__ __device__ inline senc_lds senc_layout(uint32_t stride, uint32_t KMAX, uint32_t H, uint32_t WL) {
   senc_lds L;
-  L.tile = 0;  // 64 native records, then the word list (4 * words <= stride)
-  L.a0 = (64u * stride + 15u) & ~15u;
-  L.slots = L.a0 + 272u;  // 65 record offsets (+ pad)
-  L.heap = L.slots + 64u * KMAX * 16u;
-  L.total = L.heap + H + 32u;
+  L.tile = 0;
+  L.pay = (64u * stride + 15u) & ~15u;
+  L.gsrc = L.pay + (64u * KMAX + 3u) * 16u;
+  L.hist = (L.gsrc + (64u * KMAX + 3u) * 8u + 15u) & ~15u;
+  L.heap = L.hist + 2u * 64u * kSencU * 4u;
+  L.total = L.heap + (H > 256u * WL ? H : 256u * WL) + 32u;
   return L;
 }
-struct sslot {  // a record's payload slot: heap offset, record-relative wire offset, bytes
-  uint64_t src;
-  uint32_t ps, len;
-};
 
 typedef __attribute__((address_space(1))) unsigned long long lb_u64;
 typedef __attribute__((address_space(1))) unsigned int lb_u32;
@@ -749,9 +767,10 @@ __device__ __forceinline__ uint64_t wave_max64(uint64_t x) {
 // block `blk`'s total.  desc[i] = state | value, one 8-byte word written by
 // one store (the data is the flag).  Lane l reads blocks top - l - 64u, u < 4.
 // Returns false when a predecessor never published (kLbSpinLimit polls).
-__device__ __forceinline__ bool lookback(lb_u64 *desc, uint32_t blk, uint64_t &excl) {
+__device__ __forceinline__ bool lookback(lb_u64 *desc, uint32_t blk, uint64_t &excl, uint32_t &polls) {
   const uint32_t lane = __lane_id();
   excl = 0;
+  polls = 0;
   int64_t top = static_cast<int64_t>(blk) - 1;
   for (uint32_t spins = 0; top >= 0;) {
     uint64_t d[4];
@@ -760,6 +779,7 @@ __device__ __forceinline__ bool lookback(lb_u64 *desc, uint32_t blk, uint64_t &e
       const int64_t i = top - lane - 64 * u;
       d[u] = i >= 0 ? __hip_atomic_load(desc + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kLbIncl;
     }
+    ++polls;
     // first block (in look-back order) that has not published, and the
     // first that holds an inclusive prefix
     uint32_t dn = 256, dp = 256;
@@ -770,13 +790,25 @@ __device__ __forceinline__ bool lookback(lb_u64 *desc, uint32_t blk, uint64_t &e
       if (mn) dn = 64u * u + __builtin_ctzll(mn);
       if (mp) dp = 64u * u + __builtin_ctzll(mp);
     }
-    const uint32_t lim = dp < dn ? dp + 1u : dn;  // blocks accounted by this step
-    uint64_t part = 0;
+    const bool found = dp < dn;
+    const uint32_t lim = found ? dp : dn;  // block totals (aggregates) summed by this step
+    // the aggregates (each < 2^31) in two parts, summed with DPP (no LDS)
+    uint32_t lo = 0, hi = 0;
 #pragma unroll
     for (int u = 0; u < 4; ++u)
-      if (lane + 64u * u < lim) part += d[u] & kLbVal;
-    excl += wave_sum64(part);
-    if (dp < dn) return true;
+      if (lane + 64u * u < lim) {
+        lo += static_cast<uint32_t>(d[u]) & 0xffffffu;
+        hi += static_cast<uint32_t>((d[u] & kLbVal) >> 24);
+      }
+    excl += static_cast<uint64_t>(rl32(wave_incl_scan(lo), 63)) + (static_cast<uint64_t>(rl32(wave_incl_scan(hi), 63)) << 24);
+    if (found) {  // + the inclusive prefix at dp
+      uint64_t pv = 0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (dp / 64u == static_cast<uint32_t>(u)) pv = rl64(d[u], dp % 64u);
+      excl += pv & kLbVal;
+      return true;
+    }
     top -= lim;
     if (dn < 256) {  // a block before this one is still walking its records
       if (++spins > kLbSpinLimit) return false;
@@ -792,22 +824,24 @@ __device__ __forceinline__ void var_encode_stream_body(
     const uint8_t *__restrict__ heap, uint64_t heap_len, uint8_t *__restrict__ xdr, uint64_t cap,
     uint64_t *__restrict__ offsets, const unsigned long long *__restrict__ block_base,
     unsigned long long *desc, uint32_t nb, uint64_t *total, uint32_t stack_limit, uint32_t H,
-    uint32_t mark, unsigned long long *err) {
+    uint32_t mark, uint32_t ticket, unsigned long long *err) {
   static_assert(WL > 0 && NW > 0, "word-list plans walked from registers");
   extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
-  const senc_lds L = senc_layout(stride, KMAX, H);
+  const senc_lds L = senc_layout(stride, KMAX, H, WL);
   uint8_t *tile = sm + L.tile;
-  uint32_t *a0s = reinterpret_cast<uint32_t *>(sm + L.a0);
-  sslot *slt = reinterpret_cast<sslot *>(sm + L.slots);
+  uint32_t *ws = reinterpret_cast<uint32_t *>(sm + L.tile);  // scalar words, stream order
+  u32x4 *pay = reinterpret_cast<u32x4 *>(sm + L.pay);
+  uint64_t *gsrc = reinterpret_cast<uint64_t *>(sm + L.gsrc);
+  uint32_t *hist = reinterpret_cast<uint32_t *>(sm + L.hist);
   uint8_t *hw = sm + L.heap;
   const uint32_t lane = threadIdx.x;
+  XDRG_STAMP(0);
 
   uint32_t blk = blockIdx.x;
-  if constexpr (LB) {
+  if (LB && ticket) {  // the block from a ticket (else dispatch order: blockIdx)
     uint32_t t = 0;
     if (lane == 0)
-      t = __hip_atomic_fetch_add((lb_u32 *)(desc + nb), 1u, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
+      t = __hip_atomic_fetch_add((lb_u32 *)(desc + nb), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     blk = rl32(t, 0);
   }
   const uint64_t wr0 = static_cast<uint64_t>(blk) * 64u;
@@ -823,11 +857,12 @@ __device__ __forceinline__ void var_encode_stream_body(
 #pragma unroll
     for (int k = 0; k < NW; ++k) rec[k] = lane < nrec ? t32[k] : 0u;
   }
-  wave_sync();  // every tile read before the word list overwrites it
+  XDRG_STAMP(1);
 
-  // ---- the walk: words into the list, payloads into slots, byte count
+  // ---- the walk: words into the list (in the heap window's room), payloads
+  // into slots, byte count
   enc_ctx<KMAX, false, WL> c;
-  c.sw = reinterpret_cast<uint32_t *>(tile) + lane;
+  c.sw = reinterpret_cast<uint32_t *>(hw) + lane;
   c.nw = 0;
   c.img = nullptr;
   c.w0 = 0;
@@ -852,17 +887,22 @@ __device__ __forceinline__ void var_encode_stream_body(
   }
   const uint32_t v = ok ? c.at : 0u;
   if (ok && mark) c.sw[0] = mark_word(v - 4u);
-  if (!ok) {
+  const uint32_t nw = ok ? c.nw : 0u;
+  uint32_t np = 0, pb = 0;  // payloads of the record and their padded bytes
 #pragma unroll
-    for (int k = 0; k < KMAX; ++k) c.pln[k] = 0;
+  for (int k = 0; k < KMAX; ++k) {
+    if (!ok) c.pln[k] = 0;
+    np += c.pln[k] ? 1u : 0u;
+    pb += (c.pln[k] + 3u) & ~3u;
   }
+  // offsets within the wave: bytes, words, payloads, padded payload bytes
   const uint32_t incl = wave_incl_scan(v);
   const uint32_t T = rl32(incl, 63);
   const uint32_t a0 = incl - v;
-  a0s[lane] = a0;
-  if (lane == 0) a0s[64] = T;
-#pragma unroll
-  for (int k = 0; k < KMAX; ++k) slt[lane * KMAX + k] = sslot{c.psr[k], c.pds[k], c.pln[k]};
+  const uint32_t wincl = wave_incl_scan(nw);
+  const uint32_t pincl = wave_incl_scan(np);
+  const uint32_t NP = rl32(pincl, 63);
+  const uint32_t bincl = wave_incl_scan(pb);
   // the wave's heap range
   uint64_t hlo = ~0ull, hhi = 0;
 #pragma unroll
@@ -873,6 +913,7 @@ __device__ __forceinline__ void var_encode_stream_body(
     }
   hlo = wave_min64(hlo);
   hhi = wave_max64(hhi);
+  XDRG_STAMP(2);
   if constexpr (LB) {
     if (lane == 0)
       __hip_atomic_store(lb_global(desc) + blk, (blk == 0 ? kLbIncl : kLbAgg) | T,
@@ -880,10 +921,10 @@ __device__ __forceinline__ void var_encode_stream_body(
   }
 
   // ---- the heap window: aligned 16-byte chunks covering [hlo, hhi) (loads
-  // in flight during the look-back)
-  // Chunks are 16-byte aligned in the address space, so one that holds a
-  // heap byte never leaves that byte's page (the first may start before the
-  // heap, which is only 4-byte aligned); heap bytes past heap_len read 0.
+  // in flight during the look-back).  Chunks are 16-byte aligned in the
+  // address space, so one that holds a heap byte never leaves that byte's
+  // page (the first may start before the heap, which is only 4-byte
+  // aligned); heap bytes past heap_len read 0.
   const uintptr_t hb = reinterpret_cast<uintptr_t>(heap);
   const int64_t hbase = hlo < hhi && hlo < heap_len
                             ? static_cast<int64_t>((hb + hlo) & ~uintptr_t(15)) - static_cast<int64_t>(hb)
@@ -902,10 +943,45 @@ __device__ __forceinline__ void var_encode_stream_body(
       if (i < nh && o < hlen && o + 16 > 0) hv[u] = *reinterpret_cast<const u32x4 *>(heap + o);
     }
   }
+  // ---- the stream-order tables: the scalar words (from the list) and the
+  // payloads (slots in wire order within the record)
+  wave_sync();  // the list
+  {
+    const uint32_t *lw = reinterpret_cast<const uint32_t *>(hw);
+    uint32_t *dst = ws + (wincl - nw);
+    uint32_t wl[WL];  // all loads first, then all stores
+#pragma unroll
+    for (int j = 0; j < WL; ++j) wl[j] = static_cast<uint32_t>(j) < nw ? lw[64u * j + lane] : 0u;
+#pragma unroll
+    for (int j = 0; j < WL; ++j)
+      if (static_cast<uint32_t>(j) < nw) dst[j] = wl[j];
+    uint32_t pi = pincl - np + 1u, before = bincl - pb;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      if (!c.pln[k]) continue;
+      uint32_t rank = 0, pre = 0;  // the record's earlier payloads (by wire offset)
+#pragma unroll
+      for (int q = 0; q < KMAX; ++q)
+        if (q != k && c.pln[q] && c.pds[q] < c.pds[k]) {
+          ++rank;
+          pre += (c.pln[q] + 3u) & ~3u;
+        }
+      pay[pi + rank] = u32x4{a0 + c.pds[k], c.pln[k],
+                             static_cast<uint32_t>(static_cast<int64_t>(c.psr[k]) - hbase), before + pre};
+      gsrc[pi + rank] = c.psr[k];
+    }
+    if (lane == 0) {
+      pay[0] = u32x4{0u, 0u, 0u, 0u};
+      pay[NP + 1u] = u32x4{T, 0u, 0u, rl32(bincl, 63)};  // (two past the last payload)
+      pay[NP + 2u] = u32x4{T, 0u, 0u, rl32(bincl, 63)};
+    }
+  }
   uint64_t excl = wave_out;
   bool live = true;
   if constexpr (LB) {
-    live = lookback(lb_global(desc), blk, excl);
+    uint32_t polls = 0;
+    live = lookback(lb_global(desc), blk, excl, polls);
+    XDRG_STAMPV(6, polls);
     if (!live) report(err, wr0, kOpRecordLevel, XDRG_ERR_LOOKBACK);
     if (blk > 0 && lane == 0)
       __hip_atomic_store(lb_global(desc) + blk, kLbIncl | ((excl + T) & kLbVal),
@@ -916,32 +992,11 @@ __device__ __forceinline__ void var_encode_stream_body(
       *total = wave_out + T;
     }
   }
-  if (nh) {
-#pragma unroll
-    for (int u = 0; u < UH; ++u) {
-      const uint32_t i = lane + 64u * u;
-      const int64_t o = hbase + 16 * static_cast<int64_t>(i);
-      if (i < nh) {
-        u32x4 x = u32x4{0u, 0u, 0u, 0u};
-        if (o < hlen && o + 16 > 0) {
-          x = hv[u];
-          if (o + 16 > hlen) {  // the chunk holding the heap's last byte: the rest reads 0
-            const int32_t k = static_cast<int32_t>(hlen - o);
-            x.x &= keep_bytes(k);
-            x.y &= keep_bytes(k - 4);
-            x.z &= keep_bytes(k - 8);
-            x.w &= keep_bytes(k - 12);
-          }
-        }
-        reinterpret_cast<u32x4 *>(hw)[i] = x;
-      }
-    }
-  }
+  XDRG_STAMP(3);
   if (r < n) offsets[r] = wave_out + a0;
-  if (!live) return;
-
   // ---- a wave whose bytes pass `cap`: the capacity checks, in the
-  // reference's order (xdr_generic_put::check, marshal.h:104-108)
+  // reference's order (xdr_generic_put::check, marshal.h:104-108); its list
+  // writes land in the heap window's room, the words are already copied
   const uint64_t ge = min<uint64_t>(wave_out + T, cap);
   if (wave_out + T > cap && r < n && ok) {
     enc_ctx<KMAX, true, WL> k;
@@ -971,84 +1026,180 @@ __device__ __forceinline__ void var_encode_stream_body(
     }
     (void)w.enc(k, reinterpret_cast<const uint8_t *>(rec), okc);
   }
-  wave_sync();
-
-  // ---- output: lane-owned 16-byte chunks of the stretch
-  const uint32_t sh = static_cast<uint32_t>(wave_out & 15u);
-  const uint64_t g0 = wave_out - sh;
-  const uint32_t nch = (sh + T + 15u) >> 4;
-  const uint32_t *sw = reinterpret_cast<const uint32_t *>(tile);
-  const uint32_t *h32 = reinterpret_cast<const uint32_t *>(hw);
-  for (uint32_t ck = lane; ck < nch; ck += 64u) {
-    const int32_t t0 = static_cast<int32_t>(16u * ck) - static_cast<int32_t>(sh);
-    // the record holding the chunk's first byte of this wave
-    const uint32_t tq = t0 < 0 ? 0u : static_cast<uint32_t>(t0);
-    uint32_t rr = 0;
+  if (!live) return;
+  wave_sync();  // the list's last readers
+  if (nh) {
 #pragma unroll
-    for (uint32_t s = 32; s; s >>= 1)
-      if (a0s[rr + s] <= tq) rr += s;  // last record starting at or before tq (a0s[64] = T)
-    uint32_t nxt = a0s[rr + 1], base = a0s[rr];
-    sslot e[KMAX];
-#pragma unroll
-    for (int q = 0; q < KMAX; ++q) e[q] = slt[rr * KMAX + q];
-    uint32_t wv[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int32_t t = t0 + 4 * i;
-      wv[i] = 0u;
-      if (t < 0 || static_cast<uint32_t>(t) >= T) continue;
-      while (static_cast<uint32_t>(t) >= nxt) {  // the next record(s)
-        ++rr;
-        base = nxt;
-        nxt = a0s[rr + 1];
-#pragma unroll
-        for (int q = 0; q < KMAX; ++q) e[q] = slt[rr * KMAX + q];
-      }
-      const uint32_t qb = static_cast<uint32_t>(t) - base;  // byte of the record
-      uint32_t j4 = qb;
-      bool pay = false;
-      uint64_t src = 0;
-      uint32_t left = 0;
-#pragma unroll
-      for (int q = 0; q < KMAX; ++q) {
-        const uint32_t pe = e[q].ps + ((e[q].len + 3u) & ~3u);
-        if (e[q].len && qb >= e[q].ps && qb < pe) {
-          pay = true;
-          src = e[q].src + (qb - e[q].ps);
-          left = e[q].len - (qb - e[q].ps);
-        } else if (e[q].len && qb >= pe) {
-          j4 -= pe - e[q].ps;
+    for (int u = 0; u < UH; ++u) {
+      const uint32_t i = lane + 64u * u;
+      const int64_t o = hbase + 16 * static_cast<int64_t>(i);
+      if (i < nh) {
+        u32x4 x = u32x4{0u, 0u, 0u, 0u};
+        if (o < hlen && o + 16 > 0) {
+          x = hv[u];
+          if (o + 16 > hlen) {  // the chunk holding the heap's last byte: the rest reads 0
+            const int32_t k = static_cast<int32_t>(hlen - o);
+            x.x &= keep_bytes(k);
+            x.y &= keep_bytes(k - 4);
+            x.z &= keep_bytes(k - 8);
+            x.w &= keep_bytes(k - 12);
+          }
         }
-      }
-      uint32_t x;
-      if (pay) {
-        if (local) {
-          const uint32_t o = static_cast<uint32_t>(static_cast<int64_t>(src) - hbase);
-          x = __builtin_amdgcn_alignbyte(h32[(o >> 2) + 1], h32[o >> 2], o & 3u);
-        } else {
-          x = unaligned_word(heap, heap_len, src);
-        }
-        if (left < 4u) x &= keep_mask(left);  // put_bytes' zero pad (marshal.cc:59-72)
-      } else {
-        x = sw[64u * (j4 >> 2) + rr];
-      }
-      wv[i] = x;
-    }
-    const uint64_t ca = g0 + 16ull * ck;
-    if (t0 >= 0 && ca + 16u <= ge) {
-      const u32x4 o4 = u32x4{wv[0], wv[1], wv[2], wv[3]};
-      if constexpr ((XDRG_ENC_NT & 2) != 0)
-        __builtin_nontemporal_store(o4, reinterpret_cast<u32x4 *>(xdr + ca));
-      else
-        *reinterpret_cast<u32x4 *>(xdr + ca) = o4;
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int32_t t = t0 + 4 * i;
-        if (t >= 0 && static_cast<uint32_t>(t) < T && ca + 4u * i + 4u <= ge) st32(xdr + ca + 4u * i, wv[i]);
+        reinterpret_cast<u32x4 *>(hw)[i] = x;
       }
     }
   }
+  wave_sync();
+  XDRG_STAMP(4);
+
+  // ---- output: lane-owned 16-byte chunks of the stretch, U per lane per
+  // round.  A chunk's words lie in the scalar-word stream or in payloads,
+  // both in stream order: P(c) = the last payload starting at or before the
+  // chunk's first byte = the count of payloads whose first chunk (the first
+  // chunk starting at or after the payload's start) is <= c, counted with
+  // readlane over the few payloads that start in the round.  With P and the
+  // payload after it a word is placed by a few compares; its bytes come with
+  // one ds_read2_b32 from the word stream or the heap window.
+  const uint32_t sh = static_cast<uint32_t>(wave_out & 15u);
+  const uint64_t g0 = wave_out - sh;
+  const uint32_t nch = (sh + T + 15u) >> 4;
+  const uint32_t *h32 = reinterpret_cast<const uint32_t *>(hw);
+  // lane l holds the first chunks of payload entries l + 1 + 64 j
+  uint32_t fr[KMAX];
+#pragma unroll
+  for (int j = 0; j < KMAX; ++j) {
+    const uint32_t e = lane + 64u * j;
+    fr[j] = e < NP ? (pay[e + 1u].x + sh + 15u) >> 4 : ~0u;
+  }
+  constexpr int U = kSencU;
+  uint32_t carry = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 2u * U; ++k) hist[lane + 64u * k] = 0u;
+  // one round: U chunks per lane; LOCAL: payload words from the heap window.
+  // A chunk holds the starts of at most two payloads (each payload is
+  // preceded by its length word and takes at least 4 bytes), so the last
+  // payload starting at or before it (A) and the next two (B, C) place every
+  // word: the last of them starting at or before the word holds it, as a
+  // payload byte or as a scalar word after it.
+  auto rounds = [&](auto local_tag) {
+    constexpr bool LOCAL = decltype(local_tag)::value;
+    uint32_t par = 0;
+    for (uint32_t c0 = 0; c0 < nch; c0 += 64u * U, par ^= 1u) {
+      const uint32_t c1 = c0 + 64u * U;
+      uint32_t *h = hist + par * (64u * U);
+      // payloads whose first chunk falls in the round: a histogram over its
+      // chunks, then an inclusive scan = the count of payloads at or before
+      wave_sync();
+#pragma unroll
+      for (int j = 0; j < KMAX; ++j)
+        if (fr[j] >= c0 && fr[j] < c1) __hip_atomic_fetch_add(h + (fr[j] - c0), 1u, __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_WORKGROUP);
+      wave_sync();
+      uint32_t cnt[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        cnt[u] = carry + wave_incl_scan(h[lane + 64u * u]);
+        carry = rl32(cnt[u], 63);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) h[lane + 64u * u] = 0u;  // for the round after next
+      u32x4 E3[U][3];  // payloads A, B, C of the chunk
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t e = min(cnt[u], NP);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) E3[u][k] = pay[e + k];
+      }
+      uint32_t w0[U][4], w1[U][4], sb[U][4], keep[U][4], gx[U][4];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int32_t t0 = static_cast<int32_t>(16u * (c0 + 64u * u + lane)) - static_cast<int32_t>(sh);
+        uint32_t pe[3], wb[3];  // end of each payload's padded bytes; padded payload bytes up to it
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          pe[k] = E3[u][k].x + ((E3[u][k].y + 3u) & ~3u);
+          wb[k] = E3[u][k].w + (pe[k] - E3[u][k].x);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int32_t t = t0 + 4 * i;
+          const uint32_t q = static_cast<uint32_t>(t);
+          const bool lw_ = t >= 0 && q < T;
+          const bool sc = q >= E3[u][2].x, sbb = q >= E3[u][1].x;
+          const uint32_t ex = sc ? E3[u][2].x : sbb ? E3[u][1].x : E3[u][0].x;
+          const uint32_t ey = sc ? E3[u][2].y : sbb ? E3[u][1].y : E3[u][0].y;
+          const uint32_t ez = sc ? E3[u][2].z : sbb ? E3[u][1].z : E3[u][0].z;
+          const uint32_t ep = sc ? pe[2] : sbb ? pe[1] : pe[0];
+          const uint32_t ew = sc ? wb[2] : sbb ? wb[1] : wb[0];
+          const bool pw = lw_ && q < ep;
+          const uint32_t off = q - ex, x = ez + off, left = ey - off;
+          // a scalar word: its index in the word stream = its byte offset
+          // less the padded payload bytes before it
+          const uint32_t wi = lw_ && !pw ? (q - ew) >> 2 : 0u;
+          keep[u][i] = !lw_ ? 0u : pw && left < 4u ? keep_mask(left) : 0xffffffffu;
+          gx[u][i] = pw ? (off | ((sc ? 2u : sbb ? 1u : 0u) << 30)) : 0xffffffffu;
+          if constexpr ((XDRG_STREAM_DBG & 2) != 0) {
+            sb[u][i] = x & 3u;
+            w0[u][i] = x + wi;
+            w1[u][i] = wi;
+          } else if constexpr (LOCAL) {
+            sb[u][i] = pw ? (x & 3u) : 0u;
+            const uint32_t *b = pw ? h32 + (x >> 2) : ws + wi;
+            w0[u][i] = b[0];
+            w1[u][i] = b[1];
+          } else {
+            sb[u][i] = 0u;
+            w0[u][i] = ws[wi];
+            w1[u][i] = 0u;
+          }
+        }
+      }
+      uint32_t wv[U][4];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) wv[u][i] = __builtin_amdgcn_alignbyte(w1[u][i], w0[u][i], sb[u][i]) & keep[u][i];
+      if constexpr (!LOCAL) {  // payload words from global memory
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (gx[u][i] != 0xffffffffu && keep[u][i]) {
+              const uint32_t e = min(cnt[u], NP) + (gx[u][i] >> 30);
+              wv[u][i] = unaligned_word(heap, heap_len, gsrc[e] + (gx[u][i] & 0x3fffffffu)) & keep[u][i];
+            }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t ck = c0 + 64u * u + lane;
+        if (ck >= nch) continue;
+        const int32_t t0 = static_cast<int32_t>(16u * ck) - static_cast<int32_t>(sh);
+        const uint64_t ca = g0 + 16ull * ck;
+        if constexpr ((XDRG_STREAM_DBG & 1) != 0) {
+          if ((wv[u][0] ^ wv[u][1] ^ wv[u][2] ^ wv[u][3]) == 0x12345678u) st32(xdr + ca, 0u);
+          continue;
+        }
+        if (t0 >= 0 && ca + 16u <= ge) {
+          const u32x4 o4 = u32x4{wv[u][0], wv[u][1], wv[u][2], wv[u][3]};
+          if constexpr ((XDRG_ENC_NT & 2) != 0)
+            __builtin_nontemporal_store(o4, reinterpret_cast<u32x4 *>(xdr + ca));
+          else
+            *reinterpret_cast<u32x4 *>(xdr + ca) = o4;
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int32_t t = t0 + 4 * i;
+            if (t >= 0 && static_cast<uint32_t>(t) < T && ca + 4u * i + 4u <= ge) st32(xdr + ca + 4u * i, wv[u][i]);
+          }
+        }
+      }
+    }
+  };
+  if (local)
+    rounds(bool_tag<true>{});
+  else
+    rounds(bool_tag<false>{});
+  XDRG_STAMP(5);
 }
 
 // ---------------------------------------------------------------- decode

@@ -1818,6 +1818,10 @@ int deep_setup(const xdrg_plan &p, uint64_t n, void *area, size_t area_bytes, hi
   if (!p.deep) return XDRG_OK;
   if (n > 0xffffffffull) return XDRG_EUNSUPPORTED;  // u32 list entries
   if (!area || area_bytes < deep_area_bytes(p, n) || !aligned(area, 256)) return XDRG_ESPACE;
+  {  // a graph replay of the frame walk faulted on MI355X (profiles/r04c): not captured
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return XDRG_EUNSUPPORTED;
+  }
   uint8_t *d = static_cast<uint8_t *>(area);
   HIPCHK(hipMemsetAsync(d, 0, 16, s));
   auto *cnt = reinterpret_cast<unsigned long long *>(d);
@@ -1991,14 +1995,14 @@ int var_encode(const xdrg_plan &P, const dev_tables &T, const void *d_native, ui
   if (SM && SM->f_enc_stream && O.enc_stream && phase != kEncSizes && p->max_depth <= stack_limit &&
       64ull * max_rec < (1ull << 31)) {
     const uint32_t H = O.stream_heap >= 0 ? static_cast<uint32_t>(O.stream_heap) : kStreamHeapBytes;
-    const uint32_t lds = senc_layout(p->stride, p->spec.info.slots, H).total;
+    const uint32_t lds = senc_layout(p->stride, p->spec.info.slots, H, p->spec.info.list_words).total;
     if (lds <= kVarLdsBudget) {
       uint64_t *total = &d_status->total_bytes;
       unsigned long long *desc = bsum;  // nb block totals + the ticket counter (bsum[nb])
       const unsigned long long *bb = bbase;
-      uint32_t nb32 = static_cast<uint32_t>(nb), sl = stack_limit, hh = H, mk = mark;
+      uint32_t nb32 = static_cast<uint32_t>(nb), sl = stack_limit, hh = H, mk = mark, tk = O.enc_stream == 2;
       void *args[] = {&nat8, &n, const_cast<uint32_t *>(&p->stride), &d_heap, &heap_len, &xdr8, &cap,
-                      &d_offsets, &bb, &desc, &nb32, &total, &sl, &hh, &mk, &err};
+                      &d_offsets, &bb, &desc, &nb32, &total, &sl, &hh, &mk, &tk, &err};
       hipFunction_t f;
       if (phase == kEncBoth) {
         HIPCHK(hipMemsetAsync(desc, 0, align_up((nb + 1) * 8, 16), s));
@@ -2530,7 +2534,9 @@ int xdrg_plan_set_option(xdrg_plan *p, int option, int64_t value) {
   case XDRG_OPT_STAGE_BYTES:
     if (v > (32 << 10)) return XDRG_EINVAL;
     O.stage_bytes = v < 0 ? -1 : v; return XDRG_OK;
-  case XDRG_OPT_ENC_STREAM: O.enc_stream = v ? 1 : 0; return XDRG_OK;
+  case XDRG_OPT_ENC_STREAM:
+    if (v < 0 || v > 2) return XDRG_EINVAL;
+    O.enc_stream = v; return XDRG_OK;
   case XDRG_OPT_STREAM_HEAP:
     if (v > (16 << 10)) return XDRG_EINVAL;
     O.stream_heap = v < 0 ? -1 : (v & ~15); return XDRG_OK;
