@@ -309,8 +309,6 @@ enum xdrg_plan_option {
                                      blocks in dispatch order), 2 the same with
                                      blocks taken from an atomic ticket, 0 (default)
                                      the size pass + scan + encode                  */
-  XDRG_OPT_STREAM_HEAP = 16,     /* the one-pass encode's LDS heap window per wave,
-                                     bytes (<= 16 KiB), -1 auto                      */
   XDRG_OPT_INDEX_FAST = 13        /* xdrg_index_records: 1 (default) the speculative
                                      chain walk first, then the call waits for its
                                      verdict and runs the list ranking only when a

@@ -29,6 +29,7 @@ from xdrpp_amd import objects as OB
 from xdrpp_amd import schemas as S
 from xdrpp_amd.xdr_types import compile_plan
 import oracle_bridge as O
+import oracle_bridge as O
 
 REF = "/root/reference"
 LINK = {"test_recursive": "next", "rp__list": "rpcb_next"}
@@ -293,6 +294,33 @@ def test_host_index_records(gold, name):
     cut = x[:int(offs[1]) + 8]
     got = M.host_index_records(plan_of(name), cut, len(chains))
     assert list(got[:2]) == list(offs[:2]) and (got[2:] == cut.size).all()
+
+
+@pytest.mark.parametrize("name", TYPES)
+def test_host_index_records_damaged(gold, name):
+    """Damaged streams: a word of some record overwritten with a large
+    length/count, a bad discriminant or a small value.  The host fallback
+    stops the chain where the restatement's index (xdro_index_records, no
+    window) does -- a length or count past its bound ends it as the device's
+    rx_len does -- and gives the same [off[k], len) tail."""
+    from xdrpp_amd import marshal as M
+    chains, wire, offs, recs = chains_of(gold, name)
+    x0 = np.frombuffer(b"".join(wire), dtype=np.uint8).copy()
+    n = len(chains)
+    cp = plan_of(name)
+    rng = np.random.default_rng(11)
+    for t in range(60):
+        x = x0.copy()
+        w = int(rng.integers(0, x.size // 4)) * 4
+        x[w:w + 4] = np.frombuffer(int(rng.choice([0xFFFFFFF0, 0x7FFF, 0x10001, 3, 1, 0])).to_bytes(4, "big"),
+                                   np.uint8)
+        want, _, rc, er = O.index_records(cp, x, n, 0xFFFFFFFF)
+        got = M.host_index_records(cp, x, n)
+        if rc == A.ERR_INDEX_LONG:  # nested past the device's frames: the
+            # restatement stops at that record, the host walks on
+            assert np.array_equal(got[:er + 1], want[:er + 1]), (t, w)
+        else:
+            assert rc == 0 and np.array_equal(got, want), (t, w)
 
 
 @pytest.mark.gpu

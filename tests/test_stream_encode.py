@@ -29,7 +29,7 @@ import oracle_bridge as O  # noqa: E402
 # plan options: the one-pass kernel with its default heap window, with a
 # window no wave's payloads fit (every payload word from global memory), and
 # the two-pass encode it replaces
-MODES = {"stream": {"enc_stream": 1}, "stream_global": {"enc_stream": 1, "stream_heap": 256},
+MODES = {"stream": {"enc_stream": 1}, "ticket": {"enc_stream": 2},
          "two_pass": {"enc_stream": 0}}
 _plans = {}
 
@@ -119,7 +119,7 @@ def _shuffled_heap(name, n, seed):
     return rec.reshape(-1), np.frombuffer(bytes(out), np.uint8).copy()
 
 
-@pytest.mark.parametrize("mode", ["stream", "stream_global"])
+@pytest.mark.parametrize("mode", ["stream", "ticket"])
 @pytest.mark.parametrize("name", ["recvar", "rpc"])
 def test_stream_shuffled_heap(dev, mode, name):
     n = 3000
@@ -130,7 +130,7 @@ def test_stream_shuffled_heap(dev, mode, name):
     assert err is None and np.array_equal(got, want) and np.array_equal(offs, woffs)
 
 
-@pytest.mark.parametrize("mode", ["stream", "stream_global"])
+@pytest.mark.parametrize("mode", ["stream", "ticket"])
 @pytest.mark.parametrize("cut", [1, 5, 16, 333])
 def test_stream_heap_cut_short(dev, mode, cut):
     """Payloads that run past heap_len read 0 there (as every encode kernel

@@ -10,8 +10,8 @@ output buffer past `cap` (the harness allocates the room; the library never
 sees the macro).  `run` attaches the code object (xdrg_plan_load_kernels),
 encodes 1M records through xdrg_encode (the look-back) and
 xdrg_encode_sized, checks the bytes against the library's, and prints the
-median cycles per phase and the wave lifetime.  HEAPS="16384 4096" runs
-the plan at those stream_heap options.  NOSTAMP=1: the same without stamps.
+median cycles per phase and the wave lifetime.  NOSTAMP=1: the same
+without stamps.
 """
 import ctypes as C
 import os
@@ -27,8 +27,7 @@ from xdrpp_amd import _abi as A, build as B, marshal as M, schemas as S  # noqa:
 OUT = os.path.join(ROOT, "tools", "tune", "_stamps_stream" + ("n" if os.environ.get("NOSTAMP") else "")
                    + os.environ.get("TAG", ""))
 NST = 8
-PHASES = ["start->tile", "walk+scan+table", "heap issue+lookback", "heap->LDS+cap", "assembly+stores"]
-HEAPS = [int(x) for x in os.environ.get("HEAPS", "-1").split()]
+PHASES = ["start->tile", "walk+scans", "tables+lookback", "cap", "assembly+stores"]
 STAMP = ("#define XDRG_STAMP(k) do { if (threadIdx.x == 0) { const unsigned long long t_ = "
          "__builtin_amdgcn_s_memtime(); *reinterpret_cast<volatile unsigned long long *>(xdr + "
          "((cap + 15ull) & ~15ull) + (static_cast<unsigned long long>(blockIdx.x) * " + str(NST) +
@@ -75,8 +74,8 @@ def run(schemas):
         ref = M.Marshaler(lib_plan, dev).encode(nat, n, heap)
         total = ref.xdr.numel()
         code = open(os.path.join(OUT, f"{name}.co"), "rb").read()
-        for hb in HEAPS:
-            plan = M.Plan(S.ALL[name], {"enc_stream": 1, "stream_heap": hb})
+        for hb in [0]:
+            plan = M.Plan(S.ALL[name], {"enc_stream": 1})
             A.check(L.xdrg_plan_load_kernels(plan.handle, code, len(code)), "load_kernels")
             mar = M.Marshaler(plan, dev)
             room = ((total + 15) // 16) * 16 + nb * NST * 8
@@ -109,7 +108,7 @@ def run(schemas):
                 mar.check(s.cuda_stream)
                 if not os.environ.get("NOCHECK"):
                     assert torch.equal(out[:total], ref.xdr), f"{name} {mode}: bytes differ"
-                line = f"{name:7s} heap={hb:6d} {mode:8s} {sorted(ts)[len(ts) // 2]:.4f} ms"
+                line = f"{name:7s} {mode:8s} {sorted(ts)[len(ts) // 2]:.4f} ms"
                 if not os.environ.get("NOSTAMP"):
                     st = out[((total + 15) // 16) * 16:].cpu().numpy().view(np.uint64).reshape(nb, NST)
                     st = st[:, :6].astype(np.int64)

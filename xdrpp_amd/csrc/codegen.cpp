@@ -1083,11 +1083,11 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
         << "(\n"
         << "    const uint8_t *native, uint64_t n, uint32_t stride, const uint8_t *heap, uint64_t heap_len,\n"
         << "    uint8_t *xdr, uint64_t cap, uint64_t *offsets, const unsigned long long *block_base,\n"
-        << "    unsigned long long *desc, uint32_t nb, uint64_t *total, uint32_t stack_limit, uint32_t H,\n"
+        << "    unsigned long long *desc, uint32_t nb, uint64_t *total, uint32_t stack_limit,\n"
         << "    uint32_t mark, uint32_t ticket, unsigned long long *err) {\n"
         << "  var_encode_stream_body<plan_walk, " << info.slots << ", " << p.stride / 4 << ", " << kwords + 1
         << ", " << (lb ? "true" : "false") << ">(plan_walk{}, native, n, stride, heap, heap_len,\n"
-        << "      xdr, cap, offsets, block_base, desc, nb, total, stack_limit, H, mark, ticket, err);\n}\n\n";
+        << "      xdr, cap, offsets, block_base, desc, nb, total, stack_limit, mark, ticket, err);\n}\n\n";
   for (int cp = 0; cp < 2; ++cp)
     s << "extern \"C\" __global__ __launch_bounds__(64) void xdrg_spec_decode" << (cp ? "_copy" : "") << "(\n"
       << "    const uint8_t *xdr, uint64_t len, const uint64_t *offsets, uint64_t n, uint8_t *native,\n"

@@ -111,7 +111,6 @@ struct plan_opts {
                            // (1: the host waits for its flag; 2: asynchronous; 0: off)
   int stage_bytes = -1;    // window decode of packed plans: LDS stage of a group's arrays
   int enc_stream = 0;      // word-list plans: 1 the one-pass encode (look-back), 0 two passes
-  int stream_heap = -1;    // one-pass encode: LDS heap window per wave (-1: automatic)
 };
 
 }  // namespace xdrg

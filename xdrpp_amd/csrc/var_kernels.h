@@ -689,25 +689,23 @@ __device__ __forceinline__ void var_encode_body(
 // xdr_to_opaque(r0..rn-1) (xdrpp/marshal.h:264-272) for word-list plans (every
 // payload takes a slot, no container loop: W::kWords > 0) in ONE kernel, with
 // no size pass and no scan.  One wave = 64 consecutive records:
-//   1. (LB) a ticket from an atomic counter names the wave's block, so every
-//      block before it belongs to a wave already running;
-//   2. the native tile (coalesced), the walk from registers into the word
+//   1. the native tile (coalesced), the walk from registers into the word
 //      list (xdr_generic_put's words, marshal.h:110-127) and the payload
 //      slots; the walk's byte counts are the sizes (xdr_size, types.h:240-244),
-//      and a wave scan of them the records' offsets within the wave;
-//   3. (LB) the wave's byte total is published at once, then a decoupled
+//      and wave scans of them, of the words and of the payloads place every
+//      record, scalar word and payload in the wave's stretch;
+//   2. (LB) the wave's byte total is published at once, then a decoupled
 //      look-back over the totals of the blocks before it (4 per lane, 256 per
-//      step) finds the wave's base -- while the loads of its heap bytes are
-//      in flight: the payloads of a wave lie in one heap range when the heap
-//      is staged in record order (every stager here does that), so the range
-//      is loaded as aligned 16-byte chunks into LDS (up to H bytes;
-//      otherwise payload words are read from global memory);
-//   4. the wave's output stretch is assembled chunk by chunk in registers --
-//      each lane owns 16-byte output chunks, consecutive lanes consecutive
-//      chunks; a chunk's words come from the word list or the heap window,
-//      found by a binary search over the records' offsets -- and leaves as
-//      aligned 16-byte stores (words at the stretch's two edges, shared with
-//      the neighbour waves, as single-word stores).
+//      step) finds the wave's base;
+//   3. the stretch is assembled 16-byte chunk by chunk in registers -- each
+//      lane owns chunks, consecutive lanes consecutive chunks: a chunk's
+//      scalar words come from the word stream in LDS, its payload words from
+//      one unaligned 16-byte global load per payload piece it holds (at most
+//      two: a payload is preceded by its length word) -- and leaves as aligned
+//      16-byte stores (words at the stretch's two edges, shared with the
+//      neighbour waves, as single-word stores).  Loads of payloads are
+//      coalesced (consecutive lanes read consecutive bytes of a payload) and
+//      need no particular heap layout.
 // Without LB (xdrg_encode_sized) the block's base comes from the size pass's
 // scan and nothing is published.  Every field check of xdr_generic_put is
 // kept: the walk runs unchecked only when the plan's depth fits the stack
@@ -719,28 +717,28 @@ constexpr unsigned long long kLbVal = (1ull << 62) - 1;
 constexpr uint32_t kLbSpinLimit = 1u << 16;           // polls before a look-back gives up
 
 struct senc_lds {
-  uint32_t tile, pay, gsrc, hist, heap, total;
+  uint32_t tile, pay, src, hist, total;
 };
 constexpr uint32_t kSencU = 2;  // output chunks per lane per round
 // LDS of a one-pass encode wave:
 //   tile  64 native records; then the wave's scalar words in stream order
 //         (4 * words per record <= stride, codegen.cpp)
 //   pay   the wave's payloads in stream order, 16 bytes each {stream offset
-//         in the stretch, bytes, heap-window offset, padded payload bytes
-//         before it}; entry 0 is a payload of 0 bytes at 0, the last one
-//         past the stretch
-//   gsrc  their heap offsets (payload words from global memory)
-//   hist  two histograms of the payloads' first chunks over a round's chunks
-//   heap  the heap window; before it is loaded, the walk's word list
-//         (word j of lane l at word 64 j + l)
-__host__ __device__ inline senc_lds senc_layout(uint32_t stride, uint32_t KMAX, uint32_t H, uint32_t WL) {
+//         in the stretch, bytes, end of the padded bytes, padded payload
+//         bytes up to that end}; entry 0 is a payload of 0 bytes at 0, the
+//         last two lie past the stretch.  Before it is built: the walk's word
+//         list (word j of lane l at word 64 j + l)
+//   src   the payloads' heap offsets
+//   hist  two histograms of the payloads' first chunks over a round's chunks;
+//         before them, the word list of a wave's capacity re-walk
+__host__ __device__ inline senc_lds senc_layout(uint32_t stride, uint32_t KMAX, uint32_t WL) {
   senc_lds L;
   L.tile = 0;
   L.pay = (64u * stride + 15u) & ~15u;
-  L.gsrc = L.pay + (64u * KMAX + 3u) * 16u;
-  L.hist = (L.gsrc + (64u * KMAX + 3u) * 8u + 15u) & ~15u;
-  L.heap = L.hist + 2u * 64u * kSencU * 4u;
-  L.total = L.heap + (H > 256u * WL ? H : 256u * WL) + 32u;
+  const uint32_t pb = (64u * KMAX + 3u) * 16u;
+  L.src = L.pay + (pb > 256u * WL ? pb : 256u * WL);
+  L.hist = (L.src + (64u * KMAX + 3u) * 8u + 15u) & ~15u;
+  L.total = L.hist + (2u * 64u * kSencU * 4u > 256u * WL ? 2u * 64u * kSencU * 4u : 256u * WL);
   return L;
 }
 
@@ -823,17 +821,16 @@ __device__ __forceinline__ void var_encode_stream_body(
     const W &w, const uint8_t *__restrict__ native, uint64_t n, uint32_t stride,
     const uint8_t *__restrict__ heap, uint64_t heap_len, uint8_t *__restrict__ xdr, uint64_t cap,
     uint64_t *__restrict__ offsets, const unsigned long long *__restrict__ block_base,
-    unsigned long long *desc, uint32_t nb, uint64_t *total, uint32_t stack_limit, uint32_t H,
+    unsigned long long *desc, uint32_t nb, uint64_t *total, uint32_t stack_limit,
     uint32_t mark, uint32_t ticket, unsigned long long *err) {
   static_assert(WL > 0 && NW > 0, "word-list plans walked from registers");
   extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
-  const senc_lds L = senc_layout(stride, KMAX, H, WL);
+  const senc_lds L = senc_layout(stride, KMAX, WL);
   uint8_t *tile = sm + L.tile;
   uint32_t *ws = reinterpret_cast<uint32_t *>(sm + L.tile);  // scalar words, stream order
   u32x4 *pay = reinterpret_cast<u32x4 *>(sm + L.pay);
-  uint64_t *gsrc = reinterpret_cast<uint64_t *>(sm + L.gsrc);
+  uint64_t *psrc = reinterpret_cast<uint64_t *>(sm + L.src);
   uint32_t *hist = reinterpret_cast<uint32_t *>(sm + L.hist);
-  uint8_t *hw = sm + L.heap;
   const uint32_t lane = threadIdx.x;
   XDRG_STAMP(0);
 
@@ -859,10 +856,10 @@ __device__ __forceinline__ void var_encode_stream_body(
   }
   XDRG_STAMP(1);
 
-  // ---- the walk: words into the list (in the heap window's room), payloads
-  // into slots, byte count
+  // ---- the walk: words into the list (in the payload table's room),
+  // payloads into slots, byte count
   enc_ctx<KMAX, false, WL> c;
-  c.sw = reinterpret_cast<uint32_t *>(hw) + lane;
+  c.sw = reinterpret_cast<uint32_t *>(sm + L.pay) + lane;
   c.nw = 0;
   c.img = nullptr;
   c.w0 = 0;
@@ -903,55 +900,23 @@ __device__ __forceinline__ void var_encode_stream_body(
   const uint32_t pincl = wave_incl_scan(np);
   const uint32_t NP = rl32(pincl, 63);
   const uint32_t bincl = wave_incl_scan(pb);
-  // the wave's heap range
-  uint64_t hlo = ~0ull, hhi = 0;
-#pragma unroll
-  for (int k = 0; k < KMAX; ++k)
-    if (c.pln[k]) {
-      hlo = min(hlo, c.psr[k]);
-      hhi = max(hhi, c.psr[k] + c.pln[k]);
-    }
-  hlo = wave_min64(hlo);
-  hhi = wave_max64(hhi);
   XDRG_STAMP(2);
   if constexpr (LB) {
     if (lane == 0)
       __hip_atomic_store(lb_global(desc) + blk, (blk == 0 ? kLbIncl : kLbAgg) | T,
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-
-  // ---- the heap window: aligned 16-byte chunks covering [hlo, hhi) (loads
-  // in flight during the look-back).  Chunks are 16-byte aligned in the
-  // address space, so one that holds a heap byte never leaves that byte's
-  // page (the first may start before the heap, which is only 4-byte
-  // aligned); heap bytes past heap_len read 0.
-  const uintptr_t hb = reinterpret_cast<uintptr_t>(heap);
-  const int64_t hbase = hlo < hhi && hlo < heap_len
-                            ? static_cast<int64_t>((hb + hlo) & ~uintptr_t(15)) - static_cast<int64_t>(hb)
-                            : 0;  // heap offset of hw[0] (-15..)
-  const uint64_t hspan = hlo < hhi ? hhi - static_cast<uint64_t>(hbase) : 0u;
-  const bool local = hlo >= hhi || (hlo < heap_len && hspan <= H);
-  const uint32_t nh = local ? static_cast<uint32_t>((hspan + 15u) >> 4) : 0u;
-  const int64_t hlen = static_cast<int64_t>(heap_len);
-  constexpr int UH = 16;
-  u32x4 hv[UH];
-  if (nh) {  // one batch: H <= 64 * UH * 16 bytes
-#pragma unroll
-    for (int u = 0; u < UH; ++u) {
-      const uint32_t i = lane + 64u * u;
-      const int64_t o = hbase + 16 * static_cast<int64_t>(i);
-      if (i < nh && o < hlen && o + 16 > 0) hv[u] = *reinterpret_cast<const u32x4 *>(heap + o);
-    }
-  }
-  // ---- the stream-order tables: the scalar words (from the list) and the
-  // payloads (slots in wire order within the record)
+  // ---- the stream-order tables: the scalar words (from the list, all
+  // loads before the stores) and the payloads (slots in wire order within
+  // the record)
   wave_sync();  // the list
   {
-    const uint32_t *lw = reinterpret_cast<const uint32_t *>(hw);
+    const uint32_t *lw = reinterpret_cast<const uint32_t *>(sm + L.pay);
     uint32_t *dst = ws + (wincl - nw);
-    uint32_t wl[WL];  // all loads first, then all stores
+    uint32_t wl[WL];
 #pragma unroll
     for (int j = 0; j < WL; ++j) wl[j] = static_cast<uint32_t>(j) < nw ? lw[64u * j + lane] : 0u;
+    wave_sync();  // every list read before the table overwrites it
 #pragma unroll
     for (int j = 0; j < WL; ++j)
       if (static_cast<uint32_t>(j) < nw) dst[j] = wl[j];
@@ -966,14 +931,16 @@ __device__ __forceinline__ void var_encode_stream_body(
           ++rank;
           pre += (c.pln[q] + 3u) & ~3u;
         }
-      pay[pi + rank] = u32x4{a0 + c.pds[k], c.pln[k],
-                             static_cast<uint32_t>(static_cast<int64_t>(c.psr[k]) - hbase), before + pre};
-      gsrc[pi + rank] = c.psr[k];
+      const uint32_t x = a0 + c.pds[k], p4 = (c.pln[k] + 3u) & ~3u;
+      pay[pi + rank] = u32x4{x, c.pln[k], x + p4, before + pre + p4};
+      psrc[pi + rank] = c.psr[k];
     }
     if (lane == 0) {
       pay[0] = u32x4{0u, 0u, 0u, 0u};
-      pay[NP + 1u] = u32x4{T, 0u, 0u, rl32(bincl, 63)};  // (two past the last payload)
-      pay[NP + 2u] = u32x4{T, 0u, 0u, rl32(bincl, 63)};
+      const uint32_t tb = rl32(bincl, 63);
+      pay[NP + 1u] = u32x4{T, 0u, T, tb};  // (two past the last payload)
+      pay[NP + 2u] = u32x4{T, 0u, T, tb};
+      psrc[0] = psrc[NP + 1u] = psrc[NP + 2u] = 0;
     }
   }
   uint64_t excl = wave_out;
@@ -996,11 +963,11 @@ __device__ __forceinline__ void var_encode_stream_body(
   if (r < n) offsets[r] = wave_out + a0;
   // ---- a wave whose bytes pass `cap`: the capacity checks, in the
   // reference's order (xdr_generic_put::check, marshal.h:104-108); its list
-  // writes land in the heap window's room, the words are already copied
+  // writes go to the histograms' room (cleared below)
   const uint64_t ge = min<uint64_t>(wave_out + T, cap);
   if (wave_out + T > cap && r < n && ok) {
     enc_ctx<KMAX, true, WL> k;
-    k.sw = c.sw;
+    k.sw = hist + lane;
     k.nw = 0;
     k.img = nullptr;
     k.w0 = 0;
@@ -1027,45 +994,22 @@ __device__ __forceinline__ void var_encode_stream_body(
     (void)w.enc(k, reinterpret_cast<const uint8_t *>(rec), okc);
   }
   if (!live) return;
-  wave_sync();  // the list's last readers
-  if (nh) {
-#pragma unroll
-    for (int u = 0; u < UH; ++u) {
-      const uint32_t i = lane + 64u * u;
-      const int64_t o = hbase + 16 * static_cast<int64_t>(i);
-      if (i < nh) {
-        u32x4 x = u32x4{0u, 0u, 0u, 0u};
-        if (o < hlen && o + 16 > 0) {
-          x = hv[u];
-          if (o + 16 > hlen) {  // the chunk holding the heap's last byte: the rest reads 0
-            const int32_t k = static_cast<int32_t>(hlen - o);
-            x.x &= keep_bytes(k);
-            x.y &= keep_bytes(k - 4);
-            x.z &= keep_bytes(k - 8);
-            x.w &= keep_bytes(k - 12);
-          }
-        }
-        reinterpret_cast<u32x4 *>(hw)[i] = x;
-      }
-    }
-  }
-  wave_sync();
   XDRG_STAMP(4);
 
   // ---- output: lane-owned 16-byte chunks of the stretch, U per lane per
   // round.  A chunk's words lie in the scalar-word stream or in payloads,
-  // both in stream order: P(c) = the last payload starting at or before the
+  // both in stream order.  A = the last payload starting at or before the
   // chunk's first byte = the count of payloads whose first chunk (the first
-  // chunk starting at or after the payload's start) is <= c, counted with
-  // readlane over the few payloads that start in the round.  With P and the
-  // payload after it a word is placed by a few compares; its bytes come with
-  // one ds_read2_b32 from the word stream or the heap window.
+  // chunk starting at or after the payload's start) is <= the chunk (a
+  // histogram over the round's chunks, scanned); a chunk holds the starts of
+  // at most two payloads (each is preceded by its length word and takes at
+  // least 4 bytes), so A and the next two (B, C) place every word: the last
+  // of them starting at or before it holds it, as a payload word or as a
+  // scalar word after it.
   const uint32_t sh = static_cast<uint32_t>(wave_out & 15u);
   const uint64_t g0 = wave_out - sh;
   const uint32_t nch = (sh + T + 15u) >> 4;
-  const uint32_t *h32 = reinterpret_cast<const uint32_t *>(hw);
-  // lane l holds the first chunks of payload entries l + 1 + 64 j
-  uint32_t fr[KMAX];
+  uint32_t fr[KMAX];  // lane l: the first chunks of payload entries l + 1 + 64 j
 #pragma unroll
   for (int j = 0; j < KMAX; ++j) {
     const uint32_t e = lane + 64u * j;
@@ -1075,130 +1019,120 @@ __device__ __forceinline__ void var_encode_stream_body(
   uint32_t carry = 0;
 #pragma unroll
   for (uint32_t k = 0; k < 2u * U; ++k) hist[lane + 64u * k] = 0u;
-  // one round: U chunks per lane; LOCAL: payload words from the heap window.
-  // A chunk holds the starts of at most two payloads (each payload is
-  // preceded by its length word and takes at least 4 bytes), so the last
-  // payload starting at or before it (A) and the next two (B, C) place every
-  // word: the last of them starting at or before the word holds it, as a
-  // payload byte or as a scalar word after it.
-  auto rounds = [&](auto local_tag) {
-    constexpr bool LOCAL = decltype(local_tag)::value;
-    uint32_t par = 0;
-    for (uint32_t c0 = 0; c0 < nch; c0 += 64u * U, par ^= 1u) {
-      const uint32_t c1 = c0 + 64u * U;
-      uint32_t *h = hist + par * (64u * U);
-      // payloads whose first chunk falls in the round: a histogram over its
-      // chunks, then an inclusive scan = the count of payloads at or before
-      wave_sync();
+  uint32_t par = 0;
+  for (uint32_t c0 = 0; c0 < nch; c0 += 64u * U, par ^= 1u) {
+    const uint32_t c1 = c0 + 64u * U;
+    uint32_t *h = hist + par * (64u * U);
+    wave_sync();
 #pragma unroll
-      for (int j = 0; j < KMAX; ++j)
-        if (fr[j] >= c0 && fr[j] < c1) __hip_atomic_fetch_add(h + (fr[j] - c0), 1u, __ATOMIC_RELAXED,
-                                                              __HIP_MEMORY_SCOPE_WORKGROUP);
-      wave_sync();
-      uint32_t cnt[U];
+    for (int j = 0; j < KMAX; ++j)
+      if (fr[j] >= c0 && fr[j] < c1)
+        __hip_atomic_fetch_add(h + (fr[j] - c0), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    wave_sync();
+    uint32_t cnt[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        cnt[u] = carry + wave_incl_scan(h[lane + 64u * u]);
-        carry = rl32(cnt[u], 63);
+    for (int u = 0; u < U; ++u) {
+      cnt[u] = carry + wave_incl_scan(h[lane + 64u * u]);
+      carry = rl32(cnt[u], 63);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) h[lane + 64u * u] = 0u;  // for the round after next
+    u32x4 E3[U][3];   // payloads A, B, C of the chunk: {x, len, padded end, padded bytes to it}
+    uint64_t S3[U][3];  // their heap offsets
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t e = min(cnt[u], NP);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        E3[u][k] = pay[e + k];
+        S3[u][k] = psrc[e + k];
+      }
+    }
+    // classify the words; one load per payload piece, at its first word
+    uint32_t sel[U][4], keep[U][4], wv[U][4];
+    u32x4 ld[U][3];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int32_t t0 = static_cast<int32_t>(16u * (c0 + 64u * u + lane)) - static_cast<int32_t>(sh);
+      int32_t first[3] = {4, 4, 4};
+#pragma unroll
+      for (int i = 3; i >= 0; --i) {
+        const int32_t t = t0 + 4 * i;
+        const uint32_t q = static_cast<uint32_t>(t);
+        const bool lw_ = t >= 0 && q < T;
+        const uint32_t k = q >= E3[u][2].x ? 2u : q >= E3[u][1].x ? 1u : 0u;
+        const uint32_t ex = k == 2u ? E3[u][2].x : k == 1u ? E3[u][1].x : E3[u][0].x;
+        const uint32_t ey = k == 2u ? E3[u][2].y : k == 1u ? E3[u][1].y : E3[u][0].y;
+        const uint32_t ez = k == 2u ? E3[u][2].z : k == 1u ? E3[u][1].z : E3[u][0].z;
+        const uint32_t ew = k == 2u ? E3[u][2].w : k == 1u ? E3[u][1].w : E3[u][0].w;
+        const bool pw = lw_ && q < ez;
+        const uint32_t left = ey - (q - ex);
+        keep[u][i] = !lw_ ? 0u : pw && left < 4u ? keep_mask(left) : 0xffffffffu;
+        sel[u][i] = pw ? k : 3u;
+#pragma unroll
+        for (int kk = 0; kk < 3; ++kk) first[kk] = pw && k == static_cast<uint32_t>(kk) ? i : first[kk];
+        // a scalar word: its index in the word stream = its byte offset less
+        // the padded payload bytes before it
+        wv[u][i] = lw_ && !pw ? ws[(q - ew) >> 2] : 0u;
       }
 #pragma unroll
-      for (int u = 0; u < U; ++u) h[lane + 64u * u] = 0u;  // for the round after next
-      u32x4 E3[U][3];  // payloads A, B, C of the chunk
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t e = min(cnt[u], NP);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) E3[u][k] = pay[e + k];
+      for (int k = 0; k < 3; ++k) {
+        ld[u][k] = u32x4{0u, 0u, 0u, 0u};
+        if (first[k] < 4) {
+          const uint64_t a = S3[u][k] + (static_cast<uint32_t>(t0 + 4 * first[k]) - E3[u][k].x);
+          // dword-aligned loads (a byte-misaligned 16-byte load is split
+          // by the address unit), shifted into place
+          const uint64_t a4 = a & ~3ull;
+          const uint32_t sb = static_cast<uint32_t>(a & 3u);
+          if (a4 + 20u <= heap_len) {
+            const u32x4 t = ld16u(heap + a4);
+            const uint32_t t4 = sb ? ld32(heap + a4 + 16u) : 0u;
+            ld[u][k] = u32x4{__builtin_amdgcn_alignbyte(t.y, t.x, sb), __builtin_amdgcn_alignbyte(t.z, t.y, sb),
+                             __builtin_amdgcn_alignbyte(t.w, t.z, sb), __builtin_amdgcn_alignbyte(t4, t.w, sb)};
+          } else {
+            ld[u][k] = heap_tail16(heap, heap_len, a);
+          }
+        }
       }
-      uint32_t w0[U][4], w1[U][4], sb[U][4], keep[U][4], gx[U][4];
+      // word i of piece k is word (i - first[k]) of its load
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int32_t t0 = static_cast<int32_t>(16u * (c0 + 64u * u + lane)) - static_cast<int32_t>(sh);
-        uint32_t pe[3], wb[3];  // end of each payload's padded bytes; padded payload bytes up to it
+      for (int i = 0; i < 4; ++i) {
+        uint32_t x = wv[u][i];
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-          pe[k] = E3[u][k].x + ((E3[u][k].y + 3u) & ~3u);
-          wb[k] = E3[u][k].w + (pe[k] - E3[u][k].x);
+          const int32_t f = first[k];
+          const u32x4 &g = ld[u][k];
+          const uint32_t y = i - f == 0 ? g.x : i - f == 1 ? g.y : i - f == 2 ? g.z : g.w;
+          x = sel[u][i] == static_cast<uint32_t>(k) ? y : x;
         }
+        wv[u][i] = x & keep[u][i];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t ck = c0 + 64u * u + lane;
+      if (ck >= nch) continue;
+      const int32_t t0 = static_cast<int32_t>(16u * ck) - static_cast<int32_t>(sh);
+      const uint64_t ca = g0 + 16ull * ck;
+      if constexpr ((XDRG_STREAM_DBG & 1) != 0) {
+        if ((wv[u][0] ^ wv[u][1] ^ wv[u][2] ^ wv[u][3]) == 0x12345678u) st32(xdr + ca, 0u);
+        continue;
+      }
+      if (t0 >= 0 && ca + 16u <= ge) {
+        const u32x4 o4 = u32x4{wv[u][0], wv[u][1], wv[u][2], wv[u][3]};
+        if constexpr ((XDRG_ENC_NT & 2) != 0)
+          __builtin_nontemporal_store(o4, reinterpret_cast<u32x4 *>(xdr + ca));
+        else
+          *reinterpret_cast<u32x4 *>(xdr + ca) = o4;
+      } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int32_t t = t0 + 4 * i;
-          const uint32_t q = static_cast<uint32_t>(t);
-          const bool lw_ = t >= 0 && q < T;
-          const bool sc = q >= E3[u][2].x, sbb = q >= E3[u][1].x;
-          const uint32_t ex = sc ? E3[u][2].x : sbb ? E3[u][1].x : E3[u][0].x;
-          const uint32_t ey = sc ? E3[u][2].y : sbb ? E3[u][1].y : E3[u][0].y;
-          const uint32_t ez = sc ? E3[u][2].z : sbb ? E3[u][1].z : E3[u][0].z;
-          const uint32_t ep = sc ? pe[2] : sbb ? pe[1] : pe[0];
-          const uint32_t ew = sc ? wb[2] : sbb ? wb[1] : wb[0];
-          const bool pw = lw_ && q < ep;
-          const uint32_t off = q - ex, x = ez + off, left = ey - off;
-          // a scalar word: its index in the word stream = its byte offset
-          // less the padded payload bytes before it
-          const uint32_t wi = lw_ && !pw ? (q - ew) >> 2 : 0u;
-          keep[u][i] = !lw_ ? 0u : pw && left < 4u ? keep_mask(left) : 0xffffffffu;
-          gx[u][i] = pw ? (off | ((sc ? 2u : sbb ? 1u : 0u) << 30)) : 0xffffffffu;
-          if constexpr ((XDRG_STREAM_DBG & 2) != 0) {
-            sb[u][i] = x & 3u;
-            w0[u][i] = x + wi;
-            w1[u][i] = wi;
-          } else if constexpr (LOCAL) {
-            sb[u][i] = pw ? (x & 3u) : 0u;
-            const uint32_t *b = pw ? h32 + (x >> 2) : ws + wi;
-            w0[u][i] = b[0];
-            w1[u][i] = b[1];
-          } else {
-            sb[u][i] = 0u;
-            w0[u][i] = ws[wi];
-            w1[u][i] = 0u;
-          }
-        }
-      }
-      uint32_t wv[U][4];
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) wv[u][i] = __builtin_amdgcn_alignbyte(w1[u][i], w0[u][i], sb[u][i]) & keep[u][i];
-      if constexpr (!LOCAL) {  // payload words from global memory
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (gx[u][i] != 0xffffffffu && keep[u][i]) {
-              const uint32_t e = min(cnt[u], NP) + (gx[u][i] >> 30);
-              wv[u][i] = unaligned_word(heap, heap_len, gsrc[e] + (gx[u][i] & 0x3fffffffu)) & keep[u][i];
-            }
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t ck = c0 + 64u * u + lane;
-        if (ck >= nch) continue;
-        const int32_t t0 = static_cast<int32_t>(16u * ck) - static_cast<int32_t>(sh);
-        const uint64_t ca = g0 + 16ull * ck;
-        if constexpr ((XDRG_STREAM_DBG & 1) != 0) {
-          if ((wv[u][0] ^ wv[u][1] ^ wv[u][2] ^ wv[u][3]) == 0x12345678u) st32(xdr + ca, 0u);
-          continue;
-        }
-        if (t0 >= 0 && ca + 16u <= ge) {
-          const u32x4 o4 = u32x4{wv[u][0], wv[u][1], wv[u][2], wv[u][3]};
-          if constexpr ((XDRG_ENC_NT & 2) != 0)
-            __builtin_nontemporal_store(o4, reinterpret_cast<u32x4 *>(xdr + ca));
-          else
-            *reinterpret_cast<u32x4 *>(xdr + ca) = o4;
-        } else {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int32_t t = t0 + 4 * i;
-            if (t >= 0 && static_cast<uint32_t>(t) < T && ca + 4u * i + 4u <= ge) st32(xdr + ca + 4u * i, wv[u][i]);
-          }
+          if (t >= 0 && static_cast<uint32_t>(t) < T && ca + 4u * i + 4u <= ge) st32(xdr + ca + 4u * i, wv[u][i]);
         }
       }
     }
-  };
-  if (local)
-    rounds(bool_tag<true>{});
-  else
-    rounds(bool_tag<false>{});
+  }
   XDRG_STAMP(5);
 }
 

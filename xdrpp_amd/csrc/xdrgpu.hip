@@ -1592,7 +1592,6 @@ __global__ void k_swap64(const uint64_t *__restrict__ in, uint64_t *__restrict__
 // ------------------------------------------------------------------ host
 constexpr uint64_t kMallBytes = 256ull << 20;  // MI355X Infinity Cache
 constexpr uint32_t kVarLdsBudget = 64u << 10;  // wave-cooperative var kernels
-constexpr uint32_t kStreamHeapBytes = 16u << 10;  // one-pass encode: heap window per wave
 uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 bool aligned(const void *p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) % a) == 0; }
 uint32_t gcd32(uint32_t a, uint32_t b) { while (b) { uint32_t t = a % b; a = b; b = t; } return a; }
@@ -1994,15 +1993,14 @@ int var_encode(const xdrg_plan &P, const dev_tables &T, const void *d_native, ui
   // plan's depth must fit the budget; a wave stays under 2^31 bytes.
   if (SM && SM->f_enc_stream && O.enc_stream && phase != kEncSizes && p->max_depth <= stack_limit &&
       64ull * max_rec < (1ull << 31)) {
-    const uint32_t H = O.stream_heap >= 0 ? static_cast<uint32_t>(O.stream_heap) : kStreamHeapBytes;
-    const uint32_t lds = senc_layout(p->stride, p->spec.info.slots, H, p->spec.info.list_words).total;
+    const uint32_t lds = senc_layout(p->stride, p->spec.info.slots, p->spec.info.list_words).total;
     if (lds <= kVarLdsBudget) {
       uint64_t *total = &d_status->total_bytes;
       unsigned long long *desc = bsum;  // nb block totals + the ticket counter (bsum[nb])
       const unsigned long long *bb = bbase;
-      uint32_t nb32 = static_cast<uint32_t>(nb), sl = stack_limit, hh = H, mk = mark, tk = O.enc_stream == 2;
+      uint32_t nb32 = static_cast<uint32_t>(nb), sl = stack_limit, mk = mark, tk = O.enc_stream == 2;
       void *args[] = {&nat8, &n, const_cast<uint32_t *>(&p->stride), &d_heap, &heap_len, &xdr8, &cap,
-                      &d_offsets, &bb, &desc, &nb32, &total, &sl, &hh, &mk, &tk, &err};
+                      &d_offsets, &bb, &desc, &nb32, &total, &sl, &mk, &tk, &err};
       hipFunction_t f;
       if (phase == kEncBoth) {
         HIPCHK(hipMemsetAsync(desc, 0, align_up((nb + 1) * 8, 16), s));
@@ -2537,9 +2535,6 @@ int xdrg_plan_set_option(xdrg_plan *p, int option, int64_t value) {
   case XDRG_OPT_ENC_STREAM:
     if (v < 0 || v > 2) return XDRG_EINVAL;
     O.enc_stream = v; return XDRG_OK;
-  case XDRG_OPT_STREAM_HEAP:
-    if (v > (16 << 10)) return XDRG_EINVAL;
-    O.stream_heap = v < 0 ? -1 : (v & ~15); return XDRG_OK;
   default: return XDRG_EINVAL;
   }
 }

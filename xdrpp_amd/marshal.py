@@ -403,8 +403,8 @@ class Marshaler:
 def host_index_records(cp, xdr: np.ndarray, n: int) -> np.ndarray:
     """The record boundaries xdr_from_opaque's walk finds in n records
     concatenated in `xdr` (marshal.h:299-306), walked on the host: lengths,
-    counts and discriminants only.  Where the bytes run out or a
-    discriminant is bad, record k gets [off[k], len) and the rest
+    counts and discriminants only.  Where the bytes run out, a length or
+    count passes its bound, or a discriminant is bad, record k gets [off[k], len) and the rest
     [len, len), so the decode reports the reference's error for record k;
     trailing bytes leave off[n] < len.  The fallback of decode() for the
     streams the device index hands back (include/xdrpp_gpu.hh
@@ -419,6 +419,12 @@ def host_index_records(cp, xdr: np.ndarray, n: int) -> np.ndarray:
     def elem_wire(e):
         k = int(e["kind"])
         return 8 if k == A.OP_U64 else ((int(e["arg0"]) + 3) & ~3) if k == A.OP_OPAQUE else 4
+
+    def enum_ok(o, v):  # xdr_traits<enum>::valid (the plan's value table)
+        if not int(o["flags"]) & A.F_VALIDATE:
+            return True
+        t = int(o["arg0"])
+        return any(int(table[t + i]) == v for i in range(int(o["arg1"])))
 
     def skip(p):  # one record from p: the end, or None
         stack = []  # [elements left, VECTOR pc]
@@ -447,11 +453,16 @@ def host_index_records(cp, xdr: np.ndarray, n: int) -> np.ndarray:
             elif k in (A.OP_VAROPAQUE, A.OP_STRING):
                 if p + 4 > L:
                     return None
-                p += 4 + ((word(p) + 3) & ~3)
+                v = word(p)
+                if v > int(o["arg0"]):  # past its bound: the chain ends here (rx_len)
+                    return None
+                p += 4 + ((v + 3) & ~3)
             elif k == A.OP_VECTOR:
                 if p + 4 > L:
                     return None
                 cnt = word(p)
+                if cnt > int(o["arg0"]):
+                    return None
                 p += 4
                 if int(o["flags"]) & A.F_SUB:
                     if cnt:
@@ -471,6 +482,8 @@ def host_index_records(cp, xdr: np.ndarray, n: int) -> np.ndarray:
                     return None
                 d = word(p)
                 p += 4
+                if not enum_ok(o, d):
+                    return None
                 tgt = None
                 for c in range(int(o["arg3"])):
                     if int(table[int(o["arg2"]) + 2 * c]) == d:
@@ -482,6 +495,10 @@ def host_index_records(cp, xdr: np.ndarray, n: int) -> np.ndarray:
                     return None
                 pc = tgt
                 continue
+            elif k == A.OP_ENUM:
+                if p + 4 > L or not enum_ok(o, word(p)):
+                    return None
+                p += 4
             else:
                 p += 4
             pc += 1
