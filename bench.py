@@ -203,8 +203,10 @@ def _ref_baseline(schema: str, n: int, threads: int, reps: int) -> dict | None:
     if out.returncode != 0:
         return {"error": out.stderr[-200:]}
     r = json.loads(out.stdout.strip().splitlines()[-1])
-    return {k: r[k] for k in ("encode_gib_s", "decode_gib_s", "to_opaque_gib_s", "encode_decode_gib_s",
-                              "threads")}
+    got = {k: r[k] for k in ("encode_gib_s", "decode_gib_s", "to_opaque_gib_s", "encode_decode_gib_s",
+                             "threads")}
+    got["encode_decode_gib_s_median"] = 2 * r["xdr_bytes"] / GIB / (r["encode_s_median"] + r["decode_s_median"])
+    return got
 
 
 def cpu_baseline(schema: str, n_records: int, threads: int = 0) -> dict:
@@ -212,7 +214,8 @@ def cpu_baseline(schema: str, n_records: int, threads: int = 0) -> dict:
     the real reference (oracle/_ref) when the tree carries it, and always
     the committed C restatement (oracle/cpu_bench.c).  One thread per host
     core (the affinity mask; also the cgroup quota when that is smaller),
-    best of `reps` over the whole batch."""
+    best of `reps` over the whole batch; the median of
+    the same runs beside it (`value_median`: the best swings with the box)."""
     cpus = host_cpus()
     counts = [threads] if threads else sorted({cpus["affinity"], cpus["cgroup_quota"] or cpus["affinity"], 1})
     reps = 5
@@ -228,8 +231,9 @@ def cpu_baseline(schema: str, n_records: int, threads: int = 0) -> dict:
     best_t = max(runs[kind], key=lambda t: runs[kind][t]["encode_decode_gib_s"])
     best = runs[kind][best_t]
     return {"value": round(best["encode_decode_gib_s"], 3), "unit": "GiB/s", "cores": best_t, "kind": kind,
+            "value_median": round(best["encode_decode_gib_s_median"], 3),
             "sample": f"{schema} x {n_records} (the whole batch): xdr_put / xdr_get streams over {best_t} "
-                      f"contiguous slices, one thread each, best of {reps}",
+                      f"contiguous slices, one thread each, best of {reps} (value_median: median)",
             "nproc": cpus["nproc"], "affinity_cpus": cpus["affinity"], "cgroup_quota_cpus": cpus["cgroup_quota"],
             "cpu_model": cpus["cpu_model"],
             "encode_gib_s": round(best["encode_gib_s"], 3), "decode_gib_s": round(best["decode_gib_s"], 3),

@@ -25,12 +25,13 @@ ROOT = os.path.dirname(HERE)
 GOLD = os.path.join(ROOT, "tests", "golden")
 BIN = os.path.join(HERE, "_ref", "ref_golden")
 
-SMALL = {"numerics": 1000, "rec128": 1024, "recvar": 1024, "rpc": 1024, "vecrec": 1024, "containertest": 1024}
+SMALL = {"numerics": 1000, "rec128": 1024, "recvar": 1024, "rpc": 1024, "vecrec": 1024, "containertest": 1024,
+         "rp_list": 1024}
 FULL = {"rec128": 1 << 20, "recvar": 1 << 20, "rpc": 1 << 20, "numerics": 1 << 16,
         "rec128_mgpu": 1 << 24}
 FULL2 = {"numerics": 1 << 20}  # second full-size entries (dict keys are unique per schema)
-MID = {"recvar": 1 << 16, "rpc": 1 << 16, "vecrec": 1 << 16, "containertest": 1 << 16}
-FULL3 = {"vecrec": 1 << 20, "containertest": 1 << 20}
+MID = {"recvar": 1 << 16, "rpc": 1 << 16, "vecrec": 1 << 16, "containertest": 1 << 16, "rp_list": 1 << 16}
+FULL3 = {"vecrec": 1 << 20, "containertest": 1 << 20, "rp_list": 1 << 20}
 EXTS = ("native", "heap", "xdr", "offsets", "msgs", "msgoffs")
 NOMSGS = {"rec128_mgpu"}  # 16M records: messages hashed only where they are tested
 

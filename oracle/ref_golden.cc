@@ -713,6 +713,7 @@ int main(int argc, char **argv) {
     else if (schema == "vecrec") { vector<vecrec> v; gen_vecrec(n, WG_SEED_VECREC, v); emit(v, pre, wm); }
     else if (schema == "containertest") { vector<testns::containertest> v; gen_containertest(n, WG_SEED_CONTAINERTEST, v); emit(v, pre, wm); }
     else if (schema == "rpc") { vector<xdr::rpc_msg> v; gen_rpc(n, WG_SEED_RPC, v); emit(v, pre, wm); }
+    else if (schema == "rp_list") { vector<xdr::rp__list> v; gen_rp_list(n, WG_SEED_RP_LIST, v); emit(v, pre, wm); }
     else die("unknown schema " + schema);
     return 0;
   }
@@ -725,6 +726,7 @@ int main(int argc, char **argv) {
     else if (schema == "vecrec") { vector<vecrec> v; gen_vecrec(n, WG_SEED_VECREC, v); depths_of(v, o); }
     else if (schema == "containertest") { vector<testns::containertest> v; gen_containertest(n, WG_SEED_CONTAINERTEST, v); depths_of(v, o); }
     else if (schema == "rpc") { vector<xdr::rpc_msg> v; gen_rpc(n, WG_SEED_RPC, v); depths_of(v, o); }
+    else if (schema == "rp_list") { vector<xdr::rp__list> v; gen_rp_list(n, WG_SEED_RP_LIST, v); depths_of(v, o); }
     else die("unknown schema " + schema);
     return 0;
   }
@@ -737,6 +739,7 @@ int main(int argc, char **argv) {
     else if (schema == "vecrec") { vector<vecrec> v; gen_vecrec(n, WG_SEED_VECREC, v); bench_one("vecrec", v, threads, reps); }
     else if (schema == "containertest") { vector<testns::containertest> v; gen_containertest(n, WG_SEED_CONTAINERTEST, v); bench_one("containertest", v, threads, reps); }
     else if (schema == "rpc") { vector<xdr::rpc_msg> v; gen_rpc(n, WG_SEED_RPC, v); bench_one("rpc", v, threads, reps); }
+    else if (schema == "rp_list") { vector<xdr::rp__list> v; gen_rp_list(n, WG_SEED_RP_LIST, v); bench_one("rp_list", v, threads, reps); }
     else die("unknown schema " + schema);
     return 0;
   }

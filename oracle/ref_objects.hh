@@ -16,6 +16,8 @@
 #include <string>
 #include <vector>
 
+static_assert(sizeof(st_rp_list) == 72, "rp_list staged node");
+
 namespace refobj {
 using std::size_t;
 using std::string;
@@ -159,6 +161,45 @@ template <typename T> [[maybe_unused]] static T bits_as(uint64_t v) {
       string s(len[k], '\0');
       for (uint32_t j = 0; j < len[k]; ++j) s[j] = char(0x61 + wg_byte(ps, r * 32 + 16 + 5 * k + j / 8, j) % 26);
       x.sarr[k] = s;
+    }
+  }
+}
+
+// rp_list (xdrpp/rpcb_prot.x:24-37, the RPCBPROC_DUMP reply list): record
+// r has k = 1 + draw(seed, r) % 4 nodes, k = WG_RP_LIST_LONG when
+// r % 65536 == 65535.  Node g (its index over the whole batch, records in
+// order): w0 = draw(ps, 8g), w1 = draw(ps, 8g + 1); r_prog = 100000 +
+// w0 % 1000, r_vers = (w0 >> 32) % 5; |r_netid| = w1 % 9, |r_addr| =
+// (w1 >> 16) % 25, |r_owner| = (w1 >> 32) % 13; byte j of r_netid from
+// payload word 8g + 2 + j/8, r_addr 8g + 3 + j/8, r_owner 8g + 6 + j/8.
+[[maybe_unused]] static uint32_t rp_list_nodes(uint64_t seed, uint64_t r) {
+  return (r % 65536u == 65535u) ? WG_RP_LIST_LONG : 1u + uint32_t(wg_draw(seed, r) % 4u);
+}
+[[maybe_unused]] static void gen_rp_list(size_t n, uint64_t seed, vector<xdr::rp__list> &v) {
+  v.clear();
+  v.resize(n);
+  const uint64_t ps = seed ^ WG_PAYLOAD_XOR;
+  uint64_t g = 0;
+  auto str = [&](xdr::xstring<> &s, uint32_t len, uint64_t w0) {
+    string t(len, '\0');
+    for (uint32_t j = 0; j < len; ++j) t[j] = char(wg_byte(ps, w0 + j / 8, j));
+    s = t;
+  };
+  for (size_t r = 0; r < n; ++r) {
+    const uint32_t k = rp_list_nodes(seed, r);
+    xdr::rp__list *cur = &v[r];
+    for (uint32_t i = 0; i < k; ++i, ++g) {
+      if (i) {
+        cur->rpcb_next.activate();
+        cur = cur->rpcb_next.get();
+      }
+      const uint64_t w0 = wg_draw(ps, 8 * g), w1 = wg_draw(ps, 8 * g + 1);
+      xdr::rpcb &m = cur->rpcb_map;
+      m.r_prog = 100000u + uint32_t(w0 % 1000u);
+      m.r_vers = uint32_t((w0 >> 32) % 5u);
+      str(m.r_netid, uint32_t(w1 % 9u), 8 * g + 2);
+      str(m.r_addr, uint32_t((w1 >> 16) % 25u), 8 * g + 3);
+      str(m.r_owner, uint32_t((w1 >> 32) % 13u), 8 * g + 6);
     }
   }
 }
@@ -357,6 +398,38 @@ struct st_containertest {
   }
 }
 
+// rp_list: per record (from an 8-byte boundary) the three strings of every
+// node in node order, then, for k > 1 nodes, the images of nodes 1..k-1
+// (8-byte aligned, contiguous); node i's rpcb_next = {image of node i + 1,
+// 1}, the last node's {0, 0}.  Node 0's image is the record.
+[[maybe_unused]] static void stage(const vector<xdr::rp__list> &v, vector<uint8_t> &nat, heap_t &h) {
+  nat.assign(v.size() * sizeof(st_rp_list), 0);
+  st_rp_list *s = reinterpret_cast<st_rp_list *>(nat.data());
+  vector<st_rp_list> img;
+  for (size_t r = 0; r < v.size(); ++r) {
+    h.b.resize((h.b.size() + 7) & ~size_t(7), 0);
+    img.clear();
+    for (const xdr::rp__list *c = &v[r]; c; c = c->rpcb_next.get()) {
+      st_rp_list e{};
+      const xdr::rpcb &m = c->rpcb_map;
+      e.rpcb_map.r_prog = m.r_prog;
+      e.rpcb_map.r_vers = m.r_vers;
+      e.rpcb_map.r_netid = h.put(reinterpret_cast<const uint8_t *>(m.r_netid.data()), m.r_netid.size());
+      e.rpcb_map.r_addr = h.put(reinterpret_cast<const uint8_t *>(m.r_addr.data()), m.r_addr.size());
+      e.rpcb_map.r_owner = h.put(reinterpret_cast<const uint8_t *>(m.r_owner.data()), m.r_owner.size());
+      img.push_back(e);
+    }
+    if (img.size() > 1) {
+      h.b.resize((h.b.size() + 7) & ~size_t(7), 0);
+      const uint64_t base = h.b.size();
+      for (size_t i = 0; i + 1 < img.size(); ++i) img[i].rpcb_next = xdrg_bytes_ref{base + 72 * i, 1, 0};
+      h.b.insert(h.b.end(), reinterpret_cast<const uint8_t *>(img.data() + 1),
+                 reinterpret_cast<const uint8_t *>(img.data() + img.size()));
+    }
+    s[r] = img[0];
+  }
+}
+
 // Equality for round-trip checks (byte-level for fixed structs).
 [[maybe_unused]] static bool same(const testns::numerics &a, const testns::numerics &b) {
   return a.b == b.b && a.i1 == b.i1 && a.i2 == b.i2 && a.i3 == b.i3 && a.i4 == b.i4 &&
@@ -371,6 +444,9 @@ struct st_containertest {
   return xdr::xdr_to_opaque(a) == xdr::xdr_to_opaque(b);
 }
 [[maybe_unused]] static bool same(const testns::containertest &a, const testns::containertest &b) {
+  return xdr::xdr_to_opaque(a) == xdr::xdr_to_opaque(b);
+}
+[[maybe_unused]] static bool same(const xdr::rp__list &a, const xdr::rp__list &b) {
   return xdr::xdr_to_opaque(a) == xdr::xdr_to_opaque(b);
 }
 [[maybe_unused]] static bool same(const xdr::rpc_msg &a, const xdr::rpc_msg &b) {

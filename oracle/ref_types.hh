@@ -5,6 +5,7 @@
 // over the AST oracle/xdrc_front.py builds; oracle/Makefile) run on
 //   tests/xdrtest.x     -> tests/xdrtest.hh   numerics, the container types
 //   xdrpp/rpc_msg.x     -> xdrpp/rpc_msg.hh   rpc_msg (also what server.h uses)
+//   xdrpp/rpcb_prot.x   -> xdrpp/rpcb_prot.hh rp__list (the rp_list batch)
 //   oracle/x/bench.x    -> bench.hh           rec128, recvar, vecrec
 //   oracle/x/validated.x -> validated.hh      numerics in testns_v
 //   oracle/x/kat.x      -> kat.hh             the SURVEY §8(c) known-answer types
@@ -14,6 +15,7 @@
 #define XDRG_REF_TYPES_HH
 #include <xdrpp/marshal.h>
 #include <xdrpp/rpc_msg.hh>
+#include <xdrpp/rpcb_prot.hh>
 
 #include "bench.hh"
 #include "kat.hh"

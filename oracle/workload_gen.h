@@ -27,6 +27,8 @@
 #define WG_SEED_REC128_MGPU 0x5EED0005ULL
 #define WG_SEED_VECREC 0x5EED0006ULL
 #define WG_SEED_CONTAINERTEST 0x5EED0008ULL
+#define WG_SEED_RP_LIST 0x5EED0009ULL
+#define WG_RP_LIST_LONG 500u       /* nodes of every 65536th list */
 #define WG_PAYLOAD_XOR 0xB10BB10BB10BB10BULL
 
 static inline uint64_t wg_draw(uint64_t seed, uint64_t i) {
@@ -70,6 +72,17 @@ typedef struct {
   uint8_t flag;
   uint8_t pad2_[7];
 } st_vecrec; /* 64 bytes */
+
+/* rp_list (xdrpp/rpcb_prot.x:24-37): each node's image is the record's
+ * layout; rpcb_next points at the next node's image in the heap */
+typedef struct {
+  uint32_t r_prog, r_vers;
+  xdrg_bytes_ref r_netid, r_addr, r_owner;
+} st_rpcb; /* 56 bytes */
+typedef struct {
+  st_rpcb rpcb_map;
+  xdrg_bytes_ref rpcb_next; /* st_rp_list[0 or 1] */
+} st_rp_list; /* 72 bytes */
 
 /* rpc record kinds drawn per record: sel = draw1 % 10 */
 enum { WG_RPC_CALL_MAX = 4, WG_RPC_SUCCESS = 5, WG_RPC_PROG_MISMATCH = 6,

@@ -35,7 +35,7 @@ def golden(schema: str, n: int, ext: str, dtype=np.uint8) -> np.ndarray:
 
 
 SMALL_N = {"numerics": 1000, "rec128": 1024, "recvar": 1024, "rpc": 1024, "vecrec": 1024,
-           "containertest": 1024}
+           "containertest": 1024, "rp_list": 1024}
 
 
 @pytest.fixture(scope="session")

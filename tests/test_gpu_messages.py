@@ -24,7 +24,7 @@ from xdrpp_amd import schemas as S  # noqa: E402
 from xdrpp_amd import workloads as W  # noqa: E402
 import oracle_bridge as O  # noqa: E402
 
-SCHEMAS = ["numerics", "rec128", "recvar", "rpc", "vecrec", "containertest"]
+SCHEMAS = ["numerics", "rec128", "recvar", "rpc", "vecrec", "containertest", "rp_list"]
 _plans = {}
 
 

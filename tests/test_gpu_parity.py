@@ -23,7 +23,7 @@ from xdrpp_amd import workloads as W  # noqa: E402
 import oracle_bridge as O  # noqa: E402
 from xdrpp_amd.xdr_types import compile_plan  # noqa: E402
 
-SCHEMAS = ["numerics", "rec128", "recvar", "rpc", "vecrec", "containertest"]
+SCHEMAS = ["numerics", "rec128", "recvar", "rpc", "vecrec", "containertest", "rp_list"]
 _plans = {}
 
 

@@ -30,7 +30,7 @@ from xdrpp_amd import schemas as S
 from xdrpp_amd import workloads as W
 from xdrpp_amd.xdr_types import compile_plan
 
-SCHEMAS = ["numerics", "rec128", "recvar", "rpc", "vecrec", "containertest"]
+SCHEMAS = ["numerics", "rec128", "recvar", "rpc", "vecrec", "containertest", "rp_list"]
 CP = {k: compile_plan(t) for k, t in S.ALL.items()}
 CP["numerics_v"] = compile_plan(S.numerics_validated)
 
@@ -49,7 +49,7 @@ def test_generator_matches_reference_fixture(name):
 
 
 @pytest.mark.parametrize("key", ["numerics_65536", "recvar_65536", "rpc_65536", "vecrec_65536",
-                                 "containertest_65536", "rec128_1048576"])
+                                 "containertest_65536", "rp_list_65536", "rec128_1048576"])
 def test_generator_matches_manifest(manifest, key):
     name, n = key.rsplit("_", 1)
     h = manifest["hashes"][key]
@@ -101,7 +101,7 @@ def test_oracle_decode_golden(name):
 
 
 @pytest.mark.parametrize("key", ["numerics_65536", "recvar_65536", "rpc_65536", "vecrec_65536",
-                                 "containertest_65536", "rec128_1048576"])
+                                 "containertest_65536", "rp_list_65536", "rec128_1048576"])
 def test_oracle_full_size_hash(manifest, key):
     name, n = key.rsplit("_", 1)
     n = int(n)

@@ -1089,8 +1089,8 @@ __device__ __forceinline__ void var_encode_stream_body(
             const uint32_t t4 = sb ? ld32(heap + a4 + 16u) : 0u;
             ld[u][k] = u32x4{__builtin_amdgcn_alignbyte(t.y, t.x, sb), __builtin_amdgcn_alignbyte(t.z, t.y, sb),
                              __builtin_amdgcn_alignbyte(t.w, t.z, sb), __builtin_amdgcn_alignbyte(t4, t.w, sb)};
-          } else {
-            ld[u][k] = heap_tail16(heap, heap_len, a);
+          } else {  // the heap's last 19 bytes
+            ld[u][k] = a + 16u <= heap_len ? ld16u(heap + a) : heap_tail16(heap, heap_len, a);
           }
         }
       }

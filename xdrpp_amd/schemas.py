@@ -116,4 +116,4 @@ rp__list = Struct("rp__list")
 rp__list.define([("rpcb_map", rpcb), ("rpcb_next", Pointer(rp__list))])
 
 ALL = {"numerics": numerics, "rec128": rec128, "recvar": recvar, "rpc": rpc_msg, "vecrec": vecrec,
-       "containertest": containertest}
+       "containertest": containertest, "rp_list": rp__list}

@@ -25,6 +25,8 @@ SEED_RPC = 0x5EED0004
 SEED_REC128_MGPU = 0x5EED0005
 SEED_VECREC = 0x5EED0006
 SEED_CONTAINERTEST = 0x5EED0008
+SEED_RP_LIST = 0x5EED0009
+RP_LIST_LONG = 500  # nodes of every 65536th list
 PAYLOAD_XOR = 0xB10BB10BB10BB10B
 
 _M1 = np.uint64(0xBF58476D1CE4E5B9)
@@ -303,8 +305,85 @@ def containertest(n: int, seed: int = SEED_CONTAINERTEST, first: int = 0) -> tup
     return buf.reshape(-1), heap
 
 
+def rp_list_nodes(n: int, seed: int = SEED_RP_LIST, first: int = 0) -> np.ndarray:
+    """Nodes of lists [first, first + n): 1 + draw(seed, r) % 4, and
+    RP_LIST_LONG for r % 65536 == 65535 (oracle/ref_objects.hh rp_list_nodes)."""
+    r = np.arange(first, first + n, dtype=np.uint64)
+    k = (np.uint64(1) + draw(seed, r) % np.uint64(4)).astype(np.int64)
+    k[(r % np.uint64(65536)) == np.uint64(65535)] = RP_LIST_LONG
+    return k
+
+
+def rp_list(n: int, seed: int = SEED_RP_LIST, first: int = 0) -> tuple[np.ndarray, np.ndarray]:
+    """Lists [first, first + n) of xdrpp/rpcb_prot.x rp__list (the
+    RPCBPROC_DUMP reply, a linked list: one element subroutine per node,
+    nested as deep as the list is long); oracle/ref_objects.hh gen_rp_list
+    and its stage().  Node g (over the batch from list 0): w0 = draw(ps, 8g),
+    w1 = draw(ps, 8g + 1); r_prog = 100000 + w0 % 1000, r_vers = (w0 >> 32)
+    % 5; string lengths w1 % 9, (w1 >> 16) % 25, (w1 >> 32) % 13, bytes from
+    payload words 8g + 2, 8g + 3.., 8g + 6...  Heap per list, from an 8-byte
+    boundary: the strings of every node, then (k > 1) the images of nodes
+    1..k-1, 8-byte aligned; node i's rpcb_next = {image of node i + 1, 1}."""
+    t = S.rp__list
+    stride = t.size  # 72
+    om, on = t.offsets["rpcb_map"], t.offsets["rpcb_next"]
+    ro = S.rpcb.offsets
+    g_first = int(rp_list_nodes(first, seed, 0).sum()) if first else 0
+    k = rp_list_nodes(n, seed, first)
+    G = int(k.sum())
+    ps = seed ^ PAYLOAD_XOR
+    g = np.arange(g_first, g_first + G, dtype=np.uint64)
+    rec = np.repeat(np.arange(n), k)                         # list of each node
+    nstart = np.zeros(n, dtype=np.int64)
+    if n > 1:
+        np.cumsum(k[:-1], out=nstart[1:])
+    pos = np.arange(G) - nstart[rec]                         # node's place in its list
+    w0 = draw(ps, np.uint64(8) * g)
+    w1 = draw(ps, np.uint64(8) * g + np.uint64(1))
+    lens = np.stack([(w1 % np.uint64(9)), (w1 >> np.uint64(16)) % np.uint64(25),
+                     (w1 >> np.uint64(32)) % np.uint64(13)], axis=1).astype(np.int64)   # (G, 3)
+    words = draw(ps, np.uint64(8) * g[:, None] + np.arange(2, 8, dtype=np.uint64)[None, :])  # (G, 6)
+    wb = words.astype("<u8").view(np.uint8).reshape(G, 48)
+    cols = np.concatenate([wb[:, 0:8], wb[:, 8:32], wb[:, 32:48]], axis=1)   # netid 8, addr 24, owner 16
+    widths = [8, 24, 16]
+    # per list: string bytes, then the element images
+    sbytes = np.bincount(rec, weights=lens.sum(axis=1), minlength=n).astype(np.int64)
+    size = np.where(k > 1, ((sbytes + 7) & ~7) + stride * (k - 1), sbytes)
+    H = np.zeros(n, dtype=np.int64)
+    if n > 1:
+        np.cumsum((size[:-1] + 7) & ~7, out=H[1:])
+    total = int(H[-1] + size[-1]) if n else 0
+    heap = np.zeros(total, dtype=np.uint8)
+    # string offsets: list base + the bytes of the list's earlier strings
+    flat = lens.reshape(-1)
+    cum = np.zeros(3 * G, dtype=np.int64)
+    if flat.size > 1:
+        np.cumsum(flat[:-1], out=cum[1:])
+    first_piece = cum.reshape(G, 3)[nstart, 0] if n else cum[:0]
+    soff = (cum.reshape(G, 3) - first_piece[rec][:, None]) + H[rec][:, None]          # (G, 3)
+    live = np.concatenate([np.arange(w)[None, :] < lens[:, j][:, None] for j, w in enumerate(widths)], axis=1)
+    dst = np.concatenate([soff[:, j][:, None] + np.arange(w)[None, :] for j, w in enumerate(widths)], axis=1)
+    heap[dst[live]] = cols[live]
+    # node images
+    E = H + ((sbytes + 7) & ~7)                               # list's first element image
+    img = np.zeros((G, stride), dtype=np.uint8)
+    _put(img, om + ro["r_prog"], (np.uint64(100000) + w0 % np.uint64(1000)), "<u4")
+    _put(img, om + ro["r_vers"], ((w0 >> np.uint64(32)) % np.uint64(5)), "<u4")
+    for j, f in enumerate(("r_netid", "r_addr", "r_owner")):
+        _put_ref(img, om + ro[f], soff[:, j], lens[:, j])
+    has_next = pos < (k[rec] - 1)
+    _put_ref(img, on, np.where(has_next, E[rec] + stride * pos, 0), has_next.astype(np.int64))
+    head = pos == 0
+    buf = img[head].reshape(-1).copy()
+    rest = ~head
+    if rest.any():
+        at = E[rec[rest]] + stride * (pos[rest] - 1)
+        heap[(at[:, None] + np.arange(stride)[None, :]).reshape(-1)] = img[rest].reshape(-1)
+    return buf, heap
+
+
 GENERATORS = {"numerics": numerics, "rec128": rec128, "recvar": recvar, "rpc": rpc, "vecrec": vecrec,
-              "containertest": containertest}
+              "containertest": containertest, "rp_list": rp_list}
 
 
 def generate(schema: str, n: int, chunk: int = 1 << 16) -> tuple[np.ndarray, np.ndarray]:
