@@ -80,7 +80,7 @@ def parse():
                     help="a file defining Engine, in place of the GPU step (tests only: "
                          "tests/bench_cpu_engine.py rehearses the multi-rank plumbing on CPU over gloo)")
     ap.add_argument("--schema", default="rec128",
-                    choices=["rec128", "numerics", "recvar", "rpc", "vecrec", "containertest"],
+                    choices=["rec128", "numerics", "recvar", "rpc", "vecrec", "containertest", "rp_list"],
                     help="rec128 is the headline; numerics/recvar/rpc measure BASELINE.json "
                          "configs 1, 3, 4; vecrec covers xvector<T>/pointer<T>")
     return ap.parse_args()
@@ -751,10 +751,15 @@ class GpuEngine:
         dec_alg = X + 8 * (n + 1) + n * S_ + X + self.element_bytes()
         spec = bool(info.specialized)  # plan-specialized kernels ran (built at warmup)
         sub = bool((plan.cp.ops["flags"] & A.F_SUB).any())  # element subroutines: the frame walk
-        size_k = ("k_sub_size" if sub and not spec else "k_size_linear" if plan_linear(plan)
-                  else "xdrg_spec_size" if spec else "k_var_size")
-        enc_k = "xdrg_spec_encode" if spec else "k_sub_encode" if sub else "k_var_encode_i"
-        dec_k = "xdrg_spec_decode_copy" if spec else "k_sub_decode" if sub else "k_var_decode_w"
+        deep = A.lib().xdrg_deep_workspace_size(plan.handle, 1) > 0  # recursive: frame walks only
+        if deep:  # the frame walks (+ their deep passes), generated or interpreted
+            size_k, enc_k, dec_k = (("xdrg_spec_sub_size", "xdrg_spec_sub_encode", "xdrg_spec_sub_decode") if spec
+                                    else ("k_sub_size", "k_sub_encode", "k_sub_decode"))
+        else:
+            size_k = ("k_sub_size" if sub and not spec else "k_size_linear" if plan_linear(plan)
+                      else "xdrg_spec_size" if spec else "k_var_size")
+            enc_k = "xdrg_spec_encode" if spec else "k_sub_encode" if sub else "k_var_encode_i"
+            dec_k = "xdrg_spec_decode_copy" if spec else "k_sub_decode" if sub else "k_var_decode_w"
         if np.mean(enc_ms) >= np.mean(dec_ms):
             return f"{size_k}+k_scan_blocks+{enc_k}", enc_alg, enc_ms
         return dec_k, dec_alg, dec_ms
@@ -763,6 +768,8 @@ class GpuEngine:
         """Native bytes of the element arrays a decode writes: count x stride
         of every xvector/pointer field of every record (plans whose
         containers hold fixed-size elements, read from the decoded records)."""
+        if self.schema == "rp_list":  # every node past a list's first is an element image
+            return int(W.rp_list_nodes(self.n).sum() - self.n) * self.plan.stride
         ops = self.plan.cp.ops
         vec = np.nonzero(ops["kind"] == A.OP_VECTOR)[0]
         if not vec.size:
@@ -880,7 +887,9 @@ def report(args, engine, world, rows, X, kern, alg_bytes, launches, enc_ms, dec_
           "rpc": "rpc_msg (xdrpp/rpc_msg.x) nested discriminated unions",
           "vecrec": "vecrec: int<16>, mismatch_info *, vpair<8> counted/optional containers",
           "containertest": "containertest (tests/xdrtest.x): u_4_12 uvec<> (variable-size union "
-                           "elements, element subroutines) + string sarr[2]"}[args.schema]
+                           "elements, element subroutines) + string sarr[2]",
+          "rp_list": "rp_list (xdrpp/rpcb_prot.x rp__list, the RPCBPROC_DUMP reply): linked lists of rpcb "
+                     "entries, 1-4 nodes, a 500-node list every 65536 (recursive element subroutine)"}[args.schema]
     line = {
         "metric": ("XDR encode+decode GiB/s (device-resident, 1M×128B records) + %HBM roofline"
                    if args.schema == "rec128" else

@@ -303,12 +303,12 @@ enum xdrg_plan_option {
                                      containers: LDS stage of a 64-record group's
                                      element arrays (written out as whole lines
                                      after the walk), -1 auto, 0 none           */
-  XDRG_OPT_ENC_STREAM = 15,      /* plan-specialized word-list plans: 1 xdrg_encode
-                                     in one kernel (each wave's base by a look-back
-                                     over the byte totals of the waves before it,
-                                     blocks in dispatch order), 2 the same with
-                                     blocks taken from an atomic ticket, 0 (default)
-                                     the size pass + scan + encode                  */
+  XDRG_OPT_ENC_STREAM = 15,      /* plan-specialized word-list plans: 1 the record
+                                     kernel walks first (its walk gives the sizes):
+                                     xdrg_encode runs no size pass and no scan, each
+                                     wave's base by a look-back over the byte totals
+                                     of the waves before it; 0 the size pass + scan
+                                     + record kernel                                */
   XDRG_OPT_INDEX_FAST = 13        /* xdrg_index_records: 1 (default) the speculative
                                      chain walk first, then the call waits for its
                                      verdict and runs the list ranking only when a

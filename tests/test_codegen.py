@@ -125,3 +125,24 @@ def test_foreign_code_object_refused(dev):
     info = A.XdrgPlanInfo()
     A.check(L.xdrg_plan_get_info(p.handle, C.byref(info)), "xdrg_plan_get_info")
     assert info.specialized == 0
+
+
+# ------------------------------------------------- recursive plans: frame walks
+@pytest.mark.parametrize("name", ["rp_list", "test_recursive"])
+def test_recursive_plans_get_frame_walks(name):
+    """A recursive plan (rp__list, test_recursive) gets the frame walks of
+    sub_kernels.h with its ops as constants: a pc switch whose scalar fields
+    fall through (one dispatch per struct), and the four frame-walk kernels
+    only; hiprtc compiles it and the plan reports it specialized."""
+    t = S.ALL.get(name) or S.CONTAINERS[name]
+    p = M.Plan(t)
+    src = source(p)
+    assert "struct plan_ops" in src and "[[fallthrough]]" in src
+    for k in ("xdrg_spec_sub_size", "xdrg_spec_sub_depth", "xdrg_spec_sub_encode", "xdrg_spec_sub_decode"):
+        assert k in src
+    assert "struct plan_walk" not in src
+    L = A.lib()
+    assert L.xdrg_plan_build_kernels(p.handle) == A.OK, L.xdrg_last_hip_error().decode()
+    info = A.XdrgPlanInfo()
+    A.check(L.xdrg_plan_get_info(p.handle, C.byref(info)), "xdrg_plan_get_info")
+    assert info.specialized == 1

@@ -29,7 +29,6 @@ from xdrpp_amd import objects as OB
 from xdrpp_amd import schemas as S
 from xdrpp_amd.xdr_types import compile_plan
 import oracle_bridge as O
-import oracle_bridge as O
 
 REF = "/root/reference"
 LINK = {"test_recursive": "next", "rp__list": "rpcb_next"}
@@ -178,14 +177,19 @@ def _dev(a, dev):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("spec", [1, 0])
 @pytest.mark.parametrize("name", TYPES)
-def test_gpu_matches_reference(gold, dev, name):
+def test_gpu_matches_reference(gold, dev, name, spec):
     """Every chain, 1 to 3000 nodes: bytes, offsets, sizes, depths and the
-    decode, through the main pass and both deep passes."""
+    decode, through the main pass and both deep passes -- on the plan's
+    generated frame walks (spec 1, codegen.cpp frame_walk_source) and on the
+    interpreter (spec 0)."""
+    import ctypes as C
     from xdrpp_amd import marshal as M
     chains, wire, offs, recs = chains_of(gold, name)
     cp, n = plan_of(name), len(chains)
-    mar = M.Marshaler(M.Plan(S.CONTAINERS.get(name) or getattr(S, name)), dev)
+    plan = M.Plan(S.CONTAINERS.get(name) or getattr(S, name), {"specialize": spec})
+    mar = M.Marshaler(plan, dev)
     nat, heap = stage_chains(name, chains)
     dn, dh = _dev(nat, dev), _dev(heap, dev)
     r = mar.encode(dn, n, dh)
@@ -204,6 +208,9 @@ def test_gpu_matches_reference(gold, dev, name):
     assert bytes(m.xdr.cpu().numpy()) == b"".join((len(w) | 0x80000000).to_bytes(4, "big") + w for w in wire)
     nat3, heap3 = mar.decode_msgs(m.xdr)
     assert unstage_chains(name, nat3.cpu().numpy(), heap3.cpu().numpy(), n) == chains
+    info = A.XdrgPlanInfo()
+    A.check(A.lib().xdrg_plan_get_info(plan.handle, C.byref(info)), "xdrg_plan_get_info")
+    assert info.specialized == spec
 
 
 @pytest.mark.gpu

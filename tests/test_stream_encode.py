@@ -1,16 +1,16 @@
-"""The one-pass encode of word-list plans (var_kernels.h
-var_encode_stream_body): xdrg_encode without a size pass or scan, each wave's
-base found by a look-back over the byte totals of the waves before it; and
-its sized half (xdrg_encode_sized over xdrg_encode_sizes' scan).
+"""The walk-first encode of word-list plans (var_kernels.h var_encode_body,
+PRE): xdrg_encode without a size pass or scan -- the record kernel's own
+walk gives the sizes and each wave's base comes from a decoupled look-back
+over the byte totals of the waves before it; and its sized half
+(xdrg_encode_sized over xdrg_encode_sizes' scan, the sizes not read).
 
 Checked against the C restatement (oracle/xdr_oracle.c, pinned to the real
 reference's bytes by tests/test_oracle.py) on the same inputs: the bytes,
-the record index and the total; heaps in record order (the heap window in
-LDS), shuffled heaps with gaps (payload words from global memory), a heap
-window too small for any wave, heaps cut short (bytes past heap_len read 0),
-capacity and bad-discriminant errors, record marks, and repeated 1M-record
-encodes (the look-back under a full grid).  Reference path:
-xdr_to_opaque, xdrpp/marshal.h:264-272 over xdr_generic_put :84-137.
+the record index and the total; heaps in record order, shuffled heaps with
+gaps, heaps cut short (bytes past heap_len read 0), capacity and
+bad-discriminant errors, record marks, and repeated 1M-record encodes (the
+look-back under a full grid).  Reference path: xdr_to_opaque,
+xdrpp/marshal.h:264-272 over xdr_generic_put :84-137.
 """
 import hashlib
 
@@ -26,11 +26,9 @@ from xdrpp_amd import schemas as S  # noqa: E402
 from xdrpp_amd import workloads as W  # noqa: E402
 import oracle_bridge as O  # noqa: E402
 
-# plan options: the one-pass kernel with its default heap window, with a
-# window no wave's payloads fit (every payload word from global memory), and
-# the two-pass encode it replaces
-MODES = {"stream": {"enc_stream": 1}, "ticket": {"enc_stream": 2},
-         "two_pass": {"enc_stream": 0}}
+# plan options: the walk-first encode and the two-pass encode (size pass +
+# scan + record kernel) it replaces
+MODES = {"stream": {"enc_stream": 1}, "two_pass": {"enc_stream": 0}}
 _plans = {}
 
 
@@ -119,7 +117,7 @@ def _shuffled_heap(name, n, seed):
     return rec.reshape(-1), np.frombuffer(bytes(out), np.uint8).copy()
 
 
-@pytest.mark.parametrize("mode", ["stream", "ticket"])
+@pytest.mark.parametrize("mode", ["stream"])
 @pytest.mark.parametrize("name", ["recvar", "rpc"])
 def test_stream_shuffled_heap(dev, mode, name):
     n = 3000
@@ -130,7 +128,7 @@ def test_stream_shuffled_heap(dev, mode, name):
     assert err is None and np.array_equal(got, want) and np.array_equal(offs, woffs)
 
 
-@pytest.mark.parametrize("mode", ["stream", "ticket"])
+@pytest.mark.parametrize("mode", ["stream"])
 @pytest.mark.parametrize("cut", [1, 5, 16, 333])
 def test_stream_heap_cut_short(dev, mode, cut):
     """Payloads that run past heap_len read 0 there (as every encode kernel
@@ -198,7 +196,7 @@ def test_stream_messages(dev, mode, name):
 @pytest.mark.parametrize("name", ["recvar", "rpc"])
 def test_stream_full_grid_repeated(dev, manifest, name):
     """1M records five times in a row through the one-pass kernel (16,384
-    waves taking tickets and looking back): the reference's sha256 every
+    waves looking back): the reference's sha256 every
     time."""
     n = 1 << 20
     p = plan(name, "stream")

@@ -18,7 +18,7 @@ sys.path.insert(0, ROOT)
 from xdrpp_amd import _abi as A, marshal as M, schemas as S, workloads as W  # noqa: E402
 
 VAR_OPTS = {
-    "two_pass": {"enc_stream": 0}, "ticket": {"enc_stream": 2}, "lb": {"enc_stream": 1}, "sized": {"enc_stream": 1},
+    "two_pass": {"enc_stream": 0}, "lb": {"enc_stream": 1}, "sized": {"enc_stream": 1},
 }
 VARIANTS = os.environ.get("VARIANTS", "two_pass lb sized").split()
 REPS = int(os.environ.get("REPS", "20"))

@@ -963,8 +963,71 @@ bool supported(const gen &g) {
 
 }  // namespace
 
+namespace {
+// Source hash line (xdrg_spec_src_hash, checked at module load) and the
+// finished source.
+void seal(std::string src, spec_info &info) {
+  uint64_t h = 1469598103934665603ull;  // FNV-1a
+  for (unsigned char ch : src) h = (h ^ ch) * 1099511628211ull;
+  info.src_hash = h;
+  src += "extern \"C\" __device__ __attribute__((used)) unsigned long long xdrg_spec_src_hash = " +
+         std::to_string(h) + "ull;\n";
+  info.source = std::move(src);
+}
+
+// Recursive plans (element subroutines entered from themselves: rp__list,
+// test_recursive): the frame walks of sub_kernels.h over this plan's ops as
+// compile-time constants.  plan_ops::visit switches on the walk's pc; an op
+// that always continues at the next one (a scalar field) falls through to
+// it, so a struct's run of fields is one dispatch, not one per field.
+bool frame_walk_source(const xdrg_plan &p, spec_info &info) {
+  std::ostringstream s;
+  s << "// Generated by libxdrgpu (codegen.cpp) from a recursive plan of " << p.ops.size()
+    << " ops: the frame walks of sub_kernels.h with the ops as constants.\n"
+    << "#include \"sub_kernels.h\"\n"
+    << "using namespace xdrg::dev;\n\n"
+    << "extern \"C\" __device__ __attribute__((used)) unsigned xdrg_spec_iface = " << kSpecIface << "u;\n\n"
+    << "struct plan_ops {\n"
+    << "  template <class F>\n"
+    << "  __device__ __forceinline__ static int visit(const xdrg_op *, uint32_t &pc, F &&step) {\n"
+    << "    int rc;\n"
+    << "    switch (pc) {\n";
+  const uint32_t n = static_cast<uint32_t>(p.ops.size());
+  for (uint32_t i = 0; i < n; ++i) {
+    const xdrg_op &o = p.ops[i];
+    const bool seq = o.kind == XDRG_OP_U32 || o.kind == XDRG_OP_U64 || o.kind == XDRG_OP_BOOL ||
+                     o.kind == XDRG_OP_ENUM || o.kind == XDRG_OP_OPAQUE || o.kind == XDRG_OP_VAROPAQUE ||
+                     o.kind == XDRG_OP_STRING;
+    std::ostringstream t;
+    t << "step(xop<" << unsigned(o.kind) << "u, " << unsigned(o.flags) << "u, " << unsigned(o.depth) << "u, "
+      << o.noff << "u, " << o.arg0 << "u, " << o.arg1 << "u, " << o.arg2 << "u, " << o.arg3 << "u, " << o.arg4
+      << "u>{})";
+    s << "    case " << i << "u:";
+    if (seq && i + 1 < n)
+      s << " rc = " << t.str() << "; if (rc != kWalkCont || pc != " << i + 1 << "u) return rc; [[fallthrough]];\n";
+    else
+      s << " return " << t.str() << ";\n";
+  }
+  s << "    default: return kWalkErr;\n"
+    << "    }\n  }\n};\n\n"
+    << "extern \"C\" __global__ __launch_bounds__(256) void xdrg_spec_sub_size(XDRG_SUB_SIZE_PARAMS) {\n"
+    << "  sub_size_kernel<false, plan_ops>(XDRG_SUB_SIZE_ARGS);\n}\n"
+    << "extern \"C\" __global__ __launch_bounds__(256) void xdrg_spec_sub_depth(XDRG_SUB_SIZE_PARAMS) {\n"
+    << "  sub_size_kernel<true, plan_ops>(XDRG_SUB_SIZE_ARGS);\n}\n"
+    << "extern \"C\" __global__ __launch_bounds__(256) void xdrg_spec_sub_encode(XDRG_SUB_ENCODE_PARAMS) {\n"
+    << "  sub_encode_kernel<plan_ops>(XDRG_SUB_ENCODE_ARGS);\n}\n"
+    << "extern \"C\" __global__ __launch_bounds__(256) void xdrg_spec_sub_decode(XDRG_SUB_DECODE_PARAMS) {\n"
+    << "  sub_decode_kernel<plan_ops>(XDRG_SUB_DECODE_ARGS);\n}\n\n";
+  info = spec_info{};
+  info.frame_walk = true;
+  seal(s.str(), info);
+  return true;
+}
+}  // namespace
+
 bool spec_source(const xdrg_plan &p, spec_info &info) {
-  if (p.path != XDRG_PATH_VAR || p.deep) return false;  // recursive / deep nesting: the frame walk
+  if (p.path != XDRG_PATH_VAR) return false;
+  if (p.deep) return frame_walk_source(p, info);  // recursive / deep nesting: the frame walk
   gen g(p);
   if (!supported(g)) return false;
   std::ostringstream body;
@@ -1076,18 +1139,18 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
     << "  var_encode_body<plan_walk, " << info.slots << ", 4, " << (regs ? p.stride / 4 : 0) << ", "
     << (kwords > 0 ? 4096 : 8192) << "u>(plan_walk{}, native, n, stride, heap, heap_len,\n"
     << "      xdr, cap, offsets, sizes, block_base, stack_limit, C, mark, err);\n}\n\n";
-  // word-list plans: the one-pass encode (look-back) and its sized half
+  // word-list plans: the encode walked first -- the wave's base by a
+  // look-back (no size pass, no scan), or from xdrg_encode_sizes' scan
   if (kwords > 0)
     for (int lb = 0; lb < 2; ++lb)
-      s << "extern \"C\" __global__ __launch_bounds__(64) void xdrg_spec_encode_stream" << (lb ? "" : "_sized")
-        << "(\n"
+      s << "extern \"C\" __global__ __launch_bounds__(64) void xdrg_spec_encode_" << (lb ? "lb" : "pre") << "(\n"
         << "    const uint8_t *native, uint64_t n, uint32_t stride, const uint8_t *heap, uint64_t heap_len,\n"
         << "    uint8_t *xdr, uint64_t cap, uint64_t *offsets, const unsigned long long *block_base,\n"
-        << "    unsigned long long *desc, uint32_t nb, uint64_t *total, uint32_t stack_limit,\n"
-        << "    uint32_t mark, uint32_t ticket, unsigned long long *err) {\n"
-        << "  var_encode_stream_body<plan_walk, " << info.slots << ", " << p.stride / 4 << ", " << kwords + 1
-        << ", " << (lb ? "true" : "false") << ">(plan_walk{}, native, n, stride, heap, heap_len,\n"
-        << "      xdr, cap, offsets, block_base, desc, nb, total, stack_limit, mark, ticket, err);\n}\n\n";
+        << "    unsigned long long *desc, uint32_t nb, uint64_t *total, uint32_t stack_limit, uint32_t C,\n"
+        << "    uint32_t mark, unsigned long long *err) {\n"
+        << "  var_encode_body<plan_walk, " << info.slots << ", 4, " << p.stride / 4 << ", 4096u, " << (lb ? 1 : 2)
+        << ">(plan_walk{}, native, n, stride, heap, heap_len,\n"
+        << "      xdr, cap, offsets, nullptr, block_base, stack_limit, C, mark, err, desc, nb, total);\n}\n\n";
   for (int cp = 0; cp < 2; ++cp)
     s << "extern \"C\" __global__ __launch_bounds__(64) void xdrg_spec_decode" << (cp ? "_copy" : "") << "(\n"
       << "    const uint8_t *xdr, uint64_t len, const uint64_t *offsets, uint64_t n, uint8_t *native,\n"
@@ -1099,13 +1162,7 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
   // the source's own hash, defined in it: spec_get refuses a code object
   // (kernel cache file, or one attached with xdrg_plan_load_kernels) that
   // was not compiled from this plan's source
-  std::string src = s.str();
-  uint64_t h = 1469598103934665603ull;  // FNV-1a
-  for (unsigned char ch : src) h = (h ^ ch) * 1099511628211ull;
-  info.src_hash = h;
-  src += "extern \"C\" __device__ __attribute__((used)) unsigned long long xdrg_spec_src_hash = " +
-         std::to_string(h) + "ull;\n";
-  info.source = std::move(src);
+  seal(s.str(), info);
   return true;
 }
 

@@ -180,10 +180,21 @@ const spec_module *spec_get(const xdrg_plan &cp) {
   if (hipModuleLoadData(&m, s.code.data()) != hipSuccess)
     return fail(nullptr, "specialized kernels: the code object does not load on this device");
   spec_module &d = s.dev[dev];
+  if (s.info.frame_walk) {  // a recursive plan: the frame walks only
+    hipFunction_t g[4] = {};
+    const char *gn[4] = {"xdrg_spec_sub_size", "xdrg_spec_sub_depth", "xdrg_spec_sub_encode", "xdrg_spec_sub_decode"};
+    for (int i = 0; i < 4; ++i)
+      if (hipModuleGetFunction(&g[i], m, gn[i]) != hipSuccess)
+        return fail(m, "specialized kernels: the code object lacks a frame walk");
+    d.f_sub_size = g[0];
+    d.f_sub_depth = g[1];
+    d.f_sub_enc = g[2];
+    d.f_sub_dec = g[3];
+  }
   hipFunction_t f[6] = {};
   const char *names[6] = {"xdrg_spec_size", "xdrg_spec_encode", "xdrg_spec_decode", "xdrg_spec_decode_copy",
                           "xdrg_spec_ix_seg", "xdrg_spec_rxs_walk"};
-  for (int i = 0; i < 6; ++i)
+  for (int i = 0; i < 6 && !s.info.frame_walk; ++i)
     if (hipModuleGetFunction(&f[i], m, names[i]) != hipSuccess)
       return fail(m, "specialized kernels: the code object lacks a kernel");
   // a code object of another kernel interface (an older build's AOT file),
@@ -207,13 +218,13 @@ const spec_module *spec_get(const xdrg_plan &cp) {
   d.f_dec_copy = f[3];
   d.f_ix_seg = f[4];
   d.f_rxs_walk = f[5];
-  if (s.info.word_list) {  // the one-pass encode, generated for word-list plans only
+  if (s.info.word_list) {  // the walk-first encode, generated for word-list plans only
     hipFunction_t a = nullptr, b = nullptr;
-    if (hipModuleGetFunction(&a, m, "xdrg_spec_encode_stream") != hipSuccess ||
-        hipModuleGetFunction(&b, m, "xdrg_spec_encode_stream_sized") != hipSuccess)
-      return fail(m, "specialized kernels: the code object lacks the one-pass encode");
-    d.f_enc_stream = a;
-    d.f_enc_stream_sized = b;
+    if (hipModuleGetFunction(&a, m, "xdrg_spec_encode_lb") != hipSuccess ||
+        hipModuleGetFunction(&b, m, "xdrg_spec_encode_pre") != hipSuccess)
+      return fail(m, "specialized kernels: the code object lacks the walk-first encode");
+    d.f_enc_lb = a;
+    d.f_enc_pre = b;
   }
   s.loaded[dev].store(true, std::memory_order_release);
   return &d;

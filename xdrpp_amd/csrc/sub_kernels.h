@@ -41,7 +41,17 @@
 //
 // Included by xdrgpu.hip after its element helpers (load_ops, union_target,
 // enc_vector_elems, dec_vector_elems).
+//
+// Each walk visits one op per step through an op policy OPS::visit(ops, pc,
+// step): rt_ops hands it the plan op from LDS (the library's kernels,
+// xdrgpu.hip); a generated module's plan_ops (codegen.cpp, recursive plans)
+// switches on pc to the op as compile-time constants, and lets a scalar op
+// fall through to the next one, so a straight run of fields is one step.
 #pragma once
+#include "elem_kernels.h"
+
+namespace xdrg {
+namespace dev {
 
 constexpr uint32_t kSubFrames = XDRG_SUB_FRAMES;  // private frames of the main pass
 constexpr uint32_t kReported = 0x100;  // decode: the element walk reported the error
@@ -78,7 +88,25 @@ struct sub_pass {
   uint32_t last;                   // 1: running out of frames is xdr_stack_overflow
 };
 
-enum : int { kWalkOk = 0, kWalkErr = 1, kWalkFull = 2 };
+enum : int { kWalkCont = -1, kWalkOk = 0, kWalkErr = 1, kWalkFull = 2 };
+
+// The interpreted op policy: the op from the plan table (LDS).
+struct rt_ops {
+  template <class F>
+  __device__ __forceinline__ static int visit(const xdrg_op *__restrict__ ops, uint32_t &pc, F &&step) {
+    return step(ops[pc]);
+  }
+};
+
+// A plan op as compile-time constants (generated op policies).
+template <uint32_t K, uint32_t F, uint32_t D, uint32_t NOFF, uint32_t A0, uint32_t A1, uint32_t A2, uint32_t A3,
+          uint32_t A4>
+struct xop {
+  static constexpr uint8_t kind = K;
+  static constexpr uint8_t flags = F;
+  static constexpr uint16_t depth = D;
+  static constexpr uint32_t noff = NOFF, arg0 = A0, arg1 = A1, arg2 = A2, arg3 = A3, arg4 = A4;
+};
 
 // A running out of frames: defer the record to the next pass, or report.
 __device__ __forceinline__ void sub_full(const sub_pass &P, uint64_t r, uint32_t pc, uint32_t code,
@@ -158,17 +186,13 @@ __device__ __forceinline__ void sub_records(const sub_pass &P, uint64_t n, F &&w
 // xdrpp/depth_checker.h:41-54).  kWalkErr with the op and code: a bad
 // discriminant or a record of 2^31 bytes or more; kWalkFull (op in bad_op):
 // the stack ran out.
-template <bool DEPTH, class ST>
+template <bool DEPTH, class OPS, class ST>
 __device__ int sub_size(const xdrg_op *__restrict__ ops, const uint32_t *__restrict__ table, sub_src src,
                         uint64_t &s, uint32_t &dmax, uint32_t &bad_op, uint32_t &code, ST &st) {
   uint32_t fp = 0, pc = 0, dbase = 0;
-  for (;;) {
-    const xdrg_op &op = ops[pc];
-    if (op.kind == XDRG_OP_END) {
-      if (!sub_next(ops, st, fp, pc, dbase, src.eb, src.in_heap)) return kWalkOk;
-      continue;
-    }
-    if (op.kind == XDRG_OP_JUMP) { pc = op.arg0; continue; }
+  auto step = [&](const auto &op) -> int {
+    if (op.kind == XDRG_OP_END) return sub_next(ops, st, fp, pc, dbase, src.eb, src.in_heap) ? kWalkCont : kWalkOk;
+    if (op.kind == XDRG_OP_JUMP) { pc = op.arg0; return kWalkCont; }
     if (DEPTH) dmax = max(dmax, dbase + op.depth);
     switch (op.kind) {
     case XDRG_OP_U64: s += 8; ++pc; break;
@@ -208,15 +232,40 @@ __device__ int sub_size(const xdrg_op *__restrict__ ops, const uint32_t *__restr
     // every frame adds a count word, so a walk that never ends (a cycle in
     // the staged heap) fails here or at its last frame
     if (s >= kSizeErr) { bad_op = 0; code = XDRG_ERR_OVERFLOW_PUT; return kWalkErr; }
+    return kWalkCont;
+  };
+  for (;;) {
+    const int rc = OPS::visit(ops, pc, step);
+    if (rc != kWalkCont) return rc;
   }
 }
 
-template <bool DEPTH>
-__global__ __launch_bounds__(256) void k_sub_size(
-    const uint8_t *__restrict__ native, uint64_t n, uint32_t stride, const uint8_t *__restrict__ heap,
-    uint64_t heap_len, const xdrg_op *__restrict__ ops, uint32_t nops, const uint32_t *__restrict__ table,
-    uint32_t *__restrict__ sizes, unsigned long long *__restrict__ block_sums, uint32_t mark,
-    unsigned long long *err, uint32_t *__restrict__ depths, sub_pass P) {
+// Kernel parameters of the three walks: the library's kernels (xdrgpu.hip,
+// rt_ops) and the generated ones (codegen.cpp, plan_ops) take the same.
+#define XDRG_SUB_SIZE_PARAMS                                                                                      \
+  const uint8_t *__restrict__ native, uint64_t n, uint32_t stride, const uint8_t *__restrict__ heap,               \
+      uint64_t heap_len, const xdrg_op *__restrict__ ops, uint32_t nops, const uint32_t *__restrict__ table,       \
+      uint32_t *__restrict__ sizes, unsigned long long *__restrict__ block_sums, uint32_t mark,                    \
+      unsigned long long *err, uint32_t *__restrict__ depths, xdrg::dev::sub_pass P
+#define XDRG_SUB_SIZE_ARGS native, n, stride, heap, heap_len, ops, nops, table, sizes, block_sums, mark, err, depths, P
+#define XDRG_SUB_ENCODE_PARAMS                                                                                    \
+  const uint8_t *__restrict__ native, uint64_t n, uint32_t stride, const uint8_t *__restrict__ heap,               \
+      uint64_t heap_len, uint8_t *__restrict__ xdr, uint64_t cap, uint64_t *__restrict__ offsets,                  \
+      const uint32_t *__restrict__ sizes, const unsigned long long *__restrict__ block_base,                       \
+      const xdrg_op *__restrict__ ops, uint32_t nops, const uint32_t *__restrict__ table, uint32_t stack_limit,    \
+      uint32_t mark, unsigned long long *err, xdrg::dev::sub_pass P
+#define XDRG_SUB_ENCODE_ARGS                                                                                      \
+  native, n, stride, heap, heap_len, xdr, cap, offsets, sizes, block_base, ops, nops, table, stack_limit, mark, err, P
+#define XDRG_SUB_DECODE_PARAMS                                                                                    \
+  const uint8_t *__restrict__ xdr, uint64_t len, const uint64_t *__restrict__ offsets, uint64_t n,                 \
+      uint8_t *__restrict__ native, uint32_t stride, const xdrg_op *__restrict__ ops, uint32_t nops,               \
+      const uint32_t *__restrict__ table, uint32_t stack_limit, uint8_t *__restrict__ heap, uint64_t ebase,        \
+      uint32_t F, uint32_t mark, unsigned long long *err, xdrg::dev::sub_pass P
+#define XDRG_SUB_DECODE_ARGS                                                                                      \
+  xdr, len, offsets, n, native, stride, ops, nops, table, stack_limit, heap, ebase, F, mark, err, P
+
+template <bool DEPTH, class OPS>
+__device__ __forceinline__ void sub_size_kernel(XDRG_SUB_SIZE_PARAMS) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   xdrg_op *sops = reinterpret_cast<xdrg_op *>(smem);
   load_ops(sops, ops, nops);
@@ -225,7 +274,7 @@ __global__ __launch_bounds__(256) void k_sub_size(
     const sub_src src{native + r * stride, stride, heap, heap_len, 0, false};
     uint64_t s = mark;
     uint32_t dmax = 0, bad_op = 0, code = 0, sz = kSizeErr;
-    const int rc = sub_size<DEPTH>(sops, table, src, s, dmax, bad_op, code, st);
+    const int rc = sub_size<DEPTH, OPS>(sops, table, src, s, dmax, bad_op, code, st);
     if (rc == kWalkOk) {
       sz = static_cast<uint32_t>(s);
     } else if (rc == kWalkErr) {
@@ -251,7 +300,7 @@ __global__ __launch_bounds__(256) void k_sub_size(
 // The record's walk from stream offset `off` with check(n) and the stack
 // budget before every field (marshal.h:104-108, :129-136).  Errors are
 // reported; kWalkFull when the stack ran out (op in *full_op).
-template <class ST>
+template <class OPS, class ST>
 __device__ int sub_encode_rec(const xdrg_op *__restrict__ sops, const uint32_t *__restrict__ table, sub_src src,
                               uint8_t *__restrict__ xdr, uint64_t cap, uint64_t off, uint32_t sz, uint32_t mark,
                               uint32_t stack_limit, uint64_t r, unsigned long long *err, uint32_t *full_op,
@@ -265,13 +314,9 @@ __device__ int sub_encode_rec(const xdrg_op *__restrict__ sops, const uint32_t *
     pos += 4;
   }
   uint32_t fp = 0, pc = 0, dbase = 0;
-  for (;;) {
-    const xdrg_op &op = sops[pc];
-    if (op.kind == XDRG_OP_END) {
-      if (!sub_next(sops, st, fp, pc, dbase, src.eb, src.in_heap)) return kWalkOk;
-      continue;
-    }
-    if (op.kind == XDRG_OP_JUMP) { pc = op.arg0; continue; }
+  auto step = [&](const auto &op) -> int {
+    if (op.kind == XDRG_OP_END) return sub_next(sops, st, fp, pc, dbase, src.eb, src.in_heap) ? kWalkCont : kWalkOk;
+    if (op.kind == XDRG_OP_JUMP) { pc = op.arg0; return kWalkCont; }
     if (dbase + op.depth > stack_limit) { report(err, r, pc, XDRG_ERR_STACK_PUT); return kWalkErr; }
     uint64_t need = 4;
     uint32_t len = 0;
@@ -348,17 +393,18 @@ __device__ int sub_encode_rec(const xdrg_op *__restrict__ sops, const uint32_t *
     }
     default: ++pc; break;
     }
+    return kWalkCont;
+  };
+  for (;;) {
+    const int rc = OPS::visit(sops, pc, step);
+    if (rc != kWalkCont) return rc;
   }
 }
 
 // Record offsets as k_var_encode computes them (block-local scan on top of
 // the 64-record block bases); a deep pass reads them back.
-__global__ __launch_bounds__(256) void k_sub_encode(
-    const uint8_t *__restrict__ native, uint64_t n, uint32_t stride, const uint8_t *__restrict__ heap,
-    uint64_t heap_len, uint8_t *__restrict__ xdr, uint64_t cap, uint64_t *__restrict__ offsets,
-    const uint32_t *__restrict__ sizes, const unsigned long long *__restrict__ block_base,
-    const xdrg_op *__restrict__ ops, uint32_t nops, const uint32_t *__restrict__ table,
-    uint32_t stack_limit, uint32_t mark, unsigned long long *err, sub_pass P) {
+template <class OPS>
+__device__ __forceinline__ void sub_encode_kernel(XDRG_SUB_ENCODE_PARAMS) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   xdrg_op *sops = reinterpret_cast<xdrg_op *>(smem);
   load_ops(sops, ops, nops);
@@ -383,7 +429,8 @@ __global__ __launch_bounds__(256) void k_sub_encode(
     const uint64_t o = P.list ? offsets[r] : off;
     const sub_src src{native + r * stride, stride, heap, heap_len, 0, false};
     uint32_t full_op = 0;
-    if (sub_encode_rec(sops, table, src, xdr, cap, o, sz, mark, stack_limit, r, err, &full_op, st) == kWalkFull)
+    if (sub_encode_rec<OPS>(sops, table, src, xdr, cap, o, sz, mark, stack_limit, r, err, &full_op, st) ==
+        kWalkFull)
       sub_full(P, r, full_op, XDRG_ERR_STACK_PUT, err);
   });
 }
@@ -397,7 +444,7 @@ __global__ __launch_bounds__(256) void k_sub_encode(
 // holds 1 + the index of the element that failed, the others 0 (the
 // unstager follows these marks).  kWalkFull: the stack ran out (op in
 // *full_op), nothing reported.
-template <class ST>
+template <class OPS, class ST>
 __device__ int sub_decode_rec(const xdrg_op *__restrict__ sops, const uint32_t *__restrict__ table,
                               const uint8_t *__restrict__ xdr, uint64_t a, uint64_t b, uint8_t *__restrict__ rec,
                               uint32_t stride, uint8_t *__restrict__ heap, uint64_t ecur, uint64_t eend,
@@ -408,14 +455,10 @@ __device__ int sub_decode_rec(const xdrg_op *__restrict__ sops, const uint32_t *
   uint32_t fp = 0, pc = 0, dbase = 0, code = 0;
   uint64_t eb = 0;
   bool in_heap = false;
-  for (;;) {
-    const xdrg_op &op = sops[pc];
-    if (op.kind == XDRG_OP_END) {
-      if (!sub_next(sops, st, fp, pc, dbase, eb, in_heap)) break;
-      continue;
-    }
-    if (op.kind == XDRG_OP_JUMP) { pc = op.arg0; continue; }
-    if (dbase + op.depth > stack_limit) { code = XDRG_ERR_STACK_GET; break; }
+  auto step = [&](const auto &op) -> int {
+    if (op.kind == XDRG_OP_END) return sub_next(sops, st, fp, pc, dbase, eb, in_heap) ? kWalkCont : kWalkOk;
+    if (op.kind == XDRG_OP_JUMP) { pc = op.arg0; return kWalkCont; }
+    if (dbase + op.depth > stack_limit) { code = XDRG_ERR_STACK_GET; return kWalkErr; }
     uint8_t *nat = in_heap ? heap + eb : rec;
     const uint64_t rem = b - p;
     switch (op.kind) {
@@ -522,8 +565,12 @@ __device__ int sub_decode_rec(const xdrg_op *__restrict__ sops, const uint32_t *
     }
     default: ++pc; break;
     }
-    if (code) break;
-  }
+    return code ? kWalkErr : kWalkCont;
+  };
+  int rc;
+  do rc = OPS::visit(sops, pc, step);
+  while (rc == kWalkCont);
+  if (rc == kWalkFull) return kWalkFull;
   if (code) {
     if (code != kReported) report(err, r, pc, code);
     // 1 + the failing element in every open container: the container's ref
@@ -538,11 +585,8 @@ __device__ int sub_decode_rec(const xdrg_op *__restrict__ sops, const uint32_t *
   return kWalkOk;
 }
 
-__global__ __launch_bounds__(256) void k_sub_decode(
-    const uint8_t *__restrict__ xdr, uint64_t len, const uint64_t *__restrict__ offsets, uint64_t n,
-    uint8_t *__restrict__ native, uint32_t stride, const xdrg_op *__restrict__ ops, uint32_t nops,
-    const uint32_t *__restrict__ table, uint32_t stack_limit, uint8_t *__restrict__ heap,
-    uint64_t ebase, uint32_t F, uint32_t mark, unsigned long long *err, sub_pass P) {
+template <class OPS>
+__device__ __forceinline__ void sub_decode_kernel(XDRG_SUB_DECODE_PARAMS) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   xdrg_op *sops = reinterpret_cast<xdrg_op *>(smem);
   load_ops(sops, ops, nops);
@@ -558,9 +602,12 @@ __global__ __launch_bounds__(256) void k_sub_decode(
       if ((b - a) & 3u) { report(err, r, kOpRecordLevel, XDRG_ERR_SIZE_NOT_MULT4); return; }
     }
     uint32_t full_op = 0;
-    if (sub_decode_rec(sops, table, xdr, a + mark, b, native + r * stride, stride, heap,
+    if (sub_decode_rec<OPS>(sops, table, xdr, a + mark, b, native + r * stride, stride, heap,
                        ebase + static_cast<uint64_t>(F) * a, ebase + static_cast<uint64_t>(F) * b, stack_limit, r,
                        err, &full_op, st) == kWalkFull)
       sub_full(P, r, full_op, XDRG_ERR_STACK_GET, err);
   });
 }
+
+}  // namespace dev
+}  // namespace xdrg

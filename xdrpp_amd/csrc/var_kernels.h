@@ -43,12 +43,6 @@
 #ifndef XDRG_STAMPV
 #define XDRG_STAMPV(k, v) ((void)0)
 #endif
-// Tuning switches of the one-pass encode's output loop (tools/tune/
-// stream_stamps.py CFLAGS; wrong bytes by design): 1 no stores, 2 no word
-// reads.  0 in the library.
-#ifndef XDRG_STREAM_DBG
-#define XDRG_STREAM_DBG 0
-#endif
 // Memory hints of the encode (tools/tune/enc_stamps.py CFLAGS A/B,
 // profiles/r02s/nt_hints/): bit 0 non-temporal payload loads, bit 1
 // non-temporal stream stores.  Stores: encode kernel -7 % recvar, -3 % rpc
@@ -343,6 +337,87 @@ __device__ __forceinline__ uint32_t chunks_starting_before(const enc_ctx<KMAX, B
   return s;
 }
 
+// ------------------------------------------------- decoupled look-back
+constexpr unsigned long long kLbAgg = 1ull << 62;     // block total published
+constexpr unsigned long long kLbIncl = 2ull << 62;    // block total + everything before it
+constexpr unsigned long long kLbVal = (1ull << 62) - 1;
+constexpr uint32_t kLbSpinLimit = 1u << 16;           // polls before a look-back gives up
+
+
+typedef __attribute__((address_space(1))) unsigned long long lb_u64;
+typedef __attribute__((address_space(1))) unsigned int lb_u32;
+// generic -> global address space (agent-scope atomics on global, never flat)
+__device__ __forceinline__ lb_u64 *lb_global(unsigned long long *p) { return (lb_u64 *)p; }
+
+// Sum over the lanes of a wave (every lane active).
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t x) {
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+  return x;
+}
+__device__ __forceinline__ uint64_t wave_min64(uint64_t x) {
+  for (int o = 32; o > 0; o >>= 1) x = min(x, static_cast<uint64_t>(__shfl_xor(x, o, 64)));
+  return x;
+}
+__device__ __forceinline__ uint64_t wave_max64(uint64_t x) {
+  for (int o = 32; o > 0; o >>= 1) x = max(x, static_cast<uint64_t>(__shfl_xor(x, o, 64)));
+  return x;
+}
+
+// Decoupled look-back (single-pass chained scan): the exclusive prefix of
+// block `blk`'s total.  desc[i] = state | value, one 8-byte word written by
+// one store (the data is the flag).  Lane l reads blocks top - l - 64u, u < 4.
+// Returns false when a predecessor never published (kLbSpinLimit polls).
+__device__ __forceinline__ bool lookback(lb_u64 *desc, uint32_t blk, uint64_t &excl, uint32_t &polls) {
+  const uint32_t lane = __lane_id();
+  excl = 0;
+  polls = 0;
+  int64_t top = static_cast<int64_t>(blk) - 1;
+  for (uint32_t spins = 0; top >= 0;) {
+    uint64_t d[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t i = top - lane - 64 * u;
+      d[u] = i >= 0 ? __hip_atomic_load(desc + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kLbIncl;
+    }
+    ++polls;
+    // first block (in look-back order) that has not published, and the
+    // first that holds an inclusive prefix
+    uint32_t dn = 256, dp = 256;
+#pragma unroll
+    for (int u = 3; u >= 0; --u) {
+      const unsigned long long mn = __ballot((d[u] >> 62) == 0u);
+      const unsigned long long mp = __ballot((d[u] >> 62) == 2u);
+      if (mn) dn = 64u * u + __builtin_ctzll(mn);
+      if (mp) dp = 64u * u + __builtin_ctzll(mp);
+    }
+    const bool found = dp < dn;
+    const uint32_t lim = found ? dp : dn;  // block totals (aggregates) summed by this step
+    // the aggregates (each < 2^31) in two parts, summed with DPP (no LDS)
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (lane + 64u * u < lim) {
+        lo += static_cast<uint32_t>(d[u]) & 0xffffffu;
+        hi += static_cast<uint32_t>((d[u] & kLbVal) >> 24);
+      }
+    excl += static_cast<uint64_t>(rl32(wave_incl_scan(lo), 63)) + (static_cast<uint64_t>(rl32(wave_incl_scan(hi), 63)) << 24);
+    if (found) {  // + the inclusive prefix at dp
+      uint64_t pv = 0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (dp / 64u == static_cast<uint32_t>(u)) pv = rl64(d[u], dp % 64u);
+      excl += pv & kLbVal;
+      return true;
+    }
+    top -= lim;
+    if (dn < 256) {  // a block before this one is still walking its records
+      if (++spins > kLbSpinLimit) return false;
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  return true;
+}
+
 // One wave = 64 consecutive records (xdr_generic_put, marshal.h:84-137).
 // The output stretch of the wave is produced in windows of C bytes of LDS
 // image: per window the lanes whose record reaches into it walk it (scalar
@@ -358,13 +433,24 @@ __device__ __forceinline__ uint32_t chunks_starting_before(const enc_ctx<KMAX, B
 // WL (plans with a bounded scalar word list, W::kWords > 0, walked from
 // registers): the list aliases the tile, which the walk no longer reads once
 // the lane's record is in registers; the walk runs once, in the first round.
-template <class W, int KMAX, int U, int NW = 0, uint32_t CMAX = 0>
+//
+// PRE (word-list plans walked from registers without checks: the plan's
+// depth fits the stack budget) -- no size pass: the walk runs first, with
+// record-relative positions, and its byte counts are the sizes.
+//   PRE = 1  the wave's base by a decoupled look-back over the byte totals of
+//            the waves before it (xdrg_encode: no size pass, no scan);
+//   PRE = 2  the base from block_base (xdrg_encode_sized after
+//            xdrg_encode_sizes), the sizes not read.
+// A wave whose bytes pass `cap` walks again with the checks to report the
+// failing record (xdr_generic_put::check, marshal.h:104-108).
+template <class W, int KMAX, int U, int NW = 0, uint32_t CMAX = 0, int PRE = 0>
 __device__ __forceinline__ void var_encode_body(
     const W &w, const uint8_t *__restrict__ native, uint64_t n, uint32_t stride,
     const uint8_t *__restrict__ heap, uint64_t heap_len, uint8_t *__restrict__ xdr, uint64_t cap,
     uint64_t *__restrict__ offsets, const uint32_t *__restrict__ sizes,
     const unsigned long long *__restrict__ block_base, uint32_t stack_limit, uint32_t C,
-    uint32_t mark, unsigned long long *err) {
+    uint32_t mark, unsigned long long *err, unsigned long long *lbd = nullptr, uint32_t nb = 0,
+    uint64_t *total = nullptr) {
   extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
   const enc_lds L = enc_layout(stride, KMAX, C);
   uint8_t *tile = sm + L.tile;
@@ -376,14 +462,116 @@ __device__ __forceinline__ void var_encode_body(
   const uint64_t r = wr0 + lane;
   const uint32_t nrec = static_cast<uint32_t>(min<uint64_t>(64, n - wr0));
   XDRG_STAMP(0);
+  constexpr int WL = (W::kWords > 0 && NW > 0) ? static_cast<int>(W::kWords) + 1 : 0;  // + the mark
+  static_assert(PRE == 0 || (WL > 0 && W::kFastWalk), "the pre-walk runs on word-list plans");
 
+  uint32_t sz, v, T;
+  bool szok;
+  uint64_t wave_out, off;
+  enc_ctx<KMAX, true, WL> c;
+  c.sw = reinterpret_cast<uint32_t *>(tile) + lane;
+  c.nw = 0;
+  c.img = img;
+  c.C = C;
+  c.heap = heap;
+  c.heap_len = heap_len;
+  c.cap = cap;
+  c.stack_limit = stack_limit;
+  c.r = r;
+  c.err = err;
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) { c.psr[k] = 0; c.pds[k] = 0; c.pln[k] = 0; c.rb[k] = 0; }
+  uint32_t rec[NW > 0 ? NW : 1];
+  if constexpr (PRE != 0) {
+    // ---- the walk first: the record's words into the list (tile), its
+    // payloads into slots, its byte count
+    if constexpr (PRE == 2) wave_out = block_base[blockIdx.x];
+    stage_tile<8>(tile, native + wr0 * stride, nrec * stride, lane, 64u);
+    wave_sync();
+    {
+      const uint32_t *t32 = reinterpret_cast<const uint32_t *>(tile + lane * stride);
+#pragma unroll
+      for (int k = 0; k < NW; ++k) rec[k] = lane < nrec ? t32[k] : 0u;
+    }
+    wave_sync();  // every tile read before the list overwrites it
+    enc_ctx<KMAX, false, WL> f = c.template as<false>();
+    f.at = 0;
+    f.pos = 0;
+    bool okw = r < n;
+    if (okw && mark) f.put(0u);  // the record mark, set below
+    okw = w.enc(f, reinterpret_cast<const uint8_t *>(rec), okw);
+    if (r < n && !okw) {  // an unchecked walk fails only at a bad discriminant (gen_hh.cc:645,658)
+      uint32_t bad = 0xffffffffu;
+      (void)w.size(reinterpret_cast<const uint8_t *>(rec), heap, heap_len, bad);
+      report(err, r, bad == 0xffffffffu ? 0u : bad, XDRG_ERR_BAD_DISCRIMINANT);
+    }
+    v = okw ? f.at : 0u;
+    if (okw && mark) f.sw[0] = mark_word(v - 4u);
+    szok = okw;
+    sz = okw ? v : kSizeErr;
+    if (!okw) {
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) f.pln[k] = 0;
+    }
+    c.take(f);
+    const uint32_t incl = wave_incl_scan(v);
+    T = rl32(incl, 63);
+    if constexpr (PRE == 1) {
+      const uint32_t blk = blockIdx.x;
+      if (lane == 0)
+        __hip_atomic_store(lb_global(lbd) + blk, (blk == 0 ? kLbIncl : kLbAgg) | T, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      uint64_t excl = 0;
+      uint32_t polls = 0;
+      if (!lookback(lb_global(lbd), blk, excl, polls)) {
+        report(err, wr0, kOpRecordLevel, XDRG_ERR_LOOKBACK);
+        return;
+      }
+      XDRG_STAMPV(6, polls);
+      if (blk > 0 && lane == 0)
+        __hip_atomic_store(lb_global(lbd) + blk, kLbIncl | ((excl + T) & kLbVal), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      wave_out = excl;
+      if (r + 1 == n) {  // offsets[n] and the total (k_scan_blocks' job in two passes)
+        offsets[n] = wave_out + T;
+        *total = wave_out + T;
+      }
+    }
+    off = wave_out + (incl - v);
+    if (r < n) offsets[r] = off;
+    const uint32_t a0r = static_cast<uint32_t>(incl - v) + static_cast<uint32_t>(wave_out & 15u);
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) c.pds[k] += a0r;  // image space
+    // a wave whose bytes pass `cap`: the checks, in the reference's order;
+    // the re-walk's list goes to the image (unused until the windows)
+    if (wave_out + T > cap && r < n && okw) {
+      enc_ctx<KMAX, true, WL> k = c;
+      k.sw = reinterpret_cast<uint32_t *>(img) + lane;
+      k.nw = 0;
+      k.at = 0;
+      k.pos = off;
+#pragma unroll
+      for (int q = 0; q < KMAX; ++q) { k.psr[q] = 0; k.pds[q] = 0; k.pln[q] = 0; k.rb[q] = 0; }
+      bool okc = true;
+      if (mark) {
+        if (4 > cap - min(k.pos, cap)) {
+          report(err, r, kOpRecordLevel, XDRG_ERR_OVERFLOW_PUT);
+          okc = false;
+        } else {
+          k.put(mark_word(v - 4u));
+        }
+      }
+      (void)w.enc(k, reinterpret_cast<const uint8_t *>(rec), okc);
+    }
+    wave_sync();
+  } else {
   // ---- record offsets: wave scan of the sizes on top of the block base
   // (sizes, block base and the native tile are loaded in one round trip)
-  const uint32_t sz = r < n ? sizes[r] : kSizeErr;
-  const uint64_t wave_out = block_base[blockIdx.x];
+  sz = r < n ? sizes[r] : kSizeErr;
+  wave_out = block_base[blockIdx.x];
   stage_tile<8>(tile, native + wr0 * stride, nrec * stride, lane, 64u);
-  const bool szok = !(sz & kSizeErr);
-  const uint32_t v = szok ? sz : 0u;
+  szok = !(sz & kSizeErr);
+  v = szok ? sz : 0u;
   if constexpr (W::kDirect) {
     if (__any(v >= (1u << 25))) {  // 64 records could pass 2^31 bytes: direct mode
       uint64_t inc = v;
@@ -405,10 +593,11 @@ __device__ __forceinline__ void var_encode_body(
     }
   }
   const uint32_t incl = wave_incl_scan(v);  // a wave's stretch < 2^31 bytes (direct mode above)
-  const uint32_t T = rl32(incl, 63);        // bytes of the wave's stretch
-  const uint64_t off = wave_out + (incl - v);
+  T = rl32(incl, 63);                       // bytes of the wave's stretch
+  off = wave_out + (incl - v);
   if (r < n) offsets[r] = off;
   wave_sync();
+  }
   XDRG_STAMP(1);
 
   // image space: byte j <-> stream byte g0 + j, g0 = wave_out rounded down to 16
@@ -419,20 +608,6 @@ __device__ __forceinline__ void var_encode_body(
   const uint32_t rounds = T ? (span + C - 1u) / C : 1u;
   const uint64_t ge = min<uint64_t>(wave_out + T, cap);  // last stream byte + 1 to write
 
-  constexpr int WL = (W::kWords > 0 && NW > 0) ? static_cast<int>(W::kWords) + 1 : 0;  // + the mark
-  enc_ctx<KMAX, true, WL> c;
-  c.sw = reinterpret_cast<uint32_t *>(tile) + lane;
-  c.nw = 0;
-  c.img = img;
-  c.C = C;
-  c.heap = heap;
-  c.heap_len = heap_len;
-  c.cap = cap;
-  c.stack_limit = stack_limit;
-  c.r = r;
-  c.err = err;
-#pragma unroll
-  for (int k = 0; k < KMAX; ++k) { c.psr[k] = 0; c.pds[k] = 0; c.pln[k] = 0; c.rb[k] = 0; }
   bool ok = szok;
   uint32_t M = 0;
 
@@ -540,11 +715,10 @@ __device__ __forceinline__ void var_encode_body(
     c.w0 = w0;
     // ---- walk: the window's scalar words -> image, payload slots -> registers
     // (every lane walks in the first round: it reports the record's errors)
-    if (rd == 0 || (WL == 0 && ok && a0 < w0 + C && a0 + v > w0)) {
+    if (PRE == 0 && (rd == 0 || (WL == 0 && ok && a0 < w0 + C && a0 + v > w0))) {
       c.at = a0;
       c.pos = off;
       bool okr = szok;
-      uint32_t rec[NW > 0 ? NW : 1];
       if constexpr (NW > 0) {
         const uint32_t *t32 = reinterpret_cast<const uint32_t *>(tile + lane * stride);
 #pragma unroll
@@ -685,456 +859,6 @@ __device__ __forceinline__ void var_encode_body(
   XDRG_STAMP(5);
 }
 
-// ------------------------------------------------- encode, one pass (stream)
-// xdr_to_opaque(r0..rn-1) (xdrpp/marshal.h:264-272) for word-list plans (every
-// payload takes a slot, no container loop: W::kWords > 0) in ONE kernel, with
-// no size pass and no scan.  One wave = 64 consecutive records:
-//   1. the native tile (coalesced), the walk from registers into the word
-//      list (xdr_generic_put's words, marshal.h:110-127) and the payload
-//      slots; the walk's byte counts are the sizes (xdr_size, types.h:240-244),
-//      and wave scans of them, of the words and of the payloads place every
-//      record, scalar word and payload in the wave's stretch;
-//   2. (LB) the wave's byte total is published at once, then a decoupled
-//      look-back over the totals of the blocks before it (4 per lane, 256 per
-//      step) finds the wave's base;
-//   3. the stretch is assembled 16-byte chunk by chunk in registers -- each
-//      lane owns chunks, consecutive lanes consecutive chunks: a chunk's
-//      scalar words come from the word stream in LDS, its payload words from
-//      one unaligned 16-byte global load per payload piece it holds (at most
-//      two: a payload is preceded by its length word) -- and leaves as aligned
-//      16-byte stores (words at the stretch's two edges, shared with the
-//      neighbour waves, as single-word stores).  Loads of payloads are
-//      coalesced (consecutive lanes read consecutive bytes of a payload) and
-//      need no particular heap layout.
-// Without LB (xdrg_encode_sized) the block's base comes from the size pass's
-// scan and nothing is published.  Every field check of xdr_generic_put is
-// kept: the walk runs unchecked only when the plan's depth fits the stack
-// budget (the host's condition for this kernel), and a wave whose bytes pass
-// `cap` walks again with the capacity check to report the failing record.
-constexpr unsigned long long kLbAgg = 1ull << 62;     // block total published
-constexpr unsigned long long kLbIncl = 2ull << 62;    // block total + everything before it
-constexpr unsigned long long kLbVal = (1ull << 62) - 1;
-constexpr uint32_t kLbSpinLimit = 1u << 16;           // polls before a look-back gives up
-
-struct senc_lds {
-  uint32_t tile, pay, src, hist, total;
-};
-constexpr uint32_t kSencU = 2;  // output chunks per lane per round
-// LDS of a one-pass encode wave:
-//   tile  64 native records; then the wave's scalar words in stream order
-//         (4 * words per record <= stride, codegen.cpp)
-//   pay   the wave's payloads in stream order, 16 bytes each {stream offset
-//         in the stretch, bytes, end of the padded bytes, padded payload
-//         bytes up to that end}; entry 0 is a payload of 0 bytes at 0, the
-//         last two lie past the stretch.  Before it is built: the walk's word
-//         list (word j of lane l at word 64 j + l)
-//   src   the payloads' heap offsets
-//   hist  two histograms of the payloads' first chunks over a round's chunks;
-//         before them, the word list of a wave's capacity re-walk
-__host__ __device__ inline senc_lds senc_layout(uint32_t stride, uint32_t KMAX, uint32_t WL) {
-  senc_lds L;
-  L.tile = 0;
-  L.pay = (64u * stride + 15u) & ~15u;
-  const uint32_t pb = (64u * KMAX + 3u) * 16u;
-  L.src = L.pay + (pb > 256u * WL ? pb : 256u * WL);
-  L.hist = (L.src + (64u * KMAX + 3u) * 8u + 15u) & ~15u;
-  L.total = L.hist + (2u * 64u * kSencU * 4u > 256u * WL ? 2u * 64u * kSencU * 4u : 256u * WL);
-  return L;
-}
-
-typedef __attribute__((address_space(1))) unsigned long long lb_u64;
-typedef __attribute__((address_space(1))) unsigned int lb_u32;
-// generic -> global address space (agent-scope atomics on global, never flat)
-__device__ __forceinline__ lb_u64 *lb_global(unsigned long long *p) { return (lb_u64 *)p; }
-
-// Sum over the lanes of a wave (every lane active).
-__device__ __forceinline__ uint64_t wave_sum64(uint64_t x) {
-  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-  return x;
-}
-__device__ __forceinline__ uint64_t wave_min64(uint64_t x) {
-  for (int o = 32; o > 0; o >>= 1) x = min(x, static_cast<uint64_t>(__shfl_xor(x, o, 64)));
-  return x;
-}
-__device__ __forceinline__ uint64_t wave_max64(uint64_t x) {
-  for (int o = 32; o > 0; o >>= 1) x = max(x, static_cast<uint64_t>(__shfl_xor(x, o, 64)));
-  return x;
-}
-
-// Decoupled look-back (single-pass chained scan): the exclusive prefix of
-// block `blk`'s total.  desc[i] = state | value, one 8-byte word written by
-// one store (the data is the flag).  Lane l reads blocks top - l - 64u, u < 4.
-// Returns false when a predecessor never published (kLbSpinLimit polls).
-__device__ __forceinline__ bool lookback(lb_u64 *desc, uint32_t blk, uint64_t &excl, uint32_t &polls) {
-  const uint32_t lane = __lane_id();
-  excl = 0;
-  polls = 0;
-  int64_t top = static_cast<int64_t>(blk) - 1;
-  for (uint32_t spins = 0; top >= 0;) {
-    uint64_t d[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int64_t i = top - lane - 64 * u;
-      d[u] = i >= 0 ? __hip_atomic_load(desc + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kLbIncl;
-    }
-    ++polls;
-    // first block (in look-back order) that has not published, and the
-    // first that holds an inclusive prefix
-    uint32_t dn = 256, dp = 256;
-#pragma unroll
-    for (int u = 3; u >= 0; --u) {
-      const unsigned long long mn = __ballot((d[u] >> 62) == 0u);
-      const unsigned long long mp = __ballot((d[u] >> 62) == 2u);
-      if (mn) dn = 64u * u + __builtin_ctzll(mn);
-      if (mp) dp = 64u * u + __builtin_ctzll(mp);
-    }
-    const bool found = dp < dn;
-    const uint32_t lim = found ? dp : dn;  // block totals (aggregates) summed by this step
-    // the aggregates (each < 2^31) in two parts, summed with DPP (no LDS)
-    uint32_t lo = 0, hi = 0;
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (lane + 64u * u < lim) {
-        lo += static_cast<uint32_t>(d[u]) & 0xffffffu;
-        hi += static_cast<uint32_t>((d[u] & kLbVal) >> 24);
-      }
-    excl += static_cast<uint64_t>(rl32(wave_incl_scan(lo), 63)) + (static_cast<uint64_t>(rl32(wave_incl_scan(hi), 63)) << 24);
-    if (found) {  // + the inclusive prefix at dp
-      uint64_t pv = 0;
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (dp / 64u == static_cast<uint32_t>(u)) pv = rl64(d[u], dp % 64u);
-      excl += pv & kLbVal;
-      return true;
-    }
-    top -= lim;
-    if (dn < 256) {  // a block before this one is still walking its records
-      if (++spins > kLbSpinLimit) return false;
-      __builtin_amdgcn_s_sleep(1);
-    }
-  }
-  return true;
-}
-
-template <class W, int KMAX, int NW, int WL, bool LB>
-__device__ __forceinline__ void var_encode_stream_body(
-    const W &w, const uint8_t *__restrict__ native, uint64_t n, uint32_t stride,
-    const uint8_t *__restrict__ heap, uint64_t heap_len, uint8_t *__restrict__ xdr, uint64_t cap,
-    uint64_t *__restrict__ offsets, const unsigned long long *__restrict__ block_base,
-    unsigned long long *desc, uint32_t nb, uint64_t *total, uint32_t stack_limit,
-    uint32_t mark, uint32_t ticket, unsigned long long *err) {
-  static_assert(WL > 0 && NW > 0, "word-list plans walked from registers");
-  extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
-  const senc_lds L = senc_layout(stride, KMAX, WL);
-  uint8_t *tile = sm + L.tile;
-  uint32_t *ws = reinterpret_cast<uint32_t *>(sm + L.tile);  // scalar words, stream order
-  u32x4 *pay = reinterpret_cast<u32x4 *>(sm + L.pay);
-  uint64_t *psrc = reinterpret_cast<uint64_t *>(sm + L.src);
-  uint32_t *hist = reinterpret_cast<uint32_t *>(sm + L.hist);
-  const uint32_t lane = threadIdx.x;
-  XDRG_STAMP(0);
-
-  uint32_t blk = blockIdx.x;
-  if (LB && ticket) {  // the block from a ticket (else dispatch order: blockIdx)
-    uint32_t t = 0;
-    if (lane == 0)
-      t = __hip_atomic_fetch_add((lb_u32 *)(desc + nb), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    blk = rl32(t, 0);
-  }
-  const uint64_t wr0 = static_cast<uint64_t>(blk) * 64u;
-  const uint64_t r = wr0 + lane;
-  const uint32_t nrec = static_cast<uint32_t>(min<uint64_t>(64, n - wr0));
-  uint64_t wave_out = 0;
-  if constexpr (!LB) wave_out = block_base[blk];
-  stage_tile<8>(tile, native + wr0 * stride, nrec * stride, lane, 64u);
-  wave_sync();
-  uint32_t rec[NW];
-  {
-    const uint32_t *t32 = reinterpret_cast<const uint32_t *>(tile + lane * stride);
-#pragma unroll
-    for (int k = 0; k < NW; ++k) rec[k] = lane < nrec ? t32[k] : 0u;
-  }
-  XDRG_STAMP(1);
-
-  // ---- the walk: words into the list (in the payload table's room),
-  // payloads into slots, byte count
-  enc_ctx<KMAX, false, WL> c;
-  c.sw = reinterpret_cast<uint32_t *>(sm + L.pay) + lane;
-  c.nw = 0;
-  c.img = nullptr;
-  c.w0 = 0;
-  c.C = 0;
-  c.heap = heap;
-  c.heap_len = heap_len;
-  c.cap = cap;
-  c.stack_limit = stack_limit;
-  c.r = r;
-  c.err = err;
-  c.at = 0;
-  c.pos = 0;
-#pragma unroll
-  for (int k = 0; k < KMAX; ++k) { c.psr[k] = 0; c.pds[k] = 0; c.pln[k] = 0; c.rb[k] = 0; }
-  bool ok = r < n;
-  if (ok && mark) c.put(0u);  // the record mark (message_t::alloc, marshal.cc:15-31), set below
-  ok = w.enc(c, reinterpret_cast<const uint8_t *>(rec), ok);
-  if (r < n && !ok) {  // an unchecked walk fails only at a bad discriminant (gen_hh.cc:645,658)
-    uint32_t bad = 0xffffffffu;
-    (void)w.size(reinterpret_cast<const uint8_t *>(rec), heap, heap_len, bad);
-    report(err, r, bad == 0xffffffffu ? 0u : bad, XDRG_ERR_BAD_DISCRIMINANT);
-  }
-  const uint32_t v = ok ? c.at : 0u;
-  if (ok && mark) c.sw[0] = mark_word(v - 4u);
-  const uint32_t nw = ok ? c.nw : 0u;
-  uint32_t np = 0, pb = 0;  // payloads of the record and their padded bytes
-#pragma unroll
-  for (int k = 0; k < KMAX; ++k) {
-    if (!ok) c.pln[k] = 0;
-    np += c.pln[k] ? 1u : 0u;
-    pb += (c.pln[k] + 3u) & ~3u;
-  }
-  // offsets within the wave: bytes, words, payloads, padded payload bytes
-  const uint32_t incl = wave_incl_scan(v);
-  const uint32_t T = rl32(incl, 63);
-  const uint32_t a0 = incl - v;
-  const uint32_t wincl = wave_incl_scan(nw);
-  const uint32_t pincl = wave_incl_scan(np);
-  const uint32_t NP = rl32(pincl, 63);
-  const uint32_t bincl = wave_incl_scan(pb);
-  XDRG_STAMP(2);
-  if constexpr (LB) {
-    if (lane == 0)
-      __hip_atomic_store(lb_global(desc) + blk, (blk == 0 ? kLbIncl : kLbAgg) | T,
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  // ---- the stream-order tables: the scalar words (from the list, all
-  // loads before the stores) and the payloads (slots in wire order within
-  // the record)
-  wave_sync();  // the list
-  {
-    const uint32_t *lw = reinterpret_cast<const uint32_t *>(sm + L.pay);
-    uint32_t *dst = ws + (wincl - nw);
-    uint32_t wl[WL];
-#pragma unroll
-    for (int j = 0; j < WL; ++j) wl[j] = static_cast<uint32_t>(j) < nw ? lw[64u * j + lane] : 0u;
-    wave_sync();  // every list read before the table overwrites it
-#pragma unroll
-    for (int j = 0; j < WL; ++j)
-      if (static_cast<uint32_t>(j) < nw) dst[j] = wl[j];
-    uint32_t pi = pincl - np + 1u, before = bincl - pb;
-#pragma unroll
-    for (int k = 0; k < KMAX; ++k) {
-      if (!c.pln[k]) continue;
-      uint32_t rank = 0, pre = 0;  // the record's earlier payloads (by wire offset)
-#pragma unroll
-      for (int q = 0; q < KMAX; ++q)
-        if (q != k && c.pln[q] && c.pds[q] < c.pds[k]) {
-          ++rank;
-          pre += (c.pln[q] + 3u) & ~3u;
-        }
-      const uint32_t x = a0 + c.pds[k], p4 = (c.pln[k] + 3u) & ~3u;
-      pay[pi + rank] = u32x4{x, c.pln[k], x + p4, before + pre + p4};
-      psrc[pi + rank] = c.psr[k];
-    }
-    if (lane == 0) {
-      pay[0] = u32x4{0u, 0u, 0u, 0u};
-      const uint32_t tb = rl32(bincl, 63);
-      pay[NP + 1u] = u32x4{T, 0u, T, tb};  // (two past the last payload)
-      pay[NP + 2u] = u32x4{T, 0u, T, tb};
-      psrc[0] = psrc[NP + 1u] = psrc[NP + 2u] = 0;
-    }
-  }
-  uint64_t excl = wave_out;
-  bool live = true;
-  if constexpr (LB) {
-    uint32_t polls = 0;
-    live = lookback(lb_global(desc), blk, excl, polls);
-    XDRG_STAMPV(6, polls);
-    if (!live) report(err, wr0, kOpRecordLevel, XDRG_ERR_LOOKBACK);
-    if (blk > 0 && lane == 0)
-      __hip_atomic_store(lb_global(desc) + blk, kLbIncl | ((excl + T) & kLbVal),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    wave_out = excl;
-    if (r + 1 == n) {  // offsets[n] and the total (k_scan_blocks' job in two passes)
-      offsets[n] = wave_out + T;
-      *total = wave_out + T;
-    }
-  }
-  XDRG_STAMP(3);
-  if (r < n) offsets[r] = wave_out + a0;
-  // ---- a wave whose bytes pass `cap`: the capacity checks, in the
-  // reference's order (xdr_generic_put::check, marshal.h:104-108); its list
-  // writes go to the histograms' room (cleared below)
-  const uint64_t ge = min<uint64_t>(wave_out + T, cap);
-  if (wave_out + T > cap && r < n && ok) {
-    enc_ctx<KMAX, true, WL> k;
-    k.sw = hist + lane;
-    k.nw = 0;
-    k.img = nullptr;
-    k.w0 = 0;
-    k.C = 0;
-    k.heap = heap;
-    k.heap_len = heap_len;
-    k.cap = cap;
-    k.stack_limit = stack_limit;
-    k.r = r;
-    k.err = err;
-    k.at = 0;
-    k.pos = wave_out + a0;
-#pragma unroll
-    for (int q = 0; q < KMAX; ++q) { k.psr[q] = 0; k.pds[q] = 0; k.pln[q] = 0; k.rb[q] = 0; }
-    bool okc = true;
-    if (mark) {
-      if (4 > cap - min(k.pos, cap)) {
-        report(err, r, kOpRecordLevel, XDRG_ERR_OVERFLOW_PUT);
-        okc = false;
-      } else {
-        k.put(mark_word(v - 4u));
-      }
-    }
-    (void)w.enc(k, reinterpret_cast<const uint8_t *>(rec), okc);
-  }
-  if (!live) return;
-  XDRG_STAMP(4);
-
-  // ---- output: lane-owned 16-byte chunks of the stretch, U per lane per
-  // round.  A chunk's words lie in the scalar-word stream or in payloads,
-  // both in stream order.  A = the last payload starting at or before the
-  // chunk's first byte = the count of payloads whose first chunk (the first
-  // chunk starting at or after the payload's start) is <= the chunk (a
-  // histogram over the round's chunks, scanned); a chunk holds the starts of
-  // at most two payloads (each is preceded by its length word and takes at
-  // least 4 bytes), so A and the next two (B, C) place every word: the last
-  // of them starting at or before it holds it, as a payload word or as a
-  // scalar word after it.
-  const uint32_t sh = static_cast<uint32_t>(wave_out & 15u);
-  const uint64_t g0 = wave_out - sh;
-  const uint32_t nch = (sh + T + 15u) >> 4;
-  uint32_t fr[KMAX];  // lane l: the first chunks of payload entries l + 1 + 64 j
-#pragma unroll
-  for (int j = 0; j < KMAX; ++j) {
-    const uint32_t e = lane + 64u * j;
-    fr[j] = e < NP ? (pay[e + 1u].x + sh + 15u) >> 4 : ~0u;
-  }
-  constexpr int U = kSencU;
-  uint32_t carry = 0;
-#pragma unroll
-  for (uint32_t k = 0; k < 2u * U; ++k) hist[lane + 64u * k] = 0u;
-  uint32_t par = 0;
-  for (uint32_t c0 = 0; c0 < nch; c0 += 64u * U, par ^= 1u) {
-    const uint32_t c1 = c0 + 64u * U;
-    uint32_t *h = hist + par * (64u * U);
-    wave_sync();
-#pragma unroll
-    for (int j = 0; j < KMAX; ++j)
-      if (fr[j] >= c0 && fr[j] < c1)
-        __hip_atomic_fetch_add(h + (fr[j] - c0), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    wave_sync();
-    uint32_t cnt[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      cnt[u] = carry + wave_incl_scan(h[lane + 64u * u]);
-      carry = rl32(cnt[u], 63);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) h[lane + 64u * u] = 0u;  // for the round after next
-    u32x4 E3[U][3];   // payloads A, B, C of the chunk: {x, len, padded end, padded bytes to it}
-    uint64_t S3[U][3];  // their heap offsets
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t e = min(cnt[u], NP);
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        E3[u][k] = pay[e + k];
-        S3[u][k] = psrc[e + k];
-      }
-    }
-    // classify the words; one load per payload piece, at its first word
-    uint32_t sel[U][4], keep[U][4], wv[U][4];
-    u32x4 ld[U][3];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int32_t t0 = static_cast<int32_t>(16u * (c0 + 64u * u + lane)) - static_cast<int32_t>(sh);
-      int32_t first[3] = {4, 4, 4};
-#pragma unroll
-      for (int i = 3; i >= 0; --i) {
-        const int32_t t = t0 + 4 * i;
-        const uint32_t q = static_cast<uint32_t>(t);
-        const bool lw_ = t >= 0 && q < T;
-        const uint32_t k = q >= E3[u][2].x ? 2u : q >= E3[u][1].x ? 1u : 0u;
-        const uint32_t ex = k == 2u ? E3[u][2].x : k == 1u ? E3[u][1].x : E3[u][0].x;
-        const uint32_t ey = k == 2u ? E3[u][2].y : k == 1u ? E3[u][1].y : E3[u][0].y;
-        const uint32_t ez = k == 2u ? E3[u][2].z : k == 1u ? E3[u][1].z : E3[u][0].z;
-        const uint32_t ew = k == 2u ? E3[u][2].w : k == 1u ? E3[u][1].w : E3[u][0].w;
-        const bool pw = lw_ && q < ez;
-        const uint32_t left = ey - (q - ex);
-        keep[u][i] = !lw_ ? 0u : pw && left < 4u ? keep_mask(left) : 0xffffffffu;
-        sel[u][i] = pw ? k : 3u;
-#pragma unroll
-        for (int kk = 0; kk < 3; ++kk) first[kk] = pw && k == static_cast<uint32_t>(kk) ? i : first[kk];
-        // a scalar word: its index in the word stream = its byte offset less
-        // the padded payload bytes before it
-        wv[u][i] = lw_ && !pw ? ws[(q - ew) >> 2] : 0u;
-      }
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        ld[u][k] = u32x4{0u, 0u, 0u, 0u};
-        if (first[k] < 4) {
-          const uint64_t a = S3[u][k] + (static_cast<uint32_t>(t0 + 4 * first[k]) - E3[u][k].x);
-          // dword-aligned loads (a byte-misaligned 16-byte load is split
-          // by the address unit), shifted into place
-          const uint64_t a4 = a & ~3ull;
-          const uint32_t sb = static_cast<uint32_t>(a & 3u);
-          if (a4 + 20u <= heap_len) {
-            const u32x4 t = ld16u(heap + a4);
-            const uint32_t t4 = sb ? ld32(heap + a4 + 16u) : 0u;
-            ld[u][k] = u32x4{__builtin_amdgcn_alignbyte(t.y, t.x, sb), __builtin_amdgcn_alignbyte(t.z, t.y, sb),
-                             __builtin_amdgcn_alignbyte(t.w, t.z, sb), __builtin_amdgcn_alignbyte(t4, t.w, sb)};
-          } else {  // the heap's last 19 bytes
-            ld[u][k] = a + 16u <= heap_len ? ld16u(heap + a) : heap_tail16(heap, heap_len, a);
-          }
-        }
-      }
-      // word i of piece k is word (i - first[k]) of its load
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        uint32_t x = wv[u][i];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          const int32_t f = first[k];
-          const u32x4 &g = ld[u][k];
-          const uint32_t y = i - f == 0 ? g.x : i - f == 1 ? g.y : i - f == 2 ? g.z : g.w;
-          x = sel[u][i] == static_cast<uint32_t>(k) ? y : x;
-        }
-        wv[u][i] = x & keep[u][i];
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t ck = c0 + 64u * u + lane;
-      if (ck >= nch) continue;
-      const int32_t t0 = static_cast<int32_t>(16u * ck) - static_cast<int32_t>(sh);
-      const uint64_t ca = g0 + 16ull * ck;
-      if constexpr ((XDRG_STREAM_DBG & 1) != 0) {
-        if ((wv[u][0] ^ wv[u][1] ^ wv[u][2] ^ wv[u][3]) == 0x12345678u) st32(xdr + ca, 0u);
-        continue;
-      }
-      if (t0 >= 0 && ca + 16u <= ge) {
-        const u32x4 o4 = u32x4{wv[u][0], wv[u][1], wv[u][2], wv[u][3]};
-        if constexpr ((XDRG_ENC_NT & 2) != 0)
-          __builtin_nontemporal_store(o4, reinterpret_cast<u32x4 *>(xdr + ca));
-        else
-          *reinterpret_cast<u32x4 *>(xdr + ca) = o4;
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int32_t t = t0 + 4 * i;
-          if (t >= 0 && static_cast<uint32_t>(t) < T && ca + 4u * i + 4u <= ge) st32(xdr + ca + 4u * i, wv[u][i]);
-        }
-      }
-    }
-  }
-  XDRG_STAMP(5);
-}
 
 // ---------------------------------------------------------------- decode
 // LDS of a decode wave: the native tile (none when the walk decodes into

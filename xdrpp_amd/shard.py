@@ -33,7 +33,7 @@ def seed_for(schema: str, world: int) -> int:
     if schema == "rec128":
         return W.SEED_REC128 if world == 1 else W.SEED_REC128_MGPU
     return {"numerics": W.SEED_NUMERICS, "recvar": W.SEED_RECVAR, "rpc": W.SEED_RPC,
-            "vecrec": W.SEED_VECREC, "containertest": W.SEED_CONTAINERTEST}[schema]
+            "vecrec": W.SEED_VECREC, "containertest": W.SEED_CONTAINERTEST, "rp_list": W.SEED_RP_LIST}[schema]
 
 
 def shard_inputs(schema: str, n_per_rank: int, rank: int, world: int
