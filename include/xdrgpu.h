@@ -509,7 +509,11 @@ int xdrg_decode_msgs(const xdrg_plan *plan, const void *d_stream, uint64_t len,
  * walked mark by mark on the device between list-ranking windows over the
  * rest, and the call waits on the stream once or twice per window (every
  * byte is read about twice at most).
- * Workspace: xdrg_index_workspace_size(len, max_msg_len).
+ * Workspace: xdrg_index_workspace_size(len, max_msg_len).  Its contents are
+ * the call's own: the path flag xdrg_index_records leaves in its last 256
+ * bytes is not part of this call's contract (with max_msg_len past
+ * XDRG_INDEX_MAX_MSG those bytes hold the windows' continuation block, and
+ * the index pass's own 256-byte tail sits just before them).
  */
 int xdrg_index_msgs(const void *d_stream, uint64_t len, uint32_t max_msg_len,
                     uint64_t max_msgs, uint64_t *d_offsets, uint64_t *d_count,

@@ -1,7 +1,8 @@
 """A/B of the var encode variants on 1M records, one process, interleaved:
 the two-pass encode (size pass + scan + windowed encode), the one-pass
-encode (look-back), and the one-pass kernel's sized
-half (bases from a size pass + scan run beforehand, timed alone).  Prints
+encode (look-back), its sized half alone (bases
+from a size pass + scan run beforehand) and both halves timed together
+(halves: walk-first record kernel; halves0: the two-pass record kernel).  Prints
 ms per call (HIP events on the launch stream, mean of REPS after a warmup)
 and checks every variant's bytes against the first.
 
@@ -19,8 +20,9 @@ from xdrpp_amd import _abi as A, marshal as M, schemas as S, workloads as W  # n
 
 VAR_OPTS = {
     "two_pass": {"enc_stream": 0}, "lb": {"enc_stream": 1}, "sized": {"enc_stream": 1},
+    "halves": {"enc_stream": 1}, "halves0": {"enc_stream": 0},
 }
-VARIANTS = os.environ.get("VARIANTS", "two_pass lb sized").split()
+VARIANTS = os.environ.get("VARIANTS", "two_pass halves0 halves lb sized").split()
 REPS = int(os.environ.get("REPS", "20"))
 
 dev = torch.device("cuda:0")
@@ -39,7 +41,15 @@ for schema in sys.argv[1:] or ["recvar", "rpc"]:
 
     def launch(v):
         mar = mars[v]
-        if v.startswith("sized"):
+        if v.startswith("halves"):  # xdrg_encode_sizes + xdrg_encode_sized, both timed
+            ws = mar._workspace(n)
+            A.check(L.xdrg_encode_sizes(mar.plan.handle, nat.data_ptr(), n, heap.data_ptr(), heap.numel(),
+                                        A.DEFAULT_STACK_LIMIT, 0, ws.data_ptr(), ws.numel(), mar.status.ptr,
+                                        s.cuda_stream), "sizes")
+            A.check(L.xdrg_encode_sized(mar.plan.handle, nat.data_ptr(), n, heap.data_ptr(), heap.numel(),
+                                        out.data_ptr(), total, offs.data_ptr(), A.DEFAULT_STACK_LIMIT, 0,
+                                        ws.data_ptr(), ws.numel(), mar.status.ptr, s.cuda_stream), "sized")
+        elif v.startswith("sized"):
             ws = mar._workspace(n)
             A.check(L.xdrg_encode_sized(mar.plan.handle, nat.data_ptr(), n, heap.data_ptr(), heap.numel(),
                                         out.data_ptr(), total, offs.data_ptr(), A.DEFAULT_STACK_LIMIT, 0,

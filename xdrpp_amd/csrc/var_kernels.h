@@ -365,26 +365,34 @@ __device__ __forceinline__ uint64_t wave_max64(uint64_t x) {
 
 // Decoupled look-back (single-pass chained scan): the exclusive prefix of
 // block `blk`'s total.  desc[i] = state | value, one 8-byte word written by
-// one store (the data is the flag).  Lane l reads blocks top - l - 64u, u < 4.
-// Returns false when a predecessor never published (kLbSpinLimit polls).
+// one store (the data is the flag).  Lane l reads blocks top - l - 64u,
+// u < PER (64 PER blocks per poll: a poll is a round trip past the per-XCD
+// L2s, so the window spans the waves resident at once -- 4 per lane took 4.3
+// polls on average, profiles/r04s).  Returns false when a predecessor never
+// published (kLbSpinLimit polls).
+#ifndef XDRG_LB_PER
+#define XDRG_LB_PER 16  // look-back window per poll, blocks per lane (tools/tune/stream_stamps.py CFLAGS)
+#endif
+template <int PER = XDRG_LB_PER>
 __device__ __forceinline__ bool lookback(lb_u64 *desc, uint32_t blk, uint64_t &excl, uint32_t &polls) {
+  constexpr uint32_t WIN = 64u * PER;
   const uint32_t lane = __lane_id();
   excl = 0;
   polls = 0;
   int64_t top = static_cast<int64_t>(blk) - 1;
   for (uint32_t spins = 0; top >= 0;) {
-    uint64_t d[4];
+    uint64_t d[PER];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < PER; ++u) {
       const int64_t i = top - lane - 64 * u;
       d[u] = i >= 0 ? __hip_atomic_load(desc + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kLbIncl;
     }
     ++polls;
     // first block (in look-back order) that has not published, and the
     // first that holds an inclusive prefix
-    uint32_t dn = 256, dp = 256;
+    uint32_t dn = WIN, dp = WIN;
 #pragma unroll
-    for (int u = 3; u >= 0; --u) {
+    for (int u = PER - 1; u >= 0; --u) {
       const unsigned long long mn = __ballot((d[u] >> 62) == 0u);
       const unsigned long long mp = __ballot((d[u] >> 62) == 2u);
       if (mn) dn = 64u * u + __builtin_ctzll(mn);
@@ -395,7 +403,7 @@ __device__ __forceinline__ bool lookback(lb_u64 *desc, uint32_t blk, uint64_t &e
     // the aggregates (each < 2^31) in two parts, summed with DPP (no LDS)
     uint32_t lo = 0, hi = 0;
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < PER; ++u)
       if (lane + 64u * u < lim) {
         lo += static_cast<uint32_t>(d[u]) & 0xffffffu;
         hi += static_cast<uint32_t>((d[u] & kLbVal) >> 24);
@@ -404,13 +412,13 @@ __device__ __forceinline__ bool lookback(lb_u64 *desc, uint32_t blk, uint64_t &e
     if (found) {  // + the inclusive prefix at dp
       uint64_t pv = 0;
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < PER; ++u)
         if (dp / 64u == static_cast<uint32_t>(u)) pv = rl64(d[u], dp % 64u);
       excl += pv & kLbVal;
       return true;
     }
     top -= lim;
-    if (dn < 256) {  // a block before this one is still walking its records
+    if (dn < WIN) {  // a block before this one is still walking its records
       if (++spins > kLbSpinLimit) return false;
       __builtin_amdgcn_s_sleep(1);
     }
