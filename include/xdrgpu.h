@@ -303,12 +303,13 @@ enum xdrg_plan_option {
                                      containers: LDS stage of a 64-record group's
                                      element arrays (written out as whole lines
                                      after the walk), -1 auto, 0 none           */
-  XDRG_OPT_ENC_STREAM = 15,      /* plan-specialized word-list plans: 1 the record
-                                     kernel walks first (its walk gives the sizes):
-                                     xdrg_encode runs no size pass and no scan, each
-                                     wave's base by a look-back over the byte totals
-                                     of the waves before it; 0 the size pass + scan
-                                     + record kernel                                */
+  XDRG_OPT_ENC_STREAM = 15,      /* plan-specialized word-list plans: -1 (default)
+                                     the size pass + scan + a record kernel that
+                                     walks each record once, first; 1 the same
+                                     record kernel with no size pass and no scan
+                                     (xdrg_encode: each wave's base by a look-back
+                                     over the byte totals of the waves before it);
+                                     0 the record kernel that walks per window   */
   XDRG_OPT_INDEX_FAST = 13        /* xdrg_index_records: 1 (default) the speculative
                                      chain walk first, then the call waits for its
                                      verdict and runs the list ranking only when a

@@ -105,8 +105,9 @@ static uint32_t vec_wire(const plan_t *P, uint32_t pc) {
   return w;
 }
 /* Decoded element arrays of record r come from [align16(len) + F * off[r],
- * align16(len) + F * off[r+1]) for plans with element subroutines, packed
- * per group of 64 records otherwise (rec_ebytes below).  Fixed elements:
+ * align16(len) + F * off[r+1]) for recursive plans (element subroutines
+ * that can nest past XDRG_SUB_FRAMES), packed per group of 64 records
+ * otherwise (rec_ebytes below).  Fixed elements:
  * F = 1 + the largest native/wire size ratio of an element type (+ 2 when
  * packed).  Subroutine elements: distinct elements start at distinct wire
  * words, so stride/4 per wire byte, plus 2 for the 8-byte alignment of each
@@ -147,18 +148,37 @@ static uint64_t *min_wires(const xdrg_op *ops, uint32_t nops, const uint32_t *ta
   return m;
 }
 
-/* Plans whose containers all hold fixed-size elements (no element
- * subroutine) pack each group of 64 records' arrays back to back (below);
- * their factor carries 2 more bytes per wire byte for the 8-byte rounding
- * of every array (xdrpp_amd/csrc/plan.cpp). */
+/* Element-subroutine frames a walk entering the region at `start` can
+ * open below it (UINT32_MAX: the region can enter itself -- a recursive
+ * type), as plan.cpp computes them; on[] marks the regions on the path. */
+static uint32_t sub_frames(const plan_t *P, uint32_t start, uint8_t *on) {
+  uint32_t f = 0;
+  on[start] = 1;
+  for (uint32_t pc = start; pc < P->nops && P->ops[pc].kind != XDRG_OP_END; ++pc) {
+    const xdrg_op *op = &P->ops[pc];
+    if (op->kind != XDRG_OP_VECTOR || !(op->flags & XDRG_F_SUB)) continue;
+    uint32_t g = on[op->arg4] ? UINT32_MAX : sub_frames(P, op->arg4, on);
+    g = g == UINT32_MAX ? UINT32_MAX : g + 1;
+    if (g > f) f = g;
+  }
+  on[start] = 0;
+  return f;
+}
+/* Plans with containers whose walks never need the deep passes (at most
+ * XDRG_SUB_FRAMES element frames, no recursive type) pack each group of 64
+ * records' arrays back to back (below); their factor carries 2 more bytes
+ * per wire byte for the 8-byte rounding of every array
+ * (xdrpp_amd/csrc/plan.cpp).  Recursive plans keep per-record areas. */
 static int packed_plan(const plan_t *P) {
   int vec = 0;
   for (uint32_t pc = 0; pc < P->nops; ++pc)
-    if (P->ops[pc].kind == XDRG_OP_VECTOR) {
-      if (P->ops[pc].flags & XDRG_F_SUB) return 0;
-      vec = 1;
-    }
-  return vec;
+    if (P->ops[pc].kind == XDRG_OP_VECTOR) vec = 1;
+  if (!vec) return 0;
+  uint8_t *on = (uint8_t *)calloc((size_t)P->nops + 1, 1);
+  if (!on) abort();
+  const uint32_t f = sub_frames(P, 0, on);
+  free(on);
+  return f <= XDRG_SUB_FRAMES;
 }
 static uint32_t heap_factor(const plan_t *P) {
   uint32_t f = 0;
@@ -184,45 +204,57 @@ static uint32_t heap_factor(const plan_t *P) {
  * counts, discriminants; no value checks) adding align8(min(cnt, rem /
  * wire + 1) * stride) per container, rem = the record's bytes after the
  * count, stopping where the structure stops parsing -- what the decode's
- * area check (elem_area_ok) needs, so valid records always fit -- capped at
+ * area check (elem_area_ok) needs, so valid records always fit; an element
+ * subroutine's array counts align8(cnt * stride) when the bytes left can
+ * hold its count, then its elements' own arrays -- capped at
  * align8-down(F * (b - a) - 8) so that no group outgrows its F-sized area.
  * The device kernels compute the same E(r) before their walks and place
  * the group's records by a wave scan (xdrpp_amd/csrc: dec_ebytes,
  * codegen.cpp ebytes). */
-static uint64_t rec_ebytes(const plan_t *P, const uint8_t *s, uint64_t p, uint64_t b) {
-  uint64_t E = 0;
-  uint32_t pc = 0;
+/* From pc to its region's END; *pp advanced.  Returns 0 where the
+ * structure stops parsing (E holds the arrays up to there). */
+static int ebytes_ops(const plan_t *P, const uint8_t *s, uint64_t *pp, uint64_t b, uint32_t pc, uint64_t *E) {
+  uint64_t p = *pp;
   for (;;) {
     const xdrg_op *op = &P->ops[pc];
     switch (op->kind) {
-    case XDRG_OP_END: return E;
+    case XDRG_OP_END: *pp = p; return 1;
     case XDRG_OP_JUMP: pc = op->arg0; continue;
-    case XDRG_OP_U64: if (b - p < 8) return E; p += 8; ++pc; continue;
-    case XDRG_OP_OPAQUE: if (b - p < op->arg0) return E; p += pad4(op->arg0); ++pc; continue;
-    case XDRG_OP_U32: case XDRG_OP_BOOL: case XDRG_OP_ENUM: if (b - p < 4) return E; p += 4; ++pc; continue;
+    case XDRG_OP_U64: if (b - p < 8) return 0; p += 8; ++pc; continue;
+    case XDRG_OP_OPAQUE: if (b - p < op->arg0) return 0; p += pad4(op->arg0); ++pc; continue;
+    case XDRG_OP_U32: case XDRG_OP_BOOL: case XDRG_OP_ENUM: if (b - p < 4) return 0; p += 4; ++pc; continue;
     default: break;
     }
-    if (b - p < 4) return E;
+    if (b - p < 4) return 0;
     const uint32_t v = bswap32(rd32(s + p));
     p += 4;
     switch (op->kind) {
     case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING:
-      if (v > op->arg0 || b - p < v) return E;
+      if (v > op->arg0 || b - p < v) return 0;
       p += pad4(v);
       ++pc;
       break;
     case XDRG_OP_UNION: {
       const int64_t t = union_target(P, op, v);
-      if (t < 0) return E;
+      if (t < 0) return 0;
       pc = (uint32_t)t;
       break;
     }
     case XDRG_OP_VECTOR: {
-      if (v > op->arg0) return E;
-      const uint64_t w = vec_wire(P, pc), rem = b - p;
+      if (v > op->arg0) return 0;
+      const uint64_t rem = b - p;
+      if (op->flags & XDRG_F_SUB) {  /* every element consumes at least minw[body] bytes */
+        if ((uint64_t)v * P->minw[op->arg4] > rem) return 0;
+        *E += ((uint64_t)v * op->arg1 + 7) & ~7ull;
+        for (uint32_t i = 0; i < v; ++i)
+          if (!ebytes_ops(P, s, &p, b, op->arg4, E)) return 0;
+        ++pc;
+        break;
+      }
+      const uint64_t w = vec_wire(P, pc);
       const uint64_t k = rem / w + 1 < v ? rem / w + 1 : v;
-      E += (k * op->arg1 + 7) & ~7ull;
-      if (rem < (uint64_t)v * w) return E;
+      *E += (k * op->arg1 + 7) & ~7ull;
+      if (rem < (uint64_t)v * w) return 0;
       p += (uint64_t)v * w;
       pc += 1 + op->arg2;
       break;
@@ -230,6 +262,11 @@ static uint64_t rec_ebytes(const plan_t *P, const uint8_t *s, uint64_t p, uint64
     default: ++pc; break;
     }
   }
+}
+static uint64_t rec_ebytes(const plan_t *P, const uint8_t *s, uint64_t p, uint64_t b) {
+  uint64_t E = 0;
+  (void)ebytes_ops(P, s, &p, b, 0, &E);
+  return E;
 }
 static uint64_t ebudget(uint32_t F, uint64_t a, uint64_t b) {
   const uint64_t t = (uint64_t)F * (b - a);

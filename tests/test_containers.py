@@ -186,6 +186,34 @@ def test_oracle_packed_element_areas(n):
         assert cur <= end
 
 
+@pytest.mark.parametrize("n", [1, 64, 200])
+def test_oracle_packed_subroutine_areas(n):
+    """Element-subroutine containers of a non-recursive plan (containertest's
+    u_4_12 uvec<>) pack the same way: each record's uvec array follows the
+    one before it, 8-aligned, from align8(ebase + F * off[64g]); a
+    recursive plan (test_recursive) keeps per-record areas."""
+    from xdrpp_amd import workloads as W
+    cp = compile_plan(S.containertest)
+    nat, heap = W.GENERATORS["containertest"](n)
+    x, offs = O.encode(cp, nat, n, heap)
+    dn, dh = O.decode(cp, x, n, offs)
+    assert np.array_equal(O.encode(cp, dn, n, dh)[0], x)
+    no = S.containertest.offsets["uvec"]
+    st = S.u_4_12.size
+    ebase = (x.size + 15) & ~15
+    F = (dh.size - ebase) // x.size
+    recs = dn.reshape(n, cp.stride)
+    for g in range(0, n, 64):
+        cur = (ebase + F * int(offs[g]) + 7) & ~7
+        end = ebase + F * int(offs[min(g + 64, n)])
+        for r in range(g, min(g + 64, n)):
+            off = int(recs[r, no:no + 8].view(np.uint64)[0])
+            cnt = int(recs[r, no + 8:no + 12].view(np.uint32)[0])
+            assert off == cur
+            cur = (cur + cnt * st + 7) & ~7
+        assert cur <= end
+
+
 @pytest.mark.skipif(not os.path.exists(f"{REF}/xdrpp/marshal.cc"), reason="reference tree absent")
 def test_fixture_regenerates(tmp_path):
     """containers.json is what the reference produces today (empty diff)."""

@@ -26,9 +26,10 @@ from xdrpp_amd import schemas as S  # noqa: E402
 from xdrpp_amd import workloads as W  # noqa: E402
 import oracle_bridge as O  # noqa: E402
 
-# plan options: the walk-first encode and the two-pass encode (size pass +
-# scan + record kernel) it replaces
-MODES = {"stream": {"enc_stream": 1}, "two_pass": {"enc_stream": 0}}
+# plan options: the walk-first record kernel with no size pass (look-back),
+# the default (size pass + scan + walk-first record kernel), and the record
+# kernel that walks per window
+MODES = {"stream": {"enc_stream": 1}, "walk_first": {}, "two_pass": {"enc_stream": 0}}
 _plans = {}
 
 

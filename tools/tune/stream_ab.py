@@ -19,10 +19,10 @@ sys.path.insert(0, ROOT)
 from xdrpp_amd import _abi as A, marshal as M, schemas as S, workloads as W  # noqa: E402
 
 VAR_OPTS = {
-    "two_pass": {"enc_stream": 0}, "lb": {"enc_stream": 1}, "sized": {"enc_stream": 1},
-    "halves": {"enc_stream": 1}, "halves0": {"enc_stream": 0},
+    "two_pass": {"enc_stream": 0}, "walk_first": {"enc_stream": -1}, "lb": {"enc_stream": 1},
+    "sized": {"enc_stream": -1}, "halves": {"enc_stream": -1}, "halves0": {"enc_stream": 0},
 }
-VARIANTS = os.environ.get("VARIANTS", "two_pass halves0 halves lb sized").split()
+VARIANTS = os.environ.get("VARIANTS", "two_pass walk_first lb sized").split()
 REPS = int(os.environ.get("REPS", "20"))
 
 dev = torch.device("cuda:0")

@@ -302,7 +302,8 @@ struct gen {
   // Packed element areas: the bytes a record's arrays take, each rounded up
   // to 8 (oracle/xdr_oracle.c rec_ebytes, var_kernels.h packed_area) -- a
   // walk of its lengths, counts and discriminants that stops (returns E)
-  // where the structure stops parsing.  Plans without element subroutines.
+  // where the structure stops parsing.  Element subroutines (non-recursive:
+  // packed plans are never deep) are walked inline per element.
   void eb_block(uint32_t pc, uint32_t stop) {
     auto need = [&](const std::string &n) { line("if (b - q < " + n + ") return E;"); };
     auto word = [&]() { need("4"); line("{ const uint32_t v = bswap32(rd(q)); q += 4;"); };
@@ -323,6 +324,20 @@ struct gen {
         word();
         line("  if (v > " + u32(e.arg0) + ") return E;");
         line("  const uint64_t left = b - q;");
+        if (e.flags & XDRG_F_SUB) {
+          // an element subroutine: its array when the bytes left can hold
+          // the count (arg3 = the least an element consumes), then each
+          // element's own arrays (the body inline)
+          line("  if (left < static_cast<uint64_t>(v) * " + u32(e.arg3) + ") return E;");
+          line("  E += (static_cast<uint64_t>(v) * " + u32(e.arg1) + " + 7u) & ~7ull;");
+          line("  for (uint32_t i = 0; i < v; ++i) {");
+          ind += 4;
+          eb_block(e.arg4, body_end(e.arg4));
+          ind -= 4;
+          line("  } }");
+          ++pc;
+          continue;
+        }
         line("  E += (min<uint64_t>(v, left / " + u32(e.arg3) + " + 1u) * " + u32(e.arg1) + " + 7u) & ~7ull;");
         line("  if (left < static_cast<uint64_t>(v) * " + u32(e.arg3) + ") return E;");
         line("  q += static_cast<uint64_t>(v) * " + u32(e.arg3) + "; }");

@@ -284,12 +284,6 @@ int compile_plan(xdrg_plan &p) {
       return XDRG_EINVAL;
   }
   if (!saw_end || p.ops.back().kind != XDRG_OP_END) return XDRG_EINVAL;
-  // containers of fixed-size elements only: each group of 64 records packs
-  // its decoded arrays back to back, every array rounded up to 8 bytes
-  // (include/xdrgpu.h xdrg_decode_heap_size); 2 bytes per wire byte more
-  // than the record's own arrays need cover that rounding
-  p.packed = p.has_vector && !p.has_sub;
-  if (p.packed) p.heap_factor += 2;
 
   p.has_checks = false;
   p.checks.clear();
@@ -407,6 +401,13 @@ int compile_plan(xdrg_plan &p) {
       }
       p.deep = frames[0] > XDRG_SUB_FRAMES;
     }
+    // plans whose walks never need the deep passes (no recursive type):
+    // each group of 64 records packs its decoded arrays back to back, every
+    // array rounded up to 8 bytes (include/xdrgpu.h xdrg_decode_heap_size,
+    // oracle/xdr_oracle.c packed_plan); 2 bytes per wire byte more than the
+    // record's own arrays need cover that rounding
+    p.packed = p.has_vector && !p.deep;
+    if (p.packed) p.heap_factor += 2;
     p.max_chunks16 = chunks[0];
     p.max_var_slots = slots[0];
     p.max_scalar_words = words[0];

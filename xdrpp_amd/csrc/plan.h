@@ -110,7 +110,7 @@ struct plan_opts {
   int index_fast = 1;      // record index: speculative chain walk before the list ranking
                            // (1: the host waits for its flag; 2: asynchronous; 0: off)
   int stage_bytes = -1;    // window decode of packed plans: LDS stage of a group's arrays
-  int enc_stream = 0;      // word-list plans: 1 the walk-first encode (look-back), 0 two passes
+  int enc_stream = -1;     // word-list plans: -1 walk-first record kernel, 1 + look-back (no size pass), 0 per-window walk
 };
 
 }  // namespace xdrg

@@ -86,6 +86,7 @@ struct sub_pass {
   sub_frame *slabs;                // deep: `slab` frames per lane
   uint32_t slab;
   uint32_t last;                   // 1: running out of frames is xdr_stack_overflow
+  uint32_t packed;                 // decode, main pass of a non-recursive plan: packed element areas
 };
 
 enum : int { kWalkCont = -1, kWalkOk = 0, kWalkErr = 1, kWalkFull = 2 };
@@ -585,11 +586,92 @@ __device__ int sub_decode_rec(const xdrg_op *__restrict__ sops, const uint32_t *
   return kWalkOk;
 }
 
+// Packed element areas (oracle/xdr_oracle.c rec_ebytes): the bytes the
+// element arrays of the record at [p, b) take, each rounded up to 8 -- a
+// walk of its lengths, counts and discriminants (no value checks) that
+// stops where the structure stops parsing.  An element subroutine's array
+// counts when the bytes left can hold its count (arg3 = the least an
+// element consumes), then its elements' own arrays.  Non-recursive plans
+// only (packed): kSubFrames frames always suffice.
+__device__ uint64_t sub_ebytes(const xdrg_op *__restrict__ ops, const uint32_t *__restrict__ table,
+                               const uint8_t *__restrict__ xdr, uint64_t p, uint64_t b) {
+  uint32_t left[kSubFrames], vpc[kSubFrames];
+  uint32_t fp = 0, pc = 0;
+  uint64_t E = 0;
+  for (;;) {
+    const xdrg_op &op = ops[pc];
+    if (op.kind == XDRG_OP_END) {
+      if (!fp) return E;
+      if (left[fp - 1]) { --left[fp - 1]; pc = ops[vpc[fp - 1]].arg4; }
+      else pc = vpc[--fp] + 1;
+      continue;
+    }
+    if (op.kind == XDRG_OP_JUMP) { pc = op.arg0; continue; }
+    const uint64_t rem = b - p;
+    switch (op.kind) {
+    case XDRG_OP_U64: if (rem < 8) return E; p += 8; ++pc; continue;
+    case XDRG_OP_OPAQUE: if (rem < op.arg0) return E; p += (op.arg0 + 3u) & ~3u; ++pc; continue;
+    case XDRG_OP_U32: case XDRG_OP_BOOL: case XDRG_OP_ENUM: if (rem < 4) return E; p += 4; ++pc; continue;
+    default: break;
+    }
+    if (rem < 4) return E;
+    const uint32_t v = bswap32(ld32(xdr + p));
+    p += 4;
+    const uint64_t lft = b - p;
+    switch (op.kind) {
+    case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING:
+      if (v > op.arg0 || v > lft) return E;
+      p += (static_cast<uint64_t>(v) + 3u) & ~3ull;
+      ++pc;
+      break;
+    case XDRG_OP_UNION: {
+      const int t = union_target(op, table, v);
+      if (t < 0) return E;
+      pc = static_cast<uint32_t>(t);
+      break;
+    }
+    case XDRG_OP_VECTOR:
+      if (v > op.arg0) return E;
+      if (op.flags & XDRG_F_SUB) {
+        if (lft < static_cast<uint64_t>(v) * op.arg3) return E;
+        E += (static_cast<uint64_t>(v) * op.arg1 + 7u) & ~7ull;
+        if (!v) { ++pc; break; }
+        if (fp == kSubFrames) return E;  // (a packed plan never nests this deep)
+        left[fp] = v - 1;
+        vpc[fp++] = pc;
+        pc = op.arg4;
+        break;
+      }
+      E += (min<uint64_t>(v, lft / op.arg3 + 1u) * op.arg1 + 7u) & ~7ull;
+      if (lft < static_cast<uint64_t>(v) * op.arg3) return E;
+      p += static_cast<uint64_t>(v) * op.arg3;
+      pc += 1 + op.arg2;
+      break;
+    default: ++pc; break;
+    }
+  }
+}
+
 template <class OPS>
 __device__ __forceinline__ void sub_decode_kernel(XDRG_SUB_DECODE_PARAMS) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   xdrg_op *sops = reinterpret_cast<xdrg_op *>(smem);
   load_ops(sops, ops, nops);
+  // packed element areas (main pass): the wave's 64 records are one group
+  uint64_t pk_cur = 0, pk_end = 0;
+  if (P.packed && !P.list) {
+    const uint64_t r = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const uint64_t r0 = r - (threadIdx.x & 63u);
+    if (r0 < n) {  // wave-uniform
+      const bool in = r < n;
+      const uint64_t a = in ? offsets[r] : 0, b = in ? offsets[r + 1] : 0;
+      const bool bad = in && (b < a || b > len);
+      const bool on = in && !bad && a + mark <= b;
+      const uint64_t e = on ? sub_ebytes(sops, table, xdr, a + mark, b) : 0u;
+      const uint64_t E = on ? min(e, ebudget(F, a, b)) : 0u;
+      (void)packed_area(E, bad, offsets[r0], ebase, F, pk_cur, pk_end);
+    }
+  }
   sub_records(P, n, [&](uint64_t r, auto &st) {
     const uint64_t a = offsets[r], b = offsets[r + 1];
     if (!P.list) {  // record-level checks: the main pass reports them once
@@ -602,9 +684,11 @@ __device__ __forceinline__ void sub_decode_kernel(XDRG_SUB_DECODE_PARAMS) {
       if ((b - a) & 3u) { report(err, r, kOpRecordLevel, XDRG_ERR_SIZE_NOT_MULT4); return; }
     }
     uint32_t full_op = 0;
+    const bool pk = P.packed && !P.list;
     if (sub_decode_rec<OPS>(sops, table, xdr, a + mark, b, native + r * stride, stride, heap,
-                       ebase + static_cast<uint64_t>(F) * a, ebase + static_cast<uint64_t>(F) * b, stack_limit, r,
-                       err, &full_op, st) == kWalkFull)
+                            pk ? pk_cur : ebase + static_cast<uint64_t>(F) * a,
+                            pk ? pk_end : ebase + static_cast<uint64_t>(F) * b, stack_limit, r, err, &full_op,
+                            st) == kWalkFull)
       sub_full(P, r, full_op, XDRG_ERR_STACK_GET, err);
   });
 }

@@ -965,35 +965,6 @@ struct dec_ctx {
   }
 };
 
-// Packed element areas (plans without element subroutines; oracle/
-// xdr_oracle.c rec_ebytes): the wave's 64 records are one group, whose
-// arrays follow each other from align8(ebase + F * a of the first record).
-// E = the record's share (the walker's ebytes, capped at
-// align8-down(F * (b - a) - 8)); `bad` = offsets the decode refuses (b < a,
-// b > len).  From the first bad record on the group gets empty areas: the
-// records before it lie inside [a0, b) of the stream, so their shares stay
-// inside the group's F-sized area whatever the later offsets hold, and the
-// reported error is that record's (or an earlier one's).  Every lane of the
-// wave must be active.
-__device__ __forceinline__ uint64_t ebudget(uint32_t F, uint64_t a, uint64_t b) {
-  const uint64_t t = static_cast<uint64_t>(F) * (b - a);
-  return t >= 8u ? (t - 8u) & ~7ull : 0u;
-}
-__device__ __forceinline__ uint64_t packed_area(uint64_t E, bool bad, uint64_t a0, uint64_t ebase, uint32_t F,
-                                                uint64_t &ecur, uint64_t &eend) {
-  const uint32_t lane = __lane_id();
-  const unsigned long long bm = __ballot(bad);
-  if (bm & ((2ull << lane) - 1ull)) E = 0;  // a bad record at or before this one
-  uint64_t inc = E;
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint64_t x = __shfl_up(inc, o, 64);
-    if (lane >= static_cast<uint32_t>(o)) inc += x;
-  }
-  const uint64_t g0 = (ebase + static_cast<uint64_t>(F) * a0 + 7u) & ~7ull;
-  ecur = g0 + inc - E;
-  eend = g0 + inc;
-  return g0;
-}
 
 // NWD > 0 (plan-specialized walks, whose native offsets are constants): the
 // lane decodes its record into NWD registers and stores them itself, so the

@@ -1776,29 +1776,28 @@ int var_encode(const xdrg_plan &P, const dev_tables &T, const void *d_native, ui
     if (lds_s > kVarLdsBudget || !aligned(d_native, 16)) SM = nullptr;
   }
   // Word-list plans walked first (var_kernels.h var_encode_body, PRE): the
-  // record kernel's own walk gives the sizes, so there is no size pass --
-  // xdrg_encode finds each wave's base by a decoupled look-back over the
-  // byte totals of the waves before it (no scan either); xdrg_encode_sized
-  // reads it from the scan xdrg_encode_sizes left.  The walk runs without
-  // the stack checks, so the plan's depth must fit the budget; a wave stays
-  // under 2^31 bytes; a capacity re-walk lists its words in the image.
-  if (SM && SM->f_enc_lb && O.enc_stream && phase != kEncSizes && p->max_depth <= stack_limit &&
-      64ull * max_rec < (1ull << 31) && 256u * p->spec.info.list_words <= Cs) {
+  // record kernel's walk runs once, before the windows, from registers and
+  // without the checks (the plan's depth must fit the stack budget; a wave
+  // stays under 2^31 bytes; a capacity re-walk lists its words in the
+  // image), and it reads no sizes -- fewer registers than the per-window
+  // walk (rpc 105 VGPRs vs 169): rpc size pass + scan + record kernel 0.155
+  // ms vs 0.203, recvar 0.102 vs 0.103 (profiles/r04v).  XDRG_OPT_ENC_STREAM
+  // 1 drops the size pass and scan as well, each wave's base from a
+  // decoupled look-back over the totals of the waves before it: slower here
+  // (rpc 0.262, recvar 0.187 ms): the polls cross the XCDs' L2s
+  // (profiles/r04t).
+  const bool pre = SM && SM->f_enc_pre && O.enc_stream != 0 && p->max_depth <= stack_limit &&
+                   64ull * max_rec < (1ull << 31) && 256u * p->spec.info.list_words <= Cs;
+  if (pre && O.enc_stream == 1 && phase == kEncBoth) {
     uint64_t *total = &d_status->total_bytes;
     unsigned long long *desc = bsum;  // the nb wave totals (look-back descriptors)
     const unsigned long long *bb = bbase;
     uint32_t nb32 = static_cast<uint32_t>(nb), sl = stack_limit, cc = Cs, mk = mark;
     void *args[] = {&nat8, &n, const_cast<uint32_t *>(&p->stride), &d_heap, &heap_len, &xdr8, &cap,
                     &d_offsets, &bb, &desc, &nb32, &total, &sl, &cc, &mk, &err};
-    hipFunction_t f;
-    if (phase == kEncBoth) {
-      HIPCHK(hipMemsetAsync(desc, 0, align_up(nb * 8, 16), s));
-      f = static_cast<hipFunction_t>(SM->f_enc_lb);
-    } else {  // block bases from xdrg_encode_sizes
-      HIPCHK(hipMemcpyAsync(d_offsets + n, &d_status->total_bytes, 8, hipMemcpyDeviceToDevice, s));
-      f = static_cast<hipFunction_t>(SM->f_enc_pre);
-    }
-    HIPCHK(hipModuleLaunchKernel(f, nb32, 1, 1, 64, 1, 1, lds_s, s, args, nullptr));
+    HIPCHK(hipMemsetAsync(desc, 0, align_up(nb * 8, 16), s));
+    HIPCHK(hipModuleLaunchKernel(static_cast<hipFunction_t>(SM->f_enc_lb), nb32, 1, 1, 64, 1, 1, lds_s, s, args,
+                                 nullptr));
     return XDRG_OK;
   }
   deep_passes dp;  // element subroutines nested past XDRG_SUB_FRAMES
@@ -1833,6 +1832,17 @@ int var_encode(const xdrg_plan &P, const dev_tables &T, const void *d_native, ui
       HIPCHK(go(kDeepLanesA / 256, 256, ep.A));
       HIPCHK(go(1, kDeepLanesB, ep.B));
     }
+    return XDRG_OK;
+  }
+  if (pre) {  // the walk-first record kernel over the scan's wave bases
+    const unsigned long long *bb = bbase;
+    unsigned long long *nodesc = nullptr;
+    uint64_t *nototal = nullptr;
+    uint32_t nb32 = static_cast<uint32_t>(nb), sl = stack_limit, cc = Cs, mk = mark;
+    void *args[] = {&nat8, &n, const_cast<uint32_t *>(&p->stride), &d_heap, &heap_len, &xdr8, &cap,
+                    &d_offsets, &bb, &nodesc, &nb32, &nototal, &sl, &cc, &mk, &err};
+    HIPCHK(hipModuleLaunchKernel(static_cast<hipFunction_t>(SM->f_enc_pre), nb32, 1, 1, 64, 1, 1, lds_s, s, args,
+                                 nullptr));
     return XDRG_OK;
   }
   if (SM) {
@@ -1999,7 +2009,9 @@ int var_decode(const xdrg_plan &P, const dev_tables &T, const void *d_xdr, uint6
       return frame_launch(k_sub_decode, mf, grid, block, lds, s, xdr8, len, d_offsets, n, nat8, p->stride, T.d_ops,
                           nops, T.d_table, stack_limit, d_heap_out, ebase, p->heap_factor, mark, err, P);
     };
-    HIPCHK(go(static_cast<uint32_t>((n + 255) / 256), 256, dp.main));
+    sub_pass mp = dp.main;
+    mp.packed = p->packed ? 1u : 0u;  // non-recursive plans: packed element areas (never deferred)
+    HIPCHK(go(static_cast<uint32_t>((n + 255) / 256), 256, mp));
     if (dp.on) {
       HIPCHK(go(kDeepLanesA / 256, 256, dp.A));
       HIPCHK(go(1, kDeepLanesB, dp.B));
@@ -2319,8 +2331,8 @@ int xdrg_plan_set_option(xdrg_plan *p, int option, int64_t value) {
     if (v > (32 << 10)) return XDRG_EINVAL;
     O.stage_bytes = v < 0 ? -1 : v; return XDRG_OK;
   case XDRG_OPT_ENC_STREAM:
-    if (v < 0 || v > 1) return XDRG_EINVAL;
-    O.enc_stream = v; return XDRG_OK;
+    if (v < -1 || v > 1) return XDRG_EINVAL;
+    O.enc_stream = static_cast<int>(v); return XDRG_OK;
   default: return XDRG_EINVAL;
   }
 }
