@@ -83,6 +83,9 @@ def parse():
                     choices=["rec128", "numerics", "recvar", "rpc", "vecrec", "containertest", "rp_list"],
                     help="rec128 is the headline; numerics/recvar/rpc measure BASELINE.json "
                          "configs 1, 3, 4; vecrec covers xvector<T>/pointer<T>")
+    ap.add_argument("--plan-opt", action="append", default=[], metavar="NAME=V",
+                    help="a plan option (xdrpp_amd._abi.PLAN_OPTIONS) for A/B runs, e.g. enc_stream=0; "
+                         "echoed in config.plan_options")
     return ap.parse_args()
 
 
@@ -649,9 +652,9 @@ def rpc_leg(dev, n=1 << 20, reps=20):
     return res
 
 
-def setup(schema, n, dev, rank, world):
+def setup(schema, n, dev, rank, world, opts=None):
     """Plan, resident inputs and preallocated outputs for one rank."""
-    plan = M.Plan(S.ALL[schema])
+    plan = M.Plan(S.ALL[schema], opts or None)
     mar = M.Marshaler(plan, dev)
     nat_np, heap_np = SH.shard_inputs(schema, n, rank, world)
     nat = torch.from_numpy(nat_np).to(dev)
@@ -665,6 +668,28 @@ def setup(schema, n, dev, rank, world):
     offsets = torch.empty(n + 1, dtype=torch.int64, device=dev)
     heap_out = torch.empty(plan.decode_heap_bytes(total), dtype=torch.uint8, device=dev)
     return plan, mar, nat, heap, xdr, back, offsets, heap_out
+
+
+def plan_opts(args) -> dict:
+    """--plan-opt NAME=V pairs as a plan options dict."""
+    out = {}
+    for kv in getattr(args, "plan_opt", []) or []:
+        k, v = kv.split("=", 1)
+        out[k] = int(v)
+    return out
+
+
+def walk_first(plan) -> bool:
+    """Word-list plans encode with the walk-first record kernel
+    (xdrg_spec_encode_pre, XDRG_OPT_ENC_STREAM default): its generated source
+    defines it."""
+    L = A.lib()
+    n = A.C.c_size_t(0)
+    if L.xdrg_plan_kernel_source(plan.handle, None, 0, A.C.byref(n)) != A.OK:
+        return False
+    buf = A.C.create_string_buffer(n.value + 1)
+    A.check(L.xdrg_plan_kernel_source(plan.handle, buf, n.value + 1, A.C.byref(n)), "xdrg_plan_kernel_source")
+    return b"xdrg_spec_encode_pre" in buf.value
 
 
 class GpuEngine:
@@ -681,7 +706,8 @@ class GpuEngine:
         self.dev = torch.device("cuda", local)
         self.schema, self.n = args.schema, n
         (self.plan, self.mar, self.nat, self.heap, self.xdr, self.back, self.offsets,
-         self.heap_out) = setup(args.schema, n, self.dev, rank, world)
+         self.heap_out) = setup(args.schema, n, self.dev, rank, world, plan_opts(args))
+        self.enc_stream = plan_opts(args).get("enc_stream", -1)
         self.stream = torch.cuda.current_stream()
         self.s = self.stream.cuda_stream
         self.mar.status.init(self.s)
@@ -758,7 +784,9 @@ class GpuEngine:
         else:
             size_k = ("k_sub_size" if sub and not spec else "k_size_linear" if plan_linear(plan)
                       else "xdrg_spec_size" if spec else "k_var_size")
-            enc_k = "xdrg_spec_encode" if spec else "k_sub_encode" if sub else "k_var_encode_i"
+            enc_k = (("xdrg_spec_encode_pre" if walk_first(plan) and self.enc_stream != 0 else "xdrg_spec_encode")
+                     if spec
+                     else "k_sub_encode" if sub else "k_var_encode_i")
             dec_k = "xdrg_spec_decode_copy" if spec else "k_sub_decode" if sub else "k_var_decode_w"
         if np.mean(enc_ms) >= np.mean(dec_ms):
             return f"{size_k}+k_scan_blocks+{enc_k}", enc_alg, enc_ms
@@ -908,7 +936,8 @@ def report(args, engine, world, rows, X, kern, alg_bytes, launches, enc_ms, dec_
         "config": {"workload": f"{wl}, {n} records per GPU x {world} GPU(s), encode (xdr_to_opaque) + "
                                "decode (xdr_from_opaque), device-resident",
                    "schema": args.schema, "records_per_gpu": n, "records_total": n * world,
-                   "xdr_bytes_per_gpu": X, "native_stride": S_, "parallelism": f"dp{world}"},
+                   "xdr_bytes_per_gpu": X, "native_stride": S_, "parallelism": f"dp{world}",
+                   **({"plan_options": plan_opts(args)} if plan_opts(args) else {})},
         "encode_ms": round(float(np.mean(enc_ms)), 4),
         "decode_ms": round(float(np.mean(dec_ms)), 4),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,

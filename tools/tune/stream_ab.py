@@ -21,6 +21,8 @@ from xdrpp_amd import _abi as A, marshal as M, schemas as S, workloads as W  # n
 VAR_OPTS = {
     "two_pass": {"enc_stream": 0}, "walk_first": {"enc_stream": -1}, "lb": {"enc_stream": 1},
     "sized": {"enc_stream": -1}, "halves": {"enc_stream": -1}, "halves0": {"enc_stream": 0},
+    "wf2k": {"image_bytes": 2048}, "wf3k": {"image_bytes": 3072}, "wf6k": {"image_bytes": 6144},
+    "wf8k": {"image_bytes": 8192},
 }
 VARIANTS = os.environ.get("VARIANTS", "two_pass walk_first lb sized").split()
 REPS = int(os.environ.get("REPS", "20"))
