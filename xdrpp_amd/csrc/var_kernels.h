@@ -460,7 +460,11 @@ __device__ __forceinline__ void var_encode_body(
     uint32_t mark, unsigned long long *err, unsigned long long *lbd = nullptr, uint32_t nb = 0,
     uint64_t *total = nullptr) {
   extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
-  const enc_lds L = enc_layout(stride, KMAX, C);
+  constexpr int WL = (W::kWords > 0 && NW > 0) ? static_cast<int>(W::kWords) + 1 : 0;  // + the mark
+  // PRE: no native tile -- the lane loads its record straight into
+  // registers, and the tile's room holds only the word list (rpc: 2.8 of
+  // 5 KiB; more waves per CU)
+  const enc_lds L = enc_layout(PRE != 0 ? 4u * WL : stride, KMAX, C);
   uint8_t *tile = sm + L.tile;
   echunk_desc *desc = reinterpret_cast<echunk_desc *>(sm + L.desc);
   uint32_t *cum = reinterpret_cast<uint32_t *>(sm + L.cum);
@@ -470,7 +474,6 @@ __device__ __forceinline__ void var_encode_body(
   const uint64_t r = wr0 + lane;
   const uint32_t nrec = static_cast<uint32_t>(min<uint64_t>(64, n - wr0));
   XDRG_STAMP(0);
-  constexpr int WL = (W::kWords > 0 && NW > 0) ? static_cast<int>(W::kWords) + 1 : 0;  // + the mark
   static_assert(PRE == 0 || (WL > 0 && W::kFastWalk), "the pre-walk runs on word-list plans");
 
   uint32_t sz, v, T;
@@ -494,14 +497,29 @@ __device__ __forceinline__ void var_encode_body(
     // ---- the walk first: the record's words into the list (tile), its
     // payloads into slots, its byte count
     if constexpr (PRE == 2) wave_out = block_base[blockIdx.x];
-    stage_tile<8>(tile, native + wr0 * stride, nrec * stride, lane, 64u);
-    wave_sync();
-    {
-      const uint32_t *t32 = reinterpret_cast<const uint32_t *>(tile + lane * stride);
+    {  // the record (16- or 8-byte loads: the host passes 16-aligned natives)
+      const uint8_t *src = native + r * static_cast<uint64_t>(4 * NW);
 #pragma unroll
-      for (int k = 0; k < NW; ++k) rec[k] = lane < nrec ? t32[k] : 0u;
+      for (int k = 0; k < NW; ++k) rec[k] = 0u;
+      if (lane < nrec) {
+        if constexpr (NW % 4 == 0) {
+#pragma unroll
+          for (int k = 0; k < NW; k += 4) {
+            const u32x4 q = *reinterpret_cast<const u32x4 *>(src + 4 * k);
+            rec[k] = q.x; rec[k + 1] = q.y; rec[k + 2] = q.z; rec[k + 3] = q.w;
+          }
+        } else if constexpr (NW % 2 == 0) {
+#pragma unroll
+          for (int k = 0; k < NW; k += 2) {
+            const uint2 q = *reinterpret_cast<const uint2 *>(src + 4 * k);
+            rec[k] = q.x; rec[k + 1] = q.y;
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < NW; ++k) rec[k] = ld32(src + 4 * k);
+        }
+      }
     }
-    wave_sync();  // every tile read before the list overwrites it
     enc_ctx<KMAX, false, WL> f = c.template as<false>();
     f.at = 0;
     f.pos = 0;

@@ -1788,6 +1788,8 @@ int var_encode(const xdrg_plan &P, const dev_tables &T, const void *d_native, ui
   // (profiles/r04t).
   const bool pre = SM && SM->f_enc_pre && O.enc_stream != 0 && p->max_depth <= stack_limit &&
                    64ull * max_rec < (1ull << 31) && 256u * p->spec.info.list_words <= Cs;
+  // its LDS: the word list in place of the native tile (var_encode_body PRE)
+  const uint32_t lds_pre = pre ? enc_layout(4u * p->spec.info.list_words, p->spec.info.slots, Cs).total : 0u;
   if (pre && O.enc_stream == 1 && phase == kEncBoth) {
     uint64_t *total = &d_status->total_bytes;
     unsigned long long *desc = bsum;  // the nb wave totals (look-back descriptors)
@@ -1796,7 +1798,7 @@ int var_encode(const xdrg_plan &P, const dev_tables &T, const void *d_native, ui
     void *args[] = {&nat8, &n, const_cast<uint32_t *>(&p->stride), &d_heap, &heap_len, &xdr8, &cap,
                     &d_offsets, &bb, &desc, &nb32, &total, &sl, &cc, &mk, &err};
     HIPCHK(hipMemsetAsync(desc, 0, align_up(nb * 8, 16), s));
-    HIPCHK(hipModuleLaunchKernel(static_cast<hipFunction_t>(SM->f_enc_lb), nb32, 1, 1, 64, 1, 1, lds_s, s, args,
+    HIPCHK(hipModuleLaunchKernel(static_cast<hipFunction_t>(SM->f_enc_lb), nb32, 1, 1, 64, 1, 1, lds_pre, s, args,
                                  nullptr));
     return XDRG_OK;
   }
@@ -1841,7 +1843,7 @@ int var_encode(const xdrg_plan &P, const dev_tables &T, const void *d_native, ui
     uint32_t nb32 = static_cast<uint32_t>(nb), sl = stack_limit, cc = Cs, mk = mark;
     void *args[] = {&nat8, &n, const_cast<uint32_t *>(&p->stride), &d_heap, &heap_len, &xdr8, &cap,
                     &d_offsets, &bb, &nodesc, &nb32, &nototal, &sl, &cc, &mk, &err};
-    HIPCHK(hipModuleLaunchKernel(static_cast<hipFunction_t>(SM->f_enc_pre), nb32, 1, 1, 64, 1, 1, lds_s, s, args,
+    HIPCHK(hipModuleLaunchKernel(static_cast<hipFunction_t>(SM->f_enc_pre), nb32, 1, 1, 64, 1, 1, lds_pre, s, args,
                                  nullptr));
     return XDRG_OK;
   }
