@@ -2,7 +2,7 @@
 # kernel stats + FETCH_SIZE / WRITE_SIZE passes (separate runs)
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
-O=gpurun_out/r04z
+O=gpurun_out/${TAG:-r04z}
 mkdir -p $O
 export VARIANTS="two_pass walk_first" REPS=10
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/stats -o k --output-format csv -- python3 tools/tune/stream_ab.py recvar rpc > $O/stats.log 2>&1 || exit 1

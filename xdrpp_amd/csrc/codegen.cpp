@@ -1158,7 +1158,7 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
   // look-back (no size pass, no scan), or from xdrg_encode_sizes' scan
   if (kwords > 0)
     for (int lb = 0; lb < 2; ++lb)
-      s << "extern \"C\" __global__ __launch_bounds__(64) void xdrg_spec_encode_" << (lb ? "lb" : "pre") << "(\n"
+      s << "extern \"C\" __global__ __launch_bounds__(64, XDRG_PRE_WAVES) void xdrg_spec_encode_" << (lb ? "lb" : "pre") << "(\n"
         << "    const uint8_t *native, uint64_t n, uint32_t stride, const uint8_t *heap, uint64_t heap_len,\n"
         << "    uint8_t *xdr, uint64_t cap, uint64_t *offsets, const unsigned long long *block_base,\n"
         << "    unsigned long long *desc, uint32_t nb, uint64_t *total, uint32_t stack_limit, uint32_t C,\n"

@@ -50,6 +50,14 @@
 #ifndef XDRG_ENC_NT
 #define XDRG_ENC_NT 2
 #endif
+// Waves per SIMD the walk-first record kernels are compiled for
+// (__launch_bounds__'s second argument; tools/tune/stream_stamps.py
+// CFLAGS=-DXDRG_PRE_WAVES=n, profiles/r04ad): 5 caps them at 96 VGPRs --
+// recvar even (0.080 vs 0.081 ms), rpc spills (0.141 vs 0.117); 6: 0.12 /
+// 0.20 ms.  4 is what they need anyway (102-105 VGPRs).
+#ifndef XDRG_PRE_WAVES
+#define XDRG_PRE_WAVES 4
+#endif
 // Non-temporal stores of the decode's heap copy (A/B, profiles/r02s/
 // nt_hints/dnt*.log: recvar 0.089 -> 0.084 ms, vecrec 0.153 -> 0.137, rpc
 // 0.120 -> 0.121).
