@@ -1643,8 +1643,8 @@ hipError_t launch_sub_size(const xdrg_plan &p, const dev_tables &T, const uint8_
   const spec_module *FM = frame_spec(p);
   void *mf = FM ? (DEPTH ? FM->f_sub_depth : FM->f_sub_size) : nullptr;
   auto go = [&](uint32_t grid, uint32_t block, const sub_pass &P) {
-    return frame_launch(k_sub_size<DEPTH>, mf, grid, block, lds, s, nat, n, p.stride, heap, heap_len, T.d_ops, nops,
-                        T.d_table, sizes, bsum, mark, err, depths, P);
+    return frame_launch(k_sub_size<DEPTH>, mf, grid, block, lds, s, nat, n, p.stride, heap, heap_len,
+                        T.d_ops, nops, T.d_table, sizes, bsum, mark, err, depths, P);
   };
   hipError_t e = go(static_cast<uint32_t>((n + 255) / 256), 256, dp.main);
   if (e == hipSuccess && dp.on) {
@@ -1825,9 +1825,11 @@ int var_encode(const xdrg_plan &P, const dev_tables &T, const void *d_native, ui
     const deep_passes ep = encode_passes(dp);
     const spec_module *FM = frame_spec(*p);
     void *mf = FM ? FM->f_sub_enc : nullptr;
-    auto go = [&](uint32_t grid, uint32_t block, const sub_pass &P) {
-      return frame_launch(k_sub_encode, mf, grid, block, lds_ops, s, nat8, n, p->stride, d_heap, heap_len, xdr8, cap,
-                          d_offsets, sizes, bbase, T.d_ops, nops, T.d_table, stack_limit, mark, err, P);
+    auto go = [&](uint32_t grid, uint32_t block, const sub_pass &P) {  // + each lane's line buffer
+      return frame_launch(k_sub_encode, mf, grid, block, lds_ops + 64u * block, s, nat8, n,
+                          p->stride, d_heap,
+                          heap_len, xdr8, cap, d_offsets, sizes, bbase, T.d_ops, nops, T.d_table, stack_limit, mark,
+                          err, P);
     };
     HIPCHK(go(static_cast<uint32_t>((n + 255) / 256), 256, ep.main));
     if (ep.on) {
