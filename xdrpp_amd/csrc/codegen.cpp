@@ -303,11 +303,25 @@ struct gen {
   // to 8 (oracle/xdr_oracle.c rec_ebytes, var_kernels.h packed_area) -- a
   // walk of its lengths, counts and discriminants that stops (returns E)
   // where the structure stops parsing.  Element subroutines (non-recursive:
-  // packed plans are never deep) are walked inline per element.
-  void eb_block(uint32_t pc, uint32_t stop) {
+  // packed plans are never deep) are walked inline per element.  At the
+  // record's level (top) the walk stops as soon as no container can follow
+  // (jumps go forward only, so none at a later pc means none reachable): E
+  // is final there, and containertest's shares skip its element bodies and
+  // strings altogether.
+  bool region_has_vector(uint32_t start) const {
+    for (uint32_t i = start; i < nops() && op(i).kind != XDRG_OP_END; ++i)
+      if (op(i).kind == XDRG_OP_VECTOR) return true;
+    return false;
+  }
+  bool vector_from(uint32_t pc) const { return region_has_vector(pc); }  // the record region: [pc, its END)
+  void eb_block(uint32_t pc, uint32_t stop, bool top = false) {
     auto need = [&](const std::string &n) { line("if (b - q < " + n + ") return E;"); };
     auto word = [&]() { need("4"); line("{ const uint32_t v = bswap32(rd(q)); q += 4;"); };
     while (pc != stop) {
+      if (top && !vector_from(pc)) {
+        line("return E;");
+        return;
+      }
       const xdrg_op &e = op(pc);
       switch (e.kind) {
       case XDRG_OP_END: return;
@@ -330,6 +344,10 @@ struct gen {
           // element's own arrays (the body inline)
           line("  if (left < static_cast<uint64_t>(v) * " + u32(e.arg3) + ") return E;");
           line("  E += (static_cast<uint64_t>(v) * " + u32(e.arg1) + " + 7u) & ~7ull;");
+          if (top && !region_has_vector(e.arg4) && !vector_from(pc + 1)) {  // nothing after adds to E
+            line("  return E; }");
+            return;
+          }
           line("  for (uint32_t i = 0; i < v; ++i) {");
           ind += 4;
           eb_block(e.arg4, body_end(e.arg4));
@@ -352,13 +370,13 @@ struct gen {
           for (uint32_t v : a.second) lab += "case " + u32(v) + ": ";
           line("  " + lab + "{");
           ind += 2;
-          eb_block(a.first, end);
+          eb_block(a.first, end, top);
           ind -= 2;
           line("  } break;");
         }
         line("  default: {");
         ind += 2;
-        if (e.flags & XDRG_F_DEFAULT) eb_block(e.arg4, end);
+        if (e.flags & XDRG_F_DEFAULT) eb_block(e.arg4, end, top);
         else line("return E;");
         ind -= 2;
         line("  } break;");
@@ -765,7 +783,8 @@ struct gen {
           line("*reinterpret_cast<uint64_t *>(" + f + ") = c.ecur;");
           line("st32(" + f + " + 8, cnt" + ks + ");");
           line("uint8_t *arr" + ks + " = c.heap + c.ecur;");
-          line("for (uint64_t z = 0; z < static_cast<uint64_t>(cnt" + ks + ") * " + u32(e.arg1) +
+          line("if (!c.zeroed)");
+          line("  for (uint64_t z = 0; z < static_cast<uint64_t>(cnt" + ks + ") * " + u32(e.arg1) +
                "; z += 4) st32(arr" + ks + " + z, 0u);");
           line("c.ecur += static_cast<uint64_t>(cnt" + ks + ") * " + u32(e.arg1) + ";");
           line("for (uint32_t i" + ks + " = 0; i" + ks + " < cnt" + ks + "; ++i" + ks + ") {");
@@ -907,10 +926,12 @@ struct gen {
     if (dec_elem_regs(vpc, b0, b1, es, base, dadd)) return;
     const std::string fail_done = "st32(" + base + " + " + u32(op(vpc).noff) + " + 12, i); ";
     const bool w4 = (es & 3u) == 0;  // 4-byte stores (element arrays are 8-aligned)
+    line("if (!c.zeroed) {");  // (the group's LDS stage is zeroed whole)
     if (w4)
-      for (uint32_t z = 0; z < es; z += 4) line("st32(el + " + u32(z) + ", 0u);");
+      for (uint32_t z = 0; z < es; z += 4) line("  st32(el + " + u32(z) + ", 0u);");
     else
-      line("for (uint32_t z = 0; z < " + u32(es) + "; ++z) el[z] = 0;");
+      line("  for (uint32_t z = 0; z < " + u32(es) + "; ++z) el[z] = 0;");
+    line("}");
     for (uint32_t k = b0; k < b1; ++k) {
       const xdrg_op &e = op(k);
       const std::string P = u32(k), D = depth(e, dadd), f = "el + " + u32(e.noff);
@@ -1076,7 +1097,7 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
   // element-area shares of packed plans
   g.o.str("");
   g.ind = 4;
-  if (p.packed) g.eb_block(0, kNoPc);
+  if (p.packed) g.eb_block(0, kNoPc, true);
   const std::string eb_code = g.o.str();
 
   const uint32_t maxd = g.maxd;  // deepest field: the stack budget a wave must have to skip the checks

@@ -951,6 +951,7 @@ struct dec_ctx {
   unsigned long long *err;
   uint8_t *heap;  // decoded heap (element arrays live at [ecur, eend))
   uint64_t ecur, eend;
+  bool zeroed = false;  // the arrays' bytes are zero already (the group's LDS stage)
 
   // stack budget, then check(n) of xdr_generic_get (marshal.h:166-170)
   __device__ __forceinline__ bool field(uint32_t op, uint32_t depth, uint64_t need) {
@@ -1113,6 +1114,7 @@ __device__ __forceinline__ void var_decode_body(
     }
     if (staged) {  // the same walk, its arrays into the stage
       c.heap = stage - ga;
+      c.zeroed = true;
       ok = w.dec(c, nat, ok);
     } else {
       ok = w.dec(c, nat, ok);
