@@ -469,10 +469,12 @@ __device__ __forceinline__ void var_encode_body(
     uint64_t *total = nullptr) {
   extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
   constexpr int WL = (W::kWords > 0 && NW > 0) ? static_cast<int>(W::kWords) + 1 : 0;  // + the mark
-  // PRE: no native tile -- the lane loads its record straight into
-  // registers, and the tile's room holds only the word list (rpc: 2.8 of
-  // 5 KiB; more waves per CU)
-  const enc_lds L = enc_layout(PRE != 0 ? 4u * WL : stride, KMAX, C);
+  // PRE, and register walks without a word list: no native tile -- the
+  // lane loads its record straight into registers, and the tile's room
+  // holds only the word list (rpc: 2.8 of 5 KiB), or nothing (vecrec,
+  // containertest): more waves per CU
+  constexpr bool RREG = NW > 0 && (PRE != 0 || WL == 0);
+  const enc_lds L = enc_layout(PRE != 0 ? 4u * WL : RREG ? 0u : stride, KMAX, C);
   uint8_t *tile = sm + L.tile;
   echunk_desc *desc = reinterpret_cast<echunk_desc *>(sm + L.desc);
   uint32_t *cum = reinterpret_cast<uint32_t *>(sm + L.cum);
@@ -501,33 +503,35 @@ __device__ __forceinline__ void var_encode_body(
 #pragma unroll
   for (int k = 0; k < KMAX; ++k) { c.psr[k] = 0; c.pds[k] = 0; c.pln[k] = 0; c.rb[k] = 0; }
   uint32_t rec[NW > 0 ? NW : 1];
+  // the record (16- or 8-byte loads: the host passes 16-aligned natives)
+  auto load_rec = [&]() {
+    const uint8_t *src = native + r * static_cast<uint64_t>(4 * (NW > 0 ? NW : 1));
+#pragma unroll
+    for (int k = 0; k < (NW > 0 ? NW : 1); ++k) rec[k] = 0u;
+    if (lane < nrec) {
+      if constexpr (NW % 4 == 0) {
+#pragma unroll
+        for (int k = 0; k < NW; k += 4) {
+          const u32x4 q = *reinterpret_cast<const u32x4 *>(src + 4 * k);
+          rec[k] = q.x; rec[k + 1] = q.y; rec[k + 2] = q.z; rec[k + 3] = q.w;
+        }
+      } else if constexpr (NW % 2 == 0) {
+#pragma unroll
+        for (int k = 0; k < NW; k += 2) {
+          const uint2 q = *reinterpret_cast<const uint2 *>(src + 4 * k);
+          rec[k] = q.x; rec[k + 1] = q.y;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < NW; ++k) rec[k] = ld32(src + 4 * k);
+      }
+    }
+  };
   if constexpr (PRE != 0) {
     // ---- the walk first: the record's words into the list (tile), its
     // payloads into slots, its byte count
     if constexpr (PRE == 2) wave_out = block_base[blockIdx.x];
-    {  // the record (16- or 8-byte loads: the host passes 16-aligned natives)
-      const uint8_t *src = native + r * static_cast<uint64_t>(4 * NW);
-#pragma unroll
-      for (int k = 0; k < NW; ++k) rec[k] = 0u;
-      if (lane < nrec) {
-        if constexpr (NW % 4 == 0) {
-#pragma unroll
-          for (int k = 0; k < NW; k += 4) {
-            const u32x4 q = *reinterpret_cast<const u32x4 *>(src + 4 * k);
-            rec[k] = q.x; rec[k + 1] = q.y; rec[k + 2] = q.z; rec[k + 3] = q.w;
-          }
-        } else if constexpr (NW % 2 == 0) {
-#pragma unroll
-          for (int k = 0; k < NW; k += 2) {
-            const uint2 q = *reinterpret_cast<const uint2 *>(src + 4 * k);
-            rec[k] = q.x; rec[k + 1] = q.y;
-          }
-        } else {
-#pragma unroll
-          for (int k = 0; k < NW; ++k) rec[k] = ld32(src + 4 * k);
-        }
-      }
-    }
+    load_rec();
     enc_ctx<KMAX, false, WL> f = c.template as<false>();
     f.at = 0;
     f.pos = 0;
@@ -603,7 +607,8 @@ __device__ __forceinline__ void var_encode_body(
   // (sizes, block base and the native tile are loaded in one round trip)
   sz = r < n ? sizes[r] : kSizeErr;
   wave_out = block_base[blockIdx.x];
-  stage_tile<8>(tile, native + wr0 * stride, nrec * stride, lane, 64u);
+  if constexpr (RREG) load_rec();
+  else stage_tile<8>(tile, native + wr0 * stride, nrec * stride, lane, 64u);
   szok = !(sz & kSizeErr);
   v = szok ? sz : 0u;
   if constexpr (W::kDirect) {
@@ -622,7 +627,8 @@ __device__ __forceinline__ void var_encode_body(
         if (!d.field(kOpRecordLevel, 0, 4)) return;
         d.put(mark_word(sz - 4u));
       }
-      (void)w.enc(d, tile + lane * stride, true);
+      if constexpr (RREG) (void)w.enc(d, reinterpret_cast<const uint8_t *>(rec), true);
+      else (void)w.enc(d, tile + lane * stride, true);
       return;
     }
   }
@@ -753,7 +759,7 @@ __device__ __forceinline__ void var_encode_body(
       c.at = a0;
       c.pos = off;
       bool okr = szok;
-      if constexpr (NW > 0) {
+      if constexpr (NW > 0 && !RREG) {
         const uint32_t *t32 = reinterpret_cast<const uint32_t *>(tile + lane * stride);
 #pragma unroll
         for (int k = 0; k < NW; ++k) rec[k] = t32[k];

@@ -1770,7 +1770,10 @@ int var_encode(const xdrg_plan &P, const dev_tables &T, const void *d_native, ui
     Cs = p->spec.info.word_list && O.image_bytes <= 0
              ? static_cast<uint32_t>(std::min<uint64_t>(4u << 10, (64ull * std::max<uint64_t>(max_rec, 16) + 31u) & ~15ull))
              : window();
-    lds_s = enc_layout(p->stride, p->spec.info.slots, Cs).total;
+    // register walks without a word list load the record straight into
+    // registers: no native tile (var_encode_body RREG)
+    const bool rreg = p->spec.info.dec_regs && !p->spec.info.word_list;
+    lds_s = enc_layout(rreg ? 0u : p->stride, p->spec.info.slots, Cs).total;
     // (a wave whose stretch could pass 2 GiB writes its records directly,
     // var_encode_body's direct mode)
     if (lds_s > kVarLdsBudget || !aligned(d_native, 16)) SM = nullptr;
