@@ -394,6 +394,21 @@ struct gen {
   // branch) and the test of that word: what the index loads for every
   // candidate start before parsing it (run_index in xdrgpu.hip finds the
   // same op).
+  // Least bytes the record needs after that word given its value v: a
+  // container's count times the least an element takes, a payload's length.
+  std::string first_len() {
+    for (uint32_t pc = 0; pc < nops(); ++pc) {
+      const xdrg_op &o = op(pc);
+      if (o.kind == XDRG_OP_END || o.kind == XDRG_OP_JUMP) break;
+      if (o.kind == XDRG_OP_U64 || o.kind == XDRG_OP_OPAQUE || o.kind == XDRG_OP_U32 || o.kind == XDRG_OP_BOOL ||
+          (o.kind == XDRG_OP_ENUM && !(o.flags & XDRG_F_VALIDATE)))
+        continue;
+      if (o.kind == XDRG_OP_VECTOR) return "static_cast<uint64_t>(v) * " + u32(o.arg3);
+      if (o.kind == XDRG_OP_VAROPAQUE || o.kind == XDRG_OP_STRING) return "static_cast<uint64_t>(v)";
+      return "0";
+    }
+    return "0";
+  }
   std::string first_test() {
     for (uint32_t pc = 0; pc < nops(); ++pc) {
       const xdrg_op &o = op(pc);
@@ -1093,7 +1108,7 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
   g.ind = 2;
   g.rx_block(0, kNoPc);
   const std::string rx_code = g.o.str();
-  const std::string first = g.first_test();
+  const std::string first = g.first_test(), flen = g.first_len();
   // element-area shares of packed plans
   g.o.str("");
   g.ind = 4;
@@ -1141,6 +1156,7 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
     << "struct plan_rx {  // index_kernels.h ix_seg_body's and rxs_walk_body's parser\n"
     << "  __device__ __forceinline__ void init(uint32_t *) const {}\n"
     << "  __device__ __forceinline__ bool first_ok(const uint32_t *, uint32_t v) const { return " << first << "; }\n"
+    << "  __device__ __forceinline__ uint64_t first_len(uint32_t v) const { return " << flen << "; }\n"
     << "  __device__ __forceinline__ uint32_t rlen(const uint32_t *m, const uint8_t *__restrict__ s, uint64_t len,\n"
     << "                                           uint64_t a, uint32_t maxlen) const {\n"
     << "    return rlen_rd<rx_global, uint64_t>(m, rx_global{s}, len, a, maxlen);\n  }\n"

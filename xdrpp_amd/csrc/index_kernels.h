@@ -322,6 +322,9 @@ struct mark_rx {
     const uint32_t size = v & ~XDRG_MARK_LAST;
     return !((v >> 24) & 3u) && (v & XDRG_MARK_LAST) && size <= maxlen && !(size & 3u);
   }
+  // least bytes the record needs after its first checked word (the speculative
+  // walk's second filter; first_ok already holds the size to maxlen)
+  __device__ __forceinline__ uint64_t first_len(uint32_t) const { return 0; }
   template <class RD, class U>
   __device__ __forceinline__ uint32_t rlen_rd(const uint32_t *, const RD &rd, U len, U a, uint32_t) const {
     if (len - a < 4) return RX_BAD;
@@ -411,9 +414,16 @@ __device__ __forceinline__ void rxs_walk_body(const P &parser, const uint8_t *__
 #pragma unroll
       for (uint32_t k = 0; k < kRxsSub / 4; ++k) fw[k] = stg[i0 + k];
       uint64_t m = 0;
+      // a candidate must also fit its first field's least bytes in maxlen: a
+      // record that cannot breaks the chain anyway (the walk then falls back
+      // to the list ranking, which tells INDEX_LONG apart); containertest's
+      // unbounded uvec<> and strings otherwise let every word through
+      const uint64_t room = maxlen > fd + 4u ? maxlen - fd - 4u : 0u;
 #pragma unroll
-      for (uint32_t k = 0; k < kRxsSub / 4; ++k)
-        m |= static_cast<uint64_t>(parser.first_ok(rx_smem, bswap32(fw[k]))) << k;
+      for (uint32_t k = 0; k < kRxsSub / 4; ++k) {
+        const uint32_t v = bswap32(fw[k]);
+        m |= static_cast<uint64_t>(parser.first_ok(rx_smem, v) && parser.first_len(v) <= room) << k;
+      }
       // words whose first checked word is past the staged stretch stay candidates
       const uint32_t ns = a + fd < nb ? (nb - a - fd) / 4 : 0u;
       if (ns < 64) m |= ~0ull << ns;
