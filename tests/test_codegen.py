@@ -50,6 +50,17 @@ def test_source_is_straight_line(name):
         assert "i + 4u <= cnt" in src and "i + 2u <= cnt" in src
 
 
+def test_index_candidate_filters():
+    """The speculative record index's candidate tests (index_kernels.h
+    rxs_walk_body): containertest opens with uvec<u_4_12> (unbounded), so
+    its first word alone passes almost anything; the first element's
+    discriminant (the next word) must be 4 or 12 when the count is nonzero."""
+    src = source(M.Plan(S.ALL["containertest"]))
+    assert "return (v == 0u || (w == 4u || w == 12u));" in src
+    # a record whose first field is not such a container has no second test
+    assert "bool second_ok(uint32_t v, uint32_t w) const { return true; }" in source(M.Plan(S.ALL["rpc"]))
+
+
 def test_fixed_plans_have_no_specialized_source():
     assert source(M.Plan(S.rec128)) == -3  # XDRG_EUNSUPPORTED
 

@@ -409,23 +409,43 @@ struct gen {
     }
     return "0";
   }
-  std::string first_test() {
+  std::string first_test(uint32_t pc0 = 0, const std::string &x = "v") {
+    for (uint32_t pc = pc0; pc < nops(); ++pc) {
+      const xdrg_op &o = op(pc);
+      if (o.kind == XDRG_OP_END || o.kind == XDRG_OP_JUMP) break;
+      if (o.kind == XDRG_OP_U64 || o.kind == XDRG_OP_OPAQUE || o.kind == XDRG_OP_U32 || o.kind == XDRG_OP_BOOL ||
+          (o.kind == XDRG_OP_ENUM && !(o.flags & XDRG_F_VALIDATE)))
+        continue;
+      if (o.kind == XDRG_OP_ENUM) return enum_test(x, o.arg0, o.arg1);
+      if (o.kind == XDRG_OP_UNION) {
+        if (o.flags & XDRG_F_DEFAULT) return (o.flags & XDRG_F_VALIDATE) ? enum_test(x, o.arg0, o.arg1) : "true";
+        std::string t;
+        for (auto &a : arms(o))
+          for (uint32_t v : a.second) t += (t.empty() ? "" : " || ") + x + " == " + u32(v);
+        if (t.empty()) t = "false";
+        return (o.flags & XDRG_F_VALIDATE) ? "(" + enum_test(x, o.arg0, o.arg1) + " && (" + t + "))" : "(" + t + ")";
+      }
+      return x + " <= " + u32(o.arg0);  // VAROPAQUE, STRING, VECTOR
+    }
+    return "true";
+  }
+  // The word after the first checked one, w, given that one's value v: when
+  // the record starts with a container of element-subroutine elements whose
+  // body opens with a checked field, a nonempty count's next word is that
+  // field of the first element (containertest: the union's discriminant).
+  std::string second_test() {
     for (uint32_t pc = 0; pc < nops(); ++pc) {
       const xdrg_op &o = op(pc);
       if (o.kind == XDRG_OP_END || o.kind == XDRG_OP_JUMP) break;
       if (o.kind == XDRG_OP_U64 || o.kind == XDRG_OP_OPAQUE || o.kind == XDRG_OP_U32 || o.kind == XDRG_OP_BOOL ||
           (o.kind == XDRG_OP_ENUM && !(o.flags & XDRG_F_VALIDATE)))
         continue;
-      if (o.kind == XDRG_OP_ENUM) return enum_test("v", o.arg0, o.arg1);
-      if (o.kind == XDRG_OP_UNION) {
-        if (o.flags & XDRG_F_DEFAULT) return (o.flags & XDRG_F_VALIDATE) ? enum_test("v", o.arg0, o.arg1) : "true";
-        std::string t;
-        for (auto &a : arms(o))
-          for (uint32_t v : a.second) t += (t.empty() ? "" : " || ") + std::string("v == ") + u32(v);
-        if (t.empty()) t = "false";
-        return (o.flags & XDRG_F_VALIDATE) ? "(" + enum_test("v", o.arg0, o.arg1) + " && (" + t + "))" : "(" + t + ")";
-      }
-      return "v <= " + u32(o.arg0);  // VAROPAQUE, STRING, VECTOR
+      if (o.kind != XDRG_OP_VECTOR || !(o.flags & XDRG_F_SUB)) return "true";
+      const xdrg_op &b = op(o.arg4);  // the body's first op must be the checked one (no offset)
+      const bool checked = b.kind == XDRG_OP_UNION || (b.kind == XDRG_OP_ENUM && (b.flags & XDRG_F_VALIDATE)) ||
+                           b.kind == XDRG_OP_VAROPAQUE || b.kind == XDRG_OP_STRING || b.kind == XDRG_OP_VECTOR;
+      if (!checked) return "true";
+      return "(v == 0u || " + first_test(o.arg4, "w") + ")";
     }
     return "true";
   }
@@ -1108,7 +1128,7 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
   g.ind = 2;
   g.rx_block(0, kNoPc);
   const std::string rx_code = g.o.str();
-  const std::string first = g.first_test(), flen = g.first_len();
+  const std::string first = g.first_test(), flen = g.first_len(), second = g.second_test();
   // element-area shares of packed plans
   g.o.str("");
   g.ind = 4;
@@ -1157,6 +1177,7 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
     << "  __device__ __forceinline__ void init(uint32_t *) const {}\n"
     << "  __device__ __forceinline__ bool first_ok(const uint32_t *, uint32_t v) const { return " << first << "; }\n"
     << "  __device__ __forceinline__ uint64_t first_len(uint32_t v) const { return " << flen << "; }\n"
+    << "  __device__ __forceinline__ bool second_ok(uint32_t v, uint32_t w) const { return " << second << "; }\n"
     << "  __device__ __forceinline__ uint32_t rlen(const uint32_t *m, const uint8_t *__restrict__ s, uint64_t len,\n"
     << "                                           uint64_t a, uint32_t maxlen) const {\n"
     << "    return rlen_rd<rx_global, uint64_t>(m, rx_global{s}, len, a, maxlen);\n  }\n"

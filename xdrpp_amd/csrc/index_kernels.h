@@ -325,6 +325,7 @@ struct mark_rx {
   // least bytes the record needs after its first checked word (the speculative
   // walk's second filter; first_ok already holds the size to maxlen)
   __device__ __forceinline__ uint64_t first_len(uint32_t) const { return 0; }
+  __device__ __forceinline__ bool second_ok(uint32_t, uint32_t) const { return true; }
   template <class RD, class U>
   __device__ __forceinline__ uint32_t rlen_rd(const uint32_t *, const RD &rd, U len, U a, uint32_t) const {
     if (len - a < 4) return RX_BAD;
@@ -410,9 +411,9 @@ __device__ __forceinline__ void rxs_walk_body(const P &parser, const uint8_t *__
     uint64_t mask = vmask;
     if (has_first && fd <= 1024) {  // (fd > 1024: every word is a candidate)
       const uint32_t i0 = (a + fd) >> 2;  // + kRxsSub / 4 stays inside stg for fd <= 1024
-      uint32_t fw[kRxsSub / 4];
+      uint32_t fw[kRxsSub / 4 + 1];  // (+ the word after the last, for second_ok)
 #pragma unroll
-      for (uint32_t k = 0; k < kRxsSub / 4; ++k) fw[k] = stg[i0 + k];
+      for (uint32_t k = 0; k < kRxsSub / 4 + 1; ++k) fw[k] = stg[i0 + k];
       uint64_t m = 0;
       // a candidate must also fit its first field's least bytes in maxlen: a
       // record that cannot breaks the chain anyway (the walk then falls back
@@ -422,10 +423,13 @@ __device__ __forceinline__ void rxs_walk_body(const P &parser, const uint8_t *__
 #pragma unroll
       for (uint32_t k = 0; k < kRxsSub / 4; ++k) {
         const uint32_t v = bswap32(fw[k]);
-        m |= static_cast<uint64_t>(parser.first_ok(rx_smem, v) && parser.first_len(v) <= room) << k;
+        m |= static_cast<uint64_t>(parser.first_ok(rx_smem, v) && parser.first_len(v) <= room &&
+                                   parser.second_ok(v, bswap32(fw[k + 1])))
+             << k;
       }
-      // words whose first checked word is past the staged stretch stay candidates
-      const uint32_t ns = a + fd < nb ? (nb - a - fd) / 4 : 0u;
+      // words whose first checked word (or the one after it, second_ok's) is
+      // past the staged stretch stay candidates
+      const uint32_t ns = a + fd + 4 < nb ? (nb - a - fd - 4) / 4 : 0u;
       if (ns < 64) m |= ~0ull << ns;
       mask &= m;
     }
