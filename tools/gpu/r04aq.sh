@@ -1,0 +1,6 @@
+# round 4: index-walk phase stamps with the prefix test; rpc bench index ratio
+mkdir -p gpurun_out/r04aq
+timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_record_index.py tests/test_long_messages.py tests/test_gpu_messages.py > gpurun_out/r04aq/pytest.log 2>&1 || exit 1
+timeout -k 10 300 python -u tools/tune/ix_stamps.py run containertest rpc recvar > gpurun_out/r04aq/ix_stamps.log 2>&1 || exit 1
+timeout -k 10 300 python -u bench.py --schema rpc --steps 10 --warmup 3 --no-cpu-baseline --no-large --no-cold --no-host-inclusive > gpurun_out/r04aq/bench_rpc.json 2> gpurun_out/r04aq/bench.err || exit 1
+timeout -k 10 300 python -u bench.py --schema containertest --steps 10 --warmup 3 --no-cpu-baseline --no-large --no-cold --no-host-inclusive > gpurun_out/r04aq/bench_containertest.json 2>> gpurun_out/r04aq/bench.err || exit 1

@@ -29,6 +29,13 @@ STAMP = ("#define XDRG_XSTAMP(k) do { if (threadIdx.x == 0) { const unsigned lon
          "__builtin_amdgcn_s_memtime(); *reinterpret_cast<volatile unsigned long long *>("
          "reinterpret_cast<char *>(nodes) + static_cast<unsigned long long>(gridDim.x) * (kRxsSeg / 2) + "
          "(static_cast<unsigned long long>(blockIdx.x) * " + str(NST) + "ull + (k)) * 8ull) = t_; } } while (0)\n")
+# per lane (first LBLK segments): guess-phase clocks (mask, candidate loop),
+# candidates parsed, nodes of the lane's chain
+LBLK = 2048
+LSTAMP = ("#define XDRG_LCLK() __builtin_amdgcn_s_memtime()\n"
+          "#define XDRG_LSTAMP(k, v) do { if (blockIdx.x < " + str(LBLK) + "u) { *reinterpret_cast<volatile unsigned long long *>("
+          "reinterpret_cast<char *>(nodes) + static_cast<unsigned long long>(gridDim.x) * (kRxsSeg / 2 + " + str(NST * 8) + ") + "
+          "((static_cast<unsigned long long>(blockIdx.x) * 64ull + threadIdx.x) * 4ull + (k)) * 8ull) = (v); } } while (0)\n")
 PHASES = ["stage", "guess", "agree", "count", "write"]
 
 
@@ -46,7 +53,7 @@ def build(schemas):
     for name in schemas:
         src = os.path.join(OUT, f"{name}.hip")
         with open(src, "w") as f:
-            f.write(STAMP + source(M.Plan(S.ALL[name])))
+            f.write(STAMP + LSTAMP + source(M.Plan(S.ALL[name])))
         subprocess.check_call([B.hipcc(), "--genco", f"--offload-arch={B.ARCH}", "-O3", "-std=c++17",
                                "-I", B.CSRC, "-I", os.path.join(ROOT, "include"),
                                "-o", os.path.join(OUT, f"{name}.co"), src])
@@ -87,6 +94,19 @@ def run(schemas):
             d[ph] = [int(np.median(dd)), int(np.percentile(dd, 90)), int(dd.max())]
         d["wave"] = [int(np.median(st[:, 5] - st[:, 0])), int(np.percentile(st[:, 5] - st[:, 0], 90))]
         print(name, "segments", nseg, "cycles [median, p90, max]:", d, flush=True)
+        o2 = nseg * (SEGB // 2 + NST * 8)
+        nb = min(nseg, LBLK)
+        assert o2 + nb * 64 * 32 <= ws.numel()
+        ls = ws[o2:o2 + nb * 64 * 32].cpu().numpy().view(np.uint64).reshape(nb, 64, 4).astype(np.int64)
+        lanes = ls[:, 8:, :]  # the segment proper
+        for j, nm in enumerate(["mask_clk", "loop_clk", "tries", "nodes"]):
+            x = lanes[:, :, j]
+            wmax = x.max(axis=1)
+            print(f"  {nm}: lane mean {x.mean():.1f} p90 {np.percentile(x, 90):.0f}; wave max median "
+                  f"{np.median(wmax):.0f} p90 {np.percentile(wmax, 90):.0f}", flush=True)
+        t = lanes[:, :, 2]
+        print("  tries histogram", np.bincount(t.ravel().clip(0, 8)).tolist(), flush=True)
+        print("  nodes histogram", np.bincount(lanes[:, :, 3].ravel().clip(0, 8)).tolist(), flush=True)
 
 
 if __name__ == "__main__":
