@@ -240,7 +240,7 @@ struct gen {
     };
     auto word = [&]() {
       need(u32(std::max(chk, pend + 4)));
-      line("{ const uint32_t v = bswap32(rd(" + (pend ? "p + " + u32(pend) : std::string("p")) + ")); p += " +
+      line("{ const uint32_t v = bswap32(rd.at(" + (pend ? "p + " + u32(pend) : std::string("p")) + ")); p += " +
            u32(pend + 4) + ";");
       pend = chk = 0;
     };
@@ -1306,8 +1306,9 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
     << "  __device__ __forceinline__ uint32_t rlen_rd(const uint32_t *, const RD &rd, U len,\n"
     << "                                              U a, uint32_t maxlen) const {\n"
     << "    const bool capped = static_cast<uint64_t>(a) + maxlen < len;\n"
-    << "    const U lim = capped ? static_cast<U>(a + maxlen) : len;\n"
-    << "    const uint32_t past = capped ? RX_LONG : RX_BAD;\n"
+    << "    U lim = capped ? static_cast<U>(a + maxlen) : len;\n"
+    << "    uint32_t past = capped ? RX_LONG : RX_BAD;\n"
+    << "    rd.clamp(lim, past);  // (the staged stretch's end: RX_OUT, and the caller parses from global memory)\n"
     << "    U p = a;\n"
     << rx_code << "    return static_cast<uint32_t>(p - a);\n  }\n"
     << "};\n\n"

@@ -16,6 +16,8 @@ constexpr uint64_t kIxCnt = (1ull << 40) - 1;  // table / entry word: count bits
 // Record parse results: RX_BAD (not a record start the decode accepts),
 // RX_LONG (runs past the index window, not past the stream).
 constexpr uint32_t RX_BAD = 0xffffffffu, RX_LONG = 0xfffffffeu;
+// (a generated parse over a staged stretch: the record runs past the stretch)
+constexpr uint32_t RX_OUT = 0xfffffffdu;
 
 // 16 words of a segment per thread (4 x 16 bytes, all in flight at once):
 // raw[4g + j] = word 4 * (tid + 256 g) + j of the segment (0 past the stream).
@@ -194,9 +196,15 @@ __device__ __forceinline__ void ix_seg_body(const P &parser, const uint8_t *__re
 // stretch staged in LDS (global past it).  Every read is of a 4-byte word
 // at a 4-aligned offset inside the stream (the parse checks the bound
 // before it reads).
+// Readers.  Generated parses (codegen.cpp rx_block) call clamp() on their
+// bound once and then read with at(), unchecked: every read lies inside the
+// bound tested before it.
 struct rx_global {
   const uint8_t *s;
   __device__ __forceinline__ uint32_t operator()(uint64_t p) const { return ld32(s + p); }
+  __device__ __forceinline__ uint32_t at(uint64_t p) const { return ld32(s + p); }
+  template <class U>
+  __device__ __forceinline__ void clamp(U &, uint32_t &) const {}
 };
 // The fast path (rxs_*) parses in 32-bit offsets from the start of its
 // staged stretch: rx_lds reads the stretch alone -- a read outside it sets
@@ -213,10 +221,22 @@ struct rx_lds {
     if (d >= nb) { out = true; d = 0; }
     return w[d >> 2];
   }
+  // a bound past the stretch becomes its end, and a parse that reaches it
+  // ends RX_OUT (a value test before that fails the same way from global)
+  __device__ __forceinline__ uint32_t at(uint32_t p) const { return w[p >> 2]; }
+  __device__ __forceinline__ void clamp(uint32_t &lim, uint32_t &past) const {
+    if (lim > nb) {
+      lim = nb;
+      past = RX_OUT;
+    }
+  }
 };
 struct rx_goff {
   const uint8_t *b;  // the stretch's start in global memory
   __device__ __forceinline__ uint32_t operator()(uint32_t p) const { return ld32(b + p); }
+  __device__ __forceinline__ uint32_t at(uint32_t p) const { return ld32(b + p); }
+  template <class U>
+  __device__ __forceinline__ void clamp(U &, uint32_t &) const {}
 };
 
 // ---------------------------------- speculative record index (fast path)
@@ -277,7 +297,7 @@ __device__ __forceinline__ uint32_t rxs_rlen(const P &parser, const uint32_t *sm
                                              const uint8_t *base, uint32_t lenr, uint32_t maxlen, uint32_t q) {
   st.out = false;
   const uint32_t L = parser.rlen_rd(smem, st, lenr, q, maxlen);
-  if (!st.out) return L;
+  if (!st.out && L != RX_OUT) return L;
   return parser.rlen_rd(smem, rx_goff{base}, lenr, q, maxlen);
 }
 
