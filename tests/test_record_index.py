@@ -228,6 +228,37 @@ def test_gpu_index_fast_path(dev, name, spec):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name", ["recvar", "rpc", "containertest"])
+def test_gpu_index_odd_bounds(dev, name):
+    """Bounds that are not whole words from a record start: an odd maxlen
+    (payloads are bound-tested unpadded, as the decode does, so a record may
+    end up to 3 bytes past the window) and a stream cut to a ragged length.
+    The walk's staged parse sends such records to global memory
+    (index_kernels.h rx_lds::clamp); both device paths against the C
+    restatement."""
+    from xdrpp_amd import marshal as M
+    cp = compile_plan(S.ALL.get(name) or S.CONTAINERS[name])
+    x, offs, n = gold_stream(name) if name in VAR else containers_stream(name)
+    reps = max(1, -(-(1 << 17) // int(offs[n])))
+    x, offs, n = tiled(x, offs, n, reps)
+    W = window(cp)
+    sizes = np.diff(offs.astype(np.int64))
+    cases = [(f"maxlen{m}", x, n, m) for m in (W - 1, W - 3, int(np.median(sizes)) + 1, int(np.median(sizes)) + 2)]
+    cases += [(f"ragged{c}", x[:int(offs[n]) - c], n, W) for c in (1, 2, 3)]
+    cases += [(f"ragged_mid{c}", x[:int(offs[n // 2]) + c], n, W) for c in (1, 2, 3)]
+    for fast in (1, 0):
+        mar = M.Marshaler(M.Plan(cp, {"specialize": 1, "index_fast": fast}), dev)
+        for label, y, k, m in cases:
+            want, wcnt, wrc, wer = O.index_records(cp, y, k, m)
+            got, gcnt, err = _gpu_index(mar, y, k, m, dev)
+            assert np.array_equal(got, want), (fast, label)
+            assert gcnt == wcnt, (fast, label)
+            assert (err.code if err else 0) == wrc, (fast, label)
+            if err:
+                assert err.record == wer, (fast, label)
+
+
+@pytest.mark.gpu
 def test_gpu_index_long_record(dev):
     from xdrpp_amd import marshal as M
     x, offs, n = gold_stream("recvar")

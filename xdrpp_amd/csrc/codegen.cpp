@@ -1308,7 +1308,7 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
     << "    const bool capped = static_cast<uint64_t>(a) + maxlen < len;\n"
     << "    U lim = capped ? static_cast<U>(a + maxlen) : len;\n"
     << "    uint32_t past = capped ? RX_LONG : RX_BAD;\n"
-    << "    rd.clamp(lim, past);  // (the staged stretch's end: RX_OUT, and the caller parses from global memory)\n"
+    << "    rd.clamp(lim, past, a);  // (the staged stretch's end: RX_OUT, and the caller parses from global memory)\n"
     << "    U p = a;\n"
     << rx_code << "    return static_cast<uint32_t>(p - a);\n  }\n"
     << "};\n\n"

@@ -204,7 +204,7 @@ struct rx_global {
   __device__ __forceinline__ uint32_t operator()(uint64_t p) const { return ld32(s + p); }
   __device__ __forceinline__ uint32_t at(uint64_t p) const { return ld32(s + p); }
   template <class U>
-  __device__ __forceinline__ void clamp(U &, uint32_t &) const {}
+  __device__ __forceinline__ void clamp(U &, uint32_t &, U) const {}
 };
 // The fast path (rxs_*) parses in 32-bit offsets from the start of its
 // staged stretch: rx_lds reads the stretch alone -- a read outside it sets
@@ -222,11 +222,16 @@ struct rx_lds {
     return w[d >> 2];
   }
   // a bound past the stretch becomes its end, and a parse that reaches it
-  // ends RX_OUT (a value test before that fails the same way from global)
+  // ends RX_OUT (a value test before that fails the same way from global).
+  // A bound that is not a whole number of words from a (an odd maxlen, a
+  // ragged stream end) sends the record to global memory at once: a payload
+  // tested unpadded may then end up to 3 bytes past the bound, and the
+  // tests after it wrap (the decode's own behaviour, which only the
+  // checked reads reproduce).
   __device__ __forceinline__ uint32_t at(uint32_t p) const { return w[p >> 2]; }
-  __device__ __forceinline__ void clamp(uint32_t &lim, uint32_t &past) const {
-    if (lim > nb) {
-      lim = nb;
+  __device__ __forceinline__ void clamp(uint32_t &lim, uint32_t &past, uint32_t a) const {
+    if (lim > nb || ((lim - a) & 3u)) {
+      lim = ((lim - a) & 3u) ? a : nb;
       past = RX_OUT;
     }
   }
@@ -236,7 +241,7 @@ struct rx_goff {
   __device__ __forceinline__ uint32_t operator()(uint32_t p) const { return ld32(b + p); }
   __device__ __forceinline__ uint32_t at(uint32_t p) const { return ld32(b + p); }
   template <class U>
-  __device__ __forceinline__ void clamp(U &, uint32_t &) const {}
+  __device__ __forceinline__ void clamp(U &, uint32_t &, U) const {}
 };
 
 // ---------------------------------- speculative record index (fast path)
