@@ -226,9 +226,19 @@ struct gen {
   // the most any of the skipped tests asked; nothing between them can fail
   // otherwise, so the record fails the same way).  The parse is a divergent
   // walk per lane: every instruction saved counts once per union arm.
+  // With rx_sticky set the same parse runs without early returns (the
+  // staged-stretch parse, rlen_st): the first failure is kept in r and the
+  // rest of the record runs on (its reads clamped into the stretch, its
+  // element loops stopped), so lanes rejoin at every test instead of
+  // leaving the wave's execution mask one by one.
+  bool rx_sticky = false;
+  void fail(const std::string &cond, const std::string &code) {
+    if (rx_sticky) line("r = (r == 0u && (" + cond + ")) ? " + code + " : r;");
+    else line("if (" + cond + ") return " + code + ";");
+  }
   void rx_block(uint32_t pc, uint32_t stop) {
     uint32_t pend = 0, chk = 0;
-    auto need = [&](const std::string &n) { line("if (lim - p < " + n + ") return past;"); };
+    auto need = [&](const std::string &n) { fail("lim - p < " + n, "past"); };
     auto skip = [&](uint32_t least, uint32_t adv) {
       chk = std::max(chk, pend + least);
       pend += adv;
@@ -240,8 +250,8 @@ struct gen {
     };
     auto word = [&]() {
       need(u32(std::max(chk, pend + 4)));
-      line("{ const uint32_t v = bswap32(rd.at(" + (pend ? "p + " + u32(pend) : std::string("p")) + ")); p += " +
-           u32(pend + 4) + ";");
+      line("{ const uint32_t v = bswap32(rd." + std::string(rx_sticky ? "atc(" : "at(") +
+           (pend ? "p + " + u32(pend) : std::string("p")) + ")); p += " + u32(pend + 4) + ";");
       pend = chk = 0;
     };
     while (pc != stop) {
@@ -255,24 +265,32 @@ struct gen {
       case XDRG_OP_ENUM:
         if (e.flags & XDRG_F_VALIDATE) {
           word();
-          line("  if (!" + enum_test("v", e.arg0, e.arg1) + ") return RX_BAD; }");
+          ind += 2;
+          fail("!" + enum_test("v", e.arg0, e.arg1), "RX_BAD");
+          ind -= 2;
+          line("}");
         } else {
           skip(4, 4);
         }
         break;
       case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING:
         word();
-        line("  if (v > " + u32(e.arg0) + ") return RX_BAD;");
-        line("  if (lim - p < v) return past;");
+        ind += 2;
+        fail("v > " + u32(e.arg0), "RX_BAD");
+        fail("lim - p < v", "past");
+        ind -= 2;
         line("  p += static_cast<U>((static_cast<uint64_t>(v) + 3u) & ~3ull); }");
         break;
       case XDRG_OP_VECTOR:
         if (e.flags & XDRG_F_SUB) {  // each element parsed by its body
           const std::string k = std::to_string(uid++);
           word();
-          line("  if (v > " + u32(e.arg0) + ") return RX_BAD;");
-          line("  if ((lim - p) / " + u32(e.arg3) + " < v) return past;  // the decode's least-wire check");
-          line("  for (uint32_t i" + k + " = 0; i" + k + " < v; ++i" + k + ") {");
+          ind += 2;
+          fail("v > " + u32(e.arg0), "RX_BAD");
+          fail("(lim - p) / " + u32(e.arg3) + " < v", "past");  // the decode's least-wire check
+          ind -= 2;
+          line("  for (uint32_t i" + k + " = 0; i" + k + " < v" + (rx_sticky ? " && r == 0u" : "") + "; ++i" + k +
+               ") {");
           ind += 2;
           rx_block(e.arg4, body_end(e.arg4));
           ind -= 2;
@@ -282,16 +300,20 @@ struct gen {
           continue;
         }
         word();
-        line("  if (v > " + u32(e.arg0) + ") return RX_BAD;");
-        line("  const uint64_t b = static_cast<uint64_t>(v) * " + u32(e.arg3) + ";");
-        line("  if (static_cast<uint64_t>(lim - p) < b) return past;");
+        ind += 2;
+        fail("v > " + u32(e.arg0), "RX_BAD");
+        line("const uint64_t b = static_cast<uint64_t>(v) * " + u32(e.arg3) + ";");
+        fail("static_cast<uint64_t>(lim - p) < b", "past");
+        ind -= 2;
         line("  p += static_cast<U>(b); }");
         pc += 1 + e.arg2;
         continue;
       case XDRG_OP_UNION: {
         const uint32_t end = ipdom[pc];
         word();
-        if (e.flags & XDRG_F_VALIDATE) line("  if (!" + enum_test("v", e.arg0, e.arg1) + ") return RX_BAD;");
+        ind += 2;
+        if (e.flags & XDRG_F_VALIDATE) fail("!" + enum_test("v", e.arg0, e.arg1), "RX_BAD");
+        ind -= 2;
         line("  switch (v) {");
         for (auto &a : arms(e)) {
           std::string lab;
@@ -305,6 +327,7 @@ struct gen {
         line("  default: {");
         ind += 2;
         if (e.flags & XDRG_F_DEFAULT) rx_block(e.arg4, end);
+        else if (rx_sticky) line("r = r ? r : RX_BAD;");
         else line("return RX_BAD;");
         ind -= 2;
         line("  } break;");
@@ -1241,6 +1264,11 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
   g.ind = 2;
   g.rx_block(0, kNoPc);
   const std::string rx_code = g.o.str();
+  g.o.str("");
+  g.rx_sticky = true;
+  g.rx_block(0, kNoPc);
+  g.rx_sticky = false;
+  const std::string rxs_code = g.o.str();
   const std::string first = g.first_test(), flen = g.first_len(), second = g.second_test();
   // the candidate prefix test of the speculative index
   g.o.str("");
@@ -1311,6 +1339,17 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
     << "    rd.clamp(lim, past, a);  // (the staged stretch's end: RX_OUT, and the caller parses from global memory)\n"
     << "    U p = a;\n"
     << rx_code << "    return static_cast<uint32_t>(p - a);\n  }\n"
+    << "  // the same parse over the staged stretch without early returns (index_kernels.h rxs_rlen)\n"
+    << "  __device__ __forceinline__ uint32_t rlen_st(const uint32_t *, const rx_lds &rd, uint32_t len,\n"
+    << "                                              uint32_t a, uint32_t maxlen) const {\n"
+    << "    using U = uint32_t;\n"
+    << "    const bool capped = static_cast<uint64_t>(a) + maxlen < len;\n"
+    << "    U lim = capped ? static_cast<U>(a + maxlen) : len;\n"
+    << "    uint32_t past = capped ? RX_LONG : RX_BAD;\n"
+    << "    rd.clamp(lim, past, a);\n"
+    << "    uint32_t r = 0;\n"
+    << "    U p = a;\n"
+    << rxs_code << "    return r ? r : static_cast<uint32_t>(p - a);\n  }\n"
     << "};\n\n"
     << "extern \"C\" __global__ __launch_bounds__(256) void xdrg_spec_ix_seg(\n"
     << "    const uint8_t *s, uint64_t len, uint32_t maxlen, uint32_t K, uint64_t *tab, uint32_t *list,\n"

@@ -229,6 +229,8 @@ struct rx_lds {
   // tests after it wrap (the decode's own behaviour, which only the
   // checked reads reproduce).
   __device__ __forceinline__ uint32_t at(uint32_t p) const { return w[p >> 2]; }
+  // (rlen_st: a failed record's reads go on, held inside the stretch)
+  __device__ __forceinline__ uint32_t atc(uint32_t p) const { return w[min(p, nb >= 4u ? nb - 4u : 0u) >> 2]; }
   __device__ __forceinline__ void clamp(uint32_t &lim, uint32_t &past, uint32_t a) const {
     if (lim > nb || ((lim - a) & 3u)) {
       lim = ((lim - a) & 3u) ? a : nb;
@@ -301,7 +303,7 @@ template <class P>
 __device__ __forceinline__ uint32_t rxs_rlen(const P &parser, const uint32_t *smem, const rx_lds &st,
                                              const uint8_t *base, uint32_t lenr, uint32_t maxlen, uint32_t q) {
   st.out = false;
-  const uint32_t L = parser.rlen_rd(smem, st, lenr, q, maxlen);
+  const uint32_t L = parser.rlen_st(smem, st, lenr, q, maxlen);
   if (!st.out && L != RX_OUT) return L;
   return parser.rlen_rd(smem, rx_goff{base}, lenr, q, maxlen);
 }
@@ -353,6 +355,10 @@ struct mark_rx {
   __device__ __forceinline__ uint64_t first_len(uint32_t) const { return 0; }
   __device__ __forceinline__ bool second_ok(uint32_t, uint32_t) const { return true; }
   __device__ __forceinline__ bool prefix_ok(const uint32_t *) const { return true; }
+  __device__ __forceinline__ uint32_t rlen_st(const uint32_t *m, const rx_lds &rd, uint32_t len, uint32_t a,
+                                              uint32_t maxlen) const {
+    return rlen_rd(m, rd, len, a, maxlen);
+  }
   template <class RD, class U>
   __device__ __forceinline__ uint32_t rlen_rd(const uint32_t *, const RD &rd, U len, U a, uint32_t) const {
     if (len - a < 4) return RX_BAD;
