@@ -96,6 +96,14 @@ def test_oracle_index_semantics():
     assert rc == 0 and cnt == 7 and np.array_equal(got[:8], offs[:8]) and (got[8:] == x.size).all()
     got, cnt, rc, er = O.index_records(cp, x, n, 64)  # a window shorter than the records
     assert rc == A.ERR_INDEX_LONG and er == 0
+    # a ragged stream whose last payload's padding overhangs its end: the
+    # unpadded bound test passes and the stream ends there (the record count
+    # is n, offsets[n] past len), read nowhere past the stream
+    cp = compile_plan(S.rpc_msg)
+    x, offs, n = gold_stream("rpc")
+    for c in (1, 2):
+        got, cnt, rc, _ = O.index_records(cp, x[:int(offs[n]) - c].copy(), n, window(cp))
+        assert rc == 0 and cnt == n and got[n] == offs[n], c
 
 
 # ------------------------------------------------------------------ GPU
