@@ -1363,7 +1363,8 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
     << "extern \"C\" __global__ __launch_bounds__(64) void xdrg_spec_size(\n"
     << "    const uint8_t *native, uint64_t n, uint32_t stride, const uint8_t *heap, uint64_t heap_len,\n"
     << "    uint32_t *sizes, unsigned long long *block_sums, uint32_t mark, unsigned long long *err) {\n"
-    << "  var_size_body(plan_walk{}, native, n, stride, heap, heap_len, sizes, block_sums, mark, err);\n}\n\n"
+    << "  var_size_body<plan_walk, " << (regs ? p.stride / 4 : 0)
+    << ">(plan_walk{}, native, n, stride, heap, heap_len, sizes, block_sums, mark, err);\n}\n\n"
     << "extern \"C\" __global__ __launch_bounds__(64) void xdrg_spec_encode(\n"
     << "    const uint8_t *native, uint64_t n, uint32_t stride, const uint8_t *heap, uint64_t heap_len,\n"
     << "    uint8_t *xdr, uint64_t cap, uint64_t *offsets, const uint32_t *sizes,\n"

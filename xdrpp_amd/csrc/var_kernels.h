@@ -1205,10 +1205,13 @@ __device__ __forceinline__ void var_decode_body(
 
 // ------------------------------------------------------------------ size
 // One 64-thread workgroup = 64 consecutive records, natives staged in LDS
-// with coalesced 16-byte loads.  sizes[r] = xdr_size (kSizeErr on a bad
-// discriminant, reported as the size pass of k_var_size does), block_sums
-// = the 64-record sums.
-template <class W>
+// with coalesced 16-byte loads -- or, with NW (the record's words, a
+// generated walk whose field offsets are constants), each lane's record
+// loaded straight into registers as var_encode_body's load_rec does, all of
+// its loads in flight at once and no LDS round trip.  sizes[r] = xdr_size
+// (kSizeErr on a bad discriminant, reported as the size pass of k_var_size
+// does), block_sums = the 64-record sums.
+template <class W, int NW = 0>
 __device__ __forceinline__ void var_size_body(const W &w, const uint8_t *__restrict__ native, uint64_t n,
                                               uint32_t stride, const uint8_t *__restrict__ heap,
                                               uint64_t heap_len, uint32_t *__restrict__ sizes,
@@ -1220,17 +1223,47 @@ __device__ __forceinline__ void var_size_body(const W &w, const uint8_t *__restr
   const uint64_t r = wr0 + lane;
   const uint32_t nrec = static_cast<uint32_t>(min<uint64_t>(64, n - wr0));
   const uint8_t *nsrc = native + wr0 * stride;
-  if ((reinterpret_cast<uintptr_t>(nsrc) & 15u) == 0) {
-    stage_tile<8>(tile, nsrc, nrec * stride, lane, 64u);
+  constexpr uint32_t kAl = NW % 4 == 0 ? 16u : NW % 2 == 0 ? 8u : 4u;
+  const bool regs = NW > 0 && stride == 4u * NW && (reinterpret_cast<uintptr_t>(native) & (kAl - 1)) == 0;
+  uint32_t rec[NW > 0 ? NW : 1];
+  if (regs) {
+#pragma unroll
+    for (int k = 0; k < (NW > 0 ? NW : 1); ++k) rec[k] = 0u;
+    if (lane < nrec) {
+      const uint8_t *src = nsrc + static_cast<uint64_t>(lane) * stride;
+      if constexpr (NW % 4 == 0) {
+#pragma unroll
+        for (int k = 0; k < NW; k += 4) {
+          const u32x4 q = *reinterpret_cast<const u32x4 *>(src + 4 * k);
+          rec[k] = q.x; rec[k + 1] = q.y; rec[k + 2] = q.z; rec[k + 3] = q.w;
+        }
+      } else if constexpr (NW % 2 == 0) {
+#pragma unroll
+        for (int k = 0; k < NW; k += 2) {
+          const uint2 q = *reinterpret_cast<const uint2 *>(src + 4 * k);
+          rec[k] = q.x; rec[k + 1] = q.y;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < (NW > 0 ? NW : 1); ++k) rec[k] = ld32(src + 4 * k);
+      }
+    }
   } else {
-    for (uint32_t i = lane; i < nrec * stride / 4u; i += 64u)
-      reinterpret_cast<uint32_t *>(tile)[i] = reinterpret_cast<const uint32_t *>(nsrc)[i];
+    if ((reinterpret_cast<uintptr_t>(nsrc) & 15u) == 0) {
+      stage_tile<8>(tile, nsrc, nrec * stride, lane, 64u);
+    } else {
+      for (uint32_t i = lane; i < nrec * stride / 4u; i += 64u)
+        reinterpret_cast<uint32_t *>(tile)[i] = reinterpret_cast<const uint32_t *>(nsrc)[i];
+    }
+    wave_sync();
   }
-  wave_sync();
   uint32_t size = 0;
   if (r < n) {
     uint32_t bad_op = 0xffffffffu;
-    const uint64_t s = w.size(tile + lane * stride, heap, heap_len, bad_op) + mark;
+    // (two calls, not one through a selected pointer: the register copy stays
+    // registers only when its walk sees the array itself)
+    const uint64_t s = (regs ? w.size(reinterpret_cast<const uint8_t *>(rec), heap, heap_len, bad_op)
+                             : w.size(tile + lane * stride, heap, heap_len, bad_op)) + mark;
     if (bad_op != 0xffffffffu) {
       report(err, r, bad_op, XDRG_ERR_BAD_DISCRIMINANT);
       size = kSizeErr;
