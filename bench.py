@@ -708,6 +708,7 @@ class GpuEngine:
         (self.plan, self.mar, self.nat, self.heap, self.xdr, self.back, self.offsets,
          self.heap_out) = setup(args.schema, n, self.dev, rank, world, plan_opts(args))
         self.enc_stream = plan_opts(args).get("enc_stream", -1)
+        self.size_linear = plan_opts(args).get("size_linear", -1)
         self.stream = torch.cuda.current_stream()
         self.s = self.stream.cuda_stream
         self.mar.status.init(self.s)
@@ -782,7 +783,11 @@ class GpuEngine:
             size_k, enc_k, dec_k = (("xdrg_spec_sub_size", "xdrg_spec_sub_encode", "xdrg_spec_sub_decode") if spec
                                     else ("k_sub_size", "k_sub_encode", "k_sub_decode"))
         else:
-            size_k = ("k_sub_size" if sub and not spec else "k_size_linear" if plan_linear(plan)
+            # (a linear plan sizes with the generated walk when it has one,
+            # XDRG_OPT_SIZE_LINEAR -1; 1 forces k_size_linear)
+            size_k = ("k_sub_size" if sub and not spec
+                      else "k_size_linear" if plan_linear(plan) and (self.size_linear == 1 or
+                                                                    (not spec and self.size_linear != 0))
                       else "xdrg_spec_size" if spec else "k_var_size")
             enc_k = (("xdrg_spec_encode_pre" if walk_first(plan) and self.enc_stream != 0 else "xdrg_spec_encode")
                      if spec

@@ -292,7 +292,8 @@ enum xdrg_plan_option {
   XDRG_OPT_WINDOW_BYTES = 5,      /* var decode LDS window per wave, -1 auto       */
   XDRG_OPT_ENC_UNROLL = 6,        /* payload chunks in flight per lane: 4, 8, 16   */
   XDRG_OPT_DEC_READAHEAD = 7,     /* window decode 32-byte read-ahead: 0 / 1       */
-  XDRG_OPT_SIZE_LINEAR = 8,       /* walk-free size pass for linear plans: 0 / 1   */
+  XDRG_OPT_SIZE_LINEAR = 8,       /* walk-free size pass for linear plans: 0 / 1;
+                                     -1 (default) only without generated kernels */
   XDRG_OPT_GRP_UNROLL = 9,        /* fixed group kernel chunks in flight, 0 auto   */
   XDRG_OPT_GRP_BLOCKS = 10,       /* fixed group kernel workgroups, 0 auto         */
   XDRG_OPT_GRP_NONTEMPORAL = 11,  /* fixed group kernel non-temporal stores: 0 / 1 */

@@ -580,7 +580,7 @@ def test_decode_window_shapes(dev, dec_shape, name, n):
     assert np.array_equal(bheap.cpu().numpy(), o_heap)
 
 
-@pytest.mark.parametrize("linear", [1, 0])
+@pytest.mark.parametrize("linear", [1, 0, -1])
 @pytest.mark.parametrize("n", [1, 63, 65, 300, 4099])
 def test_size_pass_linear(dev, linear, n):
     """recvar is a linear plan (no unions/containers): its size pass reads

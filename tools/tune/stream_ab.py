@@ -23,6 +23,7 @@ VAR_OPTS = {
     "sized": {"enc_stream": -1}, "halves": {"enc_stream": -1}, "halves0": {"enc_stream": 0},
     "wf2k": {"image_bytes": 2048}, "wf3k": {"image_bytes": 3072}, "wf6k": {"image_bytes": 6144},
     "wf8k": {"image_bytes": 8192},
+    "wf_nolin": {"enc_stream": -1, "size_linear": 0}, "two_pass_nolin": {"enc_stream": 0, "size_linear": 0},
 }
 VARIANTS = os.environ.get("VARIANTS", "two_pass walk_first lb sized").split()
 REPS = int(os.environ.get("REPS", "20"))

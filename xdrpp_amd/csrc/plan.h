@@ -102,7 +102,8 @@ struct plan_opts {
   int window_bytes = -1;   // var decode LDS window per wave (-1: per call)
   int enc_unroll = 8;      // payload chunks in flight per lane (4, 8, 16)
   int dec_readahead = 1;   // window decode: 32-byte read-ahead past the window
-  int size_linear = 1;     // size pass without a walk for linear plans
+  int size_linear = -1;    // size pass without a walk for linear plans: -1 when they have no generated
+                           // size walk (its register-loaded records measured faster), 1 always, 0 never
   int grp_unroll = 0;      // group kernel: chunks in flight (0: per plan)
   int grp_blocks = 0;      // group kernel: workgroups (0: 2048)
   int grp_nontemporal = 0; // group kernel: non-temporal stores
