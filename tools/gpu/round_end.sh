@@ -16,7 +16,7 @@ if [ -z "$NO_TESTS" ]; then
 fi
 timeout -k 10 400 python3 -u bench.py > "$O/bench_rec128.log" 2>&1 || exit 1
 echo "[bench] rec128 done $(date +%T)"
-for s in numerics recvar rpc vecrec containertest; do
+for s in numerics recvar rpc vecrec containertest rp_list; do
   extra="--no-cpu-baseline"
   [ "$s" = recvar ] && extra="$extra --msgs"
   [ "$s" = rpc ] && extra="$extra --msgs --rpc"
@@ -24,7 +24,7 @@ for s in numerics recvar rpc vecrec containertest; do
   echo "[bench] $s done $(date +%T)"
 done
 B="bench.py --no-cpu-baseline --no-large --no-cold --no-host-inclusive --no-plain --steps 10 --warmup 3"
-for s in rec128 numerics recvar rpc vecrec containertest; do
+for s in rec128 numerics recvar rpc vecrec containertest rp_list; do
   timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$O/stats_$s" -o k --output-format csv -- python3 $B --schema "$s" > "$O/stats_$s.log" 2>&1 || exit 1
   timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d "$O/fetch_$s" -o k --output-format csv -- python3 $B --schema "$s" > "$O/fetch_$s.log" 2>&1 || exit 1
   timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d "$O/write_$s" -o k --output-format csv -- python3 $B --schema "$s" > "$O/write_$s.log" 2>&1 || exit 1
