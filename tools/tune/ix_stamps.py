@@ -22,7 +22,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, ROOT)
 from xdrpp_amd import _abi as A, build as B, marshal as M, schemas as S  # noqa: E402
 
-OUT = os.path.join(ROOT, "tools", "tune", "_stamps_ix")
+OUT = os.path.join(ROOT, "tools", "tune", os.environ.get("STAMPS_DIR", "_stamps_ix"))
+EXTRA = os.environ.get("STAMPS_DEFINES", "")  # e.g. "XDRG_RX_NOPREFIX" (A/B builds)
 NST = 8
 SEGB = 6944  # kRxsSeg
 STAMP = ("#define XDRG_XSTAMP(k) do { if (threadIdx.x == 0) { const unsigned long long t_ = "
@@ -53,7 +54,7 @@ def build(schemas):
     for name in schemas:
         src = os.path.join(OUT, f"{name}.hip")
         with open(src, "w") as f:
-            f.write(STAMP + LSTAMP + source(M.Plan(S.ALL[name])))
+            f.write("".join(f"#define {d}\n" for d in EXTRA.split()) + STAMP + LSTAMP + source(M.Plan(S.ALL[name])))
         subprocess.check_call([B.hipcc(), "--genco", f"--offload-arch={B.ARCH}", "-O3", "-std=c++17",
                                "-I", B.CSRC, "-I", os.path.join(ROOT, "include"),
                                "-o", os.path.join(OUT, f"{name}.co"), src])

@@ -472,99 +472,6 @@ struct gen {
     }
     return "true";
   }
-  // The first op whose word is checked (nops() when none is).
-  uint32_t first_pc() const {
-    uint32_t pc = 0;
-    for (; pc < nops(); ++pc) {
-      const xdrg_op &o = op(pc);
-      if (o.kind == XDRG_OP_END || o.kind == XDRG_OP_JUMP) return nops();
-      if (!(o.kind == XDRG_OP_U64 || o.kind == XDRG_OP_OPAQUE || o.kind == XDRG_OP_U32 || o.kind == XDRG_OP_BOOL ||
-            (o.kind == XDRG_OP_ENUM && !(o.flags & XDRG_F_VALIDATE))))
-        break;
-    }
-    return pc;
-  }
-  // The candidate prefix test (index_kernels.h rxs_walk_body): the checks
-  // rx_block makes on the words at fixed offsets from the first checked word,
-  // kPxWords of them at most (f[w] holds word w, big-endian).  It follows
-  // union arms (each arm's continuation inlined, so offsets stay constants)
-  // and stops at the first field whose size is data-dependent, past its own
-  // check: a candidate it rejects is one whose parse fails with RX_BAD.
-  struct px_frame {
-    uint32_t pc, stop;
-  };
-  static constexpr uint32_t kPxWords = 8;  // index_kernels.h kRxPrefix
-  void px(uint32_t pc, uint32_t stop, uint32_t w, std::vector<px_frame> rest) {
-    auto fw = [&](uint32_t i) { return "bswap32(f[" + std::to_string(i) + "])"; };
-    for (;;) {
-      if (pc == stop) {
-        if (rest.empty()) break;
-        pc = rest.back().pc;
-        stop = rest.back().stop;
-        rest.pop_back();
-        continue;
-      }
-      if (pc >= nops() || w >= kPxWords) break;
-      const xdrg_op &e = op(pc);
-      switch (e.kind) {
-      case XDRG_OP_END: break;
-      case XDRG_OP_JUMP: pc = e.arg0; continue;
-      case XDRG_OP_U64: w += 2; ++pc; continue;
-      case XDRG_OP_OPAQUE: w += ((e.arg0 + 3u) & ~3u) / 4; ++pc; continue;
-      case XDRG_OP_U32: case XDRG_OP_BOOL: ++w; ++pc; continue;
-      case XDRG_OP_ENUM:
-        if (e.flags & XDRG_F_VALIDATE) line("if (!" + enum_test(fw(w), e.arg0, e.arg1) + ") return false;");
-        ++w;
-        ++pc;
-        continue;
-      case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING:
-        line("if (" + fw(w) + " > " + u32(e.arg0) + ") return false;");
-        break;
-      case XDRG_OP_VECTOR:
-        line("if (" + fw(w) + " > " + u32(e.arg0) + ") return false;");
-        if ((e.flags & XDRG_F_SUB) && w + 1 < kPxWords) {  // the first element's fixed-offset words
-          line("if (" + fw(w) + " != 0u) {");
-          ind += 2;
-          px(e.arg4, body_end(e.arg4), w + 1, {});
-          ind -= 2;
-          line("}");
-        }
-        break;
-      case XDRG_OP_UNION: {
-        const uint32_t end = ipdom[pc];
-        const std::string u = "u" + std::to_string(uid++);
-        line("{ const uint32_t " + u + " = " + fw(w) + ";");
-        ind += 2;
-        if (e.flags & XDRG_F_VALIDATE) line("if (!" + enum_test(u, e.arg0, e.arg1) + ") return false;");
-        std::vector<px_frame> cont = rest;
-        cont.push_back({end, stop});
-        line("switch (" + u + ") {");
-        for (auto &a : arms(e)) {
-          std::string lab;
-          for (uint32_t v : a.second) lab += "case " + u32(v) + ": ";
-          line(lab + "{");
-          ind += 2;
-          px(a.first, end, w + 1, cont);
-          ind -= 2;
-          line("}");
-        }
-        line("default: {");
-        ind += 2;
-        if (e.flags & XDRG_F_DEFAULT) px(e.arg4, end, w + 1, cont);
-        else line("return false;");
-        ind -= 2;
-        line("}");
-        line("}");
-        ind -= 2;
-        line("}");
-        return;
-      }
-      default: break;
-      }
-      break;
-    }
-    line("return true;");
-  }
   // The word after the first checked one, w, given that one's value v: when
   // the record starts with a container of element-subroutine elements whose
   // body opens with a checked field, a nonempty count's next word is that
@@ -1270,11 +1177,6 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
   g.rx_sticky = false;
   const std::string rxs_code = g.o.str();
   const std::string first = g.first_test(), flen = g.first_len(), second = g.second_test();
-  // the candidate prefix test of the speculative index
-  g.o.str("");
-  g.ind = 4;
-  g.px(g.first_pc(), kNoPc, 0, {});
-  const std::string px_code = g.o.str();
   // element-area shares of packed plans
   g.o.str("");
   g.ind = 4;
@@ -1324,8 +1226,7 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
     << "  __device__ __forceinline__ bool first_ok(const uint32_t *, uint32_t v) const { return " << first << "; }\n"
     << "  __device__ __forceinline__ uint64_t first_len(uint32_t v) const { return " << flen << "; }\n"
     << "  __device__ __forceinline__ bool second_ok(uint32_t v, uint32_t w) const { return " << second << "; }\n"
-    << "  __device__ __forceinline__ bool prefix_ok(const uint32_t *f) const {  // f: the first checked word on\n"
-    << px_code << "    return true;\n  }\n"
+
     << "  __device__ __forceinline__ uint32_t rlen(const uint32_t *m, const uint8_t *__restrict__ s, uint64_t len,\n"
     << "                                           uint64_t a, uint32_t maxlen) const {\n"
     << "    return rlen_rd<rx_global, uint64_t>(m, rx_global{s}, len, a, maxlen);\n  }\n"

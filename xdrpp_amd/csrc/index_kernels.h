@@ -289,7 +289,6 @@ constexpr uint32_t kRxsBackLanes = 8;                     // look-back: lanes 0-
 constexpr uint32_t kRxsBack = kRxsBackLanes * kRxsSub;
 constexpr uint32_t kRxsSeg = 64 * kRxsSub - kRxsBack;     // bytes per segment (one wave): lanes 8-63
 constexpr uint32_t kRxsAhead = 9u * 1024 - 64 * kRxsSub;  // staged past the segment (1280)
-constexpr uint32_t kRxPrefix = 8;  // words a parser's prefix_ok reads (codegen.cpp kPxWords)
 constexpr uint64_t kRxsBroken = ~0ull;
 // in the walk (32-bit offsets into the stretch): a broken chain, no state
 constexpr uint32_t kBrk = 0xffffffffu, kNone = 0xfffffffeu;
@@ -354,7 +353,6 @@ struct mark_rx {
   // walk's second filter; first_ok already holds the size to maxlen)
   __device__ __forceinline__ uint64_t first_len(uint32_t) const { return 0; }
   __device__ __forceinline__ bool second_ok(uint32_t, uint32_t) const { return true; }
-  __device__ __forceinline__ bool prefix_ok(const uint32_t *) const { return true; }
   __device__ __forceinline__ uint32_t rlen_st(const uint32_t *m, const rx_lds &rd, uint32_t len, uint32_t a,
                                               uint32_t maxlen) const {
     return rlen_rd(m, rd, len, a, maxlen);
@@ -450,9 +448,8 @@ __device__ __forceinline__ void rxs_walk_body(const P &parser, const uint8_t *__
     const uint32_t nv = min(nk, nf);
     const uint64_t vmask = nv >= 64 ? ~0ull : (1ull << nv) - 1;
     uint64_t mask = vmask;
-    const uint32_t i0 = (a + fd) >> 2;  // + kRxsSub / 4 + kRxPrefix stays inside stg for fd <= 1024
-    uint32_t npx = 0;                   // candidates whose prefix_ok words are all staged
     if (has_first && fd <= 1024) {  // (fd > 1024: every word is a candidate)
+      const uint32_t i0 = (a + fd) >> 2;  // + kRxsSub / 4 + 1 stays inside stg for fd <= 1024
       uint32_t fw[kRxsSub / 4 + 1];  // (+ the word after the last, for second_ok)
 #pragma unroll
       for (uint32_t k = 0; k < kRxsSub / 4 + 1; ++k) fw[k] = stg[i0 + k];
@@ -474,15 +471,11 @@ __device__ __forceinline__ void rxs_walk_body(const P &parser, const uint8_t *__
       const uint32_t ns = a + fd + 4 < nb ? (nb - a - fd - 4) / 4 : 0u;
       if (ns < 64) m |= ~0ull << ns;
       mask &= m;
-      npx = a + fd + 4 * kRxPrefix <= nb ? (nb - a - fd - 4 * kRxPrefix) / 4 + 1 : 0u;
     }
     lt1 = XDRG_LCLK();
     while (mask) {
       const uint32_t k = __builtin_ctzll(mask);
       mask &= mask - 1;
-      // the words at fixed offsets past the first checked one (rpc: a call's
-      // credential flavor and length, a reply's status words), from LDS
-      if (k < npx && !parser.prefix_ok(stg + i0 + k)) continue;
       ++ltry;
       const uint32_t p = a + 4 * k;
       const uint32_t q = rxs_chain(parser, rx_smem, st, base, lenr, maxlen, p, b, nd);

@@ -997,7 +997,6 @@ struct rx_interp {
   }
   __device__ __forceinline__ uint64_t first_len(uint32_t) const { return 0; }  // (no second filter)
   __device__ __forceinline__ bool second_ok(uint32_t, uint32_t) const { return true; }
-  __device__ __forceinline__ bool prefix_ok(const uint32_t *) const { return true; }
   __device__ __forceinline__ uint32_t rlen(const uint32_t *smem, const uint8_t *s, uint64_t len, uint64_t a,
                                            uint32_t maxlen) const {
     return rx_len(reinterpret_cast<const xdrg_op *>(smem), rp.table, rx_global{s}, len, a, maxlen);
