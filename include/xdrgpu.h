@@ -66,7 +66,7 @@
 extern "C" {
 #endif
 
-#define XDRG_ABI_VERSION 7
+#define XDRG_ABI_VERSION 8  /* 8: XDRG_SUB_FRAMES 32 -> 8 (register frames) */
 
 /* ---------------------------------------------------------------------- */
 /* Plan ops: a flat, wire-ordered walk of xdr_traits<T>::save.             */
@@ -132,8 +132,9 @@ enum xdrg_op_flags {
  * itself (test_recursive, tests/xdrtest.x:29-33; rpcbind's rp__list,
  * xdrpp/rpcb_prot.x:34).  Nesting is bounded by the data and by
  * marshaling_stack_limit only: a walk keeps XDRG_SUB_FRAMES element frames
- * in private memory, and records nested deeper are walked again by deep
- * passes whose frames live in the caller's workspace
+ * in registers (no private memory: graphs of these walks replay under
+ * ROCm's graph packet capture), and records nested deeper are walked again
+ * by deep passes whose frames live in the caller's workspace
  * (xdrg_deep_workspace_size: about 128 MiB + 8 bytes per record for a plan
  * that can nest that deep, 0 for any other).  A record that needs more than XDRG_MAX_FRAMES nested element
  * frames raises the stack-overflow error at the VECTOR op that would open
@@ -142,7 +143,10 @@ enum xdrg_op_flags {
  * elements leaves rsv = 1 + the failing element's index in every container
  * on the way to the failure (0 in the others).
  */
-#define XDRG_SUB_FRAMES 32
+#define XDRG_SUB_FRAMES 8
+/* Element frames the record index's parse follows (xdrg_index_records);
+ * a record nested deeper is XDRG_ERR_INDEX_LONG, as one past the window. */
+#define XDRG_INDEX_FRAMES 16
 #define XDRG_MAX_FRAMES (1u << 19)
 typedef struct xdrg_op {
   uint8_t kind;
@@ -396,9 +400,10 @@ int xdrg_encode(const xdrg_plan *plan, const void *d_native, uint64_t n,
  *   xdrg_encode_sized  the encode over the sizes the first half left in the
  *                      same workspace, with the same status block (not
  *                      re-initialised), records, heap and msgs flag: the
- *                      size pass does not run again.  Plans whose element
- *                      subroutines can nest past XDRG_SUB_FRAMES run both
- *                      halves here (their deep passes keep per-call lists).
+ *                      size pass does not run again (plans whose element
+ *                      subroutines nest past XDRG_SUB_FRAMES: the encode's
+ *                      deep passes walk the lists of deferred records the
+ *                      size pass left in the workspace).
  * Arguments as xdrg_encode / xdrg_encode_msgs; d_offsets is required by the
  * second half for every plan with msgs, for var plans without.
  */

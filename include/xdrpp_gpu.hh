@@ -47,6 +47,8 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -90,6 +92,16 @@ template <typename U, typename = void> struct union_cases {
   static std::vector<std::int64_t> values();
   static constexpr bool has_default = U::_xdr_has_default_case;
 };
+
+//! Plans emitted at generation time: `xdrc -plan file.x` (the plan back end,
+//! xdrpp_amd/gen/gen_plan.cc) writes file_plan.hh, which specializes this
+//! for every struct and union of file.x when it is included after this
+//! header and after file.hh (xdrc -hh).  plan_for<T>() then takes the
+//! emitted tables -- nothing is recorded from xdr_traits<T> at run time --
+//! and, when the emitted plan names a code object (`-kernels`, compiled by
+//! hipcc at build time) found in $XDRG_PLAN_KERNEL_DIR or
+//! XDRG_EMITTED_KERNEL_DIR, attaches the plan-specialized kernels too.
+template <typename T> struct emitted_plan;
 
 //! API-level failure of the C ABI (bad arguments, HIP error).
 struct api_error : std::runtime_error {
@@ -170,6 +182,19 @@ template <typename E> struct enum_validated {
   template <typename U> static decltype(xdr_validate_enum(U{}), std::true_type{}) test(int);
   static constexpr bool value = decltype(test<E>(0))::value;
 };
+
+template <typename E> using enum_validates = enum_validated<E>;  // (emitted plan headers)
+
+// T has an emitted plan (a complete emitted_plan<T> specialization)
+template <typename T, typename = void> struct has_emitted_plan : std::false_type {};
+template <typename T>
+struct has_emitted_plan<T, std::void_t<decltype(emitted_plan<T>::nops)>> : std::true_type {};
+
+// Plans recorded from xdr_traits at run time (tests: an emitted plan records none)
+inline std::atomic<std::size_t> &recorded_plans() {
+  static std::atomic<std::size_t> c{0};
+  return c;
+}
 
 template <typename U, typename = void> struct has_case_values : std::false_type {};
 template <typename U>
@@ -828,6 +853,55 @@ template <typename T> class batch_plan {
  private:
   struct deleter { void operator()(xdrg_plan *p) const { xdrg_plan_destroy(p); } };
   batch_plan() {
+    if constexpr (detail::has_emitted_plan<T>::value) {
+      using E = emitted_plan<T>;
+      ops_.assign(E::ops, E::ops + E::nops);
+      table_.assign(E::table, E::table + E::ntable);
+      msgs_ = E::msgs();
+      stride_ = E::stride;
+      // xdrc's C++ type of a fixed-size record is laid out as the plan stages
+      // it (natural alignment, bool 1 byte, enums 4) when its size agrees
+      identity_ = E::fixed && std::is_trivially_copyable_v<T> && sizeof(T) == stride_;
+      fixed_ = E::fixed;
+      validates_ = E::validates;
+      create(E::kernels);
+    } else {
+      record();
+      create("");
+    }
+  }
+  // the plan from the tables, and the emitted code object when there is one
+  void create(const char *kernels) {
+    xdrg_plan *h = nullptr;
+    detail::abicheck(xdrg_plan_create(ops_.data(), static_cast<std::uint32_t>(ops_.size()),
+                                      table_.empty() ? nullptr : table_.data(),
+                                      static_cast<std::uint32_t>(table_.size()), stride_, &h),
+                     "xdrg_plan_create");
+    h_.reset(h);
+    if (kernels && *kernels) {
+      const char *dir = std::getenv("XDRG_PLAN_KERNEL_DIR");
+#ifdef XDRG_EMITTED_KERNEL_DIR
+      if (!dir) dir = XDRG_EMITTED_KERNEL_DIR;
+#endif
+      if (dir) {
+        const std::string path = std::string(dir) + "/" + kernels + ".co";
+        if (FILE *f = std::fopen(path.c_str(), "rb")) {
+          std::vector<char> co;
+          char buf[1 << 16];
+          for (std::size_t k; (k = std::fread(buf, 1, sizeof buf, f)) > 0;) co.insert(co.end(), buf, buf + k);
+          std::fclose(f);
+          detail::abicheck(xdrg_plan_load_kernels(h, co.data(), co.size()), "xdrg_plan_load_kernels");
+        }
+      }
+    }
+    xdrg_plan_info info{};
+    detail::abicheck(xdrg_plan_get_info(h, &info), "xdrg_plan_get_info");
+    fixed_size_ = info.fixed_size;
+    max_record_bytes_ = info.max_record_bytes;
+  }
+  // the plan recorded from xdr_traits<T>
+  void record() {
+    ++detail::recorded_plans();
     // the record's ops, END, then one element subroutine per element type
     // (each ending with END); F_SUB VECTOR ops get the body's stride and pc
     detail::sub_registry subs;
@@ -882,17 +956,10 @@ template <typename T> class batch_plan {
     identity_ = sp.identity && sp.fixed && sizeof(T) == stride_;
     fixed_ = sp.fixed;
     validates_ = validates;
-    xdrg_plan *h = nullptr;
-    detail::abicheck(xdrg_plan_create(ops_.data(), static_cast<std::uint32_t>(ops_.size()),
-                                      table_.empty() ? nullptr : table_.data(),
-                                      static_cast<std::uint32_t>(table_.size()), stride_, &h),
-                     "xdrg_plan_create");
-    h_.reset(h);
-    xdrg_plan_info info{};
-    detail::abicheck(xdrg_plan_get_info(h, &info), "xdrg_plan_get_info");
-    fixed_size_ = info.fixed_size;
-    max_record_bytes_ = info.max_record_bytes;
   }
+  struct record_only {};
+  explicit batch_plan(record_only) { record(); }
+  template <typename U> friend struct recorded_plan;
   std::unique_ptr<xdrg_plan, deleter> h_;
   std::vector<xdrg_op> ops_;
   std::vector<std::uint32_t> table_;
@@ -903,6 +970,26 @@ template <typename T> class batch_plan {
 };
 
 template <typename T> const batch_plan<T> &plan_for() { return batch_plan<T>::get(); }
+
+//! The plan recorded from xdr_traits<T>, whether or not T has an emitted
+//! one (tests compare the two op for op).
+template <typename T> struct recorded_plan {
+  std::vector<xdrg_op> ops;
+  std::vector<std::uint32_t> table;
+  std::vector<std::pair<std::uint32_t, std::string>> msgs;
+  std::uint32_t stride = 0;
+  bool identity = false, fixed = false, validates = false;
+  recorded_plan() {
+    const batch_plan<T> r{typename batch_plan<T>::record_only{}};
+    ops = r.ops_;
+    table = r.table_;
+    msgs = r.msgs_;
+    stride = r.stride_;
+    identity = r.identity_;
+    fixed = r.fixed_;
+    validates = r.validates_;
+  }
+};
 
 // ---------------------------------------------------------------- staging
 //! Host staging of a batch: records in the staged layout + payload heap.

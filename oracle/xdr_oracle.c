@@ -923,9 +923,9 @@ static uint32_t rx_walk(rxctx *c, uint64_t *pp, uint32_t pc, uint32_t frames) {
         pc += 1 + op->arg2;
         break;
       }
-      /* the device index keeps XDRG_SUB_FRAMES frames: deeper records are
+      /* the device index keeps XDRG_INDEX_FRAMES frames: deeper records are
        * left to the caller's walk, as records past the window are */
-      if (v && frames == XDRG_SUB_FRAMES) return RX_LONG;
+      if (v && frames == XDRG_INDEX_FRAMES) return RX_LONG;
       for (uint32_t i = 0; i < v; ++i) {
         uint32_t rc = rx_walk(c, &p, op->arg4, frames + 1);
         if (rc) return rc;

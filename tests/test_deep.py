@@ -5,7 +5,7 @@ rpcbind's RPCBPROC_DUMP reply list rp__list (xdrpp/rpcb_prot.x:24-37)
 nest one element frame per node.  The reference recurses through them on
 its call stack (xdrpp/types.h:591-665, marshal.h:129-136, :198-205),
 bounded only by marshaling_stack_limit.  The device keeps XDRG_SUB_FRAMES
-frames per record in private memory and walks deeper records again in its
+frames per record in registers and walks deeper records again in its
 deep passes (xdrpp_amd/csrc/sub_kernels.h); only XDRG_MAX_FRAMES, far past
 the depth at which the reference's own recursion crashes, is a limit of
 its own.
@@ -350,7 +350,11 @@ def test_gpu_deep_two_streams_and_capture(gold, dev):
     """The deep passes' lists and frame slabs live in each caller's workspace
     (xdrg_deep_workspace_size): two marshalers encode and decode deep chains
     on two streams at once, each with its own workspace (no allocation, lock
-    or host wait inside the calls)."""
+    or host wait inside the calls); then an encode and a decode of the deep
+    plan captured into a graph replay three times to the reference's bytes,
+    through the generated frame walks and the interpreter.  (The main pass
+    keeps its frames in registers: with frames in private memory the second
+    replay faulted under ROCm's graph packet capture, profiles/r05a-b.)"""
     import torch
     from xdrpp_amd import marshal as M
     chains, wire, offs, recs = chains_of(gold, "test_recursive")
@@ -382,17 +386,27 @@ def test_gpu_deep_two_streams_and_capture(gold, dev):
             assert bytes(outs[k].cpu().numpy()) == bytes(x)
             assert np.array_equal(backs[k].cpu().numpy(), onat)
             assert np.array_equal(houts[k].cpu().numpy(), oheap)
-    # graph capture of a deep plan is refused before anything is queued
-    # (a replay of the frame walk faulted on MI355X, profiles/r04c): the
-    # capture ends empty and the plan still runs eagerly
-    mar = mars[0]
-    cap_s = torch.cuda.Stream(dev)
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g, stream=cap_s):
-        with pytest.raises(A.AbiError, match="EUNSUPPORTED"):
-            mar.launch_encode(dn, n, outs[0], heap=dh, offsets=offsets[0], stream=cap_s.cuda_stream)
-        with pytest.raises(A.AbiError, match="EUNSUPPORTED"):
-            mar.launch_decode(outs[0], n, backs[0], offsets=offsets[0], heap_out=houts[0], stream=cap_s.cuda_stream)
+    for spec in (1, 0):
+        mar = M.Marshaler(M.Plan(S.test_recursive, {"specialize": spec}), dev)
+        cap_s = torch.cuda.Stream(dev)
+        out, back, hout = outs[0], backs[0], houts[0]
+        mar.status.init(cap_s.cuda_stream)
+        mar.launch_encode(dn, n, out, heap=dh, offsets=offsets[0], stream=cap_s.cuda_stream)  # warm (tables, kernels)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=cap_s):
+            mar.launch_encode(dn, n, out, heap=dh, offsets=offsets[0], stream=cap_s.cuda_stream)
+            mar.launch_decode(out, n, back, offsets=offsets[0], heap_out=hout, stream=cap_s.cuda_stream)
+        for _ in range(3):
+            out.zero_()
+            back.zero_()
+            hout.zero_()
+            mar.status.init(torch.cuda.current_stream().cuda_stream)
+            g.replay()
+            torch.cuda.synchronize()
+            assert mar.check(cap_s.cuda_stream).code == 0
+            assert bytes(out.cpu().numpy()) == bytes(x), spec
+            assert np.array_equal(back.cpu().numpy(), onat), spec
+            assert np.array_equal(hout.cpu().numpy(), oheap), spec
+        del g
     torch.cuda.synchronize()
-    r = mar.encode(dn, n, dh)
-    assert bytes(r.xdr.cpu().numpy()) == bytes(x)

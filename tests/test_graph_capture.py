@@ -1,0 +1,99 @@
+"""hipGraph capture of the hot path (include/xdrgpu.h: every call except
+xdrg_index_records' default verdict wait and xdrg_index_msgs past 16,380-byte
+messages is capturable), replayed several times to the reference's bytes.
+
+Kernels with private (scratch) memory do not survive a second replay under
+ROCm's graph packet capture (DEBUG_CLR_GRAPH_PACKET_CAPTURE, on by default:
+profiles/r05a, r05b): every default kernel is scratch-free, and the two
+interpreter kernels that are not refuse a capturing stream
+(XDRG_EUNSUPPORTED).  Reference path: xdr_to_opaque / xdr_from_opaque,
+xdrpp/marshal.h:264-272, :299-306; bytes from the restatement pinned to the
+reference (tests/test_oracle.py) and the golden fixtures."""
+import numpy as np
+import pytest
+
+from conftest import golden
+
+from xdrpp_amd import _abi as A
+from xdrpp_amd import schemas as S
+from xdrpp_amd import workloads as W
+import oracle_bridge as O
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+def _dev(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+@pytest.mark.parametrize("name,n", [("rec128", 1024), ("numerics", 1000), ("recvar", 1024), ("rpc", 1024),
+                                    ("vecrec", 1024), ("containertest", 1024), ("rp_list", 1024)])
+def test_capture_encode_decode_replays(dev, name, n):
+    from xdrpp_amd import marshal as M
+    plan = M.Plan(S.ALL.get(name) or S.CONTAINERS[name])
+    mar = M.Marshaler(plan, dev)
+    nat, heap = W.GENERATORS[name](n)
+    want = golden(name, n, "xdr")
+    x, offs = O.encode(plan.cp, nat, n, heap)
+    assert np.array_equal(x, want)
+    dn = _dev(nat, dev)
+    dh = _dev(heap, dev) if heap.size else None
+    out = torch.empty(x.size, dtype=torch.uint8, device=dev)
+    offsets = torch.empty(n + 1, dtype=torch.int64, device=dev) if not plan.is_fixed else None
+    back = torch.zeros(n * plan.stride, dtype=torch.uint8, device=dev)
+    hout = torch.zeros(max(plan.decode_heap_bytes(x.size), 16), dtype=torch.uint8, device=dev) \
+        if not plan.is_fixed else None
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):  # warm: plan tables and kernels outside the capture
+        mar.status.init(side.cuda_stream)
+        mar.launch_encode(dn, n, out, heap=dh, offsets=offsets, stream=side.cuda_stream)
+        mar.launch_decode(out, n, back, offsets=offsets, heap_out=hout, stream=side.cuda_stream)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        s = torch.cuda.current_stream().cuda_stream
+        mar.launch_encode(dn, n, out, heap=dh, offsets=offsets, stream=s)
+        mar.launch_decode(out, n, back, offsets=offsets, heap_out=hout, stream=s)
+    if plan.is_fixed:
+        onat = nat
+    else:
+        onat, oheap = O.decode(plan.cp, x, n, offs)
+    for _ in range(3):
+        out.zero_()
+        back.zero_()
+        if hout is not None:
+            hout.zero_()
+        mar.status.init(torch.cuda.current_stream().cuda_stream)
+        g.replay()
+        assert mar.check().code == 0
+        assert np.array_equal(out.cpu().numpy(), want)
+        assert np.array_equal(back.cpu().numpy(), onat)
+        if hout is not None:
+            assert np.array_equal(hout.cpu().numpy()[:oheap.size], oheap)
+
+
+def test_scratch_interpreter_refuses_capture(dev):
+    """The window decode interpreter (k_var_decode_w, plans run without
+    their specialized kernels) keeps private memory: a capturing stream gets
+    XDRG_EUNSUPPORTED before anything is queued; it runs eagerly."""
+    from xdrpp_amd import marshal as M
+    n = 1024
+    plan = M.Plan(S.recvar, {"specialize": 0})
+    mar = M.Marshaler(plan, dev)
+    nat, heap = W.recvar(n)
+    x, offs = O.encode(plan.cp, nat, n, heap)
+    dx, doffs = _dev(x, dev), _dev(offs.astype(np.int64), dev)
+    back = torch.zeros(n * plan.stride, dtype=torch.uint8, device=dev)
+    hout = torch.zeros(plan.decode_heap_bytes(x.size), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        with pytest.raises(A.AbiError, match="EUNSUPPORTED"):
+            mar.launch_decode(dx, n, back, offsets=doffs, heap_out=hout,
+                              stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    nb, hb = mar.decode(dx, n, doffs)
+    onat, oheap = O.decode(plan.cp, x, n, offs)
+    assert np.array_equal(nb.cpu().numpy(), onat) and np.array_equal(hb.cpu().numpy(), oheap)

@@ -218,6 +218,51 @@ def test_stream_full_grid_repeated(dev, manifest, name):
         out.fill_(0)
 
 
+@pytest.mark.parametrize("mode", ["stream", "walk_first"])
+def test_stream_large_wave_totals(dev, mode):
+    """Waves whose byte totals run to megabytes: 65,536 records of up to 64
+    KiB blobs (about 4 MiB a wave, 4.3 GB over 1,024 waves) through the
+    look-back (its block sums are split in 16-bit halves summed in u32 over
+    up to 1,024 blocks a poll; a 24-bit split wrapped past 4 GiB a poll) and
+    through the scan.  Every blob points into one 64 KiB heap, so the bytes
+    are checked by property: the record index equals the running sum of the
+    records' sizes, the total matches, and sampled records equal the
+    restatement's encoding of the same record."""
+    from xdrpp_amd.xdr_types import Opaque, Struct, UHyper
+    t = Struct("bigblob", [("id", UHyper), ("blob", Opaque(1 << 20))])
+    p = M.Plan(t, MODES[mode])
+    n = 1 << 16
+    rng = np.random.default_rng(5)
+    heap = rng.integers(0, 256, 1 << 16, dtype=np.uint8)
+    lens = (65536 - rng.integers(0, 4096, n)).astype(np.int64)
+    nat = np.zeros((n, p.stride), dtype=np.uint8)
+    nat[:, 0:8] = np.arange(n, dtype="<u8").view(np.uint8).reshape(n, 8)
+    o = t.offsets["blob"]
+    nat[:, o + 8:o + 12] = lens.astype("<u4").view(np.uint8).reshape(n, 4)
+    sizes = 8 + 4 + ((lens + 3) & ~3)
+    woffs = np.zeros(n + 1, dtype=np.uint64)
+    woffs[1:] = np.cumsum(sizes)
+    total = int(woffs[-1])
+    assert total > (1 << 32)
+    mar = M.Marshaler(p, dev)
+    out = torch.empty(total, dtype=torch.uint8, device=dev)
+    offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    dn, dh = to_dev(nat.reshape(-1), dev), to_dev(heap, dev)
+    for _ in range(2):
+        mar.status.init(s)
+        mar.launch_encode(dn, n, out, heap=dh, offsets=offs, stream=s)
+        e = mar.status.read(s)
+        assert e.code == 0 and e.total_bytes == total
+        assert np.array_equal(offs.cpu().numpy().view(np.uint64), woffs)
+        for r in list(range(64)) + list(rng.integers(0, n, 40)) + [n - 1]:
+            want, _ = O.encode(p.cp, nat[r].copy(), 1, heap)
+            a = int(woffs[r])
+            assert np.array_equal(out[a:a + want.size].cpu().numpy(), want), r
+        out.fill_(0)
+    del out
+
+
 def test_fresh_status_reads_no_error(dev):
     """A Status that was never init()ed reads as 'no error' (it is born
     initialised), so a raw launch cannot report allocator garbage."""

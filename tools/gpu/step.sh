@@ -1,6 +1,7 @@
 # One GPU-box pass of chosen steps, each under its own time limit, chained
 # so that the first failure ends the pass.  Output under gpurun_out/$TAG.
-#   gpurun -- 'TAG=x STEPS="copy tests:tests/test_deep.py bench" bash tools/gpu/step.sh'
+#   gpurun -- 'TAG=x STEPS="copy tests:tests/test_deep.py,tests/test_kat.py bench:--schema,rpc" bash tools/gpu/step.sh'
+#   (test paths and bench/prof arguments comma-separated; "tests" alone = the whole suite)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
@@ -11,7 +12,7 @@ for st in ${STEPS:-tests bench}; do
   echo "[step] $st $(date +%T)"
   case $name in
     copy) timeout -k 10 120 ./tools/probe/copy_ceiling 256 2048 4096 > "$O/copy_ceiling.log" 2>&1 ;;
-    tests) timeout -k 10 900 python3 -u -m pytest ${arg:-tests} -m gpu -x -v --timeout 300 --timeout-method thread > "$O/pytest_${arg//\//_}.log" 2>&1 ;;
+    tests) ta=${arg:-tests}; timeout -k 10 900 python3 -u -m pytest ${ta//,/ } -m gpu -x -v --timeout 300 --timeout-method thread > "$O/pytest_$(echo "${arg:-all}" | tr '/,.' '___').log" 2>&1 ;;
     smoke) timeout -k 10 300 python3 -u -c 'import __graft_entry__ as g; g.smoke()' > "$O/smoke.log" 2>&1 ;;
     bench) timeout -k 10 400 python3 -u bench.py ${arg//,/ } > "$O/bench_${arg//[ ,-]/_}.log" 2>&1 ;;
     cppbench) timeout -k 10 300 ./oracle/_ref/dropin_test bench ${arg:-1048576} > "$O/cppbench.log" 2>&1 ;;

@@ -14,12 +14,12 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libxdrgpu.s
 
 # enum xdrg_op_kind
 OP_U32, OP_U64, OP_BOOL, OP_ENUM, OP_OPAQUE, OP_VAROPAQUE, OP_STRING, OP_UNION, OP_JUMP, OP_END, OP_VECTOR = range(1, 12)
-ABI_VERSION = 7  # XDRG_ABI_VERSION, include/xdrgpu.h
+ABI_VERSION = 8  # XDRG_ABI_VERSION, include/xdrgpu.h
 F_VALIDATE = 1
 F_DEFAULT = 2
 F_POINTER = 4
 F_SUB = 8
-SUB_FRAMES = 32  # XDRG_SUB_FRAMES (private frames of the element-subroutine walks)
+SUB_FRAMES = 8  # XDRG_SUB_FRAMES (register frames of the element-subroutine walks' main pass)
 MAX_FRAMES = 1 << 19  # XDRG_MAX_FRAMES
 
 PATH_FIXED_REG, PATH_FIXED_LDS, PATH_VAR = 1, 2, 3

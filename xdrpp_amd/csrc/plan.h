@@ -171,6 +171,13 @@ namespace xdrg {
 int launch_block_scan(const unsigned long long *in, unsigned long long *out, uint32_t nb,
                       xdrg_status *status, uint64_t *offsets, uint64_t n, void *stream);
 int record_hip_error(int hip_error, const char *what);
+// Device fills and copies as kernels of the library's own (never memset or
+// memcpy nodes in a captured graph: those do not take effect on replays
+// after the first under ROCm's graph packet capture, profiles/r05e):
+// `words` u32 of `value` at p (4-byte aligned), and n bytes src -> dst.
+// Return a hipError_t.
+int fill32(void *p, uint32_t value, uint64_t words, void *stream);
+int copy_bytes(void *dst, const void *src, uint64_t n, void *stream);
 
 // Validates ops and builds all host-side programs.  Returns XDRG_OK or an
 // API error.  Does not touch the device.

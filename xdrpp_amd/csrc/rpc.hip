@@ -427,8 +427,8 @@ int xdrg_rpc_replies(const xdrg_rpc_hdr *d_hdrs, uint64_t n, void *d_out, uint64
     return XDRG_EALIGN;
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (n == 0) {
-    HIPCHK(hipMemsetAsync(d_offsets, 0, 8, s));
-    HIPCHK(hipMemsetAsync(&d_status->total_bytes, 0, 8, s));
+    HIPCHK(static_cast<hipError_t>(xdrg::fill32(d_offsets, 0u, 2, s)));
+    HIPCHK(static_cast<hipError_t>(xdrg::fill32(&d_status->total_bytes, 0u, 2, s)));
     return XDRG_OK;
   }
   if (!d_workspace || workspace_bytes < replies_ws_bytes(n)) return XDRG_ESPACE;

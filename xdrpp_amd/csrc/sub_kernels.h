@@ -65,15 +65,49 @@ struct sub_frame {
   uint32_t vpc;
 };
 
-struct priv_stack {
+// The walks touch the top frame only (and, after an error in the decode,
+// every open frame once): top / push / pop / each with fp = the frames open.
+//
+// Main pass: the frames in registers, f[0] the top one, pushed and popped by
+// shifting (every index is a constant once unrolled), so the kernels use no
+// private (scratch) memory.  A hipGraph replayed more than once faulted
+// with HSA_STATUS_ERROR_MEMORY_APERTURE_VIOLATION in the frame walks while
+// their frames lived in private memory (520 B of scratch a lane): the
+// second and later replays under ROCm's graph packet capture
+// (DEBUG_CLR_GRAPH_PACKET_CAPTURE, on by default); the same graph replayed
+// 4 times bit-exact with the packet capture off, and graphs of
+// scratch-free kernels replay under it (profiles/r05a, r05b).
+struct reg_stack {
   sub_frame f[kSubFrames];
-  __device__ __forceinline__ sub_frame &operator[](uint32_t i) { return f[i]; }
+  __device__ __forceinline__ sub_frame &top(uint32_t) { return f[0]; }
+  __device__ __forceinline__ void push(uint32_t, const sub_frame &x) {
+#pragma unroll
+    for (int j = kSubFrames - 1; j > 0; --j) f[j] = f[j - 1];
+    f[0] = x;
+  }
+  __device__ __forceinline__ void pop(uint32_t) {
+#pragma unroll
+    for (int j = 0; j + 1 < static_cast<int>(kSubFrames); ++j) f[j] = f[j + 1];
+  }
+  // fn(k, frame k, frame k - 1) for each of the fp open frames (k = 0 is
+  // the bottom one; its "frame below" is unused)
+  template <class FN> __device__ __forceinline__ void each(uint32_t fp, FN &&fn) const {
+#pragma unroll
+    for (uint32_t j = 0; j < kSubFrames; ++j)
+      if (j < fp) fn(fp - 1u - j, f[j], f[j + 1 < kSubFrames ? j + 1 : j]);
+  }
   __device__ __forceinline__ uint32_t cap() const { return kSubFrames; }
 };
+// Deep passes: `n` frames per lane in the caller's workspace.
 struct slab_stack {
   sub_frame *f;
   uint32_t n;
-  __device__ __forceinline__ sub_frame &operator[](uint32_t i) { return f[i]; }
+  __device__ __forceinline__ sub_frame &top(uint32_t fp) { return f[fp - 1]; }
+  __device__ __forceinline__ void push(uint32_t fp, const sub_frame &x) { f[fp] = x; }
+  __device__ __forceinline__ void pop(uint32_t) {}
+  template <class FN> __device__ __forceinline__ void each(uint32_t fp, FN &&fn) const {
+    for (uint32_t k = 0; k < fp; ++k) fn(k, f[k], f[k ? k - 1 : 0]);
+  }
   __device__ __forceinline__ uint32_t cap() const { return n; }
 };
 
@@ -87,6 +121,7 @@ struct sub_pass {
   uint32_t slab;
   uint32_t last;                   // 1: running out of frames is xdr_stack_overflow
   uint32_t packed;                 // decode, main pass of a non-recursive plan: packed element areas
+  uint32_t lines;                  // encode, main pass: the host gave each lane a 64-byte line buffer
 };
 
 enum : int { kWalkCont = -1, kWalkOk = 0, kWalkErr = 1, kWalkFull = 2 };
@@ -150,7 +185,7 @@ template <class ST>
 __device__ __forceinline__ bool sub_next(const xdrg_op *__restrict__ ops, ST &st, uint32_t &fp, uint32_t &pc,
                                          uint32_t &dbase, uint64_t &eb, bool &in_heap) {
   if (!fp) return false;
-  sub_frame &f = st[fp - 1];
+  sub_frame &f = st.top(fp);
   const xdrg_op &v = ops[f.vpc];
   if (f.left) {
     --f.left;
@@ -161,7 +196,8 @@ __device__ __forceinline__ bool sub_next(const xdrg_op *__restrict__ ops, ST &st
   }
   pc = f.vpc + 1;
   dbase -= v.depth;
-  if (--fp) eb = st[fp - 1].eb;
+  st.pop(fp);
+  if (--fp) eb = st.top(fp).eb;
   else in_heap = false;
   return true;
 }
@@ -173,7 +209,7 @@ __device__ __forceinline__ void sub_records(const sub_pass &P, uint64_t n, F &&w
   const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (!P.list) {
     if (gid < n) {
-      priv_stack st;
+      reg_stack st;
       walk(gid, st);
     }
     return;
@@ -224,8 +260,8 @@ __device__ int sub_size(const xdrg_op *__restrict__ ops, const uint32_t *__restr
       if (!cnt) { ++pc; break; }
       if (fp == st.cap()) { bad_op = pc; return kWalkFull; }
       dbase += op.depth;
-      st[fp++] = sub_frame{src.w64(op.noff), cnt - 1, pc};
-      src.eb = st[fp - 1].eb;
+      st.push(fp++, sub_frame{src.w64(op.noff), cnt - 1, pc});
+      src.eb = st.top(fp).eb;
       src.in_heap = true;
       pc = op.arg4;
       break;
@@ -435,7 +471,7 @@ __device__ int sub_encode_rec(const xdrg_op *__restrict__ sops, const uint32_t *
       if (!cnt) { ++pc; break; }
       if (fp == st.cap()) { *full_op = pc; return kWalkFull; }
       dbase += op.depth;
-      st[fp++] = sub_frame{eoff, cnt - 1, pc};
+      st.push(fp++, sub_frame{eoff, cnt - 1, pc});
       src.eb = eoff;
       src.in_heap = true;
       pc = op.arg4;
@@ -474,7 +510,7 @@ __device__ __forceinline__ void sub_encode_kernel(XDRG_SUB_ENCODE_PARAMS) {
     offsets[r] = off;
   }
   // after the ops (host: + 64 B a lane for the line writer)
-  line_writer lw{smem + 8u * nops + 16u * threadIdx.x, xdr, ~0ull, 0u, !P.list};
+  line_writer lw{smem + 8u * nops + 16u * threadIdx.x, xdr, ~0ull, 0u, !P.list && P.lines != 0};
   sub_records(P, n, [&](uint64_t r, auto &st) {
     const uint32_t sz = sizes[r];
     if (sz & kSizeErr) return;  // the size pass reported this record
@@ -608,7 +644,7 @@ __device__ int sub_decode_rec(const xdrg_op *__restrict__ sops, const uint32_t *
       for (uint64_t z = 0; z < (bytes & ~3ull); z += 4) st32(arr + z, 0u);
       for (uint64_t z = bytes & ~3ull; z < bytes; ++z) arr[z] = 0;
       dbase += op.depth;
-      st[fp++] = sub_frame{ecur, cnt - 1, pc};
+      st.push(fp++, sub_frame{ecur, cnt - 1, pc});
       eb = ecur;
       in_heap = true;
       ecur += bytes;
@@ -627,10 +663,10 @@ __device__ int sub_decode_rec(const xdrg_op *__restrict__ sops, const uint32_t *
     if (code != kReported) report(err, r, pc, code);
     // 1 + the failing element in every open container: the container's ref
     // sits in the object that encloses it (the record, or the frame below)
-    for (uint32_t k = 0; k < fp; ++k) {
-      uint8_t *ref = (k ? heap + st[k - 1].eb : rec) + sops[st[k].vpc].noff;
-      st32(ref + 12, ld32(ref + 8) - st[k].left);
-    }
+    st.each(fp, [&](uint32_t k, const sub_frame &fk, const sub_frame &below) {
+      uint8_t *ref = (k ? heap + below.eb : rec) + sops[fk.vpc].noff;
+      st32(ref + 12, ld32(ref + 8) - fk.left);
+    });
     return kWalkErr;
   }
   if (p != b) report(err, r, kOpRecordLevel, XDRG_ERR_TRAILING);

@@ -408,15 +408,18 @@ __device__ __forceinline__ bool lookback(lb_u64 *desc, uint32_t blk, uint64_t &e
     }
     const bool found = dp < dn;
     const uint32_t lim = found ? dp : dn;  // block totals (aggregates) summed by this step
-    // the aggregates (each < 2^31) in two parts, summed with DPP (no LDS)
+    // the aggregates (each < 2^31: the launch guard 64 * max_rec < 2^31) in
+    // two 16-bit-split parts, summed with DPP (no LDS) in u32: a part is at
+    // most 64 * PER * 2^16 <= 2^28 over the wave
+    static_assert(PER <= 64, "16-bit split sums must fit u32 over 64 * PER blocks");
     uint32_t lo = 0, hi = 0;
 #pragma unroll
     for (int u = 0; u < PER; ++u)
       if (lane + 64u * u < lim) {
-        lo += static_cast<uint32_t>(d[u]) & 0xffffffu;
-        hi += static_cast<uint32_t>((d[u] & kLbVal) >> 24);
+        lo += static_cast<uint32_t>(d[u]) & 0xffffu;
+        hi += static_cast<uint32_t>((d[u] & kLbVal) >> 16);
       }
-    excl += static_cast<uint64_t>(rl32(wave_incl_scan(lo), 63)) + (static_cast<uint64_t>(rl32(wave_incl_scan(hi), 63)) << 24);
+    excl += static_cast<uint64_t>(rl32(wave_incl_scan(lo), 63)) + (static_cast<uint64_t>(rl32(wave_incl_scan(hi), 63)) << 16);
     if (found) {  // + the inclusive prefix at dp
       uint64_t pv = 0;
 #pragma unroll

@@ -891,7 +891,9 @@ __device__ uint32_t rx_len(const xdrg_op *__restrict__ ops, const uint32_t *__re
   const U lim = capped ? static_cast<U>(a + maxlen) : len;
   const uint32_t past = capped ? RX_LONG : RX_BAD;
   struct frame { uint32_t left, entry, ret; };
-  frame st[XDRG_SUB_FRAMES];
+  // st[0] the top frame, pushed and popped by shifting: constant indices,
+  // registers, no private memory (sub_kernels.h reg_stack)
+  frame st[XDRG_INDEX_FRAMES];
   uint32_t fp = 0, pc = 0;
   U p = a;
   for (;;) {
@@ -899,8 +901,15 @@ __device__ uint32_t rx_len(const xdrg_op *__restrict__ ops, const uint32_t *__re
     switch (op.kind) {
     case XDRG_OP_END:
       if (!fp) return static_cast<uint32_t>(p - a);
-      if (st[fp - 1].left) { --st[fp - 1].left; pc = st[fp - 1].entry; }
-      else pc = st[--fp].ret;
+      if (st[0].left) {
+        --st[0].left;
+        pc = st[0].entry;
+      } else {
+        pc = st[0].ret;
+        --fp;
+#pragma unroll
+        for (int j = 0; j + 1 < XDRG_INDEX_FRAMES; ++j) st[j] = st[j + 1];
+      }
       continue;
     case XDRG_OP_JUMP: pc = op.arg0; continue;
     case XDRG_OP_U64:
@@ -951,8 +960,11 @@ __device__ uint32_t rx_len(const xdrg_op *__restrict__ ops, const uint32_t *__re
       } else {
         // deeper records are left to the caller's walk, as records past
         // the window are (include/xdrgpu.h xdrg_index_records)
-        if (fp == XDRG_SUB_FRAMES) return RX_LONG;
-        st[fp++] = frame{v - 1, op.arg4, pc + 1};
+        if (fp == XDRG_INDEX_FRAMES) return RX_LONG;
+#pragma unroll
+        for (int j = XDRG_INDEX_FRAMES - 1; j > 0; --j) st[j] = st[j - 1];
+        st[0] = frame{v - 1, op.arg4, pc + 1};
+        ++fp;
         pc = op.arg4;
       }
       break;
@@ -1493,6 +1505,22 @@ int run_fixed(const xdrg_plan &p, const dev_tables &T, bool decode, const void *
   return XDRG_OK;
 }
 
+// Kernels with private (scratch) memory do not survive repeated replays of
+// a hipGraph under ROCm's graph packet capture (DEBUG_CLR_GRAPH_PACKET_CAPTURE,
+// on by default): the second replay of the frame walks, when their frames
+// lived in private memory, faulted with HSA_STATUS_ERROR_MEMORY_APERTURE_
+// VIOLATION, while the same graph replayed bit-exact with the packet capture
+// off and graphs of scratch-free kernels replay under it (profiles/r05a,
+// r05b).  Every default kernel is scratch-free; a capturing stream gets
+// XDRG_EUNSUPPORTED from the launches that would use one of the two that are
+// not (the interpreters' window decode, k_var_decode_w, and the encode
+// interpreter at XDRG_OPT_ENC_UNROLL 16).
+int refuse_scratch_capture(hipStream_t s) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return XDRG_EUNSUPPORTED;
+  return XDRG_OK;
+}
+
 // Var workspace: u32 sizes[n], the 64-record block sums, then their
 // exclusive scan (a separate array: the multi-workgroup scan reads the sums
 // while other workgroups write the bases).
@@ -1575,16 +1603,15 @@ struct deep_passes {
 
 // The passes of plan p over n records on stream s, their memory at `area`
 // (deep_area_bytes(p, n) bytes of the caller's workspace).
-int deep_setup(const xdrg_plan &p, uint64_t n, void *area, size_t area_bytes, hipStream_t s, deep_passes &dp) {
+// reset = false: the lists a size pass over the same area left (the sized
+// half of an encode, xdrg_encode_sized after xdrg_encode_sizes).
+int deep_setup(const xdrg_plan &p, uint64_t n, void *area, size_t area_bytes, hipStream_t s, deep_passes &dp,
+               bool reset = true) {
   if (!p.deep) return XDRG_OK;
   if (n > 0xffffffffull) return XDRG_EUNSUPPORTED;  // u32 list entries
   if (!area || area_bytes < deep_area_bytes(p, n) || !aligned(area, 256)) return XDRG_ESPACE;
-  {  // a graph replay of the frame walk faulted on MI355X (profiles/r04c): not captured
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return XDRG_EUNSUPPORTED;
-  }
   uint8_t *d = static_cast<uint8_t *>(area);
-  HIPCHK(hipMemsetAsync(d, 0, 16, s));
+  if (reset) HIPCHK(static_cast<hipError_t>(xdrg::fill32(d, 0u, 4, s)));
   auto *cnt = reinterpret_cast<unsigned long long *>(d);
   const uint64_t cap = std::max<uint64_t>(n, 1);
   uint32_t *la = reinterpret_cast<uint32_t *>(d + 256), *lb = la + cap;
@@ -1686,7 +1713,48 @@ unsigned long long *err_ptr(xdrg_status *st) {
 }
 }  // namespace
 
+namespace {
+__global__ __launch_bounds__(256) void k_fill32(uint32_t *__restrict__ p, uint32_t v, uint64_t words) {
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < words; i += stride) p[i] = v;
+}
+// 16-byte chunks when both ends allow it, else words, then the tail bytes
+__global__ __launch_bounds__(256) void k_copy_bytes(uint8_t *__restrict__ d, const uint8_t *__restrict__ s,
+                                                    uint64_t n) {
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  const uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  uint64_t done = 0;
+  if (!((reinterpret_cast<uintptr_t>(d) | reinterpret_cast<uintptr_t>(s)) & 15u)) {
+    const uint64_t c = n / 16;
+    for (uint64_t i = t; i < c; i += stride)
+      reinterpret_cast<u32x4 *>(d)[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(s) + i);
+    done = c * 16;
+  } else if (!((reinterpret_cast<uintptr_t>(d) | reinterpret_cast<uintptr_t>(s)) & 3u)) {
+    const uint64_t c = n / 4;
+    for (uint64_t i = t; i < c; i += stride)
+      reinterpret_cast<uint32_t *>(d)[i] = reinterpret_cast<const uint32_t *>(s)[i];
+    done = c * 4;
+  }
+  for (uint64_t i = done + t; i < n; i += stride) d[i] = s[i];
+}
+uint32_t copy_grid(uint64_t units) {  // a multiple of the 8 XCDs, at most 2,048 workgroups
+  const uint64_t g = (units + 255) / 256;
+  return static_cast<uint32_t>(std::max<uint64_t>(8, std::min<uint64_t>(2048, (g + 7) & ~7ull)));
+}
+}  // namespace
+
 namespace xdrg {
+int fill32(void *p, uint32_t value, uint64_t words, void *stream) {
+  if (!words) return hipSuccess;
+  k_fill32<<<copy_grid(words), 256, 0, static_cast<hipStream_t>(stream)>>>(static_cast<uint32_t *>(p), value, words);
+  return hipGetLastError();
+}
+int copy_bytes(void *dst, const void *src, uint64_t n, void *stream) {
+  if (!n) return hipSuccess;
+  k_copy_bytes<<<copy_grid(n / 16 + 1), 256, 0, static_cast<hipStream_t>(stream)>>>(
+      static_cast<uint8_t *>(dst), static_cast<const uint8_t *>(src), n);
+  return hipGetLastError();
+}
 int launch_block_scan(const unsigned long long *in, unsigned long long *out, uint32_t nb,
                       xdrg_status *status, uint64_t *offsets, uint64_t n, void *stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -1717,15 +1785,12 @@ int var_encode(const xdrg_plan &P, const dev_tables &T, const void *d_native, ui
   const xdrg_plan *p = &P;
   const plan_opts &O = P.opts;
   unsigned long long *err = err_ptr(d_status);
-  // a deep plan's lists live in the frame pool for one call: its sized half
-  // runs both halves again
-  if (phase == kEncSized && p->deep) phase = kEncBoth;
   if (phase != kEncSizes && !d_offsets) return XDRG_EINVAL;
   if (d_heap && !aligned(d_heap, 4)) return XDRG_EALIGN;
   if (!aligned(d_native, 8) || (phase != kEncSizes && (!aligned(d_xdr, 4) || !aligned(d_offsets, 8))))
     return XDRG_EALIGN;
   if (n == 0) {
-    if (d_offsets) HIPCHK(hipMemsetAsync(d_offsets, 0, 8, s));
+    if (d_offsets) HIPCHK(static_cast<hipError_t>(xdrg::fill32(d_offsets, 0u, 2, s)));
     return XDRG_OK;
   }
   size_t so, bo, bbo;
@@ -1802,16 +1867,17 @@ int var_encode(const xdrg_plan &P, const dev_tables &T, const void *d_native, ui
     uint32_t nb32 = static_cast<uint32_t>(nb), sl = stack_limit, cc = Cs, mk = mark;
     void *args[] = {&nat8, &n, const_cast<uint32_t *>(&p->stride), &d_heap, &heap_len, &xdr8, &cap,
                     &d_offsets, &bb, &desc, &nb32, &total, &sl, &cc, &mk, &err};
-    HIPCHK(hipMemsetAsync(desc, 0, align_up(nb * 8, 16), s));
+    HIPCHK(static_cast<hipError_t>(xdrg::fill32(desc, 0u, align_up(nb * 8, 16) / 4, s)));
     HIPCHK(hipModuleLaunchKernel(static_cast<hipFunction_t>(SM->f_enc_lb), nb32, 1, 1, 64, 1, 1, lds_pre, s, args,
                                  nullptr));
     return XDRG_OK;
   }
   deep_passes dp;  // element subroutines nested past XDRG_SUB_FRAMES
-  if (p->has_sub)
-    if (int rc = deep_setup(*p, n, static_cast<char *>(d_ws) + need, ws_bytes - need, s, dp)) return rc;
+  if (p->has_sub)  // (the sized half walks the lists its size pass left in the workspace)
+    if (int rc = deep_setup(*p, n, static_cast<char *>(d_ws) + need, ws_bytes - need, s, dp, phase != kEncSized))
+      return rc;
   if (phase == kEncSized) {  // sizes and block bases from xdrg_encode_sizes
-    HIPCHK(hipMemcpyAsync(d_offsets + n, &d_status->total_bytes, 8, hipMemcpyDeviceToDevice, s));
+    HIPCHK(static_cast<hipError_t>(xdrg::copy_bytes(d_offsets + n, &d_status->total_bytes, 8, s)));
   } else {
     if (SM && (!p->linear || p->opts.size_linear != 1)) {  // (recvar: 12.2 vs k_size_linear's 13.2 us)
       const size_t tile = 64ull * p->stride;
@@ -1827,11 +1893,16 @@ int var_encode(const xdrg_plan &P, const dev_tables &T, const void *d_native, ui
     if (phase == kEncSizes) return XDRG_OK;
   }
   if (p->has_sub && !SM) {
-    const deep_passes ep = encode_passes(dp);
+    deep_passes ep = encode_passes(dp);
     const spec_module *FM = frame_spec(*p);
     void *mf = FM ? FM->f_sub_enc : nullptr;
+    // the main pass's 64-byte line buffer per lane (sub_kernels.h
+    // line_writer) when it fits beside the ops (plans up to ~1,500 ops);
+    // past that the walk stores straight to the stream
+    if (lds_ops > kVarLdsBudget) return XDRG_EUNSUPPORTED;
+    ep.main.lines = lds_ops + 64u * 256u <= kVarLdsBudget ? 1u : 0u;
     auto go = [&](uint32_t grid, uint32_t block, const sub_pass &P) {  // + each lane's line buffer
-      return frame_launch(k_sub_encode, mf, grid, block, lds_ops + 64u * block, s, nat8, n,
+      return frame_launch(k_sub_encode, mf, grid, block, lds_ops + (P.lines ? 64u * block : 0u), s, nat8, n,
                           p->stride, d_heap,
                           heap_len, xdr8, cap, d_offsets, sizes, bbase, T.d_ops, nops, T.d_table, stack_limit, mark,
                           err, P);
@@ -1864,6 +1935,8 @@ int var_encode(const xdrg_plan &P, const dev_tables &T, const void *d_native, ui
     return XDRG_OK;
   }
   if (kern == 3) {
+    if (O.enc_unroll == 16)
+      if (int rc = refuse_scratch_capture(s)) return rc;
 #define LAUNCH_ENC_IU(K, UU)                                                                   \
   k_var_encode_i<K, UU><<<nb, 64, LI.total, s>>>(nat8, n, p->stride, d_heap, heap_len, xdr8,  \
                                                  cap, d_offsets, sizes, bbase, T.d_ops, nops,   \
@@ -2010,7 +2083,7 @@ int var_decode(const xdrg_plan &P, const dev_tables &T, const void *d_xdr, uint6
   if (p->has_sub && !SM) {  // containers of variable-size elements: the frame walk
     deep_passes dp;  // element subroutines nested past XDRG_SUB_FRAMES
     if (int rc = deep_setup(*p, n, d_ws, ws_bytes, s, dp)) return rc;
-    if (copy && len) HIPCHK(hipMemcpyAsync(d_heap_out, d_xdr, len, hipMemcpyDeviceToDevice, s));
+    if (copy && len) HIPCHK(static_cast<hipError_t>(xdrg::copy_bytes(d_heap_out, d_xdr, len, s)));
     const size_t lds = p->ops.size() * sizeof(xdrg_op);
     const spec_module *FM = frame_spec(*p);
     void *mf = FM ? FM->f_sub_dec : nullptr;
@@ -2052,6 +2125,7 @@ int var_decode(const xdrg_plan &P, const dev_tables &T, const void *d_xdr, uint6
     return XDRG_OK;
   }
   if (kern == 2) {
+    if (int rc = refuse_scratch_capture(s)) return rc;
     const uint64_t nb = (n + 63) / 64;
 #define LAUNCH_DEC_W(CP, RA)                                                                      \
   k_var_decode_w<CP, RA><<<nb, 64, lw, s>>>(xdr8, len, d_offsets, n, nat8, p->stride, d_heap_out, \
@@ -2064,7 +2138,7 @@ int var_decode(const xdrg_plan &P, const dev_tables &T, const void *d_xdr, uint6
     }
 #undef LAUNCH_DEC_W
   } else {
-    if (copy && len) HIPCHK(hipMemcpyAsync(d_heap_out, d_xdr, len, hipMemcpyDeviceToDevice, s));
+    if (copy && len) HIPCHK(static_cast<hipError_t>(xdrg::copy_bytes(d_heap_out, d_xdr, len, s)));
     const uint64_t nb = (n + 255) / 256;
     k_var_decode<<<nb, 256, p->ops.size() * sizeof(xdrg_op), s>>>(
         xdr8, len, d_offsets, n, nat8, p->stride, T.d_ops, nops, T.d_table, stack_limit,
@@ -2113,7 +2187,7 @@ int run_index(const xdrg_plan *p, const dev_tables *T, const void *d_stream, uin
   auto tab = [&](int l) { return reinterpret_cast<uint64_t *>(ws + L.tab[l]); };
   auto ent = [&](int l) { return reinterpret_cast<uint64_t *>(ws + L.ent[l]); };
   const uint8_t *s8 = static_cast<const uint8_t *>(d_stream);
-  if (!C.next) HIPCHK(hipMemsetAsync(d_count, 0xff, 8, s));  // (a window's caller sets it once)
+  if (!C.next) HIPCHK(static_cast<hipError_t>(xdrg::fill32(d_count, 0xffffffffu, 2, s)));  // (a window's caller sets it once)
   uint32_t *vlist = reinterpret_cast<uint32_t *>(ws + L.list);
   uint32_t *vcount = reinterpret_cast<uint32_t *>(ws + L.lcount);
   // the tables are needed above one segment; the valid-node lists always
@@ -2139,7 +2213,7 @@ int run_index(const xdrg_plan *p, const dev_tables *T, const void *d_stream, uin
   const bool walk_runs = walk_ok && !C.next && len >= 4ull * kRxsSeg && max_msgs > 0;
   if (fast_only && !walk_runs) return kIxNotHeld;
   if (REC && !C.next && !walk_runs)  // the flag says which path ran (include/xdrgpu.h)
-    HIPCHK(hipMemsetAsync(ws + L.rxs_flag, 0, 4, s));
+    HIPCHK(static_cast<hipError_t>(xdrg::fill32(ws + L.rxs_flag, 0u, 1, s)));
   if (walk_runs) {
     uint64_t *seg = reinterpret_cast<uint64_t *>(ws + L.rxs_seg);
     auto *cnt = reinterpret_cast<unsigned long long *>(ws + L.rxs_cnt);
@@ -2195,7 +2269,7 @@ int run_index(const xdrg_plan *p, const dev_tables *T, const void *d_stream, uin
       k_ix_up<false><<<L.n[l + 1], 256, 0, s>>>(tab(l), L.n[l], L.K, L.F, o, pfx(l), skip);
     HIPCHK(hipGetLastError());
   }
-  HIPCHK(hipMemsetAsync(ent(L.top), 0, 8, s));  // the chain starts at word 0 with 0 messages
+  HIPCHK(static_cast<hipError_t>(xdrg::fill32(ent(L.top), 0u, 2, s)));  // the chain starts at word 0 with 0 messages
   for (int l = L.top - 1; l >= 0; --l) {
     k_ix_down<<<L.n[l + 1], 64, 0, s>>>(pfx(l), L.n[l], L.K, L.F, ent(l + 1), ent(l), skip);
     HIPCHK(hipGetLastError());
@@ -2247,8 +2321,8 @@ int ix_windows(const uint8_t *s8, uint64_t len, uint32_t max_msg_len, uint64_t m
   auto *next = reinterpret_cast<unsigned long long *>(static_cast<char *>(d_ws) + need - kIxNextBytes);
   unsigned long long *err = err_ptr(d_status);
   unsigned long long *count = reinterpret_cast<unsigned long long *>(d_count);
-  HIPCHK(hipMemsetAsync(d_count, 0xff, 8, s));
-  HIPCHK(hipMemsetAsync(next, 0, 24, s));  // the chain starts at word 0, message 0
+  HIPCHK(static_cast<hipError_t>(xdrg::fill32(d_count, 0xffffffffu, 2, s)));
+  HIPCHK(static_cast<hipError_t>(xdrg::fill32(next, 0u, 6, s)));  // the chain starts at word 0, message 0
   unsigned long long h[3] = {0, 0, 0};
   uint64_t window = len;
   for (;;) {
@@ -2260,7 +2334,7 @@ int ix_windows(const uint8_t *s8, uint64_t len, uint32_t max_msg_len, uint64_t m
     if (!h[2]) continue;  // the hop budget ran out among long messages
     const uint64_t start = 4 * h[0], m0 = h[1];
     const uint64_t wl = std::min<uint64_t>(window, len - start);
-    HIPCHK(hipMemsetAsync(next, 0xff, 8, s));
+    HIPCHK(static_cast<hipError_t>(xdrg::fill32(next, 0xffffffffu, 2, s)));
     const ix_cont C{m0, start, s8, len, max_msg_len, next};
     if (int rc = run_index<false>(nullptr, nullptr, s8 + start, wl, XDRG_INDEX_MAX_MSG, max_msgs, d_offsets,
                                   d_count, d_ws, ws_bytes, d_status, s, C))
@@ -2444,8 +2518,8 @@ size_t xdrg_deep_workspace_size(const xdrg_plan *p, uint64_t n) { return p ? dee
 
 int xdrg_status_init(xdrg_status *st, void *stream) {
   if (!st) return XDRG_EINVAL;
-  HIPCHK(hipMemsetAsync(st, 0xff, 8, static_cast<hipStream_t>(stream)));
-  HIPCHK(hipMemsetAsync(reinterpret_cast<char *>(st) + 8, 0, 8, static_cast<hipStream_t>(stream)));
+  HIPCHK(static_cast<hipError_t>(xdrg::fill32(st, 0xffffffffu, 2, stream)));
+  HIPCHK(static_cast<hipError_t>(xdrg::fill32(reinterpret_cast<char *>(st) + 8, 0u, 2, stream)));
   return XDRG_OK;
 }
 
@@ -2545,7 +2619,7 @@ int xdrg_record_depths(const xdrg_plan *p, const void *d_native, uint64_t n, con
     return XDRG_OK;
   }
   if (p->path != XDRG_PATH_VAR || p->linear) {  // every record walks every op
-    HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_depths), int(p->max_depth), n, s));
+    HIPCHK(static_cast<hipError_t>(xdrg::fill32(d_depths, p->max_depth, n, s)));
     return XDRG_OK;
   }
   const uint64_t nb = (n + 63) / 64;
@@ -2573,7 +2647,7 @@ int xdrg_serial_sizes(const xdrg_plan *p, const void *d_native, uint64_t n, cons
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (p->path != XDRG_PATH_VAR) {
     // fixed_size for every record (xdr_struct_base_fs, types.h:691-700)
-    HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_sizes), int(p->fixed_size), n, s));
+    HIPCHK(static_cast<hipError_t>(xdrg::fill32(d_sizes, p->fixed_size, n, s)));
     return XDRG_OK;
   }
   deep_passes dp;  // element subroutines nested past XDRG_SUB_FRAMES
