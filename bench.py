@@ -173,7 +173,7 @@ def _port_baseline(schema: str, n: int, threads: int, reps: int, nat, heap) -> d
     sizes = np.zeros(n, dtype=np.uint32)
     X = n * plan.fixed_size if plan.fixed_size else None
     if X is None:
-        X = int(O.sizes(plan, nat, n).astype(np.int64).sum())
+        X = int(O.sizes(plan, nat, n, heap).astype(np.int64).sum())  # (element arrays live in the heap)
     out = np.zeros(max(X, 4), dtype=np.uint8)
     back = np.zeros(n * plan.stride, dtype=np.uint8)
     res = np.zeros(8, dtype=np.float64)

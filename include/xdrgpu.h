@@ -132,9 +132,8 @@ enum xdrg_op_flags {
  * itself (test_recursive, tests/xdrtest.x:29-33; rpcbind's rp__list,
  * xdrpp/rpcb_prot.x:34).  Nesting is bounded by the data and by
  * marshaling_stack_limit only: a walk keeps XDRG_SUB_FRAMES element frames
- * in registers (no private memory: graphs of these walks replay under
- * ROCm's graph packet capture), and records nested deeper are walked again
- * by deep passes whose frames live in the caller's workspace
+ * in registers, and records nested deeper are walked again by deep passes
+ * whose frames live in the caller's workspace
  * (xdrg_deep_workspace_size: about 128 MiB + 8 bytes per record for a plan
  * that can nest that deep, 0 for any other).  A record that needs more than XDRG_MAX_FRAMES nested element
  * frames raises the stack-overflow error at the VECTOR op that would open
@@ -271,6 +270,25 @@ typedef struct xdrg_error {
 
 int xdrg_abi_version(void);
 
+/*
+ * Graph capture.  Every encode, decode, size, depth, message and RPC call
+ * can be captured into a hipGraph (stream capture) and replayed any number
+ * of times, except xdrg_index_records' default wait for its walk's verdict
+ * (a capturing stream stays asynchronous instead) and xdrg_index_msgs past
+ * 16,380-byte messages.  The captured graph holds kernels only: the
+ * library fills and copies device memory with kernels of its own, because
+ * memset nodes of 16 bytes or more do not take effect on the replays after
+ * the first under ROCm's graph packet capture (DEBUG_CLR_GRAPH_PACKET_
+ * CAPTURE, on by default; tools/gpu/graph_node_probe.py, profiles/r05e),
+ * which left the deep passes' list counters stale and faulted a recursive
+ * plan's second replay (profiles/r04c, r05a-d).  Every default kernel is
+ * free of private (scratch) memory; the two interpreter kernels that are
+ * not (the window decode of a plan run without its specialized kernels,
+ * and the encode interpreter at XDRG_OPT_ENC_UNROLL 16) return
+ * XDRG_EUNSUPPORTED on a capturing stream.  Run a plan's first launch on a
+ * device outside the capture (it uploads the plan's tables).
+ */
+
 /* Validate and compile an immutable plan.  `table` holds enum value lists
  * and union case tables referenced by the ops.  native_stride is the byte
  * distance between consecutive native records.  Host-only: the plan's
@@ -362,8 +380,8 @@ size_t xdrg_workspace_size(const xdrg_plan *plan, uint64_t n);
  * and their frame slabs there (about 128 MiB + 8 bytes per record; 256-byte
  * aligned).  The memory is the caller's: no call allocates, locks or keeps
  * state between calls, so calls on different streams with different
- * workspaces run side by side, and graph capture records plain memsets and
- * kernels. */
+ * workspaces run side by side, and a captured graph of them holds kernels
+ * only (see "Graph capture" below). */
 size_t xdrg_deep_workspace_size(const xdrg_plan *plan, uint64_t n);
 
 /* Zero a status block (first_error = all ones) on `stream`. */

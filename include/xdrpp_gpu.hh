@@ -1295,24 +1295,21 @@ void from_opaque_batch(context &c, const void *bytes, std::size_t len, T *out, s
   const std::uint64_t hcap = P.fixed() ? 0 : xdrg_decode_heap_size(P.handle(), len);
   std::uint8_t *d_heap = hcap ? c.d_heap.get<std::uint8_t>(hcap) : nullptr;
   if (!P.fixed()) {
-    // the record index on the device (xdrg_index_records); a stream with a
-    // record longer than the index window, or nested deeper than its frames,
-    // is walked on the host instead
+    // the record index on the device (xdrg_index_records): records of any
+    // length and nesting (longer ones than the index window are walked on
+    // the device between list-ranking windows); a plan the index cannot
+    // chain (records under 4 bytes) is walked on the host
     const std::uint32_t win = static_cast<std::uint32_t>(
-        std::min<std::uint64_t>(std::max<std::uint64_t>(P.max_record_bytes(), 16), XDRG_INDEX_MAX_MSG));
+        std::min<std::uint64_t>(std::max<std::uint64_t>(P.max_record_bytes(), 16), XDRG_MAX_MSG));
     const std::size_t wsb = xdrg_index_workspace_size(len, win);
     void *ws = c.d_ws.get<std::uint8_t>(wsb);
     std::uint64_t *d_cnt = c.d_cnt.get<std::uint64_t>(1);
     const int rc = xdrg_index_records(P.handle(), d_x, len, n, win, d_off, d_cnt, ws, wsb, c.status(), s);
-    bool host = rc == XDRG_EUNSUPPORTED;
+    const bool host = rc == XDRG_EUNSUPPORTED;
     if (!host) {
       detail::abicheck(rc, "xdrg_index_records");
       const xdrg_error ie = detail::read_status<T>(c, s, false);
-      if (ie.code) {
-        if (ie.code != XDRG_ERR_INDEX_LONG) P.raise(ie);
-        host = true;
-        detail::abicheck(xdrg_status_init(c.status(), s), "xdrg_status_init");
-      }
+      if (ie.code) P.raise(ie);
     }
     if (host) {
       const std::vector<std::uint64_t> idx = index_records<T>(x, len, n);

@@ -880,6 +880,7 @@ typedef struct {
   const uint8_t *s;
   uint64_t lim;
   uint32_t past;
+  uint32_t fcap, fcode; /* element frames the parse follows, and what deeper is */
 } rxctx;
 static uint32_t rx_walk(rxctx *c, uint64_t *pp, uint32_t pc, uint32_t frames) {
   const plan_t *P = c->P;
@@ -923,9 +924,11 @@ static uint32_t rx_walk(rxctx *c, uint64_t *pp, uint32_t pc, uint32_t frames) {
         pc += 1 + op->arg2;
         break;
       }
-      /* the device index keeps XDRG_INDEX_FRAMES frames: deeper records are
-       * left to the caller's walk, as records past the window are */
-      if (v && frames == XDRG_INDEX_FRAMES) return RX_LONG;
+      /* the device index's windows follow XDRG_INDEX_FRAMES frames: deeper
+       * records are left to its long-record walk (or, with a window-sized
+       * maxlen, to the caller), as records past the window are; that walk
+       * follows XDRG_MAX_FRAMES (deeper: the decode's stack overflow) */
+      if (v && frames == c->fcap) return c->fcode;
       for (uint32_t i = 0; i < v; ++i) {
         uint32_t rc = rx_walk(c, &p, op->arg4, frames + 1);
         if (rc) return rc;
@@ -942,11 +945,16 @@ int xdro_index_records(const xdrg_op *ops, uint32_t nops, const uint32_t *table,
                        uint64_t *erec) {
   plan_t P = {ops, nops, table, 0, NULL};
   uint64_t p = 0, k = 0;
+  /* maxlen past one window (xdrg_index_records' rx_windows): the device
+   * walks records of any length and nesting, as this walk then does */
+  const int whole = maxlen > XDRG_INDEX_MAX_MSG;
+  const uint32_t fcap = whole ? XDRG_MAX_FRAMES : XDRG_INDEX_FRAMES, fcode = whole ? RX_BAD : RX_LONG;
+  if (whole) maxlen = UINT32_MAX;
   *count = UINT64_MAX;
   for (; k < n && p < len; ++k) {
     offsets[k] = p;
     const int capped = p + maxlen < len;
-    rxctx c = {&P, s, capped ? p + maxlen : len, capped ? RX_LONG : RX_BAD};
+    rxctx c = {&P, s, capped ? p + maxlen : len, capped ? RX_LONG : RX_BAD, fcap, fcode};
     uint64_t q = p;
     uint32_t rc = rx_walk(&c, &q, 0, 0);
     if (rc) {
@@ -968,7 +976,7 @@ int xdro_index_records(const xdrg_op *ops, uint32_t nops, const uint32_t *table,
   }
   /* n records and more bytes: the chain ends at record n unless it parses */
   const int capped = p + maxlen < len;
-  rxctx c = {&P, s, capped ? p + maxlen : len, capped ? RX_LONG : RX_BAD};
+  rxctx c = {&P, s, capped ? p + maxlen : len, capped ? RX_LONG : RX_BAD, fcap, fcode};
   uint64_t q = p;
   if (rx_walk(&c, &q, 0, 0)) *count = n;
   return 0;

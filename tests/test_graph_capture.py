@@ -87,6 +87,7 @@ def test_scratch_interpreter_refuses_capture(dev):
     dx, doffs = _dev(x, dev), _dev(offs.astype(np.int64), dev)
     back = torch.zeros(n * plan.stride, dtype=torch.uint8, device=dev)
     hout = torch.zeros(plan.decode_heap_bytes(x.size), dtype=torch.uint8, device=dev)
+    mar.decode(dx, n, doffs)  # warm: the plan's device tables are uploaded by its first launch
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):

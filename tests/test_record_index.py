@@ -278,6 +278,95 @@ def test_gpu_index_long_record(dev):
     assert np.array_equal(got, want) and cnt == wcnt
 
 
+BIGREC = None
+
+
+def bigrec_type():
+    """struct bigrec { unsigned hyper id; opaque blob<1048576>; string name<64>; }:
+    records from 20 bytes to past the index window."""
+    global BIGREC
+    if BIGREC is None:
+        from xdrpp_amd.xdr_types import Opaque, String, Struct, UHyper
+        BIGREC = Struct("bigrec", [("id", UHyper), ("blob", Opaque(1 << 20)), ("name", String(64))])
+    return BIGREC
+
+
+def long_records_stream(n, seed, every=29):
+    """bigrec records on the wire, mostly short (blob < 200 B), every
+    `every`-th (on average) with a 16-80 KiB blob: longer than one index
+    window (XDRG_INDEX_MAX_MSG), runs of them back to back as well."""
+    rng = np.random.default_rng(seed)
+    pad = lambda b: b + b"\0" * (-len(b) % 4)  # noqa: E731
+    out = []
+    for i in range(n):
+        long_ = rng.integers(0, every) == 0 or (i % 500 in (7, 8, 9))
+        blen = int(rng.integers(16 << 10, 80 << 10)) if long_ else int(rng.integers(0, 200))
+        blob = bytes(rng.integers(0, 256, blen, dtype=np.uint8))
+        name = bytes(rng.integers(97, 123, int(rng.integers(0, 65)), dtype=np.uint8))
+        out.append(int(i).to_bytes(8, "big") + len(blob).to_bytes(4, "big") + pad(blob)
+                   + len(name).to_bytes(4, "big") + pad(name))
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(w) for w in out])
+    return np.frombuffer(b"".join(out), dtype=np.uint8).copy(), offs, n
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("spec", [1, 0], ids=["generated", "interpreted"])
+def test_gpu_index_records_past_the_window(dev, spec):
+    """Records longer than the index window, on the device (rx_windows:
+    k_rx_long walks them, list-ranking windows index the rest): the same
+    offsets, count and error as the sequential walk of the restatement
+    (xdro_index_records with max_rec_len past one window), on good and
+    damaged streams; and decode() without offsets uses it (no host walk)."""
+    import torch
+    from xdrpp_amd import marshal as M
+    t = bigrec_type()
+    cp = compile_plan(t)
+    x, offs, n = long_records_stream(3000, 5)
+    assert int(np.diff(offs.astype(np.int64)).max()) > A.INDEX_MAX_MSG
+    want0, c0, rc0, _ = O.index_records(cp, x, n, A.MAX_MSG)
+    assert rc0 == 0 and np.array_equal(want0, offs)
+    mar = M.Marshaler(M.Plan(cp, {"specialize": spec}), dev)
+    for label, y, k in damaged(x, offs, n, 21) + damaged(x, offs, n, 22)[5:]:
+        want, wcnt, wrc, wer = O.index_records(cp, y, k, A.MAX_MSG)
+        got, gcnt, err = _gpu_index(mar, y, k, A.MAX_MSG, dev)
+        assert np.array_equal(got, want), label
+        assert gcnt == wcnt, label
+        assert (err.code if err else 0) == wrc, label
+    # a window-sized max_rec_len still hands such a stream back (INDEX_LONG)
+    got, gcnt, err = _gpu_index(mar, x, n, A.INDEX_MAX_MSG, dev)
+    want, wcnt, wrc, wer = O.index_records(cp, x, n, A.INDEX_MAX_MSG)
+    assert err is not None and err.code == A.ERR_INDEX_LONG == wrc and err.record == wer
+    dx = _dev(x, dev)
+    assert torch.equal(mar.index_records(dx, n).cpu(), torch.from_numpy(offs.view(np.int64)))
+    a, ha = mar.decode(dx, n, _dev(offs.view(np.int64), dev))
+    b, hb = mar.decode(dx, n)
+    assert torch.equal(a, b) and torch.equal(ha, hb)
+
+
+@pytest.mark.gpu
+def test_gpu_index_rp_list_full_size(dev, manifest):
+    """1M rpcbind rp__list records (xdrpp/rpcb_prot.x:32-37), 16 of them
+    500-node lists nested 500 deep and longer than the index window: the
+    device index of the encode's output is the encode's offsets, and the
+    encoded bytes are the reference's (manifest hash)."""
+    import hashlib
+    import torch
+    from xdrpp_amd import marshal as M
+    from xdrpp_amd import workloads as W
+    n = 1 << 20
+    nat, heap = W.rp_list(n)
+    mar = M.Marshaler(M.Plan(S.ALL["rp_list"]), dev)
+    r = mar.encode(_dev(nat, dev), n, _dev(heap, dev))
+    h = manifest["hashes"].get(f"rp_list_{n}")
+    if h:
+        assert hashlib.sha256(r.xdr.cpu().numpy().tobytes()).hexdigest() == h["xdr"]
+    sizes = torch.diff(r.offsets)
+    assert int(sizes.max()) > A.INDEX_MAX_MSG
+    offs = mar.index_records(r.xdr, n)
+    assert torch.equal(offs, r.offsets)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["recvar", "rpc", "vecrec", "containertest"])
 def test_gpu_index_full_size(dev, name):

@@ -220,11 +220,11 @@ def test_stream_full_grid_repeated(dev, manifest, name):
 
 @pytest.mark.parametrize("mode", ["stream", "walk_first"])
 def test_stream_large_wave_totals(dev, mode):
-    """Waves whose byte totals run to megabytes: 65,536 records of up to 64
-    KiB blobs (about 4 MiB a wave, 4.3 GB over 1,024 waves) through the
+    """Waves whose byte totals run to megabytes: 65,536 records of 64-68 KiB
+    blobs (about 4.2 MiB a wave, 4.4 GB over 1,024 waves) through the
     look-back (its block sums are split in 16-bit halves summed in u32 over
     up to 1,024 blocks a poll; a 24-bit split wrapped past 4 GiB a poll) and
-    through the scan.  Every blob points into one 64 KiB heap, so the bytes
+    through the scan.  Every blob points into one 128 KiB heap, so the bytes
     are checked by property: the record index equals the running sum of the
     records' sizes, the total matches, and sampled records equal the
     restatement's encoding of the same record."""
@@ -233,8 +233,8 @@ def test_stream_large_wave_totals(dev, mode):
     p = M.Plan(t, MODES[mode])
     n = 1 << 16
     rng = np.random.default_rng(5)
-    heap = rng.integers(0, 256, 1 << 16, dtype=np.uint8)
-    lens = (65536 - rng.integers(0, 4096, n)).astype(np.int64)
+    heap = rng.integers(0, 256, 1 << 17, dtype=np.uint8)
+    lens = (65536 + rng.integers(0, 4096, n)).astype(np.int64)
     nat = np.zeros((n, p.stride), dtype=np.uint8)
     nat[:, 0:8] = np.arange(n, dtype="<u8").view(np.uint8).reshape(n, 8)
     o = t.offsets["blob"]

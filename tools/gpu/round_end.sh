@@ -17,7 +17,7 @@ fi
 timeout -k 10 400 python3 -u bench.py > "$O/bench_rec128.log" 2>&1 || exit 1
 echo "[bench] rec128 done $(date +%T)"
 for s in numerics recvar rpc vecrec containertest rp_list; do
-  extra="--no-cpu-baseline"
+  extra=""
   [ "$s" = recvar ] && extra="$extra --msgs"
   [ "$s" = rpc ] && extra="$extra --msgs --rpc"
   timeout -k 10 300 python3 -u bench.py --schema "$s" $extra > "$O/bench_$s.log" 2>&1 || exit 1

@@ -49,8 +49,12 @@ def kernel_asm(schema, workdir):
                            src], cwd=workdir)
     s = open([os.path.join(workdir, f) for f in os.listdir(workdir)
               if f.startswith(schema) and f.endswith(".s") and "gfx" in f][0]).read()
-    i = s.index("xdrg_spec_encode:")
-    return s[i:s.index(".Lfunc_end", i)].splitlines()
+    out = {}
+    for k in ("xdrg_spec_encode", "xdrg_spec_encode_pre", "xdrg_spec_encode_lb"):
+        if f"\n{k}:" in s:
+            i = s.index(f"\n{k}:")
+            out[k] = s[i:s.index(".Lfunc_end", i)].splitlines()
+    return out
 
 
 def audit(lines):
@@ -61,7 +65,8 @@ def audit(lines):
     among them is safe (it waits for the asm loads too) but defeats the
     overlap; it is counted as not effective."""
     ins = [ln.strip() for ln in lines]
-    asm_loads = [k for k, t in enumerate(ins) if t.startswith("global_load_dwordx4") and k > 0
+    # the batch's asm loads: 16-byte chunks and (XDRG_ENC_ALIGN) the word after each
+    asm_loads = [k for k, t in enumerate(ins) if t.startswith("global_load_dword") and k > 0
                  and ins[k - 1] == ";;#ASMSTART"]
     if not asm_loads:
         return 0, 0  # no payload slots (vecrec: elements only) or XDRG_ENC_PIPE off
@@ -90,9 +95,18 @@ def audit(lines):
                 stores += 1
             elif regs(t) & dsts and not covered and not t.startswith("buffer_store"):
                 raise AssertionError(f"asm load destination touched before its wait: {t}")
-            # the only branch allowed: the skip of the wait when nothing was
-            # prefetched, after every store (the fall-through reaches the wait)
-            assert not t.startswith("s_cbranch") or stores > 0, f"branch among the loads and stores: {t}"
+            # branches allowed: the skip of the wait when nothing was
+            # prefetched, after every store (the fall-through reaches the
+            # wait), and a forward skip over straight-line code that is
+            # itself scanned here (an LDS read of one lane: its target is a
+            # label before the wait)
+            if t.startswith("s_cbranch") and stores == 0:
+                target = t.split()[-1]
+                rest = ins[j + 1:]
+                lab = next((q for q, x in enumerate(rest) if x.startswith(target + ":")), None)
+                waits = [q for q, x in enumerate(rest) if re.match(r"s_waitcnt vmcnt\(\d+\)", x)
+                         and rest[q - 1] == ";;#ASMSTART"]
+                assert lab is not None and waits and lab < waits[0], f"branch among the loads and stores: {t}"
         assert wait is not None and (covered or stores == wait), f"{stores} stores before vmcnt({wait})"
         checked += 1
         effective += not covered
@@ -103,8 +117,9 @@ def audit(lines):
 def main():
     for schema in sys.argv[1:] or ["recvar", "rpc", "vecrec"]:
         with tempfile.TemporaryDirectory() as d:
-            c, e = audit(kernel_asm(schema, d))
-            print(f"{schema}: {c} pipelined window sequence(s) safe, {e} with the loads overlapping the stores")
+            for k, lines in kernel_asm(schema, d).items():
+                c, e = audit(lines)
+                print(f"{schema} {k}: {c} pipelined window sequence(s) safe, {e} with the loads overlapping the stores")
 
 
 if __name__ == "__main__":

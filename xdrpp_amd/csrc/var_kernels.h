@@ -699,16 +699,29 @@ __device__ __forceinline__ void var_encode_body(
       b.nb[u] = live ? min(16u, ((d.len + 3u) & ~3u) - q16) : 0u;
       b.fast[u] = live && b.hs[u] + 16u <= heap_len;
     }
+    if constexpr (decltype(asm_tag)::value) {
+      // every lane loads (a lane with no fast chunk: the heap's first 16
+      // bytes -- the pipelined windows run only on heaps of 16 bytes or
+      // more), so the batch is straight-line code before the stores and
+      // their wait (tools/isa_audit.py).  (Dword-aligned loads of 16 bytes
+      // plus the next word joined with v_alignbyte, in place of these
+      // byte-misaligned ones: recvar 0.0998 vs 0.0957 ms, rpc 0.1385 vs
+      // 0.1361, slower; profiles/r05h/ab_align.log.)
 #pragma unroll
-    for (int u = 0; u < U; ++u)
-      if (b.fast[u]) {
-        if constexpr (decltype(asm_tag)::value)
-          asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(b.val[u]) : "v"(heap + b.hs[u]));
-        else if constexpr ((XDRG_ENC_NT & 1) != 0)
-          b.val[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(heap + b.hs[u]));
-        else
-          b.val[u] = ld16u(heap + b.hs[u]);
+      for (int u = 0; u < U; ++u) {
+        const uint8_t *pa = heap + (b.fast[u] ? b.hs[u] : 0ull);
+        asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(b.val[u]) : "v"(pa));
       }
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (b.fast[u]) {
+          if constexpr ((XDRG_ENC_NT & 1) != 0)
+            b.val[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(heap + b.hs[u]));
+          else
+            b.val[u] = ld16u(heap + b.hs[u]);
+        }
+    }
     if constexpr (decltype(asm_tag)::value) asm volatile("v_mov_b32 %0, 0" : "=v"(b.tok));
     __builtin_amdgcn_sched_barrier(0);
   };
@@ -750,7 +763,7 @@ __device__ __forceinline__ void var_encode_body(
   // stretch) is kept by lane 0 and written last, word by word
   constexpr uint32_t SW = CMAX / 1024u;
   constexpr bool kPipe = XDRG_ENC_PIPE && SW > 0 && (U == 2 || U == 4 || U == 8);  // vm_wait_after's shapes
-  const bool pipe = kPipe && C <= CMAX && wave_out + T <= cap;
+  const bool pipe = kPipe && C <= CMAX && wave_out + T <= cap && heap_len >= 16;
   bool pf = false;
   u32x4 head = u32x4{0u, 0u, 0u, 0u};
   for (uint32_t rd = 0; rd < rounds; ++rd) {

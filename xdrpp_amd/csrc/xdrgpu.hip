@@ -883,32 +883,62 @@ __device__ __forceinline__ uint32_t ix_mark(uint32_t raw, uint64_t w, uint64_t l
 // occupancy it costs outweighing L2-hit latency.)  The fast path
 // (rxs_walk_body) stages its segment: its walks are serial chains.
 
+// The frames of rx_len's element subroutines.  rx_reg_frames: the index's
+// own XDRG_INDEX_FRAMES in registers, st[0] the top frame, pushed and popped
+// by shifting (constant indices: no private memory, sub_kernels.h
+// reg_stack); a record nested deeper is RX_LONG, left to the long-record
+// walk (k_rx_long) like one past the window.  rx_slab_frames: that walk's
+// frames, XDRG_MAX_FRAMES of them in the index workspace; deeper is RX_BAD
+// (the decode reports the stack overflow).
+struct rx_frame { uint32_t left, entry, ret; };
+struct rx_reg_frames {
+  static constexpr uint32_t kFull = RX_LONG;
+  rx_frame st[XDRG_INDEX_FRAMES];
+  uint32_t fp = 0;
+  __device__ __forceinline__ bool full() const { return fp == XDRG_INDEX_FRAMES; }
+  __device__ __forceinline__ rx_frame &top() { return st[0]; }
+  __device__ __forceinline__ void push(const rx_frame &f) {
+#pragma unroll
+    for (int j = XDRG_INDEX_FRAMES - 1; j > 0; --j) st[j] = st[j - 1];
+    st[0] = f;
+    ++fp;
+  }
+  __device__ __forceinline__ void pop() {
+    --fp;
+#pragma unroll
+    for (int j = 0; j + 1 < XDRG_INDEX_FRAMES; ++j) st[j] = st[j + 1];
+  }
+};
+struct rx_slab_frames {
+  static constexpr uint32_t kFull = RX_BAD;
+  rx_frame *st;
+  uint32_t cap, fp = 0;
+  __device__ __forceinline__ bool full() const { return fp == cap; }
+  __device__ __forceinline__ rx_frame &top() { return st[fp - 1]; }
+  __device__ __forceinline__ void push(const rx_frame &f) { st[fp++] = f; }
+  __device__ __forceinline__ void pop() { --fp; }
+};
+
 // U: the position type (uint32_t for offsets into a staged stretch).
-template <class RD, class U = uint64_t>
+template <class RD, class U = uint64_t, class FS = rx_reg_frames>
 __device__ uint32_t rx_len(const xdrg_op *__restrict__ ops, const uint32_t *__restrict__ table,
-                           const RD &rd, U len, U a, uint32_t maxlen) {
+                           const RD &rd, U len, U a, uint32_t maxlen, FS st = FS{}) {
   const bool capped = static_cast<uint64_t>(a) + maxlen < len;
   const U lim = capped ? static_cast<U>(a + maxlen) : len;
   const uint32_t past = capped ? RX_LONG : RX_BAD;
-  struct frame { uint32_t left, entry, ret; };
-  // st[0] the top frame, pushed and popped by shifting: constant indices,
-  // registers, no private memory (sub_kernels.h reg_stack)
-  frame st[XDRG_INDEX_FRAMES];
-  uint32_t fp = 0, pc = 0;
+  uint32_t pc = 0;
   U p = a;
   for (;;) {
     const xdrg_op &op = ops[pc];
     switch (op.kind) {
     case XDRG_OP_END:
-      if (!fp) return static_cast<uint32_t>(p - a);
-      if (st[0].left) {
-        --st[0].left;
-        pc = st[0].entry;
+      if (!st.fp) return static_cast<uint32_t>(p - a);
+      if (st.top().left) {
+        --st.top().left;
+        pc = st.top().entry;
       } else {
-        pc = st[0].ret;
-        --fp;
-#pragma unroll
-        for (int j = 0; j + 1 < XDRG_INDEX_FRAMES; ++j) st[j] = st[j + 1];
+        pc = st.top().ret;
+        st.pop();
       }
       continue;
     case XDRG_OP_JUMP: pc = op.arg0; continue;
@@ -958,13 +988,8 @@ __device__ uint32_t rx_len(const xdrg_op *__restrict__ ops, const uint32_t *__re
       } else if (!v) {
         ++pc;
       } else {
-        // deeper records are left to the caller's walk, as records past
-        // the window are (include/xdrgpu.h xdrg_index_records)
-        if (fp == XDRG_INDEX_FRAMES) return RX_LONG;
-#pragma unroll
-        for (int j = XDRG_INDEX_FRAMES - 1; j > 0; --j) st[j] = st[j - 1];
-        st[0] = frame{v - 1, op.arg4, pc + 1};
-        ++fp;
+        if (st.full()) return FS::kFull;
+        st.push(rx_frame{v - 1, op.arg4, pc + 1});
         pc = op.arg4;
       }
       break;
@@ -1146,8 +1171,21 @@ __device__ void ix_final(const uint8_t *__restrict__ s, uint64_t len, uint32_t m
   if (m > max_msgs) return;
   offsets[m] = C.base + 4 * w;
   if (REC) {
-    if (4 * w < len && m < max_msgs && rx_len(rp.ops, rp.table, rx_global{s}, len, 4 * w, maxlen) == RX_LONG)
+    if (C.next) {
+      // a window of a longer stream (rx_windows): a record that parses in
+      // the whole stream -- longer than the window, nested deeper than its
+      // frames, or past the window's end -- is where the next round picks up
+      // (record n too: whether one parses after the n-th decides the count)
+      const uint64_t aw = C.base / 4 + w;
+      if (4 * aw < C.len && rx_len(rp.ops, rp.table, rx_global{C.s}, C.len, 4 * aw, maxlen) != RX_BAD) {
+        C.next[0] = aw;
+        C.next[1] = C.m0 + m;
+        return;
+      }
+    } else if (4 * w < len && m < max_msgs &&
+               rx_len(rp.ops, rp.table, rx_global{s}, len, 4 * w, maxlen) == RX_LONG) {
       report(err, m, kOpRecordLevel, XDRG_ERR_INDEX_LONG);
+    }
   } else {
     uint64_t nx = 0;
     uint32_t st = ix_mark(4 * w + 4 <= len ? ld32(s + 4 * w) : 0u, w, len, maxlen, &nx);
@@ -1340,6 +1378,59 @@ __global__ void k_ix_long(const uint8_t *__restrict__ s, uint64_t len, uint32_t 
     }
     ++m;
     w = nx;
+  }
+  next[0] = w;
+  next[1] = m;
+  next[2] = 0;
+}
+
+// Records too long for an index window (or nested deeper than its frames),
+// walked one after another from next = [word, record index] as
+// xdr_from_opaque's own walk would (marshal.h:299-306): while the record
+// there is such a record, at most `hops` of them, each parsed whole
+// (lengths, counts and discriminants; its frames in `slab`).  Leaves next at
+// the first record a window takes (next[2] = 1) or at the hop budget
+// (next[2] = 0); the end of the stream, the n-th record or a record that
+// does not parse ends the index here (next[0] = all ones; the record it
+// stops at gets its offset, k_rx_fill the rest).
+__global__ void k_rx_long(const uint8_t *__restrict__ s, uint64_t len, uint32_t maxlen, uint64_t n,
+                          const xdrg_op *__restrict__ ops, const uint32_t *__restrict__ table,
+                          uint64_t *__restrict__ offsets, unsigned long long *count, unsigned long long *next,
+                          rx_frame *slab, uint32_t hops) {
+  if (threadIdx.x || blockIdx.x) return;
+  uint64_t w = next[0], m = next[1];
+  for (uint32_t h = 0; h < hops; ++h) {
+    if (4 * w >= len) {  // the stream's end
+      offsets[m] = len;
+      atomicMin(count, m);
+      next[0] = ~0ull;
+      return;
+    }
+    if (m >= n) {  // n records and more bytes (the decode reports them): the
+      // count stays all ones if a record parses there (the chain goes on)
+      offsets[n] = 4 * w;
+      const uint32_t L = rx_len(ops, table, rx_global{s}, len, 4 * w, 0xffffffffu,
+                                rx_slab_frames{slab, XDRG_MAX_FRAMES, 0});
+      if (L == RX_BAD || L == RX_LONG) atomicMin(count, n);
+      next[0] = ~0ull;
+      return;
+    }
+    if (rx_len(ops, table, rx_global{s}, len, 4 * w, maxlen) != RX_LONG) {  // a window takes it
+      next[0] = w;
+      next[1] = m;
+      next[2] = 1;
+      return;
+    }
+    const uint32_t L = rx_len(ops, table, rx_global{s}, len, 4 * w, 0xffffffffu,
+                              rx_slab_frames{slab, XDRG_MAX_FRAMES, 0});
+    offsets[m] = 4 * w;
+    if (L == RX_BAD || L == RX_LONG) {  // a record the decode rejects
+      atomicMin(count, m);
+      next[0] = ~0ull;
+      return;
+    }
+    ++m;
+    w += L / 4;
   }
   next[0] = w;
   next[1] = m;
@@ -2278,7 +2369,7 @@ int run_index(const xdrg_plan *p, const dev_tables *T, const void *d_stream, uin
                                         max_msgs - C.m0, reinterpret_cast<unsigned long long *>(d_count), err,
                                         rp, C, skip);
   HIPCHK(hipGetLastError());
-  if (REC) {
+  if (REC && !C.next) {  // (rx_windows fills once, after its last round)
     k_rx_fill<<<static_cast<uint32_t>(std::min<uint64_t>((max_msgs + 256) / 256, 4096)), 256, 0, s>>>(
         d_offsets, reinterpret_cast<const unsigned long long *>(d_count), max_msgs, len, skip);
     HIPCHK(hipGetLastError());
@@ -2345,6 +2436,62 @@ int ix_windows(const uint8_t *s8, uint64_t len, uint32_t max_msg_len, uint64_t m
     const uint64_t covered = 4 * h[0] - start;
     window = covered < wl ? std::max<uint64_t>(2 * covered, kIxMinWindow) : 2 * wl;
   }
+}
+
+// Record index of a stream with records longer than one index window
+// (max_rec_len > XDRG_INDEX_MAX_MSG) or nested deeper than its frames: the
+// rounds of ix_windows over records.  k_rx_long walks such records from
+// where the chain stopped; a list-ranking window (run_index over records
+// up to XDRG_INDEX_MAX_MSG bytes) indexes the stream from the next record
+// until its chain reaches one again or the window's end.  The speculative
+// walk tries the whole stream first.
+int rx_windows(const xdrg_plan *p, const dev_tables *T, const uint8_t *s8, uint64_t len, uint64_t n,
+               uint64_t *d_offsets, uint64_t *d_count, void *d_ws, size_t ws_bytes, xdrg_status *d_status,
+               hipStream_t s) {
+  const size_t need = xdrg_index_workspace_size(len, XDRG_INDEX_MAX_MSG + 4u);
+  if (!d_ws || ws_bytes < need) return XDRG_ESPACE;
+  {  // the rounds wait on the stream: a stream being captured cannot be waited on
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return XDRG_EUNSUPPORTED;
+  }
+  {
+    const int rc = run_index<true>(p, T, s8, len, XDRG_INDEX_MAX_MSG, n, d_offsets, d_count, d_ws, ws_bytes,
+                                   d_status, s, ix_cont{}, true);
+    if (rc != kIxNotHeld) return rc;
+  }
+  const ix_layout L0 = ix_plan(len, XDRG_INDEX_MAX_MSG);
+  auto *next = reinterpret_cast<unsigned long long *>(static_cast<char *>(d_ws) + L0.total);
+  auto *slab = reinterpret_cast<rx_frame *>(static_cast<char *>(d_ws) + L0.total + kIxNextBytes);
+  unsigned long long *count = reinterpret_cast<unsigned long long *>(d_count);
+  HIPCHK(static_cast<hipError_t>(xdrg::fill32(d_count, 0xffffffffu, 2, s)));
+  HIPCHK(static_cast<hipError_t>(xdrg::fill32(next, 0u, 6, s)));  // the chain starts at word 0, record 0
+  unsigned long long h[3] = {0, 0, 0};
+  uint64_t window = len;
+  for (;;) {
+    k_rx_long<<<1, 64, 0, s>>>(s8, len, XDRG_INDEX_MAX_MSG, n, T->d_ops, T->d_table, d_offsets, count, next,
+                               slab, 256u);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(h, next, 24, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (h[0] == ~0ull) break;
+    if (!h[2]) continue;  // the hop budget ran out among long records
+    const uint64_t start = 4 * h[0], m0 = h[1];
+    const uint64_t wl = std::min<uint64_t>(window, len - start);
+    HIPCHK(static_cast<hipError_t>(xdrg::fill32(next, 0xffffffffu, 2, s)));
+    const ix_cont C{m0, start, s8, len, XDRG_INDEX_MAX_MSG, next};
+    if (int rc = run_index<true>(p, T, s8 + start, wl, XDRG_INDEX_MAX_MSG, n, d_offsets, d_count, d_ws, ws_bytes,
+                                 d_status, s, C))
+      return rc;
+    HIPCHK(hipMemcpyAsync(h, next, 16, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (h[0] == ~0ull) break;
+    const uint64_t covered = 4 * h[0] - start;
+    window = covered < wl ? std::max<uint64_t>(2 * covered, kIxMinWindow) : 2 * wl;
+  }
+  k_rx_fill<<<static_cast<uint32_t>(std::min<uint64_t>((n + 256) / 256, 4096)), 256, 0, s>>>(
+      d_offsets, reinterpret_cast<const unsigned long long *>(d_count), n, len, nullptr);
+  HIPCHK(hipGetLastError());
+  return XDRG_OK;
 }
 }  // namespace
 
@@ -2702,7 +2849,8 @@ int xdrg_encode_sized(const xdrg_plan *p, const void *d_native, uint64_t n, cons
 size_t xdrg_index_workspace_size(uint64_t len, uint32_t max_msg_len) {
   if (max_msg_len > XDRG_MAX_MSG) return 0;
   if (max_msg_len <= XDRG_INDEX_MAX_MSG) return ix_plan(len, max_msg_len).total;
-  return ix_plan(len, XDRG_INDEX_MAX_MSG).total + kIxNextBytes;  // + ix_windows' continuation
+  // + the windows' continuation and the long-record walk's frames (rx_windows)
+  return ix_plan(len, XDRG_INDEX_MAX_MSG).total + kIxNextBytes + sizeof(rx_frame) * size_t(XDRG_MAX_FRAMES);
 }
 
 int xdrg_index_msgs(const void *d_stream, uint64_t len, uint32_t max_msg_len, uint64_t max_msgs,
@@ -2725,12 +2873,15 @@ int xdrg_index_records(const xdrg_plan *p, const void *d_xdr, uint64_t len, uint
                        uint32_t max_rec_len, uint64_t *d_offsets, uint64_t *d_count, void *d_ws,
                        size_t ws_bytes, xdrg_status *d_status, void *stream) {
   if (!p || !d_offsets || !d_count || !d_status || (len && !d_xdr)) return XDRG_EINVAL;
-  if (max_rec_len > XDRG_INDEX_MAX_MSG) return XDRG_EUNSUPPORTED;
+  if (max_rec_len > XDRG_MAX_MSG) return XDRG_EINVAL;
   if ((d_xdr && !aligned(d_xdr, 4)) || !aligned(d_offsets, 8) || !aligned(d_count, 8)) return XDRG_EALIGN;
   if (n >= (1ull << 40)) return XDRG_EUNSUPPORTED;
   if (p->min_record_bytes < 4) return XDRG_EUNSUPPORTED;  // the chain must advance
   const dev_tables *T = nullptr;
   if (int rc = plan_upload(p, &T)) return rc;
+  if (max_rec_len > XDRG_INDEX_MAX_MSG)
+    return rx_windows(p, T, static_cast<const uint8_t *>(d_xdr), len, n, d_offsets, d_count, d_ws, ws_bytes,
+                      d_status, static_cast<hipStream_t>(stream));
   return run_index<true>(p, T, d_xdr, len, max_rec_len, n, d_offsets, d_count, d_ws, ws_bytes, d_status,
                          static_cast<hipStream_t>(stream));
 }

@@ -301,12 +301,14 @@ class Marshaler:
 
     def index_records(self, xdr: torch.Tensor, n: int, max_rec_len: int | None = None) -> torch.Tensor:
         """Record index of n records concatenated in `xdr`, on the device
-        (xdrg_index_records): int64 offsets[n + 1] for decode.  Raises
-        XdrRuntimeError (XDRG_ERR_INDEX_LONG) when a record is longer than
-        the index window (max_rec_len, default the plan's largest record
-        up to XDRG_INDEX_MAX_MSG)."""
+        (xdrg_index_records): int64 offsets[n + 1] for decode.  max_rec_len
+        (default: the plan's largest record, at most XDRG_MAX_MSG): records
+        longer than the index window (XDRG_INDEX_MAX_MSG) or nested deeper
+        than its frames are walked on the device between list-ranking
+        windows; with max_rec_len at most the window, such a record raises
+        XdrRuntimeError (XDRG_ERR_INDEX_LONG)."""
         if max_rec_len is None:
-            max_rec_len = min(self.plan.max_record_bytes, A.INDEX_MAX_MSG)
+            max_rec_len = max(min(self.plan.max_record_bytes, A.MAX_MSG), 16)
         L = A.lib()
         total = xdr.numel()
         ws = torch.empty(max(L.xdrg_index_workspace_size(total, max_rec_len), 16), dtype=torch.uint8,
@@ -325,18 +327,10 @@ class Marshaler:
                stack_limit: int = A.DEFAULT_STACK_LIMIT):
         """= xdr_from_opaque(bytes, r0, ..., rn-1) (marshal.h:299-306).
         Var plans without `offsets` index the records on the device first
-        (index_records); a stream the device index hands back (a record
-        longer than its window, or nested deeper than its frames) is walked
-        on the host instead, as the C++ layer does.  Returns (native uint8
-        tensor [n*stride], heap uint8 tensor or None)."""
+        (index_records: records of any length and nesting).  Returns (native
+        uint8 tensor [n*stride], heap uint8 tensor or None)."""
         if offsets is None and not self.plan.is_fixed:
-            try:
-                offsets = self.index_records(xdr, n)
-            except XdrRuntimeError as e:
-                if e.code != A.ERR_INDEX_LONG:
-                    raise
-                offs = host_index_records(self.plan.cp, xdr.cpu().numpy(), n)
-                offsets = torch.from_numpy(offs.view(np.int64)).to(self.device)
+            offsets = self.index_records(xdr, n)
         s = _stream()
         native = torch.zeros(max(n, 1) * self.plan.stride, dtype=torch.uint8, device=self.device)
         heap = None
