@@ -54,3 +54,17 @@ def test_bench_two_ranks(schema):
         assert g["index_sha256"] == hashlib.sha256(woffs.view(np.int64).tobytes()).hexdigest()
     X_all = len(want)
     assert line["value"] == pytest.approx(2 * X_all / 2**30 / (line["ms_per_step"] * 1e-3), rel=0.01, abs=0.01)
+
+
+@pytest.mark.parametrize("schema", ["rp_list", "containertest", "recvar", "rpc"])
+def test_port_baseline_runs(schema):
+    """bench.py's cpu_baseline port leg (oracle/cpu_bench.c) on a small
+    batch of every variable-length bench schema, two threads: the decode of
+    plans with element arrays (rp_list, containertest) gets a heap of its
+    own per thread and decodes what the encode wrote."""
+    sys.path.insert(0, ROOT)
+    import bench
+    n = 3000
+    nat, heap = W.GENERATORS[schema](n)
+    r = bench._port_baseline(schema, n, 2, 1, nat, heap)
+    assert r["encode_gib_s"] > 0 and r["decode_gib_s"] > 0 and r["threads"] == 2
