@@ -561,9 +561,12 @@ def plain_stream_leg(schema, engine, dec_ms, reps=10):
     for label, fast in (("index", 1), ("index_list_ranking", 0)):
         plan = M.Plan(S.ALL[schema], {"index_fast": fast})
         mar = M.Marshaler(plan, dev)
-        maxlen = min(plan.max_record_bytes, A.INDEX_MAX_MSG)
+        # records past one index window (rp_list's 500-node lists) take the
+        # windowed index (include/xdrgpu.h xdrg_index_records)
+        maxlen = max(min(plan.max_record_bytes, A.MAX_MSG), 16)
         total = xdr.numel()
         ws = torch.empty(max(L.xdrg_index_workspace_size(total, maxlen), 16), dtype=torch.uint8, device=dev)
+        flag_at = L.xdrg_index_workspace_size(total, min(maxlen, A.INDEX_MAX_MSG)) - 256
         offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
         cnt = torch.empty(1, dtype=torch.int64, device=dev)
         mar.status.init(s)
@@ -586,7 +589,8 @@ def plain_stream_leg(schema, engine, dec_ms, reps=10):
         res[label + "_ms"] = round(float(np.mean(t)), 4)
         res[label + "_ok"] = ok
         if fast:
-            res["walk_held"] = int(ws[-256:][:4].cpu().numpy().view(np.uint32)[0]) == 1
+            res["walk_held"] = int(ws[flag_at:flag_at + 4].cpu().numpy().view(np.uint32)[0]) == 1
+            res["windowed"] = maxlen > A.INDEX_MAX_MSG and not res["walk_held"]
     res["decode_ms"] = dec_ms
     res["index_over_decode"] = round(res["index_ms"] / dec_ms, 3)
     res["protocol"] = f"HIP events around each xdrg_index_records call, mean of {reps}; decode: the headline's"

@@ -134,7 +134,7 @@ enum xdrg_op_flags {
  * marshaling_stack_limit only: a walk keeps XDRG_SUB_FRAMES element frames
  * in registers, and records nested deeper are walked again by deep passes
  * whose frames live in the caller's workspace
- * (xdrg_deep_workspace_size: about 128 MiB + 8 bytes per record for a plan
+ * (xdrg_deep_workspace_size: about 192 MiB + 8 bytes per record for a plan
  * that can nest that deep, 0 for any other).  A record that needs more than XDRG_MAX_FRAMES nested element
  * frames raises the stack-overflow error at the VECTOR op that would open
  * the next one; the reference's own recursion ends far earlier, in a
@@ -377,7 +377,7 @@ size_t xdrg_workspace_size(const xdrg_plan *plan, uint64_t n);
 /* Workspace bytes decode, decode_msgs, serial_sizes and record_depths need
  * for n records: 0 except for plans whose element subroutines can nest past
  * XDRG_SUB_FRAMES, whose deep passes keep their lists of deferred records
- * and their frame slabs there (about 128 MiB + 8 bytes per record; 256-byte
+ * and their frame slabs there (about 192 MiB + 8 bytes per record; 256-byte
  * aligned).  The memory is the caller's: no call allocates, locks or keeps
  * state between calls, so calls on different streams with different
  * workspaces run side by side, and a captured graph of them holds kernels
@@ -557,8 +557,10 @@ size_t xdrg_index_workspace_size(uint64_t len, uint32_t max_msg_len);
  * (damaged streams, trailing or missing records, long records, or a guess
  * that missed: XDRG_OPT_INDEX_FAST = 0 forces this) every word position is
  * parsed as a possible record start and the chain of record ends from byte
- * 0 is ranked as for xdrg_index_msgs.  The first u32 of the workspace's
- * last 256 bytes says which ran (1: the speculative walk).  By default
+ * 0 is ranked as for xdrg_index_msgs.  The first u32 of the 256 bytes
+ * that end at xdrg_index_workspace_size(len, min(max_rec_len,
+ * XDRG_INDEX_MAX_MSG)) -- the workspace's last 256 bytes when max_rec_len
+ * <= XDRG_INDEX_MAX_MSG -- says which ran (1: the speculative walk).  By default
  * (XDRG_OPT_INDEX_FAST) the call waits on the stream once, for the walk's
  * verdict (not on a stream being captured into a graph: there it stays
  * asynchronous, as with XDRG_OPT_INDEX_FAST = 2).  Writes
@@ -568,11 +570,17 @@ size_t xdrg_index_workspace_size(uint64_t len, uint32_t max_msg_len);
  * so xdrg_decode reports the reference's error for record k; fewer than n
  * records end at len likewise, more leave off[n] < len (trailing bytes).
  * *d_count = the records the chain holds before it ends (all-ones when
- * it goes past record n).  A record longer than max_rec_len (<= XDRG_INDEX_MAX_MSG)
- * is reported as XDRG_ERR_INDEX_LONG at its index: the caller indexes that
- * stream another way (the C++ layer walks it on the host).  Plans whose
- * records can be empty are XDRG_EUNSUPPORTED.  Workspace:
- * xdrg_index_workspace_size(len, max_rec_len).
+ * it goes past record n).  max_rec_len <= XDRG_MAX_MSG.  Past
+ * XDRG_INDEX_MAX_MSG, when the speculative walk misses, the stream is
+ * indexed in rounds: one wave walks the records longer than a window
+ * (lengths, counts and discriminants, its element frames in the workspace)
+ * from where the chain stopped, then a list-ranking window indexes the
+ * records after them up to the next long one -- the call waits on the
+ * stream every round, so it is XDRG_EUNSUPPORTED on a stream being
+ * captured.  A record longer than max_rec_len is reported as
+ * XDRG_ERR_INDEX_LONG at its index.  Plans whose records can be empty are
+ * XDRG_EUNSUPPORTED.  Workspace: xdrg_index_workspace_size(len,
+ * max_rec_len).
  */
 int xdrg_index_records(const xdrg_plan *plan, const void *d_xdr, uint64_t len, uint64_t n,
                        uint32_t max_rec_len, uint64_t *d_offsets, uint64_t *d_count,

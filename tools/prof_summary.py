@@ -24,10 +24,19 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def counters(d):
+    """{(kernel, counter): [value per launch]} over the launches of each
+    kernel at its largest grid: a frame walk's main pass, not the deep
+    passes launched after it on a few workgroups (their counts would pull
+    the mean per launch down by the launches per step)."""
     f = [os.path.join(r, x) for r, _, fs in os.walk(d) for x in fs if x.endswith("counter_collection.csv")][0]
+    rows = list(csv.DictReader(open(f)))
+    grid = collections.defaultdict(int)
+    for r in rows:
+        grid[r["Kernel_Name"]] = max(grid[r["Kernel_Name"]], int(r["Grid_Size"]))
     agg = collections.defaultdict(list)
-    for r in csv.DictReader(open(f)):
-        agg[(r["Kernel_Name"], r["Counter_Name"])].append(float(r["Counter_Value"]))
+    for r in rows:
+        if int(r["Grid_Size"]) == grid[r["Kernel_Name"]]:
+            agg[(r["Kernel_Name"], r["Counter_Name"])].append(float(r["Counter_Value"]))
     return agg
 
 
@@ -60,11 +69,19 @@ def main():
                 traffic[f"{sch}:{k}"] = e["hbm_bytes_per_launch"]
         allpmc[sch] = out
     json.dump(allpmc, open(os.path.join(prof, f"{tag}_pmc.json"), "w"), indent=1)
+    # merged into the table: the schemas not profiled here keep their rows
+    tp = os.path.join(prof, "pmc_traffic.json")
+    old = json.load(open(tp)) if os.path.exists(tp) else {}
+    rows = {k: v for k, v in old.get("hbm_bytes_per_launch", {}).items() if k.split(":")[0] not in schemas}
+    rows.update(traffic)
+    srcs = {k: v for k, v in old.get("sources", {}).items() if k not in schemas}
+    srcs.update({s: f"profiles/{tag}_pmc.json" for s in schemas})
     json.dump({"records": 1 << 20,
-               "hbm_bytes_per_launch": traffic,
-               "source": f"profiles/{tag}_pmc.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes "
-                         "of bench.py --schema <s>; 2*FETCH_SIZE+WRITE_SIZE, gfx950 correction)"},
-              open(os.path.join(prof, "pmc_traffic.json"), "w"), indent=1)
+               "hbm_bytes_per_launch": dict(sorted(rows.items())),
+               "sources": dict(sorted(srcs.items())),
+               "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py --schema <s> "
+                         "(per schema: sources); 2*FETCH_SIZE+WRITE_SIZE, gfx950 correction"},
+              open(tp, "w"), indent=1)
     print(json.dumps(allpmc, indent=1)[:4000])
 
 

@@ -57,13 +57,23 @@ constexpr uint32_t kSubFrames = XDRG_SUB_FRAMES;  // private frames of the main 
 constexpr uint32_t kReported = 0x100;  // decode: the element walk reported the error
 
 // One open container: its current element (heap byte offset), the elements
-// after it and the VECTOR op (stride, body pc, return pc and depth come
-// from the op).
+// after it, the VECTOR op (stride and body pc come from the op) and where
+// the walk goes on when the container closes (vd: op in the low 16 bits,
+// return pc in the high 16; plans have fewer than kOpRecordLevel ops), and
+// the levels its pop gives back (the op's depth, plus those of the frames
+// it replaced -- sub_tail).
 struct sub_frame {
   uint64_t eb;
   uint32_t left;
-  uint32_t vpc;
+  uint32_t vd;
+  uint32_t dsum;
+  __device__ __forceinline__ uint32_t vpc() const { return vd & 0xffffu; }
+  __device__ __forceinline__ uint32_t ret() const { return vd >> 16; }
 };
+__device__ __forceinline__ sub_frame make_frame(uint64_t eb, uint32_t left, uint32_t vpc, uint32_t ret,
+                                                uint32_t dsum) {
+  return sub_frame{eb, left, vpc | (ret << 16), dsum};
+}
 
 // The walks touch the top frame only (and, after an error in the decode,
 // every open frame once): top / push / pop / each with fp = the frames open.
@@ -97,6 +107,7 @@ struct reg_stack {
       if (j < fp) fn(fp - 1u - j, f[j], f[j + 1 < kSubFrames ? j + 1 : j]);
   }
   __device__ __forceinline__ uint32_t cap() const { return kSubFrames; }
+  static constexpr bool kRegs = true;
 };
 // Deep passes: `n` frames per lane in the caller's workspace.
 struct slab_stack {
@@ -109,7 +120,39 @@ struct slab_stack {
     for (uint32_t k = 0; k < fp; ++k) fn(k, f[k], f[k ? k - 1 : 0]);
   }
   __device__ __forceinline__ uint32_t cap() const { return n; }
+  static constexpr bool kRegs = false;
 };
+
+// Tail containers.  A container of element subroutines whose elements are
+// the last thing the element enclosing it does (the op after it, through
+// jumps, is its body's END), opened while that element is its container's
+// last one: when it closes, so does the frame below.  Its frame replaces
+// that one instead of going on top, and takes over its return pc -- a
+// linked list (rp__list's rpcb_next, xdrpp/rpcb_prot.x:34; test_recursive's
+// nextvec, tests/xdrtest.x:29-33) walks in one frame however long it is,
+// in the main pass.  The depth levels of the replaced frames stay counted
+// (dsum) and are given back at the pop.
+__device__ __forceinline__ bool sub_tail(const xdrg_op *__restrict__ ops, uint32_t pc) {
+  uint32_t q = pc + 1;
+  while (ops[q].kind == XDRG_OP_JUMP) q = ops[q].arg0;
+  return ops[q].kind == XDRG_OP_END;
+}
+// Open the container at pc (count cnt >= 1, first element eb): on top of
+// the stack, or in place of the top frame (sub_tail; allow_tail).  Returns
+// false when the stack is full; sets *tail when it replaced a frame.
+template <class ST>
+__device__ __forceinline__ bool sub_open(const xdrg_op *__restrict__ ops, ST &st, uint32_t &fp, uint32_t pc,
+                                         uint32_t depth, uint64_t eb, uint32_t cnt, bool allow_tail, bool *tail) {
+  if (allow_tail && fp && st.top(fp).left == 0u && sub_tail(ops, pc)) {
+    sub_frame &t = st.top(fp);
+    t = make_frame(eb, cnt - 1u, pc, t.ret(), t.dsum + depth);
+    *tail = true;
+    return true;
+  }
+  if (fp == st.cap()) return false;
+  st.push(fp++, make_frame(eb, cnt - 1u, pc, pc + 1u, depth));
+  return true;
+}
 
 // The pass a launch runs (see the top of the file).
 struct sub_pass {
@@ -128,6 +171,7 @@ enum : int { kWalkCont = -1, kWalkOk = 0, kWalkErr = 1, kWalkFull = 2 };
 
 // The interpreted op policy: the op from the plan table (LDS).
 struct rt_ops {
+  static constexpr uint32_t kImgWords = 0;  // field offsets at run time: no element image
   template <class F>
   __device__ __forceinline__ static int visit(const xdrg_op *__restrict__ ops, uint32_t &pc, F &&step) {
     return step(ops[pc]);
@@ -153,24 +197,70 @@ __device__ __forceinline__ void sub_full(const sub_pass &P, uint64_t r, uint32_t
 
 // The native object a lane's walk is in: its record (frame 0, `len` bytes)
 // or an element in the heap.  Heap bytes at or past heap_len read as 0.
-struct sub_src {
+// IW > 0 (generated walks, whose field offsets are constants): the current
+// element's first 4*IW bytes in registers, loaded whole each time the walk
+// enters an element (refresh) -- one round trip per element where the
+// field-by-field reads made one per field along rp__list's chain.
+template <uint32_t IW>
+struct sub_src_t {
   const uint8_t *nat;
   uint32_t len;
   const uint8_t *heap;
   uint64_t heap_len;
   uint64_t eb;
   bool in_heap;
+  uint32_t img[IW ? IW : 1];
+  __device__ __forceinline__ void refresh() {
+    if constexpr (IW > 0) {
+      if (!in_heap) return;
+      if (!(eb & 3u) && eb + 4u * IW <= heap_len) {
+#pragma unroll
+        for (uint32_t q = 0; q + 4 <= IW; q += 4) {
+          const u32x4 t = ld16u(heap + eb + 4u * q);
+          img[q] = t.x;
+          img[q + 1] = t.y;
+          img[q + 2] = t.z;
+          img[q + 3] = t.w;
+        }
+#pragma unroll
+        for (uint32_t q = IW & ~3u; q < IW; ++q) img[q] = ld32(heap + eb + 4u * q);
+      } else {
+#pragma unroll
+        for (uint32_t q = 0; q < IW; ++q) img[q] = hword(eb + 4u * q);
+      }
+    }
+  }
+  __device__ __forceinline__ bool cached(uint32_t off) const { return IW > 0 && in_heap && off / 4u < IW; }
   // a heap word at any byte offset
   __device__ __forceinline__ uint32_t hword(uint64_t off) const { return unaligned_word(heap, heap_len, off); }
+  // the four heap words at any byte offset, their loads issued together
+  __device__ __forceinline__ void hwords4(uint64_t off, uint32_t (&w)[4]) const {
+    const uint64_t a = off & ~3ull;
+    const uint32_t sh = static_cast<uint32_t>(off & 3u);
+    if (a + 20 <= heap_len) {
+      const u32x4 t = ld16u(heap + a);
+      const uint32_t t4 = sh ? ld32(heap + a + 16) : 0u;
+      w[0] = __builtin_amdgcn_alignbyte(t.y, t.x, sh);
+      w[1] = __builtin_amdgcn_alignbyte(t.z, t.y, sh);
+      w[2] = __builtin_amdgcn_alignbyte(t.w, t.z, sh);
+      w[3] = __builtin_amdgcn_alignbyte(t4, t.w, sh);
+    } else {
+#pragma unroll
+      for (uint32_t j = 0; j < 4; ++j) w[j] = hword(off + 4u * j);
+    }
+  }
   // a naturally aligned field word
   __device__ __forceinline__ uint32_t w(uint32_t off) const {
+    if (cached(off)) return img[off / 4u];
     return in_heap ? hword(eb + off) : ld32(nat + off);
   }
   // a word at any byte offset (opaque[n] fields)
   __device__ __forceinline__ uint32_t wu(uint32_t off) const {
+    if (!(off & 3u) && cached(off)) return img[off / 4u];
     return in_heap ? hword(eb + off) : unaligned_word(nat, len, off);
   }
   __device__ __forceinline__ uint32_t b(uint32_t off) const {
+    if (cached(off)) return (img[off / 4u] >> (8u * (off & 3u))) & 0xffu;
     return in_heap ? (hword(eb + off) & 0xffu) : nat[off];
   }
   __device__ __forceinline__ uint64_t w64(uint32_t off) const {
@@ -186,7 +276,7 @@ __device__ __forceinline__ bool sub_next(const xdrg_op *__restrict__ ops, ST &st
                                          uint32_t &dbase, uint64_t &eb, bool &in_heap) {
   if (!fp) return false;
   sub_frame &f = st.top(fp);
-  const xdrg_op &v = ops[f.vpc];
+  const xdrg_op &v = ops[f.vpc()];
   if (f.left) {
     --f.left;
     f.eb += v.arg1;
@@ -194,8 +284,8 @@ __device__ __forceinline__ bool sub_next(const xdrg_op *__restrict__ ops, ST &st
     pc = v.arg4;
     return true;
   }
-  pc = f.vpc + 1;
-  dbase -= v.depth;
+  pc = f.ret();
+  dbase -= f.dsum;
   st.pop(fp);
   if (--fp) eb = st.top(fp).eb;
   else in_heap = false;
@@ -226,11 +316,16 @@ __device__ __forceinline__ void sub_records(const sub_pass &P, uint64_t n, F &&w
 // discriminant or a record of 2^31 bytes or more; kWalkFull (op in bad_op):
 // the stack ran out.
 template <bool DEPTH, class OPS, class ST>
-__device__ int sub_size(const xdrg_op *__restrict__ ops, const uint32_t *__restrict__ table, sub_src src,
+__device__ int sub_size(const xdrg_op *__restrict__ ops, const uint32_t *__restrict__ table,
+                        sub_src_t<OPS::kImgWords> src,
                         uint64_t &s, uint32_t &dmax, uint32_t &bad_op, uint32_t &code, ST &st) {
   uint32_t fp = 0, pc = 0, dbase = 0;
-  auto step = [&](const auto &op) -> int {
-    if (op.kind == XDRG_OP_END) return sub_next(ops, st, fp, pc, dbase, src.eb, src.in_heap) ? kWalkCont : kWalkOk;
+  auto step = [&](const auto &op) __attribute__((always_inline)) -> int {
+    if (op.kind == XDRG_OP_END) {
+      if (!sub_next(ops, st, fp, pc, dbase, src.eb, src.in_heap)) return kWalkOk;
+      src.refresh();
+      return kWalkCont;
+    }
     if (op.kind == XDRG_OP_JUMP) { pc = op.arg0; return kWalkCont; }
     if (DEPTH) dmax = max(dmax, dbase + op.depth);
     switch (op.kind) {
@@ -258,11 +353,12 @@ __device__ int sub_size(const xdrg_op *__restrict__ ops, const uint32_t *__restr
         break;
       }
       if (!cnt) { ++pc; break; }
-      if (fp == st.cap()) { bad_op = pc; return kWalkFull; }
+      bool tail = false;
+      if (!sub_open(ops, st, fp, pc, op.depth, src.w64(op.noff), cnt, true, &tail)) { bad_op = pc; return kWalkFull; }
       dbase += op.depth;
-      st.push(fp++, sub_frame{src.w64(op.noff), cnt - 1, pc});
       src.eb = st.top(fp).eb;
       src.in_heap = true;
+      src.refresh();
       pc = op.arg4;
       break;
     }
@@ -310,7 +406,7 @@ __device__ __forceinline__ void sub_size_kernel(XDRG_SUB_SIZE_PARAMS) {
   load_ops(sops, ops, nops);
   uint32_t size = 0;  // main pass: this lane's contribution to its block sum
   sub_records(P, n, [&](uint64_t r, auto &st) {
-    const sub_src src{native + r * stride, stride, heap, heap_len, 0, false};
+    const sub_src_t<OPS::kImgWords> src{native + r * stride, stride, heap, heap_len, 0, false, {}};
     uint64_t s = mark;
     uint32_t dmax = 0, bad_op = 0, code = 0, sz = kSizeErr;
     const int rc = sub_size<DEPTH, OPS>(sops, table, src, s, dmax, bad_op, code, st);
@@ -387,7 +483,8 @@ struct line_writer {
 // budget before every field (marshal.h:104-108, :129-136).  Errors are
 // reported; kWalkFull when the stack ran out (op in *full_op).
 template <class OPS, class ST>
-__device__ int sub_encode_rec(const xdrg_op *__restrict__ sops, const uint32_t *__restrict__ table, sub_src src,
+__device__ __forceinline__ int sub_encode_rec(const xdrg_op *__restrict__ sops, const uint32_t *__restrict__ table,
+                              sub_src_t<OPS::kImgWords> src,
                               line_writer &lw, uint64_t cap, uint64_t off, uint32_t sz, uint32_t mark,
                               uint32_t stack_limit, uint64_t r, unsigned long long *err, uint32_t *full_op,
                               ST &st) {
@@ -400,8 +497,12 @@ __device__ int sub_encode_rec(const xdrg_op *__restrict__ sops, const uint32_t *
     pos += 4;
   }
   uint32_t fp = 0, pc = 0, dbase = 0;
-  auto step = [&](const auto &op) -> int {
-    if (op.kind == XDRG_OP_END) return sub_next(sops, st, fp, pc, dbase, src.eb, src.in_heap) ? kWalkCont : kWalkOk;
+  auto step = [&](const auto &op) __attribute__((always_inline)) -> int {
+    if (op.kind == XDRG_OP_END) {
+      if (!sub_next(sops, st, fp, pc, dbase, src.eb, src.in_heap)) return kWalkOk;
+      src.refresh();
+      return kWalkCont;
+    }
     if (op.kind == XDRG_OP_JUMP) { pc = op.arg0; return kWalkCont; }
     if (dbase + op.depth > stack_limit) { report(err, r, pc, XDRG_ERR_STACK_PUT); return kWalkErr; }
     uint64_t need = 4;
@@ -438,10 +539,16 @@ __device__ int sub_encode_rec(const xdrg_op *__restrict__ sops, const uint32_t *
       const uint64_t hoff = src.w64(op.noff);
       const uint32_t nw = (len + 3u) >> 2;
       lw.put(p0, bswap32(len));
-      for (uint32_t k = 0; k < nw; ++k) {
-        uint32_t w = src.hword(hoff + 4ull * k);
-        if (4 * k + 4 > len) w &= keep_mask(len - 4 * k);
-        lw.put(p0 + 4ull + 4ull * k, w);
+      for (uint32_t k = 0; k < nw; k += 4) {  // four words' loads at a time
+        uint32_t w[4];
+        src.hwords4(hoff + 4ull * k, w);
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+          if (k + j >= nw) break;
+          uint32_t x = w[j];
+          if (4 * (k + j) + 4 > len) x &= keep_mask(len - 4 * (k + j));
+          lw.put(p0 + 4ull + 4ull * (k + j), x);
+        }
       }
       pos += 4ull + 4ull * nw;
       ++pc;
@@ -469,11 +576,12 @@ __device__ int sub_encode_rec(const xdrg_op *__restrict__ sops, const uint32_t *
         break;
       }
       if (!cnt) { ++pc; break; }
-      if (fp == st.cap()) { *full_op = pc; return kWalkFull; }
+      bool tail = false;
+      if (!sub_open(sops, st, fp, pc, op.depth, eoff, cnt, true, &tail)) { *full_op = pc; return kWalkFull; }
       dbase += op.depth;
-      st.push(fp++, sub_frame{eoff, cnt - 1, pc});
       src.eb = eoff;
       src.in_heap = true;
+      src.refresh();
       pc = op.arg4;
       break;
     }
@@ -515,7 +623,7 @@ __device__ __forceinline__ void sub_encode_kernel(XDRG_SUB_ENCODE_PARAMS) {
     const uint32_t sz = sizes[r];
     if (sz & kSizeErr) return;  // the size pass reported this record
     const uint64_t o = P.list ? offsets[r] : off;
-    const sub_src src{native + r * stride, stride, heap, heap_len, 0, false};
+    const sub_src_t<OPS::kImgWords> src{native + r * stride, stride, heap, heap_len, 0, false, {}};
     uint32_t full_op = 0;
     const int rc = sub_encode_rec<OPS>(sops, table, src, lw, cap, o, sz, mark, stack_limit, r, err, &full_op, st);
     lw.flush();
@@ -537,13 +645,19 @@ __device__ int sub_decode_rec(const xdrg_op *__restrict__ sops, const uint32_t *
                               const uint8_t *__restrict__ xdr, uint64_t a, uint64_t b, uint8_t *__restrict__ rec,
                               uint32_t stride, uint8_t *__restrict__ heap, uint64_t ecur, uint64_t eend,
                               uint32_t stack_limit, uint64_t r, unsigned long long *err, uint32_t *full_op,
-                              ST &st) {
+                              ST &st, bool defer) {
   for (uint32_t k = 0; k < stride / 4; ++k) st32(rec + 4 * k, 0u);
   uint64_t p = a;
   uint32_t fp = 0, pc = 0, dbase = 0, code = 0;
   uint64_t eb = 0;
   bool in_heap = false;
-  auto step = [&](const auto &op) -> int {
+  // Tail containers replace frames only where a record whose walk fails can
+  // be deferred to a deep pass that does not (the failing element's marks
+  // go in every open container, replaced ones too): recursive plans' main
+  // pass.
+  const bool may_tail = ST::kRegs && defer;
+  bool tailed = false;
+  auto step = [&](const auto &op) __attribute__((always_inline)) -> int {
     if (op.kind == XDRG_OP_END) return sub_next(sops, st, fp, pc, dbase, eb, in_heap) ? kWalkCont : kWalkOk;
     if (op.kind == XDRG_OP_JUMP) { pc = op.arg0; return kWalkCont; }
     if (dbase + op.depth > stack_limit) { code = XDRG_ERR_STACK_GET; return kWalkErr; }
@@ -639,12 +753,11 @@ __device__ int sub_decode_rec(const xdrg_op *__restrict__ sops, const uint32_t *
         break;
       }
       if (!cnt) { ++pc; break; }
-      if (fp == st.cap()) { *full_op = pc; return kWalkFull; }
+      if (!sub_open(sops, st, fp, pc, op.depth, ecur, cnt, may_tail, &tailed)) { *full_op = pc; return kWalkFull; }
       uint8_t *arr = heap + ecur;
       for (uint64_t z = 0; z < (bytes & ~3ull); z += 4) st32(arr + z, 0u);
       for (uint64_t z = bytes & ~3ull; z < bytes; ++z) arr[z] = 0;
       dbase += op.depth;
-      st.push(fp++, sub_frame{ecur, cnt - 1, pc});
       eb = ecur;
       in_heap = true;
       ecur += bytes;
@@ -659,12 +772,16 @@ __device__ int sub_decode_rec(const xdrg_op *__restrict__ sops, const uint32_t *
   do rc = OPS::visit(sops, pc, step);
   while (rc == kWalkCont);
   if (rc == kWalkFull) return kWalkFull;
+  if (code && tailed) {  // the deep pass walks it again with every frame
+    *full_op = pc;
+    return kWalkFull;
+  }
   if (code) {
     if (code != kReported) report(err, r, pc, code);
     // 1 + the failing element in every open container: the container's ref
     // sits in the object that encloses it (the record, or the frame below)
     st.each(fp, [&](uint32_t k, const sub_frame &fk, const sub_frame &below) {
-      uint8_t *ref = (k ? heap + below.eb : rec) + sops[fk.vpc].noff;
+      uint8_t *ref = (k ? heap + below.eb : rec) + sops[fk.vpc()].noff;
       st32(ref + 12, ld32(ref + 8) - fk.left);
     });
     return kWalkErr;
@@ -775,7 +892,7 @@ __device__ __forceinline__ void sub_decode_kernel(XDRG_SUB_DECODE_PARAMS) {
     if (sub_decode_rec<OPS>(sops, table, xdr, a + mark, b, native + r * stride, stride, heap,
                             pk ? pk_cur : ebase + static_cast<uint64_t>(F) * a,
                             pk ? pk_end : ebase + static_cast<uint64_t>(F) * b, stack_limit, r, err, &full_op,
-                            st) == kWalkFull)
+                            st, P.defer != nullptr) == kWalkFull)
       sub_full(P, r, full_op, XDRG_ERR_STACK_GET, err);
   });
 }

@@ -1674,8 +1674,8 @@ __global__ __launch_bounds__(256) void k_size_linear(const uint8_t *__restrict__
 // workspace, include/xdrgpu.h xdrg_deep_workspace_size): no allocation, no
 // lock and no state shared between calls, so calls on different streams run
 // side by side and graph capture records plain memsets and kernels.
-constexpr uint32_t kDeepLanesA = 4096, kDeepSlabA = 1024;           // 64 MiB of frames
-constexpr uint32_t kDeepLanesB = 8, kDeepSlabB = XDRG_MAX_FRAMES;   // 64 MiB
+constexpr uint32_t kDeepLanesA = 4096, kDeepSlabA = 1024;           // 96 MiB of frames (24 B each)
+constexpr uint32_t kDeepLanesB = 8, kDeepSlabB = XDRG_MAX_FRAMES;   // 96 MiB
 static_assert(kDeepLanesA % 256 == 0, "deep pass A runs 256-lane workgroups");
 constexpr uint64_t kDeepSlabBytes =
     sizeof(sub_frame) * (uint64_t(kDeepLanesA) * kDeepSlabA + uint64_t(kDeepLanesB) * kDeepSlabB);
