@@ -713,6 +713,7 @@ class GpuEngine:
          self.heap_out) = setup(args.schema, n, self.dev, rank, world, plan_opts(args))
         self.enc_stream = plan_opts(args).get("enc_stream", -1)
         self.size_linear = plan_opts(args).get("size_linear", -1)
+        self.fixed_path = plan_opts(args).get("fixed_path", 0)
         self.stream = torch.cuda.current_stream()
         self.s = self.stream.cuda_stream
         self.mar.status.init(self.s)
@@ -766,8 +767,12 @@ class GpuEngine:
         if plan.is_fixed:
             # encode and decode are the same kernel with the encode / decode
             # permutation programs: read one side, write the other
+            # (non-identity layouts: the tile kernel for records of up to 16
+            # words each way, xdrgpu.hip run_fixed)
+            tile = self.fixed_path == 0 and S_ <= 64 and plan.fixed_size <= 64
             kern = ("k_fixed_reg" if plan.path == A.PATH_FIXED_REG else
-                    "k_fixed_grp" if info.group_records else "k_fixed_lds")
+                    "k_fixed_tile" if tile else
+                    "k_fixed_grp" if info.group_records and self.fixed_path != 2 else "k_fixed_lds")
             return kern, n * S_ + X, enc_ms + dec_ms
         # dominant phase: encode (size pass + block scan + window encode) vs
         # decode (window decode).  Encode reads the native records and the

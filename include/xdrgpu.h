@@ -309,7 +309,8 @@ int xdrg_plan_get_info(const xdrg_plan *plan, xdrg_plan_info *info);
 enum xdrg_plan_option {
   XDRG_OPT_VAR_ENCODE_KERNEL = 1, /* 0 auto, 1 per-lane walk, 3 chunk-map image   */
   XDRG_OPT_VAR_DECODE_KERNEL = 2, /* 0 auto, 1 per-lane walk, 2 LDS window         */
-  XDRG_OPT_FIXED_PATH = 3,        /* 0 auto, 2 LDS kernel for non-identity layouts */
+  XDRG_OPT_FIXED_PATH = 3,        /* non-identity layouts: 0 auto (tile kernel),
+                                     2 LDS term kernel, 3 group kernel            */
   XDRG_OPT_IMAGE_BYTES = 4,       /* var encode LDS image per wave, -1 auto        */
   XDRG_OPT_WINDOW_BYTES = 5,      /* var decode LDS window per wave, -1 auto       */
   XDRG_OPT_ENC_UNROLL = 6,        /* payload chunks in flight per lane: 4, 8, 16   */

@@ -881,8 +881,20 @@ typedef struct {
   uint64_t lim;
   uint32_t past;
   uint32_t fcap, fcode; /* element frames the parse follows, and what deeper is */
+  int tail;             /* tail containers take their element's frame (the whole-record walk) */
 } rxctx;
-static uint32_t rx_walk(rxctx *c, uint64_t *pp, uint32_t pc, uint32_t frames) {
+/* The op after pc, through jumps, is its body's END: a container there,
+ * opened in the last element of its own container, takes that element's
+ * frame (xdrpp_amd/csrc/sub_kernels.h sub_tail) in the device's
+ * whole-record walk (k_rx_long): frames then counts the others.  Its
+ * window parses count every frame. */
+static int rx_tail(const plan_t *P, uint32_t pc) {
+  uint32_t q = pc + 1;
+  while (P->ops[q].kind == XDRG_OP_JUMP) q = P->ops[q].arg0;
+  return P->ops[q].kind == XDRG_OP_END;
+}
+/* last: the element being walked is the last of its container */
+static uint32_t rx_walk(rxctx *c, uint64_t *pp, uint32_t pc, uint32_t frames, int last) {
   const plan_t *P = c->P;
   uint64_t p = *pp;
   for (;;) {
@@ -928,10 +940,13 @@ static uint32_t rx_walk(rxctx *c, uint64_t *pp, uint32_t pc, uint32_t frames) {
        * records are left to its long-record walk (or, with a window-sized
        * maxlen, to the caller), as records past the window are; that walk
        * follows XDRG_MAX_FRAMES (deeper: the decode's stack overflow) */
-      if (v && frames == c->fcap) return c->fcode;
-      for (uint32_t i = 0; i < v; ++i) {
-        uint32_t rc = rx_walk(c, &p, op->arg4, frames + 1);
-        if (rc) return rc;
+      {
+        const int coll = c->tail && frames > 0 && last && rx_tail(P, pc);
+        if (v && !coll && frames == c->fcap) return c->fcode;
+        for (uint32_t i = 0; i < v; ++i) {
+          uint32_t rc = rx_walk(c, &p, op->arg4, coll ? frames : frames + 1, i + 1 == v);
+          if (rc) return rc;
+        }
       }
       ++pc;
       break;
@@ -954,9 +969,9 @@ int xdro_index_records(const xdrg_op *ops, uint32_t nops, const uint32_t *table,
   for (; k < n && p < len; ++k) {
     offsets[k] = p;
     const int capped = p + maxlen < len;
-    rxctx c = {&P, s, capped ? p + maxlen : len, capped ? RX_LONG : RX_BAD, fcap, fcode};
+    rxctx c = {&P, s, capped ? p + maxlen : len, capped ? RX_LONG : RX_BAD, fcap, fcode, whole};
     uint64_t q = p;
-    uint32_t rc = rx_walk(&c, &q, 0, 0);
+    uint32_t rc = rx_walk(&c, &q, 0, 0, 0);
     if (rc) {
       *count = k;
       for (uint64_t i = k + 1; i <= n; ++i) offsets[i] = len;
@@ -976,9 +991,9 @@ int xdro_index_records(const xdrg_op *ops, uint32_t nops, const uint32_t *table,
   }
   /* n records and more bytes: the chain ends at record n unless it parses */
   const int capped = p + maxlen < len;
-  rxctx c = {&P, s, capped ? p + maxlen : len, capped ? RX_LONG : RX_BAD, fcap, fcode};
+  rxctx c = {&P, s, capped ? p + maxlen : len, capped ? RX_LONG : RX_BAD, fcap, fcode, whole};
   uint64_t q = p;
-  if (rx_walk(&c, &q, 0, 0)) *count = n;
+  if (rx_walk(&c, &q, 0, 0, 0)) *count = n;
   return 0;
 }
 

@@ -287,6 +287,31 @@ def test_gpu_max_frames(dev):
     assert (e.value.record, e.value.op) == (0, 1)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("spec", [1, 0])
+def test_gpu_tail_cycle_ends(dev, spec):
+    """A linked list walks in one frame (its tail containers replace their
+    frames, sub_kernels.h sub_tail), so a staged rp__list node whose
+    rpcb_next is itself never runs out of frames: the walk still ends, at
+    XDRG_MAX_FRAMES open frames counted with the replaced ones, with
+    xdr_stack_overflow at rpcb_next (as a test_recursive chain through `next`
+    does, test_gpu_max_frames) -- in the main pass, in well under a second."""
+    import time
+    from xdrpp_amd import marshal as M
+    t = S.rp__list
+    plan = M.Plan(t, {"specialize": spec})
+    vpc = int(np.nonzero((plan.cp.ops["kind"] == A.OP_VECTOR))[0][-1])
+    nat = np.zeros(t.size, dtype=np.uint8)
+    struct.pack_into("<QII", nat, t.offsets["rpcb_next"], 0, 1, 0)  # element 0: the image itself
+    heap = nat.copy()
+    mar = M.Marshaler(plan, dev)
+    t0 = time.perf_counter()
+    with pytest.raises(M.XdrStackOverflow) as e:
+        mar.encode(_dev(nat, dev), 1, _dev(heap, dev))
+    assert (e.value.record, e.value.op) == (0, vpc)
+    assert time.perf_counter() - t0 < 30
+
+
 @pytest.mark.parametrize("name", TYPES)
 def test_host_index_records(gold, name):
     """decode()'s host fallback finds the same record boundaries as the

@@ -240,5 +240,103 @@ __global__ __launch_bounds__(256) void k_fixed_grp(const uint8_t *__restrict__ i
   }
 }
 
+// ------------------------------------------------------------ fixed: tile
+// Non-identity fixed layouts, every input read once as whole 16-byte chunks
+// and every output written as whole 16-byte chunks (numerics: 56-byte
+// native, 44-byte wire; the group kernel above reads each output chunk's
+// terms as 8-byte windows, 32 bytes of loads per 16 written).  A workgroup
+// takes tiles of kTileRec records: the tile's input chunks into LDS (the
+// next tile's loads in flight meanwhile), one lane per record builds its
+// output words from the term program -- the same for every lane, so it
+// lives in scalar registers (kernel arguments) -- into an LDS output tile,
+// and the tile leaves as 16-byte stores.  Records of up to IW input and OW
+// output words, up to KT terms per output word.
+constexpr uint32_t kTileRec = 256;
+template <int OW, int KT>
+struct tile_prog {
+  uint32_t src[OW][KT];  // input word of the term (within the record)
+  uint32_t sel[OW][KT];  // v_perm selector, or bool_term's with kGrpBool
+  uint32_t nterm[OW];    // terms of the output word (0: a zero word)
+};
+
+template <int IW, int OW, int KT>
+__global__ __launch_bounds__(256) void k_fixed_tile(const u32x4 *__restrict__ in, u32x4 *__restrict__ out,
+                                                    uint64_t n, uint32_t in_w, uint32_t out_w,
+                                                    const tile_prog<OW, KT> prog) {
+  // LDS (dynamic): the input tile (+ 4 zero words), then the output tile
+  extern __shared__ __attribute__((aligned(16))) uint32_t tsm[];
+  uint32_t *tin = tsm, *tout = tsm + kTileRec * in_w + 4;
+  constexpr int CH = (IW + 3) / 4;  // input chunks per lane per tile (at most)
+  const uint32_t tid = threadIdx.x;
+  const uint64_t ntiles = (n + kTileRec - 1) / kTileRec;
+  if (tid < 4) tin[kTileRec * in_w + tid] = 0u;
+  u32x4 v[CH];
+  // input chunks of tile t into v (a partial chunk at the batch's end word
+  // by word; the words past it read as 0)
+  auto load = [&](uint64_t t) {
+    const uint64_t nt = min<uint64_t>(kTileRec, n - t * kTileRec);
+    const uint32_t nw = static_cast<uint32_t>(nt) * in_w, nc = (nw + 3u) >> 2;
+    const u32x4 *src = in + t * kTileRec * in_w / 4u;  // (kTileRec * in_w words: whole chunks)
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+      const uint32_t c = tid + 256u * k;
+      if (c + 1u < nc || (c + 1u == nc && !(nw & 3u))) {
+        v[k] = src[c];
+      } else if (c < nc) {
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(src + c);
+        const uint32_t m = nw & 3u;
+        v[k] = u32x4{w[0], m > 1 ? w[1] : 0u, m > 2 ? w[2] : 0u, 0u};
+      }
+    }
+  };
+  uint64_t t = blockIdx.x;
+  if (t < ntiles) load(t);
+  for (; t < ntiles; t += gridDim.x) {
+    const uint64_t nt = min<uint64_t>(kTileRec, n - t * kTileRec);
+    const uint32_t nin = static_cast<uint32_t>(nt) * in_w;
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+      const uint32_t c = tid + 256u * k;
+      if (4u * c < nin) *reinterpret_cast<u32x4 *>(tin + 4u * c) = v[k];
+    }
+    __syncthreads();
+    if (t + gridDim.x < ntiles) load(t + gridDim.x);  // in flight during the build and the stores
+    if (tid < nt) {
+      const uint32_t *rin = tin + tid * in_w;
+      uint32_t *rout = tout + tid * out_w;
+#pragma unroll
+      for (int j = 0; j < OW; ++j) {
+        if (j < static_cast<int>(out_w)) {
+          uint32_t o = 0;
+#pragma unroll
+          for (int k = 0; k < KT; ++k) {
+            if (k < static_cast<int>(prog.nterm[j])) {
+              const uint32_t a = prog.src[j][k], sl = prog.sel[j][k];
+              if (sl & kGrpBool) o |= bool_term(rin[a], sl & 0xffffffu);
+              else o |= perm(rin[a + 1], rin[a], sl);
+            }
+          }
+          rout[j] = o;
+        }
+      }
+    }
+    __syncthreads();
+    const uint32_t nout = static_cast<uint32_t>(nt) * out_w, noc = (nout + 3u) >> 2;
+    u32x4 *dst = out + t * kTileRec * out_w / 4u;
+    for (uint32_t c = tid; c < noc; c += 256u) {
+      const u32x4 x = *reinterpret_cast<const u32x4 *>(tout + 4u * c);
+      if (4u * c + 4u <= nout) {
+        dst[c] = x;
+      } else {
+        uint32_t *w = reinterpret_cast<uint32_t *>(dst + c);
+        const uint32_t m = nout & 3u;
+        w[0] = x.x;
+        if (m > 1) w[1] = x.y;
+        if (m > 2) w[2] = x.z;
+      }
+    }
+  }
+}
+
 }  // namespace dev
 }  // namespace xdrg

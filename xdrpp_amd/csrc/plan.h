@@ -97,7 +97,7 @@ constexpr int kMaxDevices = 64;
 struct plan_opts {
   int enc_kernel = 0;      // var encode: 0 auto, 1 per-lane, 3 chunk-map image
   int dec_kernel = 0;      // var decode: 0 auto, 1 per-lane, 2 window
-  int fixed_path = 0;      // 0 auto, 2 = k_fixed_lds for non-identity fixed plans
+  int fixed_path = 0;      // non-identity fixed plans: 0 auto (k_fixed_tile), 2 k_fixed_lds, 3 k_fixed_grp
   int image_bytes = -1;    // var encode LDS image per wave (-1: per plan)
   int window_bytes = -1;   // var decode LDS window per wave (-1: per call)
   int enc_unroll = 8;      // payload chunks in flight per lane (4, 8, 16)

@@ -61,18 +61,19 @@ constexpr uint32_t kReported = 0x100;  // decode: the element walk reported the 
 // the walk goes on when the container closes (vd: op in the low 16 bits,
 // return pc in the high 16; plans have fewer than kOpRecordLevel ops), and
 // the levels its pop gives back (the op's depth, plus those of the frames
-// it replaced -- sub_tail).
+// it replaced -- sub_tail), and the frames it stands for (1 + those).
 struct sub_frame {
   uint64_t eb;
   uint32_t left;
   uint32_t vd;
   uint32_t dsum;
+  uint32_t nf;
   __device__ __forceinline__ uint32_t vpc() const { return vd & 0xffffu; }
   __device__ __forceinline__ uint32_t ret() const { return vd >> 16; }
 };
 __device__ __forceinline__ sub_frame make_frame(uint64_t eb, uint32_t left, uint32_t vpc, uint32_t ret,
-                                                uint32_t dsum) {
-  return sub_frame{eb, left, vpc | (ret << 16), dsum};
+                                                uint32_t dsum, uint32_t nf) {
+  return sub_frame{eb, left, vpc | (ret << 16), dsum, nf};
 }
 
 // The walks touch the top frame only (and, after an error in the decode,
@@ -108,6 +109,7 @@ struct reg_stack {
   }
   __device__ __forceinline__ uint32_t cap() const { return kSubFrames; }
   static constexpr bool kRegs = true;
+  uint32_t lf = 0;  // the frames open, replaced ones included (sub_open)
 };
 // Deep passes: `n` frames per lane in the caller's workspace.
 struct slab_stack {
@@ -121,6 +123,7 @@ struct slab_stack {
   }
   __device__ __forceinline__ uint32_t cap() const { return n; }
   static constexpr bool kRegs = false;
+  uint32_t lf = 0;
 };
 
 // Tail containers.  A container of element subroutines whose elements are
@@ -131,7 +134,10 @@ struct slab_stack {
 // linked list (rp__list's rpcb_next, xdrpp/rpcb_prot.x:34; test_recursive's
 // nextvec, tests/xdrtest.x:29-33) walks in one frame however long it is,
 // in the main pass.  The depth levels of the replaced frames stay counted
-// (dsum) and are given back at the pop.
+// (dsum) and are given back at the pop; so do the frames themselves (nf):
+// XDRG_MAX_FRAMES open frames, replaced ones included, is xdr_stack_overflow
+// in any pass (as running out of the last pass's frames is), which also
+// ends a walk around a cycle in a staged heap.
 __device__ __forceinline__ bool sub_tail(const xdrg_op *__restrict__ ops, uint32_t pc) {
   uint32_t q = pc + 1;
   while (ops[q].kind == XDRG_OP_JUMP) q = ops[q].arg0;
@@ -139,19 +145,24 @@ __device__ __forceinline__ bool sub_tail(const xdrg_op *__restrict__ ops, uint32
 }
 // Open the container at pc (count cnt >= 1, first element eb): on top of
 // the stack, or in place of the top frame (sub_tail; allow_tail).  Returns
-// false when the stack is full; sets *tail when it replaced a frame.
+// kOpenOk (*tail set when it replaced a frame), kOpenFull when the stack is
+// full (the next pass takes the record), or kOpenOver at XDRG_MAX_FRAMES.
+enum : int { kOpenOk = 0, kOpenFull = 1, kOpenOver = 2 };
 template <class ST>
-__device__ __forceinline__ bool sub_open(const xdrg_op *__restrict__ ops, ST &st, uint32_t &fp, uint32_t pc,
-                                         uint32_t depth, uint64_t eb, uint32_t cnt, bool allow_tail, bool *tail) {
+__device__ __forceinline__ int sub_open(const xdrg_op *__restrict__ ops, ST &st, uint32_t &fp, uint32_t pc,
+                                        uint32_t depth, uint64_t eb, uint32_t cnt, bool allow_tail, bool *tail) {
+  if (st.lf >= XDRG_MAX_FRAMES) return kOpenOver;
   if (allow_tail && fp && st.top(fp).left == 0u && sub_tail(ops, pc)) {
     sub_frame &t = st.top(fp);
-    t = make_frame(eb, cnt - 1u, pc, t.ret(), t.dsum + depth);
+    t = make_frame(eb, cnt - 1u, pc, t.ret(), t.dsum + depth, t.nf + 1u);
+    ++st.lf;
     *tail = true;
-    return true;
+    return kOpenOk;
   }
-  if (fp == st.cap()) return false;
-  st.push(fp++, make_frame(eb, cnt - 1u, pc, pc + 1u, depth));
-  return true;
+  if (fp == st.cap()) return kOpenFull;
+  st.push(fp++, make_frame(eb, cnt - 1u, pc, pc + 1u, depth, 1u));
+  ++st.lf;
+  return kOpenOk;
 }
 
 // The pass a launch runs (see the top of the file).
@@ -286,6 +297,7 @@ __device__ __forceinline__ bool sub_next(const xdrg_op *__restrict__ ops, ST &st
   }
   pc = f.ret();
   dbase -= f.dsum;
+  st.lf -= f.nf;
   st.pop(fp);
   if (--fp) eb = st.top(fp).eb;
   else in_heap = false;
@@ -320,6 +332,7 @@ __device__ int sub_size(const xdrg_op *__restrict__ ops, const uint32_t *__restr
                         sub_src_t<OPS::kImgWords> src,
                         uint64_t &s, uint32_t &dmax, uint32_t &bad_op, uint32_t &code, ST &st) {
   uint32_t fp = 0, pc = 0, dbase = 0;
+  st.lf = 0;
   auto step = [&](const auto &op) __attribute__((always_inline)) -> int {
     if (op.kind == XDRG_OP_END) {
       if (!sub_next(ops, st, fp, pc, dbase, src.eb, src.in_heap)) return kWalkOk;
@@ -354,7 +367,9 @@ __device__ int sub_size(const xdrg_op *__restrict__ ops, const uint32_t *__restr
       }
       if (!cnt) { ++pc; break; }
       bool tail = false;
-      if (!sub_open(ops, st, fp, pc, op.depth, src.w64(op.noff), cnt, true, &tail)) { bad_op = pc; return kWalkFull; }
+      const int o = sub_open(ops, st, fp, pc, op.depth, src.w64(op.noff), cnt, true, &tail);
+      if (o == kOpenFull) { bad_op = pc; return kWalkFull; }
+      if (o == kOpenOver) { bad_op = pc; code = XDRG_ERR_STACK_PUT; return kWalkErr; }
       dbase += op.depth;
       src.eb = st.top(fp).eb;
       src.in_heap = true;
@@ -497,6 +512,7 @@ __device__ __forceinline__ int sub_encode_rec(const xdrg_op *__restrict__ sops, 
     pos += 4;
   }
   uint32_t fp = 0, pc = 0, dbase = 0;
+  st.lf = 0;
   auto step = [&](const auto &op) __attribute__((always_inline)) -> int {
     if (op.kind == XDRG_OP_END) {
       if (!sub_next(sops, st, fp, pc, dbase, src.eb, src.in_heap)) return kWalkOk;
@@ -577,7 +593,9 @@ __device__ __forceinline__ int sub_encode_rec(const xdrg_op *__restrict__ sops, 
       }
       if (!cnt) { ++pc; break; }
       bool tail = false;
-      if (!sub_open(sops, st, fp, pc, op.depth, eoff, cnt, true, &tail)) { *full_op = pc; return kWalkFull; }
+      const int o = sub_open(sops, st, fp, pc, op.depth, eoff, cnt, true, &tail);
+      if (o == kOpenFull) { *full_op = pc; return kWalkFull; }
+      if (o == kOpenOver) { report(err, r, pc, XDRG_ERR_STACK_PUT); return kWalkErr; }
       dbase += op.depth;
       src.eb = eoff;
       src.in_heap = true;
@@ -648,7 +666,12 @@ __device__ int sub_decode_rec(const xdrg_op *__restrict__ sops, const uint32_t *
                               ST &st, bool defer) {
   for (uint32_t k = 0; k < stride / 4; ++k) st32(rec + 4 * k, 0u);
   uint64_t p = a;
+  // (The stream through a 32-byte read-ahead, two aligned 16-byte chunks
+  // serving up to 8 words per round trip, measured slower: rp_list's decode
+  // 3.94 vs 2.76 ms, profiles/r05o.)
+  auto word = [&](uint64_t q) -> uint32_t { return ld32(xdr + q); };
   uint32_t fp = 0, pc = 0, dbase = 0, code = 0;
+  st.lf = 0;
   uint64_t eb = 0;
   bool in_heap = false;
   // Tail containers replace frames only where a record whose walk fails can
@@ -666,44 +689,44 @@ __device__ int sub_decode_rec(const xdrg_op *__restrict__ sops, const uint32_t *
     switch (op.kind) {
     case XDRG_OP_U32:
       if (rem < 4) { code = XDRG_ERR_OVERFLOW_GET; break; }
-      st32(nat + op.noff, bswap32(ld32(xdr + p))); p += 4; ++pc; break;
+      st32(nat + op.noff, bswap32(word(p))); p += 4; ++pc; break;
     case XDRG_OP_ENUM: {
       if (rem < 4) { code = XDRG_ERR_OVERFLOW_GET; break; }
-      const uint32_t v = bswap32(ld32(xdr + p));
+      const uint32_t v = bswap32(word(p));
       st32(nat + op.noff, v); p += 4;
       if ((op.flags & XDRG_F_VALIDATE) && !enum_ok(table, op.arg0, op.arg1, v)) { code = XDRG_ERR_INVALID_ENUM; break; }
       ++pc; break;
     }
     case XDRG_OP_BOOL:
       if (rem < 4) { code = XDRG_ERR_OVERFLOW_GET; break; }
-      nat[op.noff] = ld32(xdr + p) != 0u; p += 4; ++pc; break;
+      nat[op.noff] = word(p) != 0u; p += 4; ++pc; break;
     case XDRG_OP_U64:
       if (rem < 8) { code = XDRG_ERR_OVERFLOW_GET; break; }
-      st32(nat + op.noff + 4, bswap32(ld32(xdr + p)));
-      st32(nat + op.noff, bswap32(ld32(xdr + p + 4)));
+      st32(nat + op.noff + 4, bswap32(word(p)));
+      st32(nat + op.noff, bswap32(word(p + 4)));
       p += 8; ++pc; break;
     case XDRG_OP_OPAQUE: {
       const uint32_t L = op.arg0;
       if (rem < L) { code = XDRG_ERR_OVERFLOW_GET; break; }
       for (uint32_t k = 0; k < L; ++k) nat[op.noff + k] = xdr[p + k];
-      if ((L & 3u) && (ld32(xdr + p + (L & ~3u)) & ~keep_mask(L & 3u))) { code = XDRG_ERR_NONZERO_PAD; break; }
+      if ((L & 3u) && (word(p + (L & ~3u)) & ~keep_mask(L & 3u))) { code = XDRG_ERR_NONZERO_PAD; break; }
       p += (L + 3u) & ~3u; ++pc; break;
     }
     case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
       if (rem < 4) { code = XDRG_ERR_OVERFLOW_GET; break; }
-      const uint32_t L = bswap32(ld32(xdr + p));
+      const uint32_t L = bswap32(word(p));
       if (L > rem - 4) { code = XDRG_ERR_OVERFLOW_GET; break; }
       if (L > op.arg0) { code = op.kind == XDRG_OP_STRING ? XDRG_ERR_XSTRING_BOUND : XDRG_ERR_XVECTOR_BOUND; break; }
       p += 4;
       const uint32_t nw = (L + 3u) >> 2;
-      if ((L & 3u) && (ld32(xdr + p + 4ull * (nw - 1)) & ~keep_mask(L & 3u))) { code = XDRG_ERR_NONZERO_PAD; break; }
+      if ((L & 3u) && (word(p + 4ull * (nw - 1)) & ~keep_mask(L & 3u))) { code = XDRG_ERR_NONZERO_PAD; break; }
       *reinterpret_cast<uint64_t *>(nat + op.noff) = p;  // the payload stays in the stream
       st32(nat + op.noff + 8, L);
       p += 4ull * nw; ++pc; break;
     }
     case XDRG_OP_UNION: {
       if (rem < 4) { code = XDRG_ERR_OVERFLOW_GET; break; }
-      const uint32_t d = bswap32(ld32(xdr + p));
+      const uint32_t d = bswap32(word(p));
       p += 4;
       if ((op.flags & XDRG_F_VALIDATE) && !enum_ok(table, op.arg0, op.arg1, d)) { code = XDRG_ERR_INVALID_ENUM; break; }
       const int t = union_target(op, table, d);
@@ -714,7 +737,7 @@ __device__ int sub_decode_rec(const xdrg_op *__restrict__ sops, const uint32_t *
     }
     case XDRG_OP_VECTOR: {
       if (rem < 4) { code = XDRG_ERR_OVERFLOW_GET; break; }
-      const uint32_t cnt = bswap32(ld32(xdr + p));
+      const uint32_t cnt = bswap32(word(p));
       p += 4;
       if (cnt > op.arg0) {  // check_size (types.h:486-489, 605-608)
         code = (op.flags & XDRG_F_POINTER) ? XDRG_ERR_POINTER_BOUND : XDRG_ERR_XVECTOR_BOUND;
@@ -742,7 +765,7 @@ __device__ int sub_decode_rec(const xdrg_op *__restrict__ sops, const uint32_t *
       *reinterpret_cast<uint64_t *>(nat + op.noff) = ecur;
       st32(nat + op.noff + 8, cnt);
       if (!(op.flags & XDRG_F_SUB)) {
-        auto rd = [&](uint64_t q) { return ld32(xdr + q); };
+        auto rd = [&](uint64_t q) { return word(q); };
         if (!dec_vector_elems(sops, table, pc + 1, op.arg2, cnt, op.arg1, heap + ecur, p, b,
                               stack_limit - dbase, r, err, rd, reinterpret_cast<uint32_t *>(nat + op.noff + 12))) {
           code = kReported;
@@ -753,7 +776,9 @@ __device__ int sub_decode_rec(const xdrg_op *__restrict__ sops, const uint32_t *
         break;
       }
       if (!cnt) { ++pc; break; }
-      if (!sub_open(sops, st, fp, pc, op.depth, ecur, cnt, may_tail, &tailed)) { *full_op = pc; return kWalkFull; }
+      const int o = sub_open(sops, st, fp, pc, op.depth, ecur, cnt, may_tail, &tailed);
+      if (o == kOpenFull) { *full_op = pc; return kWalkFull; }
+      if (o == kOpenOver) { code = XDRG_ERR_STACK_GET; break; }
       uint8_t *arr = heap + ecur;
       for (uint64_t z = 0; z < (bytes & ~3ull); z += 4) st32(arr + z, 0u);
       for (uint64_t z = bytes & ~3ull; z < bytes; ++z) arr[z] = 0;

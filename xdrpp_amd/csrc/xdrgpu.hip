@@ -883,13 +883,15 @@ __device__ __forceinline__ uint32_t ix_mark(uint32_t raw, uint64_t w, uint64_t l
 // occupancy it costs outweighing L2-hit latency.)  The fast path
 // (rxs_walk_body) stages its segment: its walks are serial chains.
 
-// The frames of rx_len's element subroutines.  rx_reg_frames: the index's
-// own XDRG_INDEX_FRAMES in registers, st[0] the top frame, pushed and popped
-// by shifting (constant indices: no private memory, sub_kernels.h
-// reg_stack); a record nested deeper is RX_LONG, left to the long-record
-// walk (k_rx_long) like one past the window.  rx_slab_frames: that walk's
-// frames, XDRG_MAX_FRAMES of them in the index workspace; deeper is RX_BAD
-// (the decode reports the stack overflow).
+// The frames of rx_len's element subroutines (with TAIL a tail container
+// replaces the top frame, sub_kernels.h sub_tail: these count the frames
+// open).
+// rx_reg_frames: the index's own XDRG_INDEX_FRAMES in registers, st[0] the
+// top frame, pushed and popped by shifting (constant indices: no private
+// memory, sub_kernels.h reg_stack); a record nested deeper is RX_LONG, left
+// to the long-record walk (k_rx_long) like one past the window.
+// rx_slab_frames: that walk's frames, XDRG_MAX_FRAMES of them in the index
+// workspace; deeper is RX_BAD (the decode reports the stack overflow).
 struct rx_frame { uint32_t left, entry, ret; };
 struct rx_reg_frames {
   static constexpr uint32_t kFull = RX_LONG;
@@ -920,7 +922,11 @@ struct rx_slab_frames {
 };
 
 // U: the position type (uint32_t for offsets into a staged stretch).
-template <class RD, class U = uint64_t, class FS = rx_reg_frames>
+// TAIL: a tail container takes the frame of the element it ends (the
+// long-record walk); the windows' parses count every frame, so a candidate
+// start inside a long list bails at XDRG_INDEX_FRAMES instead of parsing on
+// to the window's end (with it, rp_list's index took 836 ms, profiles/r05n).
+template <class RD, class U = uint64_t, class FS = rx_reg_frames, bool TAIL = false>
 __device__ uint32_t rx_len(const xdrg_op *__restrict__ ops, const uint32_t *__restrict__ table,
                            const RD &rd, U len, U a, uint32_t maxlen, FS st = FS{}) {
   const bool capped = static_cast<uint64_t>(a) + maxlen < len;
@@ -987,6 +993,11 @@ __device__ uint32_t rx_len(const xdrg_op *__restrict__ ops, const uint32_t *__re
         pc += 1 + op.arg2;
       } else if (!v) {
         ++pc;
+      } else if (TAIL && st.fp && st.top().left == 0 && sub_tail(ops, pc)) {
+        // a tail container takes the frame of the element it ends, and its
+        // return pc (sub_kernels.h sub_tail): a linked list parses in one frame
+        st.top() = rx_frame{v - 1, op.arg4, st.top().ret};
+        pc = op.arg4;
       } else {
         if (st.full()) return FS::kFull;
         st.push(rx_frame{v - 1, op.arg4, pc + 1});
@@ -1384,57 +1395,119 @@ __global__ void k_ix_long(const uint8_t *__restrict__ s, uint64_t len, uint32_t 
   next[2] = 0;
 }
 
+// k_rx_long's stream reader.  The wave's 64 lanes parse the same record in
+// step (the same values in every lane), through a 4 KiB block of the stream
+// in LDS: a word outside it reloads the block, each lane loading four
+// 16-byte chunks, so one round trip brings 4 KiB where a lone lane's parse
+// waited on every length and count (rp_list's 500-node lists: 64 ms for
+// the index of 1M records, profiles/r05k).  Positions are word-aligned
+// record offsets, and a word is read only when it lies inside the stream.
+struct rx_wave_cache {
+  const uint8_t *s;
+  uint64_t len;
+  uint32_t *buf;          // 1024 words of LDS
+  mutable uint64_t base;  // stream offset of buf[0] (4 KiB aligned; ~0: none)
+  __device__ __forceinline__ uint32_t operator()(uint64_t p) const {
+    if (p < base || p - base >= 4096u) {
+      const uint64_t b = p & ~4095ull;
+      wave_sync();  // every lane past its reads of the old block
+#pragma unroll
+      for (uint32_t j = 0; j < 4; ++j) {
+        const uint32_t k = threadIdx.x + 64u * j;
+        const uint64_t o = b + 16ull * k;
+        u32x4 v{0u, 0u, 0u, 0u};
+        if (o + 16 <= len) {
+          v = ld16u(s + o);
+        } else if (o < len) {
+          v.x = partial_word(s, len, o);
+          v.y = partial_word(s, len, o + 4);
+          v.z = partial_word(s, len, o + 8);
+          v.w = partial_word(s, len, o + 12);
+        }
+        *reinterpret_cast<u32x4 *>(buf + 4u * k) = v;
+      }
+      wave_sync();
+      base = b;
+    }
+    return buf[(p - base) >> 2];
+  }
+};
+
 // Records too long for an index window (or nested deeper than its frames),
 // walked one after another from next = [word, record index] as
 // xdr_from_opaque's own walk would (marshal.h:299-306): while the record
 // there is such a record, at most `hops` of them, each parsed whole
-// (lengths, counts and discriminants; its frames in `slab`).  Leaves next at
-// the first record a window takes (next[2] = 1) or at the hop budget
-// (next[2] = 0); the end of the stream, the n-th record or a record that
-// does not parse ends the index here (next[0] = all ones; the record it
-// stops at gets its offset, k_rx_fill the rest).
-__global__ void k_rx_long(const uint8_t *__restrict__ s, uint64_t len, uint32_t maxlen, uint64_t n,
-                          const xdrg_op *__restrict__ ops, const uint32_t *__restrict__ table,
-                          uint64_t *__restrict__ offsets, unsigned long long *count, unsigned long long *next,
-                          rx_frame *slab, uint32_t hops) {
-  if (threadIdx.x || blockIdx.x) return;
+// (lengths, counts and discriminants; its frames in registers, or in `slab`
+// past XDRG_INDEX_FRAMES).  Leaves next at the first record a window takes
+// (next[2] = 1) or at the hop budget (next[2] = 0); the end of the stream,
+// the n-th record or a record that does not parse ends the index here
+// (next[0] = all ones; the record it stops at gets its offset, k_rx_fill
+// the rest).  One wave, every lane on the same parse (rx_wave_cache); lane
+// 0 writes.
+__global__ __launch_bounds__(64) void k_rx_long(const uint8_t *__restrict__ s, uint64_t len, uint32_t maxlen,
+                                                uint64_t n, const xdrg_op *__restrict__ ops,
+                                                const uint32_t *__restrict__ table, uint64_t *__restrict__ offsets,
+                                                unsigned long long *count, unsigned long long *next, rx_frame *slab,
+                                                uint32_t hops, uint32_t nops, uint32_t ops_lds) {
+  __shared__ __attribute__((aligned(16))) uint32_t cbuf[1024];
+  extern __shared__ __attribute__((aligned(16))) uint32_t rsm[];  // the plan's ops (ops_lds)
+  if (blockIdx.x) return;
+  if (ops_lds) {  // each op dispatch a round trip to L2 otherwise
+    load_ops(reinterpret_cast<xdrg_op *>(rsm), ops, nops);
+    ops = reinterpret_cast<const xdrg_op *>(rsm);
+  }
+  const bool l0 = threadIdx.x == 0;
+  const rx_wave_cache rd{s, len, cbuf, ~0ull};
   uint64_t w = next[0], m = next[1];
   for (uint32_t h = 0; h < hops; ++h) {
     if (4 * w >= len) {  // the stream's end
-      offsets[m] = len;
-      atomicMin(count, m);
-      next[0] = ~0ull;
+      if (l0) {
+        offsets[m] = len;
+        atomicMin(count, m);
+        next[0] = ~0ull;
+      }
       return;
     }
+    // the whole record: in registers, or (nested past them) in the slab
+    uint32_t L = rx_len<rx_wave_cache, uint64_t, rx_reg_frames, true>(ops, table, rd, len, 4 * w, 0xffffffffu);
+    const bool deep = L == RX_LONG;
+    if (deep)
+      L = rx_len<rx_wave_cache, uint64_t, rx_slab_frames, true>(ops, table, rd, len, 4 * w, 0xffffffffu,
+                                                                rx_slab_frames{slab, XDRG_MAX_FRAMES, 0});
     if (m >= n) {  // n records and more bytes (the decode reports them): the
       // count stays all ones if a record parses there (the chain goes on)
-      offsets[n] = 4 * w;
-      const uint32_t L = rx_len(ops, table, rx_global{s}, len, 4 * w, 0xffffffffu,
-                                rx_slab_frames{slab, XDRG_MAX_FRAMES, 0});
-      if (L == RX_BAD || L == RX_LONG) atomicMin(count, n);
-      next[0] = ~0ull;
+      if (l0) {
+        offsets[n] = 4 * w;
+        if (L == RX_BAD || L == RX_LONG) atomicMin(count, n);
+        next[0] = ~0ull;
+      }
       return;
     }
-    if (rx_len(ops, table, rx_global{s}, len, 4 * w, maxlen) != RX_LONG) {  // a window takes it
-      next[0] = w;
-      next[1] = m;
-      next[2] = 1;
+    if (!deep && L != RX_BAD && L <= maxlen && rx_len(ops, table, rd, len, 4 * w, maxlen) != RX_LONG) {
+      // a window takes it (its parse, frames counted, does not call it long)
+      if (l0) {
+        next[0] = w;
+        next[1] = m;
+        next[2] = 1;
+      }
       return;
     }
-    const uint32_t L = rx_len(ops, table, rx_global{s}, len, 4 * w, 0xffffffffu,
-                              rx_slab_frames{slab, XDRG_MAX_FRAMES, 0});
-    offsets[m] = 4 * w;
+    if (l0) offsets[m] = 4 * w;
     if (L == RX_BAD || L == RX_LONG) {  // a record the decode rejects
-      atomicMin(count, m);
-      next[0] = ~0ull;
+      if (l0) {
+        atomicMin(count, m);
+        next[0] = ~0ull;
+      }
       return;
     }
     ++m;
     w += L / 4;
   }
-  next[0] = w;
-  next[1] = m;
-  next[2] = 0;
+  if (l0) {
+    next[0] = w;
+    next[1] = m;
+    next[2] = 0;
+  }
 }
 
 // xdrg_encode_sizes of a fixed plan: the total is known.
@@ -1531,6 +1604,47 @@ int run_fixed(const xdrg_plan &p, const dev_tables &T, bool decode, const void *
     return XDRG_OK;
   }
   if (!aligned(in, 4) || !aligned(out, 4)) return XDRG_EALIGN;
+  // Tile path (kernels.h k_fixed_tile): records of up to 16 words each way,
+  // up to 2 terms per output word, no decode checks.  numerics 1M: 16.5 us
+  // vs the group kernel's 19.5 (profiles/r05l, r05m; FIXED_PATH 3 runs it).
+  if (!checks && O.fixed_path == 0 && aligned(in, 16) && aligned(out, 16) && pg.in_words <= 16 &&
+      pg.out_words <= 16 && pg.in_words && pg.out_words) {
+    uint32_t kt = 0;
+    for (const term_idx &ix : pg.idx) kt = std::max<uint32_t>(kt, ix.count);
+    auto go = [&](auto tp) -> int {
+      for (uint32_t j = 0; j < pg.out_words; ++j) {
+        const term_idx ix = pg.idx[j];
+        tp.nterm[j] = ix.count;
+        for (uint32_t k = 0; k < ix.count; ++k) {
+          const term &t = pg.terms[ix.start + k];
+          tp.src[j][k] = t.src;
+          tp.sel[j][k] = t.kind == T_BOOL ? (kGrpBool | t.sel) : t.sel;
+        }
+      }
+      const uint64_t ntiles = (nrec + kTileRec - 1) / kTileRec;
+      constexpr int KT = sizeof(tp.src[0]) / sizeof(uint32_t);
+      const size_t lds = 4ull * (kTileRec * (pg.in_words + pg.out_words) + 4);
+      // one workgroup per resident slot: numerics 1M (25.6 KiB of LDS, 6 per
+      // CU) 16.5 us at 1536 workgroups, 18.4 at 1024, 18.6 at 2048, 22.0 at
+      // 512 (profiles/r05m)
+      uint64_t resident = 1024;
+      {
+        int dev = 0, cus = 0, occ = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_fixed_tile<16, 16, KT>, 256, lds) == hipSuccess &&
+            cus > 0 && occ > 0)
+          resident = uint64_t(cus) * uint64_t(occ);
+      }
+      const uint64_t blocks = std::min<uint64_t>(ntiles, O.grp_blocks ? uint64_t(O.grp_blocks) : resident);
+      k_fixed_tile<16, 16, KT><<<static_cast<uint32_t>(blocks), 256, lds, s>>>(
+          static_cast<const u32x4 *>(in), static_cast<u32x4 *>(out), nrec, pg.in_words, pg.out_words, tp);
+      HIPCHK(hipGetLastError());
+      return XDRG_OK;
+    };
+    if (kt == 1) return go(tile_prog<16, 1>{});
+    if (kt == 2) return go(tile_prog<16, 2>{});
+  }
   if (pg.grp_G && !checks && O.fixed_path != 2 && aligned(in, 16) && aligned(out, 16) &&
       nrec >= pg.grp_G) {
     // Group path over the full groups; the tail (< G records) below.
@@ -1946,7 +2060,11 @@ int var_encode(const xdrg_plan &P, const dev_tables &T, const void *d_native, ui
   // 1 drops the size pass and scan as well, each wave's base from a
   // decoupled look-back over the totals of the waves before it: slower here
   // (rpc 0.262, recvar 0.187 ms): the polls cross the XCDs' L2s
-  // (profiles/r04t).
+  // (profiles/r04t).  The look-back over totals a size pass published first
+  // (no wait on any wave's walk, no scan launch) is as slow: the record
+  // kernel 189 vs 91 us for recvar, 218 vs 117 for rpc (profiles/r05p) --
+  // the polls themselves, a kilobyte-window of uncached descriptor loads
+  // per wave, cost more than the scan they replace.
   const bool pre = SM && SM->f_enc_pre && O.enc_stream != 0 && p->max_depth <= stack_limit &&
                    64ull * max_rec < (1ull << 31) && 256u * p->spec.info.list_words <= Cs;
   // its LDS: the word list in place of the native tile (var_encode_body PRE)
@@ -2466,10 +2584,13 @@ int rx_windows(const xdrg_plan *p, const dev_tables *T, const uint8_t *s8, uint6
   HIPCHK(static_cast<hipError_t>(xdrg::fill32(d_count, 0xffffffffu, 2, s)));
   HIPCHK(static_cast<hipError_t>(xdrg::fill32(next, 0u, 6, s)));  // the chain starts at word 0, record 0
   unsigned long long h[3] = {0, 0, 0};
+  // the long-record walk's ops in LDS (up to 1,024 ops)
+  const uint32_t nops = static_cast<uint32_t>(p->ops.size());
+  const uint32_t ops_lds = nops <= 1024u ? nops * static_cast<uint32_t>(sizeof(xdrg_op)) : 0u;
   uint64_t window = len;
   for (;;) {
-    k_rx_long<<<1, 64, 0, s>>>(s8, len, XDRG_INDEX_MAX_MSG, n, T->d_ops, T->d_table, d_offsets, count, next,
-                               slab, 256u);
+    k_rx_long<<<1, 64, ops_lds, s>>>(s8, len, XDRG_INDEX_MAX_MSG, n, T->d_ops, T->d_table, d_offsets, count, next,
+                                     slab, 256u, nops, ops_lds ? 1u : 0u);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(h, next, 24, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
@@ -2533,7 +2654,7 @@ int xdrg_plan_set_option(xdrg_plan *p, int option, int64_t value) {
     if (v < 0 || v > 2) return XDRG_EINVAL;
     O.dec_kernel = v; return XDRG_OK;
   case XDRG_OPT_FIXED_PATH:
-    if (v != 0 && v != 2) return XDRG_EINVAL;
+    if (v != 0 && v != 2 && v != 3) return XDRG_EINVAL;
     O.fixed_path = v; return XDRG_OK;
   case XDRG_OPT_IMAGE_BYTES:
     if (v > (32 << 10)) return XDRG_EINVAL;
