@@ -38,6 +38,23 @@ namespace {
 
 thread_local char g_hip_err[256] = "";
 
+// This host thread's word of mapped, pinned host memory for a verdict the
+// host waits for (the record index's speculative walk): the kernel writes
+// it, the host reads it after the stream synchronises -- no device-to-host
+// copy in the stream.  Allocated once per thread (never freed: a few bytes
+// per thread that indexes); nullptr when the allocation fails.
+uint32_t *host_verdict_word() {
+  static thread_local uint32_t *w = nullptr;
+  static thread_local bool tried = false;
+  if (!tried) {
+    tried = true;
+    void *p = nullptr;
+    if (hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent) == hipSuccess)
+      w = static_cast<uint32_t *>(p);
+  }
+  return w;
+}
+
 int hip_fail(hipError_t e, const char *what) {
   snprintf(g_hip_err, sizeof g_hip_err, "%s: %s", what, hipGetErrorString(e));
   return XDRG_EHIP;
@@ -1074,13 +1091,13 @@ __global__ __launch_bounds__(256) void k_rxs_check(uint64_t *__restrict__ seg, c
   rxs_check_body(seg, nodes, nseg, len, cnt, flag);
 }
 template <bool EXACT>
-__global__ __launch_bounds__(64) void k_rxs_emit(const uint64_t *__restrict__ seg,
-                                                 const uint16_t *__restrict__ nodes,
-                                                 const unsigned long long *__restrict__ base,
-                                                 const xdrg_status *__restrict__ tot, uint64_t len, uint64_t n,
-                                                 uint64_t *__restrict__ offsets, uint64_t *__restrict__ count,
-                                                 uint32_t *__restrict__ flag) {
-  rxs_emit_body<EXACT>(seg, nodes, base, tot, len, n, offsets, count, flag);
+__global__ __launch_bounds__(256) void k_rxs_emit(const uint64_t *__restrict__ seg,
+                                                  const uint16_t *__restrict__ nodes,
+                                                  const unsigned long long *__restrict__ base,
+                                                  const xdrg_status *__restrict__ tot, uint64_t len, uint64_t n,
+                                                  uint64_t *__restrict__ offsets, uint64_t *__restrict__ count,
+                                                  uint32_t *__restrict__ flag, uint64_t nseg, uint32_t *hflag) {
+  rxs_emit_body<EXACT>(seg, nodes, base, tot, len, n, offsets, count, flag, nseg, hflag);
 }
 // The walk over a message stream's record marks (xdrg_index_msgs).
 __global__ __launch_bounds__(64) void k_rxs_walk_msgs(const uint8_t *__restrict__ s, uint64_t len,
@@ -2443,14 +2460,26 @@ int run_index(const xdrg_plan *p, const dev_tables *T, const void *d_stream, uin
     k_rxs_check<<<(ns + 255) / 256, 256, 0, s>>>(seg, nodes, L.rxs_nseg, len, cnt, flag);
     HIPCHK(hipGetLastError());
     if (int rc = launch_block_scan(cnt, base, ns, tot, nullptr, 0, s)) return rc;
-    k_rxs_emit<REC><<<ns, 64, 0, s>>>(seg, nodes, base, tot, len, max_msgs, d_offsets, d_count, flag);
+    // the verdict also into this thread's mapped host word (gate 1): the
+    // host waits for the stream alone, no copy after the kernels
+    uint32_t *hw = gate == 1 ? host_verdict_word() : nullptr;
+    uint32_t *hwd = nullptr;
+    if (hw && hipHostGetDevicePointer(reinterpret_cast<void **>(&hwd), hw, 0) != hipSuccess) hwd = nullptr;
+    if (hwd) *reinterpret_cast<volatile uint32_t *>(hw) = 0xffffffffu;
+    k_rxs_emit<REC><<<(ns + kRxsEmitWaves - 1) / kRxsEmitWaves, 64 * kRxsEmitWaves, 0, s>>>(
+        seg, nodes, base, tot, len, max_msgs, d_offsets, d_count, flag, L.rxs_nseg, hwd);
     HIPCHK(hipGetLastError());
     if (gate == 1) {
       // wait for the flag: the list ranking is launched only when a check
       // failed (its ~11 launches would otherwise cost ~45 us of skipping)
       uint32_t h = 0;
-      HIPCHK(hipMemcpyAsync(&h, flag, sizeof h, hipMemcpyDeviceToHost, s));
-      HIPCHK(hipStreamSynchronize(s));
+      if (hwd) {
+        HIPCHK(hipStreamSynchronize(s));
+        h = *reinterpret_cast<volatile uint32_t *>(hw);
+      } else {
+        HIPCHK(hipMemcpyAsync(&h, flag, sizeof h, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+      }
       if (h == 1u) return XDRG_OK;
       if (fast_only) return kIxNotHeld;
     } else {
