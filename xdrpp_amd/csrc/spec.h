@@ -16,7 +16,7 @@ constexpr int kSpecDevices = 64;
 // Interface version of the generated kernels (their parameter lists and
 // LDS layout, var_kernels.h): the source defines xdrg_spec_iface with it,
 // and a code object that carries another value is refused at load.
-constexpr unsigned kSpecIface = 11;
+constexpr unsigned kSpecIface = 12;
 
 // The generated source of a plan and the launch facts it fixes.
 struct spec_info {
@@ -39,6 +39,7 @@ struct spec_module {
   void *f_enc_lb = nullptr, *f_enc_pre = nullptr;  // word-list plans: encode walked first (look-back / sized)
   // recursive plans: the frame walks (sub_kernels.h) over the plan's ops
   void *f_sub_size = nullptr, *f_sub_depth = nullptr, *f_sub_enc = nullptr, *f_sub_dec = nullptr;
+  void *f_sub_chain = nullptr;  // the node pass (sub_kernels.h "Chains")
 };
 
 // A plan's specialized kernels: state 0 = not built yet, 1 = code object

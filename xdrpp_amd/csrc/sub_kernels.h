@@ -176,7 +176,41 @@ struct sub_pass {
   uint32_t last;                   // 1: running out of frames is xdr_stack_overflow
   uint32_t packed;                 // decode, main pass of a non-recursive plan: packed element areas
   uint32_t lines;                  // encode, main pass: the host gave each lane a 64-byte line buffer
+  // The chain log (recursive plans' size and encode main passes; see
+  // "Chains" below): null when the host gave none.
+  uint32_t *chain_of;              // per record: the chain its size walk logged, or ~0
+  uint32_t *chain_rec;             // per chain: its record
+  uint32_t *chain_end;             // per chain: the record's bytes where the chain closes
+  struct sub_node *nodes;          // the logged nodes
+  unsigned long long *chain_cnt;   // allocation counters (zeroed per call)
+  unsigned long long *node_cnt;
+  uint32_t chain_cap, node_cap;
 };
+
+// Chains.  A linked list walks in one frame (sub_tail), but one lane still
+// walks it node after node: a 500-node rp__list made the main passes one
+// lane's walk long (the encode 3.1 ms for 1M lists, its pointer chase ~2
+// us a node under the load of the million short ones).  The size pass
+// chases it anyway, so it logs the chain: at the kChainT-th frame
+// replacement of the first chain of a record to get that far (each
+// replacement opening a one-element container), every node from there to
+// the chain's end -- its element, its first byte in the record's stream
+// and its depth base -- and the record's byte count where the chain closes.
+// The encode's main pass then writes the record up to that node, jumps to
+// where the chain closes and goes on from there, and a node pass
+// (sub_chain_kernel) writes the logged nodes, one lane each: the chain in
+// parallel.  A chain that opens a container of more than one element, a
+// record the main pass does not finish, or a full log leaves the record
+// unlogged (chain_of ~0): its walk writes it all, as before.
+constexpr uint32_t kChainT = 32;
+struct sub_node {
+  uint64_t eb;     // the node's element (heap offset)
+  uint32_t s;      // its first byte, record-relative (after its count word)
+  uint32_t dbase;  // the depth levels open at its first field
+  uint32_t chain;  // its chain (~0: an unused slot)
+  uint32_t vpc;    // the chain's VECTOR op (the node ends with its count word)
+};
+constexpr uint32_t kChainChunk = 64;  // nodes a lane claims at a time
 
 enum : int { kWalkCont = -1, kWalkOk = 0, kWalkErr = 1, kWalkFull = 2 };
 
@@ -321,6 +355,49 @@ __device__ __forceinline__ void sub_records(const sub_pass &P, uint64_t n, F &&w
   for (uint64_t i = gid; i < cnt; i += lanes) walk(static_cast<uint64_t>(P.list[i]), st);
 }
 
+// The size walk's side of the chain log (see "Chains"): one per record.
+struct chain_logger {
+  sub_pass P;  // (a copy: the kernel argument's address would put it in private memory)
+  bool on;     // false: no log (deep passes, or the host gave none)
+  uint64_t r;
+  uint32_t c = ~0u;     // the chain being logged
+  uint32_t cfin = ~0u;  // the chain logged to its close
+  uint32_t lfp = 0;     // its frame level
+  bool done = false;    // the record's first chain past kChainT was met
+  uint64_t at = 0, end = 0;  // this lane's claimed node slots
+  __device__ __forceinline__ void start(uint32_t fp) {
+    const unsigned long long k = atomicAdd(P.chain_cnt, 1ull);
+    if (k >= P.chain_cap) return;
+    c = static_cast<uint32_t>(k);
+    lfp = fp;
+    P.chain_rec[c] = static_cast<uint32_t>(r);
+  }
+  __device__ __forceinline__ void add(uint64_t eb, uint64_t s, uint32_t dbase, uint32_t vpc) {
+    if (at == end) {
+      const unsigned long long a = atomicAdd(P.node_cnt, static_cast<unsigned long long>(kChainChunk));
+      if (a + kChainChunk > P.node_cap) {  // the log is full: this record walks its chain itself
+        c = ~0u;
+        return;
+      }
+      at = a;
+      end = a + kChainChunk;
+    }
+    P.nodes[at++] = sub_node{eb, static_cast<uint32_t>(s), dbase, c, vpc};
+  }
+  __device__ __forceinline__ void close(uint64_t s) {
+    P.chain_end[c] = static_cast<uint32_t>(s);
+    cfin = c;
+    c = ~0u;
+  }
+  // the walk is over (ok: it sized the record): the record's chain, and the
+  // claimed slots it did not fill marked unused
+  __device__ __forceinline__ void finish(bool ok) {
+    if (!on) return;
+    for (; at < end; ++at) P.nodes[at].chain = ~0u;
+    P.chain_of[r] = ok && c == ~0u ? cfin : ~0u;
+  }
+};
+
 // ---------------------------------------------------------------- size
 // xdr_size (xdr_traits<T>::serial_size) of one record, and with DEPTH the
 // deepest class/container level its walk enters (depth_checker,
@@ -328,14 +405,17 @@ __device__ __forceinline__ void sub_records(const sub_pass &P, uint64_t n, F &&w
 // discriminant or a record of 2^31 bytes or more; kWalkFull (op in bad_op):
 // the stack ran out.
 template <bool DEPTH, class OPS, class ST>
-__device__ int sub_size(const xdrg_op *__restrict__ ops, const uint32_t *__restrict__ table,
+__device__ __forceinline__ int sub_size(const xdrg_op *__restrict__ ops, const uint32_t *__restrict__ table,
                         sub_src_t<OPS::kImgWords> src,
-                        uint64_t &s, uint32_t &dmax, uint32_t &bad_op, uint32_t &code, ST &st) {
+                        uint64_t &s, uint32_t &dmax, uint32_t &bad_op, uint32_t &code, ST &st, chain_logger &lg) {
   uint32_t fp = 0, pc = 0, dbase = 0;
   st.lf = 0;
   auto step = [&](const auto &op) __attribute__((always_inline)) -> int {
     if (op.kind == XDRG_OP_END) {
+      // (the logged chain closes when its frame pops)
+      const bool closing = lg.c != ~0u && fp == lg.lfp && st.top(fp).left == 0u;
       if (!sub_next(ops, st, fp, pc, dbase, src.eb, src.in_heap)) return kWalkOk;
+      if (closing) lg.close(s);
       src.refresh();
       return kWalkCont;
     }
@@ -374,6 +454,17 @@ __device__ int sub_size(const xdrg_op *__restrict__ ops, const uint32_t *__restr
       src.eb = st.top(fp).eb;
       src.in_heap = true;
       src.refresh();
+      if (lg.on && tail) {  // a frame replaced: the chain log
+        if (lg.c == ~0u) {
+          if (!lg.done && st.top(fp).nf == kChainT + 1u) {  // the record's first chain this long
+            lg.done = true;
+            if (cnt == 1u) lg.start(fp);
+          }
+        } else if (fp == lg.lfp && cnt != 1u) {
+          lg.c = ~0u;  // more than one element: not a chain the node pass takes
+        }
+        if (lg.c != ~0u && fp == lg.lfp) lg.add(src.eb, s, dbase, pc);
+      }
       pc = op.arg4;
       break;
     }
@@ -424,7 +515,9 @@ __device__ __forceinline__ void sub_size_kernel(XDRG_SUB_SIZE_PARAMS) {
     const sub_src_t<OPS::kImgWords> src{native + r * stride, stride, heap, heap_len, 0, false, {}};
     uint64_t s = mark;
     uint32_t dmax = 0, bad_op = 0, code = 0, sz = kSizeErr;
-    const int rc = sub_size<DEPTH, OPS>(sops, table, src, s, dmax, bad_op, code, st);
+    chain_logger lg{P, !P.list && P.chain_of, r};
+    const int rc = sub_size<DEPTH, OPS>(sops, table, src, s, dmax, bad_op, code, st, lg);
+    lg.finish(rc == kWalkOk);
     if (rc == kWalkOk) {
       sz = static_cast<uint32_t>(s);
     } else if (rc == kWalkErr) {
@@ -494,6 +587,23 @@ struct line_writer {
   }
 };
 
+// The node pass writes a logged chain only where no field of the record can
+// fail (it fits `cap`, no stack limit): its lanes then report nothing, and a
+// record that can fail is walked whole, its error the reference's first.
+__device__ __forceinline__ bool sub_chain_writes(uint64_t off, uint32_t sz, uint64_t cap, uint32_t stack_limit) {
+  return off + sz <= cap && stack_limit == 0xffffffffu;
+}
+
+// Where an encode walk starts: the record from its first op (the
+// defaults), or a logged chain node (the node pass: its element in src,
+// record-relative byte `rel`, its body's first op and depth base, ending at
+// its chain's count word, op `stop`).  chain_end: where the record's logged
+// chain closes (record-relative; ~0: not logged), for the main pass.
+struct sub_start {
+  uint32_t pc = 0, dbase = 0, stop = ~0u, chain_end = ~0u;
+  uint64_t rel = 0;
+};
+
 // The record's walk from stream offset `off` with check(n) and the stack
 // budget before every field (marshal.h:104-108, :129-136).  Errors are
 // reported; kWalkFull when the stack ran out (op in *full_op).
@@ -502,16 +612,17 @@ __device__ __forceinline__ int sub_encode_rec(const xdrg_op *__restrict__ sops, 
                               sub_src_t<OPS::kImgWords> src,
                               line_writer &lw, uint64_t cap, uint64_t off, uint32_t sz, uint32_t mark,
                               uint32_t stack_limit, uint64_t r, unsigned long long *err, uint32_t *full_op,
-                              ST &st) {
+                              ST &st, const sub_start &at = sub_start{}) {
   const uint8_t *heap = src.heap;
   const uint64_t heap_len = src.heap_len;
-  uint64_t pos = off;
-  if (mark) {  // the message's record mark (message_t::alloc, marshal.cc:15-31)
+  uint64_t pos = off + at.rel;
+  if (mark && !at.rel) {  // the message's record mark (message_t::alloc, marshal.cc:15-31)
     if (4 > cap - min(pos, cap)) { report(err, r, kOpRecordLevel, XDRG_ERR_OVERFLOW_PUT); return kWalkErr; }
     lw.put(pos, mark_word(sz - 4u));
     pos += 4;
   }
-  uint32_t fp = 0, pc = 0, dbase = 0;
+  uint32_t fp = 0, pc = at.pc, dbase = at.dbase;
+  bool skipped = false;  // the record's first chain past kChainT was met
   st.lf = 0;
   auto step = [&](const auto &op) __attribute__((always_inline)) -> int {
     if (op.kind == XDRG_OP_END) {
@@ -591,7 +702,27 @@ __device__ __forceinline__ int sub_encode_rec(const xdrg_op *__restrict__ sops, 
         pc += 1 + op.arg2;
         break;
       }
+      if (fp == 0 && pc == at.stop) return kWalkOk;  // a logged node ends with its chain's count word
       if (!cnt) { ++pc; break; }
+      if (!skipped && fp && st.top(fp).left == 0u && st.top(fp).nf == kChainT && st.lf < XDRG_MAX_FRAMES &&
+          sub_tail(sops, pc)) {
+        // the record's first chain this long (the size walk's chain_logger
+        // met it here): logged, the node pass writes it from here on, and
+        // the walk goes on where the chain closes, its frame popped
+        skipped = true;
+        if (at.chain_end != ~0u) {
+          const sub_frame t = st.top(fp);
+          pc = t.ret();
+          dbase -= t.dsum;
+          st.lf -= t.nf;
+          st.pop(fp);
+          if (--fp) src.eb = st.top(fp).eb;
+          else src.in_heap = false;
+          src.refresh();
+          pos = off + at.chain_end;
+          break;
+        }
+      }
       bool tail = false;
       const int o = sub_open(sops, st, fp, pc, op.depth, eoff, cnt, true, &tail);
       if (o == kOpenFull) { *full_op = pc; return kWalkFull; }
@@ -643,10 +774,53 @@ __device__ __forceinline__ void sub_encode_kernel(XDRG_SUB_ENCODE_PARAMS) {
     const uint64_t o = P.list ? offsets[r] : off;
     const sub_src_t<OPS::kImgWords> src{native + r * stride, stride, heap, heap_len, 0, false, {}};
     uint32_t full_op = 0;
-    const int rc = sub_encode_rec<OPS>(sops, table, src, lw, cap, o, sz, mark, stack_limit, r, err, &full_op, st);
+    sub_start at;
+    if (!P.list && P.chain_of && sub_chain_writes(o, sz, cap, stack_limit)) {
+      const uint32_t c = P.chain_of[r];  // the record's logged chain, if any: the node pass writes it
+      if (c != ~0u) at.chain_end = P.chain_end[c];
+    }
+    const int rc = sub_encode_rec<OPS>(sops, table, src, lw, cap, o, sz, mark, stack_limit, r, err, &full_op, st, at);
     lw.flush();
     if (rc == kWalkFull) sub_full(P, r, full_op, XDRG_ERR_STACK_PUT, err);
   });
+}
+
+// The node pass (see "Chains"): every node the size walks logged, one lane
+// each, written from its element to its chain's count word at its place in
+// its record's stretch (the main pass wrote the record's offset).  A
+// record whose size walk failed is skipped; a node of a record whose main
+// pass deferred it, or whose chain was not logged to its close, writes the
+// bytes the record's own walk writes too.
+template <class OPS>
+__device__ __forceinline__ void sub_chain_kernel(XDRG_SUB_ENCODE_PARAMS) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  xdrg_op *sops = reinterpret_cast<xdrg_op *>(smem);
+  load_ops(sops, ops, nops);
+  (void)block_base;
+  (void)mark;
+  const uint64_t total = min(static_cast<uint64_t>(*P.node_cnt), static_cast<uint64_t>(P.node_cap));
+  const uint64_t lanes = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  line_writer lw{nullptr, xdr, ~0ull, 0u, false};
+  for (uint64_t k = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; k < total; k += lanes) {
+    const sub_node e = P.nodes[k];
+    if (e.chain >= P.chain_cap) continue;  // an unused slot
+    const uint64_t r = P.chain_rec[e.chain];
+    if (r >= n) continue;
+    const uint32_t sz = sizes[r];
+    if ((sz & kSizeErr) || !sub_chain_writes(offsets[r], sz, cap, stack_limit)) continue;
+    sub_src_t<OPS::kImgWords> src{native + r * stride, stride, heap, heap_len, e.eb, true, {}};
+    src.refresh();
+    sub_start at;
+    at.pc = sops[e.vpc].arg4;
+    at.dbase = e.dbase;
+    at.stop = e.vpc;
+    at.rel = e.s;
+    reg_stack st;
+    uint32_t full_op = 0;
+    // (a node nested past the main pass's frames belongs to a record the deep
+    // passes write whole: kWalkFull needs nothing here)
+    (void)sub_encode_rec<OPS>(sops, table, src, lw, cap, offsets[r], sz, 0u, stack_limit, r, err, &full_op, st, at);
+  }
 }
 
 // -------------------------------------------------------------- decode

@@ -822,6 +822,9 @@ __global__ __launch_bounds__(256) void k_sub_size(XDRG_SUB_SIZE_PARAMS) {
 __global__ __launch_bounds__(256) void k_sub_encode(XDRG_SUB_ENCODE_PARAMS) {
   sub_encode_kernel<rt_ops>(XDRG_SUB_ENCODE_ARGS);
 }
+__global__ __launch_bounds__(256) void k_sub_chain(XDRG_SUB_ENCODE_PARAMS) {
+  sub_chain_kernel<rt_ops>(XDRG_SUB_ENCODE_ARGS);
+}
 __global__ __launch_bounds__(256) void k_sub_decode(XDRG_SUB_DECODE_PARAMS) {
   sub_decode_kernel<rt_ops>(XDRG_SUB_DECODE_ARGS);
 }
@@ -1811,10 +1814,17 @@ static_assert(kDeepLanesA % 256 == 0, "deep pass A runs 256-lane workgroups");
 constexpr uint64_t kDeepSlabBytes =
     sizeof(sub_frame) * (uint64_t(kDeepLanesA) * kDeepSlabA + uint64_t(kDeepLanesB) * kDeepSlabB);
 
-// [two counters | 256][list A: n u32][list B: n u32][slab A][slab B]
+// The chain log (sub_kernels.h "Chains"): chains and logged nodes.
+constexpr uint32_t kChainCap = 1u << 16, kNodeCap = 1u << 20;  // 24 MiB of nodes
+constexpr uint32_t kChainGrid = 512;  // node pass workgroups (256 lanes, grid-stride over the nodes)
+constexpr uint64_t kChainLogBytes = 8ull * kChainCap + sizeof(sub_node) * uint64_t(kNodeCap);
+
+// [four counters | 256][list A: n u32][list B: n u32][slab A][slab B]
+// [chain of each record: n u32][chain records, chain ends: kChainCap u32 each][nodes]
 uint64_t deep_area_bytes(const xdrg_plan &p, uint64_t n) {
   if (!p.deep) return 0;
-  return 256 + align_up(8 * std::max<uint64_t>(n, 1), 256) + kDeepSlabBytes;
+  const uint64_t cap = std::max<uint64_t>(n, 1);
+  return 256 + align_up(8 * cap, 256) + kDeepSlabBytes + align_up(4 * cap, 256) + kChainLogBytes;
 }
 
 struct deep_passes {
@@ -1833,14 +1843,23 @@ int deep_setup(const xdrg_plan &p, uint64_t n, void *area, size_t area_bytes, hi
   if (n > 0xffffffffull) return XDRG_EUNSUPPORTED;  // u32 list entries
   if (!area || area_bytes < deep_area_bytes(p, n) || !aligned(area, 256)) return XDRG_ESPACE;
   uint8_t *d = static_cast<uint8_t *>(area);
-  if (reset) HIPCHK(static_cast<hipError_t>(xdrg::fill32(d, 0u, 4, s)));
+  if (reset) HIPCHK(static_cast<hipError_t>(xdrg::fill32(d, 0u, 8, s)));  // (the lists' and the log's counters)
   auto *cnt = reinterpret_cast<unsigned long long *>(d);
   const uint64_t cap = std::max<uint64_t>(n, 1);
   uint32_t *la = reinterpret_cast<uint32_t *>(d + 256), *lb = la + cap;
   sub_frame *sa = reinterpret_cast<sub_frame *>(d + 256 + align_up(8 * cap, 256));
   sub_frame *sb = sa + uint64_t(kDeepLanesA) * kDeepSlabA;
+  uint8_t *lg = d + 256 + align_up(8 * cap, 256) + kDeepSlabBytes;
   dp.on = true;
   dp.main = sub_pass{nullptr, nullptr, la, cnt, nullptr, 0, 0};
+  dp.main.chain_of = reinterpret_cast<uint32_t *>(lg);
+  dp.main.chain_rec = reinterpret_cast<uint32_t *>(lg + align_up(4 * cap, 256));
+  dp.main.chain_end = dp.main.chain_rec + kChainCap;
+  dp.main.nodes = reinterpret_cast<sub_node *>(dp.main.chain_end + kChainCap);
+  dp.main.chain_cnt = cnt + 2;
+  dp.main.node_cnt = cnt + 3;
+  dp.main.chain_cap = kChainCap;
+  dp.main.node_cap = kNodeCap;
   dp.A = sub_pass{la, cnt, lb, cnt + 1, sa, kDeepSlabA, 0};
   dp.B = sub_pass{lb, cnt + 1, nullptr, nullptr, sb, kDeepSlabB, 1};
   return XDRG_OK;
@@ -2137,6 +2156,10 @@ int var_encode(const xdrg_plan &P, const dev_tables &T, const void *d_native, ui
     if (ep.on) {
       HIPCHK(go(kDeepLanesA / 256, 256, ep.A));
       HIPCHK(go(1, kDeepLanesB, ep.B));
+      // the node pass: the logged chains' nodes (sub_kernels.h "Chains")
+      void *cf = FM ? FM->f_sub_chain : nullptr;
+      HIPCHK(frame_launch(k_sub_chain, cf, kChainGrid, 256, lds_ops, s, nat8, n, p->stride, d_heap, heap_len, xdr8,
+                          cap, d_offsets, sizes, bbase, T.d_ops, nops, T.d_table, stack_limit, mark, err, ep.main));
     }
     return XDRG_OK;
   }
