@@ -312,6 +312,53 @@ def test_gpu_tail_cycle_ends(dev, spec):
     assert time.perf_counter() - t0 < 30
 
 
+def chain_lists(lens):
+    """rp__list records of the given node counts (node i of list r: r_prog
+    100000 + i, strings of a few letters)."""
+    return [[node_value("rp__list", [100000 + i, (r + i) % 5, "61" * ((i + r) % 9), "62" * ((3 * i + r) % 25),
+                                     "63" * ((5 * i) % 13)]) for i in range(k)] for r, k in enumerate(lens)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("spec", [1, 0])
+def test_gpu_chain_log(dev, spec):
+    """The chain log (sub_kernels.h "Chains"): the size walk logs a record's
+    first tail chain past kChainT (32) replacements, the encode's main pass
+    jumps over it and the node pass writes it, one lane a node.  Lists of 1
+    to 700 nodes around the threshold encode to the restatement's bytes; a
+    capacity that ends inside a logged chain, and stack limits that end
+    inside one, fail at the restatement's record and op (those records are
+    walked whole: the node pass writes only records that cannot fail)."""
+    from xdrpp_amd import marshal as M
+    lens = [1, 31, 32, 33, 34, 35, 2, 64, 200, 3, 33, 700, 5, 100]
+    chains = chain_lists(lens)
+    n, cp = len(chains), plan_of("rp__list")
+    mar = M.Marshaler(M.Plan(S.rp__list, {"specialize": spec}), dev)
+    nat, heap = stage_chains("rp__list", chains)
+    dn, dh = _dev(nat, dev), _dev(heap, dev)
+    want, woffs = O.encode(cp, nat, n, heap)
+    r = mar.encode(dn, n, dh)
+    assert np.array_equal(r.xdr.cpu().numpy(), want)
+    assert np.array_equal(r.offsets.cpu().numpy().astype(np.uint64), woffs)
+    # a capacity inside the 700-node list's chain (record 11), past its 40th node
+    k = lens.index(700)
+    cap = int(woffs[k]) + 40 * 60
+    with pytest.raises(O.OracleError) as oe:
+        O.encode(cp, nat, n, heap, cap=cap)
+    with pytest.raises(M.XdrOverflow) as e:
+        mar.encode(dn, n, dh, capacity=cap)
+    assert (e.value.record, e.value.op) == (oe.value.record, oe.value.op)
+    for L in (40, 150, 650):
+        with pytest.raises(O.OracleError) as oe:
+            O.encode(cp, nat, n, heap, stack_limit=L)
+        with pytest.raises(M.XdrStackOverflow) as e:
+            mar.encode(dn, n, dh, stack_limit=L, capacity=int(woffs[-1]))
+        assert (e.value.record, e.value.op) == (oe.value.record, oe.value.op)
+    # the decode of the same bytes
+    nat2, heap2 = mar.decode(_dev(want, dev), n, _dev(woffs.astype(np.int64), dev))
+    assert unstage_chains("rp__list", nat2.cpu().numpy(), heap2.cpu().numpy(), n) == chains
+
+
 @pytest.mark.parametrize("name", TYPES)
 def test_host_index_records(gold, name):
     """decode()'s host fallback finds the same record boundaries as the
