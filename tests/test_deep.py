@@ -359,6 +359,69 @@ def test_gpu_chain_log(dev, spec):
     assert unstage_chains("rp__list", nat2.cpu().numpy(), heap2.cpu().numpy(), n) == chains
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("spec", [1, 0])
+def test_gpu_wave_pass(dev, spec):
+    """The decode's wave pass (sub_kernels.h "Long records"): records of 4
+    KiB or more are walked by a whole wave from LDS blocks of the stream.
+    Lists of 1 to 1000 nodes on both sides of the threshold (and of the 8 KiB
+    block) decode to the restatement's native records and heap bit for bit,
+    mixed with test_recursive chains too deep for the wave's frames (deep
+    pass A takes them).  Damaged long records -- a string length past the
+    record, a bad count, a stack limit inside the list, a record cut short --
+    fail at the restatement's record, op and code."""
+    from xdrpp_amd import marshal as M
+    lens = [1, 700, 3, 60, 64, 69, 70, 140, 141, 200, 2, 1000, 5, 130]
+    chains = chain_lists(lens)
+    n, cp = len(chains), plan_of("rp__list")
+    mar = M.Marshaler(M.Plan(S.rp__list, {"specialize": spec}), dev)
+    nat, heap = stage_chains("rp__list", chains)
+    x, offs = O.encode(cp, nat, n, heap)
+    sizes = np.diff(offs.astype(np.int64))
+    assert (sizes >= 4096).sum() >= 6 and (sizes < 4096).sum() >= 6 and (sizes > 8192).sum() >= 3
+    dx, do = _dev(x, dev), _dev(offs.astype(np.int64), dev)
+    nat2, heap2 = mar.decode(dx, n, do)
+    onat, oheap = O.decode(cp, x, n, offs)
+    assert np.array_equal(nat2.cpu().numpy(), onat) and np.array_equal(heap2.cpu().numpy(), oheap)
+    assert unstage_chains("rp__list", nat2.cpu().numpy(), heap2.cpu().numpy(), n) == chains
+
+    def same_error(xb, ob, **kw):
+        with pytest.raises(O.OracleError) as oe:
+            O.decode(cp, xb, n, ob, **kw)
+        with pytest.raises(M.XdrRuntimeError) as e:
+            mar.decode(_dev(xb, dev), n, _dev(ob.astype(np.int64), dev), **kw)
+        assert (e.value.record, e.value.op, e.value.code) == (oe.value.record, oe.value.op, oe.value.code)
+
+    k = lens.index(1000)
+    base = int(offs[k])
+    for at, word in ((base + 40 * 60, 0x7FFF0000), (base + 4000, 0x00000005), (base + 9000, 0xFFFFFFFF),
+                     (base + 20000, 0x00000002)):
+        xb = x.copy()
+        xb[at & ~3:(at & ~3) + 4] = np.frombuffer(word.to_bytes(4, "big"), np.uint8)
+        try:
+            on, oh = O.decode(cp, xb, n, offs)
+        except O.OracleError:
+            same_error(xb, offs)
+        else:  # (the word fell in a payload)
+            gn, gh = mar.decode(_dev(xb, dev), n, do)
+            assert np.array_equal(gn.cpu().numpy(), on) and np.array_equal(gh.cpu().numpy(), oh)
+    for L in (40, 150, 650):
+        same_error(x, offs, stack_limit=L)
+    cut = offs.copy()
+    cut[k + 1:] -= 8  # record k loses its last two words, the rest shift
+    same_error(x[:int(cut[-1])].copy(), cut)
+    # deep test_recursive chains (not tail containers: a frame a node) past the threshold
+    tr = plan_of("test_recursive")
+    mt = M.Marshaler(M.Plan(S.test_recursive, {"specialize": spec}), dev)
+    parts = [chain_stream(d) for d in (3, 400, 9, 1200, 2)]
+    xo = np.concatenate(parts)
+    oo = np.zeros(len(parts) + 1, dtype=np.uint64)
+    oo[1:] = np.cumsum([p.size for p in parts])
+    a, ha = mt.decode(_dev(xo, dev), len(parts), _dev(oo.astype(np.int64), dev))
+    ta, tha = O.decode(tr, xo, len(parts), oo)
+    assert np.array_equal(a.cpu().numpy(), ta) and np.array_equal(ha.cpu().numpy(), tha)
+
+
 @pytest.mark.parametrize("name", TYPES)
 def test_host_index_records(gold, name):
     """decode()'s host fallback finds the same record boundaries as the

@@ -185,7 +185,95 @@ struct sub_pass {
   unsigned long long *chain_cnt;   // allocation counters (zeroed per call)
   unsigned long long *node_cnt;
   uint32_t chain_cap, node_cap;
+  // The decode's wave pass (see "Long records" below): the main pass lists
+  // records of kWaveMin bytes or more here (null: it walks them itself);
+  // wave = 1: this launch is the wave pass (list / count are that list).
+  uint32_t *wave_list;
+  unsigned long long *wave_count;
+  uint32_t wave;
 };
+
+// Long records (decode).  A lane's walk of its record reads the stream a
+// word at a time, and on CDNA one counter covers a wave's loads and stores:
+// each read waits for every store the walk issued before it, a memory round
+// trip a field -- a 500-node rp__list took one lane 2.6 ms (profiles/r05end2).
+// The main pass lists records of kWaveMin bytes or more instead, and the
+// wave pass walks each with a whole wave in step (the same values in every
+// lane) from a block of the record in LDS (wave_rd): a read waits only on
+// LDS, and a block reload -- kWaveBlk bytes, 16 bytes a lane per load -- is
+// the one round trip per block.  Each word read goes to a scalar register
+// (readfirstlane), so the walk's values, branches and addresses are scalar
+// work.  Its frames are the main pass's (registers, tail containers); a
+// record they cannot finish goes to deep pass A as from the main pass.
+// rp_list (profiles/r05w2-w4): decode 2.60 -> 1.66 ms (main pass 0.46 ms,
+// wave pass 1.14 ms with vector values); the last 16 bytes read kept in
+// registers (a run of fields one LDS read per four words) was slower, 1.22
+// ms.  Walking the long records inside the main pass instead
+// (each wave its own, after its lanes' walks) was slower, 2.16 ms (1.83 with
+// the register line): the walks share their SIMDs with the pass's waves, and
+// two walk instances in one kernel spilled (288 bytes of scratch).
+constexpr uint32_t kWaveMin = 4096;
+constexpr uint32_t kWaveBlk = 8192;  // bytes of LDS per wave
+constexpr uint32_t kWaveWaves = 4;   // waves per workgroup of the wave pass
+
+template <class T> struct no_ref_t { using type = T; };
+template <class T> struct no_ref_t<T &> { using type = T; };
+template <class T> using no_ref = typename no_ref_t<T>::type;  // (runtime-compiled modules have no <type_traits>)
+
+// The stream as a walk reads it: a lane's own global loads ...
+struct glob_rd {
+  const uint8_t *xdr;
+  static constexpr bool kWave = false;
+  __device__ __forceinline__ uint32_t operator()(uint64_t q) const { return ld32(xdr + q); }
+};
+// ... or the wave pass's LDS block of the record [.., end) (end and every
+// position read a multiple of 4; positions below end only).
+struct wave_rd {
+  const uint8_t *xdr;
+  uint64_t end;
+  uint32_t *buf;          // kWaveBlk bytes of LDS
+  mutable uint64_t base;  // stream offset of buf[0] (16-byte aligned; ~0: none)
+  static constexpr bool kWave = true;
+  __device__ __forceinline__ uint32_t operator()(uint64_t q) const {
+    if (q < base || q - base >= kWaveBlk) {
+      const uint64_t b0 = q & ~15ull;
+      wave_sync();  // every lane past its reads of the old block
+#pragma unroll
+      for (uint32_t j = 0; j < kWaveBlk / 1024u; ++j) {
+        const uint32_t k = (threadIdx.x & 63u) + 64u * j;
+        const uint64_t o = b0 + 16ull * k;
+        u32x4 v{0u, 0u, 0u, 0u};
+        if (o + 16 <= end) {
+          v = ld16u(xdr + o);
+        } else if (o < end) {
+          v.x = ld32(xdr + o);
+          if (o + 8 <= end) v.y = ld32(xdr + o + 4);
+          if (o + 12 <= end) v.z = ld32(xdr + o + 8);
+        }
+        *reinterpret_cast<u32x4 *>(buf + 4u * k) = v;
+      }
+      wave_sync();
+      base = b0;
+    }
+    // the same word in every lane: scalar from here on (the walk's values,
+    // branches and addresses become SGPR work)
+    return __builtin_amdgcn_readfirstlane(buf[(q - base) >> 2]);
+  }
+};
+__device__ __forceinline__ uint64_t rfl64(uint64_t v) {
+  return static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v))) |
+         (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32))) << 32);
+}
+// Zero `bytes` (a multiple of 4) at p: the wave pass spreads the stores over
+// its lanes (one store instruction per 256 bytes, not per word).
+template <class RD>
+__device__ __forceinline__ void zero_words(uint8_t *p, uint64_t bytes) {
+  if constexpr (RD::kWave) {
+    for (uint64_t z = 4u * (threadIdx.x & 63u); z < bytes; z += 256u) st32(p + z, 0u);
+  } else {
+    for (uint64_t z = 0; z < bytes; z += 4) st32(p + z, 0u);
+  }
+}
 
 // Chains.  A linked list walks in one frame (sub_tail), but one lane still
 // walks it node after node: a 500-node rp__list made the main passes one
@@ -351,6 +439,11 @@ __device__ __forceinline__ void sub_records(const sub_pass &P, uint64_t n, F &&w
     return;
   }
   const uint64_t cnt = *P.count, lanes = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  if (P.wave) {  // a listed record per wave, every lane on its walk
+    reg_stack st;
+    for (uint64_t i = gid / 64u; i < cnt; i += lanes / 64u) walk(static_cast<uint64_t>(P.list[i]), st);
+    return;
+  }
   slab_stack st{P.slabs + gid * P.slab, P.slab};
   for (uint64_t i = gid; i < cnt; i += lanes) walk(static_cast<uint64_t>(P.list[i]), st);
 }
@@ -831,19 +924,20 @@ __device__ __forceinline__ void sub_chain_kernel(XDRG_SUB_ENCODE_PARAMS) {
 // alignment.  On a failure inside elements, each open container's rsv
 // holds 1 + the index of the element that failed, the others 0 (the
 // unstager follows these marks).  kWalkFull: the stack ran out (op in
-// *full_op), nothing reported.
-template <class OPS, class ST>
-__device__ int sub_decode_rec(const xdrg_op *__restrict__ sops, const uint32_t *__restrict__ table,
+// *full_op), nothing reported.  The stream's words come through rd
+// (glob_rd, or the wave pass's wave_rd).
+template <class OPS, class ST, class RD>
+__device__ __forceinline__ int sub_decode_rec(const xdrg_op *__restrict__ sops, const uint32_t *__restrict__ table,
                               const uint8_t *__restrict__ xdr, uint64_t a, uint64_t b, uint8_t *__restrict__ rec,
                               uint32_t stride, uint8_t *__restrict__ heap, uint64_t ecur, uint64_t eend,
                               uint32_t stack_limit, uint64_t r, unsigned long long *err, uint32_t *full_op,
-                              ST &st, bool defer) {
-  for (uint32_t k = 0; k < stride / 4; ++k) st32(rec + 4 * k, 0u);
+                              ST &st, bool defer, const RD &rd) {
+  zero_words<RD>(rec, stride & ~3u);
   uint64_t p = a;
   // (The stream through a 32-byte read-ahead, two aligned 16-byte chunks
   // serving up to 8 words per round trip, measured slower: rp_list's decode
   // 3.94 vs 2.76 ms, profiles/r05o.)
-  auto word = [&](uint64_t q) -> uint32_t { return ld32(xdr + q); };
+  auto word = [&](uint64_t q) -> uint32_t { return rd(q); };
   uint32_t fp = 0, pc = 0, dbase = 0, code = 0;
   st.lf = 0;
   uint64_t eb = 0;
@@ -882,7 +976,14 @@ __device__ int sub_decode_rec(const xdrg_op *__restrict__ sops, const uint32_t *
     case XDRG_OP_OPAQUE: {
       const uint32_t L = op.arg0;
       if (rem < L) { code = XDRG_ERR_OVERFLOW_GET; break; }
-      for (uint32_t k = 0; k < L; ++k) nat[op.noff + k] = xdr[p + k];
+      if constexpr (RD::kWave) {
+        for (uint32_t q = 0; q < L; q += 4) {
+          const uint32_t w = word(p + q);
+          for (uint32_t k = 0; k < 4u && q + k < L; ++k) nat[op.noff + q + k] = uint8_t(w >> (8u * k));
+        }
+      } else {
+        for (uint32_t k = 0; k < L; ++k) nat[op.noff + k] = xdr[p + k];
+      }
       if ((L & 3u) && (word(p + (L & ~3u)) & ~keep_mask(L & 3u))) { code = XDRG_ERR_NONZERO_PAD; break; }
       p += (L + 3u) & ~3u; ++pc; break;
     }
@@ -954,7 +1055,7 @@ __device__ int sub_decode_rec(const xdrg_op *__restrict__ sops, const uint32_t *
       if (o == kOpenFull) { *full_op = pc; return kWalkFull; }
       if (o == kOpenOver) { code = XDRG_ERR_STACK_GET; break; }
       uint8_t *arr = heap + ecur;
-      for (uint64_t z = 0; z < (bytes & ~3ull); z += 4) st32(arr + z, 0u);
+      zero_words<RD>(arr, bytes & ~3ull);
       for (uint64_t z = bytes & ~3ull; z < bytes; ++z) arr[z] = 0;
       dbase += op.depth;
       eb = ecur;
@@ -1085,13 +1186,31 @@ __device__ __forceinline__ void sub_decode_kernel(XDRG_SUB_DECODE_PARAMS) {
         if (c) { report(err, r, kOpRecordLevel, c); return; }
       }
       if ((b - a) & 3u) { report(err, r, kOpRecordLevel, XDRG_ERR_SIZE_NOT_MULT4); return; }
+      if (P.wave_list && b - a >= kWaveMin && !(a & 3u)) {  // the wave pass walks it
+        P.wave_list[atomicAdd(P.wave_count, 1ull)] = static_cast<uint32_t>(r);
+        return;
+      }
     }
     uint32_t full_op = 0;
     const bool pk = P.packed && !P.list;
-    if (sub_decode_rec<OPS>(sops, table, xdr, a + mark, b, native + r * stride, stride, heap,
-                            pk ? pk_cur : ebase + static_cast<uint64_t>(F) * a,
-                            pk ? pk_end : ebase + static_cast<uint64_t>(F) * b, stack_limit, r, err, &full_op,
-                            st, P.defer != nullptr) == kWalkFull)
+    const uint64_t e0 = pk ? pk_cur : ebase + static_cast<uint64_t>(F) * a;
+    const uint64_t e1 = pk ? pk_end : ebase + static_cast<uint64_t>(F) * b;
+    if constexpr (no_ref<decltype(st)>::kRegs) {  // (the wave pass's frames are registers)
+      if (P.wave) {  // every value the wave's walk starts from, scalar
+        const uint32_t lo = (static_cast<uint32_t>(nops * sizeof(xdrg_op)) + 15u) & ~15u;
+        uint32_t *blk = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(smem) + lo) +
+                        __builtin_amdgcn_readfirstlane(threadIdx.x / 64u) * (kWaveBlk / 4u);
+        const uint64_t ru = rfl64(r), au = rfl64(a), bu = rfl64(b);
+        if (sub_decode_rec<OPS>(sops, table, xdr, au + mark, bu, native + ru * stride, stride, heap,
+                                ebase + static_cast<uint64_t>(F) * au, ebase + static_cast<uint64_t>(F) * bu,
+                                stack_limit, ru, err, &full_op, st, true, wave_rd{xdr, bu, blk, ~0ull}) == kWalkFull &&
+            !(threadIdx.x & 63u))  // (one lane lists it)
+          sub_full(P, ru, full_op, XDRG_ERR_STACK_GET, err);
+        return;
+      }
+    }
+    if (sub_decode_rec<OPS>(sops, table, xdr, a + mark, b, native + r * stride, stride, heap, e0, e1, stack_limit,
+                            r, err, &full_op, st, P.defer != nullptr, glob_rd{xdr}) == kWalkFull)
       sub_full(P, r, full_op, XDRG_ERR_STACK_GET, err);
   });
 }

@@ -1819,8 +1819,11 @@ constexpr uint32_t kChainCap = 1u << 16, kNodeCap = 1u << 20;  // 24 MiB of node
 constexpr uint32_t kChainGrid = 512;  // node pass workgroups (256 lanes, grid-stride over the nodes)
 constexpr uint64_t kChainLogBytes = 8ull * kChainCap + sizeof(sub_node) * uint64_t(kNodeCap);
 
-// [four counters | 256][list A: n u32][list B: n u32][slab A][slab B]
+// [five counters | 256][list A: n u32][list B: n u32][slab A][slab B]
 // [chain of each record: n u32][chain records, chain ends: kChainCap u32 each][nodes]
+// (The decode, which logs no chains, keeps its wave list -- sub_kernels.h
+// "Long records" -- where the chain of each record goes.)
+constexpr uint32_t kWaveGrid = 256;  // wave pass workgroups (kWaveWaves waves, a listed record per wave at a time)
 uint64_t deep_area_bytes(const xdrg_plan &p, uint64_t n) {
   if (!p.deep) return 0;
   const uint64_t cap = std::max<uint64_t>(n, 1);
@@ -1843,7 +1846,8 @@ int deep_setup(const xdrg_plan &p, uint64_t n, void *area, size_t area_bytes, hi
   if (n > 0xffffffffull) return XDRG_EUNSUPPORTED;  // u32 list entries
   if (!area || area_bytes < deep_area_bytes(p, n) || !aligned(area, 256)) return XDRG_ESPACE;
   uint8_t *d = static_cast<uint8_t *>(area);
-  if (reset) HIPCHK(static_cast<hipError_t>(xdrg::fill32(d, 0u, 8, s)));  // (the lists' and the log's counters)
+  // (the lists' and the log's counters, and the decode's wave list's)
+  if (reset) HIPCHK(static_cast<hipError_t>(xdrg::fill32(d, 0u, 10, s)));
   auto *cnt = reinterpret_cast<unsigned long long *>(d);
   const uint64_t cap = std::max<uint64_t>(n, 1);
   uint32_t *la = reinterpret_cast<uint32_t *>(d + 256), *lb = la + cap;
@@ -2342,8 +2346,22 @@ int var_decode(const xdrg_plan &P, const dev_tables &T, const void *d_xdr, uint6
     };
     sub_pass mp = dp.main;
     mp.packed = p->packed ? 1u : 0u;  // non-recursive plans: packed element areas (never deferred)
+    if (dp.on) {  // long records to the wave pass
+      mp.wave_list = dp.main.chain_of;
+      mp.wave_count = dp.main.defer_count + 4;
+    }
     HIPCHK(go(static_cast<uint32_t>((n + 255) / 256), 256, mp));
     if (dp.on) {
+      sub_pass W{};
+      W.list = mp.wave_list;
+      W.count = mp.wave_count;
+      W.defer = dp.main.defer;  // what its frames cannot finish: deep pass A
+      W.defer_count = dp.main.defer_count;
+      W.wave = 1;
+      HIPCHK(frame_launch(k_sub_decode, mf, kWaveGrid, 64 * kWaveWaves,
+                          align_up(lds, 16) + size_t(kWaveWaves) * kWaveBlk, s, xdr8, len, d_offsets, n, nat8,
+                          p->stride, T.d_ops, nops, T.d_table, stack_limit, d_heap_out, ebase, p->heap_factor, mark,
+                          err, W));
       HIPCHK(go(kDeepLanesA / 256, 256, dp.A));
       HIPCHK(go(1, kDeepLanesB, dp.B));
     }
