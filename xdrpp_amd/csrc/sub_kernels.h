@@ -191,6 +191,9 @@ struct sub_pass {
   uint32_t *wave_list;
   unsigned long long *wave_count;
   uint32_t wave;
+  // decode, main pass: the host gave each wave kWaveBlk bytes of LDS after
+  // the ops, for the stream of its 64 records (win_rd)
+  uint32_t win;
 };
 
 // Long records (decode).  A lane's walk of its record reads the stream a
@@ -225,6 +228,21 @@ struct glob_rd {
   const uint8_t *xdr;
   static constexpr bool kWave = false;
   __device__ __forceinline__ uint32_t operator()(uint64_t q) const { return ld32(xdr + q); }
+};
+// ... or, in the decode's main pass, the wave's window: the stream of its
+// 64 records (their first kWaveBlk bytes) loaded to LDS by the whole wave
+// before the walks, so a lane's read of its record waits on LDS, not on the
+// stores its walk issued before (lim = 0: no window, every read global) ...
+struct win_rd {
+  const uint8_t *xdr;
+  const uint32_t *buf;
+  uint64_t base;  // stream offset of buf[0]
+  uint32_t lim;   // bytes of the window
+  static constexpr bool kWave = false;
+  __device__ __forceinline__ uint32_t operator()(uint64_t q) const {
+    const uint64_t d = q - base;
+    return d < lim ? buf[d >> 2] : ld32(xdr + q);
+  }
 };
 // ... or the wave pass's LDS block of the record [.., end) (end and every
 // position read a multiple of 4; positions below end only).
@@ -1176,6 +1194,37 @@ __device__ __forceinline__ void sub_decode_kernel(XDRG_SUB_DECODE_PARAMS) {
       (void)packed_area(E, bad, offsets[r0], ebase, F, pk_cur, pk_end);
     }
   }
+  // the main pass's window (win_rd): [wb, wb + wl) of the stream, from the
+  // wave's first record on
+  uint64_t wb = 0;
+  uint32_t wl = 0;
+  const uint32_t *wbuf = nullptr;
+  if (P.win && !P.list) {
+    const uint64_t r0 = static_cast<uint64_t>(blockIdx.x) * blockDim.x + (threadIdx.x & ~63u);
+    if (r0 < n) {  // wave-uniform
+      const uint64_t a0 = offsets[r0], a1 = offsets[min(r0 + 64u, n)];
+      wb = a0 & ~15ull;
+      const uint64_t e = min(min(a1, len), wb + kWaveBlk);  // (offsets out of order: no window)
+      wl = e > wb && a0 <= len ? static_cast<uint32_t>(e - wb) & ~3u : 0u;
+      const uint32_t lo = (static_cast<uint32_t>(nops * sizeof(xdrg_op)) + 15u) & ~15u;
+      uint32_t *buf = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(smem) + lo) +
+                      (threadIdx.x / 64u) * (kWaveBlk / 4u);
+      for (uint32_t k = threadIdx.x & 63u; 16u * k < wl; k += 64u) {
+        const uint64_t o = wb + 16ull * k;
+        u32x4 v{0u, 0u, 0u, 0u};
+        if (16u * k + 16u <= wl) {
+          v = ld16u(xdr + o);
+        } else {
+          v.x = ld32(xdr + o);
+          if (16u * k + 8u <= wl) v.y = ld32(xdr + o + 4);
+          if (16u * k + 12u <= wl) v.z = ld32(xdr + o + 8);
+        }
+        *reinterpret_cast<u32x4 *>(buf + 4u * k) = v;
+      }
+      wave_sync();
+      wbuf = buf;
+    }
+  }
   sub_records(P, n, [&](uint64_t r, auto &st) {
     const uint64_t a = offsets[r], b = offsets[r + 1];
     if (!P.list) {  // record-level checks: the main pass reports them once
@@ -1209,9 +1258,15 @@ __device__ __forceinline__ void sub_decode_kernel(XDRG_SUB_DECODE_PARAMS) {
         return;
       }
     }
-    if (sub_decode_rec<OPS>(sops, table, xdr, a + mark, b, native + r * stride, stride, heap, e0, e1, stack_limit,
-                            r, err, &full_op, st, P.defer != nullptr, glob_rd{xdr}) == kWalkFull)
-      sub_full(P, r, full_op, XDRG_ERR_STACK_GET, err);
+    int rc;
+    if constexpr (no_ref<decltype(st)>::kRegs)  // main pass
+      rc = sub_decode_rec<OPS>(sops, table, xdr, a + mark, b, native + r * stride, stride, heap, e0, e1,
+                               stack_limit, r, err, &full_op, st, P.defer != nullptr,
+                               win_rd{xdr, wbuf, wb, (a & 3u) ? 0u : wl});
+    else
+      rc = sub_decode_rec<OPS>(sops, table, xdr, a + mark, b, native + r * stride, stride, heap, e0, e1,
+                               stack_limit, r, err, &full_op, st, P.defer != nullptr, glob_rd{xdr});
+    if (rc == kWalkFull) sub_full(P, r, full_op, XDRG_ERR_STACK_GET, err);
   });
 }
 

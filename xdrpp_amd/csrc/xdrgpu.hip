@@ -2350,7 +2350,11 @@ int var_decode(const xdrg_plan &P, const dev_tables &T, const void *d_xdr, uint6
       mp.wave_list = dp.main.chain_of;
       mp.wave_count = dp.main.defer_count + 4;
     }
-    HIPCHK(go(static_cast<uint32_t>((n + 255) / 256), 256, mp));
+    mp.win = dp.on ? 1u : 0u;  // the waves' stream windows (sub_kernels.h win_rd)
+    HIPCHK(frame_launch(k_sub_decode, mf, static_cast<uint32_t>((n + 255) / 256), 256,
+                        mp.win ? align_up(lds, 16) + size_t(kWaveWaves) * kWaveBlk : lds, s, xdr8, len, d_offsets,
+                        n, nat8, p->stride, T.d_ops, nops, T.d_table, stack_limit, d_heap_out, ebase,
+                        p->heap_factor, mark, err, mp));
     if (dp.on) {
       sub_pass W{};
       W.list = mp.wave_list;
