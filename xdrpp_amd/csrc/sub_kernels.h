@@ -88,29 +88,39 @@ __device__ __forceinline__ sub_frame make_frame(uint64_t eb, uint32_t left, uint
 // (DEBUG_CLR_GRAPH_PACKET_CAPTURE, on by default); the same graph replayed
 // 4 times bit-exact with the packet capture off, and graphs of
 // scratch-free kernels replay under it (profiles/r05a, r05b).
-struct reg_stack {
-  sub_frame f[kSubFrames];
+template <uint32_t K>
+struct reg_stack_t {
+  sub_frame f[K];
   __device__ __forceinline__ sub_frame &top(uint32_t) { return f[0]; }
   __device__ __forceinline__ void push(uint32_t, const sub_frame &x) {
 #pragma unroll
-    for (int j = kSubFrames - 1; j > 0; --j) f[j] = f[j - 1];
+    for (int j = K - 1; j > 0; --j) f[j] = f[j - 1];
     f[0] = x;
   }
   __device__ __forceinline__ void pop(uint32_t) {
 #pragma unroll
-    for (int j = 0; j + 1 < static_cast<int>(kSubFrames); ++j) f[j] = f[j + 1];
+    for (int j = 0; j + 1 < static_cast<int>(K); ++j) f[j] = f[j + 1];
   }
   // fn(k, frame k, frame k - 1) for each of the fp open frames (k = 0 is
   // the bottom one; its "frame below" is unused)
   template <class FN> __device__ __forceinline__ void each(uint32_t fp, FN &&fn) const {
 #pragma unroll
-    for (uint32_t j = 0; j < kSubFrames; ++j)
-      if (j < fp) fn(fp - 1u - j, f[j], f[j + 1 < kSubFrames ? j + 1 : j]);
+    for (uint32_t j = 0; j < K; ++j)
+      if (j < fp) fn(fp - 1u - j, f[j], f[j + 1 < K ? j + 1 : j]);
   }
-  __device__ __forceinline__ uint32_t cap() const { return kSubFrames; }
+  __device__ __forceinline__ uint32_t cap() const { return K; }
   static constexpr bool kRegs = true;
+  static constexpr uint32_t kCap = K;
   uint32_t lf = 0;  // the frames open, replaced ones included (sub_open)
 };
+using reg_stack = reg_stack_t<kSubFrames>;
+// The decode's wave pass ("Long records"): its frames are scalar registers,
+// fewer of them (a list takes one; a record that needs more goes to deep
+// pass A).  Eight spilled 117 SGPRs, four 30: rp_list's wave pass 0.89 ->
+// 0.81 ms (profiles/r05w7).
+constexpr uint32_t kWaveFrames = 4;
+using wave_stack = reg_stack_t<kWaveFrames>;
+static_assert(kWaveFrames != kSubFrames, "the decode tells its passes apart by their stacks' frames");
 // Deep passes: `n` frames per lane in the caller's workspace.
 struct slab_stack {
   sub_frame *f;
@@ -123,6 +133,7 @@ struct slab_stack {
   }
   __device__ __forceinline__ uint32_t cap() const { return n; }
   static constexpr bool kRegs = false;
+  static constexpr uint32_t kCap = 0;
   uint32_t lf = 0;
 };
 
@@ -446,7 +457,7 @@ __device__ __forceinline__ bool sub_next(const xdrg_op *__restrict__ ops, ST &st
 
 // The walk of one record for a pass: the main pass walks record gid, a
 // deep pass every listed record its lane owns.
-template <class F>
+template <bool WAVE = false, class F>
 __device__ __forceinline__ void sub_records(const sub_pass &P, uint64_t n, F &&walk) {
   const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (!P.list) {
@@ -457,10 +468,12 @@ __device__ __forceinline__ void sub_records(const sub_pass &P, uint64_t n, F &&w
     return;
   }
   const uint64_t cnt = *P.count, lanes = static_cast<uint64_t>(gridDim.x) * blockDim.x;
-  if (P.wave) {  // a listed record per wave, every lane on its walk
-    reg_stack st;
-    for (uint64_t i = gid / 64u; i < cnt; i += lanes / 64u) walk(static_cast<uint64_t>(P.list[i]), st);
-    return;
+  if constexpr (WAVE) {
+    if (P.wave) {  // a listed record per wave, every lane on its walk
+      wave_stack st;
+      for (uint64_t i = gid / 64u; i < cnt; i += lanes / 64u) walk(static_cast<uint64_t>(P.list[i]), st);
+      return;
+    }
   }
   slab_stack st{P.slabs + gid * P.slab, P.slab};
   for (uint64_t i = gid; i < cnt; i += lanes) walk(static_cast<uint64_t>(P.list[i]), st);
@@ -1225,7 +1238,7 @@ __device__ __forceinline__ void sub_decode_kernel(XDRG_SUB_DECODE_PARAMS) {
       wbuf = buf;
     }
   }
-  sub_records(P, n, [&](uint64_t r, auto &st) {
+  sub_records<true>(P, n, [&](uint64_t r, auto &st) {
     const uint64_t a = offsets[r], b = offsets[r + 1];
     if (!P.list) {  // record-level checks: the main pass reports them once
       if (r == n - 1 && b != len) report(err, n, kOpRecordLevel, XDRG_ERR_TRAILING);
@@ -1244,8 +1257,8 @@ __device__ __forceinline__ void sub_decode_kernel(XDRG_SUB_DECODE_PARAMS) {
     const bool pk = P.packed && !P.list;
     const uint64_t e0 = pk ? pk_cur : ebase + static_cast<uint64_t>(F) * a;
     const uint64_t e1 = pk ? pk_end : ebase + static_cast<uint64_t>(F) * b;
-    if constexpr (no_ref<decltype(st)>::kRegs) {  // (the wave pass's frames are registers)
-      if (P.wave) {  // every value the wave's walk starts from, scalar
+    if constexpr (no_ref<decltype(st)>::kCap == kWaveFrames) {  // the wave pass
+      {  // every value the wave's walk starts from, scalar
         const uint32_t lo = (static_cast<uint32_t>(nops * sizeof(xdrg_op)) + 15u) & ~15u;
         uint32_t *blk = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(smem) + lo) +
                         __builtin_amdgcn_readfirstlane(threadIdx.x / 64u) * (kWaveBlk / 4u);
@@ -1255,18 +1268,18 @@ __device__ __forceinline__ void sub_decode_kernel(XDRG_SUB_DECODE_PARAMS) {
                                 stack_limit, ru, err, &full_op, st, true, wave_rd{xdr, bu, blk, ~0ull}) == kWalkFull &&
             !(threadIdx.x & 63u))  // (one lane lists it)
           sub_full(P, ru, full_op, XDRG_ERR_STACK_GET, err);
-        return;
       }
+    } else {
+      int rc;
+      if constexpr (no_ref<decltype(st)>::kCap == kSubFrames)  // main pass
+        rc = sub_decode_rec<OPS>(sops, table, xdr, a + mark, b, native + r * stride, stride, heap, e0, e1,
+                                 stack_limit, r, err, &full_op, st, P.defer != nullptr,
+                                 win_rd{xdr, wbuf, wb, (a & 3u) ? 0u : wl});
+      else
+        rc = sub_decode_rec<OPS>(sops, table, xdr, a + mark, b, native + r * stride, stride, heap, e0, e1,
+                                 stack_limit, r, err, &full_op, st, P.defer != nullptr, glob_rd{xdr});
+      if (rc == kWalkFull) sub_full(P, r, full_op, XDRG_ERR_STACK_GET, err);
     }
-    int rc;
-    if constexpr (no_ref<decltype(st)>::kRegs)  // main pass
-      rc = sub_decode_rec<OPS>(sops, table, xdr, a + mark, b, native + r * stride, stride, heap, e0, e1,
-                               stack_limit, r, err, &full_op, st, P.defer != nullptr,
-                               win_rd{xdr, wbuf, wb, (a & 3u) ? 0u : wl});
-    else
-      rc = sub_decode_rec<OPS>(sops, table, xdr, a + mark, b, native + r * stride, stride, heap, e0, e1,
-                               stack_limit, r, err, &full_op, st, P.defer != nullptr, glob_rd{xdr});
-    if (rc == kWalkFull) sub_full(P, r, full_op, XDRG_ERR_STACK_GET, err);
   });
 }
 
