@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-large", action="store_true",
                     help="skip the 16M-record fixed-path leg (large_batch_16m)")
+    ap.add_argument("--no-shard", action="store_true",
+                    help="skip the config-5 per-rank shard leg (shard_2m: rank 0's 2M records of 16M)")
     ap.add_argument("--host-inclusive", action="store_true",
                     help="measure pinned host->device->host rates (PCIe-bound, reported apart; "
                          "on by default for rec128)")
@@ -460,6 +462,72 @@ def large_batch(mar, dev, reps=5, n=1 << 24):
             "encode_decode_gib_s": round(2 * n * mar.plan.fixed_size / GIB / ((e + d) * 1e-3), 2),
             "achieved_GBps": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4), "round_trip_ok": ok,
             "protocol": f"HIP events around each kernel, median of {reps}, device-made record bytes"}
+
+
+SHARD_SHAPES = {-1: "default (by working set)", 0: "plain, 1024 workgroups", 1: "non-temporal, one-shot grid",
+                2: "plain, one-shot grid", 3: "non-temporal, 1024 workgroups"}
+
+
+def shard_leg(dev, reps=20, world=8, n=1 << 21) -> dict:
+    """Config 5's per-rank work on one GPU: rank 0's shard of the 16M-record
+    batch (2M rec128 records, seed 0x5EED0005 over the global record index;
+    256 MiB per buffer, 512 MiB in+out per kernel -- past the 256 MiB
+    Infinity Cache), encode + decode back to back with HIP events around
+    each kernel, median of `reps`.  Bit-exact against the reference's hash of
+    the 16M stream's first 2M records (manifest rec128_mgpu_2097152).  Every
+    k_fixed_reg launch shape (XDRG_OPT_FIXED_STREAM) is timed beside the
+    default, which is the leg's result."""
+    nat_np, _ = SH.shard_inputs("rec128", n, 0, world)
+    nat = torch.from_numpy(nat_np).to(dev)
+    del nat_np
+    W_ = 128  # rec128: 128 wire bytes, native stride 128
+    xdr = torch.empty(n * W_, dtype=torch.uint8, device=dev)
+    back = torch.empty_like(nat)
+    stream = torch.cuda.current_stream()
+    s = stream.cuda_stream
+    alg = n * (128 + W_)  # bytes in + out per kernel
+    shapes = {}
+    for fs in SHARD_SHAPES:
+        plan = M.Plan(S.ALL["rec128"], {"fixed_stream": fs} if fs != -1 else None)
+        mar = M.Marshaler(plan, dev)
+        mar.status.init(s)
+        enc, dec = [], []
+        for r in range(reps + 2):
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            ev[0].record(stream)
+            mar.launch_encode(nat, n, xdr, stream=s)
+            ev[1].record(stream)
+            mar.launch_decode(xdr, n, back, stream=s)
+            ev[2].record(stream)
+            torch.cuda.synchronize()
+            if r >= 2:
+                enc.append(ev[0].elapsed_time(ev[1]))
+                dec.append(ev[1].elapsed_time(ev[2]))
+        mar.check(s)
+        e, d = float(np.median(enc)), float(np.median(dec))
+        ach = alg / ((e + d) / 2 * 1e-3) / 1e9
+        shapes[fs] = {"shape": SHARD_SHAPES[fs], "encode_ms": round(e, 4), "decode_ms": round(d, 4),
+                      "achieved_GBps": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
+                      "round_trip_ok": bool(torch.equal(back, nat))}
+    man = os.path.join(ROOT, "tests", "golden", "manifest.json")
+    h = json.load(open(man))["hashes"].get(f"rec128_mgpu_{n}") if os.path.exists(man) else None
+    bit_exact = None if h is None else hashlib.sha256(xdr.cpu().numpy().tobytes()).hexdigest() == h["xdr"]
+    best = shapes[-1]
+    res = {"records": n, "shard": f"rank 0 of {world} (config 5: {n * world} records, seed 0x5EED0005)",
+           "encode_ms": best["encode_ms"], "decode_ms": best["decode_ms"],
+           "encode_decode_gib_s": round(2 * n * W_ / GIB / ((best["encode_ms"] + best["decode_ms"]) * 1e-3), 2),
+           "achieved_GBps": best["achieved_GBps"], "frac": best["frac"],
+           "round_trip_ok": best["round_trip_ok"], "bit_exact_vs_reference": bit_exact,
+           "shapes": {SHARD_SHAPES[k]: {kk: vv for kk, vv in v.items() if kk != "shape"} for k, v in shapes.items()},
+           "protocol": f"HIP events around each kernel, median of {reps} after 2 untimed"}
+    del nat, xdr, back
+    torch.cuda.empty_cache()
+    ceil = copy_ceiling(n * W_ >> 20)  # the same bytes per buffer
+    if ceil is not None:
+        res["copy_ceiling"] = ceil
+        if "best_tb_s" in ceil:
+            res["frac_of_copy_ceiling"] = round(res["achieved_GBps"] / (ceil["best_tb_s"] * 1e3), 4)
+    return res
 
 
 def copy_ceiling(mib: int) -> dict | None:
@@ -1034,6 +1102,11 @@ def extra_legs(args, engine, line, alg_bytes):
                 lb["frac_of_copy_ceiling"] = round(lb["achieved_GBps"] / (ceil["best_tb_s"] * 1e3), 4)
         except Exception as e:  # reported, never fatal
             line["large_batch_16m"] = {"error": str(e)[:200]}
+    if plan.is_fixed and args.schema == "rec128" and not args.no_shard:
+        try:
+            line["shard_2m"] = shard_leg(nat.device)
+        except Exception as e:  # reported, never fatal
+            line["shard_2m"] = {"error": str(e)[:200]}
     headline = args.schema == "rec128"
     if (args.cold or headline) and not args.no_cold and plan.is_fixed:
         line["cold_cache"] = cold_cache(mar, nat, engine.xdr, engine.back, n, alg_bytes)

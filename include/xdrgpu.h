@@ -334,6 +334,12 @@ enum xdrg_plan_option {
                                      (xdrg_encode: each wave's base by a look-back
                                      over the byte totals of the waves before it);
                                      0 the record kernel that walks per window   */
+  XDRG_OPT_FIXED_STREAM = 16,    /* identity fixed plans (k_fixed_reg) launch
+                                     shape: -1 (default) by working set (in+out
+                                     past 384 MiB: non-temporal one-shot grid,
+                                     else plain 1024 workgroups); 0 plain 1024;
+                                     1 non-temporal one-shot; 2 plain one-shot;
+                                     3 non-temporal 1024                         */
   XDRG_OPT_INDEX_FAST = 13        /* xdrg_index_records: 1 (default) the speculative
                                      chain walk first, then the call waits for its
                                      verdict and runs the list ranking only when a

@@ -29,7 +29,7 @@ PLAN_OPTIONS = {"var_encode_kernel": 1, "var_decode_kernel": 2, "fixed_path": 3,
                 "window_bytes": 5, "enc_unroll": 6, "dec_readahead": 7, "size_linear": 8,
                 "grp_unroll": 9, "grp_blocks": 10, "grp_nontemporal": 11, "specialize": 12,
                 "index_fast": 13, "stage_bytes": 14,
-                "enc_stream": 15}
+                "enc_stream": 15, "fixed_stream": 16}
 
 OK = 0
 API_ERRORS = {-1: "EINVAL", -2: "EALIGN", -3: "EUNSUPPORTED", -4: "EHIP", -5: "ENOMEM", -6: "ESPACE"}

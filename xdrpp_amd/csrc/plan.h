@@ -112,6 +112,8 @@ struct plan_opts {
                            // (1: the host waits for its flag; 2: asynchronous; 0: off)
   int stage_bytes = -1;    // window decode of packed plans: LDS stage of a group's arrays
   int enc_stream = -1;     // word-list plans: -1 walk-first record kernel, 1 + look-back (no size pass), 0 per-window walk
+  int fixed_stream = -1;   // k_fixed_reg shape: -1 by working set, 0 plain/1024, 1 nt/one-shot, 2 plain/one-shot,
+                           // 3 nt/1024
 };
 
 }  // namespace xdrg

@@ -19,8 +19,10 @@
 //
 // Nesting is bounded only by the data (and marshaling_stack_limit).  Each
 // kernel runs as up to three passes over the same walk:
-//   main   one lane per record, kSubFrames frames in private memory; a
-//          record that needs more is appended to list A and left alone;
+//   main   one lane per record, kSubFrames frames in registers (a push or
+//          pop shifts them, so every index is a constant and the kernel uses
+//          no scratch); a record that needs more is appended to list A and
+//          left alone;
 //   deep A a fixed grid of kDeepLanesA lanes walks list A, kDeepSlabA frames
 //          per lane in the frame pool (global memory); a record that needs
 //          more goes to list B;
@@ -53,7 +55,7 @@
 namespace xdrg {
 namespace dev {
 
-constexpr uint32_t kSubFrames = XDRG_SUB_FRAMES;  // private frames of the main pass
+constexpr uint32_t kSubFrames = XDRG_SUB_FRAMES;  // register frames of the main pass
 constexpr uint32_t kReported = 0x100;  // decode: the element walk reported the error
 
 // One open container: its current element (heap byte offset), the elements

@@ -1598,9 +1598,13 @@ int run_fixed(const xdrg_plan &p, const dev_tables &T, bool decode, const void *
     const uint32_t W = p.fixed_size;
     const uint32_t cpr = W / 16;
     const uint64_t nchunks = nrec * cpr;
-    const bool streaming = nchunks * 32ull > kMallBytes * 3 / 2;  // in+out bytes > 384 MiB
+    const bool big = nchunks * 32ull > kMallBytes * 3 / 2;  // in+out bytes > 384 MiB
+    // XDRG_OPT_FIXED_STREAM picks the shape for A/B runs (bench.py shard_2m)
+    const int fs = O.fixed_stream;
+    const bool streaming = fs < 0 ? big : (fs == 1 || fs == 3);      // non-temporal accesses
+    const bool one_shot = fs < 0 ? big : (fs == 1 || fs == 2);       // one chunk per lane
     uint64_t blocks = (nchunks + 255) / 256;
-    if (!streaming) blocks = std::min<uint64_t>(blocks, 1024);
+    if (!one_shot) blocks = std::min<uint64_t>(blocks, 1024);
     if (blocks > 0x7fffffffull) return XDRG_EUNSUPPORTED;
     const uint32_t g0 = cpr / gcd32(cpr, 256);
     blocks = align_up(std::max<uint64_t>(blocks, 1), g0);
@@ -2758,6 +2762,9 @@ int xdrg_plan_set_option(xdrg_plan *p, int option, int64_t value) {
   case XDRG_OPT_ENC_STREAM:
     if (v < -1 || v > 1) return XDRG_EINVAL;
     O.enc_stream = static_cast<int>(v); return XDRG_OK;
+  case XDRG_OPT_FIXED_STREAM:
+    if (v < -1 || v > 3) return XDRG_EINVAL;
+    O.fixed_stream = v; return XDRG_OK;
   default: return XDRG_EINVAL;
   }
 }
