@@ -422,6 +422,49 @@ def test_gpu_wave_pass(dev, spec):
     assert np.array_equal(a.cpu().numpy(), ta) and np.array_equal(ha.cpu().numpy(), tha)
 
 
+def big_node_chains(lens):
+    """A recursive plan of more than 1,024 ops: 1,100 unsigned
+    fields, a string and `bignode *next` per node, and records of the given
+    node counts, staged iteratively."""
+    from xdrpp_amd.xdr_types import Pointer, String, Struct, UInt
+    t = Struct("bignode")
+    t.define([(f"f{i}", UInt) for i in range(1100)] + [("name", String()), ("next", Pointer(t))])
+    stride = OB._align_up(t.size, t.align)
+    native, heap = bytearray(len(lens) * stride), OB._Heap()
+    for r, k in enumerate(lens):
+        buf, off = native, r * stride
+        for i in range(k):
+            for j in range(1100):
+                struct.pack_into("<I", buf, off + t.offsets[f"f{j}"], (r * 7919 + i * 104729 + j) & 0xFFFFFFFF)
+            OB._put(t.fields[1100][1], buf, off + t.offsets["name"], b"n" * ((r + i) % 11), heap)
+            nxt = i + 1 < k
+            arr = heap.alloc(stride if nxt else 0, 8)
+            struct.pack_into("<QII", buf, off + t.offsets["next"], arr, 1 if nxt else 0, 0)
+            buf, off = heap.buf, arr
+    return t, np.frombuffer(bytes(native), np.uint8).copy(), np.frombuffer(bytes(heap.buf), np.uint8).copy()
+
+
+@pytest.mark.gpu
+def test_gpu_recursive_plan_past_the_wave_lds(dev):
+    """The decode's wave pass and its windows take 32 KiB of LDS beside the
+    plan's ops (32 bytes an op): a recursive plan of more than about 1,000
+    ops leaves no room for them, and its long records (4.4 KiB a node) are
+    walked by the main pass instead -- the same natives and heap as the
+    restatement, where the launch used to fail."""
+    from xdrpp_amd import marshal as M
+    lens = [1, 3, 2, 5, 1, 4]
+    t, nat, heap = big_node_chains(lens)
+    cp = compile_plan(t)
+    assert len(cp.ops) > 1024
+    n = len(lens)
+    x, offs = O.encode(cp, nat, n, heap)
+    assert int(np.diff(offs.astype(np.int64)).min()) >= 4096  # every record is a long one
+    mar = M.Marshaler(M.Plan(t, {"specialize": 0}), dev)
+    nat2, heap2 = mar.decode(_dev(x, dev), n, _dev(offs.astype(np.int64), dev))
+    onat, oheap = O.decode(cp, x, n, offs)
+    assert np.array_equal(nat2.cpu().numpy(), onat) and np.array_equal(heap2.cpu().numpy(), oheap)
+
+
 @pytest.mark.parametrize("name", TYPES)
 def test_host_index_records(gold, name):
     """decode()'s host fallback finds the same record boundaries as the

@@ -78,6 +78,12 @@
 #ifndef XDRG_ENC_PIPE
 #define XDRG_ENC_PIPE 1
 #endif
+// Payload chunks from 16-byte-aligned loads (A/B): the two aligned blocks a
+// chunk touches, joined with v_alignbyte, in place of one byte-misaligned
+// 16-byte load (tools/tune/align_probe.hip: 6.0-6.2 TB/s vs 4.3-4.5).
+#ifndef XDRG_ENC_A16
+#define XDRG_ENC_A16 0
+#endif
 
 namespace xdrg {
 namespace dev {
@@ -113,17 +119,47 @@ __device__ __forceinline__ u32x4 heap_tail16(const uint8_t *heap, uint64_t len, 
   return u32x4{v[0], v[1], v[2], v[3]};
 }
 
+// Bytes [sh, sh + 16) of the 32 bytes lo:hi (sh 1..15).
+__device__ __forceinline__ u32x4 funnel16(const u32x4 &lo, const u32x4 &hi, uint32_t sh) {
+  const uint32_t t[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  const uint32_t q = sh >> 2, sb = sh & 3u;
+  uint32_t o[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    uint32_t a = t[k], c = t[k + 1];
+#pragma unroll
+    for (int j = 1; j < 4; ++j) {
+      a = q == static_cast<uint32_t>(j) ? t[k + j] : a;
+      c = q == static_cast<uint32_t>(j) ? t[k + j + 1] : c;
+    }
+    o[k] = __builtin_amdgcn_alignbyte(c, a, sb);
+  }
+  return u32x4{o[0], o[1], o[2], o[3]};
+}
+
 // s_waitcnt vmcnt(N) that also defines `v` (loaded by inline asm the
-// compiler does not count): nothing reads v before this wait
+// compiler does not count): nothing reads v before this wait.  The loads
+// and the wait carry "; xb1" (tools/isa_audit.py pairs them in the
+// compiled code).
 template <uint32_t N, int U>
 __device__ __forceinline__ void vm_wait_after(u32x4 (&v)[U]) {
   if constexpr (U == 2)
-    asm volatile("s_waitcnt vmcnt(%2)" : "+v"(v[0]), "+v"(v[1]) : "n"(N) : "memory");
+    asm volatile("s_waitcnt vmcnt(%2) ; xb1" : "+v"(v[0]), "+v"(v[1]) : "n"(N) : "memory");
   else if constexpr (U == 4)
-    asm volatile("s_waitcnt vmcnt(%4)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]) : "n"(N) : "memory");
+    asm volatile("s_waitcnt vmcnt(%4) ; xb1" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]) : "n"(N) : "memory");
   else if constexpr (U == 8)
-    asm volatile("s_waitcnt vmcnt(%8)"
+    asm volatile("s_waitcnt vmcnt(%8) ; xb1"
                  : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7])
+                 : "n"(N) : "memory");
+}
+// the same for the two halves of the aligned batches (XDRG_ENC_A16)
+template <uint32_t N, int U>
+__device__ __forceinline__ void vm_wait_after(u32x4 (&v)[U], u32x4 (&h)[U]) {
+  if constexpr (U == 2)
+    asm volatile("s_waitcnt vmcnt(%4) ; xb1" : "+v"(v[0]), "+v"(v[1]), "+v"(h[0]), "+v"(h[1]) : "n"(N) : "memory");
+  else if constexpr (U == 4)
+    asm volatile("s_waitcnt vmcnt(%8) ; xb1"
+                 : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(h[0]), "+v"(h[1]), "+v"(h[2]), "+v"(h[3])
                  : "n"(N) : "memory");
 }
 
@@ -657,6 +693,7 @@ __device__ __forceinline__ void var_encode_body(
   // one batch of payload chunks: U per lane, chunks c0 + 64 u + lane
   struct batch {
     u32x4 val[U];
+    u32x4 hi[XDRG_ENC_A16 ? U : 1];  // XDRG_ENC_A16: the aligned block after val's
     uint64_t hs[U];
     uint32_t at[U], nb[U], rm[U];
     bool fast[U];
@@ -710,16 +747,29 @@ __device__ __forceinline__ void var_encode_body(
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const uint8_t *pa = heap + (b.fast[u] ? b.hs[u] : 0ull);
-        asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(b.val[u]) : "v"(pa));
+        if constexpr (XDRG_ENC_A16) {  // the two 16-byte blocks the chunk touches
+          const uintptr_t a = reinterpret_cast<uintptr_t>(pa);
+          const uint8_t *lo = reinterpret_cast<const uint8_t *>(a & ~uintptr_t(15));
+          asm volatile("global_load_dwordx4 %0, %1, off ; xb1" : "=v"(b.val[u]) : "v"(lo));
+          asm volatile("global_load_dwordx4 %0, %1, off ; xb1" : "=v"(b.hi[u]) : "v"((a & 15u) ? lo + 16 : lo));
+        } else {
+          asm volatile("global_load_dwordx4 %0, %1, off ; xb1" : "=v"(b.val[u]) : "v"(pa));
+        }
       }
     } else {
 #pragma unroll
       for (int u = 0; u < U; ++u)
         if (b.fast[u]) {
-          if constexpr ((XDRG_ENC_NT & 1) != 0)
+          if constexpr (XDRG_ENC_A16) {
+            const uintptr_t a = reinterpret_cast<uintptr_t>(heap + b.hs[u]);
+            const u32x4 *lo = reinterpret_cast<const u32x4 *>(a & ~uintptr_t(15));
+            b.val[u] = lo[0];
+            b.hi[u] = (a & 15u) ? lo[1] : lo[0];
+          } else if constexpr ((XDRG_ENC_NT & 1) != 0) {
             b.val[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(heap + b.hs[u]));
-          else
+          } else {
             b.val[u] = ld16u(heap + b.hs[u]);
+          }
         }
     }
     if constexpr (decltype(asm_tag)::value) asm volatile("v_mov_b32 %0, 0" : "=v"(b.tok));
@@ -731,10 +781,20 @@ __device__ __forceinline__ void var_encode_body(
     // memory before the next write of these registers)
 #pragma unroll
     for (int u = 0; u < U; ++u) asm volatile("" ::"v"(b.val[u]));
+    if constexpr (XDRG_ENC_A16) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) asm volatile("" ::"v"(b.hi[u]));
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if (!b.nb[u]) continue;
       u32x4 x = b.val[u];
+      if constexpr (XDRG_ENC_A16) {
+        if (b.fast[u]) {  // the chunk at byte sh of the two blocks
+          const uint32_t sh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(heap + b.hs[u]) & 15u);
+          if (sh) x = funnel16(b.val[u], b.hi[u], sh);
+        }
+      }
       if (!b.fast[u]) x = heap_tail16(heap, heap_len, b.hs[u]);
       const int32_t rr = static_cast<int32_t>(b.rm[u]);
       if (rr < 16) {  // zero the pad bytes after the payload (put_bytes)
@@ -885,7 +945,10 @@ __device__ __forceinline__ void var_encode_body(
       }
       // the prefetched loads were issued before these SW stores and vmcnt
       // retires in order: at most SW outstanding = every load has landed
-      if (pf) vm_wait_after<SW>(B.val);
+      // (on every path, prefetched or not: tools/isa_audit.py's dataflow
+      // then sees every batch waited for)
+      if constexpr (XDRG_ENC_A16) vm_wait_after<SW>(B.val, B.hi);
+      else vm_wait_after<SW>(B.val);
     } else if (we > ws) {
       const uint32_t nc = static_cast<uint32_t>((we - ws + 15u) >> 4);
       for (uint32_t k = lane; k < nc; k += 64u) {

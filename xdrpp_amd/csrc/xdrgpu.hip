@@ -2350,16 +2350,21 @@ int var_decode(const xdrg_plan &P, const dev_tables &T, const void *d_xdr, uint6
     };
     sub_pass mp = dp.main;
     mp.packed = p->packed ? 1u : 0u;  // non-recursive plans: packed element areas (never deferred)
-    if (dp.on) {  // long records to the wave pass
+    // the waves' stream windows (sub_kernels.h win_rd) and the wave pass
+    // take kWaveWaves * kWaveBlk bytes of LDS beside the ops: a plan whose
+    // ops leave no room for them (about 1,000 ops) walks its long records
+    // in the main pass, as without the wave pass
+    const size_t lds_win = align_up(lds, 16) + size_t(kWaveWaves) * kWaveBlk;
+    const bool wave = dp.on && lds_win <= kVarLdsBudget;
+    if (wave) {  // long records to the wave pass
       mp.wave_list = dp.main.chain_of;
       mp.wave_count = dp.main.defer_count + 4;
     }
-    mp.win = dp.on ? 1u : 0u;  // the waves' stream windows (sub_kernels.h win_rd)
-    HIPCHK(frame_launch(k_sub_decode, mf, static_cast<uint32_t>((n + 255) / 256), 256,
-                        mp.win ? align_up(lds, 16) + size_t(kWaveWaves) * kWaveBlk : lds, s, xdr8, len, d_offsets,
-                        n, nat8, p->stride, T.d_ops, nops, T.d_table, stack_limit, d_heap_out, ebase,
-                        p->heap_factor, mark, err, mp));
-    if (dp.on) {
+    mp.win = wave ? 1u : 0u;
+    HIPCHK(frame_launch(k_sub_decode, mf, static_cast<uint32_t>((n + 255) / 256), 256, wave ? lds_win : lds, s,
+                        xdr8, len, d_offsets, n, nat8, p->stride, T.d_ops, nops, T.d_table, stack_limit,
+                        d_heap_out, ebase, p->heap_factor, mark, err, mp));
+    if (wave) {
       sub_pass W{};
       W.list = mp.wave_list;
       W.count = mp.wave_count;
@@ -2370,6 +2375,8 @@ int var_decode(const xdrg_plan &P, const dev_tables &T, const void *d_xdr, uint6
                           align_up(lds, 16) + size_t(kWaveWaves) * kWaveBlk, s, xdr8, len, d_offsets, n, nat8,
                           p->stride, T.d_ops, nops, T.d_table, stack_limit, d_heap_out, ebase, p->heap_factor, mark,
                           err, W));
+    }
+    if (dp.on) {
       HIPCHK(go(kDeepLanesA / 256, 256, dp.A));
       HIPCHK(go(1, kDeepLanesB, dp.B));
     }
