@@ -74,11 +74,9 @@
 // explicit vmcnt(SW) after the SW stores (tools/gpu/isa_audit.py checks the
 // shape in the compiled code).  MI355X, 1M records, kernel alone
 // (profiles/r03f): rpc 0.1616 -> 0.1582 ms, vecrec 0.0977 -> 0.0969,
-// recvar 0.1073 -> 0.1066.  2 (walk-first kernels): windows in pairs, the
-// two first batches of a pair loaded together before the last stores of
-// the pair before it.
+// recvar 0.1073 -> 0.1066.
 #ifndef XDRG_ENC_PIPE
-#define XDRG_ENC_PIPE 2
+#define XDRG_ENC_PIPE 1
 #endif
 
 namespace xdrg {
@@ -86,18 +84,6 @@ namespace dev {
 
 // ---------------------------------------------------------------- encode
 template <bool B> struct bool_tag { static constexpr bool value = B; };
-
-// The 16 bytes t shifted down by d bytes (1..15), zeros shifted in: the
-// chunk at byte d of a 16-byte load that ends at the heap's end.
-__device__ __forceinline__ u32x4 shr_bytes16(const u32x4 &t, uint32_t d) {
-  const uint32_t w = d >> 2, sb = d & 3u;
-  const uint32_t t0 = w == 0 ? t.x : w == 1 ? t.y : w == 2 ? t.z : t.w;
-  const uint32_t t1 = w == 0 ? t.y : w == 1 ? t.z : w == 2 ? t.w : 0u;
-  const uint32_t t2 = w == 0 ? t.z : w == 1 ? t.w : 0u;
-  const uint32_t t3 = w == 0 ? t.w : 0u;
-  return u32x4{__builtin_amdgcn_alignbyte(t1, t0, sb), __builtin_amdgcn_alignbyte(t2, t1, sb),
-               __builtin_amdgcn_alignbyte(t3, t2, sb), __builtin_amdgcn_alignbyte(0u, t3, sb)};
-}
 
 // The 16 bytes at heap offset hs, bytes at or past len reading 0, for a
 // chunk within 16 bytes of the heap's end (hs + 16 > len).  One 16-byte
@@ -127,36 +113,20 @@ __device__ __forceinline__ u32x4 heap_tail16(const uint8_t *heap, uint64_t len, 
   return u32x4{v[0], v[1], v[2], v[3]};
 }
 
-// The asm payload batch K of the pipelined encode windows (K = 1, 2: the
-// two register sets of XDRG_ENC_PIPE 2); the loads and their wait carry
-// "; xb<K>" so that tools/isa_audit.py can pair them in the compiled code.
-template <int K> struct asm_batch {
-  static constexpr bool value = true;
-  static constexpr int id = K;
-};
-
-
 // s_waitcnt vmcnt(N) that also defines `v` (loaded by inline asm the
-// compiler does not count, batch ID): nothing reads v before this wait
-template <uint32_t N, int U, int ID>
+// compiler does not count): nothing reads v before this wait.  The loads
+// and the wait carry "; xb1" (tools/isa_audit.py pairs them in the
+// compiled code).
+template <uint32_t N, int U>
 __device__ __forceinline__ void vm_wait_after(u32x4 (&v)[U]) {
   if constexpr (U == 2)
-    asm volatile("s_waitcnt vmcnt(%2) ; xb%3" : "+v"(v[0]), "+v"(v[1]) : "n"(N), "n"(ID) : "memory");
+    asm volatile("s_waitcnt vmcnt(%2) ; xb1" : "+v"(v[0]), "+v"(v[1]) : "n"(N) : "memory");
   else if constexpr (U == 4)
-    asm volatile("s_waitcnt vmcnt(%4) ; xb%5" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]) : "n"(N), "n"(ID) : "memory");
+    asm volatile("s_waitcnt vmcnt(%4) ; xb1" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]) : "n"(N) : "memory");
   else if constexpr (U == 8)
-    asm volatile("s_waitcnt vmcnt(%8) ; xb%9"
+    asm volatile("s_waitcnt vmcnt(%8) ; xb1"
                  : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7])
-                 : "n"(N), "n"(ID) : "memory");
-}
-
-// the same for two batches (IDA, IDB) waited for by one s_waitcnt
-template <uint32_t N, int U, int IDA, int IDB>
-__device__ __forceinline__ void vm_wait_after2(u32x4 (&a)[U], u32x4 (&b)[U]) {
-  static_assert(U == 4, "vm_wait_after2's shape");
-  asm volatile("s_waitcnt vmcnt(%8) ; xb%9 xb%10"
-               : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3])
-               : "n"(N), "n"(IDA), "n"(IDB) : "memory");
+                 : "n"(N) : "memory");
 }
 
 // LDS of an encode wave: the native tile (kept for every window round), the
@@ -686,34 +656,24 @@ __device__ __forceinline__ void var_encode_body(
   bool ok = szok;
   uint32_t M = 0;
 
-  // one batch of payload chunks: U per lane, chunks c0 + 64 u + lane.
-  // meta[u] = nb | min(rm, 16) << 5 | fast << 10 | e << 11 | j << 15: nb
-  // the chunk's bytes to place (0: no chunk), rm the payload bytes left
-  // from the chunk (the pad mask), fast = the 16-byte load at the chunk is
-  // the chunk; else e = heap_len - the chunk's heap offset (1..15; 0: past
-  // the heap), and on a heap of 16 bytes or more the load is of the heap's
-  // last 16 bytes, shifted by 16 - e in place(); j = the chunk's image
-  // offset - the window's + 16 (a chunk of the window starts less than 16
-  // bytes before it: 0 < j < C + 16 <= 2^17).  One word of state per chunk
-  // beside its 16 bytes, so that two batches fit in registers
-  // (XDRG_ENC_PIPE 2).
+  // one batch of payload chunks: U per lane, chunks c0 + 64 u + lane
   struct batch {
     u32x4 val[U];
-    uint32_t meta[U];
-  };
-  batch B;
-  uint32_t tok = 0;  // 0, defined after the asm loads (orders the stores after them)
-  // ASM (asm_batch<K>): the loads as inline asm, which the compiler does not
-  // count: their wait is an explicit one after a window's stores
-  auto issue = [&](uint32_t c0, uint32_t chi, uint32_t w0, batch &b, auto asm_tag) {
+    uint64_t hs[U];
+    uint32_t at[U], nb[U], rm[U];
+    bool fast[U];
+    uint32_t tok;  // 0, defined after the asm loads (orders the stores after them)
+  } B;
+  B.tok = 0;
+  // ASM: the loads as inline asm, which the compiler does not count: their
+  // wait is the explicit one after the window's stores (XDRG_ENC_PIPE)
+  auto issue = [&](uint32_t c0, uint32_t chi, batch &b, auto asm_tag) {
     uint32_t lo[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) lo[u] = 0;
     uint32_t ix[U];
-    const uint8_t *pa[U];
-    bool ld[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) ix[u] = min(c0 + 64u * u + lane, max(chi, 1u) - 1u);
+    for (int u = 0; u < U; ++u) ix[u] = min(c0 + 64u * u + lane, chi - 1u);
 #pragma unroll
     for (uint32_t s = 32; s; s >>= 1) {
 #pragma unroll
@@ -722,9 +682,8 @@ __device__ __forceinline__ void var_encode_body(
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const uint32_t l = min(lo[u], 63u);
-      uint32_t rem = ix[u] - (l ? cum[l - 1u] : 0u);
-      const echunk_desc *dl = desc + l * KMAX;
+      uint32_t rem = ix[u] - (lo[u] ? cum[lo[u] - 1u] : 0u);
+      const echunk_desc *dl = desc + lo[u] * KMAX;
       echunk_desc d = dl[0];
 #pragma unroll
       for (int k = 0; k + 1 < KMAX; ++k) {
@@ -736,38 +695,37 @@ __device__ __forceinline__ void var_encode_body(
       }
       const bool live = c0 + 64u * u + lane < chi;
       const uint32_t q16 = rem << 4;
-      const uint64_t hs = d.src + q16;
-      const uint32_t rm = live ? min(d.len - q16, 16u) : 16u;
-      const uint32_t nb = live ? min(16u, ((d.len + 3u) & ~3u) - q16) : 0u;
-      const bool fast = live && hs + 16u <= heap_len;
-      const uint32_t e = hs < heap_len ? static_cast<uint32_t>(heap_len - hs) & 15u : 0u;  // < 16 when !fast
-      b.meta[u] = nb | rm << 5 | (fast ? 1u << 10 : 0u) | e << 11 | (d.dst + q16 + 16u - w0) << 15;
-      ld[u] = fast || (live && e && heap_len >= 16);
-      pa[u] = heap + (fast ? hs : heap_len >= 16 ? heap_len - 16 : 0ull);
+      b.hs[u] = d.src + q16;
+      b.rm[u] = live ? d.len - q16 : 16u;
+      b.at[u] = d.dst + q16;
+      b.nb[u] = live ? min(16u, ((d.len + 3u) & ~3u) - q16) : 0u;
+      b.fast[u] = live && b.hs[u] + 16u <= heap_len;
     }
     if constexpr (decltype(asm_tag)::value) {
-      // every lane loads (a lane with no chunk: the heap's last 16 bytes --
-      // the pipelined windows run only on heaps of 16 bytes or more), so the
-      // batch is straight-line code (tools/isa_audit.py).  (Dword-aligned
-      // loads of 16 bytes plus the next word joined with v_alignbyte, in
-      // place of these byte-misaligned ones: recvar 0.0998 vs 0.0957 ms, rpc
-      // 0.1385 vs 0.1361, slower; profiles/r05h/ab_align.log.)
+      // every lane loads (a lane with no fast chunk: the heap's first 16
+      // bytes -- the pipelined windows run only on heaps of 16 bytes or
+      // more), so the batch is straight-line code before the stores and
+      // their wait (tools/isa_audit.py).  (Dword-aligned loads of 16 bytes
+      // plus the next word joined with v_alignbyte, in place of these
+      // byte-misaligned ones: recvar 0.0998 vs 0.0957 ms, rpc 0.1385 vs
+      // 0.1361, slower; profiles/r05h/ab_align.log.)
 #pragma unroll
-      for (int u = 0; u < U; ++u)
-        // "+v": the load's register is the batch's (tied to its last
-        // value), so a loop that carries the batch keeps it in place
-        asm volatile("global_load_dwordx4 %0, %1, off ; xb%2" : "+v"(b.val[u]) : "v"(pa[u]), "n"(decltype(asm_tag)::id));
-      asm volatile("v_mov_b32 %0, 0" : "=v"(tok));
+      for (int u = 0; u < U; ++u) {
+        const uint8_t *pa = heap + (b.fast[u] ? b.hs[u] : 0ull);
+        asm volatile("global_load_dwordx4 %0, %1, off ; xb1" : "=v"(b.val[u]) : "v"(pa));
+      }
     } else {
 #pragma unroll
       for (int u = 0; u < U; ++u)
-        if (ld[u]) {
-          if constexpr ((XDRG_ENC_NT & 1) != 0)
-            b.val[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(pa[u]));
-          else
-            b.val[u] = ld16u(pa[u]);
+        if (b.fast[u]) {
+          if constexpr ((XDRG_ENC_NT & 1) != 0) {
+            b.val[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(heap + b.hs[u]));
+          } else {
+            b.val[u] = ld16u(heap + b.hs[u]);
+          }
         }
     }
+    if constexpr (decltype(asm_tag)::value) asm volatile("v_mov_b32 %0, 0" : "=v"(b.tok));
     __builtin_amdgcn_sched_barrier(0);
   };
   auto place = [&](batch &b, uint32_t w0) {
@@ -778,37 +736,28 @@ __device__ __forceinline__ void var_encode_body(
     for (int u = 0; u < U; ++u) asm volatile("" ::"v"(b.val[u]));
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const uint32_t m = b.meta[u];
-      const uint32_t nb = m & 31u;
-      if (!nb) continue;
+      if (!b.nb[u]) continue;
       u32x4 x = b.val[u];
-      if (!(m & (1u << 10))) {  // within 16 bytes of the heap's end
-        const uint32_t e = (m >> 11) & 15u;
-        if (heap_len >= 16)
-          x = e ? shr_bytes16(x, 16u - e) : u32x4{0u, 0u, 0u, 0u};
-        else
-          x = heap_tail16(heap, heap_len, heap_len - e);
-      }
-      const int32_t rr = static_cast<int32_t>((m >> 5) & 31u);
+      if (!b.fast[u]) x = heap_tail16(heap, heap_len, b.hs[u]);
+      const int32_t rr = static_cast<int32_t>(b.rm[u]);
       if (rr < 16) {  // zero the pad bytes after the payload (put_bytes)
         x.x &= keep_bytes(rr);
         x.y &= keep_bytes(rr - 4);
         x.z &= keep_bytes(rr - 8);
         x.w &= keep_bytes(rr - 12);
       }
-      const uint32_t at = w0 + (m >> 15) - 16u;  // image offset of the chunk
-      const uint32_t j = at - w0;
-      if (j + 16u <= C && at >= w0) {
+      const uint32_t j = b.at[u] - w0;
+      if (j + 16u <= C && b.at[u] >= w0) {
         uint32_t *wp = reinterpret_cast<uint32_t *>(img + j);
         wp[0] = x.x;
-        if (nb > 4u) wp[1] = x.y;
-        if (nb > 8u) wp[2] = x.z;
-        if (nb > 12u) wp[3] = x.w;
+        if (b.nb[u] > 4u) wp[1] = x.y;
+        if (b.nb[u] > 8u) wp[2] = x.z;
+        if (b.nb[u] > 12u) wp[3] = x.w;
       } else {  // a chunk across a window edge
-        c.wput(at, x.x);
-        if (nb > 4u) c.wput(at + 4, x.y);
-        if (nb > 8u) c.wput(at + 8, x.z);
-        if (nb > 12u) c.wput(at + 12, x.w);
+        c.wput(b.at[u], x.x);
+        if (b.nb[u] > 4u) c.wput(b.at[u] + 4, x.y);
+        if (b.nb[u] > 8u) c.wput(b.at[u] + 8, x.z);
+        if (b.nb[u] > 12u) c.wput(b.at[u] + 12, x.w);
       }
     }
   };
@@ -817,132 +766,9 @@ __device__ __forceinline__ void var_encode_body(
   // stretch) is kept by lane 0 and written last, word by word
   constexpr uint32_t SW = CMAX / 1024u;
   constexpr bool kPipe = XDRG_ENC_PIPE && SW > 0 && (U == 2 || U == 4 || U == 8);  // vm_wait_after's shapes
-  // two windows' payload batches in flight (XDRG_ENC_PIPE >= 2): walk-first
-  // kernels, whose walk is done before the windows, so the window loop
-  // (two windows per iteration, each batch in its own registers) holds no
-  // walk
-  constexpr bool kPipe2 = kPipe && XDRG_ENC_PIPE >= 2 && PRE != 0 && U == 4;  // vm_wait_after2's shape
   const bool pipe = kPipe && C <= CMAX && wave_out + T <= cap && heap_len >= 16;
   bool pf = false;
   u32x4 head = u32x4{0u, 0u, 0u, 0u};
-  // the lanes' slots and inclusive chunk counts, for the chunk pass
-  auto slots = [&]() {
-    XDRG_STAMP(2);
-    uint32_t nch = 0;
-#pragma unroll
-    for (int k = 0; k < KMAX; ++k) {
-      desc[lane * KMAX + k] = echunk_desc{c.psr[k], c.pds[k], c.pln[k]};
-      nch += (c.pln[k] + 15u) >> 4;
-    }
-    const uint32_t ci = wave_incl_scan(nch);
-    cum[lane] = ci;
-    M = rl32(ci, 63);
-    XDRG_STAMP(3);
-  };
-  // the payload chunks of window [w0, w0 + C): Chunk i of the wave (stream
-  // order) belongs to the lane L with cum[L-1] <= i < cum[L] (binary search)
-  // and to the first of its slots whose chunks reach past i - cum[L-1]
-  auto range_lo = [&](uint32_t w0) { return rl32(wave_incl_scan(chunks_ending_by(c, w0)), 63); };
-  auto range_hi = [&](uint32_t w0) { return min(M, rl32(wave_incl_scan(chunks_starting_before(c, w0 + C)), 63)); };
-  // a full window (pipelined): SW buffer stores per lane, none skipped by a
-  // branch; the wave's head chunk is kept by lane 0 and written last
-  auto store_full = [&](uint32_t rd, uint64_t ws, bool keep_head) {
-    if (keep_head && rd == 0 && sh && lane == 0) head = *reinterpret_cast<const u32x4 *>(img);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>(xdr + ws) >> 32));
-    const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>(xdr + ws)));
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<void *>((static_cast<uint64_t>(hi) << 32) | lo), 0, C, 0x00020000);
-    const uint32_t nc = C >> 4;
-#pragma unroll
-    for (uint32_t j = 0; j < SW; ++j) {
-      const uint32_t k = lane + 64u * j;
-      const bool drop = k >= nc || (rd == 0 && k == 0 && sh);
-      const u32x4 v = *reinterpret_cast<const u32x4 *>(img + 16u * min(k, nc - 1u));
-      __builtin_amdgcn_raw_buffer_store_b128(v, rs, (drop ? 0x80000000u : 16u * k) + tok, 0,
-                                             (XDRG_ENC_NT & 2) != 0 ? 2 : 0);
-    }
-  };
-  // a window -> stream: aligned 16-byte chunks, words at the stretch's edges
-  auto store_part = [&](uint64_t ws, uint64_t we) {
-    if (we <= ws) return;
-    const uint32_t nc = static_cast<uint32_t>((we - ws + 15u) >> 4);
-    for (uint32_t k = lane; k < nc; k += 64u) {
-      const uint64_t ca = ws + 16ull * k;
-      const uint8_t *lsrc = img + 16u * k;
-      if (ca >= wave_out && ca + 16u <= we) {
-        if constexpr ((XDRG_ENC_NT & 2) != 0)
-          __builtin_nontemporal_store(*reinterpret_cast<const u32x4 *>(lsrc), reinterpret_cast<u32x4 *>(xdr + ca));
-        else
-          *reinterpret_cast<u32x4 *>(xdr + ca) = *reinterpret_cast<const u32x4 *>(lsrc);
-      } else {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const uint64_t wa = ca + 4u * t;
-          if (wa >= wave_out && wa + 4u <= we) st32(xdr + wa, *reinterpret_cast<const uint32_t *>(lsrc + 4 * t));
-        }
-      }
-    }
-  };
-  bool paired = false;
-  if constexpr (kPipe2) if (pipe && rounds > 1) {
-    paired = true;
-    // Windows in pairs, the pair's two first batches loaded together: the
-    // next pair's loads are issued before the stores of this pair's second
-    // window and waited for after them, so one payload round trip serves
-    // two windows (one per window in XDRG_ENC_PIPE 1).  Both batches have
-    // landed at the top of the loop: no load in flight is carried in
-    // registers the compiler may move between iterations, and every path
-    // waits for a batch before it reads it (tools/isa_audit.py checks the
-    // compiled kernels).  (As compiler-visible loads the same schedule gets
-    // a vmcnt(0) before every placing; carrying a batch in flight across
-    // the back edge, the compiler moved its registers there.)
-    slots();
-    wave_sync();
-    batch B2;
-    // the chunks of window rd (its first batch in Bc, landed) -> image
-    auto fill = [&](uint32_t rd, batch &Bc) {
-      const uint32_t w0 = rd * C;
-      c.w0 = w0;
-      if constexpr (WL > 0)
-        if (ok && a0 < w0 + C && a0 + v > w0) emit_words(c, a0);
-      const uint32_t chi = range_hi(w0);
-      place(Bc, w0);
-      for (uint32_t c0 = range_lo(w0) + 64u * U; c0 < chi; c0 += 64u * U) {
-        issue(c0, chi, w0, Bc, bool_tag<false>{});
-        place(Bc, w0);
-      }
-      wave_sync();
-    };
-    // the first batches of windows rd and rd + 1 (an empty batch past the
-    // last window: every lane loads the heap's last 16 bytes)
-    auto pair = [&](uint32_t rd) {
-      issue(range_lo(rd * C), range_hi(rd * C), rd * C, B, asm_batch<1>{});
-      issue(range_lo((rd + 1) * C), range_hi((rd + 1) * C), (rd + 1) * C, B2, asm_batch<2>{});
-    };
-    pair(0);
-    vm_wait_after2<0, U, 1, 2>(B.val, B2.val);
-    for (uint32_t rd = 0;; rd += 2) {  // both batches landed
-      fill(rd, B);
-      if (rd + 1 == rounds) {
-        XDRG_STAMP(4);
-        store_part(g0 + rd * C, ge);
-        break;
-      }
-      store_full(rd, g0 + rd * C, true);
-      wave_sync();
-      fill(rd + 1, B2);
-      if (rd + 2 == rounds) {
-        XDRG_STAMP(4);
-        store_part(g0 + (rd + 1) * C, ge);
-        break;
-      }
-      pair(rd + 2);
-      store_full(rd + 1, g0 + (rd + 1) * C, true);
-      vm_wait_after2<SW, U, 1, 2>(B.val, B2.val);
-      wave_sync();
-    }
-  }
-  if (!paired) {
   for (uint32_t rd = 0; rd < rounds; ++rd) {
     const uint32_t w0 = rd * C;
     c.w0 = w0;
@@ -996,45 +822,95 @@ __device__ __forceinline__ void var_encode_body(
         }
       }
     }
-    if (rd == 0) slots();
+    if (rd == 0) {
+      XDRG_STAMP(2);
+      // ---- the lanes' slots and inclusive chunk counts, for the chunk pass
+      uint32_t nch = 0;
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) {
+        desc[lane * KMAX + k] = echunk_desc{c.psr[k], c.pds[k], c.pln[k]};
+        nch += (c.pln[k] + 15u) >> 4;
+      }
+      const uint32_t ci = wave_incl_scan(nch);
+      cum[lane] = ci;
+      M = rl32(ci, 63);
+      XDRG_STAMP(3);
+    }
     wave_sync();
     if constexpr (WL > 0)
       if (ok && a0 < w0 + C && a0 + v > w0) emit_words(c, a0);
 
-    // ---- payload chunks of the window: heap -> image, U per lane in flight
-    const uint32_t chi = range_hi(w0);
-    uint32_t c0 = range_lo(w0);
+    // ---- payload chunks of the window: heap -> image, U per lane in flight.
+    // Chunk i of the wave (stream order) belongs to the lane L with
+    // cum[L-1] <= i < cum[L] (binary search) and to the first of its slots
+    // whose chunks reach past i - cum[L-1].
+    const uint32_t clo = rl32(wave_incl_scan(chunks_ending_by(c, w0)), 63);
+    const uint32_t chi = min(M, rl32(wave_incl_scan(chunks_starting_before(c, w0 + C)), 63));
+    uint32_t c0 = clo;
     if (pf) {  // this window's first batch was loaded during the last window's stores
       place(B, w0);
       c0 += 64u * U;
     }
     for (; c0 < chi; c0 += 64u * U) {
-      issue(c0, chi, w0, B, bool_tag<false>{});
+      issue(c0, chi, B, bool_tag<false>{});
       place(B, w0);
     }
     wave_sync();
     if (rd + 1 == rounds) XDRG_STAMP(4);
 
-    // ---- window -> stream
+    // ---- window -> stream: aligned 16-byte chunks, words at the stretch's edges
     const uint64_t ws = g0 + w0;
+    const uint64_t we = min<uint64_t>(ws + C, ge);
     pf = false;
     if (pipe && rd + 1 < rounds) {
-      // a full window: first the next window's first batch, then the stores
-      const uint32_t nlo = range_lo(w0 + C), nhi = range_hi(w0 + C);
+      // a full window (we = ws + C): first the next window's first batch...
+      const uint32_t w1 = w0 + C;
+      const uint32_t nlo = rl32(wave_incl_scan(chunks_ending_by(c, w1)), 63);
+      const uint32_t nhi = min(M, rl32(wave_incl_scan(chunks_starting_before(c, w1 + C)), 63));
       if (nlo < nhi) {
-        issue(nlo, nhi, w0 + C, B, asm_batch<1>{});
+        issue(nlo, nhi, B, bool_tag<true>{});
         pf = true;
       }
-      store_full(rd, ws, true);
+      // ...then SW stores per lane, none skipped by a branch
+      if (rd == 0 && sh && lane == 0) head = *reinterpret_cast<const u32x4 *>(img);
+      const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>(xdr + ws) >> 32));
+      const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>(xdr + ws)));
+      const auto rs = __builtin_amdgcn_make_buffer_rsrc(
+          reinterpret_cast<void *>((static_cast<uint64_t>(hi) << 32) | lo), 0, C, 0x00020000);
+      const uint32_t nc = C >> 4;
+#pragma unroll
+      for (uint32_t j = 0; j < SW; ++j) {
+        const uint32_t k = lane + 64u * j;
+        const bool drop = k >= nc || (rd == 0 && k == 0 && sh);
+        const u32x4 v = *reinterpret_cast<const u32x4 *>(img + 16u * min(k, nc - 1u));
+        __builtin_amdgcn_raw_buffer_store_b128(v, rs, (drop ? 0x80000000u : 16u * k) + B.tok, 0,
+                                               (XDRG_ENC_NT & 2) != 0 ? 2 : 0);
+      }
       // the prefetched loads were issued before these SW stores and vmcnt
       // retires in order: at most SW outstanding = every load has landed
-      // (waited for on every path, prefetched or not: tools/isa_audit.py)
-      vm_wait_after<SW, U, 1>(B.val);
-    } else {
-      store_part(ws, min<uint64_t>(ws + C, ge));
+      // (on every path, prefetched or not: tools/isa_audit.py's dataflow
+      // then sees every batch waited for)
+      vm_wait_after<SW>(B.val);
+    } else if (we > ws) {
+      const uint32_t nc = static_cast<uint32_t>((we - ws + 15u) >> 4);
+      for (uint32_t k = lane; k < nc; k += 64u) {
+        const uint64_t ca = ws + 16ull * k;
+        const uint8_t *lsrc = img + 16u * k;
+        if (ca >= wave_out && ca + 16u <= we) {
+          if constexpr ((XDRG_ENC_NT & 2) != 0)
+            __builtin_nontemporal_store(*reinterpret_cast<const u32x4 *>(lsrc), reinterpret_cast<u32x4 *>(xdr + ca));
+          else
+            *reinterpret_cast<u32x4 *>(xdr + ca) = *reinterpret_cast<const u32x4 *>(lsrc);
+        } else {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const uint64_t wa = ca + 4u * t;
+            if (wa >= wave_out && wa + 4u <= we) st32(xdr + wa, *reinterpret_cast<const uint32_t *>(lsrc + 4 * t));
+          }
+        }
+      }
     }
     wave_sync();  // the next window's walk reuses the image
-  }
   }
   if (pipe && rounds > 1 && sh && lane == 0) {  // the head chunk's words of this wave
     if (sh <= 4) st32(xdr + g0 + 4, head.y);
