@@ -346,7 +346,11 @@ enum xdrg_plan_option {
                                      check failed; 2 the same without the wait (the
                                      list ranking is queued and skips itself: the
                                      call stays asynchronous); 0 the list ranking
-                                     alone.  Same offsets, count and errors */
+                                     alone.  Same offsets, count and errors.
+                                     3 (a tuning aid) the walk alone, waited for:
+                                     when a check fails nothing else runs, the
+                                     offsets are left as they were and the
+                                     workspace keeps the walk's segment records */
 };
 int xdrg_plan_set_option(xdrg_plan *plan, int option, int64_t value);
 
@@ -577,15 +581,23 @@ size_t xdrg_index_workspace_size(uint64_t len, uint32_t max_msg_len);
  * so xdrg_decode reports the reference's error for record k; fewer than n
  * records end at len likewise, more leave off[n] < len (trailing bytes).
  * *d_count = the records the chain holds before it ends (all-ones when
- * it goes past record n).  max_rec_len <= XDRG_MAX_MSG.  Past
- * XDRG_INDEX_MAX_MSG, when the speculative walk misses, the stream is
- * indexed in rounds: one wave walks the records longer than a window
- * (lengths, counts and discriminants, its element frames in the workspace)
- * from where the chain stopped, then a list-ranking window indexes the
- * records after them up to the next long one -- the call waits on the
- * stream every round, so it is XDRG_EUNSUPPORTED on a stream being
- * captured.  A record longer than max_rec_len is reported as
- * XDRG_ERR_INDEX_LONG at its index.  Plans whose records can be empty are
+ * it goes past record n).  max_rec_len <= XDRG_MAX_MSG.
+ * max_rec_len <= XDRG_INDEX_MAX_MSG: a record longer than max_rec_len is
+ * reported as XDRG_ERR_INDEX_LONG at its index.  Past XDRG_INDEX_MAX_MSG
+ * the records have no length bound (xdr_from_opaque has none) and no
+ * nesting bound but XDRG_MAX_FRAMES: with the plan's generated parse the
+ * speculative walk takes the whole stream, records past its segments
+ * parsed by a wave each through blocks of the stream in LDS (and a linked
+ * list's plan, rpcb_prot.x's rp__list, parses its nodes in a loop); when
+ * that walk misses the stream is indexed in rounds: one wave walks the
+ * records longer than a window (lengths, counts and discriminants, its
+ * element frames in the workspace) from where the chain stopped, then a
+ * list-ranking window indexes the records after them up to the next long
+ * one -- the call waits on the stream every round.  On a stream being
+ * captured the walk runs alone, asynchronously: a stream it does not hold
+ * gets the list ranking over records up to one window, which reports
+ * XDRG_ERR_INDEX_LONG at a longer one (plans without the generated parse:
+ * XDRG_EUNSUPPORTED).  Plans whose records can be empty are
  * XDRG_EUNSUPPORTED.  Workspace: xdrg_index_workspace_size(len,
  * max_rec_len).
  */

@@ -151,9 +151,9 @@ def test_plan_options_are_per_plan_and_validated():
     assert L.xdrg_plan_set_option(p.handle, A.PLAN_OPTIONS["var_encode_kernel"], 2) == -1
     assert L.xdrg_plan_set_option(p.handle, A.PLAN_OPTIONS["enc_unroll"], 5) == -1
     assert L.xdrg_plan_set_option(p.handle, A.PLAN_OPTIONS["enc_unroll"], 16) == A.OK
-    for v in (0, 1, 2):  # record index: list ranking / host-gated walk / asynchronous walk
+    for v in (0, 1, 2, 3):  # record index: list ranking / host-gated walk / asynchronous walk / walk only
         assert L.xdrg_plan_set_option(p.handle, A.PLAN_OPTIONS["index_fast"], v) == A.OK
-    assert L.xdrg_plan_set_option(p.handle, A.PLAN_OPTIONS["index_fast"], 3) == -1
+    assert L.xdrg_plan_set_option(p.handle, A.PLAN_OPTIONS["index_fast"], 4) == -1
     for v in (-1, 0, 8192, 32768):  # LDS stage of a group's element arrays
         assert L.xdrg_plan_set_option(p.handle, A.PLAN_OPTIONS["stage_bytes"], v) == A.OK
     assert L.xdrg_plan_set_option(p.handle, A.PLAN_OPTIONS["stage_bytes"], 32769) == -1

@@ -129,7 +129,12 @@ def _gpu_index(mar, x, n, maxlen, dev, ws_tail=False):
             "xdrg_index_records")
     e = M.error_from(mar.plan, mar.status.read(s))
     res = offs.cpu().numpy().view(np.uint64), int(cnt.cpu().numpy().view(np.uint64)[0]), e
-    return res + (ws[-256:].cpu().numpy(),) if ws_tail else res
+    if not ws_tail:
+        return res
+    # the fast path's flag: the last 256 bytes of the index layout (past the
+    # window, rx_windows' continuation and frames follow it)
+    w0 = L.xdrg_index_workspace_size(x.size, min(maxlen, A.INDEX_MAX_MSG)) if x.size else 0
+    return res + (ws[max(w0, 256) - 256:max(w0, 256)].cpu().numpy(),)
 
 
 @pytest.mark.gpu
@@ -329,10 +334,12 @@ def test_gpu_index_records_past_the_window(dev, spec):
     mar = M.Marshaler(M.Plan(cp, {"specialize": spec}), dev)
     for label, y, k in damaged(x, offs, n, 21) + damaged(x, offs, n, 22)[5:]:
         want, wcnt, wrc, wer = O.index_records(cp, y, k, A.MAX_MSG)
-        got, gcnt, err = _gpu_index(mar, y, k, A.MAX_MSG, dev)
+        got, gcnt, err, tail = _gpu_index(mar, y, k, A.MAX_MSG, dev, ws_tail=True)
         assert np.array_equal(got, want), label
         assert gcnt == wcnt, label
         assert (err.code if err else 0) == wrc, label
+        if label == "good" and spec:  # the walk over the whole stream held it (rxs_long took the long records)
+            assert _fast_flag(tail) == 1
     # a window-sized max_rec_len still hands such a stream back (INDEX_LONG)
     got, gcnt, err = _gpu_index(mar, x, n, A.INDEX_MAX_MSG, dev)
     want, wcnt, wrc, wer = O.index_records(cp, x, n, A.INDEX_MAX_MSG)
@@ -365,6 +372,44 @@ def test_gpu_index_rp_list_full_size(dev, manifest):
     assert int(sizes.max()) > A.INDEX_MAX_MSG
     offs = mar.index_records(r.xdr, n)
     assert torch.equal(offs, r.offsets)
+    # the speculative walk over the whole stream held it: the lists' generated
+    # parse (codegen.cpp tail_list), the 500-node lists left to rxs_long
+    got, cnt, err, tail = _gpu_index(mar, r.xdr.cpu().numpy(), n, A.MAX_MSG, dev, ws_tail=True)
+    assert err is None and cnt == n and np.array_equal(got, r.offsets.cpu().numpy().view(np.uint64))
+    assert _fast_flag(tail) == 1
+
+
+@pytest.mark.gpu
+def test_gpu_index_rp_list_graph_capture(dev):
+    """The index of rp__list records of any length captured into a graph:
+    the walk over the whole stream runs asynchronously (no rounds, which
+    wait on the host), and each replay indexes the stream, its two 500-node
+    lists included."""
+    import torch
+    from xdrpp_amd import marshal as M
+    from xdrpp_amd import workloads as W
+    n = 1 << 17
+    nat, heap = W.rp_list(n)
+    mar = M.Marshaler(M.Plan(S.ALL["rp_list"]), dev)
+    r = mar.encode(_dev(nat, dev), n, _dev(heap, dev))
+    x = r.xdr
+    L = A.lib()
+    ws = torch.empty(L.xdrg_index_workspace_size(x.numel(), A.MAX_MSG), dtype=torch.uint8, device=dev)
+    out = torch.full((n + 1,), -1, dtype=torch.int64, device=dev)
+    cnt = torch.empty(1, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        s = torch.cuda.current_stream().cuda_stream
+        A.check(L.xdrg_index_records(mar.plan.handle, x.data_ptr(), x.numel(), n, A.MAX_MSG, out.data_ptr(),
+                                     cnt.data_ptr(), ws.data_ptr(), ws.numel(), mar.status.ptr, s), "index (capture)")
+    for _ in range(3):
+        out.fill_(-1)
+        mar.status.init(torch.cuda.current_stream().cuda_stream)
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, r.offsets) and int(cnt.item()) == n
+        assert mar.status.read(torch.cuda.current_stream().cuda_stream).code == 0
 
 
 @pytest.mark.gpu

@@ -1145,6 +1145,125 @@ void seal(std::string src, spec_info &info) {
   info.source = std::move(src);
 }
 
+// The record-start parse of the plain-stream index (plan_rx) and its index
+// kernels: the list ranking's segment parse, the speculative walk over
+// records up to the index window, the same walk over records of any length
+// (xdrg_index_records with max_rec_len past the window: records past the
+// staged stretch left to rxs_long) and rxs_long itself.
+std::string rx_source(const std::string &first, const std::string &flen, const std::string &second,
+                      const std::string &rx_code, const std::string &rxs_code) {
+  std::ostringstream s;
+  s << "struct plan_rx {  // index_kernels.h ix_seg_body's, rxs_walk_body's, rxs_long_body's and rxs_fix_body's parser\n"
+    << "  __device__ __forceinline__ void init(uint32_t *) const {}\n"
+    << "  __device__ __forceinline__ bool first_ok(const uint32_t *, uint32_t v) const { return " << first << "; }\n"
+    << "  __device__ __forceinline__ uint64_t first_len(uint32_t v) const { return " << flen << "; }\n"
+    << "  __device__ __forceinline__ bool second_ok(uint32_t v, uint32_t w) const { return " << second << "; }\n"
+    << "  __device__ __forceinline__ uint32_t rlen(const uint32_t *m, const uint8_t *__restrict__ s, uint64_t len,\n"
+    << "                                           uint64_t a, uint32_t maxlen) const {\n"
+    << "    return rlen_rd<rx_global, uint64_t>(m, rx_global{s}, len, a, maxlen);\n  }\n"
+    << "  // U: the position type (uint32_t for offsets into a staged stretch)\n"
+    << "  template <class RD, class U>\n"
+    << "  __device__ __forceinline__ uint32_t rlen_rd(const uint32_t *, const RD &rd, U len,\n"
+    << "                                              U a, uint32_t maxlen) const {\n"
+    << "    const bool capped = static_cast<uint64_t>(a) + maxlen < len;\n"
+    << "    [[maybe_unused]] const bool whole = maxlen > XDRG_INDEX_MAX_MSG;  // (tail lists: no frame bound)\n"
+    << "    U lim = capped ? static_cast<U>(a + maxlen) : len;\n"
+    << "    uint32_t past = capped ? RX_LONG : RX_BAD;\n"
+    << "    rd.clamp(lim, past, a);  // (the staged stretch's end: RX_OUT, and the caller parses from global memory)\n"
+    << "    U p = a;\n"
+    << rx_code << "    return static_cast<uint32_t>(p - a);\n  }\n"
+    << "  // the same parse over the staged stretch without early returns (index_kernels.h rxs_rlen)\n"
+    << "  __device__ __forceinline__ uint32_t rlen_st(const uint32_t *, const rx_lds &rd, uint32_t len,\n"
+    << "                                              uint32_t a, uint32_t maxlen) const {\n"
+    << "    using U = uint32_t;\n"
+    << "    const bool capped = static_cast<uint64_t>(a) + maxlen < len;\n"
+    << "    [[maybe_unused]] const bool whole = maxlen > XDRG_INDEX_MAX_MSG;\n"
+    << "    U lim = capped ? static_cast<U>(a + maxlen) : len;\n"
+    << "    uint32_t past = capped ? RX_LONG : RX_BAD;\n"
+    << "    rd.clamp(lim, past, a);\n"
+    << "    uint32_t r = 0;\n"
+    << "    U p = a;\n"
+    << rxs_code << "    return r ? r : static_cast<uint32_t>(p - a);\n  }\n"
+    << "};\n\n"
+    << "extern \"C\" __global__ __launch_bounds__(256) void xdrg_spec_ix_seg(\n"
+    << "    const uint8_t *s, uint64_t len, uint32_t maxlen, uint32_t K, uint64_t *tab, uint32_t *list,\n"
+    << "    uint32_t *lcount, uint32_t has_first, uint32_t fd, const uint32_t *skip) {\n"
+    << "  if (skip && *skip == 1u) return;  // the speculative walk holds the index\n"
+    << "  ix_seg_body<true>(plan_rx{}, s, len, maxlen, K, tab, list, lcount, has_first != 0, fd);\n}\n\n"
+    << "extern \"C\" __global__ __launch_bounds__(64) void xdrg_spec_rxs_walk(\n"
+    << "    const uint8_t *s, uint64_t len, uint32_t maxlen, uint64_t *seg, uint16_t *nodes,\n"
+    << "    uint32_t *flag, uint32_t has_first, uint32_t fd) {\n"
+    << "  rxs_walk_body(plan_rx{}, s, len, maxlen, seg, nodes, flag, has_first != 0, fd);\n}\n\n"
+    << "extern \"C\" __global__ __launch_bounds__(64) void xdrg_spec_rxs_walk_whole(\n"
+    << "    const uint8_t *s, uint64_t len, uint32_t maxlen, uint64_t *seg, uint16_t *nodes,\n"
+    << "    uint32_t *flag, uint32_t has_first, uint32_t fd) {\n"
+    << "  rxs_walk_body<true>(plan_rx{}, s, len, maxlen, seg, nodes, flag, has_first != 0, fd);\n}\n\n"
+    << "extern \"C\" __global__ __launch_bounds__(64 * kRxsLongWaves) void xdrg_spec_rxs_long(\n"
+    << "    const uint8_t *s, uint64_t len, uint32_t maxlen, uint64_t *seg, uint64_t nseg) {\n"
+    << "  rxs_long_body(plan_rx{}, s, len, maxlen, seg, nseg);\n}\n\n"
+    << "extern \"C\" __global__ __launch_bounds__(64) void xdrg_spec_rxs_fix(\n"
+    << "    const uint8_t *s, uint64_t len, uint32_t maxlen, uint64_t *seg, uint64_t nseg, uint16_t *nodes,\n"
+    << "    const uint64_t *list, const unsigned long long *nl, uint32_t *flag) {\n"
+    << "  rxs_fix_body(plan_rx{}, s, len, maxlen, seg, nseg, nodes, list, nl, flag);\n}\n\n";
+  return s.str();
+}
+
+// A recursive plan whose recursion is a linked list: the record's last
+// field is a pointer (count 0 or 1) to another record of the same plan,
+// and nothing before it holds element subroutines (rpcbind's rp__list,
+// xdrpp/rpcb_prot.x:32-37).  Its record parse is a loop over the list's
+// nodes (vpc: the pointer's op).
+bool tail_list(const gen &g, uint32_t &vpc) {
+  uint32_t end = 0;
+  while (end < g.nops() && g.op(end).kind != XDRG_OP_END) ++end;
+  if (end == 0 || end >= g.nops()) return false;
+  vpc = end - 1;
+  const xdrg_op &v = g.op(vpc);
+  if (v.kind != XDRG_OP_VECTOR || !(v.flags & XDRG_F_SUB) || v.arg4 != 0 || v.arg0 != 1) return false;
+  for (uint32_t pc = 0; pc < vpc; ++pc) {
+    const xdrg_op &o = g.op(pc);
+    if (o.kind == XDRG_OP_VECTOR && (o.flags & XDRG_F_SUB)) return false;
+    if (o.kind == XDRG_OP_JUMP && o.arg0 > vpc) return false;
+    if (o.kind == XDRG_OP_UNION && (g.ipdom[pc] == kNoPc || g.ipdom[pc] > vpc)) return false;
+  }
+  return true;
+}
+
+// The tail list's parse: the node's fields, then the pointer's count, node
+// after node.  xdro_index_records' rx_walk (oracle/xdr_oracle.c) opens a
+// frame per node in the index window (past XDRG_INDEX_FRAMES: RX_LONG) and
+// lets a tail pointer's node take its parent's frame in the whole-record
+// walk (whole: max_rec_len past the window), so there the list has no bound.
+std::string tail_rx(gen &g, uint32_t vpc, bool sticky) {
+  g.o.str("");
+  g.ind = 6;
+  g.rx_sticky = sticky;
+  g.rx_block(0, vpc);
+  g.rx_sticky = false;
+  const std::string body = g.o.str();
+  std::ostringstream s;
+  if (!sticky) {
+    s << "    for (uint32_t fr = 0;; ++fr) {  // a node of the list\n" << body
+      << "      if (lim - p < 4u) return past;\n"
+      << "      const uint32_t v = bswap32(rd.at(p));\n"
+      << "      p += 4u;\n"
+      << "      if (v > 1u) return RX_BAD;\n"
+      << "      if (!v) break;\n"
+      << "      if (!whole && fr == XDRG_INDEX_FRAMES) return RX_LONG;\n"
+      << "    }\n";
+  } else {
+    s << "    for (uint32_t fr = 0; r == 0u; ++fr) {  // a node of the list\n" << body
+      << "      r = (r == 0u && (lim - p < 4u)) ? past : r;\n"
+      << "      const uint32_t v = bswap32(rd.atc(p));\n"
+      << "      p += 4u;\n"
+      << "      r = (r == 0u && (v > 1u)) ? RX_BAD : r;\n"
+      << "      if (!v) break;\n"
+      << "      r = (r == 0u && !whole && fr == XDRG_INDEX_FRAMES) ? RX_LONG : r;\n"
+      << "    }\n";
+  }
+  return s.str();
+}
+
 // Recursive plans (element subroutines entered from themselves: rp__list,
 // test_recursive): the frame walks of sub_kernels.h over this plan's ops as
 // compile-time constants.  plan_ops::visit switches on the walk's pc; an op
@@ -1165,6 +1284,7 @@ bool frame_walk_source(const xdrg_plan &p, spec_info &info) {
   s << "// Generated by libxdrgpu (codegen.cpp) from a recursive plan of " << p.ops.size()
     << " ops: the frame walks of sub_kernels.h with the ops as constants.\n"
     << "#include \"sub_kernels.h\"\n"
+    << "#include \"index_kernels.h\"\n"
     << "using namespace xdrg::dev;\n\n"
     << "extern \"C\" __device__ __attribute__((used)) unsigned xdrg_spec_iface = " << kSpecIface << "u;\n\n"
     << "struct plan_ops {\n"
@@ -1203,6 +1323,13 @@ bool frame_walk_source(const xdrg_plan &p, spec_info &info) {
     << "  sub_chain_kernel<plan_ops>(XDRG_SUB_ENCODE_ARGS);\n}\n\n";
   info = spec_info{};
   info.frame_walk = true;
+  gen g(p);
+  uint32_t vpc = 0;
+  if (tail_list(g, vpc)) {  // the index's record parse, a loop over the list's nodes
+    const std::string rx_code = tail_rx(g, vpc, false), rxs_code = tail_rx(g, vpc, true);
+    s << rx_source(g.first_test(), g.first_len(), g.second_test(), rx_code, rxs_code);
+    info.tail_rx = true;
+  }
   seal(s.str(), info);
   return true;
 }
@@ -1290,46 +1417,7 @@ bool spec_source(const xdrg_plan &p, spec_info &info) {
     << "    {\n" << eb_code << "    }\n"
     << "    return E;\n  }\n"
     << "};\n\n"
-    << "struct plan_rx {  // index_kernels.h ix_seg_body's and rxs_walk_body's parser\n"
-    << "  __device__ __forceinline__ void init(uint32_t *) const {}\n"
-    << "  __device__ __forceinline__ bool first_ok(const uint32_t *, uint32_t v) const { return " << first << "; }\n"
-    << "  __device__ __forceinline__ uint64_t first_len(uint32_t v) const { return " << flen << "; }\n"
-    << "  __device__ __forceinline__ bool second_ok(uint32_t v, uint32_t w) const { return " << second << "; }\n"
-
-    << "  __device__ __forceinline__ uint32_t rlen(const uint32_t *m, const uint8_t *__restrict__ s, uint64_t len,\n"
-    << "                                           uint64_t a, uint32_t maxlen) const {\n"
-    << "    return rlen_rd<rx_global, uint64_t>(m, rx_global{s}, len, a, maxlen);\n  }\n"
-    << "  // U: the position type (uint32_t for offsets into a staged stretch)\n"
-    << "  template <class RD, class U>\n"
-    << "  __device__ __forceinline__ uint32_t rlen_rd(const uint32_t *, const RD &rd, U len,\n"
-    << "                                              U a, uint32_t maxlen) const {\n"
-    << "    const bool capped = static_cast<uint64_t>(a) + maxlen < len;\n"
-    << "    U lim = capped ? static_cast<U>(a + maxlen) : len;\n"
-    << "    uint32_t past = capped ? RX_LONG : RX_BAD;\n"
-    << "    rd.clamp(lim, past, a);  // (the staged stretch's end: RX_OUT, and the caller parses from global memory)\n"
-    << "    U p = a;\n"
-    << rx_code << "    return static_cast<uint32_t>(p - a);\n  }\n"
-    << "  // the same parse over the staged stretch without early returns (index_kernels.h rxs_rlen)\n"
-    << "  __device__ __forceinline__ uint32_t rlen_st(const uint32_t *, const rx_lds &rd, uint32_t len,\n"
-    << "                                              uint32_t a, uint32_t maxlen) const {\n"
-    << "    using U = uint32_t;\n"
-    << "    const bool capped = static_cast<uint64_t>(a) + maxlen < len;\n"
-    << "    U lim = capped ? static_cast<U>(a + maxlen) : len;\n"
-    << "    uint32_t past = capped ? RX_LONG : RX_BAD;\n"
-    << "    rd.clamp(lim, past, a);\n"
-    << "    uint32_t r = 0;\n"
-    << "    U p = a;\n"
-    << rxs_code << "    return r ? r : static_cast<uint32_t>(p - a);\n  }\n"
-    << "};\n\n"
-    << "extern \"C\" __global__ __launch_bounds__(256) void xdrg_spec_ix_seg(\n"
-    << "    const uint8_t *s, uint64_t len, uint32_t maxlen, uint32_t K, uint64_t *tab, uint32_t *list,\n"
-    << "    uint32_t *lcount, uint32_t has_first, uint32_t fd, const uint32_t *skip) {\n"
-    << "  if (skip && *skip == 1u) return;  // the speculative walk holds the index\n"
-    << "  ix_seg_body<true>(plan_rx{}, s, len, maxlen, K, tab, list, lcount, has_first != 0, fd);\n}\n\n"
-    << "extern \"C\" __global__ __launch_bounds__(64) void xdrg_spec_rxs_walk(\n"
-    << "    const uint8_t *s, uint64_t len, uint32_t maxlen, uint64_t *seg, uint16_t *nodes,\n"
-    << "    uint32_t *flag, uint32_t has_first, uint32_t fd) {\n"
-    << "  rxs_walk_body(plan_rx{}, s, len, maxlen, seg, nodes, flag, has_first != 0, fd);\n}\n\n"
+    << rx_source(first, flen, second, rx_code, rxs_code)
     << "extern \"C\" __global__ __launch_bounds__(64) void xdrg_spec_size(\n"
     << "    const uint8_t *native, uint64_t n, uint32_t stride, const uint8_t *heap, uint64_t heap_len,\n"
     << "    uint32_t *sizes, unsigned long long *block_sums, uint32_t mark, unsigned long long *err) {\n"

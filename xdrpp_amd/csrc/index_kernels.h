@@ -245,7 +245,6 @@ struct rx_goff {
   template <class U>
   __device__ __forceinline__ void clamp(U &, uint32_t &, U) const {}
 };
-
 // ---------------------------------- speculative record index (fast path)
 // xdrg_index_records' list ranking parses every word of the stream as a
 // possible record start.  The fast path parses (almost) only the records
@@ -297,13 +296,22 @@ constexpr uint32_t kBrk = 0xffffffffu, kNone = 0xfffffffeu;
 constexpr uint32_t kRxsSegWords = 4;
 
 // One record parse at q: from the staged stretch, or from global memory
-// when the record reaches past it.
-template <class P>
+// when the record reaches past it.  In a walk over a stream of records of
+// any length (WHOLE: xdrg_index_records with max_rec_len past the index
+// window) such a record is RX_OUT: it is left to rxs_long, whose wave
+// parses it through blocks of the stream in LDS (one lane's parse through
+// global memory waits on every length it reads: a 500-node rp__list took
+// milliseconds that way), and the walk knows where it starts -- a record
+// from the look-back that runs past the stretch is the segment's only
+// when the segment lies inside it (below), while a guess there that reads
+// a large word as a length would otherwise carry the chain far away.
+template <bool WHOLE = false, class P>
 __device__ __forceinline__ uint32_t rxs_rlen(const P &parser, const uint32_t *smem, const rx_lds &st,
                                              const uint8_t *base, uint32_t lenr, uint32_t maxlen, uint32_t q) {
   st.out = false;
   const uint32_t L = parser.rlen_st(smem, st, lenr, q, maxlen);
   if (!st.out && L != RX_OUT) return L;
+  if constexpr (WHOLE) return RX_OUT;
   return parser.rlen_rd(smem, rx_goff{base}, lenr, q, maxlen);
 }
 
@@ -321,15 +329,20 @@ struct rxs_nodes {
 };
 
 // Chain of record parses from q until it reaches b, noting its nodes: the
-// position reached, or kBrk.
-template <class P>
+// position reached, or kBrk -- or (WHOLE) kLongAt | q for a chain whose
+// record at q runs past the staged stretch: it passes every lane after it
+// (kLongAt | q is at or past any lane's end) and becomes the segment's
+// exit, which rxs_long resolves to the record's end.
+constexpr uint32_t kLongAt = 0x80000000u;  // (stretch offsets stay below 2^31)
+template <bool WHOLE = false, class P>
 __device__ __forceinline__ uint32_t rxs_chain(const P &parser, const uint32_t *smem, const rx_lds &st,
                                               const uint8_t *base, uint32_t lenr, uint32_t maxlen, uint32_t q,
                                               uint32_t b, rxs_nodes &nd) {
   nd.n = 0;
   while (q < b) {
     nd.add(q);
-    const uint32_t L = rxs_rlen(parser, smem, st, base, lenr, maxlen, q);
+    const uint32_t L = rxs_rlen<WHOLE>(parser, smem, st, base, lenr, maxlen, q);
+    if (WHOLE && L == RX_OUT) return kLongAt | q;
     if (L >= RX_LONG) return kBrk;
     q += L;
   }
@@ -377,8 +390,16 @@ struct mark_rx {
 #define XDRG_LSTAMP(k, v) ((void)0)
 #define XDRG_LCLK() 0ull
 #endif
+// ... and per-lane states of the walk (tools/gpu/rx_whole_diag.py)
+#ifndef XDRG_LDBG
+#define XDRG_LDBG(k, v) ((void)0)
+#endif
 
-template <class P>
+// The segment record's exit word for a chain whose last record was left to
+// rxs_long: that record's start, flagged.
+constexpr uint64_t kRxsLongExit = 1ull << 62;
+
+template <bool WHOLE = false, class P>
 __device__ __forceinline__ void rxs_walk_body(const P &parser, const uint8_t *__restrict__ s, uint64_t len,
                                               uint32_t maxlen, uint64_t *__restrict__ seg,
                                               uint16_t *__restrict__ nodes, uint32_t *__restrict__ flag,
@@ -396,7 +417,12 @@ __device__ __forceinline__ void rxs_walk_body(const P &parser, const uint8_t *__
   // maxlen, so the clamp changes nothing)
   const uint32_t lenr = static_cast<uint32_t>(min(len - lo, 0x7fffffffull));
   const uint32_t r0 = static_cast<uint32_t>(s0 - lo), r1 = static_cast<uint32_t>(min(len, s0 + kRxsSeg) - lo);
-  if (blockIdx.x == 0 && lane == 0) *flag = 1u;  // rxs_check clears it on a miss
+  if (blockIdx.x == 0 && lane == 0) {
+    flag[0] = 1u;  // rxs_check clears it on a miss
+    flag[2] = 0u;  // (WHOLE: rxs_mark's count, a u64 at flag + 2)
+    flag[3] = 0u;
+  }
+  if (lane == 0) seg[static_cast<uint64_t>(blockIdx.x) * kRxsSegWords + 3] = 0;  // (rxs_fix's entries)
   parser.init(rx_smem);
   // stage [lo, lo + kStg) within the stream: all of a lane's 16-byte loads
   // in flight before its stores
@@ -438,7 +464,7 @@ __device__ __forceinline__ void rxs_walk_body(const P &parser, const uint8_t *__
   [[maybe_unused]] uint32_t ltry = 0;
   if (act && first && lane == root) {
     g = 0;
-    e = rxs_chain(parser, rx_smem, st, base, lenr, maxlen, 0, b, nd);
+    e = rxs_chain<WHOLE>(parser, rx_smem, st, base, lenr, maxlen, 0, b, nd);
   } else if (act) {
     // candidates: the lane's words (before b, with a first checked word
     // inside the stream) whose first checked word passes; the lane's LDS reads
@@ -458,7 +484,10 @@ __device__ __forceinline__ void rxs_walk_body(const P &parser, const uint8_t *__
       // record that cannot breaks the chain anyway (the walk then falls back
       // to the list ranking, which tells INDEX_LONG apart); containertest's
       // unbounded uvec<> and strings otherwise let every word through
-      const uint64_t room = maxlen > fd + 4u ? maxlen - fd - 4u : 0u;
+      // (and in the rest of the stream: with no maxlen -- WHOLE -- that
+      // spares the global parse of candidates whose first length cannot fit)
+      const uint64_t room = min<uint64_t>(maxlen > fd + 4u ? maxlen - fd - 4u : 0u,
+                                          lenr > a + fd + 4u ? lenr - a - fd - 4u : 0u);
 #pragma unroll
       for (uint32_t k = 0; k < kRxsSub / 4; ++k) {
         const uint32_t v = bswap32(fw[k]);
@@ -473,13 +502,32 @@ __device__ __forceinline__ void rxs_walk_body(const P &parser, const uint8_t *__
       mask &= m;
     }
     lt1 = XDRG_LCLK();
+    // (WHOLE: a chain that ends in a record past the stretch is the guess
+    // only when no other candidate's chain leaves the lane: a word read as
+    // a large length -- rp__list's 100000-based r_prog under a string's
+    // length -- carries a wrong guess far into the stream)
+    uint32_t gl = kNone, el = kNone;
+    rxs_nodes ndl;
     while (mask) {
       const uint32_t k = __builtin_ctzll(mask);
       mask &= mask - 1;
       ++ltry;
       const uint32_t p = a + 4 * k;
-      const uint32_t q = rxs_chain(parser, rx_smem, st, base, lenr, maxlen, p, b, nd);
+      const uint32_t q = rxs_chain<WHOLE>(parser, rx_smem, st, base, lenr, maxlen, p, b, nd);
+      if (WHOLE && q != kBrk && (q & kLongAt)) {
+        if (gl == kNone) {
+          gl = p;
+          el = q;
+          ndl = nd;
+        }
+        continue;
+      }
       if (q != kBrk) { g = p; e = q; break; }
+    }
+    if (WHOLE && g == kNone && gl != kNone) {
+      g = gl;
+      e = el;
+      nd = ndl;
     }
     if (g == kNone) nd.n = 0;
   }
@@ -488,6 +536,8 @@ __device__ __forceinline__ void rxs_walk_body(const P &parser, const uint8_t *__
   XDRG_LSTAMP(2, ltry);
   XDRG_LSTAMP(3, nd.n);
   if (lane == root && g == kNone) e = kBrk;  // a root without a chain
+  XDRG_LDBG(0, g);
+  XDRG_LDBG(1, e);
   XDRG_XSTAMP(2);
   // Agree from the root on.  A lane without a guess is transparent: no
   // word of it starts a chain that leaves it, so the chain either passes
@@ -519,8 +569,15 @@ __device__ __forceinline__ void rxs_walk_body(const P &parser, const uint8_t *__
       ch = true;
       pin = g = pe;
       nd.n = 0;
-      e = pe == kBrk || pe >= b ? pe : rxs_chain(parser, rx_smem, st, base, lenr, maxlen, pe, b, nd);
-      if (e == kBrk && g0 != kNone && (lane < kRoot || !(livem & below_seg))) {
+      e = pe == kBrk || pe >= b ? pe : rxs_chain<WHOLE>(parser, rx_smem, st, base, lenr, maxlen, pe, b, nd);
+      // An entry from a look-back lane at or past the segment's end is one
+      // record from the look-back over the whole segment: a true one puts
+      // the segment inside it (rxs_check passes it over, whatever the walk
+      // says), so it gives way to the lane's own guess like a broken chain
+      // -- a wrong guess upstream that reads a large length (or a record
+      // left to rxs_long, kLongAt) must not sink the segment
+      const bool far = src < kRoot && pe != kBrk && pe >= r1;
+      if ((e == kBrk || far) && g0 != kNone && (lane < kRoot || far || !(livem & below_seg))) {
         g = g0;
         e = e0;
         nd = nd0;
@@ -531,9 +588,11 @@ __device__ __forceinline__ void rxs_walk_body(const P &parser, const uint8_t *__
   const uint32_t pt = entry(__shfl(e, src, 64));
   if (act && !stateful) {  // a transparent lane passes the chain over or breaks it
     g = pt;
-    e = g == kBrk || g < b ? kBrk : g;
+    e = g == kBrk || g < b || (src < kRoot && g >= r1) ? kBrk : g;  // (a look-back record over the segment: above)
     nd.n = 0;
   }
+  XDRG_LDBG(2, g);
+  XDRG_LDBG(3, e);
   XDRG_XSTAMP(3);
   // the segment's nodes, noted by the walk that set each lane's state (the
   // look-back lanes' nodes belong to the segment before); a lane with more
@@ -551,7 +610,7 @@ __device__ __forceinline__ void rxs_walk_body(const P &parser, const uint8_t *__
       uint32_t q = g;
       for (uint32_t k = 0; k < c; ++k) {
         if (k >= kRxsKeep) out[k] = static_cast<uint16_t>((q - r0) >> 2);
-        q += rxs_rlen(parser, rx_smem, st, base, lenr, maxlen, q);
+        q += rxs_rlen<WHOLE>(parser, rx_smem, st, base, lenr, maxlen, q);  // (the last: RX_OUT, unused)
       }
     }
   }
@@ -561,13 +620,15 @@ __device__ __forceinline__ void rxs_walk_body(const P &parser, const uint8_t *__
   // a live state
   const uint64_t amask = __ballot(act);
   const uint32_t last = 63u - static_cast<uint32_t>(__builtin_clzll(amask));
-  const uint64_t livef = __ballot(act && lane >= kRoot && e != kBrk && e != kNone);
+  // (WHOLE: lanes passed over by a record left to rxs_long hold no node)
+  const bool passed = WHOLE && g != kBrk && g != kNone && (g & kLongAt);
+  const uint64_t livef = __ballot(act && lane >= kRoot && e != kBrk && e != kNone && !passed);
   const uint32_t fl = livef ? static_cast<uint32_t>(__builtin_ctzll(livef)) : kRoot;
   const uint32_t x = __shfl(e, last, 64), E = __shfl(g, fl, 64);
   if (lane == 0) {
     uint64_t *r = seg + static_cast<uint64_t>(blockIdx.x) * kRxsSegWords;
     r[0] = !livef || E == kBrk ? kRxsBroken : lo + E;
-    r[1] = x == kBrk ? kRxsBroken : lo + x;
+    r[1] = x == kBrk ? kRxsBroken : WHOLE && (x & kLongAt) ? kRxsLongExit | (lo + (x & ~kLongAt)) : lo + x;
     r[2] = x == kBrk ? kRxsBroken : rl32(incl, 63);
   }
 }
@@ -591,18 +652,230 @@ __device__ __forceinline__ uint64_t rxs_entry(uint64_t i, uint64_t E, uint64_t C
   return lo < C && nd[lo] == w ? lo : kRxsBroken;
 }
 
+// ------------------------------------- records past the staged stretch
+// (WHOLE walks: xdrg_index_records with max_rec_len past the index window)
+//   rxs_long     one wave per segment whose exit the walk left to it
+//                (kRxsLongExit): the record at that start, parsed by the
+//                whole wave -- the same parse on every lane -- through
+//                kRxsLongBlk-byte blocks of the stream in LDS, each refilled
+//                by one round trip of the wave's 16-byte loads; the exit
+//                becomes the record's end (kRxsBroken if it does not parse).
+//   rxs_mark     one thread per segment: the segments whose check against
+//                the previous segment's exit fails (a guess that missed: a
+//                look-back inside a long record's payload has no true chain
+//                to follow) or whose exit passes over a whole segment, into
+//                a list.
+//   rxs_fix      one wave, the listed segments in stream order, each from
+//                its true entry: a segment the entry passes over is passed
+//                over (no record starts there), any other is walked again
+//                by the wave from it (nodes, count, exit), and when the exit
+//                differs from the one its own walk found -- which the next
+//                segment was checked against -- the next segment follows.
+//                The entry of the first segment of such a run is the exit
+//                of a segment whose check held, so every entry is the true
+//                chain's (by induction from byte 0) and the index stays
+//                exact; rxs_check then takes the fixed segments' entries.
+//                More than kRxsFixCap listed segments: the list ranking.
+constexpr uint32_t kRxsLongBlk = 4096;
+constexpr uint32_t kRxsLongWaves = 4;
+// Wave-uniform block reader (every lane asks for the same word).
+struct rx_blk {
+  const uint8_t *s;
+  uint64_t len;
+  uint32_t *buf;  // kRxsLongBlk bytes of LDS
+  mutable uint64_t base;
+  __device__ void load(uint64_t p) const {
+    base = p & ~15ull;
+    wave_sync();  // every lane has read the old block
+    const uint32_t lane = __lane_id();
+#pragma unroll
+    for (uint32_t k = 0; k < kRxsLongBlk / 1024u; ++k) {
+      const uint64_t o = base + 16u * lane + 1024u * k;
+      u32x4 t;
+      if (o + 16u <= len) {
+        t = ld16u(s + o);
+      } else {
+        uint32_t w[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[j] = o + 4u * j + 4u <= len ? ld32(s + o + 4u * j) : 0u;
+        t = u32x4{w[0], w[1], w[2], w[3]};
+      }
+      reinterpret_cast<u32x4 *>(buf)[lane + 64u * k] = t;
+    }
+    wave_sync();
+  }
+  __device__ __forceinline__ uint32_t at(uint64_t p) const {
+    if (p - base >= kRxsLongBlk - 3u) load(p);
+    return buf[(p - base) >> 2];
+  }
+  __device__ __forceinline__ uint32_t operator()(uint64_t p) const { return at(p); }
+  __device__ __forceinline__ uint32_t atc(uint64_t p) const { return at(p); }
+  template <class U>
+  __device__ __forceinline__ void clamp(U &, uint32_t &, U) const {}
+};
+
+template <class P>
+__device__ __forceinline__ void rxs_long_body(const P &parser, const uint8_t *__restrict__ s, uint64_t len,
+                                              uint32_t maxlen, uint64_t *__restrict__ seg, uint64_t nseg) {
+  __shared__ __attribute__((aligned(16))) uint32_t blk[kRxsLongWaves][kRxsLongBlk / 4];
+  extern __shared__ __attribute__((aligned(16))) uint32_t rx_smem[];
+  const uint32_t w = threadIdx.x >> 6;
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kRxsLongWaves + w;
+  if (i >= nseg) return;
+  uint64_t *r = seg + i * kRxsSegWords + 1;
+  const uint64_t x = *r;
+  if (x == kRxsBroken || !(x & kRxsLongExit)) return;
+  const uint64_t a = x & ~kRxsLongExit;
+  parser.init(rx_smem);
+  const rx_blk rd{s, len, blk[w], 0};
+  rd.load(a);
+  const uint32_t L = parser.template rlen_rd<rx_blk, uint64_t>(rx_smem, rd, len, a, maxlen);
+  if (__lane_id() == 0) *r = L >= RX_OUT ? kRxsBroken : a + L;
+}
+
+// The entry that rxs_check compares segment i with: the entry rxs_fix
+// set (r[3]; 0 for segment 0 and for segments it did not touch), else the
+// previous segment's exit.
+__device__ __forceinline__ uint64_t rxs_prev(const uint64_t *__restrict__ seg, uint64_t i) {
+  const uint64_t f = seg[i * kRxsSegWords + 3];
+  return f ? f : i == 0 ? 0 : seg[(i - 1) * kRxsSegWords + 1];
+}
+// The walk's own verdict on segment i given its entry prev: its node index
+// there, kRxsBroken when its chain does not hold prev; ~1ull when no record
+// starts in it (prev at or past its end).
+constexpr uint64_t kRxsPassOver = ~1ull;
+__device__ __forceinline__ uint64_t rxs_verdict(const uint64_t *__restrict__ seg, const uint16_t *__restrict__ nodes,
+                                                uint64_t i, uint64_t nseg, uint64_t len, uint64_t prev) {
+  if (prev != kRxsBroken && prev >= min(len, (i + 1) * kRxsSeg))
+    return i == nseg - 1 && prev != len ? kRxsBroken : kRxsPassOver;
+  const uint64_t *r = seg + i * kRxsSegWords;
+  const uint64_t k = rxs_entry(i, r[0], r[2], prev, len, nodes);
+  return k != kRxsBroken && (i != nseg - 1 || r[1] == len) ? k : kRxsBroken;
+}
+
+// One thread per segment: the segments rxs_fix takes, appended to list
+// (count in *nl, zeroed by the walk).
+__device__ __forceinline__ void rxs_mark_body(const uint64_t *__restrict__ seg, const uint16_t *__restrict__ nodes,
+                                              uint64_t nseg, uint64_t len, uint64_t *__restrict__ list,
+                                              unsigned long long *nl) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= nseg) return;
+  const uint64_t x = seg[i * kRxsSegWords + 1];
+  const bool far = x != kRxsBroken && x >= (i + 2) * kRxsSeg;
+  if (far || rxs_verdict(seg, nodes, i, nseg, len, i == 0 ? 0 : seg[(i - 1) * kRxsSegWords + 1]) == kRxsBroken)
+    list[atomicAdd(nl, 1ull)] = i;
+}
+
+constexpr uint32_t kRxsFixBits = 1u << 18;  // segments the fix's LDS bitmap covers (1.8 GB of stream)
+constexpr uint64_t kRxsFixCap = 4096;       // listed segments it takes at most
+template <class P>
+__device__ __forceinline__ void rxs_fix_body(const P &parser, const uint8_t *__restrict__ s, uint64_t len,
+                                             uint32_t maxlen, uint64_t *__restrict__ seg, uint64_t nseg,
+                                             uint16_t *__restrict__ nodes, const uint64_t *__restrict__ list,
+                                             const unsigned long long *nl, uint32_t *__restrict__ flag) {
+  __shared__ uint32_t bits[kRxsFixBits / 32];
+  __shared__ __attribute__((aligned(16))) uint32_t blk[kRxsLongBlk / 4];
+  extern __shared__ __attribute__((aligned(16))) uint32_t rx_smem[];
+  const uint32_t lane = threadIdx.x;
+  const uint64_t c = *nl;
+  if (c == 0) return;
+  if (nseg > kRxsFixBits || c > kRxsFixCap) {  // (the list ranking)
+    if (lane == 0) *flag = 0u;
+    return;
+  }
+  const uint32_t nw = static_cast<uint32_t>((nseg + 31) / 32);
+  for (uint32_t j = lane; j < nw; j += 64u) bits[j] = 0u;
+  wave_sync();
+  for (uint64_t j = lane; j < c; j += 64u) {
+    const uint64_t k = list[j];
+    atomicOr(&bits[k >> 5], 1u << (k & 31u));
+  }
+  wave_sync();
+  parser.init(rx_smem);
+  const rx_blk rd{s, len, blk, 0};
+  uint64_t cover = 0;  // segments below it are decided
+  for (uint32_t j0 = 0; j0 < nw; j0 += 64u) {
+    const uint32_t mine = j0 + lane < nw ? bits[j0 + lane] : 0u;
+    uint64_t any = __ballot(mine != 0u);
+    while (any) {
+      const uint32_t l = __builtin_ctzll(any);
+      any &= any - 1;
+      uint32_t word = __shfl(mine, l, 64);
+      while (word) {
+        uint64_t i = 32ull * (j0 + l) + __builtin_ctz(word);
+        word &= word - 1;
+        if (i < cover) continue;  // decided by an earlier run
+        // the run from i: its entry is the exit of segment i - 1, whose own
+        // check held (it is not listed, or a run ended there)
+        uint64_t x = i == 0 ? 0 : seg[(i - 1) * kRxsSegWords + 1];
+        for (;;) {
+          uint64_t *r = seg + i * kRxsSegWords;
+          const uint64_t own = r[1];
+          const uint64_t s0 = i * kRxsSeg, s1 = min(len, s0 + kRxsSeg);
+          uint64_t q = x;
+          bool ok = true;
+          const uint64_t v = rxs_verdict(seg, nodes, i, nseg, len, x);
+          if (v == kRxsPassOver) {  // passed over
+            if (lane == 0) r[3] = x;
+          } else if (v != kRxsBroken) {  // its own walk holds from x
+            q = own;
+            if (lane == 0) r[3] = x;
+          } else {  // walked again from x: its records' nodes, count and exit
+            uint64_t m = 0;
+            rd.load(q);
+            while (q < s1) {
+              if (lane == 0) nodes[i * (kRxsSeg / 4) + m] = static_cast<uint16_t>((q - s0) >> 2);
+              ++m;
+              const uint32_t L = parser.template rlen_rd<rx_blk, uint64_t>(rx_smem, rd, len, q, maxlen);
+              if (L >= RX_OUT) {
+                ok = false;
+                break;
+              }
+              q += L;
+            }
+            if (lane == 0) {
+              r[0] = x;
+              r[1] = ok ? q : kRxsBroken;
+              r[2] = ok ? m : kRxsBroken;
+              r[3] = x;
+            }
+          }
+          cover = i + 1;
+          if (!ok || i + 1 >= nseg) break;
+          // the next segment was checked against the exit its walk found:
+          // it follows when that is not the true one, or when the true one
+          // passes over it
+          if (q == own && q < (i + 2) * kRxsSeg) break;
+          ++i;
+          x = q;
+        }
+      }
+    }
+  }
+}
+
 // One thread per segment: the true entry among the segment's nodes.
-// cnt[i] = the segment's records (for the scan).
+// cnt[i] = the segment's records (for the scan).  Segments where no record
+// starts (the previous exit at or past their end) are passed over.  LONG
+// (WHOLE walks): the entries rxs_fix set.
+template <bool LONG = false>
 __device__ __forceinline__ void rxs_check_body(uint64_t *__restrict__ seg, const uint16_t *__restrict__ nodes,
                                                uint64_t nseg, uint64_t len, unsigned long long *__restrict__ cnt,
                                                uint32_t *__restrict__ flag) {
   const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= nseg) return;
   uint64_t *r = seg + i * kRxsSegWords;
-  const uint64_t C = r[2], k = rxs_entry(i, r[0], C, i == 0 ? 0 : seg[(i - 1) * kRxsSegWords + 1], len, nodes);
-  const bool ok = k != kRxsBroken && (i != nseg - 1 || r[1] == len);
+  const uint64_t prev = LONG ? rxs_prev(seg, i) : i == 0 ? 0 : seg[(i - 1) * kRxsSegWords + 1];
+  const uint64_t k = rxs_verdict(seg, nodes, i, nseg, len, prev);
+  if (k == kRxsPassOver) {  // no record starts in the segment
+    r[0] = 0;
+    r[2] = 0;
+    cnt[i] = 0;
+    return;
+  }
+  const bool ok = k != kRxsBroken;
   r[0] = ok ? k : 0;
-  cnt[i] = ok ? C - k : 0;
+  cnt[i] = ok ? r[2] - k : 0;
   if (!ok) *flag = 0u;
 }
 

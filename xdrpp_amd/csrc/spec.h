@@ -16,7 +16,7 @@ constexpr int kSpecDevices = 64;
 // Interface version of the generated kernels (their parameter lists and
 // LDS layout, var_kernels.h): the source defines xdrg_spec_iface with it,
 // and a code object that carries another value is refused at load.
-constexpr unsigned kSpecIface = 12;
+constexpr unsigned kSpecIface = 13;
 
 // The generated source of a plan and the launch facts it fixes.
 struct spec_info {
@@ -28,6 +28,7 @@ struct spec_info {
   uint32_t list_words = 0; // ... of this many words per record (the mark included)
   uint64_t src_hash = 0;  // FNV-1a of the source (before the line that defines it)
   bool frame_walk = false;  // a recursive plan: the module holds the frame walks only
+  bool tail_rx = false;     // ... and, a linked list (codegen.cpp tail_list), the index's record parse
 };
 
 // Kernels of one plan on one device.
@@ -36,6 +37,7 @@ struct spec_module {
   void *f_size = nullptr, *f_enc = nullptr, *f_dec = nullptr, *f_dec_copy = nullptr;  // hipFunction_t
   void *f_ix_seg = nullptr;  // record-start parse of the plain-stream index (list ranking)
   void *f_rxs_walk = nullptr;  // ... and its speculative chain walk
+  void *f_rxs_walk_whole = nullptr, *f_rxs_long = nullptr, *f_rxs_fix = nullptr;  // ... over records of any length
   void *f_enc_lb = nullptr, *f_enc_pre = nullptr;  // word-list plans: encode walked first (look-back / sized)
   // recursive plans: the frame walks (sub_kernels.h) over the plan's ops
   void *f_sub_size = nullptr, *f_sub_depth = nullptr, *f_sub_enc = nullptr, *f_sub_dec = nullptr;

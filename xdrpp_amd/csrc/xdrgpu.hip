@@ -1088,10 +1088,16 @@ __global__ __launch_bounds__(256) void k_ix_seg(const uint8_t *__restrict__ s, u
 
 // The fast path's scan-side kernels (index_kernels.h); its walk is the
 // plan's generated xdrg_spec_rxs_walk.
+template <bool LONG>
 __global__ __launch_bounds__(256) void k_rxs_check(uint64_t *__restrict__ seg, const uint16_t *__restrict__ nodes,
                                                    uint64_t nseg, uint64_t len, unsigned long long *__restrict__ cnt,
                                                    uint32_t *__restrict__ flag) {
-  rxs_check_body(seg, nodes, nseg, len, cnt, flag);
+  rxs_check_body<LONG>(seg, nodes, nseg, len, cnt, flag);
+}
+__global__ __launch_bounds__(256) void k_rxs_mark(const uint64_t *__restrict__ seg, const uint16_t *__restrict__ nodes,
+                                                  uint64_t nseg, uint64_t len, uint64_t *__restrict__ list,
+                                                  unsigned long long *nl) {
+  rxs_mark_body(seg, nodes, nseg, len, list, nl);
 }
 template <bool EXACT>
 __global__ __launch_bounds__(256) void k_rxs_emit(const uint64_t *__restrict__ seg,
@@ -2442,7 +2448,7 @@ template <bool REC>
 int run_index(const xdrg_plan *p, const dev_tables *T, const void *d_stream, uint64_t len,
               uint32_t max_msg_len, uint64_t max_msgs, uint64_t *d_offsets, uint64_t *d_count,
               void *d_ws, size_t ws_bytes, xdrg_status *d_status, hipStream_t s,
-              const ix_cont &C = ix_cont{}, bool fast_only = false) {
+              const ix_cont &C = ix_cont{}, bool fast_only = false, bool whole = false) {
   const ix_layout L = ix_plan(len, max_msg_len);
   if (!d_ws || ws_bytes < L.total) return XDRG_ESPACE;
   if (L.nseg > 0xffffffffull) return XDRG_EUNSUPPORTED;
@@ -2475,7 +2481,12 @@ int run_index(const xdrg_plan *p, const dev_tables *T, const void *d_stream, uin
   // the tables are needed above one segment; the valid-node lists always
   // record starts: the plan's generated parse when its kernels are built
   // (codegen.cpp plan_rx), else the interpreted rx_len
-  const spec_module *SM = REC && p->opts.specialize && !p->deep ? spec_get(*p) : nullptr;
+  // (recursive plans: a linked list's generated parse, codegen.cpp tail_list)
+  const spec_module *SM = REC && p->opts.specialize ? spec_get(*p) : nullptr;
+  if (SM && !SM->f_rxs_walk) SM = nullptr;
+  // whole: the walk over records of any length (rx_windows): its parse has
+  // no maxlen, and records past the staged stretch go to rxs_long
+  if (whole && !(SM && SM->f_rxs_walk_whole && SM->f_rxs_long && SM->f_rxs_fix)) whole = false;
   // Record index: the speculative chain walk first (index_kernels.h rxs_*);
   // the list ranking below runs only when its checks fail.  Short streams
   // (a few segments) go to the list ranking alone.
@@ -2487,6 +2498,8 @@ int run_index(const xdrg_plan *p, const dev_tables *T, const void *d_stream, uin
   // Message streams walk their marks (mark_rx) always.
   const bool walk_ok = REC ? SM && SM->f_rxs_walk && p->opts.index_fast : true;
   int gate = REC ? p->opts.index_fast : 1;
+  const bool walk_only = gate == 3;  // (a tuning aid: the walk's records stay in the workspace)
+  if (walk_only) gate = 1;
   if (gate == 1) {  // a stream being captured into a graph cannot be waited on: stay asynchronous
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) gate = 2;
@@ -2505,15 +2518,32 @@ int run_index(const xdrg_plan *p, const dev_tables *T, const void *d_stream, uin
     uint16_t *nodes = reinterpret_cast<uint16_t *>(vlist);  // the list ranking's lists, unused when it skips
     const uint32_t ns = static_cast<uint32_t>(L.rxs_nseg);
     if (REC) {
-      uint32_t ml = max_msg_len, hf = rp.fpc != RX_BAD, fd = rp.fd;
+      uint32_t ml = whole ? 0xffffffffu : max_msg_len, hf = rp.fpc != RX_BAD, fd = rp.fd;
       void *args[] = {&s8, &len, &ml, &seg, &nodes, &flag, &hf, &fd};
-      HIPCHK(hipModuleLaunchKernel(static_cast<hipFunction_t>(SM->f_rxs_walk), ns, 1, 1, 64, 1, 1, 0, s, args,
-                                   nullptr));
+      HIPCHK(hipModuleLaunchKernel(static_cast<hipFunction_t>(whole ? SM->f_rxs_walk_whole : SM->f_rxs_walk), ns, 1,
+                                   1, 64, 1, 1, 0, s, args, nullptr));
+      if (whole) {  // the records the walk left past its stretches, then the segments they pass over
+        uint64_t nsg = L.rxs_nseg;
+        void *largs[] = {&s8, &len, &ml, &seg, &nsg};
+        HIPCHK(hipModuleLaunchKernel(static_cast<hipFunction_t>(SM->f_rxs_long), (ns + kRxsLongWaves - 1) / kRxsLongWaves,
+                                     1, 1, 64 * kRxsLongWaves, 1, 1, 0, s, largs, nullptr));
+        // (the list of segments to fix in the counts' area, rxs_check writes them after)
+        uint64_t *list = reinterpret_cast<uint64_t *>(cnt);
+        auto *nl = reinterpret_cast<unsigned long long *>(flag + 2);
+        k_rxs_mark<<<(ns + 255) / 256, 256, 0, s>>>(seg, nodes, L.rxs_nseg, len, list, nl);
+        HIPCHK(hipGetLastError());
+        void *jargs[] = {&s8, &len, &ml, &seg, &nsg, &nodes, &list, &nl, &flag};
+        HIPCHK(hipModuleLaunchKernel(static_cast<hipFunction_t>(SM->f_rxs_fix), 1, 1, 1, 64, 1, 1, 0, s, jargs,
+                                     nullptr));
+      }
     } else {
       k_rxs_walk_msgs<<<ns, 64, 0, s>>>(s8, len, max_msg_len, seg, nodes, flag);
       HIPCHK(hipGetLastError());
     }
-    k_rxs_check<<<(ns + 255) / 256, 256, 0, s>>>(seg, nodes, L.rxs_nseg, len, cnt, flag);
+    if (whole)
+      k_rxs_check<true><<<(ns + 255) / 256, 256, 0, s>>>(seg, nodes, L.rxs_nseg, len, cnt, flag);
+    else
+      k_rxs_check<false><<<(ns + 255) / 256, 256, 0, s>>>(seg, nodes, L.rxs_nseg, len, cnt, flag);
     HIPCHK(hipGetLastError());
     if (int rc = launch_block_scan(cnt, base, ns, tot, nullptr, 0, s)) return rc;
     // the verdict also into this thread's mapped host word (gate 1): the
@@ -2538,6 +2568,7 @@ int run_index(const xdrg_plan *p, const dev_tables *T, const void *d_stream, uin
       }
       if (h == 1u) return XDRG_OK;
       if (fast_only) return kIxNotHeld;
+      if (walk_only) return XDRG_OK;
     } else {
       skip = flag;  // asynchronous: the list ranking's kernels skip themselves
     }
@@ -2653,14 +2684,27 @@ int rx_windows(const xdrg_plan *p, const dev_tables *T, const uint8_t *s8, uint6
                hipStream_t s) {
   const size_t need = xdrg_index_workspace_size(len, XDRG_INDEX_MAX_MSG + 4u);
   if (!d_ws || ws_bytes < need) return XDRG_ESPACE;
-  {  // the rounds wait on the stream: a stream being captured cannot be waited on
+  {  // the rounds wait on the stream: a stream being captured cannot be waited
+     // on.  There the walk over the whole stream runs alone, asynchronously:
+     // when its checks fail the list ranking over records up to the window
+     // follows (its kernels skip themselves otherwise), which reports
+     // XDRG_ERR_INDEX_LONG at a longer record
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return XDRG_EUNSUPPORTED;
+    if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
+      const spec_module *SM = p->opts.specialize ? spec_get(*p) : nullptr;
+      if (!(SM && SM->f_rxs_walk_whole && SM->f_rxs_long && SM->f_rxs_fix && p->opts.index_fast))
+        return XDRG_EUNSUPPORTED;
+      return run_index<true>(p, T, s8, len, XDRG_INDEX_MAX_MSG, n, d_offsets, d_count, d_ws, ws_bytes, d_status, s,
+                             ix_cont{}, false, true);
+    }
   }
-  {
+  {  // the speculative walk over the whole stream, records of any length (a
+     // plan with the generated parse: rxs_long takes the long ones); else
+     // over records up to the index window
     const int rc = run_index<true>(p, T, s8, len, XDRG_INDEX_MAX_MSG, n, d_offsets, d_count, d_ws, ws_bytes,
-                                   d_status, s, ix_cont{}, true);
+                                   d_status, s, ix_cont{}, true, true);
     if (rc != kIxNotHeld) return rc;
+    if (p->opts.index_fast == 3) return XDRG_OK;  // the walk alone (XDRG_OPT_INDEX_FAST)
   }
   const ix_layout L0 = ix_plan(len, XDRG_INDEX_MAX_MSG);
   auto *next = reinterpret_cast<unsigned long long *>(static_cast<char *>(d_ws) + L0.total);
@@ -2761,7 +2805,7 @@ int xdrg_plan_set_option(xdrg_plan *p, int option, int64_t value) {
   case XDRG_OPT_GRP_NONTEMPORAL: O.grp_nontemporal = v ? 1 : 0; return XDRG_OK;
   case XDRG_OPT_SPECIALIZE: O.specialize = v ? 1 : 0; return XDRG_OK;
   case XDRG_OPT_INDEX_FAST:
-    if (v < 0 || v > 2) return XDRG_EINVAL;
+    if (v < 0 || v > 3) return XDRG_EINVAL;
     O.index_fast = static_cast<int>(v); return XDRG_OK;
   case XDRG_OPT_STAGE_BYTES:
     if (v > (32 << 10)) return XDRG_EINVAL;
