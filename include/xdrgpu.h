@@ -281,12 +281,13 @@ int xdrg_abi_version(void);
  * the first under ROCm's graph packet capture (DEBUG_CLR_GRAPH_PACKET_
  * CAPTURE, on by default; tools/gpu/graph_node_probe.py, profiles/r05e),
  * which left the deep passes' list counters stale and faulted a recursive
- * plan's second replay (profiles/r04c, r05a-d).  Every default kernel is
- * free of private (scratch) memory; the two interpreter kernels that are
- * not (the window decode of a plan run without its specialized kernels,
- * and the encode interpreter at XDRG_OPT_ENC_UNROLL 16) return
- * XDRG_EUNSUPPORTED on a capturing stream.  Run a plan's first launch on a
- * device outside the capture (it uploads the plan's tables).
+ * plan's second replay (profiles/r04c, r05a-d).  Kernels with private
+ * (scratch) memory replay correctly, also when the runtime grows its
+ * scratch area between replays (profiles/r06_graph): the two interpreter
+ * kernels that keep private memory (the window decode of a plan run without
+ * its specialized kernels, and the encode interpreter at
+ * XDRG_OPT_ENC_UNROLL 16) are capturable like the rest.  Run a plan's first
+ * launch on a device outside the capture (it uploads the plan's tables).
  */
 
 /* Validate and compile an immutable plan.  `table` holds enum value lists

@@ -2,11 +2,12 @@
 xdrg_index_records' default verdict wait and xdrg_index_msgs past 16,380-byte
 messages is capturable), replayed several times to the reference's bytes.
 
-Kernels with private (scratch) memory do not survive a second replay under
-ROCm's graph packet capture (DEBUG_CLR_GRAPH_PACKET_CAPTURE, on by default:
-profiles/r05a, r05b): every default kernel is scratch-free, and the two
-interpreter kernels that are not refuse a capturing stream
-(XDRG_EUNSUPPORTED).  Reference path: xdr_to_opaque / xdr_from_opaque,
+Memset nodes of 16 bytes or more take effect on the first replay only
+under ROCm's graph packet capture (DEBUG_CLR_GRAPH_PACKET_CAPTURE, on by
+default: profiles/r05e, r06_graph), so the library fills and copies with its
+own kernels; kernels with private (scratch) memory replay correctly
+(profiles/r06_graph), so the interpreter kernels that keep some are
+captured too.  Reference path: xdr_to_opaque / xdr_from_opaque,
 xdrpp/marshal.h:264-272, :299-306; bytes from the restatement pinned to the
 reference (tests/test_oracle.py) and the golden fixtures."""
 import numpy as np
@@ -74,27 +75,47 @@ def test_capture_encode_decode_replays(dev, name, n):
             assert np.array_equal(hout.cpu().numpy()[:oheap.size], oheap)
 
 
-def test_scratch_interpreter_refuses_capture(dev):
-    """The window decode interpreter (k_var_decode_w, plans run without
-    their specialized kernels) keeps private memory: a capturing stream gets
-    XDRG_EUNSUPPORTED before anything is queued; it runs eagerly."""
+@pytest.mark.parametrize("name", ["recvar", "rpc"])
+@pytest.mark.parametrize("opts", [{"specialize": 0}, {"specialize": 0, "enc_unroll": 16}],
+                         ids=["window_decode_interp", "enc_unroll16"])
+def test_scratch_interpreter_capture_replays(dev, name, opts):
+    """The interpreter kernels with private memory -- the window decode
+    (k_var_decode_w, plans run without their specialized kernels) and the
+    encode interpreter at XDRG_OPT_ENC_UNROLL 16 -- captured with the rest of
+    an encode + decode and replayed 4x against the goldens."""
     from xdrpp_amd import marshal as M
     n = 1024
-    plan = M.Plan(S.recvar, {"specialize": 0})
+    plan = M.Plan(S.ALL[name], opts)
     mar = M.Marshaler(plan, dev)
-    nat, heap = W.recvar(n)
+    nat, heap = W.GENERATORS[name](n)
+    want = golden(name, n, "xdr")
     x, offs = O.encode(plan.cp, nat, n, heap)
-    dx, doffs = _dev(x, dev), _dev(offs.astype(np.int64), dev)
+    assert np.array_equal(x, want)
+    onat, oheap = O.decode(plan.cp, x, n, offs)
+    dn, dh = _dev(nat, dev), _dev(heap, dev)
+    out = torch.empty(x.size, dtype=torch.uint8, device=dev)
+    offsets = torch.empty(n + 1, dtype=torch.int64, device=dev)
     back = torch.zeros(n * plan.stride, dtype=torch.uint8, device=dev)
-    hout = torch.zeros(plan.decode_heap_bytes(x.size), dtype=torch.uint8, device=dev)
-    mar.decode(dx, n, doffs)  # warm: the plan's device tables are uploaded by its first launch
+    hout = torch.zeros(max(plan.decode_heap_bytes(x.size), 16), dtype=torch.uint8, device=dev)
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):  # warm: plan tables and kernels outside the capture
+        mar.status.init(side.cuda_stream)
+        mar.launch_encode(dn, n, out, heap=dh, offsets=offsets, stream=side.cuda_stream)
+        mar.launch_decode(out, n, back, offsets=offsets, heap_out=hout, stream=side.cuda_stream)
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
-        with pytest.raises(A.AbiError, match="EUNSUPPORTED"):
-            mar.launch_decode(dx, n, back, offsets=doffs, heap_out=hout,
-                              stream=torch.cuda.current_stream().cuda_stream)
-    torch.cuda.synchronize()
-    nb, hb = mar.decode(dx, n, doffs)
-    onat, oheap = O.decode(plan.cp, x, n, offs)
-    assert np.array_equal(nb.cpu().numpy(), onat) and np.array_equal(hb.cpu().numpy(), oheap)
+        s = torch.cuda.current_stream().cuda_stream
+        mar.launch_encode(dn, n, out, heap=dh, offsets=offsets, stream=s)
+        mar.launch_decode(out, n, back, offsets=offsets, heap_out=hout, stream=s)
+    for _ in range(4):
+        out.zero_()
+        back.zero_()
+        hout.zero_()
+        mar.status.init(torch.cuda.current_stream().cuda_stream)
+        g.replay()
+        assert mar.check().code == 0
+        assert np.array_equal(out.cpu().numpy(), want)
+        assert np.array_equal(back.cpu().numpy(), onat)
+        assert np.array_equal(hout.cpu().numpy()[:oheap.size], oheap)

@@ -1740,22 +1740,6 @@ int run_fixed(const xdrg_plan &p, const dev_tables &T, bool decode, const void *
   return XDRG_OK;
 }
 
-// Kernels with private (scratch) memory do not survive repeated replays of
-// a hipGraph under ROCm's graph packet capture (DEBUG_CLR_GRAPH_PACKET_CAPTURE,
-// on by default): the second replay of the frame walks, when their frames
-// lived in private memory, faulted with HSA_STATUS_ERROR_MEMORY_APERTURE_
-// VIOLATION, while the same graph replayed bit-exact with the packet capture
-// off and graphs of scratch-free kernels replay under it (profiles/r05a,
-// r05b).  Every default kernel is scratch-free; a capturing stream gets
-// XDRG_EUNSUPPORTED from the launches that would use one of the two that are
-// not (the interpreters' window decode, k_var_decode_w, and the encode
-// interpreter at XDRG_OPT_ENC_UNROLL 16).
-int refuse_scratch_capture(hipStream_t s) {
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return XDRG_EUNSUPPORTED;
-  return XDRG_OK;
-}
-
 // Var workspace: u32 sizes[n], the 64-record block sums, then their
 // exclusive scan (a separate array: the multi-workgroup scan reads the sums
 // while other workgroups write the bases).
@@ -2198,8 +2182,6 @@ int var_encode(const xdrg_plan &P, const dev_tables &T, const void *d_native, ui
     return XDRG_OK;
   }
   if (kern == 3) {
-    if (O.enc_unroll == 16)
-      if (int rc = refuse_scratch_capture(s)) return rc;
 #define LAUNCH_ENC_IU(K, UU)                                                                   \
   k_var_encode_i<K, UU><<<nb, 64, LI.total, s>>>(nat8, n, p->stride, d_heap, heap_len, xdr8,  \
                                                  cap, d_offsets, sizes, bbase, T.d_ops, nops,   \
@@ -2413,7 +2395,6 @@ int var_decode(const xdrg_plan &P, const dev_tables &T, const void *d_xdr, uint6
     return XDRG_OK;
   }
   if (kern == 2) {
-    if (int rc = refuse_scratch_capture(s)) return rc;
     const uint64_t nb = (n + 63) / 64;
 #define LAUNCH_DEC_W(CP, RA)                                                                      \
   k_var_decode_w<CP, RA><<<nb, 64, lw, s>>>(xdr8, len, d_offsets, n, nat8, p->stride, d_heap_out, \
