@@ -338,7 +338,7 @@ def test_gpu_index_records_past_the_window(dev, spec):
         assert np.array_equal(got, want), label
         assert gcnt == wcnt, label
         assert (err.code if err else 0) == wrc, label
-        if label == "good" and spec:  # the walk over the whole stream held it (rxs_long took the long records)
+        if label == "good" and spec:  # the walk over the whole stream held it (its waves parsed the long records)
             assert _fast_flag(tail) == 1
     # a window-sized max_rec_len still hands such a stream back (INDEX_LONG)
     got, gcnt, err = _gpu_index(mar, x, n, A.INDEX_MAX_MSG, dev)
@@ -373,7 +373,7 @@ def test_gpu_index_rp_list_full_size(dev, manifest):
     offs = mar.index_records(r.xdr, n)
     assert torch.equal(offs, r.offsets)
     # the speculative walk over the whole stream held it: the lists' generated
-    # parse (codegen.cpp tail_list), the 500-node lists left to rxs_long
+    # parse (codegen.cpp tail_list), the 500-node lists parsed by the walk's waves
     got, cnt, err, tail = _gpu_index(mar, r.xdr.cpu().numpy(), n, A.MAX_MSG, dev, ws_tail=True)
     assert err is None and cnt == n and np.array_equal(got, r.offsets.cpu().numpy().view(np.uint64))
     assert _fast_flag(tail) == 1

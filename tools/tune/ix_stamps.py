@@ -75,7 +75,10 @@ def run(schemas):
         nat, heap = (torch.from_numpy(a).to(dev) for a in W.GENERATORS[name](n))
         enc = mar.encode(nat, n, heap)
         total = enc.xdr.numel()
-        maxlen = min(p.max_record_bytes, A.INDEX_MAX_MSG)
+        # WHOLE=1: the bound the bench's plain stream passes (records of any
+        # length: the whole-stream walk when it is past the index window)
+        cap = 0xFFFFFFFF if os.environ.get("WHOLE") else A.INDEX_MAX_MSG
+        maxlen = min(p.max_record_bytes, cap)
         ws = torch.zeros(L.xdrg_index_workspace_size(total, maxlen), dtype=torch.uint8, device=dev)
         offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
         cnt = torch.empty(1, dtype=torch.int64, device=dev)
@@ -95,6 +98,17 @@ def run(schemas):
             d[ph] = [int(np.median(dd)), int(np.percentile(dd, 90)), int(dd.max())]
         d["wave"] = [int(np.median(st[:, 5] - st[:, 0])), int(np.percentile(st[:, 5] - st[:, 0], 90))]
         print(name, "segments", nseg, "cycles [median, p90, max]:", d, flush=True)
+        # the timeline: the kernel's span, the waves' summed time over it (the
+        # mean number in flight), and where the slowest waves sit in it
+        t0, t1 = st[:, 0].min(), st[:, 5].max()
+        dur = st[:, 5] - st[:, 0]
+        slow = np.argsort(dur)[-5:]
+        print(f"  span {t1 - t0} cycles; mean waves in flight {dur.sum() / (t1 - t0):.1f}; last start at "
+              f"{st[:, 0].max() - t0}; slowest waves (start, cycles): "
+              f"{[(int(st[i, 0] - t0), int(dur[i])) for i in slow]}", flush=True)
+        ends = np.sort(st[:, 5] - t0)
+        print(f"  ends: 50% at {ends[len(ends) // 2]}, 90% at {ends[int(len(ends) * 0.9)]}, "
+              f"99% at {ends[int(len(ends) * 0.99)]}, last {ends[-1]}", flush=True)
         o2 = nseg * (SEGB // 2 + NST * 8)
         nb = min(nseg, LBLK)
         assert o2 + nb * 64 * 32 <= ws.numel()

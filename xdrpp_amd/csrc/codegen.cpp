@@ -1148,12 +1148,13 @@ void seal(std::string src, spec_info &info) {
 // The record-start parse of the plain-stream index (plan_rx) and its index
 // kernels: the list ranking's segment parse, the speculative walk over
 // records up to the index window, the same walk over records of any length
-// (xdrg_index_records with max_rec_len past the window: records past the
-// staged stretch left to rxs_long) and rxs_long itself.
+// (xdrg_index_records with max_rec_len past the window: a record past the
+// staged stretch parsed by the wave through blocks of the stream) and the
+// one-wave repair of its failed segments (rxs_fix).
 std::string rx_source(const std::string &first, const std::string &flen, const std::string &second,
                       const std::string &rx_code, const std::string &rxs_code) {
   std::ostringstream s;
-  s << "struct plan_rx {  // index_kernels.h ix_seg_body's, rxs_walk_body's, rxs_long_body's and rxs_fix_body's parser\n"
+  s << "struct plan_rx {  // index_kernels.h ix_seg_body's, rxs_walk_body's and rxs_fix_body's parser\n"
     << "  __device__ __forceinline__ void init(uint32_t *) const {}\n"
     << "  __device__ __forceinline__ bool first_ok(const uint32_t *, uint32_t v) const { return " << first << "; }\n"
     << "  __device__ __forceinline__ uint64_t first_len(uint32_t v) const { return " << flen << "; }\n"
@@ -1198,13 +1199,10 @@ std::string rx_source(const std::string &first, const std::string &flen, const s
     << "    const uint8_t *s, uint64_t len, uint32_t maxlen, uint64_t *seg, uint16_t *nodes,\n"
     << "    uint32_t *flag, uint32_t has_first, uint32_t fd) {\n"
     << "  rxs_walk_body<true>(plan_rx{}, s, len, maxlen, seg, nodes, flag, has_first != 0, fd);\n}\n\n"
-    << "extern \"C\" __global__ __launch_bounds__(64 * kRxsLongWaves) void xdrg_spec_rxs_long(\n"
-    << "    const uint8_t *s, uint64_t len, uint32_t maxlen, uint64_t *seg, uint64_t nseg) {\n"
-    << "  rxs_long_body(plan_rx{}, s, len, maxlen, seg, nseg);\n}\n\n"
     << "extern \"C\" __global__ __launch_bounds__(64) void xdrg_spec_rxs_fix(\n"
     << "    const uint8_t *s, uint64_t len, uint32_t maxlen, uint64_t *seg, uint64_t nseg, uint16_t *nodes,\n"
-    << "    const uint64_t *list, const unsigned long long *nl, uint32_t *flag) {\n"
-    << "  rxs_fix_body(plan_rx{}, s, len, maxlen, seg, nseg, nodes, list, nl, flag);\n}\n\n";
+    << "    const uint64_t *list, const unsigned long long *nl, uint32_t *flag, unsigned long long *cnt) {\n"
+    << "  rxs_fix_body(plan_rx{}, s, len, maxlen, seg, nseg, nodes, list, nl, flag, cnt);\n}\n\n";
   return s.str();
 }
 

@@ -266,7 +266,11 @@ struct rx_goff {
 //              later node of this segment where a chain that entered early
 //              merged into the true one, and no chain may break; the nodes
 //              from it on are the segment's records.  (A record that spans
-//              a whole segment passes only when the guess agrees.)
+//              a whole segment passes only when the guess agrees.)  In a
+//              walk over records of any length (WHOLE) a segment that fails
+//              goes to rxs_fix instead.
+//   rxs_fix    (WHOLE) one wave re-decides the failed segments in stream
+//              order from the true entry (below).
 //   (scan)     exclusive scan of those counts (launch_block_scan).
 //   rxs_emit   when the last exit is the stream's end and the chain holds
 //              exactly n records: offsets[] from the node lists, offsets[n]
@@ -291,15 +295,15 @@ constexpr uint32_t kRxsAhead = 9u * 1024 - 64 * kRxsSub;  // staged past the seg
 constexpr uint64_t kRxsBroken = ~0ull;
 // in the walk (32-bit offsets into the stretch): a broken chain, no state
 constexpr uint32_t kBrk = 0xffffffffu, kNone = 0xfffffffeu;
-// segment record: entry E (rxs_check: the index of its first true node),
-// exit, node count (kRxsBroken: the chain broke), nodes from the true entry
+// segment record: entry E, exit, node count (kRxsBroken: the chain broke),
+// and (rxs_check / rxs_fix) the index of its first true node
 constexpr uint32_t kRxsSegWords = 4;
 
 // One record parse at q: from the staged stretch, or from global memory
 // when the record reaches past it.  In a walk over a stream of records of
 // any length (WHOLE: xdrg_index_records with max_rec_len past the index
-// window) such a record is RX_OUT: it is left to rxs_long, whose wave
-// parses it through blocks of the stream in LDS (one lane's parse through
+// window) such a record is RX_OUT: it is left to the wave, which parses it
+// at the walk's end through blocks of the stream in LDS (one lane's parse through
 // global memory waits on every length it reads: a 500-node rp__list took
 // milliseconds that way), and the walk knows where it starts -- a record
 // from the look-back that runs past the stretch is the segment's only
@@ -332,7 +336,7 @@ struct rxs_nodes {
 // position reached, or kBrk -- or (WHOLE) kLongAt | q for a chain whose
 // record at q runs past the staged stretch: it passes every lane after it
 // (kLongAt | q is at or past any lane's end) and becomes the segment's
-// exit, which rxs_long resolves to the record's end.
+// exit, which the wave resolves to the record's end (rx_blk).
 constexpr uint32_t kLongAt = 0x80000000u;  // (stretch offsets stay below 2^31)
 template <bool WHOLE = false, class P>
 __device__ __forceinline__ uint32_t rxs_chain(const P &parser, const uint32_t *smem, const rx_lds &st,
@@ -395,9 +399,47 @@ struct mark_rx {
 #define XDRG_LDBG(k, v) ((void)0)
 #endif
 
-// The segment record's exit word for a chain whose last record was left to
-// rxs_long: that record's start, flagged.
-constexpr uint64_t kRxsLongExit = 1ull << 62;
+// A WHOLE walk's chain whose last record runs past the staged stretch: the
+// wave parses that record through kRxsLongBlk-byte blocks of the stream in
+// LDS (the stretch's, free by then), each refilled by one round trip of the
+// wave's 16-byte loads -- the same parse on every lane.
+constexpr uint32_t kRxsLongBlk = 4096;
+// Wave-uniform block reader (every lane asks for the same word).
+struct rx_blk {
+  const uint8_t *s;
+  uint64_t len;
+  uint32_t *buf;  // kRxsLongBlk bytes of LDS
+  mutable uint64_t base;
+  __device__ void load(uint64_t p) const {
+    base = p & ~15ull;
+    wave_sync();  // every lane has read the old block
+    const uint32_t lane = __lane_id();
+#pragma unroll
+    for (uint32_t k = 0; k < kRxsLongBlk / 1024u; ++k) {
+      const uint64_t o = base + 16u * lane + 1024u * k;
+      u32x4 t;
+      if (o + 16u <= len) {
+        t = ld16u(s + o);
+      } else {
+        uint32_t w[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[j] = o + 4u * j + 4u <= len ? ld32(s + o + 4u * j) : 0u;
+        t = u32x4{w[0], w[1], w[2], w[3]};
+      }
+      reinterpret_cast<u32x4 *>(buf)[lane + 64u * k] = t;
+    }
+    wave_sync();
+  }
+  __device__ __forceinline__ uint32_t at(uint64_t p) const {
+    if (p - base >= kRxsLongBlk - 3u) load(p);
+    return buf[(p - base) >> 2];
+  }
+  __device__ __forceinline__ uint32_t operator()(uint64_t p) const { return at(p); }
+  __device__ __forceinline__ uint32_t atc(uint64_t p) const { return at(p); }
+  template <class U>
+  __device__ __forceinline__ void clamp(U &, uint32_t &, U) const {}
+};
+
 
 template <bool WHOLE = false, class P>
 __device__ __forceinline__ void rxs_walk_body(const P &parser, const uint8_t *__restrict__ s, uint64_t len,
@@ -419,10 +461,9 @@ __device__ __forceinline__ void rxs_walk_body(const P &parser, const uint8_t *__
   const uint32_t r0 = static_cast<uint32_t>(s0 - lo), r1 = static_cast<uint32_t>(min(len, s0 + kRxsSeg) - lo);
   if (blockIdx.x == 0 && lane == 0) {
     flag[0] = 1u;  // rxs_check clears it on a miss
-    flag[2] = 0u;  // (WHOLE: rxs_mark's count, a u64 at flag + 2)
+    flag[2] = 0u;  // (WHOLE: the count of rxs_fix's list, a u64 at flag + 2)
     flag[3] = 0u;
   }
-  if (lane == 0) seg[static_cast<uint64_t>(blockIdx.x) * kRxsSegWords + 3] = 0;  // (rxs_fix's entries)
   parser.init(rx_smem);
   // stage [lo, lo + kStg) within the stream: all of a lane's 16-byte loads
   // in flight before its stores
@@ -575,7 +616,7 @@ __device__ __forceinline__ void rxs_walk_body(const P &parser, const uint8_t *__
       // the segment inside it (rxs_check passes it over, whatever the walk
       // says), so it gives way to the lane's own guess like a broken chain
       // -- a wrong guess upstream that reads a large length (or a record
-      // left to rxs_long, kLongAt) must not sink the segment
+      // left to the wave's long parse, kLongAt) must not sink the segment
       const bool far = src < kRoot && pe != kBrk && pe >= r1;
       if ((e == kBrk || far) && g0 != kNone && (lane < kRoot || far || !(livem & below_seg))) {
         g = g0;
@@ -620,15 +661,24 @@ __device__ __forceinline__ void rxs_walk_body(const P &parser, const uint8_t *__
   // a live state
   const uint64_t amask = __ballot(act);
   const uint32_t last = 63u - static_cast<uint32_t>(__builtin_clzll(amask));
-  // (WHOLE: lanes passed over by a record left to rxs_long hold no node)
+  // (WHOLE: lanes passed over by a record left to the long parse hold no node)
   const bool passed = WHOLE && g != kBrk && g != kNone && (g & kLongAt);
   const uint64_t livef = __ballot(act && lane >= kRoot && e != kBrk && e != kNone && !passed);
   const uint32_t fl = livef ? static_cast<uint32_t>(__builtin_ctzll(livef)) : kRoot;
   const uint32_t x = __shfl(e, last, 64), E = __shfl(g, fl, 64);
+  uint64_t xe = x == kBrk ? kRxsBroken : lo + (x & ~kLongAt);
+  if constexpr (WHOLE) {
+    if (x != kBrk && (x & kLongAt)) {  // (x is the wave's: every lane parses)
+      const rx_blk rd{s, len, stg, 0};
+      rd.load(xe);  // (its wave_sync: every lane is past its reads of the stretch)
+      const uint32_t L = parser.template rlen_rd<rx_blk, uint64_t>(rx_smem, rd, len, xe, maxlen);
+      xe = L >= RX_OUT ? kRxsBroken : xe + L;
+    }
+  }
   if (lane == 0) {
     uint64_t *r = seg + static_cast<uint64_t>(blockIdx.x) * kRxsSegWords;
     r[0] = !livef || E == kBrk ? kRxsBroken : lo + E;
-    r[1] = x == kBrk ? kRxsBroken : WHOLE && (x & kLongAt) ? kRxsLongExit | (lo + (x & ~kLongAt)) : lo + x;
+    r[1] = xe;
     r[2] = x == kBrk ? kRxsBroken : rl32(incl, 63);
   }
 }
@@ -652,97 +702,9 @@ __device__ __forceinline__ uint64_t rxs_entry(uint64_t i, uint64_t E, uint64_t C
   return lo < C && nd[lo] == w ? lo : kRxsBroken;
 }
 
-// ------------------------------------- records past the staged stretch
-// (WHOLE walks: xdrg_index_records with max_rec_len past the index window)
-//   rxs_long     one wave per segment whose exit the walk left to it
-//                (kRxsLongExit): the record at that start, parsed by the
-//                whole wave -- the same parse on every lane -- through
-//                kRxsLongBlk-byte blocks of the stream in LDS, each refilled
-//                by one round trip of the wave's 16-byte loads; the exit
-//                becomes the record's end (kRxsBroken if it does not parse).
-//   rxs_mark     one thread per segment: the segments whose check against
-//                the previous segment's exit fails (a guess that missed: a
-//                look-back inside a long record's payload has no true chain
-//                to follow) or whose exit passes over a whole segment, into
-//                a list.
-//   rxs_fix      one wave, the listed segments in stream order, each from
-//                its true entry: a segment the entry passes over is passed
-//                over (no record starts there), any other is walked again
-//                by the wave from it (nodes, count, exit), and when the exit
-//                differs from the one its own walk found -- which the next
-//                segment was checked against -- the next segment follows.
-//                The entry of the first segment of such a run is the exit
-//                of a segment whose check held, so every entry is the true
-//                chain's (by induction from byte 0) and the index stays
-//                exact; rxs_check then takes the fixed segments' entries.
-//                More than kRxsFixCap listed segments: the list ranking.
-constexpr uint32_t kRxsLongBlk = 4096;
-constexpr uint32_t kRxsLongWaves = 4;
-// Wave-uniform block reader (every lane asks for the same word).
-struct rx_blk {
-  const uint8_t *s;
-  uint64_t len;
-  uint32_t *buf;  // kRxsLongBlk bytes of LDS
-  mutable uint64_t base;
-  __device__ void load(uint64_t p) const {
-    base = p & ~15ull;
-    wave_sync();  // every lane has read the old block
-    const uint32_t lane = __lane_id();
-#pragma unroll
-    for (uint32_t k = 0; k < kRxsLongBlk / 1024u; ++k) {
-      const uint64_t o = base + 16u * lane + 1024u * k;
-      u32x4 t;
-      if (o + 16u <= len) {
-        t = ld16u(s + o);
-      } else {
-        uint32_t w[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) w[j] = o + 4u * j + 4u <= len ? ld32(s + o + 4u * j) : 0u;
-        t = u32x4{w[0], w[1], w[2], w[3]};
-      }
-      reinterpret_cast<u32x4 *>(buf)[lane + 64u * k] = t;
-    }
-    wave_sync();
-  }
-  __device__ __forceinline__ uint32_t at(uint64_t p) const {
-    if (p - base >= kRxsLongBlk - 3u) load(p);
-    return buf[(p - base) >> 2];
-  }
-  __device__ __forceinline__ uint32_t operator()(uint64_t p) const { return at(p); }
-  __device__ __forceinline__ uint32_t atc(uint64_t p) const { return at(p); }
-  template <class U>
-  __device__ __forceinline__ void clamp(U &, uint32_t &, U) const {}
-};
-
-template <class P>
-__device__ __forceinline__ void rxs_long_body(const P &parser, const uint8_t *__restrict__ s, uint64_t len,
-                                              uint32_t maxlen, uint64_t *__restrict__ seg, uint64_t nseg) {
-  __shared__ __attribute__((aligned(16))) uint32_t blk[kRxsLongWaves][kRxsLongBlk / 4];
-  extern __shared__ __attribute__((aligned(16))) uint32_t rx_smem[];
-  const uint32_t w = threadIdx.x >> 6;
-  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kRxsLongWaves + w;
-  if (i >= nseg) return;
-  uint64_t *r = seg + i * kRxsSegWords + 1;
-  const uint64_t x = *r;
-  if (x == kRxsBroken || !(x & kRxsLongExit)) return;
-  const uint64_t a = x & ~kRxsLongExit;
-  parser.init(rx_smem);
-  const rx_blk rd{s, len, blk[w], 0};
-  rd.load(a);
-  const uint32_t L = parser.template rlen_rd<rx_blk, uint64_t>(rx_smem, rd, len, a, maxlen);
-  if (__lane_id() == 0) *r = L >= RX_OUT ? kRxsBroken : a + L;
-}
-
-// The entry that rxs_check compares segment i with: the entry rxs_fix
-// set (r[3]; 0 for segment 0 and for segments it did not touch), else the
-// previous segment's exit.
-__device__ __forceinline__ uint64_t rxs_prev(const uint64_t *__restrict__ seg, uint64_t i) {
-  const uint64_t f = seg[i * kRxsSegWords + 3];
-  return f ? f : i == 0 ? 0 : seg[(i - 1) * kRxsSegWords + 1];
-}
 // The walk's own verdict on segment i given its entry prev: its node index
-// there, kRxsBroken when its chain does not hold prev; ~1ull when no record
-// starts in it (prev at or past its end).
+// there, kRxsBroken when its chain does not hold prev; kRxsPassOver when no
+// record starts in it (prev at or past its end).
 constexpr uint64_t kRxsPassOver = ~1ull;
 __device__ __forceinline__ uint64_t rxs_verdict(const uint64_t *__restrict__ seg, const uint16_t *__restrict__ nodes,
                                                 uint64_t i, uint64_t nseg, uint64_t len, uint64_t prev) {
@@ -753,26 +715,61 @@ __device__ __forceinline__ uint64_t rxs_verdict(const uint64_t *__restrict__ seg
   return k != kRxsBroken && (i != nseg - 1 || r[1] == len) ? k : kRxsBroken;
 }
 
-// One thread per segment: the segments rxs_fix takes, appended to list
-// (count in *nl, zeroed by the walk).
-__device__ __forceinline__ void rxs_mark_body(const uint64_t *__restrict__ seg, const uint16_t *__restrict__ nodes,
-                                              uint64_t nseg, uint64_t len, uint64_t *__restrict__ list,
-                                              unsigned long long *nl) {
+// One thread per segment: the true entry among the segment's nodes, against
+// the previous segment's exit -- r[3] = its index, cnt[i] = the segment's
+// records from it (for the scan); a segment where no record starts (the
+// previous exit at or past its end) is passed over (0, 0).  A segment whose
+// check fails clears the flag (the list ranking), except in a WHOLE walk
+// (LONG), where it goes to rxs_fix's list -- a guess that missed there is
+// expected: a look-back inside a long record's payload has no true chain to
+// follow -- and so does a segment whose exit passes over a whole segment
+// (the segments after it were passed over on its word).
+template <bool LONG = false>
+__device__ __forceinline__ void rxs_check_body(uint64_t *__restrict__ seg, const uint16_t *__restrict__ nodes,
+                                               uint64_t nseg, uint64_t len, unsigned long long *__restrict__ cnt,
+                                               uint32_t *__restrict__ flag, uint64_t *__restrict__ list,
+                                               unsigned long long *nl) {
   const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= nseg) return;
-  const uint64_t x = seg[i * kRxsSegWords + 1];
-  const bool far = x != kRxsBroken && x >= (i + 2) * kRxsSeg;
-  if (far || rxs_verdict(seg, nodes, i, nseg, len, i == 0 ? 0 : seg[(i - 1) * kRxsSegWords + 1]) == kRxsBroken)
+  uint64_t *r = seg + i * kRxsSegWords;
+  const uint64_t prev = i == 0 ? 0 : seg[(i - 1) * kRxsSegWords + 1];
+  const uint64_t k = rxs_verdict(seg, nodes, i, nseg, len, prev);
+  const bool far = LONG && r[1] != kRxsBroken && r[1] >= (i + 2) * kRxsSeg;
+  if (LONG && (far || k == kRxsBroken)) {
     list[atomicAdd(nl, 1ull)] = i;
+    return;
+  }
+  if (k == kRxsPassOver) {  // no record starts in the segment
+    r[3] = 0;
+    cnt[i] = 0;
+    return;
+  }
+  const bool ok = k != kRxsBroken;
+  r[3] = ok ? k : 0;
+  cnt[i] = ok ? r[2] - k : 0;
+  if (!ok) *flag = 0u;
 }
 
+// rxs_fix (WHOLE walks): one wave, the listed segments in stream order, each
+// from its true entry: a segment the entry passes over is passed over (no
+// record starts there), one whose own walk holds the entry keeps its nodes,
+// and any other is walked again by the wave from it (nodes, count, exit);
+// when the exit differs from the one its own walk found -- which the next
+// segment was checked against -- the next segment follows.  The entry of
+// the first segment of such a run is the exit of a segment whose check held,
+// so every entry is the true chain's (by induction from byte 0) and the
+// index stays exact.  Each segment it decides gets r[3] and cnt as
+// rxs_check's; a chain that does not parse, or a last segment that does not
+// end at the stream's end, clears the flag, and so do more than kRxsFixCap
+// listed segments (the list ranking).
 constexpr uint32_t kRxsFixBits = 1u << 18;  // segments the fix's LDS bitmap covers (1.8 GB of stream)
 constexpr uint64_t kRxsFixCap = 4096;       // listed segments it takes at most
 template <class P>
 __device__ __forceinline__ void rxs_fix_body(const P &parser, const uint8_t *__restrict__ s, uint64_t len,
                                              uint32_t maxlen, uint64_t *__restrict__ seg, uint64_t nseg,
                                              uint16_t *__restrict__ nodes, const uint64_t *__restrict__ list,
-                                             const unsigned long long *nl, uint32_t *__restrict__ flag) {
+                                             const unsigned long long *nl, uint32_t *__restrict__ flag,
+                                             unsigned long long *__restrict__ cnt) {
   __shared__ uint32_t bits[kRxsFixBits / 32];
   __shared__ __attribute__((aligned(16))) uint32_t blk[kRxsLongBlk / 4];
   extern __shared__ __attribute__((aligned(16))) uint32_t rx_smem[];
@@ -816,28 +813,41 @@ __device__ __forceinline__ void rxs_fix_body(const P &parser, const uint8_t *__r
           bool ok = true;
           const uint64_t v = rxs_verdict(seg, nodes, i, nseg, len, x);
           if (v == kRxsPassOver) {  // passed over
-            if (lane == 0) r[3] = x;
+            if (lane == 0) {
+              r[3] = 0;
+              cnt[i] = 0;
+            }
           } else if (v != kRxsBroken) {  // its own walk holds from x
             q = own;
-            if (lane == 0) r[3] = x;
+            if (lane == 0) {
+              r[3] = v;
+              cnt[i] = r[2] - v;
+            }
           } else {  // walked again from x: its records' nodes, count and exit
             uint64_t m = 0;
-            rd.load(q);
-            while (q < s1) {
-              if (lane == 0) nodes[i * (kRxsSeg / 4) + m] = static_cast<uint16_t>((q - s0) >> 2);
-              ++m;
-              const uint32_t L = parser.template rlen_rd<rx_blk, uint64_t>(rx_smem, rd, len, q, maxlen);
-              if (L >= RX_OUT) {
-                ok = false;
-                break;
+            if (x != kRxsBroken) {
+              rd.load(q);
+              while (q < s1) {
+                if (lane == 0) nodes[i * (kRxsSeg / 4) + m] = static_cast<uint16_t>((q - s0) >> 2);
+                ++m;
+                const uint32_t L = parser.template rlen_rd<rx_blk, uint64_t>(rx_smem, rd, len, q, maxlen);
+                if (L >= RX_OUT) {
+                  ok = false;
+                  break;
+                }
+                q += L;
               }
-              q += L;
+            } else {
+              ok = false;
             }
+            if (i == nseg - 1 && q != len) ok = false;
             if (lane == 0) {
               r[0] = x;
               r[1] = ok ? q : kRxsBroken;
               r[2] = ok ? m : kRxsBroken;
-              r[3] = x;
+              r[3] = 0;
+              cnt[i] = ok ? m : 0;
+              if (!ok) *flag = 0u;
             }
           }
           cover = i + 1;
@@ -854,31 +864,6 @@ __device__ __forceinline__ void rxs_fix_body(const P &parser, const uint8_t *__r
   }
 }
 
-// One thread per segment: the true entry among the segment's nodes.
-// cnt[i] = the segment's records (for the scan).  Segments where no record
-// starts (the previous exit at or past their end) are passed over.  LONG
-// (WHOLE walks): the entries rxs_fix set.
-template <bool LONG = false>
-__device__ __forceinline__ void rxs_check_body(uint64_t *__restrict__ seg, const uint16_t *__restrict__ nodes,
-                                               uint64_t nseg, uint64_t len, unsigned long long *__restrict__ cnt,
-                                               uint32_t *__restrict__ flag) {
-  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= nseg) return;
-  uint64_t *r = seg + i * kRxsSegWords;
-  const uint64_t prev = LONG ? rxs_prev(seg, i) : i == 0 ? 0 : seg[(i - 1) * kRxsSegWords + 1];
-  const uint64_t k = rxs_verdict(seg, nodes, i, nseg, len, prev);
-  if (k == kRxsPassOver) {  // no record starts in the segment
-    r[0] = 0;
-    r[2] = 0;
-    cnt[i] = 0;
-    return;
-  }
-  const bool ok = k != kRxsBroken;
-  r[0] = ok ? k : 0;
-  cnt[i] = ok ? r[2] - k : 0;
-  if (!ok) *flag = 0u;
-}
-
 // One wave per segment (four to a 256-lane workgroup: a 64-lane workgroup
 // per segment left rpc's 36K-segment emit at 12.8 us, dispatch-bound): its
 // records' offsets, when every check held (the flag) and the chain holds
@@ -891,7 +876,8 @@ __device__ __forceinline__ void rxs_emit_body(const uint64_t *__restrict__ seg, 
                                               const unsigned long long *__restrict__ base,
                                               const xdrg_status *__restrict__ tot, uint64_t len, uint64_t n,
                                               uint64_t *__restrict__ offsets, uint64_t *__restrict__ count,
-                                              uint32_t *__restrict__ flag, uint64_t nseg, uint32_t *hflag) {
+                                              uint32_t *__restrict__ flag, uint64_t nseg, uint32_t *hflag,
+                                              const unsigned long long *__restrict__ cnt) {
   const uint64_t t = tot->total_bytes;
   const bool all = *flag == 1u && (EXACT ? t == n : t <= n);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -906,7 +892,7 @@ __device__ __forceinline__ void rxs_emit_body(const uint64_t *__restrict__ seg, 
   if (!all || i >= nseg) return;
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t *r = seg + i * kRxsSegWords;
-  const uint64_t k = r[0], c = r[2] - k, b0 = base[i], s0 = i * kRxsSeg;
+  const uint64_t k = r[3], c = cnt[i], b0 = base[i], s0 = i * kRxsSeg;
   const uint16_t *in = nodes + i * (kRxsSeg / 4) + k;
   for (uint32_t j = lane; j < c; j += 64u) offsets[b0 + j] = s0 + 4ull * in[j];
 }

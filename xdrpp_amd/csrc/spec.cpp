@@ -193,11 +193,11 @@ const spec_module *spec_get(const xdrg_plan &cp) {
     d.f_sub_dec = g[3];
     d.f_sub_chain = g[4];
   }
-  hipFunction_t f[9] = {};
-  const char *names[9] = {"xdrg_spec_size",     "xdrg_spec_encode",         "xdrg_spec_decode",
+  hipFunction_t f[8] = {};
+  const char *names[8] = {"xdrg_spec_size",     "xdrg_spec_encode",         "xdrg_spec_decode",
                           "xdrg_spec_decode_copy", "xdrg_spec_ix_seg",      "xdrg_spec_rxs_walk",
-                          "xdrg_spec_rxs_walk_whole", "xdrg_spec_rxs_long", "xdrg_spec_rxs_fix"};
-  for (int i = s.info.frame_walk ? 4 : 0; i < 9 && (!s.info.frame_walk || s.info.tail_rx); ++i)
+                          "xdrg_spec_rxs_walk_whole", "xdrg_spec_rxs_fix"};
+  for (int i = s.info.frame_walk ? 4 : 0; i < 8 && (!s.info.frame_walk || s.info.tail_rx); ++i)
     if (hipModuleGetFunction(&f[i], m, names[i]) != hipSuccess)
       return fail(m, "specialized kernels: the code object lacks a kernel");
   // a code object of another kernel interface (an older build's AOT file),
@@ -222,8 +222,7 @@ const spec_module *spec_get(const xdrg_plan &cp) {
   d.f_ix_seg = f[4];
   d.f_rxs_walk = f[5];
   d.f_rxs_walk_whole = f[6];
-  d.f_rxs_long = f[7];
-  d.f_rxs_fix = f[8];
+  d.f_rxs_fix = f[7];
   if (s.info.word_list) {  // the walk-first encode, generated for word-list plans only
     hipFunction_t a = nullptr, b = nullptr;
     if (hipModuleGetFunction(&a, m, "xdrg_spec_encode_lb") != hipSuccess ||

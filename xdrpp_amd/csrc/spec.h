@@ -16,7 +16,7 @@ constexpr int kSpecDevices = 64;
 // Interface version of the generated kernels (their parameter lists and
 // LDS layout, var_kernels.h): the source defines xdrg_spec_iface with it,
 // and a code object that carries another value is refused at load.
-constexpr unsigned kSpecIface = 13;
+constexpr unsigned kSpecIface = 14;
 
 // The generated source of a plan and the launch facts it fixes.
 struct spec_info {
@@ -37,7 +37,7 @@ struct spec_module {
   void *f_size = nullptr, *f_enc = nullptr, *f_dec = nullptr, *f_dec_copy = nullptr;  // hipFunction_t
   void *f_ix_seg = nullptr;  // record-start parse of the plain-stream index (list ranking)
   void *f_rxs_walk = nullptr;  // ... and its speculative chain walk
-  void *f_rxs_walk_whole = nullptr, *f_rxs_long = nullptr, *f_rxs_fix = nullptr;  // ... over records of any length
+  void *f_rxs_walk_whole = nullptr, *f_rxs_fix = nullptr;  // ... over records of any length
   void *f_enc_lb = nullptr, *f_enc_pre = nullptr;  // word-list plans: encode walked first (look-back / sized)
   // recursive plans: the frame walks (sub_kernels.h) over the plan's ops
   void *f_sub_size = nullptr, *f_sub_depth = nullptr, *f_sub_enc = nullptr, *f_sub_dec = nullptr;

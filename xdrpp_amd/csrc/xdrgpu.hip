@@ -1091,13 +1091,9 @@ __global__ __launch_bounds__(256) void k_ix_seg(const uint8_t *__restrict__ s, u
 template <bool LONG>
 __global__ __launch_bounds__(256) void k_rxs_check(uint64_t *__restrict__ seg, const uint16_t *__restrict__ nodes,
                                                    uint64_t nseg, uint64_t len, unsigned long long *__restrict__ cnt,
-                                                   uint32_t *__restrict__ flag) {
-  rxs_check_body<LONG>(seg, nodes, nseg, len, cnt, flag);
-}
-__global__ __launch_bounds__(256) void k_rxs_mark(const uint64_t *__restrict__ seg, const uint16_t *__restrict__ nodes,
-                                                  uint64_t nseg, uint64_t len, uint64_t *__restrict__ list,
-                                                  unsigned long long *nl) {
-  rxs_mark_body(seg, nodes, nseg, len, list, nl);
+                                                   uint32_t *__restrict__ flag, uint64_t *__restrict__ list,
+                                                   unsigned long long *nl) {
+  rxs_check_body<LONG>(seg, nodes, nseg, len, cnt, flag, list, nl);
 }
 template <bool EXACT>
 __global__ __launch_bounds__(256) void k_rxs_emit(const uint64_t *__restrict__ seg,
@@ -1105,8 +1101,9 @@ __global__ __launch_bounds__(256) void k_rxs_emit(const uint64_t *__restrict__ s
                                                   const unsigned long long *__restrict__ base,
                                                   const xdrg_status *__restrict__ tot, uint64_t len, uint64_t n,
                                                   uint64_t *__restrict__ offsets, uint64_t *__restrict__ count,
-                                                  uint32_t *__restrict__ flag, uint64_t nseg, uint32_t *hflag) {
-  rxs_emit_body<EXACT>(seg, nodes, base, tot, len, n, offsets, count, flag, nseg, hflag);
+                                                  uint32_t *__restrict__ flag, uint64_t nseg, uint32_t *hflag,
+                                                  const unsigned long long *__restrict__ cnt) {
+  rxs_emit_body<EXACT>(seg, nodes, base, tot, len, n, offsets, count, flag, nseg, hflag, cnt);
 }
 // The walk over a message stream's record marks (xdrg_index_msgs).
 __global__ __launch_bounds__(64) void k_rxs_walk_msgs(const uint8_t *__restrict__ s, uint64_t len,
@@ -1596,6 +1593,11 @@ int run_fixed(const xdrg_plan &p, const dev_tables &T, bool decode, const void *
     //  * working set (input + output) that fits the 256 MiB Infinity Cache
     //    (1M records = 256 MiB): plain 16-byte loads/stores, one chunk in
     //    flight per lane, 1024 workgroups -> 6.9 TB/s back to back;
+    //  * past the cache, up to 1 GiB in+out (config 5's 2M-record shard per
+    //    rank is 512 MiB): the same 1024-workgroup loop with non-temporal
+    //    loads and stores, 5.85-6.10 TB/s at 384-768 MiB against 5.55-5.71
+    //    for the plain loop and 5.60-5.83 for the one-shot grid
+    //    (tools/gpu/fixed_shape_sweep.py, profiles/r06_fixed);
     //  * larger batches stream from HBM: one chunk per lane over a one-shot
     //    grid with non-temporal loads and stores -- the box's best 16-byte
     //    copy past the cache, 6.58 TB/s at 2 GiB per buffer, where any
@@ -1604,11 +1606,11 @@ int run_fixed(const xdrg_plan &p, const dev_tables &T, bool decode, const void *
     const uint32_t W = p.fixed_size;
     const uint32_t cpr = W / 16;
     const uint64_t nchunks = nrec * cpr;
-    const bool big = nchunks * 32ull > kMallBytes * 3 / 2;  // in+out bytes > 384 MiB
+    const uint64_t ws_bytes = nchunks * 32ull;  // in + out
     // XDRG_OPT_FIXED_STREAM picks the shape for A/B runs (bench.py shard_2m)
     const int fs = O.fixed_stream;
-    const bool streaming = fs < 0 ? big : (fs == 1 || fs == 3);      // non-temporal accesses
-    const bool one_shot = fs < 0 ? big : (fs == 1 || fs == 2);       // one chunk per lane
+    const bool streaming = fs < 0 ? ws_bytes > kMallBytes : (fs == 1 || fs == 3);      // non-temporal accesses
+    const bool one_shot = fs < 0 ? ws_bytes > 4 * kMallBytes : (fs == 1 || fs == 2);   // one chunk per lane
     uint64_t blocks = (nchunks + 255) / 256;
     if (!one_shot) blocks = std::min<uint64_t>(blocks, 1024);
     if (blocks > 0x7fffffffull) return XDRG_EUNSUPPORTED;
@@ -2456,7 +2458,6 @@ int run_index(const xdrg_plan *p, const dev_tables *T, const void *d_stream, uin
   auto tab = [&](int l) { return reinterpret_cast<uint64_t *>(ws + L.tab[l]); };
   auto ent = [&](int l) { return reinterpret_cast<uint64_t *>(ws + L.ent[l]); };
   const uint8_t *s8 = static_cast<const uint8_t *>(d_stream);
-  if (!C.next) HIPCHK(static_cast<hipError_t>(xdrg::fill32(d_count, 0xffffffffu, 2, s)));  // (a window's caller sets it once)
   uint32_t *vlist = reinterpret_cast<uint32_t *>(ws + L.list);
   uint32_t *vcount = reinterpret_cast<uint32_t *>(ws + L.lcount);
   // the tables are needed above one segment; the valid-node lists always
@@ -2466,8 +2467,8 @@ int run_index(const xdrg_plan *p, const dev_tables *T, const void *d_stream, uin
   const spec_module *SM = REC && p->opts.specialize ? spec_get(*p) : nullptr;
   if (SM && !SM->f_rxs_walk) SM = nullptr;
   // whole: the walk over records of any length (rx_windows): its parse has
-  // no maxlen, and records past the staged stretch go to rxs_long
-  if (whole && !(SM && SM->f_rxs_walk_whole && SM->f_rxs_long && SM->f_rxs_fix)) whole = false;
+  // no maxlen, and a record past the staged stretch is parsed by the wave
+  if (whole && !(SM && SM->f_rxs_walk_whole && SM->f_rxs_fix)) whole = false;
   // Record index: the speculative chain walk first (index_kernels.h rxs_*);
   // the list ranking below runs only when its checks fail.  Short streams
   // (a few segments) go to the list ranking alone.
@@ -2487,6 +2488,11 @@ int run_index(const xdrg_plan *p, const dev_tables *T, const void *d_stream, uin
   }
   if (fast_only) gate = 1;  // ix_windows: the walk's verdict, nothing else
   const bool walk_runs = walk_ok && !C.next && len >= 4ull * kRxsSeg && max_msgs > 0;
+  // the count's fill for the list ranking (a window's caller sets it once):
+  // after the walk's verdict when the host waits for it (no launch when the
+  // walk holds: its emit writes the count), else first
+  const bool fill_late = walk_runs && gate == 1 && !fast_only && !walk_only;
+  if (!C.next && !fill_late) HIPCHK(static_cast<hipError_t>(xdrg::fill32(d_count, 0xffffffffu, 2, s)));
   if (fast_only && !walk_runs) return kIxNotHeld;
   if (REC && !C.next && !walk_runs)  // the flag says which path ran (include/xdrgpu.h)
     HIPCHK(static_cast<hipError_t>(xdrg::fill32(ws + L.rxs_flag, 0u, 1, s)));
@@ -2503,29 +2509,26 @@ int run_index(const xdrg_plan *p, const dev_tables *T, const void *d_stream, uin
       void *args[] = {&s8, &len, &ml, &seg, &nodes, &flag, &hf, &fd};
       HIPCHK(hipModuleLaunchKernel(static_cast<hipFunction_t>(whole ? SM->f_rxs_walk_whole : SM->f_rxs_walk), ns, 1,
                                    1, 64, 1, 1, 0, s, args, nullptr));
-      if (whole) {  // the records the walk left past its stretches, then the segments they pass over
-        uint64_t nsg = L.rxs_nseg;
-        void *largs[] = {&s8, &len, &ml, &seg, &nsg};
-        HIPCHK(hipModuleLaunchKernel(static_cast<hipFunction_t>(SM->f_rxs_long), (ns + kRxsLongWaves - 1) / kRxsLongWaves,
-                                     1, 1, 64 * kRxsLongWaves, 1, 1, 0, s, largs, nullptr));
-        // (the list of segments to fix in the counts' area, rxs_check writes them after)
-        uint64_t *list = reinterpret_cast<uint64_t *>(cnt);
-        auto *nl = reinterpret_cast<unsigned long long *>(flag + 2);
-        k_rxs_mark<<<(ns + 255) / 256, 256, 0, s>>>(seg, nodes, L.rxs_nseg, len, list, nl);
-        HIPCHK(hipGetLastError());
-        void *jargs[] = {&s8, &len, &ml, &seg, &nsg, &nodes, &list, &nl, &flag};
-        HIPCHK(hipModuleLaunchKernel(static_cast<hipFunction_t>(SM->f_rxs_fix), 1, 1, 1, 64, 1, 1, 0, s, jargs,
-                                     nullptr));
-      }
     } else {
       k_rxs_walk_msgs<<<ns, 64, 0, s>>>(s8, len, max_msg_len, seg, nodes, flag);
       HIPCHK(hipGetLastError());
     }
-    if (whole)
-      k_rxs_check<true><<<(ns + 255) / 256, 256, 0, s>>>(seg, nodes, L.rxs_nseg, len, cnt, flag);
-    else
-      k_rxs_check<false><<<(ns + 255) / 256, 256, 0, s>>>(seg, nodes, L.rxs_nseg, len, cnt, flag);
-    HIPCHK(hipGetLastError());
+    if (whole) {
+      // the failed segments' list in the scan's output area (written after
+      // the fix), its count a u64 at flag + 2 (zeroed by the walk)
+      uint64_t *list = reinterpret_cast<uint64_t *>(base);
+      auto *nl = reinterpret_cast<unsigned long long *>(flag + 2);
+      k_rxs_check<true><<<(ns + 255) / 256, 256, 0, s>>>(seg, nodes, L.rxs_nseg, len, cnt, flag, list, nl);
+      HIPCHK(hipGetLastError());
+      uint32_t ml = 0xffffffffu;
+      uint64_t nsg = L.rxs_nseg;
+      void *jargs[] = {&s8, &len, &ml, &seg, &nsg, &nodes, &list, &nl, &flag, &cnt};
+      HIPCHK(hipModuleLaunchKernel(static_cast<hipFunction_t>(SM->f_rxs_fix), 1, 1, 1, 64, 1, 1, 0, s, jargs,
+                                   nullptr));
+    } else {
+      k_rxs_check<false><<<(ns + 255) / 256, 256, 0, s>>>(seg, nodes, L.rxs_nseg, len, cnt, flag, nullptr, nullptr);
+      HIPCHK(hipGetLastError());
+    }
     if (int rc = launch_block_scan(cnt, base, ns, tot, nullptr, 0, s)) return rc;
     // the verdict also into this thread's mapped host word (gate 1): the
     // host waits for the stream alone, no copy after the kernels
@@ -2534,7 +2537,7 @@ int run_index(const xdrg_plan *p, const dev_tables *T, const void *d_stream, uin
     if (hw && hipHostGetDevicePointer(reinterpret_cast<void **>(&hwd), hw, 0) != hipSuccess) hwd = nullptr;
     if (hwd) *reinterpret_cast<volatile uint32_t *>(hw) = 0xffffffffu;
     k_rxs_emit<REC><<<(ns + kRxsEmitWaves - 1) / kRxsEmitWaves, 64 * kRxsEmitWaves, 0, s>>>(
-        seg, nodes, base, tot, len, max_msgs, d_offsets, d_count, flag, L.rxs_nseg, hwd);
+        seg, nodes, base, tot, len, max_msgs, d_offsets, d_count, flag, L.rxs_nseg, hwd, cnt);
     HIPCHK(hipGetLastError());
     if (gate == 1) {
       // wait for the flag: the list ranking is launched only when a check
@@ -2550,6 +2553,7 @@ int run_index(const xdrg_plan *p, const dev_tables *T, const void *d_stream, uin
       if (h == 1u) return XDRG_OK;
       if (fast_only) return kIxNotHeld;
       if (walk_only) return XDRG_OK;
+      if (fill_late) HIPCHK(static_cast<hipError_t>(xdrg::fill32(d_count, 0xffffffffu, 2, s)));
     } else {
       skip = flag;  // asynchronous: the list ranking's kernels skip themselves
     }
@@ -2673,14 +2677,14 @@ int rx_windows(const xdrg_plan *p, const dev_tables *T, const uint8_t *s8, uint6
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
       const spec_module *SM = p->opts.specialize ? spec_get(*p) : nullptr;
-      if (!(SM && SM->f_rxs_walk_whole && SM->f_rxs_long && SM->f_rxs_fix && p->opts.index_fast))
+      if (!(SM && SM->f_rxs_walk_whole && SM->f_rxs_fix && p->opts.index_fast))
         return XDRG_EUNSUPPORTED;
       return run_index<true>(p, T, s8, len, XDRG_INDEX_MAX_MSG, n, d_offsets, d_count, d_ws, ws_bytes, d_status, s,
                              ix_cont{}, false, true);
     }
   }
   {  // the speculative walk over the whole stream, records of any length (a
-     // plan with the generated parse: rxs_long takes the long ones); else
+     // plan with the generated parse: the walk parses the long ones); else
      // over records up to the index window
     const int rc = run_index<true>(p, T, s8, len, XDRG_INDEX_MAX_MSG, n, d_offsets, d_count, d_ws, ws_bytes,
                                    d_status, s, ix_cont{}, true, true);
