@@ -134,7 +134,7 @@ enum xdrg_op_flags {
  * marshaling_stack_limit only: a walk keeps XDRG_SUB_FRAMES element frames
  * in registers, and records nested deeper are walked again by deep passes
  * whose frames live in the caller's workspace
- * (xdrg_deep_workspace_size: about 217 MiB + 12 bytes per record for a plan
+ * (xdrg_deep_workspace_size: about 218 MiB + 12 bytes per record for a plan
  * that can nest that deep, 0 for any other).  A record that needs more than XDRG_MAX_FRAMES nested element
  * frames raises the stack-overflow error at the VECTOR op that would open
  * the next one; the reference's own recursion ends far earlier, in a
@@ -390,7 +390,7 @@ size_t xdrg_workspace_size(const xdrg_plan *plan, uint64_t n);
  * for n records: 0 except for plans whose element subroutines can nest past
  * XDRG_SUB_FRAMES, whose deep passes keep their lists of deferred records
  * and their frame slabs there, and the size walk its log of long chains
- * (about 217 MiB + 12 bytes per record; 256-byte aligned).  The memory is the caller's: no call allocates, locks or keeps
+ * (about 218 MiB + 12 bytes per record; 256-byte aligned).  The memory is the caller's: no call allocates, locks or keeps
  * state between calls, so calls on different streams with different
  * workspaces run side by side, and a captured graph of them holds kernels
  * only (see "Graph capture" below). */

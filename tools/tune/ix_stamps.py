@@ -77,7 +77,7 @@ def run(schemas):
         total = enc.xdr.numel()
         # WHOLE=1: the bound the bench's plain stream passes (records of any
         # length: the whole-stream walk when it is past the index window)
-        cap = 0xFFFFFFFF if os.environ.get("WHOLE") else A.INDEX_MAX_MSG
+        cap = A.MAX_MSG if os.environ.get("WHOLE") else A.INDEX_MAX_MSG
         maxlen = min(p.max_record_bytes, cap)
         ws = torch.zeros(L.xdrg_index_workspace_size(total, maxlen), dtype=torch.uint8, device=dev)
         offs = torch.empty(n + 1, dtype=torch.int64, device=dev)

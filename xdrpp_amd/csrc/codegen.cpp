@@ -1318,7 +1318,9 @@ bool frame_walk_source(const xdrg_plan &p, spec_info &info) {
     << "extern \"C\" __global__ __launch_bounds__(256) void xdrg_spec_sub_decode(XDRG_SUB_DECODE_PARAMS) {\n"
     << "  sub_decode_kernel<plan_ops>(XDRG_SUB_DECODE_ARGS);\n}\n"
     << "extern \"C\" __global__ __launch_bounds__(256) void xdrg_spec_sub_chain(XDRG_SUB_ENCODE_PARAMS) {\n"
-    << "  sub_chain_kernel<plan_ops>(XDRG_SUB_ENCODE_ARGS);\n}\n\n";
+    << "  sub_chain_kernel<plan_ops>(XDRG_SUB_ENCODE_ARGS);\n}\n"
+    << "extern \"C\" __global__ __launch_bounds__(256) void xdrg_spec_sub_chain_size(XDRG_SUB_SIZE_PARAMS) {\n"
+    << "  sub_chain_size_kernel<plan_ops>(XDRG_SUB_SIZE_ARGS);\n}\n\n";
   info = spec_info{};
   info.frame_walk = true;
   gen g(p);

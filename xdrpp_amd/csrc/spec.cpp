@@ -181,10 +181,10 @@ const spec_module *spec_get(const xdrg_plan &cp) {
     return fail(nullptr, "specialized kernels: the code object does not load on this device");
   spec_module &d = s.dev[dev];
   if (s.info.frame_walk) {  // a recursive plan: the frame walks only
-    hipFunction_t g[5] = {};
-    const char *gn[5] = {"xdrg_spec_sub_size", "xdrg_spec_sub_depth", "xdrg_spec_sub_encode", "xdrg_spec_sub_decode",
-                         "xdrg_spec_sub_chain"};
-    for (int i = 0; i < 5; ++i)
+    hipFunction_t g[6] = {};
+    const char *gn[6] = {"xdrg_spec_sub_size", "xdrg_spec_sub_depth", "xdrg_spec_sub_encode", "xdrg_spec_sub_decode",
+                         "xdrg_spec_sub_chain", "xdrg_spec_sub_chain_size"};
+    for (int i = 0; i < 6; ++i)
       if (hipModuleGetFunction(&g[i], m, gn[i]) != hipSuccess)
         return fail(m, "specialized kernels: the code object lacks a frame walk");
     d.f_sub_size = g[0];
@@ -192,6 +192,7 @@ const spec_module *spec_get(const xdrg_plan &cp) {
     d.f_sub_enc = g[2];
     d.f_sub_dec = g[3];
     d.f_sub_chain = g[4];
+    d.f_sub_chain_size = g[5];
   }
   hipFunction_t f[8] = {};
   const char *names[8] = {"xdrg_spec_size",     "xdrg_spec_encode",         "xdrg_spec_decode",

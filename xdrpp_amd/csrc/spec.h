@@ -16,7 +16,7 @@ constexpr int kSpecDevices = 64;
 // Interface version of the generated kernels (their parameter lists and
 // LDS layout, var_kernels.h): the source defines xdrg_spec_iface with it,
 // and a code object that carries another value is refused at load.
-constexpr unsigned kSpecIface = 14;
+constexpr unsigned kSpecIface = 15;
 
 // The generated source of a plan and the launch facts it fixes.
 struct spec_info {
@@ -42,6 +42,7 @@ struct spec_module {
   // recursive plans: the frame walks (sub_kernels.h) over the plan's ops
   void *f_sub_size = nullptr, *f_sub_depth = nullptr, *f_sub_enc = nullptr, *f_sub_dec = nullptr;
   void *f_sub_chain = nullptr;  // the node pass (sub_kernels.h "Chains")
+  void *f_sub_chain_size = nullptr;  // the size walk's chain pass (sub_kernels.h "Chains")
 };
 
 // A plan's specialized kernels: state 0 = not built yet, 1 = code object

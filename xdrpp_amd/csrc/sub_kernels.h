@@ -207,6 +207,9 @@ struct sub_pass {
   // decode, main pass: the host gave each wave kWaveBlk bytes of LDS after
   // the ops, for the stream of its 64 records (win_rd)
   uint32_t win;
+  // size, main pass: per chain, where the chain pass takes it over (see
+  // "Chains"; null: the size walk chases every chain itself)
+  struct sub_node *heads;
 };
 
 // Long records (decode).  A lane's walk of its record reads the stream a
@@ -321,6 +324,19 @@ __device__ __forceinline__ void zero_words(uint8_t *p, uint64_t bytes) {
 // parallel.  A chain that opens a container of more than one element, a
 // record the main pass does not finish, or a full log leaves the record
 // unlogged (chain_of ~0): its walk writes it all, as before.
+// The size walk's own chase of a long chain was then its critical path (one
+// lane, a round trip a node: 1.3 ms for rp_list's 500-node lists), so a
+// chain whose close ends the record -- an optional (`*`, at most one
+// element) tail container in the record's only frame, rp__list's rpcb_next
+// -- is handed over at that node instead (heads[c]: the node, its first
+// byte, depth base and the frames open), and the chain pass
+// (sub_chain_size_kernel) sizes it a wave at a time: each lane loads the
+// node a stride further on (the element size, then the spacing seen), sizes
+// it to its chain's count word and reads its link; the nodes from the
+// wave's first on whose links each lead to the next lane's are the chain's
+// (every address is checked against its predecessor's link, so a heap laid
+// out otherwise costs a round trip a node, as the lane's chase did), their
+// first bytes a prefix sum, and they are logged as the lane would have.
 constexpr uint32_t kChainT = 32;
 struct sub_node {
   uint64_t eb;     // the node's element (heap offset)
@@ -331,7 +347,7 @@ struct sub_node {
 };
 constexpr uint32_t kChainChunk = 64;  // nodes a lane claims at a time
 
-enum : int { kWalkCont = -1, kWalkOk = 0, kWalkErr = 1, kWalkFull = 2 };
+enum : int { kWalkCont = -1, kWalkOk = 0, kWalkErr = 1, kWalkFull = 2, kWalkChain = 3 };
 
 // The interpreted op policy: the op from the plan table (LDS).
 struct rt_ops {
@@ -497,6 +513,7 @@ struct chain_logger {
     c = static_cast<uint32_t>(k);
     lfp = fp;
     P.chain_rec[c] = static_cast<uint32_t>(r);
+    if (P.heads) P.heads[c].chain = ~0u;  // (not handed over, unless below)
   }
   __device__ __forceinline__ void add(uint64_t eb, uint64_t s, uint32_t dbase, uint32_t vpc) {
     if (at == end) {
@@ -530,12 +547,27 @@ struct chain_logger {
 // xdrpp/depth_checker.h:41-54).  kWalkErr with the op and code: a bad
 // discriminant or a record of 2^31 bytes or more; kWalkFull (op in bad_op):
 // the stack ran out.
-template <bool DEPTH, class OPS, class ST>
+// NODE (the chain pass): one node of a chain from its element body (nd.pc)
+// to its chain's count word (the VECTOR op nd.stop in the element's own
+// frame), with nd.lf frames open (replaced ones included); nd.next / nd.cnt
+// are that count word's container.
+struct sub_size_node {
+  uint32_t pc = 0, stop = ~0u, lf = 0, cnt = 0;
+  uint64_t next = 0;
+};
+// A tail container's frame whose return is the record's END (the walk ends
+// when the chain closes).
+__device__ __forceinline__ bool sub_ret_end(const xdrg_op *__restrict__ ops, uint32_t q) {
+  while (ops[q].kind == XDRG_OP_JUMP) q = ops[q].arg0;
+  return ops[q].kind == XDRG_OP_END;
+}
+template <bool DEPTH, class OPS, class ST, bool NODE = false>
 __device__ __forceinline__ int sub_size(const xdrg_op *__restrict__ ops, const uint32_t *__restrict__ table,
                         sub_src_t<OPS::kImgWords> src,
-                        uint64_t &s, uint32_t &dmax, uint32_t &bad_op, uint32_t &code, ST &st, chain_logger &lg) {
-  uint32_t fp = 0, pc = 0, dbase = 0;
-  st.lf = 0;
+                        uint64_t &s, uint32_t &dmax, uint32_t &bad_op, uint32_t &code, ST &st, chain_logger &lg,
+                        sub_size_node *nd = nullptr) {
+  uint32_t fp = 0, pc = NODE ? nd->pc : 0, dbase = 0;
+  st.lf = NODE ? nd->lf : 0;
   auto step = [&](const auto &op) __attribute__((always_inline)) -> int {
     if (op.kind == XDRG_OP_END) {
       // (the logged chain closes when its frame pops)
@@ -571,6 +603,12 @@ __device__ __forceinline__ int sub_size(const xdrg_op *__restrict__ ops, const u
         pc += 1 + op.arg2;
         break;
       }
+      if (NODE && fp == 0 && pc == nd->stop) {  // the node's count word: its link
+        nd->next = src.w64(op.noff);
+        nd->cnt = cnt;
+        if (cnt && st.lf >= XDRG_MAX_FRAMES) { bad_op = pc; code = XDRG_ERR_STACK_PUT; return kWalkErr; }
+        return kWalkOk;
+      }
       if (!cnt) { ++pc; break; }
       bool tail = false;
       const int o = sub_open(ops, st, fp, pc, op.depth, src.w64(op.noff), cnt, true, &tail);
@@ -579,18 +617,25 @@ __device__ __forceinline__ int sub_size(const xdrg_op *__restrict__ ops, const u
       dbase += op.depth;
       src.eb = st.top(fp).eb;
       src.in_heap = true;
-      src.refresh();
       if (lg.on && tail) {  // a frame replaced: the chain log
         if (lg.c == ~0u) {
           if (!lg.done && st.top(fp).nf == kChainT + 1u) {  // the record's first chain this long
             lg.done = true;
             if (cnt == 1u) lg.start(fp);
+            // handed over to the chain pass: a chain whose close ends the record
+            if (!DEPTH && lg.c != ~0u && lg.P.heads && fp == 1u && op.arg0 == 1u && sub_ret_end(ops, st.top(fp).ret())) {
+              lg.P.heads[lg.c] = sub_node{src.eb, static_cast<uint32_t>(s), dbase, st.lf, pc};
+              lg.cfin = lg.c;
+              lg.c = ~0u;
+              return kWalkChain;
+            }
           }
         } else if (fp == lg.lfp && cnt != 1u) {
           lg.c = ~0u;  // more than one element: not a chain the node pass takes
         }
         if (lg.c != ~0u && fp == lg.lfp) lg.add(src.eb, s, dbase, pc);
       }
+      src.refresh();
       pc = op.arg4;
       break;
     }
@@ -643,8 +688,8 @@ __device__ __forceinline__ void sub_size_kernel(XDRG_SUB_SIZE_PARAMS) {
     uint32_t dmax = 0, bad_op = 0, code = 0, sz = kSizeErr;
     chain_logger lg{P, !P.list && P.chain_of, r};
     const int rc = sub_size<DEPTH, OPS>(sops, table, src, s, dmax, bad_op, code, st, lg);
-    lg.finish(rc == kWalkOk);
-    if (rc == kWalkOk) {
+    lg.finish(rc == kWalkOk || rc == kWalkChain);
+    if (rc == kWalkOk || rc == kWalkChain) {  // (a chain handed over: its bytes so far, the chain pass adds the rest)
       sz = static_cast<uint32_t>(s);
     } else if (rc == kWalkErr) {
       report(err, r, bad_op, code);
@@ -663,6 +708,121 @@ __device__ __forceinline__ void sub_size_kernel(XDRG_SUB_SIZE_PARAMS) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   const uint64_t blk = r / 64u;
   if (block_sums && (threadIdx.x & 63u) == 0 && blk * 64u < n) block_sums[blk] = v;
+}
+
+// The chain pass of the size walk (see "Chains"): the chains the main pass
+// handed over, one wave each.  A node's events are the serial walk's: its
+// first error in chain order, or xdr_overflow where the record's running
+// size reaches kSizeErr first (the walk tests it after every field); a node
+// that needs more frames than the registers hold, or a container of more
+// than one element at a chain's link, sends the record to deep pass A, which
+// walks it whole (its bytes so far taken back out of the block sum).
+template <class OPS>
+__device__ __forceinline__ void sub_chain_size_kernel(XDRG_SUB_SIZE_PARAMS) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  xdrg_op *sops = reinterpret_cast<xdrg_op *>(smem);
+  load_ops(sops, ops, nops);
+  (void)mark;
+  (void)depths;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t nwv = static_cast<uint64_t>(gridDim.x) * (blockDim.x / 64u);
+  const uint64_t nc = min(static_cast<uint64_t>(*P.chain_cnt), static_cast<uint64_t>(P.chain_cap));
+  for (uint64_t c = static_cast<uint64_t>(blockIdx.x) * (blockDim.x / 64u) + (threadIdx.x >> 6); c < nc; c += nwv) {
+    const sub_node h = P.heads[c];
+    if (h.chain == ~0u) continue;  // logged by its lane
+    const uint64_t r = P.chain_rec[c];
+    const uint32_t part = sizes[r];
+    const xdrg_op &v = sops[h.vpc];
+    uint64_t eb = h.eb, start = h.s, k = 0;
+    int64_t d = static_cast<int64_t>(v.arg1);  // the spacing guessed: the element size, then the one seen
+    bool logged = true;
+    int fate = 0;  // 1: closed, 2: an event (reported), 3: to deep pass A
+    uint64_t total = 0;
+    while (!fate) {
+      const uint64_t a = eb + static_cast<uint64_t>(d * static_cast<int64_t>(lane));
+      sub_src_t<OPS::kImgWords> src{native + r * stride, stride, heap, heap_len, a, true, {}};
+      src.refresh();
+      sub_size_node nd;
+      nd.pc = v.arg4;
+      nd.stop = h.vpc;
+      nd.lf = h.chain + static_cast<uint32_t>(k) + lane;
+      uint64_t sz = 0;
+      uint32_t dmax = 0, bad_op = 0, code = 0;
+      reg_stack st;
+      chain_logger nolog{P, false, r};
+      const int rc = sub_size<false, OPS, reg_stack, true>(sops, table, src, sz, dmax, bad_op, code, st, nolog, &nd);
+      // the chain's nodes in this wave: lanes 0..J, each reached by the link before it
+      const bool link = rc == kWalkOk && nd.cnt == 1u && nd.next == a + static_cast<uint64_t>(d);
+      const uint64_t nl = __ballot(!link);
+      const uint32_t J = nl ? static_cast<uint32_t>(__builtin_ctzll(nl)) : 63u;
+      const bool mine = lane <= J;
+      // first bytes: a prefix sum of the sizes (an error lane counts the bytes
+      // before its failing field, for the overflow test below)
+      const uint64_t w = !mine ? 0ull : rc == kWalkOk ? sz : rc == kWalkErr && sz >= 4 ? sz - 4 : 0ull;
+      uint64_t incl = w;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t x = __shfl_up(incl, o, 64);
+        if (lane >= static_cast<uint32_t>(o)) incl += x;
+      }
+      const uint64_t first = start + incl - w;  // the node's first byte
+      const bool over = mine && first + w >= kSizeErr;
+      const bool event = mine && (over || rc == kWalkErr);
+      const bool bail = mine && (rc == kWalkFull || (rc == kWalkOk && nd.cnt > 1u));
+      const uint64_t em = __ballot(event), bm = __ballot(bail);
+      const uint32_t E = em ? static_cast<uint32_t>(__builtin_ctzll(em)) : 64u;
+      const uint32_t B = bm ? static_cast<uint32_t>(__builtin_ctzll(bm)) : 64u;
+      if (E < 64u && E <= B) {
+        if (lane == E) {
+          if (over) report(err, r, 0, XDRG_ERR_OVERFLOW_PUT);
+          else report(err, r, bad_op, code);
+        }
+        fate = 2;
+        break;
+      }
+      if (B < 64u) {
+        fate = 3;
+        break;
+      }
+      // log lanes 0..J (a chunk of kChainChunk slots for the wave)
+      if (logged) {
+        unsigned long long at = 0;
+        if (lane == 0) at = atomicAdd(P.node_cnt, static_cast<unsigned long long>(kChainChunk));
+        at = __shfl(at, 0, 64);
+        if (at + kChainChunk > P.node_cap) {
+          logged = false;  // the log is full: the encode's walk writes this record whole
+        } else {
+          P.nodes[at + lane] = mine ? sub_node{a, static_cast<uint32_t>(first), h.dbase + static_cast<uint32_t>(k + lane) * v.depth,
+                                               static_cast<uint32_t>(c), h.vpc}
+                                    : sub_node{0, 0, 0, ~0u, 0};
+        }
+      }
+      const uint64_t end = __shfl(first + sz, J, 64);  // past node J's count word
+      const uint32_t cj = __shfl(nd.cnt, J, 64);
+      const uint64_t nx = __shfl(nd.next, J, 64), aj = __shfl(a, J, 64);
+      k += J + 1u;
+      start = end;
+      if (cj == 0u) {
+        total = end;
+        fate = 1;
+      } else {
+        d = static_cast<int64_t>(nx - aj);
+        eb = nx;
+      }
+    }
+    if (lane != 0) continue;
+    const uint64_t blk = r / 64u;
+    if (fate == 1) {
+      sizes[r] = static_cast<uint32_t>(total);
+      P.chain_end[c] = static_cast<uint32_t>(total);
+      if (!logged) P.chain_of[r] = ~0u;
+      if (block_sums) atomicAdd(&block_sums[blk], static_cast<unsigned long long>(total - part));
+    } else {
+      P.chain_of[r] = ~0u;
+      if (block_sums) atomicAdd(&block_sums[blk], 0ull - static_cast<unsigned long long>(part));
+      if (fate == 2) sizes[r] = kSizeErr;
+      else P.defer[atomicAdd(P.defer_count, 1ull)] = static_cast<uint32_t>(r);
+    }
+  }
 }
 
 // -------------------------------------------------------------- encode

@@ -825,6 +825,9 @@ __global__ __launch_bounds__(256) void k_sub_encode(XDRG_SUB_ENCODE_PARAMS) {
 __global__ __launch_bounds__(256) void k_sub_chain(XDRG_SUB_ENCODE_PARAMS) {
   sub_chain_kernel<rt_ops>(XDRG_SUB_ENCODE_ARGS);
 }
+__global__ __launch_bounds__(256) void k_sub_chain_size(XDRG_SUB_SIZE_PARAMS) {
+  sub_chain_size_kernel<rt_ops>(XDRG_SUB_SIZE_ARGS);
+}
 __global__ __launch_bounds__(256) void k_sub_decode(XDRG_SUB_DECODE_PARAMS) {
   sub_decode_kernel<rt_ops>(XDRG_SUB_DECODE_ARGS);
 }
@@ -1813,10 +1816,10 @@ constexpr uint64_t kDeepSlabBytes =
 // The chain log (sub_kernels.h "Chains"): chains and logged nodes.
 constexpr uint32_t kChainCap = 1u << 16, kNodeCap = 1u << 20;  // 24 MiB of nodes
 constexpr uint32_t kChainGrid = 512;  // node pass workgroups (256 lanes, grid-stride over the nodes)
-constexpr uint64_t kChainLogBytes = 8ull * kChainCap + sizeof(sub_node) * uint64_t(kNodeCap);
+constexpr uint64_t kChainLogBytes = 8ull * kChainCap + sizeof(sub_node) * (uint64_t(kNodeCap) + kChainCap);
 
 // [five counters | 256][list A: n u32][list B: n u32][slab A][slab B]
-// [chain of each record: n u32][chain records, chain ends: kChainCap u32 each][nodes]
+// [chain of each record: n u32][chain records, chain ends: kChainCap u32 each][nodes][chain heads]
 // (The decode, which logs no chains, keeps its wave list -- sub_kernels.h
 // "Long records" -- where the chain of each record goes.)
 constexpr uint32_t kWaveGrid = 256;  // wave pass workgroups (kWaveWaves waves, a listed record per wave at a time)
@@ -1860,6 +1863,7 @@ int deep_setup(const xdrg_plan &p, uint64_t n, void *area, size_t area_bytes, hi
   dp.main.node_cnt = cnt + 3;
   dp.main.chain_cap = kChainCap;
   dp.main.node_cap = kNodeCap;
+  dp.main.heads = dp.main.nodes + kNodeCap;
   dp.A = sub_pass{la, cnt, lb, cnt + 1, sa, kDeepSlabA, 0};
   dp.B = sub_pass{lb, cnt + 1, nullptr, nullptr, sb, kDeepSlabB, 1};
   return XDRG_OK;
@@ -1917,6 +1921,11 @@ hipError_t launch_sub_size(const xdrg_plan &p, const dev_tables &T, const uint8_
                         T.d_ops, nops, T.d_table, sizes, bsum, mark, err, depths, P);
   };
   hipError_t e = go(static_cast<uint32_t>((n + 255) / 256), 256, dp.main);
+  if (e == hipSuccess && dp.on && !DEPTH && dp.main.heads) {  // the chains the main pass handed over
+    void *cf = FM ? FM->f_sub_chain_size : nullptr;
+    e = frame_launch(k_sub_chain_size, cf, kChainGrid, 256, lds, s, nat, n, p.stride, heap, heap_len, T.d_ops, nops,
+                     T.d_table, sizes, bsum, mark, err, depths, dp.main);
+  }
   if (e == hipSuccess && dp.on) {
     e = go(kDeepLanesA / 256, 256, dp.A);
     if (e == hipSuccess) e = go(1, kDeepLanesB, dp.B);
