@@ -23,7 +23,7 @@ for s in numerics recvar rpc vecrec containertest rp_list; do
   timeout -k 10 300 python3 -u bench.py --schema "$s" $extra > "$O/bench_$s.log" 2>&1 || exit 1
   echo "[bench] $s done $(date +%T)"
 done
-B="bench.py --no-cpu-baseline --no-large --no-cold --no-host-inclusive --no-plain --steps 10 --warmup 3"
+B="bench.py --no-cpu-baseline --no-large --no-cold --no-host-inclusive --no-plain --no-shard --steps 10 --warmup 3"
 for s in rec128 numerics recvar rpc vecrec containertest rp_list; do
   timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$O/stats_$s" -o k --output-format csv -- python3 $B --schema "$s" > "$O/stats_$s.log" 2>&1 || exit 1
   timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d "$O/fetch_$s" -o k --output-format csv -- python3 $B --schema "$s" > "$O/fetch_$s.log" 2>&1 || exit 1
