@@ -505,15 +505,23 @@ struct chain_logger {
   uint32_t c = ~0u;     // the chain being logged
   uint32_t cfin = ~0u;  // the chain logged to its close
   uint32_t lfp = 0;     // its frame level
+  uint32_t vpc0 = ~0u;  // the VECTOR op its replacements open
   bool done = false;    // the record's first chain past kChainT was met
   uint64_t at = 0, end = 0;  // this lane's claimed node slots
-  __device__ __forceinline__ void start(uint32_t fp) {
+  __device__ __forceinline__ void start(uint32_t fp, uint32_t vpc) {
     const unsigned long long k = atomicAdd(P.chain_cnt, 1ull);
     if (k >= P.chain_cap) return;
     c = static_cast<uint32_t>(k);
     lfp = fp;
+    vpc0 = vpc;
     P.chain_rec[c] = static_cast<uint32_t>(r);
     if (P.heads) P.heads[c].chain = ~0u;  // (not handed over, unless below)
+  }
+  // not a chain the node pass takes: the record's walks write it whole, and
+  // the node pass skips the nodes logged so far
+  __device__ __forceinline__ void drop() {
+    P.chain_rec[c] = ~0u;
+    c = ~0u;
   }
   __device__ __forceinline__ void add(uint64_t eb, uint64_t s, uint32_t dbase, uint32_t vpc) {
     if (at == end) {
@@ -621,7 +629,7 @@ __device__ __forceinline__ int sub_size(const xdrg_op *__restrict__ ops, const u
         if (lg.c == ~0u) {
           if (!lg.done && st.top(fp).nf == kChainT + 1u) {  // the record's first chain this long
             lg.done = true;
-            if (cnt == 1u) lg.start(fp);
+            if (cnt == 1u) lg.start(fp, pc);
             // handed over to the chain pass: a chain whose close ends the record
             if (!DEPTH && lg.c != ~0u && lg.P.heads && fp == 1u && op.arg0 == 1u && sub_ret_end(ops, st.top(fp).ret())) {
               lg.P.heads[lg.c] = sub_node{src.eb, static_cast<uint32_t>(s), dbase, st.lf, pc};
@@ -630,8 +638,11 @@ __device__ __forceinline__ int sub_size(const xdrg_op *__restrict__ ops, const u
               return kWalkChain;
             }
           }
-        } else if (fp == lg.lfp && cnt != 1u) {
-          lg.c = ~0u;  // more than one element: not a chain the node pass takes
+        } else if (fp == lg.lfp && (cnt != 1u || pc != lg.vpc0)) {
+          // more than one element, or a node of another type (a chain that
+          // alternates tail containers: a node's walk in the node pass stops
+          // at its own chain's count word only when every node opens the same)
+          lg.drop();
         }
         if (lg.c != ~0u && fp == lg.lfp) lg.add(src.eb, s, dbase, pc);
       }

@@ -27,8 +27,10 @@
 #include <cstdio>
 #include <cstring>
 #include <new>
+#include <mutex>
 #include <tuple>
 #include <utility>
+#include <vector>
 
 #include "plan.h"
 
@@ -1662,14 +1664,30 @@ int run_fixed(const xdrg_plan &p, const dev_tables &T, bool decode, const void *
       // one workgroup per resident slot: numerics 1M (25.6 KiB of LDS, 6 per
       // CU) 16.5 us at 1536 workgroups, 18.4 at 1024, 18.6 at 2048, 22.0 at
       // 512 (profiles/r05m)
+      // (the query's answer cached per device, term count and LDS size: it
+      // cost host time on every call of a 16 us kernel)
       uint64_t resident = 1024;
       {
-        int dev = 0, cus = 0, occ = 0;
-        if (hipGetDevice(&dev) == hipSuccess &&
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_fixed_tile<16, 16, KT>, 256, lds) == hipSuccess &&
-            cus > 0 && occ > 0)
-          resident = uint64_t(cus) * uint64_t(occ);
+        struct occ_key { int dev, kt; size_t lds; uint64_t resident; };
+        static std::mutex mu;
+        static std::vector<occ_key> seen;
+        int dev = 0;
+        bool hit = false;
+        if (hipGetDevice(&dev) == hipSuccess) {
+          {
+            std::lock_guard<std::mutex> g(mu);
+            for (const occ_key &k : seen)
+              if (k.dev == dev && k.kt == KT && k.lds == lds) { resident = k.resident; hit = true; break; }
+          }
+          int cus = 0, occ = 0;
+          if (!hit && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+              hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_fixed_tile<16, 16, KT>, 256, lds) == hipSuccess &&
+              cus > 0 && occ > 0) {
+            resident = uint64_t(cus) * uint64_t(occ);
+            std::lock_guard<std::mutex> g(mu);
+            seen.push_back(occ_key{dev, KT, lds, resident});
+          }
+        }
       }
       const uint64_t blocks = std::min<uint64_t>(ntiles, O.grp_blocks ? uint64_t(O.grp_blocks) : resident);
       k_fixed_tile<16, 16, KT><<<static_cast<uint32_t>(blocks), 256, lds, s>>>(
