@@ -1299,18 +1299,29 @@ void from_opaque_batch(context &c, const void *bytes, std::size_t len, T *out, s
     // length and nesting (longer ones than the index window are walked on
     // the device between list-ranking windows); a plan the index cannot
     // chain (records under 4 bytes) is walked on the host
-    const std::uint32_t win = static_cast<std::uint32_t>(
+    std::uint32_t win = static_cast<std::uint32_t>(
         std::min<std::uint64_t>(std::max<std::uint64_t>(P.max_record_bytes(), 16), XDRG_MAX_MSG));
-    const std::size_t wsb = xdrg_index_workspace_size(len, win);
-    void *ws = c.d_ws.get<std::uint8_t>(wsb);
     std::uint64_t *d_cnt = c.d_cnt.get<std::uint64_t>(1);
-    const int rc = xdrg_index_records(P.handle(), d_x, len, n, win, d_off, d_cnt, ws, wsb, c.status(), s);
-    const bool host = rc == XDRG_EUNSUPPORTED;
-    if (!host) {
+    int rc = XDRG_OK;
+    for (;;) {
+      const std::size_t wsb = xdrg_index_workspace_size(len, win);
+      void *ws = c.d_ws.get<std::uint8_t>(wsb);
+      rc = xdrg_index_records(P.handle(), d_x, len, n, win, d_off, d_cnt, ws, wsb, c.status(), s);
+      if (rc == XDRG_EUNSUPPORTED) break;
       detail::abicheck(rc, "xdrg_index_records");
       const xdrg_error ie = detail::read_status<T>(c, s, false);
+      if (ie.code == XDRG_ERR_INDEX_LONG && win <= XDRG_INDEX_MAX_MSG) {
+        // a record nested past the window parse's frames, or longer than
+        // the plan's bound: the whole-stream walk (no length bound, nesting
+        // to XDRG_MAX_FRAMES), and the decode reports the record's own error
+        win = XDRG_MAX_MSG;
+        detail::abicheck(xdrg_status_init(c.status(), s), "xdrg_status_init");
+        continue;
+      }
       if (ie.code) P.raise(ie);
+      break;
     }
+    const bool host = rc == XDRG_EUNSUPPORTED;
     if (host) {
       const std::vector<std::uint64_t> idx = index_records<T>(x, len, n);
       c.h_off.resize((n + 1) * 8);

@@ -481,3 +481,54 @@ def test_gpu_index_graph_capture(dev):
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy().view(np.uint64), offs) and int(cnt.item()) == n
     assert _fast_flag(ws[-256:].cpu().numpy()) == 1
+
+
+def _nest_plan(depth):
+    """n0 { int v; }, n_i { n_{i-1} *p; int x; }: bounded records (a
+    pointer holds at most one element) nested depth - 1 element frames,
+    past the window parse's XDRG_INDEX_FRAMES."""
+    from xdrpp_amd.xdr_types import Int, Pointer, Struct
+    t = Struct("n0", [("v", Int)])
+    for i in range(1, depth + 1):
+        t = Struct(f"n{i}", [("p", Pointer(t)), ("x", Int)])
+    return t
+
+
+def _nest_stream(depth, n, seed):
+    rng = np.random.default_rng(seed)
+    recs, offs = [], [0]
+    for _ in range(n):
+        d = int(rng.integers(0, depth + 1))  # levels holding their pointer
+        w = []
+        for lvl in range(depth, 0, -1):
+            if depth - lvl < d:
+                w.append(1)
+            else:
+                w.append(0)
+                break
+        else:
+            w.append(int(rng.integers(0, 1 << 31)))  # n0.v
+        w += [int(v) for v in rng.integers(0, 1 << 31, size=min(d, depth) + (0 if d >= depth else 1))]
+        recs.append(np.array(w, dtype=">u4").tobytes())
+        offs.append(offs[-1] + len(recs[-1]))
+    return np.frombuffer(b"".join(recs), dtype=np.uint8).copy(), np.array(offs, dtype=np.int64)
+
+
+@pytest.mark.gpu
+def test_gpu_decode_without_offsets_nested_past_index_frames(dev):
+    """A plan whose records fit the index window but nest past its
+    XDRG_INDEX_FRAMES: decode() without offsets hands the INDEX_LONG of the
+    window parse to the whole-stream walk, and decodes as with offsets."""
+    import torch
+    from xdrpp_amd import marshal as M
+    depth = 24
+    plan = M.Plan(compile_plan(_nest_plan(depth)))
+    assert plan.max_record_bytes <= A.INDEX_MAX_MSG
+    x, offs = _nest_stream(depth, 3000, 7)
+    mar = M.Marshaler(plan, dev)
+    xd = torch.from_numpy(x).to(dev)
+    a, ha = mar.decode(xd, len(offs) - 1, torch.from_numpy(offs).to(dev))
+    b, hb = mar.decode(xd, len(offs) - 1)
+    assert torch.equal(a, b) and torch.equal(ha, hb)
+    got = mar.index_records(xd, len(offs) - 1, A.MAX_MSG)
+    assert np.array_equal(got.cpu().numpy(), offs)

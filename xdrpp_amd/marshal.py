@@ -330,7 +330,15 @@ class Marshaler:
         (index_records: records of any length and nesting).  Returns (native
         uint8 tensor [n*stride], heap uint8 tensor or None)."""
         if offsets is None and not self.plan.is_fixed:
-            offsets = self.index_records(xdr, n)
+            try:
+                offsets = self.index_records(xdr, n)
+            except XdrRuntimeError as e:
+                # a record nested past the window parse's frames, or longer
+                # than the plan's bound: the whole-stream walk has neither
+                # bound, and the decode reports that record's own error
+                if e.code != A.ERR_INDEX_LONG:
+                    raise
+                offsets = self.index_records(xdr, n, A.MAX_MSG)
         s = _stream()
         native = torch.zeros(max(n, 1) * self.plan.stride, dtype=torch.uint8, device=self.device)
         heap = None
