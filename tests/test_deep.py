@@ -405,6 +405,18 @@ def test_gpu_wave_pass(dev, spec):
         else:  # (the word fell in a payload)
             gn, gh = mar.decode(_dev(xb, dev), n, do)
             assert np.array_equal(gn.cpu().numpy(), on) and np.array_equal(gh.cpu().numpy(), oh)
+    # one byte flipped across the list (pads, lengths, counts, values), in
+    # and past the list decode's batches of 64 nodes and 8 KiB blocks
+    for at in range(base + 3, int(offs[k + 1]), 1531):
+        xb = x.copy()
+        xb[at] ^= 0x5A
+        try:
+            on, oh = O.decode(cp, xb, n, offs)
+        except O.OracleError:
+            same_error(xb, offs)
+        else:
+            gn, gh = mar.decode(_dev(xb, dev), n, do)
+            assert np.array_equal(gn.cpu().numpy(), on) and np.array_equal(gh.cpu().numpy(), oh), at
     for L in (40, 150, 650):
         same_error(x, offs, stack_limit=L)
     cut = offs.copy()

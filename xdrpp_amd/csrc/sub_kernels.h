@@ -205,7 +205,9 @@ struct sub_pass {
   unsigned long long *wave_count;
   uint32_t wave;
   // decode, main pass: the host gave each wave kWaveBlk bytes of LDS after
-  // the ops, for the stream of its 64 records (win_rd)
+  // the ops, for the stream of its 64 records (win_rd); wave pass: each
+  // wave also has kWaveBlk / 2 bytes after the blocks for list_decode's
+  // node candidates
   uint32_t win;
   // size, main pass: per chain, where the chain pass takes it over (see
   // "Chains"; null: the size walk chases every chain itself)
@@ -1360,6 +1362,309 @@ __device__ uint64_t sub_ebytes(const xdrg_op *__restrict__ ops, const uint32_t *
   }
 }
 
+// Linked lists in the wave pass.  A plan that is one node of a list -- flat
+// fields, then an optional pointer to its own type as the last field, the
+// RPCBPROC_DUMP reply's rp__list (xdrpp/rpcb_prot.x:32-37) -- decodes a long
+// record a batch of up to 64 nodes at a time instead of a node per step of
+// the whole wave: the wave walks the nodes' lengths and counts alone, in step
+// (scalar, from the LDS block: each node's first byte and element area, and
+// every check the walk makes on them), then each lane decodes one node of
+// the batch from the block, the value checks first (pads, enums) and the
+// batch written only when all its nodes pass.  A record that leaves that
+// shape (a failed check, a node longer than the block, trailing bytes) goes
+// to the walk from its start (false), which writes again every node the
+// batches wrote, since they all come before its failure.
+__device__ __forceinline__ bool flat_kind(uint32_t k) {
+  return k == XDRG_OP_U32 || k == XDRG_OP_U64 || k == XDRG_OP_BOOL || k == XDRG_OP_ENUM ||
+         k == XDRG_OP_OPAQUE || k == XDRG_OP_VAROPAQUE || k == XDRG_OP_STRING;
+}
+// The list's VECTOR op, or ~0u when the plan is not one node of a list.
+__device__ __forceinline__ uint32_t list_vpc(const xdrg_op *__restrict__ ops, uint32_t nops) {
+  uint32_t pc = 0;
+  while (pc < nops && flat_kind(ops[pc].kind)) ++pc;
+  if (pc == 0 || pc >= nops) return ~0u;
+  const xdrg_op &v = ops[pc];
+  constexpr uint32_t kPtr = XDRG_F_SUB | XDRG_F_POINTER;
+  if (v.kind != XDRG_OP_VECTOR || (v.flags & kPtr) != kPtr || v.arg0 != 1u || v.arg4 != 0u || !v.arg3)
+    return ~0u;
+  return sub_tail(ops, pc) ? pc : ~0u;
+}
+
+template <class OPS>
+__device__ __forceinline__ bool list_decode(const xdrg_op *__restrict__ sops, uint32_t vpc,
+                                         const uint32_t *__restrict__ table, const uint8_t *__restrict__ xdr,
+                                         uint64_t a, uint64_t b, uint8_t *__restrict__ rec, uint32_t stride,
+                                         uint8_t *__restrict__ heap, uint64_t ecur, uint64_t eend,
+                                         uint32_t stack_limit, uint32_t *blk, uint16_t *nxt) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const xdrg_op &V = sops[vpc];
+  const uint32_t vdepth = V.depth, esz = V.arg1, emin = V.arg3, vnoff = V.noff;
+  uint32_t maxd = 0;
+  for (uint32_t q = 0; q <= vpc; ++q) maxd = max(maxd, static_cast<uint32_t>(sops[q].depth));
+  uint64_t base = ~0ull;  // stream offset of blk[0]
+  auto load = [&](uint64_t q) {
+    const uint64_t b0 = q & ~15ull;
+    wave_sync();  // every lane past its reads of the old block
+    // (all eight loads in flight before the stores took 27 more VGPRs in a
+    // kernel the main pass shares)
+    for (uint32_t j = 0; j < kWaveBlk / 1024u; ++j) {
+      const uint32_t k = lane + 64u * j;
+      const uint64_t o = b0 + 16ull * k;
+      u32x4 v{0u, 0u, 0u, 0u};
+      if (o + 16 <= b) {
+        v = ld16u(xdr + o);
+      } else if (o < b) {
+        v.x = ld32(xdr + o);
+        if (o + 8 <= b) v.y = ld32(xdr + o + 4);
+        if (o + 12 <= b) v.z = ld32(xdr + o + 8);
+      }
+      *reinterpret_cast<u32x4 *>(blk + 4u * k) = v;
+    }
+    wave_sync();
+    base = b0;
+    if (!nxt) return;
+    // every word of the block as a node start, a lane a word at a time: the
+    // node's words and its pointer's count, (words << 1 | count), or 0 where
+    // a check fails or a read leaves the block.  The chain from the record's
+    // first byte meets only true node starts, so it follows these in one
+    // LDS read a node (a 0 on it: the scalar walk below takes that node).
+    for (uint32_t w = lane; w < kWaveBlk / 4u; w += 64u) {
+      const uint64_t q = b0 + 4ull * w;
+      uint64_t c = q;
+      uint32_t res = 0, cn = 0;
+      if (q < b) {
+        uint32_t pc = 0;
+        auto cand = [&](const auto &op) __attribute__((always_inline)) -> int {
+          const uint64_t rem = b - c;
+          switch (op.kind) {
+          case XDRG_OP_U32: case XDRG_OP_BOOL: case XDRG_OP_ENUM:
+            if (rem < 4) return 1;
+            c += 4; break;
+          case XDRG_OP_U64:
+            if (rem < 8) return 1;
+            c += 8; break;
+          case XDRG_OP_OPAQUE:
+            if (rem < op.arg0) return 1;
+            c += (op.arg0 + 3u) & ~3u; break;
+          case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
+            if (rem < 4 || c - b0 >= kWaveBlk) return 1;
+            const uint32_t L = bswap32(blk[(c - b0) >> 2]);
+            if (L > rem - 4 || L > op.arg0) return 1;
+            c += 4 + 4ull * ((L + 3u) >> 2); break;
+          }
+          default:
+            if (rem < 4 || c - b0 >= kWaveBlk) return 1;
+            cn = bswap32(blk[(c - b0) >> 2]);
+            c += 4;
+            return 0;
+          }
+          ++pc;
+          return kWalkCont;
+        };
+        int rc;
+        do rc = OPS::visit(sops, pc, cand);
+        while (rc == kWalkCont);
+        if (!rc && cn <= 1u && static_cast<uint64_t>(cn) * emin <= b - c && c - q <= 4ull * (kWaveBlk / 4u))
+          res = static_cast<uint32_t>((c - q) >> 1) | cn;  // (words << 1 | count)
+      }
+      nxt[w] = static_cast<uint16_t>(res);
+    }
+    wave_sync();
+  };
+  // the batch: lane j holds node kb + j's first byte (record-relative), its
+  // object (~0: the record, else its element's heap offset), the element
+  // area its pointer gets and the pointer's count
+  uint32_t m_p = 0, m_obj_lo = 0, m_obj_hi = 0, m_ref_lo = 0, m_ref_hi = 0, m_cnt = 0;
+  uint32_t nb = 0;
+#ifdef XDRG_LIST_STAMPS
+  uint64_t ts_val = 0, ts_wr = 0, ts_ld = 0, ts_all = clock64(), n_fl = 0, n_ld = 0;
+#define XLS(v, t) (v) += clock64() - (t)
+#else
+#define XLS(v, t) ((void)0)
+#endif
+  // lane decode of the batch from the block: checks, then (all pass) writes
+  auto flush = [&]() -> bool {
+    if (!nb) return true;
+#ifdef XDRG_LIST_STAMPS
+    uint64_t t0 = clock64(); ++n_fl;
+#endif
+    const bool on = lane < nb;
+    uint64_t p = a + m_p;
+    auto wd = [&](uint64_t q) -> uint32_t { return blk[(q - base) >> 2]; };
+    bool bad = false;
+    if (on) {
+      uint32_t pc = 0;
+      auto check = [&](const auto &op) __attribute__((always_inline)) -> int {
+        switch (op.kind) {
+        case XDRG_OP_U32: case XDRG_OP_BOOL: p += 4; break;
+        case XDRG_OP_ENUM:
+          if ((op.flags & XDRG_F_VALIDATE) && !enum_ok(table, op.arg0, op.arg1, bswap32(wd(p)))) bad = true;
+          p += 4; break;
+        case XDRG_OP_U64: p += 8; break;
+        case XDRG_OP_OPAQUE: {
+          const uint32_t L = op.arg0;
+          if ((L & 3u) && (wd(p + (L & ~3u)) & ~keep_mask(L & 3u))) bad = true;
+          p += (L + 3u) & ~3u; break;
+        }
+        case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
+          const uint32_t L = bswap32(wd(p));
+          p += 4;
+          const uint32_t nw = (L + 3u) >> 2;
+          if ((L & 3u) && (wd(p + 4ull * (nw - 1)) & ~keep_mask(L & 3u))) bad = true;
+          p += 4ull * nw; break;
+        }
+        default: return kWalkOk;  // the list's VECTOR
+        }
+        ++pc;
+        return kWalkCont;
+      };
+      while (OPS::visit(sops, pc, check) == kWalkCont) {}
+    }
+    if (__any(bad)) return false;
+    XLS(ts_val, t0);
+#ifdef XDRG_LIST_STAMPS
+    t0 = clock64();
+#endif
+    if (on) {
+      const uint64_t obj = (static_cast<uint64_t>(m_obj_hi) << 32) | m_obj_lo;
+      uint8_t *nat = obj == ~0ull ? rec : heap + obj;
+      if (obj == ~0ull) {
+        for (uint32_t z = 0; z + 4 <= stride; z += 4) st32(nat + z, 0u);
+      } else {
+        for (uint32_t z = 0; z + 4 <= esz; z += 4) st32(nat + z, 0u);
+        for (uint32_t z = esz & ~3u; z < esz; ++z) nat[z] = 0;
+      }
+      p = a + m_p;
+      uint32_t pc = 0;
+      auto put = [&](const auto &op) __attribute__((always_inline)) -> int {
+        switch (op.kind) {
+        case XDRG_OP_U32: case XDRG_OP_ENUM: st32(nat + op.noff, bswap32(wd(p))); p += 4; break;
+        case XDRG_OP_BOOL: nat[op.noff] = wd(p) != 0u; p += 4; break;
+        case XDRG_OP_U64:
+          st32(nat + op.noff + 4, bswap32(wd(p)));
+          st32(nat + op.noff, bswap32(wd(p + 4)));
+          p += 8; break;
+        case XDRG_OP_OPAQUE: {
+          const uint32_t L = op.arg0;
+          for (uint32_t q = 0; q < L; q += 4) {
+            const uint32_t w = wd(p + q);
+            for (uint32_t k = 0; k < 4u && q + k < L; ++k) nat[op.noff + q + k] = uint8_t(w >> (8u * k));
+          }
+          p += (L + 3u) & ~3u; break;
+        }
+        case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
+          const uint32_t L = bswap32(wd(p));
+          p += 4;
+          *reinterpret_cast<uint64_t *>(nat + op.noff) = p;
+          st32(nat + op.noff + 8, L);
+          p += 4ull * ((L + 3u) >> 2); break;
+        }
+        default: return kWalkOk;
+        }
+        ++pc;
+        return kWalkCont;
+      };
+      while (OPS::visit(sops, pc, put) == kWalkCont) {}
+      *reinterpret_cast<uint64_t *>(nat + vnoff) = (static_cast<uint64_t>(m_ref_hi) << 32) | m_ref_lo;
+      st32(nat + vnoff + 8, m_cnt);
+    }
+    nb = 0;
+    XLS(ts_wr, t0);
+    return true;
+  };
+  uint64_t p = a, obj = ~0ull;
+  uint32_t k = 0;  // the node (0: the record)
+  for (;;) {
+    if (base == ~0ull) {
+#ifdef XDRG_LIST_STAMPS
+      const uint64_t t0 = clock64(); ++n_ld;
+#endif
+      load(p);
+      XLS(ts_ld, t0);
+    }
+    // the node's lengths and counts, scalar: 0 its pointer's count word
+    // read, 1 a check failed, 2 a read past the block
+    const uint64_t p0 = p;
+    const uint32_t dbase = k * vdepth;
+    uint32_t cnt = 0;
+    int rc = (static_cast<uint64_t>(dbase) + maxd > stack_limit) ? 1 : 0;
+    const uint32_t e = !rc && nxt && p - base < kWaveBlk
+                           ? __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(nxt[(p - base) >> 2]))
+                           : 0u;
+    if (e) {  // the candidate pass's node
+      cnt = e & 1u;
+      p += 2ull * (e & ~1u);
+    } else if (!rc) {
+      uint32_t pc = 0;
+      auto skel = [&](const auto &op) __attribute__((always_inline)) -> int {
+        const uint64_t rem = b - p;
+        switch (op.kind) {
+        case XDRG_OP_U32: case XDRG_OP_BOOL: case XDRG_OP_ENUM:
+          if (rem < 4) return 1;
+          p += 4; break;
+        case XDRG_OP_U64:
+          if (rem < 8) return 1;
+          p += 8; break;
+        case XDRG_OP_OPAQUE:
+          if (rem < op.arg0) return 1;
+          p += (op.arg0 + 3u) & ~3u; break;
+        case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
+          if (rem < 4) return 1;
+          if (p - base >= kWaveBlk) return 2;
+          const uint32_t L = bswap32(__builtin_amdgcn_readfirstlane(blk[(p - base) >> 2]));
+          if (L > rem - 4 || L > op.arg0) return 1;
+          p += 4 + 4ull * ((L + 3u) >> 2); break;
+        }
+        default:  // the list's VECTOR: its count word
+          if (rem < 4) return 1;
+          if (p - base >= kWaveBlk) return 2;
+          cnt = bswap32(__builtin_amdgcn_readfirstlane(blk[(p - base) >> 2]));
+          p += 4;
+          return 0;
+        }
+        ++pc;
+        return kWalkCont;
+      };
+      do rc = OPS::visit(sops, pc, skel);
+      while (rc == kWalkCont);
+    }
+    if (rc == 2) {  // the node leaves the block: write the batch, reload at the node
+      if (!flush()) return false;
+      if (base == (p0 & ~15ull)) return false;  // a node longer than the block
+      p = p0;
+      base = ~0ull;
+      continue;
+    }
+    if (rc) return false;
+    if (cnt > 1u || static_cast<uint64_t>(cnt) * emin > b - p) return false;
+    if (cnt && k + 1u >= XDRG_MAX_FRAMES) return false;
+    ecur = (ecur + 7u) & ~7ull;
+    if (ecur > eend || static_cast<uint64_t>(cnt) * esz > eend - ecur) return false;
+    const uint64_t ref = ecur;
+    ecur += static_cast<uint64_t>(cnt) * esz;
+    const uint32_t rp = static_cast<uint32_t>(p0 - a);
+    m_p = lane == nb ? rp : m_p;
+    m_obj_lo = lane == nb ? static_cast<uint32_t>(obj) : m_obj_lo;
+    m_obj_hi = lane == nb ? static_cast<uint32_t>(obj >> 32) : m_obj_hi;
+    m_ref_lo = lane == nb ? static_cast<uint32_t>(ref) : m_ref_lo;
+    m_ref_hi = lane == nb ? static_cast<uint32_t>(ref >> 32) : m_ref_hi;
+    m_cnt = lane == nb ? cnt : m_cnt;
+    ++nb;
+    ++k;
+    obj = ref;
+    if (!cnt) {  // the list's end: the record's own END follows
+      if (p != b) return false;
+      const bool fin = flush();
+#ifdef XDRG_LIST_STAMPS
+      if (!lane) printf("LIST nodes %u flushes %lu loads %lu all %lu val %lu wr %lu ld %lu\n", k, n_fl, n_ld,
+                        clock64() - ts_all, ts_val, ts_wr, ts_ld);
+#endif
+      return fin;
+    }
+    if (nb == 64u && !flush()) return false;
+  }
+}
+
 template <class OPS>
 __device__ __forceinline__ void sub_decode_kernel(XDRG_SUB_DECODE_PARAMS) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -1436,6 +1741,15 @@ __device__ __forceinline__ void sub_decode_kernel(XDRG_SUB_DECODE_PARAMS) {
         uint32_t *blk = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(smem) + lo) +
                         __builtin_amdgcn_readfirstlane(threadIdx.x / 64u) * (kWaveBlk / 4u);
         const uint64_t ru = rfl64(r), au = rfl64(a), bu = rfl64(b);
+        const uint32_t lvpc = list_vpc(sops, nops);
+        uint16_t *nxt = P.win ? reinterpret_cast<uint16_t *>(reinterpret_cast<uint8_t *>(smem) + lo +
+                                                             kWaveWaves * kWaveBlk) +
+                                    __builtin_amdgcn_readfirstlane(threadIdx.x / 64u) * (kWaveBlk / 4u)
+                              : nullptr;
+        if (lvpc != ~0u && list_decode<OPS>(sops, lvpc, table, xdr, au + mark, bu, native + ru * stride, stride,
+                                            heap, ebase + static_cast<uint64_t>(F) * au,
+                                            ebase + static_cast<uint64_t>(F) * bu, stack_limit, blk, nxt))
+          return;
         if (sub_decode_rec<OPS>(sops, table, xdr, au + mark, bu, native + ru * stride, stride, heap,
                                 ebase + static_cast<uint64_t>(F) * au, ebase + static_cast<uint64_t>(F) * bu,
                                 stack_limit, ru, err, &full_op, st, true, wave_rd{xdr, bu, blk, ~0ull}) == kWalkFull &&

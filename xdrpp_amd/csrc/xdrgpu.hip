@@ -2388,8 +2388,12 @@ int var_decode(const xdrg_plan &P, const dev_tables &T, const void *d_xdr, uint6
       W.defer = dp.main.defer;  // what its frames cannot finish: deep pass A
       W.defer_count = dp.main.defer_count;
       W.wave = 1;
-      HIPCHK(frame_launch(k_sub_decode, mf, kWaveGrid, 64 * kWaveWaves,
-                          align_up(lds, 16) + size_t(kWaveWaves) * kWaveBlk, s, xdr8, len, d_offsets, n, nat8,
+      // linked lists' node candidates (sub_kernels.h list_decode), when the
+      // ops leave room for them
+      const size_t lds_list = lds_win + size_t(kWaveWaves) * (kWaveBlk / 2);
+      W.win = lds_list <= kVarLdsBudget ? 1u : 0u;
+      HIPCHK(frame_launch(k_sub_decode, mf, kWaveGrid, 64 * kWaveWaves, W.win ? lds_list : lds_win, s, xdr8, len,
+                          d_offsets, n, nat8,
                           p->stride, T.d_ops, nops, T.d_table, stack_limit, d_heap_out, ebase, p->heap_factor, mark,
                           err, W));
     }
