@@ -1423,59 +1423,73 @@ __device__ __forceinline__ bool list_decode(const xdrg_op *__restrict__ sops, ui
     wave_sync();
     base = b0;
     if (!nxt) return;
-    // every word of the block as a node start, a lane a word at a time: the
-    // node's words and its pointer's count, (words << 1 | count), or 0 where
-    // a check fails or a read leaves the block.  The chain from the record's
-    // first byte meets only true node starts, so it follows these in one
-    // LDS read a node (a 0 on it: the scalar walk below takes that node).
-    for (uint32_t w = lane; w < kWaveBlk / 4u; w += 64u) {
-      const uint64_t q = b0 + 4ull * w;
-      uint64_t c = q;
-      uint32_t res = 0, cn = 0;
-      if (q < b) {
+    // every word of the block as a node start, a lane two words at a time
+    // (their LDS reads in flight together): the node's words and its
+    // pointer's count, (words << 1 | count), or 0 where a check fails or a
+    // read leaves the block.  The chain from the record's first byte meets
+    // only true node starts, so it follows these in one LDS read a node (a 0
+    // on it: the scalar walk below takes that node).
+    constexpr uint32_t kHalf = kWaveBlk / 8u;  // words per cursor
+    for (uint32_t w = lane; w < kHalf; w += 64u) {
+      uint64_t c[2] = {b0 + 4ull * w, b0 + 4ull * (w + kHalf)};
+      const uint64_t q[2] = {c[0], c[1]};
+      bool live[2] = {q[0] < b, q[1] < b};
+      uint32_t cn[2] = {0u, 0u};
+      if (live[0] || live[1]) {
         uint32_t pc = 0;
         auto cand = [&](const auto &op) __attribute__((always_inline)) -> int {
-          const uint64_t rem = b - c;
-          switch (op.kind) {
-          case XDRG_OP_U32: case XDRG_OP_BOOL: case XDRG_OP_ENUM:
-            if (rem < 4) return 1;
-            c += 4; break;
-          case XDRG_OP_U64:
-            if (rem < 8) return 1;
-            c += 8; break;
-          case XDRG_OP_OPAQUE:
-            if (rem < op.arg0) return 1;
-            c += (op.arg0 + 3u) & ~3u; break;
-          case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
-            if (rem < 4 || c - b0 >= kWaveBlk) return 1;
-            const uint32_t L = bswap32(blk[(c - b0) >> 2]);
-            if (L > rem - 4 || L > op.arg0) return 1;
-            c += 4 + 4ull * ((L + 3u) >> 2); break;
+#pragma unroll
+          for (uint32_t i = 0; i < 2; ++i) {
+            const uint64_t rem = b - c[i];
+            bool ok = live[i];
+            switch (op.kind) {
+            case XDRG_OP_U32: case XDRG_OP_BOOL: case XDRG_OP_ENUM:
+              ok = ok && rem >= 4;
+              c[i] += 4; break;
+            case XDRG_OP_U64:
+              ok = ok && rem >= 8;
+              c[i] += 8; break;
+            case XDRG_OP_OPAQUE:
+              ok = ok && rem >= op.arg0;
+              c[i] += (op.arg0 + 3u) & ~3u; break;
+            case XDRG_OP_VAROPAQUE: case XDRG_OP_STRING: {
+              ok = ok && rem >= 4 && c[i] - b0 < kWaveBlk;
+              const uint32_t L = ok ? bswap32(blk[(c[i] - b0) >> 2]) : 0u;
+              ok = ok && L <= rem - 4 && L <= op.arg0;
+              c[i] += 4 + 4ull * ((L + 3u) >> 2); break;
+            }
+            default:
+              ok = ok && rem >= 4 && c[i] - b0 < kWaveBlk;
+              cn[i] = ok ? bswap32(blk[(c[i] - b0) >> 2]) : 0u;
+              c[i] += 4;
+              break;
+            }
+            live[i] = ok;
           }
-          default:
-            if (rem < 4 || c - b0 >= kWaveBlk) return 1;
-            cn = bswap32(blk[(c - b0) >> 2]);
-            c += 4;
-            return 0;
-          }
+          if (op.kind == XDRG_OP_VECTOR) return 0;
+          if (!live[0] && !live[1]) return 1;
           ++pc;
           return kWalkCont;
         };
         int rc;
         do rc = OPS::visit(sops, pc, cand);
         while (rc == kWalkCont);
-        if (!rc && cn <= 1u && static_cast<uint64_t>(cn) * emin <= b - c && c - q <= 4ull * (kWaveBlk / 4u))
-          res = static_cast<uint32_t>((c - q) >> 1) | cn;  // (words << 1 | count)
       }
-      nxt[w] = static_cast<uint16_t>(res);
+#pragma unroll
+      for (uint32_t i = 0; i < 2; ++i) {
+        const bool ok = live[i] && cn[i] <= 1u && static_cast<uint64_t>(cn[i]) * emin <= b - c[i];
+        nxt[w + i * kHalf] = static_cast<uint16_t>(ok ? static_cast<uint32_t>((c[i] - q[i]) >> 1) | cn[i] : 0u);
+      }
     }
     wave_sync();
   };
-  // the batch: lane j holds node kb + j's first byte (record-relative), its
-  // object (~0: the record, else its element's heap offset), the element
-  // area its pointer gets and the pointer's count
-  uint32_t m_p = 0, m_obj_lo = 0, m_obj_hi = 0, m_ref_lo = 0, m_ref_hi = 0, m_cnt = 0;
-  uint32_t nb = 0;
+  // the batch: lane j holds node k - nb + j's first byte, record-relative,
+  // or'ed with its pointer's count.  Every pointer but the last holds one
+  // element, so node k's pointer gets the area ref0 + k * align8(esz) (the
+  // walk's bump pointer: aligned to 8, then one element on) and node k >= 1
+  // is the element its predecessor's pointer got.
+  uint32_t m_pc = 0, nb = 0, k = 0;  // k: the next node (0: the record)
+  const uint64_t ref0 = (ecur + 7u) & ~7ull, esz8 = (static_cast<uint64_t>(esz) + 7u) & ~7ull;
 #ifdef XDRG_LIST_STAMPS
   uint64_t ts_val = 0, ts_wr = 0, ts_ld = 0, ts_all = clock64(), n_fl = 0, n_ld = 0;
 #define XLS(v, t) (v) += clock64() - (t)
@@ -1489,9 +1503,15 @@ __device__ __forceinline__ bool list_decode(const xdrg_op *__restrict__ sops, ui
     uint64_t t0 = clock64(); ++n_fl;
 #endif
     const bool on = lane < nb;
-    uint64_t p = a + m_p;
+    const uint32_t kk = k - nb + lane, cnt = m_pc & 1u;
+    const uint64_t ref = ref0 + static_cast<uint64_t>(kk) * esz8;
+    uint64_t p = a + (m_pc & ~3u);
     auto wd = [&](uint64_t q) -> uint32_t { return blk[(q - base) >> 2]; };
-    bool bad = false;
+    // the walk's checks on the node's depth, frames and element area, then
+    // its pads and enums
+    bool bad = on && (static_cast<uint64_t>(kk) * vdepth + maxd > stack_limit ||
+                      (cnt && kk + 1u >= XDRG_MAX_FRAMES) || ref > eend ||
+                      static_cast<uint64_t>(cnt) * esz > eend - ref);
     if (on) {
       uint32_t pc = 0;
       auto check = [&](const auto &op) __attribute__((always_inline)) -> int {
@@ -1526,15 +1546,14 @@ __device__ __forceinline__ bool list_decode(const xdrg_op *__restrict__ sops, ui
     t0 = clock64();
 #endif
     if (on) {
-      const uint64_t obj = (static_cast<uint64_t>(m_obj_hi) << 32) | m_obj_lo;
-      uint8_t *nat = obj == ~0ull ? rec : heap + obj;
-      if (obj == ~0ull) {
+      uint8_t *nat = kk ? heap + (ref - esz8) : rec;
+      if (!kk) {
         for (uint32_t z = 0; z + 4 <= stride; z += 4) st32(nat + z, 0u);
       } else {
         for (uint32_t z = 0; z + 4 <= esz; z += 4) st32(nat + z, 0u);
         for (uint32_t z = esz & ~3u; z < esz; ++z) nat[z] = 0;
       }
-      p = a + m_p;
+      p = a + (m_pc & ~3u);
       uint32_t pc = 0;
       auto put = [&](const auto &op) __attribute__((always_inline)) -> int {
         switch (op.kind) {
@@ -1565,15 +1584,14 @@ __device__ __forceinline__ bool list_decode(const xdrg_op *__restrict__ sops, ui
         return kWalkCont;
       };
       while (OPS::visit(sops, pc, put) == kWalkCont) {}
-      *reinterpret_cast<uint64_t *>(nat + vnoff) = (static_cast<uint64_t>(m_ref_hi) << 32) | m_ref_lo;
-      st32(nat + vnoff + 8, m_cnt);
+      *reinterpret_cast<uint64_t *>(nat + vnoff) = ref;
+      st32(nat + vnoff + 8, cnt);
     }
     nb = 0;
     XLS(ts_wr, t0);
     return true;
   };
-  uint64_t p = a, obj = ~0ull;
-  uint32_t k = 0;  // the node (0: the record)
+  uint64_t p = a;
   for (;;) {
     if (base == ~0ull) {
 #ifdef XDRG_LIST_STAMPS
@@ -1582,19 +1600,18 @@ __device__ __forceinline__ bool list_decode(const xdrg_op *__restrict__ sops, ui
       load(p);
       XLS(ts_ld, t0);
     }
-    // the node's lengths and counts, scalar: 0 its pointer's count word
-    // read, 1 a check failed, 2 a read past the block
+    // the node's lengths and counts: its candidate, or scalar (0 its
+    // pointer's count word read, 1 a check failed, 2 a read past the block)
     const uint64_t p0 = p;
-    const uint32_t dbase = k * vdepth;
     uint32_t cnt = 0;
-    int rc = (static_cast<uint64_t>(dbase) + maxd > stack_limit) ? 1 : 0;
-    const uint32_t e = !rc && nxt && p - base < kWaveBlk
+    int rc = 0;
+    const uint32_t e = nxt && p - base < kWaveBlk
                            ? __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(nxt[(p - base) >> 2]))
                            : 0u;
     if (e) {  // the candidate pass's node
       cnt = e & 1u;
       p += 2ull * (e & ~1u);
-    } else if (!rc) {
+    } else {
       uint32_t pc = 0;
       auto skel = [&](const auto &op) __attribute__((always_inline)) -> int {
         const uint64_t rem = b - p;
@@ -1627,6 +1644,7 @@ __device__ __forceinline__ bool list_decode(const xdrg_op *__restrict__ sops, ui
       };
       do rc = OPS::visit(sops, pc, skel);
       while (rc == kWalkCont);
+      if (!rc && (cnt > 1u || static_cast<uint64_t>(cnt) * emin > b - p)) rc = 1;
     }
     if (rc == 2) {  // the node leaves the block: write the batch, reload at the node
       if (!flush()) return false;
@@ -1636,22 +1654,9 @@ __device__ __forceinline__ bool list_decode(const xdrg_op *__restrict__ sops, ui
       continue;
     }
     if (rc) return false;
-    if (cnt > 1u || static_cast<uint64_t>(cnt) * emin > b - p) return false;
-    if (cnt && k + 1u >= XDRG_MAX_FRAMES) return false;
-    ecur = (ecur + 7u) & ~7ull;
-    if (ecur > eend || static_cast<uint64_t>(cnt) * esz > eend - ecur) return false;
-    const uint64_t ref = ecur;
-    ecur += static_cast<uint64_t>(cnt) * esz;
-    const uint32_t rp = static_cast<uint32_t>(p0 - a);
-    m_p = lane == nb ? rp : m_p;
-    m_obj_lo = lane == nb ? static_cast<uint32_t>(obj) : m_obj_lo;
-    m_obj_hi = lane == nb ? static_cast<uint32_t>(obj >> 32) : m_obj_hi;
-    m_ref_lo = lane == nb ? static_cast<uint32_t>(ref) : m_ref_lo;
-    m_ref_hi = lane == nb ? static_cast<uint32_t>(ref >> 32) : m_ref_hi;
-    m_cnt = lane == nb ? cnt : m_cnt;
+    m_pc = lane == nb ? static_cast<uint32_t>(p0 - a) | cnt : m_pc;
     ++nb;
     ++k;
-    obj = ref;
     if (!cnt) {  // the list's end: the record's own END follows
       if (p != b) return false;
       const bool fin = flush();
