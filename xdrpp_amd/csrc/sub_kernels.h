@@ -1591,6 +1591,16 @@ __device__ __forceinline__ bool list_decode(const xdrg_op *__restrict__ sops, ui
     XLS(ts_wr, t0);
     return true;
   };
+  // the list's end: the record's own END follows
+  auto finish = [&](uint64_t p) -> bool {
+    if (p != b) return false;
+    const bool fin = flush();
+#ifdef XDRG_LIST_STAMPS
+    if (!lane) printf("LIST nodes %u flushes %lu loads %lu all %lu val %lu wr %lu ld %lu\n", k, n_fl, n_ld,
+                      clock64() - ts_all, ts_val, ts_wr, ts_ld);
+#endif
+    return fin;
+  };
   uint64_t p = a;
   for (;;) {
     if (base == ~0ull) {
@@ -1599,6 +1609,25 @@ __device__ __forceinline__ bool list_decode(const xdrg_op *__restrict__ sops, ui
 #endif
       load(p);
       XLS(ts_ld, t0);
+    }
+    if (nxt) {  // the chain through the candidates: one LDS read a node
+      uint32_t rel = static_cast<uint32_t>(p - a), off = static_cast<uint32_t>(p - base), e = 1u;
+      while (nb < 64u && off < kWaveBlk) {
+        e = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(nxt[off >> 2]));
+        if (!e) break;
+        m_pc = lane == nb ? rel | (e & 1u) : m_pc;
+        ++nb;
+        ++k;
+        rel += 2u * (e & ~1u);
+        off += 2u * (e & ~1u);
+        if (!(e & 1u)) break;
+      }
+      p = a + rel;
+      if (e && !(e & 1u)) return finish(p);
+      if (nb == 64u) {
+        if (!flush()) return false;
+        continue;
+      }
     }
     // the node's lengths and counts: its candidate, or scalar (0 its
     // pointer's count word read, 1 a check failed, 2 a read past the block)
@@ -1657,15 +1686,7 @@ __device__ __forceinline__ bool list_decode(const xdrg_op *__restrict__ sops, ui
     m_pc = lane == nb ? static_cast<uint32_t>(p0 - a) | cnt : m_pc;
     ++nb;
     ++k;
-    if (!cnt) {  // the list's end: the record's own END follows
-      if (p != b) return false;
-      const bool fin = flush();
-#ifdef XDRG_LIST_STAMPS
-      if (!lane) printf("LIST nodes %u flushes %lu loads %lu all %lu val %lu wr %lu ld %lu\n", k, n_fl, n_ld,
-                        clock64() - ts_all, ts_val, ts_wr, ts_ld);
-#endif
-      return fin;
-    }
+    if (!cnt) return finish(p);
     if (nb == 64u && !flush()) return false;
   }
 }
