@@ -434,21 +434,21 @@ def test_gpu_wave_pass(dev, spec):
     assert np.array_equal(a.cpu().numpy(), ta) and np.array_equal(ha.cpu().numpy(), tha)
 
 
-def big_node_chains(lens):
+def big_node_chains(lens, fields=1100):
     """A recursive plan of more than 1,024 ops: 1,100 unsigned
-    fields, a string and `bignode *next` per node, and records of the given
-    node counts, staged iteratively."""
+    fields (or `fields`), a string and `bignode *next` per node, and records
+    of the given node counts, staged iteratively."""
     from xdrpp_amd.xdr_types import Pointer, String, Struct, UInt
     t = Struct("bignode")
-    t.define([(f"f{i}", UInt) for i in range(1100)] + [("name", String()), ("next", Pointer(t))])
+    t.define([(f"f{i}", UInt) for i in range(fields)] + [("name", String()), ("next", Pointer(t))])
     stride = OB._align_up(t.size, t.align)
     native, heap = bytearray(len(lens) * stride), OB._Heap()
     for r, k in enumerate(lens):
         buf, off = native, r * stride
         for i in range(k):
-            for j in range(1100):
+            for j in range(fields):
                 struct.pack_into("<I", buf, off + t.offsets[f"f{j}"], (r * 7919 + i * 104729 + j) & 0xFFFFFFFF)
-            OB._put(t.fields[1100][1], buf, off + t.offsets["name"], b"n" * ((r + i) % 11), heap)
+            OB._put(t.fields[fields][1], buf, off + t.offsets["name"], b"n" * ((r + i) % 11), heap)
             nxt = i + 1 < k
             arr = heap.alloc(stride if nxt else 0, 8)
             struct.pack_into("<QII", buf, off + t.offsets["next"], arr, 1 if nxt else 0, 0)
@@ -475,6 +475,43 @@ def test_gpu_recursive_plan_past_the_wave_lds(dev):
     nat2, heap2 = mar.decode(_dev(x, dev), n, _dev(offs.astype(np.int64), dev))
     onat, oheap = O.decode(cp, x, n, offs)
     assert np.array_equal(nat2.cpu().numpy(), onat) and np.array_equal(heap2.cpu().numpy(), oheap)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fields", [300, 600])
+def test_gpu_list_decode_wide_nodes(dev, fields):
+    """The wave pass's list decode (sub_kernels.h list_decode) on lists of
+    wide nodes (1.2 / 2.4 KiB): with 300 fields the ops leave LDS for the
+    node candidates; with 600 they do not, and the lengths are walked
+    scalar.  Natives and heap as the restatement's, and a flipped byte in
+    each long record decodes or fails exactly as it does."""
+    from xdrpp_amd import marshal as M
+    lens = [1, 3, 2, 5, 1, 4, 9]
+    t, nat, heap = big_node_chains(lens, fields)
+    cp = compile_plan(t)
+    n = len(lens)
+    x, offs = O.encode(cp, nat, n, heap)
+    mar = M.Marshaler(M.Plan(t, {"specialize": 0}), dev)
+    do = _dev(offs.astype(np.int64), dev)
+    nat2, heap2 = mar.decode(_dev(x, dev), n, do)
+    onat, oheap = O.decode(cp, x, n, offs)
+    assert np.array_equal(nat2.cpu().numpy(), onat) and np.array_equal(heap2.cpu().numpy(), oheap)
+    for r in range(n):
+        if offs[r + 1] - offs[r] < 4096:
+            continue
+        # a value byte inside, and the last node's count made 2
+        for at, v in ((int(offs[r]) + int(0.61 * (offs[r + 1] - offs[r])) | 3, None), (int(offs[r + 1]) - 1, 2)):
+            xb = x.copy()
+            xb[at] = xb[at] ^ 0x21 if v is None else v
+            try:
+                on, oh = O.decode(cp, xb, n, offs)
+            except O.OracleError as oe:
+                with pytest.raises(M.XdrRuntimeError) as e:
+                    mar.decode(_dev(xb, dev), n, do)
+                assert (e.value.record, e.value.op, e.value.code) == (oe.record, oe.op, oe.code)
+            else:
+                gn, gh = mar.decode(_dev(xb, dev), n, do)
+                assert np.array_equal(gn.cpu().numpy(), on) and np.array_equal(gh.cpu().numpy(), oh), r
 
 
 @pytest.mark.parametrize("name", TYPES)
